@@ -1,0 +1,129 @@
+#!/usr/bin/env python3
+"""Benchmark: the reference's TPC-H benchmark suite (sd/tools/TpchBenchMark.scala:135-323) on
+MI355X -- 8 queries over the flattened, Druid-indexed TPC-H table, geometric-mean latency.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 launched by
+torchrun, one rank per GPU.  A "step" = one pass over the 8-query suite (each query planned
+once like the reference's DataFrame, executed per step with results collected to host numpy
+columns, i.e. ``df.collect()``).  Weak scaling: every GPU holds SF=--sf (default 100) of
+synthetic TPC-H (random dictionary values), so N GPUs hold SF=100*N.  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_GEOMEAN_MS = 5163.0  # reference Druid-backed geomean, 8 queries (SF10, 4x2-core)
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--sf", type=float, default=float(os.environ.get("SDO_BENCH_SF", "100")))
+    ap.add_argument("--mode", choices=["sql", "spec"], default=os.environ.get("SDO_BENCH_MODE", "sql"))
+    ap.add_argument("--verbose", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    from spark_druid_olap_amd.parallel.world import init_world
+
+    world = init_world()
+    dev = world.device()
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    t0 = time.time()
+    from spark_druid_olap_amd.engine.executor import Engine
+    from spark_druid_olap_amd.models import tpch
+
+    flat = tpch.generate_flat(args.sf, dev, rank=world.rank, world=world.size)
+    ds = tpch.to_datasource(flat, profile="bench")
+    nrows = ds.num_rows
+    del flat
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    log(f"[bench] rank0 shard: {nrows} rows, {ds.size_bytes() / 1e9:.1f} GB resident, gen+index {time.time() - t0:.1f}s")
+
+    engine = Engine(world)
+    if args.mode == "sql":
+        from spark_druid_olap_amd.session import Session
+
+        sess = Session(engine=engine)
+        sess.register_datasource(ds)
+        sess.sql(tpch.druid_ddl(source="orderLineItemPartSupplierBase", datasource="tpch",
+                                with_column_mapping=False))
+        queries = [(name, sess.sql(q).prepared()) for name, q in tpch.BENCH_QUERIES]
+    else:
+        from spark_druid_olap_amd.models.bench_queries import bench_specs
+
+        queries = [(name, engine.prepare(q, ds)) for name, q in bench_specs()]
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+
+    lat = {name: [] for name, _ in queries}
+    for _ in range(args.warmup):
+        for name, pq in queries:
+            pq.run()
+    world.barrier()
+    sync()
+    tstart = time.perf_counter()
+    for _ in range(args.steps):
+        for name, pq in queries:
+            a = time.perf_counter()
+            r = pq.run()
+            lat[name].append((time.perf_counter() - a) * 1e3)
+    sync()
+    world.barrier()
+    total_ms = (time.perf_counter() - tstart) * 1e3
+    total_ms = world.max_float(total_ms)
+    means = {k: world.max_float(sum(v) / len(v)) for k, v in lat.items()}
+    geo = math.exp(sum(math.log(max(m, 1e-6)) for m in means.values()) / len(means))
+    nq = len(queries) * args.steps
+    if world.rank == 0:
+        if args.verbose:
+            for k, v in means.items():
+                log(f"[bench] {k:55s} {v:9.3f} ms")
+        out = {
+            "metric": "tpch_flat_8query_geomean_latency_ms",
+            "value": round(geo, 4),
+            "unit": "ms",
+            "n_gpus": world.size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(total_ms / args.steps, 4),
+            "higher_is_better": False,
+            "scaling": "weak",
+            "vs_baseline": round(geo / BASELINE_GEOMEAN_MS, 8),
+            "dtype": "int64-exact-decimal/f64",
+            "data": "synthetic (TPC-H dbgen-like distributions, random dictionary values, generated on device)",
+            "config": {"model": f"TPC-H flattened orderLineItemPartSupplier, SF{args.sf:g} per GPU "
+                                f"(SF{args.sf * world.size:g} total), Druid bench index",
+                       "global_batch": nq, "seq_len": int(nrows), "parallelism": f"dp{world.size} (segment shards)",
+                       "queries": 8, "mode": args.mode},
+            "qps": round(nq / (total_ms / 1e3), 3),
+            "per_query_ms": {k: round(v, 4) for k, v in means.items()},
+            "rows_per_gpu": int(nrows),
+        }
+        print(json.dumps(out), flush=True)
+    from spark_druid_olap_amd.parallel.world import shutdown
+
+    shutdown()
+
+
+if __name__ == "__main__":
+    main()

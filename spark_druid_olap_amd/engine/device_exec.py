@@ -1,0 +1,169 @@
+"""Run a ScanProgram on the GPU with the HIP kernel (``ops/csrc/olap_scan.hip``).
+
+``PreparedScan`` owns the device buffers (descriptor, accumulators, HLL registers, hash table)
+so a prepared query re-executes with a handful of fills + ONE kernel launch -- the descriptor is
+uploaded once at prepare time, pointers are stable across runs.
+
+Mode choice (per shard): accumulators + HLL registers that fit the LDS budget run fully in LDS
+(flushed once per workgroup); larger dense key spaces accumulate with global atomics; key spaces
+too large for a dense array use the global open-addressing hash table, sized from the cost
+model's row estimate and grown on overflow.
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from ..ops import desc as D
+from ..ops import native
+from .lower import ScanProgram, pack
+from .partials import Partials
+
+LDS_BUDGET = int(os.environ.get("SDO_LDS_BUDGET", 64 * 1024))
+DENSE_GLOBAL_MAX_BYTES = int(os.environ.get("SDO_DENSE_MAX_BYTES", 1 << 30))
+BLOCK = 512
+UNROLL = int(os.environ.get("SDO_UNROLL", "2"))
+
+_cu_cache = {}
+
+
+def num_cus(dev: torch.device) -> int:
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx not in _cu_cache:
+        _cu_cache[idx] = int(torch.cuda.get_device_properties(idx).multi_processor_count)
+    return _cu_cache[idx]
+
+
+def _next_pow2(x: int) -> int:
+    return 1 << max(10, int(math.ceil(math.log2(max(2, x)))))
+
+
+class PreparedScan:
+    def __init__(self, prog: ScanProgram, mode: Optional[int] = None):
+        self.prog = prog
+        ds = prog.ds
+        self.dev = ds.device
+        self.m = 1 << prog.hll_p
+        G, ns = prog.G, prog.nslots
+        acc_bytes = G * ns * 8
+        hll_bytes = prog.nhll * G * self.m * 4
+        self.hll_lds = 0
+        if mode is None:
+            if acc_bytes + hll_bytes <= LDS_BUDGET:
+                mode = D.M_DENSE_LDS
+                self.hll_lds = 1 if prog.nhll else 0
+            elif acc_bytes <= LDS_BUDGET // 2 and hll_bytes <= DENSE_GLOBAL_MAX_BYTES:
+                mode = D.M_DENSE_LDS
+            elif acc_bytes + hll_bytes <= DENSE_GLOBAL_MAX_BYTES:
+                mode = D.M_DENSE_GLOBAL
+            else:
+                mode = D.M_HASH
+        self.mode = mode
+        self.dedup = 1 if G <= 64 else 0
+        if mode == D.M_DENSE_LDS:
+            self.lds = acc_bytes + (hll_bytes if self.hll_lds else 0)
+            self.lds = (self.lds + 15) // 16 * 16
+        else:
+            self.lds = 0
+        if mode == D.M_HASH:
+            est = max(1024, min(prog.G, int(prog.est_rows * 1.2) + 1024))
+            self.cap = _next_pow2(2 * est)
+        else:
+            self.cap = 0
+        self._alloc()
+
+    # ------------------------------------------------------------------ buffers
+    def _alloc(self):
+        prog, dev = self.prog, self.dev
+        rows = self.cap if self.mode == D.M_HASH else prog.G
+        self.rows = rows
+        self.init_row = torch.tensor([init for _, init in prog.slots], dtype=torch.int64, device=dev)
+        self.acc = torch.empty((rows, prog.nslots), dtype=torch.int64, device=dev)
+        self.keys = torch.empty(rows if self.mode == D.M_HASH else 1, dtype=torch.int64, device=dev)
+        self.hll = [torch.empty(rows * self.m, dtype=torch.int32, device=dev) for _ in range(prog.nhll)]
+        self.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
+        hll_offs = []
+        off = prog.G * prog.nslots * 8
+        for _ in range(prog.nhll):
+            hll_offs.append(off)
+            off += prog.G * self.m * 4
+        d = pack(prog, self.mode, self.dedup, self.hll_lds, self.lds, self.acc.data_ptr(), self.keys.data_ptr(),
+                 self.cap, self.overflow.data_ptr(), 0, 0, [h.data_ptr() for h in self.hll], hll_offs)
+        self.desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
+        cus = num_cus(dev)
+        waves = BLOCK // 64
+        need = max(1, (int(d[0]["total_chunks"]) + waves - 1) // waves)
+        if self.mode == D.M_DENSE_LDS and self.lds > 0:
+            per_cu = max(1, min(2, (160 * 1024) // max(self.lds, 1)))
+        else:
+            per_cu = 2
+        self.grid = max(1, min(need, cus * per_cu))
+
+    def _reset(self):
+        self.acc.copy_(self.init_row.expand_as(self.acc))
+        if self.mode == D.M_HASH:
+            self.keys.fill_(-1)
+        for h in self.hll:
+            h.zero_()
+        self.overflow.zero_()
+
+    # ------------------------------------------------------------------ run
+    def run(self) -> Partials:
+        prog = self.prog
+        if prog.empty:
+            return self._empty()
+        while True:
+            self._reset()
+            native.scan(self.desc, self.grid, BLOCK, self.lds, UNROLL)
+            if self.mode != D.M_HASH:
+                break
+            if int(self.overflow.item()) == 0:
+                break
+            self.cap *= 4  # grow and retry
+            self._alloc()
+        if self.mode == D.M_HASH:
+            valid = torch.nonzero(self.keys != -1).flatten()
+            return Partials("sparse", self.acc.index_select(0, valid), self.keys.index_select(0, valid),
+                            [h.view(self.rows, self.m).index_select(0, valid) for h in self.hll])
+        return Partials("dense", self.acc, None, [h.view(self.rows, self.m) for h in self.hll])
+
+    def _empty(self) -> Partials:
+        prog = self.prog
+        acc = torch.empty((0, prog.nslots), dtype=torch.int64, device=self.dev)
+        return Partials("sparse", acc, torch.zeros(0, dtype=torch.int64, device=self.dev),
+                        [torch.zeros((0, self.m), dtype=torch.int32, device=self.dev) for _ in range(prog.nhll)])
+
+
+class PreparedMask:
+    """Filter-only scan: writes one u64 mask word per 64 rows (select queries)."""
+
+    def __init__(self, prog: ScanProgram):
+        self.prog = prog
+        ds = prog.ds
+        self.dev = ds.device
+        self.mask = torch.zeros(ds.nwords, dtype=torch.int64, device=self.dev)
+        self.count = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        d = pack(prog, D.M_MASK, 0, 0, 0, 0, 0, 0, 0, self.mask.data_ptr(), self.count.data_ptr(), [], [])
+        self.desc = torch.from_numpy(d.view(np.uint8).copy()).to(self.dev)
+        waves = BLOCK // 64
+        need = max(1, (int(d[0]["total_chunks"]) + waves - 1) // waves)
+        self.grid = max(1, min(need, num_cus(self.dev) * 4))
+
+    def run(self) -> torch.Tensor:
+        """Row ids passing the filter (sorted)."""
+        if self.prog.empty:
+            return torch.zeros(0, dtype=torch.int64, device=self.dev)
+        self.mask.zero_()
+        self.count.zero_()
+        native.scan(self.desc, self.grid, BLOCK, 0, UNROLL)
+        nzw = torch.nonzero(self.mask).flatten()
+        if nzw.numel() == 0:
+            return nzw
+        words = self.mask.index_select(0, nzw)
+        bits = (words.unsqueeze(1) >> torch.arange(64, device=self.dev)) & 1
+        r, c = torch.nonzero(bits, as_tuple=True)
+        return nzw[r] * 64 + c

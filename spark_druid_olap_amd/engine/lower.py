@@ -1,0 +1,1042 @@
+"""Lower a Druid QuerySpec into a kernel ``ScanProgram`` for one datasource shard.
+
+This is where Druid's per-segment engine semantics are re-designed for the GPU:
+
+* filters  -> dictionary-domain evaluation of every leaf (selector / in / bound / regex /
+  search / javascript / extraction; reference ``sd/DruidQuerySpec.scala:152-281``) into an id
+  set, then the cheapest device encoding: inverted-bitmap words (<= 4 id runs on an indexed
+  dimension), an id range, or an id bitset; time leaves become row ranges;
+* dimensions -> mixed-radix key components: dictionary ids, dictionary-domain remaps
+  (extraction functions, evaluated once per distinct value) or in-register time buckets;
+* aggregators -> accumulator slots (exact int64 for integral/decimal metrics, f64 otherwise),
+  HLL registers, and a float expression VM for javascript aggregators.
+"""
+from __future__ import annotations
+
+import math
+import re
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..ops import desc as D
+from ..query import joda
+from ..query import spec as S
+from ..query.granularity import Granularity, bucket_start_from_value, bucket_value
+from ..query.intervals import Interval, parse_iso_ms
+from ..query.jsfunc import JSError, compile_function, jsagg_to_expr, parse_expr
+from ..segment.datasource import CHUNK_ROWS, DataSource, dtype_code
+from ..segment.dictionary import Dictionary
+
+TIME = "__time"
+HLL_P = 11  # 2048 registers, the precision of Druid's HyperUnique
+
+
+class LoweringError(ValueError):
+    pass
+
+
+# =================================================================================== boolean IR
+# ('true',) ('false',) ('and', [..]) ('or', [..]) ('not', x)
+# ('ids', dim, mask)                       dictionary-domain id set (np.bool_[card])
+# ('time', lo_ms, hi_ms)                   half open
+# ('int', col, lo, hi)                     inclusive, integer domain (scaled decimals)
+# ('flt', col, lo, hi, flags)              flags bit0 lo strict, bit1 hi strict
+TRUE = ("true",)
+FALSE = ("false",)
+
+
+def _is(x, k):
+    return x[0] == k
+
+
+def b_and(xs):
+    out = []
+    for x in xs:
+        if _is(x, "false"):
+            return FALSE
+        if _is(x, "true"):
+            continue
+        out.extend(x[1] if _is(x, "and") else [x])
+    # merge id-set leaves on the same dimension
+    merged: Dict[str, np.ndarray] = {}
+    rest = []
+    for x in out:
+        if _is(x, "ids"):
+            merged[x[1]] = merged[x[1]] & x[2] if x[1] in merged else x[2].copy()
+        else:
+            rest.append(x)
+    leaves = [("ids", k, v) for k, v in merged.items()]
+    for lf in leaves:
+        if not lf[2].any():
+            return FALSE
+    out = [lf for lf in leaves if not lf[2].all()] + rest
+    if not out:
+        return TRUE
+    return out[0] if len(out) == 1 else ("and", out)
+
+
+def b_or(xs):
+    out = []
+    for x in xs:
+        if _is(x, "true"):
+            return TRUE
+        if _is(x, "false"):
+            continue
+        out.extend(x[1] if _is(x, "or") else [x])
+    merged: Dict[str, np.ndarray] = {}
+    rest = []
+    for x in out:
+        if _is(x, "ids"):
+            merged[x[1]] = merged[x[1]] | x[2] if x[1] in merged else x[2].copy()
+        else:
+            rest.append(x)
+    leaves = [("ids", k, v) for k, v in merged.items()]
+    for lf in leaves:
+        if lf[2].all():
+            return TRUE
+    out = [lf for lf in leaves if lf[2].any()] + rest
+    if not out:
+        return FALSE
+    return out[0] if len(out) == 1 else ("or", out)
+
+
+def b_not(x):
+    k = x[0]
+    if k == "true":
+        return FALSE
+    if k == "false":
+        return TRUE
+    if k == "not":
+        return x[1]
+    if k == "and":
+        return b_or([b_not(c) for c in x[1]])
+    if k == "or":
+        return b_and([b_not(c) for c in x[1]])
+    if k == "ids":
+        return ("ids", x[1], ~x[2])
+    return ("not", x)
+
+
+# =================================================================================== extraction
+def extraction_callable(fn) -> Callable[[Any], Any]:
+    """Python callable for a Druid extraction function (evaluated over a dictionary)."""
+    if fn is None:
+        return lambda v: v
+    if isinstance(fn, S.RegexExtractionFunctionSpec):
+        rx = re.compile(fn.expr)
+
+        def f(v):
+            if v is None:
+                return None
+            m = rx.search(str(v))
+            if not m:
+                return v
+            return m.group(1) if m.groups() else m.group(0)
+
+        return f
+    if isinstance(fn, S.PartialExtractionFunctionSpec):
+        rx = re.compile(fn.expr)
+        return lambda v: v if v is not None and rx.search(str(v)) else None
+    if isinstance(fn, S.SearchQueryExtractionFunctionSpec):
+        q = str(fn.query).lower()
+        return lambda v: v if v is not None and q in str(v).lower() else None
+    if isinstance(fn, S.SubstringExtractionFunctionSpec):
+        i, n = int(fn.index), fn.length
+        return lambda v: None if v is None else (str(v)[i:i + int(n)] if n is not None else str(v)[i:]) or None
+    if isinstance(fn, S.UpperExtractionFunctionSpec):
+        return lambda v: None if v is None else str(v).upper()
+    if isinstance(fn, S.LowerExtractionFunctionSpec):
+        return lambda v: None if v is None else str(v).lower()
+    if isinstance(fn, S.TimeParsingExtractionFunctionSpec):
+        inf, outf = fn.timeFormat, fn.resultFormat
+
+        def f(v):
+            ms = joda.parse(inf, v)
+            return None if ms is None else joda.format_ms(outf, ms)
+
+        return f
+    if isinstance(fn, S.TimeFormatExtractionFunctionSpec):
+        fmt = fn.format
+
+        def f(v):
+            if v is None:
+                return None
+            if isinstance(v, (int, np.integer)):
+                ms = int(v)
+            else:
+                try:
+                    ms = parse_iso_ms(str(v))
+                except ValueError:
+                    return None
+            return joda.format_ms(fmt, ms)
+
+        return f
+    if isinstance(fn, S.JavaScriptExtractionFunctionSpec):
+        py = getattr(fn, "_pyfn", None)
+        if py is not None:
+            return py
+        jf = compile_function(fn.function)
+
+        def f(v):
+            r = jf(v)
+            if isinstance(r, float) and r.is_integer():
+                return str(int(r))
+            return None if r is None else (r if isinstance(r, str) else str(r))
+
+        return f
+    if isinstance(fn, S.InExtractionFnSpec):
+        mp = (fn.lookup or {}).get("map", {})
+        keep, repl = fn.retainMissingValue, fn.replaceMissingValueWith
+
+        def f(v):
+            key = None if v is None else _druid_str(v)
+            if key in mp:
+                return mp[key]
+            return v if keep else repl
+
+        return f
+    raise LoweringError(f"unsupported extraction function {type(fn).__name__}")
+
+
+def _druid_str(v) -> str:
+    if isinstance(v, float) and v.is_integer():
+        return str(int(v))
+    return str(v)
+
+
+def tz_offset_ms(tz: Optional[str], at_ms: int = 0) -> int:
+    if tz is None or tz.upper() in ("UTC", "Z", "GMT", "ETC/UTC"):
+        return 0
+    m = re.match(r"^(?:UTC|GMT)?([+-])(\d{1,2}):?(\d{2})?$", tz)
+    if m:
+        sgn = -1 if m.group(1) == "-" else 1
+        return sgn * (int(m.group(2)) * 60 + int(m.group(3) or 0)) * 60_000
+    try:
+        import datetime as _dt
+        from zoneinfo import ZoneInfo
+
+        z = ZoneInfo(tz)
+        dt = _dt.datetime.fromtimestamp(at_ms / 1000.0, tz=_dt.timezone.utc).astimezone(z)
+        return int(dt.utcoffset().total_seconds() * 1000)
+    except Exception:
+        return 0
+
+
+# =================================================================================== program
+@dataclass
+class KeyComp:
+    name: str
+    kind: int
+    col: str
+    card: int
+    stride: int = 1
+    base: int = 0
+    tfield: int = 0
+    tz_ms: int = 0
+    period_ms: int = 0
+    origin_ms: int = 0
+    remap: Optional[np.ndarray] = None
+    decoder: Optional[Callable[[np.ndarray], np.ndarray]] = None
+    collapse: bool = False        # decoded values may coincide: re-aggregate on host
+    is_timestamp: bool = False    # granularity bucket (output 'timestamp' ms)
+
+
+@dataclass
+class AggOut:
+    name: str
+    kind: str                     # count|sum_i|sum_f|min_i|max_i|min_f|max_f|hll|theta
+    slot: int = -1
+    hll_index: int = -1
+    scale: int = 0                # decimal digits of an exact integer sum
+    out_type: str = "double"      # long|double
+    combine: str = "sum"          # host re-aggregation: sum|min|max|hll
+
+
+@dataclass
+class ScanProgram:
+    ds: DataSource
+    cols: List[str] = field(default_factory=list)
+    fops: List[tuple] = field(default_factory=list)     # (op, col, flags, lo, hi, flo, fhi, bits_tensor)
+    filter_len: int = 0
+    keys: List[KeyComp] = field(default_factory=list)
+    aops: List[dict] = field(default_factory=list)
+    eops: List[tuple] = field(default_factory=list)
+    zones: List[tuple] = field(default_factory=list)    # (col, lo, hi)
+    ranges: List[Tuple[int, int]] = field(default_factory=list)
+    slots: List[Tuple[int, int]] = field(default_factory=list)  # (slot op, init)
+    aggs: List[AggOut] = field(default_factory=list)
+    nhll: int = 0
+    hll_p: int = HLL_P
+    G: int = 1
+    est_rows: float = 0.0
+    empty: bool = False
+    bexpr: Any = TRUE                                    # normalized filter (for the reference executor)
+    agg_filters: List[Any] = field(default_factory=list) # per aop bexpr or None
+    keepalive: List[torch.Tensor] = field(default_factory=list)
+    thetas: List[Tuple[str, str, int]] = field(default_factory=list)  # (name, column, size)
+
+    def col(self, name: str) -> int:
+        if name not in self.cols:
+            if len(self.cols) >= D.MAX_COLS:
+                raise LoweringError("too many columns referenced by one query")
+            self.cols.append(name)
+        return self.cols.index(name)
+
+    @property
+    def nslots(self) -> int:
+        return len(self.slots)
+
+    @property
+    def rows_in_ranges(self) -> int:
+        return sum(b - a for a, b in self.ranges)
+
+
+def column_tensor(ds: DataSource, name: str) -> torch.Tensor:
+    if name == TIME:
+        return ds.time
+    if name in ds.dims:
+        return ds.dims[name].ids
+    if name in ds.metrics:
+        return ds.metrics[name].data
+    raise LoweringError(f"unknown column {name!r} in datasource {ds.name}")
+
+
+class Lowerer:
+    """QuerySpec -> ScanProgram for a datasource shard."""
+
+    def __init__(self, ds: DataSource, bitmap_max_values: int = 4):
+        self.ds = ds
+        self.bitmap_max_values = bitmap_max_values
+        self._time_values: Optional[np.ndarray] = None
+
+    # ------------------------------------------------------------------ filters -> IR
+    def filter_ir(self, f) -> tuple:
+        ds = self.ds
+        if f is None or isinstance(f, S.NoopFilterSpec):
+            return TRUE
+        if isinstance(f, S.LogicalFilterSpec):
+            parts = [self.filter_ir(c) for c in f.fields]
+            return b_and(parts) if f.type == "and" else b_or(parts)
+        if isinstance(f, S.NotFilterSpec):
+            return b_not(self.filter_ir(f.field))
+        dim = getattr(f, "dimension", None)
+        if dim == TIME or (dim is not None and dim not in ds.dims and dim not in ds.metrics and dim == "timestamp"):
+            return self._time_filter(f)
+        if dim is not None and dim in ds.metrics and not isinstance(f, S.SpatialFilterSpec):
+            return self._metric_filter(f, dim)
+        if isinstance(f, S.SpatialFilterSpec):
+            return self._spatial(f)
+        if dim not in ds.dims:
+            raise LoweringError(f"filter on unknown dimension {dim!r}")
+        d = ds.dims[dim].dictionary
+        if isinstance(f, S.SelectorFilterSpec):
+            v = f.value
+            mask = np.zeros(len(d), dtype=bool)
+            i = d.lookup(None if v in (None, "") and d.has_null else v)
+            if i >= 0:
+                mask[i] = True
+            return ("ids", dim, mask)
+        if isinstance(f, S.InFilterSpec):
+            mask = np.zeros(len(d), dtype=bool)
+            for v in f.values:
+                i = d.lookup(v)
+                if i >= 0:
+                    mask[i] = True
+            return ("ids", dim, mask)
+        if isinstance(f, S.BoundFilterSpec):
+            if f.alphaNumeric and d.vtype == "string":
+                lo = None if f.lower is None else float(f.lower)
+                hi = None if f.upper is None else float(f.upper)
+
+                def pred(v):
+                    try:
+                        x = float(v)
+                    except (TypeError, ValueError):
+                        return False
+                    ok = True
+                    if lo is not None:
+                        ok = ok and (x > lo if f.lowerStrict else x >= lo)
+                    if hi is not None:
+                        ok = ok and (x < hi if f.upperStrict else x <= hi)
+                    return ok
+
+                return ("ids", dim, d.eval_mask(pred))
+            a, b = d.id_range(f.lower, f.lowerStrict, f.upper, f.upperStrict)
+            mask = np.zeros(len(d), dtype=bool)
+            mask[a:b] = True
+            return ("ids", dim, mask)
+        if isinstance(f, S.RegexFilterSpec):
+            rx = re.compile(f.pattern)
+            return ("ids", dim, d.eval_mask(lambda v: v is not None and rx.search(str(v)) is not None))
+        if isinstance(f, S.ContainsFilterSpec):
+            q = f.query or {}
+            val = str(q.get("value", ""))
+            cs = bool(q.get("caseSensitive", False)) and q.get("type") != "insensitive_contains"
+            if cs:
+                return ("ids", dim, d.eval_mask(lambda v: v is not None and val in str(v)))
+            lv = val.lower()
+            return ("ids", dim, d.eval_mask(lambda v: v is not None and lv in str(v).lower()))
+        if isinstance(f, S.ExtractionFilterSpec):
+            fn = extraction_callable(f.extractionFn)
+            target = f.value
+
+            def pred(v):
+                r = fn(v)
+                return r is not None and _druid_str(r) == _druid_str(target)
+
+            return ("ids", dim, d.eval_mask(pred))
+        if isinstance(f, S.JavascriptFilterSpec):
+            py = getattr(f, "_pyfn", None)
+            if py is None:
+                jf = compile_function(f.function)
+                py = lambda v: bool(jf(v))  # noqa: E731
+            return ("ids", dim, d.eval_mask(py))
+        raise LoweringError(f"unsupported filter {type(f).__name__}")
+
+    def _time_values(self) -> np.ndarray:
+        if self._time_values is None:
+            self._time_values = np.unique(self.ds.time_host)
+        return self._time_values
+
+    def _time_filter(self, f) -> tuple:
+        ds = self.ds
+        u = ds.time_unit_ms
+        if isinstance(f, S.SelectorFilterSpec):
+            ms = _to_ms(f.value)
+            return ("time", ms, ms + 1)
+        if isinstance(f, S.BoundFilterSpec):
+            lo = -(2 ** 62) if f.lower is None else _to_ms(f.lower) + (1 if f.lowerStrict else 0)
+            hi = 2 ** 62 if f.upper is None else _to_ms(f.upper) + (0 if f.upperStrict else 1)
+            return ("time", lo, hi)
+        if isinstance(f, S.IntervalFilterSpec):
+            return b_or([("time", iv.lo, iv.hi) for iv in (Interval.parse(s) for s in f.intervals)])
+        # generic predicate over the distinct time values -> set of allowed time units
+        if isinstance(f, S.JavascriptFilterSpec):
+            py = getattr(f, "_pyfn", None)
+            if py is None:
+                jf = compile_function(f.function)
+                py = lambda ms: bool(jf(joda.format_ms("yyyy-MM-dd'T'HH:mm:ss.SSS'Z'", ms)))  # noqa: E731
+        elif isinstance(f, S.ExtractionFilterSpec):
+            fn = extraction_callable(f.extractionFn)
+            tgt = _druid_str(f.value)
+            py = lambda ms: (lambda r: r is not None and _druid_str(r) == tgt)(fn(ms))  # noqa: E731
+        else:
+            raise LoweringError(f"unsupported time filter {type(f).__name__}")
+        tv = self._time_values()
+        ok = np.fromiter((bool(py(int(t) * u)) for t in tv), dtype=bool, count=len(tv))
+        return ("timeset", tv[ok])
+
+    def _metric_filter(self, f, name) -> tuple:
+        m = self.ds.metrics[name]
+        scale = 10 ** m.scale if m.kind == "decimal" else 1
+        if isinstance(f, S.SelectorFilterSpec):
+            v = float(f.value)
+            if m.is_integral:
+                x = v * scale
+                if x != math.floor(x):
+                    return FALSE
+                return ("int", name, int(x), int(x))
+            return ("flt", name, v, v, 0)
+        if isinstance(f, S.BoundFilterSpec):
+            lo = None if f.lower is None else float(f.lower)
+            hi = None if f.upper is None else float(f.upper)
+            if m.is_integral:
+                ilo = -(2 ** 62) if lo is None else (math.floor(lo * scale) + 1 if f.lowerStrict else math.ceil(lo * scale))
+                ihi = 2 ** 62 if hi is None else (math.ceil(hi * scale) - 1 if f.upperStrict else math.floor(hi * scale))
+                return ("int", name, int(ilo), int(ihi))
+            flags = (1 if f.lowerStrict else 0) | (2 if f.upperStrict else 0)
+            return ("flt", name, -math.inf if lo is None else lo, math.inf if hi is None else hi, flags)
+        raise LoweringError(f"unsupported metric filter {type(f).__name__}")
+
+    def _spatial(self, f) -> tuple:
+        comps = self.ds.spatial.get(f.dimension) if hasattr(self.ds, "spatial") else None
+        if not comps:
+            raise LoweringError(f"no spatial dimension {f.dimension!r}")
+        b = f.bound
+        mins, maxs = b.get("minCoords", []), b.get("maxCoords", [])
+        parts = [("flt", comps[i], float(mins[i]), float(maxs[i]), 0) for i in range(min(len(comps), len(mins)))]
+        return b_and(parts)
+
+    # ------------------------------------------------------------------ intervals
+    def query_ranges(self, intervals: Sequence[str], bexpr) -> Tuple[List[Tuple[int, int]], tuple, List[Interval]]:
+        """Row ranges from the query intervals AND top-level time conjuncts (pruning)."""
+        ivs = [Interval.parse(s) for s in intervals] if intervals else [Interval.eternity()]
+        rest = bexpr
+        conj = bexpr[1] if _is(bexpr, "and") else [bexpr]
+        tleaves = [c for c in conj if _is(c, "time")]
+        if tleaves:
+            t = Interval(-(2 ** 62), 2 ** 62)
+            for lf in tleaves:
+                t = t.intersect(Interval(lf[1], lf[2]))
+            ivs = [iv.intersect(t) for iv in ivs]
+            others = [c for c in conj if not _is(c, "time")]
+            rest = b_and(others) if others else TRUE
+        ivs = [iv for iv in ivs if not iv.empty]
+        ranges = []
+        for iv in sorted(ivs, key=lambda i: i.lo):
+            a, b = self.ds.rows_for_interval(iv.lo, iv.hi)
+            if b > a:
+                if ranges and a <= ranges[-1][1]:
+                    ranges[-1] = (ranges[-1][0], max(ranges[-1][1], b))
+                else:
+                    ranges.append((a, b))
+        if len(ranges) > D.MAX_RANGES:  # coalesce: keep exactness through a time filter
+            lo_all, hi_all = ranges[0][0], ranges[-1][1]
+            rest = b_and([rest, b_or([("time", iv.lo, iv.hi) for iv in ivs])])
+            ranges = [(lo_all, hi_all)]
+        return ranges, rest, ivs
+
+    # ------------------------------------------------------------------ emit filter program
+    def emit_filter(self, prog: ScanProgram, x) -> int:
+        """Append postfix ops for x; returns max stack depth used."""
+        k = x[0]
+        if k == "true":
+            prog.fops.append((D.F_TRUE, 0, 0, 0, 0, 0.0, 0.0, None))
+            return 1
+        if k == "false":
+            prog.fops.append((D.F_FALSE, 0, 0, 0, 0, 0.0, 0.0, None))
+            return 1
+        if k in ("and", "or"):
+            kids = sorted(x[1], key=_depth, reverse=True)
+            d = self.emit_filter(prog, kids[0])
+            for c in kids[1:]:
+                d = max(d, 1 + self.emit_filter(prog, c))
+                prog.fops.append((D.F_AND if k == "and" else D.F_OR, 0, 0, 0, 0, 0.0, 0.0, None))
+            return d
+        if k == "not":
+            d = self.emit_filter(prog, x[1])
+            prog.fops.append((D.F_NOT, 0, 0, 0, 0, 0.0, 0.0, None))
+            return d
+        if k == "ids":
+            return self._emit_ids(prog, x[1], x[2])
+        if k == "time":
+            ci = prog.col(TIME)
+            u = self.ds.time_unit_ms
+            lo = -(-x[1] // u)
+            hi = -(-x[2] // u) - 1
+            prog.fops.append((D.F_INT_RANGE, ci, 0, max(lo, -(2 ** 62)), min(hi, 2 ** 62), 0.0, 0.0, None))
+            return 1
+        if k == "timeset":
+            vals = x[1]
+            if len(vals) == 0:
+                prog.fops.append((D.F_FALSE, 0, 0, 0, 0, 0.0, 0.0, None))
+                return 1
+            ci = prog.col(TIME)
+            # contiguous runs of allowed time values -> OR of ranges (typically 1-2 runs)
+            tv = self._time_values()
+            allowed = np.isin(tv, vals)
+            runs = _runs(allowed)
+            for j, (a, b) in enumerate(runs):
+                prog.fops.append((D.F_INT_RANGE, ci, 0, int(tv[a]), int(tv[b - 1]), 0.0, 0.0, None))
+                if j:
+                    prog.fops.append((D.F_OR, 0, 0, 0, 0, 0.0, 0.0, None))
+            return 2 if len(runs) > 1 else 1
+        if k == "int":
+            ci = prog.col(x[1])
+            prog.fops.append((D.F_INT_RANGE, ci, 0, int(x[2]), int(x[3]), 0.0, 0.0, None))
+            return 1
+        if k == "flt":
+            ci = prog.col(x[1])
+            prog.fops.append((D.F_FLT_RANGE, ci, int(x[4]), 0, 0, float(x[2]), float(x[3]), None))
+            return 1
+        raise LoweringError(f"bad filter IR {k}")
+
+    def _emit_ids(self, prog: ScanProgram, dim: str, mask: np.ndarray) -> int:
+        dc = self.ds.dims[dim]
+        card = len(mask)
+        k = int(mask.sum())
+        if k == 0:
+            prog.fops.append((D.F_FALSE, 0, 0, 0, 0, 0.0, 0.0, None))
+            return 1
+        if k == card:
+            prog.fops.append((D.F_TRUE, 0, 0, 0, 0, 0.0, 0.0, None))
+            return 1
+        runs = _runs(mask)
+        neg_runs = _runs(~mask)
+        if dc.bitmap is not None:
+            for use_neg, rr in ((False, runs), (True, neg_runs)):
+                if len(rr) <= self.bitmap_max_values and sum(b - a for a, b in rr) <= 64:
+                    nw = dc.bitmap.shape[1]
+                    for j, (a, b) in enumerate(rr):
+                        row = dc.bitmap[a]
+                        if b - a == 1:
+                            prog.fops.append((D.F_BITMAP, 0, 0, 0, 0, 0.0, 0.0, row))
+                        else:
+                            prog.fops.append((D.F_BITMAP_OR, 0, 0, nw, b - a, 0.0, 0.0, row))
+                        if j:
+                            prog.fops.append((D.F_OR, 0, 0, 0, 0, 0.0, 0.0, None))
+                    if use_neg:
+                        prog.fops.append((D.F_NOT, 0, 0, 0, 0, 0.0, 0.0, None))
+                    return 2 if len(rr) > 1 else 1
+        ci = prog.col(dim)
+        if len(runs) == 1:
+            prog.fops.append((D.F_ID_RANGE, ci, 0, runs[0][0], runs[0][1], 0.0, 0.0, None))
+            return 1
+        if len(neg_runs) == 1:
+            prog.fops.append((D.F_ID_RANGE, ci, 0, neg_runs[0][0], neg_runs[0][1], 0.0, 0.0, None))
+            prog.fops.append((D.F_NOT, 0, 0, 0, 0, 0.0, 0.0, None))
+            return 1
+        nbits = (card + 63) // 64 * 64
+        bits = np.zeros(nbits, dtype=bool)
+        bits[:card] = mask
+        words = np.packbits(bits.reshape(-1, 8)[:, ::-1], axis=1).reshape(-1, 8)[:, ::-1].copy().view("<i8").ravel()
+        t = torch.from_numpy(words.copy()).to(self.ds.device)
+        prog.keepalive.append(t)
+        prog.fops.append((D.F_IN_SET, ci, 0, 0, 0, 0.0, 0.0, t))
+        return 1
+
+    # ------------------------------------------------------------------ zones
+    def pick_zones(self, prog: ScanProgram, bexpr) -> None:
+        conj = bexpr[1] if _is(bexpr, "and") else [bexpr]
+        cands = []
+        for c in conj:
+            if _is(c, "ids") and self.ds.dims[c[1]].zmin is not None:
+                nz = np.flatnonzero(c[2])
+                lo, hi = int(nz[0]), int(nz[-1]) + 1
+                frac = (hi - lo) / max(1, len(c[2]))
+                if frac < 0.9:
+                    cands.append((frac, c[1], lo, hi))
+        cands.sort()
+        for frac, dim, lo, hi in cands[: D.MAX_ZONES]:
+            prog.zones.append((dim, lo, hi))
+
+    # ------------------------------------------------------------------ selectivity
+    def selectivity(self, x) -> float:
+        k = x[0]
+        if k == "true":
+            return 1.0
+        if k == "false":
+            return 0.0
+        if k == "and":
+            p = 1.0
+            for c in x[1]:
+                p *= self.selectivity(c)
+            return p
+        if k == "or":
+            return min(1.0, sum(self.selectivity(c) for c in x[1]))
+        if k == "not":
+            return 1.0 - self.selectivity(x[1])
+        if k == "ids":
+            return float(x[2].mean())
+        return 1.0 / 3.0
+
+    # ------------------------------------------------------------------ dimensions
+    def key_for_dimension(self, dspec, ivs: List[Interval]) -> KeyComp:
+        ds = self.ds
+        if isinstance(dspec, str):
+            dspec = S.DefaultDimensionSpec(dspec)
+        dim = dspec.dimension
+        name = dspec.outputName or dim
+        fn = getattr(dspec, "extractionFn", None) if isinstance(dspec, S.ExtractionDimensionSpec) else None
+        if dim == TIME:
+            return self._time_key(name, fn, ivs)
+        if dim not in ds.dims:
+            raise LoweringError(f"group by unknown dimension {dim!r}")
+        d = ds.dims[dim].dictionary
+        if fn is None:
+            return KeyComp(name, D.K_ID, dim, len(d), decoder=d.decode)
+        if isinstance(fn, S.TimeFormatExtractionFunctionSpec) and d.vtype != "string":
+            pass
+        f = extraction_callable(fn)
+        derived = d.map_values(f)
+        uniq = sorted({v for v in derived.tolist() if v is not None}, key=lambda v: (str(type(v)), v))
+        has_null = any(v is None for v in derived.tolist())
+        dd = Dictionary(uniq, "string" if all(isinstance(v, str) for v in uniq) else "double", has_null)
+        remap = np.array([dd.lookup(v) for v in derived.tolist()], dtype=np.int32)
+        return KeyComp(name, D.K_REMAP, dim, len(dd), remap=remap, decoder=dd.decode)
+
+    def _time_key(self, name, fn, ivs: List[Interval]) -> KeyComp:
+        lo, hi = self._data_span(ivs)
+        if fn is None:
+            tf, exact, fmt, tz = self._unit_field(), True, None, 0
+        elif isinstance(fn, S.TimeFormatExtractionFunctionSpec):
+            tz = tz_offset_ms(fn.timeZone, lo)
+            tf, exact = joda.format_to_field(fn.format)
+            fmt = fn.format
+        else:
+            tf, exact, fmt, tz = self._unit_field(), False, None, 0
+        kc = KeyComp(name, D.K_TIME, TIME, 1, tfield=tf, tz_ms=tz)
+        if tf in joda.ABSOLUTE:
+            b0 = bucket_value(lo + tz, tf)
+            b1 = bucket_value(hi - 1 + tz, tf)
+            kc.base, kc.card = b0, max(1, b1 - b0 + 1)
+        else:
+            a, b = joda.field_domain(tf)
+            kc.base, kc.card = a, b - a + 1
+        base, tfv = kc.base, tf
+        if fn is None:
+            kc.decoder = lambda ids: np.array([bucket_start_from_value(int(i) + base, tfv) for i in ids], dtype=np.int64)
+        elif fmt is not None:
+            tzv = tz
+            kc.decoder = lambda ids: np.array(
+                [joda.format_ms(fmt, joda.representative_ms(tfv, int(i) + base) - (tzv if tfv in joda.ABSOLUTE else 0), tzv if tfv in joda.ABSOLUTE else 0)
+                 for i in ids], dtype=object)
+            kc.collapse = not exact
+        else:
+            f = extraction_callable(fn)
+            kc.decoder = lambda ids: np.array([f(bucket_start_from_value(int(i) + base, tfv)) for i in ids], dtype=object)
+            kc.collapse = True
+        return kc
+
+    def _unit_field(self) -> int:
+        from ..query.granularity import T_DAY, T_MS, T_SECOND
+
+        u = self.ds.time_unit_ms
+        return T_DAY if u == 86_400_000 else (T_SECOND if u == 1000 else T_MS)
+
+    def _data_span(self, ivs: List[Interval]) -> Tuple[int, int]:
+        ds = self.ds
+        lo, hi = ds.min_time_ms(), ds.max_time_ms() + ds.time_unit_ms
+        if ivs:
+            lo = max(lo, min(iv.lo for iv in ivs))
+            hi = min(hi, max(iv.hi for iv in ivs))
+        if hi <= lo:
+            hi = lo + 1
+        return lo, hi
+
+    def granularity_key(self, g: Granularity, ivs: List[Interval]) -> Optional[KeyComp]:
+        if g is None or g.is_all:
+            return None
+        tf, p, o = g.kernel_field()
+        lo, hi = self._data_span(ivs)
+        b0 = bucket_value(lo + g.tz_ms, tf, p, o)
+        b1 = bucket_value(hi - 1 + g.tz_ms, tf, p, o)
+        kc = KeyComp("timestamp", D.K_TIME, TIME, max(1, b1 - b0 + 1), base=b0, tfield=tf, tz_ms=g.tz_ms,
+                     period_ms=p, origin_ms=o, is_timestamp=True)
+        kc.decoder = lambda ids: np.array([bucket_start_from_value(int(i) + b0, tf, p, o) - g.tz_ms for i in ids],
+                                          dtype=np.int64)
+        return kc
+
+    # ------------------------------------------------------------------ aggregators
+    def add_aggregator(self, prog: ScanProgram, a, filt=None) -> None:
+        ds = self.ds
+        if isinstance(a, S.FilteredAggregationSpec):
+            inner = a.aggregator.copy(name=a.name or a.aggregator.name)
+            fx = self.filter_ir(a.filter)
+            if filt is not None:
+                fx = b_and([filt, fx])
+            return self.add_aggregator(prog, inner, fx)
+        if len(prog.aops) >= D.MAX_AOPS:
+            raise LoweringError("too many aggregators")
+
+        def aop(kind, col=-1, expr=None):
+            d = {"kind": kind, "col": col, "expr": expr, "filter": filt, "slot": -1, "hll": -1}
+            prog.aops.append(d)
+            return d
+
+        def slot(op, init):
+            if len(prog.slots) >= D.MAX_SLOTS:
+                raise LoweringError("too many accumulator slots")
+            prog.slots.append((op, init))
+            return len(prog.slots) - 1
+
+        if isinstance(a, S.FunctionAggregationSpec):
+            t = a.type
+            if t == "count":
+                d = aop(D.A_COUNT)
+                d["slot"] = slot(D.S_SUM_I, 0)
+                prog.aggs.append(AggOut(a.name, "count", d["slot"], out_type="long"))
+                return
+            fname = a.fieldName
+            if fname == "count" and fname not in ds.metrics:
+                # longSum(count) over an index without an explicit count metric == count
+                d = aop(D.A_COUNT)
+                d["slot"] = slot(D.S_SUM_I, 0)
+                prog.aggs.append(AggOut(a.name, "count", d["slot"], out_type="long"))
+                return
+            if fname not in ds.metrics:
+                raise LoweringError(f"aggregation over unknown metric {fname!r}")
+            m = ds.metrics[fname]
+            ci = prog.col(fname)
+            is_long = t.startswith("long")
+            op = t[4:] if is_long else t[6:]  # Sum / Min / Max
+            integral = m.is_integral
+            scale = m.scale if m.kind == "decimal" else 0
+            if op == "Sum":
+                if integral or is_long:
+                    d = aop(D.A_SUM_I, ci)
+                    d["slot"] = slot(D.S_SUM_I, 0)
+                    prog.aggs.append(AggOut(a.name, "sum_i", d["slot"], scale=scale if not is_long else scale,
+                                            out_type="long" if is_long and scale == 0 else "double"))
+                else:
+                    d = aop(D.A_SUM_F, ci)
+                    d["slot"] = slot(D.S_SUM_F, 0)
+                    prog.aggs.append(AggOut(a.name, "sum_f", d["slot"], out_type="double"))
+                return
+            mn = op == "Min"
+            if integral or is_long:
+                d = aop(D.A_MIN_I if mn else D.A_MAX_I, ci)
+                d["slot"] = slot(D.S_MIN_I if mn else D.S_MAX_I, D.INT64_MAX if mn else D.INT64_MIN)
+                prog.aggs.append(AggOut(a.name, "min_i" if mn else "max_i", d["slot"], scale=scale,
+                                        out_type="long" if is_long and scale == 0 else "double",
+                                        combine="min" if mn else "max"))
+            else:
+                d = aop(D.A_MIN_F if mn else D.A_MAX_F, ci)
+                init = _f2ord(math.inf) if mn else _f2ord(-math.inf)
+                d["slot"] = slot(D.S_MIN_I if mn else D.S_MAX_I, init)
+                prog.aggs.append(AggOut(a.name, "min_f" if mn else "max_f", d["slot"], out_type="double",
+                                        combine="min" if mn else "max"))
+            return
+        if isinstance(a, (S.CardinalityAggregationSpec, S.HyperUniqueAggregationSpec)):
+            fields = a.fieldNames if isinstance(a, S.CardinalityAggregationSpec) else [a.fieldName]
+            if len(fields) != 1:
+                raise LoweringError("cardinality over several fields is not supported")
+            col = fields[0]
+            if col not in ds.dims and col not in ds.metrics:
+                raise LoweringError(f"cardinality over unknown column {col!r}")
+            ci = prog.col(col)
+            d = aop(D.A_HLL, ci)
+            d["hll"] = prog.nhll
+            d["salt"] = _salt(col)
+            prog.aggs.append(AggOut(a.name, "hll", hll_index=prog.nhll, out_type="double", combine="hll"))
+            prog.nhll += 1
+            return
+        if isinstance(a, S.JavascriptAggregationSpec):
+            try:
+                op, params, expr = jsagg_to_expr(a.fnAggregate)
+            except JSError as e:
+                raise LoweringError(f"javascript aggregator not translatable: {e}")
+            ast = parse_expr(expr)
+            mapping = dict(zip(params, a.fieldNames))
+            eops = self._emit_expr(prog, ast, mapping)
+            kind = {"sum": D.A_SUM_F, "max": D.A_MAX_F, "min": D.A_MIN_F}[op]
+            d = aop(kind, -1, eops)
+            if op == "sum":
+                d["slot"] = slot(D.S_SUM_F, 0)
+                prog.aggs.append(AggOut(a.name, "sum_f", d["slot"]))
+            else:
+                mn = op == "min"
+                d["slot"] = slot(D.S_MIN_I if mn else D.S_MAX_I, _f2ord(math.inf) if mn else _f2ord(-math.inf))
+                prog.aggs.append(AggOut(a.name, "min_f" if mn else "max_f", d["slot"], combine=op))
+            return
+        if isinstance(a, S.ThetaSketchAggregationSpec):
+            if a.fieldName not in ds.dims and a.fieldName not in ds.metrics:
+                raise LoweringError(f"thetaSketch over unknown column {a.fieldName!r}")
+            prog.thetas.append((a.name, a.fieldName, int(a.size)))
+            prog.aggs.append(AggOut(a.name, "theta", combine="theta"))
+            return
+        raise LoweringError(f"unsupported aggregator {type(a).__name__}")
+
+    def _emit_expr(self, prog: ScanProgram, ast, mapping: Dict[str, str]) -> List[tuple]:
+        out: List[tuple] = []
+
+        def rec(n, depth):
+            k = n[0]
+            if k == "const":
+                out.append((D.E_CONST, 0, float(n[1])))
+                return 1
+            if k == "col":
+                name = mapping.get(n[1], n[1])
+                if name not in self.ds.metrics and name not in self.ds.dims:
+                    raise LoweringError(f"unknown column {name!r} in expression")
+                m = self.ds.metrics.get(name)
+                sc = (10.0 ** -m.scale) if (m is not None and m.kind == "decimal" and m.scale) else 0.0
+                out.append((D.E_COL, prog.col(name), sc))
+                return 1
+            if k in ("neg", "abs"):
+                d = rec(n[1], depth)
+                out.append((D.E_NEG if k == "neg" else D.E_ABS, 0, 0.0))
+                return d
+            op = {"add": D.E_ADD, "sub": D.E_SUB, "mul": D.E_MUL, "div": D.E_DIV, "min": D.E_MIN, "max": D.E_MAX}[k]
+            d1 = rec(n[1], depth)
+            d2 = rec(n[2], depth + 1)
+            out.append((op, 0, 0.0))
+            return max(d1, d2 + 1)
+
+        if rec(ast, 0) > 4:
+            raise LoweringError("aggregator expression too deep for the device VM")
+        return out
+
+    # ------------------------------------------------------------------ whole query
+    def lower_aggregate(self, intervals, filter_spec, dimensions, granularity, aggregations,
+                        extra_keys: Sequence[KeyComp] = ()) -> ScanProgram:
+        prog = ScanProgram(self.ds)
+        bexpr = self.filter_ir(filter_spec)
+        ranges, bexpr, ivs = self.query_ranges(intervals, bexpr)
+        prog.ranges = ranges
+        prog.bexpr = bexpr
+        if _is(bexpr, "false") or not ranges:
+            prog.empty = True
+        # hidden presence count (slot 0)
+        prog.slots.append((D.S_SUM_I, 0))
+        prog.aops.append({"kind": D.A_COUNT, "col": -1, "expr": None, "filter": None, "slot": 0, "hll": -1})
+        gk = self.granularity_key(granularity, ivs)
+        if gk is not None:
+            prog.keys.append(gk)
+        for dspec in dimensions:
+            prog.keys.append(self.key_for_dimension(dspec, ivs))
+        prog.keys.extend(extra_keys)
+        if len(prog.keys) > D.MAX_KOPS:
+            raise LoweringError("too many grouping keys")
+        for a in aggregations:
+            self.add_aggregator(prog, a)
+        # mixed radix strides (last key fastest)
+        G = 1
+        for kc in reversed(prog.keys):
+            kc.stride = G
+            G *= max(1, kc.card)
+        if G >= 2 ** 62:
+            raise LoweringError("group key space exceeds 64 bits")
+        prog.G = G
+        prog.est_rows = prog.rows_in_ranges * self.selectivity(bexpr)
+        if not prog.empty:
+            depth = self.emit_filter(prog, bexpr) if not _is(bexpr, "true") else 0
+            prog.filter_len = len(prog.fops)
+            if depth > D.STACK_DEPTH:
+                raise LoweringError("filter too deep for the device stack")
+            for d in prog.aops:
+                if d["filter"] is not None:
+                    off = len(prog.fops)
+                    dep = self.emit_filter(prog, d["filter"])
+                    if dep > D.STACK_DEPTH:
+                        raise LoweringError("aggregator filter too deep")
+                    d["filt_off"], d["filt_len"] = off, len(prog.fops) - off
+            for kc in prog.keys:
+                prog.col(kc.col)
+            for d in prog.aops:
+                if d["expr"] is not None:
+                    d["expr_off"] = len(prog.eops)
+                    prog.eops.extend(d["expr"])
+                    d["expr_len"] = len(d["expr"])
+            if len(prog.fops) > D.MAX_FOPS or len(prog.eops) > D.MAX_EOPS:
+                raise LoweringError("query program too large for the device descriptor")
+            self.pick_zones(prog, bexpr)
+        return prog
+
+    def lower_mask(self, intervals, filter_spec) -> ScanProgram:
+        prog = ScanProgram(self.ds)
+        bexpr = self.filter_ir(filter_spec)
+        ranges, bexpr, ivs = self.query_ranges(intervals, bexpr)
+        prog.ranges, prog.bexpr = ranges, bexpr
+        if _is(bexpr, "false") or not ranges:
+            prog.empty = True
+            return prog
+        if not _is(bexpr, "true"):
+            if self.emit_filter(prog, bexpr) > D.STACK_DEPTH:
+                raise LoweringError("filter too deep for the device stack")
+        prog.filter_len = len(prog.fops)
+        self.pick_zones(prog, bexpr)
+        return prog
+
+
+def _depth(x) -> int:
+    if x[0] in ("and", "or"):
+        ds = sorted((_depth(c) for c in x[1]), reverse=True)
+        return max(ds[0], 1 + (ds[1] if len(ds) > 1 else 0))
+    if x[0] == "not":
+        return _depth(x[1])
+    return 1
+
+
+def _runs(mask: np.ndarray) -> List[Tuple[int, int]]:
+    m = np.concatenate([[False], mask.astype(bool), [False]])
+    d = np.diff(m.astype(np.int8))
+    starts = np.flatnonzero(d == 1)
+    ends = np.flatnonzero(d == -1)
+    return list(zip(starts.tolist(), ends.tolist()))
+
+
+def _f2ord(f: float) -> int:
+    b = int(np.array([f], dtype=np.float64).view(np.int64)[0])
+    return b if b >= 0 else b ^ 0x7FFFFFFFFFFFFFFF
+
+
+def ord2f(v: np.ndarray) -> np.ndarray:
+    v = np.asarray(v, dtype=np.int64)
+    b = np.where(v >= 0, v, v ^ np.int64(0x7FFFFFFFFFFFFFFF))
+    return b.view(np.float64)
+
+
+def _salt(col: str) -> int:
+    import zlib
+
+    return zlib.crc32(col.encode()) & 0x7FFFFFFF
+
+
+def _to_ms(v) -> int:
+    if isinstance(v, (int, np.integer)):
+        return int(v)
+    if isinstance(v, float):
+        return int(v)
+    s = str(v)
+    if re.fullmatch(r"-?\d+", s):
+        return int(s)
+    return parse_iso_ms(s)
+
+
+def pack(prog: ScanProgram, mode: int, dedup: int, hll_lds: int, lds_bytes: int, out_acc: int, out_keys: int,
+         hash_cap: int, overflow: int, out_mask: int, out_count: int, hll_ptrs: Sequence[int],
+         hll_lds_offs: Sequence[int]) -> np.ndarray:
+    """Serialize a program into ScanDesc bytes (device pointers are plain integers)."""
+    ds = prog.ds
+    d = D.new_desc()
+    r = d[0]
+    r["ncols"] = len(prog.cols)
+    for i, name in enumerate(prog.cols):
+        t = column_tensor(ds, name)
+        r["cols"][i]["ptr"] = t.data_ptr()
+        r["cols"][i]["dtype"] = dtype_code(t)
+    r["nfops"] = len(prog.fops)
+    r["filter_len"] = prog.filter_len
+    for i, (op, col, flags, lo, hi, flo, fhi, bits) in enumerate(prog.fops):
+        f = r["fops"][i]
+        f["op"], f["col"], f["flags"], f["lo"], f["hi"], f["flo"], f["fhi"] = op, col, flags, lo, hi, flo, fhi
+        f["bits"] = bits.data_ptr() if bits is not None else 0
+    r["nkops"] = len(prog.keys)
+    for i, kc in enumerate(prog.keys):
+        k = r["kops"][i]
+        k["kind"], k["col"], k["tfield"] = kc.kind, prog.col(kc.col), kc.tfield
+        k["stride"], k["base"], k["card"] = kc.stride, kc.base, kc.card
+        k["unit_ms"] = ds.time_unit_ms
+        k["tz_ms"], k["period_ms"], k["origin_ms"] = kc.tz_ms, kc.period_ms or 1, kc.origin_ms
+        if kc.remap is not None:
+            t = getattr(kc, "_remap_dev", None)
+            if t is None or t.device != ds.device:
+                t = torch.from_numpy(kc.remap).to(ds.device)
+                kc._remap_dev = t  # type: ignore[attr-defined]
+            prog.keepalive.append(t)
+            k["remap"] = t.data_ptr()
+    r["naggs"] = len(prog.aops)
+    kind_map = {}
+    for i, a in enumerate(prog.aops):
+        o = r["aops"][i]
+        o["kind"], o["col"], o["slot"] = a["kind"], a["col"], max(a["slot"], 0)
+        o["expr_off"], o["expr_len"] = a.get("expr_off", 0), a.get("expr_len", 0)
+        o["filt_off"], o["filt_len"] = a.get("filt_off", 0), a.get("filt_len", 0)
+        if a["kind"] == D.A_HLL:
+            o["hll_regs"] = hll_ptrs[a["hll"]]
+            o["hll_lds_off"] = hll_lds_offs[a["hll"]] if hll_lds_offs else 0
+            o["salt"] = a.get("salt", 0)
+    r["neops"] = len(prog.eops)
+    for i, (op, col, c) in enumerate(prog.eops):
+        e = r["eops"][i]
+        e["op"], e["col"], e["c"] = op, col, c
+    r["nzones"] = len(prog.zones)
+    for i, (dim, lo, hi) in enumerate(prog.zones):
+        z = r["zones"][i]
+        dc = ds.dims[dim]
+        z["col"], z["lo"], z["hi"] = 0, lo, hi
+        z["zmin"], z["zmax"] = dc.zmin.data_ptr(), dc.zmax.data_ptr()
+    total = 0
+    r["nranges"] = len(prog.ranges)
+    for i, (a, b) in enumerate(prog.ranges):
+        g = r["ranges"][i]
+        c0 = a // CHUNK_ROWS
+        c1 = (b + CHUNK_ROWS - 1) // CHUNK_ROWS
+        g["lo"], g["hi"], g["chunk_begin"], g["nchunks"] = a, b, c0, c1 - c0
+        total += c1 - c0
+    r["total_chunks"] = total
+    r["num_rows"] = ds.num_rows
+    r["nslots"] = len(prog.slots)
+    for i, (op, init) in enumerate(prog.slots):
+        r["slot_op"][i] = op
+        r["slot_init"][i] = init
+    r["mode"], r["dedup"], r["hll_lds"], r["hll_p"], r["nhll"] = mode, dedup, hll_lds, prog.hll_p, prog.nhll
+    r["lds_bytes"] = lds_bytes
+    r["G"] = prog.G
+    r["out_acc"], r["out_keys"], r["hash_cap"], r["overflow"] = out_acc, out_keys, hash_cap, overflow
+    r["out_mask"], r["out_count"] = out_mask, out_count
+    return d

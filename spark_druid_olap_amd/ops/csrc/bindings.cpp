@@ -1,0 +1,118 @@
+// Host-side launchers + pybind11 module for the CDNA4 OLAP kernels.  All device pointers cross
+// the Python boundary as integers (torch.Tensor.data_ptr()) and streams as raw hipStream_t
+// handles (torch.cuda.current_stream().cuda_stream), so this module needs no torch headers and
+// builds in seconds with hipcc.  It must be imported after torch so that the HIP runtime torch
+// loaded (same SONAME) is the one this module binds to.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <stdexcept>
+#include <string>
+#include "scan_desc.h"
+
+namespace sdo {
+template <int U>
+__global__ void olap_scan_kernel(const ScanDesc* __restrict__ d);
+__global__ void bitmap_build_kernel(const void* ids, int dtype, int64_t n, int64_t nwords, uint64_t* out,
+                                    int64_t card);
+__global__ void hll_estimate_kernel(const uint32_t* regs, int64_t G, int p, double* est);
+}  // namespace sdo
+
+namespace py = pybind11;
+
+static void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+static bool g_attr_set[8] = {false};
+
+template <int U>
+static void launch_scan(uint64_t desc, int grid, int block, int lds, hipStream_t s) {
+  if (lds > 65536 && !g_attr_set[U]) {
+    check(hipFuncSetAttribute((const void*)sdo::olap_scan_kernel<U>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024),
+          "hipFuncSetAttribute");
+    g_attr_set[U] = true;
+  }
+  hipLaunchKernelGGL(sdo::olap_scan_kernel<U>, dim3(grid), dim3(block), lds, s, (const sdo::ScanDesc*)desc);
+  check(hipGetLastError(), "olap_scan_kernel launch");
+}
+
+static void scan(uint64_t desc, int grid, int block, int lds, int unroll, uint64_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (block % 64 != 0 || block > 1024 || block <= 0) throw std::invalid_argument("block must be a multiple of 64 <= 1024");
+  if (lds < 0 || lds > 160 * 1024) throw std::invalid_argument("lds bytes out of range");
+  switch (unroll) {
+    case 1: launch_scan<1>(desc, grid, block, lds, s); break;
+    case 2: launch_scan<2>(desc, grid, block, lds, s); break;
+    case 4: launch_scan<4>(desc, grid, block, lds, s); break;
+    default: throw std::invalid_argument("unroll must be 1, 2 or 4");
+  }
+}
+
+static void bitmap_build(uint64_t ids, int dtype, int64_t n, int64_t nwords, uint64_t out, int64_t card,
+                         uint64_t stream) {
+  if (nwords <= 0) return;
+  int64_t blocks = (nwords + 3) / 4;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(sdo::bitmap_build_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     (const void*)ids, dtype, n, nwords, (uint64_t*)out, card);
+  check(hipGetLastError(), "bitmap_build_kernel launch");
+}
+
+static void hll_estimate(uint64_t regs, int64_t G, int p, uint64_t est, uint64_t stream) {
+  if (G <= 0) return;
+  if (p < 4 || p > 18) throw std::invalid_argument("hll precision out of range");
+  const unsigned blocks = (unsigned)((G + 31) / 32);
+  hipLaunchKernelGGL(sdo::hll_estimate_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream,
+                     (const uint32_t*)regs, G, p, (double*)est);
+  check(hipGetLastError(), "hll_estimate_kernel launch");
+}
+
+static int desc_size() { return (int)sizeof(sdo::ScanDesc); }
+
+static py::dict layout() {
+  py::dict d;
+  d["ScanDesc"] = sizeof(sdo::ScanDesc);
+  d["ColRef"] = sizeof(sdo::ColRef);
+  d["FOp"] = sizeof(sdo::FOp);
+  d["KOp"] = sizeof(sdo::KOp);
+  d["AOp"] = sizeof(sdo::AOp);
+  d["EOp"] = sizeof(sdo::EOp);
+  d["ZoneP"] = sizeof(sdo::ZoneP);
+  d["Range"] = sizeof(sdo::Range);
+  d["off_cols"] = offsetof(sdo::ScanDesc, cols);
+  d["off_fops"] = offsetof(sdo::ScanDesc, fops);
+  d["off_kops"] = offsetof(sdo::ScanDesc, kops);
+  d["off_aops"] = offsetof(sdo::ScanDesc, aops);
+  d["off_eops"] = offsetof(sdo::ScanDesc, eops);
+  d["off_zones"] = offsetof(sdo::ScanDesc, zones);
+  d["off_ranges"] = offsetof(sdo::ScanDesc, ranges);
+  d["off_slot_init"] = offsetof(sdo::ScanDesc, slot_init);
+  return d;
+}
+
+static py::dict device_info(int dev) {
+  hipDeviceProp_t p;
+  check(hipGetDeviceProperties(&p, dev), "hipGetDeviceProperties");
+  py::dict d;
+  d["name"] = std::string(p.name);
+  d["gcnArchName"] = std::string(p.gcnArchName);
+  d["multiProcessorCount"] = p.multiProcessorCount;
+  d["sharedMemPerBlock"] = (int64_t)p.sharedMemPerBlock;
+  d["maxSharedMemoryPerMultiProcessor"] = (int64_t)p.maxSharedMemoryPerMultiProcessor;
+  d["totalGlobalMem"] = (int64_t)p.totalGlobalMem;
+  d["l2CacheSize"] = p.l2CacheSize;
+  return d;
+}
+
+PYBIND11_MODULE(_sdo_native, m) {
+  m.doc() = "MI355X (gfx950) OLAP scan kernels";
+  m.def("scan", &scan, "launch the fused scan/filter/group-by kernel", py::arg("desc"), py::arg("grid"),
+        py::arg("block"), py::arg("lds"), py::arg("unroll"), py::arg("stream"));
+  m.def("bitmap_build", &bitmap_build);
+  m.def("hll_estimate", &hll_estimate);
+  m.def("desc_size", &desc_size);
+  m.def("layout", &layout);
+  m.def("device_info", &device_info);
+  m.attr("ARCH") = "gfx950";
+}

@@ -1,0 +1,163 @@
+// Query-program descriptor shared by the host lowering (engine/lower.py builds the identical
+// byte layout with numpy structured dtypes, see ops/desc.py) and the CDNA4 scan kernels.
+//
+// A Druid QuerySpec (reference: src/main/scala/org/sparklinedata/druid/DruidQuerySpec.scala:573-1127)
+// is lowered into ONE of these per (query, GPU).  The kernel is an interpreter over the descriptor:
+// every opcode is wave-uniform, so interpretation costs scalar branches only, and the
+// per-row work is loads + a handful of VALU ops.  The layout is plain-old-data with explicit
+// padding; never reorder fields without updating ops/desc.py (a unit test checks the sizes).
+#pragma once
+#include <stdint.h>
+
+namespace sdo {
+
+constexpr int MAX_COLS = 16;
+constexpr int MAX_FOPS = 48;
+constexpr int MAX_KOPS = 8;
+constexpr int MAX_AOPS = 12;
+constexpr int MAX_EOPS = 64;
+constexpr int MAX_ZONES = 4;
+constexpr int MAX_RANGES = 8;
+constexpr int MAX_SLOTS = 16;
+constexpr int STACK_DEPTH = 6;       // filter / expression register stack depth
+constexpr int CHUNK_ROWS = 4096;     // zone-map granule == scheduling unit (64 words of 64 rows)
+constexpr int CHUNK_WORDS = CHUNK_ROWS / 64;
+
+enum DType : int32_t { DT_U8 = 0, DT_I16 = 1, DT_I32 = 2, DT_I64 = 3, DT_F32 = 4, DT_F64 = 5, DT_U16 = 6 };
+
+// ---- filter opcodes (postfix program; evaluated on 64-bit wave masks, one bit per lane/row) ----
+enum FOpCode : int32_t {
+  F_TRUE = 0,
+  F_BITMAP = 1,     // push inverted-bitmap word: bits + word  (dimension value bitmap index)
+  F_ID_RANGE = 2,   // push lo <= id < hi
+  F_IN_SET = 3,     // push bitset[id]    (dictionary-domain predicate, evaluated once per dict entry)
+  F_INT_RANGE = 4,  // push lo <= v <= hi   (integer / decimal-scaled metric or time)
+  F_FLT_RANGE = 5,  // push flo <= v <= fhi (flags: bit0 lo-strict, bit1 hi-strict)
+  F_AND = 6,
+  F_OR = 7,
+  F_NOT = 8,
+  F_FALSE = 9,
+  F_BITMAP_OR = 10  // push OR of `hi` consecutive bitmap rows starting at bits (stride lo words)
+};
+
+struct ColRef {
+  uint64_t ptr;
+  int32_t dtype;
+  int32_t pad;
+};
+
+struct FOp {
+  int32_t op;
+  int32_t col;
+  int32_t flags;
+  int32_t pad;
+  int64_t lo;
+  int64_t hi;
+  double flo;
+  double fhi;
+  uint64_t bits;
+};
+
+// ---- group-key components: key = sum(component * stride) ----
+enum KKind : int32_t { K_ID = 0, K_REMAP = 1, K_TIME = 2, K_INT = 3 };
+enum TField : int32_t {
+  T_MS = 0, T_SECOND = 1, T_MINUTE = 2, T_HOUR = 3, T_DAY = 4, T_WEEK = 5, T_MONTH = 6,
+  T_QUARTER = 7, T_YEAR = 8, T_MOY = 9, T_DOM = 10, T_DOW = 11, T_HOD = 12, T_MOH = 13,
+  T_DOY = 14, T_SOM = 15, T_QOY = 16, T_PERIOD = 17
+};
+
+struct KOp {
+  int32_t kind;
+  int32_t col;
+  int32_t tfield;
+  int32_t pad;
+  int64_t stride;
+  int64_t base;
+  int64_t card;
+  int64_t unit_ms;    // time column storage unit
+  int64_t tz_ms;      // fixed timezone offset applied before bucketing
+  int64_t period_ms;  // T_PERIOD
+  int64_t origin_ms;  // T_PERIOD
+  uint64_t remap;     // int32 table for K_REMAP (dictionary-domain derived key)
+};
+
+// ---- aggregators ----
+enum AKind : int32_t {
+  A_COUNT = 0, A_SUM_I = 1, A_SUM_F = 2, A_MIN_I = 3, A_MAX_I = 4, A_MIN_F = 5, A_MAX_F = 6, A_HLL = 7
+};
+// accumulator slot update ops
+enum SlotOp : int32_t { S_SUM_I = 0, S_SUM_F = 1, S_MIN_I = 2, S_MAX_I = 3 };
+
+struct AOp {
+  int32_t kind;
+  int32_t col;        // input column (or -1 when expr_len > 0)
+  int32_t expr_off;   // expression program (float VM) offset into eops
+  int32_t expr_len;
+  int32_t filt_off;   // per-aggregator filter program (Druid "filtered" aggregator)
+  int32_t filt_len;
+  int32_t slot;       // accumulator slot (non-HLL)
+  int32_t hll_lds_off;// byte offset of this HLL's registers in LDS (when desc.hll_lds)
+  uint64_t hll_regs;  // global u32 registers [groups][1<<hll_p]
+  int64_t salt;
+};
+
+enum EOpCode : int32_t {
+  E_COL = 0, E_CONST = 1, E_ADD = 2, E_SUB = 3, E_MUL = 4, E_DIV = 5, E_NEG = 6, E_ABS = 7,
+  E_MIN = 8, E_MAX = 9
+};
+struct EOp {
+  int32_t op;
+  int32_t col;
+  double c;
+};
+
+struct ZoneP {
+  int32_t col;
+  int32_t pad;
+  int64_t lo;    // zone survives iff zmax >= lo && zmin < hi
+  int64_t hi;
+  uint64_t zmin; // int32 per chunk
+  uint64_t zmax;
+};
+
+struct Range {
+  int64_t lo;
+  int64_t hi;
+  int64_t chunk_begin;  // first absolute chunk index of this range
+  int64_t nchunks;
+};
+
+enum Mode : int32_t { M_DENSE_LDS = 0, M_DENSE_GLOBAL = 1, M_HASH = 2, M_MASK = 3 };
+
+struct ScanDesc {
+  int32_t ncols, nfops, nkops, naggs;
+  int32_t neops, nranges, nzones, nslots;
+  int32_t mode;
+  int32_t dedup;
+  int32_t hll_lds;
+  int32_t hll_p;
+  int32_t nhll;
+  int32_t lds_bytes;
+  int32_t filter_len;   // main filter program = fops[0 .. filter_len)
+  int32_t pad0;
+  int64_t G;            // dense groups
+  int64_t total_chunks;
+  int64_t num_rows;
+  uint64_t out_acc;     // u64 [G or cap][nslots]
+  uint64_t out_keys;    // u64 [cap]   (hash mode)
+  int64_t hash_cap;     // power of two
+  uint64_t overflow;    // int32 flag (hash mode)
+  uint64_t out_mask;    // u64 per 64-row word (mask mode)
+  uint64_t out_count;   // u64 rows passing (mask mode)
+  int64_t slot_init[MAX_SLOTS];
+  int32_t slot_op[MAX_SLOTS];
+  ColRef cols[MAX_COLS];
+  FOp fops[MAX_FOPS];
+  KOp kops[MAX_KOPS];
+  AOp aops[MAX_AOPS];
+  EOp eops[MAX_EOPS];
+  ZoneP zones[MAX_ZONES];
+  Range ranges[MAX_RANGES];
+};
+
+}  // namespace sdo

@@ -1,0 +1,311 @@
+"""Plain-PyTorch executor of a ``ScanProgram`` -- the CPU backend and the numerics oracle for the
+HIP scan kernel (tests compare the two on the same shard).
+
+It evaluates the same normalized filter IR, group keys, accumulator slots and HLL hashing as
+``ops/csrc/olap_scan.hip`` with vectorized torch ops (no interpretation per row), producing the
+same partial structures (dense ``[G, nslots]`` or sparse keys + accumulators).
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import desc as D
+
+_C1 = 0xFF51AFD7ED558CCD - (1 << 64)
+_C2 = 0xC4CEB9FE1A85EC53 - (1 << 64)
+
+
+def _lsr(x: torch.Tensor, s: int) -> torch.Tensor:
+    """logical shift right of int64 bit patterns"""
+    if s == 0:
+        return x
+    return (x >> s) & ((1 << (64 - s)) - 1)
+
+
+def mix64(x: torch.Tensor) -> torch.Tensor:
+    x = x ^ _lsr(x, 33)
+    x = x * _C1
+    x = x ^ _lsr(x, 33)
+    x = x * _C2
+    x = x ^ _lsr(x, 33)
+    return x
+
+
+def clz64(x: torch.Tensor) -> torch.Tensor:
+    n = torch.zeros_like(x)
+    for s in (32, 16, 8, 4, 2, 1):
+        top = _lsr(x, 64 - s) == 0
+        n = torch.where(top, n + s, n)
+        x = torch.where(top, x << s, x)
+    return n
+
+
+def hll_update_values(vals: torch.Tensor, salt: int, p: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(bucket, rho) per value, bit-identical to the kernel's hashing."""
+    h = mix64(vals.to(torch.int64) ^ int(salt))
+    bucket = _lsr(h, 64 - p)
+    rest = (h << p) | (1 << (p - 1))
+    rho = clz64(rest) + 1
+    return bucket, rho
+
+
+def hll_estimate_torch(regs: torch.Tensor, p: int) -> torch.Tensor:
+    """regs [G, m] int -> estimates [G] float64 (same formula as hll_estimate_kernel)."""
+    m = float(1 << p)
+    r = regs.to(torch.float64)
+    s = torch.pow(2.0, -r).sum(dim=1)
+    zeros = (regs == 0).sum(dim=1).to(torch.float64)
+    alpha = 0.7213 / (1.0 + 1.079 / m)
+    e = alpha * m * m / s
+    lin = m * torch.log(m / torch.clamp(zeros, min=1.0))
+    return torch.where((e <= 2.5 * m) & (zeros > 0), lin, e)
+
+
+def _col(prog, name: str) -> torch.Tensor:
+    from ..engine.lower import column_tensor
+
+    return column_tensor(prog.ds, name)
+
+
+def _rows(prog) -> torch.Tensor:
+    parts = [torch.arange(a, b, dtype=torch.int64, device=prog.ds.device) for a, b in prog.ranges]
+    return torch.cat(parts) if parts else torch.zeros(0, dtype=torch.int64, device=prog.ds.device)
+
+
+def eval_bexpr(prog, x, rows: torch.Tensor) -> torch.Tensor:
+    k = x[0]
+    n = rows.numel()
+    dev = rows.device
+    if k == "true":
+        return torch.ones(n, dtype=torch.bool, device=dev)
+    if k == "false":
+        return torch.zeros(n, dtype=torch.bool, device=dev)
+    if k == "and":
+        out = torch.ones(n, dtype=torch.bool, device=dev)
+        for c in x[1]:
+            out &= eval_bexpr(prog, c, rows)
+        return out
+    if k == "or":
+        out = torch.zeros(n, dtype=torch.bool, device=dev)
+        for c in x[1]:
+            out |= eval_bexpr(prog, c, rows)
+        return out
+    if k == "not":
+        return ~eval_bexpr(prog, x[1], rows)
+    if k == "ids":
+        ids = _col(prog, x[1])[rows].to(torch.int64)
+        m = torch.from_numpy(np.ascontiguousarray(x[2])).to(dev)
+        return m[ids]
+    if k == "time":
+        u = prog.ds.time_unit_ms
+        t = prog.ds.time[rows].to(torch.int64)
+        lo = -(-x[1] // u)
+        hi = -(-x[2] // u)
+        return (t >= lo) & (t < hi)
+    if k == "timeset":
+        t = prog.ds.time[rows].to(torch.int64)
+        allowed = torch.from_numpy(np.asarray(x[1], dtype=np.int64)).to(dev)
+        return torch.isin(t, allowed)
+    if k == "int":
+        v = _col(prog, x[1])[rows].to(torch.int64)
+        return (v >= x[2]) & (v <= x[3])
+    if k == "flt":
+        v = _col(prog, x[1])[rows].to(torch.float64)
+        lo_ok = v > x[2] if x[4] & 1 else v >= x[2]
+        hi_ok = v < x[3] if x[4] & 2 else v <= x[3]
+        return lo_ok & hi_ok
+    raise ValueError(k)
+
+
+def _time_field(ms: torch.Tensor, kc) -> torch.Tensor:
+    from ..query import granularity as Gr
+
+    tf = kc.tfield
+    ms = ms + kc.tz_ms
+    fd = lambda a, b: torch.div(a, b, rounding_mode="floor")  # noqa: E731
+    if tf == Gr.T_MS:
+        return ms
+    if tf == Gr.T_SECOND:
+        return fd(ms, 1000)
+    if tf == Gr.T_MINUTE:
+        return fd(ms, 60_000)
+    if tf == Gr.T_HOUR:
+        return fd(ms, 3_600_000)
+    if tf == Gr.T_DAY:
+        return fd(ms, 86_400_000)
+    if tf == Gr.T_WEEK:
+        return fd(fd(ms, 86_400_000) + 3, 7)
+    if tf == Gr.T_PERIOD:
+        return fd(ms - kc.origin_ms, kc.period_ms)
+    if tf == Gr.T_HOD:
+        return fd(ms, 3_600_000) - fd(ms, 86_400_000) * 24
+    if tf == Gr.T_MOH:
+        return fd(ms, 60_000) - fd(ms, 3_600_000) * 60
+    if tf == Gr.T_SOM:
+        return fd(ms, 1000) - fd(ms, 60_000) * 60
+    days = fd(ms, 86_400_000)
+    if tf == Gr.T_DOW:
+        return torch.remainder(days + 3, 7) + 1
+    z = days + 719468
+    era = fd(z, 146097)
+    doe = z - era * 146097
+    yoe = torch.div(doe - torch.div(doe, 1460, rounding_mode="trunc") + torch.div(doe, 36524, rounding_mode="trunc")
+                    - torch.div(doe, 146096, rounding_mode="trunc"), 365, rounding_mode="trunc")
+    y = yoe + era * 400
+    doy = doe - (365 * yoe + torch.div(yoe, 4, rounding_mode="trunc") - torch.div(yoe, 100, rounding_mode="trunc"))
+    mp = torch.div(5 * doy + 2, 153, rounding_mode="trunc")
+    d = doy - torch.div(153 * mp + 2, 5, rounding_mode="trunc") + 1
+    m = torch.where(mp < 10, mp + 3, mp - 9)
+    y = y + (m <= 2).to(torch.int64)
+    if tf == Gr.T_MONTH:
+        return y * 12 + (m - 1)
+    if tf == Gr.T_QUARTER:
+        return y * 4 + torch.div(m - 1, 3, rounding_mode="trunc")
+    if tf == Gr.T_YEAR:
+        return y
+    if tf == Gr.T_MOY:
+        return m
+    if tf == Gr.T_DOM:
+        return d
+    if tf == Gr.T_QOY:
+        return torch.div(m - 1, 3, rounding_mode="trunc") + 1
+    if tf == Gr.T_DOY:
+        from ..query.intervals import days_from_civil
+
+        yy = y.cpu().numpy()
+        jan1 = torch.from_numpy(np.array([days_from_civil(int(a), 1, 1) for a in yy], dtype=np.int64)).to(ms.device)
+        return days - jan1 + 1
+    raise ValueError(tf)
+
+
+def compute_keys(prog, rows: torch.Tensor) -> torch.Tensor:
+    key = torch.zeros(rows.numel(), dtype=torch.int64, device=rows.device)
+    for kc in prog.keys:
+        v = _col(prog, kc.col)[rows].to(torch.int64)
+        if kc.kind == D.K_REMAP:
+            rm = torch.from_numpy(kc.remap.astype(np.int64)).to(rows.device)
+            v = rm[v]
+        elif kc.kind == D.K_TIME:
+            v = _time_field(v * prog.ds.time_unit_ms, kc) - kc.base
+            v = v.clamp(0, kc.card - 1)
+        elif kc.kind == D.K_INT:
+            v = (v - kc.base).clamp(0, kc.card - 1)
+        key += v * kc.stride
+    return key
+
+
+def _expr_values(prog, eops, rows: torch.Tensor) -> torch.Tensor:
+    st: List[torch.Tensor] = []
+    for op, col, c in eops:
+        if op == D.E_COL:
+            v = _col(prog, prog.cols[col])[rows].to(torch.float64)
+            st.append(v * c if c != 0.0 else v)
+        elif op == D.E_CONST:
+            st.append(torch.full((rows.numel(),), c, dtype=torch.float64, device=rows.device))
+        elif op == D.E_NEG:
+            st[-1] = -st[-1]
+        elif op == D.E_ABS:
+            st[-1] = st[-1].abs()
+        else:
+            b = st.pop()
+            a = st.pop()
+            st.append({D.E_ADD: a + b, D.E_SUB: a - b, D.E_MUL: a * b, D.E_DIV: a / b,
+                       D.E_MIN: torch.minimum(a, b), D.E_MAX: torch.maximum(a, b)}[op])
+    return st[-1]
+
+
+def _agg_values(prog, a, rows: torch.Tensor) -> torch.Tensor:
+    """int64 payload per row for an aggregator (float kinds: f64 bits / ordered ints)."""
+    k = a["kind"]
+    if k == D.A_COUNT:
+        return torch.ones(rows.numel(), dtype=torch.int64, device=rows.device)
+    if k in (D.A_SUM_F, D.A_MIN_F, D.A_MAX_F):
+        if a.get("expr"):
+            f = _expr_values(prog, a["expr"], rows)
+        else:
+            f = _col(prog, prog.cols[a["col"]])[rows].to(torch.float64)
+        if k == D.A_SUM_F:
+            return f
+        b = f.view(torch.int64)
+        return torch.where(b >= 0, b, b ^ 0x7FFFFFFFFFFFFFFF)
+    v = _col(prog, prog.cols[a["col"]])[rows]
+    if v.dtype.is_floating_point:
+        v = v.to(torch.float64).trunc()
+    return v.to(torch.int64)
+
+
+def run_reference(prog, sparse: Optional[bool] = None):
+    """Execute a program with torch.  Returns (kind, keys, acc, hll_list)."""
+    from ..engine.partials import Partials
+
+    ds = prog.ds
+    dev = ds.device
+    m = 1 << prog.hll_p
+    nslots = prog.nslots
+    if sparse is None:
+        sparse = prog.G > (1 << 22)
+    rows = _rows(prog) if not prog.empty else torch.zeros(0, dtype=torch.int64, device=dev)
+    mask = eval_bexpr(prog, prog.bexpr, rows) if rows.numel() else torch.zeros(0, dtype=torch.bool, device=dev)
+    rows = rows[mask]
+    key = compute_keys(prog, rows)
+    if sparse:
+        uk, inv = torch.unique(key, return_inverse=True)
+        R = uk.numel()
+        idx = inv
+    else:
+        R = prog.G
+        idx = key
+    acc = torch.empty((R, nslots), dtype=torch.int64, device=dev)
+    for s, (op, init) in enumerate(prog.slots):
+        acc[:, s] = init
+    for a in prog.aops:
+        if a["kind"] == D.A_HLL:
+            continue
+        amask = torch.ones(rows.numel(), dtype=torch.bool, device=dev)
+        if a.get("filter") is not None:
+            amask = eval_bexpr(prog, a["filter"], rows)
+        r, ix = rows[amask], idx[amask]
+        vals = _agg_values(prog, a, r)
+        s = a["slot"]
+        op = prog.slots[s][0]
+        col = acc[:, s].clone()
+        if op == D.S_SUM_I:
+            col.index_add_(0, ix, vals)
+        elif op == D.S_SUM_F:
+            cf = col.view(torch.float64).clone()
+            cf.index_add_(0, ix, vals)
+            col = cf.view(torch.int64)
+        elif op == D.S_MIN_I:
+            col.scatter_reduce_(0, ix, vals, reduce="amin", include_self=True)
+        else:
+            col.scatter_reduce_(0, ix, vals, reduce="amax", include_self=True)
+        acc[:, s] = col
+    hlls = []
+    for a in prog.aops:
+        if a["kind"] != D.A_HLL:
+            continue
+        amask = torch.ones(rows.numel(), dtype=torch.bool, device=dev)
+        if a.get("filter") is not None:
+            amask = eval_bexpr(prog, a["filter"], rows)
+        r, ix = rows[amask], idx[amask]
+        v = _col(prog, prog.cols[a["col"]])[r].to(torch.int64)
+        bucket, rho = hll_update_values(v, a.get("salt", 0), prog.hll_p)
+        regs = torch.zeros(R * m, dtype=torch.int64, device=dev)
+        regs.scatter_reduce_(0, ix * m + bucket, rho, reduce="amax", include_self=True)
+        hlls.append(regs.view(R, m).to(torch.int32))
+    if sparse:
+        return Partials("sparse", acc, uk, hlls)
+    return Partials("dense", acc, None, hlls)
+
+
+def run_reference_mask(prog) -> torch.Tensor:
+    """Row ids passing the filter (select queries)."""
+    dev = prog.ds.device
+    if prog.empty:
+        return torch.zeros(0, dtype=torch.int64, device=dev)
+    rows = _rows(prog)
+    return rows[eval_bexpr(prog, prog.bexpr, rows)]

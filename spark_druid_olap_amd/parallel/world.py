@@ -1,0 +1,139 @@
+"""Process-group abstraction: one process per GPU, torch.distributed over RCCL ("nccl" backend
+on ROCm) for device tensors, gloo for CPU tests.
+
+The reference scatters queries to Druid historicals over HTTP and merges on the broker or in a
+Spark shuffle (``sd/DruidRDD.scala:62-99``, ``asd/PostAggregate.scala:97-103``); here every rank
+owns a shard of every datasource in HBM and ranks merge partial aggregates with collectives
+over xGMI (see ``parallel/merge.py``).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Any, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class World:
+    rank: int = 0
+    size: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+    group: Any = None
+
+    @property
+    def distributed(self) -> bool:
+        return self.size > 1
+
+    @property
+    def is_root(self) -> bool:
+        return self.rank == 0
+
+    def device(self) -> torch.device:
+        if torch.cuda.is_available() and self.backend != "gloo":
+            return torch.device("cuda", self.local_rank % max(1, torch.cuda.device_count()))
+        return torch.device("cpu")
+
+    # ---------------------------------------------------------------- collectives
+    def barrier(self):
+        if self.distributed:
+            if self.backend == "nccl":
+                dist.barrier(group=self.group, device_ids=[self.local_rank])
+            else:
+                dist.barrier(group=self.group)
+
+    def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        if not self.distributed:
+            return t
+        o = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+        dist.all_reduce(t, op=o, group=self.group)
+        return t
+
+    def all_gather_tensor(self, t: torch.Tensor) -> torch.Tensor:
+        """[size, *t.shape] stacked gather (same shape on every rank)."""
+        if not self.distributed:
+            return t.unsqueeze(0)
+        out = torch.empty((self.size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        return out
+
+    def all_gather_varlen(self, t: torch.Tensor) -> List[torch.Tensor]:
+        """Gather tensors whose first dimension differs per rank."""
+        if not self.distributed:
+            return [t]
+        n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+        ns = self.all_gather_tensor(n).flatten().tolist()
+        mx = max(ns) if ns else 0
+        pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        if t.shape[0]:
+            pad[: t.shape[0]] = t
+        g = self.all_gather_tensor(pad)
+        return [g[i, : ns[i]] for i in range(self.size)]
+
+    def broadcast_object(self, obj: Any, src: int = 0) -> Any:
+        if not self.distributed:
+            return obj
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=src, group=self.group)
+        return lst[0]
+
+    def max_float(self, x: float) -> float:
+        if not self.distributed:
+            return x
+        dev = self.device()
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return float(t.item())
+
+
+_WORLD: Optional[World] = None
+
+
+def init_world(backend: Optional[str] = None, timeout_s: int = 600) -> World:
+    """Initialise from torchrun env vars (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*)."""
+    global _WORLD
+    size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if size <= 1:
+        _WORLD = World(0, 1, local, "none")
+        return _WORLD
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(local % torch.cuda.device_count())
+    if not dist.is_initialized():
+        kw = {}
+        if backend == "nccl":
+            kw["device_id"] = torch.device("cuda", local % torch.cuda.device_count())
+        dist.init_process_group(backend=backend, rank=rank, world_size=size,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    _WORLD = World(rank, size, local, backend, None)
+    return _WORLD
+
+
+def get_world() -> World:
+    global _WORLD
+    if _WORLD is None:
+        if dist.is_available() and dist.is_initialized():
+            b = dist.get_backend()
+            _WORLD = World(dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", dist.get_rank())), b)
+        else:
+            _WORLD = World()
+    return _WORLD
+
+
+def set_world(w: World) -> None:
+    global _WORLD
+    _WORLD = w
+
+
+def shutdown() -> None:
+    global _WORLD
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+    _WORLD = None
