@@ -27,6 +27,7 @@ LDS_BUDGET = int(os.environ.get("SDO_LDS_BUDGET", 64 * 1024))
 DENSE_GLOBAL_MAX_BYTES = int(os.environ.get("SDO_DENSE_MAX_BYTES", 1 << 30))
 BLOCK = 512
 UNROLL = int(os.environ.get("SDO_UNROLL", "2"))
+BLOCKS_PER_CU = int(os.environ.get("SDO_BLOCKS_PER_CU", "3"))
 
 _cu_cache = {}
 
@@ -49,7 +50,7 @@ class PreparedScan:
         self.dev = ds.device
         self.m = 1 << prog.hll_p
         G, ns = prog.G, prog.nslots
-        acc_bytes = G * ns * 8
+        acc_bytes = G * ns * 8 * (BLOCK // 64)  # one private copy per wave
         hll_bytes = prog.nhll * G * self.m * 4
         self.hll_lds = 0
         if mode is None:
@@ -78,6 +79,8 @@ class PreparedScan:
 
     # ------------------------------------------------------------------ buffers
     def _alloc(self):
+        from .lower import lds_layout
+
         prog, dev = self.prog, self.dev
         rows = self.cap if self.mode == D.M_HASH else prog.G
         self.rows = rows
@@ -87,21 +90,23 @@ class PreparedScan:
         self.hll = [torch.empty(rows * self.m, dtype=torch.int32, device=dev) for _ in range(prog.nhll)]
         self.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
         hll_offs = []
-        off = prog.G * prog.nslots * 8
+        off = prog.G * prog.nslots * 8 * (BLOCK // 64)
         for _ in range(prog.nhll):
             hll_offs.append(off)
             off += prog.G * self.m * 4
+        cache_off, wave_bytes, _, total = lds_layout(prog, self.lds, UNROLL, BLOCK // 64)
+        if total > 160 * 1024 and self.mode == D.M_DENSE_LDS:
+            # accumulators + staging planes exceed the CU's LDS: accumulate in HBM instead
+            self.mode, self.lds, self.hll_lds = D.M_DENSE_GLOBAL, 0, 0
+            cache_off, wave_bytes, _, total = lds_layout(prog, 0, UNROLL, BLOCK // 64)
+        if total > 160 * 1024:
+            raise RuntimeError(f"query needs {total} bytes of LDS staging; reduce SDO_UNROLL")
         d = pack(prog, self.mode, self.dedup, self.hll_lds, self.lds, self.acc.data_ptr(), self.keys.data_ptr(),
-                 self.cap, self.overflow.data_ptr(), 0, 0, [h.data_ptr() for h in self.hll], hll_offs)
+                 self.cap, self.overflow.data_ptr(), 0, 0, [h.data_ptr() for h in self.hll], hll_offs,
+                 unroll=UNROLL, cache_off=cache_off, wave_bytes=wave_bytes)
+        self.lds_total = total
         self.desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
-        cus = num_cus(dev)
-        waves = BLOCK // 64
-        need = max(1, (int(d[0]["total_chunks"]) + waves - 1) // waves)
-        if self.mode == D.M_DENSE_LDS and self.lds > 0:
-            per_cu = max(1, min(2, (160 * 1024) // max(self.lds, 1)))
-        else:
-            per_cu = 2
-        self.grid = max(1, min(need, cus * per_cu))
+        self.grid = _grid(dev, int(d[0]["total_chunks"]), total)
 
     def _reset(self):
         self.acc.copy_(self.init_row.expand_as(self.acc))
@@ -118,7 +123,7 @@ class PreparedScan:
             return self._empty()
         while True:
             self._reset()
-            native.scan(self.desc, self.grid, BLOCK, self.lds, UNROLL)
+            native.scan(self.desc, self.grid, BLOCK, self.lds_total, UNROLL)
             if self.mode != D.M_HASH:
                 break
             if int(self.overflow.item()) == 0:
@@ -142,16 +147,19 @@ class PreparedMask:
     """Filter-only scan: writes one u64 mask word per 64 rows (select queries)."""
 
     def __init__(self, prog: ScanProgram):
+        from .lower import lds_layout
+
         self.prog = prog
         ds = prog.ds
         self.dev = ds.device
         self.mask = torch.zeros(ds.nwords, dtype=torch.int64, device=self.dev)
         self.count = torch.zeros(1, dtype=torch.int64, device=self.dev)
-        d = pack(prog, D.M_MASK, 0, 0, 0, 0, 0, 0, 0, self.mask.data_ptr(), self.count.data_ptr(), [], [])
+        cache_off, wave_bytes, _, total = lds_layout(prog, 0, UNROLL, BLOCK // 64)
+        d = pack(prog, D.M_MASK, 0, 0, 0, 0, 0, 0, 0, self.mask.data_ptr(), self.count.data_ptr(), [], [],
+                 unroll=UNROLL, cache_off=cache_off, wave_bytes=wave_bytes)
+        self.lds_total = total
         self.desc = torch.from_numpy(d.view(np.uint8).copy()).to(self.dev)
-        waves = BLOCK // 64
-        need = max(1, (int(d[0]["total_chunks"]) + waves - 1) // waves)
-        self.grid = max(1, min(need, num_cus(self.dev) * 4))
+        self.grid = _grid(self.dev, int(d[0]["total_chunks"]), total)
 
     def run(self) -> torch.Tensor:
         """Row ids passing the filter (sorted)."""
@@ -159,7 +167,7 @@ class PreparedMask:
             return torch.zeros(0, dtype=torch.int64, device=self.dev)
         self.mask.zero_()
         self.count.zero_()
-        native.scan(self.desc, self.grid, BLOCK, 0, UNROLL)
+        native.scan(self.desc, self.grid, BLOCK, self.lds_total, UNROLL)
         nzw = torch.nonzero(self.mask).flatten()
         if nzw.numel() == 0:
             return nzw
@@ -167,3 +175,11 @@ class PreparedMask:
         bits = (words.unsqueeze(1) >> torch.arange(64, device=self.dev)) & 1
         r, c = torch.nonzero(bits, as_tuple=True)
         return nzw[r] * 64 + c
+
+
+def _grid(dev: torch.device, total_chunks: int, lds_total: int) -> int:
+    """Persistent grid: enough 8-wave blocks for the chunks, at most what the CUs hold at once."""
+    waves = BLOCK // 64
+    need = max(1, (total_chunks + waves - 1) // waves)
+    per_cu = max(1, min(BLOCKS_PER_CU, (160 * 1024) // max(lds_total, 1)))
+    return max(1, min(need, num_cus(dev) * per_cu))

@@ -128,10 +128,18 @@ class PreparedQuery:
         qt = self.qs.queryType
         if qt in ("groupBy", "timeseries", "topN"):
             _, prog, prep = self.scans[0]
-            part = self._merged(prog, prep)
+            part = self._scan(prog, prep)
+            t1 = time.perf_counter()
+            disjoint = bool(self.ds.shard_key) and any(k.col == self.ds.shard_key for k in prog.keys)
+            part = merge_partials(self.world, prog, part, disjoint_keys=disjoint)
+            t2 = time.perf_counter()
             cols = finalize(prog, part)
+            t3 = time.perf_counter()
             self._theta(prog, cols)
             res = self._post(prog, cols)
+            t4 = time.perf_counter()
+            res.stats.update(scan_ms=(t1 - t0) * 1e3, merge_ms=(t2 - t1) * 1e3, finalize_ms=(t3 - t2) * 1e3,
+                             post_ms=(t4 - t3) * 1e3)
         elif qt == "search":
             res = self._search()
         else:

@@ -242,6 +242,7 @@ class KeyComp:
     decoder: Optional[Callable[[np.ndarray], np.ndarray]] = None
     collapse: bool = False        # decoded values may coincide: re-aggregate on host
     is_timestamp: bool = False    # granularity bucket (output 'timestamp' ms)
+    col_idx: int = -1             # descriptor column index (payload section)
 
 
 @dataclass
@@ -258,9 +259,15 @@ class AggOut:
 @dataclass
 class ScanProgram:
     ds: DataSource
-    cols: List[str] = field(default_factory=list)
+    fcols: List[str] = field(default_factory=list)      # filter-phase columns -> desc.cols[0..8)
+    pcols: List[str] = field(default_factory=list)      # payload columns      -> desc.cols[8..24)
+    section: str = "p"                                  # where col() registers
     fops: List[tuple] = field(default_factory=list)     # (op, col, flags, lo, hi, flo, fhi, bits_tensor)
     filter_len: int = 0
+    pre_off: int = 0
+    pre_len: int = 0
+    final_pre: bool = False
+    bm_leaves: List[Tuple[torch.Tensor, int, int]] = field(default_factory=list)  # (first row, stride, count)
     keys: List[KeyComp] = field(default_factory=list)
     aops: List[dict] = field(default_factory=list)
     eops: List[tuple] = field(default_factory=list)
@@ -279,11 +286,31 @@ class ScanProgram:
     thetas: List[Tuple[str, str, int]] = field(default_factory=list)  # (name, column, size)
 
     def col(self, name: str) -> int:
-        if name not in self.cols:
-            if len(self.cols) >= D.MAX_COLS:
-                raise LoweringError("too many columns referenced by one query")
-            self.cols.append(name)
-        return self.cols.index(name)
+        """Absolute descriptor column index of `name` in the current section."""
+        if self.section == "f":
+            if name not in self.fcols:
+                if len(self.fcols) >= D.PAYLOAD_BASE:
+                    raise LoweringError("too many filter columns in one query")
+                self.fcols.append(name)
+            return self.fcols.index(name)
+        if name not in self.pcols:
+            if len(self.pcols) >= D.MAX_COLS - D.PAYLOAD_BASE:
+                raise LoweringError("too many payload columns in one query")
+            self.pcols.append(name)
+        return D.PAYLOAD_BASE + self.pcols.index(name)
+
+    def colname(self, idx: int) -> str:
+        return self.fcols[idx] if idx < D.PAYLOAD_BASE else self.pcols[idx - D.PAYLOAD_BASE]
+
+    @property
+    def cols(self) -> List[str]:
+        return self.fcols + self.pcols
+
+    def bm_leaf(self, row: torch.Tensor, stride: int, count: int) -> int:
+        if len(self.bm_leaves) >= D.MAX_BM:
+            raise LoweringError("too many bitmap leaves")
+        self.bm_leaves.append((row, stride, count))
+        return len(self.bm_leaves) - 1
 
     @property
     def nslots(self) -> int:
@@ -544,6 +571,39 @@ class Lowerer:
             return 1
         raise LoweringError(f"bad filter IR {k}")
 
+    def bitmap_plan(self, dim: str, mask: np.ndarray):
+        """(negate, runs) when the id set is cheap as OR of inverted-bitmap rows, else None."""
+        dc = self.ds.dims.get(dim)
+        if dc is None or dc.bitmap is None:
+            return None
+        k = int(mask.sum())
+        if k == 0 or k == len(mask):
+            return None
+        for use_neg, rr in ((False, _runs(mask)), (True, _runs(~mask))):
+            if len(rr) <= self.bitmap_max_values and sum(b - a for a, b in rr) <= 64:
+                return (use_neg, rr)
+        return None
+
+    def bitmap_only(self, x) -> int:
+        """number of bitmap leaves x needs if it is evaluable from bitmaps alone, else -1"""
+        k = x[0]
+        if k in ("true", "false"):
+            return 0
+        if k in ("and", "or"):
+            tot = 0
+            for c in x[1]:
+                n = self.bitmap_only(c)
+                if n < 0:
+                    return -1
+                tot += n
+            return tot
+        if k == "not":
+            return self.bitmap_only(x[1])
+        if k == "ids":
+            plan = self.bitmap_plan(x[1], x[2])
+            return -1 if plan is None else len(plan[1])
+        return -1
+
     def _emit_ids(self, prog: ScanProgram, dim: str, mask: np.ndarray) -> int:
         dc = self.ds.dims[dim]
         card = len(mask)
@@ -556,21 +616,18 @@ class Lowerer:
             return 1
         runs = _runs(mask)
         neg_runs = _runs(~mask)
-        if dc.bitmap is not None:
-            for use_neg, rr in ((False, runs), (True, neg_runs)):
-                if len(rr) <= self.bitmap_max_values and sum(b - a for a, b in rr) <= 64:
-                    nw = dc.bitmap.shape[1]
-                    for j, (a, b) in enumerate(rr):
-                        row = dc.bitmap[a]
-                        if b - a == 1:
-                            prog.fops.append((D.F_BITMAP, 0, 0, 0, 0, 0.0, 0.0, row))
-                        else:
-                            prog.fops.append((D.F_BITMAP_OR, 0, 0, nw, b - a, 0.0, 0.0, row))
-                        if j:
-                            prog.fops.append((D.F_OR, 0, 0, 0, 0, 0.0, 0.0, None))
-                    if use_neg:
-                        prog.fops.append((D.F_NOT, 0, 0, 0, 0, 0.0, 0.0, None))
-                    return 2 if len(rr) > 1 else 1
+        plan = self.bitmap_plan(dim, mask)
+        if plan is not None and len(prog.bm_leaves) + len(plan[1]) <= D.MAX_BM:
+            use_neg, rr = plan
+            nw = dc.bitmap.shape[1]
+            for j, (a, b) in enumerate(rr):
+                leaf = prog.bm_leaf(dc.bitmap[a], nw, b - a)
+                prog.fops.append((D.F_BITMAP, 0, 0, leaf, 0, 0.0, 0.0, None))
+                if j:
+                    prog.fops.append((D.F_OR, 0, 0, 0, 0, 0.0, 0.0, None))
+            if use_neg:
+                prog.fops.append((D.F_NOT, 0, 0, 0, 0, 0.0, 0.0, None))
+            return 2 if len(rr) > 1 else 1
         ci = prog.col(dim)
         if len(runs) == 1:
             prog.fops.append((D.F_ID_RANGE, ci, 0, runs[0][0], runs[0][1], 0.0, 0.0, None))
@@ -579,11 +636,8 @@ class Lowerer:
             prog.fops.append((D.F_ID_RANGE, ci, 0, neg_runs[0][0], neg_runs[0][1], 0.0, 0.0, None))
             prog.fops.append((D.F_NOT, 0, 0, 0, 0, 0.0, 0.0, None))
             return 1
-        nbits = (card + 63) // 64 * 64
-        bits = np.zeros(nbits, dtype=bool)
-        bits[:card] = mask
-        words = np.packbits(bits.reshape(-1, 8)[:, ::-1], axis=1).reshape(-1, 8)[:, ::-1].copy().view("<i8").ravel()
-        t = torch.from_numpy(words.copy()).to(self.ds.device)
+        words = pack_bitset(mask)
+        t = torch.from_numpy(words).to(self.ds.device)
         prog.keepalive.append(t)
         prog.fops.append((D.F_IN_SET, ci, 0, 0, 0, 0.0, 0.0, t))
         return 1
@@ -873,6 +927,14 @@ class Lowerer:
             raise LoweringError("too many grouping keys")
         for a in aggregations:
             self.add_aggregator(prog, a)
+        # filter-implied key domains: a dimension the filter pins to a few values only needs
+        # that many key slots (Q7: s_nation x c_nation shrinks 25x25 -> 2x2), which keeps the
+        # accumulators in LDS instead of contended HBM atomics
+        for i, kc in enumerate(prog.keys):
+            if kc.kind == D.K_ID:
+                imp = implied_ids(bexpr, kc.col)
+                if imp is not None and int(imp.sum()) < kc.card:
+                    prog.keys[i] = compact_key(kc, imp)
         # mixed radix strides (last key fastest)
         G = 1
         for kc in reversed(prog.keys):
@@ -883,10 +945,10 @@ class Lowerer:
         prog.G = G
         prog.est_rows = prog.rows_in_ranges * self.selectivity(bexpr)
         if not prog.empty:
-            depth = self.emit_filter(prog, bexpr) if not _is(bexpr, "true") else 0
-            prog.filter_len = len(prog.fops)
-            if depth > D.STACK_DEPTH:
-                raise LoweringError("filter too deep for the device stack")
+            for kc in prog.keys:
+                kc.col_idx = prog.col(kc.col)  # payload section
+            self.emit_main_filter(prog, bexpr)
+            prog.section = "p"
             for d in prog.aops:
                 if d["filter"] is not None:
                     off = len(prog.fops)
@@ -894,8 +956,6 @@ class Lowerer:
                     if dep > D.STACK_DEPTH:
                         raise LoweringError("aggregator filter too deep")
                     d["filt_off"], d["filt_len"] = off, len(prog.fops) - off
-            for kc in prog.keys:
-                prog.col(kc.col)
             for d in prog.aops:
                 if d["expr"] is not None:
                     d["expr_off"] = len(prog.eops)
@@ -906,6 +966,34 @@ class Lowerer:
             self.pick_zones(prog, bexpr)
         return prog
 
+    def emit_main_filter(self, prog: ScanProgram, bexpr) -> None:
+        """Split the filter's top-level conjuncts: bitmap-only ones become the chunk-level
+        pre-filter (one vector load per leaf per 4096 rows, lane = 64-row word); the rest is the
+        per-word program over filter-phase columns staged into LDS."""
+        conj = bexpr[1] if _is(bexpr, "and") else ([] if _is(bexpr, "true") else [bexpr])
+        pre, rest, nleaves = [], [], 0
+        for c in conj:
+            n = self.bitmap_only(c)
+            if n >= 0 and nleaves + n <= D.MAX_BM:
+                pre.append(c)
+                nleaves += n
+            else:
+                rest.append(c)
+        prog.section = "f"
+        if rest:
+            depth = self.emit_filter(prog, b_and(rest))
+            if depth > D.STACK_DEPTH:
+                raise LoweringError("filter too deep for the device stack")
+        prog.filter_len = len(prog.fops)
+        prog.final_pre = not rest
+        prog.pre_off = len(prog.fops)
+        if pre:
+            depth = self.emit_filter(prog, b_and(pre))
+            if depth > D.STACK_DEPTH:
+                raise LoweringError("filter too deep for the device stack")
+        prog.pre_len = len(prog.fops) - prog.pre_off
+        prog.section = "p"
+
     def lower_mask(self, intervals, filter_spec) -> ScanProgram:
         prog = ScanProgram(self.ds)
         bexpr = self.filter_ir(filter_spec)
@@ -914,12 +1002,55 @@ class Lowerer:
         if _is(bexpr, "false") or not ranges:
             prog.empty = True
             return prog
-        if not _is(bexpr, "true"):
-            if self.emit_filter(prog, bexpr) > D.STACK_DEPTH:
-                raise LoweringError("filter too deep for the device stack")
-        prog.filter_len = len(prog.fops)
+        self.emit_main_filter(prog, bexpr)
         self.pick_zones(prog, bexpr)
         return prog
+
+
+def implied_ids(x, dim: str) -> Optional[np.ndarray]:
+    """Ids of `dim` that can satisfy filter x (None = unrestricted)."""
+    k = x[0]
+    if k == "ids":
+        return x[2] if x[1] == dim else None
+    if k == "and":
+        out = None
+        for c in x[1]:
+            m = implied_ids(c, dim)
+            if m is not None:
+                out = m.copy() if out is None else (out & m)
+        return out
+    if k == "or":
+        out = None
+        for c in x[1]:
+            m = implied_ids(c, dim)
+            if m is None:
+                return None
+            out = m.copy() if out is None else (out | m)
+        return out
+    if k == "false":
+        return None
+    return None
+
+
+def compact_key(kc: KeyComp, mask: np.ndarray) -> KeyComp:
+    ids = np.flatnonzero(mask)
+    if len(ids) == 0:
+        ids = np.array([0])
+    remap = np.zeros(len(mask), dtype=np.int32)
+    remap[ids] = np.arange(len(ids), dtype=np.int32)
+    dec = kc.decoder
+    ids_t = ids.astype(np.int64)
+    return KeyComp(kc.name, D.K_REMAP, kc.col, len(ids), remap=remap,
+                   decoder=(lambda c: dec(ids_t[np.asarray(c, dtype=np.int64)])) if dec else (lambda c: ids_t[c]))
+
+
+def pack_bitset(mask: np.ndarray) -> np.ndarray:
+    """bool[n] -> int64 words, bit (i & 63) of word (i >> 6) == mask[i] (the kernel's F_IN_SET layout)"""
+    n64 = (len(mask) + 63) // 64
+    words = np.zeros(n64, dtype=np.uint64)
+    idx = np.flatnonzero(mask).astype(np.uint64)
+    np.bitwise_or.at(words, (idx >> np.uint64(6)).astype(np.int64), np.left_shift(np.uint64(1), idx & np.uint64(63)))
+    return words.view(np.int64)
 
 
 def _depth(x) -> int:
@@ -967,18 +1098,51 @@ def _to_ms(v) -> int:
     return parse_iso_ms(s)
 
 
+def col_meta(t: torch.Tensor, plane: int) -> Tuple[int, int]:
+    """(meta, planes) for the kernel's LDS staging: lg | signed << 4 | float << 5 | plane << 8"""
+    lg = {1: 0, 2: 1, 4: 2, 8: 3}[t.element_size()]
+    sgn = 1 if t.dtype in (torch.int16, torch.int32, torch.int64) else 0
+    flt = 1 if t.dtype.is_floating_point else 0
+    return lg | (sgn << 4) | (flt << 5) | (plane << 8), (2 if lg == 3 else 1)
+
+
+def lds_layout(prog: ScanProgram, acc_hll_bytes: int, unroll: int, waves: int) -> Tuple[int, int, int, int]:
+    """(cache_off, wave_bytes, nplanes, total_lds) of the kernel's dynamic LDS."""
+    nplanes = 0
+    for name in prog.cols:
+        nplanes += 2 if column_tensor(prog.ds, name).element_size() == 8 else 1
+    cache_off = (acc_hll_bytes + 15) // 16 * 16
+    wave_bytes = nplanes * unroll * 256 + len(prog.bm_leaves) * 512
+    wave_bytes = (wave_bytes + 15) // 16 * 16
+    return cache_off, wave_bytes, nplanes, cache_off + waves * wave_bytes
+
+
 def pack(prog: ScanProgram, mode: int, dedup: int, hll_lds: int, lds_bytes: int, out_acc: int, out_keys: int,
          hash_cap: int, overflow: int, out_mask: int, out_count: int, hll_ptrs: Sequence[int],
-         hll_lds_offs: Sequence[int]) -> np.ndarray:
+         hll_lds_offs: Sequence[int], unroll: int = 2, cache_off: int = 0, wave_bytes: int = 0) -> np.ndarray:
     """Serialize a program into ScanDesc bytes (device pointers are plain integers)."""
     ds = prog.ds
     d = D.new_desc()
     r = d[0]
     r["ncols"] = len(prog.cols)
-    for i, name in enumerate(prog.cols):
-        t = column_tensor(ds, name)
-        r["cols"][i]["ptr"] = t.data_ptr()
-        r["cols"][i]["dtype"] = dtype_code(t)
+    plane = 0
+    for base, names in ((0, prog.fcols), (D.PAYLOAD_BASE, prog.pcols)):
+        for j, name in enumerate(names):
+            t = column_tensor(ds, name)
+            meta, npl = col_meta(t, plane)
+            plane += npl
+            c = r["cols"][base + j]
+            c["ptr"], c["dtype"], c["meta"] = t.data_ptr(), dtype_code(t), meta
+    r["nfc"], r["npc"], r["nplanes"] = len(prog.fcols), len(prog.pcols), plane
+    r["lds_cache_off"], r["lds_wave_bytes"], r["unroll"] = cache_off, wave_bytes, unroll
+    if ds.device.type == "cuda":
+        from ..ops import native
+
+        r["narrow4"] = native.narrow4()
+    r["pre_off"], r["pre_len"], r["final_pre"] = prog.pre_off, prog.pre_len, 1 if prog.final_pre else 0
+    r["nbm"] = len(prog.bm_leaves)
+    for j, (row, stride, count) in enumerate(prog.bm_leaves):
+        r["bm_bits"][j], r["bm_stride"][j], r["bm_count"][j] = row.data_ptr(), stride, count
     r["nfops"] = len(prog.fops)
     r["filter_len"] = prog.filter_len
     for i, (op, col, flags, lo, hi, flo, fhi, bits) in enumerate(prog.fops):
@@ -988,7 +1152,7 @@ def pack(prog: ScanProgram, mode: int, dedup: int, hll_lds: int, lds_bytes: int,
     r["nkops"] = len(prog.keys)
     for i, kc in enumerate(prog.keys):
         k = r["kops"][i]
-        k["kind"], k["col"], k["tfield"] = kc.kind, prog.col(kc.col), kc.tfield
+        k["kind"], k["col"], k["tfield"] = kc.kind, kc.col_idx, kc.tfield
         k["stride"], k["base"], k["card"] = kc.stride, kc.base, kc.card
         k["unit_ms"] = ds.time_unit_ms
         k["tz_ms"], k["period_ms"], k["origin_ms"] = kc.tz_ms, kc.period_ms or 1, kc.origin_ms
@@ -1000,7 +1164,6 @@ def pack(prog: ScanProgram, mode: int, dedup: int, hll_lds: int, lds_bytes: int,
             prog.keepalive.append(t)
             k["remap"] = t.data_ptr()
     r["naggs"] = len(prog.aops)
-    kind_map = {}
     for i, a in enumerate(prog.aops):
         o = r["aops"][i]
         o["kind"], o["col"], o["slot"] = a["kind"], a["col"], max(a["slot"], 0)

@@ -15,6 +15,7 @@ __global__ void olap_scan_kernel(const ScanDesc* __restrict__ d);
 __global__ void bitmap_build_kernel(const void* ids, int dtype, int64_t n, int64_t nwords, uint64_t* out,
                                     int64_t card);
 __global__ void hll_estimate_kernel(const uint32_t* regs, int64_t G, int p, double* est);
+__global__ void glds_probe_kernel(const unsigned char* src, uint32_t* out);
 }  // namespace sdo
 
 namespace py = pybind11;
@@ -23,30 +24,23 @@ static void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
-static bool g_attr_set[8] = {false};
-
-template <int U>
-static void launch_scan(uint64_t desc, int grid, int block, int lds, hipStream_t s) {
-  if (lds > 65536 && !g_attr_set[U]) {
-    check(hipFuncSetAttribute((const void*)sdo::olap_scan_kernel<U>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024),
-          "hipFuncSetAttribute");
-    g_attr_set[U] = true;
-  }
-  hipLaunchKernelGGL(sdo::olap_scan_kernel<U>, dim3(grid), dim3(block), lds, s, (const sdo::ScanDesc*)desc);
-  check(hipGetLastError(), "olap_scan_kernel launch");
-}
-
 static void scan(uint64_t desc, int grid, int block, int lds, int unroll, uint64_t stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (block % 64 != 0 || block > 1024 || block <= 0) throw std::invalid_argument("block must be a multiple of 64 <= 1024");
+  if (block % 64 != 0 || block > 512 || block <= 0) throw std::invalid_argument("block must be a multiple of 64 <= 512");
   if (lds < 0 || lds > 160 * 1024) throw std::invalid_argument("lds bytes out of range");
+  if (grid <= 0) return;
+  const void* f;
   switch (unroll) {
-    case 1: launch_scan<1>(desc, grid, block, lds, s); break;
-    case 2: launch_scan<2>(desc, grid, block, lds, s); break;
-    case 4: launch_scan<4>(desc, grid, block, lds, s); break;
+    case 1: f = (const void*)sdo::olap_scan_kernel<1>; break;
+    case 2: f = (const void*)sdo::olap_scan_kernel<2>; break;
+    case 4: f = (const void*)sdo::olap_scan_kernel<4>; break;
     default: throw std::invalid_argument("unroll must be 1, 2 or 4");
   }
+  if (lds > 65536) {
+    check(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024), "hipFuncSetAttribute");
+  }
+  void* args[] = {(void*)&desc};
+  check(hipLaunchKernel(f, dim3(grid), dim3(block), args, (size_t)lds, s), "olap_scan_kernel launch");
 }
 
 static void bitmap_build(uint64_t ids, int dtype, int64_t n, int64_t nwords, uint64_t out, int64_t card,
@@ -62,10 +56,36 @@ static void bitmap_build(uint64_t ids, int dtype, int64_t n, int64_t nwords, uin
 static void hll_estimate(uint64_t regs, int64_t G, int p, uint64_t est, uint64_t stream) {
   if (G <= 0) return;
   if (p < 4 || p > 18) throw std::invalid_argument("hll precision out of range");
+  if ((1 << p) % (16 * 2) != 0) throw std::invalid_argument("hll registers must split over 16 waves");
   const unsigned blocks = (unsigned)((G + 31) / 32);
-  hipLaunchKernelGGL(sdo::hll_estimate_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(sdo::hll_estimate_kernel, dim3(blocks), dim3(1024), 0, (hipStream_t)stream,
                      (const uint32_t*)regs, G, p, (double*)est);
   check(hipGetLastError(), "hll_estimate_kernel launch");
+}
+
+// Returns 4 when 1/2-byte LDS-DMA elements land one dword per lane, 1 when packed (lane*size).
+static int glds_probe() {
+  unsigned char h_src[256];
+  for (int i = 0; i < 256; ++i) h_src[i] = (unsigned char)(i + 1);
+  unsigned char* d_src = nullptr;
+  uint32_t* d_out = nullptr;
+  check(hipMalloc(&d_src, 256), "hipMalloc");
+  check(hipMalloc(&d_out, 128 * 4), "hipMalloc");
+  check(hipMemcpy(d_src, h_src, 256, hipMemcpyHostToDevice), "hipMemcpy");
+  hipLaunchKernelGGL(sdo::glds_probe_kernel, dim3(1), dim3(64), 0, 0, d_src, d_out);
+  check(hipGetLastError(), "glds_probe launch");
+  uint32_t h_out[128];
+  check(hipMemcpy(h_out, d_out, sizeof(h_out), hipMemcpyDeviceToHost), "hipMemcpy");
+  hipFree(d_src);
+  hipFree(d_out);
+  bool dword = true, packed = true;
+  for (int l = 0; l < 64; ++l) {
+    if ((h_out[l] & 0xff) != (uint32_t)((l + 1) & 0xff)) dword = false;
+    if (((const unsigned char*)h_out)[l] != (unsigned char)(l + 1)) packed = false;
+  }
+  if (dword) return 4;
+  if (packed) return 1;
+  return -1;
 }
 
 static int desc_size() { return (int)sizeof(sdo::ScanDesc); }
@@ -112,6 +132,7 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("bitmap_build", &bitmap_build);
   m.def("hll_estimate", &hll_estimate);
   m.def("desc_size", &desc_size);
+  m.def("glds_probe", &glds_probe);
   m.def("layout", &layout);
   m.def("device_info", &device_info);
   m.attr("ARCH") = "gfx950";

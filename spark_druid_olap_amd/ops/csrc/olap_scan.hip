@@ -52,186 +52,6 @@ __device__ __forceinline__ uint64_t range_bits(int lo, int hi) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Batched column loads: U independent loads are issued inside one wave-uniform dtype branch so
-// the compiler waits once per batch, not once per element.
-template <int U>
-__device__ __forceinline__ void load_int(const ColRef& c, const int64_t (&row)[U], int64_t (&v)[U]) {
-  switch (c.dtype) {
-    case DT_U8: {
-      const uint8_t* p = (const uint8_t*)c.ptr;
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = p[row[u]];
-    } break;
-    case DT_I16: {
-      const int16_t* p = (const int16_t*)c.ptr;
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = p[row[u]];
-    } break;
-    case DT_U16: {
-      const uint16_t* p = (const uint16_t*)c.ptr;
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = p[row[u]];
-    } break;
-    case DT_I32: {
-      const int32_t* p = (const int32_t*)c.ptr;
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = p[row[u]];
-    } break;
-    case DT_I64: {
-      const int64_t* p = (const int64_t*)c.ptr;
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = p[row[u]];
-    } break;
-    case DT_F32: {
-      const float* p = (const float*)c.ptr;
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = (int64_t)p[row[u]];
-    } break;
-    default: {
-      const double* p = (const double*)c.ptr;
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = (int64_t)p[row[u]];
-    } break;
-  }
-}
-
-template <int U>
-__device__ __forceinline__ void load_flt(const ColRef& c, const int64_t (&row)[U], double (&v)[U]) {
-  switch (c.dtype) {
-    case DT_F64: {
-      const double* p = (const double*)c.ptr;
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = p[row[u]];
-    } break;
-    case DT_F32: {
-      const float* p = (const float*)c.ptr;
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = (double)p[row[u]];
-    } break;
-    default: {
-      int64_t t[U];
-      load_int<U>(c, row, t);
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = (double)t[u];
-    } break;
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Filter program: postfix ops over a shifting register stack of wave masks (static indexing only:
-// runtime-indexed register arrays would spill to scratch on CDNA).
-template <int U>
-struct MaskStack {
-  uint64_t s[STACK_DEPTH][U];
-  __device__ __forceinline__ void push(const uint64_t (&m)[U]) {
-#pragma unroll
-    for (int d = STACK_DEPTH - 1; d > 0; --d)
-#pragma unroll
-      for (int u = 0; u < U; ++u) s[d][u] = s[d - 1][u];
-#pragma unroll
-    for (int u = 0; u < U; ++u) s[0][u] = m[u];
-  }
-  template <int OP>
-  __device__ __forceinline__ void binop() {
-#pragma unroll
-    for (int u = 0; u < U; ++u) s[0][u] = OP == 0 ? (s[1][u] & s[0][u]) : (s[1][u] | s[0][u]);
-#pragma unroll
-    for (int d = 1; d < STACK_DEPTH - 1; ++d)
-#pragma unroll
-      for (int u = 0; u < U; ++u) s[d][u] = s[d + 1][u];
-  }
-};
-
-template <int U>
-__device__ __forceinline__ void eval_filter(const ScanDesc* __restrict__ d, int off, int len,
-                                            const int64_t (&word)[U], const int64_t (&row)[U],
-                                            const uint64_t (&valid)[U], uint64_t (&out)[U]) {
-  if (len == 0) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) out[u] = valid[u];
-    return;
-  }
-  MaskStack<U> st;
-  for (int i = off; i < off + len; ++i) {
-    const FOp f = d->fops[i];
-    uint64_t m[U];
-    switch (f.op) {
-      case F_TRUE:
-#pragma unroll
-        for (int u = 0; u < U; ++u) m[u] = ~0ull;
-        st.push(m);
-        break;
-      case F_FALSE:
-#pragma unroll
-        for (int u = 0; u < U; ++u) m[u] = 0ull;
-        st.push(m);
-        break;
-      case F_BITMAP: {
-        const uint64_t* b = (const uint64_t*)f.bits;
-#pragma unroll
-        for (int u = 0; u < U; ++u) m[u] = valid[u] ? b[word[u]] : 0ull;
-        st.push(m);
-      } break;
-      case F_BITMAP_OR: {
-        const uint64_t* b = (const uint64_t*)f.bits;
-#pragma unroll
-        for (int u = 0; u < U; ++u) m[u] = 0ull;
-        for (int64_t j = 0; j < f.hi; ++j) {
-#pragma unroll
-          for (int u = 0; u < U; ++u) m[u] |= valid[u] ? b[j * f.lo + word[u]] : 0ull;
-        }
-        st.push(m);
-      } break;
-      case F_ID_RANGE:
-      case F_INT_RANGE: {
-        int64_t v[U];
-        load_int<U>(d->cols[f.col], row, v);
-#pragma unroll
-        for (int u = 0; u < U; ++u) m[u] = __ballot(v[u] >= f.lo && (f.op == F_ID_RANGE ? v[u] < f.hi : v[u] <= f.hi));
-        st.push(m);
-      } break;
-      case F_IN_SET: {
-        int64_t v[U];
-        load_int<U>(d->cols[f.col], row, v);
-        const uint64_t* b = (const uint64_t*)f.bits;
-        uint64_t w[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) w[u] = b[((uint64_t)v[u]) >> 6];
-#pragma unroll
-        for (int u = 0; u < U; ++u) m[u] = __ballot((w[u] >> (v[u] & 63)) & 1ull);
-        st.push(m);
-      } break;
-      case F_FLT_RANGE: {
-        double v[U];
-        load_flt<U>(d->cols[f.col], row, v);
-        const bool los = f.flags & 1, his = f.flags & 2;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          bool a = los ? (v[u] > f.flo) : (v[u] >= f.flo);
-          bool b = his ? (v[u] < f.fhi) : (v[u] <= f.fhi);
-          m[u] = __ballot(a && b);
-        }
-        st.push(m);
-      } break;
-      case F_AND:
-        st.template binop<0>();
-        break;
-      case F_OR:
-        st.template binop<1>();
-        break;
-      case F_NOT:
-#pragma unroll
-        for (int u = 0; u < U; ++u) st.s[0][u] = ~st.s[0][u];
-        break;
-      default:
-        break;
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < U; ++u) out[u] = st.s[0][u] & valid[u];
-}
-
-// ---------------------------------------------------------------------------------------------
 // Time bucketing: civil-from-days integer math, all in registers.
 __device__ __forceinline__ void civil_from_days(int64_t z, int64_t& y, int64_t& m, int64_t& dd) {
   z += 719468;
@@ -349,54 +169,243 @@ __device__ __forceinline__ int64_t hash_slot(uint64_t* keys, int64_t cap, uint64
   return -1;
 }
 
-// float expression VM (Druid javascript aggregators over several columns, reference
-// src/main/scala/org/sparklinedata/druid/jscodegen/JSAggGenerator.scala:37-60)
+// ---------------------------------------------------------------------------------------------
+// Per-wave LDS staging of column tiles.  For a step of U words the wave DMAs every referenced
+// column straight from HBM into its private LDS planes with global_load_lds (LDS-DMA: no VGPR
+// destination, so all loads of the step are in flight together and retire under ONE
+// `s_waitcnt vmcnt(0)` of the issuing wave -- no barrier needed, only this wave reads them).
+// Plane p, word u lives at wave_base + (p * U + u) * 256; lane l's element at + l * esize
+// (64-bit columns: low / high dword planes).  Any column is then read by LDS address arithmetic,
+// so the interpreter indexes columns dynamically without register arrays (which hipcc would
+// spill to scratch).
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
+
 template <int U>
-__device__ __forceinline__ void eval_expr(const ScanDesc* __restrict__ d, int off, int len,
-                                          const int64_t (&row)[U], double (&out)[U]) {
-  double s0[U], s1[U], s2[U], s3[U];
+__device__ __forceinline__ void stage_cols(const ScanDesc* __restrict__ d, int first, int n, const int64_t (&row)[U],
+                                           unsigned char* wbase) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // WAR: earlier LDS reads of these planes retired
+  for (int c = first; c < first + n; ++c) {
+    const ColRef r = d->cols[c];
+    const int plane = (r.meta >> 8) & 255;
+    const int lg = r.meta & 15;
+    const unsigned char* base = (const unsigned char*)r.ptr;
 #pragma unroll
-  for (int u = 0; u < U; ++u) { s0[u] = s1[u] = s2[u] = s3[u] = 0.0; }
-  for (int i = off; i < off + len; ++i) {
-    const EOp e = d->eops[i];
-    if (e.op == E_COL || e.op == E_CONST) {
-      double v[U];
-      if (e.op == E_COL) {
-        load_flt<U>(d->cols[e.col], row, v);
-        if (e.c != 0.0) {
-#pragma unroll
-          for (int u = 0; u < U; ++u) v[u] *= e.c;  // decimal scale
-        }
-      } else {
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = e.c;
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) { s3[u] = s2[u]; s2[u] = s1[u]; s1[u] = s0[u]; s0[u] = v[u]; }
-    } else if (e.op == E_NEG) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) s0[u] = -s0[u];
-    } else if (e.op == E_ABS) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) s0[u] = fabs(s0[u]);
-    } else {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        double a = s1[u], b = s0[u], r;
-        switch (e.op) {
-          case E_ADD: r = a + b; break;
-          case E_SUB: r = a - b; break;
-          case E_MUL: r = a * b; break;
-          case E_DIV: r = a / b; break;
-          case E_MIN: r = fmin(a, b); break;
-          default: r = fmax(a, b); break;
-        }
-        s0[u] = r; s1[u] = s2[u]; s2[u] = s3[u];
+    for (int u = 0; u < U; ++u) {
+      unsigned char* dst = wbase + (plane * U + u) * 256;
+      const unsigned char* src = base + (row[u] << lg);
+      switch (lg) {
+        case 0: __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)dst, 1, 0, 0); break;
+        case 1: __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)dst, 2, 0, 0); break;
+        case 2: __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)dst, 4, 0, 0); break;
+        default:
+          // 64-bit: the two dword halves of lane l land in planes `plane` and `plane + 1`
+          __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)dst, 4, 0, 0);
+          __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + 4), (lds_ptr_t)(dst + U * 256), 4, 0, 0);
+          break;
       }
     }
   }
+}
+
+__device__ __forceinline__ void stage_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// read column c (absolute index) for word u of the current step; raw bits (64-bit columns whole)
+template <int U>
+__device__ __forceinline__ uint64_t col_bits(const ScanDesc* __restrict__ d, const unsigned char* wbase, int c, int u,
+                                             int lane) {
+  const int meta = d->cols[c].meta;
+  const int plane = (meta >> 8) & 255;
+  const unsigned char* p = wbase + (plane * U + u) * 256;
+  switch (meta & 15) {
+    case 0: return d->narrow4 ? (uint64_t)(((const uint32_t*)p)[lane] & 0xffu) : (uint64_t)p[lane];
+    case 1: return d->narrow4 ? (uint64_t)(((const uint32_t*)p)[lane] & 0xffffu) : (uint64_t)((const uint16_t*)p)[lane];
+    case 2: return (uint64_t)((const uint32_t*)p)[lane];
+    default: {
+      const uint64_t lo = ((const uint32_t*)p)[lane];
+      const uint64_t hi = ((const uint32_t*)(p + U * 256))[lane];
+      return lo | (hi << 32);
+    }
+  }
+}
+
+__device__ __forceinline__ int64_t bits_int(uint64_t v, int meta) {
+  const int lg = meta & 15;
+  if ((meta >> 5) & 1) return lg == 2 ? (int64_t)__uint_as_float((uint32_t)v) : (int64_t)__longlong_as_double(v);
+  if ((meta >> 4) & 1) {
+    const int s2 = 64 - (8 << lg);
+    return (int64_t)(v << s2) >> s2;
+  }
+  return (int64_t)v;
+}
+
+__device__ __forceinline__ double bits_dbl(uint64_t v, int meta) {
+  const int lg = meta & 15;
+  if ((meta >> 5) & 1) return lg == 2 ? (double)__uint_as_float((uint32_t)v) : __longlong_as_double(v);
+  return (double)bits_int(v, meta);
+}
+
+template <int U>
+__device__ __forceinline__ int64_t col_int(const ScanDesc* __restrict__ d, const unsigned char* wb, int c, int u, int lane) {
+  return bits_int(col_bits<U>(d, wb, c, u, lane), d->cols[c].meta);
+}
+template <int U>
+__device__ __forceinline__ double col_dbl(const ScanDesc* __restrict__ d, const unsigned char* wb, int c, int u, int lane) {
+  return bits_dbl(col_bits<U>(d, wb, c, u, lane), d->cols[c].meta);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Boolean programs: postfix ops over a shifting register stack (static indexing only).
+template <int U>
+struct MaskStack {
+  uint64_t s[STACK_DEPTH][U];
+  __device__ __forceinline__ void push(const uint64_t (&m)[U]) {
 #pragma unroll
-  for (int u = 0; u < U; ++u) out[u] = s0[u];
+    for (int k = STACK_DEPTH - 1; k > 0; --k)
+#pragma unroll
+      for (int u = 0; u < U; ++u) s[k][u] = s[k - 1][u];
+#pragma unroll
+    for (int u = 0; u < U; ++u) s[0][u] = m[u];
+  }
+  template <int OP>
+  __device__ __forceinline__ void binop() {
+#pragma unroll
+    for (int u = 0; u < U; ++u) s[0][u] = OP == 0 ? (s[1][u] & s[0][u]) : (s[1][u] | s[0][u]);
+#pragma unroll
+    for (int k = 1; k < STACK_DEPTH - 1; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u) s[k][u] = s[k + 1][u];
+  }
+};
+
+// chunk level: lane = one 64-row word; bitmap leaf j's words sit in LDS at bmw + j * 512
+__device__ __forceinline__ uint64_t eval_chunk_program(const ScanDesc* __restrict__ d, int off, int len,
+                                                       const uint64_t* bmw, int lane) {
+  MaskStack<1> st;
+  for (int i = off; i < off + len; ++i) {
+    const int op = d->fops[i].op;
+    uint64_t m[1];
+    if (op == F_BITMAP) {
+      m[0] = bmw[d->fops[i].lo * 64 + lane];
+      st.push(m);
+    } else if (op == F_TRUE || op == F_FALSE) {
+      m[0] = op == F_TRUE ? ~0ull : 0ull;
+      st.push(m);
+    } else if (op == F_AND) {
+      st.template binop<0>();
+    } else if (op == F_OR) {
+      st.template binop<1>();
+    } else if (op == F_NOT) {
+      st.s[0][0] = ~st.s[0][0];
+    }
+  }
+  return st.s[0][0];
+}
+
+// word level: lane = one row; bitmap leaves read (uniform) from the chunk-level words in LDS
+template <int U>
+__device__ __forceinline__ void eval_word_program(const ScanDesc* __restrict__ d, int off, int len,
+                                                  const unsigned char* wb, const int (&wl)[U], const uint64_t* bmw,
+                                                  int lane, uint64_t (&out)[U]) {
+  MaskStack<U> st;
+  for (int i = off; i < off + len; ++i) {
+    const FOp f = d->fops[i];
+    uint64_t m[U];
+    switch (f.op) {
+      case F_TRUE:
+      case F_FALSE:
+#pragma unroll
+        for (int u = 0; u < U; ++u) m[u] = f.op == F_TRUE ? ~0ull : 0ull;
+        st.push(m);
+        break;
+      case F_BITMAP: {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint64_t w = bmw[f.lo * 64 + wl[u]];
+          m[u] = readlane64(w, 0);  // uniform address: every lane read the same word
+        }
+        st.push(m);
+      } break;
+      case F_ID_RANGE:
+      case F_INT_RANGE:
+      case F_IN_SET: {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t v = col_int<U>(d, wb, f.col, u, lane);
+          bool p;
+          if (f.op == F_IN_SET) {
+            const uint64_t w = ((const uint64_t*)f.bits)[((uint64_t)v) >> 6];
+            p = (w >> (v & 63)) & 1ull;
+          } else {
+            p = v >= f.lo && (f.op == F_ID_RANGE ? v < f.hi : v <= f.hi);
+          }
+          m[u] = __ballot(p);
+        }
+        st.push(m);
+      } break;
+      case F_FLT_RANGE: {
+        const bool los = f.flags & 1, his = f.flags & 2;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const double v = col_dbl<U>(d, wb, f.col, u, lane);
+          const bool a = los ? (v > f.flo) : (v >= f.flo);
+          const bool b = his ? (v < f.fhi) : (v <= f.fhi);
+          m[u] = __ballot(a && b);
+        }
+        st.push(m);
+      } break;
+      case F_AND:
+        st.template binop<0>();
+        break;
+      case F_OR:
+        st.template binop<1>();
+        break;
+      case F_NOT:
+#pragma unroll
+        for (int u = 0; u < U; ++u) st.s[0][u] = ~st.s[0][u];
+        break;
+      default:
+        break;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) out[u] = st.s[0][u];
+}
+
+// float expression VM over staged columns (Druid javascript aggregators over several columns,
+// reference sd/jscodegen/JSAggGenerator.scala:37-60)
+template <int U>
+__device__ __forceinline__ double eval_expr(const ScanDesc* __restrict__ d, int off, int len, const unsigned char* wb,
+                                            int u, int lane) {
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  for (int i = off; i < off + len; ++i) {
+    const EOp e = d->eops[i];
+    if (e.op == E_COL || e.op == E_CONST) {
+      double v = e.c;
+      if (e.op == E_COL) {
+        v = col_dbl<U>(d, wb, e.col, u, lane);
+        if (e.c != 0.0) v *= e.c;  // decimal scale
+      }
+      s3 = s2; s2 = s1; s1 = s0; s0 = v;
+    } else if (e.op == E_NEG) {
+      s0 = -s0;
+    } else if (e.op == E_ABS) {
+      s0 = fabs(s0);
+    } else {
+      const double a = s1, b = s0;
+      double r;
+      switch (e.op) {
+        case E_ADD: r = a + b; break;
+        case E_SUB: r = a - b; break;
+        case E_MUL: r = a * b; break;
+        case E_DIV: r = a / b; break;
+        case E_MIN: r = fmin(a, b); break;
+        default: r = fmax(a, b); break;
+      }
+      s0 = r; s1 = s2; s2 = s3;
+    }
+  }
+  return s0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -412,27 +421,35 @@ __global__ __launch_bounds__(512) void olap_scan_kernel(const ScanDesc* __restri
   const int hll_p = d->hll_p;
   const int64_t hll_m = 1ll << hll_p;
   uint64_t* acc_lds = (uint64_t*)lds;
+  unsigned char* wb = lds + d->lds_cache_off + wave * d->lds_wave_bytes;   // this wave's staging planes
+  uint64_t* bmw = (uint64_t*)(wb + d->nplanes * U * 256);                  // this wave's bitmap words
 
+  // LDS mode: every wave owns a private accumulator copy (acc_lds + wave * G * nslots), so lanes
+  // update it with plain per-lane LDS atomics -- no cross-lane reduction chains, and the copies
+  // are summed once at the end.  HLL registers stay block-shared (random buckets rarely collide).
+  const int64_t accn = G * nslots;
   if (mode == M_DENSE_LDS) {
-    const int64_t n = G * nslots;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) acc_lds[i] = (uint64_t)d->slot_init[i % nslots];
+    for (int64_t i = threadIdx.x; i < accn * wpb; i += blockDim.x) acc_lds[i] = (uint64_t)d->slot_init[i % nslots];
     if (d->hll_lds) {
-      uint32_t* r = (uint32_t*)(lds + n * 8);
+      uint32_t* r = (uint32_t*)(lds + accn * wpb * 8);
       const int64_t nr = (int64_t)d->nhll * G * hll_m;
       for (int64_t i = threadIdx.x; i < nr; i += blockDim.x) r[i] = 0u;
     }
     __syncthreads();
   }
+  uint64_t* acc_wave = acc_lds + wave * accn;
   uint64_t* gacc = (uint64_t*)d->out_acc;
   uint64_t* hkeys = (uint64_t*)d->out_keys;
   int* overflow = (int*)d->overflow;
+  const int nbm = d->nbm;
+  const bool final_pre = d->final_pre != 0;
+  const int nfc = d->nfc, npc = d->npc;
 
   const int64_t total_waves = (int64_t)gridDim.x * wpb;
   const int64_t gw = (int64_t)blockIdx.x * wpb + wave;
   const int64_t num_rows = d->num_rows;
 
   for (int64_t c = gw; c < d->total_chunks; c += total_waves) {
-    // linear chunk -> (range, absolute chunk)
     int r = 0;
     int64_t cc = c;
     while (r < d->nranges - 1 && cc >= d->ranges[r].nchunks) { cc -= d->ranges[r].nchunks; ++r; }
@@ -442,7 +459,6 @@ __global__ __launch_bounds__(512) void olap_scan_kernel(const ScanDesc* __restri
     if (chi > d->ranges[r].hi) chi = d->ranges[r].hi;
     if (chi > num_rows) chi = num_rows;
     if (chi <= clo) continue;
-    // zone-map pruning (min/max of dictionary ids per 4096-row chunk)
     bool skip = false;
     for (int z = 0; z < d->nzones; ++z) {
       const ZoneP zp = d->zones[z];
@@ -452,46 +468,81 @@ __global__ __launch_bounds__(512) void olap_scan_kernel(const ScanDesc* __restri
     }
     if (skip) continue;
 
-    const int64_t wbeg = clo >> 6, wend = (chi + 63) >> 6;
-    for (int64_t w0 = wbeg; w0 < wend; w0 += U) {
-      int64_t word[U], row[U];
-      uint64_t valid[U];
+    // ---- chunk level: lane w holds word w (rows 64w .. 64w+63 of the chunk) ----
+    const int64_t cw0 = kchunk * CHUNK_WORDS;
+    const int64_t my_r0 = (cw0 + lane) * 64;
+    const int64_t lo_off = clo - my_r0, hi_off = chi - my_r0;
+    uint64_t pre = range_bits((int)(lo_off < 0 ? 0 : (lo_off > 64 ? 64 : lo_off)),
+                              (int)(hi_off < 0 ? 0 : (hi_off > 64 ? 64 : hi_off)));
+    if (nbm > 0) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      for (int j = 0; j < nbm; ++j) {
+        const uint64_t* b = (const uint64_t*)d->bm_bits[j];
+        const int64_t stride = d->bm_stride[j];
+        uint64_t v = 0ull;
+        for (int64_t k = 0; k < d->bm_count[j]; ++k) v |= b[k * stride + cw0 + lane];
+        bmw[j * 64 + lane] = v;
+      }
+      if (d->pre_len > 0) pre &= eval_chunk_program(d, d->pre_off, d->pre_len, bmw, lane);
+    }
+    uint64_t nz = __ballot(pre != 0ull);
+
+    while (nz) {
+      int wl[U];
+      uint64_t m[U];
+      int64_t row[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        word[u] = w0 + u;
-        const int64_t r0 = word[u] << 6;
-        row[u] = r0 + lane;
-        valid[u] = (word[u] < wend) ? range_bits((int)(clo > r0 ? clo - r0 : 0), (int)(chi - r0 > 64 ? 64 : chi - r0)) : 0ull;
+        if (nz) {
+          wl[u] = __builtin_ctzll(nz);
+          nz &= nz - 1ull;
+          m[u] = readlane64(pre, wl[u]);
+        } else {
+          wl[u] = 0;
+          m[u] = 0ull;
+        }
+        row[u] = (cw0 + wl[u]) * 64 + lane;
       }
-      uint64_t m[U];
-      eval_filter<U>(d, 0, d->filter_len, word, row, valid, m);
+      if (!final_pre) {
+        if (nfc > 0) {
+          stage_cols<U>(d, 0, nfc, row, wb);
+          stage_wait();
+        }
+        uint64_t f[U];
+        eval_word_program<U>(d, 0, d->filter_len, wb, wl, bmw, lane, f);
+#pragma unroll
+        for (int u = 0; u < U; ++u) m[u] &= f[u];
+      }
       uint64_t any = 0;
 #pragma unroll
       for (int u = 0; u < U; ++u) any |= m[u];
       if (any == 0) continue;
 
       if (mode == M_MASK) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (valid[u] != 0 && lane == 0) ((uint64_t*)d->out_mask)[word[u]] = m[u];
-        }
         if (lane == 0) {
           unsigned long long cnt = 0;
 #pragma unroll
-          for (int u = 0; u < U; ++u) cnt += __popcll(m[u]);
+          for (int u = 0; u < U; ++u) {
+            if (m[u]) ((uint64_t*)d->out_mask)[cw0 + wl[u]] = m[u];
+            cnt += __popcll(m[u]);
+          }
           atomicAdd((unsigned long long*)d->out_count, cnt);
         }
         continue;
       }
 
-      // rows used for dependent loads: inactive lanes alias the first active lane's row
+      // payload: inactive lanes alias the first active lane's row (only qualifying lines are read)
       int64_t lrow[U];
       bool act[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         act[u] = (m[u] >> lane) & 1ull;
-        const int64_t lead = (word[u] << 6) + (m[u] ? __builtin_ctzll(m[u]) : 0);
+        const int64_t lead = (cw0 + wl[u]) * 64 + (m[u] ? __builtin_ctzll(m[u]) : 0);
         lrow[u] = act[u] ? row[u] : lead;
+      }
+      if (npc > 0) {
+        stage_cols<U>(d, PAYLOAD_BASE, npc, lrow, wb);
+        stage_wait();
       }
 
       // ---- group key ----
@@ -500,60 +551,54 @@ __global__ __launch_bounds__(512) void olap_scan_kernel(const ScanDesc* __restri
       for (int u = 0; u < U; ++u) key[u] = 0;
       for (int k = 0; k < d->nkops; ++k) {
         const KOp ko = d->kops[k];
-        int64_t v[U];
-        load_int<U>(d->cols[ko.col], lrow, v);
-        if (ko.kind == K_REMAP) {
-          const int32_t* rm = (const int32_t*)ko.remap;
-#pragma unroll
-          for (int u = 0; u < U; ++u) v[u] = rm[v[u]];
-        } else if (ko.kind == K_TIME) {
-#pragma unroll
-          for (int u = 0; u < U; ++u) v[u] = time_field(v[u] * ko.unit_ms, ko) - ko.base;
-        } else if (ko.kind == K_INT) {
-#pragma unroll
-          for (int u = 0; u < U; ++u) v[u] -= ko.base;
-        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          int64_t vv = v[u];
-          if (ko.kind == K_TIME || ko.kind == K_INT) {  // clamp out-of-domain buckets (never hit for planned intervals)
-            vv = vv < 0 ? 0 : (vv >= ko.card ? ko.card - 1 : vv);
+          int64_t v = col_int<U>(d, wb, ko.col, u, lane);
+          if (ko.kind == K_REMAP) {
+            v = ((const int32_t*)ko.remap)[v];
+          } else if (ko.kind == K_TIME) {
+            v = time_field(v * ko.unit_ms, ko) - ko.base;
+            v = v < 0 ? 0 : (v >= ko.card ? ko.card - 1 : v);
+          } else if (ko.kind == K_INT) {
+            v -= ko.base;
+            v = v < 0 ? 0 : (v >= ko.card ? ko.card - 1 : v);
           }
-          key[u] += (uint64_t)vv * (uint64_t)ko.stride;
+          key[u] += (uint64_t)v * (uint64_t)ko.stride;
         }
       }
-      // ---- slot resolution ----
       int64_t slot[U];
       if (mode == M_HASH) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           slot[u] = act[u] ? hash_slot(hkeys, d->hash_cap, key[u], overflow) : -1;
           if (slot[u] < 0) act[u] = false;
+          m[u] = __ballot(act[u]);
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u) m[u] = __ballot(act[u]);
       } else {
 #pragma unroll
         for (int u = 0; u < U; ++u) slot[u] = (int64_t)key[u];
       }
 
       // ---- aggregators ----
+      const bool lds_acc = mode == M_DENSE_LDS;
+      uint64_t* accbase = lds_acc ? acc_wave : gacc;
       for (int a = 0; a < d->naggs; ++a) {
         const AOp ao = d->aops[a];
         uint64_t ma[U];
         if (ao.filt_len > 0) {
-          eval_filter<U>(d, ao.filt_off, ao.filt_len, word, lrow, m, ma);
+          eval_word_program<U>(d, ao.filt_off, ao.filt_len, wb, wl, bmw, lane, ma);
+#pragma unroll
+          for (int u = 0; u < U; ++u) ma[u] &= m[u];
         } else {
 #pragma unroll
           for (int u = 0; u < U; ++u) ma[u] = m[u];
         }
         if (ao.kind == A_HLL) {
-          int64_t v[U];
-          load_int<U>(d->cols[ao.col], lrow, v);
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             if ((ma[u] >> lane) & 1ull) {
-              const uint64_t h = mix64((uint64_t)v[u] ^ (uint64_t)ao.salt);
+              const int64_t v = col_int<U>(d, wb, ao.col, u, lane);
+              const uint64_t h = mix64((uint64_t)v ^ (uint64_t)ao.salt);
               const uint32_t bucket = (uint32_t)(h >> (64 - hll_p));
               const uint64_t rest = (h << hll_p) | (1ull << (hll_p - 1));
               const uint32_t rho = (uint32_t)__builtin_clzll(rest) + 1u;
@@ -567,32 +612,25 @@ __global__ __launch_bounds__(512) void olap_scan_kernel(const ScanDesc* __restri
           }
           continue;
         }
-        // value in int64 bits (float kinds: double bits, min/max: order-preserving int64)
-        int64_t val[U];
         const int sop = d->slot_op[ao.slot];
-        if (ao.kind == A_COUNT) {
-#pragma unroll
-          for (int u = 0; u < U; ++u) val[u] = 1;
-        } else if (ao.kind == A_SUM_F || ao.kind == A_MIN_F || ao.kind == A_MAX_F) {
-          double fv[U];
-          if (ao.expr_len > 0) {
-            eval_expr<U>(d, ao.expr_off, ao.expr_len, lrow, fv);
-          } else {
-            load_flt<U>(d->cols[ao.col], lrow, fv);
-          }
-#pragma unroll
-          for (int u = 0; u < U; ++u) val[u] = (ao.kind == A_SUM_F) ? __double_as_longlong(fv[u]) : f2ord(fv[u]);
-        } else {
-          load_int<U>(d->cols[ao.col], lrow, val);
-        }
-        uint64_t* accbase = (mode == M_DENSE_LDS) ? acc_lds : gacc;
+        const bool fl = ao.kind == A_SUM_F || ao.kind == A_MIN_F || ao.kind == A_MAX_F;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           uint64_t pend = ma[u];
           if (!pend) continue;
+          int64_t val;
+          if (ao.kind == A_COUNT) {
+            val = 1;
+          } else if (fl) {
+            const double fv = ao.expr_len > 0 ? eval_expr<U>(d, ao.expr_off, ao.expr_len, wb, u, lane)
+                                              : col_dbl<U>(d, wb, ao.col, u, lane);
+            val = (ao.kind == A_SUM_F) ? __double_as_longlong(fv) : f2ord(fv);
+          } else {
+            val = col_int<U>(d, wb, ao.col, u, lane);
+          }
           const bool mine = (pend >> lane) & 1ull;
-          if (!d->dedup) {
-            if (mine) slot_atomic(accbase + slot[u] * nslots + ao.slot, sop, val[u]);
+          if (lds_acc || !d->dedup) {
+            if (mine) slot_atomic(accbase + slot[u] * nslots + ao.slot, sop, val);
             continue;
           }
           while (pend) {
@@ -604,13 +642,13 @@ __global__ __launch_bounds__(512) void olap_scan_kernel(const ScanDesc* __restri
             if (ao.kind == A_COUNT) {
               res = (int64_t)__popcll(same);
             } else if (sop == S_SUM_I) {
-              res = wave_sum_i(in ? val[u] : 0);
+              res = wave_sum_i(in ? val : 0);
             } else if (sop == S_SUM_F) {
-              res = __double_as_longlong(wave_sum_f(in ? __longlong_as_double(val[u]) : 0.0));
+              res = __double_as_longlong(wave_sum_f(in ? __longlong_as_double(val) : 0.0));
             } else if (sop == S_MIN_I) {
-              res = wave_min_i(in ? val[u] : INT64_MAX);
+              res = wave_min_i(in ? val : INT64_MAX);
             } else {
-              res = wave_max_i(in ? val[u] : INT64_MIN);
+              res = wave_max_i(in ? val : INT64_MIN);
             }
             if (lane == leader) slot_atomic(accbase + kk * nslots + ao.slot, sop, res);
             pend &= ~same;
@@ -622,25 +660,53 @@ __global__ __launch_bounds__(512) void olap_scan_kernel(const ScanDesc* __restri
 
   if (mode == M_DENSE_LDS) {
     __syncthreads();
-    const int64_t n = G * nslots;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    for (int64_t i = threadIdx.x; i < accn; i += blockDim.x) {
       const int s = (int)(i % nslots);
-      const int64_t v = (int64_t)acc_lds[i];
-      if (v != d->slot_init[s]) slot_atomic(gacc + i, d->slot_op[s], v);
+      const int op = d->slot_op[s];
+      int64_t v = (int64_t)acc_lds[i];
+      for (int w = 1; w < wpb; ++w) {  // fold the per-wave copies
+        const int64_t x = (int64_t)acc_lds[w * accn + i];
+        if (op == S_SUM_I) v += x;
+        else if (op == S_SUM_F) v = __double_as_longlong(__longlong_as_double(v) + __longlong_as_double(x));
+        else if (op == S_MIN_I) v = x < v ? x : v;
+        else v = x > v ? x : v;
+      }
+      if (v != d->slot_init[s]) slot_atomic(gacc + i, op, v);
     }
     if (d->hll_lds) {
       for (int a = 0; a < d->naggs; ++a) {
         const AOp ao = d->aops[a];
         if (ao.kind != A_HLL) continue;
-        const uint32_t* r = (const uint32_t*)(lds + ao.hll_lds_off);
+        const uint32_t* rr = (const uint32_t*)(lds + ao.hll_lds_off);
         uint32_t* g = (uint32_t*)ao.hll_regs;
         for (int64_t i = threadIdx.x; i < G * hll_m; i += blockDim.x) {
-          const uint32_t v = r[i];
+          const uint32_t v = rr[i];
           if (v) atomicMax(g + i, v);
         }
       }
     }
   }
+}
+
+template __global__ void olap_scan_kernel<1>(const ScanDesc* __restrict__);
+template __global__ void olap_scan_kernel<2>(const ScanDesc* __restrict__);
+template __global__ void olap_scan_kernel<4>(const ScanDesc* __restrict__);
+
+// ---------------------------------------------------------------------------------------------
+// Probe of the LDS-DMA element layout for 1- and 2-byte loads (lane * size vs lane * 4): the
+// host runs it once and records the answer in every descriptor (desc.narrow4).
+__global__ void glds_probe_kernel(const unsigned char* src, uint32_t* out) {
+  __shared__ __attribute__((aligned(16))) uint32_t buf[2][64];
+  const int lane = threadIdx.x;
+  buf[0][lane] = 0xdeadbeefu;
+  buf[1][lane] = 0xdeadbeefu;
+  __syncthreads();
+  __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + lane), (lds_ptr_t)&buf[0][0], 1, 0, 0);
+  __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + 2 * lane), (lds_ptr_t)&buf[1][0], 2, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  out[lane] = buf[0][lane];
+  out[64 + lane] = buf[1][lane];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -676,23 +742,24 @@ __global__ __launch_bounds__(256) void bitmap_build_kernel(const void* ids, int 
 // ---------------------------------------------------------------------------------------------
 // HyperLogLog finalize for G groups x m registers: sum(2^-M) and zero counts per group.
 // The register matrix is multiplied by a ones vector on the matrix cores (MFMA 32x32x2 f32:
-// A = 2^-M tile [32 groups x 2 regs], B = ones [2 x 32]), which is the batched sketch reduction
-// the BASELINE north-star calls for; zero counting rides along as a second B column block.
+// A = 2^-M tile [32 groups x 2 regs], B = e0 [2 x 32]) -- the batched sketch reduction of the
+// BASELINE north-star.  16 waves per block split the registers; partial column-0 sums meet in LDS.
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-__global__ __launch_bounds__(64) void hll_estimate_kernel(const uint32_t* regs, int64_t G, int p,
-                                                          double* est) {
-  const int lane = threadIdx.x;
+__global__ __launch_bounds__(1024) void hll_estimate_kernel(const uint32_t* regs, int64_t G, int p, double* est) {
+  __shared__ float part[16][2][32];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
   const int64_t m = 1ll << p;
   const int64_t g0 = (int64_t)blockIdx.x * 32;
-  // A operand: lane l holds A[i = l & 31][k = l >> 5] = 2^-M[g0+i][kbase + k]
-  // B operand: lane l holds B[k = l >> 5][j = l & 31] = (j == 0) ? 1 : (j == 1 ? isZeroMarker : 0)
   f32x16 acc_sum = {0};
   f32x16 acc_zero = {0};
   const int i = lane & 31;
   const int kk = lane >> 5;
   const int64_t g = g0 + i;
-  const float bsel = (i == 0) ? 1.0f : 0.0f;  // column 0 of B
-  for (int64_t kb = 0; kb < m; kb += 2) {
+  const float bsel = (i == 0) ? 1.0f : 0.0f;
+  const int64_t per = m / nw;
+  for (int64_t kb = wave * per; kb < (wave + 1) * per; kb += 2) {
     float a = 0.f, z = 0.f;
     if (g < G) {
       const uint32_t r = regs[g * m + kb + kk];
@@ -702,28 +769,31 @@ __global__ __launch_bounds__(64) void hll_estimate_kernel(const uint32_t* regs, 
     acc_sum = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bsel, acc_sum, 0, 0, 0);
     acc_zero = __builtin_amdgcn_mfma_f32_32x32x2f32(z, bsel, acc_zero, 0, 0, 0);
   }
-  // D[row][col]: col = lane & 31, row = (reg & 3) + 8*(reg >> 2) + 4*(lane >> 5). Column 0 holds sums.
+  // D[row][col]: col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); column 0 = sums
   if ((lane & 31) == 0) {
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
       const int row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
-      const int64_t gg = g0 + row;
-      if (gg < G) {
-        const double s = acc_sum[reg];
-        const double zeros = acc_zero[reg];
-        const double mm = (double)m;
-        const double alpha = 0.7213 / (1.0 + 1.079 / mm);
-        double e = alpha * mm * mm / s;
-        if (e <= 2.5 * mm && zeros > 0) e = mm * log(mm / zeros);
-        est[gg] = e;
+      part[wave][0][row] = acc_sum[reg];
+      part[wave][1][row] = acc_zero[reg];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    const int64_t gg = g0 + threadIdx.x;
+    if (gg < G) {
+      double s = 0.0, zeros = 0.0;
+      for (int w = 0; w < nw; ++w) {
+        s += part[w][0][threadIdx.x];
+        zeros += part[w][1][threadIdx.x];
       }
+      const double mm = (double)m;
+      const double alpha = 0.7213 / (1.0 + 1.079 / mm);
+      double e = alpha * mm * mm / s;
+      if (e <= 2.5 * mm && zeros > 0) e = mm * log(mm / zeros);
+      est[gg] = e;
     }
   }
 }
 
 }  // namespace sdo
-
-// explicit instantiations launched from bindings.cpp
-template __global__ void sdo::olap_scan_kernel<1>(const sdo::ScanDesc* __restrict__);
-template __global__ void sdo::olap_scan_kernel<2>(const sdo::ScanDesc* __restrict__);
-template __global__ void sdo::olap_scan_kernel<4>(const sdo::ScanDesc* __restrict__);

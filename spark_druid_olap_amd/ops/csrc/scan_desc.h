@@ -11,7 +11,8 @@
 
 namespace sdo {
 
-constexpr int MAX_COLS = 16;
+constexpr int MAX_COLS = 24;      // cols[0..8): filter-phase columns, cols[8..24): payload columns
+constexpr int PAYLOAD_BASE = 8;
 constexpr int MAX_FOPS = 48;
 constexpr int MAX_KOPS = 8;
 constexpr int MAX_AOPS = 12;
@@ -19,6 +20,7 @@ constexpr int MAX_EOPS = 64;
 constexpr int MAX_ZONES = 4;
 constexpr int MAX_RANGES = 8;
 constexpr int MAX_SLOTS = 16;
+constexpr int MAX_BM = 8;           // inverted-bitmap leaves evaluated at chunk level
 constexpr int STACK_DEPTH = 6;       // filter / expression register stack depth
 constexpr int CHUNK_ROWS = 4096;     // zone-map granule == scheduling unit (64 words of 64 rows)
 constexpr int CHUNK_WORDS = CHUNK_ROWS / 64;
@@ -28,7 +30,7 @@ enum DType : int32_t { DT_U8 = 0, DT_I16 = 1, DT_I32 = 2, DT_I64 = 3, DT_F32 = 4
 // ---- filter opcodes (postfix program; evaluated on 64-bit wave masks, one bit per lane/row) ----
 enum FOpCode : int32_t {
   F_TRUE = 0,
-  F_BITMAP = 1,     // push inverted-bitmap word: bits + word  (dimension value bitmap index)
+  F_BITMAP = 1,     // push bitmap leaf `lo` (chunk-level OR of bm_count rows of an inverted bitmap index)
   F_ID_RANGE = 2,   // push lo <= id < hi
   F_IN_SET = 3,     // push bitset[id]    (dictionary-domain predicate, evaluated once per dict entry)
   F_INT_RANGE = 4,  // push lo <= v <= hi   (integer / decimal-scaled metric or time)
@@ -43,7 +45,7 @@ enum FOpCode : int32_t {
 struct ColRef {
   uint64_t ptr;
   int32_t dtype;
-  int32_t pad;
+  int32_t meta;  // host-packed: lg | signed << 4 | float << 5 | LDS plane << 8
 };
 
 struct FOp {
@@ -158,6 +160,22 @@ struct ScanDesc {
   EOp eops[MAX_EOPS];
   ZoneP zones[MAX_ZONES];
   Range ranges[MAX_RANGES];
+  // ---- v3: chunk-level bitmap pre-filter + per-wave LDS staging of column tiles (LDS-DMA) ----
+  int32_t nfc;            // filter-phase columns: cols[0 .. nfc)
+  int32_t npc;            // payload columns: cols[PAYLOAD_BASE .. PAYLOAD_BASE + npc)
+  int32_t pre_off;        // bitmap-only conjuncts: fops[pre_off .. pre_off + pre_len), evaluated per chunk
+  int32_t pre_len;
+  int32_t final_pre;      // the pre-filter IS the whole filter (no per-row leaves)
+  int32_t nbm;
+  int32_t nplanes;        // 4-byte x 64-lane LDS planes per word (64-bit columns take two)
+  int32_t lds_cache_off;  // byte offset of the per-wave staging regions in dynamic LDS
+  int32_t lds_wave_bytes; // bytes per wave: nplanes * U * 256 + nbm * 512
+  int32_t unroll;         // U (words per step) the host sized the regions for
+  int32_t narrow4;        // LDS-DMA of 1/2-byte elements lands at lane*4 (probed at load time)
+  int32_t pad2;
+  uint64_t bm_bits[MAX_BM];
+  int64_t bm_stride[MAX_BM];
+  int64_t bm_count[MAX_BM];
 };
 
 }  // namespace sdo

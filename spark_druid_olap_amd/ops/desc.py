@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import numpy as np
 
-MAX_COLS = 16
+MAX_COLS = 24
 MAX_FOPS = 48
 MAX_KOPS = 8
 MAX_AOPS = 12
@@ -17,6 +17,8 @@ MAX_EOPS = 64
 MAX_ZONES = 4
 MAX_RANGES = 8
 MAX_SLOTS = 16
+MAX_BM = 8
+PAYLOAD_BASE = 8
 STACK_DEPTH = 6
 CHUNK_ROWS = 4096
 
@@ -31,7 +33,7 @@ M_DENSE_LDS, M_DENSE_GLOBAL, M_HASH, M_MASK = range(4)
 INT64_MAX = np.iinfo(np.int64).max
 INT64_MIN = np.iinfo(np.int64).min
 
-COLREF = np.dtype([("ptr", "<u8"), ("dtype", "<i4"), ("pad", "<i4")], align=True)
+COLREF = np.dtype([("ptr", "<u8"), ("dtype", "<i4"), ("meta", "<i4")], align=True)
 FOP = np.dtype([("op", "<i4"), ("col", "<i4"), ("flags", "<i4"), ("pad", "<i4"), ("lo", "<i8"), ("hi", "<i8"),
                 ("flo", "<f8"), ("fhi", "<f8"), ("bits", "<u8")], align=True)
 KOP = np.dtype([("kind", "<i4"), ("col", "<i4"), ("tfield", "<i4"), ("pad", "<i4"), ("stride", "<i8"),
@@ -57,6 +59,10 @@ SCANDESC = np.dtype([
     ("cols", COLREF, (MAX_COLS,)), ("fops", FOP, (MAX_FOPS,)), ("kops", KOP, (MAX_KOPS,)),
     ("aops", AOP, (MAX_AOPS,)), ("eops", EOP, (MAX_EOPS,)), ("zones", ZONEP, (MAX_ZONES,)),
     ("ranges", RANGE, (MAX_RANGES,)),
+    ("nfc", "<i4"), ("npc", "<i4"), ("pre_off", "<i4"), ("pre_len", "<i4"), ("final_pre", "<i4"), ("nbm", "<i4"),
+    ("nplanes", "<i4"), ("lds_cache_off", "<i4"), ("lds_wave_bytes", "<i4"), ("unroll", "<i4"),
+    ("narrow4", "<i4"), ("pad2", "<i4"),
+    ("bm_bits", "<u8", (MAX_BM,)), ("bm_stride", "<i8", (MAX_BM,)), ("bm_count", "<i8", (MAX_BM,)),
 ], align=True)
 
 

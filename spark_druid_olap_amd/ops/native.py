@@ -43,6 +43,20 @@ def load(build_if_missing: bool = True):
         return _mod
 
 
+_narrow4 = None
+
+
+def narrow4() -> int:
+    """1 if 1/2-byte LDS-DMA elements land at lane*4 on this GPU (probed once per process)."""
+    global _narrow4
+    if _narrow4 is None:
+        r = load().glds_probe()
+        if r not in (1, 4):
+            raise NativeUnavailable(f"unexpected LDS-DMA layout (probe={r})")
+        _narrow4 = 1 if r == 4 else 0
+    return _narrow4
+
+
 def available() -> bool:
     try:
         load()

@@ -202,7 +202,7 @@ def _expr_values(prog, eops, rows: torch.Tensor) -> torch.Tensor:
     st: List[torch.Tensor] = []
     for op, col, c in eops:
         if op == D.E_COL:
-            v = _col(prog, prog.cols[col])[rows].to(torch.float64)
+            v = _col(prog, prog.colname(col))[rows].to(torch.float64)
             st.append(v * c if c != 0.0 else v)
         elif op == D.E_CONST:
             st.append(torch.full((rows.numel(),), c, dtype=torch.float64, device=rows.device))
@@ -227,12 +227,12 @@ def _agg_values(prog, a, rows: torch.Tensor) -> torch.Tensor:
         if a.get("expr"):
             f = _expr_values(prog, a["expr"], rows)
         else:
-            f = _col(prog, prog.cols[a["col"]])[rows].to(torch.float64)
+            f = _col(prog, prog.colname(a["col"]))[rows].to(torch.float64)
         if k == D.A_SUM_F:
             return f
         b = f.view(torch.int64)
         return torch.where(b >= 0, b, b ^ 0x7FFFFFFFFFFFFFFF)
-    v = _col(prog, prog.cols[a["col"]])[rows]
+    v = _col(prog, prog.colname(a["col"]))[rows]
     if v.dtype.is_floating_point:
         v = v.to(torch.float64).trunc()
     return v.to(torch.int64)
@@ -292,7 +292,7 @@ def run_reference(prog, sparse: Optional[bool] = None):
         if a.get("filter") is not None:
             amask = eval_bexpr(prog, a["filter"], rows)
         r, ix = rows[amask], idx[amask]
-        v = _col(prog, prog.cols[a["col"]])[r].to(torch.int64)
+        v = _col(prog, prog.colname(a["col"]))[r].to(torch.int64)
         bucket, rho = hll_update_values(v, a.get("salt", 0), prog.hll_p)
         regs = torch.zeros(R * m, dtype=torch.int64, device=dev)
         regs.scatter_reduce_(0, ix * m + bucket, rho, reduce="amax", include_self=True)

@@ -419,24 +419,41 @@ def compile_function(src: str) -> Callable[..., Any]:
 
 # ------------------------------------------------------------------------------------------------
 # javascript aggregator -> (combine op, expression over fields)
-_AGG_SUM = re.compile(r"return\s*\(?\s*(?P<cur>\w+)\s*\+\s*(?P<e>.+?)\)?\s*;?\s*\}\s*$", re.S)
-_AGG_MINMAX = re.compile(r"return\s*\(?\s*Math\.(?P<f>max|min)\s*\(\s*(?P<cur>\w+)\s*,\s*(?P<e>.+)\)\s*\)?\s*;?\s*\}\s*$", re.S)
+def _strip_parens(e: str) -> str:
+    e = e.strip()
+    while e.startswith("(") and e.endswith(")"):
+        depth = 0
+        for i, ch in enumerate(e):
+            depth += ch == "("
+            depth -= ch == ")"
+            if depth == 0 and i < len(e) - 1:
+                return e
+        e = e[1:-1].strip()
+    return e
 
 
 def jsagg_to_expr(fn_aggregate: str):
     """Recognize ``current + <expr>`` / ``Math.max(current, <expr>)`` aggregate bodies.
 
     Returns (op in {'sum','max','min'}, param names, expression string) or raises JSError."""
-    m = re.match(r"\s*function\s*\w*\s*\((?P<p>[^)]*)\)\s*\{(?P<body>.*)$", fn_aggregate, re.S)
+    m = re.match(r"\s*function\s*\w*\s*\((?P<p>[^)]*)\)\s*\{(?P<body>.*)\}\s*$", fn_aggregate, re.S)
     if not m:
         raise JSError("not a javascript function")
     params = [x.strip() for x in m.group("p").split(",") if x.strip()]
-    body = m.group("body")
-    for rx, op in ((_AGG_MINMAX, None), (_AGG_SUM, "sum")):
-        mm = rx.search(body)
-        if mm and mm.group("cur") == params[0]:
-            expr = mm.group("e").strip()
-            return (op or mm.group("f"), params[1:], expr)
+    body = m.group("body").strip()
+    r = re.match(r"^return\s*(?P<e>.*?)\s*;?\s*$", body, re.S)
+    if not r or not params:
+        raise JSError("unsupported javascript aggregator body")
+    e = _strip_parens(r.group("e"))
+    cur = params[0]
+    mm = re.match(r"^Math\.(?P<f>max|min)\s*\((?P<rest>.*)\)$", e, re.S)
+    if mm:
+        rest = mm.group("rest").strip()
+        if rest.startswith(cur) and rest[len(cur):].lstrip().startswith(","):
+            return (mm.group("f"), params[1:], rest[len(cur):].lstrip()[1:].strip())
+    ms = re.match(r"^%s\s*\+\s*(?P<e>.*)$" % re.escape(cur), e, re.S)
+    if ms:
+        return ("sum", params[1:], ms.group("e").strip())
     raise JSError("unsupported javascript aggregator body")
 
 

@@ -38,8 +38,9 @@ def gpu_ds():
 def assert_same(a, b, hll_cols=(), rtol=1e-9):
     assert a.columns == b.columns
     assert a.num_rows == b.num_rows, (a.num_rows, b.num_rows)
-    ka = sorted(range(a.num_rows), key=lambda i: tuple(str(a.data[c][i]) for c in a.columns if a.data[c].dtype == object))
-    kb = sorted(range(b.num_rows), key=lambda i: tuple(str(b.data[c][i]) for c in b.columns if b.data[c].dtype == object))
+    keycols = [c for c in a.columns if a.data[c].dtype.kind in "OiuU"]
+    ka = sorted(range(a.num_rows), key=lambda i: tuple(str(a.data[c][i]) for c in keycols))
+    kb = sorted(range(b.num_rows), key=lambda i: tuple(str(b.data[c][i]) for c in keycols))
     for c in a.columns:
         va, vb = np.asarray(a.data[c])[ka], np.asarray(b.data[c])[kb]
         if va.dtype == object:

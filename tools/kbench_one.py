@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""Run one benchmark query's scan kernel N times (for rocprofv3 --pmc / kernel-trace focus)."""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sf", type=float, default=10)
+    ap.add_argument("--query", default="Ship Date Range")
+    ap.add_argument("--iters", type=int, default=3)
+    args = ap.parse_args()
+    from spark_druid_olap_amd.engine import device_exec as DE
+    from spark_druid_olap_amd.engine.executor import Engine
+    from spark_druid_olap_amd.models import tpch
+    from spark_druid_olap_amd.models.bench_queries import bench_specs
+    from spark_druid_olap_amd.ops import native
+
+    flat = tpch.generate_flat(args.sf, "cuda")
+    ds = tpch.to_datasource(flat, profile="bench")
+    del flat
+    eng = Engine()
+    names = [args.query] if args.query != "all" else [n for n, _ in bench_specs()]
+    for name in names:
+        q = dict(bench_specs())[name]
+        pq = eng.prepare(q, ds)
+        _, prog, prep = pq.scans[0]
+        pq.run()
+        torch.cuda.synchronize()
+        for _ in range(args.iters):
+            prep._reset()
+            native.scan(prep.desc, prep.grid, DE.BLOCK, prep.lds_total, DE.UNROLL)
+        torch.cuda.synchronize()
+        print("done", name, flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,17 @@
+#!/usr/bin/env python3
+"""Average PMC counter values per kernel from rocprofv3 counter_collection.csv files."""
+import csv
+import glob
+import sys
+from collections import defaultdict
+
+root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
+filt = sys.argv[2] if len(sys.argv) > 2 else "olap_scan"
+vals = defaultdict(list)
+for f in glob.glob(f"{root}/pmc*/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        if filt in r.get("Kernel_Name", ""):
+            vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k in sorted(vals):
+    v = vals[k]
+    print(f"{k:28s} n={len(v):3d} mean={sum(v)/len(v):16.1f} last={v[-1]:16.1f}")
