@@ -28,6 +28,34 @@ DENSE_GLOBAL_MAX_BYTES = int(os.environ.get("SDO_DENSE_MAX_BYTES", 1 << 30))
 BLOCK = 512
 UNROLL = int(os.environ.get("SDO_UNROLL", "2"))
 BLOCKS_PER_CU = int(os.environ.get("SDO_BLOCKS_PER_CU", "3"))
+USE_JIT = os.environ.get("SDO_JIT", "1") != "0"
+
+
+def _jit_for(prog, mode: int, hll_lds: bool, m: int):
+    """Specialized kernel for this program shape (None -> use the interpreter)."""
+    if not USE_JIT:
+        return None
+    from ..ops import jit
+
+    nplanes = sum(2 if column_tensor_size(prog, c) == 8 else 1 for c in prog.cols)
+    prefs = [16, 8, 4, 2] if nplanes <= 3 else ([8, 4, 2] if nplanes <= 8 else [4, 2])
+    for U in prefs:
+        lay = jit.layout(prog, mode, U, hll_lds, m)
+        if lay.total <= 160 * 1024 and (mode != D.M_DENSE_LDS or lay.ncopy >= 4 or U == prefs[-1]):
+            try:
+                return jit.JitScan(prog, mode, U, hll_lds, m, bool(native.narrow4()))
+            except Exception as e:  # pragma: no cover - compile problems fall back loudly
+                import warnings
+
+                warnings.warn(f"JIT compile failed, using the interpreter kernel: {e}")
+                return None
+    return None
+
+
+def column_tensor_size(prog, name: str) -> int:
+    from .lower import column_tensor
+
+    return column_tensor(prog.ds, name).element_size()
 
 _cu_cache = {}
 
@@ -75,6 +103,10 @@ class PreparedScan:
             self.cap = _next_pow2(2 * est)
         else:
             self.cap = 0
+        self.jit = None
+        if not prog.empty:
+            jit_hll_lds = bool(prog.nhll) and mode == D.M_DENSE_LDS and hll_bytes <= LDS_BUDGET
+            self.jit = _jit_for(prog, mode, jit_hll_lds, self.m)
         self._alloc()
 
     # ------------------------------------------------------------------ buffers
@@ -106,7 +138,13 @@ class PreparedScan:
                  unroll=UNROLL, cache_off=cache_off, wave_bytes=wave_bytes)
         self.lds_total = total
         self.desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
-        self.grid = _grid(dev, int(d[0]["total_chunks"]), total)
+        self.grid = _grid(dev, int(d[0]["total_chunks"]), self.jit.lay.total if self.jit else total)
+
+    def _launch(self):
+        if self.jit is not None:
+            self.jit.launch(self.desc, self.grid)
+        else:
+            native.scan(self.desc, self.grid, BLOCK, self.lds_total, UNROLL)
 
     def _reset(self):
         self.acc.copy_(self.init_row.expand_as(self.acc))
@@ -123,7 +161,7 @@ class PreparedScan:
             return self._empty()
         while True:
             self._reset()
-            native.scan(self.desc, self.grid, BLOCK, self.lds_total, UNROLL)
+            self._launch()
             if self.mode != D.M_HASH:
                 break
             if int(self.overflow.item()) == 0:
@@ -159,7 +197,8 @@ class PreparedMask:
                  unroll=UNROLL, cache_off=cache_off, wave_bytes=wave_bytes)
         self.lds_total = total
         self.desc = torch.from_numpy(d.view(np.uint8).copy()).to(self.dev)
-        self.grid = _grid(self.dev, int(d[0]["total_chunks"]), total)
+        self.jit = _jit_for(prog, D.M_MASK, False, 2048) if not prog.empty else None
+        self.grid = _grid(self.dev, int(d[0]["total_chunks"]), self.jit.lay.total if self.jit else total)
 
     def run(self) -> torch.Tensor:
         """Row ids passing the filter (sorted)."""
@@ -167,7 +206,10 @@ class PreparedMask:
             return torch.zeros(0, dtype=torch.int64, device=self.dev)
         self.mask.zero_()
         self.count.zero_()
-        native.scan(self.desc, self.grid, BLOCK, self.lds_total, UNROLL)
+        if self.jit is not None:
+            self.jit.launch(self.desc, self.grid)
+        else:
+            native.scan(self.desc, self.grid, BLOCK, self.lds_total, UNROLL)
         nzw = torch.nonzero(self.mask).flatten()
         if nzw.numel() == 0:
             return nzw

@@ -22,6 +22,7 @@ from ..parallel.world import World, get_world
 from ..query import spec as S
 from ..query.jsfunc import compile_function
 from ..segment.datasource import DataSource
+from .columns import DictColumn, materialize, take
 from .lower import Lowerer, LoweringError, ScanProgram
 from .partials import Partials, finalize
 
@@ -42,13 +43,13 @@ class QueryResult:
         return self.data[name]
 
     def rows(self) -> List[tuple]:
-        cols = [self.data[c] for c in self.columns]
-        return [tuple(_py(c[i]) for c in cols) for i in range(self.num_rows)]
+        cols = [materialize(self.data[c]).tolist() for c in self.columns]
+        return list(zip(*cols)) if cols else []
 
     def to_pandas(self):
         import pandas as pd
 
-        return pd.DataFrame({c: self.data[c] for c in self.columns}, columns=self.columns)
+        return pd.DataFrame({c: materialize(self.data[c]) for c in self.columns}, columns=self.columns)
 
     def sorted_rows(self) -> List[tuple]:
         return sorted(self.rows(), key=lambda r: tuple((x is None, str(x)) for x in r))
@@ -215,7 +216,7 @@ class PreparedQuery:
             idx = idx[np.argsort(cols["timestamp"][idx], kind="stable")]
             if getattr(qs, "descending", False):
                 idx = idx[::-1]
-        data = {c: np.asarray(cols[c])[idx] for c in out_cols}
+        data = {c: take(cols[c], idx) for c in out_cols}
         return QueryResult(out_cols, data, qt, {"groups": n})
 
     def _topn_order(self, cols, idx, prog) -> np.ndarray:
@@ -230,7 +231,7 @@ class PreparedQuery:
             key = np.asarray(cols[metric.metric], dtype=np.float64)[idx]
             order = np.argsort(key if invert else -key, kind="stable")
         else:
-            vals = np.asarray(cols[dimname])[idx]
+            vals = materialize(take(cols[dimname], idx))
             if isinstance(metric, S.AlphaNumericTopNMetricSpec):
                 skey = [(_alnum_key(v)) for v in vals]
             else:
@@ -296,7 +297,7 @@ class PreparedQuery:
         data["timestamp"] = ds.time[page].to(torch.int64).cpu().numpy() * u
         for d in dims:
             ids = column_tensor(ds, d)[page].to(torch.int64).cpu().numpy()
-            data[d] = ds.dims[d].dictionary.decode(ids)
+            data[d] = DictColumn(ids, ds.dims[d].dictionary)
         for m in mets:
             mc = ds.metrics[m]
             v = mc.data[page].cpu().numpy()
@@ -316,7 +317,7 @@ def _gather_columns(world: World, data: Dict[str, np.ndarray]) -> Dict[str, np.n
     import torch.distributed as dist
 
     lst = [None] * world.size
-    dist.all_gather_object(lst, data)
+    dist.all_gather_object(lst, {k: materialize(v) for k, v in data.items()})
     out = {}
     for k in data:
         out[k] = np.concatenate([np.asarray(d[k]) for d in lst])
@@ -422,7 +423,12 @@ def order_and_limit(cols: Dict[str, np.ndarray], idx: np.ndarray, order_cols, li
         for oc in reversed(order_cols):
             if isinstance(oc, str):
                 oc = S.OrderByColumnSpec(oc)
-            v = np.asarray(cols[oc.dimension])[idx]
+            col = cols[oc.dimension]
+            if isinstance(col, DictColumn):  # sorted dictionaries: code order == value order
+                v = col.codes[idx]
+                keys.append(v.astype(np.float64) if oc.ascending else -v.astype(np.float64))
+                continue
+            v = np.asarray(col)[idx]
             if v.dtype == object:
                 _, codes = np.unique(np.array([("" if x is None else str(x)) for x in v], dtype=object).astype(str),
                                      return_inverse=True)

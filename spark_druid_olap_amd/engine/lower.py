@@ -29,6 +29,7 @@ from ..query.intervals import Interval, parse_iso_ms
 from ..query.jsfunc import JSError, compile_function, jsagg_to_expr, parse_expr
 from ..segment.datasource import CHUNK_ROWS, DataSource, dtype_code
 from ..segment.dictionary import Dictionary
+from .columns import DictColumn
 
 TIME = "__time"
 HLL_P = 11  # 2048 registers, the precision of Druid's HyperUnique
@@ -691,7 +692,7 @@ class Lowerer:
             raise LoweringError(f"group by unknown dimension {dim!r}")
         d = ds.dims[dim].dictionary
         if fn is None:
-            return KeyComp(name, D.K_ID, dim, len(d), decoder=d.decode)
+            return KeyComp(name, D.K_ID, dim, len(d), decoder=lambda ids, _d=d: DictColumn(ids, _d))
         if isinstance(fn, S.TimeFormatExtractionFunctionSpec) and d.vtype != "string":
             pass
         f = extraction_callable(fn)
@@ -700,7 +701,7 @@ class Lowerer:
         has_null = any(v is None for v in derived.tolist())
         dd = Dictionary(uniq, "string" if all(isinstance(v, str) for v in uniq) else "double", has_null)
         remap = np.array([dd.lookup(v) for v in derived.tolist()], dtype=np.int32)
-        return KeyComp(name, D.K_REMAP, dim, len(dd), remap=remap, decoder=dd.decode)
+        return KeyComp(name, D.K_REMAP, dim, len(dd), remap=remap, decoder=lambda ids, _d=dd: DictColumn(ids, _d))
 
     def _time_key(self, name, fn, ivs: List[Interval]) -> KeyComp:
         lo, hi = self._data_span(ivs)

@@ -80,7 +80,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         subprocess.run(cmd, check=True)
         objs.append(str(obj))
     tmp = target.with_suffix(".tmp.so")
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", str(tmp)]
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", str(tmp), "-lhiprtc"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

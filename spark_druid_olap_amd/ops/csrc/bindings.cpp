@@ -4,9 +4,13 @@
 // builds in seconds with hipcc.  It must be imported after torch so that the HIP runtime torch
 // loaded (same SONAME) is the one this module binds to.
 #include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <vector>
 #include "scan_desc.h"
 
 namespace sdo {
@@ -88,6 +92,63 @@ static int glds_probe() {
   return -1;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Per-query JIT kernels (ops/jit.py): hipRTC compile -> code object bytes (cached on disk by the
+// caller) -> hipModuleLoadData -> launch.  Compilation needs no GPU.
+static py::bytes rtc_compile(const std::string& src, const std::string& name, const std::vector<std::string>& opts) {
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), (name + ".hip").c_str(), 0, nullptr, nullptr) != HIPRTC_SUCCESS)
+    throw std::runtime_error("hiprtcCreateProgram failed");
+  std::vector<const char*> o;
+  for (auto& x : opts) o.push_back(x.c_str());
+  const hiprtcResult r = hiprtcCompileProgram(prog, (int)o.size(), o.data());
+  size_t ls = 0;
+  hiprtcGetProgramLogSize(prog, &ls);
+  std::string log(ls, '\0');
+  if (ls) hiprtcGetProgramLog(prog, &log[0]);
+  if (r != HIPRTC_SUCCESS) {
+    hiprtcDestroyProgram(&prog);
+    throw std::runtime_error("hiprtc compile failed: " + log);
+  }
+  size_t cs = 0;
+  hiprtcGetCodeSize(prog, &cs);
+  std::string code(cs, '\0');
+  hiprtcGetCode(prog, &code[0]);
+  hiprtcDestroyProgram(&prog);
+  return py::bytes(code);
+}
+
+struct JitKernel {
+  hipModule_t mod;
+  hipFunction_t fn;
+};
+static std::vector<JitKernel> g_jit;
+static std::mutex g_jit_mu;
+
+static int module_load(const std::string& code, const std::string& name) {
+  JitKernel k;
+  check(hipModuleLoadData(&k.mod, code.data()), "hipModuleLoadData");
+  check(hipModuleGetFunction(&k.fn, k.mod, name.c_str()), "hipModuleGetFunction");
+  std::lock_guard<std::mutex> g(g_jit_mu);
+  g_jit.push_back(k);
+  return (int)g_jit.size() - 1;
+}
+
+static void module_launch(int h, uint64_t desc, int grid, int block, int lds, uint64_t stream) {
+  hipFunction_t fn;
+  {
+    std::lock_guard<std::mutex> g(g_jit_mu);
+    if (h < 0 || h >= (int)g_jit.size()) throw std::invalid_argument("bad jit handle");
+    fn = g_jit[h].fn;
+  }
+  if (block % 64 != 0 || block > 1024 || block <= 0) throw std::invalid_argument("bad block size");
+  if (lds < 0 || lds > 160 * 1024) throw std::invalid_argument("lds bytes out of range");
+  if (grid <= 0) return;
+  void* args[] = {(void*)&desc};
+  check(hipModuleLaunchKernel(fn, grid, 1, 1, block, 1, 1, (unsigned)lds, (hipStream_t)stream, args, nullptr),
+        "jit kernel launch");
+}
+
 static int desc_size() { return (int)sizeof(sdo::ScanDesc); }
 
 static py::dict layout() {
@@ -132,6 +193,9 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("bitmap_build", &bitmap_build);
   m.def("hll_estimate", &hll_estimate);
   m.def("desc_size", &desc_size);
+  m.def("rtc_compile", &rtc_compile);
+  m.def("module_load", [](py::bytes code, const std::string& name) { return module_load(std::string(code), name); });
+  m.def("module_launch", &module_launch);
   m.def("glds_probe", &glds_probe);
   m.def("layout", &layout);
   m.def("device_info", &device_info);

@@ -7,7 +7,18 @@
 // per-row work is loads + a handful of VALU ops.  The layout is plain-old-data with explicit
 // padding; never reorder fields without updating ops/desc.py (a unit test checks the sizes).
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <stdint.h>
+#else
+using __hip_internal::int8_t;
+using __hip_internal::int16_t;
+using __hip_internal::int32_t;
+using __hip_internal::int64_t;
+using __hip_internal::uint8_t;
+using __hip_internal::uint16_t;
+using __hip_internal::uint32_t;
+using __hip_internal::uint64_t;
+#endif
 
 namespace sdo {
 

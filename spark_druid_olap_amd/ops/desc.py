@@ -21,6 +21,7 @@ MAX_BM = 8
 PAYLOAD_BASE = 8
 STACK_DEPTH = 6
 CHUNK_ROWS = 4096
+CHUNK_WORDS = CHUNK_ROWS // 64
 
 # opcodes
 F_TRUE, F_BITMAP, F_ID_RANGE, F_IN_SET, F_INT_RANGE, F_FLT_RANGE, F_AND, F_OR, F_NOT, F_FALSE, F_BITMAP_OR = range(11)

@@ -1,0 +1,495 @@
+"""Per-query kernel specialization (JIT) for the fused scan.
+
+The precompiled interpreter (``csrc/olap_scan.hip``) decodes opcodes, column widths and key
+strides from the descriptor at run time; on CDNA4 that costs ~80 scalar instructions and several
+dependent scalar loads per LDS-DMA (measured: profiles/pmc_shipdate_sf10_v3.txt).  Here the same
+ScanProgram is emitted as C++ in which every opcode, column width, LDS plane, key stride and
+aggregator is a compile-time constant and filters are straight boolean expressions over
+``__ballot`` masks / bitmap words; hipRTC compiles it for gfx950 once per query shape and the
+code object is cached on disk by source hash.  Device pointers still come from the descriptor,
+so one compiled kernel serves every shard/rank and every re-execution of a prepared query.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import threading
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from . import desc as D
+
+CSRC = Path(__file__).resolve().parent / "csrc"
+OPTS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-munsafe-fp-atomics", f"-I{CSRC}"]
+W = 8  # waves per block (512 threads)
+
+_lock = threading.Lock()
+_handles: Dict[str, int] = {}
+
+
+def cache_dir() -> Path:
+    p = Path(os.environ.get("SDO_JIT_CACHE", os.path.join(os.path.expanduser("~"), ".cache", "sdo_jit")))
+    p.mkdir(parents=True, exist_ok=True)
+    return p
+
+
+@dataclass
+class ColInfo:
+    name: str
+    idx: int       # descriptor column index
+    lg: int
+    sgn: bool
+    flt: bool
+    plane: int
+
+
+@dataclass
+class JitLayout:
+    acc_off: int
+    acc_bytes: int
+    hll_off: int
+    hll_bytes: int
+    cache_off: int
+    wave_bytes: int
+    total: int
+    ncopy: int
+
+
+def col_infos(prog) -> Dict[int, ColInfo]:
+    from ..engine.lower import column_tensor
+
+    out = {}
+    plane = 0
+    for base, names in ((0, prog.fcols), (D.PAYLOAD_BASE, prog.pcols)):
+        for j, name in enumerate(names):
+            t = column_tensor(prog.ds, name)
+            lg = {1: 0, 2: 1, 4: 2, 8: 3}[t.element_size()]
+            out[base + j] = ColInfo(name, base + j, lg, t.dtype in (torch.int16, torch.int32, torch.int64),
+                                    t.dtype.is_floating_point, plane)
+            plane += 2 if lg == 3 else 1
+    return out
+
+
+def layout(prog, mode: int, U: int, hll_lds: bool, m: int) -> JitLayout:
+    cols = col_infos(prog)
+    nplanes = sum(2 if c.lg == 3 else 1 for c in cols.values())
+    need_bmw = _needs_word_bitmaps(prog)
+    wave_bytes = U * nplanes * 256 + (len(prog.bm_leaves) * 512 if need_bmw else 0)
+    wave_bytes = (wave_bytes + 15) // 16 * 16
+    hll_bytes = prog.nhll * prog.G * m * 4 if hll_lds else 0
+    stage = W * wave_bytes
+    ncopy = 1
+    acc_bytes = 0
+    if mode == D.M_DENSE_LDS:
+        base = prog.G * prog.nslots * 8 * W
+        ncopy = 16
+        while ncopy > 1 and base * ncopy + hll_bytes + stage > 150 * 1024:
+            ncopy //= 2
+        acc_bytes = base * ncopy
+    acc_off = 0
+    hll_off = (acc_bytes + 15) // 16 * 16
+    cache_off = (hll_off + hll_bytes + 15) // 16 * 16
+    total = cache_off + stage
+    return JitLayout(acc_off, acc_bytes, hll_off, hll_bytes, cache_off, wave_bytes, total, ncopy)
+
+
+def _needs_word_bitmaps(prog) -> bool:
+    spans = [(0, prog.filter_len)] if not prog.final_pre else []
+    for a in prog.aops:
+        if a.get("filt_len"):
+            spans.append((a["filt_off"], a["filt_off"] + a["filt_len"]))
+    return any(prog.fops[i][0] == D.F_BITMAP for a, b in spans for i in range(a, b))
+
+
+def _lit(v: int) -> str:
+    v = int(v)
+    if v == -(2 ** 63):
+        return "(-9223372036854775807LL - 1)"
+    return f"{v}LL"
+
+
+def _dlit(v: float) -> str:
+    if v == float("inf"):
+        return "__builtin_inf()"
+    if v == float("-inf"):
+        return "(-__builtin_inf())"
+    return repr(float(v))
+
+
+class _Gen:
+    def __init__(self, prog, mode: int, U: int, hll_lds: bool, narrow4: bool, lay: JitLayout, m: int):
+        self.p = prog
+        self.mode = mode
+        self.U = U
+        self.hll_lds = hll_lds
+        self.n4 = "true" if narrow4 else "false"
+        self.lay = lay
+        self.m = m
+        self.cols = col_infos(prog)
+        self.NP = sum(2 if c.lg == 3 else 1 for c in self.cols.values())
+        self.pre_lines: List[str] = []  # kernel-entry pointer loads
+
+    # ---------------------------------------------------------------- values
+    def ival(self, idx: int) -> str:
+        c = self.cols[idx]
+        return (f"ld_int<{c.lg}, {'true' if c.sgn else 'false'}, {'true' if c.flt else 'false'}, {self.n4}>"
+                f"(wb + (u * {self.NP} + {c.plane}) * 256, lane)")
+
+    def dval(self, idx: int) -> str:
+        c = self.cols[idx]
+        return (f"ld_dbl<{c.lg}, {'true' if c.sgn else 'false'}, {'true' if c.flt else 'false'}, {self.n4}>"
+                f"(wb + (u * {self.NP} + {c.plane}) * 256, lane)")
+
+    # ---------------------------------------------------------------- filters
+    def word_expr(self, lo: int, hi: int) -> str:
+        st: List[str] = []
+        for i in range(lo, hi):
+            op, col, flags, a, b, fa, fb, bits = self.p.fops[i]
+            if op == D.F_TRUE:
+                st.append("(~0ull)")
+            elif op == D.F_FALSE:
+                st.append("(0ull)")
+            elif op == D.F_BITMAP:
+                st.append(f"uniform64(bmw[{int(a)} * 64 + wl[u]])")
+            elif op in (D.F_ID_RANGE, D.F_INT_RANGE):
+                cmp = "<" if op == D.F_ID_RANGE else "<="
+                st.append(f"([&]() {{ const int64_t v = {self.ival(col)}; "
+                          f"return (uint64_t)__ballot(v >= {_lit(a)} && v {cmp} {_lit(b)}); }}())")
+            elif op == D.F_IN_SET:
+                self.pre_lines.append(f"const uint64_t* inset{i} = (const uint64_t*)d->fops[{i}].bits;")
+                st.append(f"([&]() {{ const int64_t v = {self.ival(col)}; "
+                          f"return (uint64_t)__ballot((inset{i}[((uint64_t)v) >> 6] >> (v & 63)) & 1ull); }}())")
+            elif op == D.F_FLT_RANGE:
+                lo_c = ">" if flags & 1 else ">="
+                hi_c = "<" if flags & 2 else "<="
+                st.append(f"([&]() {{ const double v = {self.dval(col)}; "
+                          f"return (uint64_t)__ballot(v {lo_c} {_dlit(fa)} && v {hi_c} {_dlit(fb)}); }}())")
+            elif op in (D.F_AND, D.F_OR):
+                y, x = st.pop(), st.pop()
+                st.append(f"({x} {'&' if op == D.F_AND else '|'} {y})")
+            elif op == D.F_NOT:
+                st.append(f"(~{st.pop()})")
+            else:
+                raise ValueError(f"opcode {op} not supported in jit word filter")
+        return st[-1] if st else "(~0ull)"
+
+    def chunk_expr(self) -> str:
+        st: List[str] = []
+        p = self.p
+        for i in range(p.pre_off, p.pre_off + p.pre_len):
+            op, col, flags, a, b, fa, fb, bits = p.fops[i]
+            if op == D.F_BITMAP:
+                st.append(f"lw{int(a)}")
+            elif op == D.F_TRUE:
+                st.append("(~0ull)")
+            elif op == D.F_FALSE:
+                st.append("(0ull)")
+            elif op in (D.F_AND, D.F_OR):
+                y, x = st.pop(), st.pop()
+                st.append(f"({x} {'&' if op == D.F_AND else '|'} {y})")
+            elif op == D.F_NOT:
+                st.append(f"(~{st.pop()})")
+            else:
+                raise ValueError(f"opcode {op} in chunk-level program")
+        return st[-1] if st else "(~0ull)"
+
+    # ---------------------------------------------------------------- expression VM -> C++
+    def expr(self, eops) -> str:
+        st: List[str] = []
+        for op, col, c in eops:
+            if op == D.E_COL:
+                v = self.dval(col)
+                st.append(f"({v} * {_dlit(c)})" if c != 0.0 else f"({v})")
+            elif op == D.E_CONST:
+                st.append(f"({_dlit(c)})")
+            elif op == D.E_NEG:
+                st.append(f"(-{st.pop()})")
+            elif op == D.E_ABS:
+                st.append(f"fabs({st.pop()})")
+            else:
+                y, x = st.pop(), st.pop()
+                sym = {D.E_ADD: "+", D.E_SUB: "-", D.E_MUL: "*", D.E_DIV: "/"}.get(op)
+                if sym:
+                    st.append(f"({x} {sym} {y})")
+                else:
+                    st.append(f"{'fmin' if op == D.E_MIN else 'fmax'}({x}, {y})")
+        return st[-1]
+
+    # ---------------------------------------------------------------- whole kernel
+    def source(self, name: str) -> str:
+        p, U, NP, lay = self.p, self.U, self.NP, self.lay
+        mode = self.mode
+        L: List[str] = []
+        fcols = [i for i in sorted(self.cols) if i < D.PAYLOAD_BASE]
+        pcols = [i for i in sorted(self.cols) if i >= D.PAYLOAD_BASE]
+        need_bmw = _needs_word_bitmaps(p)
+        word_filter = None if p.final_pre else self.word_expr(0, p.filter_len)
+        pre = self.chunk_expr() if p.pre_len else None
+        G, NS = p.G, p.nslots
+        NCT = W * lay.ncopy
+        for i in sorted(self.cols):
+            L.append(f"  const unsigned char* c{i} = (const unsigned char*)d->cols[{i}].ptr;")
+        for j, (row, stride, count) in enumerate(p.bm_leaves):
+            L.append(f"  const uint64_t* bm{j} = (const uint64_t*)d->bm_bits[{j}];")
+        for k, kc in enumerate(p.keys):
+            if kc.kind == D.K_REMAP:
+                L.append(f"  const int32_t* rm{k} = (const int32_t*)d->kops[{k}].remap;")
+        for z in range(len(p.zones)):
+            L.append(f"  const int32_t* zmin{z} = (const int32_t*)d->zones[{z}].zmin;")
+            L.append(f"  const int32_t* zmax{z} = (const int32_t*)d->zones[{z}].zmax;")
+        for ai, a in enumerate(p.aops):
+            if a["kind"] == D.A_HLL:
+                if self.hll_lds and mode == D.M_DENSE_LDS:
+                    L.append(f"  uint32_t* hll{ai} = (uint32_t*)(lds + {lay.hll_off + a['hll'] * G * self.m * 4});")
+                else:
+                    L.append(f"  uint32_t* hll{ai} = (uint32_t*)d->aops[{ai}].hll_regs;")
+        body = []
+        # ---------------- per-word processing
+        body.append("      // ---- payload staging (inactive lanes alias the first active row) ----")
+        body.append(f"      int64_t lrow[{U}];")
+        body.append(f"      bool act[{U}];")
+        body.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{")
+        body.append("        act[u] = (m[u] >> lane) & 1ull;")
+        body.append("        lrow[u] = act[u] ? row[u] : (cw0 + wl[u]) * 64 + (m[u] ? __builtin_ctzll(m[u]) : 0);")
+        body.append("      }")
+        if pcols:
+            body.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
+            body.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{")
+            for i in pcols:
+                c = self.cols[i]
+                body.append(f"        dma<{c.lg}>(c{i}, lrow[u], wb + (u * {NP} + {c.plane}) * 256);")
+            body.append("      }")
+            body.append('      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
+        body.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{")
+        body.append("        if (!m[u]) continue;")
+        body.append("        uint64_t key = 0;")
+        for k, kc in enumerate(p.keys):
+            v = self.ival(kc.col_idx)
+            if kc.kind == D.K_ID:
+                body.append(f"        key += (uint64_t)({v}) * {kc.stride}ull;")
+            elif kc.kind == D.K_REMAP:
+                body.append(f"        key += (uint64_t)rm{k}[{v}] * {kc.stride}ull;")
+            elif kc.kind == D.K_TIME:
+                body.append(f"        {{ int64_t t = time_field_t<{kc.tfield}>(({v}) * {_lit(p.ds.time_unit_ms)} + "
+                            f"{_lit(kc.tz_ms)}, {_lit(kc.period_ms or 1)}, {_lit(kc.origin_ms)}) - {_lit(kc.base)};")
+                body.append(f"          t = t < 0 ? 0 : (t >= {_lit(kc.card)} ? {_lit(kc.card - 1)} : t);")
+                body.append(f"          key += (uint64_t)t * {kc.stride}ull; }}")
+            else:
+                body.append(f"        {{ int64_t t = ({v}) - {_lit(kc.base)};")
+                body.append(f"          t = t < 0 ? 0 : (t >= {_lit(kc.card)} ? {_lit(kc.card - 1)} : t);")
+                body.append(f"          key += (uint64_t)t * {kc.stride}ull; }}")
+        if mode == D.M_HASH:
+            body.append("        int64_t slot = act[u] ? hash_slot(hkeys, hcap, key, overflow) : -1;")
+            body.append("        const bool mine = act[u] && slot >= 0;")
+        else:
+            body.append("        const int64_t slot = (int64_t)key;")
+            body.append("        const bool mine = act[u];")
+        for ai, a in enumerate(p.aops):
+            cond = "mine"
+            if a.get("filt_len"):
+                fx = self.word_expr(a["filt_off"], a["filt_off"] + a["filt_len"])
+                body.append(f"        const bool f{ai} = mine && ((({fx}) >> lane) & 1ull);")
+                cond = f"f{ai}"
+            kind = a["kind"]
+            if kind == D.A_HLL:
+                body.append(f"        if ({cond}) hll_update(hll{ai}, slot, {p.hll_p}, {self.ival(a['col'])}, {_lit(a.get('salt', 0))});")
+                continue
+            s = a["slot"]
+            op = p.slots[s][0]
+            if kind == D.A_COUNT:
+                val = "1LL"
+            elif kind in (D.A_SUM_F, D.A_MIN_F, D.A_MAX_F):
+                dv = self.expr(a["expr"]) if a.get("expr") else self.dval(a["col"])
+                val = f"__double_as_longlong({dv})" if kind == D.A_SUM_F else f"f2ord({dv})"
+            else:
+                val = self.ival(a["col"])
+            if mode == D.M_DENSE_LDS:
+                tgt = f"acc + (slot * {NS} + {s}) * {NCT} + copy"
+            else:
+                tgt = f"gacc + slot * {NS} + {s}"
+            body.append(f"        if ({cond}) acc_update<{op}>({tgt}, {val});")
+        body.append("      }")
+        # ---------------- kernel text
+        out = []
+        out.append('#include "sdo_device.h"')
+        out.append("using namespace sdo;")
+        out.append("using namespace sdo::dev;")
+        out.append(f'extern "C" __global__ __launch_bounds__({W * 64}) void {name}(const ScanDesc* __restrict__ d) {{')
+        out.append("  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];")
+        out.append("  const int lane = threadIdx.x & 63;")
+        out.append("  const int wave = threadIdx.x >> 6;")
+        out.append(f"  unsigned char* wb = lds + {lay.cache_off} + wave * {lay.wave_bytes};")
+        out.append(f"  uint64_t* bmw = (uint64_t*)(wb + {U * NP * 256});")
+        out.append("  uint64_t* acc = (uint64_t*)lds;")
+        out.append(f"  const int copy = wave * {lay.ncopy} + (lane & {lay.ncopy - 1});")
+        out.append("  uint64_t* gacc = (uint64_t*)d->out_acc;")
+        out.append("  uint64_t* hkeys = (uint64_t*)d->out_keys;")
+        out.append("  const int64_t hcap = d->hash_cap;")
+        out.append("  int* overflow = (int*)d->overflow;")
+        out.append("  (void)bmw; (void)acc; (void)copy; (void)gacc; (void)hkeys; (void)hcap; (void)overflow;")
+        out.extend(L)
+        out.extend("  " + x for x in self.pre_lines)
+        if mode == D.M_DENSE_LDS:
+            out.append(f"  for (int i = threadIdx.x; i < {G * NS * NCT}; i += {W * 64}) {{")
+            inits = ", ".join(_lit(init) for _, init in p.slots)
+            out.append(f"    constexpr int64_t init[{NS}] = {{{inits}}};")
+            out.append(f"    acc[i] = (uint64_t)init[(i / {NCT}) % {NS}];")
+            out.append("  }")
+            if self.hll_lds and p.nhll:
+                out.append(f"  for (int i = threadIdx.x; i < {lay.hll_bytes // 4}; i += {W * 64}) "
+                           f"((uint32_t*)(lds + {lay.hll_off}))[i] = 0u;")
+            out.append("  __syncthreads();")
+        out.append(f"  const int64_t total_waves = (int64_t)gridDim.x * {W};")
+        out.append(f"  const int64_t gw = (int64_t)blockIdx.x * {W} + wave;")
+        out.append("  const int64_t num_rows = d->num_rows;")
+        out.append("  const int nranges = d->nranges;")
+        out.append("  for (int64_t c = gw; c < d->total_chunks; c += total_waves) {")
+        out.append("    int r = 0;")
+        out.append("    int64_t cc = c;")
+        out.append("    while (r < nranges - 1 && cc >= d->ranges[r].nchunks) { cc -= d->ranges[r].nchunks; ++r; }")
+        out.append("    const int64_t kchunk = d->ranges[r].chunk_begin + cc;")
+        out.append(f"    int64_t clo = kchunk * {D.CHUNK_ROWS}, chi = clo + {D.CHUNK_ROWS};")
+        out.append("    if (clo < d->ranges[r].lo) clo = d->ranges[r].lo;")
+        out.append("    if (chi > d->ranges[r].hi) chi = d->ranges[r].hi;")
+        out.append("    if (chi > num_rows) chi = num_rows;")
+        out.append("    if (chi <= clo) continue;")
+        for z, (dim, zlo, zhi) in enumerate(p.zones):
+            out.append(f"    if ((int64_t)zmax{z}[kchunk] < {_lit(zlo)} || (int64_t)zmin{z}[kchunk] >= {_lit(zhi)}) continue;")
+        out.append(f"    const int64_t cw0 = kchunk * {D.CHUNK_WORDS};")
+        out.append("    const int64_t my_r0 = (cw0 + lane) * 64;")
+        out.append("    const int64_t lo_off = clo - my_r0, hi_off = chi - my_r0;")
+        out.append("    uint64_t pre = range_bits((int)(lo_off < 0 ? 0 : (lo_off > 64 ? 64 : lo_off)),")
+        out.append("                              (int)(hi_off < 0 ? 0 : (hi_off > 64 ? 64 : hi_off)));")
+        for j, (row, stride, count) in enumerate(p.bm_leaves):
+            if count == 1:
+                out.append(f"    const uint64_t lw{j} = bm{j}[cw0 + lane];")
+            else:
+                out.append(f"    uint64_t lw{j} = 0;")
+                out.append(f"    for (int k = 0; k < {count}; ++k) lw{j} |= bm{j}[(int64_t)k * {stride} + cw0 + lane];")
+            if need_bmw:
+                out.append(f"    bmw[{j} * 64 + lane] = lw{j};")
+        if pre:
+            out.append(f"    pre &= {pre};")
+        out.append("    uint64_t nz = __ballot(pre != 0ull);")
+        out.append("    while (nz) {")
+        out.append(f"      int wl[{U}];")
+        out.append(f"      uint64_t m[{U}];")
+        out.append(f"      int64_t row[{U}];")
+        out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{")
+        out.append("        if (nz) { wl[u] = __builtin_ctzll(nz); nz &= nz - 1ull; m[u] = readlane64(pre, wl[u]); }")
+        out.append("        else { wl[u] = 0; m[u] = 0ull; }")
+        out.append("        row[u] = (cw0 + wl[u]) * 64 + lane;")
+        out.append("      }")
+        if word_filter is not None:
+            if fcols:
+                out.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
+                out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{")
+                for i in fcols:
+                    c = self.cols[i]
+                    out.append(f"        dma<{c.lg}>(c{i}, row[u], wb + (u * {NP} + {c.plane}) * 256);")
+                out.append("      }")
+                out.append('      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
+            out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) m[u] &= {word_filter};")
+        out.append("      uint64_t any = 0;")
+        out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) any |= m[u];")
+        out.append("      if (any == 0) continue;")
+        if mode == D.M_MASK:
+            out.append("      if (lane == 0) {")
+            out.append("        unsigned long long cnt = 0;")
+            out.append(f"#pragma unroll\n        for (int u = 0; u < {U}; ++u) {{")
+            out.append("          if (m[u]) ((uint64_t*)d->out_mask)[cw0 + wl[u]] = m[u];")
+            out.append("          cnt += __popcll(m[u]);")
+            out.append("        }")
+            out.append("        atomicAdd((unsigned long long*)d->out_count, cnt);")
+            out.append("      }")
+        else:
+            out.extend(body)
+        out.append("    }")
+        out.append("  }")
+        if mode == D.M_DENSE_LDS:
+            out.append("  __syncthreads();")
+            out.append(f"  for (int i = threadIdx.x; i < {G * NS}; i += {W * 64}) {{")
+            out.append(f"    const int s = i % {NS};")
+            ops = ", ".join(str(op) for op, _ in p.slots)
+            inits = ", ".join(_lit(init) for _, init in p.slots)
+            out.append(f"    constexpr int ops[{NS}] = {{{ops}}};")
+            out.append(f"    constexpr int64_t init[{NS}] = {{{inits}}};")
+            out.append(f"    const uint64_t* a = acc + (int64_t)i * {NCT};")
+            out.append("    int64_t v = (int64_t)a[0];")
+            out.append(f"    for (int k = 1; k < {NCT}; ++k) {{")
+            out.append("      const int64_t x = (int64_t)a[k];")
+            out.append("      switch (ops[s]) {")
+            out.append(f"        case {D.S_SUM_I}: v += x; break;")
+            out.append(f"        case {D.S_SUM_F}: v = __double_as_longlong(__longlong_as_double(v) + __longlong_as_double(x)); break;")
+            out.append(f"        case {D.S_MIN_I}: v = x < v ? x : v; break;")
+            out.append("        default: v = x > v ? x : v; break;")
+            out.append("      }")
+            out.append("    }")
+            out.append("    if (v != init[s]) acc_update_rt(gacc + i, ops[s], v);")
+            out.append("  }")
+            if self.hll_lds and p.nhll:
+                for ai, a in enumerate(p.aops):
+                    if a["kind"] != D.A_HLL:
+                        continue
+                    out.append(f"  {{ uint32_t* g = (uint32_t*)d->aops[{ai}].hll_regs;")
+                    out.append(f"    for (int i = threadIdx.x; i < {G * self.m}; i += {W * 64}) {{")
+                    out.append(f"      const uint32_t v = hll{ai}[i];")
+                    out.append("      if (v) atomicMax(g + i, v);")
+                    out.append("    } }")
+        out.append("}")
+        return "\n".join(out) + "\n"
+
+
+def compile_code(src: str, name: str) -> bytes:
+    """hipRTC-compile for gfx950 (no GPU needed), disk-cached by source hash."""
+    from . import native
+
+    key = hashlib.sha256((src + "\0".join(OPTS)).encode()).hexdigest()[:24]
+    path = cache_dir() / f"{key}.co"
+    if path.exists():
+        return path.read_bytes()
+    code = native.load().rtc_compile(src, name, OPTS)
+    tmp = path.with_suffix(f".tmp{os.getpid()}")
+    tmp.write_bytes(code)
+    os.replace(tmp, path)
+    return code
+
+
+def compile_source(src: str, name: str) -> int:
+    """Compile (cached) and load into the current HIP context; returns a launch handle."""
+    from . import native
+
+    key = hashlib.sha256((src + "\0".join(OPTS)).encode()).hexdigest()[:24]
+    with _lock:
+        if key in _handles:
+            return _handles[key]
+        code = compile_code(src, name)
+        h = native.load().module_load(code, name)
+        _handles[key] = h
+        return h
+
+
+class JitScan:
+    """A compiled, specialized scan kernel for one ScanProgram shape."""
+
+    def __init__(self, prog, mode: int, U: int, hll_lds: bool, m: int, narrow4: bool, load: bool = True):
+        self.lay = layout(prog, mode, U, hll_lds, m)
+        if self.lay.total > 160 * 1024:
+            raise ValueError(f"jit layout needs {self.lay.total} B of LDS")
+        g = _Gen(prog, mode, U, hll_lds, narrow4, self.lay, m)
+        tag = hashlib.sha1(repr((mode, U)).encode()).hexdigest()[:6]
+        self.name = f"sdo_jit_{tag}"
+        self.src = g.source(self.name)
+        self.handle = compile_source(self.src, self.name) if load else -1
+        if not load:
+            compile_code(self.src, self.name)
+        self.U = U
+
+    def launch(self, desc: torch.Tensor, grid: int) -> None:
+        from . import native
+
+        native.load().module_launch(self.handle, desc.data_ptr(), int(grid), W * 64, int(self.lay.total),
+                                    torch.cuda.current_stream(desc.device).cuda_stream)

@@ -27,6 +27,17 @@ def _bench_json_queries():
     return out
 
 
+@pytest.fixture(scope="module", params=["jit", "interp"], autouse=True)
+def kernel_path(request):
+    """Run every GPU test against both the per-query JIT kernels and the precompiled interpreter."""
+    from spark_druid_olap_amd.engine import device_exec as DE
+
+    old = DE.USE_JIT
+    DE.USE_JIT = request.param == "jit"
+    yield request.param
+    DE.USE_JIT = old
+
+
 @pytest.fixture(scope="module")
 def gpu_ds():
     from spark_druid_olap_amd.models import tpch

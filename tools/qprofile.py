@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--sf", type=float, default=10)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--unroll", type=str, default="2")
+    ap.add_argument("--both", action="store_true")
     args = ap.parse_args()
     from spark_druid_olap_amd.engine import device_exec as DE
     from spark_druid_olap_amd.engine.executor import Engine
@@ -31,8 +32,10 @@ def main():
     eng = Engine()
     for un in [int(x) for x in args.unroll.split(",")]:
         DE.UNROLL = un
-        print(f"rows={ds.num_rows} unroll={DE.UNROLL}")
-        run_all(eng, ds, args)
+        for use_jit in ([True, False] if args.both else [True]):
+            DE.USE_JIT = use_jit
+            print(f"rows={ds.num_rows} unroll={DE.UNROLL} jit={use_jit}")
+            run_all(eng, ds, args)
 
 
 def run_all(eng, ds, args):
@@ -53,7 +56,7 @@ def run_all(eng, ds, args):
             ev[0].record()
             prep._reset()
             ev[1].record()
-            native.scan(prep.desc, prep.grid, DE.BLOCK, prep.lds_total, DE.UNROLL)
+            prep._launch()
             ev[2].record()
             torch.cuda.synchronize()
             tr.append(ev[0].elapsed_time(ev[1]))
@@ -66,7 +69,8 @@ def run_all(eng, ds, args):
         rows = prog.rows_in_ranges
         byts = sum(column_tensor(ds, c).element_size() for c in prog.cols) * rows
         bw = byts / (min(tk) * 1e-3) / 1e9
-        print(f"{name[:40]:40s} mode={prep.mode} G={prog.G:<8d} grid={prep.grid:<5d} lds={prep.lds:<6d} "
+        ju = prep.jit.U if prep.jit else 0
+        print(f"{name[:40]:40s} mode={prep.mode} G={prog.G:<8d} grid={prep.grid:<5d} jitU={ju} "
               f"reset={min(tr):7.3f}ms kernel={min(tk):7.3f}ms query={tq:7.3f}ms rows={rows/1e6:7.1f}M "
               f"cols={len(prog.cols)} zones={len(prog.zones)} bm={len(prog.bm_leaves)} fin={int(prog.final_pre)} "
               f"colGB/s={bw:7.0f} " + " ".join(f"{k}={v:.2f}" for k, v in res.stats.items() if k.endswith("_ms")))
