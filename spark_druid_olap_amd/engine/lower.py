@@ -342,14 +342,18 @@ class Lowerer:
 
     # ------------------------------------------------------------------ filters -> IR
     def filter_ir(self, f) -> tuple:
+        """Filter spec -> normalized boolean IR (constant-folded id-set leaves)."""
+        return b_and([self._filter_ir(f)])
+
+    def _filter_ir(self, f) -> tuple:
         ds = self.ds
         if f is None or isinstance(f, S.NoopFilterSpec):
             return TRUE
         if isinstance(f, S.LogicalFilterSpec):
-            parts = [self.filter_ir(c) for c in f.fields]
+            parts = [self._filter_ir(c) for c in f.fields]
             return b_and(parts) if f.type == "and" else b_or(parts)
         if isinstance(f, S.NotFilterSpec):
-            return b_not(self.filter_ir(f.field))
+            return b_not(self._filter_ir(f.field))
         dim = getattr(f, "dimension", None)
         if dim == TIME or (dim is not None and dim not in ds.dims and dim not in ds.metrics and dim == "timestamp"):
             return self._time_filter(f)
@@ -417,6 +421,9 @@ class Lowerer:
 
             return ("ids", dim, d.eval_mask(pred))
         if isinstance(f, S.JavascriptFilterSpec):
+            pv = getattr(f, "_pyvec", None)
+            if pv is not None:  # vectorised dictionary-domain predicate (SQL planner)
+                return ("ids", dim, np.asarray(pv(d.all_values()), dtype=bool))
             py = getattr(f, "_pyfn", None)
             if py is None:
                 jf = compile_function(f.function)
@@ -425,9 +432,9 @@ class Lowerer:
         raise LoweringError(f"unsupported filter {type(f).__name__}")
 
     def _time_values(self) -> np.ndarray:
-        if self._time_values is None:
-            self._time_values = np.unique(self.ds.time_host)
-        return self._time_values
+        if self._tv_cache is None:
+            self._tv_cache = np.unique(self.ds.time_host)
+        return self._tv_cache
 
     def _time_filter(self, f) -> tuple:
         ds = self.ds
@@ -695,8 +702,11 @@ class Lowerer:
             return KeyComp(name, D.K_ID, dim, len(d), decoder=lambda ids, _d=d: DictColumn(ids, _d))
         if isinstance(fn, S.TimeFormatExtractionFunctionSpec) and d.vtype != "string":
             pass
-        f = extraction_callable(fn)
-        derived = d.map_values(f)
+        pv = getattr(fn, "_pyvec", None)
+        if pv is not None:  # vectorised dictionary-domain extraction (SQL planner)
+            derived = np.asarray(pv(d.all_values()), dtype=object)
+        else:
+            derived = d.map_values(extraction_callable(fn))
         uniq = sorted({v for v in derived.tolist() if v is not None}, key=lambda v: (str(type(v)), v))
         has_null = any(v is None for v in derived.tolist())
         dd = Dictionary(uniq, "string" if all(isinstance(v, str) for v in uniq) else "double", has_null)

@@ -398,15 +398,21 @@ def to_pandas(flat: FlatTPCH):
 
 # --------------------------------------------------------------------------- DDL and queries
 def druid_ddl(table: str = "orderLineItemPartSupplier", source: str = "orderLineItemPartSupplierBase",
-              datasource: str = "tpch", extra_options: str = "") -> str:
+              datasource: str = "tpch", extra_options: str = "", with_column_mapping: bool = True,
+              star_schema: Optional[str] = None) -> str:
+    """The reference's Druid DDL (``tc/BaseTest.scala:167-182``).  The benchmark index
+    (``docs/benchmark/druid/tpch_index.json``) keeps SQL column names, so the bench passes
+    ``with_column_mapping=False``."""
     import json
 
+    cm = f"columnMapping '{json.dumps(COLUMN_MAPPING)}', " if with_column_mapping else ""
+    ss = star_schema or f'{{"factTable" : "{table}", "relations" : []}}'
     return (f"CREATE TABLE if not exists {table} USING org.sparklinedata.druid OPTIONS ("
             f"sourceDataframe \"{source}\", timeDimensionColumn \"l_shipdate\", druidDatasource \"{datasource}\", "
             f"druidHost 'localhost', zkQualifyDiscoveryNames \"true\", "
-            f"columnMapping '{json.dumps(COLUMN_MAPPING)}', numProcessingThreadsPerHistorical '1', "
+            f"{cm}numProcessingThreadsPerHistorical '1', "
             f"allowTopNRewrite \"true\", functionalDependencies '{json.dumps(FUNCTIONAL_DEPENDENCIES)}', "
-            f"starSchema '{{\"factTable\" : \"{table}\", \"relations\" : []}}'{extra_options})")
+            f"starSchema '{ss}'{extra_options})")
 
 
 T = "orderLineItemPartSupplier"

@@ -1,0 +1,455 @@
+"""Session: SQL entry point over the GPU engine (the reference's ``SPLSessionState`` + Spark
+``SQLContext.sql`` + ``DruidStrategy``; ``asql/hive/sparklinedata/SPLSessionState.scala:77-190``).
+
+    sess = Session()
+    sess.register_datasource(ds)                    # a device-resident Druid index shard
+    sess.register_table("orderLineItemPartSupplierBase", df_or_schema)
+    sess.sql("CREATE TABLE t USING org.sparklinedata.druid OPTIONS (sourceDataframe ..., ...)")
+    sess.sql("select l_returnflag, count(*) from t group by l_returnflag").collect()
+
+Every rank of a multi-GPU job runs the same statements; ``DruidQuery`` leaves execute on the
+rank's shard and merge over RCCL inside the engine, so results are global on every rank.
+"""
+from __future__ import annotations
+
+import json
+import threading
+import time
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import pandas as pd
+
+from .catalog.catalog import (CSV_PROVIDERS, DRUID_PROVIDERS, BaseTable, Catalog, DruidTable, ViewTable,
+                              csv_loader)
+from .catalog.history import DruidQueryHistory
+from .catalog.options import Conf
+from .catalog import views as V
+from .query import spec as S
+from .sql import ast as A
+from .sql import plan as P
+from .sql.analyzer import Analyzer
+from .sql.druid_rewrite import DruidRewriter
+from .sql.execute import Batch, Executor
+from .sql.optimizer import optimize
+from .sql.parser import ParseError, parse
+from .sql.types import AnalysisError, series_to_list, to_series
+
+_PANDAS_TO_SQL = {"i": "bigint", "u": "bigint", "f": "double", "b": "boolean", "M": "timestamp"}
+
+
+def _infer_schema(df: pd.DataFrame) -> List[Tuple[str, str]]:
+    out = []
+    for c in df.columns:
+        dt = df[c].dtype
+        s = str(dt)
+        if s == "Int64":
+            out.append((c, "bigint"))
+        elif s == "Float64":
+            out.append((c, "double"))
+        elif s == "boolean":
+            out.append((c, "boolean"))
+        else:
+            out.append((c, _PANDAS_TO_SQL.get(dt.kind, "string")))
+    return out
+
+
+class DataFrame:
+    """Result of ``Session.sql``: an optimized plan (lazy) or a command's rows."""
+
+    def __init__(self, session: "Session", plan: Optional[P.Plan], names: List[str], sql: str = "",
+                 batch: Optional[Batch] = None, analyzed: Optional[P.Plan] = None, rewrite_log=None):
+        self.session = session
+        self.plan = plan
+        self.names = names
+        self.sql_text = sql
+        self._batch = batch
+        self.analyzed = analyzed
+        self.rewrite_log = rewrite_log or []
+        self.last_stats: Dict[str, Any] = {}
+
+    # -- execution ---------------------------------------------------------------------------
+    def _run(self) -> Batch:
+        if self._batch is not None:
+            return self._batch
+        ex = Executor(self.session)
+        t0 = time.perf_counter()
+        b = self.session._with_sql(self.sql_text, lambda: ex.run(self.plan))
+        self.last_stats = {"ms": (time.perf_counter() - t0) * 1e3, "druid": ex.druid_stats}
+        return b
+
+    def prepared(self) -> "DataFrame":
+        return self
+
+    def run(self) -> Batch:
+        return self._run()
+
+    def collect(self) -> List[tuple]:
+        b = self._run()
+        cols = [series_to_list(b.cols[r.rid], r.dtype) for r in b.refs]
+        return list(zip(*cols)) if cols else [() for _ in range(b.n)]
+
+    def to_pandas(self) -> pd.DataFrame:
+        return self._run().to_pandas(self.names)
+
+    toPandas = to_pandas
+
+    def count(self) -> int:
+        return self._run().n
+
+    @property
+    def columns(self) -> List[str]:
+        return list(self.names)
+
+    @property
+    def schema(self) -> List[Tuple[str, str]]:
+        refs = self.plan.output if self.plan is not None else self._batch.refs
+        return [(n, r.dtype) for n, r in zip(self.names, refs)]
+
+    # -- introspection (plan-shape tests, DruidPlanner.getDruidQuerySpecs) ----------------------
+    def druid_queries(self) -> List[P.DruidQuery]:
+        return P.find_all(self.plan, P.DruidQuery) if self.plan is not None else []
+
+    def druid_query_specs(self) -> List[S.QuerySpec]:
+        return [d.spec for d in self.druid_queries()]
+
+    def explain(self, extended: bool = False) -> str:
+        if self.plan is None:
+            return "<command>"
+        s = ""
+        if extended and self.analyzed is not None:
+            s += "== Analyzed Logical Plan ==\n" + self.analyzed.tree_string() + "\n"
+        s += "== Physical Plan ==\n" + self.plan.tree_string()
+        return s
+
+    def show(self, n: int = 20) -> None:
+        print(self.to_pandas().head(n).to_string())
+
+    def __repr__(self):
+        return f"DataFrame[{', '.join(f'{n}: {t}' for n, t in self.schema)}]"
+
+
+class Session:
+    def __init__(self, engine=None, conf: Optional[Dict[str, Any]] = None, world=None):
+        if engine is None:
+            from .engine.executor import Engine
+
+            engine = Engine(world)
+        self.engine = engine
+        self.conf = Conf(conf)
+        self.catalog = Catalog()
+        self.history = DruidQueryHistory(int(self.conf.typed("sparkline.queryhistory.maxsize")))
+        self._plan_cache: Dict[Tuple[str, int, int, str], DataFrame] = {}
+        self._lock = threading.RLock()
+        self._tl = threading.local()
+
+    # ------------------------------------------------------------------------------ registration
+    def register_datasource(self, ds, name: Optional[str] = None) -> None:
+        """Make a device-resident datasource shard queryable (the 'Druid cluster' contents)."""
+        self._global_interval(ds)
+        self.catalog.cluster.register(ds, name)
+        self._plan_cache.clear()
+
+    def _global_interval(self, ds) -> None:
+        from .sql.druid_rewrite import data_interval
+
+        if getattr(ds, "global_interval_ms", None) is not None:
+            return
+        lo, hi = data_interval(ds)
+        w = self.engine.world
+        if w.size > 1:
+            lo = -w.max_float(-float(lo))
+            hi = w.max_float(float(hi))
+        ds.global_interval_ms = (int(lo), int(hi))
+
+    def register_table(self, name: str, df: Optional[pd.DataFrame] = None,
+                       schema: Optional[Sequence[Tuple[str, str]]] = None, loader=None,
+                       temporary: bool = False) -> BaseTable:
+        db, tname = self.catalog._split(name)
+        db = db or self.catalog.current_db
+        if schema is None:
+            if df is None:
+                raise AnalysisError("register_table needs data or a schema")
+            schema = _infer_schema(df)
+        schema = [(c, _norm_type(t)) for c, t in schema]
+        t = BaseTable(db, tname, list(schema), data=None, loader=(lambda d=df: d) if df is not None else loader)
+        self.catalog.register(t, temporary=temporary)
+        self._plan_cache.clear()
+        return t
+
+    def table(self, name: str) -> DataFrame:
+        return self.sql(f"select * from {name}")
+
+    # ------------------------------------------------------------------------------ SQL
+    def sql(self, text: str) -> DataFrame:
+        try:
+            st = parse(text)
+        except ParseError as pe:
+            raise ParseError(f"{pe}\n\n== SQL ==\n{text}") from None
+        if isinstance(st, (A.Select, A.SetOp, A.With)):
+            return self._query(text, st)
+        return self._command(text, st)
+
+    def _query(self, text: str, st) -> DataFrame:
+        cache_on = bool(self.conf.typed("spark.sparklinedata.druid.planCache.enabled"))
+        key = (text, self.catalog.version, self.catalog.cluster.generation, json.dumps(self.conf.items(), sort_keys=True))
+        if cache_on:
+            hit = self._plan_cache.get(key)
+            if hit is not None:
+                return hit
+        df = self.plan(text, st)
+        if cache_on:
+            with self._lock:
+                if len(self._plan_cache) > 256:
+                    self._plan_cache.clear()
+                self._plan_cache[key] = df
+        return df
+
+    def plan(self, text: str, st=None) -> DataFrame:
+        st = st if st is not None else parse(text)
+        an = Analyzer(self.catalog, self)
+        analyzed = an.analyze(st)
+        names = [r.name for r in analyzed.output]
+        opt = optimize(analyzed, self.conf)
+        rw = DruidRewriter(self)
+        phys = rw.rewrite(opt)
+        if self.conf.typed("spark.sparklinedata.druid.debug.transformations"):
+            import logging
+
+            logging.getLogger("sdo.planner").info("rewrite log:\n%s\nplan:\n%s", "\n".join(rw.log),
+                                                  phys.tree_string())
+        return DataFrame(self, phys, names, text, analyzed=analyzed, rewrite_log=rw.log)
+
+    def _with_sql(self, sql: str, fn):
+        prev = getattr(self._tl, "sql", None)
+        self._tl.sql = sql
+        try:
+            return fn()
+        finally:
+            self._tl.sql = prev
+
+    # ------------------------------------------------------------------------------ druid exec
+    def run_druid(self, dq: P.DruidQuery):
+        ds = dq.relation.info.datasource
+        spec = dq.spec
+        t0 = time.perf_counter()
+        run_spec = spec
+        if isinstance(spec, S.SelectSpec):
+            # one page holding every row (the reference's paging loop, DruidSelectResultIterator.scala:116-137,
+            # collapsed: the scan compacts on device and ships all selected rows at once)
+            run_spec = spec.copy(pagingSpec=S.PagingSpec({}, 2 ** 31 - 1))
+        prep = getattr(dq, "_prepared", None)
+        if prep is None or getattr(dq, "_prepared_spec", None) is not spec:
+            prep = self.engine.prepare(run_spec, ds)
+            dq._prepared = prep
+            dq._prepared_spec = spec
+        res = prep.run()
+        if isinstance(spec, S.TimeSeriesQuerySpec) and res.num_rows == 0:
+            res = _empty_global_agg(res, spec)
+        ms = (time.perf_counter() - t0) * 1e3
+        if self.conf.typed("spark.sparklinedata.enable.druid.query.history"):
+            self.history.record(spec, res.stats.get("exec_ms", ms), ms, res.num_rows,
+                                f"gpu:0-{self.engine.world.size - 1}", getattr(self._tl, "sql", None),
+                                len(ds.segments))
+        return res
+
+    # ------------------------------------------------------------------------------ commands
+    def _rows_df(self, cols: List[Tuple[str, str]], rows: List[tuple]) -> DataFrame:
+        refs = [A.Ref(A.new_id(), c, t) for c, t in cols]
+        data = {}
+        for i, r in enumerate(refs):
+            data[r.rid] = to_series(pd.Series([row[i] for row in rows], dtype=object), r.dtype)
+        return DataFrame(self, None, [c for c, _ in cols], batch=Batch(refs, data, len(rows)))
+
+    def _command(self, text: str, st) -> DataFrame:
+        cat = self.catalog
+        if isinstance(st, A.CreateTable):
+            return self._create_table(st)
+        if isinstance(st, A.CreateView):
+            db, name = cat._split(st.name)
+            v = ViewTable(db or cat.current_db, name, st.query, st.text)
+            if not st.replace and cat.lookup(st.name) is not None and not st.temporary:
+                raise AnalysisError(f"View {name} already exists")
+            cat.register(v, temporary=st.temporary)
+            self._plan_cache.clear()
+            return self._rows_df([], [])
+        if isinstance(st, A.DropTable):
+            cat.drop(st.name, st.if_exists)
+            self._plan_cache.clear()
+            return self._rows_df([], [])
+        if isinstance(st, A.CreateDatabase):
+            cat.create_database(st.name, st.if_not_exists)
+            return self._rows_df([], [])
+        if isinstance(st, A.UseDatabase):
+            cat.use(st.name)
+            self._plan_cache.clear()
+            return self._rows_df([], [])
+        if isinstance(st, A.SetConf):
+            if st.key is None:
+                items = sorted(self.conf.items().items())
+                return self._rows_df([("key", "string"), ("value", "string")], items)
+            if st.value is None:
+                return self._rows_df([("key", "string"), ("value", "string")],
+                                     [(st.key, self.conf.get(st.key, "<undefined>"))])
+            self.conf.set(st.key, st.value)
+            self._plan_cache.clear()
+            return self._rows_df([("key", "string"), ("value", "string")], [(st.key, st.value)])
+        if isinstance(st, A.ShowTables):
+            rows = [(t.db, t.name.lower(), t in cat.temp.values()) for t in cat.tables(st.db)]
+            return self._rows_df([("database", "string"), ("tableName", "string"), ("isTemporary", "boolean")], rows)
+        if isinstance(st, A.Describe):
+            t = self.lookup_table(st.name)
+            return self._rows_df([("col_name", "string"), ("data_type", "string"), ("comment", "string")],
+                                 [(c, ty, None) for c, ty in t.schema])
+        if isinstance(st, A.CacheTable):
+            t = cat.get(st.name)
+            if isinstance(t, BaseTable):
+                t.cached = not st.uncache
+                if t.cached:
+                    t.frame()
+            return self._rows_df([], [])
+        if isinstance(st, A.ClearDruidCache):
+            cat.cluster.clear_cache(st.host)
+            self._plan_cache.clear()
+            return self._rows_df([], [])
+        if isinstance(st, A.ExecuteDruidQuery):
+            return self._execute_query(st)
+        if isinstance(st, A.ExplainDruidRewrite):
+            return self._explain_rewrite(st)
+        if isinstance(st, A.Explain):
+            df = self.plan("", st.query)
+            return self._rows_df([("plan", "string")], [(df.explain(st.extended),)])
+        raise AnalysisError(f"unsupported statement {type(st).__name__}")
+
+    def lookup_table(self, name):
+        if isinstance(name, tuple) and len(name) == 1 and name[0].lower() in V.VIEWS:
+            return self.metadata_view(name[0])
+        return self.catalog.get(name)
+
+    def metadata_view(self, name: str) -> BaseTable:
+        df = V.VIEWS[name.lower()](self)
+        return BaseTable("default", name.lower(), V.schema_of(df), data=df)
+
+    def _create_table(self, st: A.CreateTable) -> DataFrame:
+        cat = self.catalog
+        if cat.lookup(st.name) is not None:
+            if st.if_not_exists:
+                return self._rows_df([], [])
+            raise AnalysisError(f"Table {'.'.join(st.name)} already exists")
+        prov = (st.provider or "").lower()
+        db, name = cat._split(st.name)
+        db = db or cat.current_db
+        if prov in DRUID_PROVIDERS:
+            t = cat.create_druid_relation(st.name, st.options)
+            cat.register(t, temporary=st.temporary)
+        elif st.as_query is not None:
+            df = self.sql_ast(st.as_query)
+            data = df.to_pandas()
+            schema = list(df.schema)
+            cat.register(BaseTable(db, name, schema, data=None, loader=lambda d=data: d), temporary=st.temporary)
+        elif prov in CSV_PROVIDERS:
+            path = st.options.get("path")
+            if path is None:
+                raise AnalysisError("csv tables need a path option")
+            schema = [(c.name, c.dtype) for c in st.columns]
+            cat.register(BaseTable(db, name, schema, loader=csv_loader(path, schema, st.options), provider=prov,
+                                   options=st.options), temporary=st.temporary)
+        elif prov in ("parquet", "json", "orc"):
+            path = st.options.get("path")
+            schema = [(c.name, c.dtype) for c in st.columns] or None
+
+            def load(path=path, prov=prov):
+                if prov == "parquet":
+                    return pd.read_parquet(path)
+                if prov == "json":
+                    return pd.read_json(path, lines=True)
+                raise AnalysisError("orc is not supported")
+            if schema is None:
+                probe = load()
+                schema = _infer_schema(probe)
+            cat.register(BaseTable(db, name, schema, loader=load, provider=prov, options=st.options),
+                         temporary=st.temporary)
+        elif not prov:
+            schema = [(c.name, c.dtype) for c in st.columns]
+            empty = pd.DataFrame({c: to_series([], t) for c, t in schema})
+            cat.register(BaseTable(db, name, schema, data=None, loader=lambda d=empty: d), temporary=st.temporary)
+        else:
+            raise AnalysisError(f"Failed to find data source: {st.provider}")
+        self._plan_cache.clear()
+        return self._rows_df([], [])
+
+    def sql_ast(self, st) -> DataFrame:
+        return self.plan("", st)
+
+    def _execute_query(self, st: A.ExecuteDruidQuery) -> DataFrame:
+        """``ON DRUIDDATASOURCE t EXECUTE QUERY <json>`` (PlanUtil.logicalPlan, asql/util/PlanUtil.scala:48-61)."""
+        from .query.spec import query_from_json
+
+        t = self.catalog.get(st.table)
+        if not isinstance(t, DruidTable):
+            raise AnalysisError(f"{'.'.join(st.table)} is not a Druid relation")
+        spec = query_from_json(json.loads(st.json_text))
+        res = self.engine.execute(spec, t.info.datasource)
+        if self.conf.typed("spark.sparklinedata.enable.druid.query.history"):
+            self.history.record(spec, res.stats.get("exec_ms", 0.0), res.stats.get("exec_ms", 0.0), res.num_rows,
+                                f"gpu:0-{self.engine.world.size - 1}", None)
+        from .engine.columns import materialize
+
+        cols = []
+        rows_cols = []
+        for c in res.columns:
+            arr = materialize(res.data[c])
+            k = np.asarray(arr).dtype.kind
+            t_ = "bigint" if k in "iu" else "double" if k == "f" else "string"
+            cols.append((c, t_))
+            rows_cols.append([x.item() if isinstance(x, np.generic) else x for x in np.asarray(arr).tolist()])
+        rows = list(zip(*rows_cols)) if rows_cols else []
+        return self._rows_df(cols, rows)
+
+    def _explain_rewrite(self, st: A.ExplainDruidRewrite) -> DataFrame:
+        """``EXPLAIN DRUID REWRITE`` (ExplainDruidRewrite.run, DruidMetadataCommands.scala:58-77)."""
+        from .planner.cost import explain_cost
+
+        df = self.plan("", st.query)
+        lines = df.plan.tree_string().rstrip("\n").split("\n")
+        for i, dq in enumerate(df.druid_queries()):
+            lines.append(f"DruidQuery({i}) details ::")
+            lines.append(json.dumps(dq.spec.to_json(), indent=2))
+            lines.extend(explain_cost(self, dq).split("\n"))
+        return self._rows_df([("plan", "string")], [(l,) for l in lines])
+
+
+def _norm_type(t: str) -> str:
+    from .sql.parser import TYPE_NAMES
+
+    t = t.strip()
+    u = t.upper()
+    if "(" in u:
+        head = u[: u.index("(")]
+        if TYPE_NAMES.get(head) == "decimal":
+            return "decimal" + t[t.index("("):].replace(" ", "")
+        return TYPE_NAMES.get(head, t.lower())
+    return TYPE_NAMES.get(u, t.lower())
+
+
+def _empty_global_agg(res, spec):
+    """SQL global aggregates return one row even over no input (count = 0, others NULL)."""
+    from .engine.executor import QueryResult
+
+    data = {}
+    cols = list(res.columns) if res.columns else ["timestamp"] + [a.name for a in spec.aggregations]
+    for c in cols:
+        data[c] = np.array([0 if c in _count_names(spec) else np.nan], dtype=object)
+    return QueryResult(cols, data, res.query_type, res.stats)
+
+
+def _count_names(spec) -> set:
+    out = set()
+    for a in spec.aggregations or []:
+        if isinstance(a, S.FunctionAggregationSpec) and a.type == "count":
+            out.add(a.name)
+        if isinstance(a, S.FilteredAggregationSpec):
+            out.add(a.name)
+        if isinstance(a, S.CardinalityAggregationSpec):
+            out.add(a.name)
+    return out

@@ -1,0 +1,1046 @@
+"""Druid rewrite: replace plan fragments over Druid-backed relations with GPU QuerySpecs.
+
+Parity map (reference -> here):
+  * ``ProjectFilterTransfom`` (``asd/ProjectFilterTransfom.scala:32-417``): Project/Filter chains over
+    a Druid relation -> ``_collect``; time predicates -> query intervals
+    (``sd/QueryIntervals.scala:96-130``, ``sd/DateTimeExtractor.scala:374-436``); dimension predicates
+    -> selector / bound / IN(extraction-lookup) / isNull / not / and / or / spatial filters
+    (``dimFilterExpression`` 321-416); anything else over one dimension -> a JavaScript filter, which
+    here carries a vectorised dictionary-domain evaluator (``_pyvec``) instead of running JS per row.
+  * ``JoinTransform`` (``asd/JoinTransform.scala:238-385``): inner equi-join trees that follow the
+    declared star schema collapse onto the single denormalized index.
+  * ``AggregateTransform`` (``asd/AggregateTransform.scala:48-543``): grouping expressions ->
+    default / time-format / time-parsing / JavaScript(dictionary-domain) dimension specs; aggregates
+    -> count / long|double Sum|Min|Max / cardinality / hyperUnique / JavaScript (metric expression
+    VM); ``avg`` -> sum + count with the division on the host; grouping sets -> one query per set.
+  * ``LimitTransfom`` (``asd/DruidTransforms.scala:26-98``): Sort / Limit over a pushed aggregate ->
+    ``LimitSpec``.
+  * ``DruidStrategy.selectPlan`` (``asd/DruidStrategy.scala:86-282``): non-aggregate scans -> Select
+    with paging when ``nonAggregateQueryHandling`` allows it.
+  * ``QuerySpecTransforms`` (search / timeseries / topN / between / spatial) run on the result.
+"""
+from __future__ import annotations
+
+import re
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Set, Tuple
+
+import numpy as np
+import pandas as pd
+
+from ..query import spec as S
+from ..query import transforms as QT
+from ..query.intervals import fmt_iso
+from . import ast as A
+from . import plan as P
+from .functions import Frame, Period, evaluate, typeof
+from .jscodegen import JSGenError, js_aggregator, js_single_column_fn, vm_compatible
+from .types import AnalysisError, base, is_vec, to_series
+
+DAY_MS = 86_400_000
+MIN_MS = -(2 ** 62)
+MAX_MS = 2 ** 62
+
+
+class NotPushable(Exception):
+    pass
+
+
+# ------------------------------------------------------------------------------------------------
+@dataclass
+class PF:
+    """A Project/Filter(/star-join) fragment over one Druid relation, in terms of base columns."""
+    table: object                                 # DruidTable (None while only dimension tables seen)
+    cols: Dict[int, object] = field(default_factory=dict)   # base ref id -> DruidRelationColumn | None
+    refs: Dict[int, A.Ref] = field(default_factory=dict)    # base ref id -> Ref
+    tables: Dict[int, str] = field(default_factory=dict)     # base ref id -> star table short name
+    subst: Dict[int, A.Expr] = field(default_factory=dict)   # projected alias id -> expr over base refs
+    conds: List[A.Expr] = field(default_factory=list)
+    noop_conds: List[A.Expr] = field(default_factory=list)
+    dim_scans: List[Tuple[str, List[A.Ref]]] = field(default_factory=list)
+    pairs: List[Tuple[Tuple[str, str], List[Tuple[str, str]]]] = field(default_factory=list)
+
+    def sub(self, e: A.Expr) -> A.Expr:
+        if not self.subst:
+            return e
+
+        def f(x):
+            if isinstance(x, A.Ref) and x.rid in self.subst:
+                return self.subst[x.rid]
+            return None
+        return e.transform(f)
+
+
+def _short(n: str) -> str:
+    return n.split(".")[-1].lower()
+
+
+class DruidRewriter:
+    def __init__(self, session):
+        self.session = session
+        self.conf = session.conf
+        self.approx_distinct = bool(self.conf.typed("spark.sparklinedata.druid.approxCountDistinct"))
+        self.log: List[str] = []
+
+    # ============================================================================== driver
+    def rewrite(self, plan: P.Plan) -> P.Plan:
+        p = self._top_down(plan)
+        return p.transform_up(self._finalize)
+
+    def _try(self, fn, p):
+        try:
+            return fn(p)
+        except NotPushable as ex:
+            self.log.append(f"{type(p).__name__}: not pushed ({ex})")
+            return None
+
+    def _top_down(self, p: P.Plan) -> P.Plan:
+        # structural rules first: they need the original Project/Filter/Join chains below them
+        if isinstance(p, P.Aggregate):
+            r = self._try(self._aggregate, p)
+            if r is not None:
+                return r
+        elif isinstance(p, (P.Project, P.Filter)):
+            r = self._try(self._select, p)
+            if r is not None:
+                return r
+        ch = [self._top_down(c) for c in p.children]
+        if any(a is not b for a, b in zip(ch, p.children)):
+            p = p.with_children(ch)
+        if isinstance(p, P.Sort):
+            r = self._try(self._sort, p)
+            if r is not None:
+                p = r
+        elif isinstance(p, P.Limit):
+            self._try(self._limit, p)
+        return p
+
+    # ============================================================================== fragments
+    def _collect(self, p: P.Plan) -> PF:
+        if isinstance(p, P.TableScan):
+            t = p.table
+            if t.kind == "druid":
+                info = t.info
+                pf = PF(t)
+                fact = info.star.fact.name
+                for r in p.refs:
+                    pf.cols[r.rid] = info.column(r.name)
+                    pf.refs[r.rid] = r
+                    pf.tables[r.rid] = fact
+                return pf
+            pf = PF(None)
+            pf.dim_scans.append((_short(t.name), p.refs))
+            for r in p.refs:
+                pf.refs[r.rid] = r
+                pf.tables[r.rid] = _short(t.name)
+            return pf
+        if isinstance(p, P.Filter):
+            pf = self._collect(p.child)
+            pf.conds.extend(A.conjuncts(pf.sub(p.cond)))
+            return pf
+        if isinstance(p, P.Project):
+            pf = self._collect(p.child)
+            new = {}
+            for e in p.exprs:
+                if isinstance(e, A.Alias):
+                    new[e.rid] = pf.sub(e.child)
+            pf.subst.update(new)
+            return pf
+        if isinstance(p, P.Join) and p.kind in ("inner", "cross"):
+            return self._join(p)
+        raise NotPushable(f"{type(p).__name__} is not a project/filter/star-join over a Druid relation")
+
+    def _join(self, p: P.Join) -> PF:
+        l = self._collect(p.left)
+        r = self._collect(p.right)
+        if l.table is not None and r.table is not None:
+            raise NotPushable("join of two Druid relations")
+        if l.table is None and r.table is None:
+            pf = PF(None)
+        else:
+            pf = PF(l.table or r.table)
+        for x in (l, r):
+            pf.cols.update(x.cols)
+            pf.refs.update(x.refs)
+            pf.tables.update(x.tables)
+            pf.subst.update(x.subst)
+            pf.conds += x.conds
+            pf.noop_conds += x.noop_conds
+            pf.dim_scans += x.dim_scans
+        cond = pf.sub(p.cond) if p.cond is not None else None
+        pairs: Dict[Tuple[str, str], List[Tuple[str, str]]] = {}
+        lt = set(l.tables.values())
+        rt = set(r.tables.values())
+        for c in A.conjuncts(cond):
+            if isinstance(c, A.BinOp) and c.op == "=" and isinstance(c.l, A.Ref) and isinstance(c.r, A.Ref):
+                a, b = c.l, c.r
+                ta, tb = pf.tables.get(a.rid), pf.tables.get(b.rid)
+                if ta is not None and tb is not None and ta != tb and \
+                        ((ta in lt and tb in rt) or (ta in rt and tb in lt)):
+                    if ta in rt:
+                        a, b, ta, tb = b, a, tb, ta
+                    pairs.setdefault((ta, tb), []).append((a.name, b.name))
+                    continue
+            pf.conds.append(c)
+        if not pairs:
+            raise NotPushable("join without equi-join keys (cross product)")
+        pf.pairs = l.pairs + r.pairs + list(pairs.items())
+        return pf
+
+    def _finish_pf(self, pf: PF) -> PF:
+        """Bind dimension-table columns to the Druid relation and validate the star joins."""
+        if pf.table is None:
+            raise NotPushable("no Druid relation in fragment")
+        info = pf.table.info
+        star = info.star
+        for tname, refs in pf.dim_scans:
+            if tname not in star.table_map:
+                raise NotPushable(f"table {tname} is not in the star schema of {pf.table.name}")
+            for r in refs:
+                pf.cols[r.rid] = info.column(r.name)
+        for (ta, tb), keys in pf.pairs:
+            lcols = [k[0] for k in keys]
+            rcols = [k[1] for k in keys]
+            if star.is_star_join(lcols, rcols) is None:
+                raise NotPushable(f"join {ta}-{tb} on {keys} is not a star-schema join")
+        if pf.dim_scans:
+            joined = {t for (ta, tb), _ in pf.pairs for t in (ta, tb)}
+            for tname, _ in pf.dim_scans:
+                if tname not in joined:
+                    raise NotPushable(f"table {tname} is not joined")
+        # IsNotNull on a star-join column that is not in the index: always true for the index
+        # (ProjectFilterTransfom.scala:383-388)
+        keep = []
+        for c in pf.conds:
+            if isinstance(c, A.IsNull) and c.negated and isinstance(c.child, A.Ref):
+                col = pf.cols.get(c.child.rid)
+                if col is None and star.is_joining_column(None, c.child.name):
+                    pf.noop_conds.append(c)
+                    continue
+            keep.append(c)
+        pf.conds = keep
+        return pf
+
+    def _column(self, pf: PF, r: A.Ref):
+        c = pf.cols.get(r.rid)
+        if c is None:
+            raise NotPushable(f"column {r.name} is not mapped to the Druid index")
+        return c
+
+    # ============================================================================== filters
+    def _filters(self, pf: PF) -> Tuple[List[str], Optional[object]]:
+        ds = pf.table.info.datasource
+        lo, hi = data_interval(ds)
+        specs = []
+        for c in pf.conds:
+            iv = self._time_interval(pf, c)
+            if iv is not None:
+                lo, hi = max(lo, iv[0]), min(hi, iv[1])
+                continue
+            f = self._filter(pf, c)
+            if f is not None:
+                specs.append(f)
+        if hi <= lo:
+            hi = lo  # empty interval -> empty result (NULL scan)
+        intervals = [f"{fmt_iso(lo)}/{fmt_iso(hi)}"]
+        filt = None
+        if len(specs) == 1:
+            filt = specs[0]
+        elif specs:
+            filt = S.LogicalFilterSpec("and", specs)
+        return intervals, filt
+
+    # -- time ---------------------------------------------------------------------------------
+    def _time_ref(self, pf: PF, e: A.Expr) -> Optional[Tuple[object, bool]]:
+        """(column, truncates_to_day) if e is a reference to the time column (optionally wrapped in
+        dateTime / to_date / cast)."""
+        trunc = False
+        while True:
+            if isinstance(e, A.Call) and e.name in ("datetime", "datetimewithtz") and len(e.args) == 1:
+                e = e.args[0]
+            elif isinstance(e, A.Call) and e.name == "to_date" and len(e.args) == 1:
+                e, trunc = e.args[0], True
+            elif isinstance(e, A.Cast) and e.to in ("date", "timestamp"):
+                trunc = trunc or e.to == "date"
+                e = e.child
+            else:
+                break
+        if isinstance(e, A.Ref):
+            c = pf.cols.get(e.rid)
+            if c is not None and c.is_time:
+                return c, trunc or base(c.sql_type) in ("date", "string")
+        return None
+
+    def _time_interval(self, pf: PF, c: A.Expr) -> Optional[Tuple[int, int]]:
+        cmp = _as_comparison(c)
+        if cmp is None:
+            return None
+        op, l, r = cmp
+        tr = self._time_ref(pf, l)
+        if tr is None:
+            tr = self._time_ref(pf, r)
+            if tr is None:
+                return None
+            op = _FLIP[op]
+            l, r = r, l
+        if not isinstance(r, A.Lit):
+            return None
+        ms = _lit_ms(r)
+        if ms is None:
+            return None
+        _, day = tr
+        unit = DAY_MS if day else 1
+        if day and ms % DAY_MS != 0:
+            # a day-valued column compared with a timestamp inside a day
+            if op in ("<", "<="):
+                return (MIN_MS, (ms // DAY_MS + 1) * DAY_MS)
+            if op in (">", ">="):
+                return ((ms // DAY_MS + 1) * DAY_MS, MAX_MS)
+            return (0, 0)
+        if op == "<":
+            return (MIN_MS, ms)
+        if op == "<=":
+            return (MIN_MS, ms + unit)
+        if op == ">":
+            return (ms + unit, MAX_MS)
+        if op == ">=":
+            return (ms, MAX_MS)
+        if op == "=":
+            return (ms, ms + unit)
+        return None
+
+    # -- dimension / metric predicates ----------------------------------------------------------
+    def _filter(self, pf: PF, e: A.Expr):
+        f = self._native_filter(pf, e)
+        if f is not None:
+            return f
+        return self._expr_filter(pf, e)
+
+    def _native_filter(self, pf: PF, e: A.Expr):
+        if isinstance(e, A.Lit):
+            if e.value is True:
+                return None
+            return S.SelectorFilterSpec("__time", "")  # NULL scan (ProjectFilterTransfom.scala:402-404)
+        if isinstance(e, A.BinOp) and e.op in ("and", "or"):
+            a = self._filter(pf, e.l)
+            b = self._filter(pf, e.r)
+            fields = [x for x in (a, b) if x is not None]
+            if not fields:
+                return None
+            if len(fields) == 1:
+                return fields[0] if e.op == "and" else None
+            return S.LogicalFilterSpec(e.op, fields)
+        if isinstance(e, A.UnOp) and e.op == "not":
+            inner = self._filter(pf, e.child)
+            if inner is None:
+                raise NotPushable("NOT over a trivially-true predicate")
+            return S.NotFilterSpec(inner)
+        if isinstance(e, A.IsNull) and isinstance(e.child, A.Ref):
+            c = pf.cols.get(e.child.rid)
+            if c is not None and c.kind == "dimension":
+                sel = S.SelectorFilterSpec(c.druid_column, "")
+                return S.NotFilterSpec(sel) if e.negated else sel
+            if c is not None and (c.is_metric or c.is_time):
+                if e.negated:
+                    return None
+                return S.SelectorFilterSpec("__time", "")
+        if isinstance(e, A.InList) and isinstance(e.child, A.Ref) and all(isinstance(i, A.Lit) for i in e.items):
+            c = pf.cols.get(e.child.rid)
+            if c is not None and c.kind == "dimension" and _same_domain(c, e.child):
+                vals = [_druid_str(i.value) for i in e.items if i.value is not None]
+                f = S.ExtractionFilterSpec(c.druid_column, "true", S.InExtractionFnSpec.for_values(vals))
+                return S.NotFilterSpec(f) if e.negated else f
+        cmp = _as_comparison(e)
+        if cmp is not None:
+            op, l, r = cmp
+            if isinstance(l, A.Lit) and isinstance(r, A.Ref):
+                op, l, r = _FLIP[op], r, l
+            if isinstance(l, A.Ref) and isinstance(r, A.Lit) and r.value is not None:
+                c = pf.cols.get(l.rid)
+                if c is not None:
+                    if c.spatial is not None and c.kind is None and op in ("<", "<=", ">", ">="):
+                        return self._spatial(pf, c, op, r.value)
+                    if c.kind == "dimension" and _same_domain(c, l, r):
+                        return _dim_compare(c, op, r.value, l.dtype)
+                    if c.kind == "metric" and isinstance(r.value, (int, float)) and not isinstance(r.value, bool):
+                        return _metric_compare(c, op, r.value)
+                    if c.is_time:
+                        iv = self._time_interval(pf, e)
+                        if iv is not None:
+                            return S.IntervalFilterSpec("__time", [f"{fmt_iso(max(iv[0], 0))}/{fmt_iso(iv[1])}"])
+            # date comparisons on a date-string dimension: ISO dates order lexicographically
+            df = self._date_dim_compare(pf, op, l, r)
+            if df is not None:
+                return df
+        return None
+
+    def _date_dim_compare(self, pf, op, l, r):
+        if isinstance(l, A.Lit):
+            op, l, r = _FLIP[op], r, l
+        if not isinstance(r, A.Lit):
+            return None
+        inner = l
+        wrapped = False
+        while isinstance(inner, (A.Call, A.Cast)):
+            if isinstance(inner, A.Call) and inner.name in ("datetime", "to_date") and len(inner.args) == 1:
+                inner = inner.args[0]
+                wrapped = True
+            elif isinstance(inner, A.Cast) and inner.to in ("date", "timestamp"):
+                inner = inner.child
+                wrapped = True
+            else:
+                break
+        if not wrapped or not isinstance(inner, A.Ref):
+            return None
+        c = pf.cols.get(inner.rid)
+        if c is None or c.kind != "dimension" or base(c.sql_type) != "string":
+            return None
+        if not _iso_date_dictionary(pf.table.info.datasource, c.druid_column):
+            return None
+        ms = _lit_ms(r)
+        if ms is None:
+            return None
+        if ms % DAY_MS == 0:
+            v = fmt_iso(ms)[:10]
+            strict_hi = op == "<"
+            strict_lo = op == ">"
+        else:
+            v = fmt_iso((ms // DAY_MS) * DAY_MS)[:10]
+            strict_hi = False
+            strict_lo = True
+        if op in ("<", "<="):
+            return S.BoundFilterSpec(c.druid_column, None, v, False, strict_hi)
+        if op in (">", ">="):
+            return S.BoundFilterSpec(c.druid_column, v, None, strict_lo, False)
+        if op == "=":
+            return S.SelectorFilterSpec(c.druid_column, v) if ms % DAY_MS == 0 else S.SelectorFilterSpec("__time", "")
+        return None
+
+    def _spatial(self, pf, c, op, value):
+        idx = pf.table.info.spatial_indexes()[c.spatial.druid_column]
+        mins = [x.spatial.min_value if x.spatial.min_value is not None else -1.7976931348623157e308 for x in idx]
+        maxs = [x.spatial.max_value if x.spatial.max_value is not None else 1.7976931348623157e308 for x in idx]
+        pos = [x.column for x in idx].index(c.column)
+        v = float(value)
+        if op in (">", ">="):
+            mins[pos] = v if op == ">=" else np.nextafter(v, np.inf)
+        else:
+            maxs[pos] = v if op == "<=" else np.nextafter(v, -np.inf)
+        return S.SpatialFilterSpec(c.spatial.druid_column, {"type": "rectangular", "minCoords": mins,
+                                                            "maxCoords": maxs})
+
+    def _expr_filter(self, pf: PF, e: A.Expr):
+        refs = {r.rid: r for r in e.refs()}
+        if len(refs) != 1:
+            raise NotPushable(f"predicate over {len(refs)} columns: {e.sql()}")
+        r = next(iter(refs.values()))
+        c = self._column(pf, r)
+        if any(isinstance(x, A.SubqueryExpr) for x in e.walk()):
+            raise NotPushable("subquery in predicate")
+        if c.kind == "dimension":
+            js = js_single_column_fn(e, r, c.druid_column)
+            f = S.JavascriptFilterSpec(c.druid_column, js)
+            f._pyvec = _dict_predicate(e, r, c)  # type: ignore[attr-defined]
+            return f
+        if c.is_time:
+            js = js_single_column_fn(e, r, "__time")
+            f = S.JavascriptFilterSpec("__time", js)
+            f._pyfn = _time_predicate(e, r, c)  # type: ignore[attr-defined]
+            return f
+        raise NotPushable(f"predicate over metric {c.column}: {e.sql()}")
+
+    # ============================================================================== aggregate
+    def _aggregate(self, agg: P.Aggregate) -> Optional[P.Plan]:
+        pf = self._finish_pf(self._collect(agg.child))
+        if agg.grouping_sets is not None:
+            return self._grouping_sets(agg, pf)
+        return self._groupby(agg, pf, list(range(len(agg.groups))), None)
+
+    def _grouping_sets(self, agg: P.Aggregate, pf: PF) -> P.Plan:
+        outs = agg.output
+        kids = []
+        ngr = len(agg.groups)
+        for st in agg.grouping_sets:
+            sub = self._groupby(agg, pf, st, None)
+            # sub outputs agg.output rids; give each branch fresh ids for union
+            refs = sub.output
+            exprs = []
+            for i, r in enumerate(outs):
+                if i < ngr and i not in st:
+                    exprs.append(A.Alias(A.Lit(None, r.dtype) if r.dtype != "null" else A.Lit(None, "null"), r.name))
+                elif agg.gid is not None and i == len(outs) - 1:
+                    gid = 0
+                    for j in range(ngr):
+                        if j not in st:
+                            gid |= 1 << (ngr - 1 - j)
+                    exprs.append(A.Alias(A.Lit(gid, "int"), r.name))
+                else:
+                    src = [x for x in refs if x.rid == r.rid][0]
+                    exprs.append(A.Alias(src, r.name))
+            kids.append(P.Project(exprs, sub))
+        return P.Union(kids, outs, distinct=False)
+
+    def _groupby(self, agg: P.Aggregate, pf: PF, gset: List[int], _unused) -> P.Plan:
+        info = pf.table.info
+        ds = info.datasource
+        intervals, filt = self._filters(pf)
+        names = _Names()
+        dims = []
+        columns = []   # (druid out name, sql type, kind)
+        drefs = []     # DruidQuery output refs
+        final = {}     # agg.output rid -> expr over drefs
+        outs = agg.output
+        for i in gset:
+            g = agg.groups[i]
+            e = pf.sub(g.child)
+            spec, kind = self._dim_spec(pf, e, names.dim(g.name))
+            dims.append(spec)
+            t = typeof(e)
+            r = A.Ref(A.new_id(), g.name, t)
+            drefs.append(r)
+            columns.append((spec.outputName, t, kind))
+            final[outs[i].rid] = r
+        aggs = []
+        for j, a in enumerate(agg.aggs):
+            call = a.child
+            call = A.Call(call.name, tuple(pf.sub(x) for x in call.args), call.distinct)
+            parts, combine = self._agg_spec(pf, call, names)
+            prefs = []
+            for spec_, t in parts:
+                aggs.append(spec_)
+                r = A.Ref(A.new_id(), spec_.name, t)
+                drefs.append(r)
+                columns.append((spec_.name, t, "value"))
+                prefs.append(r)
+            out_t = outs[len(agg.groups) + j].dtype
+            ex = combine(prefs)
+            if typeof(ex) != out_t:
+                ex = A.Cast(ex, out_t)
+            final[outs[len(agg.groups) + j].rid] = ex
+        if not gset and agg.aggs:
+            # global aggregate: SQL returns one row with NULL sum/min/max/avg over no input rows
+            cname = names.agg()
+            aggs.append(S.FunctionAggregationSpec("count", cname, "count"))
+            cref = A.Ref(A.new_id(), cname, "bigint")
+            drefs.append(cref)
+            columns.append((cname, "bigint", "value"))
+            for j, a in enumerate(agg.aggs):
+                if a.child.name in ("count", "approx_count_distinct"):
+                    continue
+                rid = outs[len(agg.groups) + j].rid
+                final[rid] = A.Case(((A.BinOp("=", cref, A.Lit(0, "int")), A.Lit(None, typeof(final[rid]))),),
+                                    final[rid])
+        q = S.GroupByQuerySpec(info.ds_name, dims, None, None, S.Granularity.parse("all"), filt, aggs, None,
+                               intervals)
+        dq = P.DruidQuery(pf.table, q, columns, drefs, {"groupby": True, "noop_conds": pf.noop_conds})
+        exprs = []
+        for r in outs:
+            if r.rid in final:
+                exprs.append(A.Alias(final[r.rid], r.name, r.rid))
+        return P.Project(exprs, dq)
+
+    # -- grouping expressions ------------------------------------------------------------------
+    def _dim_spec(self, pf: PF, e: A.Expr, out: str):
+        if isinstance(e, A.Ref):
+            c = self._column(pf, e)
+            if c.kind == "dimension":
+                return S.DefaultDimensionSpec(c.druid_column, out), "value"
+            if c.is_time:
+                fmt = _time_format_for(c.sql_type, pf.table.info.datasource)
+                return S.ExtractionDimensionSpec("__time", out, S.TimeFormatExtractionFunctionSpec(fmt)), "string"
+            raise NotPushable(f"cannot group by metric {c.column}")
+        te = self._time_element(pf, e)
+        if te is not None:
+            col, fmt = te
+            if col.is_time:
+                return S.ExtractionDimensionSpec("__time", out, S.TimeFormatExtractionFunctionSpec(fmt)), "string"
+            return (S.ExtractionDimensionSpec(col.druid_column, out,
+                                              S.TimeParsingExtractionFunctionSpec("yyyy-MM-dd", fmt)), "string")
+        refs = {r.rid: r for r in e.refs()}
+        if len(refs) == 0:
+            raise NotPushable("constant grouping expression")
+        if len(refs) > 1:
+            raise NotPushable(f"grouping expression over {len(refs)} columns: {e.sql()}")
+        r = next(iter(refs.values()))
+        c = self._column(pf, r)
+        if c.kind == "dimension":
+            fn = S.JavaScriptExtractionFunctionSpec(js_single_column_fn(e, r, c.druid_column))
+            fn._pyvec = _dict_extraction(e, r, c)  # type: ignore[attr-defined]
+            return S.ExtractionDimensionSpec(c.druid_column, out, fn), "value"
+        if c.is_time:
+            fn = S.JavaScriptExtractionFunctionSpec(js_single_column_fn(e, r, "__time"))
+            fn._pyfn = _time_extraction(e, r, c)  # type: ignore[attr-defined]
+            return S.ExtractionDimensionSpec("__time", out, fn), "value"
+        raise NotPushable(f"cannot group by an expression over metric {c.column}")
+
+    def _time_element(self, pf: PF, e: A.Expr):
+        """year(dateTime(col)) / month(col) / date_format(col, fmt) / to_date(col) ... ->
+        (column, Joda format) when col is the time column or an ISO-date string dimension."""
+        fmt = None
+        arg = None
+        if isinstance(e, A.Call):
+            n = e.name
+            if n in _TIME_FIELD_FMT and len(e.args) == 1:
+                fmt, arg = _TIME_FIELD_FMT[n], e.args[0]
+            elif n == "date_format" and len(e.args) == 2 and isinstance(e.args[1], A.Lit):
+                fmt, arg = str(e.args[1].value), e.args[0]
+            elif n == "to_date" and len(e.args) == 1:
+                fmt, arg = "yyyy-MM-dd", e.args[0]
+        elif isinstance(e, A.Cast) and e.to == "date":
+            fmt, arg = "yyyy-MM-dd", e.child
+        if fmt is None:
+            return None
+        while True:
+            if isinstance(arg, A.Call) and arg.name in ("datetime", "to_date") and len(arg.args) == 1:
+                arg = arg.args[0]
+            elif isinstance(arg, A.Cast) and arg.to in ("date", "timestamp"):
+                arg = arg.child
+            else:
+                break
+        if not isinstance(arg, A.Ref):
+            return None
+        c = pf.cols.get(arg.rid)
+        if c is None:
+            return None
+        if c.is_time:
+            return c, fmt
+        if c.kind == "dimension" and base(c.sql_type) == "string" and \
+                _iso_date_dictionary(pf.table.info.datasource, c.druid_column):
+            return c, fmt
+        return None
+
+    # -- aggregates ------------------------------------------------------------------------------
+    def _agg_spec(self, pf: PF, call: A.Call, names: "_Names"):
+        info = pf.table.info
+        ds = info.datasource
+        n = call.name
+        rolled = "count" in ds.metrics and getattr(ds, "rollup", False)
+
+        def count_spec():
+            nm = names.agg()
+            if rolled:
+                return S.FunctionAggregationSpec("longSum", nm, "count"), "bigint"
+            return S.FunctionAggregationSpec("count", nm, "count"), "bigint"
+
+        if n == "count" and not call.args:
+            return [count_spec()], lambda rs: rs[0]
+        if n == "count" and not call.distinct:
+            if len(call.args) != 1 or not isinstance(call.args[0], A.Ref):
+                raise NotPushable("count over an expression")
+            c = self._column(pf, call.args[0])
+            if c.kind == "dimension":
+                cs, t = count_spec()
+                f = S.FilteredAggregationSpec(S.NotFilterSpec(S.SelectorFilterSpec(c.druid_column, "")), cs, cs.name)
+                return [(f, t)], lambda rs: rs[0]
+            return [count_spec()], lambda rs: rs[0]
+        if (n == "count" and call.distinct) or n == "approx_count_distinct":
+            if n == "count" and not self.approx_distinct:
+                raise NotPushable("exact COUNT(DISTINCT) (rewritten to a two-level aggregate)")
+            if not info.options.pushHLLTODruid:
+                raise NotPushable("pushHLLTODruid is false")
+            if len(call.args) != 1 or not isinstance(call.args[0], A.Ref):
+                raise NotPushable("distinct count over an expression")
+            c = self._column(pf, call.args[0])
+            nm = names.agg()
+            if c.hll_metric is not None:
+                return [(S.HyperUniqueAggregationSpec(nm, c.hll_metric), "double")], \
+                    lambda rs: A.Call("round", (rs[0],))
+            if c.kind != "dimension":
+                raise NotPushable(f"cardinality over non-dimension {c.column}")
+            return [(S.CardinalityAggregationSpec(nm, [c.druid_column], True), "double")], \
+                lambda rs: A.Call("round", (rs[0],))
+        if n in ("sum", "min", "max", "avg", "mean"):
+            if call.distinct:
+                raise NotPushable(f"{n}(DISTINCT)")
+            x = call.args[0]
+            kind = "sum" if n in ("avg", "mean") else n
+            spec_, t = self._numeric_agg(pf, kind, x, names)
+            if n in ("avg", "mean"):
+                cnt, ct = count_spec()
+                return [(spec_, t), (cnt, ct)], \
+                    lambda rs: A.BinOp("/", A.Cast(rs[0], "double"), rs[1])
+            return [(spec_, t)], lambda rs: rs[0]
+        raise NotPushable(f"aggregate {n} is not pushable")
+
+    def _numeric_agg(self, pf: PF, kind: str, x: A.Expr, names: "_Names"):
+        if isinstance(x, A.Cast) and (x.to in ("double", "float") or x.to.startswith("decimal")):
+            x = x.child
+        nm = names.agg()
+        if isinstance(x, A.Ref):
+            c = self._column(pf, x)
+            if c.is_metric:
+                integral = c.metric_kind == "long"
+                prefix = "long" if integral else "double"
+                op = {"sum": "Sum", "min": "Min", "max": "Max"}[kind]
+                return S.FunctionAggregationSpec(prefix + op, nm, c.druid_column), ("bigint" if integral else "double")
+            raise NotPushable(f"{kind} over non-metric column {c.column}")
+        refs = {r.rid: r for r in x.refs()}
+        if not refs:
+            raise NotPushable("aggregate of a constant")
+        cols = []
+        for r in refs.values():
+            c = self._column(pf, r)
+            if not c.is_metric:
+                raise NotPushable(f"aggregate expression over non-metric {c.column}")
+            cols.append((r, c))
+        if not vm_compatible(x):
+            raise NotPushable(f"aggregate expression not supported by the scan VM: {x.sql()}")
+        stripped = x.transform(lambda e: e.child if isinstance(e, A.Cast) else None)
+        params = []
+        pnames = {}
+        for r, c in cols:
+            p = _js_ident(c.druid_column)
+            if p in params:
+                continue
+            params.append(p)
+            pnames[r.rid] = p
+        try:
+            agg, comb, reset = js_aggregator(kind, stripped, pnames, params)
+        except JSGenError as ex:
+            raise NotPushable(str(ex))
+        fields = []
+        seen = set()
+        for r, c in cols:
+            if c.druid_column not in seen:
+                seen.add(c.druid_column)
+                fields.append(c.druid_column)
+        return S.JavascriptAggregationSpec(nm, fields, agg, comb, reset), "double"
+
+    # ============================================================================== sort / limit
+    def _druid_below(self, p: P.Plan):
+        """Follow row-preserving Projects down to a DruidQuery groupBy; returns (dq, ref map) where
+        ref map sends each visible ref id to the DruidQuery output ref it is a plain copy of."""
+        m: Dict[int, int] = {}
+        chain = []
+        while isinstance(p, P.Project):
+            chain.append(p)
+            p = p.child
+        if not isinstance(p, P.DruidQuery) or not p.info.get("groupby"):
+            return None, None
+        ids = {r.rid for r in p.refs}
+        ident = {rid: rid for rid in ids}
+        for proj in reversed(chain):
+            nxt = {}
+            for e, r in zip(proj.exprs, proj.output):
+                src = e.child if isinstance(e, A.Alias) else e
+                while isinstance(src, A.Cast):
+                    src = src.child
+                if isinstance(src, A.Ref) and src.rid in ident:
+                    nxt[r.rid] = ident[src.rid]
+            ident = nxt
+        return p, ident
+
+    def _sort(self, s: P.Sort) -> Optional[P.Plan]:
+        dq, m = self._druid_below(s.child)
+        if dq is None:
+            return None
+        q = dq.spec
+        if q.limitSpec is not None and (q.limitSpec.columns or q.limitSpec.limit is not None):
+            return None
+        cols = []
+        names = {r.rid: c[0] for r, c in zip(dq.refs, dq.columns)}
+        for o in s.orders:
+            if not isinstance(o.expr, A.Ref) or o.expr.rid not in m:
+                raise NotPushable("ORDER BY expression is not a pushed column")
+            if o.nulls_first is not None and o.nulls_first != o.ascending:
+                raise NotPushable("non-default NULLS ordering")
+            cols.append(S.OrderByColumnSpec(names[m[o.expr.rid]], "ascending" if o.ascending else "descending"))
+        dq.spec = q.copy(limitSpec=S.LimitSpec(None, cols))
+        return s.child
+
+    def _limit(self, l: P.Limit) -> Optional[P.Plan]:
+        dq, m = self._druid_below(l.child)
+        if dq is None:
+            return None
+        q = dq.spec
+        ls = q.limitSpec
+        if ls is None:
+            dq.spec = q.copy(limitSpec=S.LimitSpec(l.n, []))
+        else:
+            lim = l.n if ls.limit is None else min(ls.limit, l.n)
+            dq.spec = q.copy(limitSpec=S.LimitSpec(lim, ls.columns))
+        return None
+
+    # ============================================================================== select
+    def _select(self, p: P.Plan) -> Optional[P.Plan]:
+        """Non-aggregate Project/Filter over a Druid relation -> Select query (paged)."""
+        chain = p
+        try:
+            pf = self._collect(chain)
+        except NotPushable:
+            return None
+        if pf.table is None:
+            return None
+        pf = self._finish_pf(pf)
+        info = pf.table.info
+        mode = info.options.nonAggQueryHandling
+        src = self.session.catalog.lookup(info.source_name)
+        has_src = src is not None and getattr(src, "has_data", False)
+        if mode == "push_none" and has_src:
+            return None
+        if mode == "push_filters" and not pf.conds and has_src:
+            return None
+        # only fire at the top of a maximal Project/Filter chain: the parent rule sees it otherwise
+        intervals, filt = self._filters(pf)
+        outs = p.output
+        needed: Dict[int, A.Ref] = {}
+        exprs = []
+        for r in outs:
+            e = pf.sub(r) if r.rid in pf.subst else r
+            for x in e.refs():
+                needed[x.rid] = x
+            exprs.append((r, e))
+        dims, mets = [], []
+        columns = []
+        drefs = []
+        rmap = {}
+        for rid, x in needed.items():
+            c = self._column(pf, x)
+            if c.is_time:
+                name = "timestamp"
+                kind = "time"
+            elif c.kind == "dimension":
+                name = c.druid_column
+                dims.append(name) if name not in dims else None
+                kind = "value"
+            elif c.is_metric:
+                name = c.druid_column
+                mets.append(name) if name not in mets else None
+                kind = "value"
+            else:
+                raise NotPushable(f"column {c.column} has no direct Druid column")
+            nr = A.Ref(A.new_id(), x.name, x.dtype)
+            drefs.append(nr)
+            columns.append((name, x.dtype, kind))
+            rmap[rid] = nr
+        page = int(self.conf.typed("spark.sparklinedata.druid.selectquery.pagesize"))
+        q = S.SelectSpec(info.ds_name, dims, mets, filt, S.PagingSpec({}, page), intervals)
+        dq = P.DruidQuery(pf.table, q, columns, drefs, {"select": True})
+
+        def remap(e):
+            return e.transform(lambda x: rmap[x.rid] if isinstance(x, A.Ref) and x.rid in rmap else None)
+        proj = [A.Alias(remap(e), r.name, r.rid) for r, e in exprs]
+        return P.Project(proj, dq)
+
+    # ============================================================================== finalize
+    def _finalize(self, p: P.Plan) -> Optional[P.Plan]:
+        if not isinstance(p, P.DruidQuery) or not p.info.get("groupby"):
+            return None
+        info = p.relation.info
+        ds = info.datasource
+        q = p.spec
+        lo, hi = data_interval(ds)
+        whole = f"{fmt_iso(lo)}/{fmt_iso(hi)}"
+        ctx = QT.TransformContext(
+            allow_topn=info.options.allow_topn(self.conf),
+            topn_max=info.options.topn_max_threshold(self.conf),
+            covers_all=lambda qq: list(qq.intervals) == [whole],
+            metric_is_numeric=lambda m: True)
+        nq = QT.transform(q, ctx)
+        if isinstance(nq, S.SearchQuerySpec):
+            cols = [("value", t, k) for (_, t, k) in p.columns]
+            p.columns = cols
+            p.info["search"] = True
+        p.spec = nq
+        return None
+
+
+# ------------------------------------------------------------------------------------------------
+class _Names:
+    def __init__(self):
+        self.n = 0
+        self.used: Set[str] = set()
+
+    def agg(self) -> str:
+        self.n += 1
+        nm = f"alias-{self.n}"
+        self.used.add(nm)
+        return nm
+
+    def dim(self, base_: str) -> str:
+        nm = base_
+        k = 1
+        while nm in self.used:
+            nm = f"{base_}_{k}"
+            k += 1
+        self.used.add(nm)
+        return nm
+
+
+_FLIP = {"<": ">", "<=": ">=", ">": "<", ">=": "<=", "=": "=", "<>": "<>"}
+_DATE_CMP = {"dateisbefore": "<", "dateisafter": ">", "dateisbeforeorequal": "<=", "dateisafterorequal": ">=",
+             "dateisequal": "="}
+
+_TIME_FIELD_FMT = {
+    "year": "yyyy", "month": "MM", "monthofyear": "MM", "dayofmonth": "dd", "day": "dd", "hour": "HH",
+    "hourofday": "HH", "minute": "mm", "minuteofhour": "mm", "second": "ss", "secondofminute": "ss",
+    "weekofyear": "ww", "weekofweekyear": "ww", "dayofyear": "DDD", "monthofyearname": "MMMM",
+    "dayofweekname": "EEEE", "weekyear": "xxxx", "yearofcentury": "yy", "yearofera": "YYYY",
+}
+
+
+def _as_comparison(e: A.Expr):
+    if isinstance(e, A.BinOp) and e.op in ("=", "<", "<=", ">", ">="):
+        return e.op, e.l, e.r
+    if isinstance(e, A.Call) and e.name in _DATE_CMP and len(e.args) == 2:
+        return _DATE_CMP[e.name], e.args[0], e.args[1]
+    return None
+
+
+def _lit_ms(l: A.Lit) -> Optional[int]:
+    v = l.value
+    if v is None:
+        return None
+    if isinstance(v, pd.Timestamp):
+        return int(v.value // 10 ** 6)
+    if isinstance(v, str):
+        s = v.strip()
+        if not re.match(r"^\d{4}-\d{2}-\d{2}", s):
+            return None
+        try:
+            return int(pd.Timestamp(s.replace("Z", "")).value // 10 ** 6)
+        except ValueError:
+            return None
+    return None
+
+
+def data_interval(ds) -> Tuple[int, int]:
+    gi = getattr(ds, "global_interval_ms", None)
+    if gi is not None:
+        return gi
+    segs = getattr(ds, "segments", None)
+    if segs:
+        return min(s.interval_lo_ms for s in segs), max(s.interval_hi_ms for s in segs)
+    return ds.min_time_ms(), ds.max_time_ms() + ds.time_unit_ms
+
+
+def _druid_str(v) -> str:
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, float) and v == int(v):
+        return str(int(v))
+    if isinstance(v, pd.Timestamp):
+        return v.strftime("%Y-%m-%d")
+    return str(v)
+
+
+def _same_domain(c, ref: A.Ref, lit: Optional[A.Lit] = None) -> bool:
+    """Comparisons on the raw dimension values only mean the same thing when the SQL column type
+    and the literal agree with the dictionary's domain (DruidDataType.sparkDataType == dT)."""
+    if lit is None:
+        return True
+    st = base(ref.dtype)
+    if st == "string":
+        return isinstance(lit.value, str)
+    if st in ("tinyint", "smallint", "int", "bigint", "double", "float", "decimal"):
+        return isinstance(lit.value, (int, float)) and not isinstance(lit.value, bool)
+    return False
+
+
+def _dim_compare(c, op, value, sqlt):
+    d = c.druid_column
+    numeric = base(sqlt) in ("tinyint", "smallint", "int", "bigint", "double", "float", "decimal")
+    v = _druid_str(value)
+    if op == "=":
+        return S.SelectorFilterSpec(d, v)
+    if op == "<":
+        return S.BoundFilterSpec(d, None, v, False, True, numeric)
+    if op == "<=":
+        return S.BoundFilterSpec(d, None, v, False, False, numeric)
+    if op == ">":
+        return S.BoundFilterSpec(d, v, None, True, False, numeric)
+    if op == ">=":
+        return S.BoundFilterSpec(d, v, None, False, False, numeric)
+    return None
+
+
+def _metric_compare(c, op, value):
+    d = c.druid_column
+    v = str(value)
+    if op == "=":
+        return S.BoundFilterSpec(d, v, v, False, False, True)
+    if op == "<":
+        return S.BoundFilterSpec(d, None, v, False, True, True)
+    if op == "<=":
+        return S.BoundFilterSpec(d, None, v, False, False, True)
+    if op == ">":
+        return S.BoundFilterSpec(d, v, None, True, False, True)
+    return S.BoundFilterSpec(d, v, None, False, False, True)
+
+
+def _iso_date_dictionary(ds, dim: str) -> bool:
+    dc = ds.dims.get(dim) if hasattr(ds, "dims") else None
+    if dc is None:
+        return False
+    d = dc.dictionary
+    n = len(d)
+    if n == 0:
+        return False
+    probe = [d.value(i) for i in sorted({0, n // 2, n - 1})]
+    return all(isinstance(v, str) and re.match(r"^\d{4}-\d{2}-\d{2}$", v) for v in probe if v is not None)
+
+
+def _time_format_for(sqlt: str, ds) -> str:
+    if base(sqlt) in ("string", "date"):
+        return "yyyy-MM-dd" if ds.time_unit_ms >= DAY_MS else "yyyy-MM-dd'T'HH:mm:ss.SSS'Z'"
+    return "yyyy-MM-dd'T'HH:mm:ss.SSS'Z'"
+
+
+def _js_ident(name: str) -> str:
+    s = re.sub(r"[^A-Za-z0-9_$]", "_", name)
+    return s if not s[0].isdigit() else "_" + s
+
+
+# -- dictionary-domain evaluators ------------------------------------------------------------------
+def _dict_frame(values, r: A.Ref, c) -> Frame:
+    s = to_series(pd.Series(np.asarray(values, dtype=object)), c.sql_type)
+    return Frame({r.rid: s}, len(s))
+
+
+def _dict_predicate(e: A.Expr, r: A.Ref, c) -> Callable:
+    def fn(values):
+        fr = _dict_frame(values, r, c)
+        v = evaluate(e, fr)
+        if is_vec(v):
+            return v.fillna(False).to_numpy(dtype=bool)
+        return np.full(fr.n, bool(v), dtype=bool)
+    return fn
+
+
+def _dict_extraction(e: A.Expr, r: A.Ref, c) -> Callable:
+    def fn(values):
+        fr = _dict_frame(values, r, c)
+        v = evaluate(e, fr)
+        if not is_vec(v):
+            v = pd.Series([v] * fr.n)
+        return np.array([None if (x is pd.NA or x is pd.NaT or x is None or (isinstance(x, float) and x != x))
+                         else (x.item() if isinstance(x, np.generic) else x) for x in v], dtype=object)
+    return fn
+
+
+def _time_value(ms: int, c):
+    ts = pd.Timestamp(int(ms) * 10 ** 6)
+    t = base(c.sql_type)
+    if t == "string":
+        return ts.strftime("%Y-%m-%d") if ms % DAY_MS == 0 else ts.strftime("%Y-%m-%dT%H:%M:%S.%f")[:-3] + "Z"
+    if t == "date":
+        return ts.normalize()
+    if t in ("bigint", "int"):
+        return int(ms)
+    return ts
+
+
+def _time_predicate(e: A.Expr, r: A.Ref, c) -> Callable:
+    def fn(ms):
+        v = evaluate(e, Frame({r.rid: _time_value(ms, c)}, 1))
+        return bool(v) if v is not None else False
+    return fn
+
+
+def _time_extraction(e: A.Expr, r: A.Ref, c) -> Callable:
+    def fn(ms):
+        if ms is None:
+            return None
+        v = evaluate(e, Frame({r.rid: _time_value(ms, c)}, 1))
+        return v.item() if isinstance(v, np.generic) else v
+    return fn

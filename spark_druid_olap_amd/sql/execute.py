@@ -1,0 +1,525 @@
+"""Host executor for logical plans.
+
+Runs whatever the Druid rewrite left on the host: residual projections (``avg = sum / count``,
+casts, expressions over aggregates), HAVING filters, sorts/limits the GPU did not absorb, joins
+with non-star tables, unions, and plain (non-Druid) tables -- the roles Spark's physical operators
+play around ``DruidRDD`` in the reference (``asd/DruidStrategy.scala:368-461``).  ``DruidQuery``
+leaves execute on the GPU engine (one fused scan kernel per shard + RCCL merge) and come back as
+typed columns.
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+import pandas as pd
+
+from . import ast as A
+from . import plan as P
+from .functions import Frame, eval_series, evaluate, typeof
+from .types import AnalysisError, base, broadcast, is_vec, pandas_dtype, to_series
+
+
+class Batch:
+    """Columns (by attribute id) of equal length, in ``refs`` order."""
+
+    def __init__(self, refs: List[A.Ref], cols: Dict[int, pd.Series], n: int):
+        self.refs = refs
+        self.cols = cols
+        self.n = n
+
+    def frame(self, subq=None) -> Frame:
+        return Frame(self.cols, self.n, subq)
+
+    def take(self, idx: np.ndarray) -> "Batch":
+        return Batch(self.refs, {k: v.iloc[idx].reset_index(drop=True) for k, v in self.cols.items()}, len(idx))
+
+    def to_pandas(self, names: Optional[List[str]] = None) -> pd.DataFrame:
+        names = names or [r.name for r in self.refs]
+        data = {}
+        for i, (r, nm) in enumerate(zip(self.refs, names)):
+            key = nm if nm not in data else f"{nm}_{i}"
+            data[key] = self.cols[r.rid].reset_index(drop=True)
+        return pd.DataFrame(data)
+
+
+class Executor:
+    def __init__(self, session):
+        self.session = session
+        self.druid_stats: List[dict] = []
+        self._subq_cache: Dict[int, object] = {}
+
+    # ----------------------------------------------------------------------------------------
+    def run(self, plan: P.Plan) -> Batch:
+        m = getattr(self, "_" + type(plan).__name__, None)
+        if m is None:
+            raise AnalysisError(f"cannot execute {type(plan).__name__}")
+        return m(plan)
+
+    def _subquery(self, e: A.SubqueryExpr, fr: Frame):
+        key = id(e.query)
+        if key not in self._subq_cache:
+            b = self.run(e.query)
+            self._subq_cache[key] = b
+        b = self._subq_cache[key]
+        if e.kind == "scalar":
+            if b.n > 1:
+                raise AnalysisError("more than one row returned by a subquery used as an expression")
+            if b.n == 0:
+                return None
+            v = b.cols[b.refs[0].rid].iloc[0]
+            return None if v is pd.NA or v is pd.NaT else (v.item() if isinstance(v, np.generic) else v)
+        if e.kind == "exists":
+            r = b.n > 0
+            return (not r) if e.negated else r
+        # IN (subquery)
+        vals = b.cols[b.refs[0].rid]
+        v = evaluate(e.child, fr)
+        has_null = bool(vals.isna().any())
+        vset = vals.dropna()
+        if not is_vec(v):
+            if v is None:
+                return None
+            hit = bool((vset == v).any())
+            r = True if hit else (None if has_null else False)
+            return (None if r is None else not r) if e.negated else r
+        res = v.isin(vset.tolist()).astype("boolean")
+        res = res.mask(v.isna().to_numpy(), pd.NA)
+        if has_null:
+            res = res.mask(~res.fillna(False).to_numpy(dtype=bool), pd.NA)
+        return ~res if e.negated else res
+
+    # ----------------------------------------------------------------------------------------
+    def _TableScan(self, p: P.TableScan) -> Batch:
+        t = p.table
+        if t.kind == "druid":
+            src = self.session.catalog.get(t.info.source_name)
+            df = src.frame()
+        else:
+            df = t.frame()
+        cols = {}
+        for r, (c, _) in zip(p.refs, t.schema):
+            cols[r.rid] = df[c].reset_index(drop=True)
+        return Batch(p.refs, cols, len(df))
+
+    def _LocalRelation(self, p: P.LocalRelation) -> Batch:
+        cols = {}
+        for r in p.refs:
+            v = p.data.get(r.rid)
+            cols[r.rid] = v if isinstance(v, pd.Series) else to_series(pd.Series(v if v is not None else [],
+                                                                                 dtype=object), r.dtype)
+        return Batch(p.refs, cols, p.nrows)
+
+    def _Filter(self, p: P.Filter) -> Batch:
+        b = self.run(p.child)
+        m = evaluate(p.cond, b.frame(self._subquery))
+        if not is_vec(m):
+            return b if m else b.take(np.zeros(0, dtype=np.int64))
+        mask = m.fillna(False).to_numpy(dtype=bool)
+        if mask.all():
+            return b
+        return b.take(np.nonzero(mask)[0])
+
+    def _Project(self, p: P.Project) -> Batch:
+        b = self.run(p.child)
+        fr = b.frame(self._subquery)
+        cols = {}
+        refs = p.output
+        for e, r in zip(p.exprs, refs):
+            if isinstance(e, A.Ref):
+                cols[r.rid] = b.cols[e.rid]
+            elif isinstance(e, A.Alias) and isinstance(e.child, A.Ref) and e.child.dtype == r.dtype:
+                cols[r.rid] = b.cols[e.child.rid]
+            else:
+                s = eval_series(e, fr)
+                cols[r.rid] = _conform(s, r.dtype)
+        return Batch(refs, cols, b.n)
+
+    def _Sort(self, p: P.Sort) -> Batch:
+        b = self.run(p.child)
+        if b.n <= 1:
+            return b
+        fr = b.frame(self._subquery)
+        keys = []
+        for o in p.orders:
+            s = eval_series(o.expr, fr)
+            keys.append((s, o.ascending, o.nulls_first))
+        idx = sort_indices(keys, b.n)
+        return b.take(idx)
+
+    def _Limit(self, p: P.Limit) -> Batch:
+        b = self.run(p.child)
+        if b.n <= p.n:
+            return b
+        return b.take(np.arange(p.n))
+
+    def _Aggregate(self, p: P.Aggregate) -> Batch:
+        b = self.run(p.child)
+        return aggregate(p, b, self._subquery)
+
+    def _Join(self, p: P.Join) -> Batch:
+        lb = self.run(p.left)
+        rb = self.run(p.right)
+        return join(p, lb, rb, self._subquery)
+
+    def _Union(self, p: P.Union) -> Batch:
+        parts = [self.run(c) for c in p.children]
+        cols = {}
+        n = sum(b.n for b in parts)
+        for i, r in enumerate(p.refs):
+            ss = [_conform(b.cols[b.refs[i].rid], r.dtype).reset_index(drop=True) for b in parts]
+            cols[r.rid] = pd.concat(ss, ignore_index=True) if ss else to_series([], r.dtype)
+        out = Batch(p.refs, cols, n)
+        if p.distinct:
+            out = distinct(out)
+        return out
+
+    def _SetOperation(self, p: P.SetOperation) -> Batch:
+        lb = distinct(self.run(p.left)) if not p.all else self.run(p.left)
+        rb = self.run(p.right)
+        ldf = lb.to_pandas([f"c{i}" for i in range(len(lb.refs))])
+        rdf = rb.to_pandas([f"c{i}" for i in range(len(rb.refs))])
+        keys = list(ldf.columns)
+        ltag = ldf.astype(object).where(ldf.notna(), None)
+        rtag = rdf.astype(object).where(rdf.notna(), None).drop_duplicates()
+        m = ltag.merge(rtag, on=keys, how="left", indicator=True)
+        keep = (m["_merge"] == "both") if p.kind == "intersect" else (m["_merge"] == "left_only")
+        idx = np.nonzero(keep.to_numpy())[0]
+        return lb.take(idx)
+
+    def _DruidQuery(self, p: P.DruidQuery) -> Batch:
+        t0 = time.perf_counter()
+        res = self.session.run_druid(p)
+        cols = {}
+        n = res.num_rows
+        for r, (name, sqlt, kind) in zip(p.refs, p.columns):
+            cols[r.rid] = druid_value_series(res.data[name], sqlt, kind, n)
+        self.druid_stats.append({"spec": p.spec, "ms": (time.perf_counter() - t0) * 1e3, "rows": n})
+        return Batch(p.refs, cols, n)
+
+
+# ------------------------------------------------------------------------------------------------
+def _conform(s: pd.Series, t: str) -> pd.Series:
+    want = pandas_dtype(t)
+    if str(s.dtype) == want or (want == "datetime64[ns]" and s.dtype.kind == "M"):
+        return s
+    # plain numpy numerics (no NULLs, NaN == NULL for floats) are accepted as-is
+    if (want == "Float64" and s.dtype.kind == "f") or (want == "Int64" and s.dtype.kind in "iu"):
+        return s
+    if want == "object":
+        return s
+    return to_series(s, t)
+
+
+def druid_value_series(col, sqlt: str, kind: str, n: int) -> pd.Series:
+    """Druid result column -> typed Series (``DruidValTransform``, ``sd/DruidRDD.scala:285-418``)."""
+    from ..engine.columns import DictColumn, materialize
+
+    if isinstance(col, DictColumn):
+        return _dict_series(col, sqlt)
+    arr = np.asarray(col)
+    if kind == "time":
+        if arr.dtype.kind in "iu":
+            ts = pd.Series(pd.to_datetime(arr.astype(np.int64), unit="ms"))
+        else:
+            ts = pd.Series(pd.to_datetime(pd.Series(arr).astype(str).str.replace("Z", "", regex=False)))
+        if base(sqlt) in ("date", "timestamp"):
+            return to_series(ts, sqlt)
+        if base(sqlt) == "string":
+            midnight = bool((ts.dt.normalize() == ts).all())
+            fmt = "%Y-%m-%d" if midnight else "%Y-%m-%dT%H:%M:%S.000Z"
+            return pd.Series(ts.dt.strftime(fmt), dtype="string")
+        return to_series(ts, sqlt)
+    bt = base(sqlt)
+    if arr.dtype.kind in "fiu" and bt in ("double", "float", "decimal"):
+        return pd.Series(arr.astype(np.float64, copy=False))       # numpy float64: NaN == NULL
+    if arr.dtype.kind in "iu" and bt in ("tinyint", "smallint", "int", "bigint"):
+        return pd.Series(arr.astype(np.int64, copy=False))
+    if arr.dtype.kind == "f" and bt in ("tinyint", "smallint", "int", "bigint"):
+        if not np.isnan(arr).any():
+            return pd.Series(np.rint(arr).astype(np.int64))
+        return to_series(pd.Series(arr), sqlt)
+    if arr.dtype.kind == "O" and base(sqlt) != "string":
+        return to_series(pd.Series(arr), sqlt)
+    return to_series(pd.Series(arr), sqlt)
+
+
+_FULL_DICT_MAX = 1 << 20
+
+
+def _dict_series(col, sqlt: str) -> pd.Series:
+    """Typed values of a dictionary-coded result column.  Small dictionaries are converted once and
+    cached on the (immutable) dictionary; large ones (e.g. o_orderkey) decode only the distinct
+    codes present in the result."""
+    d = col.dictionary
+    codes = np.asarray(col.codes, dtype=np.int64)
+    nd = len(d)
+    if nd <= _FULL_DICT_MAX and (nd <= 65536 or nd <= 2 * len(codes)):
+        cache = d.__dict__.setdefault("_sql_typed", {})
+        full = cache.get(sqlt)
+        if full is None:
+            full = to_series(_raw(d.all_values()), sqlt)
+            cache[sqlt] = full
+        return pd.Series(full.array.take(codes))
+    uniq, inv = np.unique(codes, return_inverse=True)
+    typed = to_series(_raw(d.decode(uniq)), sqlt)
+    return pd.Series(typed.array.take(inv))
+
+
+def _raw(vals) -> pd.Series:
+    a = np.asarray(vals)
+    if a.dtype != object:
+        return pd.Series(a)
+    return pd.Series(a, dtype=object)
+
+
+def sort_indices(keys, n: int) -> np.ndarray:
+    """Stable multi-key sort; Spark default null ordering: NULLS FIRST for ASC, NULLS LAST for DESC."""
+    idx = np.arange(n)
+    for s, asc, nulls_first in reversed(keys):
+        s = s.iloc[idx].reset_index(drop=True)
+        isna = s.isna().to_numpy()
+        nf = asc if nulls_first is None else nulls_first
+        vals = s
+        if s.dtype.kind == "M":
+            arr = s.astype("int64").to_numpy()
+            arr = np.where(isna, 0, arr)
+        elif str(s.dtype) in ("Int64", "Float64", "boolean") or s.dtype.kind in "iufb":
+            arr = s.astype("Float64").to_numpy(dtype="float64", na_value=0.0) if str(s.dtype) != "Int64" else \
+                s.to_numpy(dtype="int64", na_value=0)
+        else:
+            codes, uniq = pd.factorize(vals, sort=True)
+            arr = codes
+        order = np.argsort(arr if asc else _neg(arr), kind="stable")
+        if isna.any():
+            na_o = order[isna[order]]
+            ok_o = order[~isna[order]]
+            order = np.concatenate([na_o, ok_o]) if nf else np.concatenate([ok_o, na_o])
+        idx = idx[order]
+    return idx
+
+
+def _neg(arr):
+    if arr.dtype.kind == "f":
+        return -arr
+    return -(arr.astype(np.int64))
+
+
+def distinct(b: Batch) -> Batch:
+    if b.n == 0:
+        return b
+    df = b.to_pandas([f"c{i}" for i in range(len(b.refs))])
+    dup = df.astype(object).where(df.notna(), None).duplicated()
+    idx = np.nonzero(~dup.to_numpy())[0]
+    return b.take(idx)
+
+
+# ------------------------------------------------------------------------------------------------
+# aggregation
+def _group_codes(keys: List[pd.Series], n: int):
+    if not keys:
+        return np.zeros(n, dtype=np.int64), 1, np.zeros(1 if n else 0, dtype=np.int64)
+    if len(keys) == 1:
+        codes, uniq = pd.factorize(keys[0], use_na_sentinel=False)
+        codes = np.asarray(codes, dtype=np.int64)
+    else:
+        df = pd.DataFrame({i: k.reset_index(drop=True) for i, k in enumerate(keys)})
+        codes = df.groupby(list(range(len(keys))), dropna=False, sort=False).ngroup().to_numpy().astype(np.int64)
+    ng = int(codes.max()) + 1 if n else 0
+    first = np.full(ng, n, dtype=np.int64)
+    np.minimum.at(first, codes, np.arange(n, dtype=np.int64))
+    return codes, ng, first
+
+
+def _agg_one(call: A.Call, fr: Frame, codes: np.ndarray, ng: int, n: int, out_t: str) -> pd.Series:
+    name = call.name
+    if name == "count" and not call.args:
+        cnt = np.bincount(codes, minlength=ng) if n else np.zeros(ng, dtype=np.int64)
+        return pd.Series(cnt.astype(np.int64), dtype="Int64")
+    args = [eval_series(a, fr) for a in call.args]
+    x = args[0] if args else None
+    if name == "count":
+        valid = np.ones(n, dtype=bool)
+        for a in args:
+            valid &= ~a.isna().to_numpy()
+        if call.distinct:
+            if len(args) == 1:
+                s = x[valid]
+                r = s.groupby(codes[valid]).nunique(dropna=True)
+            else:
+                df = pd.DataFrame({i: a[valid].astype(object) for i, a in enumerate(args)})
+                df["_g"] = codes[valid]
+                r = df.drop_duplicates().groupby("_g").size()
+            return pd.Series(r.reindex(range(ng), fill_value=0).to_numpy().astype(np.int64), dtype="Int64")
+        cnt = np.bincount(codes[valid], minlength=ng) if n else np.zeros(ng, dtype=np.int64)
+        return pd.Series(cnt.astype(np.int64), dtype="Int64")
+    if name == "approx_count_distinct":
+        valid = ~x.isna().to_numpy()
+        r = x[valid].groupby(codes[valid]).nunique()
+        return pd.Series(r.reindex(range(ng), fill_value=0).to_numpy().astype(np.int64), dtype="Int64")
+    xt = typeof(call.args[0]) if call.args else "null"
+    if name in ("sum", "avg", "mean", "stddev", "stddev_samp", "stddev_pop", "variance", "var_samp", "var_pop"):
+        if base(xt) == "string":
+            x = to_series(x, "double")
+        if call.distinct:
+            df = pd.DataFrame({"v": x, "g": codes}).dropna().drop_duplicates()
+            x, codes_ = df["v"].reset_index(drop=True), df["g"].to_numpy()
+        else:
+            codes_ = codes
+        g = x.groupby(codes_)
+        if name == "sum":
+            r = g.sum(min_count=1)
+        elif name in ("avg", "mean"):
+            r = g.mean()
+        elif name in ("stddev", "stddev_samp"):
+            r = g.std(ddof=1)
+        elif name == "stddev_pop":
+            r = g.std(ddof=0)
+        elif name in ("variance", "var_samp"):
+            r = g.var(ddof=1)
+        else:
+            r = g.var(ddof=0)
+        r = r.reindex(range(ng))
+        return to_series(r, out_t)
+    if name in ("min", "max"):
+        valid = ~x.isna().to_numpy()
+        g = x[valid].groupby(codes[valid])
+        r = (g.min() if name == "min" else g.max()).reindex(range(ng))
+        return to_series(r, out_t)
+    if name in ("first", "last"):
+        g = x.groupby(codes)
+        r = (g.first() if name == "first" else g.last()).reindex(range(ng))
+        return to_series(r, out_t)
+    if name in ("collect_list", "collect_set"):
+        valid = ~x.isna().to_numpy()
+        g = x[valid].astype(object).groupby(codes[valid])
+        r = g.agg(lambda v: list(v) if name == "collect_list" else sorted(set(v), key=str)).reindex(range(ng))
+        return pd.Series(r.to_numpy(), dtype=object)
+    raise AnalysisError(f"unsupported aggregate {name}")
+
+
+def aggregate(p: P.Aggregate, b: Batch, subq=None) -> Batch:
+    fr = b.frame(subq)
+    outs = p.output
+    gkeys = [eval_series(g.child, fr) for g in p.groups]
+    sets = p.grouping_sets if p.grouping_sets is not None else [list(range(len(p.groups)))]
+    results = []
+    ngr = len(p.groups)
+    for st in sets:
+        keys = [gkeys[i] for i in st]
+        codes, ng, first = _group_codes(keys, b.n)
+        if not p.groups and p.grouping_sets is None:
+            ng = 1
+            first = np.zeros(1, dtype=np.int64)
+        cols = {}
+        for i, g in enumerate(p.groups):
+            r = outs[i]
+            if i in st:
+                cols[r.rid] = gkeys[i].iloc[first].reset_index(drop=True) if b.n else to_series([], r.dtype)
+            else:
+                cols[r.rid] = broadcast(None, ng, r.dtype)
+        for j, a in enumerate(p.aggs):
+            r = outs[ngr + j]
+            cols[r.rid] = _agg_one(a.child, fr, codes, ng, b.n, r.dtype).reset_index(drop=True)
+        if p.gid is not None:
+            gid = 0
+            for i in range(ngr):
+                if i not in st:
+                    gid |= 1 << (ngr - 1 - i)
+            cols[outs[-1].rid] = pd.Series([gid] * ng, dtype="Int64")
+        results.append((cols, ng))
+    if len(results) == 1:
+        cols, ng = results[0]
+        return Batch(outs, cols, ng)
+    cols = {r.rid: pd.concat([c[r.rid] for c, _ in results], ignore_index=True) for r in outs}
+    return Batch(outs, cols, sum(n for _, n in results))
+
+
+# ------------------------------------------------------------------------------------------------
+# joins
+def _equi_keys(cond: Optional[A.Expr], lrefs, rrefs):
+    lids = {r.rid for r in lrefs}
+    rids = {r.rid for r in rrefs}
+    keys = []
+    rest = []
+    for c in A.conjuncts(cond):
+        if isinstance(c, A.BinOp) and c.op in ("=", "<=>"):
+            lr = {x.rid for x in c.l.refs()}
+            rr = {x.rid for x in c.r.refs()}
+            if lr and rr and lr <= lids and rr <= rids:
+                keys.append((c.l, c.r, c.op == "<=>"))
+                continue
+            if lr and rr and lr <= rids and rr <= lids:
+                keys.append((c.r, c.l, c.op == "<=>"))
+                continue
+        rest.append(c)
+    return keys, rest
+
+
+def _key_frame(exprs, b: Batch, subq, null_safe):
+    fr = b.frame(subq)
+    d = {}
+    for i, e in enumerate(exprs):
+        s = eval_series(e, fr)
+        d[f"k{i}"] = s.astype(object).where(s.notna(), None) if s.dtype.kind != "M" else s
+    return pd.DataFrame(d)
+
+
+def join(p: P.Join, lb: Batch, rb: Batch, subq=None) -> Batch:
+    keys, rest = _equi_keys(p.cond, lb.refs, rb.refs)
+    kind = p.kind
+    if keys:
+        lkf = _key_frame([k[0] for k in keys], lb, subq, None)
+        rkf = _key_frame([k[1] for k in keys], rb, subq, None)
+        # SQL: NULL keys never match (unless <=>)
+        lnull = np.zeros(lb.n, dtype=bool)
+        rnull = np.zeros(rb.n, dtype=bool)
+        for i, (_, _, ns) in enumerate(keys):
+            if not ns:
+                lnull |= lkf[f"k{i}"].isna().to_numpy()
+                rnull |= rkf[f"k{i}"].isna().to_numpy()
+        lkf["_li"] = np.arange(lb.n)
+        rkf["_ri"] = np.arange(rb.n)
+        cols = [f"k{i}" for i in range(len(keys))]
+        m = lkf[~lnull].merge(rkf[~rnull], on=cols, how="inner")
+        li = m["_li"].to_numpy(dtype=np.int64)
+        ri = m["_ri"].to_numpy(dtype=np.int64)
+    else:
+        li = np.repeat(np.arange(lb.n), rb.n)
+        ri = np.tile(np.arange(rb.n), lb.n)
+    if rest:
+        both = _pair_batch(lb, rb, li, ri)
+        m = evaluate(A.and_all(rest), both.frame(subq))
+        ok = m.fillna(False).to_numpy(dtype=bool) if is_vec(m) else np.full(len(li), bool(m))
+        li, ri = li[ok], ri[ok]
+    if kind in ("inner", "cross"):
+        return _pair_batch(lb, rb, li, ri)
+    if kind == "leftsemi":
+        return lb.take(np.unique(li))
+    if kind == "leftanti":
+        keep = np.ones(lb.n, dtype=bool)
+        keep[li] = False
+        return lb.take(np.nonzero(keep)[0])
+    # outer joins: matched pairs + unmatched rows padded with NULL
+    extra_l = np.setdiff1d(np.arange(lb.n), li) if kind in ("left", "full") else np.zeros(0, dtype=np.int64)
+    extra_r = np.setdiff1d(np.arange(rb.n), ri) if kind in ("right", "full") else np.zeros(0, dtype=np.int64)
+    out = _pair_batch(lb, rb, li, ri)
+    parts = [out]
+    if len(extra_l):
+        parts.append(_pair_batch(lb, rb, extra_l, None))
+    if len(extra_r):
+        parts.append(_pair_batch(lb, rb, None, extra_r))
+    refs = lb.refs + rb.refs
+    cols = {r.rid: pd.concat([pb.cols[r.rid] for pb in parts], ignore_index=True) for r in refs}
+    return Batch(refs, cols, sum(pb.n for pb in parts))
+
+
+def _pair_batch(lb: Batch, rb: Batch, li, ri) -> Batch:
+    n = len(li) if li is not None else len(ri)
+    cols = {}
+    for r in lb.refs:
+        cols[r.rid] = lb.cols[r.rid].iloc[li].reset_index(drop=True) if li is not None else broadcast(None, n, r.dtype)
+    for r in rb.refs:
+        cols[r.rid] = rb.cols[r.rid].iloc[ri].reset_index(drop=True) if ri is not None else broadcast(None, n, r.dtype)
+    return Batch(lb.refs + rb.refs, cols, n)
