@@ -99,10 +99,12 @@ def main():
     means = {k: world.max_float(sum(v) / len(v)) for k, v in lat.items()}
     geo = math.exp(sum(math.log(max(m, 1e-6)) for m in means.values()) / len(means))
     nq = len(queries) * args.steps
+    mins = {k: world.max_float(min(v)) for k, v in lat.items()}
+    maxs = {k: world.max_float(max(v)) for k, v in lat.items()}
     if world.rank == 0:
         if args.verbose:
             for k, v in means.items():
-                log(f"[bench] {k:55s} {v:9.3f} ms")
+                log(f"[bench] {k:55s} avg {v:9.3f}  min {mins[k]:9.3f}  max {maxs[k]:9.3f} ms")
         out = {
             "metric": "tpch_flat_8query_geomean_latency_ms",
             "value": round(geo, 4),
@@ -122,6 +124,8 @@ def main():
                        "queries": 8, "mode": args.mode},
             "qps": round(nq / (total_ms / 1e3), 3),
             "per_query_ms": {k: round(v, 4) for k, v in means.items()},
+            "per_query_min_ms": {k: round(v, 4) for k, v in mins.items()},
+            "per_query_max_ms": {k: round(v, 4) for k, v in maxs.items()},
             "rows_per_gpu": int(nrows),
         }
         print(json.dumps(out), flush=True)

@@ -216,7 +216,12 @@ class PreparedQuery:
             idx = idx[np.argsort(cols["timestamp"][idx], kind="stable")]
             if getattr(qs, "descending", False):
                 idx = idx[::-1]
-        data = {c: take(cols[c], idx) for c in out_cols}
+        identity = having is None and qt != "topN" and not (qt == "groupBy" and qs.limitSpec is not None) \
+            and not (qt == "timeseries" and "timestamp" in cols)
+        if identity:
+            data = {c: cols[c] for c in out_cols}  # identity order: no copies
+        else:
+            data = {c: take(cols[c], idx) for c in out_cols}
         return QueryResult(out_cols, data, qt, {"groups": n})
 
     def _topn_order(self, cols, idx, prog) -> np.ndarray:

@@ -79,30 +79,53 @@ def hll_estimates(regs: torch.Tensor, p: int) -> np.ndarray:
     return hll_estimate_torch(regs, p).numpy()
 
 
+def d2h(ts: List[torch.Tensor]) -> List[np.ndarray]:
+    """Device -> host through pinned (cached) staging buffers with one stream sync."""
+    outs = []
+    dev = False
+    for t in ts:
+        if t.is_cuda:
+            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            h.copy_(t, non_blocking=True)
+            outs.append(h)
+            dev = True
+        else:
+            outs.append(t)
+    if dev:
+        torch.cuda.current_stream().synchronize()
+    return [o.numpy() for o in outs]
+
+
 def finalize(prog, parts: Partials) -> Dict[str, np.ndarray]:
     """Decode groups into host columns: key outputs then aggregator outputs (Druid types)."""
     from .lower import ord2f
 
+    want_gid = bool(getattr(prog, "thetas", None))
     if parts.kind == "dense":
         small = parts.rows * parts.acc.shape[1] <= (1 << 20)
         if small:
-            acc_h = parts.acc.cpu().numpy()
+            (acc_h,) = d2h([parts.acc])
             gid = np.flatnonzero(acc_h[:, 0] > 0)
             acc_h = acc_h[gid]
             hll_d = [h.index_select(0, torch.from_numpy(gid).to(h.device)) for h in parts.hll]
+            key_ids = [(gid // kc.stride) % max(1, kc.card) for kc in prog.keys]
         else:
-            sp = parts.compact()
-            gid = sp.keys.cpu().numpy()
-            acc_h = sp.acc.cpu().numpy()
-            hll_d = sp.hll
-    else:
-        gid = parts.keys.cpu().numpy()
-        acc_h = parts.acc.cpu().numpy()
+            parts = parts.compact()
+    if parts.kind == "sparse":
+        # decode key components on the device, then one pinned D2H per array
+        g = parts.keys
+        dev_ids = []
+        for kc in prog.keys:
+            ids = torch.remainder(torch.div(g, kc.stride, rounding_mode="floor"), max(1, kc.card))
+            dev_ids.append(ids.to(torch.int32) if kc.card < 2 ** 31 else ids)
+        host = d2h(dev_ids + [parts.acc] + ([g] if want_gid else []))
+        key_ids = [h.astype(np.int64, copy=False) for h in host[:len(dev_ids)]]
+        acc_h = host[len(dev_ids)]
+        gid = host[-1] if want_gid else np.arange(acc_h.shape[0])
         hll_d = parts.hll
     cols: Dict[str, np.ndarray] = {}
     key_vals = []
-    for kc in prog.keys:
-        ids = (gid // kc.stride) % max(1, kc.card)
+    for kc, ids in zip(prog.keys, key_ids):
         vals = kc.decoder(ids) if kc.decoder is not None else ids
         key_vals.append(vals)
         cols[kc.name] = vals

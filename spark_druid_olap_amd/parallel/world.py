@@ -57,9 +57,11 @@ class World:
         """[size, *t.shape] stacked gather (same shape on every rank)."""
         if not self.distributed:
             return t.unsqueeze(0)
-        out = torch.empty((self.size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
-        return out
+        src = t.contiguous().reshape(-1)
+        # concatenated layout works on both RCCL and gloo (gloo rejects the stacked form)
+        out = torch.empty((self.size * src.numel(),), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, src, group=self.group)
+        return out.view((self.size,) + tuple(t.shape))
 
     def all_gather_varlen(self, t: torch.Tensor) -> List[torch.Tensor]:
         """Gather tensors whose first dimension differs per rank."""

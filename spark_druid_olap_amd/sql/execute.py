@@ -262,8 +262,14 @@ def _dict_series(col, sqlt: str) -> pd.Series:
             full = to_series(_raw(d.all_values()), sqlt)
             cache[sqlt] = full
         return pd.Series(full.array.take(codes))
-    uniq, inv = np.unique(codes, return_inverse=True)
-    typed = to_series(_raw(d.decode(uniq)), sqlt)
+    if hasattr(d, "start") and not getattr(d, "has_null", False) and not hasattr(d, "prefix"):
+        # integer range dictionary: value = start + code
+        vals = d.decode(codes)
+        if base(sqlt) in ("tinyint", "smallint", "int", "bigint"):
+            return pd.Series(vals.astype(np.int64, copy=False))
+        return to_series(pd.Series(vals), sqlt)
+    inv, uniq = pd.factorize(codes)
+    typed = to_series(_raw(d.decode(np.asarray(uniq, dtype=np.int64))), sqlt)
     return pd.Series(typed.array.take(inv))
 
 
