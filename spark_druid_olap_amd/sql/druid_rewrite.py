@@ -517,13 +517,19 @@ class DruidRewriter:
             if typeof(ex) != out_t:
                 ex = A.Cast(ex, out_t)
             final[outs[len(agg.groups) + j].rid] = ex
-        if not gset and agg.aggs:
+        if not gset and agg.aggs and any(a.child.name not in ("count", "approx_count_distinct") for a in agg.aggs):
             # global aggregate: SQL returns one row with NULL sum/min/max/avg over no input rows
-            cname = names.agg()
-            aggs.append(S.FunctionAggregationSpec("count", cname, "count"))
-            cref = A.Ref(A.new_id(), cname, "bigint")
-            drefs.append(cref)
-            columns.append((cname, "bigint", "value"))
+            cref = None
+            for a_, r_ in zip(aggs, drefs[len(dims):]):
+                if isinstance(a_, S.FunctionAggregationSpec) and a_.type == "count" and r_.name == a_.name:
+                    cref = r_
+                    break
+            if cref is None:
+                cname = names.agg()
+                aggs.append(S.FunctionAggregationSpec("count", cname, "count"))
+                cref = A.Ref(A.new_id(), cname, "bigint")
+                drefs.append(cref)
+                columns.append((cname, "bigint", "value"))
             for j, a in enumerate(agg.aggs):
                 if a.child.name in ("count", "approx_count_distinct"):
                     continue
