@@ -603,11 +603,9 @@ __global__ __launch_bounds__(512) void olap_scan_kernel(const ScanDesc* __restri
               const uint64_t rest = (h << hll_p) | (1ull << (hll_p - 1));
               const uint32_t rho = (uint32_t)__builtin_clzll(rest) + 1u;
               const int64_t idx = slot[u] * hll_m + bucket;
-              if (mode == M_DENSE_LDS && d->hll_lds) {
-                atomicMax((uint32_t*)(lds + ao.hll_lds_off) + idx, rho);
-              } else {
-                atomicMax((uint32_t*)ao.hll_regs + idx, rho);
-              }
+              uint32_t* r = (mode == M_DENSE_LDS && d->hll_lds) ? (uint32_t*)(lds + ao.hll_lds_off) + idx
+                                                                 : (uint32_t*)ao.hll_regs + idx;
+              if (rho > *(volatile uint32_t*)r) atomicMax(r, rho);  // saturated registers: skip the atomic
             }
           }
           continue;
@@ -681,7 +679,7 @@ __global__ __launch_bounds__(512) void olap_scan_kernel(const ScanDesc* __restri
         uint32_t* g = (uint32_t*)ao.hll_regs;
         for (int64_t i = threadIdx.x; i < G * hll_m; i += blockDim.x) {
           const uint32_t v = rr[i];
-          if (v) atomicMax(g + i, v);
+          if (v > *(volatile uint32_t*)(g + i)) atomicMax(g + i, v);
         }
       }
     }

@@ -437,7 +437,7 @@ class _Gen:
                     out.append(f"  {{ uint32_t* g = (uint32_t*)d->aops[{ai}].hll_regs;")
                     out.append(f"    for (int i = threadIdx.x; i < {G * self.m}; i += {W * 64}) {{")
                     out.append(f"      const uint32_t v = hll{ai}[i];")
-                    out.append("      if (v) atomicMax(g + i, v);")
+                    out.append("      if (v > *(volatile uint32_t*)(g + i)) atomicMax(g + i, v);")
                     out.append("    } }")
         out.append("}")
         return "\n".join(out) + "\n"

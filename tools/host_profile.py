@@ -49,6 +49,22 @@ def main():
         for _ in range(5):
             q.run()
         print(f"{n:55s} {(time.perf_counter() - t) / 5 * 1e3:8.3f} ms")
+    # interleaved (bench) order, with and without the cyclic GC
+    import gc
+
+    for gc_on in (True, False):
+        if not gc_on:
+            gc.disable()
+        lat = {n: [] for n, _ in qs}
+        for _ in range(5):
+            for n, q in qs:
+                t = time.perf_counter()
+                q.run()
+                lat[n].append((time.perf_counter() - t) * 1e3)
+        gc.enable()
+        print(f"--- interleaved, gc={'on' if gc_on else 'off'}")
+        for n, v in lat.items():
+            print(f"{n:55s} avg {sum(v) / len(v):8.3f}  min {min(v):8.3f}  max {max(v):8.3f} ms")
     pr = cProfile.Profile()
     pr.enable()
     for _ in range(a.steps):
