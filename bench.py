@@ -86,6 +86,12 @@ def main():
             pq.run()
     world.barrier()
     sync()
+    prof = None
+    if os.environ.get("SDO_BENCH_PROFILE") and world.rank == 0:
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
     tstart = time.perf_counter()
     for _ in range(args.steps):
         for name, pq in queries:
@@ -95,6 +101,11 @@ def main():
     sync()
     world.barrier()
     total_ms = (time.perf_counter() - tstart) * 1e3
+    if prof is not None:
+        import pstats
+
+        prof.disable()
+        pstats.Stats(prof, stream=sys.stderr).sort_stats("cumulative").print_stats(40)
     total_ms = world.max_float(total_ms)
     means = {k: world.max_float(sum(v) / len(v)) for k, v in lat.items()}
     geo = math.exp(sum(math.log(max(m, 1e-6)) for m in means.values()) / len(means))

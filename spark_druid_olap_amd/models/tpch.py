@@ -467,3 +467,105 @@ Q10 = ("TPCH Q10", f"""select c_name, c_nation, c_address, c_phone, c_comment, s
       and dateIsBefore(dateTime(`o_orderdate`), datePlus(dateTime("1993-10-01"), period("P3M")))
       and l_returnflag = 'R'
     group by c_name, c_nation, c_address, c_phone, c_comment""")
+
+
+# --------------------------------------------------------------------------- star schema
+# The reference's TPC-H star schema over the same denormalized index (tc/BaseTest.scala:59-141,
+# documented at sd/metadata/StarSchemaInfo.scala:138-165): nation/region are split into customer-
+# and supplier-side copies so every table has a unique join path and column names stay unique.
+STAR_COLUMN_MAPPING = {"cn_name": "c_nation", "cr_name": "c_region", "sn_name": "s_nation", "sr_name": "s_region"}
+
+
+def star_schema_json(fact_db: str = "default", dim_db: str = "default") -> str:
+    import json
+
+    def rel(l, r, keys):
+        return {"leftTable": l, "rightTable": r, "relationType": "n-1",
+                "joinCondition": [{"leftAttribute": a, "rightAttribute": b} for a, b in keys]}
+    f, d = fact_db, dim_db
+    rels = [rel(f"{f}.lineitem", f"{d}.orders", [("l_orderkey", "o_orderkey")]),
+            rel(f"{f}.lineitem", f"{d}.partsupp", [("l_partkey", "ps_partkey"), ("l_suppkey", "ps_suppkey")]),
+            rel(f"{d}.partsupp", f"{d}.part", [("ps_partkey", "p_partkey")]),
+            rel(f"{d}.partsupp", f"{d}.supplier", [("ps_suppkey", "s_suppkey")]),
+            rel(f"{d}.orders", f"{d}.customer", [("o_custkey", "c_custkey")]),
+            rel(f"{d}.customer", f"{d}.custnation", [("c_nationkey", "cn_nationkey")]),
+            rel(f"{d}.custnation", f"{d}.custregion", [("cn_regionkey", "cr_regionkey")]),
+            rel(f"{d}.supplier", f"{d}.suppnation", [("s_nationkey", "sn_nationkey")]),
+            rel(f"{d}.suppnation", f"{d}.suppregion", [("sn_regionkey", "sr_regionkey")])]
+    return json.dumps({"factTable": f"{f}.lineitem", "relations": rels})
+
+
+STAR_SCHEMAS = {
+    "lineitembase": [("l_orderkey", "integer"), ("l_partkey", "integer"), ("l_suppkey", "integer"),
+                     ("l_linenumber", "integer"), ("l_quantity", "double"), ("l_extendedprice", "double"),
+                     ("l_discount", "double"), ("l_tax", "double"), ("l_returnflag", "string"),
+                     ("l_linestatus", "string"), ("l_shipdate", "string"), ("l_commitdate", "string"),
+                     ("l_receiptdate", "string"), ("l_shipinstruct", "string"), ("l_shipmode", "string"),
+                     ("l_comment", "string")],
+    "orders": [("o_orderkey", "integer"), ("o_custkey", "integer"), ("o_orderstatus", "string"),
+               ("o_totalprice", "double"), ("o_orderdate", "string"), ("o_orderpriority", "string"),
+               ("o_clerk", "string"), ("o_shippriority", "integer"), ("o_comment", "string")],
+    "partsupp": [("ps_partkey", "integer"), ("ps_suppkey", "integer"), ("ps_availqty", "integer"),
+                 ("ps_supplycost", "double"), ("ps_comment", "string")],
+    "part": [("p_partkey", "integer"), ("p_name", "string"), ("p_mfgr", "string"), ("p_brand", "string"),
+             ("p_type", "string"), ("p_size", "integer"), ("p_container", "string"), ("p_retailprice", "double"),
+             ("p_comment", "string")],
+    "supplier": [("s_suppkey", "integer"), ("s_name", "string"), ("s_address", "string"), ("s_nationkey", "integer"),
+                 ("s_phone", "string"), ("s_acctbal", "double"), ("s_comment", "string")],
+    "customer": [("c_custkey", "integer"), ("c_name", "string"), ("c_address", "string"), ("c_nationkey", "integer"),
+                 ("c_phone", "string"), ("c_acctbal", "double"), ("c_mktsegment", "string"), ("c_comment", "string")],
+    "custnation": [("cn_nationkey", "integer"), ("cn_name", "string"), ("cn_regionkey", "integer"),
+                   ("cn_comment", "string")],
+    "custregion": [("cr_regionkey", "integer"), ("cr_name", "string"), ("cr_comment", "string")],
+    "suppnation": [("sn_nationkey", "integer"), ("sn_name", "string"), ("sn_regionkey", "integer"),
+                   ("sn_comment", "string")],
+    "suppregion": [("sr_regionkey", "integer"), ("sr_name", "string"), ("sr_comment", "string")],
+}
+
+
+def star_tables(df):
+    """Split the flattened table back into the star-schema tables (distinct rows per key)."""
+    import pandas as pd
+
+    nat_key = {n: i for i, (n, _) in enumerate(NATIONS)}
+    nat_reg = {n: r for n, r in NATIONS}
+    out = {}
+    li = df.rename(columns={"o_orderkey": "l_orderkey"})
+    out["lineitembase"] = li[[c for c, _ in STAR_SCHEMAS["lineitembase"]]].reset_index(drop=True)
+    out["orders"] = df[[c for c, _ in STAR_SCHEMAS["orders"]]].drop_duplicates("o_orderkey").reset_index(drop=True)
+    out["partsupp"] = df[[c for c, _ in STAR_SCHEMAS["partsupp"]]].drop_duplicates(
+        ["ps_partkey", "ps_suppkey"]).reset_index(drop=True)
+    p = df[["l_partkey"] + [c for c, _ in STAR_SCHEMAS["part"][1:]]].rename(columns={"l_partkey": "p_partkey"})
+    out["part"] = p.drop_duplicates("p_partkey").reset_index(drop=True)
+    s = df[["l_suppkey", "s_name", "s_address", "s_nation", "s_phone", "s_acctbal", "s_comment"]].drop_duplicates(
+        "l_suppkey")
+    out["supplier"] = pd.DataFrame({"s_suppkey": s.l_suppkey, "s_name": s.s_name, "s_address": s.s_address,
+                                    "s_nationkey": s.s_nation.map(nat_key), "s_phone": s.s_phone,
+                                    "s_acctbal": s.s_acctbal, "s_comment": s.s_comment}).reset_index(drop=True)
+    c = df[["o_custkey", "c_name", "c_address", "c_nation", "c_phone", "c_acctbal", "c_mktsegment",
+            "c_comment"]].drop_duplicates("o_custkey")
+    out["customer"] = pd.DataFrame({"c_custkey": c.o_custkey, "c_name": c.c_name, "c_address": c.c_address,
+                                    "c_nationkey": c.c_nation.map(nat_key), "c_phone": c.c_phone,
+                                    "c_acctbal": c.c_acctbal, "c_mktsegment": c.c_mktsegment,
+                                    "c_comment": c.c_comment}).reset_index(drop=True)
+    nations = pd.DataFrame({"k": [nat_key[n] for n, _ in NATIONS], "n": [n for n, _ in NATIONS],
+                            "r": [nat_reg[n] for n, _ in NATIONS], "c": [f"nation {n}" for n, _ in NATIONS]})
+    regions = pd.DataFrame({"k": list(range(len(REGIONS))), "n": REGIONS, "c": [f"region {r}" for r in REGIONS]})
+    for pre in ("cn", "sn"):
+        out[f"{pre[0]}{'ustnation' if pre == 'cn' else 'uppnation'}"] = nations.rename(
+            columns={"k": f"{pre}_nationkey", "n": f"{pre}_name", "r": f"{pre}_regionkey", "c": f"{pre}_comment"})
+    for pre in ("cr", "sr"):
+        out[f"{pre[0]}{'ustregion' if pre == 'cr' else 'uppregion'}"] = regions.rename(
+            columns={"k": f"{pre}_regionkey", "n": f"{pre}_name", "c": f"{pre}_comment"})
+    return out
+
+
+def star_ddl(datasource: str = "tpch", fact_db: str = "default", dim_db: str = "default") -> str:
+    import json
+
+    return (f"CREATE TABLE if not exists {fact_db}.lineitem USING org.sparklinedata.druid OPTIONS ("
+            f"sourceDataframe \"{fact_db}.lineitembase\", timeDimensionColumn \"l_shipdate\", "
+            f"druidDatasource \"{datasource}\", druidHost 'localhost', "
+            f"columnMapping '{json.dumps(STAR_COLUMN_MAPPING)}', numProcessingThreadsPerHistorical '1', "
+            f"functionalDependencies '{json.dumps(FUNCTIONAL_DEPENDENCIES)}', "
+            f"starSchema '{star_schema_json(fact_db, dim_db)}')")

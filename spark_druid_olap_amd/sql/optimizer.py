@@ -27,7 +27,7 @@ def optimize(plan: P.Plan, conf=None) -> P.Plan:
     p = p.transform_up(_sum_of_literal)
     if not approx:
         p = p.transform_up(_distinct_rewrite)
-    for _ in range(8):
+    for _ in range(64):
         q = _push_down(p)
         if q is p:
             break
