@@ -54,7 +54,8 @@ def main():
     del flat
     if dev.type == "cuda":
         torch.cuda.synchronize()
-        torch.cuda.empty_cache()
+        if not os.environ.get("SDO_BENCH_KEEP_CACHE"):
+            torch.cuda.empty_cache()
     log(f"[bench] rank0 shard: {nrows} rows, {ds.size_bytes() / 1e9:.1f} GB resident, gen+index {time.time() - t0:.1f}s")
 
     engine = Engine(world)
@@ -81,6 +82,7 @@ def main():
             torch.cuda.synchronize()
 
     lat = {name: [] for name, _ in queries}
+    stats = {name: {} for name, _ in queries}
     for _ in range(args.warmup):
         for name, pq in queries:
             pq.run()
@@ -98,6 +100,11 @@ def main():
             a = time.perf_counter()
             r = pq.run()
             lat[name].append((time.perf_counter() - a) * 1e3)
+            st = getattr(r, "stats", None) if args.verbose else None
+            if st:
+                for k, v in st.items():
+                    if k.endswith("_ms"):
+                        stats[name].setdefault(k, []).append(v)
     sync()
     world.barrier()
     total_ms = (time.perf_counter() - tstart) * 1e3
@@ -115,7 +122,8 @@ def main():
     if world.rank == 0:
         if args.verbose:
             for k, v in means.items():
-                log(f"[bench] {k:55s} avg {v:9.3f}  min {mins[k]:9.3f}  max {maxs[k]:9.3f} ms")
+                log(f"[bench] {k:55s} avg {v:9.3f}  min {mins[k]:9.3f}  max {maxs[k]:9.3f} ms  " +
+                    " ".join(f"{sk}={sum(sv) / len(sv):.3f}" for sk, sv in stats[k].items()))
         out = {
             "metric": "tpch_flat_8query_geomean_latency_ms",
             "value": round(geo, 4),

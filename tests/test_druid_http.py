@@ -1,0 +1,67 @@
+"""Druid-compatible HTTP API over the engine + the Druid clients (DruidClient,
+broker/coordinator/overlord clients, retry utils)."""
+import json
+import os
+
+import pytest
+
+from spark_druid_olap_amd.client.druid_client import (DruidCoordinatorClient, DruidOverlordClient,
+                                                      DruidQueryServerClient)
+from spark_druid_olap_amd.engine.executor import Engine
+from spark_druid_olap_amd.models.bench_queries import DRUID_JSON
+from spark_druid_olap_amd.server.druid_http import DruidHTTPServer
+from spark_druid_olap_amd.session import Session
+from spark_druid_olap_amd.utils.errors import DruidDataSourceException
+
+
+@pytest.fixture(scope="module")
+def srv(ds_small):
+    s = Session(engine=Engine(use_native=False))
+    s.register_datasource(ds_small)
+    h = DruidHTTPServer(s, port=0).start()
+    yield h
+    h.stop()
+
+
+def test_native_queries_roundtrip(srv, ds_small):
+    c = DruidQueryServerClient("127.0.0.1", srv.port)
+    for name, q in DRUID_JSON.items():
+        r = c.execute_query(q)
+        assert isinstance(r, list) and r, name
+        if q["queryType"] == "groupBy":
+            assert {"version", "timestamp", "event"} <= set(r[0])
+    q1 = c.execute_query(DRUID_JSON["TPCH Q1"])
+    assert sum(e["event"]["alias-1"] for e in q1) == ds_small.num_rows
+    ts = c.execute_query({"queryType": "timeseries", "dataSource": "tpch", "granularity": "all",
+                          "intervals": ["1992-01-01/1999-01-01"],
+                          "aggregations": [{"type": "count", "name": "c"}]})
+    assert ts[0]["result"]["c"] == ds_small.num_rows
+    tb = c.time_boundary("tpch")
+    assert tb["minTime"].startswith("1992")
+    md = c.metadata("tpch")
+    assert md["columns"]["l_returnflag"]["cardinality"] == 3
+    assert "tpch" in c.datasources()
+
+
+def test_coordinator_and_errors(srv):
+    co = DruidCoordinatorClient("127.0.0.1", srv.port)
+    assert co.segments("tpch", full=False)
+    assert co.servers_info()[0]["type"] == "historical"
+    with pytest.raises(DruidDataSourceException):
+        DruidQueryServerClient("127.0.0.1", srv.port).execute_query({"queryType": "groupBy", "dataSource": "nope",
+                                                                     "dimensions": [], "intervals": []})
+
+
+@pytest.mark.skipif(not os.path.exists("/root/reference/src/test/resources/zip_code.json.template"),
+                    reason="reference checkout not mounted")
+def test_overlord_index_task(srv):
+    ref = "/root/reference/src/test/resources"
+    text = open(f"{ref}/zip_code.json.template").read().replace(":DATA_DIR:", f"{ref}/zipCodes/sample")
+    ov = DruidOverlordClient("127.0.0.1", srv.port)
+    tid = ov.submit_task(json.loads(text))
+    st = ov.wait_until_task_completes(tid, timeout_s=30, poll_s=0.05)
+    assert st["status"] == "SUCCESS"
+    r = DruidQueryServerClient("127.0.0.1", srv.port).execute_query(
+        {"queryType": "timeseries", "dataSource": "zipCodes", "granularity": "all",
+         "intervals": ["2015-01-01/2017-01-01"], "aggregations": [{"type": "count", "name": "c"}]})
+    assert r[0]["result"]["c"] >= 1
