@@ -19,7 +19,8 @@ class DictColumn:
     __array_priority__ = 10
 
     def __init__(self, codes: np.ndarray, dictionary):
-        self.codes = np.asarray(codes, dtype=np.int64)
+        codes = np.asarray(codes)
+        self.codes = codes if codes.dtype in (np.int32, np.int64) else codes.astype(np.int64)
         self.dictionary = dictionary
         self._decoded = None
 

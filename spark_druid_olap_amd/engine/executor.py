@@ -449,6 +449,9 @@ class Engine:
     """Executes QuerySpecs on the current rank's shards, merging across the process group."""
 
     def __init__(self, world: Optional[World] = None, use_native: Optional[bool] = None):
+        from ..utils.memory import tune_host_malloc
+
+        tune_host_malloc()
         self.world = world or get_world()
         if use_native is None:
             use_native = torch.cuda.is_available()

@@ -118,10 +118,11 @@ def finalize(prog, parts: Partials) -> Dict[str, np.ndarray]:
         for kc in prog.keys:
             ids = torch.remainder(torch.div(g, kc.stride, rounding_mode="floor"), max(1, kc.card))
             dev_ids.append(ids.to(torch.int32) if kc.card < 2 ** 31 else ids)
-        host = d2h(dev_ids + [parts.acc] + ([g] if want_gid else []))
-        key_ids = [h.astype(np.int64, copy=False) for h in host[:len(dev_ids)]]
-        acc_h = host[len(dev_ids)]
-        gid = host[-1] if want_gid else np.arange(acc_h.shape[0])
+        # slot-major accumulators so every output column is a contiguous view (no host copies)
+        host = d2h(dev_ids + [parts.acc.t().contiguous()] + ([g] if want_gid else []))
+        key_ids = host[:len(dev_ids)]
+        acc_h = host[len(dev_ids)].T
+        gid = host[-1] if want_gid else None
         hll_d = parts.hll
     cols: Dict[str, np.ndarray] = {}
     key_vals = []
@@ -168,23 +169,24 @@ def finalize(prog, parts: Partials) -> Dict[str, np.ndarray]:
         acc_h, hll_d = new_acc, new_hll
     for a in prog.aggs:
         if a.kind in ("count",):
-            cols[a.name] = acc_h[:, a.slot].astype(np.int64)
+            cols[a.name] = acc_h[:, a.slot]
         elif a.kind in ("sum_i", "min_i", "max_i"):
             v = acc_h[:, a.slot]
             if a.scale:
                 cols[a.name] = v.astype(np.float64) / (10.0 ** a.scale)
             elif a.out_type == "long":
-                cols[a.name] = v.astype(np.int64)
+                cols[a.name] = v
             else:
                 cols[a.name] = v.astype(np.float64)
         elif a.kind == "sum_f":
-            cols[a.name] = acc_h[:, a.slot].view(np.float64).copy()
+            col = acc_h[:, a.slot]
+            cols[a.name] = col.view(np.float64) if col.flags.c_contiguous else col.copy().view(np.float64)
         elif a.kind in ("min_f", "max_f"):
             cols[a.name] = ord2f(acc_h[:, a.slot]).copy()
         elif a.kind == "hll":
             cols[a.name] = hll_estimates(hll_d[a.hll_index], prog.hll_p) if len(acc_h) else np.zeros(0)
         elif a.kind == "theta":
             pass  # filled by the executor
-    cols["__rows__"] = acc_h[:, 0].astype(np.int64)
+    cols["__rows__"] = acc_h[:, 0]
     cols["__gid__"] = gid if not collapse else np.arange(len(acc_h))
     return cols
