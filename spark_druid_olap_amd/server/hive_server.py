@@ -50,6 +50,9 @@ class Operation:
         self.completed = 0
         self.thread: Optional[threading.Thread] = None
         self.cancelled = threading.Event()
+        from ..utils.cancel import CancelToken
+
+        self.token = CancelToken()
 
     def handle(self) -> Dict[str, Any]:
         return {"operationId": {"guid": self.id, "secret": self.secret}, "operationType": self.kind,
@@ -210,6 +213,8 @@ class HiveThriftServer:
         self.ops[op.id] = op
         stmt = req.get("statement", "")
         overlay = req.get("confOverlay") or {}
+        if req.get("queryTimeout"):
+            op.token.deadline = time.monotonic() + float(req["queryTimeout"])
         if req.get("runAsync"):
             op.state = T.OP_RUNNING
             op.thread = threading.Thread(target=self._run, args=(op, stmt, overlay), daemon=True)
@@ -230,7 +235,7 @@ class HiveThriftServer:
                 for k, v in overlay.items():
                     self.session.conf.set(k, v)
                 df = self.session.sql(stmt.strip().rstrip(";"))
-                pdf = df.to_pandas()
+                pdf = df.to_pandas(token=op.token)
                 op.set_frame(df.columns, [t for _, t in df.schema], pdf)
             op.state = T.OP_FINISHED if not op.cancelled.is_set() else T.OP_CANCELED
         except Exception as e:  # noqa: BLE001
@@ -252,6 +257,7 @@ class HiveThriftServer:
         op = self.ops.get(_oid(req))
         if op is not None:
             op.cancelled.set()
+            op.token.cancel("cancelled by client")
             if op.state in (T.OP_INITIALIZED, T.OP_RUNNING):
                 op.state = T.OP_CANCELED
         return {"status": _ok()}

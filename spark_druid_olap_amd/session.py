@@ -69,10 +69,16 @@ class DataFrame:
         self.last_stats: Dict[str, Any] = {}
 
     # -- execution ---------------------------------------------------------------------------
-    def _run(self) -> Batch:
+    def _run(self, token=None) -> Batch:
         if self._batch is not None:
             return self._batch
-        ex = Executor(self.session)
+        if token is None:
+            tmo = self.session.conf.typed("spark.sparklinedata.druid.query.timeout.ms")
+            if tmo:
+                from .utils.cancel import CancelToken
+
+                token = CancelToken(tmo)
+        ex = Executor(self.session, token)
         t0 = time.perf_counter()
         b = self.session._with_sql(self.sql_text, lambda: ex.run(self.plan))
         self.last_stats = {"ms": (time.perf_counter() - t0) * 1e3, "druid": ex.druid_stats}
@@ -81,16 +87,16 @@ class DataFrame:
     def prepared(self) -> "DataFrame":
         return self
 
-    def run(self) -> Batch:
-        return self._run()
+    def run(self, token=None) -> Batch:
+        return self._run(token)
 
-    def collect(self) -> List[tuple]:
-        b = self._run()
+    def collect(self, token=None) -> List[tuple]:
+        b = self._run(token)
         cols = [series_to_list(b.cols[r.rid], r.dtype) for r in b.refs]
         return list(zip(*cols)) if cols else [() for _ in range(b.n)]
 
-    def to_pandas(self) -> pd.DataFrame:
-        return self._run().to_pandas(self.names)
+    def to_pandas(self, token=None) -> pd.DataFrame:
+        return self._run(token).to_pandas(self.names)
 
     toPandas = to_pandas
 
@@ -142,6 +148,24 @@ class Session:
         self._plan_cache: Dict[Tuple[str, int, int, str], DataFrame] = {}
         self._lock = threading.RLock()
         self._tl = threading.local()
+        from .modules import load_modules
+
+        self.modules = load_modules(self)
+
+    # ------------------------------------------------------------------------------ extension points
+    def register_udf(self, name: str, fn, return_type: str = "string", vectorized: bool = False) -> None:
+        """Register a scalar SQL function.  ``fn`` takes Python values (NULL-propagating, called per
+        row) or, with ``vectorized=True``, pandas Series/scalars and returns the same shape.  Over a
+        Druid dimension the function is still pushed down: it is evaluated once per dictionary
+        entry, like every other single-dimension expression."""
+        from .sql import functions as F
+
+        if vectorized:
+            impl = lambda args, ts, n: fn(*args)  # noqa: E731
+        else:
+            impl = F._map_scalar(fn, return_type)
+        F._FUNCS[name.lower()] = F.Fn(name.lower(), lambda ts, t=return_type: t, impl)
+        self._plan_cache.clear()
 
     # ------------------------------------------------------------------------------ registration
     def register_datasource(self, ds, name: Optional[str] = None) -> None:
@@ -182,6 +206,12 @@ class Session:
 
     # ------------------------------------------------------------------------------ SQL
     def sql(self, text: str) -> DataFrame:
+        for m in self.modules:
+            p = getattr(m, "parse", None)
+            if p is not None:
+                r = p(text, self)
+                if r is not None:
+                    return r
         try:
             st = parse(text)
         except ParseError as pe:
@@ -211,8 +241,14 @@ class Session:
         analyzed = an.analyze(st)
         names = [r.name for r in analyzed.output]
         opt = optimize(analyzed, self.conf)
+        for m in self.modules:
+            for rule in getattr(m, "logical_rules", []) or []:
+                opt = rule(opt, self) or opt
         rw = DruidRewriter(self)
         phys = rw.rewrite(opt)
+        for m in self.modules:
+            for rule in getattr(m, "physical_rules", []) or []:
+                phys = rule(phys, self) or phys
         if self.conf.typed("spark.sparklinedata.druid.debug.transformations"):
             import logging
 

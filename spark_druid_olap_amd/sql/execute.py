@@ -45,13 +45,16 @@ class Batch:
 
 
 class Executor:
-    def __init__(self, session):
+    def __init__(self, session, token=None):
         self.session = session
+        self.token = token
         self.druid_stats: List[dict] = []
         self._subq_cache: Dict[int, object] = {}
 
     # ----------------------------------------------------------------------------------------
     def run(self, plan: P.Plan) -> Batch:
+        if self.token is not None:
+            self.token.check()
         m = getattr(self, "_" + type(plan).__name__, None)
         if m is None:
             raise AnalysisError(f"cannot execute {type(plan).__name__}")
@@ -190,6 +193,8 @@ class Executor:
 
     def _DruidQuery(self, p: P.DruidQuery) -> Batch:
         t0 = time.perf_counter()
+        if self.token is not None:
+            self.token.check()
         res = self.session.run_druid(p)
         cols = {}
         n = res.num_rows
