@@ -338,7 +338,7 @@ class Lowerer:
     def __init__(self, ds: DataSource, bitmap_max_values: int = 4):
         self.ds = ds
         self.bitmap_max_values = bitmap_max_values
-        self._time_values: Optional[np.ndarray] = None
+        self._tv_cache: Optional[np.ndarray] = None
 
     # ------------------------------------------------------------------ filters -> IR
     def filter_ir(self, f) -> tuple:
@@ -440,6 +440,8 @@ class Lowerer:
         ds = self.ds
         u = ds.time_unit_ms
         if isinstance(f, S.SelectorFilterSpec):
+            if f.value is None or f.value == "":
+                return FALSE  # __time is never null (the reference's NULL-scan marker)
             ms = _to_ms(f.value)
             return ("time", ms, ms + 1)
         if isinstance(f, S.BoundFilterSpec):
@@ -707,10 +709,14 @@ class Lowerer:
             derived = np.asarray(pv(d.all_values()), dtype=object)
         else:
             derived = d.map_values(extraction_callable(fn))
-        uniq = sorted({v for v in derived.tolist() if v is not None}, key=lambda v: (str(type(v)), v))
-        has_null = any(v is None for v in derived.tolist())
-        dd = Dictionary(uniq, "string" if all(isinstance(v, str) for v in uniq) else "double", has_null)
-        remap = np.array([dd.lookup(v) for v in derived.tolist()], dtype=np.int32)
+        vals = derived.tolist()
+        uniq = sorted({v for v in vals if v is not None}, key=lambda v: (str(type(v)), v))
+        has_null = any(v is None for v in vals)
+        numeric = all(isinstance(v, (int, float)) and not isinstance(v, bool) for v in uniq)
+        # non-numeric, non-string derived values (dates, timestamps, booleans) keep their Python objects
+        dd = Dictionary(uniq, "double" if numeric and uniq else "string", has_null)
+        pos = {v: i + (1 if has_null else 0) for i, v in enumerate(uniq)}
+        remap = np.array([0 if v is None else pos[v] for v in vals], dtype=np.int32)
         return KeyComp(name, D.K_REMAP, dim, len(dd), remap=remap, decoder=lambda ids, _d=dd: DictColumn(ids, _d))
 
     def _time_key(self, name, fn, ivs: List[Interval]) -> KeyComp:
@@ -901,11 +907,14 @@ class Lowerer:
                 sc = (10.0 ** -m.scale) if (m is not None and m.kind == "decimal" and m.scale) else 0.0
                 out.append((D.E_COL, prog.col(name), sc))
                 return 1
-            if k in ("neg", "abs"):
+            unary = {"neg": D.E_NEG, "abs": D.E_ABS, "floor": D.E_FLOOR, "ceil": D.E_CEIL, "sqrt": D.E_SQRT,
+                     "log": D.E_LOG, "exp": D.E_EXP}
+            if k in unary:
                 d = rec(n[1], depth)
-                out.append((D.E_NEG if k == "neg" else D.E_ABS, 0, 0.0))
+                out.append((unary[k], 0, 0.0))
                 return d
-            op = {"add": D.E_ADD, "sub": D.E_SUB, "mul": D.E_MUL, "div": D.E_DIV, "min": D.E_MIN, "max": D.E_MAX}[k]
+            op = {"add": D.E_ADD, "sub": D.E_SUB, "mul": D.E_MUL, "div": D.E_DIV, "min": D.E_MIN, "max": D.E_MAX,
+                  "mod": D.E_MOD, "pmod": D.E_PMOD, "pow": D.E_POW}[k]
             d1 = rec(n[1], depth)
             d2 = rec(n[2], depth + 1)
             out.append((op, 0, 0.0))

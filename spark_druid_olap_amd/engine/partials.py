@@ -131,7 +131,7 @@ def finalize(prog, parts: Partials) -> Dict[str, np.ndarray]:
         key_vals.append(vals)
         cols[kc.name] = vals
     collapse = any(kc.collapse for kc in prog.keys)
-    if collapse and len(gid):
+    if collapse and len(acc_h):
         # non-injective key formatting: re-aggregate groups that format identically
         tup = list(zip(*[v.tolist() for v in key_vals]))
         uniq = {}

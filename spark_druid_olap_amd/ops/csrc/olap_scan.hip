@@ -391,6 +391,14 @@ __device__ __forceinline__ double eval_expr(const ScanDesc* __restrict__ d, int 
       s0 = -s0;
     } else if (e.op == E_ABS) {
       s0 = fabs(s0);
+    } else if (e.op >= E_FLOOR && e.op <= E_EXP) {
+      switch (e.op) {
+        case E_FLOOR: s0 = floor(s0); break;
+        case E_CEIL: s0 = ceil(s0); break;
+        case E_SQRT: s0 = sqrt(s0); break;
+        case E_LOG: s0 = log(s0); break;
+        default: s0 = exp(s0); break;
+      }
     } else {
       const double a = s1, b = s0;
       double r;
@@ -400,6 +408,9 @@ __device__ __forceinline__ double eval_expr(const ScanDesc* __restrict__ d, int 
         case E_MUL: r = a * b; break;
         case E_DIV: r = a / b; break;
         case E_MIN: r = fmin(a, b); break;
+        case E_MOD: r = fmod(a, b); break;
+        case E_PMOD: { const double m = fmod(a, b); r = m < 0.0 ? fmod(m + b, b) : m; } break;  // Spark Pmod
+        case E_POW: r = pow(a, b); break;
         default: r = fmax(a, b); break;
       }
       s0 = r; s1 = s2; s2 = s3;

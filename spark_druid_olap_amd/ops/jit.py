@@ -209,6 +209,18 @@ class _Gen:
                 st.append(f"(-{st.pop()})")
             elif op == D.E_ABS:
                 st.append(f"fabs({st.pop()})")
+            elif op in (D.E_FLOOR, D.E_CEIL, D.E_SQRT, D.E_LOG, D.E_EXP):
+                fn = {D.E_FLOOR: "floor", D.E_CEIL: "ceil", D.E_SQRT: "sqrt", D.E_LOG: "log", D.E_EXP: "exp"}[op]
+                st.append(f"{fn}({st.pop()})")
+            elif op in (D.E_MOD, D.E_PMOD, D.E_POW):
+                y, x = st.pop(), st.pop()
+                if op == D.E_MOD:
+                    st.append(f"fmod({x}, {y})")
+                elif op == D.E_POW:
+                    st.append(f"pow({x}, {y})")
+                else:
+                    st.append(f"([](double a_, double b_) {{ const double m_ = fmod(a_, b_); "
+                              f"return m_ < 0.0 ? fmod(m_ + b_, b_) : m_; }})({x}, {y})")
             else:
                 y, x = st.pop(), st.pop()
                 sym = {D.E_ADD: "+", D.E_SUB: "-", D.E_MUL: "*", D.E_DIV: "/"}.get(op)

@@ -210,6 +210,19 @@ def _expr_values(prog, eops, rows: torch.Tensor) -> torch.Tensor:
             st[-1] = -st[-1]
         elif op == D.E_ABS:
             st[-1] = st[-1].abs()
+        elif op in (D.E_FLOOR, D.E_CEIL, D.E_SQRT, D.E_LOG, D.E_EXP):
+            st[-1] = {D.E_FLOOR: torch.floor, D.E_CEIL: torch.ceil, D.E_SQRT: torch.sqrt, D.E_LOG: torch.log,
+                      D.E_EXP: torch.exp}[op](st[-1])
+        elif op in (D.E_MOD, D.E_PMOD, D.E_POW):
+            b = st.pop()
+            a = st.pop()
+            if op == D.E_POW:
+                st.append(torch.pow(a, b))
+            else:
+                m = torch.fmod(a, b)
+                if op == D.E_PMOD:
+                    m = torch.where(m < 0, torch.fmod(m + b, b), m)
+                st.append(m)
         else:
             b = st.pop()
             a = st.pop()

@@ -486,9 +486,9 @@ class _ExprAst:
 
     def term(self):
         a = self.unary()
-        while self.peek()[1] in ("*", "/"):
+        while self.peek()[1] in ("*", "/", "%"):
             op = self.next()[1]
-            a = ("mul" if op == "*" else "div", a, self.unary())
+            a = ({"*": "mul", "/": "div", "%": "mod"}[op], a, self.unary())
         return a
 
     def unary(self):
@@ -514,8 +514,10 @@ class _ExprAst:
                     self.next()
                     args.append(self.expr())
                 self.next()  # )
-                if fn == "abs":
-                    return ("abs", args[0])
+                if fn in ("abs", "floor", "ceil", "sqrt", "log", "exp"):
+                    return (fn, args[0])
+                if fn in ("pow", "pmod"):  # Math.pmod: Spark pmod (extension used by the SQL planner)
+                    return (fn, args[0], args[1])
                 if fn in ("max", "min"):
                     out = args[0]
                     for a in args[1:]:

@@ -33,7 +33,7 @@ from ..query import transforms as QT
 from ..query.intervals import fmt_iso
 from . import ast as A
 from . import plan as P
-from .functions import Frame, Period, evaluate, typeof
+from .functions import Frame, Period, evaluate, is_deterministic, typeof
 from .jscodegen import JSGenError, js_aggregator, js_single_column_fn, vm_compatible
 from .types import AnalysisError, base, is_vec, to_series
 
@@ -311,6 +311,11 @@ class DruidRewriter:
 
     # -- dimension / metric predicates ----------------------------------------------------------
     def _filter(self, pf: PF, e: A.Expr):
+        if not is_deterministic(e):
+            raise NotPushable(f"non-deterministic predicate {e.sql()}")
+        nn = self._null_test_constant(pf, e)
+        if nn is not None:
+            return None if nn else S.SelectorFilterSpec("__time", "")
         f = self._native_filter(pf, e)
         if f is not None:
             return f
@@ -373,6 +378,29 @@ class DruidRewriter:
             if df is not None:
                 return df
         return None
+
+    def _null_test_constant(self, pf: PF, e: A.Expr) -> Optional[bool]:
+        """IS [NOT] NULL over metric / spatial-axis expressions: those columns are never NULL in the
+        index, so the test folds to a constant when the expression cannot introduce a NULL."""
+        if not isinstance(e, A.IsNull):
+            return None
+        refs = e.child.refs()
+        if not refs:
+            return None
+        for r in refs:
+            c = pf.cols.get(r.rid)
+            if c is None or not (c.is_metric or (c.kind is None and c.spatial is not None)):
+                return None
+        for x in e.child.walk():
+            if isinstance(x, A.BinOp) and x.op in ("/", "div") or (isinstance(x, A.BinOp) and x.op == "%" and
+                                                                   not isinstance(x.r, A.Lit)):
+                return None
+            if isinstance(x, A.Call) and x.name not in ("abs", "floor", "ceil", "round", "greatest", "least"):
+                return None
+            if isinstance(x, A.Cast) and x.to not in ("double", "float", "bigint", "int") and \
+                    not x.to.startswith("decimal"):
+                return None
+        return bool(e.negated)  # NOT NULL -> always true ; IS NULL -> always false
 
     def _date_dim_compare(self, pf, op, l, r):
         if isinstance(l, A.Lit):
@@ -493,6 +521,11 @@ class DruidRewriter:
         for i in gset:
             g = agg.groups[i]
             e = pf.sub(g.child)
+            if not is_deterministic(e):
+                raise NotPushable(f"non-deterministic grouping expression {e.sql()}")
+            if not e.refs():
+                final[outs[i].rid] = e  # grouping by a constant does not split groups
+                continue
             spec, kind = self._dim_spec(pf, e, names.dim(g.name))
             dims.append(spec)
             t = typeof(e)
@@ -504,6 +537,8 @@ class DruidRewriter:
         for j, a in enumerate(agg.aggs):
             call = a.child
             call = A.Call(call.name, tuple(pf.sub(x) for x in call.args), call.distinct)
+            if not is_deterministic(call):
+                raise NotPushable(f"non-deterministic aggregate {call.sql()}")
             parts, combine = self._agg_spec(pf, call, names)
             prefs = []
             for spec_, t in parts:
@@ -517,7 +552,7 @@ class DruidRewriter:
             if typeof(ex) != out_t:
                 ex = A.Cast(ex, out_t)
             final[outs[len(agg.groups) + j].rid] = ex
-        if not gset and agg.aggs and any(a.child.name not in ("count", "approx_count_distinct") for a in agg.aggs):
+        if not dims and agg.aggs and any(a.child.name not in ("count", "approx_count_distinct") for a in agg.aggs):
             # global aggregate: SQL returns one row with NULL sum/min/max/avg over no input rows
             cref = None
             for a_, r_ in zip(aggs, drefs[len(dims):]):
@@ -811,6 +846,12 @@ class DruidRewriter:
                 kind = "value"
             elif c.is_metric:
                 name = c.druid_column
+                mets.append(name) if name not in mets else None
+                kind = "value"
+            elif c.spatial is not None and f"{c.spatial.druid_column}.{c.spatial.position}" in \
+                    pf.table.info.datasource.metrics:
+                # a spatial axis: the point's component column (DruidValTransform "dimN")
+                name = f"{c.spatial.druid_column}.{c.spatial.position}"
                 mets.append(name) if name not in mets else None
                 kind = "value"
             else:

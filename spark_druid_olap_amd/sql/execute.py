@@ -207,6 +207,8 @@ class Executor:
 # ------------------------------------------------------------------------------------------------
 def _conform(s: pd.Series, t: str) -> pd.Series:
     want = pandas_dtype(t)
+    if want == "string" and isinstance(s.dtype, pd.CategoricalDtype):
+        return s  # dictionary-encoded strings stay encoded until something needs the values
     if str(s.dtype) == want or (want == "datetime64[ns]" and s.dtype.kind == "M"):
         return s
     # plain numpy numerics (no NULLs, NaN == NULL for floats) are accepted as-is
@@ -258,15 +260,35 @@ def _dict_series(col, sqlt: str) -> pd.Series:
     cached on the (immutable) dictionary; large ones (e.g. o_orderkey) decode only the distinct
     codes present in the result."""
     d = col.dictionary
-    codes = np.asarray(col.codes, dtype=np.int64)
+    codes = np.asarray(col.codes)
     nd = len(d)
     if nd <= _FULL_DICT_MAX and (nd <= 65536 or nd <= 2 * len(codes)):
         cache = d.__dict__.setdefault("_sql_typed", {})
-        full = cache.get(sqlt)
+        key = sqlt if base(sqlt) != "string" else "__categories__"
+        full = cache.get(key)
+        bt = base(sqlt)
         if full is None:
-            full = to_series(_raw(d.all_values()), sqlt)
-            cache[sqlt] = full
-        return pd.Series(full.array.take(codes))
+            if bt == "string":
+                # zero-copy dictionary encoding: a pandas Categorical over the (sorted, unique) values
+                vals = d.all_values()
+                has_null = bool(getattr(d, "has_null", False))
+                cats = pd.Index(np.asarray(vals[1:] if has_null else vals, dtype=object).astype(str), dtype=object)
+                full = (cats, has_null)
+            else:
+                typed = to_series(_raw(d.all_values()), sqlt)
+                if typed.isna().any() or bt not in ("tinyint", "smallint", "int", "bigint", "double", "float"):
+                    full = ("typed", typed)
+                else:
+                    full = ("numpy", typed.to_numpy(dtype=np.int64 if bt in ("tinyint", "smallint", "int", "bigint")
+                                                    else np.float64))
+            cache[key] = full
+        if bt == "string":
+            cats, has_null = full
+            c = codes.astype(np.int32, copy=False) - (1 if has_null else 0) if has_null else codes
+            return pd.Series(pd.Categorical.from_codes(c, categories=cats, validate=False))
+        if full[0] == "numpy":
+            return pd.Series(full[1][codes])
+        return pd.Series(full[1].array.take(codes))
     if hasattr(d, "start") and not getattr(d, "has_null", False) and not hasattr(d, "prefix"):
         # integer range dictionary: value = start + code
         vals = d.decode(codes)
@@ -329,6 +351,7 @@ def distinct(b: Batch) -> Batch:
 # ------------------------------------------------------------------------------------------------
 # aggregation
 def _group_codes(keys: List[pd.Series], n: int):
+    keys = [k.cat.codes if isinstance(k.dtype, pd.CategoricalDtype) else k for k in keys]
     if not keys:
         return np.zeros(n, dtype=np.int64), 1, np.zeros(1 if n else 0, dtype=np.int64)
     if len(keys) == 1:

@@ -431,6 +431,8 @@ def _ts(v, t, n=0):
 
 def _str(v, t, n=0):
     if base(t) == "string":
+        if is_vec(v) and isinstance(v.dtype, pd.CategoricalDtype):
+            return v.astype("string")
         return v
     return cast_vec(v, t, "string", n)
 

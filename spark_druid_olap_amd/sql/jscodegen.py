@@ -98,8 +98,14 @@ def js_expr(e: A.Expr, names: Dict[int, str]) -> str:
             return f"Math.{'max' if n == 'greatest' else 'min'}({', '.join(a)})"
         if n in ("sqrt", "exp", "floor", "ceil", "sin", "cos", "tan", "log"):
             return f"Math.{n}({a[0]})"
+        if n == "ceiling":
+            return f"Math.ceil({a[0]})"
         if n in ("pow", "power"):
             return f"Math.pow({a[0]}, {a[1]})"
+        if n == "pmod":
+            return f"Math.pmod({a[0]}, {a[1]})"
+        if n == "ln":
+            return f"Math.log({a[0]})"
         if n == "round":
             return f"Math.round({a[0]})"
         if n == "coalesce":
@@ -158,7 +164,7 @@ def vm_compatible(e: A.Expr) -> bool:
             if not isinstance(x.value, (int, float)) or isinstance(x.value, bool):
                 return False
             continue
-        if isinstance(x, A.BinOp) and x.op in ("+", "-", "*", "/"):
+        if isinstance(x, A.BinOp) and x.op in ("+", "-", "*", "/", "%"):
             continue
         if isinstance(x, A.UnOp) and x.op == "-":
             continue
@@ -166,7 +172,10 @@ def vm_compatible(e: A.Expr) -> bool:
             if x.to in ("bigint", "int") and typeof(x.child) not in ("bigint", "int", "smallint", "tinyint"):
                 return False
             continue
-        if isinstance(x, A.Call) and x.name in ("abs", "greatest", "least") and not x.is_agg:
+        if isinstance(x, A.Call) and x.name in ("abs", "greatest", "least", "floor", "ceil", "ceiling", "sqrt",
+                                                  "log", "ln", "exp", "pow", "power", "pmod") and not x.is_agg:
+            if x.name == "log" and len(x.args) != 1:
+                return False
             continue
         return False
     return True

@@ -360,7 +360,17 @@ class Parser:
             r = self._set_term()
             q = A.SetOp(kind, all_, q, r)
         if isinstance(q, A.SetOp):
-            q.order_by, q.limit = self._order_limit()
+            # ORDER BY / LIMIT written after the last operand bind to the whole set operation
+            last = q.right
+            if isinstance(last, A.Select) and not getattr(last, "_paren", False) and (last.order_by or
+                                                                                       last.limit is not None):
+                q.order_by, q.limit = last.order_by, last.limit
+                last.order_by, last.limit = [], None
+            o, l = self._order_limit()
+            if o:
+                q.order_by = o
+            if l is not None:
+                q.limit = l
         return q
 
     def _set_term(self):
@@ -368,6 +378,7 @@ class Parser:
             self.expect("(")
             q = self.query()
             self.expect(")")
+            q._paren = True
             return q
         return self.select()
 

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import datetime as _dt
 import math
+import re
 from typing import Any, Optional
 
 import numpy as np
@@ -91,14 +92,23 @@ EPOCH = pd.Timestamp("1970-01-01")
 
 # ------------------------------------------------------------------------------------------------
 # scalar helpers
+_TZ_SUFFIX = re.compile(r"(Z|[+-]\d{2}:?\d{2})$")
+
+
 def _parse_date(s: str):
+    """ISO-ish date/timestamp string -> naive UTC pd.Timestamp (offsets are applied, like Spark with
+    the session time zone set to UTC); unparseable -> None."""
     s = s.strip()
     try:
-        if len(s) >= 10 and s[4] == "-":
-            if len(s) == 10:
-                return pd.Timestamp(s)
-            return pd.Timestamp(s.replace("Z", "").replace("T", " ")[:26])
-        return pd.Timestamp(s)
+        if len(s) == 10 and s[4] == "-":
+            return pd.Timestamp(s)
+        if _TZ_SUFFIX.search(s):
+            t = pd.Timestamp(s)
+            return t.tz_convert("UTC").tz_localize(None) if t.tzinfo is not None else t
+        parts = s.split()
+        if len(parts) == 3 and re.match(r"^[A-Z]{2,5}$", parts[2]):
+            s = parts[0] + " " + parts[1]  # trailing zone abbreviation (e.g. PST): ignored
+        return pd.Timestamp(s.replace("T", " ")[:26])
     except (ValueError, TypeError):
         return None
 

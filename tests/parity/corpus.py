@@ -1,0 +1,105 @@
+"""Session fixture + runner for the reference SQL corpus (tests/parity/extract.py)."""
+import math
+import os
+import re
+
+REF = "/root/reference/src/test/resources"
+
+
+def build_session(sf=0.01):
+    import json
+
+    from spark_druid_olap_amd.engine.executor import Engine
+    from spark_druid_olap_amd.models import tpch
+    from spark_druid_olap_amd.segment.ingest import ingest
+    from spark_druid_olap_amd.session import Session
+
+    flat = tpch.generate_flat(sf, "cpu")
+    ds = tpch.to_datasource(flat, profile="test")
+    df = tpch.to_pandas(flat)
+    s = Session(engine=Engine(use_native=False))
+    s.register_datasource(ds)
+    s.register_table("orderLineItemPartSupplierBase", df, schema=tpch.FLAT_SCHEMA)
+    s.sql(tpch.druid_ddl())
+    for name, frame in tpch.star_tables(df).items():
+        s.register_table(name, frame, schema=tpch.STAR_SCHEMAS[name])
+    s.sql(tpch.star_ddl())
+    if os.path.exists(f"{REF}/zip_codeAll.json.template"):
+        for tmpl in ("zip_code.json.template", "zip_codeAll.json.template"):
+            s.register_datasource(ingest(f"{REF}/{tmpl}", data_dir=f"{REF}/zipCodes/sample"))
+        s.sql(f"""CREATE TABLE zipCodesBase(record_date string, zip_code string, latitude double, longitude double,
+          city string, state string, county string) USING com.databricks.spark.csv
+          OPTIONS (path "{REF}/zipCodes/sample/zip_codes_states.csv", header "false", delimiter ",")""")
+        for full in (False, True):
+            infos = json.dumps([
+                {"column": "city", **({"druidColumn": "city"} if full else {}), "hllMetric": "unique_city",
+                 "sketchMetric": "city_sketch"},
+                {"column": "latitude", "spatialIndex": {"druidColumn": "coordinates", "spatialPosition": 0,
+                                                        "minValue": -90.0, "maxValue": 90.0}},
+                {"column": "longitude", "spatialIndex": {"druidColumn": "coordinates", "spatialPosition": 1,
+                                                         "minValue": -180.0, "maxValue": 180.0}}])
+            s.sql(f"""CREATE TABLE if not exists {'zipCodesFull' if full else 'zipCodes'} USING org.sparklinedata.druid
+              OPTIONS (sourceDataframe "default.zipCodesBase", timeDimensionColumn "record_date",
+              druidDatasource "{'zipCodesAll' if full else 'zipCodes'}", columnInfos '{infos}',
+              nonAggregateQueryHandling "push_project_and_filters", allowTopNRewrite "true")""")
+    return s
+
+
+def norm_rows(rows):
+    out = []
+    for r in rows:
+        t = []
+        for v in r:
+            if isinstance(v, float):
+                v = None if math.isnan(v) else round(v, 1)
+            elif hasattr(v, "isoformat"):
+                v = str(v)[:19]
+            t.append(v)
+        out.append(tuple(t))
+    return sorted(out, key=lambda r: tuple((x is None, str(x)) for x in r))
+
+
+def rows_equal(a, b):
+    """Cell-by-cell with the reference's 1-decimal rounding tolerance (tc/AbstractTest.scala:184-190)."""
+    if len(a) != len(b):
+        return False
+    for x, y in zip(a, b):
+        for u, v in zip(x, y):
+            if isinstance(u, float) or isinstance(v, float):
+                if u is None or v is None or abs(u - v) > 0.11 + 1e-9 * max(abs(u), abs(v)):
+                    return False
+            elif u != v:
+                return False
+    return True
+
+
+def to_base(sql):
+    return re.sub(r"\borderLineItemPartSupplier\b", "orderLineItemPartSupplierBase",
+                  re.sub(r"\blineitem\b", "lineitembase", sql))
+
+
+def run_case(s, case):
+    """-> (status, detail) ; status in ok | shape | mismatch | error"""
+    fn, name, kind, sql, ndruid, base_sql = case
+    try:
+        d = s.sql(sql)
+        nq = len(d.druid_queries())
+        rows = norm_rows(d.collect())
+    except Exception as e:  # noqa: BLE001
+        return "error", f"{type(e).__name__}: {str(e)[:200]}"
+    bsql = base_sql or to_base(sql)
+    cmp_status = None
+    if bsql != sql:
+        try:
+            b = norm_rows(s.sql(bsql).collect())
+            if not rows_equal(rows, b):
+                ordered = "limit" in sql.lower()
+                if not (ordered and len(b) == len(rows)):
+                    cmp_status = f"rows differ ({len(rows)} vs {len(b)})"
+        except Exception as e:  # noqa: BLE001
+            cmp_status = f"base failed: {type(e).__name__}: {str(e)[:120]}"
+    if cmp_status:
+        return "mismatch", cmp_status
+    if ndruid is not None and nq != ndruid:
+        return "shape", f"druid queries {nq} != {ndruid}"
+    return "ok", ""
