@@ -798,7 +798,15 @@ class Lowerer:
             prog.aops.append(d)
             return d
 
-        def slot(op, init):
+        def slot(op, init, d):
+            # identical aggregators (count(*) for both COUNT and AVG, ...) share one accumulator: every
+            # slot is one more update per row in the scan kernel's inner loop
+            sig = (d["kind"], d["col"], repr(d["expr"]), repr(d["filter"]), op, init)
+            for prev in prog.aops[:-1]:
+                if prev.get("sig") == sig:
+                    prog.aops.pop()
+                    return prev["slot"]
+            d["sig"] = sig
             if len(prog.slots) >= D.MAX_SLOTS:
                 raise LoweringError("too many accumulator slots")
             prog.slots.append((op, init))
@@ -808,14 +816,14 @@ class Lowerer:
             t = a.type
             if t == "count":
                 d = aop(D.A_COUNT)
-                d["slot"] = slot(D.S_SUM_I, 0)
+                d["slot"] = slot(D.S_SUM_I, 0, d)
                 prog.aggs.append(AggOut(a.name, "count", d["slot"], out_type="long"))
                 return
             fname = a.fieldName
             if fname == "count" and fname not in ds.metrics:
                 # longSum(count) over an index without an explicit count metric == count
                 d = aop(D.A_COUNT)
-                d["slot"] = slot(D.S_SUM_I, 0)
+                d["slot"] = slot(D.S_SUM_I, 0, d)
                 prog.aggs.append(AggOut(a.name, "count", d["slot"], out_type="long"))
                 return
             if fname not in ds.metrics:
@@ -829,25 +837,25 @@ class Lowerer:
             if op == "Sum":
                 if integral or is_long:
                     d = aop(D.A_SUM_I, ci)
-                    d["slot"] = slot(D.S_SUM_I, 0)
+                    d["slot"] = slot(D.S_SUM_I, 0, d)
                     prog.aggs.append(AggOut(a.name, "sum_i", d["slot"], scale=scale if not is_long else scale,
                                             out_type="long" if is_long and scale == 0 else "double"))
                 else:
                     d = aop(D.A_SUM_F, ci)
-                    d["slot"] = slot(D.S_SUM_F, 0)
+                    d["slot"] = slot(D.S_SUM_F, 0, d)
                     prog.aggs.append(AggOut(a.name, "sum_f", d["slot"], out_type="double"))
                 return
             mn = op == "Min"
             if integral or is_long:
                 d = aop(D.A_MIN_I if mn else D.A_MAX_I, ci)
-                d["slot"] = slot(D.S_MIN_I if mn else D.S_MAX_I, D.INT64_MAX if mn else D.INT64_MIN)
+                d["slot"] = slot(D.S_MIN_I if mn else D.S_MAX_I, D.INT64_MAX if mn else D.INT64_MIN, d)
                 prog.aggs.append(AggOut(a.name, "min_i" if mn else "max_i", d["slot"], scale=scale,
                                         out_type="long" if is_long and scale == 0 else "double",
                                         combine="min" if mn else "max"))
             else:
                 d = aop(D.A_MIN_F if mn else D.A_MAX_F, ci)
                 init = _f2ord(math.inf) if mn else _f2ord(-math.inf)
-                d["slot"] = slot(D.S_MIN_I if mn else D.S_MAX_I, init)
+                d["slot"] = slot(D.S_MIN_I if mn else D.S_MAX_I, init, d)
                 prog.aggs.append(AggOut(a.name, "min_f" if mn else "max_f", d["slot"], out_type="double",
                                         combine="min" if mn else "max"))
             return
@@ -876,11 +884,11 @@ class Lowerer:
             kind = {"sum": D.A_SUM_F, "max": D.A_MAX_F, "min": D.A_MIN_F}[op]
             d = aop(kind, -1, eops)
             if op == "sum":
-                d["slot"] = slot(D.S_SUM_F, 0)
+                d["slot"] = slot(D.S_SUM_F, 0, d)
                 prog.aggs.append(AggOut(a.name, "sum_f", d["slot"]))
             else:
                 mn = op == "min"
-                d["slot"] = slot(D.S_MIN_I if mn else D.S_MAX_I, _f2ord(math.inf) if mn else _f2ord(-math.inf))
+                d["slot"] = slot(D.S_MIN_I if mn else D.S_MAX_I, _f2ord(math.inf) if mn else _f2ord(-math.inf), d)
                 prog.aggs.append(AggOut(a.name, "min_f" if mn else "max_f", d["slot"], combine=op))
             return
         if isinstance(a, S.ThetaSketchAggregationSpec):
@@ -936,7 +944,8 @@ class Lowerer:
             prog.empty = True
         # hidden presence count (slot 0)
         prog.slots.append((D.S_SUM_I, 0))
-        prog.aops.append({"kind": D.A_COUNT, "col": -1, "expr": None, "filter": None, "slot": 0, "hll": -1})
+        prog.aops.append({"kind": D.A_COUNT, "col": -1, "expr": None, "filter": None, "slot": 0, "hll": -1,
+                          "sig": (D.A_COUNT, -1, "None", "None", D.S_SUM_I, 0)})
         gk = self.granularity_key(granularity, ivs)
         if gk is not None:
             prog.keys.append(gk)

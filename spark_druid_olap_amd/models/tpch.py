@@ -581,12 +581,18 @@ def star_tables(df):
     return out
 
 
-def star_ddl(datasource: str = "tpch", fact_db: str = "default", dim_db: str = "default") -> str:
+def star_ddl(datasource: str = "tpch", fact_db: str = "default", dim_db: str = "default",
+             table: str = "lineitem", extra_options: str = "") -> str:
+    """Star-schema fact table DDL (``tc/StarSchemaBaseTest.scala:88-101``); ``table`` renames the fact
+    table (``SelectQueryTest.scala:51-63`` registers ``lineitem_select`` over the same index)."""
     import json
 
-    return (f"CREATE TABLE if not exists {fact_db}.lineitem USING org.sparklinedata.druid OPTIONS ("
+    ss = star_schema_json(fact_db, dim_db)
+    if table != "lineitem":
+        ss = ss.replace(f"{fact_db}.lineitem\"", f"{fact_db}.{table}\"")
+    return (f"CREATE TABLE if not exists {fact_db}.{table} USING org.sparklinedata.druid OPTIONS ("
             f"sourceDataframe \"{fact_db}.lineitembase\", timeDimensionColumn \"l_shipdate\", "
             f"druidDatasource \"{datasource}\", druidHost 'localhost', "
             f"columnMapping '{json.dumps(STAR_COLUMN_MAPPING)}', numProcessingThreadsPerHistorical '1', "
             f"functionalDependencies '{json.dumps(FUNCTIONAL_DEPENDENCIES)}', "
-            f"starSchema '{star_schema_json(fact_db, dim_db)}')")
+            f"starSchema '{ss}'{extra_options})")

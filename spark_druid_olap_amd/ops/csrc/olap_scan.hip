@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "scan_desc.h"
+#include "sdo_device.h"  // hll_bucket_rho (shared with the JIT kernels, bit-exact with ops/reference.py)
 
 namespace sdo {
 
@@ -609,10 +610,8 @@ __global__ __launch_bounds__(512) void olap_scan_kernel(const ScanDesc* __restri
           for (int u = 0; u < U; ++u) {
             if ((ma[u] >> lane) & 1ull) {
               const int64_t v = col_int<U>(d, wb, ao.col, u, lane);
-              const uint64_t h = mix64((uint64_t)v ^ (uint64_t)ao.salt);
-              const uint32_t bucket = (uint32_t)(h >> (64 - hll_p));
-              const uint64_t rest = (h << hll_p) | (1ull << (hll_p - 1));
-              const uint32_t rho = (uint32_t)__builtin_clzll(rest) + 1u;
+              uint32_t bucket, rho;
+              dev::hll_bucket_rho(v, ao.salt, hll_p, bucket, rho);
               const int64_t idx = slot[u] * hll_m + bucket;
               uint32_t* r = (mode == M_DENSE_LDS && d->hll_lds) ? (uint32_t*)(lds + ao.hll_lds_off) + idx
                                                                  : (uint32_t*)ao.hll_regs + idx;

@@ -56,6 +56,19 @@ class JitLayout:
     wave_bytes: int
     total: int
     ncopy: int
+    pipe: bool = False
+    regstage: bool = False
+
+
+def pipe_eligible(prog, mode: int, U: int) -> bool:
+    """Double-buffer the payload DMA (see ``_Gen._pipelined_words``)."""
+    if mode != D.M_DENSE_LDS or prog.filter_len and not prog.final_pre or not prog.pcols:
+        return False
+    if any(a.get("filt_len") or a.get("filter") is not None for a in prog.aops):
+        return False
+    cols = col_infos(prog)
+    nld = sum(2 if c.lg == 3 else 1 for i, c in cols.items() if i >= D.PAYLOAD_BASE) * U
+    return nld <= 63
 
 
 def col_infos(prog) -> Dict[int, ColInfo]:
@@ -73,27 +86,69 @@ def col_infos(prog) -> Dict[int, ColInfo]:
     return out
 
 
-def layout(prog, mode: int, U: int, hll_lds: bool, m: int) -> JitLayout:
+REG_BUDGET = int(os.environ.get("SDO_JIT_REG_BUDGET", "96"))  # VGPRs for register accumulators
+
+
+def _narrow_slot(prog, s: int, cols) -> bool:
+    """Slot whose per-chunk partial fits int32: counts and sums of <=2-byte integer columns
+    (a lane sees at most 64 rows per 4096-row chunk)."""
+    for a in prog.aops:
+        if a.get("slot") != s:
+            continue
+        if a["kind"] == D.A_COUNT:
+            return True
+        if a["kind"] == D.A_SUM_I and a["col"] in cols and cols[a["col"]].lg <= 1 and not cols[a["col"]].flt:
+            return True
+        return False
+    return False
+
+
+def reg_eligible(prog, mode: int) -> bool:
+    """Small dense key spaces (TPC-H Q1: 6 groups) accumulate in per-lane registers.
+
+    With a handful of groups, every lane of a wave updates one of a few LDS words: the LDS atomic
+    unit serializes same-address lanes and the accumulator rows alias onto the same banks.  A
+    one-hot register update (``acc[g] += key == g ? v : 0``) costs a few VALU ops per group and no
+    LDS traffic; partials are wave-reduced once at the end."""
+    if mode != D.M_DENSE_LDS or prog.G > 16 or not prog.slots:
+        return False
     cols = col_infos(prog)
-    nplanes = sum(2 if c.lg == 3 else 1 for c in cols.values())
+    regs = sum(3 if _narrow_slot(prog, s, cols) else 2 for s in range(prog.nslots)) * prog.G
+    return regs <= REG_BUDGET
+
+
+def layout(prog, mode: int, U: int, hll_lds: bool, m: int, reg: bool = False, pipe: bool = False,
+           budget: int = 150 * 1024, regstage: bool = False) -> JitLayout:
+    cols = col_infos(prog)
+    nplanes = 0 if regstage else sum(2 if c.lg == 3 else 1 for c in cols.values())
     need_bmw = _needs_word_bitmaps(prog)
-    wave_bytes = U * nplanes * 256 + (len(prog.bm_leaves) * 512 if need_bmw else 0)
+    wave_bytes = U * nplanes * 256 * (2 if pipe else 1) + (len(prog.bm_leaves) * 512 if need_bmw else 0)
     wave_bytes = (wave_bytes + 15) // 16 * 16
-    hll_bytes = prog.nhll * prog.G * m * 4 if hll_lds else 0
+    hll_bytes = prog.nhll * prog.G * m if hll_lds else 0  # byte registers (hll_update8)
     stage = W * wave_bytes
     ncopy = 1
     acc_bytes = 0
     if mode == D.M_DENSE_LDS:
         base = prog.G * prog.nslots * 8 * W
-        ncopy = 16
-        while ncopy > 1 and base * ncopy + hll_bytes + stage > 150 * 1024:
+        ncopy = 1 if reg else 16
+        while ncopy > 1 and base * ncopy + hll_bytes + stage > budget:
             ncopy //= 2
         acc_bytes = base * ncopy
     acc_off = 0
     hll_off = (acc_bytes + 15) // 16 * 16
     cache_off = (hll_off + hll_bytes + 15) // 16 * 16
     total = cache_off + stage
-    return JitLayout(acc_off, acc_bytes, hll_off, hll_bytes, cache_off, wave_bytes, total, ncopy)
+    return JitLayout(acc_off, acc_bytes, hll_off, hll_bytes, cache_off, wave_bytes, total, ncopy, pipe, regstage)
+
+
+def prefer_regstage(prog) -> bool:
+    """Staging choice measured on MI355X (tools/query_probe.py, SF100): VGPR staging wins for wide
+    unfiltered payloads (TPC-H Q1: 1.9 vs 2.2 ms), LDS-DMA staging for word-filtered scans and tiny
+    payloads (Q8: 0.14 vs 0.29 ms, 2-byte payload count: 0.46 vs 0.65 ms)."""
+    if prog.filter_len and not prog.final_pre:
+        return False
+    cols = col_infos(prog)
+    return sum(1 << c.lg for i, c in cols.items() if i >= D.PAYLOAD_BASE) > 4
 
 
 def _needs_word_bitmaps(prog) -> bool:
@@ -120,8 +175,13 @@ def _dlit(v: float) -> str:
 
 
 class _Gen:
-    def __init__(self, prog, mode: int, U: int, hll_lds: bool, narrow4: bool, lay: JitLayout, m: int):
+    def __init__(self, prog, mode: int, U: int, hll_lds: bool, narrow4: bool, lay: JitLayout, m: int,
+                 reg: bool = False):
         self.p = prog
+        self.reg = reg
+        self.pipe = lay.pipe
+        self.regstage = lay.regstage
+        self.wbv = "wbp" if lay.pipe else "wb"
         self.mode = mode
         self.U = U
         self.hll_lds = hll_lds
@@ -135,13 +195,17 @@ class _Gen:
     # ---------------------------------------------------------------- values
     def ival(self, idx: int) -> str:
         c = self.cols[idx]
+        if self.regstage:
+            return f"cv_int<{c.lg}, {'true' if c.sgn else 'false'}, {'true' if c.flt else 'false'}>(x{idx}[u])"
         return (f"ld_int<{c.lg}, {'true' if c.sgn else 'false'}, {'true' if c.flt else 'false'}, {self.n4}>"
-                f"(wb + (u * {self.NP} + {c.plane}) * 256, lane)")
+                f"({self.wbv} + (u * {self.NP} + {c.plane}) * 256, lane)")
 
     def dval(self, idx: int) -> str:
         c = self.cols[idx]
+        if self.regstage:
+            return f"cv_dbl<{c.lg}, {'true' if c.sgn else 'false'}, {'true' if c.flt else 'false'}>(x{idx}[u])"
         return (f"ld_dbl<{c.lg}, {'true' if c.sgn else 'false'}, {'true' if c.flt else 'false'}, {self.n4}>"
-                f"(wb + (u * {self.NP} + {c.plane}) * 256, lane)")
+                f"({self.wbv} + (u * {self.NP} + {c.plane}) * 256, lane)")
 
     # ---------------------------------------------------------------- filters
     def word_expr(self, lo: int, hi: int) -> str:
@@ -230,6 +294,72 @@ class _Gen:
                     st.append(f"{'fmin' if op == D.E_MIN else 'fmax'}({x}, {y})")
         return st[-1]
 
+    def stage_words(self, o: List[str], cols, wl: str, dst: str, ind: str = "      ") -> None:
+        """Load the given columns of U whole 64-row words through the per-chunk buffer resources
+        (``rs<i>``) -- into VGPR arrays ``x<i>[u]`` (register staging) or LDS planes (DMA);
+        ``wl`` names the per-u word-in-chunk array."""
+        U, NP = self.U, self.NP
+        if self.regstage:
+            for i in cols:
+                o.append(f"{ind}{'uint64_t' if self.cols[i].lg == 3 else 'uint32_t'} x{i}[{U}];")
+            o.append(f"#pragma unroll\n{ind}for (int u = 0; u < {U}; ++u) {{")
+            for i in cols:
+                c = self.cols[i]
+                o.append(f"{ind}  x{i}[u] = ld_b<{c.lg}>(rs{i}, (uint32_t){wl}[u] << {6 + c.lg}, lo{c.lg});")
+            o.append(f"{ind}}}")
+            return
+        o.append(f"#pragma unroll\n{ind}for (int u = 0; u < {U}; ++u) {{")
+        for i in cols:
+            c = self.cols[i]
+            o.append(f"{ind}  dma_b<{c.lg}>(rs{i}, (uint32_t){wl}[u] << {6 + c.lg}, lo{c.lg}, "
+                     f"{dst} + (u * {NP} + {c.plane}) * 256);")
+        o.append(f"{ind}}}")
+
+    def _pipelined_words(self, pcols, stage, body) -> List[str]:
+        """Double-buffered word loop: the payload DMA of the next U words is in flight while the
+        current U words are aggregated (one ``s_waitcnt vmcnt(N)`` instead of a full drain).  Only
+        used when the body issues no vector-memory ops of its own (LDS/register accumulators)."""
+        U, NP = self.U, self.NP
+        SB = U * NP * 256
+        nld = sum(2 if self.cols[i].lg == 3 else 1 for i in pcols) * U
+        o: List[str] = []
+
+        def take(wl, m, any_):
+            o.append(f"#pragma unroll\n    for (int u = 0; u < {U}; ++u) {{")
+            o.append(f"      if (nz) {{ {wl}[u] = __builtin_ctzll(nz); nz &= nz - 1ull; {m}[u] = readlane64(pre, {wl}[u]); }}")
+            o.append(f"      else {{ {wl}[u] = 0; {m}[u] = 0ull; }}")
+            o.append(f"      {any_} |= {m}[u];")
+            o.append("    }")
+
+        def issue(wl, m, bufexpr):
+            o.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
+            o.append(f"      unsigned char* wbi = wb + ({bufexpr}) * {SB};")
+            self.stage_words(o, pcols, wl, "wbi")
+
+        o.append(f"    int wl[{U}]; uint64_t m[{U}]; int wl2[{U}]; uint64_t m2[{U}];")
+        o.append("    uint64_t any = 0;")
+        take("wl", "m", "any")
+        o.append("    int buf = 0;")
+        o.append("    if (any) {")
+        issue("wl", "m", "0")
+        o.append("    }")
+        o.append("    while (any) {")
+        o.append("      uint64_t any2 = 0;")
+        take("wl2", "m2", "any2")
+        o.append("      if (any2) {")
+        issue("wl2", "m2", "buf ^ 1")
+        o.append(f'        asm volatile("s_waitcnt vmcnt({nld})" ::: "memory");')
+        o.append("      } else {")
+        o.append('        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
+        o.append("      }")
+        o.append(f"      unsigned char* wbp = wb + buf * {SB};")
+        o.extend(body)
+        o.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{ wl[u] = wl2[u]; m[u] = m2[u]; }}")
+        o.append("      any = any2;")
+        o.append("      buf ^= 1;")
+        o.append("    }")
+        return o
+
     # ---------------------------------------------------------------- whole kernel
     def source(self, name: str) -> str:
         p, U, NP, lay = self.p, self.U, self.NP, self.lay
@@ -242,6 +372,7 @@ class _Gen:
         pre = self.chunk_expr() if p.pre_len else None
         G, NS = p.G, p.nslots
         NCT = W * lay.ncopy
+        narrow = {s for s in range(NS) if _narrow_slot(p, s, self.cols)} if self.reg else set()
         for i in sorted(self.cols):
             L.append(f"  const unsigned char* c{i} = (const unsigned char*)d->cols[{i}].ptr;")
         for j, (row, stride, count) in enumerate(p.bm_leaves):
@@ -255,28 +386,32 @@ class _Gen:
         for ai, a in enumerate(p.aops):
             if a["kind"] == D.A_HLL:
                 if self.hll_lds and mode == D.M_DENSE_LDS:
-                    L.append(f"  uint32_t* hll{ai} = (uint32_t*)(lds + {lay.hll_off + a['hll'] * G * self.m * 4});")
+                    L.append(f"  unsigned char* hll{ai} = lds + {lay.hll_off + a['hll'] * G * self.m};")
                 else:
                     L.append(f"  uint32_t* hll{ai} = (uint32_t*)d->aops[{ai}].hll_regs;")
-        body = []
+        stage = []
+        body = stage
         # ---------------- per-word processing
-        body.append("      // ---- payload staging (inactive lanes alias the first active row) ----")
-        body.append(f"      int64_t lrow[{U}];")
+        body.append("      // ---- payload staging (whole words) ----")
         body.append(f"      bool act[{U}];")
-        body.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{")
-        body.append("        act[u] = (m[u] >> lane) & 1ull;")
-        body.append("        lrow[u] = act[u] ? row[u] : (cw0 + wl[u]) * 64 + (m[u] ? __builtin_ctzll(m[u]) : 0);")
-        body.append("      }")
+        body.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) act[u] = (m[u] >> lane) & 1ull;")
         if pcols:
-            body.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
-            body.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{")
-            for i in pcols:
-                c = self.cols[i]
-                body.append(f"        dma<{c.lg}>(c{i}, lrow[u], wb + (u * {NP} + {c.plane}) * 256);")
-            body.append("      }")
-            body.append('      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
+            if not self.regstage:
+                body.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
+            self.stage_words(body, pcols, "wl", "wb")
+            if not self.regstage:
+                body.append('      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
+        body = []
+        if self.pipe:
+            body.append(f"      bool act[{U}];")
+            body.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) act[u] = (m[u] >> lane) & 1ull;")
+        # phase 1: every staged read for the U words (keys + aggregator inputs) -- straight-line
+        # LDS reads the compiler can issue back to back; phase 2 applies the updates.
+        body.append(f"      uint64_t key_[{U}];")
+        vals: Dict[int, str] = {}
+        for ai, a in enumerate(p.aops):
+            body.append(f"      int64_t v{ai}_[{U}];")
         body.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{")
-        body.append("        if (!m[u]) continue;")
         body.append("        uint64_t key = 0;")
         for k, kc in enumerate(p.keys):
             v = self.ival(kc.col_idx)
@@ -293,6 +428,22 @@ class _Gen:
                 body.append(f"        {{ int64_t t = ({v}) - {_lit(kc.base)};")
                 body.append(f"          t = t < 0 ? 0 : (t >= {_lit(kc.card)} ? {_lit(kc.card - 1)} : t);")
                 body.append(f"          key += (uint64_t)t * {kc.stride}ull; }}")
+        body.append("        key_[u] = key;")
+        for ai, a in enumerate(p.aops):
+            kind = a["kind"]
+            if kind == D.A_HLL:
+                val = self.ival(a["col"])
+            elif kind == D.A_COUNT:
+                val = "1LL"
+            elif kind in (D.A_SUM_F, D.A_MIN_F, D.A_MAX_F):
+                dv = self.expr(a["expr"]) if a.get("expr") else self.dval(a["col"])
+                val = f"__double_as_longlong({dv})" if kind == D.A_SUM_F else f"f2ord({dv})"
+            else:
+                val = self.ival(a["col"])
+            body.append(f"        v{ai}_[u] = {val};")
+        body.append("      }")
+        body.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{")
+        body.append("        const uint64_t key = key_[u];")
         if mode == D.M_HASH:
             body.append("        int64_t slot = act[u] ? hash_slot(hkeys, hcap, key, overflow) : -1;")
             body.append("        const bool mine = act[u] && slot >= 0;")
@@ -306,18 +457,30 @@ class _Gen:
                 body.append(f"        const bool f{ai} = mine && ((({fx}) >> lane) & 1ull);")
                 cond = f"f{ai}"
             kind = a["kind"]
+            val = f"v{ai}_[u]"
             if kind == D.A_HLL:
-                body.append(f"        if ({cond}) hll_update(hll{ai}, slot, {p.hll_p}, {self.ival(a['col'])}, {_lit(a.get('salt', 0))});")
+                fn = "hll_update8" if self.hll_lds and mode == D.M_DENSE_LDS else "hll_update"
+                body.append(f"        if ({cond}) {fn}(hll{ai}, slot, {p.hll_p}, {val}, {_lit(a.get('salt', 0))});")
                 continue
             s = a["slot"]
             op = p.slots[s][0]
-            if kind == D.A_COUNT:
-                val = "1LL"
-            elif kind in (D.A_SUM_F, D.A_MIN_F, D.A_MAX_F):
-                dv = self.expr(a["expr"]) if a.get("expr") else self.dval(a["col"])
-                val = f"__double_as_longlong({dv})" if kind == D.A_SUM_F else f"f2ord({dv})"
-            else:
-                val = self.ival(a["col"])
+            if self.reg:
+                body.append(f"        {{ const int64_t v_ = {val}; const int kk_ = (int)key;")
+                for g in range(G):
+                    r = f"r{g}_{s}"
+                    pg = f"({cond} && kk_ == {g})"
+                    if s in narrow:
+                        body.append(f"          n{g}_{s} += {pg} ? (int32_t)v_ : 0;")
+                    elif op == D.S_SUM_I:
+                        body.append(f"          {r} += {pg} ? v_ : 0LL;")
+                    elif op == D.S_SUM_F:
+                        body.append(f"          {r} += {pg} ? __longlong_as_double(v_) : 0.0;")
+                    elif op == D.S_MIN_I:
+                        body.append(f"          {r} = ({pg} && v_ < {r}) ? v_ : {r};")
+                    else:
+                        body.append(f"          {r} = ({pg} && v_ > {r}) ? v_ : {r};")
+                body.append("        }")
+                continue
             if mode == D.M_DENSE_LDS:
                 tgt = f"acc + (slot * {NS} + {s}) * {NCT} + copy"
             else:
@@ -332,9 +495,12 @@ class _Gen:
         out.append(f'extern "C" __global__ __launch_bounds__({W * 64}) void {name}(const ScanDesc* __restrict__ d) {{')
         out.append("  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];")
         out.append("  const int lane = threadIdx.x & 63;")
-        out.append("  const int wave = threadIdx.x >> 6;")
+        out.append("  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);")
+        for lg in sorted({c.lg for c in self.cols.values()}):
+            out.append(f"  const uint32_t lo{lg} = (uint32_t)lane << {lg};")
         out.append(f"  unsigned char* wb = lds + {lay.cache_off} + wave * {lay.wave_bytes};")
-        out.append(f"  uint64_t* bmw = (uint64_t*)(wb + {U * NP * 256});")
+        stage_bytes = 0 if self.regstage else U * NP * 256 * (2 if self.pipe else 1)
+        out.append(f"  uint64_t* bmw = (uint64_t*)(wb + {stage_bytes});")
         out.append("  uint64_t* acc = (uint64_t*)lds;")
         out.append(f"  const int copy = wave * {lay.ncopy} + (lane & {lay.ncopy - 1});")
         out.append("  uint64_t* gacc = (uint64_t*)d->out_acc;")
@@ -354,6 +520,16 @@ class _Gen:
                 out.append(f"  for (int i = threadIdx.x; i < {lay.hll_bytes // 4}; i += {W * 64}) "
                            f"((uint32_t*)(lds + {lay.hll_off}))[i] = 0u;")
             out.append("  __syncthreads();")
+        if self.reg:
+            for g in range(G):
+                for s in range(NS):
+                    op, init = p.slots[s]
+                    if op == D.S_SUM_F:
+                        out.append(f"  double r{g}_{s} = 0.0;")
+                    else:
+                        out.append(f"  int64_t r{g}_{s} = {_lit(init)};")
+                    if s in narrow:
+                        out.append(f"  int32_t n{g}_{s} = 0;")
         out.append(f"  const int64_t total_waves = (int64_t)gridDim.x * {W};")
         out.append(f"  const int64_t gw = (int64_t)blockIdx.x * {W} + wave;")
         out.append("  const int64_t num_rows = d->num_rows;")
@@ -371,6 +547,11 @@ class _Gen:
         for z, (dim, zlo, zhi) in enumerate(p.zones):
             out.append(f"    if ((int64_t)zmax{z}[kchunk] < {_lit(zlo)} || (int64_t)zmin{z}[kchunk] >= {_lit(zhi)}) continue;")
         out.append(f"    const int64_t cw0 = kchunk * {D.CHUNK_WORDS};")
+        out.append(f"    const int64_t crow0 = kchunk * {D.CHUNK_ROWS};")
+        out.append(f"    const int64_t crows = num_rows - crow0 < {D.CHUNK_ROWS} ? num_rows - crow0 : {D.CHUNK_ROWS};")
+        staged = (fcols if word_filter is not None else []) + (pcols if mode != D.M_MASK else [])
+        for i in staged:
+            out.append(f"    const __amdgpu_buffer_rsrc_t rs{i} = chunk_rsrc(c{i}, crow0, crows, {self.cols[i].lg});")
         out.append("    const int64_t my_r0 = (cw0 + lane) * 64;")
         out.append("    const int64_t lo_off = clo - my_r0, hi_off = chi - my_r0;")
         out.append("    uint64_t pre = range_bits((int)(lo_off < 0 ? 0 : (lo_off > 64 ? 64 : lo_off)),")
@@ -386,41 +567,60 @@ class _Gen:
         if pre:
             out.append(f"    pre &= {pre};")
         out.append("    uint64_t nz = __ballot(pre != 0ull);")
-        out.append("    while (nz) {")
-        out.append(f"      int wl[{U}];")
-        out.append(f"      uint64_t m[{U}];")
-        out.append(f"      int64_t row[{U}];")
-        out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{")
-        out.append("        if (nz) { wl[u] = __builtin_ctzll(nz); nz &= nz - 1ull; m[u] = readlane64(pre, wl[u]); }")
-        out.append("        else { wl[u] = 0; m[u] = 0ull; }")
-        out.append("        row[u] = (cw0 + wl[u]) * 64 + lane;")
-        out.append("      }")
-        if word_filter is not None:
-            if fcols:
-                out.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
-                out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{")
-                for i in fcols:
-                    c = self.cols[i]
-                    out.append(f"        dma<{c.lg}>(c{i}, row[u], wb + (u * {NP} + {c.plane}) * 256);")
-                out.append("      }")
-                out.append('      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
-            out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) m[u] &= {word_filter};")
-        out.append("      uint64_t any = 0;")
-        out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) any |= m[u];")
-        out.append("      if (any == 0) continue;")
-        if mode == D.M_MASK:
-            out.append("      if (lane == 0) {")
-            out.append("        unsigned long long cnt = 0;")
-            out.append(f"#pragma unroll\n        for (int u = 0; u < {U}; ++u) {{")
-            out.append("          if (m[u]) ((uint64_t*)d->out_mask)[cw0 + wl[u]] = m[u];")
-            out.append("          cnt += __popcll(m[u]);")
-            out.append("        }")
-            out.append("        atomicAdd((unsigned long long*)d->out_count, cnt);")
-            out.append("      }")
+        if self.pipe:
+            out.extend(self._pipelined_words(pcols, stage, body))
         else:
-            out.extend(body)
-        out.append("    }")
+            out.append("    while (nz) {")
+            out.append(f"      int wl[{U}];")
+            out.append(f"      uint64_t m[{U}];")
+            out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{")
+            out.append("        if (nz) { wl[u] = __builtin_ctzll(nz); nz &= nz - 1ull; m[u] = readlane64(pre, wl[u]); }")
+            out.append("        else { wl[u] = 0; m[u] = 0ull; }")
+            out.append("      }")
+            if word_filter is not None:
+                if fcols:
+                    if not self.regstage:
+                        out.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
+                    self.stage_words(out, fcols, "wl", "wb")
+                    if not self.regstage:
+                        out.append('      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
+                out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) m[u] &= {word_filter};")
+            out.append("      uint64_t any = 0;")
+            out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) any |= m[u];")
+            out.append("      if (any == 0) continue;")
+            if mode == D.M_MASK:
+                out.append("      if (lane == 0) {")
+                out.append("        unsigned long long cnt = 0;")
+                out.append(f"#pragma unroll\n        for (int u = 0; u < {U}; ++u) {{")
+                out.append("          if (m[u]) ((uint64_t*)d->out_mask)[cw0 + wl[u]] = m[u];")
+                out.append("          cnt += __popcll(m[u]);")
+                out.append("        }")
+                out.append("        atomicAdd((unsigned long long*)d->out_count, cnt);")
+                out.append("      }")
+            else:
+                out.extend(stage + body)
+            out.append("    }")
+        for g in range(G if narrow else 0):
+            for s in sorted(narrow):
+                out.append(f"    r{g}_{s} += n{g}_{s}; n{g}_{s} = 0;")
         out.append("  }")
+        if self.reg:
+            # wave-reduce each register partial; lane 0 stores the wave's copy for the block flush
+            for g in range(G):
+                for s in range(NS):
+                    op = p.slots[s][0]
+                    v = f"r{g}_{s}"
+                    out.append("  {")
+                    if op == D.S_SUM_F:
+                        out.append(f"    double v = {v};")
+                        out.append("    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);")
+                        out.append("    const int64_t b = __double_as_longlong(v);")
+                    else:
+                        out.append(f"    int64_t v = {v};")
+                        out.append(f"    for (int o = 32; o > 0; o >>= 1) v = acc_combine<{op}>(v, __shfl_xor(v, o));")
+                        out.append("    const int64_t b = v;")
+                    out.append(f"    if (lane == 0) acc[({g} * {NS} + {s}) * {NCT} + wave] = (uint64_t)b;")
+                    out.append("  }")
         if mode == D.M_DENSE_LDS:
             out.append("  __syncthreads();")
             out.append(f"  for (int i = threadIdx.x; i < {G * NS}; i += {W * 64}) {{")
@@ -448,7 +648,7 @@ class _Gen:
                         continue
                     out.append(f"  {{ uint32_t* g = (uint32_t*)d->aops[{ai}].hll_regs;")
                     out.append(f"    for (int i = threadIdx.x; i < {G * self.m}; i += {W * 64}) {{")
-                    out.append(f"      const uint32_t v = hll{ai}[i];")
+                    out.append(f"      const uint32_t v = hll{ai}[i];  // byte register")
                     out.append("      if (v > *(volatile uint32_t*)(g + i)) atomicMax(g + i, v);")
                     out.append("    } }")
         out.append("}")
@@ -487,12 +687,15 @@ def compile_source(src: str, name: str) -> int:
 class JitScan:
     """A compiled, specialized scan kernel for one ScanProgram shape."""
 
-    def __init__(self, prog, mode: int, U: int, hll_lds: bool, m: int, narrow4: bool, load: bool = True):
-        self.lay = layout(prog, mode, U, hll_lds, m)
+    def __init__(self, prog, mode: int, U: int, hll_lds: bool, m: int, narrow4: bool, load: bool = True,
+                 reg: Optional[bool] = None, pipe: bool = False, budget: int = 150 * 1024,
+                 regstage: bool = False):
+        self.reg = reg_eligible(prog, mode) if reg is None else reg
+        self.lay = layout(prog, mode, U, hll_lds, m, self.reg, pipe and not regstage, budget, regstage)
         if self.lay.total > 160 * 1024:
             raise ValueError(f"jit layout needs {self.lay.total} B of LDS")
-        g = _Gen(prog, mode, U, hll_lds, narrow4, self.lay, m)
-        tag = hashlib.sha1(repr((mode, U)).encode()).hexdigest()[:6]
+        g = _Gen(prog, mode, U, hll_lds, narrow4, self.lay, m, self.reg)
+        tag = hashlib.sha1(repr((mode, U, self.reg, pipe, self.lay.ncopy, regstage)).encode()).hexdigest()[:6]
         self.name = f"sdo_jit_{tag}"
         self.src = g.source(self.name)
         self.handle = compile_source(self.src, self.name) if load else -1

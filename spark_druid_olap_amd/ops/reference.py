@@ -44,13 +44,33 @@ def clz64(x: torch.Tensor) -> torch.Tensor:
     return n
 
 
+def fmix32(x: torch.Tensor) -> torch.Tensor:
+    """murmur3 finalizer on uint32 values held in int64."""
+    m = 0xFFFFFFFF
+    x = x ^ (x >> 16)
+    x = (x * 0x85EBCA6B) & m
+    x = x ^ (x >> 13)
+    x = (x * 0xC2B2AE35) & m
+    return x ^ (x >> 16)
+
+
 def hll_update_values(vals: torch.Tensor, salt: int, p: int) -> Tuple[torch.Tensor, torch.Tensor]:
-    """(bucket, rho) per value, bit-identical to the kernel's hashing."""
-    h = mix64(vals.to(torch.int64) ^ int(salt))
-    bucket = _lsr(h, 64 - p)
+    """(bucket, rho) per value, bit-identical to ``hll_bucket_rho`` in csrc/sdo_device.h: values in
+    [0, 2^32) use the 32-bit mix, others the 64-bit one."""
+    v = vals.to(torch.int64)
+    salt = int(salt)
+    small = (v >= 0) & (v < (1 << 32))
+    s32 = (salt ^ (salt >> 32)) & 0xFFFFFFFF
+    h32 = fmix32((v & 0xFFFFFFFF) ^ s32)
+    b32 = h32 >> (32 - p)
+    rest32 = ((h32 << p) & 0xFFFFFFFF) | (1 << (p - 1))
+    rho32 = clz64(rest32) - 32 + 1
+    salt64 = salt - (1 << 64) if salt >= (1 << 63) else salt
+    h = mix64(v ^ salt64)
+    b64 = _lsr(h, 64 - p)
     rest = (h << p) | (1 << (p - 1))
-    rho = clz64(rest) + 1
-    return bucket, rho
+    rho64 = clz64(rest) + 1
+    return torch.where(small, b32, b64), torch.where(small, rho32, rho64)
 
 
 def hll_estimate_torch(regs: torch.Tensor, p: int) -> torch.Tensor:

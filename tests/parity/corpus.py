@@ -24,6 +24,29 @@ def build_session(sf=0.01):
     for name, frame in tpch.star_tables(df).items():
         s.register_table(name, frame, schema=tpch.STAR_SCHEMAS[name])
     s.sql(tpch.star_ddl())
+    # SelectQueryTest.scala:37-63: push_project_and_filters variants of the flat and star tables
+    nah = ', nonAggregateQueryHandling "push_project_and_filters"'
+    s.sql(tpch.druid_ddl(table="orderLineItemPartSupplier_select", extra_options=nah,
+                         star_schema='{"factTable" : "orderLineItemPartSupplier_select", "relations" : []}'))
+    s.sql(tpch.star_ddl(table="lineitem_select", extra_options=nah))
+    # DataTypesTest.scala:53-134: the same rows with date / timestamp typed source columns
+    import pandas as pd
+
+    dt = df.copy()
+    dt["o_orderdate"] = pd.to_datetime(dt["o_orderdate"]).dt.date
+    dt["l_commitdate"] = pd.to_datetime(dt["l_commitdate"]).dt.date
+    dt["l_receiptdate"] = pd.to_datetime(dt["l_receiptdate"])
+    typ = {"o_orderdate": "date", "l_commitdate": "date", "l_receiptdate": "timestamp"}
+    schema1 = [(c, typ.get(c, t)) for c, t in tpch.FLAT_SCHEMA]
+    s.register_table("orderLineItemPartSupplierDataTypesBase", dt, schema=schema1)
+    dt2 = dt.copy()
+    dt2["l_shipdate"] = pd.to_datetime(dt2["l_shipdate"])
+    s.register_table("orderLineItemPartSupplierDataTypes2Base", dt2,
+                     schema=[(c, "timestamp" if c == "l_shipdate" else t) for c, t in schema1])
+    for suffix, src in (("datatypes", "orderLineItemPartSupplierDataTypesBase"),
+                        ("datatypes2", "orderLineItemPartSupplierDataTypes2Base")):
+        tn = f"orderLineItemPartSupplier_{suffix}"
+        s.sql(tpch.druid_ddl(table=tn, source=src, star_schema=f'{{"factTable" : "{tn}", "relations" : []}}'))
     if os.path.exists(f"{REF}/zip_codeAll.json.template"):
         for tmpl in ("zip_code.json.template", "zip_codeAll.json.template"):
             s.register_datasource(ingest(f"{REF}/{tmpl}", data_dir=f"{REF}/zipCodes/sample"))

@@ -24,16 +24,20 @@ def main():
     ds = tpch.to_datasource(flat, profile="bench")
     del flat
     eng = Engine()
-    names = [args.query] if args.query != "all" else [n for n, _ in bench_specs()]
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from query_probe import extra_specs
+
+    specs = dict(bench_specs() + extra_specs())
+    names = args.query.split(",") if args.query != "all" else [n for n, _ in bench_specs()]
     for name in names:
-        q = dict(bench_specs())[name]
+        q = specs[name]
         pq = eng.prepare(q, ds)
         _, prog, prep = pq.scans[0]
         pq.run()
         torch.cuda.synchronize()
         for _ in range(args.iters):
             prep._reset()
-            native.scan(prep.desc, prep.grid, DE.BLOCK, prep.lds_total, DE.UNROLL)
+            prep._launch()  # the specialized (JIT) kernel when one was built, else the interpreter
         torch.cuda.synchronize()
         print("done", name, flush=True)
 
