@@ -135,6 +135,10 @@ class Executor:
             elif isinstance(e, A.Alias) and isinstance(e.child, A.Ref) and e.child.dtype == r.dtype:
                 cols[r.rid] = b.cols[e.child.rid]
             else:
+                a = _np_eval(e, b) if b.n <= _NP_FAST_MAX_ROWS else None
+                if a is not None:
+                    cols[r.rid] = pd.Series(a)
+                    continue
                 s = eval_series(e, fr)
                 cols[r.rid] = _conform(s, r.dtype)
         return Batch(refs, cols, b.n)
@@ -205,6 +209,94 @@ class Executor:
 
 
 # ------------------------------------------------------------------------------------------------
+_NP_FAST_MAX_ROWS = 1 << 16
+_INT_T = ("tinyint", "smallint", "int", "bigint")
+
+
+def _np_eval(e: A.Expr, b: Batch) -> Optional[np.ndarray]:
+    """numpy evaluation of the arithmetic projections that sit on top of Druid results (AVG =
+    sum / count, CAST(round(cardinality) AS BIGINT), ...) when every input column is a NULL-free
+    numpy column (floats: NaN is NULL and propagates).  Each pandas nullable-array op costs tens of
+    microseconds of interpreter time -- most of a small query's host latency -- while these numpy
+    ops cost a few.  Returns None for anything else (the general evaluator handles it)."""
+    try:
+        v = _np_rec(e, b)
+    except _NoFast:
+        return None
+    if not isinstance(v, np.ndarray):
+        return None
+    t = base(typeof(e))
+    if t in ("double", "float") and v.dtype.kind == "f":
+        return v
+    if t in _INT_T and v.dtype.kind in "iu":
+        return v.astype(np.int64, copy=False)
+    return None
+
+
+class _NoFast(Exception):
+    pass
+
+
+def _np_rec(e: A.Expr, b: Batch):
+    if isinstance(e, A.Alias):
+        return _np_rec(e.child, b)
+    if isinstance(e, A.Ref):
+        s = b.cols.get(e.rid)
+        if s is None or not isinstance(s.dtype, np.dtype) or s.dtype.kind not in "iuf":
+            raise _NoFast
+        return s.to_numpy()
+    if isinstance(e, A.Lit):
+        if isinstance(e.value, bool) or not isinstance(e.value, (int, float)):
+            raise _NoFast
+        return e.value
+    if isinstance(e, A.Cast):
+        x = _np_rec(e.child, b)
+        to = base(e.to)
+        if to in ("double", "float"):
+            return np.asarray(x, dtype=np.float64) if isinstance(x, np.ndarray) else float(x)
+        if to in _INT_T and isinstance(x, np.ndarray):
+            if x.dtype.kind == "f":
+                if not np.isfinite(x).all():
+                    raise _NoFast
+                return np.trunc(x).astype(np.int64)
+            return x.astype(np.int64, copy=False)
+        raise _NoFast
+    if isinstance(e, A.UnOp) and e.op == "-":
+        return -_np_rec(e.child, b)
+    if isinstance(e, A.BinOp) and e.op in ("+", "-", "*", "/"):
+        l, r = _np_rec(e.l, b), _np_rec(e.r, b)
+        if e.op == "/":
+            lf = np.asarray(l, dtype=np.float64)
+            rf = np.asarray(r, dtype=np.float64)
+            with np.errstate(divide="ignore", invalid="ignore"):
+                out = lf / rf
+            return np.where(rf == 0, np.nan, out)      # x / 0 is NULL in Spark SQL
+        if base(typeof(e)) in _INT_T:
+            if (isinstance(l, np.ndarray) and l.dtype.kind == "f") or (isinstance(r, np.ndarray) and r.dtype.kind == "f"):
+                raise _NoFast
+        elif base(typeof(e)) not in ("double", "float"):
+            raise _NoFast
+        return {"+": np.add, "-": np.subtract, "*": np.multiply}[e.op](l, r)
+    if isinstance(e, A.Call) and e.name in ("round", "bround") and not e.is_agg and e.name == "round":
+        x = _np_rec(e.args[0], b)
+        d = 0
+        if len(e.args) > 1:
+            dv = _np_rec(e.args[1], b)
+            if isinstance(dv, np.ndarray):
+                raise _NoFast
+            d = int(dv)
+        if not isinstance(x, np.ndarray):
+            raise _NoFast
+        if x.dtype.kind in "iu":
+            if d >= 0:
+                return x
+            raise _NoFast
+        from .functions import _half_up_np
+
+        return _half_up_np(x, d)
+    raise _NoFast
+
+
 def _conform(s: pd.Series, t: str) -> pd.Series:
     want = pandas_dtype(t)
     if want == "string" and isinstance(s.dtype, pd.CategoricalDtype):
