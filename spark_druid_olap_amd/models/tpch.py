@@ -582,7 +582,7 @@ def star_tables(df):
 
 
 def star_ddl(datasource: str = "tpch", fact_db: str = "default", dim_db: str = "default",
-             table: str = "lineitem", extra_options: str = "") -> str:
+             table: str = "lineitem", extra_options: str = "", column_mapping: Optional[dict] = None) -> str:
     """Star-schema fact table DDL (``tc/StarSchemaBaseTest.scala:88-101``); ``table`` renames the fact
     table (``SelectQueryTest.scala:51-63`` registers ``lineitem_select`` over the same index)."""
     import json
@@ -593,6 +593,7 @@ def star_ddl(datasource: str = "tpch", fact_db: str = "default", dim_db: str = "
     return (f"CREATE TABLE if not exists {fact_db}.{table} USING org.sparklinedata.druid OPTIONS ("
             f"sourceDataframe \"{fact_db}.lineitembase\", timeDimensionColumn \"l_shipdate\", "
             f"druidDatasource \"{datasource}\", druidHost 'localhost', "
-            f"columnMapping '{json.dumps(STAR_COLUMN_MAPPING)}', numProcessingThreadsPerHistorical '1', "
+            f"columnMapping '{json.dumps(COLUMN_MAPPING if column_mapping is None else column_mapping)}', "
+            f"numProcessingThreadsPerHistorical '1', "
             f"functionalDependencies '{json.dumps(FUNCTIONAL_DEPENDENCIES)}', "
             f"starSchema '{ss}'{extra_options})")

@@ -339,6 +339,10 @@ class DruidRewriter:
             inner = self._filter(pf, e.child)
             if inner is None:
                 raise NotPushable("NOT over a trivially-true predicate")
+            if isinstance(inner, S.JavascriptFilterSpec):
+                # NOT(expr) must exclude the values where expr is NULL (SQL three-valued logic):
+                # evaluate the negated expression itself instead of complementing its TRUE set
+                return self._expr_filter(pf, e)
             return S.NotFilterSpec(inner)
         if isinstance(e, A.IsNull) and isinstance(e.child, A.Ref):
             c = pf.cols.get(e.child.rid)

@@ -727,16 +727,31 @@ def _positive(args, ts, n):
 def _pmod(args, ts, n):
     a, b = args
     rt = wider(ts[0], ts[1])
+    # Spark's Pmod: r = a % n with Java (truncated, sign-of-dividend) remainder; r < 0 -> (r + n) % n.
+    # A negative divisor therefore keeps non-negative remainders: pmod(7, -5) = 2.
     if not is_vec(a) and not is_vec(b):
         if a is None or b is None or b == 0:
             return None
-        r = a % b
-        return r
+        if isinstance(a, int) and isinstance(b, int):
+            r = int(np.fmod(a, b))
+            return int(np.fmod(r + b, b)) if r < 0 else r
+        r = math.fmod(a, b)
+        return math.fmod(r + b, b) if r < 0 else r
     av = broadcast(a, n, ts[0])
     bv = broadcast(b, n, ts[1])
-    bv = bv.mask(bv == 0, pd.NA)
-    r = ((av % bv) + bv) % bv
-    return r.astype(pandas_dtype(rt))
+    bad = (bv.isna() | (bv == 0)).to_numpy(dtype=bool, na_value=True) | av.isna().to_numpy(dtype=bool)
+    if base(rt) in INTEGRAL:
+        x = av.astype("Int64").to_numpy(dtype=np.int64, na_value=0)
+        y = bv.astype("Int64").to_numpy(dtype=np.int64, na_value=1)
+        y = np.where(y == 0, 1, y)
+    else:
+        x = av.astype("Float64").to_numpy(dtype=np.float64, na_value=0.0)
+        y = bv.astype("Float64").to_numpy(dtype=np.float64, na_value=1.0)
+        y = np.where(y == 0, 1.0, y)
+    r = np.fmod(x, y)
+    r = np.where(r < 0, np.fmod(r + y, y), r)
+    out = pd.Series(r).astype(pandas_dtype(rt))
+    return out.mask(bad, pd.NA)
 
 
 @_reg("round bround", lambda ts: ts[0] if base(ts[0]) in INTEGRAL else "double")
@@ -1268,6 +1283,59 @@ def _md5(args, ts, n):
 
     return _map_scalar(lambda s: hashlib.md5(str(s).encode()).hexdigest(), "string")(
         [_str(args[0], ts[0], n)], ["string"], n)
+
+
+def _hex_of(v):
+    if isinstance(v, (bytes, bytearray)):
+        return bytes(v).hex().upper()
+    if isinstance(v, bool):
+        v = int(v)
+    if isinstance(v, (int, np.integer)):
+        return format(int(v) & 0xFFFFFFFFFFFFFFFF, "X")
+    if isinstance(v, float):
+        return format(int(v) & 0xFFFFFFFFFFFFFFFF, "X")
+    return str(v).encode("utf-8").hex().upper()
+
+
+@_reg("hex", _const("string"))
+def _hex(args, ts, n):
+    return _map_scalar(_hex_of, "string")(args, ts, n)
+
+
+def _unhex_of(s):
+    s = str(s)
+    if len(s) % 2:
+        s = "0" + s
+    try:
+        return bytes.fromhex(s)
+    except ValueError:
+        return None
+
+
+@_reg("unhex", _const("binary"))
+def _unhex(args, ts, n):
+    return _map_scalar(_unhex_of, "binary")(args, ts, n)
+
+
+@_reg("base64", _const("string"))
+def _base64(args, ts, n):
+    import base64
+
+    return _map_scalar(lambda v: base64.b64encode(v if isinstance(v, (bytes, bytearray)) else str(v).encode())
+                       .decode(), "string")(args, ts, n)
+
+
+@_reg("unbase64", _const("binary"))
+def _unbase64(args, ts, n):
+    import base64
+    import binascii
+
+    def f(v):
+        try:
+            return base64.b64decode(str(v))
+        except (binascii.Error, ValueError):
+            return None
+    return _map_scalar(f, "binary")(args, ts, n)
 
 
 def function_names() -> List[str]:

@@ -27,6 +27,14 @@ def optimize(plan: P.Plan, conf=None) -> P.Plan:
     p = p.transform_up(_sum_of_literal)
     if not approx:
         p = p.transform_up(_distinct_rewrite)
+    p = _push_down_all(p)
+    q = p.transform_up(_push_gb)
+    if q is not p:
+        p = _push_down_all(q)
+    return p
+
+
+def _push_down_all(p: P.Plan) -> P.Plan:
     for _ in range(64):
         q = _push_down(p)
         if q is p:
@@ -140,6 +148,89 @@ def _distinct_rewrite(p: P.Plan):
 
 
 # ------------------------------------------------------------------------------------------------
+def _max_card_one(p: P.Plan) -> bool:
+    """At most one row: a global (no GROUP BY) aggregate under filters / projections / LIMIT 1
+    (``PlanUtil.maxCardinalityIsOne``, ``asql/util/PlanUtil.scala``)."""
+    if isinstance(p, P.Aggregate):
+        return not p.groups and p.grouping_sets is None
+    if isinstance(p, (P.Filter, P.Project, P.Sort)):
+        return _max_card_one(p.child)
+    if isinstance(p, P.Limit):
+        return p.n <= 1 or _max_card_one(p.child)
+    return False
+
+
+def _has_aggregate(p: P.Plan) -> bool:
+    return any(isinstance(x, P.Aggregate) for x in p.walk())
+
+
+def _push_gb(p: P.Plan):
+    """PushGB (``asql/planner/logical/DruidLogicalOptimizer.scala:60-243``): an Aggregate over a
+    cross product whose other side has at most one row (typically a scalar aggregate subquery)
+    aggregates the big side first and joins the single row afterwards:
+
+        Aggregate(g_big, g_one, aggs(big)) (Join cross (big, one))
+          -> Project(..., g_one re-evaluated) (Join cross (Aggregate(g_big, aggs)(big), one))
+
+    which turns the big side into a pushable Druid GroupBy (the one-row side is its own query)."""
+    if not isinstance(p, P.Aggregate) or p.grouping_sets is not None or p.gid is not None:
+        return None
+    child = p.child
+    subst: Dict[int, A.Expr] = {}
+    if isinstance(child, P.Project) and isinstance(child.child, P.Join):
+        if not all(_pushable(e.child) for e in child.exprs if isinstance(e, A.Alias)) or \
+                any(_has_agg_or_window(e) for e in child.exprs):
+            return None
+        subst = {e.rid: e.child for e in child.exprs if isinstance(e, A.Alias)}
+        j = child.child
+    elif isinstance(child, P.Join):
+        j = child
+    else:
+        return None
+    if j.kind not in ("inner", "cross") or j.cond is not None:
+        return None
+
+    def inline(e: A.Expr) -> A.Expr:
+        return e.transform(lambda x: subst[x.rid] if isinstance(x, A.Ref) and x.rid in subst else None)
+
+    groups = [inline(g.child) for g in p.groups]
+    aggs = [inline(a.child) for a in p.aggs]
+    l_big = not _has_aggregate(j.left) and _max_card_one(j.right)
+    r_big = not _has_aggregate(j.right) and _max_card_one(j.left)
+    if l_big == r_big:
+        return None
+    big, one = (j.left, j.right) if l_big else (j.right, j.left)
+    big_ids = {r.rid for r in big.output}
+    one_ids = {r.rid for r in one.output}
+    if not all(is_deterministic(e) for e in groups + aggs):
+        return None
+    if any(not (_refs_of(a) <= big_ids) for a in aggs):
+        return None
+    big_groups = []
+    for gi, g in enumerate(groups):
+        rs = _refs_of(g)
+        if rs and rs <= one_ids:
+            continue
+        if not (rs <= big_ids):
+            return None
+        big_groups.append(gi)
+    if not big_groups:
+        return None
+    new_groups = [A.Alias(groups[gi], p.groups[gi].name) for gi in big_groups]
+    new_aggs = [A.Alias(a, p.aggs[i].name) for i, a in enumerate(aggs)]
+    inner = P.Aggregate(new_groups, new_aggs, big)
+    io = inner.output
+    nj = P.Join("cross", inner, one, None) if l_big else P.Join("cross", one, inner, None)
+    exprs: List[A.Expr] = []
+    gpos = {gi: k for k, gi in enumerate(big_groups)}
+    for gi, g in enumerate(p.groups):
+        src = io[gpos[gi]] if gi in gpos else groups[gi]
+        exprs.append(A.Alias(src, g.name, g.rid))
+    for i, a in enumerate(p.aggs):
+        exprs.append(A.Alias(io[len(new_groups) + i], a.name, a.rid))
+    return P.Project(exprs, nj)
+
+
 def _refs_of(e: A.Expr) -> Set[int]:
     return {r.rid for r in e.refs()}
 

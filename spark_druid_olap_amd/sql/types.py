@@ -193,6 +193,8 @@ def format_value(v: Any, t: str) -> Optional[str]:
         return s
     if bt == "boolean":
         return "true" if v else "false"
+    if isinstance(v, (bytes, bytearray)):
+        return bytes(v).decode("utf-8", errors="replace")
     if isinstance(v, float):
         if v == int(v) and abs(v) < 1e7:
             return f"{v:.1f}"
@@ -306,6 +308,9 @@ def cast_vec(x, frm: str, to: str, n: int):
         return x.dt.strftime(fmt).astype("string")
     if bt in INTEGRAL and base(frm) == "boolean":
         return x.astype("Int64")
+    if bt == "string" and base(frm) == "binary":
+        return pd.Series([None if v is None or v is pd.NA else format_value(v, "binary") for v in x],
+                         dtype="string")
     return to_series(x, to)
 
 

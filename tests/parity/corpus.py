@@ -79,7 +79,10 @@ def norm_rows(rows):
                 v = str(v)[:19]
             t.append(v)
         out.append(tuple(t))
-    return sorted(out, key=lambda r: tuple((x is None, str(x)) for x in r))
+    # exact cells order first, floats numerically after: a 1-decimal rounding difference must not
+    # reorder otherwise-equal result sets
+    return sorted(out, key=lambda r: (tuple((x is None, str(x)) for x in r if not isinstance(x, float)),
+                                      tuple(-1e300 if x is None else x for x in r if isinstance(x, float))))
 
 
 def rows_equal(a, b):
