@@ -285,6 +285,7 @@ class ScanProgram:
     agg_filters: List[Any] = field(default_factory=list) # per aop bexpr or None
     keepalive: List[torch.Tensor] = field(default_factory=list)
     thetas: List[Tuple[str, str, int]] = field(default_factory=list)  # (name, column, size)
+    luts: Dict[str, torch.Tensor] = field(default_factory=dict)       # dim -> f64 value per dictionary id
 
     def col(self, name: str) -> int:
         """Absolute descriptor column index of `name` in the current section."""
@@ -826,6 +827,16 @@ class Lowerer:
                 d["slot"] = slot(D.S_SUM_I, 0, d)
                 prog.aggs.append(AggOut(a.name, "count", d["slot"], out_type="long"))
                 return
+            if fname == TIME and t in ("longMin", "longMax"):
+                # longMin/longMax over __time (epoch ms): through the f64 expression path (exact
+                # below 2^53 ms)
+                mn = t == "longMin"
+                d = aop(D.A_MIN_F if mn else D.A_MAX_F, -1, [(D.E_COL, prog.col(TIME), float(ds.time_unit_ms))])
+                init = _f2ord(math.inf) if mn else _f2ord(-math.inf)
+                d["slot"] = slot(D.S_MIN_I if mn else D.S_MAX_I, init, d)
+                prog.aggs.append(AggOut(a.name, "min_f" if mn else "max_f", d["slot"], out_type="long",
+                                        combine="min" if mn else "max"))
+                return
             if fname not in ds.metrics:
                 raise LoweringError(f"aggregation over unknown metric {fname!r}")
             m = ds.metrics[fname]
@@ -909,7 +920,20 @@ class Lowerer:
                 return 1
             if k == "col":
                 name = mapping.get(n[1], n[1])
-                if name not in self.ds.metrics and name not in self.ds.dims:
+                if name == TIME:
+                    # __time in epoch ms (stored in time units)
+                    out.append((D.E_COL, prog.col(TIME), float(self.ds.time_unit_ms)))
+                    return 1
+                if name in self.ds.dims:
+                    # a dimension in a row expression: the value is its dictionary entry read as a
+                    # number (javascript coercion: numeric strings -> numbers, ISO dates -> epoch
+                    # ms, anything else NaN), one f64 table lookup per row (E_LUT)
+                    lut = dim_numeric_lut(self.ds, name)
+                    prog.luts[name] = lut
+                    prog.keepalive.append(lut)
+                    out.append((D.E_LUT, prog.col(name), _ptr_as_double(lut.data_ptr())))
+                    return 1
+                if name not in self.ds.metrics:
                     raise LoweringError(f"unknown column {name!r} in expression")
                 m = self.ds.metrics.get(name)
                 sc = (10.0 ** -m.scale) if (m is not None and m.kind == "decimal" and m.scale) else 0.0
@@ -1034,6 +1058,49 @@ class Lowerer:
         self.emit_main_filter(prog, bexpr)
         self.pick_zones(prog, bexpr)
         return prog
+
+
+def _ptr_as_double(ptr: int) -> float:
+    import struct
+
+    return struct.unpack("<d", struct.pack("<Q", int(ptr)))[0]
+
+
+def _numeric_value(v) -> float:
+    if v is None:
+        return math.nan
+    if isinstance(v, (bool, np.bool_)):
+        return float(v)
+    if isinstance(v, (int, float, np.integer, np.floating)):
+        return float(v)
+    s = str(v).strip()
+    try:
+        return float(s)
+    except ValueError:
+        pass
+    if len(s) >= 10 and s[4:5] == "-" and s[7:8] == "-":
+        try:
+            return float(parse_iso_ms(s))
+        except Exception:  # noqa: BLE001
+            return math.nan
+    return math.nan
+
+
+def dim_numeric_lut(ds: DataSource, dim: str) -> torch.Tensor:
+    """f64 value of every dictionary entry of `dim` (cached on the column)."""
+    dc = ds.dims[dim]
+    lut = getattr(dc, "_numlut", None)
+    if lut is not None:
+        return lut
+    dic = dc.dictionary
+    if dic.vtype != "string" and (dic.lazy or not dic.has_null):
+        vals = np.asarray(dic.values, dtype=np.float64) if not dic.lazy else \
+            dic.decode(np.arange(len(dic))).astype(np.float64)
+    else:
+        vals = np.asarray(dic.map_values(_numeric_value), dtype=np.float64)
+    lut = torch.from_numpy(np.ascontiguousarray(vals)).to(dc.ids.device)
+    dc._numlut = lut  # type: ignore[attr-defined]
+    return lut
 
 
 def implied_ids(x, dim: str) -> Optional[np.ndarray]:

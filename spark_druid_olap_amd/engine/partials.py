@@ -182,7 +182,11 @@ def finalize(prog, parts: Partials) -> Dict[str, np.ndarray]:
             col = acc_h[:, a.slot]
             cols[a.name] = col.view(np.float64) if col.flags.c_contiguous else col.copy().view(np.float64)
         elif a.kind in ("min_f", "max_f"):
-            cols[a.name] = ord2f(acc_h[:, a.slot]).copy()
+            v = ord2f(acc_h[:, a.slot]).copy()
+            if a.out_type == "long":
+                # longMin/longMax over __time: empty groups keep the +-inf identity
+                v = np.where(np.isfinite(v), v, 0).astype(np.int64)
+            cols[a.name] = v
         elif a.kind == "hll":
             cols[a.name] = hll_estimates(hll_d[a.hll_index], prog.hll_p) if len(acc_h) else np.zeros(0)
         elif a.kind == "theta":

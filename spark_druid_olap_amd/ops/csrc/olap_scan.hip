@@ -381,9 +381,12 @@ __device__ __forceinline__ double eval_expr(const ScanDesc* __restrict__ d, int 
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   for (int i = off; i < off + len; ++i) {
     const EOp e = d->eops[i];
-    if (e.op == E_COL || e.op == E_CONST) {
+    if (e.op == E_COL || e.op == E_CONST || e.op == E_LUT) {
       double v = e.c;
-      if (e.op == E_COL) {
+      if (e.op == E_LUT) {
+        const double* lut = (const double*)__double_as_longlong(e.c);
+        v = lut[col_int<U>(d, wb, e.col, u, lane)];
+      } else if (e.op == E_COL) {
         v = col_dbl<U>(d, wb, e.col, u, lane);
         if (e.c != 0.0) v *= e.c;  // decimal scale
       }

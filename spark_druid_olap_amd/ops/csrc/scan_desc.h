@@ -118,7 +118,8 @@ enum EOpCode : int32_t {
   E_COL = 0, E_CONST = 1, E_ADD = 2, E_SUB = 3, E_MUL = 4, E_DIV = 5, E_NEG = 6, E_ABS = 7,
   E_MIN = 8, E_MAX = 9,
   // unary math (floor ceil sqrt ln exp) and binary mod / pmod / pow
-  E_FLOOR = 10, E_CEIL = 11, E_SQRT = 12, E_LOG = 13, E_EXP = 14, E_MOD = 15, E_PMOD = 16, E_POW = 17
+  E_FLOOR = 10, E_CEIL = 11, E_SQRT = 12, E_LOG = 13, E_EXP = 14, E_MOD = 15, E_PMOD = 16, E_POW = 17,
+  E_LUT = 18  // push lut[id]: f64 dictionary-domain value of a dimension (pointer bits in c)
 };
 struct EOp {
   int32_t op;

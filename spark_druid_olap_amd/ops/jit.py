@@ -261,10 +261,15 @@ class _Gen:
         return st[-1] if st else "(~0ull)"
 
     # ---------------------------------------------------------------- expression VM -> C++
-    def expr(self, eops) -> str:
+    def expr(self, eops, off: int = 0) -> str:
         st: List[str] = []
-        for op, col, c in eops:
-            if op == D.E_COL:
+        for j, (op, col, c) in enumerate(eops):
+            if op == D.E_LUT:
+                # dictionary-domain value table: pointer read from the descriptor, so the JIT
+                # source (and its cache key) does not depend on the allocation
+                st.append(f"(((const double*)__double_as_longlong(d->eops[{off + j}].c))"
+                          f"[{self.ival(col)}])")
+            elif op == D.E_COL:
                 v = self.dval(col)
                 st.append(f"({v} * {_dlit(c)})" if c != 0.0 else f"({v})")
             elif op == D.E_CONST:
@@ -436,7 +441,7 @@ class _Gen:
             elif kind == D.A_COUNT:
                 val = "1LL"
             elif kind in (D.A_SUM_F, D.A_MIN_F, D.A_MAX_F):
-                dv = self.expr(a["expr"]) if a.get("expr") else self.dval(a["col"])
+                dv = self.expr(a["expr"], a.get("expr_off", 0)) if a.get("expr") else self.dval(a["col"])
                 val = f"__double_as_longlong({dv})" if kind == D.A_SUM_F else f"f2ord({dv})"
             else:
                 val = self.ival(a["col"])

@@ -221,7 +221,10 @@ def compute_keys(prog, rows: torch.Tensor) -> torch.Tensor:
 def _expr_values(prog, eops, rows: torch.Tensor) -> torch.Tensor:
     st: List[torch.Tensor] = []
     for op, col, c in eops:
-        if op == D.E_COL:
+        if op == D.E_LUT:
+            ids = _col(prog, prog.colname(col))[rows].to(torch.int64)
+            st.append(prog.luts[prog.colname(col)].to(rows.device)[ids])
+        elif op == D.E_COL:
             v = _col(prog, prog.colname(col))[rows].to(torch.float64)
             st.append(v * c if c != 0.0 else v)
         elif op == D.E_CONST:

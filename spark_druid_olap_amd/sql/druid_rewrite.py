@@ -71,6 +71,13 @@ class PF:
         return e.transform(f)
 
 
+def _numeric_dimension(c) -> bool:
+    """A dimension whose SQL type is numeric: row expressions read it through its dictionary
+    (engine E_LUT: one f64 per dictionary entry)."""
+    return c.kind == "dimension" and not c.is_time and \
+        base(c.sql_type) in ("tinyint", "smallint", "int", "integer", "bigint", "float", "double", "decimal")
+
+
 def _short(n: str) -> str:
     return n.split(".")[-1].lower()
 
@@ -545,11 +552,12 @@ class DruidRewriter:
                 raise NotPushable(f"non-deterministic aggregate {call.sql()}")
             parts, combine = self._agg_spec(pf, call, names)
             prefs = []
-            for spec_, t in parts:
+            for part in parts:
+                spec_, t = part[0], part[1]
                 aggs.append(spec_)
                 r = A.Ref(A.new_id(), spec_.name, t)
                 drefs.append(r)
-                columns.append((spec_.name, t, "value"))
+                columns.append((spec_.name, t, part[2] if len(part) > 2 else "value"))
                 prefs.append(r)
             out_t = outs[len(agg.groups) + j].dtype
             ex = combine(prefs)
@@ -699,6 +707,10 @@ class DruidRewriter:
                 raise NotPushable(f"{n}(DISTINCT)")
             x = call.args[0]
             kind = "sum" if n in ("avg", "mean") else n
+            if kind in ("min", "max"):
+                tv = self._time_valued_agg(pf, kind, x, names)
+                if tv is not None:
+                    return [tv], lambda rs: rs[0]
             spec_, t = self._numeric_agg(pf, kind, x, names)
             if n in ("avg", "mean"):
                 cnt, ct = count_spec()
@@ -706,6 +718,34 @@ class DruidRewriter:
                     lambda rs: A.BinOp("/", A.Cast(rs[0], "double"), rs[1])
             return [(spec_, t)], lambda rs: rs[0]
         raise NotPushable(f"aggregate {n} is not pushable")
+
+    def _time_valued_agg(self, pf: PF, kind: str, x: A.Expr, names: "_Names"):
+        """MIN/MAX of a timestamp/date-valued column: the time column (``longMin``/``longMax`` over
+        ``__time``) or an ISO-date string dimension cast to a timestamp/date (javascript aggregator
+        over the dimension: its dictionary entries as epoch ms).  The Druid output is epoch ms,
+        converted back like a time column (kind "time")."""
+        e, casted = x, False
+        while True:
+            if isinstance(e, A.Cast) and e.to in ("timestamp", "date"):
+                e, casted = e.child, True
+            elif isinstance(e, A.Call) and e.name in ("datetime", "to_date", "to_timestamp") and len(e.args) == 1:
+                e, casted = e.args[0], True
+            else:
+                break
+        if not isinstance(e, A.Ref):
+            return None
+        c = pf.cols.get(e.rid)
+        if c is None:
+            return None
+        op = "Min" if kind == "min" else "Max"
+        if c.is_time and (casted or base(typeof(e)) in ("date", "timestamp")):
+            return S.FunctionAggregationSpec("long" + op, names.agg(), "__time"), "timestamp", "time"
+        if casted and c.kind == "dimension" and base(c.sql_type) == "string" and \
+                _iso_date_dictionary(pf.table.info.datasource, c.druid_column):
+            p = _js_ident(c.druid_column)
+            agg, comb, reset = js_aggregator(kind, A.Ref(e.rid, p, "double"), {e.rid: p}, [p])
+            return S.JavascriptAggregationSpec(names.agg(), [c.druid_column], agg, comb, reset), "timestamp", "time"
+        return None
 
     def _numeric_agg(self, pf: PF, kind: str, x: A.Expr, names: "_Names"):
         if isinstance(x, A.Cast) and (x.to in ("double", "float") or x.to.startswith("decimal")):
@@ -718,14 +758,15 @@ class DruidRewriter:
                 prefix = "long" if integral else "double"
                 op = {"sum": "Sum", "min": "Min", "max": "Max"}[kind]
                 return S.FunctionAggregationSpec(prefix + op, nm, c.druid_column), ("bigint" if integral else "double")
-            raise NotPushable(f"{kind} over non-metric column {c.column}")
+            if not _numeric_dimension(c):
+                raise NotPushable(f"{kind} over non-metric column {c.column}")
         refs = {r.rid: r for r in x.refs()}
         if not refs:
             raise NotPushable("aggregate of a constant")
         cols = []
         for r in refs.values():
             c = self._column(pf, r)
-            if not c.is_metric:
+            if not c.is_metric and not _numeric_dimension(c):
                 raise NotPushable(f"aggregate expression over non-metric {c.column}")
             cols.append((r, c))
         if not vm_compatible(x):

@@ -321,6 +321,8 @@ def druid_value_series(col, sqlt: str, kind: str, n: int) -> pd.Series:
     if kind == "time":
         if arr.dtype.kind in "iu":
             ts = pd.Series(pd.to_datetime(arr.astype(np.int64), unit="ms"))
+        elif arr.dtype.kind == "f":  # epoch ms from a f64 aggregator (NaN / inf = NULL)
+            ts = pd.Series(pd.to_datetime(np.where(np.isfinite(arr), arr, np.nan), unit="ms"))
         else:
             ts = pd.Series(pd.to_datetime(pd.Series(arr).astype(str).str.replace("Z", "", regex=False)))
         if base(sqlt) in ("date", "timestamp"):

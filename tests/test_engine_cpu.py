@@ -178,3 +178,32 @@ def test_reference_json_roundtrip_and_executes(path, ds_small):
     assert strip(q.to_json()) == strip(d)
     r = run(q, ds_small)
     assert r.num_rows >= 1
+
+
+def test_dimension_lut_aggregators(ds_small, df_small):
+    """Dimensions in row expressions read their dictionary entries as numbers (E_LUT);
+    longMin/longMax over __time."""
+    import numpy as np
+
+    from spark_druid_olap_amd.engine.executor import Engine
+    from spark_druid_olap_amd.query import spec as S
+
+    aggs = [S.JavascriptAggregationSpec("s_ln", ["l_linenumber"], "function(current, a) { return current + a; }",
+                                        "function(a,b){return a+b;}", "function(){return 0;}"),
+            S.JavascriptAggregationSpec("mn_od", ["o_orderdate"], "function(current, a) { return Math.min(current, a); }",
+                                        "function(a,b){return Math.min(a,b);}", "function(){return Infinity;}"),
+            S.FunctionAggregationSpec("longMin", "t0", "__time"),
+            S.FunctionAggregationSpec("longMax", "t1", "__time")]
+    q = S.TimeSeriesQuerySpec("tpch", ["1992-01-01/1999-01-01"], aggregations=aggs)
+    r = Engine(use_native=False).execute(q, ds_small)
+    assert int(r.data["s_ln"][0]) == int(df_small["l_linenumber"].sum())
+    od = pd_ms(df_small["o_orderdate"].min())
+    assert int(r.data["mn_od"][0]) == od
+    assert int(r.data["t0"][0]) == pd_ms(df_small["l_shipdate"].min())
+    assert int(r.data["t1"][0]) == pd_ms(df_small["l_shipdate"].max())
+
+
+def pd_ms(s):
+    import pandas as pd
+
+    return int(pd.Timestamp(s).value // 1_000_000)

@@ -162,3 +162,26 @@ def test_hll_estimate_kernel_vs_torch():
     want = hll_estimate_torch(regs, 11).numpy()
     got = hll_estimates(regs.cuda(), 11)
     np.testing.assert_allclose(got, want, rtol=1e-5)
+
+
+def test_dimension_lut_and_time_minmax(gpu_ds):
+    """E_LUT: dimensions inside javascript aggregators read through a per-dictionary f64 table;
+    longMin/longMax over __time (the reference's MIN/MAX(CAST(l_shipdate AS TIMESTAMP)))."""
+    aggs = [S.JavascriptAggregationSpec("mx_ln", ["l_linenumber"],
+                                        "function(current, a) { return Math.max(current, a); }",
+                                        "function(a,b){return Math.max(a,b);}", "function(){return -Infinity;}"),
+            S.JavascriptAggregationSpec("rev_ln", ["l_linenumber", "l_extendedprice"],
+                                        "function(current, a, b) { return current + a * b; }",
+                                        "function(a,b){return a+b;}", "function(){return 0;}"),
+            S.JavascriptAggregationSpec("mn_od", ["o_orderdate"],
+                                        "function(current, a) { return Math.min(current, a); }",
+                                        "function(a,b){return Math.min(a,b);}", "function(){return Infinity;}"),
+            S.FunctionAggregationSpec("longMin", "t0", "__time"),
+            S.FunctionAggregationSpec("longMax", "t1", "__time")]
+    q = S.GroupByQuerySpec("tpch", [S.DefaultDimensionSpec("l_returnflag")], aggregations=aggs,
+                           intervals=["1993-01-01/1997-01-01"])
+    nat = Engine(use_native=True).execute(q, gpu_ds)
+    ref = Engine(use_native=False).execute(q, gpu_ds)
+    assert nat.num_rows == 3
+    assert_same(nat, ref, rtol=1e-9)
+    assert (nat.data["mx_ln"] == 7).all()
