@@ -17,6 +17,7 @@ import requests
 from requests.adapters import HTTPAdapter
 
 from ..query import spec as S
+from . import smile
 from ..utils.errors import DruidDataSourceException
 from ..utils.retry import exec_with_backoff, retry_until
 
@@ -43,18 +44,26 @@ class DruidClient:
                  max_connections: int = 100, max_per_route: int = 20):
         self.base = f"http://{host}:{port}"
         self.timeout = timeout_s
-        self.use_smile = use_smile  # accepted for option parity; requests are JSON
+        self.use_smile = use_smile  # Smile request bodies + responses (DruidClient.scala:183-189, 244-251)
         self.http = _pool(max_connections, max_per_route)
 
     def _check(self, r: requests.Response):
         if r.status_code >= 300:
-            raise DruidDataSourceException(f"{r.request.method} {r.url} -> {r.status_code}: {r.text[:500]}")
-        return r.json() if r.content else None
+            body = r.content
+            if smile.is_smile(body):
+                body = json.dumps(smile.loads(body)).encode()
+            raise DruidDataSourceException(f"{r.request.method} {r.url} -> {r.status_code}: {body[:500]!r}")
+        if not r.content:
+            return None
+        return smile.decode_body(r.content, r.headers.get("Content-Type"))
 
     def post(self, path: str, obj: Any):
+        if self.use_smile:
+            data, hdr = smile.dumps(obj), {"Content-Type": smile.MIME, "Accept": smile.MIME}
+        else:
+            data, hdr = json.dumps(obj), {"Content-Type": "application/json"}
         try:
-            r = self.http.post(self.base + path, data=json.dumps(obj), headers={"Content-Type": "application/json"},
-                               timeout=self.timeout)
+            r = self.http.post(self.base + path, data=data, headers=hdr, timeout=self.timeout)
         except requests.RequestException as e:
             raise DruidDataSourceException(str(e)) from e
         return self._check(r)

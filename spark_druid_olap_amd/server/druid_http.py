@@ -16,7 +16,8 @@ the reference itself) can use the GPUs as its "Druid cluster":
   GET    /status
 
 ``timeBoundary`` and ``segmentMetadata`` queries are answered from the catalog (K19 in SURVEY §2.3).
-Smile-encoded bodies are rejected with 415 (``useSmile`` is a client option; JSON is always accepted).
+Request bodies may be JSON or Smile (``client/smile.py``, the reference's ``useSmile`` wire format);
+a Smile request (or ``Accept: application/x-jackson-smile``) gets a Smile response.
 """
 from __future__ import annotations
 
@@ -31,6 +32,7 @@ from urllib.parse import parse_qs, urlparse
 
 import numpy as np
 
+from ..client import smile
 from ..query import spec as S
 from ..query.intervals import fmt_iso
 
@@ -238,8 +240,12 @@ class DruidHTTPServer:
                 n = int(self.headers.get("Content-Length") or 0)
                 body = self.rfile.read(n) if n else None
                 ctype = self.headers.get("Content-Type", "application/json")
+                self._smile = "smile" in ctype or "smile" in (self.headers.get("Accept") or "")
                 if body and "smile" in ctype:
-                    return self._send(415, {"error": "Smile encoding is not supported; send application/json"})
+                    try:
+                        body = json.dumps(smile.loads(body), default=_py).encode()
+                    except smile.SmileError as e:
+                        return self._send(400, {"error": "bad Smile body", "errorMessage": str(e)})
                 try:
                     code, obj = app.handle(method, u.path, parse_qs(u.query, keep_blank_values=True), body)
                 except KeyError as e:
@@ -250,9 +256,12 @@ class DruidHTTPServer:
                 self._send(code, obj)
 
             def _send(self, code, obj):
-                data = json.dumps(obj, default=_py).encode()
+                if getattr(self, "_smile", False):
+                    data, ct = smile.dumps(json.loads(json.dumps(obj, default=_py))), smile.MIME
+                else:
+                    data, ct = json.dumps(obj, default=_py).encode(), "application/json"
                 self.send_response(code)
-                self.send_header("Content-Type", "application/json")
+                self.send_header("Content-Type", ct)
                 self.send_header("Content-Length", str(len(data)))
                 self.end_headers()
                 self.wfile.write(data)
