@@ -218,11 +218,33 @@ class DruidCluster:
         self.datasources: Dict[str, Any] = {}
         self.generation = 0
         self._lock = threading.Lock()
+        self.discovery = None
+        self.server_name = "gpu:0"
+
+    def attach_discovery(self, disc, rank: int = 0, server_info: Optional[dict] = None) -> None:
+        """Announce this rank as a historical, announce its segments, and clear the metadata cache
+        whenever any server or segment comes or goes (CuratorConnection.scala:77-133)."""
+        if self.discovery is disc:
+            return
+        self.discovery = disc
+        self.server_name = f"gpu:{rank}"
+        disc.announce_server(self.server_name, server_info or {"type": "historical", "tier": "_default_tier",
+                                                               "priority": 0, "rank": rank})
+        for name, ds in list(self.datasources.items()):
+            self._announce(name, ds)
+        disc.watch_membership(lambda ev, path: self.clear_cache())
+
+    def _announce(self, name: str, ds) -> None:
+        if self.discovery is None:
+            return
+        for s in getattr(ds, "segments", []) or []:
+            self.discovery.announce_segment(self.server_name, s.identifier, {"dataSource": name})
 
     def register(self, ds, name: Optional[str] = None) -> None:
         with self._lock:
             self.datasources[name or ds.name] = ds
             self.generation += 1
+        self._announce(name or ds.name, ds)
 
     def get(self, name: str):
         ds = self.datasources.get(name)

@@ -137,3 +137,20 @@ class DruidOverlordClient(DruidClient):
         if st.get("status") != "SUCCESS":
             raise DruidDataSourceException(f"task {task_id} failed: {st}")
         return st
+
+
+def discover_clients(druid_host: str = "localhost", druid_path: str = "/druid", qualify_names: bool = False,
+                     use_smile: bool = False):
+    """(broker, coordinator, overlord) clients located through service discovery, the way the
+    reference finds them through ZooKeeper (CuratorConnection.scala:203-209)."""
+    from .discovery import Discovery, registry_for
+
+    d = Discovery(registry_for(druid_host), druid_path, qualify_names)
+    out = []
+    for svc, cls in (("broker", DruidQueryServerClient), ("coordinator", DruidCoordinatorClient),
+                     ("overlord", DruidOverlordClient)):
+        hp = d.get_service(svc)
+        if hp is None:
+            raise DruidDataSourceException(f"no {svc} registered under {druid_path}/discovery at {druid_host}")
+        out.append(cls(hp[0], hp[1], use_smile=use_smile) if cls is DruidQueryServerClient else cls(hp[0], hp[1]))
+    return tuple(out)

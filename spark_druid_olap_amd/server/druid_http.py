@@ -279,9 +279,19 @@ class DruidHTTPServer:
         self._srv.daemon_threads = True
         self.port = self._srv.server_address[1]
         threading.Thread(target=self._srv.serve_forever, daemon=True, name="druid-http").start()
+        disc = getattr(self.session, "discovery", None)
+        self._announced = []
+        if disc is not None:
+            # one endpoint plays every Druid service role (CuratorConnection.getBroker/getCoordinator)
+            for svc in ("broker", "coordinator", "overlord"):
+                self._announced.append(disc.announce_service(svc, self.host, self.port))
         return self
 
     def stop(self):
+        disc = getattr(self.session, "discovery", None)
+        for p in getattr(self, "_announced", []):
+            disc.unannounce(p)
+        self._announced = []
         if self._srv is not None:
             self._srv.shutdown()
             self._srv.server_close()

@@ -151,6 +151,18 @@ class Session:
         from .modules import load_modules
 
         self.modules = load_modules(self)
+        self.discovery = None
+        if self.conf.get("spark.sparklinedata.druid.discovery", "true") not in ("false", False):
+            self.attach_discovery(self.conf.get("spark.sparklinedata.druid.zkHost", "localhost"))
+
+    def attach_discovery(self, druid_host: str = "localhost", druid_path: str = "/druid",
+                         qualify_names: bool = False):
+        """Join the service registry named by a ``druidHost`` connect string (client/discovery.py)."""
+        from .client.discovery import Discovery, registry_for
+
+        self.discovery = Discovery(registry_for(druid_host), druid_path, qualify_names)
+        self.catalog.cluster.attach_discovery(self.discovery, self.engine.world.rank)
+        return self.discovery
 
     # ------------------------------------------------------------------------------ extension points
     def register_udf(self, name: str, fn, return_type: str = "string", vectorized: bool = False) -> None:
