@@ -35,6 +35,7 @@ import numpy as np
 from ..client import smile
 from ..query import spec as S
 from ..query.intervals import fmt_iso
+from .ui import HTMLPage, queries_page
 
 log = logging.getLogger("sdo.druid_http")
 
@@ -159,6 +160,10 @@ class DruidHTTPServer:
     def handle(self, method: str, path: str, query: Dict[str, List[str]], body: Optional[bytes]):
         cluster = self.session.catalog.cluster
         parts = [p for p in path.split("/") if p]
+        if method == "GET" and parts == ["sparklinedata", "druid", "queries"]:
+            return 200, queries_page(self.session.history.entries())
+        if method == "GET" and parts == ["sparklinedata", "druid", "queries.json"]:
+            return 200, self.session.history.rows()
         if method == "GET" and parts == ["status"]:
             return 200, {"version": "spark-druid-olap-amd", "modules": [], "gpus": self.session.engine.world.size}
         if parts[:2] == ["druid", "v2"]:
@@ -256,7 +261,9 @@ class DruidHTTPServer:
                 self._send(code, obj)
 
             def _send(self, code, obj):
-                if getattr(self, "_smile", False):
+                if isinstance(obj, HTMLPage):
+                    data, ct = obj.encode("utf-8"), "text/html; charset=utf-8"
+                elif getattr(self, "_smile", False):
                     data, ct = smile.dumps(json.loads(json.dumps(obj, default=_py))), smile.MIME
                 else:
                     data, ct = json.dumps(obj, default=_py).encode(), "application/json"

@@ -519,13 +519,16 @@ def main(argv=None):
     ap.add_argument("--port", type=int, default=int(os.environ.get("SDO_THRIFT_PORT", "10000")))
     ap.add_argument("--tpch-sf", type=float, default=0.0, help="preload a synthetic TPC-H datasource")
     ap.add_argument("--init-sql", default=None, help="file of ';'-separated statements to run at startup")
+    ap.add_argument("--ui-port", type=int, default=int(os.environ.get("SDO_UI_PORT", "4040")),
+                    help="Druid HTTP API + 'Druid Query Details' page (0 = any free port, -1 = off)")
+    ap.add_argument("--conf", action="append", default=[], help="key=value session conf (repeatable)")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
     import torch
 
     from ..session import Session
 
-    sess = Session()
+    sess = Session(conf=dict(kv.split("=", 1) for kv in a.conf))
     if a.tpch_sf > 0:
         from ..models import tpch
 
@@ -539,6 +542,14 @@ def main(argv=None):
             for st in f.read().split(";"):
                 if st.strip():
                     sess.sql(st)
+    if a.ui_port >= 0:
+        # the reference attaches its "Druid Query Details" UI tab next to the Thrift server
+        # (HiveThriftServer2.scala:73-77); here the same process also serves the Druid HTTP API
+        from .druid_http import DruidHTTPServer
+
+        ui = DruidHTTPServer(sess, a.host, a.ui_port).start()
+        logging.getLogger("sdo.thrift").info("query history page: http://%s:%d/sparklinedata/druid/queries",
+                                             a.host, ui.port)
     HiveThriftServer(sess, a.host, a.port).serve_forever()
 
 

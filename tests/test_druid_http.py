@@ -65,3 +65,20 @@ def test_overlord_index_task(srv):
         {"queryType": "timeseries", "dataSource": "zipCodes", "granularity": "all",
          "intervals": ["2015-01-01/2017-01-01"], "aggregations": [{"type": "count", "name": "c"}]})
     assert r[0]["result"]["c"] >= 1
+
+
+def test_query_history_page(ds_small):
+    import requests
+
+    s = Session(engine=Engine(use_native=False), conf={"spark.sparklinedata.enable.druid.query.history": "true"})
+    s.register_datasource(ds_small)
+    h = DruidHTTPServer(s, port=0).start()
+    try:
+        DruidQueryServerClient("127.0.0.1", h.port).execute_query(DRUID_JSON["TPCH Q1"])
+        r = requests.get(f"http://127.0.0.1:{h.port}/sparklinedata/druid/queries", timeout=10)
+        assert r.status_code == 200 and r.headers["Content-Type"].startswith("text/html")
+        assert "Druid Query Details" in r.text and "GroupByQuerySpec" in r.text or "groupBy" in r.text
+        js = requests.get(f"http://127.0.0.1:{h.port}/sparklinedata/druid/queries.json", timeout=10).json()
+        assert len(js) == 1 and js[0]["numRows"] == 4
+    finally:
+        h.stop()
