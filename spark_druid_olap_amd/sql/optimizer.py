@@ -4,6 +4,8 @@
     become inner equi-joins (Spark's PushPredicateThroughJoin / ReorderJoin), which is what lets the
     star-join elimination see ``lineitem ⋈ orders ⋈ customer`` trees (``tc/StarSchemaBaseTest.scala:46-60``);
   * filter simplification / NULL scans (``asql/util/ExprUtil.scala:156-183``);
+  * ``PullVColsIntoAgg`` (``DruidLogicalOptimizer.scala:304-329``): computed projection columns
+    are inlined into the Aggregate above them;
   * ``SumOfLiteralRewrite`` (``asql/planner/logical/DruidLogicalOptimizer.scala:245-302``):
     ``sum(lit)`` -> ``count(1) * lit``;
   * exact ``COUNT(DISTINCT)`` rewrite (``SPLRewriteDistinctAggregates.scala:37-205``): the distinct
@@ -31,7 +33,7 @@ def optimize(plan: P.Plan, conf=None) -> P.Plan:
     q = p.transform_up(_push_gb)
     if q is not p:
         p = _push_down_all(q)
-    return p
+    return p.transform_up(_pull_vcols_into_agg)
 
 
 def _push_down_all(p: P.Plan) -> P.Plan:
@@ -229,6 +231,40 @@ def _push_gb(p: P.Plan):
     for i, a in enumerate(p.aggs):
         exprs.append(A.Alias(io[len(new_groups) + i], a.name, a.rid))
     return P.Project(exprs, nj)
+
+
+def _pull_vcols_into_agg(p: P.Plan):
+    """PullVColsIntoAgg (``asql/planner/logical/DruidLogicalOptimizer.scala:304-329``): an Aggregate
+    over a Project that computes virtual columns (aliases of expressions over several inputs) gets
+    those expressions inlined into its grouping / aggregate expressions; the Project below keeps
+    only the plain columns they reference.  Grouping by ``(a + b)`` then appears to the Druid
+    rewrite as an expression over index columns instead of an opaque projected column."""
+    if not isinstance(p, P.Aggregate) or not isinstance(p.child, P.Project):
+        return None
+    proj = p.child
+    if not all(is_deterministic(e) for e in proj.exprs) or any(_has_agg_or_window(e) for e in proj.exprs) or \
+            any(isinstance(x, A.SubqueryExpr) for e in proj.exprs for x in e.walk()):
+        return None
+    aliases = {e.rid: e.child for e in proj.exprs if isinstance(e, A.Alias)}
+    if not any(len(list(c.refs())) > 1 or (not isinstance(c, A.Ref) and c.children)
+               for c in aliases.values() if not isinstance(c, A.Ref)):
+        return None
+
+    def inline(e: A.Expr) -> A.Expr:
+        return e.transform(lambda x: aliases[x.rid] if isinstance(x, A.Ref) and x.rid in aliases else None)
+
+    groups = [A.Alias(inline(g.child), g.name, g.rid) for g in p.groups]
+    aggs = [A.Alias(inline(a.child), a.name, a.rid) for a in p.aggs]
+    gid = p.gid
+    need: Dict[int, A.Ref] = {}
+    for e in groups + aggs:
+        for r in e.refs():
+            need.setdefault(r.rid, r)
+    child_out = {r.rid for r in proj.child.output}
+    if not set(need) <= child_out:
+        return None
+    keep = [r for r in proj.child.output if r.rid in need]
+    return P.Aggregate(groups, aggs, P.Project(keep, proj.child), p.grouping_sets, gid)
 
 
 def _refs_of(e: A.Expr) -> Set[int]:

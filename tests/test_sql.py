@@ -255,3 +255,20 @@ def test_query_history(sess):
         assert r and "GroupByQuerySpec" in r[-1][0] and r[-1][2] == 3
     finally:
         sess.sql("set spark.sparklinedata.enable.druid.query.history=false")
+
+
+def test_pull_vcols_into_agg(sess):
+    """PullVColsIntoAgg (DruidLogicalOptimizer.scala:304-329): a computed projection column used as
+    an aggregate input is inlined into the Aggregate, so the whole query is one Druid GroupBy."""
+    from spark_druid_olap_amd.sql import plan as P
+    from spark_druid_olap_amd.sql.optimizer import optimize
+
+    q = (f"select l_returnflag, sum(rev) as r from (select l_returnflag, l_extendedprice * (1 - l_discount) as rev "
+         f"from {T}) t group by l_returnflag")
+    ctest(sess, q, ndruid=1)
+    an = sess.sql(q.replace(T, B))
+    opt = optimize(an.analyzed, sess.conf)
+    aggs = [p for p in opt.walk() if isinstance(p, P.Aggregate)]
+    assert aggs and isinstance(aggs[0].child, P.Project)
+    assert all(type(e).__name__ == "Ref" for e in aggs[0].child.exprs)
+    assert "l_discount" in aggs[0].aggs[0].sql()
