@@ -68,13 +68,14 @@ def is_cuda_ds(ds: DataSource) -> bool:
 class PreparedQuery:
     """A lowered query bound to a shard; run() can be called repeatedly (benchmarks, dashboards)."""
 
-    def __init__(self, engine: "Engine", qs: S.QuerySpec, ds: DataSource):
+    def __init__(self, engine: "Engine", qs: S.QuerySpec, ds: DataSource, segments_per_query: Optional[int] = None):
         self.engine = engine
         self.qs = qs
         self.ds = ds
         self.world = engine.world
         self.low = Lowerer(ds)
         self.scans: List[tuple] = []  # (tag, prog, prepared)
+        self.segments_per_query = segments_per_query
         qt = qs.queryType
         if qt in ("groupBy", "timeseries", "topN"):
             dims = []
@@ -83,7 +84,15 @@ class PreparedQuery:
             elif qt == "topN":
                 dims = [qs.dimension]
             prog = self.low.lower_aggregate(qs.intervals, qs.filter, dims, qs.granularity, qs.aggregations)
-            self.scans.append(("agg", prog, self._prepare(prog)))
+            self._full_prog = prog
+            if segments_per_query:
+                # "historical" execution: one partial query per batch of segments, merged here
+                for bprog in segment_batches(prog, ds, segments_per_query):
+                    self.scans.append(("agg", bprog, self._prepare(bprog)))
+                if not self.scans:
+                    self.scans.append(("agg", prog, self._prepare(prog)))
+            else:
+                self.scans.append(("agg", prog, self._prepare(prog)))
         elif qt == "search":
             for dim in (qs.searchDimensions or list(ds.dims)):
                 f = _search_filter(dim, qs.query)
@@ -130,13 +139,16 @@ class PreparedQuery:
         if qt in ("groupBy", "timeseries", "topN"):
             _, prog, prep = self.scans[0]
             part = self._scan(prog, prep)
+            if len(self.scans) > 1:
+                parts = [part] + [self._scan(p_, q_) for _, p_, q_ in self.scans[1:]]
+                part = combine_local(prog, parts)
             t1 = time.perf_counter()
             disjoint = bool(self.ds.shard_key) and any(k.col == self.ds.shard_key for k in prog.keys)
             part = merge_partials(self.world, prog, part, disjoint_keys=disjoint)
             t2 = time.perf_counter()
             cols = finalize(prog, part)
             t3 = time.perf_counter()
-            self._theta(prog, cols)
+            self._theta(self._full_prog, cols)
             res = self._post(prog, cols)
             t4 = time.perf_counter()
             res.stats.update(scan_ms=(t1 - t0) * 1e3, merge_ms=(t2 - t1) * 1e3, finalize_ms=(t3 - t2) * 1e3,
@@ -318,6 +330,58 @@ class PreparedQuery:
         return QueryResult(cols, data, "select", {"rows": int(rows.numel())}, paging=nxt)
 
 
+def segment_batches(prog: ScanProgram, ds: DataSource, per_query: int) -> List[ScanProgram]:
+    """Split a lowered scan into per-segment-batch scans (same key/slot layout, row ranges cut to
+    each batch of ``per_query`` consecutive segments), like the reference's HistoricalPartitions
+    sliding over a server's (segment, interval) list (``sd/DruidRDD.scala:244-269``)."""
+    import dataclasses
+
+    if prog.empty:
+        return []
+    segs = [sg for sg in ds.segments
+            if any(min(hi, sg.row_hi) > max(lo, sg.row_lo) for lo, hi in prog.ranges)]
+    out = []
+    per_query = max(1, int(per_query))
+    for i in range(0, len(segs), per_query):
+        batch = segs[i:i + per_query]
+        spans = _merge_spans(sorted((sg.row_lo, sg.row_hi) for sg in batch))
+        ranges = []
+        for lo, hi in prog.ranges:
+            for a, b in spans:
+                x, y = max(lo, a), min(hi, b)
+                if y > x:
+                    ranges.append((x, y))
+        if not ranges:
+            continue
+        ranges = _merge_spans(sorted(ranges))
+        if len(ranges) > D.MAX_RANGES:
+            raise ValueError("segment batch spans too many row ranges")
+        out.append(dataclasses.replace(prog, ranges=ranges))
+    return out
+
+
+def _merge_spans(spans):
+    out = []
+    for a, b in spans:
+        if out and a <= out[-1][1]:
+            out[-1] = (out[-1][0], max(out[-1][1], b))
+        else:
+            out.append((a, b))
+    return out
+
+
+def combine_local(prog: ScanProgram, parts: List[Partials]) -> Partials:
+    """Merge partial aggregates of one query computed over disjoint row sets (same layout)."""
+    from ..engine.partials import merge_sparse
+    from ..parallel.merge import _reduce_stacked
+
+    if all(p.kind == "dense" for p in parts):
+        acc = _reduce_stacked(prog, torch.stack([p.acc for p in parts]))
+        hll = [torch.stack([p.hll[i] for p in parts]).amax(dim=0) for i in range(len(parts[0].hll))]
+        return Partials("dense", acc, None, hll)
+    return merge_sparse([p.compact() for p in parts], prog.slots)
+
+
 def _gather_columns(world: World, data: Dict[str, np.ndarray]) -> Dict[str, np.ndarray]:
     import torch.distributed as dist
 
@@ -457,8 +521,12 @@ class Engine:
             use_native = torch.cuda.is_available()
         self.use_native = use_native
 
-    def prepare(self, qs: S.QuerySpec, ds: DataSource) -> PreparedQuery:
-        return PreparedQuery(self, qs, ds)
+    def prepare(self, qs: S.QuerySpec, ds: DataSource, segments_per_query: Optional[int] = None) -> PreparedQuery:
+        """``segments_per_query`` set = historical execution (``sd/DruidRDD.scala:62-84, 244-277``):
+        the query runs as one partial per batch of that many segments and the partials are merged
+        by the engine (the reference's Spark-side PostAggregate, ``asd/PostAggregate.scala``);
+        unset = broker execution, one fused scan over every segment."""
+        return PreparedQuery(self, qs, ds, segments_per_query)
 
-    def execute(self, qs: S.QuerySpec, ds: DataSource) -> QueryResult:
-        return self.prepare(qs, ds).run()
+    def execute(self, qs: S.QuerySpec, ds: DataSource, segments_per_query: Optional[int] = None) -> QueryResult:
+        return self.prepare(qs, ds, segments_per_query).run()

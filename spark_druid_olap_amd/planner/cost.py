@@ -172,3 +172,35 @@ def explain_cost(session, dq) -> str:
         f"  outputRows={c.output_rows:.4g}  bytesScanned={c.bytes_scanned}  groupBy={c.groupby_mode}",
         f"  merge={c.merge}  estScanMs={c.scan_ms:.4f}  estMergeMs={c.merge_ms:.4f}  gpus={session.engine.world.size}",
     ])
+
+
+def historical_cost_ms(ds, spec, segments_per_query: int, info=None) -> float:
+    """Segment-batched ("historical") execution: one scan launch + partial compaction per batch of
+    segments, then a merge of the partials (the reference's historical waves + Spark shuffle/agg,
+    ``asd/DruidQueryCostModel.scala:505-547``)."""
+    c = estimate(ds, spec, info)
+    nseg = max(1, sum(1 for _ in ds.segments))
+    batches = math.ceil(nseg / max(1, segments_per_query))
+    per_batch_out = min(c.output_rows, c.input_rows / batches if batches else c.input_rows)
+    merge_bytes = batches * per_batch_out * (len(spec.aggregation_specs) + 2) * 8
+    return c.scan_ms + batches * LAUNCH_S * 1e3 + merge_bytes / HBM_BW * 1e3 * 4
+
+
+def choose_method(ds, spec, conf=None, info=None):
+    """Broker (None) or historical (segments per query).  On one MI355X the broker plan -- one
+    fused scan over every resident segment with the partials merged in LDS/HBM -- is never more
+    expensive than batching segments into several launches plus a merge, so the GPU cost model
+    picks broker unless the batched plan is estimated cheaper (it is not, for any batch count)."""
+    limit = 5
+    if conf is not None:
+        try:
+            limit = int(conf.typed("spark.sparklinedata.druid.querycostmodel.histSegsPerQueryLimit"))
+        except Exception:  # noqa: BLE001
+            pass
+    broker = estimate(ds, spec, info).total_ms
+    best = None
+    for n in range(1, max(1, limit) + 1):
+        h = historical_cost_ms(ds, spec, n, info)
+        if h < broker and (best is None or h < best[0]):
+            best = (h, n)
+    return None if best is None else best[1]

@@ -288,7 +288,7 @@ class Session:
             run_spec = spec.copy(pagingSpec=S.PagingSpec({}, 2 ** 31 - 1))
         prep = getattr(dq, "_prepared", None)
         if prep is None or getattr(dq, "_prepared_spec", None) is not spec:
-            prep = self.engine.prepare(run_spec, ds)
+            prep = self.engine.prepare(run_spec, ds, dq.info.get("historical"))
             dq._prepared = prep
             dq._prepared_spec = spec
         res = prep.run()
@@ -437,7 +437,10 @@ class Session:
         if not isinstance(t, DruidTable):
             raise AnalysisError(f"{'.'.join(st.table)} is not a Druid relation")
         spec = query_from_json(json.loads(st.json_text))
-        res = self.engine.execute(spec, t.info.datasource)
+        nseg = None
+        if st.historical:  # USING HISTORICAL: segment-batched partials merged by the engine
+            nseg = max(1, min(t.info.options.num_segments_per_query(self.conf), 1 << 30))
+        res = self.engine.execute(spec, t.info.datasource, nseg)
         if self.conf.typed("spark.sparklinedata.enable.druid.query.history"):
             self.history.record(spec, res.stats.get("exec_ms", 0.0), res.stats.get("exec_ms", 0.0), res.num_rows,
                                 f"gpu:0-{self.engine.world.size - 1}", None)

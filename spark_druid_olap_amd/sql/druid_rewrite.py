@@ -585,12 +585,28 @@ class DruidRewriter:
                                     final[rid])
         q = S.GroupByQuerySpec(info.ds_name, dims, None, None, S.Granularity.parse("all"), filt, aggs, None,
                                intervals)
-        dq = P.DruidQuery(pf.table, q, columns, drefs, {"groupby": True, "noop_conds": pf.noop_conds})
+        dq = P.DruidQuery(pf.table, q, columns, drefs, {"groupby": True, "noop_conds": pf.noop_conds,
+                                                         "historical": self._historical(pf, q)})
         exprs = []
         for r in outs:
             if r.rid in final:
                 exprs.append(A.Alias(final[r.rid], r.name, r.rid))
         return P.Project(exprs, dq)
+
+    def _historical(self, pf: PF, q) -> Optional[int]:
+        """Broker vs historical execution (``asd/DruidStrategy.scala:324-332``).  With the cost model
+        on, the GPU cost model decides (planner/cost.py: ``choose_method``); with it off, the
+        relation's ``queryHistoricalServers`` / ``numSegmentsPerHistoricalQuery`` options (and their
+        ``spark.sparklinedata.druid.option.*`` session overrides) decide.  Returns segments per
+        historical query, or None for broker execution."""
+        from ..planner.cost import choose_method
+
+        opts = pf.table.info.options
+        if bool(self.conf.typed("spark.sparklinedata.druid.querycostmodel.enabled")):
+            return choose_method(pf.table.info.datasource, q, self.conf)
+        if not opts.query_historical(self.conf):
+            return None
+        return max(1, min(opts.num_segments_per_query(self.conf), 1 << 30))
 
     # -- grouping expressions ------------------------------------------------------------------
     def _dim_spec(self, pf: PF, e: A.Expr, out: str):

@@ -1355,6 +1355,18 @@ def constant_fold(e: A.Expr) -> A.Expr:
             return None
         if isinstance(x, A.Call) and x.is_agg:
             return None
+        if isinstance(x, A.Case):
+            # branches with a constant condition: drop the false / NULL ones, stop at a true one
+            whens = [(c, v) for c, v in x.whens if not (isinstance(c, A.Lit) and c.value in (False, None))]
+            t = typeof(x)
+            if whens and isinstance(whens[0][0], A.Lit) and whens[0][0].value is True:
+                r = whens[0][1]
+                return r if typeof(r) == t else A.Cast(r, t)
+            if not whens:
+                r = x.else_ if x.else_ is not None else A.Lit(None, t)
+                return r if typeof(r) == t else A.Cast(r, t)
+            if len(whens) != len(x.whens):
+                return A.Case(tuple(whens), x.else_)
         if any(not isinstance(c, A.Lit) for c in x.children):
             return None
         if not is_deterministic(x):

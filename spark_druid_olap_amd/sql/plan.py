@@ -267,7 +267,9 @@ class DruidQuery(Plan):
     def describe(self):
         import json
 
-        return (f"DruidQuery[{self.relation.qualified_name}] {type(self.spec).__name__} -> "
+        h = self.info.get("historical")
+        mode = f" queryHistorical=true numSegmentsPerQuery={h}" if h else ""
+        return (f"DruidQuery[{self.relation.qualified_name}]{mode} {type(self.spec).__name__} -> "
                 f"({', '.join(r.sql() for r in self.refs)})\n      "
                 + json.dumps(self.spec.to_json(), sort_keys=False)[:2000])
 

@@ -185,3 +185,16 @@ def test_dimension_lut_and_time_minmax(gpu_ds):
     assert nat.num_rows == 3
     assert_same(nat, ref, rtol=1e-9)
     assert (nat.data["mx_ln"] == 7).all()
+
+
+@pytest.mark.parametrize("name", ["TPCH Q1", "TPCH Q3", "TPCH Q7"])
+def test_historical_segment_batches_native(gpu_ds, name):
+    """Segment-batched ("historical") execution on device: per-batch partial scans merged by the
+    engine equal the single fused scan."""
+    from spark_druid_olap_amd.models.bench_queries import DRUID_JSON
+
+    q = query_from_json(DRUID_JSON[name])
+    eng = Engine(use_native=True)
+    a = eng.execute(q, gpu_ds)
+    b = eng.execute(q, gpu_ds, segments_per_query=9)
+    assert_same(a, b, hll_cols=_hll_names(q), rtol=1e-9)
