@@ -176,6 +176,11 @@ class PreparedScan:
     def run(self) -> Partials:
         prog = self.prog
         if prog.empty:
+            if self.mode != D.M_HASH:
+                # dense layout even when this shard has nothing to scan: every rank must issue the
+                # same merge collective (parallel/merge.py) for the same query
+                self._reset()
+                return Partials("dense", self.acc, None, [h.view(self.rows, self.m) for h in self.hll])
             return self._empty()
         while True:
             self._reset()

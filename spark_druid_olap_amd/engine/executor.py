@@ -120,7 +120,29 @@ class PreparedQuery:
             return PreparedMask(prog)
         return None
 
+    def _placeholder(self, prog, prep) -> Partials:
+        """Layout-compatible empty partials for a rank whose scan failed (same collective pattern as
+        its peers, so the failure can be agreed on inside the merge)."""
+        dev = self.ds.device
+        m = 1 << prog.hll_p
+        if prep is not None:
+            from ..ops import desc as D_
+
+            if prep.mode == D_.M_HASH:
+                return prep._empty()
+            return Partials("dense", _init_acc(prog, prog.G, dev), None,
+                            [torch.zeros((prog.G, m), dtype=torch.int32, device=dev) for _ in range(prog.nhll)])
+        if prog.G > (1 << 22):
+            return Partials("sparse", torch.empty((0, prog.nslots), dtype=torch.int64, device=dev),
+                            torch.zeros(0, dtype=torch.int64, device=dev),
+                            [torch.zeros((0, m), dtype=torch.int32, device=dev) for _ in range(prog.nhll)])
+        return Partials("dense", _init_acc(prog, prog.G, dev), None,
+                        [torch.zeros((prog.G, m), dtype=torch.int32, device=dev) for _ in range(prog.nhll)])
+
     def _scan(self, prog, prep) -> Partials:
+        from ..parallel.fault import FAULTS
+
+        FAULTS.maybe_fail("scan", self.world.rank)
         if prep is not None:
             return prep.run()
         from ..ops.reference import run_reference
@@ -138,13 +160,19 @@ class PreparedQuery:
         qt = self.qs.queryType
         if qt in ("groupBy", "timeseries", "topN"):
             _, prog, prep = self.scans[0]
-            part = self._scan(prog, prep)
-            if len(self.scans) > 1:
-                parts = [part] + [self._scan(p_, q_) for _, p_, q_ in self.scans[1:]]
-                part = combine_local(prog, parts)
+            err = None
+            try:
+                part = self._scan(prog, prep)
+                if len(self.scans) > 1:
+                    parts = [part] + [self._scan(p_, q_) for _, p_, q_ in self.scans[1:]]
+                    part = combine_local(prog, parts)
+            except Exception as e:  # noqa: BLE001  (peers learn about it in the merge collective)
+                if not self.world.distributed:
+                    raise
+                err, part = e, self._placeholder(prog, prep)
             t1 = time.perf_counter()
             disjoint = bool(self.ds.shard_key) and any(k.col == self.ds.shard_key for k in prog.keys)
-            part = merge_partials(self.world, prog, part, disjoint_keys=disjoint)
+            part = merge_partials(self.world, prog, part, disjoint_keys=disjoint, local_error=err)
             t2 = time.perf_counter()
             cols = finalize(prog, part)
             t3 = time.perf_counter()
@@ -328,6 +356,11 @@ class PreparedQuery:
         cols = ["timestamp"] + list(dims) + list(mets)
         nxt = {ident: start + int(page.numel()) - 1} if page.numel() else {ident: start - 1}
         return QueryResult(cols, data, "select", {"rows": int(rows.numel())}, paging=nxt)
+
+
+def _init_acc(prog: ScanProgram, rows: int, dev) -> torch.Tensor:
+    init = torch.tensor([int(i) for _, i in prog.slots], dtype=torch.int64, device=dev)
+    return init.reshape(1, -1).repeat(rows, 1)
 
 
 def segment_batches(prog: ScanProgram, ds: DataSource, per_query: int) -> List[ScanProgram]:

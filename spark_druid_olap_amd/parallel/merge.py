@@ -13,12 +13,13 @@ final aggregate, ``asd/PostAggregate.scala:39-103``, re-designed for RCCL over x
 """
 from __future__ import annotations
 
-from typing import List
+from typing import List, Optional
 
 import torch
 
 from ..engine.partials import Partials, merge_sparse
 from ..ops import desc as D
+from .fault import STATUS_FAILED, STATUS_OK, raise_if_failed
 from .world import World
 
 ONE_SHOT_BYTES = 4 << 20
@@ -40,14 +41,25 @@ def _reduce_stacked(prog, acc_all: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def merge_partials(world: World, prog, part: Partials, disjoint_keys: bool = False) -> Partials:
+def merge_partials(world: World, prog, part: Partials, disjoint_keys: bool = False,
+                   local_error: Optional[BaseException] = None) -> Partials:
+    """Merge this rank's partials with every other rank's.  ``local_error`` set = this rank failed
+    its scan and ``part`` is a layout-compatible placeholder: the status word travels in the
+    merge's own collective and every rank raises (parallel/fault.py)."""
     if not world.distributed:
+        if local_error is not None:
+            raise local_error
         return part
+    status = STATUS_FAILED if local_error is not None else STATUS_OK
     if part.kind == "dense" and part.acc.numel() * 8 * world.size <= ONE_SHOT_BYTES:
         R, ns = part.acc.shape
-        pieces = [part.acc.reshape(-1)] + [h.reshape(-1).to(torch.int64) for h in part.hll]
-        buf = torch.cat(pieces) if len(pieces) > 1 else pieces[0]
+        st = torch.full((1,), status, dtype=torch.int64, device=part.acc.device)
+        pieces = [part.acc.reshape(-1)] + [h.reshape(-1).to(torch.int64) for h in part.hll] + [st]
+        buf = torch.cat(pieces)
         g = world.all_gather_tensor(buf)  # [ranks, L]
+        sts = g[:, -1]
+        if local_error is not None or bool((sts != 0).any()):
+            raise_if_failed(sts.tolist(), world.rank, local_error)
         acc_all = g[:, : R * ns].reshape(world.size, R, ns)
         acc = _reduce_stacked(prog, acc_all)
         off = R * ns
@@ -58,6 +70,10 @@ def merge_partials(world: World, prog, part: Partials, disjoint_keys: bool = Fal
             off += n
         return Partials("dense", acc, None, hll)
     if part.kind == "dense":
+        st = torch.full((1,), status, dtype=torch.int64, device=part.acc.device)
+        world.all_reduce(st, "max")
+        if local_error is not None or int(st.item()):
+            raise_if_failed([int(st.item())], world.rank, local_error)
         acc = part.acc.clone()
         for op in (D.S_SUM_I, D.S_SUM_F, D.S_MIN_I, D.S_MAX_I):
             cols = [s for s, (o, _) in enumerate(prog.slots) if o == op]
@@ -79,10 +95,14 @@ def merge_partials(world: World, prog, part: Partials, disjoint_keys: bool = Fal
         return Partials("dense", acc, None, hll)
     # sparse
     sp = part.compact()
-    keys = world.all_gather_varlen(sp.keys)
-    accs = world.all_gather_varlen(sp.acc)
+    # keys + accumulators travel as one [n, 1 + nslots] int64 block: one length exchange (which also
+    # carries the status word) + one gather
+    kv = torch.cat([sp.keys.reshape(-1, 1).to(torch.int64), sp.acc], dim=1)
+    kvs, sts = world.all_gather_varlen(kv, status=status)
+    if local_error is not None or any(sts):
+        raise_if_failed(sts, world.rank, local_error)
     hlls = [world.all_gather_varlen(h) for h in sp.hll]
-    parts = [Partials("sparse", accs[i], keys[i], [h[i] for h in hlls]) for i in range(world.size)]
+    parts = [Partials("sparse", kvs[i][:, 1:], kvs[i][:, 0], [h[i] for h in hlls]) for i in range(world.size)]
     if disjoint_keys:
         return Partials("sparse", torch.cat([p.acc for p in parts]), torch.cat([p.keys for p in parts]),
                         [torch.cat([p.hll[i] for p in parts]) for i in range(len(sp.hll))])

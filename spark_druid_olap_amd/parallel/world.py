@@ -63,18 +63,25 @@ class World:
         dist.all_gather_into_tensor(out, src, group=self.group)
         return out.view((self.size,) + tuple(t.shape))
 
-    def all_gather_varlen(self, t: torch.Tensor) -> List[torch.Tensor]:
-        """Gather tensors whose first dimension differs per rank."""
+    def all_gather_varlen(self, t: torch.Tensor, status: Optional[int] = None):
+        """Gather tensors whose first dimension differs per rank.  With ``status`` set, every rank's
+        status word rides along with the length exchange and ``(tensors, statuses)`` is returned
+        (failure agreement without an extra collective, parallel/fault.py)."""
         if not self.distributed:
-            return [t]
-        n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
-        ns = self.all_gather_tensor(n).flatten().tolist()
+            return ([t], [status]) if status is not None else [t]
+        n = torch.tensor([t.shape[0], status or 0], dtype=torch.int64, device=t.device)
+        g = self.all_gather_tensor(n).reshape(self.size, 2).tolist()
+        ns = [x[0] for x in g]
+        sts = [x[1] for x in g]
+        if status is not None and any(sts):
+            return [t[:0]] * self.size, sts
         mx = max(ns) if ns else 0
         pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         if t.shape[0]:
             pad[: t.shape[0]] = t
         g = self.all_gather_tensor(pad)
-        return [g[i, : ns[i]] for i in range(self.size)]
+        out = [g[i, : ns[i]] for i in range(self.size)]
+        return (out, sts) if status is not None else out
 
     def broadcast_object(self, obj: Any, src: int = 0) -> Any:
         if not self.distributed:
@@ -112,6 +119,7 @@ def init_world(backend: Optional[str] = None, timeout_s: int = 600) -> World:
         kw = {}
         if backend == "nccl":
             kw["device_id"] = torch.device("cuda", local % torch.cuda.device_count())
+        timeout_s = int(os.environ.get("SDO_COLLECTIVE_TIMEOUT_S", timeout_s))
         dist.init_process_group(backend=backend, rank=rank, world_size=size,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
     _WORLD = World(rank, size, local, backend, None)

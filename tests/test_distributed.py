@@ -115,3 +115,62 @@ def test_two_rank_sql_equals_union():
     exact = dict(s.sql("select l_returnflag, count(distinct o_orderkey) from base group by l_returnflag").collect())
     for k, v in outs[0]["res"][APPROX]:
         assert v == pytest.approx(exact[k], rel=0.08)
+
+
+def _fault_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), SDO_COLLECTIVE_TIMEOUT_S="60")
+    import json
+
+    from spark_druid_olap_amd.engine.executor import Engine
+    from spark_druid_olap_amd.models import tpch
+    from spark_druid_olap_amd.parallel.fault import FAULTS, InjectedFault, RankFailure
+    from spark_druid_olap_amd.parallel.world import init_world, shutdown
+    from spark_druid_olap_amd.session import Session
+
+    w = init_world(backend="gloo")
+    ds = tpch.to_datasource(tpch.generate_flat(0.002, "cpu", rank=rank, world=world), profile="bench")
+    s = Session(engine=Engine(w, use_native=False))
+    s.register_datasource(ds)
+    s.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)
+    s.sql(tpch.druid_ddl(with_column_mapping=False))
+    log = []
+    for q in (QUERIES[0], QUERIES[2]):          # dense (one-shot all-gather) and sparse (varlen) merges
+        d = s.sql(q)
+        FAULTS.configure(1, "scan", 1)          # rank 1 fails its next local scan
+        try:
+            d.collect()
+            log.append("ok")
+        except InjectedFault:
+            log.append("injected")
+        except RankFailure:
+            log.append("peer-failed")
+        FAULTS.clear()
+        log.append(len(d.collect()))           # the process group is still in lock-step
+    with open(os.path.join(outdir, f"f{rank}.json"), "w") as f:
+        json.dump(log, f)
+    w.barrier()
+    shutdown()
+
+
+@pytest.mark.timeout(300)
+def test_rank_failure_is_agreed_and_recoverable():
+    """Fault injection: one rank fails its scan; every rank aborts the query in the
+    same merge collective (no hang until the process-group timeout) and the next query runs."""
+    import json
+
+    world = 2
+    with tempfile.TemporaryDirectory() as td:
+        ctx = mp.get_context("spawn")
+        port = _free_port()
+        ps = [ctx.Process(target=_fault_worker, args=(r, world, port, td)) for r in range(world)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(250)
+            assert p.exitcode == 0, f"rank failed with {p.exitcode}"
+        logs = [json.load(open(os.path.join(td, f"f{r}.json"))) for r in range(world)]
+    assert logs[0][0] == "peer-failed" and logs[1][0] == "injected"
+    assert logs[0][2] == "peer-failed" and logs[1][2] == "injected"
+    assert logs[0][1] == logs[1][1] and logs[0][1] > 0
+    assert logs[0][3] == logs[1][3] and logs[0][3] > 0
