@@ -19,6 +19,7 @@ import torch
 from ..ops import desc as D
 from ..parallel.merge import merge_partials
 from ..parallel.world import World, get_world
+from ..utils import trace as T
 from ..query import spec as S
 from ..query.jsfunc import compile_function
 from ..segment.datasource import DataSource
@@ -162,22 +163,26 @@ class PreparedQuery:
             _, prog, prep = self.scans[0]
             err = None
             try:
-                part = self._scan(prog, prep)
-                if len(self.scans) > 1:
-                    parts = [part] + [self._scan(p_, q_) for _, p_, q_ in self.scans[1:]]
-                    part = combine_local(prog, parts)
+                with T.span("sdo.scan"):
+                    part = self._scan(prog, prep)
+                    if len(self.scans) > 1:
+                        parts = [part] + [self._scan(p_, q_) for _, p_, q_ in self.scans[1:]]
+                        part = combine_local(prog, parts)
             except Exception as e:  # noqa: BLE001  (peers learn about it in the merge collective)
                 if not self.world.distributed:
                     raise
                 err, part = e, self._placeholder(prog, prep)
             t1 = time.perf_counter()
             disjoint = bool(self.ds.shard_key) and any(k.col == self.ds.shard_key for k in prog.keys)
-            part = merge_partials(self.world, prog, part, disjoint_keys=disjoint, local_error=err)
+            with T.span("sdo.merge"):
+                part = merge_partials(self.world, prog, part, disjoint_keys=disjoint, local_error=err)
             t2 = time.perf_counter()
-            cols = finalize(prog, part)
+            with T.span("sdo.finalize"):
+                cols = finalize(prog, part)
             t3 = time.perf_counter()
-            self._theta(self._full_prog, cols)
-            res = self._post(prog, cols)
+            with T.span("sdo.post"):
+                self._theta(self._full_prog, cols)
+                res = self._post(prog, cols)
             t4 = time.perf_counter()
             res.stats.update(scan_ms=(t1 - t0) * 1e3, merge_ms=(t2 - t1) * 1e3, finalize_ms=(t3 - t2) * 1e3,
                              post_ms=(t4 - t3) * 1e3)

@@ -224,12 +224,16 @@ class Session:
                 r = p(text, self)
                 if r is not None:
                     return r
+        from .utils import trace as T
+
         try:
-            st = parse(text)
+            with T.span("sdo.parse"):
+                st = parse(text)
         except ParseError as pe:
             raise ParseError(f"{pe}\n\n== SQL ==\n{text}") from None
         if isinstance(st, (A.Select, A.SetOp, A.With)):
-            return self._query(text, st)
+            with T.span("sdo.plan"):
+                return self._query(text, st)
         return self._command(text, st)
 
     def _query(self, text: str, st) -> DataFrame:
@@ -286,12 +290,16 @@ class Session:
             # one page holding every row (the reference's paging loop, DruidSelectResultIterator.scala:116-137,
             # collapsed: the scan compacts on device and ships all selected rows at once)
             run_spec = spec.copy(pagingSpec=S.PagingSpec({}, 2 ** 31 - 1))
+        from .utils import trace as T
+
         prep = getattr(dq, "_prepared", None)
         if prep is None or getattr(dq, "_prepared_spec", None) is not spec:
-            prep = self.engine.prepare(run_spec, ds, dq.info.get("historical"))
+            with T.span("sdo.lower"):
+                prep = self.engine.prepare(run_spec, ds, dq.info.get("historical"))
             dq._prepared = prep
             dq._prepared_spec = spec
-        res = prep.run()
+        with T.span(f"sdo.druid.{spec.queryType}"):
+            res = prep.run()
         if isinstance(spec, S.TimeSeriesQuerySpec) and res.num_rows == 0:
             res = _empty_global_agg(res, spec)
         ms = (time.perf_counter() - t0) * 1e3
