@@ -1,0 +1,176 @@
+#!/usr/bin/env python3
+"""BASELINE config 5: the HiveServer2 Thrift endpoint under many concurrent JDBC-style clients.
+
+The reference's BI benchmark drives its Thrift server with JMeter threads over JDBC
+(``docs/bi-benchmark/snap-sales-demo.jmx:87-101``: 5 threads x 5 loops, fair scheduler pool); it
+publishes no results.  Here:
+
+* the server (``server/hive_server.py``) runs in this process with a synthetic TPC-H datasource
+  resident on the GPU (``--sf``) and the reference's DDL;
+* ``--clients`` concurrent clients (spread over ``--procs`` client processes, each with its own
+  Thrift connection and session) issue the 8 benchmark queries round-robin -- TPC-H Q3 with its
+  standard ``ORDER BY ... LIMIT 10`` so a dashboard client does not pull a million rows;
+* open loop at a fixed aggregate rate ``--qps`` (each client sends on its own schedule; latency is
+  measured from the *scheduled* send time, so queueing delay counts -- no coordinated omission),
+  or closed loop (``--qps 0``: every client sends its next query when the previous one returns);
+* prints one JSON line: achieved QPS, p50/p90/p99/max latency overall and per query.
+
+  python tools/concurrency_bench.py --sf 100 --clients 64 --qps 400 --duration 30
+"""
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def queries():
+    from spark_druid_olap_amd.models import tpch
+
+    out = []
+    for name, q in tpch.BENCH_QUERIES:
+        if name == "TPCH Q3":
+            q = q.rstrip() + " order by price desc, o_orderdate limit 10"
+        out.append((name, " ".join(q.split())))
+    return out
+
+
+def _client_proc(pid, nthreads, nclients, start_q, out_q):
+    import threading
+
+    from spark_druid_olap_amd.server.hive_client import connect
+
+    global NCLIENTS
+    NCLIENTS = nclients
+    port, t_start, duration, interval = start_q.get()
+
+    qs = queries()
+    res = []
+    lock = threading.Lock()
+
+    def worker(k):
+        cid = pid * nthreads + k
+        conn = connect(port=port)
+        i = cid
+        # stagger the open-loop schedules so the aggregate arrival rate is uniform
+        nxt = t_start + (cid * interval / max(1, NCLIENTS)) if interval else t_start
+        while True:
+            now = time.time()
+            if interval:
+                if nxt > t_start + duration:
+                    break
+                if nxt > now:
+                    time.sleep(nxt - now)
+                sched = nxt
+                nxt += interval
+            else:
+                if now > t_start + duration:
+                    break
+                sched = now
+            name, sql = qs[i % len(qs)]
+            i += 1
+            err = None
+            try:
+                cur = conn.cursor().execute(sql)
+                rows = cur.fetchall()
+                cur.close()
+                n = len(rows)
+            except Exception as e:  # noqa: BLE001
+                err, n = f"{type(e).__name__}: {e}", 0
+            done = time.time()
+            with lock:
+                res.append((name, sched, done, n, err))
+        conn.close()
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(nthreads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    out_q.put(res)
+
+
+NCLIENTS = 1
+
+
+def pct(xs, p):
+    if not xs:
+        return None
+    xs = sorted(xs)
+    k = min(len(xs) - 1, max(0, int(round(p / 100.0 * (len(xs) - 1)))))
+    return xs[k]
+
+
+def main():
+    global NCLIENTS
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sf", type=float, default=1.0)
+    ap.add_argument("--clients", type=int, default=64)
+    ap.add_argument("--procs", type=int, default=8)
+    ap.add_argument("--qps", type=float, default=200.0, help="aggregate target rate; 0 = closed loop")
+    ap.add_argument("--duration", type=float, default=20.0)
+    ap.add_argument("--warmup", type=float, default=3.0)
+    a = ap.parse_args()
+    NCLIENTS = a.clients
+    nthreads = max(1, a.clients // a.procs)
+    nproc = max(1, a.clients // nthreads)
+    # client processes start BEFORE this process touches the GPU (no fork/exec of a GPU process)
+    ctx = mp.get_context("spawn")
+    res_q = ctx.Queue()
+    start_q = ctx.Queue()
+    ps = [ctx.Process(target=_client_proc, args=(i, nthreads, a.clients, start_q, res_q)) for i in range(nproc)]
+    for p in ps:
+        p.start()
+    import torch
+
+    from spark_druid_olap_amd.models import tpch
+    from spark_druid_olap_amd.server.hive_client import connect
+    from spark_druid_olap_amd.server.hive_server import HiveThriftServer
+    from spark_druid_olap_amd.session import Session
+
+    dev = "cuda" if torch.cuda.is_available() else "cpu"
+    t0 = time.time()
+    ds = tpch.to_datasource(tpch.generate_flat(a.sf, dev), profile="bench")
+    s = Session(conf={"spark.sparklinedata.druid.approxCountDistinct": "true"})
+    s.register_datasource(ds)
+    s.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)
+    s.sql(tpch.druid_ddl(source="orderLineItemPartSupplierBase", datasource="tpch", with_column_mapping=False))
+    srv = HiveThriftServer(s, port=0).start()
+    print(f"[conc] server up on {srv.port}: SF{a.sf:g} {ds.num_rows} rows on {dev} in {time.time() - t0:.1f}s",
+          file=sys.stderr, flush=True)
+    # warm every query's plan + kernel once through the server
+    with connect(port=srv.port) as c:
+        for _, sql in queries():
+            c.cursor().execute(sql).fetchall()
+    interval = (a.clients / a.qps) if a.qps > 0 else 0.0
+    t_start = time.time() + 1.0 + a.warmup
+    for _ in ps:
+        start_q.put((srv.port, t_start - a.warmup, a.duration + a.warmup, interval))
+    res = []
+    for _ in ps:
+        res.extend(res_q.get())
+    for p in ps:
+        p.join()
+    srv.stop()
+    res = [r for r in res if r[1] >= t_start]  # drop the warm-up window
+    errs = [r for r in res if r[4]]
+    lat = [(r[2] - r[1]) * 1e3 for r in res if not r[4]]
+    span = max((r[2] for r in res), default=t_start) - t_start
+    per = {}
+    for name, _ in queries():
+        xs = [(r[2] - r[1]) * 1e3 for r in res if r[0] == name and not r[4]]
+        per[name] = {"n": len(xs), "p50_ms": pct(xs, 50), "p99_ms": pct(xs, 99)}
+    out = {"metric": "thrift_concurrent_latency", "clients": nproc * nthreads, "target_qps": a.qps,
+           "achieved_qps": round(len(lat) / span, 2) if span > 0 else None, "queries": len(res),
+           "errors": len(errs), "p50_ms": pct(lat, 50), "p90_ms": pct(lat, 90), "p99_ms": pct(lat, 99),
+           "max_ms": max(lat) if lat else None, "sf": a.sf, "device": dev, "per_query": per,
+           "first_error": errs[0][4] if errs else None}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
