@@ -351,8 +351,9 @@ class Analyzer:
             oe = o.expr
             if isinstance(oe, A.Lit) and isinstance(oe.value, int) and oe.dtype in ("int", "bigint"):
                 ex = items[oe.value - 1][0]
-            elif isinstance(oe, A.Col) and len(oe.parts) == 1 and oe.parts[0].lower() in alias_map \
-                    and scope.resolve(oe.parts) is None:
+            elif isinstance(oe, A.Col) and len(oe.parts) == 1 and oe.parts[0].lower() in alias_map:
+                # Spark resolves ORDER BY of an aggregate against the SELECT output first: an alias
+                # shadows an input column of the same name (SSB Q3.1 "sum(lo_revenue) as lo_revenue")
                 ex = alias_map[oe.parts[0].lower()]
             else:
                 ex = self._resolve_with_aliases(oe, scope, alias_map)

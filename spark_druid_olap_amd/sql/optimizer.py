@@ -30,6 +30,7 @@ def optimize(plan: P.Plan, conf=None) -> P.Plan:
     if not approx:
         p = p.transform_up(_distinct_rewrite)
     p = _push_down_all(p)
+    p = _push_down_all(_reorder_joins(p))
     q = p.transform_up(_push_gb)
     if q is not p:
         p = _push_down_all(q)
@@ -338,6 +339,57 @@ def _push_down(p: P.Plan) -> P.Plan:
             right = P.Filter(A.and_all(rc), p.right) if rc else p.right
             return P.Join("inner", left, right, A.and_all(jc))
     ch = [_push_down(c) for c in p.children]
+    if any(a is not b for a, b in zip(ch, p.children)):
+        return p.with_children(ch)
+    return p
+
+
+def _flatten_joins(p: P.Plan, items: List[P.Plan], conds: List[A.Expr]) -> bool:
+    """Leaves and conjuncts of a tree of inner/cross joins; True if any join in it is a cross join."""
+    if isinstance(p, P.Join) and p.kind in ("inner", "cross"):
+        a = _flatten_joins(p.left, items, conds)
+        b = _flatten_joins(p.right, items, conds)
+        if p.cond is not None:
+            conds.extend(A.conjuncts(p.cond))
+        return a or b or p.cond is None
+    items.append(p)
+    return False
+
+
+def _reorder_joins(p: P.Plan) -> P.Plan:
+    """Spark's ReorderJoin: a FROM list ``a, b, c`` with the join predicates in WHERE becomes a
+    left-deep tree of cross joins with the conditions pushed to the top.  Re-build it so each
+    leaf joins to the leaves before it through a condition (keeping the written order otherwise),
+    which is the shape the star-join elimination (asd/JoinTransform.scala) walks.  SSB Q4.x list
+    the fact table last: ``dwdate, customer, supplier, part, lineorder``."""
+    if isinstance(p, P.Join) and p.kind in ("inner", "cross"):
+        items: List[P.Plan] = []
+        conds: List[A.Expr] = []
+        has_cross = _flatten_joins(p, items, conds)
+        if has_cross and len(items) > 2 and conds:
+            items = [_reorder_joins(i) for i in items]
+            ids = [{r.rid for r in i.output} for i in items]
+            cur, cur_ids = items[0], set(ids[0])
+            rest = list(range(1, len(items)))
+            pending = list(conds)
+            while rest:
+                pick = None
+                for k in rest:
+                    both = cur_ids | ids[k]
+                    if any((_refs_of(c) & ids[k]) and (_refs_of(c) & cur_ids) and _refs_of(c) <= both
+                           for c in pending):
+                        pick = k
+                        break
+                if pick is None:
+                    pick = rest[0]
+                rest.remove(pick)
+                cur_ids |= ids[pick]
+                use = [c for c in pending if _refs_of(c) <= cur_ids]
+                pending = [c for c in pending if not _refs_of(c) <= cur_ids]
+                cond = A.and_all(use)
+                cur = P.Join("inner" if cond is not None else "cross", cur, items[pick], cond)
+            return P.Filter(A.and_all(pending), cur) if pending else cur
+    ch = [_reorder_joins(c) for c in p.children]
     if any(a is not b for a, b in zip(ch, p.children)):
         return p.with_children(ch)
     return p
