@@ -24,6 +24,9 @@ from .lower import ScanProgram, pack
 from .partials import Partials
 
 LDS_BUDGET = int(os.environ.get("SDO_LDS_BUDGET", 64 * 1024))
+# one accumulator table per workgroup (JIT only) for key spaces whose per-wave copies do not fit:
+# up to this many bytes of LDS, instead of HBM atomics contending on the touched groups
+SHARED_LDS_MAX = int(os.environ.get("SDO_SHARED_LDS_MAX", 112 * 1024))
 DENSE_GLOBAL_MAX_BYTES = int(os.environ.get("SDO_DENSE_MAX_BYTES", 1 << 30))
 BLOCK = 512
 UNROLL = int(os.environ.get("SDO_UNROLL", "2"))
@@ -37,7 +40,7 @@ JIT_BLOCKS = int(os.environ.get("SDO_JIT_BLOCKS", "3"))  # target resident workg
 JIT_STAGE = os.environ.get("SDO_JIT_STAGE", "auto")       # auto | reg (VGPR loads) | lds (LDS-DMA planes)
 
 
-def _jit_for(prog, mode: int, hll_lds: bool, m: int):
+def _jit_for(prog, mode: int, hll_lds: bool, m: int, shared: bool = False):
     """Specialized kernel for this program shape (None -> use the interpreter)."""
     if not USE_JIT:
         return None
@@ -45,7 +48,7 @@ def _jit_for(prog, mode: int, hll_lds: bool, m: int):
 
     nplanes = sum(2 if column_tensor_size(prog, c) == 8 else 1 for c in prog.cols)
     prefs = [16, 8, 4, 2] if nplanes <= 3 else ([8, 4, 2] if nplanes <= 8 else [4, 2])
-    reg = jit.reg_eligible(prog, mode) if USE_REG else False
+    reg = jit.reg_eligible(prog, mode) if USE_REG and not shared else False
     cands = [(U, True) for U in prefs if USE_PIPE and jit.pipe_eligible(prog, mode, U)]
     cands += [(U, False) for U in prefs]
     # occupancy first: the scan is latency-bound at 8 waves/CU, so prefer the largest U that still
@@ -56,11 +59,12 @@ def _jit_for(prog, mode: int, hll_lds: bool, m: int):
         cands = [(U, False) for U in prefs]
     for budget in budgets:
         for U, pipe in cands:
-            lay = jit.layout(prog, mode, U, hll_lds, m, reg, pipe, budget, regstage)
-            if lay.total <= budget and (reg or mode != D.M_DENSE_LDS or lay.ncopy >= 4 or U == prefs[-1]):
+            lay = jit.layout(prog, mode, U, hll_lds, m, reg, pipe, budget, regstage, shared)
+            if lay.total <= budget and (reg or shared or mode != D.M_DENSE_LDS or lay.ncopy >= 4
+                                        or U == prefs[-1]):
                 try:
                     return jit.JitScan(prog, mode, U, hll_lds, m, bool(native.narrow4()), reg=reg, pipe=pipe,
-                                       budget=budget, regstage=regstage)
+                                       budget=budget, regstage=regstage, shared=shared)
                 except Exception as e:  # pragma: no cover - compile problems fall back loudly
                     import warnings
 
@@ -98,12 +102,18 @@ class PreparedScan:
         acc_bytes = G * ns * 8 * (BLOCK // 64)  # one private copy per wave
         hll_bytes = prog.nhll * G * self.m * 4
         self.hll_lds = 0
+        self.shared = False
+        shared_bytes = G * ns * 8
         if mode is None:
             if acc_bytes + hll_bytes <= LDS_BUDGET:
                 mode = D.M_DENSE_LDS
                 self.hll_lds = 1 if prog.nhll else 0
             elif acc_bytes <= LDS_BUDGET // 2 and hll_bytes <= DENSE_GLOBAL_MAX_BYTES:
                 mode = D.M_DENSE_LDS
+            elif USE_JIT and not prog.empty and shared_bytes <= SHARED_LDS_MAX \
+                    and hll_bytes <= DENSE_GLOBAL_MAX_BYTES:
+                mode = D.M_DENSE_LDS
+                self.shared = True
             elif acc_bytes + hll_bytes <= DENSE_GLOBAL_MAX_BYTES:
                 mode = D.M_DENSE_GLOBAL
             else:
@@ -111,7 +121,7 @@ class PreparedScan:
         self.mode = mode
         self.dedup = 1 if G <= 64 else 0
         if mode == D.M_DENSE_LDS:
-            self.lds = acc_bytes + (hll_bytes if self.hll_lds else 0)
+            self.lds = (shared_bytes if self.shared else acc_bytes) + (hll_bytes if self.hll_lds else 0)
             self.lds = (self.lds + 15) // 16 * 16
         else:
             self.lds = 0
@@ -123,8 +133,13 @@ class PreparedScan:
         self.jit = None
         if not prog.empty:
             # the JIT keeps LDS registers one byte each (hll_update8)
-            jit_hll_lds = bool(prog.nhll) and mode == D.M_DENSE_LDS and hll_bytes // 4 <= LDS_BUDGET
-            self.jit = _jit_for(prog, mode, jit_hll_lds, self.m)
+            jit_hll_lds = bool(prog.nhll) and mode == D.M_DENSE_LDS and hll_bytes // 4 <= LDS_BUDGET \
+                and not self.shared
+            self.jit = _jit_for(prog, mode, jit_hll_lds, self.m, self.shared)
+            if self.shared and self.jit is None:
+                # the interpreter kernel only knows per-wave copies: accumulate in HBM instead
+                self.mode, self.shared, self.lds = D.M_DENSE_GLOBAL, False, 0
+                self.jit = _jit_for(prog, self.mode, False, self.m)
         self._alloc()
 
     # ------------------------------------------------------------------ buffers
@@ -144,14 +159,17 @@ class PreparedScan:
         for _ in range(prog.nhll):
             hll_offs.append(off)
             off += prog.G * self.m * 4
-        cache_off, wave_bytes, _, total = lds_layout(prog, self.lds, UNROLL, BLOCK // 64)
+        # (the shared-table layout lives in the JIT kernel only; the descriptor's interpreter layout
+        # then carries no LDS accumulators)
+        cache_off, wave_bytes, _, total = lds_layout(prog, 0 if self.shared else self.lds, UNROLL, BLOCK // 64)
         if total > 160 * 1024 and self.mode == D.M_DENSE_LDS:
             # accumulators + staging planes exceed the CU's LDS: accumulate in HBM instead
             self.mode, self.lds, self.hll_lds = D.M_DENSE_GLOBAL, 0, 0
             cache_off, wave_bytes, _, total = lds_layout(prog, 0, UNROLL, BLOCK // 64)
         if total > 160 * 1024:
             raise RuntimeError(f"query needs {total} bytes of LDS staging; reduce SDO_UNROLL")
-        d = pack(prog, self.mode, self.dedup, self.hll_lds, self.lds, self.acc.data_ptr(), self.keys.data_ptr(),
+        d = pack(prog, self.mode, self.dedup, self.hll_lds, 0 if self.shared else self.lds, self.acc.data_ptr(),
+                 self.keys.data_ptr(),
                  self.cap, self.overflow.data_ptr(), 0, 0, [h.data_ptr() for h in self.hll], hll_offs,
                  unroll=UNROLL, cache_off=cache_off, wave_bytes=wave_bytes)
         self.lds_total = total

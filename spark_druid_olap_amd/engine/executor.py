@@ -176,6 +176,7 @@ class PreparedQuery:
             disjoint = bool(self.ds.shard_key) and any(k.col == self.ds.shard_key for k in prog.keys)
             with T.span("sdo.merge"):
                 part = merge_partials(self.world, prog, part, disjoint_keys=disjoint, local_error=err)
+            part = self._device_prune(prog, part)
             t2 = time.perf_counter()
             with T.span("sdo.finalize"):
                 cols = finalize(prog, part)
@@ -192,6 +193,44 @@ class PreparedQuery:
             res = self._select()
         res.stats["exec_ms"] = (time.perf_counter() - t0) * 1e3
         return res
+
+    def _device_prune(self, prog: ScanProgram, part: Partials) -> Partials:
+        """ORDER BY <aggregate> LIMIT k (groupBy limitSpec) and numeric topN, applied to the merged
+        partials ON THE DEVICE before finalize: keep only groups whose leading sort key ties or
+        beats the k-th best (torch.topk), so a million-group query (TPC-H Q3 by o_orderkey) ships and
+        decodes a few rows instead of every group.  Ties at the k-th value are all kept, so the host
+        ``order_and_limit`` over the survivors gives exactly the unpruned answer."""
+        qs = self.qs
+        qt = qs.queryType
+        if qt == "groupBy":
+            ls = qs.limitSpec
+            if ls is None or ls.limit is None or ls.limit < 0 or not ls.columns or \
+                    getattr(qs, "having", None) is not None:
+                return part
+            oc = ls.columns[0]
+            oc = S.OrderByColumnSpec(oc) if isinstance(oc, str) else oc
+            name, desc, limit = oc.dimension, not oc.ascending, int(ls.limit)
+        elif qt == "topN" and isinstance(qs.metric, S.NumericTopNMetricSpec) and len(prog.keys) == 1:
+            name, desc, limit = qs.metric.metric, True, int(qs.threshold)
+        else:
+            return part
+        if limit <= 0 or part.rows <= max(4 * limit, 4096) or prog.thetas or any(kc.collapse for kc in prog.keys):
+            return part
+        agg = next((a for a in prog.aggs if a.name == name), None)
+        if agg is None or agg.kind not in ("count", "sum_i", "sum_f", "min_i", "max_i"):
+            return part
+        if part.kind == "dense":
+            part = part.compact()
+            if part.rows <= max(4 * limit, 4096):
+                return part
+        col = part.acc[:, agg.slot]
+        v = col.view(torch.float64) if agg.kind == "sum_f" else col.to(torch.float64)
+        key = v if desc else -v
+        key = torch.nan_to_num(key, nan=-math.inf)  # NaN sorts last either way
+        kth = torch.topk(key, limit, sorted=False).values.min()
+        keep = torch.nonzero(key >= kth).flatten()
+        return Partials("sparse", part.acc.index_select(0, keep), part.keys.index_select(0, keep),
+                        [h.index_select(0, keep) for h in part.hll])
 
     # ------------------------------------------------------------------ theta sketches
     def _theta(self, prog: ScanProgram, cols: Dict[str, np.ndarray]) -> None:

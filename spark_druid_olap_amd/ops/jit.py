@@ -58,6 +58,7 @@ class JitLayout:
     ncopy: int
     pipe: bool = False
     regstage: bool = False
+    shared: bool = False  # one accumulator copy per workgroup (LDS atomics shared by its 8 waves)
 
 
 def pipe_eligible(prog, mode: int, U: int) -> bool:
@@ -118,7 +119,7 @@ def reg_eligible(prog, mode: int) -> bool:
 
 
 def layout(prog, mode: int, U: int, hll_lds: bool, m: int, reg: bool = False, pipe: bool = False,
-           budget: int = 150 * 1024, regstage: bool = False) -> JitLayout:
+           budget: int = 150 * 1024, regstage: bool = False, shared: bool = False) -> JitLayout:
     cols = col_infos(prog)
     nplanes = 0 if regstage else sum(2 if c.lg == 3 else 1 for c in cols.values())
     need_bmw = _needs_word_bitmaps(prog)
@@ -128,7 +129,12 @@ def layout(prog, mode: int, U: int, hll_lds: bool, m: int, reg: bool = False, pi
     stage = W * wave_bytes
     ncopy = 1
     acc_bytes = 0
-    if mode == D.M_DENSE_LDS:
+    if mode == D.M_DENSE_LDS and shared:
+        # key spaces too large for per-wave copies (thousands of groups, e.g. SSB brand x year):
+        # ONE table per workgroup; lanes hitting the same group serialize in the LDS atomic unit,
+        # which is still far cheaper than contending HBM atomics on a few hundred hot addresses
+        acc_bytes = prog.G * prog.nslots * 8
+    elif mode == D.M_DENSE_LDS:
         base = prog.G * prog.nslots * 8 * W
         ncopy = 1 if reg else 16
         while ncopy > 1 and base * ncopy + hll_bytes + stage > budget:
@@ -138,7 +144,8 @@ def layout(prog, mode: int, U: int, hll_lds: bool, m: int, reg: bool = False, pi
     hll_off = (acc_bytes + 15) // 16 * 16
     cache_off = (hll_off + hll_bytes + 15) // 16 * 16
     total = cache_off + stage
-    return JitLayout(acc_off, acc_bytes, hll_off, hll_bytes, cache_off, wave_bytes, total, ncopy, pipe, regstage)
+    return JitLayout(acc_off, acc_bytes, hll_off, hll_bytes, cache_off, wave_bytes, total, ncopy, pipe, regstage,
+                     shared and mode == D.M_DENSE_LDS)
 
 
 def prefer_regstage(prog) -> bool:
@@ -376,7 +383,7 @@ class _Gen:
         word_filter = None if p.final_pre else self.word_expr(0, p.filter_len)
         pre = self.chunk_expr() if p.pre_len else None
         G, NS = p.G, p.nslots
-        NCT = W * lay.ncopy
+        NCT = 1 if lay.shared else W * lay.ncopy
         narrow = {s for s in range(NS) if _narrow_slot(p, s, self.cols)} if self.reg else set()
         for i in sorted(self.cols):
             L.append(f"  const unsigned char* c{i} = (const unsigned char*)d->cols[{i}].ptr;")
@@ -507,7 +514,10 @@ class _Gen:
         stage_bytes = 0 if self.regstage else U * NP * 256 * (2 if self.pipe else 1)
         out.append(f"  uint64_t* bmw = (uint64_t*)(wb + {stage_bytes});")
         out.append("  uint64_t* acc = (uint64_t*)lds;")
-        out.append(f"  const int copy = wave * {lay.ncopy} + (lane & {lay.ncopy - 1});")
+        if lay.shared:
+            out.append("  const int copy = 0;")
+        else:
+            out.append(f"  const int copy = wave * {lay.ncopy} + (lane & {lay.ncopy - 1});")
         out.append("  uint64_t* gacc = (uint64_t*)d->out_acc;")
         out.append("  uint64_t* hkeys = (uint64_t*)d->out_keys;")
         out.append("  const int64_t hcap = d->hash_cap;")
@@ -694,13 +704,14 @@ class JitScan:
 
     def __init__(self, prog, mode: int, U: int, hll_lds: bool, m: int, narrow4: bool, load: bool = True,
                  reg: Optional[bool] = None, pipe: bool = False, budget: int = 150 * 1024,
-                 regstage: bool = False):
-        self.reg = reg_eligible(prog, mode) if reg is None else reg
-        self.lay = layout(prog, mode, U, hll_lds, m, self.reg, pipe and not regstage, budget, regstage)
+                 regstage: bool = False, shared: bool = False):
+        self.reg = False if shared else (reg_eligible(prog, mode) if reg is None else reg)
+        self.lay = layout(prog, mode, U, hll_lds, m, self.reg, pipe and not regstage, budget, regstage, shared)
         if self.lay.total > 160 * 1024:
             raise ValueError(f"jit layout needs {self.lay.total} B of LDS")
         g = _Gen(prog, mode, U, hll_lds, narrow4, self.lay, m, self.reg)
-        tag = hashlib.sha1(repr((mode, U, self.reg, pipe, self.lay.ncopy, regstage)).encode()).hexdigest()[:6]
+        tag = hashlib.sha1(repr((mode, U, self.reg, pipe, self.lay.ncopy, regstage, self.lay.shared)).encode()
+                           ).hexdigest()[:6]
         self.name = f"sdo_jit_{tag}"
         self.src = g.source(self.name)
         self.handle = compile_source(self.src, self.name) if load else -1

@@ -236,7 +236,8 @@ class HiveThriftServer:
                     self.session.conf.set(k, v)
                 df = self.session.sql(stmt.strip().rstrip(";"))
                 pdf = df.to_pandas(token=op.token)
-                op.set_frame(df.columns, [t for _, t in df.schema], pdf)
+            # row-set encoding (host only) runs outside the engine lock, overlapping the next query
+            op.set_frame(df.columns, [t for _, t in df.schema], pdf)
             op.state = T.OP_FINISHED if not op.cancelled.is_set() else T.OP_CANCELED
         except Exception as e:  # noqa: BLE001
             op.error = f"{type(e).__name__}: {e}"

@@ -207,3 +207,25 @@ def pd_ms(s):
     import pandas as pd
 
     return int(pd.Timestamp(s).value // 1_000_000)
+
+
+@pytest.mark.parametrize("direction,metric", [("descending", "p"), ("ascending", "p"), ("descending", "c")])
+def test_device_topk_prune_matches_full_sort(ds_small, direction, metric):
+    """ORDER BY <aggregate> LIMIT k prunes the merged partials on the device (ties at the k-th value
+    kept) and must equal sorting every group."""
+    from spark_druid_olap_amd.engine.executor import Engine
+    from spark_druid_olap_amd.query import spec as S
+
+    dims = [S.DefaultDimensionSpec("o_orderkey")]
+    aggs = [S.FunctionAggregationSpec("doubleSum", "p", "l_extendedprice"), S.FunctionAggregationSpec("count", "c")]
+    ls = S.LimitSpec(25, [S.OrderByColumnSpec("p" if metric == "p" else "c", direction),
+                          S.OrderByColumnSpec("o_orderkey", "ascending")])
+    q = S.GroupByQuerySpec("tpch", dims, aggregations=aggs, intervals=["1992-01-01/1999-01-01"], limitSpec=ls)
+    full = Engine(use_native=False).execute(q.copy(limitSpec=None), ds_small)
+    assert full.num_rows > 4096
+    got = Engine(use_native=False).execute(q, ds_small)
+    rows = full.rows()
+    m = 1 if metric == "p" else 2
+    sign = -1 if direction == "descending" else 1
+    rows.sort(key=lambda r: (sign * r[m], r[0]))
+    assert got.rows() == rows[:25]

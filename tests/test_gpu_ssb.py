@@ -1,0 +1,53 @@
+"""SSB (BASELINE config 4) through the HIP kernels vs the plain-PyTorch reference executor on the
+same device shard: every query, including the shared-LDS-table key spaces (thousands of groups)
+and the topN / HLL count-distinct additions."""
+import pytest
+
+from spark_druid_olap_amd.engine.executor import Engine
+from spark_druid_olap_amd.models import ssb
+from spark_druid_olap_amd.session import Session
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sessions():
+    ds = ssb.to_datasource(ssb.generate_flat(0.05, "cuda"))
+    out = []
+    for native in (True, False):
+        s = Session(engine=Engine(use_native=native))
+        s.register_datasource(ds)
+        ssb.register(s)
+        out.append(s)
+    return ds, out
+
+
+def _norm(rows):
+    return sorted([tuple(round(v, 2) if isinstance(v, float) else v for v in r) for r in rows],
+                  key=lambda r: tuple((x is None, str(x)) for x in r))
+
+
+@pytest.mark.parametrize("name", [n for n, _ in ssb.ALL_QUERIES])
+def test_ssb_native_vs_reference(sessions, name):
+    _, (nat, ref) = sessions
+    q = dict(ssb.ALL_QUERIES)[name]
+    a, b = nat.sql(q).collect(), ref.sql(q).collect()
+    if name.startswith("HLL"):
+        ga, gb = {r[:-1]: r[-1] for r in a}, {r[:-1]: r[-1] for r in b}
+        assert ga.keys() == gb.keys()
+        for k in ga:
+            assert ga[k] == pytest.approx(gb[k], rel=1e-6)
+    else:
+        assert _norm(a) == _norm(b)
+
+
+def test_shared_lds_mode_chosen(sessions):
+    from spark_druid_olap_amd.engine.device_exec import PreparedScan
+    from spark_druid_olap_amd.ops import desc as D
+
+    ds, (nat, _) = sessions
+    for name in ("Q2.1", "TopN brand", "Q3.1"):
+        spec = nat.sql(dict(ssb.ALL_QUERIES)[name]).druid_query_specs()[0]
+        prep = nat.engine.prepare(spec, ds).scans[0][2]
+        assert isinstance(prep, PreparedScan)
+        assert prep.mode == D.M_DENSE_LDS and prep.shared and prep.jit is not None and prep.jit.lay.shared, name

@@ -30,3 +30,26 @@ def test_jit_kernels_compile_for_bench_queries(ds_small, tmp_path, monkeypatch):
         assert js.lay.total <= 160 * 1024
         assert "sdo_jit_" in js.src
     assert len(list(tmp_path.glob("*.co"))) >= 3
+
+
+def test_jit_shared_table_kernel_compiles(tmp_path, monkeypatch):
+    """Thousands-of-groups key spaces (SSB brand x year) use ONE LDS table per workgroup."""
+    from spark_druid_olap_amd.engine.executor import Engine
+    from spark_druid_olap_amd.models import ssb
+    from spark_druid_olap_amd.ops import desc as D
+    from spark_druid_olap_amd.ops import jit
+    from spark_druid_olap_amd.session import Session
+
+    monkeypatch.setenv("SDO_JIT_CACHE", str(tmp_path))
+    ds = ssb.to_datasource(ssb.generate_flat(0.002, "cpu"))
+    s = Session(engine=Engine(use_native=False))
+    s.register_datasource(ds)
+    ssb.register(s)
+    for name in ("Q2.1", "TopN brand"):
+        spec = s.sql(dict(ssb.ALL_QUERIES)[name]).druid_query_specs()[0]
+        prog = s.engine.prepare(spec, ds).scans[0][1]
+        assert prog.G * prog.nslots * 8 * 8 > 64 * 1024  # per-wave copies would not fit
+        js = jit.JitScan(prog, D.M_DENSE_LDS, 4, False, 2048, True, load=False, shared=True,
+                         budget=159 * 1024)
+        assert js.lay.shared and js.lay.acc_bytes == prog.G * prog.nslots * 8
+        assert "const int copy = 0;" in js.src and js.lay.total <= 160 * 1024
