@@ -33,8 +33,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--sf", type=float, default=float(os.environ.get("SDO_BENCH_SF", "100")))
     ap.add_argument("--mode", choices=["sql", "spec"], default=os.environ.get("SDO_BENCH_MODE", "sql"))
-    ap.add_argument("--model", choices=["tpch", "ssb"], default=os.environ.get("SDO_BENCH_MODEL", "tpch"),
-                    help="tpch: the reference's 8-query TPC-H suite (headline); ssb: BASELINE config 4")
+    ap.add_argument("--model", choices=["tpch", "ssb", "tpch22"], default=os.environ.get("SDO_BENCH_MODEL", "tpch"),
+                    help="tpch: the reference's 8-query TPC-H suite (headline); ssb: BASELINE config 4; "
+                         "tpch22: the full 22-query TPC-H sweep over the flattened index (BASELINE config 2)")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
 
@@ -50,8 +51,9 @@ def main():
     from spark_druid_olap_amd.engine.executor import Engine
     from spark_druid_olap_amd.models import ssb, tpch
 
-    if args.model == "ssb":
+    if args.model in ("ssb", "tpch22"):
         args.mode = "sql"
+    if args.model == "ssb":
         flat = ssb.generate_flat(args.sf, dev, rank=world.rank, world=world.size)
         ds = ssb.to_datasource(flat)
     else:
@@ -73,6 +75,19 @@ def main():
         sess.register_datasource(ds)
         ssb.register(sess)
         queries = [(name, sess.sql(q).prepared()) for name, q in ssb.ALL_QUERIES]
+        for name, df in queries:
+            assert df.druid_queries(), f"{name} was not pushed to the GPU engine"
+    elif args.model == "tpch22":
+        from spark_druid_olap_amd.models import tpch22
+        from spark_druid_olap_amd.session import Session
+
+        # exact count(distinct) (TPC-H answers), unlike the reference's 8-query benchmark
+        sess = Session(engine=engine)
+        sess.register_datasource(ds)
+        sess.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)  # schema only
+        sess.sql(tpch.druid_ddl(source="orderLineItemPartSupplierBase", datasource="tpch",
+                                with_column_mapping=False))
+        queries = [(name, sess.sql(q).prepared()) for name, q in tpch22.QUERIES]
         for name, df in queries:
             assert df.druid_queries(), f"{name} was not pushed to the GPU engine"
     elif args.mode == "sql":
@@ -144,6 +159,11 @@ def main():
             metric = "ssb_17query_geomean_latency_ms"
             model = f"SSB lineorder star schema, SF{args.sf:g} per GPU (SF{args.sf * world.size:g} total)"
             vs = None  # the reference publishes no SSB numbers
+        elif args.model == "tpch22":
+            metric = "tpch_flat_22query_geomean_latency_ms"
+            model = (f"TPC-H 22 queries over flattened orderLineItemPartSupplier, SF{args.sf:g} per GPU "
+                     f"(SF{args.sf * world.size:g} total)")
+            vs = None  # the reference publishes no 22-query numbers
         else:
             metric = "tpch_flat_8query_geomean_latency_ms"
             model = (f"TPC-H flattened orderLineItemPartSupplier, SF{args.sf:g} per GPU "

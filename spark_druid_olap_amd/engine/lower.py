@@ -286,6 +286,7 @@ class ScanProgram:
     keepalive: List[torch.Tensor] = field(default_factory=list)
     thetas: List[Tuple[str, str, int]] = field(default_factory=list)  # (name, column, size)
     luts: Dict[str, torch.Tensor] = field(default_factory=dict)       # dim -> f64 value per dictionary id
+    lut_ptrs: Dict[float, torch.Tensor] = field(default_factory=dict)  # E_LUT operand -> its table
 
     def col(self, name: str) -> int:
         """Absolute descriptor column index of `name` in the current section."""
@@ -355,6 +356,8 @@ class Lowerer:
             return b_and(parts) if f.type == "and" else b_or(parts)
         if isinstance(f, S.NotFilterSpec):
             return b_not(self._filter_ir(f.field))
+        if isinstance(f, S.ExpressionFilterSpec):
+            return self._expression_filter(f.expression)
         dim = getattr(f, "dimension", None)
         if dim == TIME or (dim is not None and dim not in ds.dims and dim not in ds.metrics and dim == "timestamp"):
             return self._time_filter(f)
@@ -422,6 +425,16 @@ class Lowerer:
 
             return ("ids", dim, d.eval_mask(pred))
         if isinstance(f, S.JavascriptFilterSpec):
+            pl = getattr(f, "_pylike", None)
+            if pl is not None and hasattr(d, "like_mask"):
+                # structured LIKE over a lazy phrase dictionary (no per-entry strings)
+                m = d.like_mask(pl[0])
+                if m is not None:
+                    if pl[1]:
+                        m = ~m
+                        if d.has_null:
+                            m[0] = False
+                    return ("ids", dim, m)
             pv = getattr(f, "_pyvec", None)
             if pv is not None:  # vectorised dictionary-domain predicate (SQL planner)
                 return ("ids", dim, np.asarray(pv(d.all_values()), dtype=bool))
@@ -431,6 +444,38 @@ class Lowerer:
                 py = lambda v: bool(jf(v))  # noqa: E731
             return ("ids", dim, d.eval_mask(py))
         raise LoweringError(f"unsupported filter {type(f).__name__}")
+
+    def _expression_filter(self, text: str) -> tuple:
+        """``<arith> <cmp> <arith>`` -> ("fexpr", ast of lhs - rhs, lo, hi, flags): a row predicate
+        the scan kernel evaluates in its expression VM (F_EXPR).  Two bare string dimensions are
+        compared through rank tables over the union of their dictionaries (exact string order /
+        equality, ISO dates included); anything else compares numeric values (metrics, numeric
+        dimension values through E_LUT)."""
+        m = re.match(r"^(.*?)(==|!=|<=|>=|<|>)(.*)$", text.strip(), re.S)
+        if m is None:
+            raise LoweringError(f"expression filter needs one comparison: {text!r}")
+        lhs, op, rhs = m.group(1).strip(), m.group(2), m.group(3).strip()
+        try:
+            la, ra = parse_expr(lhs), parse_expr(rhs)
+        except JSError as e:
+            raise LoweringError(f"expression filter not translatable: {e}")
+        for a in (la, ra):
+            for name in _ast_cols(a):
+                if name != TIME and name not in self.ds.dims and name not in self.ds.metrics:
+                    raise LoweringError(f"expression filter over unknown column {name!r}")
+        if la[0] == "col" and ra[0] == "col" and la[1] in self.ds.dims and ra[1] in self.ds.dims and \
+                (self.ds.dims[la[1]].dictionary.vtype == "string" or self.ds.dims[ra[1]].dictionary.vtype == "string"):
+            lt, rt = rank_luts(self.ds, la[1], ra[1])
+            la, ra = ("lut", la[1], lt), ("lut", ra[1], rt)
+        ast = ("sub", la, ra)
+        inf = math.inf
+        lo, hi, flags = {"<": (-inf, 0.0, 2), "<=": (-inf, 0.0, 0), ">": (0.0, inf, 1), ">=": (0.0, inf, 0),
+                         "==": (0.0, 0.0, 0), "!=": (0.0, 0.0, 0)}[op]
+        leaf = ("fexpr", ast, lo, hi, flags)
+        if op == "!=":
+            # NaN (NULL) operands fail both the leaf and its negation, like SQL's 3-valued logic
+            return b_and([b_not(leaf), ("fexpr", ast, -inf, inf, 0)])
+        return leaf
 
     def _time_values(self) -> np.ndarray:
         if self._tv_cache is None:
@@ -580,6 +625,12 @@ class Lowerer:
             ci = prog.col(x[1])
             prog.fops.append((D.F_FLT_RANGE, ci, int(x[4]), 0, 0, float(x[2]), float(x[3]), None))
             return 1
+        if k == "fexpr":
+            eops = self._emit_expr(prog, x[1], {})
+            off = len(prog.eops)
+            prog.eops.extend(eops)
+            prog.fops.append((D.F_EXPR, 0, int(x[4]), off, len(eops), float(x[2]), float(x[3]), None))
+            return 1
         raise LoweringError(f"bad filter IR {k}")
 
     def bitmap_plan(self, dim: str, mask: np.ndarray):
@@ -698,6 +749,8 @@ class Lowerer:
         fn = getattr(dspec, "extractionFn", None) if isinstance(dspec, S.ExtractionDimensionSpec) else None
         if dim == TIME:
             return self._time_key(name, fn, ivs)
+        if dim in ds.metrics and dim not in ds.dims and fn is None:
+            return self._metric_key(name, dim)
         if dim not in ds.dims:
             raise LoweringError(f"group by unknown dimension {dim!r}")
         d = ds.dims[dim].dictionary
@@ -719,6 +772,28 @@ class Lowerer:
         pos = {v: i + (1 if has_null else 0) for i, v in enumerate(uniq)}
         remap = np.array([0 if v is None else pos[v] for v in vals], dtype=np.int32)
         return KeyComp(name, D.K_REMAP, dim, len(dd), remap=remap, decoder=lambda ids, _d=dd: DictColumn(ids, _d))
+
+    def _metric_key(self, name: str, metric: str) -> KeyComp:
+        """Group by an integral metric (K_INT over its stored value range, <= 2^20 values)."""
+        m = self.ds.metrics[metric]
+        if not m.is_integral:
+            raise LoweringError(f"cannot group by floating metric {metric!r}")
+        rng = getattr(m, "_value_range", None)
+        if rng is None:
+            t = column_tensor(self.ds, metric)
+            rng = (int(t.min().item()), int(t.max().item())) if t.numel() else (0, 0)
+            m._value_range = rng  # type: ignore[attr-defined]
+        lo, hi = rng
+        card = hi - lo + 1
+        if card > (1 << 20):
+            raise LoweringError(f"metric {metric!r} spans {card} values: too many to group by")
+        scale = m.scale if m.kind == "decimal" else 0
+
+        def decode(ids, _lo=lo, _sc=scale):
+            v = np.asarray(ids, dtype=np.int64) + _lo
+            return v / (10.0 ** _sc) if _sc else v
+
+        return KeyComp(name, D.K_INT, metric, card, base=lo, decoder=decode)
 
     def _time_key(self, name, fn, ivs: List[Interval]) -> KeyComp:
         lo, hi = self._data_span(ivs)
@@ -918,6 +993,13 @@ class Lowerer:
             if k == "const":
                 out.append((D.E_CONST, 0, float(n[1])))
                 return 1
+            if k == "lut":  # explicit per-dictionary table (rank_luts)
+                t = n[2]
+                prog.keepalive.append(t)
+                c = _ptr_as_double(t.data_ptr())
+                prog.lut_ptrs[c] = t
+                out.append((D.E_LUT, prog.col(n[1]), c))
+                return 1
             if k == "col":
                 name = mapping.get(n[1], n[1])
                 if name == TIME:
@@ -931,7 +1013,9 @@ class Lowerer:
                     lut = dim_numeric_lut(self.ds, name)
                     prog.luts[name] = lut
                     prog.keepalive.append(lut)
-                    out.append((D.E_LUT, prog.col(name), _ptr_as_double(lut.data_ptr())))
+                    c = _ptr_as_double(lut.data_ptr())
+                    prog.lut_ptrs[c] = lut
+                    out.append((D.E_LUT, prog.col(name), c))
                     return 1
                 if name not in self.ds.metrics:
                     raise LoweringError(f"unknown column {name!r} in expression")
@@ -1084,6 +1168,37 @@ def _numeric_value(v) -> float:
         except Exception:  # noqa: BLE001
             return math.nan
     return math.nan
+
+
+def _ast_cols(a) -> List[str]:
+    if a[0] == "col":
+        return [a[1]]
+    if a[0] in ("const", "lut"):
+        return []
+    return [c for x in a[1:] for c in _ast_cols(x)]
+
+
+def rank_luts(ds: DataSource, a: str, b: str) -> Tuple[torch.Tensor, torch.Tensor]:
+    """f64 rank of every dictionary value of dims a and b in the sorted union of both
+    dictionaries (NULL -> NaN): comparing ranks == comparing the values as strings."""
+    key = ("_ranklut", a, b)
+    cache = ds.__dict__.setdefault("_lut_cache", {})
+    if key in cache:
+        return cache[key]
+    va = ds.dims[a].dictionary.all_values()
+    vb = ds.dims[b].dictionary.all_values()
+
+    def strs(vs):
+        return [None if v is None else str(v) for v in vs]
+
+    sa, sb = strs(va), strs(vb)
+    union = sorted({v for v in sa + sb if v is not None})
+    pos = {v: float(i) for i, v in enumerate(union)}
+    dev = ds.dims[a].ids.device
+    ta = torch.tensor([pos[v] if v is not None else math.nan for v in sa], dtype=torch.float64, device=dev)
+    tb = torch.tensor([pos[v] if v is not None else math.nan for v in sb], dtype=torch.float64, device=dev)
+    cache[key] = (ta, tb)
+    return ta, tb
 
 
 def dim_numeric_lut(ds: DataSource, dim: str) -> torch.Tensor:

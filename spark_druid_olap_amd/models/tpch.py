@@ -24,7 +24,7 @@ import torch
 
 from ..query.intervals import civil_from_days, days_from_civil
 from ..segment.datasource import DataSource, make_datasource
-from ..segment.dictionary import LONG, STRING, DOUBLE, Dictionary, FormattedDictionary, RangeDictionary
+from ..segment.dictionary import LONG, STRING, DOUBLE, Dictionary, FormattedDictionary, RangeDictionary, WordsDictionary
 
 NATIONS = [("ALGERIA", 0), ("ARGENTINA", 1), ("BRAZIL", 1), ("CANADA", 1), ("EGYPT", 4), ("ETHIOPIA", 0),
            ("FRANCE", 3), ("GERMANY", 3), ("INDIA", 2), ("INDONESIA", 2), ("IRAN", 4), ("IRAQ", 4), ("JAPAN", 2),
@@ -41,6 +41,27 @@ TYPE_S2 = ["ANODIZED", "BURNISHED", "PLATED", "POLISHED", "BRUSHED"]
 TYPE_S3 = ["TIN", "NICKEL", "BRASS", "STEEL", "COPPER"]
 CONT_S1 = ["SM", "LG", "MED", "JUMBO", "WRAP"]
 CONT_S2 = ["CASE", "BOX", "BAG", "JAR", "PKG", "PACK", "CAN", "DRUM"]
+
+# TPC-H 4.2.3: the 92 part-name colours (p_name = 5 of them)
+P_NAME_WORDS = [
+    "almond", "antique", "aquamarine", "azure", "beige", "bisque", "black", "blanched", "blue", "blush", "brown",
+    "burlywood", "burnished", "chartreuse", "chiffon", "chocolate", "coral", "cornflower", "cornsilk", "cream",
+    "cyan", "dark", "deep", "dim", "dodger", "drab", "firebrick", "floral", "forest", "frosted", "gainsboro",
+    "ghost", "goldenrod", "green", "grey", "honeydew", "hot", "indian", "ivory", "khaki", "lace", "lavender",
+    "lawn", "lemon", "light", "lime", "linen", "magenta", "maroon", "medium", "metallic", "midnight", "mint",
+    "misty", "moccasin", "navajo", "navy", "olive", "orange", "orchid", "pale", "papaya", "peach", "peru", "pink",
+    "plum", "powder", "puff", "purple", "red", "rose", "rosy", "royal", "saddle", "salmon", "sandy", "seashell",
+    "sienna", "sky", "slate", "smoke", "snow", "spring", "steel", "tan", "thistle", "tomato", "turquoise",
+    "violet", "wheat", "white", "yellow"]
+# comment text: a slice of the TPC-H 4.2.2.10 text-grammar vocabulary (nouns, verbs, adjectives,
+# adverbs, prepositions) including the words Q13 / Q16 look for
+COMMENT_WORDS = [
+    "foxes", "ideas", "theodolites", "pinto", "beans", "instructions", "dependencies", "excuses", "platelets",
+    "asymptotes", "courts", "dolphins", "packages", "requests", "accounts", "deposits", "sleep", "wake", "are",
+    "cajole", "haggle", "nag", "use", "boost", "affix", "detect", "integrate", "furious", "sly", "careful",
+    "blithe", "quick", "fluffy", "slow", "quiet", "ruthless", "thin", "close", "regular", "special", "pending",
+    "unusual", "express", "final", "ironic", "even", "bold", "silent", "about", "above", "according", "across",
+    "after", "against", "along", "among", "around", "Customer", "Complaints", "Recommends"]
 
 START_DAY = days_from_civil(1992, 1, 1)
 CURRENT_DAY = days_from_civil(1995, 6, 17)
@@ -70,7 +91,7 @@ INDEX_METRICS = {
 BENCH_INDEX_DIMS = ["o_orderkey", "o_custkey", "o_orderdate", "o_orderstatus", "o_orderpriority", "o_clerk",
                     "o_shippriority", "o_comment", "l_partkey", "l_suppkey", "l_linenumber", "l_returnflag",
                     "l_linestatus", "l_commitdate", "l_receiptdate", "l_shipinstruct", "l_shipmode", "l_comment",
-                    "ps_comment", "s_name", "s_address", "s_phone", "s_comment", "s_nation", "s_region", "p_name",
+                    "ps_comment", "s_name", "s_address", "s_phone", "s_acctbal", "s_comment", "s_nation", "s_region", "p_name",
                     "p_mfgr", "p_brand", "p_type", "p_container", "p_comment", "c_name", "c_address", "c_phone",
                     "c_mktsegment", "c_comment", "c_nation", "c_region"]
 BENCH_INDEX_METRICS = {
@@ -163,6 +184,15 @@ class FlatTPCH:
     dims: Dict[str, Tuple[Dictionary, torch.Tensor]] = field(default_factory=dict)
     nums: Dict[str, Tuple[torch.Tensor, str, int]] = field(default_factory=dict)  # tensor, kind, scale
     counts: Dict[str, int] = field(default_factory=dict)
+
+
+def _bijection(x: torch.Tensor, n: int, salt: int) -> torch.Tensor:
+    """x -> (a x + b) mod n, a permutation of [0, n) (a coprime with n): scatters entity keys over
+    a phrase dictionary so the leading words do not track the key order."""
+    for a in (1_000_003, 999_983, 1_000_033, 998_999, 1_000_037):
+        if math.gcd(a, n) == 1:
+            break
+    return torch.remainder(x.to(torch.int64) * a + salt * 7_919, n)
 
 
 def generate_flat(sf: float = 1.0, device="cpu", rank: int = 0, world: int = 1, seed: int = 20260101,
@@ -265,7 +295,7 @@ def generate_flat(sf: float = 1.0, device="cpu", rank: int = 0, world: int = 1, 
     dim("o_orderpriority", Dictionary(PRIORITIES), opri[oidx].to(torch.uint8))
     dim("o_clerk", FormattedDictionary("Clerk#", 9, clerks, start=1), clerk[oidx])
     dim("o_shippriority", Dictionary([0], LONG), torch.zeros(L, dtype=torch.uint8, device=dev))
-    dim("o_comment", FormattedDictionary("ocomment-", 10, tot_orders, start=1), (ok_l - 1).to(torch.int32))
+    dim("o_comment", WordsDictionary(COMMENT_WORDS, 6, tot_orders), _bijection(ok_l - 1, tot_orders, 1).to(torch.int32))
     # lineitem
     num("l_partkey", pk.to(torch.int32), "long")
     num("l_suppkey", sk.to(torch.int32), "long")
@@ -308,7 +338,7 @@ def generate_flat(sf: float = 1.0, device="cpu", rank: int = 0, world: int = 1, 
     dim("s_address", FormattedDictionary("saddr-", 9, Sn, start=1), (sk - 1).to(torch.int32))
     dim("s_phone", FormattedDictionary("sphone-", 9, Sn, start=1), (sk - 1).to(torch.int32))
     num("s_acctbal", (khash(sk, 12) % 1099999 - 99999).to(torch.int32), "decimal", 2)
-    dim("s_comment", FormattedDictionary("scomment-", 9, Sn, start=1), (sk - 1).to(torch.int32))
+    dim("s_comment", WordsDictionary(COMMENT_WORDS, 6, Sn), _bijection(sk - 1, Sn, 2).to(torch.int32))
     dim("s_nation", nat_d, nat_remap_t[s_nk].to(torch.uint8))
     dim("s_region", reg_d, reg_of_nation[s_nk].to(torch.uint8))
     # part
@@ -317,7 +347,7 @@ def generate_flat(sf: float = 1.0, device="cpu", rank: int = 0, world: int = 1, 
     conts = [f"{a} {b}" for a in CONT_S1 for b in CONT_S2]
     cont_d, cont_remap = _sorted_codes(conts)
     mfgr = khash(pk, 5) % 5
-    dim("p_name", FormattedDictionary("part-", 9, P, start=1), (pk - 1).to(torch.int32))
+    dim("p_name", WordsDictionary(P_NAME_WORDS, 5, P), _bijection(pk - 1, P, 3).to(torch.int32))
     dim("p_mfgr", Dictionary([f"Manufacturer#{i}" for i in range(1, 6)]), mfgr.to(torch.uint8))
     dim("p_brand", Dictionary([f"Brand#{i}{j}" for i in range(1, 6) for j in range(1, 6)]),
         (mfgr * 5 + khash(pk, 6) % 5).to(torch.uint8))

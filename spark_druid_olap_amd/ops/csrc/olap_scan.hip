@@ -303,6 +303,56 @@ __device__ __forceinline__ uint64_t eval_chunk_program(const ScanDesc* __restric
   return st.s[0][0];
 }
 
+// float expression VM over staged columns (Druid javascript aggregators over several columns,
+// reference sd/jscodegen/JSAggGenerator.scala:37-60)
+template <int U>
+__device__ __forceinline__ double eval_expr(const ScanDesc* __restrict__ d, int off, int len, const unsigned char* wb,
+                                            int u, int lane) {
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  for (int i = off; i < off + len; ++i) {
+    const EOp e = d->eops[i];
+    if (e.op == E_COL || e.op == E_CONST || e.op == E_LUT) {
+      double v = e.c;
+      if (e.op == E_LUT) {
+        const double* lut = (const double*)__double_as_longlong(e.c);
+        v = lut[col_int<U>(d, wb, e.col, u, lane)];
+      } else if (e.op == E_COL) {
+        v = col_dbl<U>(d, wb, e.col, u, lane);
+        if (e.c != 0.0) v *= e.c;  // decimal scale
+      }
+      s3 = s2; s2 = s1; s1 = s0; s0 = v;
+    } else if (e.op == E_NEG) {
+      s0 = -s0;
+    } else if (e.op == E_ABS) {
+      s0 = fabs(s0);
+    } else if (e.op >= E_FLOOR && e.op <= E_EXP) {
+      switch (e.op) {
+        case E_FLOOR: s0 = floor(s0); break;
+        case E_CEIL: s0 = ceil(s0); break;
+        case E_SQRT: s0 = sqrt(s0); break;
+        case E_LOG: s0 = log(s0); break;
+        default: s0 = exp(s0); break;
+      }
+    } else {
+      const double a = s1, b = s0;
+      double r;
+      switch (e.op) {
+        case E_ADD: r = a + b; break;
+        case E_SUB: r = a - b; break;
+        case E_MUL: r = a * b; break;
+        case E_DIV: r = a / b; break;
+        case E_MIN: r = fmin(a, b); break;
+        case E_MOD: r = fmod(a, b); break;
+        case E_PMOD: { const double m = fmod(a, b); r = m < 0.0 ? fmod(m + b, b) : m; } break;  // Spark Pmod
+        case E_POW: r = pow(a, b); break;
+        default: r = fmax(a, b); break;
+      }
+      s0 = r; s1 = s2; s2 = s3;
+    }
+  }
+  return s0;
+}
+
 // word level: lane = one row; bitmap leaves read (uniform) from the chunk-level words in LDS
 template <int U>
 __device__ __forceinline__ void eval_word_program(const ScanDesc* __restrict__ d, int off, int len,
@@ -355,6 +405,17 @@ __device__ __forceinline__ void eval_word_program(const ScanDesc* __restrict__ d
         }
         st.push(m);
       } break;
+      case F_EXPR: {
+        const bool los = f.flags & 1, his = f.flags & 2;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const double v = eval_expr<U>(d, (int)f.lo, (int)f.hi, wb, u, lane);
+          const bool a = los ? (v > f.flo) : (v >= f.flo);
+          const bool b = his ? (v < f.fhi) : (v <= f.fhi);
+          m[u] = __ballot(a && b);
+        }
+        st.push(m);
+      } break;
       case F_AND:
         st.template binop<0>();
         break;
@@ -373,55 +434,6 @@ __device__ __forceinline__ void eval_word_program(const ScanDesc* __restrict__ d
   for (int u = 0; u < U; ++u) out[u] = st.s[0][u];
 }
 
-// float expression VM over staged columns (Druid javascript aggregators over several columns,
-// reference sd/jscodegen/JSAggGenerator.scala:37-60)
-template <int U>
-__device__ __forceinline__ double eval_expr(const ScanDesc* __restrict__ d, int off, int len, const unsigned char* wb,
-                                            int u, int lane) {
-  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-  for (int i = off; i < off + len; ++i) {
-    const EOp e = d->eops[i];
-    if (e.op == E_COL || e.op == E_CONST || e.op == E_LUT) {
-      double v = e.c;
-      if (e.op == E_LUT) {
-        const double* lut = (const double*)__double_as_longlong(e.c);
-        v = lut[col_int<U>(d, wb, e.col, u, lane)];
-      } else if (e.op == E_COL) {
-        v = col_dbl<U>(d, wb, e.col, u, lane);
-        if (e.c != 0.0) v *= e.c;  // decimal scale
-      }
-      s3 = s2; s2 = s1; s1 = s0; s0 = v;
-    } else if (e.op == E_NEG) {
-      s0 = -s0;
-    } else if (e.op == E_ABS) {
-      s0 = fabs(s0);
-    } else if (e.op >= E_FLOOR && e.op <= E_EXP) {
-      switch (e.op) {
-        case E_FLOOR: s0 = floor(s0); break;
-        case E_CEIL: s0 = ceil(s0); break;
-        case E_SQRT: s0 = sqrt(s0); break;
-        case E_LOG: s0 = log(s0); break;
-        default: s0 = exp(s0); break;
-      }
-    } else {
-      const double a = s1, b = s0;
-      double r;
-      switch (e.op) {
-        case E_ADD: r = a + b; break;
-        case E_SUB: r = a - b; break;
-        case E_MUL: r = a * b; break;
-        case E_DIV: r = a / b; break;
-        case E_MIN: r = fmin(a, b); break;
-        case E_MOD: r = fmod(a, b); break;
-        case E_PMOD: { const double m = fmod(a, b); r = m < 0.0 ? fmod(m + b, b) : m; } break;  // Spark Pmod
-        case E_POW: r = pow(a, b); break;
-        default: r = fmax(a, b); break;
-      }
-      s0 = r; s1 = s2; s2 = s3;
-    }
-  }
-  return s0;
-}
 
 // ---------------------------------------------------------------------------------------------
 template <int U>

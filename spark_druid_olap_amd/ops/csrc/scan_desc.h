@@ -50,7 +50,8 @@ enum FOpCode : int32_t {
   F_OR = 7,
   F_NOT = 8,
   F_FALSE = 9,
-  F_BITMAP_OR = 10  // push OR of `hi` consecutive bitmap rows starting at bits (stride lo words)
+  F_BITMAP_OR = 10,  // push OR of `hi` consecutive bitmap rows starting at bits (stride lo words)
+  F_EXPR = 11        // push flo <= expr(eops[lo, lo+hi)) <= fhi (flags as F_FLT_RANGE; NaN fails)
 };
 
 struct ColRef {

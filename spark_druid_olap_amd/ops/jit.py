@@ -238,6 +238,12 @@ class _Gen:
                 hi_c = "<" if flags & 2 else "<="
                 st.append(f"([&]() {{ const double v = {self.dval(col)}; "
                           f"return (uint64_t)__ballot(v {lo_c} {_dlit(fa)} && v {hi_c} {_dlit(fb)}); }}())")
+            elif op == D.F_EXPR:
+                lo_c = ">" if flags & 1 else ">="
+                hi_c = "<" if flags & 2 else "<="
+                ev = self.expr(self.p.eops[int(a):int(a) + int(b)], int(a))
+                st.append(f"([&]() {{ const double v = {ev}; "
+                          f"return (uint64_t)__ballot(v {lo_c} {_dlit(fa)} && v {hi_c} {_dlit(fb)}); }}())")
             elif op in (D.F_AND, D.F_OR):
                 y, x = st.pop(), st.pop()
                 st.append(f"({x} {'&' if op == D.F_AND else '|'} {y})")

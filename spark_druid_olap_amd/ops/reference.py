@@ -138,7 +138,48 @@ def eval_bexpr(prog, x, rows: torch.Tensor) -> torch.Tensor:
         lo_ok = v > x[2] if x[4] & 1 else v >= x[2]
         hi_ok = v < x[3] if x[4] & 2 else v <= x[3]
         return lo_ok & hi_ok
+    if k == "fexpr":
+        v = _ast_values(prog, x[1], rows)
+        lo_ok = v > x[2] if x[4] & 1 else v >= x[2]
+        hi_ok = v < x[3] if x[4] & 2 else v <= x[3]
+        return lo_ok & hi_ok
     raise ValueError(k)
+
+
+def _ast_values(prog, n, rows: torch.Tensor) -> torch.Tensor:
+    """f64 value per row of an expression AST (expression filters; same value model as the
+    device VM: metrics with decimal scale, dimensions through their f64 dictionary table)."""
+    from ..engine.lower import dim_numeric_lut
+
+    k = n[0]
+    if k == "const":
+        return torch.full((rows.numel(),), float(n[1]), dtype=torch.float64, device=rows.device)
+    if k == "lut":
+        ids = _col(prog, n[1])[rows].to(torch.int64)
+        return n[2].to(rows.device)[ids]
+    if k == "col":
+        name = n[1]
+        ds = prog.ds
+        if name in ds.dims:
+            ids = _col(prog, name)[rows].to(torch.int64)
+            return dim_numeric_lut(ds, name).to(rows.device)[ids]
+        if name == "__time":
+            return ds.time[rows].to(torch.float64) * float(ds.time_unit_ms)
+        v = _col(prog, name)[rows].to(torch.float64)
+        m = ds.metrics.get(name)
+        if m is not None and m.kind == "decimal" and m.scale:
+            v = v * (10.0 ** -m.scale)
+        return v
+    if k in ("neg", "abs", "floor", "ceil", "sqrt", "log", "exp"):
+        a = _ast_values(prog, n[1], rows)
+        return {"neg": torch.neg, "abs": torch.abs, "floor": torch.floor, "ceil": torch.ceil, "sqrt": torch.sqrt,
+                "log": torch.log, "exp": torch.exp}[k](a)
+    a, b = _ast_values(prog, n[1], rows), _ast_values(prog, n[2], rows)
+    if k == "pmod":
+        m = torch.fmod(a, b)
+        return torch.where(m < 0, torch.fmod(m + b, b), m)
+    return {"add": torch.add, "sub": torch.sub, "mul": torch.mul, "div": torch.div, "min": torch.minimum,
+            "max": torch.maximum, "mod": torch.fmod, "pow": torch.pow}[k](a, b)
 
 
 def _time_field(ms: torch.Tensor, kc) -> torch.Tensor:
@@ -223,7 +264,10 @@ def _expr_values(prog, eops, rows: torch.Tensor) -> torch.Tensor:
     for op, col, c in eops:
         if op == D.E_LUT:
             ids = _col(prog, prog.colname(col))[rows].to(torch.int64)
-            st.append(prog.luts[prog.colname(col)].to(rows.device)[ids])
+            lut = prog.lut_ptrs.get(c)
+            if lut is None:
+                lut = prog.luts[prog.colname(col)]
+            st.append(lut.to(rows.device)[ids])
         elif op == D.E_COL:
             v = _col(prog, prog.colname(col))[rows].to(torch.float64)
             st.append(v * c if c != 0.0 else v)

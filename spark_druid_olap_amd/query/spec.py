@@ -296,6 +296,73 @@ class JavascriptFilterSpec(Spec, _Decodable):
     type: str = "javascript"
 
 
+@_register("filter", "expression")
+@dataclass
+class ExpressionFilterSpec(Spec, _Decodable):
+    """Row predicate over several columns, ``<arith> <cmp> <arith>`` (Druid's native expression
+    filter syntax, arithmetic in the javascript-aggregator subset).  The reference cannot push
+    these (a Druid javascript filter sees one dimension, ``sd/jscodegen/JSCodeGenerator.scala``);
+    here they run in the scan kernel's expression VM (TPC-H Q4/Q12 ``l_commitdate < l_receiptdate``,
+    Q5 ``c_nation = s_nation``)."""
+    expression: str
+    type: str = "expression"
+
+
+@dataclass
+class DeferredFilterSpec(Spec):
+    """A filter whose operand is an uncorrelated scalar subquery (TPC-H Q22 ``c_acctbal >
+    (select avg(c_acctbal) ...)``).  Spark runs such subqueries before the main plan
+    (``ScalarSubquery``); the planner keeps the predicate here with ``build(values)`` -> concrete
+    filter, and the executor runs the subqueries (pushed GPU queries themselves) and calls
+    ``resolve_deferred`` before lowering.  Never reaches the engine unresolved."""
+    expression: str
+    type: str = "deferred"
+
+    def __post_init__(self):
+        self.subqueries: list = []
+        self.build = None
+
+
+def find_deferred(spec) -> List["DeferredFilterSpec"]:
+    out: List[DeferredFilterSpec] = []
+
+    def go(v):
+        if isinstance(v, DeferredFilterSpec):
+            out.append(v)
+        elif isinstance(v, Spec):
+            for f in dataclasses.fields(v):
+                go(getattr(v, f.name))
+        elif isinstance(v, (list, tuple)):
+            for x in v:
+                go(x)
+
+    go(spec)
+    return out
+
+
+def resolve_deferred(spec, values: Dict[int, Any]):
+    """Copy of ``spec`` with every DeferredFilterSpec replaced by ``build(values)`` (``values``:
+    id(subquery expr) -> its scalar result).  Unchanged sub-specs are shared, not copied."""
+
+    def go(v):
+        if isinstance(v, DeferredFilterSpec):
+            return v.build(values)
+        if isinstance(v, Spec):
+            changes = {}
+            for f in dataclasses.fields(v):
+                x = getattr(v, f.name)
+                y = go(x)
+                if y is not x:
+                    changes[f.name] = y
+            return v.copy(**changes) if changes else v
+        if isinstance(v, list):
+            ys = [go(x) for x in v]
+            return ys if any(a is not b for a, b in zip(ys, v)) else v
+        return v
+
+    return go(spec)
+
+
 @_register("filter", "bound")
 @dataclass
 class BoundFilterSpec(Spec, _Decodable):

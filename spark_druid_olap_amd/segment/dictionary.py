@@ -16,7 +16,8 @@ high-cardinality columns (values are generated from the id and are monotone in i
 """
 from __future__ import annotations
 
-from typing import Any, Callable, Iterable, Optional, Sequence, Tuple
+import math
+from typing import Any, Callable, Dict, Iterable, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -170,6 +171,8 @@ class Dictionary:
             return FormattedDictionary(d["prefix"], d["width"], d["n"], d.get("start", 0), d.get("suffix", ""))
         if k == "range":
             return RangeDictionary(d["start"], d["n"])
+        if k == "words":
+            return WordsDictionary(d["vocab"], d["k"], d["n"])
         return Dictionary(d["values"], d["vtype"], d.get("has_null", False))
 
     @staticmethod
@@ -356,3 +359,209 @@ def id_dtype_for(card: int) -> str:
     if card <= 32767:
         return "int16"
     return "int32"
+
+
+class WordsDictionary(Dictionary):
+    """Lazy dictionary of k-word phrases over a vocabulary (TPC-H ``p_name`` colour names, comment
+    text).  Entry i is the i-th of n phrases spread evenly over the V^k word combinations: the
+    combination index ``i * step`` written in base V picks the words (most significant first).
+    With the vocabulary sorted and all words free of characters below ' ', phrase order == tuple
+    order == id order, so the dictionary stays sorted like every Druid dictionary.
+
+    LIKE patterns whose literal pieces contain no space are evaluated structurally
+    (``like_mask``): a per-word automaton table over (pieces matched so far, word) -- V x (m+2)
+    entries -- is applied column by column to the k word codes of all n entries, instead of
+    materializing n strings (20M part names at SF100, 150M order comments)."""
+
+    lazy = True
+    _CHUNK = 1 << 22
+
+    def __init__(self, vocab: Sequence[str], k: int, n: int):
+        self.vocab = sorted(set(vocab))
+        assert all(min(w) > " " for w in self.vocab), "vocabulary words must not contain spaces"
+        self.k = int(k)
+        self.n = int(n)
+        V = len(self.vocab)
+        total = V ** self.k
+        if total < self.n:
+            raise ValueError(f"{V}^{k} phrases cannot hold {n} distinct entries")
+        step = max(1, total // max(self.n, 1))
+        while step > 1 and math.gcd(step, V) != 1:  # keep the last word cycling through the vocabulary
+            step -= 1
+        self.step = step
+        self.vtype = STRING
+        self.has_null = False
+        self._index = None
+        self._like_cache: Dict[Tuple[str, bool], np.ndarray] = {}
+
+    def __len__(self):
+        return self.n
+
+    # -- codes -------------------------------------------------------------------------------
+    def codes(self, ids) -> np.ndarray:
+        """[len(ids), k] word indices of the given entries."""
+        x = np.asarray(ids, dtype=np.int64) * self.step
+        V = len(self.vocab)
+        out = np.empty((x.shape[0], self.k), dtype=np.int16)
+        for j in range(self.k - 1, -1, -1):
+            out[:, j] = x % V
+            x = x // V
+        return out
+
+    def value(self, i):
+        return " ".join(self.vocab[c] for c in self.codes([int(i)])[0])
+
+    @property
+    def values(self):
+        if self.n > 1 << 22:
+            raise MemoryError("refusing to materialize a huge lazy dictionary")
+        return self.decode(np.arange(self.n))
+
+    def decode(self, ids):
+        voc = np.asarray(self.vocab, dtype=object)
+        c = self.codes(ids)
+        if c.shape[0] == 0:
+            return np.empty(0, dtype=object)
+        out = voc[c[:, 0]]
+        for j in range(1, self.k):
+            out = out + " " + voc[c[:, j]]
+        return out.astype(object)
+
+    def lookup(self, v):
+        if v is None:
+            return -1
+        ws = str(v).split(" ")
+        if len(ws) != self.k:
+            return -1
+        pos = {w: i for i, w in enumerate(self.vocab)}
+        x = 0
+        for w in ws:
+            if w not in pos:
+                return -1
+            x = x * len(self.vocab) + pos[w]
+        if x % self.step:
+            return -1
+        i = x // self.step
+        return i if i < self.n else -1
+
+    def _pos(self, s: str, side: str) -> int:
+        lo, hi = 0, self.n
+        while lo < hi:
+            mid = (lo + hi) // 2
+            v = self.value(mid)
+            if v < s or (side == "right" and v == s):
+                lo = mid + 1
+            else:
+                hi = mid
+        return lo
+
+    def id_range(self, lo=None, lo_strict=False, hi=None, hi_strict=False):
+        a, b = 0, self.n
+        if lo is not None:
+            a = self._pos(str(lo), "right" if lo_strict else "left")
+        if hi is not None:
+            b = self._pos(str(hi), "left" if hi_strict else "right")
+        return (a, max(a, b))
+
+    def eval_mask(self, fn):
+        if self.n > 1 << 22:
+            raise MemoryError("dictionary-domain evaluation over a huge lazy dictionary")
+        vals = self.values
+        return np.fromiter((bool(fn(v)) for v in vals), dtype=bool, count=self.n)
+
+    def map_values(self, fn):
+        vals = self.values
+        out = np.empty(self.n, dtype=object)
+        for i, v in enumerate(vals):
+            out[i] = fn(v)
+        return out
+
+    def all_values(self):
+        return self.values
+
+    def to_json(self):
+        return {"kind": "words", "vocab": list(self.vocab), "k": self.k, "n": self.n}
+
+    # -- structured LIKE ---------------------------------------------------------------------
+    def like_mask(self, pattern: str, escape: str = "\\") -> Optional[np.ndarray]:
+        """bool[n]: entries matching the SQL LIKE ``pattern``; None when the pattern is outside the
+        structured subset ('_' wildcards, a space inside a literal piece, no '%' at all)."""
+        key = (pattern, escape)
+        hit = self._like_cache.get(key)
+        if hit is not None:
+            return hit
+        pieces, cur, i = [], [], 0
+        while i < len(pattern):
+            ch = pattern[i]
+            if escape and ch == escape and i + 1 < len(pattern):
+                cur.append(pattern[i + 1])
+                i += 2
+                continue
+            if ch == "%":
+                pieces.append("".join(cur))
+                cur = []
+            elif ch == "_":
+                return None
+            else:
+                cur.append(ch)
+            i += 1
+        pieces.append("".join(cur))
+        if len(pieces) < 2:
+            return None  # no '%': an equality, handled by lookup()
+        a_start, a_end = pieces[0] != "", pieces[-1] != ""
+        segs = [p for p in pieces if p != ""]
+        if any(" " in s for s in segs):
+            return None
+        m = len(segs)
+        if m == 0:
+            out = np.ones(self.n, dtype=bool)
+            self._like_cache[key] = out
+            return out
+        DEAD = m + 1
+
+        def advance(s, w, first, last):
+            if s == DEAD:
+                return DEAD
+            pos = 0
+            if first and a_start:
+                if not w.startswith(segs[0]):
+                    return DEAD
+                pos, s = len(segs[0]), 1
+            if last and a_end:
+                while s < m - 1:
+                    p = w.find(segs[s], pos)
+                    if p < 0:
+                        return DEAD
+                    pos, s = p + len(segs[s]), s + 1
+                if s == m - 1:
+                    ok = w.endswith(segs[-1]) and len(w) - len(segs[-1]) >= pos
+                    return m if ok else DEAD
+                return DEAD
+            limit = m - 1 if a_end else m
+            while s < limit:
+                p = w.find(segs[s], pos)
+                if p < 0:
+                    break
+                pos, s = p + len(segs[s]), s + 1
+            return s
+
+        V = len(self.vocab)
+        tables = {}
+        for first in (False, True):
+            for last in (False, True):
+                t = np.empty((m + 2, V), dtype=np.int8)
+                for s in range(m + 2):
+                    for wi, w in enumerate(self.vocab):
+                        t[s, wi] = advance(s, w, first, last)
+                tables[(first, last)] = t
+        out = np.empty(self.n, dtype=bool)
+        for a in range(0, self.n, self._CHUNK):
+            c = self.codes(np.arange(a, min(self.n, a + self._CHUNK)))
+            st = np.zeros(c.shape[0], dtype=np.int8)
+            for j in range(self.k):
+                st = tables[(j == 0, j == self.k - 1)][st, c[:, j]]
+            out[a:a + c.shape[0]] = st == m
+        if len(self._like_cache) > 32:
+            self._like_cache.clear()
+        self._like_cache[key] = out
+        return out

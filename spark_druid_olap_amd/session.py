@@ -114,7 +114,7 @@ class DataFrame:
 
     # -- introspection (plan-shape tests, DruidPlanner.getDruidQuerySpecs) ----------------------
     def druid_queries(self) -> List[P.DruidQuery]:
-        return P.find_all(self.plan, P.DruidQuery) if self.plan is not None else []
+        return P.find_all_deep(self.plan, P.DruidQuery) if self.plan is not None else []
 
     def druid_query_specs(self) -> List[S.QuerySpec]:
         return [d.spec for d in self.druid_queries()]
@@ -256,21 +256,33 @@ class Session:
         an = Analyzer(self.catalog, self)
         analyzed = an.analyze(st)
         names = [r.name for r in analyzed.output]
-        opt = optimize(analyzed, self.conf)
-        for m in self.modules:
-            for rule in getattr(m, "logical_rules", []) or []:
-                opt = rule(opt, self) or opt
         rw = DruidRewriter(self)
-        phys = rw.rewrite(opt)
-        for m in self.modules:
-            for rule in getattr(m, "physical_rules", []) or []:
-                phys = rule(phys, self) or phys
+        phys = self._physical(analyzed, rw)
         if self.conf.typed("spark.sparklinedata.druid.debug.transformations"):
             import logging
 
             logging.getLogger("sdo.planner").info("rewrite log:\n%s\nplan:\n%s", "\n".join(rw.log),
                                                   phys.tree_string())
         return DataFrame(self, phys, names, text, analyzed=analyzed, rewrite_log=rw.log)
+
+    def _physical(self, analyzed: P.Plan, rw: "DruidRewriter") -> P.Plan:
+        """optimize -> module logical rules -> Druid rewrite -> module physical rules.  Subquery
+        plans inside expressions (scalar / IN / EXISTS) go through the same pipeline first, so a
+        scalar subquery over a Druid table is itself a pushed GPU query (Spark plans them as
+        separate physical plans too, ``ScalarSubquery`` / ``PlanSubqueries``)."""
+        for sq in P.subquery_exprs(analyzed):
+            if not getattr(sq, "_planned", False):
+                object.__setattr__(sq, "query", self._physical(sq.query, rw))
+                object.__setattr__(sq, "_planned", True)
+        opt = optimize(analyzed, self.conf)
+        for m in self.modules:
+            for rule in getattr(m, "logical_rules", []) or []:
+                opt = rule(opt, self) or opt
+        phys = rw.rewrite(opt)
+        for m in self.modules:
+            for rule in getattr(m, "physical_rules", []) or []:
+                phys = rule(phys, self) or phys
+        return phys
 
     def _with_sql(self, sql: str, fn):
         prev = getattr(self._tl, "sql", None)

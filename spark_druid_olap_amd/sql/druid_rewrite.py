@@ -33,8 +33,8 @@ from ..query import transforms as QT
 from ..query.intervals import fmt_iso
 from . import ast as A
 from . import plan as P
-from .functions import Frame, Period, evaluate, is_deterministic, typeof
-from .jscodegen import JSGenError, js_aggregator, js_single_column_fn, vm_compatible
+from .functions import Frame, Period, constant_fold, evaluate, is_deterministic, typeof
+from .jscodegen import JSGenError, js_aggregator, js_expr, js_single_column_fn, vm_compatible
 from .types import AnalysisError, base, is_vec, to_series
 
 DAY_MS = 86_400_000
@@ -320,6 +320,9 @@ class DruidRewriter:
     def _filter(self, pf: PF, e: A.Expr):
         if not is_deterministic(e):
             raise NotPushable(f"non-deterministic predicate {e.sql()}")
+        sqs = [x for x in e.walk() if isinstance(x, A.SubqueryExpr)]
+        if sqs:
+            return self._deferred_filter(pf, e, sqs)
         nn = self._null_test_constant(pf, e)
         if nn is not None:
             return None if nn else S.SelectorFilterSpec("__time", "")
@@ -327,6 +330,34 @@ class DruidRewriter:
         if f is not None:
             return f
         return self._expr_filter(pf, e)
+
+    def _deferred_filter(self, pf: PF, e: A.Expr, sqs: List[A.SubqueryExpr]):
+        """Predicate over uncorrelated scalar subqueries: pushed as a DeferredFilterSpec whose
+        concrete filter is built from the subquery values at execution time.  A trial build with
+        placeholder values decides pushability now (the value never changes the filter's shape,
+        only its constants)."""
+        if any(x.kind != "scalar" for x in sqs):
+            raise NotPushable("IN / EXISTS subquery in predicate")
+
+        def build(values, _e=e, _pf=pf):
+            def sub(x):
+                if isinstance(x, A.SubqueryExpr):
+                    return A.Lit(values[id(x)], typeof(x))
+                return None
+
+            f = self._filter(_pf, constant_fold(_e.transform(sub)))
+            # trivially true -> NOT(NULL scan), so the filter tree keeps its shape
+            return f if f is not None else S.NotFilterSpec(S.SelectorFilterSpec("__time", ""))
+
+        probe = {}
+        for x in sqs:
+            t = base(typeof(x))
+            probe[id(x)] = "x" if t == "string" else (0.5 if t in ("double", "float", "decimal") else 1)
+        build(probe)  # raises NotPushable when the predicate shape is not pushable
+        d = S.DeferredFilterSpec(e.sql())
+        d.subqueries = sqs
+        d.build = build
+        return d
 
     def _native_filter(self, pf: PF, e: A.Expr):
         if isinstance(e, A.Lit):
@@ -365,6 +396,11 @@ class DruidRewriter:
             if c is not None and c.kind == "dimension" and _same_domain(c, e.child):
                 vals = [_druid_str(i.value) for i in e.items if i.value is not None]
                 f = S.ExtractionFilterSpec(c.druid_column, "true", S.InExtractionFnSpec.for_values(vals))
+                return S.NotFilterSpec(f) if e.negated else f
+            if c is not None and c.kind == "metric" and e.items and \
+                    all(isinstance(i.value, (int, float)) and not isinstance(i.value, bool) for i in e.items):
+                # metric IN (v1, v2, ...) -> OR of metric equalities (TPC-H Q16 p_size IN (...))
+                f = S.LogicalFilterSpec("or", [_metric_compare(c, "=", i.value) for i in e.items])
                 return S.NotFilterSpec(f) if e.negated else f
         cmp = _as_comparison(e)
         if cmp is not None:
@@ -468,8 +504,51 @@ class DruidRewriter:
         return S.SpatialFilterSpec(c.spatial.druid_column, {"type": "rectangular", "minCoords": mins,
                                                             "maxCoords": maxs})
 
+    def _multi_column_filter(self, pf: PF, e: A.Expr, refs: Dict[int, A.Ref]):
+        """``a <cmp> b`` over several index columns -> an expression filter evaluated per row in the
+        scan kernel's expression VM (string dimensions compared as bare columns only)."""
+        if not (isinstance(e, A.BinOp) and e.op in ("=", "<>", "<", "<=", ">", ">=")):
+            raise NotPushable(f"predicate over {len(refs)} columns: {e.sql()}")
+        names = {}
+        strings = set()
+        times = set()
+        ds = pf.table.info.datasource
+        for rid, r in refs.items():
+            c = self._column(pf, r)
+            if c.is_time:
+                names[rid] = "__time"
+                times.add(rid)
+                continue
+            if c.kind not in ("dimension", "metric"):
+                raise NotPushable(f"predicate over {len(refs)} columns: {e.sql()}")
+            names[rid] = c.druid_column
+            if c.kind == "dimension" and base(c.sql_type) == "string":
+                strings.add(rid)
+        sides = (e.l, e.r)
+        if times:
+            # time column vs an ISO-date dimension (TPC-H Q12 l_shipdate < l_commitdate): both
+            # compared as epoch ms in the kernel (day-grain dates order like their strings)
+            if not all(isinstance(x, A.Ref) and (x.rid in times or
+                                                 (x.rid in strings and _iso_date_dictionary(ds, names[x.rid])))
+                       for x in sides):
+                raise NotPushable(f"predicate over {len(refs)} columns: {e.sql()}")
+        elif strings:
+            # string comparison: both sides bare string columns (rank-compared in the kernel)
+            if not all(isinstance(x, A.Ref) and x.rid in strings for x in sides):
+                raise NotPushable(f"predicate over {len(refs)} columns: {e.sql()}")
+        elif not all(vm_compatible(x) for x in sides):
+            raise NotPushable(f"predicate over {len(refs)} columns: {e.sql()}")
+        try:
+            lhs, rhs = js_expr(e.l, names), js_expr(e.r, names)
+        except JSGenError as ex:
+            raise NotPushable(str(ex))
+        op = {"=": "==", "<>": "!="}.get(e.op, e.op)
+        return S.ExpressionFilterSpec(f"{lhs} {op} {rhs}")
+
     def _expr_filter(self, pf: PF, e: A.Expr):
         refs = {r.rid: r for r in e.refs()}
+        if len(refs) > 1 and not any(isinstance(x, A.SubqueryExpr) for x in e.walk()):
+            return self._multi_column_filter(pf, e, refs)
         if len(refs) != 1:
             raise NotPushable(f"predicate over {len(refs)} columns: {e.sql()}")
         r = next(iter(refs.values()))
@@ -480,6 +559,9 @@ class DruidRewriter:
             js = js_single_column_fn(e, r, c.druid_column)
             f = S.JavascriptFilterSpec(c.druid_column, js)
             f._pyvec = _dict_predicate(e, r, c)  # type: ignore[attr-defined]
+            lk = _bare_like(e, r)
+            if lk is not None:
+                f._pylike = lk  # type: ignore[attr-defined]
             return f
         if c.is_time:
             js = js_single_column_fn(e, r, "__time")
@@ -617,6 +699,10 @@ class DruidRewriter:
             if c.is_time:
                 fmt = _time_format_for(c.sql_type, pf.table.info.datasource)
                 return S.ExtractionDimensionSpec("__time", out, S.TimeFormatExtractionFunctionSpec(fmt)), "string"
+            if c.is_metric and c.metric_kind == "long":
+                # integral metric with a bounded value range: the engine keys it directly (K_INT;
+                # TPC-H Q17 groups lineitems by l_quantity), beyond what a Druid broker can do
+                return S.DefaultDimensionSpec(c.druid_column, out), "value"
             raise NotPushable(f"cannot group by metric {c.column}")
         te = self._time_element(pf, e)
         if te is not None:
@@ -722,6 +808,9 @@ class DruidRewriter:
             if call.distinct:
                 raise NotPushable(f"{n}(DISTINCT)")
             x = call.args[0]
+            fa = self._filtered_agg(pf, n, x, names, count_spec) if n == "sum" else None
+            if fa is not None:
+                return [fa], lambda rs: rs[0]
             kind = "sum" if n in ("avg", "mean") else n
             if kind in ("min", "max"):
                 tv = self._time_valued_agg(pf, kind, x, names)
@@ -734,6 +823,24 @@ class DruidRewriter:
                     lambda rs: A.BinOp("/", A.Cast(rs[0], "double"), rs[1])
             return [(spec_, t)], lambda rs: rs[0]
         raise NotPushable(f"aggregate {n} is not pushable")
+
+    def _filtered_agg(self, pf: PF, n: str, x: A.Expr, names: "_Names", count_spec):
+        """``sum(CASE WHEN p THEN v ELSE 0 END)`` -> Druid filtered aggregator (filter p over sum(v),
+        or count for ``THEN 1``): TPC-H Q8 / Q12 / Q14 market-share and line-count ratios."""
+        if not (isinstance(x, A.Case) and len(x.whens) == 1):
+            return None
+        cond, val = x.whens[0]
+        el = x.else_
+        if not (el is None or (isinstance(el, A.Lit) and el.value in (0, 0.0) and not isinstance(el.value, bool))):
+            return None
+        f = self._filter(pf, cond)
+        if isinstance(val, A.Lit) and val.value == 1 and not isinstance(val.value, bool):
+            inner, t = count_spec()
+        else:
+            inner, t = self._numeric_agg(pf, "sum", val, names)
+        if f is None:
+            return inner, t
+        return S.FilteredAggregationSpec(f, inner, inner.name), t
 
     def _time_valued_agg(self, pf: PF, kind: str, x: A.Expr, names: "_Names"):
         """MIN/MAX of a timestamp/date-valued column: the time column (``longMin``/``longMax`` over
@@ -1103,6 +1210,17 @@ def _js_ident(name: str) -> str:
 def _dict_frame(values, r: A.Ref, c) -> Frame:
     s = to_series(pd.Series(np.asarray(values, dtype=object)), c.sql_type)
     return Frame({r.rid: s}, len(s))
+
+
+def _bare_like(e: A.Expr, r: A.Ref) -> Optional[Tuple[str, bool]]:
+    """(pattern, negated) when e is ``r [NOT] LIKE '<literal>'`` over the bare column."""
+    neg = False
+    if isinstance(e, A.UnOp) and e.op == "not":
+        e, neg = e.child, True
+    if isinstance(e, A.Like) and e.kind == "like" and isinstance(e.child, A.Ref) and e.child.rid == r.rid and \
+            isinstance(e.pattern, A.Lit) and isinstance(e.pattern.value, str):
+        return e.pattern.value, neg != e.negated
+    return None
 
 
 def _dict_predicate(e: A.Expr, r: A.Ref, c) -> Callable:

@@ -15,6 +15,7 @@ from typing import Dict, List, Optional
 import numpy as np
 import pandas as pd
 
+from ..query import spec as S
 from . import ast as A
 from . import plan as P
 from .functions import Frame, eval_series, evaluate, typeof
@@ -199,6 +200,22 @@ class Executor:
         t0 = time.perf_counter()
         if self.token is not None:
             self.token.check()
+        deferred = getattr(p, "_deferred", None)
+        if deferred is None:
+            deferred = p._deferred = S.find_deferred(p.spec)
+        if deferred:
+            # scalar subqueries first (pushed queries themselves), then the filter they parameterise;
+            # the resolved query (and its lowered program) is cached per subquery-value tuple
+            vals = {id(sq): self._subquery(sq, None) for d in deferred for sq in d.subqueries}
+            key = tuple(repr(vals[k]) for k in sorted(vals))
+            cache = p.__dict__.setdefault("_resolved", {})
+            q = cache.get(key)
+            if q is None:
+                if len(cache) > 16:
+                    cache.clear()
+                q = cache[key] = P.DruidQuery(p.relation, S.resolve_deferred(p.spec, vals), p.columns, p.refs,
+                                              p.info)
+            p = q
         res = self.session.run_druid(p)
         cols = {}
         n = res.num_rows

@@ -276,3 +276,43 @@ class DruidQuery(Plan):
 
 def find_all(plan: Plan, cls) -> List[Any]:
     return [p for p in plan.walk() if isinstance(p, cls)]
+
+
+def node_exprs(p: Plan) -> List[A.Expr]:
+    """Every expression a plan node holds (conditions, projections, groupings, sort keys)."""
+    out: List[A.Expr] = []
+
+    def add(v):
+        if isinstance(v, A.Expr):
+            out.append(v)
+        elif isinstance(v, A.SortOrder):
+            out.append(v.expr)
+        elif isinstance(v, (list, tuple)):
+            for x in v:
+                add(x)
+
+    for k, v in vars(p).items():
+        if k != "children":
+            add(v)
+    return out
+
+
+def subquery_exprs(plan: Plan) -> List[A.SubqueryExpr]:
+    """Subquery expressions of a plan (not descending into the subqueries themselves)."""
+    seen, out = set(), []
+    for p in plan.walk():
+        for e in node_exprs(p):
+            for x in e.walk():
+                if isinstance(x, A.SubqueryExpr) and id(x) not in seen:
+                    seen.add(id(x))
+                    out.append(x)
+    return out
+
+
+def find_all_deep(plan: Plan, cls) -> List[Any]:
+    """find_all, also inside the plans of subquery expressions."""
+    out = find_all(plan, cls)
+    for sq in subquery_exprs(plan):
+        if isinstance(sq.query, Plan):
+            out.extend(find_all_deep(sq.query, cls))
+    return out
