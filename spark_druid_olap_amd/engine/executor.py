@@ -74,7 +74,7 @@ class PreparedQuery:
         self.qs = qs
         self.ds = ds
         self.world = engine.world
-        self.low = Lowerer(ds)
+        self.low = Lowerer(ds, world=engine.world)
         self.scans: List[tuple] = []  # (tag, prog, prepared)
         self.segments_per_query = segments_per_query
         qt = qs.queryType
@@ -280,9 +280,9 @@ class PreparedQuery:
                     cols[a.name] = np.zeros(1, dtype=np.int64 if a.out_type == "long" else np.float64)
                 cols["__rows__"] = np.zeros(1, dtype=np.int64)
                 n = 1
-        for kc in prog.keys:
-            if kc.name not in out_cols:
-                out_cols.append(kc.name)
+        for name in (prog.key_order or [kc.name for kc in prog.keys]):
+            if name not in out_cols:
+                out_cols.append(name)
         for a in prog.aggs:
             out_cols.append(a.name)
         for pa in (getattr(qs, "postAggregations", None) or []):
@@ -315,7 +315,7 @@ class PreparedQuery:
         while isinstance(metric, S.InvertedTopNMetricSpec):
             invert = not invert
             metric = metric.metric
-        dimname = prog.keys[-1].name
+        dimname = (prog.key_order or [kc.name for kc in prog.keys])[-1]
         if isinstance(metric, S.NumericTopNMetricSpec):
             key = np.asarray(cols[metric.metric], dtype=np.float64)[idx]
             order = np.argsort(key if invert else -key, kind="stable")

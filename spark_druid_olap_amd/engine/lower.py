@@ -243,6 +243,7 @@ class KeyComp:
     decoder: Optional[Callable[[np.ndarray], np.ndarray]] = None
     collapse: bool = False        # decoded values may coincide: re-aggregate on host
     is_timestamp: bool = False    # granularity bucket (output 'timestamp' ms)
+    orig: Optional[np.ndarray] = None  # compacted key: key id -> original dictionary id
     col_idx: int = -1             # descriptor column index (payload section)
 
 
@@ -287,6 +288,10 @@ class ScanProgram:
     thetas: List[Tuple[str, str, int]] = field(default_factory=list)  # (name, column, size)
     luts: Dict[str, torch.Tensor] = field(default_factory=dict)       # dim -> f64 value per dictionary id
     lut_ptrs: Dict[float, torch.Tensor] = field(default_factory=dict)  # E_LUT operand -> its table
+    # grouping keys functionally determined by a packed key: (key, index of determinant in keys,
+    # np.int64 table determinant dictionary id -> dependent dictionary id)
+    derived: List[Tuple["KeyComp", int, np.ndarray]] = field(default_factory=list)
+    key_order: List[str] = field(default_factory=list)  # output order of all grouping keys
 
     def col(self, name: str) -> int:
         """Absolute descriptor column index of `name` in the current section."""
@@ -337,9 +342,10 @@ def column_tensor(ds: DataSource, name: str) -> torch.Tensor:
 class Lowerer:
     """QuerySpec -> ScanProgram for a datasource shard."""
 
-    def __init__(self, ds: DataSource, bitmap_max_values: int = 4):
+    def __init__(self, ds: DataSource, bitmap_max_values: int = 4, world=None):
         self.ds = ds
         self.bitmap_max_values = bitmap_max_values
+        self.world = world
         self._tv_cache: Optional[np.ndarray] = None
 
     # ------------------------------------------------------------------ filters -> IR
@@ -780,8 +786,16 @@ class Lowerer:
             raise LoweringError(f"cannot group by floating metric {metric!r}")
         rng = getattr(m, "_value_range", None)
         if rng is None:
-            t = column_tensor(self.ds, metric)
-            rng = (int(t.min().item()), int(t.max().item())) if t.numel() else (0, 0)
+            # global value range (every rank must build the same key space)
+            t = column_tensor(self.ds, metric)[:self.ds.num_rows]
+            big = 2 ** 62
+            lo_t = (t.min() if t.numel() else torch.tensor(big, device=t.device)).to(torch.int64).reshape(1)
+            hi_t = (t.max() if t.numel() else torch.tensor(-big, device=t.device)).to(torch.int64).reshape(1)
+            if self.world is not None and self.world.distributed:
+                lo_t = self.world.all_reduce(lo_t, "min")
+                hi_t = self.world.all_reduce(hi_t, "max")
+            lo, hi = int(lo_t.item()), int(hi_t.item())
+            rng = (lo, hi) if lo <= hi else (0, 0)
             m._value_range = rng  # type: ignore[attr-defined]
         lo, hi = rng
         card = hi - lo + 1
@@ -1040,6 +1054,46 @@ class Lowerer:
             raise LoweringError("aggregator expression too deep for the device VM")
         return out
 
+    # ------------------------------------------------------------------ functional dependencies
+    def eliminate_dependent_keys(self, prog: ScanProgram) -> None:
+        """Drop grouping keys that another grouping key functionally determines in the data
+        (``s_name, s_address, s_phone`` given ``l_suppkey``; ``o_orderdate, o_custkey`` given
+        ``o_orderkey``).  They do not split groups, so the packed key covers the determinants only
+        -- wide TPC-H group-bys (Q2, Q10, Q18) stay far inside 64 bits and in the dense/LDS
+        paths -- and the dependent values are decoded from the determinant's id through the FD
+        table (``prog.derived``).  The reference only declares FDs for its cost model
+        (``functionalDependencies`` DDL option, ``sd/FunctionalDependencies.scala``); here they
+        are verified on the index itself (and across ranks), so no declaration can make results
+        wrong."""
+        cand = [i for i, kc in enumerate(prog.keys) if kc.kind == D.K_ID and kc.card > 1]
+        if len(cand) < 2:
+            return
+        alive = set(cand)
+        derived = []
+        while True:
+            best, best_deps = None, []
+            for i in sorted(alive):
+                deps = [j for j in sorted(alive) if j != i and fd_table(self.ds, prog.keys[i].col, prog.keys[j].col,
+                                                                         self.world) is not None]
+                if len(deps) > len(best_deps):
+                    best, best_deps = i, deps
+            if not best_deps:
+                break
+            for j in best_deps:
+                alive.discard(j)
+                derived.append((j, best))
+            alive.discard(best)
+        if not derived:
+            return
+        drop = {j for j, _ in derived}
+        keep = [i for i in range(len(prog.keys)) if i not in drop]
+        pos = {old: new for new, old in enumerate(keep)}
+        for j, i in derived:
+            kc = prog.keys[j]
+            lut = fd_table(self.ds, prog.keys[i].col, kc.col, self.world)
+            prog.derived.append((kc, pos[i], lut))
+        prog.keys = [prog.keys[i] for i in keep]
+
     # ------------------------------------------------------------------ whole query
     def lower_aggregate(self, intervals, filter_spec, dimensions, granularity, aggregations,
                         extra_keys: Sequence[KeyComp] = ()) -> ScanProgram:
@@ -1064,6 +1118,8 @@ class Lowerer:
             raise LoweringError("too many grouping keys")
         for a in aggregations:
             self.add_aggregator(prog, a)
+        prog.key_order = [kc.name for kc in prog.keys]
+        self.eliminate_dependent_keys(prog)
         # filter-implied key domains: a dimension the filter pins to a few values only needs
         # that many key slots (Q7: s_nation x c_nation shrinks 25x25 -> 2x2), which keeps the
         # accumulators in LDS instead of contended HBM atomics
@@ -1178,6 +1234,44 @@ def _ast_cols(a) -> List[str]:
     return [c for x in a[1:] for c in _ast_cols(x)]
 
 
+_FD_CHUNK = 1 << 26
+
+
+def fd_table(ds: DataSource, a: str, b: str, world=None) -> Optional[np.ndarray]:
+    """If dimension ``a`` functionally determines dimension ``b`` over every row of the index
+    (all shards), the table a-id -> b-id (int64, -1 for ids absent everywhere); else None.
+    Two scatter/gather passes over the id columns on the device, cached per datasource."""
+    cache = ds.__dict__.setdefault("_fd_cache", {})
+    key = (a, b)
+    if key in cache:
+        return cache[key]
+    da, db = ds.dims[a], ds.dims[b]
+    ca = len(da.dictionary)
+    dev = da.ids.device
+    lut = torch.full((ca,), -1, dtype=torch.int64, device=dev)
+    n = ds.num_rows
+    for s0 in range(0, n, _FD_CHUNK):  # (id columns are padded past num_rows)
+        ia = da.ids[s0:min(n, s0 + _FD_CHUNK)].to(torch.int64)
+        ib = db.ids[s0:min(n, s0 + _FD_CHUNK)].to(torch.int64)
+        lut.scatter_(0, ia, ib)
+    ok = torch.ones((), dtype=torch.int64, device=dev)
+    for s0 in range(0, n, _FD_CHUNK):
+        ia = da.ids[s0:min(n, s0 + _FD_CHUNK)].to(torch.int64)
+        ib = db.ids[s0:min(n, s0 + _FD_CHUNK)].to(torch.int64)
+        ok &= (lut[ia] == ib).all().to(torch.int64)
+    if world is not None and world.distributed:
+        # global FD: every rank's table agrees wherever two ranks both saw an a-id
+        hi = world.all_reduce(lut.clone(), "max")
+        big = torch.iinfo(torch.int64).max
+        lo = world.all_reduce(torch.where(lut < 0, torch.full_like(lut, big), lut), "min")
+        ok &= ((lo == big) | (lo == hi)).all().to(torch.int64)
+        ok = world.all_reduce(ok, "min")
+        lut = hi
+    out = lut.cpu().numpy() if bool(ok.item()) else None
+    cache[key] = out
+    return out
+
+
 def rank_luts(ds: DataSource, a: str, b: str) -> Tuple[torch.Tensor, torch.Tensor]:
     """f64 rank of every dictionary value of dims a and b in the sorted union of both
     dictionaries (NULL -> NaN): comparing ranks == comparing the values as strings."""
@@ -1251,7 +1345,7 @@ def compact_key(kc: KeyComp, mask: np.ndarray) -> KeyComp:
     remap[ids] = np.arange(len(ids), dtype=np.int32)
     dec = kc.decoder
     ids_t = ids.astype(np.int64)
-    return KeyComp(kc.name, D.K_REMAP, kc.col, len(ids), remap=remap,
+    return KeyComp(kc.name, D.K_REMAP, kc.col, len(ids), remap=remap, orig=ids_t,
                    decoder=(lambda c: dec(ids_t[np.asarray(c, dtype=np.int64)])) if dec else (lambda c: ids_t[c]))
 
 

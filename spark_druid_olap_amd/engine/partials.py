@@ -130,6 +130,17 @@ def finalize(prog, parts: Partials) -> Dict[str, np.ndarray]:
         vals = kc.decoder(ids) if kc.decoder is not None else ids
         key_vals.append(vals)
         cols[kc.name] = vals
+    for kc, det, lut in getattr(prog, "derived", ()):
+        # functionally dependent key: its id through the FD table of the determinant's original id
+        did = np.asarray(key_ids[det], dtype=np.int64)
+        orig = prog.keys[det].orig
+        if orig is not None:
+            did = orig[did]
+        ids = lut[did]
+        vals = kc.decoder(ids) if kc.decoder is not None else ids
+        key_vals.append(vals)
+        cols[kc.name] = vals
+    key_names = [kc.name for kc in prog.keys] + [kc.name for kc, _, _ in getattr(prog, "derived", ())]
     collapse = any(kc.collapse for kc in prog.keys)
     if collapse and len(acc_h):
         # non-injective key formatting: re-aggregate groups that format identically
@@ -164,8 +175,8 @@ def finalize(prog, parts: Partials) -> Dict[str, np.ndarray]:
         keys_first = [None] * R
         for t, i in uniq.items():
             keys_first[i] = t
-        for j, kc in enumerate(prog.keys):
-            cols[kc.name] = np.array([t[j] for t in keys_first], dtype=object)
+        for j, name in enumerate(key_names):
+            cols[name] = np.array([t[j] for t in keys_first], dtype=object)
         acc_h, hll_d = new_acc, new_hll
     for a in prog.aggs:
         if a.kind in ("count",):

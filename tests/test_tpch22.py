@@ -79,3 +79,27 @@ def test_words_dictionary_like(pattern):
     exp = np.array([rx.match(v) is not None for v in vals])
     assert (d.like_mask(pattern) == exp).all()
     assert d.lookup(vals[1234]) == 1234
+
+
+def test_functional_dependency_key_elimination(ds_small):
+    """Q10-style wide grouping: the customer attributes are determined by o_custkey, so only the
+    determinant is packed into the device key; attributes are decoded through FD tables."""
+    from spark_druid_olap_amd.engine.lower import Lowerer, fd_table
+    from spark_druid_olap_amd.query import spec as S
+
+    dims = [S.DefaultDimensionSpec(d) for d in ("o_custkey", "c_name", "c_phone", "c_nation", "l_shipmode")]
+    prog = Lowerer(ds_small).lower_aggregate(["1992-01-01/1999-01-01"], None, dims, None,
+                                             [S.FunctionAggregationSpec("count", "n")])
+    assert sorted(kc.name for kc in prog.keys) == ["l_shipmode", "o_custkey"]
+    assert sorted(kc.name for kc, _, _ in prog.derived) == ["c_name", "c_nation", "c_phone"]
+    assert prog.key_order == ["o_custkey", "c_name", "c_phone", "c_nation", "l_shipmode"]
+    assert fd_table(ds_small, "l_shipmode", "l_returnflag") is None
+    r = Engine(use_native=False).execute(S.GroupByQuerySpec("tpch", dims, aggregations=[
+        S.FunctionAggregationSpec("count", "n")], intervals=["1992-01-01/1999-01-01"]), ds_small)
+    assert r.columns[:5] == ["o_custkey", "c_name", "c_phone", "c_nation", "l_shipmode"]
+    assert int(np.asarray(r.data["n"]).sum()) == ds_small.num_rows
+    name_of = {}
+    for ck, cn in zip(r.data["o_custkey"], r.data["c_name"]):
+        assert name_of.setdefault(ck, cn) == cn
+    assert all(str(cn).startswith("Customer#") and int(str(cn)[9:]) == int(ck)
+               for ck, cn in zip(r.data["o_custkey"], r.data["c_name"]))
