@@ -779,11 +779,9 @@ class Lowerer:
         remap = np.array([0 if v is None else pos[v] for v in vals], dtype=np.int32)
         return KeyComp(name, D.K_REMAP, dim, len(dd), remap=remap, decoder=lambda ids, _d=dd: DictColumn(ids, _d))
 
-    def _metric_key(self, name: str, metric: str) -> KeyComp:
-        """Group by an integral metric (K_INT over its stored value range, <= 2^20 values)."""
+    def _metric_range(self, metric: str) -> Tuple[int, int]:
+        """Global (all ranks) min/max of a metric's stored integer values, cached on the metric."""
         m = self.ds.metrics[metric]
-        if not m.is_integral:
-            raise LoweringError(f"cannot group by floating metric {metric!r}")
         rng = getattr(m, "_value_range", None)
         if rng is None:
             # global value range (every rank must build the same key space)
@@ -797,7 +795,59 @@ class Lowerer:
             lo, hi = int(lo_t.item()), int(hi_t.item())
             rng = (lo, hi) if lo <= hi else (0, 0)
             m._value_range = rng  # type: ignore[attr-defined]
-        lo, hi = rng
+        return rng
+
+    def _exact_decimal(self, ast, mapping: Dict[str, str]) -> Optional[int]:
+        """Result scale when ``ast`` is +,-,* over decimal/long metrics and decimal constants and the
+        scaled value stays exactly representable (row < 2^52, total < 2^62); else None."""
+        def rec(n):
+            k = n[0]
+            if k == "const":
+                v = float(n[1])
+                if not math.isfinite(v):
+                    return None
+                txt = repr(v)
+                if "e" in txt or "E" in txt:
+                    return None
+                sc = len(txt.split(".")[1].rstrip("0")) if "." in txt else 0
+                return sc, abs(v)
+            if k == "col":
+                name = mapping.get(n[1], n[1])
+                m = self.ds.metrics.get(name)
+                if m is None or name in self.ds.dims or not m.is_integral:
+                    return None
+                lo, hi = self._metric_range(name)
+                sc = m.scale if m.kind == "decimal" else 0
+                return sc, max(abs(lo), abs(hi)) / 10.0 ** sc
+            if k == "neg":
+                return rec(n[1])
+            if k in ("add", "sub", "mul"):
+                a, b = rec(n[1]), rec(n[2])
+                if a is None or b is None:
+                    return None
+                if k == "mul":
+                    return a[0] + b[0], a[1] * b[1]
+                return max(a[0], b[0]), a[1] + b[1]
+            return None
+
+        r = rec(ast)
+        if r is None:
+            return None
+        sc, bound = r
+        if sc > 9:
+            return None
+        row = bound * 10.0 ** sc
+        rows = self.ds.num_rows * (self.world.size if self.world is not None else 1)
+        if row >= 2.0 ** 52 or row * max(rows, 1) >= 2.0 ** 62:
+            return None
+        return sc
+
+    def _metric_key(self, name: str, metric: str) -> KeyComp:
+        """Group by an integral metric (K_INT over its stored value range, <= 2^20 values)."""
+        m = self.ds.metrics[metric]
+        if not m.is_integral:
+            raise LoweringError(f"cannot group by floating metric {metric!r}")
+        lo, hi = self._metric_range(metric)
         card = hi - lo + 1
         if card > (1 << 20):
             raise LoweringError(f"metric {metric!r} spans {card} values: too many to group by")
@@ -981,6 +1031,18 @@ class Lowerer:
             ast = parse_expr(expr)
             mapping = dict(zip(params, a.fieldNames))
             eops = self._emit_expr(prog, ast, mapping)
+            if op == "sum":
+                ex = self._exact_decimal(ast, mapping)
+                if ex is not None:
+                    # exact decimal sum: per-row value * 10^scale rounded to int64 (exact: the bound
+                    # keeps every row < 2^52 and the total < 2^62), summed like a long metric --
+                    # deterministic under any atomic order and equal across queries (Q15's
+                    # total_revenue = max(total_revenue))
+                    sc = ex
+                    d = aop(D.A_SUM_X, -1, eops + [(D.E_CONST, 0, float(10 ** sc)), (D.E_MUL, 0, 0.0)])
+                    d["slot"] = slot(D.S_SUM_I, 0, d)
+                    prog.aggs.append(AggOut(a.name, "sum_i", d["slot"], scale=sc, out_type="double"))
+                    return
             kind = {"sum": D.A_SUM_F, "max": D.A_MAX_F, "min": D.A_MIN_F}[op]
             d = aop(kind, -1, eops)
             if op == "sum":

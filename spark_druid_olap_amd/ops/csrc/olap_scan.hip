@@ -644,6 +644,8 @@ __global__ __launch_bounds__(512) void olap_scan_kernel(const ScanDesc* __restri
           int64_t val;
           if (ao.kind == A_COUNT) {
             val = 1;
+          } else if (ao.kind == A_SUM_X) {
+            val = (int64_t)rint(eval_expr<U>(d, ao.expr_off, ao.expr_len, wb, u, lane));
           } else if (fl) {
             const double fv = ao.expr_len > 0 ? eval_expr<U>(d, ao.expr_off, ao.expr_len, wb, u, lane)
                                               : col_dbl<U>(d, wb, ao.col, u, lane);

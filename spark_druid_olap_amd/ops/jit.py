@@ -453,6 +453,8 @@ class _Gen:
                 val = self.ival(a["col"])
             elif kind == D.A_COUNT:
                 val = "1LL"
+            elif kind == D.A_SUM_X:
+                val = f"(int64_t)rint({self.expr(a['expr'], a.get('expr_off', 0))})"
             elif kind in (D.A_SUM_F, D.A_MIN_F, D.A_MAX_F):
                 dv = self.expr(a["expr"], a.get("expr_off", 0)) if a.get("expr") else self.dval(a["col"])
                 val = f"__double_as_longlong({dv})" if kind == D.A_SUM_F else f"f2ord({dv})"

@@ -303,6 +303,8 @@ def _agg_values(prog, a, rows: torch.Tensor) -> torch.Tensor:
     k = a["kind"]
     if k == D.A_COUNT:
         return torch.ones(rows.numel(), dtype=torch.int64, device=rows.device)
+    if k == D.A_SUM_X:
+        return torch.round(_expr_values(prog, a["expr"], rows)).to(torch.int64)
     if k in (D.A_SUM_F, D.A_MIN_F, D.A_MAX_F):
         if a.get("expr"):
             f = _expr_values(prog, a["expr"], rows)
