@@ -210,7 +210,7 @@ class PreparedScan:
             self.cap *= 4  # grow and retry
             self._alloc()
         if self.mode == D.M_HASH:
-            valid = torch.nonzero(self.keys != -1).flatten()
+            valid = _nonzero_big(self.keys != -1)
             return Partials("sparse", self.acc.index_select(0, valid), self.keys.index_select(0, valid),
                             [h.view(self.rows, self.m).index_select(0, valid) for h in self.hll])
         return Partials("dense", self.acc, None, [h.view(self.rows, self.m) for h in self.hll])
@@ -266,3 +266,14 @@ def _grid(dev: torch.device, total_chunks: int, lds_total: int) -> int:
     need = max(1, (total_chunks + waves - 1) // waves)
     per_cu = max(1, min(BLOCKS_PER_CU, (160 * 1024) // max(lds_total, 1)))
     return max(1, min(need, num_cus(dev) * per_cu))
+
+
+def _nonzero_big(mask: torch.Tensor) -> torch.Tensor:
+    """torch.nonzero in 2^30-element pieces (ROCm's nonzero miscounts past 2^31 elements: a hash
+    table for 10^9 groups would ask for an absurd allocation)."""
+    n = mask.numel()
+    if n <= (1 << 30):
+        return torch.nonzero(mask).flatten()
+    step = 1 << 30
+    return torch.cat([torch.nonzero(mask[a:a + step]).flatten() + a for a in range(0, n, step)])
+

@@ -160,23 +160,7 @@ class PreparedQuery:
         t0 = time.perf_counter()
         qt = self.qs.queryType
         if qt in ("groupBy", "timeseries", "topN"):
-            _, prog, prep = self.scans[0]
-            err = None
-            try:
-                with T.span("sdo.scan"):
-                    part = self._scan(prog, prep)
-                    if len(self.scans) > 1:
-                        parts = [part] + [self._scan(p_, q_) for _, p_, q_ in self.scans[1:]]
-                        part = combine_local(prog, parts)
-            except Exception as e:  # noqa: BLE001  (peers learn about it in the merge collective)
-                if not self.world.distributed:
-                    raise
-                err, part = e, self._placeholder(prog, prep)
-            t1 = time.perf_counter()
-            disjoint = bool(self.ds.shard_key) and any(k.col == self.ds.shard_key for k in prog.keys)
-            with T.span("sdo.merge"):
-                part = merge_partials(self.world, prog, part, disjoint_keys=disjoint, local_error=err)
-            part = self._device_prune(prog, part)
+            prog, part, t1 = self.run_partials(t0)
             t2 = time.perf_counter()
             with T.span("sdo.finalize"):
                 cols = finalize(prog, part)
@@ -194,7 +178,83 @@ class PreparedQuery:
         res.stats["exec_ms"] = (time.perf_counter() - t0) * 1e3
         return res
 
-    def _device_prune(self, prog: ScanProgram, part: Partials) -> Partials:
+    def run_partials(self, t0: float):
+        """scan -> merge across ranks -> device HAVING / top-K pruning; (prog, merged partials,
+        scan end time).  The partials stay on the device (nested queries consume them there)."""
+        _, prog, prep = self.scans[0]
+        err = None
+        try:
+            with T.span("sdo.scan"):
+                part = self._scan(prog, prep)
+                if len(self.scans) > 1:
+                    parts = [part] + [self._scan(p_, q_) for _, p_, q_ in self.scans[1:]]
+                    part = combine_local(prog, parts)
+        except Exception as e:  # noqa: BLE001  (peers learn about it in the merge collective)
+            if not self.world.distributed:
+                raise
+            err, part = e, self._placeholder(prog, prep)
+        t1 = time.perf_counter()
+        disjoint = bool(self.ds.shard_key) and any(k.col == self.ds.shard_key for k in prog.keys)
+        with T.span("sdo.merge"):
+            part = merge_partials(self.world, prog, part, disjoint_keys=disjoint, local_error=err)
+        part, hv = self._device_having(prog, part)
+        part = self._device_prune(prog, part, hv)
+        return prog, part, t1
+
+    def _device_having(self, prog: ScanProgram, part: Partials):
+        """groupBy havingSpec evaluated over the merged accumulators ON THE DEVICE (TPC-H Q18:
+        15M order groups -> a few hundred survive ``sum(l_quantity) > 300``), so only survivors are
+        shipped and decoded.  Returns (partials, applied); the host re-applies the same spec in
+        ``_post`` (idempotent).  Specs over sketches / post-aggregations stay on the host."""
+        h = getattr(self.qs, "having", None)
+        if h is None or self.qs.queryType != "groupBy" or prog.thetas or any(kc.collapse for kc in prog.keys):
+            return part, h is None
+        if part.rows <= 4096:
+            return part, False
+        aggs = {a.name: a for a in prog.aggs}
+
+        def value(name):
+            a = aggs.get(name)
+            if a is None or a.kind not in ("count", "sum_i", "sum_f", "min_i", "max_i", "min_f", "max_f"):
+                return None
+            col = part.acc[:, a.slot]
+            if a.kind == "sum_f":
+                return col.view(torch.float64)
+            if a.kind in ("min_f", "max_f"):
+                return torch.where(col >= 0, col, col ^ 0x7FFFFFFFFFFFFFFF).view(torch.float64)
+            v = col.to(torch.float64)
+            return v / (10.0 ** a.scale) if a.scale else v
+
+        def ev(x):
+            if isinstance(x, S.ComparisonHavingSpec):
+                v = value(x.aggregation)
+                if v is None:
+                    return None
+                c = float(x.value)
+                return v == c if x.type == "equalTo" else (v > c if x.type == "greaterThan" else v < c)
+            if isinstance(x, S.LogicalHavingSpec):
+                ms = [ev(y) for y in x.havingSpecs]
+                if any(m is None for m in ms):
+                    return None
+                out = ms[0]
+                for m in ms[1:]:
+                    out = (out & m) if x.type == "and" else (out | m)
+                return out
+            if isinstance(x, S.NotHavingSpec):
+                m = ev(x.havingSpec)
+                return None if m is None else ~m
+            return None
+
+        if part.kind == "dense":
+            part = part.compact()
+        mask = ev(h)
+        if mask is None:
+            return part, False
+        keep = torch.nonzero(mask).flatten()
+        return Partials("sparse", part.acc.index_select(0, keep), part.keys.index_select(0, keep),
+                        [x.index_select(0, keep) for x in part.hll]), True
+
+    def _device_prune(self, prog: ScanProgram, part: Partials, having_done: bool = True) -> Partials:
         """ORDER BY <aggregate> LIMIT k (groupBy limitSpec) and numeric topN, applied to the merged
         partials ON THE DEVICE before finalize: keep only groups whose leading sort key ties or
         beats the k-th best (torch.topk), so a million-group query (TPC-H Q3 by o_orderkey) ships and
@@ -204,8 +264,7 @@ class PreparedQuery:
         qt = qs.queryType
         if qt == "groupBy":
             ls = qs.limitSpec
-            if ls is None or ls.limit is None or ls.limit < 0 or not ls.columns or \
-                    getattr(qs, "having", None) is not None:
+            if ls is None or ls.limit is None or ls.limit < 0 or not ls.columns or not having_done:
                 return part
             oc = ls.columns[0]
             oc = S.OrderByColumnSpec(oc) if isinstance(oc, str) else oc
@@ -603,6 +662,10 @@ class Engine:
         the query runs as one partial per batch of that many segments and the partials are merged
         by the engine (the reference's Spark-side PostAggregate, ``asd/PostAggregate.scala``);
         unset = broker execution, one fused scan over every segment."""
+        if isinstance(getattr(qs, "dataSource", None), S.QueryDataSourceSpec):
+            from .nested import NestedPreparedQuery
+
+            return NestedPreparedQuery(self, qs, ds, segments_per_query)
         return PreparedQuery(self, qs, ds, segments_per_query)
 
     def execute(self, qs: S.QuerySpec, ds: DataSource, segments_per_query: Optional[int] = None) -> QueryResult:

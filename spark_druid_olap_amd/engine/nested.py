@@ -1,0 +1,274 @@
+"""Nested groupBy (Druid query data source) executed on the device.
+
+The outer groupBy of ``{"dataSource": {"type": "query", "query": <inner groupBy>}}`` aggregates the
+inner query's result rows.  Druid brokers run the outer level over the merged inner results; the
+reference never issues nested queries (its Spark plans aggregate the Druid rows again on the
+executors, ``asd/PostAggregate.scala``).  Here the inner query's merged partials never leave HBM:
+key components are decoded to dictionary ids on the device, the outer keys are packed and
+grouped with ``torch.unique``, and the outer aggregates reduce with scatter ops -- TPC-H Q13's
+150M (customer, order) groups at SF100 collapse to ~40 rows before anything is copied to the host.
+
+Outer dimensions name inner output columns (inner dimensions, or inner aggregates used as keys:
+Q13 groups customers by their order count); outer aggregators are count / long|double
+Sum|Min|Max over inner columns.  Outer having / limitSpec / postAggregations run like any other
+query's (executor._post).
+"""
+from __future__ import annotations
+
+import time
+from typing import Callable, Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from ..query import spec as S
+from ..segment.datasource import DataSource
+from .lower import LoweringError
+
+
+class DeviceColumn:
+    """One inner output column on the device.  ``ids`` (int64) for dimensions with ``decode``
+    (ids -> values); ``vals`` (int64 with decimal ``scale``, or float64) for aggregates."""
+
+    def __init__(self, name: str, t: torch.Tensor, decode: Optional[Callable] = None, scale: int = 0):
+        self.name = name
+        self.t = t
+        self.decode = decode
+        self.scale = scale
+
+    @property
+    def is_float(self) -> bool:
+        return self.t.dtype == torch.float64
+
+    def as_float(self) -> torch.Tensor:
+        if self.is_float:
+            return self.t
+        v = self.t.to(torch.float64)
+        return v / (10.0 ** self.scale) if self.scale else v
+
+    def host_values(self, t: torch.Tensor) -> np.ndarray:
+        h = t.cpu().numpy()
+        if self.decode is not None:
+            return self.decode(h)
+        if self.is_float:
+            return h
+        return h / (10.0 ** self.scale) if self.scale else h
+
+
+def device_columns(pq) -> Tuple[Dict[str, DeviceColumn], int]:
+    """Run a (non-nested) groupBy PreparedQuery up to its merged partials and expose every output
+    column as a device tensor.  Returns (columns, row count)."""
+    prog, part, _ = pq.run_partials(time.perf_counter())
+    if prog.thetas or any(kc.collapse for kc in prog.keys):
+        raise LoweringError("nested query over theta sketches / non-injective keys")
+    if part.kind == "dense":
+        part = part.compact()
+    g = part.keys
+    dev = part.acc.device
+    cols: Dict[str, DeviceColumn] = {}
+    ids_of = []
+    for kc in prog.keys:
+        ids = torch.remainder(torch.div(g, kc.stride, rounding_mode="floor"), max(1, kc.card))
+        ids_of.append(ids)
+        cols[kc.name] = DeviceColumn(kc.name, ids, kc.decoder if kc.decoder is not None else (lambda x: x))
+    for kc, det, lut in getattr(prog, "derived", ()):
+        did = ids_of[det]
+        orig = prog.keys[det].orig
+        if orig is not None:
+            did = torch.from_numpy(orig).to(dev)[did]
+        ids = torch.from_numpy(lut).to(dev)[did]
+        cols[kc.name] = DeviceColumn(kc.name, ids, kc.decoder if kc.decoder is not None else (lambda x: x))
+    for a in prog.aggs:
+        col = part.acc[:, a.slot] if a.slot >= 0 else None
+        if a.kind in ("count", "min_i", "max_i"):
+            cols[a.name] = DeviceColumn(a.name, col, scale=a.scale)
+        elif a.kind == "sum_i":
+            cols[a.name] = DeviceColumn(a.name, col, scale=a.scale)
+        elif a.kind == "sum_f":
+            cols[a.name] = DeviceColumn(a.name, col.contiguous().view(torch.float64))
+        elif a.kind in ("min_f", "max_f"):
+            cols[a.name] = DeviceColumn(a.name, torch.where(col >= 0, col, col ^ 0x7FFFFFFFFFFFFFFF).view(torch.float64))
+        else:
+            raise LoweringError(f"nested query over a {a.kind} aggregate")
+    return cols, int(part.acc.shape[0])
+
+
+class NestedPreparedQuery:
+    """groupBy over a query data source (see module doc)."""
+
+    def __init__(self, engine, qs: S.GroupByQuerySpec, ds: DataSource, segments_per_query: Optional[int] = None):
+        if qs.queryType != "groupBy":
+            raise LoweringError("only groupBy runs over a query data source")
+        if qs.filter is not None and not isinstance(qs.filter, S.NoopFilterSpec):
+            raise LoweringError("filters on a nested groupBy are not supported")
+        self.engine = engine
+        self.qs = qs
+        self.ds = ds
+        self.world = engine.world
+        self.inner = engine.prepare(qs.dataSource.query, ds, segments_per_query)
+        for d in qs.dimensions:
+            if not isinstance(d, S.DefaultDimensionSpec):
+                raise LoweringError("nested groupBy dimensions must be default dimension specs")
+        for a in qs.aggregations:
+            if not (isinstance(a, S.FunctionAggregationSpec) and
+                    a.type in ("count", "longSum", "doubleSum", "longMin", "longMax", "doubleMin", "doubleMax")):
+                raise LoweringError(f"nested groupBy aggregator {type(a).__name__}")
+
+    # ------------------------------------------------------------------ run
+    def _compute(self) -> Tuple[Dict[str, DeviceColumn], int, float]:
+        """Outer groups on the device: (columns by output name, row count, inner time ms)."""
+        t0 = time.perf_counter()
+        inner = self.inner
+        if isinstance(inner, NestedPreparedQuery):
+            cols, n = inner.device_result()
+        else:
+            cols, n = device_columns(inner)
+        inner_ms = (time.perf_counter() - t0) * 1e3
+        qs = self.qs
+        dev = next(iter(cols.values())).t.device if cols else self.ds.device
+        # ---- outer keys: pack inner columns (ids / integral values) into one int64
+        keycols = []
+        for d in qs.dimensions:
+            c = cols.get(d.dimension)
+            if c is None:
+                raise LoweringError(f"nested dimension {d.dimension!r} is not an inner output")
+            if c.is_float:
+                raise LoweringError(f"nested dimension {d.dimension!r} is floating point")
+            keycols.append((d, c))
+        if n == 0:
+            inv = torch.zeros(0, dtype=torch.int64, device=dev)
+            R = 0
+            firsts = torch.zeros(0, dtype=torch.int64, device=dev)
+        elif keycols:
+            packed = torch.zeros(n, dtype=torch.int64, device=dev)
+            span = 1
+            for _, c in reversed(keycols):
+                lo = int(c.t.min().item())
+                hi = int(c.t.max().item())
+                card = hi - lo + 1
+                if span * card >= 2 ** 62:
+                    raise LoweringError("nested group key space exceeds 64 bits")
+                packed += (c.t - lo) * span
+                span *= card
+            uk, inv = torch.unique(packed, return_inverse=True)
+            R = int(uk.numel())
+            # first inner row of every outer group: where its key values come from
+            firsts = torch.full((R,), n, dtype=torch.int64, device=dev)
+            firsts.scatter_reduce_(0, inv, torch.arange(n, device=dev), reduce="amin")
+        else:
+            inv = torch.zeros(n, dtype=torch.int64, device=dev)
+            R = 1
+            firsts = torch.zeros(1, dtype=torch.int64, device=dev)
+        out: Dict[str, DeviceColumn] = {}
+        for d, c in keycols:
+            out[d.outputName] = DeviceColumn(d.outputName, c.t.index_select(0, firsts), c.decode, c.scale)
+        for a in qs.aggregations:
+            if a.type == "count":
+                v = torch.zeros(R, dtype=torch.int64, device=dev).index_add_(0, inv, torch.ones_like(inv))
+                out[a.name] = DeviceColumn(a.name, v)
+                continue
+            c = cols.get(a.fieldName)
+            if c is None:
+                raise LoweringError(f"nested aggregator over unknown column {a.fieldName!r}")
+            op = a.type[4:].lower() if a.type.startswith("long") else a.type[6:].lower()
+            exact = not c.is_float and c.decode is None  # integral (scaled) values stay int64
+            src = c.t if exact else (c.t.to(torch.float64) if c.decode is not None else c.as_float())
+            if op == "sum":
+                acc = torch.zeros(R, dtype=src.dtype, device=dev).index_add_(0, inv, src)
+            else:
+                if src.dtype == torch.int64:
+                    init = torch.iinfo(torch.int64).max if op == "min" else torch.iinfo(torch.int64).min
+                else:
+                    init = float("inf") if op == "min" else float("-inf")
+                acc = torch.full((R,), init, dtype=src.dtype, device=dev)
+                acc.scatter_reduce_(0, inv, src, reduce="amin" if op == "min" else "amax")
+            if a.type.startswith("long") and not exact:
+                acc = acc.to(torch.int64)
+            out[a.name] = DeviceColumn(a.name, acc, scale=c.scale if exact else 0)
+        return out, R, inner_ms
+
+    def device_result(self) -> Tuple[Dict[str, DeviceColumn], int]:
+        """This nested query's groups as device columns (input of a further nesting level)."""
+        qs = self.qs
+        if qs.having is not None or qs.limitSpec is not None or qs.postAggregations:
+            raise LoweringError("having / limit / post-aggregations on an inner nested groupBy")
+        cols, R, _ = self._compute()
+        return cols, R
+
+    def _host_inner(self):
+        """Fallback: the inner result on the host (non-injective keys, sketches): numpy columns."""
+        from .executor import materialize
+
+        res = self.inner.run()
+        return {c: materialize(res.data[c]) for c in res.columns}, res.num_rows
+
+    def _host_compute(self):
+        """Outer aggregation over host columns (pandas), same semantics as ``_compute``."""
+        import pandas as pd
+
+        qs = self.qs
+        t0 = time.perf_counter()
+        cols, n = self._host_inner()
+        inner_ms = (time.perf_counter() - t0) * 1e3
+        df = pd.DataFrame({k: pd.Series(v) for k, v in cols.items()})
+        keys = [d.dimension for d in qs.dimensions]
+        df["__one__"] = 1
+        spec = {}
+        for a in qs.aggregations:
+            if a.type == "count":
+                spec[a.name] = ("__one__", "sum")
+            else:
+                op = a.type[4:].lower() if a.type.startswith("long") else a.type[6:].lower()
+                spec[a.name] = (a.fieldName, op)
+        g = df.groupby(keys, dropna=False, sort=False).agg(**spec).reset_index() if n else \
+            pd.DataFrame({**{k: [] for k in keys}, **{a.name: [] for a in qs.aggregations}})
+        out = {}
+        for d in qs.dimensions:
+            out[d.outputName] = np.asarray(g[d.dimension].to_numpy(), dtype=object)
+        for a in qs.aggregations:
+            v = g[a.name].to_numpy()
+            out[a.name] = v.astype(np.int64) if (a.type == "count" or a.type.startswith("long")) else \
+                v.astype(np.float64)
+        return out, len(g), inner_ms
+
+    def run(self):
+        t0 = time.perf_counter()
+        qs = self.qs
+        try:
+            dcols, R, inner_ms = self._compute()
+        except LoweringError:
+            if isinstance(self.inner, NestedPreparedQuery):
+                raise
+            out, R, inner_ms = self._host_compute()
+            return self._finish(out, R, inner_ms, t0)
+        out: Dict[str, np.ndarray] = {}
+        names: List[str] = []
+        for d in qs.dimensions:
+            c = dcols[d.outputName]
+            out[d.outputName] = c.host_values(c.t)
+            names.append(d.outputName)
+        for a in qs.aggregations:
+            c = dcols[a.name]
+            h = c.host_values(c.t)
+            out[a.name] = np.asarray(h, dtype=np.int64) if ((a.type == "count" or a.type.startswith("long")) and not c.scale) \
+                else np.asarray(h, dtype=np.float64)
+            names.append(a.name)
+        return self._finish(out, R, inner_ms, t0)
+
+    def _finish(self, out, R, inner_ms, t0):
+        from .executor import QueryResult, eval_having, eval_postagg, order_and_limit, take
+
+        qs = self.qs
+        names = [d.outputName for d in qs.dimensions] + [a.name for a in qs.aggregations]
+        for pa in (getattr(qs, "postAggregations", None) or []):
+            out[pa.name] = np.asarray(eval_postagg(pa, out, R), dtype=np.float64) * np.ones(R)
+            names.append(pa.name)
+        idx = np.arange(R)
+        if qs.having is not None:
+            idx = idx[eval_having(qs.having, out)[idx]]
+        if qs.limitSpec is not None:
+            idx = order_and_limit(out, idx, qs.limitSpec.columns, qs.limitSpec.limit)
+        data = {k: take(out[k], idx) for k in names}
+        res = QueryResult(names, data, "groupBy", {"groups": R})
+        res.stats.update(inner_ms=inner_ms, exec_ms=(time.perf_counter() - t0) * 1e3)
+        return res

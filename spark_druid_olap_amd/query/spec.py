@@ -308,6 +308,18 @@ class ExpressionFilterSpec(Spec, _Decodable):
     type: str = "expression"
 
 
+@_register("datasource", "query")
+@dataclass
+class QueryDataSourceSpec(Spec, _Decodable):
+    """Druid's query data source: the rows of an inner (groupBy) query are the input of the outer
+    groupBy -- nested aggregation (TPC-H Q13 ``count(*) ... group by c_count`` over per-customer
+    order counts; SQL count(DISTINCT) rewritten as two aggregation levels).  The engine runs the
+    outer level on the inner query's device-resident partials (engine/nested.py)."""
+    query: Any
+    type: str = "query"
+    _nested = {"query": "query"}
+
+
 @dataclass
 class DeferredFilterSpec(Spec):
     """A filter whose operand is an uncorrelated scalar subquery (TPC-H Q22 ``c_acctbal >
@@ -690,7 +702,8 @@ class GroupByQuerySpec(QuerySpec, _Decodable):
     intervals: List[str] = field(default_factory=list)
     context: Optional[QuerySpecContext] = None
     queryType: str = "groupBy"
-    _nested = {"dimensions": "dimension", "limitSpec": "limit", "having": "having", "granularity": "granularity",
+    _nested = {"dataSource": "datasource", "dimensions": "dimension", "limitSpec": "limit", "having": "having",
+               "granularity": "granularity",
                "filter": "filter", "aggregations": "aggregation", "postAggregations": "postagg"}
 
     @classmethod

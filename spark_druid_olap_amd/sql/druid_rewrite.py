@@ -114,12 +114,18 @@ class DruidRewriter:
         ch = [self._top_down(c) for c in p.children]
         if any(a is not b for a, b in zip(ch, p.children)):
             p = p.with_children(ch)
+        if isinstance(p, P.Aggregate):
+            r = self._try(self._nested_aggregate, p)
+            if r is not None:
+                return r
         if isinstance(p, P.Sort):
             r = self._try(self._sort, p)
             if r is not None:
                 p = r
         elif isinstance(p, P.Limit):
             self._try(self._limit, p)
+        elif isinstance(p, P.Filter):
+            self._try(self._having, p)
         return p
 
     # ============================================================================== fragments
@@ -957,6 +963,124 @@ class DruidRewriter:
         dq.spec = q.copy(limitSpec=S.LimitSpec(None, cols))
         return s.child
 
+    def _nested_aggregate(self, agg: P.Aggregate) -> Optional[P.Plan]:
+        """Aggregate over a pushed groupBy -> nested groupBy over a query data source, executed on
+        the device (engine/nested.py): COUNT(DISTINCT) rewritten as two aggregation levels (TPC-H
+        Q16), orders per customer then customers per order count (Q13), orders with a late line
+        per priority (Q4).  Outer keys and aggregate inputs must be plain inner output columns;
+        count(*) / count(agg) / sum / min / max aggregate."""
+        if agg.grouping_sets is not None:
+            return None
+        dq, m = self._druid_below(agg.child)
+        if dq is None or not isinstance(dq.spec, S.GroupByQuerySpec):
+            return None
+        q = dq.spec
+        if q.limitSpec is not None or q.having is not None or q.postAggregations:
+            raise NotPushable("nested aggregate over a limited / filtered inner groupBy")
+        names = {r.rid: c for r, c in zip(dq.refs, dq.columns)}   # inner ref -> (name, type, kind)
+        inner_aggs = {a.name for a in (q.aggregations or [])}
+        used = {d.outputName for d in q.dimensions} | inner_aggs
+        nm = _Names()
+        dims, columns, drefs, final = [], [], [], {}
+        outs = agg.output
+
+        def inner_col(e):
+            if not (isinstance(e, A.Ref) and e.rid in m):
+                raise NotPushable(f"nested aggregate over expression {e.sql()}")
+            return names[m[e.rid]]
+
+        for i, g in enumerate(agg.groups):
+            name, t, kind = inner_col(g.child)
+            out = nm.dim(g.name)
+            while out in used:
+                out = out + "_"
+            dims.append(S.DefaultDimensionSpec(name, out))
+            r = A.Ref(A.new_id(), g.name, typeof(g.child))
+            drefs.append(r)
+            columns.append((out, typeof(g.child), kind))
+            final[outs[i].rid] = r
+        aggs = []
+        for j, a in enumerate(agg.aggs):
+            call = a.child
+            if call.distinct:
+                raise NotPushable("nested DISTINCT aggregate")
+            n = call.name
+            out_t = outs[len(agg.groups) + j].dtype
+            aname = nm.agg()
+            while aname in used:
+                aname = aname + "_"
+            if n == "count" and not call.args:
+                spec_ = S.FunctionAggregationSpec("count", aname, "count")
+            elif n == "count" and len(call.args) == 1 and (inner_col(call.args[0])[0] in inner_aggs or
+                                                           _non_null_dim(q, inner_col(call.args[0])[0],
+                                                                         dq.relation.info.datasource)):
+                # inner aggregates / NULL-free dimensions: count(x) == count(*)
+                spec_ = S.FunctionAggregationSpec("count", aname, "count")
+            elif n in ("sum", "min", "max") and len(call.args) == 1:
+                name, t, kind = inner_col(call.args[0])
+                if name not in inner_aggs:
+                    raise NotPushable(f"nested {n} over a dimension")
+                pre = "long" if base(t) in ("tinyint", "smallint", "int", "bigint") else "double"
+                spec_ = S.FunctionAggregationSpec(pre + n.capitalize(), aname, name)
+            else:
+                raise NotPushable(f"nested aggregate {call.sql()}")
+            aggs.append(spec_)
+            rt = "bigint" if spec_.type in ("count", "longSum", "longMin", "longMax") else "double"
+            r = A.Ref(A.new_id(), aname, rt)
+            drefs.append(r)
+            columns.append((aname, rt, "value"))
+            ex = r if rt == out_t else A.Cast(r, out_t)
+            final[outs[len(agg.groups) + j].rid] = ex
+        if not dims:
+            raise NotPushable("global aggregate over a groupBy")
+        outer = S.GroupByQuerySpec(S.QueryDataSourceSpec(q), dims, None, None, S.Granularity.parse("all"), None,
+                                   aggs, None, q.intervals)
+        nq = P.DruidQuery(dq.relation, outer, columns, drefs, {"groupby": True, "nested": True,
+                                                              "historical": dq.info.get("historical")})
+        exprs = [A.Alias(final[r.rid], r.name, r.rid) for r in outs if r.rid in final]
+        return P.Project(exprs, nq)
+
+    def _having(self, f: P.Filter) -> None:
+        """HAVING over a pushed groupBy -> Druid ``havingSpec`` (comparisons of aggregate outputs
+        with numeric literals under AND / OR / NOT).  The engine evaluates it on the device before
+        any group is shipped; the host Filter stays for exact SQL semantics over the survivors."""
+        dq, m = self._druid_below(f.child)
+        if dq is None or not isinstance(dq.spec, S.GroupByQuerySpec):
+            return None
+        q = dq.spec
+        if q.having is not None or (q.limitSpec is not None and q.limitSpec.limit is not None):
+            return None
+        names = {r.rid: c[0] for r, c in zip(dq.refs, dq.columns)}
+        aggs = {a.name for a in (q.aggregations or [])}
+        flip = {"<": ">", ">": "<", "<=": ">=", ">=": "<=", "=": "=", "<>": "<>"}
+
+        def conv(e):
+            if isinstance(e, A.BinOp) and e.op in ("and", "or"):
+                return S.LogicalHavingSpec(e.op, [conv(e.l), conv(e.r)])
+            if isinstance(e, A.UnOp) and e.op == "not":
+                return S.NotHavingSpec(conv(e.child))
+            if isinstance(e, A.BinOp) and e.op in flip:
+                l, r, op = e.l, e.r, e.op
+                if isinstance(l, A.Lit):
+                    l, r, op = r, l, flip[op]
+                if not (isinstance(l, A.Ref) and l.rid in m and isinstance(r, A.Lit) and
+                        isinstance(r.value, (int, float)) and not isinstance(r.value, bool)):
+                    raise NotPushable(f"HAVING term {e.sql()}")
+                name = names[m[l.rid]]
+                if name not in aggs:
+                    raise NotPushable(f"HAVING over non-aggregate {e.sql()}")
+                v = float(r.value)
+
+                def cmp(t):
+                    return S.ComparisonHavingSpec(t, name, v)
+                return {">": cmp("greaterThan"), "<": cmp("lessThan"), "=": cmp("equalTo"),
+                        ">=": S.NotHavingSpec(cmp("lessThan")), "<=": S.NotHavingSpec(cmp("greaterThan")),
+                        "<>": S.NotHavingSpec(cmp("equalTo"))}[op]
+            raise NotPushable(f"HAVING term {e.sql()}")
+
+        dq.spec = q.copy(having=conv(f.cond))
+        return None
+
     def _limit(self, l: P.Limit) -> Optional[P.Plan]:
         dq, m = self._druid_below(l.child)
         if dq is None:
@@ -1061,6 +1185,14 @@ class DruidRewriter:
 
 
 # ------------------------------------------------------------------------------------------------
+def _non_null_dim(q, out_name: str, ds) -> bool:
+    for d in q.dimensions:
+        if d.outputName == out_name and isinstance(d, S.DefaultDimensionSpec):
+            dc = ds.dims.get(d.dimension) if ds is not None else None
+            return dc is not None and not dc.dictionary.has_null
+    return False
+
+
 class _Names:
     def __init__(self):
         self.n = 0

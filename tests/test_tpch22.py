@@ -103,3 +103,43 @@ def test_functional_dependency_key_elimination(ds_small):
         assert name_of.setdefault(ck, cn) == cn
     assert all(str(cn).startswith("Customer#") and int(str(cn)[9:]) == int(ck)
                for ck, cn in zip(r.data["o_custkey"], r.data["c_name"]))
+
+
+def test_nested_groupby_three_levels(ds_small, df_small):
+    """Query data source nesting on the engine: orders per customer, then customers per order
+    count (TPC-H Q13's shape) -- equal to pandas over the base rows; JSON round trip keeps it."""
+    import json
+
+    from spark_druid_olap_amd.query import spec as S
+
+    iv = ["1992-01-01/1999-01-01"]
+    inner = S.GroupByQuerySpec("tpch", [S.DefaultDimensionSpec("o_custkey"), S.DefaultDimensionSpec("o_orderkey")],
+                               aggregations=[S.FunctionAggregationSpec("longSum", "q", "l_quantity")], intervals=iv)
+    mid = S.GroupByQuerySpec(S.QueryDataSourceSpec(inner), [S.DefaultDimensionSpec("o_custkey")],
+                             aggregations=[S.FunctionAggregationSpec("count", "c_count"),
+                                           S.FunctionAggregationSpec("longSum", "qq", "q")], intervals=iv)
+    outer = S.GroupByQuerySpec(S.QueryDataSourceSpec(mid), [S.DefaultDimensionSpec("c_count")],
+                               aggregations=[S.FunctionAggregationSpec("count", "custdist"),
+                                             S.FunctionAggregationSpec("longMax", "mq", "qq")], intervals=iv)
+    outer = S.from_json(json.dumps(outer.to_json()))
+    r = Engine(use_native=False).execute(outer, ds_small)
+    got = sorted(zip(r.data["c_count"].tolist(), r.data["custdist"].tolist(), r.data["mq"].tolist()))
+    g = df_small.groupby("o_custkey").agg(c=("o_orderkey", "nunique"), q=("l_quantity", "sum")).reset_index()
+    e = g.groupby("c").agg(n=("o_custkey", "size"), mq=("q", "max")).reset_index()
+    assert got == sorted(zip(e.c.tolist(), e.n.tolist(), [int(x) for x in e.mq.tolist()]))
+
+
+@pytest.mark.parametrize("name", ["Q4", "Q13", "Q16"])
+def test_two_level_aggregates_become_one_nested_query(sess, name):
+    from spark_druid_olap_amd.query import spec as S
+
+    d = sess.sql(dict(tpch22.QUERIES)[name])
+    dq = d.druid_queries()
+    assert len(dq) == 1 and isinstance(dq[0].spec.dataSource, S.QueryDataSourceSpec), d.explain()
+
+
+def test_having_pushed_to_groupby(sess):
+    d = sess.sql(dict(tpch22.QUERIES)["Q18"])
+    (dq,) = d.druid_queries()
+    h = dq.spec.having
+    assert h is not None and h.aggregation and h.type == "greaterThan" and h.value == 300.0
