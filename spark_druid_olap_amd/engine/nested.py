@@ -30,11 +30,13 @@ class DeviceColumn:
     """One inner output column on the device.  ``ids`` (int64) for dimensions with ``decode``
     (ids -> values); ``vals`` (int64 with decimal ``scale``, or float64) for aggregates."""
 
-    def __init__(self, name: str, t: torch.Tensor, decode: Optional[Callable] = None, scale: int = 0):
+    def __init__(self, name: str, t: torch.Tensor, decode: Optional[Callable] = None, scale: int = 0,
+                 card: Optional[int] = None):
         self.name = name
         self.t = t
         self.decode = decode
         self.scale = scale
+        self.card = card  # key ids are known to lie in [0, card) (no min/max pass needed)
 
     @property
     def is_float(self) -> bool:
@@ -70,14 +72,16 @@ def device_columns(pq) -> Tuple[Dict[str, DeviceColumn], int]:
     for kc in prog.keys:
         ids = torch.remainder(torch.div(g, kc.stride, rounding_mode="floor"), max(1, kc.card))
         ids_of.append(ids)
-        cols[kc.name] = DeviceColumn(kc.name, ids, kc.decoder if kc.decoder is not None else (lambda x: x))
+        cols[kc.name] = DeviceColumn(kc.name, ids, kc.decoder if kc.decoder is not None else (lambda x: x),
+                                     card=max(1, kc.card))
     for kc, det, lut in getattr(prog, "derived", ()):
         did = ids_of[det]
         orig = prog.keys[det].orig
         if orig is not None:
             did = torch.from_numpy(orig).to(dev)[did]
         ids = torch.from_numpy(lut).to(dev)[did]
-        cols[kc.name] = DeviceColumn(kc.name, ids, kc.decoder if kc.decoder is not None else (lambda x: x))
+        cols[kc.name] = DeviceColumn(kc.name, ids, kc.decoder if kc.decoder is not None else (lambda x: x),
+                                     card=max(1, kc.card))
     for a in prog.aggs:
         col = part.acc[:, a.slot] if a.slot >= 0 else None
         if a.kind in ("count", "min_i", "max_i"):
@@ -142,26 +146,47 @@ class NestedPreparedQuery:
         elif keycols:
             packed = torch.zeros(n, dtype=torch.int64, device=dev)
             span = 1
+            radix = []  # (lo, card, stride) per key column
             for _, c in reversed(keycols):
-                lo = int(c.t.min().item())
-                hi = int(c.t.max().item())
-                card = hi - lo + 1
+                if c.card is not None:
+                    lo, card = 0, c.card
+                else:
+                    mm = torch.aminmax(c.t)
+                    lo, hi = int(mm.min.item()), int(mm.max.item())
+                    card = hi - lo + 1
                 if span * card >= 2 ** 62:
                     raise LoweringError("nested group key space exceeds 64 bits")
                 packed += (c.t - lo) * span
+                radix.append((lo, card, span))
                 span *= card
-            uk, inv = torch.unique(packed, return_inverse=True)
-            R = int(uk.numel())
-            # first inner row of every outer group: where its key values come from
-            firsts = torch.full((R,), n, dtype=torch.int64, device=dev)
-            firsts.scatter_reduce_(0, inv, torch.arange(n, device=dev), reduce="amin")
+            radix.reverse()
+            if span <= max(1 << 26, 4 * n):
+                # dense key space: presence bitmap + prefix ranks, no sort (Q13: 15M customers)
+                present = torch.zeros(span, dtype=torch.bool, device=dev)
+                present[packed] = True
+                rank = torch.cumsum(present, 0, dtype=torch.int64) - 1
+                inv = rank[packed]
+                slots = torch.nonzero(present).flatten()
+                R = int(slots.numel())
+                firsts = None
+            else:
+                uk, inv = torch.unique(packed, return_inverse=True)
+                R = int(uk.numel())
+                slots = uk
+                firsts = None
         else:
             inv = torch.zeros(n, dtype=torch.int64, device=dev)
             R = 1
             firsts = torch.zeros(1, dtype=torch.int64, device=dev)
         out: Dict[str, DeviceColumn] = {}
-        for d, c in keycols:
-            out[d.outputName] = DeviceColumn(d.outputName, c.t.index_select(0, firsts), c.decode, c.scale)
+        for j, (d, c) in enumerate(keycols):
+            if n == 0:
+                t = c.t[:0]
+            else:
+                lo, card, stride = radix[j]
+                # key components straight from the packed group key
+                t = torch.remainder(torch.div(slots, stride, rounding_mode="floor"), card) + lo
+            out[d.outputName] = DeviceColumn(d.outputName, t, c.decode, c.scale, c.card)
         for a in qs.aggregations:
             if a.type == "count":
                 v = torch.zeros(R, dtype=torch.int64, device=dev).index_add_(0, inv, torch.ones_like(inv))

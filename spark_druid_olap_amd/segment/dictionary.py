@@ -297,8 +297,9 @@ class FormattedDictionary(Dictionary):
         return np.array([self.value(i) for i in range(self.n)], dtype=object)
 
     def decode(self, ids):
-        ids = np.asarray(ids, dtype=np.int64)
-        return np.array([self.value(i) for i in ids], dtype=object)
+        ids = np.asarray(ids, dtype=np.int64) + self.start
+        fmt = self.prefix.replace("%", "%%") + f"%0{self.width}d" + self.suffix.replace("%", "%%")
+        return np.array([fmt % i for i in ids.tolist()], dtype=object)
 
     def lookup(self, v):
         if v is None:
