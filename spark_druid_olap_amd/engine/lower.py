@@ -14,6 +14,7 @@ This is where Druid's per-segment engine semantics are re-designed for the GPU:
 from __future__ import annotations
 
 import math
+import os
 import re
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
@@ -289,8 +290,8 @@ class ScanProgram:
     luts: Dict[str, torch.Tensor] = field(default_factory=dict)       # dim -> f64 value per dictionary id
     lut_ptrs: Dict[float, torch.Tensor] = field(default_factory=dict)  # E_LUT operand -> its table
     # grouping keys functionally determined by a packed key: (key, index of determinant in keys,
-    # np.int64 table determinant dictionary id -> dependent dictionary id)
-    derived: List[Tuple["KeyComp", int, np.ndarray]] = field(default_factory=list)
+    # device int32 table determinant dictionary id -> dependent dictionary id)
+    derived: List[Tuple["KeyComp", int, torch.Tensor]] = field(default_factory=list)
     key_order: List[str] = field(default_factory=list)  # output order of all grouping keys
 
     def col(self, name: str) -> int:
@@ -1031,7 +1032,7 @@ class Lowerer:
             ast = parse_expr(expr)
             mapping = dict(zip(params, a.fieldNames))
             eops = self._emit_expr(prog, ast, mapping)
-            if op == "sum":
+            if op == "sum" and not os.environ.get("SDO_NO_EXACT_SUM"):
                 ex = self._exact_decimal(ast, mapping)
                 if ex is not None:
                     # exact decimal sum: per-row value * 10^scale rounded to int64 (exact: the bound
@@ -1127,6 +1128,8 @@ class Lowerer:
         (``functionalDependencies`` DDL option, ``sd/FunctionalDependencies.scala``); here they
         are verified on the index itself (and across ranks), so no declaration can make results
         wrong."""
+        if os.environ.get("SDO_NO_FD"):
+            return
         cand = [i for i, kc in enumerate(prog.keys) if kc.kind == D.K_ID and kc.card > 1]
         if len(cand) < 2:
             return
@@ -1299,9 +1302,9 @@ def _ast_cols(a) -> List[str]:
 _FD_CHUNK = 1 << 26
 
 
-def fd_table(ds: DataSource, a: str, b: str, world=None) -> Optional[np.ndarray]:
+def fd_table(ds: DataSource, a: str, b: str, world=None) -> Optional[torch.Tensor]:
     """If dimension ``a`` functionally determines dimension ``b`` over every row of the index
-    (all shards), the table a-id -> b-id (int64, -1 for ids absent everywhere); else None.
+    (all shards), the device table a-id -> b-id (int32, -1 for ids absent everywhere); else None.
     Two scatter/gather passes over the id columns on the device, cached per datasource."""
     cache = ds.__dict__.setdefault("_fd_cache", {})
     key = (a, b)
@@ -1329,7 +1332,9 @@ def fd_table(ds: DataSource, a: str, b: str, world=None) -> Optional[np.ndarray]
         ok &= ((lo == big) | (lo == hi)).all().to(torch.int64)
         ok = world.all_reduce(ok, "min")
         lut = hi
-    out = lut.cpu().numpy() if bool(ok.item()) else None
+    # kept on the device (int32): finalize gathers the dependent ids of the result groups there --
+    # a host gather into a 150M-entry table costs a cache miss per group
+    out = lut.to(torch.int32) if bool(ok.item()) else None
     cache[key] = out
     return out
 

@@ -79,7 +79,7 @@ def device_columns(pq) -> Tuple[Dict[str, DeviceColumn], int]:
         orig = prog.keys[det].orig
         if orig is not None:
             did = torch.from_numpy(orig).to(dev)[did]
-        ids = torch.from_numpy(lut).to(dev)[did]
+        ids = lut.to(dev)[did].to(torch.int64)
         cols[kc.name] = DeviceColumn(kc.name, ids, kc.decoder if kc.decoder is not None else (lambda x: x),
                                      card=max(1, kc.card))
     for a in prog.aggs:

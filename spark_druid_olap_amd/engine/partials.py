@@ -109,6 +109,7 @@ def finalize(prog, parts: Partials) -> Dict[str, np.ndarray]:
             acc_h = acc_h[gid]
             hll_d = [h.index_select(0, torch.from_numpy(gid).to(h.device)) for h in parts.hll]
             key_ids = [(gid // kc.stride) % max(1, kc.card) for kc in prog.keys]
+            derived_ids = None
         else:
             parts = parts.compact()
     if parts.kind == "sparse":
@@ -118,9 +119,18 @@ def finalize(prog, parts: Partials) -> Dict[str, np.ndarray]:
         for kc in prog.keys:
             ids = torch.remainder(torch.div(g, kc.stride, rounding_mode="floor"), max(1, kc.card))
             dev_ids.append(ids.to(torch.int32) if kc.card < 2 ** 31 else ids)
+        nk = len(dev_ids)
+        for kc, det, lut in getattr(prog, "derived", ()):
+            # functionally dependent keys: gather their ids on the device
+            did = dev_ids[det].to(torch.int64)
+            orig = prog.keys[det].orig
+            if orig is not None:
+                did = torch.from_numpy(orig).to(did.device)[did]
+            dev_ids.append(lut.to(did.device)[did])
         # slot-major accumulators so every output column is a contiguous view (no host copies)
         host = d2h(dev_ids + [parts.acc.t().contiguous()] + ([g] if want_gid else []))
-        key_ids = host[:len(dev_ids)]
+        key_ids = host[:nk]
+        derived_ids = host[nk:len(dev_ids)]
         acc_h = host[len(dev_ids)].T
         gid = host[-1] if want_gid else None
         hll_d = parts.hll
@@ -130,13 +140,16 @@ def finalize(prog, parts: Partials) -> Dict[str, np.ndarray]:
         vals = kc.decoder(ids) if kc.decoder is not None else ids
         key_vals.append(vals)
         cols[kc.name] = vals
-    for kc, det, lut in getattr(prog, "derived", ()):
+    for j, (kc, det, lut) in enumerate(getattr(prog, "derived", ())):
         # functionally dependent key: its id through the FD table of the determinant's original id
-        did = np.asarray(key_ids[det], dtype=np.int64)
-        orig = prog.keys[det].orig
-        if orig is not None:
-            did = orig[did]
-        ids = lut[did]
+        if derived_ids is not None:
+            ids = derived_ids[j]
+        else:
+            did = np.asarray(key_ids[det], dtype=np.int64)
+            orig = prog.keys[det].orig
+            if orig is not None:
+                did = orig[did]
+            ids = lut[torch.from_numpy(did).to(lut.device)].cpu().numpy()
         vals = kc.decoder(ids) if kc.decoder is not None else ids
         key_vals.append(vals)
         cols[kc.name] = vals

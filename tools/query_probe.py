@@ -103,7 +103,8 @@ def main():
             else:
                 base[name] = r
             print(f"  {name[:40]:40s} med {statistics.median(ts[1:]):7.3f} ms  first {ts[0]:7.2f}  {info} "
-                  f"prep {time.time() - t - sum(ts) / 1e3:.2f}s rows={r.num_rows} {ok}", flush=True)
+                  f"prep {time.time() - t - sum(ts) / 1e3:.2f}s rows={r.num_rows} {ok} "
+                  + " ".join(f"{k}={v:.2f}" for k, v in r.stats.items() if k.endswith("_ms")), flush=True)
 
 
 if __name__ == "__main__":
