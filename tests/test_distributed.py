@@ -27,6 +27,11 @@ QUERIES = [
     "select l_shipmode, count(distinct o_orderkey) from orderLineItemPartSupplier group by l_shipmode",
     "select l_returnflag, count(*) from orderLineItemPartSupplier group by l_returnflag with rollup",
 ]
+# the full TPC-H sweep: FD tables all-reduced across ranks, nested device aggregation over merged
+# partials, execution-time scalar subqueries, device HAVING, expression filters
+from spark_druid_olap_amd.models import tpch22 as _tpch22  # noqa: E402
+
+QUERIES += [q for _, q in _tpch22.QUERIES]
 APPROX = "select l_returnflag, approx_count_distinct(o_orderkey) from orderLineItemPartSupplier group by l_returnflag"
 
 
