@@ -1078,6 +1078,25 @@ class DruidRewriter:
                         "<>": S.NotHavingSpec(cmp("equalTo"))}[op]
             raise NotPushable(f"HAVING term {e.sql()}")
 
+        sqs = [x for x in f.cond.walk() if isinstance(x, A.SubqueryExpr)]
+        if sqs:
+            # HAVING against scalar subqueries (TPC-H Q11): resolved when the subqueries have run
+            if any(x.kind != "scalar" for x in sqs):
+                raise NotPushable("IN / EXISTS subquery in HAVING")
+
+            def build(values, _c=f.cond):
+                def sub(x):
+                    if isinstance(x, A.SubqueryExpr):
+                        return A.Lit(values[id(x)], typeof(x))
+                    return None
+                return conv(constant_fold(_c.transform(sub)))
+
+            build({id(x): 1.5 for x in sqs})  # shape check with placeholder values
+            d = S.DeferredFilterSpec(f.cond.sql())
+            d.subqueries, d.build = sqs, build
+            dq.spec = q.copy(having=d)
+            dq.__dict__.pop("_deferred", None)
+            return None
         dq.spec = q.copy(having=conv(f.cond))
         return None
 

@@ -51,6 +51,7 @@ class Executor:
         self.token = token
         self.druid_stats: List[dict] = []
         self._subq_cache: Dict[int, object] = {}
+        self._druid_results: Dict[str, object] = {}
 
     # ----------------------------------------------------------------------------------------
     def run(self, plan: P.Plan) -> Batch:
@@ -216,7 +217,16 @@ class Executor:
                 q = cache[key] = P.DruidQuery(p.relation, S.resolve_deferred(p.spec, vals), p.columns, p.refs,
                                               p.info)
             p = q
-        res = self.session.run_druid(p)
+        # identical pushed queries within one statement (a CTE referenced twice, TPC-H Q15) run once
+        key = p.__dict__.get("_share_key")
+        if key is None:
+            import json
+
+            key = p._share_key = json.dumps(p.spec.to_json(), sort_keys=True, default=str) + \
+                str(id(p.relation.info.datasource)) + repr(p.info.get("historical"))
+        res = self._druid_results.get(key)
+        if res is None:
+            res = self._druid_results[key] = self.session.run_druid(p)
         cols = {}
         n = res.num_rows
         for r, (name, sqlt, kind) in zip(p.refs, p.columns):
@@ -364,6 +374,7 @@ def druid_value_series(col, sqlt: str, kind: str, n: int) -> pd.Series:
 
 
 _FULL_DICT_MAX = 1 << 20
+_LAZY_DICT_MAX = 1 << 22
 
 
 def _dict_series(col, sqlt: str) -> pd.Series:
@@ -373,7 +384,10 @@ def _dict_series(col, sqlt: str) -> pd.Series:
     d = col.dictionary
     codes = np.asarray(col.codes)
     nd = len(d)
-    if nd <= _FULL_DICT_MAX and (nd <= 65536 or nd <= 2 * len(codes)):
+    lazy_ok = getattr(d, "lazy", False) and nd <= _LAZY_DICT_MAX and base(sqlt) == "string"
+    if (nd <= _FULL_DICT_MAX and (nd <= 65536 or nd <= 2 * len(codes))) or lazy_ok:
+        # (lazy synthetic dictionaries up to a few million entries are materialised once, like the
+        # string dictionaries a Druid historical keeps in memory; per query only codes move)
         cache = d.__dict__.setdefault("_sql_typed", {})
         key = sqlt if base(sqlt) != "string" else "__categories__"
         full = cache.get(key)
