@@ -93,7 +93,7 @@ def _next_pow2(x: int) -> int:
 
 
 class PreparedScan:
-    def __init__(self, prog: ScanProgram, mode: Optional[int] = None):
+    def __init__(self, prog: ScanProgram, mode: Optional[int] = None, dense_max: Optional[int] = None):
         self.prog = prog
         ds = prog.ds
         self.dev = ds.device
@@ -114,7 +114,9 @@ class PreparedScan:
                     and hll_bytes <= DENSE_GLOBAL_MAX_BYTES:
                 mode = D.M_DENSE_LDS
                 self.shared = True
-            elif acc_bytes + hll_bytes <= DENSE_GLOBAL_MAX_BYTES:
+            elif (acc_bytes + hll_bytes <= DENSE_GLOBAL_MAX_BYTES) if dense_max is None else \
+                    (G * ns * 8 + hll_bytes <= dense_max):
+                # one HBM table indexed by the packed key (dense_max: real table bytes, one GPU)
                 mode = D.M_DENSE_GLOBAL
             else:
                 mode = D.M_HASH

@@ -9,6 +9,7 @@ reference gets back from the Druid broker and post-processes in Spark
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence
@@ -111,7 +112,11 @@ class PreparedQuery:
         if is_cuda_ds(self.ds) and self.engine.use_native:
             from .device_exec import PreparedScan
 
-            return PreparedScan(prog)
+            # one GPU: a dense HBM table of up to 16 GB beats a hash table over the same key space
+            # (TPC-H Q18: 150M order groups); with several ranks dense partials are reduced whole,
+            # so huge key spaces stay sparse (hash) and merge by present keys
+            dense_max = None if self.world.distributed else int(os.environ.get("SDO_DENSE_MAX_1GPU", 16 << 30))
+            return PreparedScan(prog, dense_max=dense_max)
         return None
 
     def _prepare_mask(self, prog: ScanProgram):
