@@ -1117,6 +1117,39 @@ class Lowerer:
             raise LoweringError("aggregator expression too deep for the device VM")
         return out
 
+    def fold_presence_slot(self, prog: ScanProgram) -> None:
+        """The hidden presence count (slot 0) only has to be > 0 for groups that exist.  An
+        unfiltered long sum over a metric whose values are all >= 1 (l_quantity) has exactly that
+        property, so it becomes slot 0 and the scan does one atomic less per row (TPC-H Q18 over
+        150M order groups: 3 -> 2 HBM atomics per line)."""
+        if os.environ.get("SDO_NO_FOLD_PRESENCE") or len(prog.aops) < 2 or prog.aops[0]["slot"] != 0:
+            return
+        if any(d["slot"] == 0 for d in prog.aops[1:]) or any(a.slot == 0 for a in prog.aggs):
+            return  # a user count(*) already shares the presence slot
+        for d in prog.aops[1:]:
+            if d["kind"] != D.A_SUM_I or d["filter"] is not None or d["expr"] is not None or d["col"] < 0:
+                continue
+            name = prog.colname(d["col"])
+            m = self.ds.metrics.get(name)
+            if m is None or name in self.ds.dims or not m.is_integral or self._metric_range(name)[0] < 1:
+                continue
+            s_old = d["slot"]
+            if sum(1 for x in prog.aops if x["slot"] == s_old) != 1:
+                continue
+            prog.aops.pop(0)
+            prog.slots.pop(s_old)
+            for x in prog.aops:
+                if x is d:
+                    x["slot"] = 0
+                elif x["slot"] > s_old:
+                    x["slot"] -= 1
+            for a in prog.aggs:
+                if a.slot == s_old:
+                    a.slot = 0
+                elif a.slot > s_old:
+                    a.slot -= 1
+            return
+
     # ------------------------------------------------------------------ functional dependencies
     def eliminate_dependent_keys(self, prog: ScanProgram) -> None:
         """Drop grouping keys that another grouping key functionally determines in the data
@@ -1183,6 +1216,7 @@ class Lowerer:
             raise LoweringError("too many grouping keys")
         for a in aggregations:
             self.add_aggregator(prog, a)
+        self.fold_presence_slot(prog)
         prog.key_order = [kc.name for kc in prog.keys]
         self.eliminate_dependent_keys(prog)
         # filter-implied key domains: a dimension the filter pins to a few values only needs

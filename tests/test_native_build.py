@@ -41,6 +41,7 @@ def test_jit_shared_table_kernel_compiles(tmp_path, monkeypatch):
     from spark_druid_olap_amd.session import Session
 
     monkeypatch.setenv("SDO_JIT_CACHE", str(tmp_path))
+    monkeypatch.setenv("SDO_NO_FOLD_PRESENCE", "1")  # keep the two-slot layout this test sizes
     ds = ssb.to_datasource(ssb.generate_flat(0.002, "cpu"))
     s = Session(engine=Engine(use_native=False))
     s.register_datasource(ds)

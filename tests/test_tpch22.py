@@ -143,3 +143,21 @@ def test_having_pushed_to_groupby(sess):
     (dq,) = d.druid_queries()
     h = dq.spec.having
     assert h is not None and h.aggregation and h.type == "greaterThan" and h.value == 300.0
+
+
+def test_presence_slot_folds_into_positive_sum(ds_small, df_small):
+    """sum(l_quantity) (all values >= 1) doubles as the group-presence slot: one accumulator."""
+    from spark_druid_olap_amd.engine.lower import Lowerer
+    from spark_druid_olap_amd.query import spec as S
+
+    dims = [S.DefaultDimensionSpec("l_shipmode")]
+    aggs = [S.FunctionAggregationSpec("longSum", "q", "l_quantity"),
+            S.FunctionAggregationSpec("doubleSum", "e", "l_extendedprice")]
+    prog = Lowerer(ds_small).lower_aggregate(["1992-01-01/1999-01-01"], None, dims, None, aggs)
+    assert prog.nslots == 2 and {a.name: a.slot for a in prog.aggs}["q"] == 0
+    r = Engine(use_native=False).execute(S.GroupByQuerySpec("tpch", dims, aggregations=aggs,
+                                                            intervals=["1992-01-01/1999-01-01"]), ds_small)
+    exp = df_small.groupby("l_shipmode")["l_quantity"].sum()
+    got = dict(zip(r.data["l_shipmode"].tolist() if hasattr(r.data["l_shipmode"], "tolist") else
+                   list(r.data["l_shipmode"]), r.data["q"].tolist()))
+    assert {str(k): int(v) for k, v in got.items()} == {k: int(v) for k, v in exp.items()}
