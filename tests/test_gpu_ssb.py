@@ -50,4 +50,8 @@ def test_shared_lds_mode_chosen(sessions):
         spec = nat.sql(dict(ssb.ALL_QUERIES)[name]).druid_query_specs()[0]
         prep = nat.engine.prepare(spec, ds).scans[0][2]
         assert isinstance(prep, PreparedScan)
-        assert prep.mode == D.M_DENSE_LDS and prep.shared and prep.jit is not None and prep.jit.lay.shared, name
+        assert prep.mode == D.M_DENSE_LDS and prep.jit is not None, name
+        # thousand-group key spaces: one shared LDS table per workgroup, unless the accumulators
+        # are narrow enough (presence slot folded into sum(lo_revenue)) for per-wave copies
+        per_wave = prep.prog.G * prep.prog.nslots * 8 * 4 <= 64 * 1024
+        assert per_wave or (prep.shared and prep.jit.lay.shared), name
