@@ -21,6 +21,8 @@ def main():
     ap.add_argument("db")
     ap.add_argument("--all", action="store_true")
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--tail-ms", type=float, default=0.0,
+                    help="only kernels starting in the last T ms of the trace (the timed steps)")
     a = ap.parse_args()
     con = sqlite3.connect(a.db)
     rows = con.execute("select name, start, end from kernels order by start").fetchall()
@@ -30,6 +32,8 @@ def main():
             if n.startswith("sdo_jit") or n.startswith("sdo::olap_scan"):
                 t0 = s
                 break
+    if a.tail_ms > 0 and rows:
+        t0 = max(e for _, _, e in rows) - int(a.tail_ms * 1e6)
     agg = defaultdict(lambda: [0, 0.0, 1e30, 0.0])
     total = 0.0
     for n, s, e in rows:
