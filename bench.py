@@ -108,6 +108,10 @@ def main():
 
         queries = [(name, engine.prepare(q, ds)) for name, q in bench_specs()]
 
+    only = [x for x in os.environ.get("SDO_BENCH_ONLY", "").split(",") if x]
+    if only:  # diagnostics: a subset of the suite (the JSON line then describes only that subset)
+        queries = [(n, q) for n, q in queries if n in only]
+
     def sync():
         if dev.type == "cuda":
             torch.cuda.synchronize()

@@ -272,3 +272,21 @@ def test_pull_vcols_into_agg(sess):
     assert aggs and isinstance(aggs[0].child, P.Project)
     assert all(type(e).__name__ == "Ref" for e in aggs[0].child.exprs)
     assert "l_discount" in aggs[0].aggs[0].sql()
+
+
+def test_numeric_key_join_matches_pandas_merge():
+    import numpy as np
+
+    from spark_druid_olap_amd.sql.execute import _numeric_key_join
+
+    rng = np.random.default_rng(7)
+    l1, l2 = rng.integers(0, 50, 3000), rng.integers(0, 4, 3000).astype(np.float64) / 2
+    r1, r2 = rng.integers(0, 60, 800), rng.integers(0, 4, 800).astype(np.float64) / 2
+    lok, rok = rng.random(3000) > 0.1, rng.random(800) > 0.1
+    li, ri = _numeric_key_join([pd.Series(l1), pd.Series(l2)], [pd.Series(r1), pd.Series(r2)], lok, rok)
+    L = pd.DataFrame({"a": l1, "b": l2, "_li": np.arange(3000)})[lok]
+    R = pd.DataFrame({"a": r1, "b": r2, "_ri": np.arange(800)})[rok]
+    m = L.merge(R, on=["a", "b"], how="inner")
+    assert sorted(zip(li.tolist(), ri.tolist())) == sorted(zip(m._li.tolist(), m._ri.tolist()))
+    assert list(li) == sorted(li)  # left-row order
+    assert _numeric_key_join([pd.Series(["x"])], [pd.Series(["x"])], np.ones(1, bool), np.ones(1, bool)) is None
