@@ -97,6 +97,30 @@ def device_columns(pq) -> Tuple[Dict[str, DeviceColumn], int]:
     return cols, int(part.acc.shape[0])
 
 
+def _torch_eval(n, pmap: Dict[str, str], cols: Dict[str, DeviceColumn]) -> torch.Tensor:
+    """f64 value per inner row of a javascript-aggregator expression AST (query/jsfunc.parse_expr)."""
+    k = n[0]
+    if k == "const":
+        return torch.tensor(float(n[1]), dtype=torch.float64)
+    if k == "col":
+        c = cols.get(pmap.get(n[1], n[1]))
+        if c is None:
+            raise LoweringError(f"nested expression over unknown column {n[1]!r}")
+        return c.as_float() if c.decode is None else c.t.to(torch.float64)
+    if k in ("neg", "abs", "floor", "ceil", "sqrt", "log", "exp"):
+        a = _torch_eval(n[1], pmap, cols)
+        return {"neg": torch.neg, "abs": torch.abs, "floor": torch.floor, "ceil": torch.ceil, "sqrt": torch.sqrt,
+                "log": torch.log, "exp": torch.exp}[k](a)
+    a, b = _torch_eval(n[1], pmap, cols), _torch_eval(n[2], pmap, cols)
+    if a.device != b.device:
+        a, b = a.to(b.device) if a.dim() == 0 else a, b.to(a.device) if b.dim() == 0 else b
+    fns = {"add": torch.add, "sub": torch.sub, "mul": torch.mul, "div": torch.div, "min": torch.minimum,
+           "max": torch.maximum, "mod": torch.fmod, "pow": torch.pow}
+    if k not in fns:
+        raise LoweringError(f"nested expression operator {k}")
+    return fns[k](a, b)
+
+
 class NestedPreparedQuery:
     """groupBy over a query data source (see module doc)."""
 
@@ -113,7 +137,17 @@ class NestedPreparedQuery:
         for d in qs.dimensions:
             if not isinstance(d, S.DefaultDimensionSpec):
                 raise LoweringError("nested groupBy dimensions must be default dimension specs")
+        self._js = {}
         for a in qs.aggregations:
+            if isinstance(a, S.JavascriptAggregationSpec):
+                from ..query.jsfunc import JSError, jsagg_to_expr, parse_expr
+
+                try:
+                    op, params, expr = jsagg_to_expr(a.fnAggregate)
+                    self._js[a.name] = (op, dict(zip(params, a.fieldNames)), parse_expr(expr))
+                except JSError as e:
+                    raise LoweringError(f"nested javascript aggregator not translatable: {e}")
+                continue
             if not (isinstance(a, S.FunctionAggregationSpec) and
                     a.type in ("count", "longSum", "doubleSum", "longMin", "longMax", "doubleMin", "doubleMax")):
                 raise LoweringError(f"nested groupBy aggregator {type(a).__name__}")
@@ -188,6 +222,19 @@ class NestedPreparedQuery:
                 t = torch.remainder(torch.div(slots, stride, rounding_mode="floor"), card) + lo
             out[d.outputName] = DeviceColumn(d.outputName, t, c.decode, c.scale, c.card)
         for a in qs.aggregations:
+            if a.name in self._js:
+                op, pmap, ast = self._js[a.name]
+                src = _torch_eval(ast, pmap, cols)
+                if src.dim() == 0:
+                    src = src.expand(n).contiguous()
+                if op == "sum":
+                    acc = torch.zeros(R, dtype=torch.float64, device=dev).index_add_(0, inv, src)
+                else:
+                    acc = torch.full((R,), float("inf") if op == "min" else float("-inf"), dtype=torch.float64,
+                                     device=dev)
+                    acc.scatter_reduce_(0, inv, src, reduce="amin" if op == "min" else "amax")
+                out[a.name] = DeviceColumn(a.name, acc)
+                continue
             if a.type == "count":
                 v = torch.zeros(R, dtype=torch.int64, device=dev).index_add_(0, inv, torch.ones_like(inv))
                 out[a.name] = DeviceColumn(a.name, v)
@@ -232,6 +279,8 @@ class NestedPreparedQuery:
         import pandas as pd
 
         qs = self.qs
+        if self._js:
+            raise LoweringError("javascript aggregators of a nested groupBy need the device path")
         t0 = time.perf_counter()
         cols, n = self._host_inner()
         inner_ms = (time.perf_counter() - t0) * 1e3
@@ -275,7 +324,8 @@ class NestedPreparedQuery:
         for a in qs.aggregations:
             c = dcols[a.name]
             h = c.host_values(c.t)
-            out[a.name] = np.asarray(h, dtype=np.int64) if ((a.type == "count" or a.type.startswith("long")) and not c.scale) \
+            t_ = getattr(a, "type", "")
+            out[a.name] = np.asarray(h, dtype=np.int64) if ((t_ == "count" or t_.startswith("long")) and not c.scale) \
                 else np.asarray(h, dtype=np.float64)
             names.append(a.name)
         return self._finish(out, R, inner_ms, t0)

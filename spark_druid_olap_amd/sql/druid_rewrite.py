@@ -1016,16 +1016,34 @@ class DruidRewriter:
                                                                          dq.relation.info.datasource)):
                 # inner aggregates / NULL-free dimensions: count(x) == count(*)
                 spec_ = S.FunctionAggregationSpec("count", aname, "count")
-            elif n in ("sum", "min", "max") and len(call.args) == 1:
+            elif n in ("sum", "min", "max") and len(call.args) == 1 and isinstance(call.args[0], A.Ref):
                 name, t, kind = inner_col(call.args[0])
                 if name not in inner_aggs:
                     raise NotPushable(f"nested {n} over a dimension")
                 pre = "long" if base(t) in ("tinyint", "smallint", "int", "bigint") else "double"
                 spec_ = S.FunctionAggregationSpec(pre + n.capitalize(), aname, name)
+            elif n in ("sum", "min", "max") and len(call.args) == 1 and vm_compatible(call.args[0]):
+                # arithmetic over inner aggregates (TPC-H Q17 sum(qty * n)): javascript aggregator
+                # over the inner columns, evaluated with device tensor ops in the nested engine
+                x = call.args[0]
+                jn: Dict[int, str] = {}
+                fields: List[str] = []
+                for r_ in x.refs():
+                    name, t, kind = inner_col(r_)
+                    if name not in inner_aggs and kind != "value":
+                        raise NotPushable(f"nested expression over dimension {name}")
+                    if r_.rid not in jn:
+                        jn[r_.rid] = f"p{len(fields)}"
+                        fields.append(name)
+                try:
+                    fa, fc, fr = js_aggregator(n, x, jn, [f"p{i}" for i in range(len(fields))])
+                except JSGenError as ex:
+                    raise NotPushable(str(ex))
+                spec_ = S.JavascriptAggregationSpec(aname, fields, fa, fc, fr)
             else:
                 raise NotPushable(f"nested aggregate {call.sql()}")
             aggs.append(spec_)
-            rt = "bigint" if spec_.type in ("count", "longSum", "longMin", "longMax") else "double"
+            rt = "bigint" if getattr(spec_, "type", "") in ("count", "longSum", "longMin", "longMax") else "double"
             r = A.Ref(A.new_id(), aname, rt)
             drefs.append(r)
             columns.append((aname, rt, "value"))
