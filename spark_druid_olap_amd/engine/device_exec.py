@@ -220,8 +220,16 @@ class PreparedScan:
             self._alloc()
         if self.mode == D.M_HASH:
             valid = _nonzero_big(self.keys != -1)
-            return Partials("sparse", self.acc.index_select(0, valid), self.keys.index_select(0, valid),
-                            [h.view(self.rows, self.m).index_select(0, valid) for h in self.hll])
+            out = Partials("sparse", self.acc.index_select(0, valid), self.keys.index_select(0, valid),
+                           [h.view(self.rows, self.m).index_select(0, valid) for h in self.hll])
+            # adaptive capacity: the planner's row estimate sizes the first table (TPC-H Q16's NOT
+            # filters: 2^31 slots for 12M groups); later runs of this prepared query size it from
+            # the observed group count (an overflow still grows it and retries)
+            want = _next_pow2(2 * int(valid.numel()) + 1024)
+            if want * 4 <= self.cap:
+                self.cap = want
+                self._alloc()
+            return out
         return Partials("dense", self.acc, None, [h.view(self.rows, self.m) for h in self.hll])
 
     def _empty(self) -> Partials:

@@ -1370,6 +1370,8 @@ def fd_table(ds: DataSource, a: str, b: str, world=None) -> Optional[torch.Tenso
     # a host gather into a 150M-entry table costs a cache miss per group
     out = lut.to(torch.int32) if bool(ok.item()) else None
     cache[key] = out
+    if os.environ.get("SDO_TRACE_FD"):
+        print(f"[fd] {a} -> {b}: {'yes' if out is not None else 'no'}", flush=True)
     return out
 
 
