@@ -684,12 +684,23 @@ def _numeric_key_join(lks, rks, lok: np.ndarray, rok: np.ndarray):
     into one int64 code, the right side is sorted once and every left row finds its match range
     with a binary search.  Output pairs are in left-row order (like pandas' inner merge).  None
     when a key is not a plain numeric column."""
+    def plain(x: pd.Series):
+        dt = x.dtype
+        if isinstance(dt, np.dtype):
+            return x.to_numpy() if dt.kind in "iuf" else None
+        kind = getattr(getattr(dt, "numpy_dtype", None), "kind", "")
+        if kind in "iu" and kind:  # nullable Int64 (NULL rows are masked out by the caller)
+            return x.to_numpy(dtype=np.int64, na_value=0)
+        if kind == "f":
+            return x.to_numpy(dtype=np.float64, na_value=np.nan)
+        return None
+
     arrs = []
     for a, b in zip(lks, rks):
-        if not (isinstance(a.dtype, np.dtype) and isinstance(b.dtype, np.dtype) and a.dtype.kind in "iuf"
-                and b.dtype.kind in "iuf"):
+        x, y = plain(a), plain(b)
+        if x is None or y is None:
             return None
-        arrs.append((a.to_numpy(), b.to_numpy()))
+        arrs.append((x, y))
     li_all = np.nonzero(lok)[0]
     ri_all = np.nonzero(rok)[0]
     lc = np.zeros(len(li_all), dtype=np.int64)

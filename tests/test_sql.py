@@ -290,3 +290,14 @@ def test_numeric_key_join_matches_pandas_merge():
     assert sorted(zip(li.tolist(), ri.tolist())) == sorted(zip(m._li.tolist(), m._ri.tolist()))
     assert list(li) == sorted(li)  # left-row order
     assert _numeric_key_join([pd.Series(["x"])], [pd.Series(["x"])], np.ones(1, bool), np.ones(1, bool)) is None
+
+
+def test_numeric_key_join_nullable_ints():
+    import numpy as np
+
+    from spark_druid_olap_amd.sql.execute import _numeric_key_join
+
+    l = pd.Series([1, 2, None, 2], dtype="Int64")
+    r = pd.Series([2, 1, 2], dtype="Int64")
+    li, ri = _numeric_key_join([l], [r], l.notna().to_numpy(), r.notna().to_numpy())
+    assert sorted(zip(li.tolist(), ri.tolist())) == [(0, 1), (1, 0), (1, 2), (3, 0), (3, 2)]
