@@ -616,33 +616,42 @@ def _equi_keys(cond: Optional[A.Expr], lrefs, rrefs):
     return keys, rest
 
 
-def _key_frame(exprs, b: Batch, subq, null_safe):
+def _key_series(exprs, b: Batch, subq) -> List[pd.Series]:
     fr = b.frame(subq)
+    return [eval_series(e, fr) for e in exprs]
+
+
+def _key_frame_of(series: List[pd.Series]) -> pd.DataFrame:
     d = {}
-    for i, e in enumerate(exprs):
-        s = eval_series(e, fr)
+    for i, s in enumerate(series):
         d[f"k{i}"] = s.astype(object).where(s.notna(), None) if s.dtype.kind != "M" else s
     return pd.DataFrame(d)
+
+
+def _key_frame(exprs, b: Batch, subq, null_safe):
+    return _key_frame_of(_key_series(exprs, b, subq))
 
 
 def join(p: P.Join, lb: Batch, rb: Batch, subq=None) -> Batch:
     keys, rest = _equi_keys(p.cond, lb.refs, rb.refs)
     kind = p.kind
     if keys:
-        lkf = _key_frame([k[0] for k in keys], lb, subq, None)
-        rkf = _key_frame([k[1] for k in keys], rb, subq, None)
+        lks = _key_series([k[0] for k in keys], lb, subq)
+        rks = _key_series([k[1] for k in keys], rb, subq)
         # SQL: NULL keys never match (unless <=>)
         lnull = np.zeros(lb.n, dtype=bool)
         rnull = np.zeros(rb.n, dtype=bool)
         for i, (_, _, ns) in enumerate(keys):
             if not ns:
-                lnull |= lkf[f"k{i}"].isna().to_numpy()
-                rnull |= rkf[f"k{i}"].isna().to_numpy()
+                lnull |= lks[i].isna().to_numpy()
+                rnull |= rks[i].isna().to_numpy()
         cols = [f"k{i}" for i in range(len(keys))]
-        fast = _numeric_key_join([lkf[c] for c in cols], [rkf[c] for c in cols], ~lnull, ~rnull)
+        null_safe = any(ns for _, _, ns in keys)
+        fast = None if null_safe else _numeric_key_join(lks, rks, ~lnull, ~rnull)
         if fast is not None:
             li, ri = fast
         else:
+            lkf, rkf = _key_frame_of(lks), _key_frame_of(rks)
             lkf["_li"] = np.arange(lb.n)
             rkf["_ri"] = np.arange(rb.n)
             m = lkf[~lnull].merge(rkf[~rnull], on=cols, how="inner")
