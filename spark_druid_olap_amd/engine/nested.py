@@ -15,6 +15,7 @@ query's (executor._post).
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Callable, Dict, List, Optional, Tuple
 
@@ -24,6 +25,9 @@ import torch
 from ..query import spec as S
 from ..segment.datasource import DataSource
 from .lower import LoweringError
+
+
+_TRACE = bool(os.environ.get("SDO_TRACE_NESTED"))
 
 
 class DeviceColumn:
@@ -60,7 +64,12 @@ class DeviceColumn:
 def device_columns(pq) -> Tuple[Dict[str, DeviceColumn], int]:
     """Run a (non-nested) groupBy PreparedQuery up to its merged partials and expose every output
     column as a device tensor.  Returns (columns, row count)."""
-    prog, part, _ = pq.run_partials(time.perf_counter())
+    t0 = time.perf_counter()
+    prog, part, _ = pq.run_partials(t0)
+    if _TRACE:
+        torch.cuda.synchronize()
+        print(f"[nested] inner scan+merge {(time.perf_counter() - t0) * 1e3:.2f} ms mode="
+              f"{getattr(pq.scans[0][2], 'mode', None)} G={prog.G} rows={part.rows}", flush=True)
     if prog.thetas or any(kc.collapse for kc in prog.keys):
         raise LoweringError("nested query over theta sketches / non-injective keys")
     if part.kind == "dense":
@@ -161,6 +170,8 @@ class NestedPreparedQuery:
             cols, n = inner.device_result()
         else:
             cols, n = device_columns(inner)
+        if _TRACE:
+            torch.cuda.synchronize()
         inner_ms = (time.perf_counter() - t0) * 1e3
         qs = self.qs
         dev = next(iter(cols.values())).t.device if cols else self.ds.device
@@ -212,6 +223,10 @@ class NestedPreparedQuery:
             inv = torch.zeros(n, dtype=torch.int64, device=dev)
             R = 1
             firsts = torch.zeros(1, dtype=torch.int64, device=dev)
+        if _TRACE:
+            torch.cuda.synchronize()
+            print(f"[nested] inner {inner_ms:.2f} ms rows={n}; grouping {(time.perf_counter() - t0) * 1e3 - inner_ms:.2f}"
+                  f" ms -> {R} groups", flush=True)
         out: Dict[str, DeviceColumn] = {}
         for j, (d, c) in enumerate(keycols):
             if n == 0:
@@ -257,6 +272,9 @@ class NestedPreparedQuery:
             if a.type.startswith("long") and not exact:
                 acc = acc.to(torch.int64)
             out[a.name] = DeviceColumn(a.name, acc, scale=c.scale if exact else 0)
+        if _TRACE:
+            torch.cuda.synchronize()
+            print(f"[nested] done {(time.perf_counter() - t0) * 1e3:.2f} ms", flush=True)
         return out, R, inner_ms
 
     def device_result(self) -> Tuple[Dict[str, DeviceColumn], int]:
