@@ -293,6 +293,7 @@ class ScanProgram:
     # device int32 table determinant dictionary id -> dependent dictionary id)
     derived: List[Tuple["KeyComp", int, torch.Tensor]] = field(default_factory=list)
     key_order: List[str] = field(default_factory=list)  # output order of all grouping keys
+    presence_only: bool = False  # no aggregator reads slot 0's count: group existence only
 
     def col(self, name: str) -> int:
         """Absolute descriptor column index of `name` in the current section."""
@@ -1216,6 +1217,7 @@ class Lowerer:
             raise LoweringError("too many grouping keys")
         for a in aggregations:
             self.add_aggregator(prog, a)
+        prog.presence_only = not aggregations and not extra_keys
         self.fold_presence_slot(prog)
         prog.key_order = [kc.name for kc in prog.keys]
         self.eliminate_dependent_keys(prog)

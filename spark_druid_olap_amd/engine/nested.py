@@ -142,7 +142,19 @@ class NestedPreparedQuery:
         self.qs = qs
         self.ds = ds
         self.world = engine.world
-        self.inner = engine.prepare(qs.dataSource.query, ds, segments_per_query)
+        inner_q = qs.dataSource.query
+        if isinstance(inner_q, S.GroupByQuerySpec) and not isinstance(inner_q.dataSource, S.QueryDataSourceSpec):
+            # inner aggregates the outer level never reads are not computed; with none left the
+            # inner scan only records which groups exist (Q13: 600M lines -> order existence)
+            used = {d.dimension for d in qs.dimensions}
+            for a in qs.aggregations:
+                used.add(getattr(a, "fieldName", None))
+                used.update(getattr(a, "fieldNames", None) or [])
+            keep = [a for a in (inner_q.aggregations or []) if a.name in used]
+            if len(keep) != len(inner_q.aggregations or []) and not inner_q.postAggregations and \
+                    inner_q.having is None and inner_q.limitSpec is None:
+                inner_q = inner_q.copy(aggregations=keep)
+        self.inner = engine.prepare(inner_q, ds, segments_per_query)
         for d in qs.dimensions:
             if not isinstance(d, S.DefaultDimensionSpec):
                 raise LoweringError("nested groupBy dimensions must be default dimension specs")

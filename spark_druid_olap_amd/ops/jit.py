@@ -505,6 +505,11 @@ class _Gen:
                 tgt = f"acc + (slot * {NS} + {s}) * {NCT} + copy"
             else:
                 tgt = f"gacc + slot * {NS} + {s}"
+            if getattr(p, "presence_only", False) and mode == D.M_DENSE_GLOBAL and kind == D.A_COUNT and NS == 1:
+                # existence only (nested inner level, SELECT DISTINCT): a plain vector store of 1
+                # instead of an HBM read-modify-write atomic per row (same-value races are benign)
+                body.append(f"        if ({cond}) *({tgt}) = 1ull;")
+                continue
             body.append(f"        if ({cond}) acc_update<{op}>({tgt}, {val});")
         body.append("      }")
         # ---------------- kernel text

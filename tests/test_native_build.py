@@ -54,3 +54,18 @@ def test_jit_shared_table_kernel_compiles(tmp_path, monkeypatch):
                          budget=159 * 1024)
         assert js.lay.shared and js.lay.acc_bytes == prog.G * prog.nslots * 8
         assert "const int copy = 0;" in js.src and js.lay.total <= 160 * 1024
+
+
+def test_jit_presence_only_kernel_compiles(tmp_path, monkeypatch, ds_small):
+    """Existence-only dense HBM scans (nested inner level) store 1 instead of an atomic add."""
+    from spark_druid_olap_amd.engine.lower import Lowerer
+    from spark_druid_olap_amd.ops import desc as D
+    from spark_druid_olap_amd.ops import jit
+    from spark_druid_olap_amd.query import spec as S
+
+    monkeypatch.setenv("SDO_JIT_CACHE", str(tmp_path))
+    prog = Lowerer(ds_small).lower_aggregate(["1992-01-01/1999-01-01"], None,
+                                             [S.DefaultDimensionSpec("o_orderkey")], None, [])
+    assert prog.presence_only and prog.nslots == 1
+    js = jit.JitScan(prog, D.M_DENSE_GLOBAL, 4, False, 2048, True, load=False)
+    assert "= 1ull;" in js.src and "acc_update" not in js.src.split("void sdo_jit")[-1]
