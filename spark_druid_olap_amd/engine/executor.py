@@ -220,7 +220,8 @@ class PreparedQuery:
 
         def value(name):
             a = aggs.get(name)
-            if a is None or a.kind not in ("count", "sum_i", "sum_f", "min_i", "max_i", "min_f", "max_f"):
+            if a is None or a.slot < 0 or a.kind not in ("count", "sum_i", "sum_f", "min_i", "max_i", "min_f",
+                                                         "max_f"):
                 return None
             col = part.acc[:, a.slot]
             if a.kind == "sum_f":
@@ -281,7 +282,7 @@ class PreparedQuery:
         if limit <= 0 or part.rows <= max(4 * limit, 4096) or prog.thetas or any(kc.collapse for kc in prog.keys):
             return part
         agg = next((a for a in prog.aggs if a.name == name), None)
-        if agg is None or agg.kind not in ("count", "sum_i", "sum_f", "min_i", "max_i"):
+        if agg is None or agg.slot < 0 or agg.kind not in ("count", "sum_i", "sum_f", "min_i", "max_i"):
             return part
         if part.kind == "dense":
             part = part.compact()

@@ -294,6 +294,9 @@ class ScanProgram:
     derived: List[Tuple["KeyComp", int, torch.Tensor]] = field(default_factory=list)
     key_order: List[str] = field(default_factory=list)  # output order of all grouping keys
     presence_only: bool = False  # no aggregator reads slot 0's count: group existence only
+    # min/max of a metric constant per group key: (AggOut, determinant key index, device int64 table
+    # determinant dictionary id -> stored metric value); no accumulator, gathered at finalize
+    derived_aggs: List[Tuple["AggOut", int, torch.Tensor]] = field(default_factory=list)
 
     def col(self, name: str) -> int:
         """Absolute descriptor column index of `name` in the current section."""
@@ -1193,6 +1196,48 @@ class Lowerer:
             prog.derived.append((kc, pos[i], lut))
         prog.keys = [prog.keys[i] for i in keep]
 
+    def eliminate_dependent_aggs(self, prog: ScanProgram) -> None:
+        """MIN/MAX of a metric that is constant per value of a grouping key (TPC-H Q18
+        ``max(o_totalprice)`` per order, Q10 ``max(c_acctbal)`` per customer) needs no per-row
+        accumulator: the value is gathered per result group from an FD table (verified on the
+        index, all ranks).  Q18 over 150M order groups: one HBM atomic less per line."""
+        if os.environ.get("SDO_NO_FD") or any(kc.collapse for kc in prog.keys):
+            return
+        dets = [i for i, kc in enumerate(prog.keys) if kc.kind == D.K_ID and kc.card > 1]
+        if not dets:
+            return
+        for a in list(prog.aggs):
+            s = a.slot
+            if a.kind not in ("min_i", "max_i") or s <= 0:
+                continue
+            users = [d for d in prog.aops if d["slot"] == s]
+            if len(users) != 1 or any(x is not a and x.slot == s for x in prog.aggs):
+                continue
+            d = users[0]
+            if d["filter"] is not None or d["expr"] is not None or d["col"] < 0:
+                continue
+            name = prog.colname(d["col"])
+            if name not in self.ds.metrics or name in self.ds.dims:
+                continue
+            hit = None
+            for i in dets:
+                lut = fd_metric_table(self.ds, prog.keys[i].col, name, self.world)
+                if lut is not None:
+                    hit = (i, lut)
+                    break
+            if hit is None:
+                continue
+            prog.aops.remove(d)
+            prog.slots.pop(s)
+            for x in prog.aops:
+                if x["slot"] > s:
+                    x["slot"] -= 1
+            for x in prog.aggs:
+                if x.slot > s:
+                    x.slot -= 1
+            a.slot = -1
+            prog.derived_aggs.append((a, hit[0], hit[1]))
+
     # ------------------------------------------------------------------ whole query
     def lower_aggregate(self, intervals, filter_spec, dimensions, granularity, aggregations,
                         extra_keys: Sequence[KeyComp] = ()) -> ScanProgram:
@@ -1221,6 +1266,7 @@ class Lowerer:
         self.fold_presence_slot(prog)
         prog.key_order = [kc.name for kc in prog.keys]
         self.eliminate_dependent_keys(prog)
+        self.eliminate_dependent_aggs(prog)
         # filter-implied key domains: a dimension the filter pins to a few values only needs
         # that many key slots (Q7: s_nation x c_nation shrinks 25x25 -> 2x2), which keeps the
         # accumulators in LDS instead of contended HBM atomics
@@ -1336,6 +1382,41 @@ def _ast_cols(a) -> List[str]:
 
 
 _FD_CHUNK = 1 << 26
+
+
+_FD_MISSING = -(2 ** 63)
+
+
+def _fd_lut(ids_a: torch.Tensor, card_a: int, vals_b: torch.Tensor, n: int, world=None) -> Optional[torch.Tensor]:
+    """int64 table a-id -> b-value when every row's b is a function of its a (all ranks), with
+    _FD_MISSING for a-ids no rank holds; None when the dependency does not hold."""
+    dev = ids_a.device
+    lut = torch.full((card_a,), _FD_MISSING, dtype=torch.int64, device=dev)
+    for s0 in range(0, n, _FD_CHUNK):
+        lut.scatter_(0, ids_a[s0:min(n, s0 + _FD_CHUNK)].to(torch.int64), vals_b[s0:min(n, s0 + _FD_CHUNK)].to(torch.int64))
+    ok = torch.ones((), dtype=torch.int64, device=dev)
+    for s0 in range(0, n, _FD_CHUNK):
+        ia = ids_a[s0:min(n, s0 + _FD_CHUNK)].to(torch.int64)
+        ok &= (lut[ia] == vals_b[s0:min(n, s0 + _FD_CHUNK)].to(torch.int64)).all().to(torch.int64)
+    if world is not None and world.distributed:
+        hi = world.all_reduce(lut.clone(), "max")
+        big = torch.iinfo(torch.int64).max
+        lo = world.all_reduce(torch.where(lut == _FD_MISSING, torch.full_like(lut, big), lut), "min")
+        ok &= ((lo == big) | (lo == hi)).all().to(torch.int64)
+        ok = world.all_reduce(ok, "min")
+        lut = hi
+    return lut if bool(ok.item()) else None
+
+
+def fd_metric_table(ds: DataSource, a: str, metric: str, world=None) -> Optional[torch.Tensor]:
+    """Device table a-id -> stored metric value when the metric is constant per value of
+    dimension ``a`` (o_totalprice per order, c_acctbal per customer); cached per datasource."""
+    cache = ds.__dict__.setdefault("_fd_cache", {})
+    key = (a, "metric:" + metric)
+    if key not in cache:
+        cache[key] = _fd_lut(ds.dims[a].ids, len(ds.dims[a].dictionary), column_tensor(ds, metric), ds.num_rows,
+                             world)
+    return cache[key]
 
 
 def fd_table(ds: DataSource, a: str, b: str, world=None) -> Optional[torch.Tensor]:

@@ -91,7 +91,15 @@ def device_columns(pq) -> Tuple[Dict[str, DeviceColumn], int]:
         ids = lut.to(dev)[did].to(torch.int64)
         cols[kc.name] = DeviceColumn(kc.name, ids, kc.decoder if kc.decoder is not None else (lambda x: x),
                                      card=max(1, kc.card))
+    for a, det, lut in getattr(prog, "derived_aggs", ()):
+        did = ids_of[det]
+        orig = prog.keys[det].orig
+        if orig is not None:
+            did = torch.from_numpy(orig).to(dev)[did]
+        cols[a.name] = DeviceColumn(a.name, lut.to(dev)[did], scale=a.scale)
     for a in prog.aggs:
+        if a.name in cols:
+            continue
         col = part.acc[:, a.slot] if a.slot >= 0 else None
         if a.kind in ("count", "min_i", "max_i"):
             cols[a.name] = DeviceColumn(a.name, col, scale=a.scale)

@@ -110,6 +110,13 @@ def finalize(prog, parts: Partials) -> Dict[str, np.ndarray]:
             hll_d = [h.index_select(0, torch.from_numpy(gid).to(h.device)) for h in parts.hll]
             key_ids = [(gid // kc.stride) % max(1, kc.card) for kc in prog.keys]
             derived_ids = None
+            derived_agg_vals = []
+            for a, det, lut in getattr(prog, "derived_aggs", ()):
+                did = np.asarray(key_ids[det], dtype=np.int64)
+                orig = prog.keys[det].orig
+                if orig is not None:
+                    did = orig[did]
+                derived_agg_vals.append(lut[torch.from_numpy(did).to(lut.device)].cpu().numpy())
         else:
             parts = parts.compact()
     if parts.kind == "sparse":
@@ -120,6 +127,14 @@ def finalize(prog, parts: Partials) -> Dict[str, np.ndarray]:
             ids = torch.remainder(torch.div(g, kc.stride, rounding_mode="floor"), max(1, kc.card))
             dev_ids.append(ids.to(torch.int32) if kc.card < 2 ** 31 else ids)
         nk = len(dev_ids)
+        dag = []
+        for a, det, lut in getattr(prog, "derived_aggs", ()):
+            # min/max of a metric constant per key: gathered from its FD table, no accumulator
+            did = dev_ids[det].to(torch.int64)
+            orig = prog.keys[det].orig
+            if orig is not None:
+                did = torch.from_numpy(orig).to(did.device)[did]
+            dag.append(lut.to(did.device)[did])
         for kc, det, lut in getattr(prog, "derived", ()):
             # functionally dependent keys: gather their ids on the device
             did = dev_ids[det].to(torch.int64)
@@ -128,10 +143,11 @@ def finalize(prog, parts: Partials) -> Dict[str, np.ndarray]:
                 did = torch.from_numpy(orig).to(did.device)[did]
             dev_ids.append(lut.to(did.device)[did])
         # slot-major accumulators so every output column is a contiguous view (no host copies)
-        host = d2h(dev_ids + [parts.acc.t().contiguous()] + ([g] if want_gid else []))
+        host = d2h(dev_ids + dag + [parts.acc.t().contiguous()] + ([g] if want_gid else []))
         key_ids = host[:nk]
         derived_ids = host[nk:len(dev_ids)]
-        acc_h = host[len(dev_ids)].T
+        derived_agg_vals = host[len(dev_ids):len(dev_ids) + len(dag)]
+        acc_h = host[len(dev_ids) + len(dag)].T
         gid = host[-1] if want_gid else None
         hll_d = parts.hll
     cols: Dict[str, np.ndarray] = {}
@@ -191,8 +207,15 @@ def finalize(prog, parts: Partials) -> Dict[str, np.ndarray]:
         for j, name in enumerate(key_names):
             cols[name] = np.array([t[j] for t in keys_first], dtype=object)
         acc_h, hll_d = new_acc, new_hll
+    derived_names = {}
+    for (a, _, _), v in zip(getattr(prog, "derived_aggs", ()), derived_agg_vals):
+        v = np.asarray(v, dtype=np.int64)
+        derived_names[a.name] = v.astype(np.float64) / (10.0 ** a.scale) if a.scale else \
+            (v if a.out_type == "long" else v.astype(np.float64))
     for a in prog.aggs:
-        if a.kind in ("count",):
+        if a.name in derived_names:
+            cols[a.name] = derived_names[a.name]
+        elif a.kind in ("count",):
             cols[a.name] = acc_h[:, a.slot]
         elif a.kind in ("sum_i", "min_i", "max_i"):
             v = acc_h[:, a.slot]

@@ -161,3 +161,23 @@ def test_presence_slot_folds_into_positive_sum(ds_small, df_small):
     got = dict(zip(r.data["l_shipmode"].tolist() if hasattr(r.data["l_shipmode"], "tolist") else
                    list(r.data["l_shipmode"]), r.data["q"].tolist()))
     assert {str(k): int(v) for k, v in got.items()} == {k: int(v) for k, v in exp.items()}
+
+
+def test_dependent_metric_aggregate_needs_no_accumulator(ds_small, df_small):
+    """max(o_totalprice) per order is read from an FD table (the metric is constant per order);
+    sum(l_quantity) doubles as the presence slot: one accumulator for Q18's inner scan."""
+    from spark_druid_olap_amd.engine.lower import Lowerer
+    from spark_druid_olap_amd.query import spec as S
+
+    dims = [S.DefaultDimensionSpec("o_orderkey")]
+    aggs = [S.FunctionAggregationSpec("doubleMax", "tp", "o_totalprice"),
+            S.FunctionAggregationSpec("longSum", "q", "l_quantity")]
+    iv = ["1992-01-01/1999-01-01"]
+    prog = Lowerer(ds_small).lower_aggregate(iv, None, dims, None, aggs)
+    assert prog.nslots == 1 and [a.name for a, _, _ in prog.derived_aggs] == ["tp"]
+    r = Engine(use_native=False).execute(S.GroupByQuerySpec("tpch", dims, aggregations=aggs, intervals=iv), ds_small)
+    got = dict(zip(np.asarray(r.data["o_orderkey"]).tolist(), np.asarray(r.data["tp"]).tolist()))
+    exp = df_small.groupby("o_orderkey")["o_totalprice"].max()
+    assert len(got) == len(exp)
+    for k, v in exp.items():
+        assert got[int(k)] == pytest.approx(v, abs=0.005)
