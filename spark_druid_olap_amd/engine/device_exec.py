@@ -140,11 +140,20 @@ class PreparedScan:
         else:
             self.cap = 0
         self.jit = None
+        # existence-only dense HBM scan on one GPU: one byte per group (150M order groups -> 150 MB,
+        # which stays in the 256 MB Infinity Cache) instead of an 8-byte counter row
+        self.pres_bytes = bool(USE_JIT and dense_max is not None and mode == D.M_DENSE_GLOBAL and
+                               getattr(prog, "presence_only", False) and prog.nslots == 1 and not prog.nhll
+                               and not prog.empty and not os.environ.get("SDO_NO_PRES_BYTES"))
+        prog.presence_bytes = self.pres_bytes
         if not prog.empty:
             # the JIT keeps LDS registers one byte each (hll_update8)
             jit_hll_lds = bool(prog.nhll) and mode == D.M_DENSE_LDS and hll_bytes // 4 <= LDS_BUDGET \
                 and not self.shared
             self.jit = _jit_for(prog, mode, jit_hll_lds, self.m, self.shared)
+            if self.pres_bytes and self.jit is None:
+                self.pres_bytes = prog.presence_bytes = False
+                self.jit = _jit_for(prog, mode, jit_hll_lds, self.m, self.shared)
             if self.shared and self.jit is None:
                 # the interpreter kernel only knows per-wave copies: accumulate in HBM instead
                 self.mode, self.shared, self.lds = D.M_DENSE_GLOBAL, False, 0
@@ -159,7 +168,10 @@ class PreparedScan:
         rows = self.cap if self.mode == D.M_HASH else prog.G
         self.rows = rows
         self.init_row = torch.tensor([init for _, init in prog.slots], dtype=torch.int64, device=dev)
-        self.acc = torch.empty((rows, prog.nslots), dtype=torch.int64, device=dev)
+        if self.pres_bytes:
+            self.acc = torch.empty((rows,), dtype=torch.uint8, device=dev)
+        else:
+            self.acc = torch.empty((rows, prog.nslots), dtype=torch.int64, device=dev)
         self.keys = torch.empty(rows if self.mode == D.M_HASH else 1, dtype=torch.int64, device=dev)
         self.hll = [torch.empty(rows * self.m, dtype=torch.int32, device=dev) for _ in range(prog.nhll)]
         self.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -192,7 +204,10 @@ class PreparedScan:
             native.scan(self.desc, self.grid, BLOCK, self.lds_total, UNROLL)
 
     def _reset(self):
-        self.acc.copy_(self.init_row.expand_as(self.acc))
+        if self.pres_bytes:
+            self.acc.zero_()
+        else:
+            self.acc.copy_(self.init_row.expand_as(self.acc))
         if self.mode == D.M_HASH:
             self.keys.fill_(-1)
         for h in self.hll:
@@ -212,6 +227,9 @@ class PreparedScan:
         while True:
             self._reset()
             self._launch()
+            if self.pres_bytes:
+                idx = _nonzero_big(self.acc)
+                return Partials("sparse", torch.ones((idx.numel(), 1), dtype=torch.int64, device=self.dev), idx, [])
             if self.mode != D.M_HASH:
                 break
             if int(self.overflow.item()) == 0:

@@ -294,6 +294,7 @@ class ScanProgram:
     derived: List[Tuple["KeyComp", int, torch.Tensor]] = field(default_factory=list)
     key_order: List[str] = field(default_factory=list)  # output order of all grouping keys
     presence_only: bool = False  # no aggregator reads slot 0's count: group existence only
+    presence_bytes: bool = False  # (set by the device executor) existence table is one byte per group
     # min/max of a metric constant per group key: (AggOut, determinant key index, device int64 table
     # determinant dictionary id -> stored metric value); no accumulator, gathered at finalize
     derived_aggs: List[Tuple["AggOut", int, torch.Tensor]] = field(default_factory=list)

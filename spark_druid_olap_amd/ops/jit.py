@@ -507,8 +507,12 @@ class _Gen:
                 tgt = f"gacc + slot * {NS} + {s}"
             if getattr(p, "presence_only", False) and mode == D.M_DENSE_GLOBAL and kind == D.A_COUNT and NS == 1:
                 # existence only (nested inner level, SELECT DISTINCT): a plain vector store of 1
-                # instead of an HBM read-modify-write atomic per row (same-value races are benign)
-                body.append(f"        if ({cond}) *({tgt}) = 1ull;")
+                # instead of an HBM read-modify-write atomic per row (same-value races are benign);
+                # with presence_bytes the table is one byte per group
+                if getattr(p, "presence_bytes", False):
+                    body.append(f"        if ({cond}) ((unsigned char*)gacc)[slot] = (unsigned char)1;")
+                else:
+                    body.append(f"        if ({cond}) *({tgt}) = 1ull;")
                 continue
             body.append(f"        if ({cond}) acc_update<{op}>({tgt}, {val});")
         body.append("      }")

@@ -44,3 +44,24 @@ def test_tpch22_native_vs_reference(sessions, name):
                 assert u == pytest.approx(v, rel=1e-9, abs=0.011), (name, x, y)
             else:
                 assert u == v, (name, x, y)
+
+
+def test_presence_byte_table_matches_reference():
+    """Existence-only dense HBM scan with a one-byte-per-group table (nested inner levels)."""
+    import torch
+
+    from spark_druid_olap_amd.engine.device_exec import PreparedScan
+    from spark_druid_olap_amd.engine.lower import Lowerer
+    from spark_druid_olap_amd.ops import desc as D
+    from spark_druid_olap_amd.ops.reference import run_reference
+    from spark_druid_olap_amd.query import spec as S
+
+    ds = tpch.to_datasource(tpch.generate_flat(0.05, "cuda"), profile="bench")
+    f = S.SelectorFilterSpec("l_shipmode", "MAIL")
+    prog = Lowerer(ds).lower_aggregate(["1992-01-01/1999-01-01"], f, [S.DefaultDimensionSpec("o_orderkey")], None, [])
+    prep = PreparedScan(prog, mode=D.M_DENSE_GLOBAL, dense_max=1 << 34)
+    assert prep.pres_bytes and prep.acc.dtype == torch.uint8
+    got = prep.run()
+    ref = run_reference(prog)
+    ref_keys = ref.compact().keys
+    assert torch.equal(torch.sort(got.keys).values, torch.sort(ref_keys.to(got.keys.device)).values)

@@ -69,3 +69,7 @@ def test_jit_presence_only_kernel_compiles(tmp_path, monkeypatch, ds_small):
     assert prog.presence_only and prog.nslots == 1
     js = jit.JitScan(prog, D.M_DENSE_GLOBAL, 4, False, 2048, True, load=False)
     assert "= 1ull;" in js.src and "acc_update" not in js.src.split("void sdo_jit")[-1]
+    prog.presence_bytes = True
+    js = jit.JitScan(prog, D.M_DENSE_GLOBAL, 4, False, 2048, True, load=False)
+    assert "(unsigned char*)gacc)[slot]" in js.src
+
