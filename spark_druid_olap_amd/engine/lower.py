@@ -428,6 +428,19 @@ class Lowerer:
             lv = val.lower()
             return ("ids", dim, d.eval_mask(lambda v: v is not None and lv in str(v).lower()))
         if isinstance(f, S.ExtractionFilterSpec):
+            ef = f.extractionFn
+            if isinstance(ef, S.InExtractionFnSpec) and _druid_str(f.value) == "true" and \
+                    not ef.retainMissingValue and ef.replaceMissingValueWith in (None, "") and \
+                    (ef.lookup or {}).get("type", "map") == "map" and getattr(d, "lazy", False):
+                # IN list over a large lazy dictionary (o_orderkey IN (subquery)): one lookup per
+                # listed value instead of evaluating every dictionary entry
+                mask = np.zeros(len(d), dtype=bool)
+                for v, out in (ef.lookup.get("map") or {}).items():
+                    if _druid_str(out) == "true":
+                        i = d.lookup(v)
+                        if i >= 0:
+                            mask[i] = True
+                return ("ids", dim, mask)
             fn = extraction_callable(f.extractionFn)
             target = f.value
 

@@ -342,13 +342,23 @@ class DruidRewriter:
         concrete filter is built from the subquery values at execution time.  A trial build with
         placeholder values decides pushability now (the value never changes the filter's shape,
         only its constants)."""
-        if any(x.kind != "scalar" for x in sqs):
-            raise NotPushable("IN / EXISTS subquery in predicate")
+        if any(x.kind not in ("scalar", "in") for x in sqs):
+            raise NotPushable("EXISTS subquery in predicate")
 
         def build(values, _e=e, _pf=pf):
             def sub(x):
                 if isinstance(x, A.SubqueryExpr):
-                    return A.Lit(values[id(x)], typeof(x))
+                    v = values[id(x.query)]
+                    if x.kind == "scalar":
+                        return A.Lit(v, typeof(x))
+                    # IN (subquery) -> IN list of the subquery's distinct values (semi-join pushdown)
+                    vals, has_null = v
+                    if not vals:
+                        return A.Lit(bool(x.negated) and not has_null, "boolean")
+                    if x.negated and has_null:
+                        return A.Lit(False, "boolean")  # NOT IN over a NULL-containing set: never true
+                    t = typeof(x.child)
+                    return A.InList(x.child, tuple(A.Lit(u, t) for u in vals), x.negated)
                 return None
 
             f = self._filter(_pf, constant_fold(_e.transform(sub)))
@@ -357,8 +367,9 @@ class DruidRewriter:
 
         probe = {}
         for x in sqs:
-            t = base(typeof(x))
-            probe[id(x)] = "x" if t == "string" else (0.5 if t in ("double", "float", "decimal") else 1)
+            t = base(typeof(x) if x.kind == "scalar" else typeof(x.child))
+            pv = "x" if t == "string" else (0.5 if t in ("double", "float", "decimal") else 1)
+            probe[id(x.query)] = pv if x.kind == "scalar" else ([pv], False)
         build(probe)  # raises NotPushable when the predicate shape is not pushable
         d = S.DeferredFilterSpec(e.sql())
         d.subqueries = sqs
@@ -1105,11 +1116,11 @@ class DruidRewriter:
             def build(values, _c=f.cond):
                 def sub(x):
                     if isinstance(x, A.SubqueryExpr):
-                        return A.Lit(values[id(x)], typeof(x))
+                        return A.Lit(values[id(x.query)], typeof(x))
                     return None
                 return conv(constant_fold(_c.transform(sub)))
 
-            build({id(x): 1.5 for x in sqs})  # shape check with placeholder values
+            build({id(x.query): 1.5 for x in sqs})  # shape check with placeholder values
             d = S.DeferredFilterSpec(f.cond.sql())
             d.subqueries, d.build = sqs, build
             dq.spec = q.copy(having=d)

@@ -95,6 +95,22 @@ class Executor:
             res = res.mask(~res.fillna(False).to_numpy(dtype=bool), pd.NA)
         return ~res if e.negated else res
 
+    def _subquery_param(self, e: A.SubqueryExpr):
+        """Value a deferred filter needs from a subquery: the scalar, or for IN (subquery) the
+        distinct non-NULL values plus whether a NULL was among them."""
+        if e.kind == "scalar":
+            return self._subquery(e, None)
+        key = id(e.query)
+        if key not in self._subq_cache:
+            self._subq_cache[key] = self.run(e.query)
+        b = self._subq_cache[key]
+        col = b.cols[b.refs[0].rid]
+        has_null = bool(col.isna().any())
+        vals = []
+        for v in pd.unique(col.dropna()):
+            vals.append(v.item() if isinstance(v, np.generic) else v)
+        return vals, has_null
+
     # ----------------------------------------------------------------------------------------
     def _TableScan(self, p: P.TableScan) -> Batch:
         t = p.table
@@ -207,7 +223,7 @@ class Executor:
         if deferred:
             # scalar subqueries first (pushed queries themselves), then the filter they parameterise;
             # the resolved query (and its lowered program) is cached per subquery-value tuple
-            vals = {id(sq): self._subquery(sq, None) for d in deferred for sq in d.subqueries}
+            vals = {id(sq.query): self._subquery_param(sq) for d in deferred for sq in d.subqueries}
             key = tuple(repr(vals[k]) for k in sorted(vals))
             cache = p.__dict__.setdefault("_resolved", {})
             q = cache.get(key)

@@ -311,8 +311,16 @@ def subquery_exprs(plan: Plan) -> List[A.SubqueryExpr]:
 
 def find_all_deep(plan: Plan, cls) -> List[Any]:
     """find_all, also inside the plans of subquery expressions."""
+    from ..query.spec import find_deferred
+
     out = find_all(plan, cls)
-    for sq in subquery_exprs(plan):
-        if isinstance(sq.query, Plan):
+    sqs = list(subquery_exprs(plan))
+    for dq in find_all(plan, DruidQuery):  # subqueries parameterising pushed filters / having
+        for d in find_deferred(dq.spec):
+            sqs.extend(d.subqueries)
+    seen = set()
+    for sq in sqs:
+        if isinstance(sq.query, Plan) and id(sq.query) not in seen:
+            seen.add(id(sq.query))
             out.extend(find_all_deep(sq.query, cls))
     return out
