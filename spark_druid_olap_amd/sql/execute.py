@@ -462,6 +462,9 @@ def sort_indices(keys, n: int) -> np.ndarray:
         elif str(s.dtype) in ("Int64", "Float64", "boolean") or s.dtype.kind in "iufb":
             arr = s.astype("Float64").to_numpy(dtype="float64", na_value=0.0) if str(s.dtype) != "Int64" else \
                 s.to_numpy(dtype="int64", na_value=0)
+        elif isinstance(s.dtype, pd.CategoricalDtype) and s.cat.categories.is_monotonic_increasing:
+            # dictionary-coded strings: categories are the sorted dictionary, so codes order like values
+            arr = s.cat.codes.to_numpy().astype(np.int64)
         else:
             codes, uniq = pd.factorize(vals, sort=True)
             arr = codes
