@@ -4,9 +4,10 @@ final aggregate, ``asd/PostAggregate.scala:39-103``, re-designed for RCCL over x
 * Small dense states (the common OLAP case: Q1 is 6 groups) are latency-bound: ONE
   ``all_gather_into_tensor`` of the packed state (accumulators + HLL registers as int64 words)
   followed by a local per-slot reduction -- one collective instead of one per reduce-op.
-* Large dense states use bandwidth-optimal ``all_reduce`` per reduce-op (sum / min / max;
-  HLL registers with MAX -- mergeable sketches, which the reference could not merge across
-  historicals, ``asd/PostAggregate.scala:62-70``).
+* Large dense states use bandwidth-optimal ring ``all_reduce`` over at most three buckets (int
+  sums + status word, float sums, max + bitwise-NOT(min)) with one host sync at the end; HLL
+  registers reduce with MAX -- mergeable sketches, which the reference could not merge across
+  historicals, ``asd/PostAggregate.scala:62-70``.
 * Sparse (hash) states are compacted per GPU, gathered (variable length), and merged by key.
   When the datasource is partitioned on a grouping key the groups are disjoint across ranks and
   the merge degenerates to a concatenation.
@@ -41,6 +42,49 @@ def _reduce_stacked(prog, acc_all: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def _merge_dense_bucketed(world: World, prog, part: Partials, status: int,
+                          local_error: Optional[BaseException]) -> Partials:
+    """Large dense state: at most three ring all-reduces (each per-xGMI-link bandwidth bound) plus
+    one per HLL register block, with ONE host synchronisation after all of them were enqueued.
+
+    * int sums + the status word (sum of the ranks' statuses is non-zero iff one failed);
+    * float64 sums;
+    * int max slots and the bitwise NOT of int min slots (``min x == ~max ~x``, no overflow at
+      INT64_MIN unlike negation), so min and max share one MAX collective.
+    A failed rank contributes a layout-compatible placeholder, so every rank issues the same
+    collectives in the same order and then raises together (parallel/fault.py)."""
+    acc = part.acc.clone()
+    R = acc.shape[0]
+    by_op = {op: [s for s, (o, _) in enumerate(prog.slots) if o == op]
+             for op in (D.S_SUM_I, D.S_SUM_F, D.S_MIN_I, D.S_MAX_I)}
+    si, sf, mn, mx = by_op[D.S_SUM_I], by_op[D.S_SUM_F], by_op[D.S_MIN_I], by_op[D.S_MAX_I]
+    st = torch.full((1,), status, dtype=torch.int64, device=acc.device)
+    b_sum = torch.cat([acc[:, si].reshape(-1), st]) if si else st
+    world.all_reduce(b_sum, "sum")
+    if sf:
+        b_f = acc[:, sf].contiguous().view(torch.float64)
+        world.all_reduce(b_f, "sum")
+        acc[:, sf] = b_f.view(torch.int64)
+    if mn or mx:
+        b_max = torch.cat([acc[:, mx].reshape(-1), torch.bitwise_not(acc[:, mn]).reshape(-1)])
+        world.all_reduce(b_max, "max")
+        if mx:
+            acc[:, mx] = b_max[: R * len(mx)].reshape(R, len(mx))
+        if mn:
+            acc[:, mn] = torch.bitwise_not(b_max[R * len(mx):].reshape(R, len(mn)))
+    hll = []
+    for h in part.hll:
+        hh = h.clone()
+        world.all_reduce(hh, "max")
+        hll.append(hh)
+    failed = int(b_sum[-1].item())
+    if local_error is not None or failed:
+        raise_if_failed([failed], world.rank, local_error)
+    if si:
+        acc[:, si] = b_sum[:-1].reshape(R, len(si))
+    return Partials("dense", acc, None, hll)
+
+
 def merge_partials(world: World, prog, part: Partials, disjoint_keys: bool = False,
                    local_error: Optional[BaseException] = None) -> Partials:
     """Merge this rank's partials with every other rank's.  ``local_error`` set = this rank failed
@@ -70,29 +114,7 @@ def merge_partials(world: World, prog, part: Partials, disjoint_keys: bool = Fal
             off += n
         return Partials("dense", acc, None, hll)
     if part.kind == "dense":
-        st = torch.full((1,), status, dtype=torch.int64, device=part.acc.device)
-        world.all_reduce(st, "max")
-        if local_error is not None or int(st.item()):
-            raise_if_failed([int(st.item())], world.rank, local_error)
-        acc = part.acc.clone()
-        for op in (D.S_SUM_I, D.S_SUM_F, D.S_MIN_I, D.S_MAX_I):
-            cols = [s for s, (o, _) in enumerate(prog.slots) if o == op]
-            if not cols:
-                continue
-            sub = acc[:, cols].contiguous()
-            if op == D.S_SUM_F:
-                f = sub.view(torch.float64)
-                world.all_reduce(f, "sum")
-                sub = f.view(torch.int64)
-            else:
-                world.all_reduce(sub, {D.S_SUM_I: "sum", D.S_MIN_I: "min", D.S_MAX_I: "max"}[op])
-            acc[:, cols] = sub
-        hll = []
-        for h in part.hll:
-            hh = h.clone()
-            world.all_reduce(hh, "max")
-            hll.append(hh)
-        return Partials("dense", acc, None, hll)
+        return _merge_dense_bucketed(world, prog, part, status, local_error)
     # sparse
     sp = part.compact()
     # keys + accumulators travel as one [n, 1 + nslots] int64 block: one length exchange (which also
