@@ -26,6 +26,47 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int) -> int:
+    """``--gpus N`` without torchrun: start N rank processes (one per GPU) and wait for them.
+
+    This parent never imports torch nor touches a GPU -- it only starts children with the torchrun
+    environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*) and returns the worst exit code; rank 0's
+    stdout (the JSON line) passes straight through.  A failed rank takes the others down."""
+    import subprocess
+
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0:
+                rc = rc or code
+                for q in live:  # a dead rank would leave its peers blocked in a collective
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -38,12 +79,16 @@ def main():
                          "tpch22: the full 22-query TPC-H sweep over the flattened index (BASELINE config 2)")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
 
     import torch
 
     from spark_druid_olap_amd.parallel.world import init_world
 
     world = init_world()
+    if world.size != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but the process group has {world.size} rank(s)")
     dev = world.device()
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
@@ -188,7 +233,8 @@ def main():
             "data": f"synthetic ({args.model.upper()} dbgen-like distributions, random dictionary values, generated on device)",
             "config": {"model": model,
                        "global_batch": nq, "seq_len": int(nrows), "parallelism": f"dp{world.size} (segment shards)",
-                       "queries": len(queries), "mode": args.mode},
+                       "queries": len(queries), "mode": args.mode,
+                       "world": {"size": world.size, "backend": world.backend}},
             "qps": round(nq / (total_ms / 1e3), 3),
             "per_query_ms": {k: round(v, 4) for k, v in means.items()},
             "per_query_min_ms": {k: round(v, 4) for k, v in mins.items()},

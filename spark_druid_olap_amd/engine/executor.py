@@ -78,6 +78,7 @@ class PreparedQuery:
         self.low = Lowerer(ds, world=engine.world)
         self.scans: List[tuple] = []  # (tag, prog, prepared)
         self.segments_per_query = segments_per_query
+        self.window: Optional["ShardWindow"] = None
         qt = qs.queryType
         if qt in ("groupBy", "timeseries", "topN"):
             dims = []
@@ -87,6 +88,10 @@ class PreparedQuery:
                 dims = [qs.dimension]
             prog = self.low.lower_aggregate(qs.intervals, qs.filter, dims, qs.granularity, qs.aggregations)
             self._full_prog = prog
+            # grouped on the shard key across several ranks: scan this shard's key window only
+            self.window = shard_window(prog, ds, self.world)
+            if self.window is not None:
+                prog = self.window.local
             if segments_per_query:
                 # "historical" execution: one partial query per batch of segments, merged here
                 for bprog in segment_batches(prog, ds, segments_per_query):
@@ -115,7 +120,8 @@ class PreparedQuery:
             # one GPU: a dense HBM table of up to 16 GB beats a hash table over the same key space
             # (TPC-H Q18: 150M order groups); with several ranks dense partials are reduced whole,
             # so huge key spaces stay sparse (hash) and merge by present keys
-            dense_max = None if self.world.distributed else int(os.environ.get("SDO_DENSE_MAX_1GPU", 16 << 30))
+            local = not self.world.distributed or (self.window is not None and prog is not self._full_prog)
+            dense_max = int(os.environ.get("SDO_DENSE_MAX_1GPU", 16 << 30)) if local else None
             return PreparedScan(prog, dense_max=dense_max)
         return None
 
@@ -131,6 +137,8 @@ class PreparedQuery:
         its peers, so the failure can be agreed on inside the merge)."""
         dev = self.ds.device
         m = 1 << prog.hll_p
+        if self.window is not None:
+            return self.window.empty(dev)
         if prep is not None:
             from ..ops import desc as D_
 
@@ -194,10 +202,14 @@ class PreparedQuery:
                 if len(self.scans) > 1:
                     parts = [part] + [self._scan(p_, q_) for _, p_, q_ in self.scans[1:]]
                     part = combine_local(prog, parts)
+            if self.window is not None:
+                part = self.window.to_global(part)
         except Exception as e:  # noqa: BLE001  (peers learn about it in the merge collective)
             if not self.world.distributed:
                 raise
             err, part = e, self._placeholder(prog, prep)
+        if self.window is not None:
+            prog = self._full_prog
         t1 = time.perf_counter()
         disjoint = bool(self.ds.shard_key) and any(k.col == self.ds.shard_key for k in prog.keys)
         with T.span("sdo.merge"):
@@ -465,6 +477,84 @@ class PreparedQuery:
         cols = ["timestamp"] + list(dims) + list(mets)
         nxt = {ident: start + int(page.numel()) - 1} if page.numel() else {ident: start - 1}
         return QueryResult(cols, data, "select", {"rows": int(rows.numel())}, paging=nxt)
+
+
+class ShardWindow:
+    """Grouping on the datasource's shard key across ranks: every rank only holds its own key range
+    (TPC-H orders are range-partitioned on ``o_orderkey``), so the scan accumulates into a dense
+    table of the LOCAL key window -- the same table size as one GPU instead of an N-times larger
+    key space that would force the hash table -- and the partial keys are rebased to the global
+    packed layout before the (disjoint, concatenating) merge.  The reference's equivalent is the
+    historical query over a server's own segments (``sd/DruidRDD.scala:62-84``)."""
+
+    MIN_SAVING = 4  # only when the local window is at most 1/4 of the global key space
+
+    def __init__(self, glob: ScanProgram, local: ScanProgram):
+        self.glob = glob
+        self.local = local
+
+    def empty(self, dev) -> Partials:
+        m = 1 << self.glob.hll_p
+        return Partials("sparse", torch.empty((0, self.glob.nslots), dtype=torch.int64, device=dev),
+                        torch.zeros(0, dtype=torch.int64, device=dev),
+                        [torch.zeros((0, m), dtype=torch.int32, device=dev) for _ in range(self.glob.nhll)])
+
+    def to_global(self, part: Partials) -> Partials:
+        sp = part.compact()
+        g = sp.keys.to(torch.int64)
+        out = torch.zeros_like(g)
+        for kl, kg in zip(self.local.keys, self.glob.keys):
+            ids = torch.remainder(torch.div(g, kl.stride, rounding_mode="floor"), max(1, kl.card)) + kl.base
+            out += (ids - kg.base) * kg.stride
+        return Partials("sparse", sp.acc, out, sp.hll)
+
+
+_ID_RANGE_CACHE: Dict[tuple, tuple] = {}
+
+
+def shard_id_range(ds: DataSource, col: str) -> tuple:
+    """(min, max) dictionary id of ``col`` on this shard (cached per datasource + column)."""
+    from .lower import column_tensor
+
+    key = (id(ds), col)
+    hit = _ID_RANGE_CACHE.get(key)
+    if hit is not None and hit[0] is ds:
+        return hit[1]
+    t = column_tensor(ds, col)
+    if t.numel() == 0:
+        r = (0, -1)
+    else:
+        lo, hi = torch.aminmax(t)
+        r = (int(lo), int(hi))
+    _ID_RANGE_CACHE[key] = (ds, r)
+    return r
+
+
+def shard_window(prog: ScanProgram, ds: DataSource, world: World) -> Optional[ShardWindow]:
+    import copy
+
+    if world is None or not world.distributed or not ds.shard_key or prog.empty or prog.thetas:
+        return None
+    if os.environ.get("SDO_NO_SHARD_WINDOW"):
+        return None
+    idx = next((i for i, kc in enumerate(prog.keys)
+                if kc.kind == D.K_ID and kc.col == ds.shard_key and kc.orig is None and kc.base == 0), None)
+    if idx is None or prog.G < int(os.environ.get("SDO_SHARD_WINDOW_MIN_G", 1 << 16)):
+        return None
+    lo, hi = shard_id_range(ds, ds.shard_key)
+    card = max(1, hi - lo + 1)
+    if card * ShardWindow.MIN_SAVING > prog.keys[idx].card:
+        return None
+    keys = [copy.copy(kc) for kc in prog.keys]
+    keys[idx].base, keys[idx].card = max(0, lo), card
+    G = 1
+    for kc in reversed(keys):
+        kc.stride = G
+        G *= max(1, kc.card)
+    import dataclasses
+
+    local = dataclasses.replace(prog, keys=keys, G=G)
+    return ShardWindow(prog, local)
 
 
 def _init_acc(prog: ScanProgram, rows: int, dev) -> torch.Tensor:

@@ -22,6 +22,8 @@ from typing import Callable, Dict, List, Optional, Tuple
 import numpy as np
 import torch
 
+from ..ops import desc as D
+
 from ..query import spec as S
 from ..segment.datasource import DataSource
 from .lower import LoweringError
@@ -41,6 +43,7 @@ class DeviceColumn:
         self.decode = decode
         self.scale = scale
         self.card = card  # key ids are known to lie in [0, card) (no min/max pass needed)
+        self.num: Optional[Tuple[int, int]] = None  # integral key: value = (id + base) / 10^scale
 
     @property
     def is_float(self) -> bool:
@@ -83,6 +86,9 @@ def device_columns(pq) -> Tuple[Dict[str, DeviceColumn], int]:
         ids_of.append(ids)
         cols[kc.name] = DeviceColumn(kc.name, ids, kc.decoder if kc.decoder is not None else (lambda x: x),
                                      card=max(1, kc.card))
+        if kc.kind == D.K_INT and kc.col in pq.ds.metrics:
+            m = pq.ds.metrics[kc.col]
+            cols[kc.name].num = (int(kc.base), m.scale if m.kind == "decimal" else 0)
     for kc, det, lut in getattr(prog, "derived", ()):
         did = ids_of[det]
         orig = prog.keys[det].orig
@@ -123,6 +129,9 @@ def _torch_eval(n, pmap: Dict[str, str], cols: Dict[str, DeviceColumn]) -> torch
         c = cols.get(pmap.get(n[1], n[1]))
         if c is None:
             raise LoweringError(f"nested expression over unknown column {n[1]!r}")
+        if c.num is not None:  # grouped integral metric: key id -> stored value
+            v = (c.t + c.num[0]).to(torch.float64)
+            return v / (10.0 ** c.num[1]) if c.num[1] else v
         return c.as_float() if c.decode is None else c.t.to(torch.float64)
     if k in ("neg", "abs", "floor", "ceil", "sqrt", "log", "exp"):
         a = _torch_eval(n[1], pmap, cols)

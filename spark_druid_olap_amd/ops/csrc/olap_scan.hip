@@ -589,6 +589,8 @@ __global__ __launch_bounds__(512) void olap_scan_kernel(const ScanDesc* __restri
           } else if (ko.kind == K_INT) {
             v -= ko.base;
             v = v < 0 ? 0 : (v >= ko.card ? ko.card - 1 : v);
+          } else {
+            v -= ko.base;  // K_ID: 0, or the shard-local key window's first id
           }
           key[u] += (uint64_t)v * (uint64_t)ko.stride;
         }

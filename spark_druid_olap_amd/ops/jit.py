@@ -433,7 +433,9 @@ class _Gen:
         body.append("        uint64_t key = 0;")
         for k, kc in enumerate(p.keys):
             v = self.ival(kc.col_idx)
-            if kc.kind == D.K_ID:
+            if kc.kind == D.K_ID and kc.base:  # shard-local key window (engine/executor.py ShardWindow)
+                body.append(f"        key += (uint64_t)((int64_t)({v}) - {_lit(kc.base)}) * {kc.stride}ull;")
+            elif kc.kind == D.K_ID:
                 body.append(f"        key += (uint64_t)({v}) * {kc.stride}ull;")
             elif kc.kind == D.K_REMAP:
                 body.append(f"        key += (uint64_t)rm{k}[{v}] * {kc.stride}ull;")

@@ -7,6 +7,8 @@ same partial structures (dense ``[G, nslots]`` or sparse keys + accumulators).
 """
 from __future__ import annotations
 
+import os
+
 import math
 from typing import List, Optional, Tuple
 
@@ -255,6 +257,8 @@ def compute_keys(prog, rows: torch.Tensor) -> torch.Tensor:
             v = v.clamp(0, kc.card - 1)
         elif kc.kind == D.K_INT:
             v = (v - kc.base).clamp(0, kc.card - 1)
+        elif kc.base:
+            v = v - kc.base  # K_ID in a shard-local key window
         key += v * kc.stride
     return key
 
@@ -329,7 +333,7 @@ def run_reference(prog, sparse: Optional[bool] = None):
     m = 1 << prog.hll_p
     nslots = prog.nslots
     if sparse is None:
-        sparse = prog.G > (1 << 22)
+        sparse = prog.G > int(os.environ.get("SDO_REF_SPARSE_G", 1 << 22))
     rows = _rows(prog) if not prog.empty else torch.zeros(0, dtype=torch.int64, device=dev)
     mask = eval_bexpr(prog, prog.bexpr, rows) if rows.numel() else torch.zeros(0, dtype=torch.bool, device=dev)
     rows = rows[mask]

@@ -8,9 +8,12 @@ final aggregate, ``asd/PostAggregate.scala:39-103``, re-designed for RCCL over x
   sums + status word, float sums, max + bitwise-NOT(min)) with one host sync at the end; HLL
   registers reduce with MAX -- mergeable sketches, which the reference could not merge across
   historicals, ``asd/PostAggregate.scala:62-70``.
-* Sparse (hash) states are compacted per GPU, gathered (variable length), and merged by key.
-  When the datasource is partitioned on a grouping key the groups are disjoint across ranks and
-  the merge degenerates to a concatenation.
+* Sparse (hash) states are compacted per GPU and shuffled by key hash with one
+  ``all_to_all_single`` (the reference's hash-partitioned Exchange before Spark's final aggregate,
+  ``asd/PostAggregate.scala:97-103``): each rank receives ~1/N of the partial rows, merges its key
+  range locally, and only the merged (now disjoint) groups are gathered.  When the datasource is
+  partitioned on a grouping key the groups are already disjoint across ranks and the merge
+  degenerates to a concatenation (no shuffle).
 """
 from __future__ import annotations
 
@@ -58,7 +61,8 @@ def _merge_dense_bucketed(world: World, prog, part: Partials, status: int,
     by_op = {op: [s for s, (o, _) in enumerate(prog.slots) if o == op]
              for op in (D.S_SUM_I, D.S_SUM_F, D.S_MIN_I, D.S_MAX_I)}
     si, sf, mn, mx = by_op[D.S_SUM_I], by_op[D.S_SUM_F], by_op[D.S_MIN_I], by_op[D.S_MAX_I]
-    st = torch.full((1,), status, dtype=torch.int64, device=acc.device)
+    st = torch.zeros((world.size,), dtype=torch.int64, device=acc.device)
+    st[world.rank] = status
     b_sum = torch.cat([acc[:, si].reshape(-1), st]) if si else st
     world.all_reduce(b_sum, "sum")
     if sf:
@@ -77,11 +81,11 @@ def _merge_dense_bucketed(world: World, prog, part: Partials, status: int,
         hh = h.clone()
         world.all_reduce(hh, "max")
         hll.append(hh)
-    failed = int(b_sum[-1].item())
-    if local_error is not None or failed:
-        raise_if_failed([failed], world.rank, local_error)
+    sts = b_sum[-world.size:].tolist()  # one status word per rank (each rank wrote its own slot)
+    if local_error is not None or any(sts):
+        raise_if_failed(sts, world.rank, local_error)
     if si:
-        acc[:, si] = b_sum[:-1].reshape(R, len(si))
+        acc[:, si] = b_sum[:-world.size].reshape(R, len(si))
     return Partials("dense", acc, None, hll)
 
 
@@ -95,7 +99,7 @@ def merge_partials(world: World, prog, part: Partials, disjoint_keys: bool = Fal
             raise local_error
         return part
     status = STATUS_FAILED if local_error is not None else STATUS_OK
-    if part.kind == "dense" and part.acc.numel() * 8 * world.size <= ONE_SHOT_BYTES:
+    if part.kind == "dense" and dense_state_bytes(part) * world.size <= ONE_SHOT_BYTES:
         R, ns = part.acc.shape
         st = torch.full((1,), status, dtype=torch.int64, device=part.acc.device)
         pieces = [part.acc.reshape(-1)] + [h.reshape(-1).to(torch.int64) for h in part.hll] + [st]
@@ -117,6 +121,20 @@ def merge_partials(world: World, prog, part: Partials, disjoint_keys: bool = Fal
         return _merge_dense_bucketed(world, prog, part, status, local_error)
     # sparse
     sp = part.compact()
+    if disjoint_keys:
+        return _gather_disjoint(world, sp, status, local_error)
+    return _merge_sparse_shuffle(world, prog, sp, status, local_error)
+
+
+def dense_state_bytes(part: Partials) -> int:
+    """Bytes one rank contributes to the one-shot gather: accumulators plus HLL registers (widened
+    to int64 words in the gather buffer) -- the registers are usually the bulk (2048 per group per
+    sketch at HLL_P=11)."""
+    return (part.acc.numel() + sum(h.numel() for h in part.hll)) * 8
+
+
+def _gather_disjoint(world: World, sp: Partials, status: int, local_error) -> Partials:
+    """Groups are disjoint across ranks (grouped on the shard key): concatenate, no merge."""
     # keys + accumulators travel as one [n, 1 + nslots] int64 block: one length exchange (which also
     # carries the status word) + one gather
     kv = torch.cat([sp.keys.reshape(-1, 1).to(torch.int64), sp.acc], dim=1)
@@ -124,8 +142,32 @@ def merge_partials(world: World, prog, part: Partials, disjoint_keys: bool = Fal
     if local_error is not None or any(sts):
         raise_if_failed(sts, world.rank, local_error)
     hlls = [world.all_gather_varlen(h) for h in sp.hll]
-    parts = [Partials("sparse", kvs[i][:, 1:], kvs[i][:, 0], [h[i] for h in hlls]) for i in range(world.size)]
-    if disjoint_keys:
-        return Partials("sparse", torch.cat([p.acc for p in parts]), torch.cat([p.keys for p in parts]),
-                        [torch.cat([p.hll[i] for p in parts]) for i in range(len(sp.hll))])
-    return merge_sparse(parts, prog.slots)
+    kv = torch.cat(kvs)
+    return Partials("sparse", kv[:, 1:], kv[:, 0], [torch.cat(h) for h in hlls])
+
+
+def shuffle_owner(keys: torch.Tensor, n: int) -> torch.Tensor:
+    """Destination rank of each group key: a multiplicative hash, so the mixed-radix packed keys
+    (whose low digits are the fastest key) spread evenly over the ranks."""
+    h = (keys.to(torch.int64) * -7046029254386353131) >> 29  # 0x9E3779B97F4A7C15 as int64
+    return torch.remainder(h, n)
+
+
+def _merge_sparse_shuffle(world: World, prog, sp: Partials, status: int, local_error) -> Partials:
+    """Hash-partitioned shuffle + local merge + gather of the merged groups."""
+    n = world.size
+    dest = shuffle_owner(sp.keys, n)
+    order = torch.argsort(dest, stable=True)
+    counts = torch.bincount(dest, minlength=n)
+    kv = torch.cat([sp.keys.reshape(-1, 1).to(torch.int64), sp.acc], dim=1).index_select(0, order)
+    recv, rc, sts = world.all_to_all_varlen(kv, counts, status=status)
+    if local_error is not None or any(sts):
+        raise_if_failed(sts, world.rank, local_error)
+    hll = []
+    for h in sp.hll:
+        r, _ = world.all_to_all_varlen(h.index_select(0, order), counts)
+        hll.append(r)
+    mine = Partials("sparse", recv[:, 1:], recv[:, 0], hll)
+    merged = merge_sparse([mine], prog.slots) if recv.shape[0] else mine
+    # this rank owns a disjoint key range now: the final groups are a concatenation
+    return _gather_disjoint(world, merged, STATUS_OK, None)

@@ -34,9 +34,21 @@ class World:
         return self.rank == 0
 
     def device(self) -> torch.device:
-        if torch.cuda.is_available() and self.backend != "gloo":
+        if torch.cuda.is_available() and (self.backend != "gloo" or _gloo_on_gpu()):
             return torch.device("cuda", self.local_rank % max(1, torch.cuda.device_count()))
         return torch.device("cpu")
+
+    # gloo over device tensors (the one-GPU rehearsal of the multi-rank path: several ranks share
+    # one card, which RCCL refuses): collectives stage through host memory.  RCCL takes device
+    # tensors directly.
+    def _stage(self, t: torch.Tensor) -> torch.Tensor:
+        return t.cpu() if (t.is_cuda and self.backend == "gloo") else t
+
+    def _unstage(self, h: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
+        if h is t:
+            return t
+        t.copy_(h)
+        return t
 
     # ---------------------------------------------------------------- collectives
     def barrier(self):
@@ -50,18 +62,51 @@ class World:
         if not self.distributed:
             return t
         o = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
-        dist.all_reduce(t, op=o, group=self.group)
-        return t
+        h = self._stage(t)
+        dist.all_reduce(h, op=o, group=self.group)
+        return self._unstage(h, t)
 
     def all_gather_tensor(self, t: torch.Tensor) -> torch.Tensor:
         """[size, *t.shape] stacked gather (same shape on every rank)."""
         if not self.distributed:
             return t.unsqueeze(0)
-        src = t.contiguous().reshape(-1)
+        src = self._stage(t.contiguous().reshape(-1))
         # concatenated layout works on both RCCL and gloo (gloo rejects the stacked form)
-        out = torch.empty((self.size * src.numel(),), dtype=t.dtype, device=t.device)
+        out = torch.empty((self.size * src.numel(),), dtype=t.dtype, device=src.device)
         dist.all_gather_into_tensor(out, src, group=self.group)
-        return out.view((self.size,) + tuple(t.shape))
+        return out.to(t.device).view((self.size,) + tuple(t.shape))
+
+    def all_to_all_varlen(self, t: torch.Tensor, counts: torch.Tensor, status: Optional[int] = None):
+        """Personalized exchange (the reference's hash-partitioned shuffle before the final
+        aggregate, ``asd/PostAggregate.scala:97-103``): ``t``'s rows are grouped by destination rank
+        (``counts[r]`` rows for rank r, in rank order); returns the rows every rank sent here,
+        concatenated in source-rank order, plus the per-source counts.  One ``all_to_all_single`` of
+        the counts (carrying the status word, parallel/fault.py) and one of the payload: each rank
+        receives ~total/N rows instead of the all-gather's total.  With ``status`` set,
+        ``(rows, recv_counts, statuses)`` is returned and a failure skips the payload exchange."""
+        if not self.distributed:
+            return (t, counts.clone(), [status]) if status is not None else (t, counts.clone())
+        n = self.size
+        dev = t.device
+        send_meta = torch.stack([counts.to(torch.int64).cpu(), torch.full((n,), int(status or 0), dtype=torch.int64)], 1)
+        send_meta = send_meta.to(dev if self.backend == "nccl" else "cpu").reshape(-1).contiguous()
+        recv_meta = torch.empty_like(send_meta)
+        dist.all_to_all_single(recv_meta, send_meta, group=self.group)
+        meta = recv_meta.reshape(n, 2).cpu()
+        rc = meta[:, 0]
+        sts = meta[:, 1].tolist()
+        if status is not None and any(sts):
+            return t[:0], rc, sts
+        row = tuple(t.shape[1:])
+        width = 1
+        for x in row:
+            width *= x
+        src = self._stage(t.contiguous().reshape(-1))
+        out = torch.empty((int(rc.sum()) * width,), dtype=t.dtype, device=src.device)
+        dist.all_to_all_single(out, src, output_split_sizes=[int(x) * width for x in rc.tolist()],
+                               input_split_sizes=[int(x) * width for x in counts.cpu().tolist()], group=self.group)
+        out = out.to(dev).reshape((-1,) + row)
+        return (out, rc, sts) if status is not None else (out, rc)
 
     def all_gather_varlen(self, t: torch.Tensor, status: Optional[int] = None):
         """Gather tensors whose first dimension differs per rank.  With ``status`` set, every rank's
@@ -93,13 +138,19 @@ class World:
     def max_float(self, x: float) -> float:
         if not self.distributed:
             return x
-        dev = self.device()
+        dev = self.device() if self.backend == "nccl" else torch.device("cpu")
         t = torch.tensor([x], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return float(t.item())
 
 
 _WORLD: Optional[World] = None
+
+
+def _gloo_on_gpu() -> bool:
+    """``SDO_GLOO_GPU=1``: ranks keep their shards on the GPU but talk over gloo (several ranks on
+    one card -- a rehearsal of the multi-GPU code paths on a one-GPU box)."""
+    return os.environ.get("SDO_GLOO_GPU", "0") not in ("0", "")
 
 
 def init_world(backend: Optional[str] = None, timeout_s: int = 600) -> World:
@@ -112,7 +163,9 @@ def init_world(backend: Optional[str] = None, timeout_s: int = 600) -> World:
         _WORLD = World(0, 1, local, "none")
         return _WORLD
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = "nccl" if torch.cuda.is_available() and not _gloo_on_gpu() else "gloo"
+    if backend == "gloo" and _gloo_on_gpu() and torch.cuda.is_available():
+        torch.cuda.set_device(local % torch.cuda.device_count())
     if backend == "nccl":
         torch.cuda.set_device(local % torch.cuda.device_count())
     if not dist.is_initialized():

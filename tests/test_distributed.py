@@ -1,4 +1,4 @@
-"""Multi-process (gloo, world_size 2) tests of the data-parallel path.
+"""Multi-process (gloo, world_size 2 / 4 / 8) tests of the data-parallel path.
 
 Each rank owns a different shard of the flattened TPC-H table (as each GPU does in the 8-GPU
 bench).  Every rank plans the same SQL, scans its shard and merges partials with collectives; the
@@ -29,9 +29,14 @@ QUERIES = [
 ]
 # the full TPC-H sweep: FD tables all-reduced across ranks, nested device aggregation over merged
 # partials, execution-time scalar subqueries, device HAVING, expression filters
+from spark_druid_olap_amd.models import tpch as _tpch  # noqa: E402
 from spark_druid_olap_amd.models import tpch22 as _tpch22  # noqa: E402
 
 QUERIES += [q for _, q in _tpch22.QUERIES]
+# group-bys on non-shard keys with many groups: hash-partitioned all-to-all shuffle merge
+QUERIES += [_tpch.Q10[1],
+            "select c_name, count(*), sum(l_quantity), max(l_discount) from orderLineItemPartSupplier group by c_name",
+            "select o_orderkey, o_orderdate, count(*) from orderLineItemPartSupplier group by o_orderkey, o_orderdate"]
 APPROX = "select l_returnflag, approx_count_distinct(o_orderkey) from orderLineItemPartSupplier group by l_returnflag"
 
 
@@ -43,9 +48,9 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, env=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
+                      LOCAL_RANK=str(rank), OMP_NUM_THREADS="1", **(env or {}))
     import pickle
 
     from spark_druid_olap_amd.engine.executor import Engine
@@ -54,7 +59,7 @@ def _worker(rank, world, port, outdir):
     from spark_druid_olap_amd.session import Session
 
     w = init_world(backend="gloo")
-    flat = tpch.generate_flat(0.004, "cpu", rank=rank, world=world)
+    flat = tpch.generate_flat(0.008 / world, "cpu", rank=rank, world=world)
     ds = tpch.to_datasource(flat, profile="bench")
     df = tpch.to_pandas(flat)
     s = Session(engine=Engine(w, use_native=False))
@@ -79,8 +84,16 @@ def _norm(rows):
     return sorted(out, key=lambda r: tuple((x is None, str(x)) for x in r))
 
 
-@pytest.mark.timeout(600)
-def test_two_rank_sql_equals_union():
+# (world size, env): 2 ranks with the default merge paths (dense one-shot / bucketed, disjoint
+# concatenation); 4 and 8 ranks with every group-by of more than 512 groups forced onto the sparse
+# path (hash-partitioned all-to-all shuffle) and shard-key group-bys onto the local key window
+WORLDS = [(2, {}), (4, {"SDO_REF_SPARSE_G": "512", "SDO_SHARD_WINDOW_MIN_G": "0"}),
+          (8, {"SDO_REF_SPARSE_G": "512", "SDO_SHARD_WINDOW_MIN_G": "0"})]
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("world,env", WORLDS, ids=[f"ranks{w}" for w, _ in WORLDS])
+def test_multi_rank_sql_equals_union(world, env):
     import pickle
 
     import pandas as pd
@@ -89,15 +102,14 @@ def test_two_rank_sql_equals_union():
     from spark_druid_olap_amd.models import tpch
     from spark_druid_olap_amd.session import Session
 
-    world = 2
     with tempfile.TemporaryDirectory() as td:
         ctx = mp.get_context("spawn")
         port = _free_port()
-        ps = [ctx.Process(target=_worker, args=(r, world, port, td)) for r in range(world)]
+        ps = [ctx.Process(target=_worker, args=(r, world, port, td, env)) for r in range(world)]
         for p in ps:
             p.start()
         for p in ps:
-            p.join(500)
+            p.join(800)
             assert p.exitcode == 0, f"rank failed with {p.exitcode}"
         outs = []
         for r in range(world):
