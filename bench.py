@@ -26,47 +26,6 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def _free_port() -> int:
-    import socket
-
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
-
-
-def spawn_ranks(n: int) -> int:
-    """``--gpus N`` without torchrun: start N rank processes (one per GPU) and wait for them.
-
-    This parent never imports torch nor touches a GPU -- it only starts children with the torchrun
-    environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*) and returns the worst exit code; rank 0's
-    stdout (the JSON line) passes straight through.  A failed rank takes the others down."""
-    import subprocess
-
-    port = os.environ.get("MASTER_PORT") or str(_free_port())
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
-                                      stdout=None if r == 0 else subprocess.DEVNULL))
-    rc = 0
-    live = list(procs)
-    while live:
-        for p in list(live):
-            code = p.poll()
-            if code is None:
-                continue
-            live.remove(p)
-            if code != 0:
-                rc = rc or code
-                for q in live:  # a dead rank would leave its peers blocked in a collective
-                    q.terminate()
-        time.sleep(0.2)
-    return rc
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -80,7 +39,10 @@ def main():
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(spawn_ranks(args.gpus))
+        # one process per GPU, started here (never from a process that touched the GPU)
+        from spark_druid_olap_amd.utils.launch import spawn_ranks
+
+        sys.exit(spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
 
     import torch
 

@@ -263,8 +263,29 @@ class Catalog:
         self.current_db = "default"
         self.cluster = cluster or DruidCluster()
         self.temp: Dict[str, Table] = {}
-        self.version = 0
+        self._ver = [0]  # shared with session views (plan caches key on it)
         self._lock = threading.RLock()
+
+    @property
+    def version(self) -> int:
+        return self._ver[0]
+
+    @version.setter
+    def version(self, v: int) -> None:
+        self._ver[0] = v
+
+    def session_view(self) -> "Catalog":
+        """A per-client view (one HiveServer2 session): the databases, tables and Druid cluster are
+        shared, the current database and temporary views are the session's own -- Spark's
+        SessionCatalog split between the shared external catalog and session state."""
+        v = Catalog.__new__(Catalog)
+        v.dbs = self.dbs
+        v.current_db = "default"
+        v.cluster = self.cluster
+        v.temp = {}
+        v._ver = self._ver
+        v._lock = self._lock
+        return v
 
     def _split(self, parts) -> Tuple[Optional[str], str]:
         if isinstance(parts, str):

@@ -150,6 +150,11 @@ class Conf:
             for k, v in init.items():
                 self.set(k, v)
 
+    def copy(self) -> "Conf":
+        c = Conf.__new__(Conf)
+        c._vals = dict(self._vals)
+        return c
+
     def set(self, key: str, value: Any) -> None:
         self._vals[key] = value if isinstance(value, str) else json.dumps(value) if not isinstance(
             value, (int, float, bool)) else str(value).lower() if isinstance(value, bool) else str(value)

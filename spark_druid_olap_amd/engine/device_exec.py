@@ -158,23 +158,44 @@ class PreparedScan:
                 # the interpreter kernel only knows per-wave copies: accumulate in HBM instead
                 self.mode, self.shared, self.lds = D.M_DENSE_GLOBAL, False, 0
                 self.jit = _jit_for(prog, self.mode, False, self.m)
-        self._alloc()
+        import threading
+
+        self._slot_lock = threading.Lock()
+        self._slots = {}
+        self._bufs()  # the preparing slot's buffers (settles the LDS-budget mode fallback)
 
     # ------------------------------------------------------------------ buffers
-    def _alloc(self):
+    # Every execution slot (engine/scheduler.py) gets its own accumulators / hash table / HLL
+    # registers / descriptor, so concurrent runs of one prepared query on different streams never
+    # share device state; the generated kernel, grid and mode are shared.
+    def _bufs(self) -> "_Bufs":
+        from .scheduler import current_slot
+
+        slot = current_slot()
+        b = self._slots.get(slot)
+        if b is None:
+            with self._slot_lock:
+                b = self._slots.get(slot)
+                if b is None:
+                    b = self._slots[slot] = self._alloc(self.cap)
+        return b
+
+    def _alloc(self, cap: int) -> "_Bufs":
         from .lower import lds_layout
 
         prog, dev = self.prog, self.dev
-        rows = self.cap if self.mode == D.M_HASH else prog.G
-        self.rows = rows
-        self.init_row = torch.tensor([init for _, init in prog.slots], dtype=torch.int64, device=dev)
+        b = _Bufs()
+        b.cap = cap
+        rows = cap if self.mode == D.M_HASH else prog.G
+        b.rows = rows
+        b.init_row = torch.tensor([init for _, init in prog.slots], dtype=torch.int64, device=dev)
         if self.pres_bytes:
-            self.acc = torch.empty((rows,), dtype=torch.uint8, device=dev)
+            b.acc = torch.empty((rows,), dtype=torch.uint8, device=dev)
         else:
-            self.acc = torch.empty((rows, prog.nslots), dtype=torch.int64, device=dev)
-        self.keys = torch.empty(rows if self.mode == D.M_HASH else 1, dtype=torch.int64, device=dev)
-        self.hll = [torch.empty(rows * self.m, dtype=torch.int32, device=dev) for _ in range(prog.nhll)]
-        self.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
+            b.acc = torch.empty((rows, prog.nslots), dtype=torch.int64, device=dev)
+        b.keys = torch.empty(rows if self.mode == D.M_HASH else 1, dtype=torch.int64, device=dev)
+        b.hll = [torch.empty(rows * self.m, dtype=torch.int32, device=dev) for _ in range(prog.nhll)]
+        b.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
         hll_offs = []
         off = prog.G * prog.nslots * 8 * (BLOCK // 64)
         for _ in range(prog.nhll):
@@ -189,66 +210,79 @@ class PreparedScan:
             cache_off, wave_bytes, _, total = lds_layout(prog, 0, UNROLL, BLOCK // 64)
         if total > 160 * 1024:
             raise RuntimeError(f"query needs {total} bytes of LDS staging; reduce SDO_UNROLL")
-        d = pack(prog, self.mode, self.dedup, self.hll_lds, 0 if self.shared else self.lds, self.acc.data_ptr(),
-                 self.keys.data_ptr(),
-                 self.cap, self.overflow.data_ptr(), 0, 0, [h.data_ptr() for h in self.hll], hll_offs,
+        d = pack(prog, self.mode, self.dedup, self.hll_lds, 0 if self.shared else self.lds, b.acc.data_ptr(),
+                 b.keys.data_ptr(),
+                 cap, b.overflow.data_ptr(), 0, 0, [h.data_ptr() for h in b.hll], hll_offs,
                  unroll=UNROLL, cache_off=cache_off, wave_bytes=wave_bytes)
         self.lds_total = total
-        self.desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
+        b.desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
         self.grid = _grid(dev, int(d[0]["total_chunks"]), self.jit.lay.total if self.jit else total)
+        return b
 
-    def _launch(self):
+    def _launch(self, b: "_Bufs"):
         if self.jit is not None:
-            self.jit.launch(self.desc, self.grid)
+            self.jit.launch(b.desc, self.grid)
         else:
-            native.scan(self.desc, self.grid, BLOCK, self.lds_total, UNROLL)
+            native.scan(b.desc, self.grid, BLOCK, self.lds_total, UNROLL)
 
-    def _reset(self):
+    def _reset(self, b: "_Bufs"):
         if self.pres_bytes:
-            self.acc.zero_()
+            b.acc.zero_()
         else:
-            self.acc.copy_(self.init_row.expand_as(self.acc))
+            b.acc.copy_(b.init_row.expand_as(b.acc))
         if self.mode == D.M_HASH:
-            self.keys.fill_(-1)
-        for h in self.hll:
+            b.keys.fill_(-1)
+        for h in b.hll:
             h.zero_()
-        self.overflow.zero_()
+        b.overflow.zero_()
 
     # ------------------------------------------------------------------ run
     def run(self) -> Partials:
+        from .scheduler import current_slot
+
         prog = self.prog
+        b = self._bufs()
         if prog.empty:
             if self.mode != D.M_HASH:
                 # dense layout even when this shard has nothing to scan: every rank must issue the
                 # same merge collective (parallel/merge.py) for the same query
-                self._reset()
-                return Partials("dense", self.acc, None, [h.view(self.rows, self.m) for h in self.hll])
+                self._reset(b)
+                return Partials("dense", b.acc, None, [h.view(b.rows, self.m) for h in b.hll])
             return self._empty()
         while True:
-            self._reset()
-            self._launch()
+            self._reset(b)
+            self._launch(b)
             if self.pres_bytes:
-                idx = _nonzero_big(self.acc)
+                idx = native.nonzero_rows(b.acc)
                 return Partials("sparse", torch.ones((idx.numel(), 1), dtype=torch.int64, device=self.dev), idx, [])
             if self.mode != D.M_HASH:
                 break
-            if int(self.overflow.item()) == 0:
+            if int(b.overflow.item()) == 0:
                 break
-            self.cap *= 4  # grow and retry
-            self._alloc()
+            b = self._slots[current_slot()] = self._alloc(b.cap * 4)  # grow and retry
+            self.cap = max(self.cap, b.cap)
         if self.mode == D.M_HASH:
-            valid = _nonzero_big(self.keys != -1)
-            out = Partials("sparse", self.acc.index_select(0, valid), self.keys.index_select(0, valid),
-                           [h.view(self.rows, self.m).index_select(0, valid) for h in self.hll])
+            valid = _nonzero_big(b.keys != -1)
+            out = Partials("sparse", b.acc.index_select(0, valid), b.keys.index_select(0, valid),
+                           [h.view(b.rows, self.m).index_select(0, valid) for h in b.hll])
             # adaptive capacity: the planner's row estimate sizes the first table (TPC-H Q16's NOT
             # filters: 2^31 slots for 12M groups); later runs of this prepared query size it from
             # the observed group count (an overflow still grows it and retries)
             want = _next_pow2(2 * int(valid.numel()) + 1024)
-            if want * 4 <= self.cap:
+            if want * 4 <= b.cap:
                 self.cap = want
-                self._alloc()
+                self._slots[current_slot()] = self._alloc(want)
             return out
-        return Partials("dense", self.acc, None, [h.view(self.rows, self.m) for h in self.hll])
+        return Partials("dense", b.acc, None, [h.view(b.rows, self.m) for h in b.hll])
+
+    # single-slot views (tests and tools inspect the implicit slot's buffers)
+    @property
+    def acc(self):
+        return self._bufs().acc
+
+    @property
+    def desc(self):
+        return self._bufs().desc
 
     def _empty(self) -> Partials:
         prog = self.prog
@@ -257,42 +291,63 @@ class PreparedScan:
                         [torch.zeros((0, self.m), dtype=torch.int32, device=self.dev) for _ in range(prog.nhll)])
 
 
+class _Bufs:
+    """One execution slot's device buffers for a prepared scan."""
+    __slots__ = ("cap", "rows", "init_row", "acc", "keys", "hll", "overflow", "desc")
+
+
 class PreparedMask:
-    """Filter-only scan: writes one u64 mask word per 64 rows (select queries)."""
+    """Filter-only scan: writes one u64 mask word per 64 rows (select queries); the mask becomes
+    row ids with the ``compact_rows`` kernel (ops/csrc/post_scan.hip).  Mask + descriptor are
+    per execution slot, like PreparedScan's buffers."""
 
     def __init__(self, prog: ScanProgram):
+        import threading
+
         from .lower import lds_layout
 
         self.prog = prog
-        ds = prog.ds
-        self.dev = ds.device
-        self.mask = torch.zeros(ds.nwords, dtype=torch.int64, device=self.dev)
-        self.count = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self.dev = prog.ds.device
         cache_off, wave_bytes, _, total = lds_layout(prog, 0, UNROLL, BLOCK // 64)
-        d = pack(prog, D.M_MASK, 0, 0, 0, 0, 0, 0, 0, self.mask.data_ptr(), self.count.data_ptr(), [], [],
-                 unroll=UNROLL, cache_off=cache_off, wave_bytes=wave_bytes)
+        self._layout = (cache_off, wave_bytes)
         self.lds_total = total
-        self.desc = torch.from_numpy(d.view(np.uint8).copy()).to(self.dev)
         self.jit = _jit_for(prog, D.M_MASK, False, 2048) if not prog.empty else None
-        self.grid = _grid(self.dev, int(d[0]["total_chunks"]), self.jit.lay.total if self.jit else total)
+        self._slot_lock = threading.Lock()
+        self._slots = {}
+        self._bufs()
+
+    def _bufs(self):
+        from .scheduler import current_slot
+
+        slot = current_slot()
+        b = self._slots.get(slot)
+        if b is None:
+            with self._slot_lock:
+                b = self._slots.get(slot)
+                if b is None:
+                    prog = self.prog
+                    mask = torch.zeros(prog.ds.nwords, dtype=torch.int64, device=self.dev)
+                    count = torch.zeros(1, dtype=torch.int64, device=self.dev)
+                    d = pack(prog, D.M_MASK, 0, 0, 0, 0, 0, 0, 0, mask.data_ptr(), count.data_ptr(), [], [],
+                             unroll=UNROLL, cache_off=self._layout[0], wave_bytes=self._layout[1])
+                    desc = torch.from_numpy(d.view(np.uint8).copy()).to(self.dev)
+                    self.grid = _grid(self.dev, int(d[0]["total_chunks"]),
+                                      self.jit.lay.total if self.jit else self.lds_total)
+                    b = self._slots[slot] = (mask, count, desc)
+        return b
 
     def run(self) -> torch.Tensor:
         """Row ids passing the filter (sorted)."""
         if self.prog.empty:
             return torch.zeros(0, dtype=torch.int64, device=self.dev)
-        self.mask.zero_()
-        self.count.zero_()
+        mask, count, desc = self._bufs()
+        mask.zero_()
+        count.zero_()
         if self.jit is not None:
-            self.jit.launch(self.desc, self.grid)
+            self.jit.launch(desc, self.grid)
         else:
-            native.scan(self.desc, self.grid, BLOCK, self.lds_total, UNROLL)
-        nzw = torch.nonzero(self.mask).flatten()
-        if nzw.numel() == 0:
-            return nzw
-        words = self.mask.index_select(0, nzw)
-        bits = (words.unsqueeze(1) >> torch.arange(64, device=self.dev)) & 1
-        r, c = torch.nonzero(bits, as_tuple=True)
-        return nzw[r] * 64 + c
+            native.scan(desc, self.grid, BLOCK, self.lds_total, UNROLL)
+        return native.compact_rows(mask)
 
 
 def _grid(dev: torch.device, total_chunks: int, lds_total: int) -> int:

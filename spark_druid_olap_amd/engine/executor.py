@@ -164,6 +164,10 @@ class PreparedQuery:
         return run_reference(prog)
 
     def _merged(self, prog, prep) -> Partials:
+        if not self.world.distributed:
+            from ..utils.cancel import checkpoint
+
+            checkpoint()
         part = self._scan(prog, prep)
         disjoint = bool(self.ds.shard_key) and any(k.col == self.ds.shard_key for k in prog.keys)
         return merge_partials(self.world, prog, part, disjoint_keys=disjoint)
@@ -194,13 +198,19 @@ class PreparedQuery:
     def run_partials(self, t0: float):
         """scan -> merge across ranks -> device HAVING / top-K pruning; (prog, merged partials,
         scan end time).  The partials stay on the device (nested queries consume them there)."""
+        from ..utils.cancel import checkpoint
+
         _, prog, prep = self.scans[0]
         err = None
         try:
             with T.span("sdo.scan"):
+                checkpoint()  # inside the merge's failure agreement: every rank aborts together
                 part = self._scan(prog, prep)
                 if len(self.scans) > 1:
-                    parts = [part] + [self._scan(p_, q_) for _, p_, q_ in self.scans[1:]]
+                    parts = [part]
+                    for _, p_, q_ in self.scans[1:]:
+                        checkpoint()  # between segment batches
+                        parts.append(self._scan(p_, q_))
                     part = combine_local(prog, parts)
             if self.window is not None:
                 part = self.window.to_global(part)
@@ -300,12 +310,19 @@ class PreparedQuery:
             part = part.compact()
             if part.rows <= max(4 * limit, 4096):
                 return part
-        col = part.acc[:, agg.slot]
-        v = col.view(torch.float64) if agg.kind == "sum_f" else col.to(torch.float64)
-        key = v if desc else -v
-        key = torch.nan_to_num(key, nan=-math.inf)  # NaN sorts last either way
-        kth = torch.topk(key, limit, sorted=False).values.min()
-        keep = torch.nonzero(key >= kth).flatten()
+        if part.acc.is_cuda and self.engine.use_native:
+            # device radix select (ops/csrc/post_scan.hip topk_*): keeps every group in or above the
+            # k-th best key's 48-bit bucket -- a superset of the top k, no host round trip
+            from ..ops import native
+
+            keep = native.topk_keep(part.acc.contiguous(), agg.slot, agg.kind == "sum_f", desc, limit)
+        else:
+            col = part.acc[:, agg.slot]
+            v = col.view(torch.float64) if agg.kind == "sum_f" else col.to(torch.float64)
+            key = v if desc else -v
+            key = torch.nan_to_num(key, nan=-math.inf)  # NaN sorts last either way
+            kth = torch.topk(key, limit, sorted=False).values.min()
+            keep = torch.nonzero(key >= kth).flatten()
         return Partials("sparse", part.acc.index_select(0, keep), part.keys.index_select(0, keep),
                         [h.index_select(0, keep) for h in part.hll])
 
@@ -752,6 +769,17 @@ class Engine:
         if use_native is None:
             use_native = torch.cuda.is_available()
         self.use_native = use_native
+        self._coalescer = None
+
+    def coalescer(self, slots: Optional[int] = None):
+        """The engine's stream scheduler + identical-statement batching (engine/scheduler.py),
+        created on first use with ``slots`` HIP streams (``SDO_STREAMS``, default 4)."""
+        if self._coalescer is None:
+            from .scheduler import Coalescer, StreamScheduler
+
+            n = slots or int(os.environ.get("SDO_STREAMS", "4"))
+            self._coalescer = Coalescer(StreamScheduler(n, self.world.device()))
+        return self._coalescer
 
     def prepare(self, qs: S.QuerySpec, ds: DataSource, segments_per_query: Optional[int] = None) -> PreparedQuery:
         """``segments_per_query`` set = historical execution (``sd/DruidRDD.scala:62-84, 244-277``):

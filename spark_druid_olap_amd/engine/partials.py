@@ -27,7 +27,12 @@ class Partials:
         """dense -> sparse keeping groups with a non-zero presence count (slot 0)."""
         if self.kind == "sparse":
             return self
-        idx = torch.nonzero(self.acc[:, 0] > 0).flatten()
+        if self.acc.is_cuda:
+            from ..ops import native
+
+            idx = native.nonzero_rows(self.acc[:, 0])  # ballot mask + compact_rows kernels
+        else:
+            idx = torch.nonzero(self.acc[:, 0] > 0).flatten()
         return Partials("sparse", self.acc.index_select(0, idx), idx, [h.index_select(0, idx) for h in self.hll])
 
 

@@ -20,6 +20,16 @@ __global__ void bitmap_build_kernel(const void* ids, int dtype, int64_t n, int64
                                     int64_t card);
 __global__ void hll_estimate_kernel(const uint32_t* regs, int64_t G, int p, double* est);
 __global__ void glds_probe_kernel(const unsigned char* src, uint32_t* out);
+// post_scan.hip
+__global__ void compact_count_kernel(const uint64_t* mask, int64_t nwords, int* block_counts);
+__global__ void compact_offsets_kernel(const int* block_counts, int64_t nblocks, int64_t* offsets, int64_t* total);
+__global__ void compact_write_kernel(const uint64_t* mask, int64_t nwords, const int64_t* offsets, int64_t* rows);
+__global__ void topk_hist_kernel(const int64_t* acc, int64_t n, int nslots, int slot, int is_f64, int desc,
+                                 const uint64_t* state, int level, unsigned int* hist);
+__global__ void topk_pick_kernel(unsigned int* hist, uint64_t* state, int level);
+__global__ void nonzero_mask_kernel(const unsigned char* base, int esize, int64_t n, int64_t stride, uint64_t* words);
+__global__ void topk_keep_kernel(const int64_t* acc, int64_t n, int nslots, int slot, int is_f64, int desc,
+                                 const uint64_t* state, uint64_t* keep);
 }  // namespace sdo
 
 namespace py = pybind11;
@@ -65,6 +75,61 @@ static void hll_estimate(uint64_t regs, int64_t G, int p, uint64_t est, uint64_t
   hipLaunchKernelGGL(sdo::hll_estimate_kernel, dim3(blocks), dim3(1024), 0, (hipStream_t)stream,
                      (const uint32_t*)regs, G, p, (double*)est);
   check(hipGetLastError(), "hll_estimate_kernel launch");
+}
+
+// ---------------------------------------------------------------------------------------------
+// Row compaction (post_scan.hip): mask words -> sorted row ids.  65536 rows (1024 words) per block.
+static int64_t compact_blocks(int64_t nwords) { return (nwords + 1023) / 1024; }
+
+static void compact_count(uint64_t mask, int64_t nwords, uint64_t block_counts, uint64_t offsets, uint64_t total,
+                          uint64_t stream) {
+  const int64_t nb = compact_blocks(nwords);
+  if (nb <= 0) return;
+  if (nb > (int64_t)1 << 31) throw std::invalid_argument("mask too large");
+  hipLaunchKernelGGL(sdo::compact_count_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream,
+                     (const uint64_t*)mask, nwords, (int*)block_counts);
+  check(hipGetLastError(), "compact_count_kernel launch");
+  hipLaunchKernelGGL(sdo::compact_offsets_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream,
+                     (const int*)block_counts, nb, (int64_t*)offsets, (int64_t*)total);
+  check(hipGetLastError(), "compact_offsets_kernel launch");
+}
+
+static void compact_write(uint64_t mask, int64_t nwords, uint64_t offsets, uint64_t rows, uint64_t stream) {
+  const int64_t nb = compact_blocks(nwords);
+  if (nb <= 0) return;
+  hipLaunchKernelGGL(sdo::compact_write_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream,
+                     (const uint64_t*)mask, nwords, (const int64_t*)offsets, (int64_t*)rows);
+  check(hipGetLastError(), "compact_write_kernel launch");
+}
+
+static void nonzero_mask(uint64_t base, int esize, int64_t n, int64_t stride, uint64_t words, uint64_t stream) {
+  if (n <= 0) return;
+  if (esize != 1 && esize != 8) throw std::invalid_argument("esize must be 1 or 8");
+  int64_t nwords = (n + 63) / 64;
+  int64_t blocks = (nwords + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(sdo::nonzero_mask_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     (const unsigned char*)base, esize, n, stride, (uint64_t*)words);
+  check(hipGetLastError(), "nonzero_mask_kernel launch");
+}
+
+// Top-k threshold (post_scan.hip): 4 radix levels of histogram + pick, then the keep bitmask.
+// state: 3 x uint64 {prefix, k, all} initialised to {0, k, 0}; hist: 4096 x uint32 zeroed.
+static void topk_keep(uint64_t acc, int64_t n, int nslots, int slot, int is_f64, int desc, uint64_t state,
+                      uint64_t hist, uint64_t keep, int grid, uint64_t stream) {
+  if (n <= 0) return;
+  if (slot < 0 || slot >= nslots) throw std::invalid_argument("bad slot");
+  hipStream_t s = (hipStream_t)stream;
+  for (int level = 0; level < 4; ++level) {  // TK_LEVELS
+    hipLaunchKernelGGL(sdo::topk_hist_kernel, dim3(grid), dim3(512), 0, s, (const int64_t*)acc, n, nslots, slot, is_f64,
+                       desc, (const uint64_t*)state, level, (unsigned int*)hist);
+    check(hipGetLastError(), "topk_hist_kernel launch");
+    hipLaunchKernelGGL(sdo::topk_pick_kernel, dim3(1), dim3(1024), 0, s, (unsigned int*)hist, (uint64_t*)state, level);
+    check(hipGetLastError(), "topk_pick_kernel launch");
+  }
+  hipLaunchKernelGGL(sdo::topk_keep_kernel, dim3(grid), dim3(256), 0, s, (const int64_t*)acc, n, nslots, slot, is_f64,
+                     desc, (const uint64_t*)state, (uint64_t*)keep);
+  check(hipGetLastError(), "topk_keep_kernel launch");
 }
 
 // Returns 4 when 1/2-byte LDS-DMA elements land one dword per lane, 1 when packed (lane*size).
@@ -192,6 +257,10 @@ PYBIND11_MODULE(_sdo_native, m) {
         py::arg("block"), py::arg("lds"), py::arg("unroll"), py::arg("stream"));
   m.def("bitmap_build", &bitmap_build);
   m.def("hll_estimate", &hll_estimate);
+  m.def("compact_count", &compact_count);
+  m.def("compact_write", &compact_write);
+  m.def("topk_keep", &topk_keep);
+  m.def("nonzero_mask", &nonzero_mask);
   m.def("desc_size", &desc_size);
   m.def("rtc_compile", &rtc_compile);
   m.def("module_load", [](py::bytes code, const std::string& name) { return module_load(std::string(code), name); });

@@ -1,0 +1,236 @@
+// Post-scan kernels for CDNA4 (gfx950): row compaction for Select/scan queries and threshold
+// (top-k) selection over merged partial aggregates.
+//
+// Reference behaviour these implement:
+//  * compact_rows -- the Select query's filtered-row cursor (SelectSpecWithIntervals + PagingSpec,
+//    sd/DruidQuerySpec.scala:977-1070; paging loop asd/DruidSelectResultIterator.scala:116-137):
+//    the scan kernel writes one 64-bit mask word per 64 rows; this turns the mask into sorted row ids
+//    with one popcount pass, one workgroup-level scan of the per-block counts and one scatter pass.
+//  * topk_* -- TopN / ORDER BY metric LIMIT k (TopNQuerySpec, sd/DruidQuerySpec.scala:767-822;
+//    LimitSpec 437-456): a 4-level radix select (4 x 12 high bits of the order-preserving key) that
+//    finds the 48-bit bucket of the k-th best value of a metric slot on the device without a host round
+//    trip; every group whose key ties or beats that bucket is kept (a superset of the top k, exact
+//    after the host's final order + limit).
+//
+// Wave64 everywhere: per-wave prefix sums use __shfl_up over 64 lanes, and block-level scans combine
+// the (blockDim/64) wave totals through LDS.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sdo {
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t = __shfl_up(v, d, 64);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
+
+// Exclusive scan of one int per thread across a block of up to 1024 threads.  Returns the
+// thread's exclusive prefix; *total receives the block total.
+__device__ __forceinline__ int block_excl_scan(int v, int* lds_waves, int* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  const int incl = wave_incl_scan(v);
+  if (lane == 63) lds_waves[wave] = incl;
+  __syncthreads();
+  if (wave == 0) {
+    int w = lane < nw ? lds_waves[lane] : 0;
+    const int wi = wave_incl_scan(w);
+    if (lane < nw) lds_waves[lane] = wi - w;
+    if (lane == nw - 1) lds_waves[32] = wi;
+  }
+  __syncthreads();
+  const int out = lds_waves[wave] + incl - v;
+  *total = lds_waves[32];
+  __syncthreads();
+  return out;
+}
+
+constexpr int CW_THREADS = 256;   // threads per compaction block
+constexpr int CW_WORDS = 4;       // mask words per thread -> 1024 words (65536 rows) per block
+
+// Pass 1: set rows per block.
+__global__ void __launch_bounds__(CW_THREADS) compact_count_kernel(const uint64_t* __restrict__ mask, int64_t nwords,
+                                                                  int* __restrict__ block_counts) {
+  __shared__ int lds[40];
+  const int64_t w0 = ((int64_t)blockIdx.x * CW_THREADS + threadIdx.x) * CW_WORDS;
+  int c = 0;
+#pragma unroll
+  for (int i = 0; i < CW_WORDS; ++i)
+    if (w0 + i < nwords) c += __popcll(mask[w0 + i]);
+  int total;
+  block_excl_scan(c, lds, &total);
+  if (threadIdx.x == 0) block_counts[blockIdx.x] = total;
+}
+
+// Pass 2 (one workgroup): exclusive scan of the per-block counts -> int64 block offsets + total.
+__global__ void __launch_bounds__(1024) compact_offsets_kernel(const int* __restrict__ block_counts, int64_t nblocks,
+                                                              int64_t* __restrict__ offsets, int64_t* __restrict__ total) {
+  __shared__ int lds[40];
+  __shared__ int64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < nblocks; base += blockDim.x) {
+    const int64_t i = base + threadIdx.x;
+    const int v = i < nblocks ? block_counts[i] : 0;
+    int tot;
+    const int ex = block_excl_scan(v, lds, &tot);
+    if (i < nblocks) offsets[i] = carry + ex;
+    __syncthreads();
+    if (threadIdx.x == 0) carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
+// Pass 3: every set bit writes its row id at (block offset + prefix within the block).
+__global__ void __launch_bounds__(CW_THREADS) compact_write_kernel(const uint64_t* __restrict__ mask, int64_t nwords,
+                                                                  const int64_t* __restrict__ offsets,
+                                                                  int64_t* __restrict__ rows) {
+  __shared__ int lds[40];
+  const int64_t w0 = ((int64_t)blockIdx.x * CW_THREADS + threadIdx.x) * CW_WORDS;
+  uint64_t w[CW_WORDS];
+  int c = 0;
+#pragma unroll
+  for (int i = 0; i < CW_WORDS; ++i) {
+    w[i] = (w0 + i < nwords) ? mask[w0 + i] : 0ull;
+    c += __popcll(w[i]);
+  }
+  int total;
+  int64_t pos = offsets[blockIdx.x] + block_excl_scan(c, lds, &total);
+#pragma unroll
+  for (int i = 0; i < CW_WORDS; ++i) {
+    uint64_t m = w[i];
+    const int64_t rbase = (w0 + i) << 6;
+    while (m) {
+      const int b = __ffsll((unsigned long long)m) - 1;
+      rows[pos++] = rbase + b;
+      m &= m - 1;
+    }
+  }
+}
+
+// Presence bitmask of a strided column (element i = base[i * stride] != 0; 1- or 8-byte elements):
+// the "which groups exist" test of a dense accumulator table (slot 0 = row count) or of the
+// one-byte existence table, as one ballot word per 64 groups for compact_rows.
+__global__ void __launch_bounds__(256) nonzero_mask_kernel(const unsigned char* __restrict__ base, int esize,
+                                                          int64_t n, int64_t stride, uint64_t* __restrict__ words) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwords = (n + 63) >> 6;
+  const int64_t wstride = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t w = (((int64_t)blockIdx.x * blockDim.x) >> 6) + (threadIdx.x >> 6); w < nwords; w += wstride) {
+    const int64_t i = (w << 6) + lane;
+    bool nz = false;
+    if (i < n) {
+      nz = esize == 8 ? ((const int64_t*)base)[i * stride] != 0 : base[i * stride] != 0;
+    }
+    const uint64_t b = __ballot(nz);
+    if (lane == 0) words[w] = b;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// top-k threshold over one accumulator slot of the merged partials ([rows, nslots] int64).
+// The slot is mapped to an order-preserving unsigned key (larger = better) on the fly: f64 sums by
+// their IEEE bits, integer slots by flipping the sign bit; ascending order inverts the key.
+constexpr int TK_BITS = 12, TK_BINS = 1 << TK_BITS, TK_THREADS = 512, TK_LEVELS = 4;
+
+__device__ __forceinline__ uint64_t ord_key(int64_t raw, int is_f64, int desc) {
+  uint64_t u = (uint64_t)raw;
+  if (is_f64) {
+    u = (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+  } else {
+    u ^= 0x8000000000000000ull;
+  }
+  return desc ? u : ~u;
+}
+
+// Histogram of key bits [shift, shift+12) over the keys whose higher (12*level) bits equal the
+// prefix chosen so far (state[0]).
+__global__ void __launch_bounds__(TK_THREADS) topk_hist_kernel(const int64_t* __restrict__ acc, int64_t n, int nslots,
+                                                              int slot, int is_f64, int desc,
+                                                              const uint64_t* __restrict__ state, int level,
+                                                              unsigned int* __restrict__ hist) {
+  __shared__ unsigned int h[TK_BINS];
+  for (int i = threadIdx.x; i < TK_BINS; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const int shift = 64 - TK_BITS * (level + 1);
+  const uint64_t prefix = level ? state[0] : 0ull;
+  const int pshift = 64 - TK_BITS * level;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t k = ord_key(acc[i * nslots + slot], is_f64, desc);
+    if (level == 0 || (k >> pshift) == prefix) atomicAdd(&h[(k >> shift) & (TK_BINS - 1)], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < TK_BINS; i += blockDim.x)
+    if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// One workgroup of TK_BINS/4 threads: walk the histogram from the top bin down until the k-th key
+// is covered; extend the prefix with that bin and make k relative to it.  state = {prefix, k}.
+__global__ void __launch_bounds__(TK_BINS / 4) topk_pick_kernel(unsigned int* __restrict__ hist,
+                                                               uint64_t* __restrict__ state, int level) {
+  __shared__ int lds[40];
+  __shared__ int pick;
+  __shared__ int64_t knew;
+  const int t = threadIdx.x;
+  const int owner = (TK_BINS / 4) - 1 - t;  // thread 0 owns the 4 highest bins
+  unsigned int c[4];
+  int s = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    c[j] = hist[owner * 4 + (3 - j)];
+    s += (int)c[j];
+  }
+  int total;
+  const int above = block_excl_scan(s, lds, &total);
+  const int64_t k = (int64_t)state[1];
+  if (t == 0) {
+    pick = -1;
+    knew = k;
+  }
+  __syncthreads();
+  int64_t run = above;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (run < k && run + (int64_t)c[j] >= k) {
+      pick = owner * 4 + (3 - j);
+      knew = k - run;
+    }
+    run += (int64_t)c[j];
+  }
+  __syncthreads();
+  if (t == 0) {
+    const uint64_t b = pick < 0 ? 0ull : (uint64_t)pick;  // fewer than k keys: keep everything
+    state[0] = (level == 0 ? 0ull : (state[0] << TK_BITS)) | b;
+    state[1] = (uint64_t)knew;
+    if (pick < 0) state[2] = 1;
+  }
+  for (int i = t; i < TK_BINS; i += blockDim.x) hist[i] = 0;
+}
+
+// keep bit per row: its key's top 12*TK_LEVELS bits >= the chosen prefix (every row that ties or
+// beats the k-th best); one 64-bit word per 64 rows via a wave ballot, compacted by compact_rows.
+__global__ void __launch_bounds__(256) topk_keep_kernel(const int64_t* __restrict__ acc, int64_t n, int nslots, int slot,
+                                                       int is_f64, int desc, const uint64_t* __restrict__ state,
+                                                       uint64_t* __restrict__ keep) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwords = (n + 63) >> 6;
+  const int64_t wstride = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int shift = 64 - TK_BITS * TK_LEVELS;
+  const uint64_t prefix = state[0];
+  const bool all = state[2] != 0;
+  for (int64_t w = (((int64_t)blockIdx.x * blockDim.x) >> 6) + (threadIdx.x >> 6); w < nwords; w += wstride) {
+    const int64_t i = (w << 6) + lane;
+    bool k = false;
+    if (i < n) k = all || (ord_key(acc[i * nslots + slot], is_f64, desc) >> shift) >= prefix;
+    const uint64_t b = __ballot(k);
+    if (lane == 0) keep[w] = b;
+  }
+}
+
+}  // namespace sdo

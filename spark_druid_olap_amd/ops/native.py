@@ -92,3 +92,57 @@ def hll_estimate(regs: torch.Tensor, G: int, p: int, est: torch.Tensor) -> None:
 
 def device_info(dev: int = 0) -> dict:
     return load().device_info(dev)
+
+
+def compact_rows(mask: torch.Tensor) -> torch.Tensor:
+    """Row ids (int64, ascending) of the set bits of a [nwords] int64 mask (post_scan.hip
+    compact_*: popcount per 65536-row block, one-workgroup offset scan, scatter).  Temporaries are
+    O(nwords / 1024); the output is exactly the selected rows."""
+    m = load()
+    assert mask.dtype == torch.int64 and mask.is_contiguous() and mask.is_cuda
+    nw = mask.numel()
+    dev = mask.device
+    nb = (nw + 1023) // 1024
+    if nb == 0:
+        return torch.zeros(0, dtype=torch.int64, device=dev)
+    counts = torch.empty(nb, dtype=torch.int32, device=dev)
+    offs = torch.empty(nb, dtype=torch.int64, device=dev)
+    total = torch.empty(1, dtype=torch.int64, device=dev)
+    st = _stream(dev)
+    m.compact_count(mask.data_ptr(), nw, counts.data_ptr(), offs.data_ptr(), total.data_ptr(), st)
+    n = int(total.item())
+    rows = torch.empty(n, dtype=torch.int64, device=dev)
+    if n:
+        m.compact_write(mask.data_ptr(), nw, offs.data_ptr(), rows.data_ptr(), st)
+    return rows
+
+
+def topk_keep(acc: torch.Tensor, slot: int, is_f64: bool, desc: bool, k: int) -> torch.Tensor:
+    """Indices (ascending) of the rows of ``acc`` [R, nslots] int64 whose slot value ties or beats
+    the bucket of the k-th best (post_scan.hip topk_*: 4-level 12-bit radix select, no host
+    round trip until the final compaction): a superset of the top k, exact after an order+limit."""
+    m = load()
+    assert acc.dtype == torch.int64 and acc.is_contiguous() and acc.dim() == 2 and acc.is_cuda
+    R, ns = acc.shape
+    dev = acc.device
+    state = torch.tensor([0, int(k), 0], dtype=torch.int64, device=dev)
+    hist = torch.zeros(4096, dtype=torch.int32, device=dev)
+    keep = torch.empty((R + 63) // 64, dtype=torch.int64, device=dev)
+    grid = int(max(1, min(2048, (R + 4095) // 4096)))
+    m.topk_keep(acc.data_ptr(), R, ns, int(slot), int(bool(is_f64)), int(bool(desc)), state.data_ptr(),
+                hist.data_ptr(), keep.data_ptr(), grid, _stream(dev))
+    return compact_rows(keep)
+
+
+def nonzero_rows(col: torch.Tensor) -> torch.Tensor:
+    """Indices (int64, ascending) of the non-zero elements of a 1-D (possibly strided) int64 or
+    uint8 device tensor: ballot mask (post_scan.hip nonzero_mask) + compact_rows.  Replaces
+    ``torch.nonzero`` for group-existence compaction of dense accumulator tables."""
+    m = load()
+    assert col.dim() == 1 and col.is_cuda and col.dtype in (torch.int64, torch.uint8)
+    n = col.numel()
+    if n == 0:
+        return torch.zeros(0, dtype=torch.int64, device=col.device)
+    words = torch.empty((n + 63) // 64, dtype=torch.int64, device=col.device)
+    m.nonzero_mask(col.data_ptr(), col.element_size(), n, col.stride(0), words.data_ptr(), _stream(col.device))
+    return compact_rows(words)

@@ -122,7 +122,7 @@ class DruidHTTPServer:
         self.host = host
         self.port = port
         self.lock = threading.Lock()
-        self.running: Dict[str, float] = {}
+        self.running: Dict[str, Any] = {}  # queryId -> CancelToken of the running query
         self.cancelled: set = set()
         self._srv: Optional[ThreadingHTTPServer] = None
         from ..segment.ingest import Overlord
@@ -142,13 +142,23 @@ class DruidHTTPServer:
         if qt == "segmentMetadata":
             return segment_metadata(ds)
         spec = S.query_from_json(body)
-        qid = (body.get("context") or {}).get("queryId") or uuid.uuid4().hex
-        self.running[qid] = time.time()
+        ctx = body.get("context") or {}
+        qid = ctx.get("queryId") or uuid.uuid4().hex
+        from ..utils.cancel import CancelToken, scope
+
+        # Druid's context timeout (ms); DELETE /druid/v2/{queryId} cancels the token of a running
+        # query, which the engine honours at its next stage boundary (before each scan / batch)
+        token = CancelToken(float(ctx["timeout"]) if ctx.get("timeout") else None)
+        with self.lock:
+            self.running[qid] = token
+            if qid in self.cancelled:
+                self.cancelled.discard(qid)
+                token.cancel(f"query {qid} cancelled")
         try:
-            with self.lock:
-                if qid in self.cancelled:
-                    raise RuntimeError(f"query {qid} cancelled")
-                res = self.session.engine.execute(spec, ds)
+            with scope(token):
+                token.check()
+                res = self.session.engine.coalescer().run(None, lambda: self.session.engine.execute(spec, ds)) \
+                    if not self.session.engine.world.distributed else self.session.engine.execute(spec, ds)
             if self.session.conf.typed("spark.sparklinedata.enable.druid.query.history"):
                 self.session.history.record(spec, res.stats.get("exec_ms", 0.0), res.stats.get("exec_ms", 0.0),
                                             res.num_rows, "http", None)
@@ -170,7 +180,12 @@ class DruidHTTPServer:
             if method == "POST" and len(parts) == 2:
                 return 200, self.query(json.loads(body or b"{}"))
             if method == "DELETE" and len(parts) == 3:
-                self.cancelled.add(parts[2])
+                with self.lock:
+                    tok = self.running.get(parts[2])
+                    if tok is not None:
+                        tok.cancel(f"query {parts[2]} cancelled")
+                    else:  # not started yet: cancel it on arrival
+                        self.cancelled.add(parts[2])
                 return 202, {}
             if method == "GET" and len(parts) >= 3 and parts[2] == "datasources":
                 if len(parts) == 3:

@@ -7,9 +7,13 @@ first byte.  Statements run through the SQL front-end, so Druid rewrites, the ``
 ``EXPLAIN DRUID REWRITE`` and ``ON DRUIDDATASOURCE ... EXECUTE QUERY`` all work remotely.  Results
 go back as column-based ``TRowSet`` pages (protocol V8).
 
-One GPU engine serves all client sessions: statements are executed one at a time per process
-(each is a fused GPU scan of a few ms) while connections, result paging and metadata calls are
-concurrent.  Query history records the SQL text of every Druid query (the ``HS2Listener``).
+Every client session gets its own ``Session`` view (``Session.new_session``: own ``SET`` conf,
+current database and temporary views; shared tables, datasources and cached plans).  On one GPU,
+statements from different sessions execute concurrently on K HIP-stream slots with per-slot device
+buffers, and identical queued statements run once (``engine/scheduler.py``).  With several ranks
+(one per GPU) rank 0 serves the clients and broadcasts every statement to the other ranks, which
+execute it over their shards (``server/spmd.py``).  Query history records the SQL text of every
+Druid query (the ``HS2Listener``).
 """
 from __future__ import annotations
 
@@ -65,14 +69,19 @@ class Operation:
 
 
 class HiveThriftServer:
-    def __init__(self, session, host: str = "127.0.0.1", port: int = 10000, auth: str = "auto"):
+    def __init__(self, session, host: str = "127.0.0.1", port: int = 10000, auth: str = "auto", world=None):
         self.session = session
         self.host = host
         self.port = port
         self.auth = auth
         self.sessions: Dict[bytes, Dict[str, Any]] = {}
         self.ops: Dict[bytes, Operation] = {}
-        self.exec_lock = threading.Lock()
+        self.world = world if world is not None else session.engine.world
+        self.spmd = None
+        if self.world.distributed:
+            from .spmd import SpmdDispatcher
+
+            self.spmd = SpmdDispatcher(session, self.world)
         self._srv: Optional[socketserver.ThreadingTCPServer] = None
         self._thread: Optional[threading.Thread] = None
 
@@ -100,6 +109,8 @@ class HiveThriftServer:
             self._srv.shutdown()
             self._srv.server_close()
             self._srv = None
+        if self.spmd is not None:
+            self.spmd.shutdown()
 
     def serve_forever(self):
         self.start()
@@ -177,23 +188,31 @@ class HiveThriftServer:
 
     def rpc_OpenSession(self, req):
         sid = uuid.uuid4().bytes
-        self.sessions[sid] = {"user": req.get("username"), "conf": dict(req.get("configuration") or {}),
-                              "opened": time.time()}
+        conf, db = {}, None
         for k, v in (req.get("configuration") or {}).items():
             if k.startswith("set:hiveconf:") or k.startswith("set:hivevar:"):
-                self.session.conf.set(k.split(":", 2)[2], v)
-            elif k == "use:database":
-                try:
-                    self.session.catalog.use(v)
-                except Exception:  # noqa: BLE001
-                    pass
+                conf[k.split(":", 2)[2]] = v
+            elif k == "use:database" and v.lower() in self.session.catalog.dbs:
+                db = v
+        if self.spmd is not None:
+            self.spmd.open_session(sid, conf, db)
+            sess = self.spmd.session(sid)
+        else:
+            sess = self.session.new_session()
+            for k, v in conf.items():
+                sess.conf.set(k, v)
+            if db:
+                sess.catalog.use(db)
+        self.sessions[sid] = {"user": req.get("username"), "conf": dict(req.get("configuration") or {}),
+                              "opened": time.time(), "session": sess}
         proto = min(int(req.get("client_protocol", T.PROTOCOL_V8)), T.PROTOCOL_V8)
         return {"status": _ok(), "serverProtocolVersion": proto,
                 "sessionHandle": {"sessionId": {"guid": sid, "secret": uuid.uuid4().bytes}}, "configuration": {}}
 
     def rpc_CloseSession(self, req):
         sid = _sid(req)
-        self.sessions.pop(sid, None)
+        if self.sessions.pop(sid, None) is not None and self.spmd is not None:
+            self.spmd.close_session(sid)
         for oid in [k for k, o in self.ops.items() if o.session_id == sid]:
             self.ops.pop(oid, None)
         return {"status": _ok()}
@@ -228,15 +247,29 @@ class HiveThriftServer:
     def _run(self, op: Operation, stmt: str, overlay: Dict[str, str]):
         op.state = T.OP_RUNNING
         try:
-            with self.exec_lock:
-                if op.cancelled.is_set():
-                    op.state = T.OP_CANCELED
-                    return
+            if op.cancelled.is_set():
+                op.state = T.OP_CANCELED
+                return
+            stmt = stmt.strip().rstrip(";")
+            if self.spmd is not None:
+                tmo = None
+                if op.token.deadline is not None:
+                    tmo = max(0.001, op.token.deadline - time.monotonic())
+                df, pdf = self.spmd.execute(op.session_id, stmt, overlay, tmo)
+            else:
+                sess = self.sessions[op.session_id]["session"]
                 for k, v in overlay.items():
-                    self.session.conf.set(k, v)
-                df = self.session.sql(stmt.strip().rstrip(";"))
-                pdf = df.to_pandas(token=op.token)
-            # row-set encoding (host only) runs outside the engine lock, overlapping the next query
+                    sess.conf.set(k, v)
+                df = sess.sql(stmt)
+                if df.plan is None:  # a command: already executed by sql()
+                    pdf = df.to_pandas()
+                else:
+                    # a stream slot per execution; identical queued statements (same cached plan,
+                    # i.e. same text + conf + database) execute once
+                    co = sess.engine.coalescer()
+                    key = id(df) if sess.conf.typed("spark.sparklinedata.druid.planCache.enabled") else None
+                    pdf = co.run(key, lambda: df.to_pandas(token=op.token))
+            # row-set encoding (host only) runs after the slot is released
             op.set_frame(df.columns, [t for _, t in df.schema], pdf)
             op.state = T.OP_FINISHED if not op.cancelled.is_set() else T.OP_CANCELED
         except Exception as e:  # noqa: BLE001
@@ -511,30 +544,46 @@ class _Tee:
 
 
 def main(argv=None):
-    """``python -m spark_druid_olap_amd.server.hive_server --port 10000 [--tpch-sf 1]``
-    (the ``start-sparklinedatathriftserver.sh`` entry, scripts/start-sparklinedatathriftserver.sh)."""
+    """``python -m spark_druid_olap_amd.server.hive_server --port 10000 [--tpch-sf 1] [--gpus N]``
+    (the ``start-sparklinedatathriftserver.sh`` entry, scripts/start-sparklinedatathriftserver.sh).
+
+    ``--gpus N`` (without torchrun): starts N rank processes, one per GPU; every rank holds
+    ``--tpch-sf`` of synthetic TPC-H as its shard, rank 0 serves the clients and the others execute
+    the broadcast statement stream (server/spmd.py)."""
     import argparse
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=int(os.environ.get("SDO_THRIFT_PORT", "10000")))
-    ap.add_argument("--tpch-sf", type=float, default=0.0, help="preload a synthetic TPC-H datasource")
+    ap.add_argument("--tpch-sf", type=float, default=0.0, help="preload a synthetic TPC-H datasource (per rank)")
     ap.add_argument("--init-sql", default=None, help="file of ';'-separated statements to run at startup")
     ap.add_argument("--ui-port", type=int, default=int(os.environ.get("SDO_UI_PORT", "4040")),
                     help="Druid HTTP API + 'Druid Query Details' page (0 = any free port, -1 = off)")
     ap.add_argument("--conf", action="append", default=[], help="key=value session conf (repeatable)")
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU) to start when not under torchrun")
+    ap.add_argument("--port-file", default=None, help="write the bound Thrift port here (rank 0)")
     a = ap.parse_args(argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        import sys
+
+        from ..utils.launch import spawn_ranks
+
+        sys.exit(spawn_ranks(a.gpus, [sys.executable, "-m", "spark_druid_olap_amd.server.hive_server"] +
+                             list(argv if argv is not None else sys.argv[1:]), quiet_peers=False))
     logging.basicConfig(level=logging.INFO)
     import torch
 
+    from ..parallel.world import init_world
     from ..session import Session
 
-    sess = Session(conf=dict(kv.split("=", 1) for kv in a.conf))
+    world = init_world()
+    dev = world.device()
+    sess = Session(conf=dict(kv.split("=", 1) for kv in a.conf), world=world)
     if a.tpch_sf > 0:
         from ..models import tpch
 
-        dev = "cuda" if torch.cuda.is_available() else "cpu"
-        ds = tpch.to_datasource(tpch.generate_flat(a.tpch_sf, dev), profile="bench")
+        ds = tpch.to_datasource(tpch.generate_flat(a.tpch_sf, dev, rank=world.rank, world=world.size),
+                                profile="bench")
         sess.register_datasource(ds)
         sess.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)
         sess.sql(tpch.druid_ddl(with_column_mapping=False))
@@ -543,7 +592,14 @@ def main(argv=None):
             for st in f.read().split(";"):
                 if st.strip():
                     sess.sql(st)
-    if a.ui_port >= 0:
+    if world.rank != 0:
+        from ..parallel.world import shutdown
+        from .spmd import serve_peer
+
+        serve_peer(sess, world)
+        shutdown()
+        return
+    if a.ui_port >= 0 and not world.distributed:
         # the reference attaches its "Druid Query Details" UI tab next to the Thrift server
         # (HiveThriftServer2.scala:73-77); here the same process also serves the Druid HTTP API
         from .druid_http import DruidHTTPServer
@@ -551,7 +607,25 @@ def main(argv=None):
         ui = DruidHTTPServer(sess, a.host, a.ui_port).start()
         logging.getLogger("sdo.thrift").info("query history page: http://%s:%d/sparklinedata/druid/queries",
                                              a.host, ui.port)
-    HiveThriftServer(sess, a.host, a.port).serve_forever()
+    srv = HiveThriftServer(sess, a.host, a.port, world=world).start()
+    if a.port_file:
+        with open(a.port_file + ".tmp", "w") as f:
+            f.write(str(srv.port))
+        os.replace(a.port_file + ".tmp", a.port_file)
+    import signal
+
+    stop = threading.Event()
+    signal.signal(signal.SIGTERM, lambda *_: stop.set())
+    try:
+        while not stop.wait(1.0):
+            pass
+    except KeyboardInterrupt:
+        pass
+    srv.stop()
+    if world.distributed:
+        from ..parallel.world import shutdown
+
+        shutdown()
 
 
 if __name__ == "__main__":

@@ -78,9 +78,12 @@ class DataFrame:
                 from .utils.cancel import CancelToken
 
                 token = CancelToken(tmo)
+        from .utils.cancel import scope
+
         ex = Executor(self.session, token)
         t0 = time.perf_counter()
-        b = self.session._with_sql(self.sql_text, lambda: ex.run(self.plan))
+        with scope(token):
+            b = self.session._with_sql(self.sql_text, lambda: ex.run(self.plan))
         self.last_stats = {"ms": (time.perf_counter() - t0) * 1e3, "druid": ex.druid_stats}
         return b
 
@@ -154,6 +157,25 @@ class Session:
         self.discovery = None
         if self.conf.get("spark.sparklinedata.druid.discovery", "true") not in ("false", False):
             self.attach_discovery(self.conf.get("spark.sparklinedata.druid.zkHost", "localhost"))
+
+    def new_session(self) -> "Session":
+        """A client session over the same engine, tables and datasources with its own ``SET``
+        configuration, current database, temporary views and plan cache (Spark's
+        ``SparkSession.newSession``; one per HiveServer2 client session)."""
+        s = Session.__new__(Session)
+        s.engine = self.engine
+        s.conf = self.conf.copy()
+        s.catalog = self.catalog.session_view()
+        s.history = self.history
+        # plans (and their prepared GPU queries and per-slot device buffers) are shared by every
+        # session whose statement text, conf, current database and temp views match (the cache key)
+        s._plan_cache = self._plan_cache
+        s._lock = self._lock
+        s._tl = threading.local()
+        s.modules = self.modules
+        s.discovery = self.discovery
+        s.parent = self
+        return s
 
     def attach_discovery(self, druid_host: str = "localhost", druid_path: str = "/druid",
                          qualify_names: bool = False):
@@ -238,7 +260,8 @@ class Session:
 
     def _query(self, text: str, st) -> DataFrame:
         cache_on = bool(self.conf.typed("spark.sparklinedata.druid.planCache.enabled"))
-        key = (text, self.catalog.version, self.catalog.cluster.generation, json.dumps(self.conf.items(), sort_keys=True))
+        key = (text, self.catalog.version, self.catalog.current_db, id(self.catalog.temp) if self.catalog.temp else 0,
+               self.catalog.cluster.generation, json.dumps(self.conf.items(), sort_keys=True))
         if cache_on:
             hit = self._plan_cache.get(key)
             if hit is not None:
@@ -306,10 +329,13 @@ class Session:
 
         prep = getattr(dq, "_prepared", None)
         if prep is None or getattr(dq, "_prepared_spec", None) is not spec:
-            with T.span("sdo.lower"):
-                prep = self.engine.prepare(run_spec, ds, dq.info.get("historical"))
-            dq._prepared = prep
-            dq._prepared_spec = spec
+            with self._lock:  # concurrent sessions share cached plans: prepare once
+                prep = getattr(dq, "_prepared", None)
+                if prep is None or getattr(dq, "_prepared_spec", None) is not spec:
+                    with T.span("sdo.lower"):
+                        prep = self.engine.prepare(run_spec, ds, dq.info.get("historical"))
+                    dq._prepared = prep
+                    dq._prepared_spec = spec
         with T.span(f"sdo.druid.{spec.queryType}"):
             res = prep.run()
         if isinstance(spec, S.TimeSeriesQuerySpec) and res.num_rows == 0:

@@ -49,13 +49,16 @@ class Executor:
     def __init__(self, session, token=None):
         self.session = session
         self.token = token
+        # host-side checks between operators only on one rank: across ranks the engine's pre-scan
+        # checkpoint (agreed inside the merge collective) is the only place a query may stop
+        self._host_checks = token is not None and not session.engine.world.distributed
         self.druid_stats: List[dict] = []
         self._subq_cache: Dict[int, object] = {}
         self._druid_results: Dict[str, object] = {}
 
     # ----------------------------------------------------------------------------------------
     def run(self, plan: P.Plan) -> Batch:
-        if self.token is not None:
+        if self._host_checks:
             self.token.check()
         m = getattr(self, "_" + type(plan).__name__, None)
         if m is None:
@@ -215,7 +218,7 @@ class Executor:
 
     def _DruidQuery(self, p: P.DruidQuery) -> Batch:
         t0 = time.perf_counter()
-        if self.token is not None:
+        if self._host_checks:
             self.token.check()
         deferred = getattr(p, "_deferred", None)
         if deferred is None:

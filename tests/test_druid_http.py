@@ -82,3 +82,46 @@ def test_query_history_page(ds_small):
         assert len(js) == 1 and js[0]["numRows"] == 4
     finally:
         h.stop()
+
+
+def test_delete_cancels_a_running_query(srv, monkeypatch):
+    """DELETE /druid/v2/{queryId} aborts a query that is already executing: the engine stops at
+    its next stage boundary (here: between the segment batches of a historical-style query)."""
+    import threading
+    import time as _t
+    import urllib.request
+
+    from spark_druid_olap_amd.engine import executor as X
+
+    started = threading.Event()
+    real = X.PreparedQuery._scan
+
+    def slow_scan(self, prog, prep):
+        started.set()
+        _t.sleep(0.3)
+        return real(self, prog, prep)
+    monkeypatch.setattr(X.PreparedQuery, "_scan", slow_scan)
+    # many segment batches -> many scans with a checkpoint before each
+    monkeypatch.setattr(srv.session.engine, "execute",
+                        lambda spec, ds, nseg=None, _e=srv.session.engine: _e.prepare(spec, ds, 1).run())
+    q = {"queryType": "timeseries", "dataSource": "tpch", "granularity": "all",
+         "intervals": ["1992-01-01/1999-01-01"], "aggregations": [{"type": "count", "name": "c"}],
+         "context": {"queryId": "cancel-me"}}
+    out = {}
+
+    def run():
+        c = DruidQueryServerClient("127.0.0.1", srv.port)
+        t0 = _t.time()
+        try:
+            out["r"] = c.execute_query(q)
+        except DruidDataSourceException as e:
+            out["err"] = str(e)
+        out["s"] = _t.time() - t0
+    th = threading.Thread(target=run)
+    th.start()
+    assert started.wait(30)
+    req = urllib.request.Request(f"http://127.0.0.1:{srv.port}/druid/v2/cancel-me", method="DELETE")
+    urllib.request.urlopen(req).read()
+    th.join(60)
+    assert "err" in out and "cancel" in out["err"].lower(), out
+    assert out["s"] < 10  # far less than scanning every monthly segment batch at 0.3 s each

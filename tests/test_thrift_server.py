@@ -81,3 +81,106 @@ def test_concurrent_clients(server):
     for t in ts:
         t.join(120)
     assert not errs, errs
+
+
+def test_sessions_do_not_share_set_or_use(server):
+    """Per-client session state (Session.new_session): SET and USE in one client session are not
+    seen by another; tables stay shared."""
+    srv_sess = server.session
+    srv_sess.sql("create database if not exists other_db")
+    with connect(port=server.port) as a, connect(port=server.port) as b:
+        a.cursor().execute("set spark.sparklinedata.druid.selectquery.pagesize=17")
+        a.cursor().execute("use other_db")
+        got_a = a.cursor().execute("set spark.sparklinedata.druid.selectquery.pagesize").fetchall()
+        got_b = b.cursor().execute("set spark.sparklinedata.druid.selectquery.pagesize").fetchall()
+        assert got_a[0][1] == "17" and got_b[0][1] != "17"
+        # b still resolves unqualified names in `default`; a needs the qualified name now
+        assert b.cursor().execute("select count(*) from orderLineItemPartSupplier").fetchall()[0][0] > 0
+        with pytest.raises(HiveError):
+            a.cursor().execute("select count(*) from orderLineItemPartSupplier")
+        assert a.cursor().execute("select count(*) from default.orderLineItemPartSupplier").fetchall()[0][0] > 0
+    assert srv_sess.catalog.current_db == "default"
+    assert srv_sess.conf.get("spark.sparklinedata.druid.selectquery.pagesize") != "17"
+
+
+def test_identical_queued_statements_execute_once():
+    """engine/scheduler.py: with one stream slot busy, identical statements that queue up together
+    run once and every waiter gets the result."""
+    import time as _t
+
+    from spark_druid_olap_amd.engine.scheduler import Coalescer, StreamScheduler
+
+    co = Coalescer(StreamScheduler(1))
+    calls = []
+    gate = threading.Event()
+
+    def slow():
+        calls.append(1)
+        gate.wait(5)
+        return len(calls)
+
+    blocker = threading.Thread(target=lambda: co.run("other", slow))
+    blocker.start()
+    _t.sleep(0.1)  # the only slot is now held
+    outs = []
+    ts = [threading.Thread(target=lambda: outs.append(co.run("q", lambda: (calls.append(2), "r")[1])))
+          for _ in range(5)]
+    for t in ts:
+        t.start()
+    _t.sleep(0.2)
+    gate.set()
+    for t in ts + [blocker]:
+        t.join(10)
+    assert outs == ["r"] * 5
+    assert calls.count(2) == 1 and co.stats["coalesced"] == 4
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_server_returns_merged_answer(tmp_path):
+    """HiveServer2 over all ranks (server/spmd.py): ``--gpus 2`` starts two ranks (gloo on CPU),
+    each holding its own TPC-H shard; a client of rank 0 gets the answer over the union of both
+    shards, and SET in its session travels to the peer."""
+    import os
+    import signal
+    import subprocess
+    import sys
+    import time as _t
+
+    import pandas as pd
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pf = tmp_path / "port"
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(OMP_NUM_THREADS="2", PYTHONPATH=root)
+    p = subprocess.Popen([sys.executable, "-m", "spark_druid_olap_amd.server.hive_server", "--gpus", "2",
+                          "--tpch-sf", "0.003", "--port", "0", "--port-file", str(pf), "--ui-port", "-1"],
+                         cwd=root, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+    try:
+        t0 = _t.time()
+        while not pf.exists():
+            assert p.poll() is None, p.stderr.read().decode()[-3000:]
+            assert _t.time() - t0 < 200, "server did not start"
+            _t.sleep(0.2)
+        port = int(pf.read_text())
+        full = pd.concat([tpch.to_pandas(tpch.generate_flat(0.003, "cpu", rank=r, world=2)) for r in range(2)])
+        exp = full.groupby("l_returnflag").agg(c=("l_extendedprice", "size"), s=("l_extendedprice", "sum"))
+        q = ("select l_returnflag, count(*) c, sum(l_extendedprice) s from orderLineItemPartSupplier "
+             "group by l_returnflag order by l_returnflag")
+        with connect(port=port) as c1, connect(port=port) as c2:
+            for c in (c1, c2):
+                rows = c.cursor().execute(q).fetchall()
+                assert [r[0] for r in rows] == list(exp.index)
+                assert [r[1] for r in rows] == list(exp.c)
+                for r, s in zip(rows, exp.s):
+                    assert r[2] == pytest.approx(s)
+            c1.cursor().execute("set spark.sparklinedata.druid.selectquery.pagesize=5")
+            assert c1.cursor().execute("set spark.sparklinedata.druid.selectquery.pagesize").fetchall()[0][1] == "5"
+            n = c2.cursor().execute("select count(distinct o_orderkey) from orderLineItemPartSupplier").fetchall()
+            assert n[0][0] == full.o_orderkey.nunique()
+    finally:
+        p.send_signal(signal.SIGTERM)
+        try:
+            p.wait(60)
+        except subprocess.TimeoutExpired:
+            p.kill()
+    assert p.returncode == 0, p.stderr.read().decode()[-3000:]

@@ -37,7 +37,7 @@ def main():
         torch.cuda.synchronize()
         for _ in range(args.iters):
             prep._reset()
-            prep._launch()  # the specialized (JIT) kernel when one was built, else the interpreter
+            prep._launch(prep._bufs())  # the specialized (JIT) kernel when one was built, else the interpreter
         torch.cuda.synchronize()
         print("done", name, flush=True)
 

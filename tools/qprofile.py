@@ -56,7 +56,7 @@ def run_all(eng, ds, args):
             ev[0].record()
             prep._reset()
             ev[1].record()
-            prep._launch()
+            prep._launch(prep._bufs())
             ev[2].record()
             torch.cuda.synchronize()
             tr.append(ev[0].elapsed_time(ev[1]))
