@@ -35,9 +35,15 @@ def _relations(session) -> pd.DataFrame:
                                        "columnMapping", "functionalDeps", "starSchema", "options", "numRows"])
 
 
-def _servers(session) -> pd.DataFrame:
+SEGMENT_COLS = ["druidHost", "druidDataSource", "interval", "version", "binaryVersion", "size",
+                "identifier", "shardSpec", "numRows"]
+
+
+def _local_inventory(session) -> dict:
+    """This rank's server record + segment list (the coordinator's ``servers?full=true`` entry for
+    one historical, ``sd/client/DruidClient.scala:488-492``)."""
     w = session.engine.world
-    rows = []
+    host = f"gpu:{w.rank}"
     info = {}
     try:
         from ..ops import native
@@ -45,25 +51,35 @@ def _servers(session) -> pd.DataFrame:
         info = native.device_info() if session.engine.use_native else {}
     except Exception:
         info = {}
-    for r in range(w.size):
-        rows.append({"druidHost": f"gpu:{r}", "host": f"rank{r}", "maxSize": int(info.get("total_mem", 0)),
-                     "serverType": "historical", "tier": "_default_tier", "priority": 0,
-                     "numSegments": sum(len(ds.segments) for ds in session.catalog.cluster.datasources.values()),
-                     "currSize": int(sum(ds.size_bytes() for ds in session.catalog.cluster.datasources.values()))})
-    return pd.DataFrame(rows)
+    dss = session.catalog.cluster.datasources
+    segs = []
+    for name, ds in dss.items():
+        row_bytes = max(1, ds.size_bytes() // max(ds.num_rows, 1))
+        for s in ds.segments:
+            segs.append({"druidHost": host, "druidDataSource": name,
+                         "interval": s.identifier.split("_")[0], "version": s.version, "binaryVersion": "sdo-1",
+                         "size": int((s.row_hi - s.row_lo) * row_bytes),
+                         "identifier": s.identifier, "shardSpec": json.dumps({"partitionNum": s.partition}),
+                         "numRows": int(s.row_hi - s.row_lo)})
+    server = {"druidHost": host, "host": f"rank{w.rank}", "maxSize": int(info.get("totalGlobalMem", 0)),
+              "serverType": "historical", "tier": "_default_tier", "priority": 0,
+              "numSegments": len(segs), "currSize": int(sum(ds.size_bytes() for ds in dss.values()))}
+    return {"server": server, "segments": segs}
+
+
+def cluster_inventory(session) -> List[dict]:
+    """Every rank's inventory, in rank order.  Collective when the world is distributed: view
+    queries run SPMD like every other statement (server/spmd.py), so all ranks reach it together."""
+    return session.engine.world.all_gather_object(_local_inventory(session))
+
+
+def _servers(session) -> pd.DataFrame:
+    return pd.DataFrame([inv["server"] for inv in cluster_inventory(session)])
 
 
 def _segments(session) -> pd.DataFrame:
-    rows = []
-    for name, ds in session.catalog.cluster.datasources.items():
-        for s in ds.segments:
-            rows.append({"druidHost": f"gpu:{session.engine.world.rank}", "druidDataSource": name,
-                         "interval": s.identifier.split("_")[0], "version": s.version, "binaryVersion": "sdo-1",
-                         "size": int((s.row_hi - s.row_lo) * max(1, ds.size_bytes() // max(ds.num_rows, 1))),
-                         "identifier": s.identifier, "shardSpec": json.dumps({"partitionNum": s.partition}),
-                         "numRows": int(s.row_hi - s.row_lo)})
-    return pd.DataFrame(rows, columns=["druidHost", "druidDataSource", "interval", "version", "binaryVersion", "size",
-                                       "identifier", "shardSpec", "numRows"])
+    rows = [s for inv in cluster_inventory(session) for s in inv["segments"]]
+    return pd.DataFrame(rows, columns=SEGMENT_COLS)
 
 
 def _assignments(session) -> pd.DataFrame:

@@ -135,6 +135,14 @@ class World:
         dist.broadcast_object_list(lst, src=src, group=self.group)
         return lst[0]
 
+    def all_gather_object(self, obj: Any) -> List[Any]:
+        """Small host metadata from every rank (catalog views, segment inventories)."""
+        if not self.distributed:
+            return [obj]
+        out: List[Any] = [None] * self.size
+        dist.all_gather_object(out, obj, group=self.group)
+        return out
+
     def max_float(self, x: float) -> float:
         if not self.distributed:
             return x

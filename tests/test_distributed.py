@@ -71,8 +71,12 @@ def _worker(rank, world, port, outdir, env=None):
         d = s.sql(q)
         assert d.druid_queries(), q
         res[q] = d.collect()
+    # metadata views are cluster-wide on every rank (segment -> GPU assignment of all shards)
+    servers = s.sql("select druidHost, numSegments from `d$druidservers`").collect()
+    assigns = s.sql("select druidHost, count(*) from `d$druidserverassignments` group by druidHost").collect()
+    views = {"servers": servers, "assign": assigns, "nseg_local": len(ds.segments)}
     with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
-        pickle.dump({"res": res, "df": df}, f)
+        pickle.dump({"res": res, "df": df, "views": views}, f)
     w.barrier()
     shutdown()
 
@@ -129,6 +133,10 @@ def test_multi_rank_sql_equals_union(world, env):
                         assert x == pytest.approx(y, rel=1e-9, abs=0.02), (q, a, b)
                     else:
                         assert x == y, (q, a, b)
+    nseg = {f"gpu:{r}": o["views"]["nseg_local"] for r, o in enumerate(outs)}
+    for o in outs:
+        assert {h: n for h, n in o["views"]["servers"]} == nseg
+        assert {h: n for h, n in o["views"]["assign"]} == nseg
     exact = dict(s.sql("select l_returnflag, count(distinct o_orderkey) from base group by l_returnflag").collect())
     for k, v in outs[0]["res"][APPROX]:
         assert v == pytest.approx(exact[k], rel=0.08)

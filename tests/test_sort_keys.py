@@ -1,0 +1,46 @@
+"""Host sort of dictionary-coded (Categorical) string keys: the code fast path in
+``sql/execute.py:sort_indices`` must order exactly like the same values as plain object strings,
+for ASC/DESC and both null placements (Spark default: NULLS FIRST for ASC, NULLS LAST for DESC)."""
+import itertools
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from spark_druid_olap_amd.sql.execute import sort_indices
+
+
+def _categorical(values, has_null):
+    """Built like ``_dict_series``: sorted unique categories, code -1 for the null entry."""
+    cats = pd.Index(sorted({v for v in values if v is not None}), dtype=object)
+    codes = np.array([-1 if v is None else cats.get_loc(v) for v in values], dtype=np.int32)
+    if not has_null:
+        assert (codes >= 0).all()
+    return pd.Series(pd.Categorical.from_codes(codes, categories=cats, validate=False))
+
+
+@pytest.mark.parametrize("has_null,asc,nulls_first",
+                         list(itertools.product([False, True], [True, False], [None, True, False])))
+def test_categorical_sort_matches_object_sort(has_null, asc, nulls_first):
+    rng = np.random.default_rng(7)
+    pool = ["ASIA", "EUROPE", "AFRICA", "AMERICA", "MIDDLE EAST", "b", "B", "aa"]
+    vals = [pool[i] for i in rng.integers(0, len(pool), 200)]
+    if has_null:
+        for i in rng.integers(0, 200, 25):
+            vals[i] = None
+    other = pd.Series(rng.integers(0, 5, 200))
+    cat = _categorical(vals, has_null)
+    assert isinstance(cat.dtype, pd.CategoricalDtype)
+    obj = pd.Series(np.array(vals, dtype=object))
+    # two keys: the string key first, then a tie-breaker, so stability + ordering both show
+    got = sort_indices([(cat, asc, nulls_first), (other, True, None)], 200)
+    exp = sort_indices([(obj, asc, nulls_first), (other, True, None)], 200)
+    assert np.array_equal(got, exp)
+    # and against an independent oracle for the leading key
+    nf = asc if nulls_first is None else nulls_first
+    lead = [vals[i] for i in got]
+    nn = [v for v in lead if v is not None]
+    assert nn == sorted(nn, reverse=not asc)
+    if has_null:
+        k = sum(v is None for v in lead)
+        assert all(v is None for v in (lead[:k] if nf else lead[-k:]))
