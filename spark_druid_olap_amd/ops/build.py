@@ -89,6 +89,42 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     return target
 
 
+# ------------------------------------------------------------------ native HiveServer2 gateway
+# Host-only C++ (sockets, threads, Thrift binary protocol): built with g++, no HIP toolchain needed.
+GW_SRC = HERE.parent / "server" / "csrc" / "hs2_gateway.cpp"
+
+
+def gateway_path() -> Path:
+    return HERE.parent / "server" / ("_sdo_gateway" + _ext_suffix())
+
+
+def _gateway_hash() -> str:
+    return hashlib.sha256(GW_SRC.read_bytes()).hexdigest()[:16]
+
+
+def build_gateway(force: bool = False, verbose: bool = False, extra_flags=()) -> Path:
+    target = gateway_path()
+    stamp = target.parent / "_sdo_gateway.stamp"
+    if not force and not extra_flags and target.exists() and stamp.exists() and \
+            stamp.read_text().strip() == _gateway_hash():
+        return target
+    import pybind11
+
+    cxx = os.environ.get("CXX", "g++")
+    tmp = target.with_suffix(".tmp.so")
+    cmd = [cxx, "-O2", "-std=c++17", "-shared", "-fPIC", "-Wall", "-Wextra", *extra_flags,
+           f"-I{sysconfig.get_paths()['include']}", f"-I{pybind11.get_include()}", str(GW_SRC), "-o", str(tmp),
+           "-lpthread"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, target)
+    if not extra_flags:
+        stamp.write_text(_gateway_hash())
+    return target
+
+
 if __name__ == "__main__":
     p = build(force="--force" in sys.argv, verbose=True)
     print(p)
+    print(build_gateway(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,245 @@
+"""HiveServer2 endpoint with the native gateway (``server/csrc/hs2_gateway.cpp``) in front.
+
+``NativeHiveServer`` is a ``HiveThriftServer`` whose connections are served by the C++ gateway:
+per-statement work (socket I/O, SASL, Thrift decoding/encoding, identical-statement batching,
+status polls and result paging) never takes the GIL.  What remains in Python scales with the number
+of *executions*:
+
+* ``K`` executor threads pull batches from the gateway (``next_batch`` waits with the GIL released),
+  run the statement on the leader's session inside a HIP-stream slot lease (engine/scheduler.py) --
+  or through the SPMD dispatcher when several ranks serve (server/spmd.py) -- and hand the typed
+  columns back once (``finish_batch``); the gateway slices pages for every attached operation;
+* every RPC the gateway does not handle natively (OpenSession / CloseSession, commands such as
+  SET / USE / CREATE, metadata calls, statements with a confOverlay or a timeout, operations the
+  Python side owns) arrives here as raw message bytes and runs through the inherited ``rpc_*``
+  methods;
+* after anything that can change a session's planning context (open, SET, USE, temp views) the
+  session's context token is re-published, so only statements that would plan identically batch.
+
+The pure-Python server stays available (``SDO_NATIVE_GATEWAY=0`` or when the extension is absent on
+a CPU-only checkout) and is the reference the native one is tested against (tests/test_gateway.py).
+"""
+from __future__ import annotations
+
+import importlib
+import json
+import logging
+import os
+import threading
+import time
+from typing import List, Optional, Tuple
+
+import numpy as np
+import pandas as pd
+
+from . import thrift as T
+from .hive_server import HiveThriftServer, Operation
+
+log = logging.getLogger("sdo.gateway")
+
+
+def load_native():
+    """The compiled gateway module (built in-tree by ops/build.py:build_gateway)."""
+    try:
+        return importlib.import_module("spark_druid_olap_amd.server._sdo_gateway")
+    except ImportError:
+        from ..ops import build as B
+
+        B.build_gateway()
+        return importlib.import_module("spark_druid_olap_amd.server._sdo_gateway")
+
+
+def context_token(sess) -> int:
+    """Everything per-session that changes how a statement plans (the plan cache key minus the
+    statement text and the shared catalog state)."""
+    cat = sess.catalog
+    key = (cat.current_db, id(cat.temp) if cat.temp else 0, json.dumps(sess.conf.items(), sort_keys=True))
+    return hash(key) & 0x7FFFFFFFFFFFFFFF
+
+
+# column kinds understood by the gateway's TRowSet encoder
+_KIND = {"boolean": (0, np.uint8), "tinyint": (1, np.int8), "smallint": (2, np.int16), "int": (3, np.int32),
+         "bigint": (4, np.int64), "double": (5, np.float64), "float": (5, np.float64), "decimal": (5, np.float64)}
+
+
+def encode_columns(types: List[str], df: pd.DataFrame) -> List[Tuple[int, bytes, bytes, bytes]]:
+    """Typed columns for the gateway: (kind, little-endian values | utf-8 blob, int64 offsets for
+    strings, one null byte per row).  Same value rendering as the Python server (_tcolumn)."""
+    out = []
+    for i, t in enumerate(types):
+        s = df.iloc[:, i]
+        base = t.split("(")[0]
+        isna = s.isna().to_numpy(dtype=bool) if len(s) else np.zeros(0, dtype=bool)
+        nulls = isna.astype(np.uint8).tobytes()
+        if base in _KIND:
+            kind, dt = _KIND[base]
+            if base == "boolean":
+                vals = np.array([bool(v) if not n else False for v, n in zip(s.tolist(), isna)], dtype=np.uint8)
+            else:
+                num = pd.to_numeric(s, errors="coerce")
+                if kind == 5:
+                    vals = num.to_numpy(dtype=np.float64, na_value=0.0)
+                else:
+                    vals = num.fillna(0).to_numpy().astype(dt)
+            out.append((kind, np.ascontiguousarray(vals, dtype=dt).tobytes(), b"", nulls))
+            continue
+        strs = []
+        for v, n in zip(s.tolist(), isna):
+            if n:
+                strs.append(b"")
+            elif isinstance(v, pd.Timestamp):
+                strs.append((v.strftime("%Y-%m-%d") if base == "date" else str(v)).encode())
+            else:
+                strs.append(str(v).encode())
+        lens = np.fromiter((len(x) for x in strs), dtype=np.int64, count=len(strs))
+        offs = np.zeros(len(strs) + 1, dtype=np.int64)
+        np.cumsum(lens, out=offs[1:])
+        out.append((6, b"".join(strs), offs.tobytes(), nulls))
+    return out
+
+
+def encode_schema(names: List[str], types: List[str]) -> bytes:
+    """A complete TTableSchema struct (the gateway splices it into GetResultSetMetadata)."""
+    cols = []
+    for i, (n, t) in enumerate(zip(names, types)):
+        tid = T.TYPE_IDS.get(t.split("(")[0], T.TYPE_IDS["string"])
+        cols.append({"columnName": n, "typeDesc": {"types": [{"primitiveEntry": {"type": tid}}]}, "position": i + 1})
+    w = T.Writer()
+    w.struct("TTableSchema", {"columns": cols})
+    return bytes(w.buf)
+
+
+class _BatchToken:
+    """Cancellation for a batch: set once every operation attached to it was cancelled/closed."""
+
+    def __init__(self, gw, bid):
+        from ..utils.cancel import CancelToken
+
+        self._gw, self._bid = gw, bid
+        self._tok = CancelToken()
+        self.deadline = None
+        self.reason = "cancelled by client"
+
+    @property
+    def cancelled(self) -> bool:
+        return self._gw.is_cancelled(self._bid)
+
+    def cancel(self, reason: str = "cancelled") -> None:
+        self._tok.cancel(reason)
+
+    def check(self) -> None:
+        from ..utils.errors import QueryCancelled
+
+        if self._tok.cancelled or self._gw.is_cancelled(self._bid):
+            raise QueryCancelled(self.reason)
+
+
+class NativeHiveServer(HiveThriftServer):
+    def __init__(self, session, host: str = "127.0.0.1", port: int = 10000, auth: str = "auto", world=None,
+                 executors: Optional[int] = None):
+        super().__init__(session, host, port, auth, world)
+        self.nexec = executors or int(os.environ.get("SDO_GATEWAY_EXECUTORS", "0")) or \
+            (int(os.environ.get("SDO_STREAMS", "4")) + 2)
+        self._gw = None
+        self._stop = threading.Event()
+        self._threads: List[threading.Thread] = []
+
+    # ------------------------------------------------------------------ lifecycle
+    def start(self) -> "NativeHiveServer":
+        mod = load_native()
+        self._gw = mod.Gateway(self.host, self.port, self._forward)
+        self.port = self._gw.start()
+        for i in range(self.nexec):
+            t = threading.Thread(target=self._executor, daemon=True, name=f"hs2-exec-{i}")
+            t.start()
+            self._threads.append(t)
+        log.info("HiveServer2 endpoint (native gateway) on %s:%d, %d executors", self.host, self.port, self.nexec)
+        return self
+
+    def stop(self):
+        self._stop.set()
+        if self._gw is not None:
+            self._gw.stop()
+        for t in self._threads:
+            t.join(5)
+        if self.spmd is not None:
+            self.spmd.shutdown()
+
+    def stats(self) -> dict:
+        return dict(self._gw.stats()) if self._gw is not None else {}
+
+    # ------------------------------------------------------------------ forwarded RPCs
+    def _forward(self, msg: bytes) -> bytes:
+        return self._dispatch(msg)
+
+    def _publish(self, sid: bytes) -> None:
+        ent = self.sessions.get(sid)
+        if ent is not None and self._gw is not None:
+            self._gw.set_context(sid, context_token(ent["session"]))
+
+    def rpc_OpenSession(self, req):
+        r = super().rpc_OpenSession(req)
+        self._publish(r["sessionHandle"]["sessionId"]["guid"])
+        return r
+
+    def rpc_CloseSession(self, req):
+        sid = req["sessionHandle"]["sessionId"]["guid"]
+        if self._gw is not None:
+            self._gw.drop_context(sid)
+        return super().rpc_CloseSession(req)
+
+    def _run(self, op: Operation, stmt: str, overlay):
+        try:
+            super()._run(op, stmt, overlay)
+        finally:
+            self._publish(op.session_id)  # SET / USE / CREATE TEMPORARY VIEW may have changed it
+
+    # ------------------------------------------------------------------ batch executors
+    def _executor(self):
+        gw = self._gw
+        while not self._stop.is_set():
+            b = gw.next_batch(0.25)
+            if b is None:
+                continue
+            bid, sid, stmt = b
+            try:
+                names, types, pdf = self._execute(bid, sid, stmt)
+                schema = encode_schema(names, types)
+                cols = encode_columns(types, pdf)
+                gw.finish_batch(bid, schema, cols, len(pdf), None)
+            except Exception as e:  # noqa: BLE001  (every attached operation reports it)
+                log.debug("batch %d failed: %s", bid, e)
+                try:
+                    gw.finish_batch(bid, b"", [], 0, f"{type(e).__name__}: {e}")
+                except Exception:  # pragma: no cover
+                    log.exception("finish_batch failed")
+
+    def _execute(self, bid: int, sid: bytes, stmt: str):
+        ent = self.sessions.get(sid)
+        if ent is None:
+            raise RuntimeError("invalid session")
+        token = _BatchToken(self._gw, bid)
+        if self.spmd is not None:
+            df, pdf = self.spmd.execute(sid, stmt, {}, None)
+            return list(df.columns), [t for _, t in df.schema], pdf
+        sess = ent["session"]
+        df = sess.sql(stmt)
+        if df.plan is None:  # a command that looked like a query: already executed
+            pdf = df.to_pandas()
+        else:
+            with sess.engine.coalescer().scheduler.lease():
+                pdf = df.to_pandas(token=token)
+        return list(df.columns), [t for _, t in df.schema], pdf
+
+
+def make_server(session, host: str = "127.0.0.1", port: int = 10000, world=None, native: Optional[bool] = None):
+    """The native-gateway server when its extension builds/loads (default), else the Python one."""
+    if native is None:
+        native = os.environ.get("SDO_NATIVE_GATEWAY", "1") != "0"
+    if native:
+        try:
+            load_native()
+            return NativeHiveServer(session, host, port, world=world)
+        except Exception as e:  # noqa: BLE001
+            log.warning("native gateway unavailable (%s); using the Python server", e)
+    return HiveThriftServer(session, host, port, world=world)

@@ -607,7 +607,9 @@ def main(argv=None):
         ui = DruidHTTPServer(sess, a.host, a.ui_port).start()
         logging.getLogger("sdo.thrift").info("query history page: http://%s:%d/sparklinedata/druid/queries",
                                              a.host, ui.port)
-    srv = HiveThriftServer(sess, a.host, a.port, world=world).start()
+    from .gateway import make_server
+
+    srv = make_server(sess, a.host, a.port, world=world).start()  # native gateway unless SDO_NATIVE_GATEWAY=0
     if a.port_file:
         with open(a.port_file + ".tmp", "w") as f:
             f.write(str(srv.port))

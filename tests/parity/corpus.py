@@ -3,10 +3,9 @@ import math
 import os
 import re
 
-REF = "/root/reference/src/test/resources"
-
-
-def build_session(sf=0.01):
+def build_session(sf=0.01, device="cpu", use_native=False):
+    """Every table the reference's test suites query (TPC-H flat + star, select/datatype variants,
+    zip codes).  ``device="cuda"`` + ``use_native=True`` runs the same corpus through the HIP engine."""
     import json
 
     from spark_druid_olap_amd.engine.executor import Engine
@@ -14,10 +13,10 @@ def build_session(sf=0.01):
     from spark_druid_olap_amd.segment.ingest import ingest
     from spark_druid_olap_amd.session import Session
 
-    flat = tpch.generate_flat(sf, "cpu")
+    flat = tpch.generate_flat(sf, device)
     ds = tpch.to_datasource(flat, profile="test")
     df = tpch.to_pandas(flat)
-    s = Session(engine=Engine(use_native=False))
+    s = Session(engine=Engine(use_native=use_native))
     s.register_datasource(ds)
     s.register_table("orderLineItemPartSupplierBase", df, schema=tpch.FLAT_SCHEMA)
     s.sql(tpch.druid_ddl())
@@ -47,24 +46,29 @@ def build_session(sf=0.01):
                         ("datatypes2", "orderLineItemPartSupplierDataTypes2Base")):
         tn = f"orderLineItemPartSupplier_{suffix}"
         s.sql(tpch.druid_ddl(table=tn, source=src, star_schema=f'{{"factTable" : "{tn}", "relations" : []}}'))
-    if os.path.exists(f"{REF}/zip_codeAll.json.template"):
-        for tmpl in ("zip_code.json.template", "zip_codeAll.json.template"):
-            s.register_datasource(ingest(f"{REF}/{tmpl}", data_dir=f"{REF}/zipCodes/sample"))
-        s.sql(f"""CREATE TABLE zipCodesBase(record_date string, zip_code string, latitude double, longitude double,
-          city string, state string, county string) USING com.databricks.spark.csv
-          OPTIONS (path "{REF}/zipCodes/sample/zip_codes_states.csv", header "false", delimiter ",")""")
-        for full in (False, True):
-            infos = json.dumps([
-                {"column": "city", **({"druidColumn": "city"} if full else {}), "hllMetric": "unique_city",
-                 "sketchMetric": "city_sketch"},
-                {"column": "latitude", "spatialIndex": {"druidColumn": "coordinates", "spatialPosition": 0,
-                                                        "minValue": -90.0, "maxValue": 90.0}},
-                {"column": "longitude", "spatialIndex": {"druidColumn": "coordinates", "spatialPosition": 1,
-                                                         "minValue": -180.0, "maxValue": 180.0}}])
-            s.sql(f"""CREATE TABLE if not exists {'zipCodesFull' if full else 'zipCodes'} USING org.sparklinedata.druid
-              OPTIONS (sourceDataframe "default.zipCodesBase", timeDimensionColumn "record_date",
-              druidDatasource "{'zipCodesAll' if full else 'zipCodes'}", columnInfos '{infos}',
-              nonAggregateQueryHandling "push_project_and_filters", allowTopNRewrite "true")""")
+    import tempfile
+
+    from parity.zipcodes import index_spec, write_csv
+
+    zdir = tempfile.mkdtemp(prefix="sdo_zip_")
+    zcsv = write_csv(os.path.join(zdir, "zip_codes_states.csv"))
+    for dsn, full in (("zipCodes", False), ("zipCodesAll", True)):
+        s.register_datasource(ingest(index_spec(dsn, full, zdir), device=device))
+    s.sql(f"""CREATE TABLE zipCodesBase(record_date string, zip_code string, latitude double, longitude double,
+      city string, state string, county string) USING com.databricks.spark.csv
+      OPTIONS (path "{zcsv}", header "false", delimiter ",")""")
+    for full in (False, True):
+        infos = json.dumps([
+            {"column": "city", **({"druidColumn": "city"} if full else {}), "hllMetric": "unique_city",
+             "sketchMetric": "city_sketch"},
+            {"column": "latitude", "spatialIndex": {"druidColumn": "coordinates", "spatialPosition": 0,
+                                                    "minValue": -90.0, "maxValue": 90.0}},
+            {"column": "longitude", "spatialIndex": {"druidColumn": "coordinates", "spatialPosition": 1,
+                                                     "minValue": -180.0, "maxValue": 180.0}}])
+        s.sql(f"""CREATE TABLE if not exists {'zipCodesFull' if full else 'zipCodes'} USING org.sparklinedata.druid
+          OPTIONS (sourceDataframe "default.zipCodesBase", timeDimensionColumn "record_date",
+          druidDatasource "{'zipCodesAll' if full else 'zipCodes'}", columnInfos '{infos}',
+          nonAggregateQueryHandling "push_project_and_filters", allowTopNRewrite "true")""")
     return s
 
 

@@ -24,8 +24,6 @@ Known deviations (each one documented, none silently skipped):
   ``druidColumn`` (``DruidRelationColumn.scala:114-224`` maps it to no Druid column), so a
   projection of it cannot be answered from the index.
 """
-import os
-
 import pytest
 
 from parity.corpus import build_session, run_case
@@ -44,9 +42,7 @@ def session():
     return build_session()
 
 
-@pytest.mark.skipif(not CASES, reason="reference checkout not mounted")
-@pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}::{c[1]}::{c[2]}" for c in CASES])
-def test_reference_case(session, case):
+def _check(session, case):
     key = (case[0], case[1])
     status, detail = run_case(session, case)
     if key in SPARK_SEMANTICS:
@@ -62,7 +58,39 @@ def test_reference_case(session, case):
     assert status == "ok", f"{status}: {detail}"
 
 
+@pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}::{c[1]}::{c[2]}" for c in CASES])
+def test_reference_case(session, case):
+    _check(session, case)
+
+
 def test_corpus_size():
-    if not os.path.isdir("/root/reference"):
-        pytest.skip("reference checkout not mounted")
-    assert len(CASES) >= 240
+    # vendored (tests/parity/cases.json): plain-SQL and date-DSL cases of the reference's suites
+    assert len(CASES) >= 280
+    assert sum(c[0] == "StarSchemaTpchQueriesCTest" for c in CASES) >= 6
+    assert sum("dateIsBefore" in c[3] or "dateIsAfter" in c[3] for c in CASES) >= 20
+
+
+@pytest.fixture(scope="module")
+def gpu_session():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    return build_session(device="cuda", use_native=True)
+
+
+@pytest.mark.gpu
+def test_reference_corpus_on_hip_engine(gpu_session):
+    """The whole corpus through the HIP kernels (datasources resident on the GPU, native engine):
+    same plan-shape and base-table checks as the CPU run, one test so the GPU box runs it in one
+    process."""
+    from spark_druid_olap_amd.ops import native
+
+    assert native.available(), "HIP extension not loaded"
+    bad = []
+    for case in CASES:
+        try:
+            _check(gpu_session, case)
+        except AssertionError as e:
+            bad.append(f"{case[0]}::{case[1]}: {str(e)[:160]}")
+    assert not bad, f"{len(bad)} of {len(CASES)} failed:\n" + "\n".join(bad[:20])

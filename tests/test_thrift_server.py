@@ -11,13 +11,20 @@ from spark_druid_olap_amd.server.hive_server import HiveThriftServer
 from spark_druid_olap_amd.session import Session
 
 
-@pytest.fixture(scope="module")
-def server(ds_small, df_small):
+@pytest.fixture(scope="module", params=["python", "native"])
+def server(request, ds_small, df_small):
+    """Every endpoint test runs against the pure-Python server and the native C++ gateway
+    (server/csrc/hs2_gateway.cpp) in front of the same session."""
     s = Session(engine=Engine(use_native=False))
     s.register_datasource(ds_small)
     s.register_table("orderLineItemPartSupplierBase", df_small, schema=tpch.FLAT_SCHEMA)
     s.sql(tpch.druid_ddl(with_column_mapping=False))
-    srv = HiveThriftServer(s, port=0).start()
+    if request.param == "native":
+        from spark_druid_olap_amd.server.gateway import NativeHiveServer
+
+        srv = NativeHiveServer(s, port=0).start()
+    else:
+        srv = HiveThriftServer(s, port=0).start()
     yield srv
     srv.stop()
 
@@ -81,6 +88,65 @@ def test_concurrent_clients(server):
     for t in ts:
         t.join(120)
     assert not errs, errs
+    if hasattr(server, "stats"):
+        st = server.stats()
+        # every statement went through the native path; batches <= statements
+        assert st["statements"] >= 24 and st["batches"] <= st["statements"]
+
+
+def test_native_gateway_batches_identical_waiting_statements(ds_small, df_small):
+    """With every executor busy, identical statements from different sessions that queue together
+    execute once (one batch) and every client gets the full, correct result; a different statement
+    is its own batch."""
+    import time as _t
+
+    from spark_druid_olap_amd.server.gateway import NativeHiveServer
+
+    s = Session(engine=Engine(use_native=False))
+    s.register_datasource(ds_small)
+    s.register_table("orderLineItemPartSupplierBase", df_small, schema=tpch.FLAT_SCHEMA)
+    s.sql(tpch.druid_ddl(with_column_mapping=False))
+    srv = NativeHiveServer(s, port=0, executors=1)
+    gate = threading.Event()
+    real = srv._execute
+
+    def gated(bid, sid, stmt):
+        if "s_region" in stmt:
+            gate.wait(10)
+        return real(bid, sid, stmt)
+
+    srv._execute = gated
+    srv.start()
+    try:
+        q_block = "select s_region, count(*) from orderLineItemPartSupplier group by s_region"
+        q = "select l_returnflag, count(*) from orderLineItemPartSupplier group by l_returnflag order by l_returnflag"
+        exp = [tuple(r) for r in df_small.groupby("l_returnflag").size().reset_index().itertuples(index=False)]
+        outs, errs = [], []
+
+        def run(sql, sink):
+            try:
+                with connect(port=srv.port) as c:
+                    sink.append(c.cursor().execute(sql).fetchall())
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+
+        blocker = threading.Thread(target=run, args=(q_block, []))
+        blocker.start()
+        _t.sleep(0.3)  # the only executor now holds the blocking batch
+        ts = [threading.Thread(target=run, args=(q, outs)) for _ in range(6)]
+        for t in ts:
+            t.start()
+        _t.sleep(0.5)
+        before = srv.stats()
+        gate.set()
+        for t in ts + [blocker]:
+            t.join(60)
+        assert not errs, errs
+        assert len(outs) == 6 and all([tuple(r) for r in o] == exp for o in outs)
+        st = srv.stats()
+        assert before["coalesced"] >= 5 and st["batches"] == 2, (before, st)
+    finally:
+        srv.stop()
 
 
 def test_sessions_do_not_share_set_or_use(server):

@@ -114,6 +114,9 @@ def main():
     ap.add_argument("--qps", type=float, default=200.0, help="aggregate target rate; 0 = closed loop")
     ap.add_argument("--duration", type=float, default=20.0)
     ap.add_argument("--warmup", type=float, default=3.0)
+    ap.add_argument("--server", default="native", choices=["native", "python"],
+                    help="native C++ gateway (server/csrc/hs2_gateway.cpp) or the pure-Python server")
+    ap.add_argument("--sample", default=None, help="write a sampling profile of the server threads here")
     a = ap.parse_args()
     NCLIENTS = a.clients
     nthreads = max(1, a.clients // a.procs)
@@ -139,7 +142,12 @@ def main():
     s.register_datasource(ds)
     s.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)
     s.sql(tpch.druid_ddl(source="orderLineItemPartSupplierBase", datasource="tpch", with_column_mapping=False))
-    srv = HiveThriftServer(s, port=0).start()
+    if a.server == "native":
+        from spark_druid_olap_amd.server.gateway import NativeHiveServer
+
+        srv = NativeHiveServer(s, port=0).start()
+    else:
+        srv = HiveThriftServer(s, port=0).start()
     print(f"[conc] server up on {srv.port}: SF{a.sf:g} {ds.num_rows} rows on {dev} in {time.time() - t0:.1f}s",
           file=sys.stderr, flush=True)
     # warm every query's plan + kernel once through the server
@@ -150,6 +158,31 @@ def main():
     t_start = time.time() + 1.0 + a.warmup
     for _ in ps:
         start_q.put((srv.port, t_start - a.warmup, a.duration + a.warmup, interval))
+    # server-side counters over the measured window: process CPU (GIL-bound if ~1 core), number of
+    # executions vs statements (identical-statement batching), stream-slot waits
+    co = s.engine.coalescer()
+
+    def counters():
+        if a.server == "native":
+            st = srv.stats()
+            return st["coalesced"], st["batches"]
+        return co.stats["coalesced"], co.stats["executions"]
+
+    time.sleep(max(0.0, t_start - time.time()))
+    cpu0 = time.process_time()
+    co0, ex0 = counters()
+    sampler = None
+    if a.sample:
+        from spark_druid_olap_amd.utils.sampler import Sampler
+
+        sampler = Sampler().start()
+    time.sleep(a.duration)
+    if sampler is not None:
+        sampler.stop()
+        with open(a.sample, "w") as f:
+            f.write(sampler.report(60))
+    cpu1 = time.process_time()
+    co1, ex1 = counters()
     res = []
     for _ in ps:
         res.extend(res_q.get())
@@ -168,7 +201,10 @@ def main():
            "achieved_qps": round(len(lat) / span, 2) if span > 0 else None, "queries": len(res),
            "errors": len(errs), "p50_ms": pct(lat, 50), "p90_ms": pct(lat, 90), "p99_ms": pct(lat, 99),
            "max_ms": max(lat) if lat else None, "sf": a.sf, "device": dev, "per_query": per,
-           "first_error": errs[0][4] if errs else None}
+           "first_error": errs[0][4] if errs else None,
+           "server": {"kind": a.server, "cpu_cores": round((cpu1 - cpu0) / a.duration, 2), "executions": ex1 - ex0,
+                      "coalesced": co1 - co0, "slots": co.scheduler.nslots,
+                      "slot_wait_ms_total": round(co.scheduler.stats["wait_ms"], 1)}}
     print(json.dumps(out), flush=True)
 
 
