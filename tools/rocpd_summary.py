@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--tail-ms", type=float, default=0.0,
                     help="only kernels starting in the last T ms of the trace (the timed steps)")
+    ap.add_argument("--timeline-ms", type=float, default=0.0,
+                    help="also print every kernel of the last T ms in order (start offset, duration, gap)")
     a = ap.parse_args()
     con = sqlite3.connect(a.db)
     rows = con.execute("select name, start, end from kernels order by start").fetchall()
@@ -50,6 +52,15 @@ def main():
     for n, (c, t, mn, mx) in sorted(agg.items(), key=lambda kv: -kv[1][1])[: a.top]:
         print(f"{n:110s} {c:6d} {t:11.1f} {t / c:9.1f} {mn:9.1f} {mx:9.1f} {100 * t / max(total, 1e-9):6.2f}")
     print(f"{'TOTAL':110s} {sum(v[0] for v in agg.values()):6d} {total:11.1f}")
+    if a.timeline_ms > 0 and rows:
+        end = max(e for _, _, e in rows)
+        tl = [(n, s, e) for n, s, e in rows if s >= end - int(a.timeline_ms * 1e6)]
+        print(f"--- timeline of the last {a.timeline_ms} ms ({len(tl)} kernels)")
+        prev = None
+        for n, s, e in tl:
+            gap = (s - prev) / 1e3 if prev is not None else 0.0
+            print(f"{(s - tl[0][1]) / 1e3:10.1f} us  dur {(e - s) / 1e3:8.1f}  gap {gap:8.1f}  {short(n)[:90]}")
+            prev = e
     try:
         mc = con.execute("select start, end, size from memory_copies").fetchall()
         if t0 is not None:
