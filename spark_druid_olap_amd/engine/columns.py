@@ -20,7 +20,7 @@ class DictColumn:
 
     def __init__(self, codes: np.ndarray, dictionary):
         codes = np.asarray(codes)
-        self.codes = codes if codes.dtype in (np.int32, np.int64) else codes.astype(np.int64)
+        self.codes = codes if codes.dtype in (np.int16, np.int32, np.int64) else codes.astype(np.int64)
         self.dictionary = dictionary
         self._decoded = None
 

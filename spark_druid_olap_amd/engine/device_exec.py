@@ -29,6 +29,8 @@ LDS_BUDGET = int(os.environ.get("SDO_LDS_BUDGET", 64 * 1024))
 SHARED_LDS_MAX = int(os.environ.get("SDO_SHARED_LDS_MAX", 112 * 1024))
 SHARED_MIN_GROUPS = int(os.environ.get("SDO_SHARED_MIN_GROUPS", 512))
 DENSE_GLOBAL_MAX_BYTES = int(os.environ.get("SDO_DENSE_MAX_BYTES", 1 << 30))
+# dense HBM tables of at least this many groups keep a first-touch byte table (see PreparedScan.run)
+TOUCH_MIN_G = int(os.environ.get("SDO_TOUCH_MIN_G", 1 << 20))
 BLOCK = 512
 UNROLL = int(os.environ.get("SDO_UNROLL", "2"))
 BLOCKS_PER_CU = int(os.environ.get("SDO_BLOCKS_PER_CU", "3"))
@@ -146,6 +148,12 @@ class PreparedScan:
                                getattr(prog, "presence_only", False) and prog.nslots == 1 and not prog.nhll
                                and not prog.empty and not os.environ.get("SDO_NO_PRES_BYTES"))
         prog.presence_bytes = self.pres_bytes
+        # large dense HBM table (TPC-H Q3: 150M order groups, ~1M touched): a first-touch byte per
+        # group written by the scan; compaction reads G bytes instead of G x nslots x 8, and only
+        # the touched rows are re-initialised after the run (no full-table fill per execution)
+        self.touch = bool(USE_JIT and mode == D.M_DENSE_GLOBAL and not self.pres_bytes and not prog.nhll
+                          and not prog.empty and G >= TOUCH_MIN_G and not os.environ.get("SDO_NO_TOUCH"))
+        prog.touch_table = self.touch
         if not prog.empty:
             # the JIT keeps LDS registers one byte each (hll_update8)
             jit_hll_lds = bool(prog.nhll) and mode == D.M_DENSE_LDS and hll_bytes // 4 <= LDS_BUDGET \
@@ -154,6 +162,8 @@ class PreparedScan:
             if self.pres_bytes and self.jit is None:
                 self.pres_bytes = prog.presence_bytes = False
                 self.jit = _jit_for(prog, mode, jit_hll_lds, self.m, self.shared)
+            if self.touch and self.jit is None:
+                self.touch = prog.touch_table = False
             if self.shared and self.jit is None:
                 # the interpreter kernel only knows per-wave copies: accumulate in HBM instead
                 self.mode, self.shared, self.lds = D.M_DENSE_GLOBAL, False, 0
@@ -196,6 +206,8 @@ class PreparedScan:
         b.keys = torch.empty(rows if self.mode == D.M_HASH else 1, dtype=torch.int64, device=dev)
         b.hll = [torch.empty(rows * self.m, dtype=torch.int32, device=dev) for _ in range(prog.nhll)]
         b.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
+        b.touch = torch.zeros(rows if self.touch else 1, dtype=torch.uint8, device=dev)
+        b.clean = False
         hll_offs = []
         off = prog.G * prog.nslots * 8 * (BLOCK // 64)
         for _ in range(prog.nhll):
@@ -212,7 +224,8 @@ class PreparedScan:
             raise RuntimeError(f"query needs {total} bytes of LDS staging; reduce SDO_UNROLL")
         d = pack(prog, self.mode, self.dedup, self.hll_lds, 0 if self.shared else self.lds, b.acc.data_ptr(),
                  b.keys.data_ptr(),
-                 cap, b.overflow.data_ptr(), 0, 0, [h.data_ptr() for h in b.hll], hll_offs,
+                 cap, b.overflow.data_ptr(), b.touch.data_ptr() if self.touch else 0, 0,
+                 [h.data_ptr() for h in b.hll], hll_offs,
                  unroll=UNROLL, cache_off=cache_off, wave_bytes=wave_bytes)
         self.lds_total = total
         b.desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
@@ -228,8 +241,12 @@ class PreparedScan:
     def _reset(self, b: "_Bufs"):
         if self.pres_bytes:
             b.acc.zero_()
+        elif self.touch and b.clean:
+            pass  # the previous run re-initialised exactly the rows it touched
         else:
             b.acc.copy_(b.init_row.expand_as(b.acc))
+            if self.touch:
+                b.touch.zero_()
         if self.mode == D.M_HASH:
             b.keys.fill_(-1)
         for h in b.hll:
@@ -251,7 +268,15 @@ class PreparedScan:
             return self._empty()
         while True:
             self._reset(b)
+            b.clean = False  # dirty until the touched rows are re-initialised below
             self._launch(b)
+            if self.touch:
+                idx = native.nonzero_rows(b.touch)
+                acc = b.acc.index_select(0, idx)
+                b.acc.index_copy_(0, idx, b.init_row.expand(idx.numel(), -1).contiguous())
+                b.touch.index_fill_(0, idx, 0)
+                b.clean = True
+                return Partials("sparse", acc, idx, [])
             if self.pres_bytes:
                 idx = native.nonzero_rows(b.acc)
                 return Partials("sparse", torch.ones((idx.numel(), 1), dtype=torch.int64, device=self.dev), idx, [])
@@ -293,7 +318,7 @@ class PreparedScan:
 
 class _Bufs:
     """One execution slot's device buffers for a prepared scan."""
-    __slots__ = ("cap", "rows", "init_row", "acc", "keys", "hll", "overflow", "desc")
+    __slots__ = ("cap", "rows", "init_row", "acc", "keys", "hll", "overflow", "desc", "touch", "clean")
 
 
 class PreparedMask:

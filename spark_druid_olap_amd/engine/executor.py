@@ -180,7 +180,7 @@ class PreparedQuery:
             prog, part, t1 = self.run_partials(t0)
             t2 = time.perf_counter()
             with T.span("sdo.finalize"):
-                cols = finalize(prog, part)
+                cols = finalize(prog, part, getattr(self, "out_types", None))
             t3 = time.perf_counter()
             with T.span("sdo.post"):
                 self._theta(self._full_prog, cols)
@@ -193,6 +193,7 @@ class PreparedQuery:
         else:
             res = self._select()
         res.stats["exec_ms"] = (time.perf_counter() - t0) * 1e3
+        self.last_stats = res.stats
         return res
 
     def run_partials(self, t0: float):
@@ -382,8 +383,12 @@ class PreparedQuery:
         for pa in (getattr(qs, "postAggregations", None) or []):
             cols[pa.name] = np.asarray(eval_postagg(pa, cols, n), dtype=np.float64) * np.ones(n)
             out_cols.append(pa.name)
-        idx = np.arange(n)
         having = getattr(qs, "having", None)
+        identity = having is None and qt != "topN" and not (qt == "groupBy" and qs.limitSpec is not None) \
+            and not (qt == "timeseries" and "timestamp" in cols)
+        if identity:  # result order as produced: no index array, no copies (million-group results)
+            return QueryResult(out_cols, {c: cols[c] for c in out_cols}, qt, {"groups": n})
+        idx = np.arange(n)
         if having is not None:
             idx = idx[eval_having(having, cols)[idx]]
         if qt == "topN":
@@ -394,12 +399,7 @@ class PreparedQuery:
             idx = idx[np.argsort(cols["timestamp"][idx], kind="stable")]
             if getattr(qs, "descending", False):
                 idx = idx[::-1]
-        identity = having is None and qt != "topN" and not (qt == "groupBy" and qs.limitSpec is not None) \
-            and not (qt == "timeseries" and "timestamp" in cols)
-        if identity:
-            data = {c: cols[c] for c in out_cols}  # identity order: no copies
-        else:
-            data = {c: take(cols[c], idx) for c in out_cols}
+        data = {c: take(cols[c], idx) for c in out_cols}
         return QueryResult(out_cols, data, qt, {"groups": n})
 
     def _topn_order(self, cols, idx, prog) -> np.ndarray:

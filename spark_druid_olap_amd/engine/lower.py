@@ -246,6 +246,7 @@ class KeyComp:
     is_timestamp: bool = False    # granularity bucket (output 'timestamp' ms)
     orig: Optional[np.ndarray] = None  # compacted key: key id -> original dictionary id
     col_idx: int = -1             # descriptor column index (payload section)
+    dictionary: Any = None        # plain dictionary-id key: its dictionary (device-side typed decode)
 
 
 @dataclass
@@ -780,7 +781,7 @@ class Lowerer:
             raise LoweringError(f"group by unknown dimension {dim!r}")
         d = ds.dims[dim].dictionary
         if fn is None:
-            return KeyComp(name, D.K_ID, dim, len(d), decoder=lambda ids, _d=d: DictColumn(ids, _d))
+            return KeyComp(name, D.K_ID, dim, len(d), decoder=lambda ids, _d=d: DictColumn(ids, _d), dictionary=d)
         if isinstance(fn, S.TimeFormatExtractionFunctionSpec) and d.vtype != "string":
             pass
         pv = getattr(fn, "_pyvec", None)

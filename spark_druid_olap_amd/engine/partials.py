@@ -101,17 +101,124 @@ def d2h(ts: List[torch.Tensor]) -> List[np.ndarray]:
     return [o.numpy() for o in outs]
 
 
-def finalize(prog, parts: Partials) -> Dict[str, np.ndarray]:
-    """Decode groups into host columns: key outputs then aggregator outputs (Druid types)."""
+_INT_T = ("tinyint", "smallint", "int", "bigint")
+_NO_DEVICE_DECODE = bool(__import__("os").environ.get("SDO_NO_DEVICE_DECODE"))
+_I32 = (-(1 << 31), (1 << 31) - 1)
+
+
+class _Const:
+    """A key whose every value is the same (a one-entry dictionary): nothing crosses the link."""
+
+    def __init__(self, value, dtype):
+        self.value, self.dtype = value, dtype
+
+
+def _device_typed(kc, ids: torch.Tensor, sqlt: Optional[str]):
+    """Typed values of a dictionary-id key computed ON THE DEVICE for a numeric SQL output type
+    (the same values ``sql/execute.py:_dict_series`` would produce on the host): integer range
+    dictionaries are ``start + id``; other dictionaries of up to 4M entries gather from a cached
+    device table of their typed values; a one-entry dictionary is a constant.  ``int`` and narrower
+    SQL types travel as int32.  A million-group result (TPC-H Q3: o_orderkey, o_shippriority) then
+    ships final values at their SQL width and the host does no per-row decode pass.  None when not
+    applicable (strings, NULL-bearing dictionaries, huge non-range dictionaries)."""
+    d = getattr(kc, "dictionary", None)
+    if d is None or sqlt is None or kc.orig is not None:
+        return None
+    from ..sql.types import base
+
+    bt = base(sqlt)
+    if bt not in _INT_T and bt not in ("double", "float"):
+        return None
+    narrow = bt in ("tinyint", "smallint", "int")
+    if hasattr(d, "start") and not getattr(d, "has_null", False) and not hasattr(d, "prefix"):
+        lo, hi = int(d.start), int(d.start) + len(d) - 1
+        if narrow and _I32[0] <= lo and hi <= _I32[1]:
+            return ids.to(torch.int32) + lo
+        v = ids.to(torch.int64) + lo
+        return v if bt in _INT_T else v.to(torch.float64)
+    if len(d) > (1 << 22):
+        return None
+    cache = d.__dict__.setdefault("_dev_typed", {})
+    key = (bt, str(ids.device))
+    tab = cache.get(key)
+    if tab is None:
+        from ..sql.execute import _raw
+        from ..sql.types import to_series
+
+        typed = to_series(_raw(d.all_values()), sqlt)
+        if typed.isna().any() or len(typed) == 0:
+            tab = False
+        else:
+            arr = typed.to_numpy(dtype=np.int64 if bt in _INT_T else np.float64)
+            if len(arr) == 1:
+                tab = _Const(arr[0], arr.dtype)
+            else:
+                if narrow and _I32[0] <= int(arr.min()) and int(arr.max()) <= _I32[1]:
+                    arr = arr.astype(np.int32)
+                tab = torch.from_numpy(np.ascontiguousarray(arr)).to(ids.device)
+        cache[key] = tab
+    if tab is False:
+        return None
+    if isinstance(tab, _Const):
+        return tab
+    return tab.index_select(0, ids.to(torch.int64))
+
+
+def _narrow_ids(kc, ids: torch.Tensor) -> torch.Tensor:
+    """Dictionary ids at the narrowest width their cardinality allows (fewer D2H bytes)."""
+    if kc.card <= (1 << 15) and getattr(kc, "dictionary", None) is not None:
+        return ids.to(torch.int16)
+    return ids.to(torch.int32) if kc.card < 2 ** 31 else ids
+
+
+def _agg_outputs_dev(prog, acc: torch.Tensor, skip) -> Dict[str, torch.Tensor]:
+    """Final aggregator columns on the device (same values as finalize's host conversions)."""
+    out = {}
+    for a in prog.aggs:
+        if a.name in skip or a.slot < 0 or a.kind in ("hll", "theta"):
+            continue
+        col = acc[:, a.slot]
+        if a.kind == "count":
+            v = col
+        elif a.kind in ("sum_i", "min_i", "max_i"):
+            if a.scale:
+                v = col.to(torch.float64) / (10.0 ** a.scale)
+            elif a.out_type == "long":
+                v = col
+            else:
+                v = col.to(torch.float64)
+        elif a.kind == "sum_f":
+            v = col.contiguous().view(torch.float64)
+        elif a.kind in ("min_f", "max_f"):
+            v = torch.where(col >= 0, col, col ^ 0x7FFFFFFFFFFFFFFF).view(torch.float64)
+            if a.out_type == "long":
+                v = torch.where(torch.isfinite(v), v, torch.zeros_like(v)).to(torch.int64)
+        else:
+            continue
+        out[a.name] = v.contiguous()
+    return out
+
+
+def finalize(prog, parts: Partials, out_types: Optional[Dict[str, str]] = None) -> Dict[str, np.ndarray]:
+    """Decode groups into host columns: key outputs then aggregator outputs (Druid types).
+
+    Large (sparse) results are decoded on the device and cross the host link narrow: key ids at
+    their dictionary's width, numeric dictionary keys as final SQL-typed values when ``out_types``
+    (output name -> SQL type, from the SQL layer) asks for them, constant keys not at all, and only
+    the accumulator slots an output reads."""
     from .lower import ord2f
 
     want_gid = bool(getattr(prog, "thetas", None))
+    collapse = any(kc.collapse for kc in prog.keys)
+    typed: Dict[int, object] = {}
     if parts.kind == "dense":
         small = parts.rows * parts.acc.shape[1] <= (1 << 20)
         if small:
             (acc_h,) = d2h([parts.acc])
             gid = np.flatnonzero(acc_h[:, 0] > 0)
             acc_h = acc_h[gid]
+            acc_cols = {s: acc_h[:, s] for s in range(acc_h.shape[1])}
+            R = len(gid)
             hll_d = [h.index_select(0, torch.from_numpy(gid).to(h.device)) for h in parts.hll]
             key_ids = [(gid // kc.stride) % max(1, kc.card) for kc in prog.keys]
             derived_ids = None
@@ -125,40 +232,72 @@ def finalize(prog, parts: Partials) -> Dict[str, np.ndarray]:
         else:
             parts = parts.compact()
     if parts.kind == "sparse":
-        # decode key components on the device, then one pinned D2H per array
+        # decode key components on the device, then one pinned D2H of every array
         g = parts.keys
-        dev_ids = []
+        R = int(g.numel())
+        full_ids = []
         for kc in prog.keys:
             ids = torch.remainder(torch.div(g, kc.stride, rounding_mode="floor"), max(1, kc.card))
-            dev_ids.append(ids.to(torch.int32) if kc.card < 2 ** 31 else ids)
-        nk = len(dev_ids)
+            full_ids.append(ids)
+        nk = len(full_ids)
         dag = []
         for a, det, lut in getattr(prog, "derived_aggs", ()):
             # min/max of a metric constant per key: gathered from its FD table, no accumulator
-            did = dev_ids[det].to(torch.int64)
+            did = full_ids[det]
             orig = prog.keys[det].orig
             if orig is not None:
                 did = torch.from_numpy(orig).to(did.device)[did]
             dag.append(lut.to(did.device)[did])
+        all_kcs = list(prog.keys)
         for kc, det, lut in getattr(prog, "derived", ()):
             # functionally dependent keys: gather their ids on the device
-            did = dev_ids[det].to(torch.int64)
+            did = full_ids[det]
             orig = prog.keys[det].orig
             if orig is not None:
                 did = torch.from_numpy(orig).to(did.device)[did]
-            dev_ids.append(lut.to(did.device)[did])
-        # slot-major accumulators so every output column is a contiguous view (no host copies)
-        host = d2h(dev_ids + dag + [parts.acc.t().contiguous()] + ([g] if want_gid else []))
-        key_ids = host[:nk]
-        derived_ids = host[nk:len(dev_ids)]
-        derived_agg_vals = host[len(dev_ids):len(dev_ids) + len(dag)]
-        acc_h = host[len(dev_ids) + len(dag)].T
-        gid = host[-1] if want_gid else None
+            full_ids.append(lut.to(did.device)[did].to(torch.int64))
+            all_kcs.append(kc)
+        dev_ids = []
+        for i, (kc, ids) in enumerate(zip(all_kcs, full_ids)):
+            v = None
+            if out_types and g.is_cuda and not _NO_DEVICE_DECODE and not collapse:
+                v = _device_typed(kc, ids, out_types.get(kc.name))
+            if v is not None:
+                typed[i] = v
+                dev_ids.append(None if isinstance(v, _Const) else v)
+            else:
+                dev_ids.append(_narrow_ids(kc, ids) if g.is_cuda else (ids.to(torch.int32) if kc.card < 2 ** 31 else ids))
+        # aggregator outputs finished on the device (decimal scaling, float views, ordered-float
+        # decode) so the host receives final columns; with non-injective key formatting the raw
+        # slots travel instead (the host re-aggregates)
+        nslots = parts.acc.shape[1]
+        derived_names = {a.name for a, _, _ in getattr(prog, "derived_aggs", ())}
+        agg_dev = {} if collapse else _agg_outputs_dev(prog, parts.acc, derived_names)
+        need = list(range(nslots)) if collapse else []
+        acc_dev = parts.acc[:, need].t().contiguous() if need else None
+        agg_names = list(agg_dev)
+        ship = [t for t in dev_ids if t is not None] + dag + ([acc_dev] if acc_dev is not None else []) + \
+            [agg_dev[n] for n in agg_names] + ([g] if want_gid else [])
+        host = d2h(ship)
+        it = iter(host)
+        hid = [None if t is None else next(it) for t in dev_ids]
+        key_ids = hid[:nk]
+        derived_ids = hid[nk:]
+        derived_agg_vals = [next(it) for _ in dag]
+        acc_rows = next(it) if acc_dev is not None else None
+        acc_cols = {s: acc_rows[k] for k, s in enumerate(need)}
+        agg_host = {n: next(it) for n in agg_names}
+        gid = next(it) if want_gid else None
         hll_d = parts.hll
+        for i, v in typed.items():
+            if isinstance(v, _Const):
+                (key_ids if i < nk else derived_ids)[i if i < nk else i - nk] = np.full(R, v.value, dtype=v.dtype)
+    if parts.kind != "sparse":
+        agg_host = {}
     cols: Dict[str, np.ndarray] = {}
     key_vals = []
-    for kc, ids in zip(prog.keys, key_ids):
-        vals = kc.decoder(ids) if kc.decoder is not None else ids
+    for i, (kc, ids) in enumerate(zip(prog.keys, key_ids)):
+        vals = ids if (i in typed or kc.decoder is None) else kc.decoder(ids)
         key_vals.append(vals)
         cols[kc.name] = vals
     for j, (kc, det, lut) in enumerate(getattr(prog, "derived", ())):
@@ -171,12 +310,12 @@ def finalize(prog, parts: Partials) -> Dict[str, np.ndarray]:
             if orig is not None:
                 did = orig[did]
             ids = lut[torch.from_numpy(did).to(lut.device)].cpu().numpy()
-        vals = kc.decoder(ids) if kc.decoder is not None else ids
+        done = (len(prog.keys) + j) in typed
+        vals = ids if (done or kc.decoder is None) else kc.decoder(ids)
         key_vals.append(vals)
         cols[kc.name] = vals
     key_names = [kc.name for kc in prog.keys] + [kc.name for kc, _, _ in getattr(prog, "derived", ())]
-    collapse = any(kc.collapse for kc in prog.keys)
-    if collapse and len(acc_h):
+    if collapse and R:
         # non-injective key formatting: re-aggregate groups that format identically
         tup = list(zip(*[v.tolist() for v in key_vals]))
         uniq = {}
@@ -184,21 +323,22 @@ def finalize(prog, parts: Partials) -> Dict[str, np.ndarray]:
         for i, t in enumerate(tup):
             inv[i] = uniq.setdefault(t, len(uniq))
         R = len(uniq)
-        new_acc = np.empty((R, acc_h.shape[1]), dtype=np.int64)
+        new_cols = {}
         for s, (op, init) in enumerate(prog.slots):
             col = np.full(R, init, dtype=np.int64)
+            src = acc_cols[s]
             if op == D.S_SUM_I:
                 col[:] = 0
-                np.add.at(col, inv, acc_h[:, s])
+                np.add.at(col, inv, src)
             elif op == D.S_SUM_F:
                 cf = np.zeros(R, dtype=np.float64)
-                np.add.at(cf, inv, acc_h[:, s].view(np.float64))
+                np.add.at(cf, inv, src.view(np.float64) if src.flags.c_contiguous else src.copy().view(np.float64))
                 col = cf.view(np.int64)
             elif op == D.S_MIN_I:
-                np.minimum.at(col, inv, acc_h[:, s])
+                np.minimum.at(col, inv, src)
             else:
-                np.maximum.at(col, inv, acc_h[:, s])
-            new_acc[:, s] = col
+                np.maximum.at(col, inv, src)
+            new_cols[s] = col
         inv_t = torch.from_numpy(inv)
         new_hll = []
         for h in hll_d:
@@ -211,7 +351,7 @@ def finalize(prog, parts: Partials) -> Dict[str, np.ndarray]:
             keys_first[i] = t
         for j, name in enumerate(key_names):
             cols[name] = np.array([t[j] for t in keys_first], dtype=object)
-        acc_h, hll_d = new_acc, new_hll
+        acc_cols, hll_d = new_cols, new_hll
     derived_names = {}
     for (a, _, _), v in zip(getattr(prog, "derived_aggs", ()), derived_agg_vals):
         v = np.asarray(v, dtype=np.int64)
@@ -220,10 +360,12 @@ def finalize(prog, parts: Partials) -> Dict[str, np.ndarray]:
     for a in prog.aggs:
         if a.name in derived_names:
             cols[a.name] = derived_names[a.name]
+        elif parts.kind == "sparse" and a.name in agg_host:
+            cols[a.name] = agg_host[a.name]
         elif a.kind in ("count",):
-            cols[a.name] = acc_h[:, a.slot]
+            cols[a.name] = acc_cols[a.slot]
         elif a.kind in ("sum_i", "min_i", "max_i"):
-            v = acc_h[:, a.slot]
+            v = acc_cols[a.slot]
             if a.scale:
                 cols[a.name] = v.astype(np.float64) / (10.0 ** a.scale)
             elif a.out_type == "long":
@@ -231,18 +373,19 @@ def finalize(prog, parts: Partials) -> Dict[str, np.ndarray]:
             else:
                 cols[a.name] = v.astype(np.float64)
         elif a.kind == "sum_f":
-            col = acc_h[:, a.slot]
+            col = acc_cols[a.slot]
             cols[a.name] = col.view(np.float64) if col.flags.c_contiguous else col.copy().view(np.float64)
         elif a.kind in ("min_f", "max_f"):
-            v = ord2f(acc_h[:, a.slot]).copy()
+            v = ord2f(acc_cols[a.slot]).copy()
             if a.out_type == "long":
                 # longMin/longMax over __time: empty groups keep the +-inf identity
                 v = np.where(np.isfinite(v), v, 0).astype(np.int64)
             cols[a.name] = v
         elif a.kind == "hll":
-            cols[a.name] = hll_estimates(hll_d[a.hll_index], prog.hll_p) if len(acc_h) else np.zeros(0)
+            cols[a.name] = hll_estimates(hll_d[a.hll_index], prog.hll_p) if R else np.zeros(0)
         elif a.kind == "theta":
             pass  # filled by the executor
-    cols["__rows__"] = acc_h[:, 0]
-    cols["__gid__"] = gid if not collapse else np.arange(len(acc_h))
+    # group count of the result (only its length is read downstream)
+    cols["__rows__"] = acc_cols[0] if 0 in acc_cols else np.zeros(R, dtype=np.int8)
+    cols["__gid__"] = gid if not collapse else np.arange(R)
     return cols

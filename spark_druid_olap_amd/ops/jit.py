@@ -472,6 +472,12 @@ class _Gen:
         else:
             body.append("        const int64_t slot = (int64_t)key;")
             body.append("        const bool mine = act[u];")
+            if mode == D.M_DENSE_GLOBAL and getattr(p, "touch_table", False):
+                # first-touch byte table (engine/device_exec.py): every group a qualifying row
+                # reaches is marked with a plain byte store (same-value races are benign); the
+                # touched groups compact from this table instead of the accumulator table, and only
+                # they are re-initialised after the run (no full-table fill per execution)
+                body.append("        if (mine) ((unsigned char*)d->out_mask)[slot] = (unsigned char)1;")
         for ai, a in enumerate(p.aops):
             cond = "mine"
             if a.get("filt_len"):

@@ -334,6 +334,8 @@ class Session:
                 if prep is None or getattr(dq, "_prepared_spec", None) is not spec:
                     with T.span("sdo.lower"):
                         prep = self.engine.prepare(run_spec, ds, dq.info.get("historical"))
+                    # output SQL types: large results decode numeric dictionary keys on the device
+                    prep.out_types = {n: t for n, t, k in dq.columns if k == "value"}
                     dq._prepared = prep
                     dq._prepared_spec = spec
         with T.span(f"sdo.druid.{spec.queryType}"):

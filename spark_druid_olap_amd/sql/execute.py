@@ -382,6 +382,8 @@ def druid_value_series(col, sqlt: str, kind: str, n: int) -> pd.Series:
     if arr.dtype.kind in "fiu" and bt in ("double", "float", "decimal"):
         return pd.Series(arr.astype(np.float64, copy=False))       # numpy float64: NaN == NULL
     if arr.dtype.kind in "iu" and bt in ("tinyint", "smallint", "int", "bigint"):
+        if arr.dtype == np.int32 and bt != "bigint":
+            return pd.Series(arr)  # 32-bit SQL ints stay 32-bit (no widening pass)
         return pd.Series(arr.astype(np.int64, copy=False))
     if arr.dtype.kind == "f" and bt in ("tinyint", "smallint", "int", "bigint"):
         if not np.isnan(arr).any():

@@ -65,3 +65,58 @@ def test_presence_byte_table_matches_reference():
     ref = run_reference(prog)
     ref_keys = ref.compact().keys
     assert torch.equal(torch.sort(got.keys).values, torch.sort(ref_keys.to(got.keys.device)).values)
+
+
+@pytest.mark.parametrize("name", ["TPCH Q3", "TPCH Q7", "Basic Aggregation"])
+def test_device_typed_key_decode_matches_host_decode(sessions, name):
+    """finalize decodes numeric dictionary keys on the device when the SQL layer passes output
+    types (partials.py:_device_typed); dropping the types falls back to the host DictColumn path --
+    both must give identical rows and column dtypes."""
+    nat, _ = sessions
+    q = dict(tpch.BENCH_QUERIES)[name]
+    d = nat.sql(q)
+    a = _rows(d)
+    pa = d.to_pandas()
+    prep = d.druid_queries()[0]._prepared
+    assert prep.out_types
+    saved, prep.out_types = prep.out_types, None
+    try:
+        d2 = nat.sql(q)
+        b = _rows(d2)
+        pb = d2.to_pandas()
+    finally:
+        prep.out_types = saved
+    assert a == b
+    assert [str(t) for t in pa.dtypes] == [str(t) for t in pb.dtypes]
+
+
+@pytest.mark.parametrize("name", ["Q3", "Q10", "Q18"])
+def test_first_touch_table_matches_reference_across_reruns(sessions, name, monkeypatch):
+    """Dense HBM group tables with the first-touch byte table (device_exec.py TOUCH_MIN_G): the
+    touched groups compact from the byte table and only they are re-initialised after a run, so
+    re-running the prepared query (no full-table fill) must keep giving the reference answer."""
+    from spark_druid_olap_amd.engine import device_exec
+
+    monkeypatch.setattr(device_exec, "TOUCH_MIN_G", 0)
+    nat, ref = sessions
+    q = dict(tpch22.QUERIES)[name]
+    s2 = Session(engine=Engine(use_native=True))
+    ds = nat.catalog.cluster.get("tpch")
+    s2.register_datasource(ds)
+    s2.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)
+    s2.sql(tpch.druid_ddl(with_column_mapping=False))
+    d = s2.sql(q)
+    exp = _rows(ref.sql(q))
+    for _ in range(3):
+        got = _rows(d)
+        assert len(got) == len(exp)
+        for x, y in zip(got, exp):
+            for u, v in zip(x, y):
+                if isinstance(u, float) or isinstance(v, float):
+                    assert u == pytest.approx(v, rel=1e-9, abs=0.011), (name, x, y)
+                else:
+                    assert u == v, (name, x, y)
+    touched = [p for dq in d.druid_queries() for _, _, p in getattr(getattr(dq, "_prepared", None), "scans", [])
+               if p is not None and getattr(p, "touch", False)]
+    if name == "Q3":
+        assert touched, "Q3 should run with a first-touch table"
