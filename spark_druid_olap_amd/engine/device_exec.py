@@ -200,13 +200,15 @@ class PreparedScan:
         b.rows = rows
         b.init_row = torch.tensor([init for _, init in prog.slots], dtype=torch.int64, device=dev)
         if self.pres_bytes:
-            b.acc = torch.empty((rows,), dtype=torch.uint8, device=dev)
+            # padded to whole 8-byte words (the fused reset zeroes words; padding bytes stay 0 and
+            # never compact)
+            b.acc = torch.empty(((rows + 7) // 8 * 8,), dtype=torch.uint8, device=dev)
         else:
             b.acc = torch.empty((rows, prog.nslots), dtype=torch.int64, device=dev)
         b.keys = torch.empty(rows if self.mode == D.M_HASH else 1, dtype=torch.int64, device=dev)
         b.hll = [torch.empty(rows * self.m, dtype=torch.int32, device=dev) for _ in range(prog.nhll)]
         b.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
-        b.touch = torch.zeros(rows if self.touch else 1, dtype=torch.uint8, device=dev)
+        b.touch = torch.zeros(((rows + 7) // 8 * 8) if self.touch else 8, dtype=torch.uint8, device=dev)
         b.clean = False
         hll_offs = []
         off = prog.G * prog.nslots * 8 * (BLOCK // 64)
@@ -239,19 +241,26 @@ class PreparedScan:
             native.scan(b.desc, self.grid, BLOCK, self.lds_total, UNROLL)
 
     def _reset(self, b: "_Bufs"):
+        if self.touch and b.clean:
+            return  # the previous run re-initialised exactly the rows it touched
+        # one fused launch (ops/csrc/post_scan.hip reset_bufs_kernel) instead of a fill per buffer
+        zeros = list(b.hll)
+        if self.touch:
+            zeros.append(b.touch)
+        acc = b.acc
         if self.pres_bytes:
-            b.acc.zero_()
-        elif self.touch and b.clean:
-            pass  # the previous run re-initialised exactly the rows it touched
+            zeros.append(b.acc)
+            acc = None
+        if len(zeros) <= 4:
+            native.reset_bufs(acc, b.init_row, zeros, b.overflow)
         else:
-            b.acc.copy_(b.init_row.expand_as(b.acc))
-            if self.touch:
-                b.touch.zero_()
+            if acc is not None:
+                acc.copy_(b.init_row.expand_as(acc))
+            for z in zeros:
+                z.zero_()
+            b.overflow.zero_()
         if self.mode == D.M_HASH:
             b.keys.fill_(-1)
-        for h in b.hll:
-            h.zero_()
-        b.overflow.zero_()
 
     # ------------------------------------------------------------------ run
     def run(self) -> Partials:

@@ -211,15 +211,28 @@ def finalize(prog, parts: Partials, out_types: Optional[Dict[str, str]] = None) 
     want_gid = bool(getattr(prog, "thetas", None))
     collapse = any(kc.collapse for kc in prog.keys)
     typed: Dict[int, object] = {}
+    est_host: List[np.ndarray] = []
     if parts.kind == "dense":
         small = parts.rows * parts.acc.shape[1] <= (1 << 20)
         if small:
-            (acc_h,) = d2h([parts.acc])
+            # HLL estimates of every group computed before the one D2H (one sync, not two)
+            est_dev = []
+            G = parts.rows
+            if parts.hll and parts.acc.is_cuda and G * (1 << prog.hll_p) <= (1 << 26) and not collapse:
+                from ..ops import native
+
+                for h in parts.hll:
+                    e = torch.empty(G, dtype=torch.float64, device=h.device)
+                    native.hll_estimate(h.contiguous(), G, prog.hll_p, e)
+                    est_dev.append(e)
+            host = d2h([parts.acc] + est_dev)
+            acc_h = host[0]
             gid = np.flatnonzero(acc_h[:, 0] > 0)
             acc_h = acc_h[gid]
             acc_cols = {s: acc_h[:, s] for s in range(acc_h.shape[1])}
             R = len(gid)
-            hll_d = [h.index_select(0, torch.from_numpy(gid).to(h.device)) for h in parts.hll]
+            est_host = [e[gid] for e in host[1:]]
+            hll_d = [] if est_host else [h.index_select(0, torch.from_numpy(gid).to(h.device)) for h in parts.hll]
             key_ids = [(gid // kc.stride) % max(1, kc.card) for kc in prog.keys]
             derived_ids = None
             derived_agg_vals = []
@@ -382,7 +395,10 @@ def finalize(prog, parts: Partials, out_types: Optional[Dict[str, str]] = None) 
                 v = np.where(np.isfinite(v), v, 0).astype(np.int64)
             cols[a.name] = v
         elif a.kind == "hll":
-            cols[a.name] = hll_estimates(hll_d[a.hll_index], prog.hll_p) if R else np.zeros(0)
+            if est_host:
+                cols[a.name] = est_host[a.hll_index]
+            else:
+                cols[a.name] = hll_estimates(hll_d[a.hll_index], prog.hll_p) if R else np.zeros(0)
         elif a.kind == "theta":
             pass  # filled by the executor
     # group count of the result (only its length is read downstream)

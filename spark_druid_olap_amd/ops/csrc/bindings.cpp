@@ -28,6 +28,17 @@ __global__ void topk_hist_kernel(const int64_t* acc, int64_t n, int nslots, int 
                                  const uint64_t* state, int level, unsigned int* hist);
 __global__ void topk_pick_kernel(unsigned int* hist, uint64_t* state, int level);
 __global__ void nonzero_mask_kernel(const unsigned char* base, int esize, int64_t n, int64_t stride, uint64_t* words);
+struct ResetArgs {
+  int64_t* acc;
+  const int64_t* init;
+  int64_t rows;
+  int nslots;
+  int nz;
+  uint64_t* z[4];
+  int64_t zn[4];
+  int* overflow;
+};
+__global__ void reset_bufs_kernel(ResetArgs a);
 __global__ void topk_keep_kernel(const int64_t* acc, int64_t n, int nslots, int slot, int is_f64, int desc,
                                  const uint64_t* state, uint64_t* keep);
 }  // namespace sdo
@@ -111,6 +122,30 @@ static void nonzero_mask(uint64_t base, int esize, int64_t n, int64_t stride, ui
   hipLaunchKernelGGL(sdo::nonzero_mask_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
                      (const unsigned char*)base, esize, n, stride, (uint64_t*)words);
   check(hipGetLastError(), "nonzero_mask_kernel launch");
+}
+
+// One-launch re-initialisation of a prepared scan's buffers (post_scan.hip reset_bufs_kernel).
+static void reset_bufs(uint64_t acc, uint64_t init, int64_t rows, int nslots, std::vector<uint64_t> zptr,
+                       std::vector<int64_t> zwords, uint64_t overflow, uint64_t stream) {
+  if (zptr.size() != zwords.size() || zptr.size() > 4) throw std::invalid_argument("at most 4 zero regions");
+  sdo::ResetArgs a{};
+  a.acc = (int64_t*)acc;
+  a.init = (const int64_t*)init;
+  a.rows = acc ? rows : 0;
+  a.nslots = nslots;
+  a.nz = (int)zptr.size();
+  int64_t work = a.rows * nslots;
+  for (size_t i = 0; i < zptr.size(); ++i) {
+    a.z[i] = (uint64_t*)zptr[i];
+    a.zn[i] = zwords[i];
+    if (zwords[i] > work) work = zwords[i];
+  }
+  a.overflow = (int*)overflow;
+  int64_t blocks = (work + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(sdo::reset_bufs_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+  check(hipGetLastError(), "reset_bufs_kernel launch");
 }
 
 // Top-k threshold (post_scan.hip): 4 radix levels of histogram + pick, then the keep bitmask.
@@ -261,6 +296,7 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("compact_write", &compact_write);
   m.def("topk_keep", &topk_keep);
   m.def("nonzero_mask", &nonzero_mask);
+  m.def("reset_bufs", &reset_bufs);
   m.def("desc_size", &desc_size);
   m.def("rtc_compile", &rtc_compile);
   m.def("module_load", [](py::bytes code, const std::string& name) { return module_load(std::string(code), name); });

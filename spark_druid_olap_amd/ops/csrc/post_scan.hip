@@ -233,4 +233,31 @@ __global__ void __launch_bounds__(256) topk_keep_kernel(const int64_t* __restric
   }
 }
 
+// Re-initialisation of a prepared scan's execution buffers in ONE launch (instead of one fill per
+// buffer): the accumulator table gets its per-slot identity row (0 for sums/counts, +/-max for
+// min/max), up to four HLL register arrays and the hash-overflow flag are zeroed.  Grid-stride,
+// 64-bit vector stores.
+struct ResetArgs {
+  int64_t* acc;
+  const int64_t* init;   // nslots identities
+  int64_t rows;
+  int nslots;
+  int nz;                // zero regions in use
+  uint64_t* z[4];        // zeroed regions (64-bit words)
+  int64_t zn[4];         // their lengths in words
+  int* overflow;
+};
+
+__global__ void __launch_bounds__(256) reset_bufs_kernel(ResetArgs a) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nth = (int64_t)gridDim.x * blockDim.x;
+  const int64_t na = a.rows * a.nslots;
+  for (int64_t i = tid; i < na; i += nth) a.acc[i] = a.init[i % a.nslots];
+  for (int r = 0; r < a.nz; ++r) {
+    uint64_t* z = a.z[r];
+    for (int64_t i = tid; i < a.zn[r]; i += nth) z[i] = 0ull;
+  }
+  if (tid == 0 && a.overflow) *a.overflow = 0;
+}
+
 }  // namespace sdo

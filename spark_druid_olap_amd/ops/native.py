@@ -11,6 +11,8 @@ import importlib
 import os
 import threading
 
+from typing import Optional, Sequence
+
 import torch
 
 _lock = threading.Lock()
@@ -88,6 +90,24 @@ def hll_estimate(regs: torch.Tensor, G: int, p: int, est: torch.Tensor) -> None:
     assert regs.dtype == torch.int32 and regs.is_contiguous() and regs.numel() >= G * (1 << p)
     assert est.dtype == torch.float64 and est.numel() >= G
     m.hll_estimate(regs.data_ptr(), int(G), int(p), est.data_ptr(), _stream(regs.device))
+
+
+def reset_bufs(acc: Optional[torch.Tensor], init: torch.Tensor, zeros: Sequence[torch.Tensor],
+               overflow: Optional[torch.Tensor]) -> None:
+    """One launch: ``acc[r, s] = init[s]`` for every row, every tensor in ``zeros`` (<= 4, sizes a
+    multiple of 8 bytes) set to 0, ``overflow[0] = 0``."""
+    m = load()
+    dev = init.device
+    zp, zw = [], []
+    for z in zeros:
+        nb = z.numel() * z.element_size()
+        assert z.is_contiguous() and nb % 8 == 0
+        zp.append(z.data_ptr())
+        zw.append(nb // 8)
+    if acc is not None:
+        assert acc.dtype == torch.int64 and acc.is_contiguous() and acc.dim() == 2 and acc.shape[1] == init.numel()
+    m.reset_bufs(acc.data_ptr() if acc is not None else 0, init.data_ptr(), int(acc.shape[0]) if acc is not None else 0,
+                 int(init.numel()), zp, zw, overflow.data_ptr() if overflow is not None else 0, _stream(dev))
 
 
 def device_info(dev: int = 0) -> dict:

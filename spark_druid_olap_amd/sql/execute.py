@@ -19,7 +19,7 @@ from ..query import spec as S
 from . import ast as A
 from . import plan as P
 from .functions import Frame, eval_series, evaluate, typeof
-from .types import AnalysisError, base, broadcast, is_vec, pandas_dtype, to_series
+from .types import AnalysisError, base, broadcast, fast_series, is_vec, pandas_dtype, to_series
 
 
 class Batch:
@@ -147,21 +147,29 @@ class Executor:
 
     def _Project(self, p: P.Project) -> Batch:
         b = self.run(p.child)
-        fr = b.frame(self._subquery)
+        prog = p.__dict__.get("_proj")
+        if prog is None:
+            # compiled once per plan node: column passthroughs and numpy closures for the
+            # arithmetic over Druid results (no per-run expression-tree dispatch)
+            prog = p._proj = [_compile_proj(e, r) for e, r in zip(p.exprs, p.output)]
+        fr = None
         cols = {}
         refs = p.output
-        for e, r in zip(p.exprs, refs):
-            if isinstance(e, A.Ref):
-                cols[r.rid] = b.cols[e.rid]
-            elif isinstance(e, A.Alias) and isinstance(e.child, A.Ref) and e.child.dtype == r.dtype:
-                cols[r.rid] = b.cols[e.child.rid]
-            else:
-                a = _np_eval(e, b) if b.n <= _NP_FAST_MAX_ROWS else None
+        for (kind, x), e, r in zip(prog, p.exprs, refs):
+            if kind == "ref":
+                cols[r.rid] = b.cols[x]
+                continue
+            if x is not None and b.n <= _NP_FAST_MAX_ROWS:
+                try:
+                    a = x(b.cols)
+                except _NoFast:
+                    a = None
                 if a is not None:
-                    cols[r.rid] = pd.Series(a)
+                    cols[r.rid] = fast_series(a)
                     continue
-                s = eval_series(e, fr)
-                cols[r.rid] = _conform(s, r.dtype)
+            if fr is None:
+                fr = b.frame(self._subquery)
+            cols[r.rid] = _conform(eval_series(e, fr), r.dtype)
         return Batch(refs, cols, b.n)
 
     def _Sort(self, p: P.Sort) -> Batch:
@@ -343,6 +351,122 @@ def _np_rec(e: A.Expr, b: Batch):
     raise _NoFast
 
 
+def _compile_proj(e: A.Expr, r: A.Ref):
+    """("ref", rid) for a passthrough, else ("expr", closure | None): the closure evaluates ``e``
+    over NULL-free numpy input columns (same semantics as ``_np_rec``; raises _NoFast otherwise)."""
+    if isinstance(e, A.Ref):
+        return ("ref", e.rid)
+    if isinstance(e, A.Alias) and isinstance(e.child, A.Ref) and e.child.dtype == r.dtype:
+        return ("ref", e.child.rid)
+    try:
+        f = _np_compile(e)
+    except _NoFast:
+        return ("expr", None)
+    t = base(typeof(e))
+
+    def run(cols, f=f, t=t):
+        v = f(cols)
+        if not isinstance(v, np.ndarray):
+            raise _NoFast
+        if t in ("double", "float") and v.dtype.kind == "f":
+            return v
+        if t in _INT_T and v.dtype.kind in "iu":
+            return v.astype(np.int64, copy=False)
+        raise _NoFast
+    return ("expr", run)
+
+
+def _np_compile(e: A.Expr):
+    """Closure form of ``_np_rec`` (type decisions taken at compile time)."""
+    if isinstance(e, A.Alias):
+        return _np_compile(e.child)
+    if isinstance(e, A.Ref):
+        rid = e.rid
+
+        def ref(cols):
+            s = cols.get(rid)
+            if s is None:
+                raise _NoFast
+            dt = s.dtype
+            if not isinstance(dt, np.dtype) or dt.kind not in "iuf":
+                raise _NoFast
+            return s.to_numpy()
+        return ref
+    if isinstance(e, A.Lit):
+        if isinstance(e.value, bool) or not isinstance(e.value, (int, float)):
+            raise _NoFast
+        v = e.value
+        return lambda cols: v
+    if isinstance(e, A.Cast):
+        f = _np_compile(e.child)
+        to = base(e.to)
+        if to in ("double", "float"):
+            def cast_f(cols):
+                x = f(cols)
+                return np.asarray(x, dtype=np.float64) if isinstance(x, np.ndarray) else float(x)
+            return cast_f
+        if to in _INT_T:
+            def cast_int(cols):
+                x = f(cols)
+                if not isinstance(x, np.ndarray):
+                    raise _NoFast
+                if x.dtype.kind == "f":
+                    if not np.isfinite(x).all():
+                        raise _NoFast
+                    return np.trunc(x).astype(np.int64)
+                return x.astype(np.int64, copy=False)
+            return cast_int
+        raise _NoFast
+    if isinstance(e, A.UnOp) and e.op == "-":
+        f = _np_compile(e.child)
+        return lambda cols: -f(cols)
+    if isinstance(e, A.BinOp) and e.op in ("+", "-", "*", "/"):
+        fl, fr_ = _np_compile(e.l), _np_compile(e.r)
+        if e.op == "/":
+            def div(cols):
+                lf = np.asarray(fl(cols), dtype=np.float64)
+                rf = np.asarray(fr_(cols), dtype=np.float64)
+                with np.errstate(divide="ignore", invalid="ignore"):
+                    out = lf / rf
+                return np.where(rf == 0, np.nan, out)      # x / 0 is NULL in Spark SQL
+            return div
+        t = base(typeof(e))
+        if t not in _INT_T and t not in ("double", "float"):
+            raise _NoFast
+        op = {"+": np.add, "-": np.subtract, "*": np.multiply}[e.op]
+        is_int = t in _INT_T
+
+        def arith(cols):
+            l, r = fl(cols), fr_(cols)
+            if is_int and ((isinstance(l, np.ndarray) and l.dtype.kind == "f") or
+                           (isinstance(r, np.ndarray) and r.dtype.kind == "f")):
+                raise _NoFast
+            return op(l, r)
+        return arith
+    if isinstance(e, A.Call) and e.name == "round" and not e.is_agg:
+        f = _np_compile(e.args[0])
+        d = 0
+        if len(e.args) > 1:
+            a1 = e.args[1]
+            a1 = a1.child if isinstance(a1, A.Alias) else a1
+            if not isinstance(a1, A.Lit) or isinstance(a1.value, bool) or not isinstance(a1.value, (int, float)):
+                raise _NoFast
+            d = int(a1.value)
+        from .functions import _half_up_np
+
+        def rnd(cols):
+            x = f(cols)
+            if not isinstance(x, np.ndarray):
+                raise _NoFast
+            if x.dtype.kind in "iu":
+                if d >= 0:
+                    return x
+                raise _NoFast
+            return _half_up_np(x, d)
+        return rnd
+    raise _NoFast
+
+
 def _conform(s: pd.Series, t: str) -> pd.Series:
     want = pandas_dtype(t)
     if want == "string" and isinstance(s.dtype, pd.CategoricalDtype):
@@ -380,11 +504,11 @@ def druid_value_series(col, sqlt: str, kind: str, n: int) -> pd.Series:
         return to_series(ts, sqlt)
     bt = base(sqlt)
     if arr.dtype.kind in "fiu" and bt in ("double", "float", "decimal"):
-        return pd.Series(arr.astype(np.float64, copy=False))       # numpy float64: NaN == NULL
+        return fast_series(arr.astype(np.float64, copy=False))       # numpy float64: NaN == NULL
     if arr.dtype.kind in "iu" and bt in ("tinyint", "smallint", "int", "bigint"):
         if arr.dtype == np.int32 and bt != "bigint":
-            return pd.Series(arr)  # 32-bit SQL ints stay 32-bit (no widening pass)
-        return pd.Series(arr.astype(np.int64, copy=False))
+            return fast_series(arr)  # 32-bit SQL ints stay 32-bit (no widening pass)
+        return fast_series(arr.astype(np.int64, copy=False))
     if arr.dtype.kind == "f" and bt in ("tinyint", "smallint", "int", "bigint"):
         if not np.isnan(arr).any():
             return pd.Series(np.rint(arr).astype(np.int64))
@@ -431,15 +555,18 @@ def _dict_series(col, sqlt: str) -> pd.Series:
         if bt == "string":
             cats, has_null = full
             c = codes.astype(np.int32, copy=False) - (1 if has_null else 0) if has_null else codes
-            return pd.Series(pd.Categorical.from_codes(c, categories=cats, validate=False))
+            cdt = cache.get("__cdtype__")
+            if cdt is None:
+                cdt = cache["__cdtype__"] = pd.CategoricalDtype(cats)
+            return fast_series(pd.Categorical.from_codes(c, dtype=cdt, validate=False))
         if full[0] == "numpy":
-            return pd.Series(full[1][codes])
+            return fast_series(full[1][codes])
         return pd.Series(full[1].array.take(codes))
     if hasattr(d, "start") and not getattr(d, "has_null", False) and not hasattr(d, "prefix"):
         # integer range dictionary: value = start + code
         vals = d.decode(codes)
         if base(sqlt) in ("tinyint", "smallint", "int", "bigint"):
-            return pd.Series(vals.astype(np.int64, copy=False))
+            return fast_series(vals.astype(np.int64, copy=False))
         return to_series(pd.Series(vals), sqlt)
     inv, uniq = pd.factorize(codes)
     typed = to_series(_raw(d.decode(np.asarray(uniq, dtype=np.int64))), sqlt)

@@ -214,6 +214,35 @@ def broadcast(x, n: int, t: str) -> pd.Series:
     return pd.Series([x] * n, dtype=pandas_dtype(t)) if x is not None else pd.Series([None] * n, dtype=pandas_dtype(t))
 
 
+def fast_series(arr) -> pd.Series:
+    """``pd.Series(arr)`` for a numpy array or pandas ExtensionArray without pandas' input
+    sanitising (about half the construction cost; result columns of small queries are built many
+    times per second).  Falls back to the public constructor if the internal API moves."""
+    try:
+        n = len(arr)
+        idx = _RANGES.get(n)
+        if idx is None:
+            idx = pd.RangeIndex(n)
+            if n <= 4096:  # immutable, shared by every small result column of that length
+                if len(_RANGES) > 256:
+                    _RANGES.clear()
+                _RANGES[n] = idx
+        mgr = _SBM.from_array(arr, idx)
+        out = pd.Series._from_mgr(mgr, mgr.axes)
+        out._name = None
+        return out
+    except Exception:  # pragma: no cover - pandas internals changed
+        return pd.Series(arr)
+
+
+_RANGES: dict = {}
+
+try:
+    from pandas.core.internals import SingleBlockManager as _SBM
+except ImportError:  # pragma: no cover
+    _SBM = None
+
+
 def to_series(values, t: str) -> pd.Series:
     """Build a typed Series from raw values (numpy / list / Series)."""
     pdt = pandas_dtype(t)
