@@ -23,14 +23,10 @@ from ..ops import native
 from .lower import ScanProgram, pack
 from .partials import Partials
 
-LDS_BUDGET = int(os.environ.get("SDO_LDS_BUDGET", 64 * 1024))
+from ..planner.cost import PLAN_LDS_BUDGET as LDS_BUDGET  # noqa: E402  (single source: the cost model)
 # one accumulator table per workgroup (JIT only) for key spaces whose per-wave copies do not fit:
 # up to this many bytes of LDS, instead of HBM atomics contending on the touched groups
-SHARED_LDS_MAX = int(os.environ.get("SDO_SHARED_LDS_MAX", 112 * 1024))
-SHARED_MIN_GROUPS = int(os.environ.get("SDO_SHARED_MIN_GROUPS", 512))
-DENSE_GLOBAL_MAX_BYTES = int(os.environ.get("SDO_DENSE_MAX_BYTES", 1 << 30))
-# dense HBM tables of at least this many groups keep a first-touch byte table (see PreparedScan.run)
-TOUCH_MIN_G = int(os.environ.get("SDO_TOUCH_MIN_G", 1 << 20))
+from ..planner.cost import SHARED_LDS_MAX  # noqa: E402,F401
 BLOCK = 512
 UNROLL = int(os.environ.get("SDO_UNROLL", "2"))
 BLOCKS_PER_CU = int(os.environ.get("SDO_BLOCKS_PER_CU", "3"))
@@ -107,28 +103,15 @@ class PreparedScan:
         self.hll_lds = 0
         self.shared = False
         shared_bytes = G * ns * 8
+        # the cost model decides the group-by table (planner/cost.py plan_groupby): LDS copies /
+        # shared LDS table / HBM table (with first-touch or presence byte tables) / hash table
+        from ..planner.cost import plan_groupby
+
+        self.plan = plan_groupby(prog, USE_JIT, dense_max is not None)
         if mode is None:
-            if USE_JIT and not prog.empty and G > SHARED_MIN_GROUPS and shared_bytes <= SHARED_LDS_MAX \
-                    and not prog.nhll:
-                # hundreds+ of groups: one shared LDS table per workgroup beats per-wave copies
-                # (SSB TopN brand, 1000 groups: 2.8 -> 1.2 ms) -- fewer LDS bytes, more workgroups
-                mode = D.M_DENSE_LDS
-                self.shared = True
-            elif acc_bytes + hll_bytes <= LDS_BUDGET:
-                mode = D.M_DENSE_LDS
-                self.hll_lds = 1 if prog.nhll else 0
-            elif acc_bytes <= LDS_BUDGET // 2 and hll_bytes <= DENSE_GLOBAL_MAX_BYTES:
-                mode = D.M_DENSE_LDS
-            elif USE_JIT and not prog.empty and shared_bytes <= SHARED_LDS_MAX \
-                    and hll_bytes <= DENSE_GLOBAL_MAX_BYTES:
-                mode = D.M_DENSE_LDS
-                self.shared = True
-            elif (acc_bytes + hll_bytes <= DENSE_GLOBAL_MAX_BYTES) if dense_max is None else \
-                    (G * ns * 8 + hll_bytes <= dense_max):
-                # one HBM table indexed by the packed key (dense_max: real table bytes, one GPU)
-                mode = D.M_DENSE_GLOBAL
-            else:
-                mode = D.M_HASH
+            mode = {"dense-lds": D.M_DENSE_LDS, "dense-global": D.M_DENSE_GLOBAL, "hash": D.M_HASH}[self.plan.mode]
+            self.shared = self.plan.shared
+            self.hll_lds = 1 if self.plan.hll_lds else 0
         self.mode = mode
         self.dedup = 1 if G <= 64 else 0
         if mode == D.M_DENSE_LDS:
@@ -144,15 +127,12 @@ class PreparedScan:
         self.jit = None
         # existence-only dense HBM scan on one GPU: one byte per group (150M order groups -> 150 MB,
         # which stays in the 256 MB Infinity Cache) instead of an 8-byte counter row
-        self.pres_bytes = bool(USE_JIT and dense_max is not None and mode == D.M_DENSE_GLOBAL and
-                               getattr(prog, "presence_only", False) and prog.nslots == 1 and not prog.nhll
-                               and not prog.empty and not os.environ.get("SDO_NO_PRES_BYTES"))
+        self.pres_bytes = bool(mode == D.M_DENSE_GLOBAL and self.plan.presence_bytes)
         prog.presence_bytes = self.pres_bytes
         # large dense HBM table (TPC-H Q3: 150M order groups, ~1M touched): a first-touch byte per
         # group written by the scan; compaction reads G bytes instead of G x nslots x 8, and only
         # the touched rows are re-initialised after the run (no full-table fill per execution)
-        self.touch = bool(USE_JIT and mode == D.M_DENSE_GLOBAL and not self.pres_bytes and not prog.nhll
-                          and not prog.empty and G >= TOUCH_MIN_G and not os.environ.get("SDO_NO_TOUCH"))
+        self.touch = bool(mode == D.M_DENSE_GLOBAL and self.plan.touch and not self.pres_bytes)
         prog.touch_table = self.touch
         if not prog.empty:
             # the JIT keeps LDS registers one byte each (hll_update8)

@@ -121,8 +121,9 @@ class PreparedQuery:
             # (TPC-H Q18: 150M order groups); with several ranks dense partials are reduced whole,
             # so huge key spaces stay sparse (hash) and merge by present keys
             local = not self.world.distributed or (self.window is not None and prog is not self._full_prog)
-            dense_max = int(os.environ.get("SDO_DENSE_MAX_1GPU", 16 << 30)) if local else None
-            return PreparedScan(prog, dense_max=dense_max)
+            from ..planner.cost import DENSE_MAX_1GPU
+
+            return PreparedScan(prog, dense_max=DENSE_MAX_1GPU if local else None)
         return None
 
     def _prepare_mask(self, prog: ScanProgram):

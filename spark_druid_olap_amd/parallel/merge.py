@@ -1,6 +1,8 @@
 """Cross-GPU merge of partial aggregates (the reference's broker merge / Spark shuffle +
 final aggregate, ``asd/PostAggregate.scala:39-103``, re-designed for RCCL over xGMI).
 
+The path is the cost model's (``planner/cost.py plan_merge``), priced from the state's layout:
+
 * Small dense states (the common OLAP case: Q1 is 6 groups) are latency-bound: ONE
   ``all_gather_into_tensor`` of the packed state (accumulators + HLL registers as int64 words)
   followed by a local per-slot reduction -- one collective instead of one per reduce-op.
@@ -26,7 +28,6 @@ from ..ops import desc as D
 from .fault import STATUS_FAILED, STATUS_OK, raise_if_failed
 from .world import World
 
-ONE_SHOT_BYTES = 4 << 20
 
 
 def _reduce_stacked(prog, acc_all: torch.Tensor) -> torch.Tensor:
@@ -99,7 +100,8 @@ def merge_partials(world: World, prog, part: Partials, disjoint_keys: bool = Fal
             raise local_error
         return part
     status = STATUS_FAILED if local_error is not None else STATUS_OK
-    if part.kind == "dense" and dense_state_bytes(part) * world.size <= ONE_SHOT_BYTES:
+    plan = merge_plan_for(world, part, disjoint_keys)
+    if plan.kind == "oneshot-allgather":
         R, ns = part.acc.shape
         st = torch.full((1,), status, dtype=torch.int64, device=part.acc.device)
         pieces = [part.acc.reshape(-1)] + [h.reshape(-1).to(torch.int64) for h in part.hll] + [st]
@@ -117,13 +119,22 @@ def merge_partials(world: World, prog, part: Partials, disjoint_keys: bool = Fal
             hll.append(g[:, off: off + n].amax(dim=0).to(torch.int32).reshape(h.shape))
             off += n
         return Partials("dense", acc, None, hll)
-    if part.kind == "dense":
+    if plan.kind == "bucketed-allreduce":
         return _merge_dense_bucketed(world, prog, part, status, local_error)
     # sparse
     sp = part.compact()
     if disjoint_keys:
         return _gather_disjoint(world, sp, status, local_error)
     return _merge_sparse_shuffle(world, prog, sp, status, local_error)
+
+
+def merge_plan_for(world: World, part: Partials, disjoint_keys: bool = False):
+    """The cost model's merge choice (planner/cost.py plan_merge) for these partials: decided from
+    the layout only, so every rank takes the same collective path."""
+    from ..planner.cost import plan_merge
+
+    return plan_merge(part.kind == "dense", dense_state_bytes(part) if part.kind == "dense" else 0, world.size,
+                      disjoint_keys)
 
 
 def dense_state_bytes(part: Partials) -> int:

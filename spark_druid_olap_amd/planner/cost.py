@@ -17,8 +17,9 @@ kernel, so the decisions are different, but the estimation machinery is the same
 from __future__ import annotations
 
 import math
-from dataclasses import dataclass
-from typing import List, Optional
+import os
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
 
 from ..query import spec as S
 from ..query.intervals import Interval
@@ -166,12 +167,30 @@ def estimate(ds, spec, info=None, world_size: int = 1) -> CostEstimate:
 def explain_cost(session, dq) -> str:
     ds = dq.relation.info.datasource
     c = estimate(ds, dq.spec, dq.relation.info, session.engine.world.size)
-    return "\n".join([
+    lines = [
         "DruidQuery cost ::",
         f"  rowsInInterval={c.rows_in_interval}  selectivity={c.selectivity:.4g}  inputRows={c.input_rows:.4g}",
-        f"  outputRows={c.output_rows:.4g}  bytesScanned={c.bytes_scanned}  groupBy={c.groupby_mode}",
-        f"  merge={c.merge}  estScanMs={c.scan_ms:.4f}  estMergeMs={c.merge_ms:.4f}  gpus={session.engine.world.size}",
-    ])
+        f"  outputRows={c.output_rows:.4g}  bytesScanned={c.bytes_scanned}",
+        f"  estScanMs={c.scan_ms:.4f}  estMergeMs={c.merge_ms:.4f}  gpus={session.engine.world.size}",
+    ]
+    prep = getattr(dq, "_prepared", None)
+    if prep is None:
+        try:  # plan it now (EXPLAIN before the first execution)
+            prep = session.engine.prepare(dq.spec, ds, dq.info.get("historical"))
+        except Exception:  # noqa: BLE001
+            prep = None
+    w = session.engine.world
+    for _, prog, ps in getattr(prep, "scans", []) or []:
+        gp = getattr(ps, "plan", None)
+        if gp is None and hasattr(prog, "nslots"):
+            gp = plan_groupby(prog, True, not w.distributed)
+        if gp is not None:
+            lines.append(f"  execution: groupBy={gp.describe()}")
+            if w.distributed:
+                dense = gp.mode != "hash" and not gp.touch and not gp.presence_bytes
+                mp = plan_merge(dense, prog.G * prog.nslots * 8 + prog.nhll * prog.G * (8 << prog.hll_p), w.size)
+                lines.append(f"  execution: merge={mp.describe()}")
+    return "\n".join(lines)
 
 
 def historical_cost_ms(ds, spec, segments_per_query: int, info=None) -> float:
@@ -204,3 +223,120 @@ def choose_method(ds, spec, conf=None, info=None):
         if h < broker and (best is None or h < best[0]):
             best = (h, n)
     return None if best is None else best[1]
+
+
+# ================================================================================================
+# Execution planning: the decisions the engine takes per prepared query come from here (the GPU
+# analogue of the reference's broker-vs-historical / segments-per-query choice,
+# ``asd/DruidQueryCostModel.scala:343-413, 724-829``).  Feasibility limits are device facts (LDS per
+# CU, table budgets); between feasible alternatives the cheaper estimate wins.
+# ------------------------------------------------------------------------------------------------
+BLOCK_WAVES = 8                                             # 512-thread workgroups
+PLAN_LDS_BUDGET = int(os.environ.get("SDO_LDS_BUDGET", 64 * 1024))
+SHARED_LDS_MAX = int(os.environ.get("SDO_SHARED_LDS_MAX", 112 * 1024))
+SHARED_MIN_GROUPS = int(os.environ.get("SDO_SHARED_MIN_GROUPS", 512))
+DENSE_MAX_MULTI = int(os.environ.get("SDO_DENSE_MAX_BYTES", 128 << 20))     # dense partials merged whole
+DENSE_MAX_SPARSE_MULTI = int(os.environ.get("SDO_DENSE_MAX_SPARSE", 4 << 30))  # touched rows only
+DENSE_MAX_1GPU = int(os.environ.get("SDO_DENSE_MAX_1GPU", 16 << 30))
+TOUCH_MIN_G = int(os.environ.get("SDO_TOUCH_MIN_G", 1 << 20))
+PROBE_S = 1.0e-9        # hash-table insert (CAS probe + key compare) per qualifying row
+ONESHOT_MAX_BYTES = 256 << 20   # gather buffer (world x state) ceiling for the one-shot merge
+
+
+@dataclass
+class GroupByPlan:
+    mode: str                      # dense-lds | dense-global | hash
+    shared: bool = False           # one LDS table per workgroup (else one copy per wave)
+    hll_lds: bool = False          # HLL registers in LDS
+    touch: bool = False            # first-touch byte table (dense-global)
+    presence_bytes: bool = False   # existence-only byte table (dense-global)
+    costs: Dict[str, float] = field(default_factory=dict)   # priced alternatives, ms
+    reason: str = ""
+
+    def describe(self) -> str:
+        extra = [k for k in ("shared", "hll_lds", "touch", "presence_bytes") if getattr(self, k)]
+        alts = "  ".join(f"{k}={v:.3f}ms" for k, v in sorted(self.costs.items(), key=lambda kv: kv[1]))
+        return f"{self.mode}{'(' + ','.join(extra) + ')' if extra else ''} [{self.reason}] {alts}"
+
+
+def plan_groupby(prog, jit: bool, local: bool) -> GroupByPlan:
+    """Group-by table for one lowered program on one shard.
+
+    ``local``: the partials stay on this GPU (one rank, or a shard-local key window), so a dense HBM
+    table may be as large as ``DENSE_MAX_1GPU``.  Across ranks dense partials that are merged whole
+    are capped at ``DENSE_MAX_MULTI``; tables whose partials come back sparse (first-touch /
+    presence byte tables) at ``DENSE_MAX_SPARSE_MULTI``."""
+    G, ns = prog.G, prog.nslots
+    m = 1 << prog.hll_p
+    per_wave = G * ns * 8 * BLOCK_WAVES
+    hll_bytes = prog.nhll * G * m * 4
+    shared_bytes = G * ns * 8
+    empty = bool(prog.empty)
+    if jit and not empty and G > SHARED_MIN_GROUPS and shared_bytes <= SHARED_LDS_MAX and not prog.nhll:
+        return GroupByPlan("dense-lds", shared=True, reason=f"{G} groups: one LDS table per workgroup")
+    if per_wave + hll_bytes <= PLAN_LDS_BUDGET:
+        return GroupByPlan("dense-lds", hll_lds=bool(prog.nhll), reason="per-wave LDS copies")
+    if per_wave <= PLAN_LDS_BUDGET // 2 and hll_bytes <= DENSE_MAX_MULTI:
+        return GroupByPlan("dense-lds", reason="per-wave LDS copies, HLL registers in HBM")
+    if jit and not empty and shared_bytes <= SHARED_LDS_MAX and hll_bytes <= DENSE_MAX_MULTI:
+        return GroupByPlan("dense-lds", shared=True, reason="shared LDS table")
+    # HBM table vs hash table: priced
+    presence = bool(jit and local and getattr(prog, "presence_only", False) and ns == 1 and not prog.nhll
+                    and not empty and not os.environ.get("SDO_NO_PRES_BYTES"))
+    touch = bool(jit and not presence and not prog.nhll and not empty and G >= TOUCH_MIN_G
+                 and not os.environ.get("SDO_NO_TOUCH"))
+    table = G * ns * 8 + hll_bytes
+    if local:
+        limit = DENSE_MAX_1GPU
+    else:
+        limit = DENSE_MAX_SPARSE_MULTI if (touch or presence) else DENSE_MAX_MULTI
+    est_rows = max(1.0, float(getattr(prog, "est_rows", G)))
+    costs = {}
+    if table <= limit:
+        if presence:
+            dense = 2 * G / HBM_BW
+        elif touch:
+            touched = min(G, est_rows)
+            dense = (2 * G + touched * ns * 8 * 2) / HBM_BW
+        else:
+            dense = 2 * table / HBM_BW
+        costs["dense-global"] = dense * 1e3
+    cap = 1 << max(10, math.ceil(math.log2(max(2.0, 2 * (min(G, est_rows * 1.2) + 1024)))))
+    costs["hash"] = (2 * cap * (8 + ns * 8) / HBM_BW + est_rows * PROBE_S) * 1e3
+    if "dense-global" in costs and costs["dense-global"] <= costs["hash"]:
+        return GroupByPlan("dense-global", touch=touch, presence_bytes=presence, costs=costs,
+                           reason="HBM table indexed by the packed key")
+    why = "table over budget" if "dense-global" not in costs else "few qualifying rows for the key space"
+    return GroupByPlan("hash", costs=costs, reason=why)
+
+
+@dataclass
+class MergePlan:
+    kind: str                      # none | oneshot-allgather | bucketed-allreduce | alltoall-shuffle | disjoint-concat
+    costs: Dict[str, float] = field(default_factory=dict)
+
+    def describe(self) -> str:
+        alts = "  ".join(f"{k}={v:.3f}ms" for k, v in sorted(self.costs.items(), key=lambda kv: kv[1]))
+        return f"{self.kind} {alts}"
+
+
+def plan_merge(dense: bool, state_bytes: int, world_size: int, disjoint: bool = False) -> MergePlan:
+    """Cross-GPU merge of one query's partials.  Inputs must be identical on every rank (layout
+    sizes, never local row counts) so every rank takes the same collective path.
+
+    * dense state: one all-gather of the whole state + local reduction (latency-bound, every peer
+      read over its own xGMI link) vs a bucketed ring all-reduce (bandwidth-optimal, three
+      collectives); the one-shot gather buffer is capped at ``ONESHOT_MAX_BYTES``;
+    * sparse state: concatenation when the groups are disjoint across ranks (grouped on the shard
+      key), else the hash-partitioned all-to-all shuffle."""
+    n = world_size
+    if n <= 1:
+        return MergePlan("none")
+    if not dense:
+        return MergePlan("disjoint-concat" if disjoint else "alltoall-shuffle")
+    b = float(state_bytes)
+    costs = {}
+    if b * n <= ONESHOT_MAX_BYTES:
+        costs["oneshot-allgather"] = (COLL_LAT_S + b * (n - 1) / (min(7, n - 1) * XGMI_LINK_BW) + n * b / HBM_BW) * 1e3
+    costs["bucketed-allreduce"] = (3 * COLL_LAT_S + 2 * b * (n - 1) / n / XGMI_LINK_BW) * 1e3
+    return MergePlan(min(costs, key=costs.get), costs)

@@ -1,0 +1,90 @@
+"""The GPU cost model drives execution (planner/cost.py): group-by table choice per shard, the
+cross-GPU merge path, and broker vs historical -- priced alternatives, with the decision visible in
+EXPLAIN DRUID REWRITE (the reference's DruidQueryCostModel, asd/DruidQueryCostModel.scala:343-413,
+724-829, whose decisions are broker/historical and segments per query)."""
+import types
+
+import pytest
+
+from spark_druid_olap_amd.planner import cost
+
+
+def _prog(G, ns=2, nhll=0, est_rows=None, presence=False, empty=False, hll_p=11):
+    return types.SimpleNamespace(G=G, nslots=ns, nhll=nhll, hll_p=hll_p, est_rows=est_rows if est_rows is not None else G,
+                                 presence_only=presence, empty=empty)
+
+
+def test_small_key_space_uses_per_wave_lds_copies():
+    p = cost.plan_groupby(_prog(6, ns=4, nhll=1), jit=True, local=True)
+    assert p.mode == "dense-lds" and not p.shared and p.hll_lds
+
+
+def test_thousand_groups_use_one_shared_lds_table():
+    p = cost.plan_groupby(_prog(1000, ns=3), jit=True, local=True)
+    assert p.mode == "dense-lds" and p.shared
+    # without the JIT (interpreter kernel) there is no shared-table variant
+    assert not cost.plan_groupby(_prog(1000, ns=3), jit=False, local=True).shared
+
+
+def test_huge_key_space_on_one_gpu_is_a_touch_table():
+    # TPC-H Q3 at SF100: 150M order groups, ~30M qualifying rows
+    p = cost.plan_groupby(_prog(150_000_000, ns=2, est_rows=30e6), jit=True, local=True)
+    assert p.mode == "dense-global" and p.touch
+    assert p.costs["dense-global"] < p.costs["hash"]
+
+
+def test_selective_query_over_huge_key_space_prefers_hash():
+    # a few thousand qualifying rows: a 2 GB table to reset and compact costs more than a small hash table
+    p = cost.plan_groupby(_prog(150_000_000, ns=2, est_rows=2000), jit=True, local=True)
+    assert p.mode == "hash" and p.costs["hash"] < p.costs["dense-global"]
+
+
+def test_across_ranks_dense_tables_are_capped_unless_partials_come_back_sparse():
+    big = _prog(150_000_000, ns=2, est_rows=30e6)
+    assert cost.plan_groupby(big, jit=True, local=False).mode == "dense-global"   # touch -> sparse partials
+    hll = _prog(20_000_000, ns=2, nhll=1, est_rows=30e6)
+    assert cost.plan_groupby(hll, jit=True, local=False).mode == "hash"           # would be merged whole
+    assert cost.plan_groupby(big, jit=False, local=False).mode == "hash"          # no touch table without the JIT
+
+
+def test_presence_only_scan_uses_a_byte_table_on_one_gpu():
+    p = cost.plan_groupby(_prog(150_000_000, ns=1, presence=True), jit=True, local=True)
+    assert p.mode == "dense-global" and p.presence_bytes and not p.touch
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_merge_plan(n):
+    assert cost.plan_merge(True, 288, 1).kind == "none"
+    small = cost.plan_merge(True, 288, n)               # Q1: 6 groups x 6 slots
+    assert small.kind == "oneshot-allgather" and small.costs["oneshot-allgather"] < small.costs["bucketed-allreduce"]
+    huge = cost.plan_merge(True, 512 << 20, n)          # a gather buffer of n x 512 MB is not allowed
+    assert huge.kind == "bucketed-allreduce" and "oneshot-allgather" not in huge.costs
+    assert cost.plan_merge(False, 0, n).kind == "alltoall-shuffle"
+    assert cost.plan_merge(False, 0, n, disjoint=True).kind == "disjoint-concat"
+
+
+def test_engine_takes_the_planned_mode_and_explain_shows_it(ds_small, df_small):
+    """PreparedScan's mode is the cost model's (checked without a GPU by planning the lowered
+    program the engine prepares) and EXPLAIN DRUID REWRITE prints the priced plan."""
+    from spark_druid_olap_amd.engine.executor import Engine
+    from spark_druid_olap_amd.models import tpch
+    from spark_druid_olap_amd.session import Session
+
+    s = Session(engine=Engine(use_native=False))
+    s.register_datasource(ds_small)
+    s.register_table("orderLineItemPartSupplierBase", df_small, schema=tpch.FLAT_SCHEMA)
+    s.sql(tpch.druid_ddl(with_column_mapping=False))
+    d = s.sql("select l_returnflag, count(*) from orderLineItemPartSupplier group by l_returnflag")
+    prog = d.druid_queries()[0]
+    rows = s.sql("explain druid rewrite select l_returnflag, count(*) from orderLineItemPartSupplier "
+                 "group by l_returnflag").collect()
+    text = "\n".join(str(r[0]) for r in rows)
+    assert "DruidQuery cost" in text and "execution: groupBy=dense-lds" in text
+
+
+def test_historical_is_chosen_only_when_cheaper(ds_small):
+    from spark_druid_olap_amd.query import spec as S
+
+    q = S.GroupByQuerySpec("tpch", [S.DefaultDimensionSpec("l_returnflag")],
+                           aggregations=[S.FunctionAggregationSpec("count", "c")], intervals=["1992-01-01/1999-01-01"])
+    assert cost.choose_method(ds_small, q) is None      # one fused scan beats batched launches + merge

@@ -92,12 +92,12 @@ def test_device_typed_key_decode_matches_host_decode(sessions, name):
 
 @pytest.mark.parametrize("name", ["Q3", "Q10", "Q18"])
 def test_first_touch_table_matches_reference_across_reruns(sessions, name, monkeypatch):
-    """Dense HBM group tables with the first-touch byte table (device_exec.py TOUCH_MIN_G): the
+    """Dense HBM group tables with the first-touch byte table (planner/cost.py TOUCH_MIN_G): the
     touched groups compact from the byte table and only they are re-initialised after a run, so
     re-running the prepared query (no full-table fill) must keep giving the reference answer."""
-    from spark_druid_olap_amd.engine import device_exec
+    from spark_druid_olap_amd.planner import cost
 
-    monkeypatch.setattr(device_exec, "TOUCH_MIN_G", 0)
+    monkeypatch.setattr(cost, "TOUCH_MIN_G", 0)
     nat, ref = sessions
     q = dict(tpch22.QUERIES)[name]
     s2 = Session(engine=Engine(use_native=True))

@@ -80,8 +80,11 @@ def _worker(rank, world, port, outdir):
     from spark_druid_olap_amd.parallel.fault import RankFailure
     from spark_druid_olap_amd.parallel.world import init_world, shutdown
 
+    from spark_druid_olap_amd.planner import cost
+
     w = init_world(backend="gloo")
-    merge.ONE_SHOT_BYTES = 0          # force the large-state (bucketed all-reduce) path
+    cost.ONESHOT_MAX_BYTES = 0        # the one-shot gather is infeasible -> bucketed all-reduce path
+    assert merge.merge_plan_for(w, Partials("dense", *_partial(rank))).kind == "bucketed-allreduce"
     acc, hll = _partial(rank)
     m = merge.merge_partials(w, _Prog(), Partials("dense", acc, None, hll))
     exp_acc, exp_hll = _expected(world)

@@ -36,8 +36,9 @@ def main():
         pq.run()
         torch.cuda.synchronize()
         for _ in range(args.iters):
-            prep._reset()
-            prep._launch(prep._bufs())  # the specialized (JIT) kernel when one was built, else the interpreter
+            b = prep._bufs()
+            prep._reset(b)
+            prep._launch(b)  # the specialized (JIT) kernel when one was built, else the interpreter
         torch.cuda.synchronize()
         print("done", name, flush=True)
 
