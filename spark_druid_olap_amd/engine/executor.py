@@ -75,7 +75,9 @@ class PreparedQuery:
         self.qs = qs
         self.ds = ds
         self.world = engine.world
-        self.low = Lowerer(ds, world=engine.world)
+        ctx = getattr(qs, "context", None)
+        self.deterministic = bool(engine.deterministic or (ctx is not None and getattr(ctx, "deterministic", None)))
+        self.low = Lowerer(ds, world=engine.world, deterministic=self.deterministic)
         self.scans: List[tuple] = []  # (tag, prog, prepared)
         self.segments_per_query = segments_per_query
         self.window: Optional["ShardWindow"] = None
@@ -244,12 +246,16 @@ class PreparedQuery:
 
         def value(name):
             a = aggs.get(name)
-            if a is None or a.slot < 0 or a.kind not in ("count", "sum_i", "sum_f", "min_i", "max_i", "min_f",
-                                                         "max_f"):
+            if a is None or a.slot < 0 or a.kind not in ("count", "sum_i", "sum_f", "sum_fx", "min_i", "max_i",
+                                                         "min_f", "max_f"):
                 return None
             col = part.acc[:, a.slot]
             if a.kind == "sum_f":
                 return col.view(torch.float64)
+            if a.kind == "sum_fx":
+                from .lower import fixed_value
+
+                return fixed_value(col, part.acc[:, a.slot2])
             if a.kind in ("min_f", "max_f"):
                 return torch.where(col >= 0, col, col ^ 0x7FFFFFFFFFFFFFFF).view(torch.float64)
             v = col.to(torch.float64)
@@ -762,7 +768,8 @@ def order_and_limit(cols: Dict[str, np.ndarray], idx: np.ndarray, order_cols, li
 class Engine:
     """Executes QuerySpecs on the current rank's shards, merging across the process group."""
 
-    def __init__(self, world: Optional[World] = None, use_native: Optional[bool] = None):
+    def __init__(self, world: Optional[World] = None, use_native: Optional[bool] = None,
+                 deterministic: Optional[bool] = None):
         from ..utils.memory import tune_host_malloc
 
         tune_host_malloc()
@@ -770,6 +777,11 @@ class Engine:
         if use_native is None:
             use_native = torch.cuda.is_available()
         self.use_native = use_native
+        # bitwise reproducible float sums for every query (engine/lower.py Lowerer.deterministic);
+        # per query: context {"deterministic": true}
+        if deterministic is None:
+            deterministic = os.environ.get("SDO_DETERMINISTIC", "0") not in ("", "0")
+        self.deterministic = deterministic
         self._coalescer = None
 
     def coalescer(self, slots: Optional[int] = None):

@@ -252,8 +252,9 @@ class KeyComp:
 @dataclass
 class AggOut:
     name: str
-    kind: str                     # count|sum_i|sum_f|min_i|max_i|min_f|max_f|hll|theta
+    kind: str                     # count|sum_i|sum_f|sum_fx|min_i|max_i|min_f|max_f|hll|theta
     slot: int = -1
+    slot2: int = -1               # sum_fx: fraction slot (value = slot + slot2 * 2^-32)
     hll_index: int = -1
     scale: int = 0                # decimal digits of an exact integer sum
     out_type: str = "double"      # long|double
@@ -349,10 +350,14 @@ def column_tensor(ds: DataSource, name: str) -> torch.Tensor:
 class Lowerer:
     """QuerySpec -> ScanProgram for a datasource shard."""
 
-    def __init__(self, ds: DataSource, bitmap_max_values: int = 4, world=None):
+    def __init__(self, ds: DataSource, bitmap_max_values: int = 4, world=None, deterministic: bool = False):
         self.ds = ds
         self.bitmap_max_values = bitmap_max_values
         self.world = world
+        # floating-point sums in exact 64.32 fixed point (two integer slots) instead of f64 atomics:
+        # integer addition is associative, so per-wave LDS folds, workgroup flush atomics, segment
+        # batches and the cross-GPU merge give bitwise-identical results in any order (SURVEY 5.2)
+        self.deterministic = deterministic
         self._tv_cache: Optional[np.ndarray] = None
 
     # ------------------------------------------------------------------ filters -> IR
@@ -972,6 +977,21 @@ class Lowerer:
             prog.slots.append((op, init))
             return len(prog.slots) - 1
 
+        def fixed_sum(name, eops, out_type="double"):
+            # value v -> floor(v) (integer part) and rint((v - floor(v)) * 2^32) (fraction), each an
+            # exact integer sum; finalize returns int + frac * 2^-32.  |v| < 2^63 per row, |sum| <
+            # 2^63; per-row resolution 2^-33, the same for every order of accumulation.
+            if len(prog.aops) + 1 >= D.MAX_AOPS:
+                raise LoweringError("too many aggregators")
+            if _eops_depth(eops) + 1 > 4:
+                raise LoweringError("aggregator expression too deep for a deterministic sum")
+            hi = aop(D.A_SUM_X, -1, list(eops) + [(D.E_FLOOR, 0, 0.0)])
+            hi["slot"] = slot(D.S_SUM_I, 0, hi)
+            lo = aop(D.A_SUM_X, -1, list(eops) + list(eops) + [(D.E_FLOOR, 0, 0.0), (D.E_SUB, 0, 0.0),
+                                                                 (D.E_CONST, 0, FIX_ONE), (D.E_MUL, 0, 0.0)])
+            lo["slot"] = slot(D.S_SUM_I, 0, lo)
+            prog.aggs.append(AggOut(name, "sum_fx", hi["slot"], slot2=lo["slot"], out_type=out_type))
+
         if isinstance(a, S.FunctionAggregationSpec):
             t = a.type
             if t == "count":
@@ -1010,6 +1030,8 @@ class Lowerer:
                     d["slot"] = slot(D.S_SUM_I, 0, d)
                     prog.aggs.append(AggOut(a.name, "sum_i", d["slot"], scale=scale if not is_long else scale,
                                             out_type="long" if is_long and scale == 0 else "double"))
+                elif self.deterministic:
+                    fixed_sum(a.name, [(D.E_COL, ci, 0.0)])
                 else:
                     d = aop(D.A_SUM_F, ci)
                     d["slot"] = slot(D.S_SUM_F, 0, d)
@@ -1063,6 +1085,9 @@ class Lowerer:
                     d["slot"] = slot(D.S_SUM_I, 0, d)
                     prog.aggs.append(AggOut(a.name, "sum_i", d["slot"], scale=sc, out_type="double"))
                     return
+            if op == "sum" and self.deterministic:
+                fixed_sum(a.name, eops)
+                return
             kind = {"sum": D.A_SUM_F, "max": D.A_MAX_F, "min": D.A_MIN_F}[op]
             d = aop(kind, -1, eops)
             if op == "sum":
@@ -1360,6 +1385,28 @@ class Lowerer:
         self.emit_main_filter(prog, bexpr)
         self.pick_zones(prog, bexpr)
         return prog
+
+
+FIX_ONE = float(1 << 32)  # fixed-point unit of deterministic float sums (AggOut.kind sum_fx)
+
+
+def fixed_value(hi, lo):
+    """Value of a deterministic float sum from its integer-part and fraction slots (numpy or
+    torch int64 arrays) as float64."""
+    return hi.astype(np.float64) + lo.astype(np.float64) / FIX_ONE if isinstance(hi, np.ndarray) else \
+        hi.to(torch.float64) + lo.to(torch.float64) / FIX_ONE
+
+
+def _eops_depth(eops) -> int:
+    """Peak stack depth of a postfix expression program (the device VM keeps 4 registers)."""
+    d = peak = 0
+    for op, _, _ in eops:
+        if op in (D.E_COL, D.E_CONST, D.E_LUT):
+            d += 1
+        elif op not in D.E_UNARY:
+            d -= 1
+        peak = max(peak, d)
+    return peak
 
 
 def _ptr_as_double(ptr: int) -> float:

@@ -113,6 +113,10 @@ def device_columns(pq) -> Tuple[Dict[str, DeviceColumn], int]:
             cols[a.name] = DeviceColumn(a.name, col, scale=a.scale)
         elif a.kind == "sum_f":
             cols[a.name] = DeviceColumn(a.name, col.contiguous().view(torch.float64))
+        elif a.kind == "sum_fx":
+            from .lower import fixed_value
+
+            cols[a.name] = DeviceColumn(a.name, fixed_value(col, part.acc[:, a.slot2]))
         elif a.kind in ("min_f", "max_f"):
             cols[a.name] = DeviceColumn(a.name, torch.where(col >= 0, col, col ^ 0x7FFFFFFFFFFFFFFF).view(torch.float64))
         else:
@@ -147,6 +151,20 @@ def _torch_eval(n, pmap: Dict[str, str], cols: Dict[str, DeviceColumn]) -> torch
     return fns[k](a, b)
 
 
+def _group_sum(R: int, inv: torch.Tensor, src: torch.Tensor, deterministic: bool) -> torch.Tensor:
+    """Per-group sum of ``src`` rows (group ``inv``).  Deterministic float sums go through the same
+    64.32 fixed point as the scan (engine/lower.py fixed_sum): integer index_add is order-free."""
+    if not deterministic or src.dtype != torch.float64:
+        return torch.zeros(R, dtype=src.dtype, device=src.device).index_add_(0, inv, src)
+    from .lower import FIX_ONE, fixed_value
+
+    fl = torch.floor(src)
+    hi = torch.zeros(R, dtype=torch.int64, device=src.device).index_add_(0, inv, fl.to(torch.int64))
+    lo = torch.zeros(R, dtype=torch.int64, device=src.device).index_add_(
+        0, inv, torch.round((src - fl) * FIX_ONE).to(torch.int64))
+    return fixed_value(hi, lo)
+
+
 class NestedPreparedQuery:
     """groupBy over a query data source (see module doc)."""
 
@@ -171,6 +189,12 @@ class NestedPreparedQuery:
             if len(keep) != len(inner_q.aggregations or []) and not inner_q.postAggregations and \
                     inner_q.having is None and inner_q.limitSpec is None:
                 inner_q = inner_q.copy(aggregations=keep)
+        ctx = getattr(qs, "context", None)
+        self.deterministic = bool(engine.deterministic or (ctx is not None and getattr(ctx, "deterministic", None)))
+        if self.deterministic and not engine.deterministic:
+            ictx = getattr(inner_q, "context", None)
+            inner_q = inner_q.copy(context=ictx.copy(deterministic=True) if ictx is not None
+                                   else S.QuerySpecContext(deterministic=True))
         self.inner = engine.prepare(inner_q, ds, segments_per_query)
         for d in qs.dimensions:
             if not isinstance(d, S.DefaultDimensionSpec):
@@ -272,7 +296,7 @@ class NestedPreparedQuery:
                 if src.dim() == 0:
                     src = src.expand(n).contiguous()
                 if op == "sum":
-                    acc = torch.zeros(R, dtype=torch.float64, device=dev).index_add_(0, inv, src)
+                    acc = _group_sum(R, inv, src, self.deterministic)
                 else:
                     acc = torch.full((R,), float("inf") if op == "min" else float("-inf"), dtype=torch.float64,
                                      device=dev)
@@ -290,7 +314,7 @@ class NestedPreparedQuery:
             exact = not c.is_float and c.decode is None  # integral (scaled) values stay int64
             src = c.t if exact else (c.t.to(torch.float64) if c.decode is not None else c.as_float())
             if op == "sum":
-                acc = torch.zeros(R, dtype=src.dtype, device=dev).index_add_(0, inv, src)
+                acc = _group_sum(R, inv, src, self.deterministic)
             else:
                 if src.dtype == torch.int64:
                     init = torch.iinfo(torch.int64).max if op == "min" else torch.iinfo(torch.int64).min

@@ -10,6 +10,7 @@ import numpy as np
 import torch
 
 from ..ops import desc as D
+from .lower import fixed_value
 
 
 @dataclass
@@ -189,6 +190,8 @@ def _agg_outputs_dev(prog, acc: torch.Tensor, skip) -> Dict[str, torch.Tensor]:
                 v = col.to(torch.float64)
         elif a.kind == "sum_f":
             v = col.contiguous().view(torch.float64)
+        elif a.kind == "sum_fx":
+            v = fixed_value(col, acc[:, a.slot2])
         elif a.kind in ("min_f", "max_f"):
             v = torch.where(col >= 0, col, col ^ 0x7FFFFFFFFFFFFFFF).view(torch.float64)
             if a.out_type == "long":
@@ -388,6 +391,8 @@ def finalize(prog, parts: Partials, out_types: Optional[Dict[str, str]] = None) 
         elif a.kind == "sum_f":
             col = acc_cols[a.slot]
             cols[a.name] = col.view(np.float64) if col.flags.c_contiguous else col.copy().view(np.float64)
+        elif a.kind == "sum_fx":
+            cols[a.name] = fixed_value(np.asarray(acc_cols[a.slot]), np.asarray(acc_cols[a.slot2]))
         elif a.kind in ("min_f", "max_f"):
             v = ord2f(acc_cols[a.slot]).copy()
             if a.out_type == "long":

@@ -645,6 +645,9 @@ class QuerySpecContext(Spec, _Decodable):
     maxResults: Optional[int] = None
     maxIntermediateRows: Optional[int] = None
     groupByStrategy: Optional[str] = None
+    # engine extension: floating-point sums in exact fixed point (bitwise run-to-run reproducible
+    # under any atomic / merge order); see engine/lower.py Lowerer.deterministic
+    deterministic: Optional[bool] = None
 
 
 _BY_CLASS["QuerySpecContext"] = QuerySpecContext

@@ -325,13 +325,20 @@ class Session:
             # one page holding every row (the reference's paging loop, DruidSelectResultIterator.scala:116-137,
             # collapsed: the scan compacts on device and ships all selected rows at once)
             run_spec = spec.copy(pagingSpec=S.PagingSpec({}, 2 ** 31 - 1))
+        det = bool(self.conf.typed("spark.sparklinedata.druid.deterministic"))
+        if det:
+            ctx = getattr(run_spec, "context", None)
+            run_spec = run_spec.copy(context=ctx.copy(deterministic=True) if ctx is not None
+                                     else S.QuerySpecContext(deterministic=True))
         from .utils import trace as T
 
         prep = getattr(dq, "_prepared", None)
-        if prep is None or getattr(dq, "_prepared_spec", None) is not spec:
+        stale = lambda p: p is None or getattr(dq, "_prepared_spec", None) is not spec or \
+            getattr(p, "deterministic", False) != (det or getattr(p, "deterministic", False))  # noqa: E731
+        if stale(prep):
             with self._lock:  # concurrent sessions share cached plans: prepare once
                 prep = getattr(dq, "_prepared", None)
-                if prep is None or getattr(dq, "_prepared_spec", None) is not spec:
+                if stale(prep):
                     with T.span("sdo.lower"):
                         prep = self.engine.prepare(run_spec, ds, dq.info.get("historical"))
                     # output SQL types: large results decode numeric dictionary keys on the device
