@@ -12,6 +12,7 @@ import subprocess
 import sys
 import sysconfig
 from pathlib import Path
+from typing import Optional
 
 HERE = Path(__file__).resolve().parent
 CSRC = HERE / "csrc"
@@ -102,10 +103,12 @@ def _gateway_hash() -> str:
     return hashlib.sha256(GW_SRC.read_bytes()).hexdigest()[:16]
 
 
-def build_gateway(force: bool = False, verbose: bool = False, extra_flags=()) -> Path:
-    target = gateway_path()
+def build_gateway(force: bool = False, verbose: bool = False, extra_flags=(), out: Optional[Path] = None) -> Path:
+    """``extra_flags`` + ``out``: an instrumented variant (e.g. the host ASan build) written beside,
+    never over, the in-tree module."""
+    target = Path(out) if out is not None else gateway_path()
     stamp = target.parent / "_sdo_gateway.stamp"
-    if not force and not extra_flags and target.exists() and stamp.exists() and \
+    if not force and not extra_flags and out is None and target.exists() and stamp.exists() and \
             stamp.read_text().strip() == _gateway_hash():
         return target
     import pybind11
@@ -119,7 +122,7 @@ def build_gateway(force: bool = False, verbose: bool = False, extra_flags=()) ->
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(tmp, target)
-    if not extra_flags:
+    if not extra_flags and out is None:
         stamp.write_text(_gateway_hash())
     return target
 

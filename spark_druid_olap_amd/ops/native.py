@@ -32,6 +32,18 @@ def load(build_if_missing: bool = True):
             return _mod
         from . import build as _build
 
+        alt = os.environ.get("SDO_NATIVE_SO")
+        if alt:
+            # an instrumented build of the same module (tools/asan_host.py: host-side ASan)
+            import sys
+            from importlib import util as _ilu
+
+            name = "spark_druid_olap_amd.ops._sdo_native"
+            spec = _ilu.spec_from_file_location(name, alt)
+            _mod = _ilu.module_from_spec(spec)
+            spec.loader.exec_module(_mod)
+            sys.modules[name] = _mod
+            return _mod
         if not _build.target_path().exists():
             if not build_if_missing:
                 raise NativeUnavailable(f"native extension missing: {_build.target_path()}")

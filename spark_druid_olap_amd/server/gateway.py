@@ -39,7 +39,20 @@ log = logging.getLogger("sdo.gateway")
 
 
 def load_native():
-    """The compiled gateway module (built in-tree by ops/build.py:build_gateway)."""
+    """The compiled gateway module (built in-tree by ops/build.py:build_gateway).  ``SDO_GATEWAY_SO``
+    names an alternative build of the same module (the host ASan/UBSan build of tools/asan_host.py)."""
+    alt = os.environ.get("SDO_GATEWAY_SO")
+    if alt:
+        import sys
+        from importlib import util as _ilu
+
+        name = "spark_druid_olap_amd.server._sdo_gateway"
+        if name not in sys.modules:
+            spec = _ilu.spec_from_file_location(name, alt)
+            mod = _ilu.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            sys.modules[name] = mod
+        return sys.modules[name]
     try:
         return importlib.import_module("spark_druid_olap_amd.server._sdo_gateway")
     except ImportError:
