@@ -138,6 +138,13 @@ class PreparedQuery:
     def _placeholder(self, prog, prep) -> Partials:
         """Layout-compatible empty partials for a rank whose scan failed (same collective pattern as
         its peers, so the failure can be agreed on inside the merge)."""
+        part = self._placeholder_scan(prog, prep)
+        m = 1 << prog.hll_p
+        extra = [torch.zeros((part.rows, m), dtype=torch.int32, device=self.ds.device)
+                 for _ in range(prog.nhll_total - len(part.hll))]
+        return Partials(part.kind, part.acc, part.keys, list(part.hll) + extra) if extra else part
+
+    def _placeholder_scan(self, prog, prep) -> Partials:
         dev = self.ds.device
         m = 1 << prog.hll_p
         if self.window is not None:
@@ -161,10 +168,56 @@ class PreparedQuery:
 
         FAULTS.maybe_fail("scan", self.world.rank)
         if prep is not None:
-            return prep.run()
-        from ..ops.reference import run_reference
+            part = prep.run()
+        else:
+            from ..ops.reference import run_reference
 
-        return run_reference(prog)
+            part = run_reference(prog)
+        if prog.stored_hll:
+            part = self._merge_stored_hll(prog, part)
+        return part
+
+    def _merge_stored_hll(self, prog, part: Partials) -> Partials:
+        """Registers of hyperUnique aggregators over rolled-up sketch metrics: the stored sparse
+        sketches of every selected row are unioned into its group's registers (sketch.hip
+        hll_merge_stored on the GPU; a torch scatter-max on the CPU).  Appended after the scan's own
+        HLL blocks, so merge / estimate / finalize treat them like query-time cardinality."""
+        from ..ops.reference import _rows, compute_keys, eval_bexpr
+
+        dev = self.ds.device
+        m = 1 << prog.hll_p
+        rows = _rows(prog) if not prog.empty else torch.zeros(0, dtype=torch.int64, device=dev)
+        if rows.numel():
+            rows = rows[eval_bexpr(prog, prog.bexpr, rows)]
+        keys = compute_keys(prog, rows)
+        if part.kind == "dense":
+            slot = keys
+        else:  # group key -> row of the sparse partials
+            order = torch.argsort(part.keys)
+            pos = torch.searchsorted(part.keys[order], keys).clamp_(max=max(0, part.rows - 1))
+            slot = order[pos] if part.rows else torch.full_like(keys, -1)
+        hll = list(part.hll)
+        for name, metric, filt in prog.stored_hll:
+            sk = self.ds.metrics[metric].sketch
+            regs = torch.zeros((part.rows, m), dtype=torch.int32, device=dev)
+            r, g = rows, slot
+            if filt is not None and rows.numel():
+                keep = eval_bexpr(prog, filt, rows)
+                r, g = rows[keep], slot[keep]
+            if regs.is_cuda and self.engine.use_native:
+                from ..ops import native
+
+                native.hll_merge_stored(regs, r, g, sk.offsets, sk.values, prog.hll_p)
+            elif r.numel():
+                lo, hi = sk.offsets[r], sk.offsets[r + 1]
+                cnt = hi - lo
+                gi = torch.repeat_interleave(g, cnt)
+                first = torch.repeat_interleave(lo - (torch.cumsum(cnt, 0) - cnt), cnt)
+                pk = sk.values[torch.arange(int(cnt.sum()), device=dev) + first].to(torch.int64)
+                flat = regs.view(-1)
+                flat.scatter_reduce_(0, gi * m + ((pk >> 8) & (m - 1)), (pk & 0xFF).to(torch.int32), reduce="amax")
+            hll.append(regs)
+        return Partials(part.kind, part.acc, part.keys, hll)
 
     def _merged(self, prog, prep) -> Partials:
         if not self.world.distributed:
@@ -336,36 +389,41 @@ class PreparedQuery:
 
     # ------------------------------------------------------------------ theta sketches
     def _theta(self, prog: ScanProgram, cols: Dict[str, np.ndarray]) -> None:
+        """thetaSketch aggregators (KMV, k = size): per group the k smallest distinct 62-bit hashes of
+        the selected rows -- from the rows' value hashes, or from the rows' stored sketches when the
+        metric was rolled up at ingest -- selected by a device radix sort; ranks exchange their
+        per-group candidates (all-gather) and re-select.  Estimate = (k-1) / (h_k / 2^62), or the
+        exact distinct count below k hashes."""
         if not prog.thetas:
             return
-        from ..ops.reference import _rows, compute_keys, eval_bexpr, mix64
+        from ..ops.reference import _rows, compute_keys, eval_bexpr
+        from ..segment.ingest import theta_hash
 
         ds = self.ds
-        rows = _rows(prog) if not prog.empty else torch.zeros(0, dtype=torch.int64, device=ds.device)
+        dev = ds.device
+        rows = _rows(prog) if not prog.empty else torch.zeros(0, dtype=torch.int64, device=dev)
         if rows.numel():
             rows = rows[eval_bexpr(prog, prog.bexpr, rows)]
         keys = compute_keys(prog, rows)
-        gid_order = cols["__gid__"]
+        gid_order = np.asarray(cols["__gid__"], dtype=np.int64)
         for name, col, size in prog.thetas:
             from .lower import column_tensor
 
-            v = column_tensor(ds, col)[rows].to(torch.int64)
-            h = mix64(v ^ 0x5BD1E995) & ((1 << 62) - 1)
-            pairs = torch.unique(torch.stack([keys, h], dim=1), dim=0) if rows.numel() else torch.zeros((0, 2), dtype=torch.int64, device=ds.device)
-            # per-group k smallest hashes (KMV); union across ranks then re-select
-            pairs = _kmv(pairs, size)
+            m = ds.metrics.get(col)
+            if m is not None and m.sketch is not None:
+                sk = m.sketch
+                lo, hi = sk.offsets[rows], sk.offsets[rows + 1]
+                cnt = hi - lo
+                g = torch.repeat_interleave(keys, cnt)
+                first = torch.repeat_interleave(lo - (torch.cumsum(cnt, 0) - cnt), cnt)
+                h = sk.values[torch.arange(int(cnt.sum()), device=dev) + first]
+            else:
+                g, h = keys, theta_hash(column_tensor(ds, col)[rows])
+            pairs = _kmv(_sorted_unique_pairs(g, h), size)
             if self.world.distributed:
-                pairs = torch.cat(self.world.all_gather_varlen(pairs))
-                pairs = _kmv(torch.unique(pairs, dim=0), size)
-            ph = pairs.cpu().numpy()
-            est = {}
-            for g in np.unique(ph[:, 0]) if len(ph) else []:
-                hs = np.sort(ph[ph[:, 0] == g, 1])
-                if len(hs) < size:
-                    est[int(g)] = float(len(hs))
-                else:
-                    est[int(g)] = (size - 1) / (float(hs[size - 1]) / float(1 << 62))
-            cols[name] = np.array([est.get(int(g), 0.0) for g in gid_order], dtype=np.float64)
+                allp = torch.cat(self.world.all_gather_varlen(pairs))
+                pairs = _kmv(_sorted_unique_pairs(allp[:, 0], allp[:, 1]), size)
+            cols[name] = _kmv_estimates(pairs, size, gid_order)
 
     # ------------------------------------------------------------------ post processing
     def _post(self, prog: ScanProgram, cols: Dict[str, np.ndarray]) -> QueryResult:
@@ -647,6 +705,34 @@ def _gather_columns(world: World, data: Dict[str, np.ndarray]) -> Dict[str, np.n
     for k in data:
         out[k] = np.concatenate([np.asarray(d[k]) for d in lst])
     return out
+
+
+def _sorted_unique_pairs(g: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
+    """Distinct (group, hash) pairs sorted by group then hash: two stable device radix sorts (LSD)
+    instead of a lexicographic unique over rows."""
+    if g.numel() == 0:
+        return torch.zeros((0, 2), dtype=torch.int64, device=g.device)
+    o = torch.sort(h, stable=True).indices
+    o = o[torch.sort(g[o], stable=True).indices]
+    g, h = g[o].to(torch.int64), h[o].to(torch.int64)
+    keep = torch.ones(g.numel(), dtype=torch.bool, device=g.device)
+    keep[1:] = (g[1:] != g[:-1]) | (h[1:] != h[:-1])
+    return torch.stack([g[keep], h[keep]], dim=1)
+
+
+def _kmv_estimates(pairs: torch.Tensor, k: int, gid_order: np.ndarray) -> np.ndarray:
+    """Theta estimate per group of ``gid_order`` from sorted per-group KMV pairs (vectorized)."""
+    if pairs.numel() == 0:
+        return np.zeros(len(gid_order), dtype=np.float64)
+    g = pairs[:, 0]
+    ug, counts = torch.unique_consecutive(g, return_counts=True)
+    start = torch.cumsum(counts, 0) - counts
+    kth = pairs[(start + min(k, 1 << 62) - 1).clamp(max=g.numel() - 1), 1].to(torch.float64)
+    est = torch.where(counts < k, counts.to(torch.float64), (k - 1) / (kth / float(1 << 62)))
+    ug, est = ug.cpu().numpy(), est.cpu().numpy()
+    pos = np.searchsorted(ug, gid_order)
+    ok = (pos < len(ug)) & (ug[np.minimum(pos, len(ug) - 1)] == gid_order)
+    return np.where(ok, est[np.minimum(pos, len(ug) - 1)], 0.0)
 
 
 def _kmv(pairs: torch.Tensor, k: int) -> torch.Tensor:

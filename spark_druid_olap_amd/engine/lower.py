@@ -300,6 +300,13 @@ class ScanProgram:
     # min/max of a metric constant per group key: (AggOut, determinant key index, device int64 table
     # determinant dictionary id -> stored metric value); no accumulator, gathered at finalize
     derived_aggs: List[Tuple["AggOut", int, torch.Tensor]] = field(default_factory=list)
+    # hyperUnique over rolled-up sketch metrics: (output name, metric, aggregator filter or None);
+    # their registers follow the scan's ``nhll`` query-time HLL blocks in Partials.hll
+    stored_hll: List[Tuple[str, str, Any]] = field(default_factory=list)
+
+    @property
+    def nhll_total(self) -> int:
+        return self.nhll + len(self.stored_hll)
 
     def col(self, name: str) -> int:
         """Absolute descriptor column index of `name` in the current section."""
@@ -1051,6 +1058,16 @@ class Lowerer:
                 prog.aggs.append(AggOut(a.name, "min_f" if mn else "max_f", d["slot"], out_type="double",
                                         combine="min" if mn else "max"))
             return
+        if isinstance(a, S.HyperUniqueAggregationSpec) and a.fieldName in ds.metrics and \
+                ds.metrics[a.fieldName].sketch is not None:
+            # rolled-up hyperUnique metric: the rows' stored sparse sketches are unioned after the
+            # scan (sketch.hip hll_merge_stored) into the same register layout as query-time HLL
+            sk = ds.metrics[a.fieldName].sketch
+            if sk.kind != "hll" or sk.p != prog.hll_p:
+                raise LoweringError(f"hyperUnique over a {sk.kind} sketch metric {a.fieldName!r}")
+            prog.stored_hll.append((a.name, a.fieldName, filt))
+            prog.aggs.append(AggOut(a.name, "hll", hll_index=-len(prog.stored_hll), out_type="double", combine="hll"))
+            return
         if isinstance(a, (S.CardinalityAggregationSpec, S.HyperUniqueAggregationSpec)):
             fields = a.fieldNames if isinstance(a, S.CardinalityAggregationSpec) else [a.fieldName]
             if len(fields) != 1:
@@ -1058,6 +1075,8 @@ class Lowerer:
             col = fields[0]
             if col not in ds.dims and col not in ds.metrics:
                 raise LoweringError(f"cardinality over unknown column {col!r}")
+            if col in ds.metrics and ds.metrics[col].sketch is not None:
+                raise LoweringError(f"cardinality by row over the sketch metric {col!r}")
             ci = prog.col(col)
             d = aop(D.A_HLL, ci)
             d["hll"] = prog.nhll
@@ -1101,6 +1120,9 @@ class Lowerer:
         if isinstance(a, S.ThetaSketchAggregationSpec):
             if a.fieldName not in ds.dims and a.fieldName not in ds.metrics:
                 raise LoweringError(f"thetaSketch over unknown column {a.fieldName!r}")
+            m = ds.metrics.get(a.fieldName)
+            if m is not None and m.sketch is not None and m.sketch.kind != "theta":
+                raise LoweringError(f"thetaSketch over the {m.sketch.kind} sketch metric {a.fieldName!r}")
             prog.thetas.append((a.name, a.fieldName, int(a.size)))
             prog.aggs.append(AggOut(a.name, "theta", combine="theta"))
             return
@@ -1302,6 +1324,9 @@ class Lowerer:
             raise LoweringError("too many grouping keys")
         for a in aggregations:
             self.add_aggregator(prog, a)
+        for a in prog.aggs:  # stored-sketch registers come after the scan's HLL blocks
+            if a.kind == "hll" and a.hll_index < 0:
+                a.hll_index = prog.nhll + (-a.hll_index - 1)
         prog.presence_only = not aggregations and not extra_keys
         self.fold_presence_slot(prog)
         prog.key_order = [kc.name for kc in prog.keys]

@@ -41,6 +41,10 @@ struct ResetArgs {
 __global__ void reset_bufs_kernel(ResetArgs a);
 __global__ void topk_keep_kernel(const int64_t* acc, int64_t n, int nslots, int slot, int is_f64, int desc,
                                  const uint64_t* state, uint64_t* keep);
+// sketch.hip
+__global__ void hll_pairs_kernel(const int64_t* vals, int64_t n, int p, int64_t salt, int32_t* out);
+__global__ void hll_merge_stored_kernel(const int64_t* rows, const int64_t* gid, int64_t nsel, const int64_t* offsets,
+                                        const int32_t* pairs, int p, int64_t G, int32_t* regs);
 }  // namespace sdo
 
 namespace py = pybind11;
@@ -86,6 +90,33 @@ static void hll_estimate(uint64_t regs, int64_t G, int p, uint64_t est, uint64_t
   hipLaunchKernelGGL(sdo::hll_estimate_kernel, dim3(blocks), dim3(1024), 0, (hipStream_t)stream,
                      (const uint32_t*)regs, G, p, (double*)est);
   check(hipGetLastError(), "hll_estimate_kernel launch");
+}
+
+// ---------------------------------------------------------------------------------------------
+// Stored HLL sketches (sketch.hip)
+static unsigned grid_for(int64_t n, int64_t per_block, int64_t cap) {
+  int64_t b = (n + per_block - 1) / per_block;
+  if (b < 1) b = 1;
+  if (b > cap) b = cap;
+  return (unsigned)b;
+}
+
+static void hll_pairs(uint64_t vals, int64_t n, int p, int64_t salt, uint64_t out, uint64_t stream) {
+  if (n <= 0) return;
+  if (p < 4 || p > 18) throw std::invalid_argument("hll precision out of range");
+  hipLaunchKernelGGL(sdo::hll_pairs_kernel, dim3(grid_for(n, 256, 65536)), dim3(256), 0, (hipStream_t)stream,
+                     (const int64_t*)vals, n, p, salt, (int32_t*)out);
+  check(hipGetLastError(), "hll_pairs_kernel launch");
+}
+
+static void hll_merge_stored(uint64_t rows, uint64_t gid, int64_t nsel, uint64_t offsets, uint64_t pairs, int p,
+                             int64_t G, uint64_t regs, uint64_t stream) {
+  if (nsel <= 0 || G <= 0) return;
+  if (p < 4 || p > 18) throw std::invalid_argument("hll precision out of range");
+  hipLaunchKernelGGL(sdo::hll_merge_stored_kernel, dim3(grid_for(nsel, 256, 65536)), dim3(256), 0,
+                     (hipStream_t)stream, (const int64_t*)rows, (const int64_t*)gid, nsel, (const int64_t*)offsets,
+                     (const int32_t*)pairs, p, G, (int32_t*)regs);
+  check(hipGetLastError(), "hll_merge_stored_kernel launch");
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -297,6 +328,8 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("topk_keep", &topk_keep);
   m.def("nonzero_mask", &nonzero_mask);
   m.def("reset_bufs", &reset_bufs);
+  m.def("hll_pairs", &hll_pairs);
+  m.def("hll_merge_stored", &hll_merge_stored);
   m.def("desc_size", &desc_size);
   m.def("rtc_compile", &rtc_compile);
   m.def("module_load", [](py::bytes code, const std::string& name) { return module_load(std::string(code), name); });

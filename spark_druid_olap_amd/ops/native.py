@@ -178,3 +178,28 @@ def nonzero_rows(col: torch.Tensor) -> torch.Tensor:
     words = torch.empty((n + 63) // 64, dtype=torch.int64, device=col.device)
     m.nonzero_mask(col.data_ptr(), col.element_size(), n, col.stride(0), words.data_ptr(), _stream(col.device))
     return compact_rows(words)
+
+
+def hll_pairs(vals: torch.Tensor, p: int, salt: int) -> torch.Tensor:
+    """Packed (bucket << 8 | rho) int32 HLL pair of every 64-bit value (sketch.hip hll_pairs)."""
+    m = load()
+    v = vals.to(torch.int64).contiguous()
+    assert v.is_cuda
+    out = torch.empty(v.numel(), dtype=torch.int32, device=v.device)
+    m.hll_pairs(v.data_ptr(), v.numel(), int(p), int(salt), out.data_ptr(), _stream(v.device))
+    return out
+
+
+def hll_merge_stored(regs: torch.Tensor, rows: torch.Tensor, gid: torch.Tensor, offsets: torch.Tensor,
+                     pairs: torch.Tensor, p: int) -> None:
+    """Union the stored sparse HLL sketches of ``rows`` into ``regs[gid[i]]`` (sketch.hip
+    hll_merge_stored); ``regs`` is [G, 2^p] int32, gid < 0 skips a row."""
+    m = load()
+    G = regs.shape[0]
+    assert regs.dtype == torch.int32 and regs.is_contiguous() and regs.shape[1] == (1 << p) and regs.is_cuda
+    assert rows.dtype == torch.int64 and gid.dtype == torch.int64 and rows.numel() == gid.numel()
+    assert offsets.dtype == torch.int64 and pairs.dtype == torch.int32
+    if rows.numel():
+        assert int(rows.max()) < offsets.numel() - 1 and int(rows.min()) >= 0
+    m.hll_merge_stored(rows.contiguous().data_ptr(), gid.contiguous().data_ptr(), rows.numel(),
+                       offsets.data_ptr(), pairs.data_ptr(), int(p), int(G), regs.data_ptr(), _stream(regs.device))

@@ -70,15 +70,33 @@ class DimColumn:
 
 
 @dataclass
+class SketchColumn:
+    """A sketch metric kept per rolled-up row (segment/ingest.py), CSR over the shard's rows:
+    row r owns ``values[offsets[r]:offsets[r+1]]``.  hll: packed (bucket << 8 | rho) int32 pairs,
+    distinct buckets with their max rho; theta: the row's k smallest distinct 62-bit hashes."""
+    name: str
+    kind: str                 # hll | theta
+    offsets: torch.Tensor     # [num_rows + 1] int64
+    values: torch.Tensor
+    p: int = 11
+    salt: int = 0
+    size: int = 16384
+
+    def nbytes(self) -> int:
+        return self.offsets.numel() * 8 + self.values.numel() * self.values.element_size()
+
+
+@dataclass
 class MetricColumn:
     name: str
-    kind: str                 # long | double | decimal | hll
-    data: torch.Tensor        # padded
+    kind: str                 # long | double | decimal | hll | theta
+    data: torch.Tensor        # padded (a one-byte placeholder when ``sketch`` holds the values)
     scale: int = 0            # decimal digits for kind == decimal
+    sketch: Optional[SketchColumn] = None  # rolled-up sketch metric (hyperUnique / thetaSketch)
 
     @property
     def is_integral(self) -> bool:
-        return self.kind in ("long", "decimal", "hll")
+        return self.kind in ("long", "decimal", "hll") and self.sketch is None
 
 
 @dataclass
@@ -154,6 +172,8 @@ class DataSource:
                 n += d.bitmap.numel() * 8
         for m in self.metrics.values():
             n += m.data.numel() * m.data.element_size()
+            if m.sketch is not None:
+                n += m.sketch.nbytes()
         return n
 
     # ----------------------------------------------------------------- time
@@ -231,6 +251,13 @@ class DataSource:
         for name, m in self.metrics.items():
             np.save(os.path.join(path, f"met.{name}.npy"), m.data[:n].cpu().numpy())
             man["metrics"][name] = {"kind": m.kind, "scale": m.scale}
+            if m.sketch is not None:
+                sk = m.sketch
+                np.save(os.path.join(path, f"sk.{name}.offsets.npy"), sk.offsets.cpu().numpy())
+                np.save(os.path.join(path, f"sk.{name}.values.npy"), sk.values.cpu().numpy())
+                man["metrics"][name]["sketch"] = {"kind": sk.kind, "p": sk.p, "salt": sk.salt, "size": sk.size}
+        man["spatial"] = getattr(self, "spatial", {})
+        man["rollup"] = bool(getattr(self, "rollup", False))
         with open(os.path.join(path, "manifest.json"), "w") as f:
             json.dump(man, f)
 
@@ -250,11 +277,19 @@ class DataSource:
         for name, meta in man["metrics"].items():
             data = torch.from_numpy(np.load(os.path.join(path, f"met.{name}.npy"), allow_pickle=False))
             metrics[name] = MetricColumn(name, meta["kind"], _pad(data.to(dev), n), meta.get("scale", 0))
+            if "sketch" in meta:
+                sm = meta["sketch"]
+                off = torch.from_numpy(np.load(os.path.join(path, f"sk.{name}.offsets.npy"), allow_pickle=False))
+                val = torch.from_numpy(np.load(os.path.join(path, f"sk.{name}.values.npy"), allow_pickle=False))
+                metrics[name].sketch = SketchColumn(name, sm["kind"], off.to(dev), val.to(dev), sm["p"], sm["salt"],
+                                                    sm["size"])
         th = t.numpy().astype(np.int64)
         ds = DataSource(man["name"], n, _pad(t.to(dev), n, fill=int(t[-1]) if n else 0), man["time_unit_ms"],
                         dims, metrics, man["segment_granularity"], man["query_granularity"],
                         man.get("partition", 0), man.get("num_partitions", 1), time_host=th)
         ds.shard_key = man.get("shard_key")
+        ds.spatial = man.get("spatial", {})
+        ds.rollup = man.get("rollup", False)
         ds.build_indexes(bitmap_max_card=bitmap_max_card)
         return ds
 

@@ -5,16 +5,27 @@ Parity: the reference builds its test/bench indexes by submitting Druid index ta
 ``src/test/resources/tpch_index_task.json.template`` and ``zip_codeAll.json.template``.  This module
 reads the same JSON and builds a device-resident datasource in-process:
 
-  parse (csv / tsv / json) -> timestamp (iso / auto / posix / millis / Joda pattern) -> interval
-  filter -> queryGranularity truncation -> global sorted dictionaries per dimension -> metrics
-  (count, long/double sum/min/max, javascript, hyperUnique, thetaSketch) -> rollup (group by
-  truncated time + all dimensions) -> time sort -> hash partition across ranks -> zone maps and
-  inverted bitmaps (``bitmap_build`` HIP kernel on GPU).
+  The pipeline is device-first; the host only parses bytes:
+
+  streamed Arrow CSV/TSV batches (``block_bytes`` each, never the whole file in host memory)
+  -> per batch, Arrow's C++ ``dictionary_encode`` of every string column: the per-row codes go
+     to the GPU, Python touches only each batch's DISTINCT values (timestamps are parsed once per
+     distinct string, sketch inputs hashed once per distinct value, then gathered on the device)
+  -> ``dict_build``: the batch dictionaries are unified once (one encode of their concatenation +
+     one sort) into global SORTED dictionaries; every batch's codes are remapped by a device gather
+  -> interval filter + queryGranularity truncation on the device
+  -> ``rollup``: lexicographic device sort of (time, dimension ids, spatial point) -- packed into
+     as few int64 radix keys as the value ranges allow -- then segmented reductions (sum/min/max)
+  -> ``hll_build`` (sketch.hip ``hll_pairs`` + sort/dedup): hyperUnique metrics keep a sparse HLL
+     sketch per rolled-up row; thetaSketch metrics keep the row's k smallest 62-bit hashes (KMV).
+     Both are CSR columns (``SketchColumn``) that queries union (``hll_merge_stored``), so rollup
+     stays on with sketch metrics and answers match the raw index exactly
+  -> hash partition across ranks (global dictionaries, so every rank agrees) -> zone maps and
+     inverted bitmaps (``bitmap_build`` HIP kernel on GPU).
 
 Spatial dimensions (``spatialDimensions: [{dimName, dims}]``) become float coordinate columns
-registered in ``ds.spatial``; hyperUnique / thetaSketch metrics store a per-row 64-bit hash of the
-input field (exact input to the query-time HLL / KMV sketches), and rows carrying them are not
-rolled up so no sketch input is lost.
+registered in ``ds.spatial`` (and part of the rollup key, like Druid's spatial dimension value).
+Without rollup a sketch metric stores the per-row 64-bit hash of its input field.
 """
 from __future__ import annotations
 
@@ -23,16 +34,18 @@ import json
 import os
 import re
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Optional, Sequence
+from typing import Any, Dict, Iterator, List, Optional, Sequence, Tuple
 
 import numpy as np
 import pandas as pd
+import pyarrow as pa
+import pyarrow.compute as pc
 import torch
 
 from ..query import joda
 from ..query.granularity import bucket_start_ms
 from ..query.intervals import Interval
-from .datasource import DataSource, make_datasource
+from .datasource import DataSource, SketchColumn, make_datasource
 from .dictionary import DOUBLE, LONG, STRING, Dictionary
 
 DAY_MS = 86_400_000
@@ -112,34 +125,89 @@ class IndexSpec:
             target_partition_size=tps, raw=d)
 
 
+HLL_P = 11  # register index bits of stored sketches (== the query kernels' HLL_P, engine/lower.py)
+
+
+def _salt(name: str) -> int:
+    import zlib
+
+    return zlib.crc32(name.encode()) & 0x7FFFFFFF  # == engine/lower.py _salt (column-keyed HLL salt)
+
+
 # ------------------------------------------------------------------------------------------------
-def read_rows(spec: IndexSpec) -> pd.DataFrame:
+# Input: streamed Arrow record batches (the host does byte parsing only, in Arrow's C++ readers)
+def _used_columns(spec: IndexSpec) -> List[str]:
+    cols = [spec.ts_column] + list(spec.dimensions)
+    for m in spec.metrics:
+        if m.get("fieldName"):
+            cols.append(m["fieldName"])
+        cols += list(m.get("fieldNames") or [])
+    for sd in spec.spatial:
+        cols += list(sd["dims"])
+    out = []
+    for c in cols:
+        if c not in out:
+            out.append(c)
+    return out
+
+
+def _field_count(path: str, delimiter: str) -> int:
+    with open(path, "rb") as f:
+        line = f.readline().decode("utf-8", "replace").rstrip("\r\n")
+    return line.count(delimiter) + 1 if line else 0
+
+
+def _batches(spec: IndexSpec, data: Optional[pd.DataFrame], block_bytes: int) -> Iterator[pa.RecordBatch]:
+    """Arrow record batches of string columns (nulls = empty fields), ``block_bytes`` of input each:
+    the whole file never sits in host memory."""
+    import pyarrow.csv as pacsv
+
+    if data is not None:
+        cols = {}
+        for c in data.columns:
+            v = data[c]
+            cols[str(c)] = pa.array([None if (x is None or (isinstance(x, float) and x != x)) else str(x)
+                                     for x in v.tolist()], type=pa.string())
+        tbl = pa.table(cols)
+        yield from tbl.to_batches(max_chunksize=max(1, block_bytes // 64))
+        return
     if not spec.paths:
         raise IngestError("index spec has no input paths (firehose.baseDir/filter or inputSpec.paths)")
-    frames = []
     for p in spec.paths:
         if spec.fmt in ("csv", "tsv"):
-            f = pd.read_csv(p, sep=spec.delimiter, header=None, dtype=str, keep_default_na=False, na_values=[""],
-                            index_col=False)
-            cols = spec.columns or [f"c{i}" for i in range(f.shape[1])]
-            k = min(len(cols), f.shape[1])
-            f = f.iloc[:, :k]
-            f.columns = cols[:k]
-            frames.append(f)
+            nf = _field_count(p, spec.delimiter)
+            if nf == 0:
+                continue
+            names = list(spec.columns) or [f"c{i}" for i in range(nf)]
+            names = names[:nf] + [f"__extra{i}" for i in range(nf - len(names))]
+            use = [c for c in _used_columns(spec) if c in names]
+            reader = pacsv.open_csv(
+                p, read_options=pacsv.ReadOptions(column_names=names, block_size=block_bytes),
+                parse_options=pacsv.ParseOptions(delimiter=spec.delimiter, quote_char='"' if spec.fmt == "csv" else False,
+                                                 invalid_row_handler=lambda row: "skip"),
+                convert_options=pacsv.ConvertOptions(column_types={n: pa.string() for n in names},
+                                                     strings_can_be_null=True, null_values=[""], include_columns=use))
+            for rb in reader:
+                yield rb
         elif spec.fmt == "json":
-            frames.append(pd.read_json(p, lines=True, dtype=False))
+            df = pd.read_json(p, lines=True, dtype=False)
+            yield from _batches(spec, df, block_bytes)
         else:
             raise IngestError(f"unsupported input format {spec.fmt}")
-    return pd.concat(frames, ignore_index=True)
+
+
+def read_rows(spec: IndexSpec) -> pd.DataFrame:
+    """The input as one host DataFrame of strings (small inputs / debugging only; ``ingest`` streams)."""
+    return pa.Table.from_batches(list(_batches(spec, None, 64 << 20))).to_pandas()
 
 
 def parse_timestamps(col: pd.Series, fmt: str) -> np.ndarray:
     """-> int64 ms since epoch (NaT rows -> INT64_MIN)."""
     f = (fmt or "auto").lower()
     if f in ("posix",):
-        return (pd.to_numeric(col, errors="coerce").to_numpy(dtype=np.float64) * 1000).astype(np.int64)
+        return (pd.to_numeric(col, errors="coerce").fillna(-9.3e15).to_numpy(dtype=np.float64) * 1000).astype(np.int64)
     if f in ("millis",):
-        return pd.to_numeric(col, errors="coerce").to_numpy(dtype=np.float64).astype(np.int64)
+        return pd.to_numeric(col, errors="coerce").fillna(-9.3e18).to_numpy(dtype=np.float64).astype(np.int64)
     if f in ("iso", "auto"):
         ts = pd.to_datetime(col.astype(str).str.replace("Z", "", regex=False), errors="coerce", utc=False,
                             format="mixed")
@@ -147,15 +215,10 @@ def parse_timestamps(col: pd.Series, fmt: str) -> np.ndarray:
         out[ts.isna().to_numpy()] = np.iinfo(np.int64).min
         return out
     vals = col.astype(str).tolist()
-    cache: Dict[str, int] = {}
     out = np.empty(len(vals), dtype=np.int64)
     for i, v in enumerate(vals):
-        ms = cache.get(v)
-        if ms is None:
-            ms = joda.parse(fmt, v)
-            ms = np.iinfo(np.int64).min if ms is None else ms
-            cache[v] = ms
-        out[i] = ms
+        ms = joda.parse(fmt, v)
+        out[i] = np.iinfo(np.int64).min if ms is None else ms
     return out
 
 
@@ -163,143 +226,407 @@ def _hash64(values: pd.Series) -> np.ndarray:
     return pd.util.hash_pandas_object(values.astype(str), index=False).to_numpy().view(np.int64)
 
 
-def _metric_values(m: Dict[str, Any], df: pd.DataFrame) -> tuple:
-    """-> (values ndarray, kind, reduce op for rollup)"""
-    t = m["type"]
-    n = len(df)
-    if t == "count":
-        return np.ones(n, dtype=np.int64), "long", "sum"
-    fn = m.get("fieldName")
-    if t in ("longSum", "longMin", "longMax"):
-        v = pd.to_numeric(df[fn], errors="coerce").fillna(0).to_numpy(dtype=np.float64).astype(np.int64)
-        return v, "long", t[4:].lower()
-    if t in ("doubleSum", "doubleMin", "doubleMax", "floatSum", "floatMin", "floatMax"):
-        v = pd.to_numeric(df[fn], errors="coerce").fillna(0).to_numpy(dtype=np.float64)
-        return v, "double", re.sub(r"^(double|float)", "", t).lower()
-    if t == "javascript":
-        from ..query.jsfunc import jsagg_to_expr, parse_expr
-
-        op, params, expr = jsagg_to_expr(m["fnAggregate"])
-        env = {p: pd.to_numeric(df[f], errors="coerce").fillna(0).to_numpy(dtype=np.float64)
-               for p, f in zip(params, m["fieldNames"])}
-        return _eval_js_ast(parse_expr(expr), env, n), "double", op
-    if t in ("hyperUnique", "thetaSketch", "cardinality"):
-        return _hash64(df[fn]), "hll", "sketch"
-    raise IngestError(f"unsupported metric type {t}")
+# ------------------------------------------------------------------------------------------------
+# Per-column builders: each batch is dictionary-encoded by Arrow (C++ hash), only the batch
+# DICTIONARY is touched by Python; the per-row codes go straight to the device.
+_NULL_MS = np.iinfo(np.int64).min
 
 
-def _eval_js_ast(a, env, n):
+class _DimBuilder:
+    """Global sorted dictionary of a string dimension: batch-local codes live on the device, the
+    batch dictionaries are unified once at the end (one Arrow dictionary_encode over their
+    concatenation + one sort), then every batch's codes are remapped with a device gather."""
+
+    def __init__(self, dev: torch.device):
+        self.dev = dev
+        self.codes: List[torch.Tensor] = []
+        self.dicts: List[pa.Array] = []
+        self.has_null = False
+
+    def add(self, arr: pa.Array) -> None:
+        enc = pc.dictionary_encode(arr)
+        idx = enc.indices
+        if idx.null_count:
+            self.has_null = True
+            idx = pc.fill_null(idx, -1)
+        self.codes.append(torch.from_numpy(idx.to_numpy(zero_copy_only=False).astype(np.int32)).to(self.dev))
+        self.dicts.append(enc.dictionary)
+
+    def finish(self) -> Tuple[Dictionary, torch.Tensor]:
+        lens = [len(d) for d in self.dicts]
+        allv = pa.concat_arrays(self.dicts) if self.dicts else pa.array([], type=pa.string())
+        enc = pc.dictionary_encode(allv)
+        uniq = enc.dictionary
+        order = pc.sort_indices(uniq).to_numpy()
+        rank = np.empty(len(uniq), dtype=np.int64)
+        rank[order] = np.arange(len(uniq), dtype=np.int64)
+        off = 1 if self.has_null else 0
+        gid = rank[enc.indices.to_numpy(zero_copy_only=False)] + off
+        values = np.asarray(uniq.take(pa.array(order)).to_pylist(), dtype=object)
+        d = Dictionary(values, STRING, self.has_null)
+        outs, at = [], 0
+        for codes, n in zip(self.codes, lens):
+            table = torch.from_numpy(np.concatenate([[0], gid[at: at + n]])).to(self.dev)  # code -1 -> NULL id 0
+            outs.append(table[(codes + 1).to(torch.int64)])
+            at += n
+        self.codes, self.dicts = [], []
+        ids = torch.cat(outs) if outs else torch.zeros(0, dtype=torch.int64, device=self.dev)
+        return d, ids
+
+
+def _numbers(arr: pa.Array) -> np.ndarray:
+    """float64 values of a string column (unparseable / missing -> 0, like Druid's metric parsing)."""
+    try:
+        v = pc.cast(arr, pa.float64())
+    except (pa.ArrowInvalid, pa.ArrowNotImplementedError):
+        return pd.to_numeric(pd.Series(arr.to_pylist(), dtype=object), errors="coerce").fillna(0.0) \
+            .to_numpy(dtype=np.float64)
+    return np.array(pc.fill_null(v, 0.0).to_numpy(zero_copy_only=False), dtype=np.float64)
+
+
+def _dict_gather(arr: pa.Array, fn, dtype, dev, null_value) -> torch.Tensor:
+    """Evaluate ``fn`` over the batch's distinct values only (timestamps, sketch hashes) and gather
+    the per-row result on the device."""
+    enc = pc.dictionary_encode(arr)
+    idx = enc.indices
+    if idx.null_count:
+        idx = pc.fill_null(idx, -1)
+    vals = np.asarray(fn(pd.Series(enc.dictionary.to_pylist(), dtype=object)), dtype=dtype)
+    table = torch.from_numpy(np.concatenate([np.array([null_value], dtype=dtype), vals])).to(dev)
+    codes = torch.from_numpy(idx.to_numpy(zero_copy_only=False).astype(np.int64)).to(dev)
+    return table[codes + 1]
+
+
+def _eval_js(a, env: Dict[str, torch.Tensor], n: int, dev) -> torch.Tensor:
     k = a[0]
     if k == "col":
         return env[a[1]]
     if k == "const":
-        return np.full(n, a[1])
+        return torch.full((n,), float(a[1]), dtype=torch.float64, device=dev)
     if k == "neg":
-        return -_eval_js_ast(a[1], env, n)
+        return -_eval_js(a[1], env, n, dev)
     if k == "abs":
-        return np.abs(_eval_js_ast(a[1], env, n))
-    x, y = _eval_js_ast(a[1], env, n), _eval_js_ast(a[2], env, n)
-    return {"add": np.add, "sub": np.subtract, "mul": np.multiply, "div": np.divide,
-            "min": np.minimum, "max": np.maximum}[k](x, y)
+        return torch.abs(_eval_js(a[1], env, n, dev))
+    x, y = _eval_js(a[1], env, n, dev), _eval_js(a[2], env, n, dev)
+    return {"add": torch.add, "sub": torch.sub, "mul": torch.mul, "div": torch.div,
+            "min": torch.minimum, "max": torch.maximum}[k](x, y)
 
 
-def _gran_truncate(ms: np.ndarray, g: str) -> np.ndarray:
+def _metric_plan(m: Dict[str, Any]) -> Tuple[str, str]:
+    """-> (kind, rollup op) of a metricsSpec entry."""
+    t = m["type"]
+    if t == "count":
+        return "long", "sum"
+    if t in ("longSum", "longMin", "longMax"):
+        return "long", t[4:].lower()
+    if t in ("doubleSum", "doubleMin", "doubleMax", "floatSum", "floatMin", "floatMax"):
+        return "double", re.sub(r"^(double|float)", "", t).lower()
+    if t == "javascript":
+        from ..query.jsfunc import jsagg_to_expr
+
+        return "double", jsagg_to_expr(m["fnAggregate"])[0]
+    if t in ("hyperUnique", "cardinality"):
+        return "hll", "sketch"
+    if t == "thetaSketch":
+        return "theta", "sketch"
+    raise IngestError(f"unsupported metric type {t}")
+
+
+def _gran_truncate(ms: torch.Tensor, g: str) -> torch.Tensor:
     g = g.lower()
-    if g in ("none", ""):
+    if g in ("none", "") or ms.numel() == 0:
         return ms
     if g == "all":
-        return np.full_like(ms, ms.min() if len(ms) else 0)
+        return torch.full_like(ms, int(ms.min()))
     step = {"second": 1000, "minute": 60_000, "fifteen_minute": 900_000, "thirty_minute": 1_800_000,
             "hour": 3_600_000, "day": DAY_MS}.get(g)
     if step is not None:
-        return (ms // step) * step
-    uniq, inv = np.unique(ms, return_inverse=True)
-    b = np.array([bucket_start_ms(int(x), g) for x in uniq], dtype=np.int64)
-    return b[inv]
+        return torch.div(ms, step, rounding_mode="floor") * step
+    uniq, inv = torch.unique(ms, return_inverse=True)
+    b = np.array([bucket_start_ms(int(x), g) for x in uniq.cpu().numpy()], dtype=np.int64)
+    return torch.from_numpy(b).to(ms.device)[inv]
+
+
+# ------------------------------------------------------------------------------------------------
+# Device rollup: lexicographic sort of the rollup key + segmented reductions
+def _lex_order(keys: List[torch.Tensor]) -> torch.Tensor:
+    """Permutation sorting rows by (keys[0], keys[1], ...).  Keys whose value ranges fit are packed
+    into one int64 radix key (one device sort); the rest are applied as stable sorts, least
+    significant first (LSD order)."""
+    n = keys[0].numel()
+    groups: List[List[Tuple[torch.Tensor, int, int]]] = [[]]
+    bits = 0
+    for k in keys:
+        lo, hi = int(k.min()), int(k.max())
+        need = max(1, (hi - lo).bit_length())
+        if need > 62:  # full-width key (float bits): sorted on its own, unpacked
+            groups.append([(k, 0, 64)])
+            groups.append([])
+            bits = 0
+            continue
+        if bits + need > 62:
+            groups.append([])
+            bits = 0
+        groups[-1].append((k, lo, need))
+        bits += need
+    packed = []
+    for grp in groups:
+        if not grp:
+            continue
+        if grp[0][2] == 64:
+            packed.append(grp[0][0])
+            continue
+        acc = torch.zeros(n, dtype=torch.int64, device=keys[0].device)
+        for k, lo, need in grp:
+            acc = (acc << need) | (k - lo)
+        packed.append(acc)
+    perm = torch.arange(n, device=keys[0].device)
+    for pk in reversed(packed):
+        perm = perm[torch.sort(pk[perm], stable=True).indices]
+    return perm
+
+
+def _segments(sorted_keys: List[torch.Tensor]) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(segment id per sorted row, index of each segment's first row)."""
+    n = sorted_keys[0].numel()
+    change = torch.zeros(n, dtype=torch.bool, device=sorted_keys[0].device)
+    if n:
+        change[0] = True
+    for k in sorted_keys:
+        change[1:] |= k[1:] != k[:-1]
+    seg = torch.cumsum(change.to(torch.int64), 0) - 1
+    return seg, torch.nonzero(change).flatten()
+
+
+def _reduce(vals: torch.Tensor, seg: torch.Tensor, R: int, op: str) -> torch.Tensor:
+    if op == "sum":
+        return torch.zeros(R, dtype=vals.dtype, device=vals.device).index_add_(0, seg, vals)
+    init = (float("inf") if op == "min" else float("-inf")) if vals.dtype == torch.float64 else \
+        (np.iinfo(np.int64).max if op == "min" else np.iinfo(np.int64).min)
+    out = torch.full((R,), init, dtype=vals.dtype, device=vals.device)
+    return out.scatter_reduce_(0, seg, vals, reduce="amin" if op == "min" else "amax")
+
+
+def build_hll_sketch(name: str, hashes: torch.Tensor, seg: torch.Tensor, R: int, p: int = HLL_P) -> SketchColumn:
+    """Per rolled-up row, the distinct (bucket, max rho) pairs of its raw rows' values (CSR).  The
+    pairs come from ``hll_pairs`` (sketch.hip) on the GPU, bit-identical to the query kernels' HLL
+    update, so a rolled-up hyperUnique answers exactly like the raw per-row hash column."""
+    salt = _salt(name)
+    if hashes.is_cuda:
+        from ..ops import native
+
+        packed = native.hll_pairs(hashes, p, salt)
+    else:
+        from ..ops.reference import hll_update_values
+
+        b, r = hll_update_values(hashes, salt, p)
+        packed = ((b << 8) | r).to(torch.int32)
+    bucket = (packed >> 8).to(torch.int64)
+    rho = (packed & 0xFF).to(torch.int64)
+    # (row, bucket, rho) ascending: the last entry of each (row, bucket) run carries the max rho
+    key = (seg << (p + 6)) | (bucket << 6) | rho
+    key = torch.sort(key).values
+    rb = key >> 6
+    last = torch.ones(key.numel(), dtype=torch.bool, device=key.device)
+    if key.numel():
+        last[:-1] = rb[1:] != rb[:-1]
+    key = key[last]
+    rows = key >> (p + 6)
+    vals = ((((key >> 6) & ((1 << p) - 1)) << 8) | (key & 0x3F)).to(torch.int32)
+    offsets = torch.zeros(R + 1, dtype=torch.int64, device=key.device)
+    offsets[1:] = torch.cumsum(torch.bincount(rows, minlength=R), 0)
+    return SketchColumn(name, "hll", offsets, vals, p=p, salt=salt)
+
+
+def theta_hash(v: torch.Tensor) -> torch.Tensor:
+    """62-bit KMV hash of a stored 64-bit value hash (the same mix the query path applies to a
+    per-row hash column, engine/executor.py _theta)."""
+    from ..ops.reference import mix64
+
+    return mix64(v.to(torch.int64) ^ 0x5BD1E995) & ((1 << 62) - 1)
+
+
+def build_theta_sketch(name: str, hashes: torch.Tensor, seg: torch.Tensor, R: int, size: int) -> SketchColumn:
+    """Per rolled-up row, its k = ``size`` smallest distinct 62-bit hashes (KMV, CSR)."""
+    h = theta_hash(hashes)
+    o = torch.sort(h, stable=True).indices
+    o = o[torch.sort(seg[o], stable=True).indices]
+    sg, hh = seg[o], h[o]
+    keep = torch.ones(sg.numel(), dtype=torch.bool, device=sg.device)
+    if sg.numel():
+        keep[1:] = (sg[1:] != sg[:-1]) | (hh[1:] != hh[:-1])
+    sg, hh = sg[keep], hh[keep]
+    counts = torch.bincount(sg, minlength=R)
+    start = torch.cumsum(counts, 0) - counts
+    rank = torch.arange(sg.numel(), device=sg.device) - start[sg]
+    sel = rank < size
+    sg, hh = sg[sel], hh[sel]
+    offsets = torch.zeros(R + 1, dtype=torch.int64, device=sg.device)
+    offsets[1:] = torch.cumsum(torch.bincount(sg, minlength=R), 0)
+    return SketchColumn(name, "theta", offsets, hh.contiguous(), size=size)
+
+
+def _shard_hash(cols: List[torch.Tensor], n: int, dev) -> torch.Tensor:
+    from ..ops.reference import mix64
+
+    h = torch.zeros(n, dtype=torch.int64, device=dev)
+    for c in cols:
+        h = mix64(h * 31 + c.to(torch.int64))
+    return h
 
 
 def ingest(spec, device="cpu", rank: int = 0, world: int = 1, data: Optional[pd.DataFrame] = None,
-           data_dir: Optional[str] = None, bitmap_max_card: int = 256) -> DataSource:
-    """Build this rank's shard of the datasource described by ``spec``."""
+           data_dir: Optional[str] = None, bitmap_max_card: int = 256, block_bytes: int = 64 << 20) -> DataSource:
+    """Build this rank's shard of the datasource described by ``spec`` (see the module doc)."""
     if not isinstance(spec, IndexSpec):
         spec = IndexSpec.parse(spec, data_dir)
-    df = data if data is not None else read_rows(spec)
-    if spec.ts_column not in df.columns:
-        raise IngestError(f"timestamp column {spec.ts_column!r} missing")
-    ms = parse_timestamps(df[spec.ts_column], spec.ts_format)
-    keep = ms != np.iinfo(np.int64).min
+    dev = torch.device(device)
+    plans = {m["name"]: _metric_plan(m) for m in spec.metrics}
+    dims = list(spec.dimensions)
+    dim_b: Dict[str, _DimBuilder] = {}
+    parts: Dict[str, List[torch.Tensor]] = {"__t": []}
+    seen_cols = None
+    n_total = 0
+    for rb in _batches(spec, data, block_bytes):
+        names = rb.schema.names
+        if seen_cols is None:
+            seen_cols = set(names)
+            if spec.ts_column not in seen_cols:
+                raise IngestError(f"timestamp column {spec.ts_column!r} missing")
+            dims = [d for d in dims if d in seen_cols]
+            dim_b = {d: _DimBuilder(dev) for d in dims}
+        n = rb.num_rows
+        if n == 0:
+            continue
+        n_total += n
+        col = {nm: rb.column(i) for i, nm in enumerate(names)}
+        parts["__t"].append(_dict_gather(col[spec.ts_column], lambda u: parse_timestamps(u, spec.ts_format),
+                                         np.int64, dev, _NULL_MS))
+        for d in dims:
+            dim_b[d].add(col[d])
+        num_cache: Dict[str, torch.Tensor] = {}
+
+        def num(c):
+            if c not in num_cache:
+                num_cache[c] = torch.from_numpy(_numbers(col[c])).to(dev)
+            return num_cache[c]
+
+        for m in spec.metrics:
+            nm, t = m["name"], m["type"]
+            kind, op = plans[nm]
+            if t == "count":
+                v = torch.ones(n, dtype=torch.int64, device=dev)
+            elif kind == "long":
+                v = num(m["fieldName"]).to(torch.int64)
+            elif t == "javascript":
+                from ..query.jsfunc import jsagg_to_expr, parse_expr
+
+                _, params, expr = jsagg_to_expr(m["fnAggregate"])
+                env = {p_: num(f) for p_, f in zip(params, m["fieldNames"])}
+                v = _eval_js(parse_expr(expr), env, n, dev).to(torch.float64)
+            elif kind == "double":
+                v = num(m["fieldName"])
+            else:  # sketch input: 64-bit hash of the value string
+                v = _dict_gather(col[m["fieldName"]].fill_null("nan"), _hash64, np.int64, dev, 0)
+            parts.setdefault("m:" + nm, []).append(v)
+        for sd in spec.spatial:
+            for i, c in enumerate(sd["dims"]):
+                parts.setdefault(f"s:{sd['dimName']}.{i}", []).append(num(c) if c in col else
+                                                                      torch.zeros(n, dtype=torch.float64, device=dev))
+    if seen_cols is None:
+        raise IngestError("index task input is empty")
+    cat = {k: (torch.cat(v) if v else torch.zeros(0, device=dev)) for k, v in parts.items()}
+    ms = cat.pop("__t")
+    keep = ms != _NULL_MS
     if spec.intervals:
-        ivs = [Interval.parse(s) for s in spec.intervals]
-        inside = np.zeros(len(ms), dtype=bool)
-        for iv in ivs:
+        inside = torch.zeros_like(keep)
+        for iv in (Interval.parse(s_) for s_ in spec.intervals):
             inside |= (ms >= iv.lo) & (ms < iv.hi)
         keep &= inside
-    df = df.loc[keep].reset_index(drop=True)
-    ms = _gran_truncate(ms[keep], spec.query_granularity)
-    # metrics
-    mvals, mkinds, mops = {}, {}, {}
-    for m in spec.metrics:
-        v, kind, op = _metric_values(m, df)
-        mvals[m["name"]], mkinds[m["name"]], mops[m["name"]] = v, kind, op
-    # spatial coordinates
-    spatial: Dict[str, List[str]] = {}
-    for sd in spec.spatial:
-        comps = []
-        for i, c in enumerate(sd["dims"]):
-            nm = f"{sd['dimName']}.{i}"
-            mvals[nm] = pd.to_numeric(df[c], errors="coerce").to_numpy(dtype=np.float64)
-            mkinds[nm], mops[nm] = "double", "first"
-            comps.append(nm)
-        spatial[sd["dimName"]] = comps
-    dims = [d for d in spec.dimensions if d in df.columns]
-    # rollup: group by (time, dims); sketch inputs / spatial points are never rolled up
-    rollup = spec.rollup and not any(op in ("sketch", "first") for op in mops.values())
-    work = pd.DataFrame({"__t": ms})
-    for d in dims:
-        work[d] = df[d].astype(object).where(df[d].notna(), None)
-    for k, v in mvals.items():
-        work["m:" + k] = v
-    if rollup and len(work):
-        keys = ["__t"] + dims
-        agg = {}
-        for k, op in mops.items():
-            agg["m:" + k] = {"sum": "sum", "min": "min", "max": "max"}[op]
-        work = work.fillna({d: "\0null" for d in dims}).groupby(keys, sort=False, dropna=False).agg(agg).reset_index()
-        for d in dims:
-            work[d] = work[d].where(work[d] != "\0null", None)
-    work = work.sort_values("__t", kind="stable").reset_index(drop=True)
-    # global dictionaries (identical on every rank), then this rank's hash partition
+    sel = torch.nonzero(keep).flatten()
+    ms = _gran_truncate(ms[sel], spec.query_granularity)
+    cols = {k: v[sel] for k, v in cat.items()}
     dicts, ids = {}, {}
     for d in dims:
-        dic, idv = Dictionary.build(work[d].to_numpy(dtype=object), STRING)
-        dicts[d], ids[d] = dic, idv
-    if world > 1:
-        h = pd.util.hash_pandas_object(work[dims].astype(str) if dims else work[["__t"]], index=False).to_numpy()
-        mine = (h % np.uint64(world)).astype(np.int64) == rank
-        sel = np.nonzero(mine)[0]
+        dicts[d], full = dim_b[d].finish()
+        ids[d] = full[sel]
+    spatial = {sd["dimName"]: [f"{sd['dimName']}.{i}" for i in range(len(sd["dims"]))] for sd in spec.spatial}
+    n = int(ms.numel())
+    # ---- rollup on the device: rows with equal (truncated time, every dimension, spatial point)
+    rollup = spec.rollup and n > 0
+    keys = [ms] + [ids[d] for d in dims] + [cols[f"s:{c}"].view(torch.int64) for cs in spatial.values() for c in cs]
+    perm = _lex_order(keys) if rollup else torch.sort(ms, stable=True).indices
+    if rollup:
+        sk = [k[perm] for k in keys]
+        seg, first = _segments(sk)
+        first = perm[first]  # original row of each rolled-up row's first member
+        R = int(first.numel())
     else:
-        sel = np.arange(len(work))
-    t_ms = work["__t"].to_numpy(dtype=np.int64)[sel]
-    unit = DAY_MS if len(t_ms) and np.all(t_ms % DAY_MS == 0) else (1000 if np.all(t_ms % 1000 == 0) else 1)
-    dev = torch.device(device)
-    n = len(sel)
-    tu = torch.from_numpy(t_ms // unit).to(dev)
-    dim_ids = {d: torch.from_numpy(ids[d][sel]).to(dev) for d in dims}
+        seg = torch.arange(n, device=dev)
+        first = perm
+        R = n
+    # ---- this rank's hash partition of the (rolled-up) rows; dictionaries are global
+    row_keep = None
+    if world > 1:
+        hk = [ids[d][first] for d in dims] or [ms[first]]
+        row_keep = torch.remainder(_shard_hash(hk, R, dev), world) == rank
+    out_rows = torch.nonzero(row_keep).flatten() if row_keep is not None else torch.arange(R, device=dev)
+    src_first = first[out_rows]
+    t_ms = ms[src_first]
     mdata, mk = {}, {}
-    for k in mvals:
-        v = work["m:" + k].to_numpy()[sel]
-        kind = mkinds[k]
-        if kind == "double":
-            mdata[k] = torch.from_numpy(np.ascontiguousarray(v, dtype=np.float64)).to(dev)
+    sketches: Dict[str, SketchColumn] = {}
+    for m in spec.metrics:
+        nm = m["name"]
+        kind, op = plans[nm]
+        v = cols["m:" + nm]
+        if kind in ("hll", "theta"):
+            if rollup:
+                vs = v[perm]
+                if row_keep is not None:  # raw rows of this rank's rolled-up rows, renumbered
+                    newid = torch.full((R,), -1, dtype=torch.int64, device=dev)
+                    newid[out_rows] = torch.arange(out_rows.numel(), device=dev)
+                    mine = newid[seg] >= 0
+                    vs, sg = vs[mine], newid[seg][mine]
+                else:
+                    sg = seg
+                nr = int(out_rows.numel())
+                sketches[nm] = build_hll_sketch(nm, vs, sg, nr) if kind == "hll" else \
+                    build_theta_sketch(nm, vs, sg, nr, int(m.get("size", 16384)))
+                mdata[nm] = torch.zeros(nr, dtype=torch.uint8, device=dev)
+                mk[nm] = "hll" if kind == "hll" else "theta"
+            else:
+                mdata[nm] = v[src_first].to(torch.int64)
+                mk[nm] = "hll"
+            continue
+        if rollup:
+            red = _reduce(v[perm], seg, R, op if op in ("sum", "min", "max") else "sum")
+            mdata[nm] = red[out_rows]
         else:
-            mdata[k] = torch.from_numpy(np.ascontiguousarray(v, dtype=np.int64)).to(dev)
-        mk[k] = kind
-    ds = make_datasource(spec.data_source, n, tu, unit, dim_ids, dicts, mdata, mk,
+            mdata[nm] = v[src_first]
+        mdata[nm] = mdata[nm].to(torch.float64 if kind == "double" else torch.int64).contiguous()
+        mk[nm] = kind
+    for cs in spatial.values():
+        for c in cs:
+            mdata[c] = cols[f"s:{c}"][src_first].contiguous()
+            mk[c] = "double"
+    nloc = int(out_rows.numel())
+    if nloc and bool((t_ms % DAY_MS == 0).all()):
+        unit = DAY_MS
+    elif nloc and bool((t_ms % 1000 == 0).all()):
+        unit = 1000
+    else:
+        unit = 1 if nloc else DAY_MS
+    tu = torch.div(t_ms, unit, rounding_mode="floor")
+    dim_ids = {d: ids[d][src_first] for d in dims}
+    ds = make_datasource(spec.data_source, nloc, tu, unit, dim_ids, dicts, mdata, mk,
                          segment_granularity=spec.segment_granularity, query_granularity=spec.query_granularity,
                          partition=rank, num_partitions=world)
+    for nm, skc in sketches.items():
+        ds.metrics[nm].sketch = skc
     ds.spatial = spatial
     ds.rollup = rollup
-    ds.global_num_rows = len(work)
+    ds.global_num_rows = R
+    ds.ingested_rows = n_total
     ds.build_indexes(bitmap_max_card=bitmap_max_card)
     return ds
 
