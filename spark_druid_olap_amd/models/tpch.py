@@ -417,27 +417,28 @@ def to_datasource(flat: FlatTPCH, name: str = "tpch", bitmap_max_card: int = 256
     return ds
 
 
-def to_pandas(flat: FlatTPCH):
-    """The raw 53-column base table (`orderLineItemPartSupplierBase`) as a pandas DataFrame."""
+def to_pandas(flat: FlatTPCH, lo: int = 0, hi: Optional[int] = None):
+    """The raw 53-column base table (`orderLineItemPartSupplierBase`) as a pandas DataFrame (rows
+    ``[lo, hi)``; chunked export keeps host memory bounded at large scale factors)."""
     import pandas as pd
 
-    n = flat.num_rows
+    n = flat.num_rows if hi is None else min(hi, flat.num_rows)
     out = {}
-    ship = flat.ship_day.cpu().numpy().astype(np.int64)
+    ship = flat.ship_day[lo:n].cpu().numpy().astype(np.int64)
     date_d = Dictionary(date_strings(START_DAY, DATE_DICT_END), STRING)
     for name, typ in FLAT_SCHEMA:
         if name == "l_shipdate":
             out[name] = date_d.decode(ship - START_DAY)
         elif name == "order_year":
-            od = flat.dims["o_orderdate"][1].cpu().numpy().astype(np.int64)
+            od = flat.dims["o_orderdate"][1][lo:n].cpu().numpy().astype(np.int64)
             years = np.array([s[:4] for s in date_d.values], dtype=object)
             out[name] = years[od]
         elif name in flat.dims:
             d, ids = flat.dims[name]
-            out[name] = d.decode(ids[:n].cpu().numpy().astype(np.int64))
+            out[name] = d.decode(ids[lo:n].cpu().numpy().astype(np.int64))
         elif name in flat.nums:
             t, kind, scale = flat.nums[name]
-            v = t[:n].cpu().numpy()
+            v = t[lo:n].cpu().numpy()
             if kind == "decimal":
                 v = v.astype(np.float64) / (10.0 ** scale)
             elif typ == "double":
