@@ -244,7 +244,7 @@ class DataSource:
         man = {"name": self.name, "num_rows": n, "time_unit_ms": self.time_unit_ms,
                "segment_granularity": self.segment_granularity, "query_granularity": self.query_granularity,
                "partition": self.partition, "num_partitions": self.num_partitions,
-               "shard_key": self.shard_key, "dims": {}, "metrics": {}}
+               "shard_key": self.shard_key, "global_num_rows": int(self.global_num_rows), "dims": {}, "metrics": {}}
         for name, d in self.dims.items():
             np.save(os.path.join(path, f"dim.{name}.npy"), d.ids[:n].cpu().numpy())
             man["dims"][name] = {"dictionary": d.dictionary.to_json(), "spatial": d.spatial}
@@ -288,6 +288,7 @@ class DataSource:
                         dims, metrics, man["segment_granularity"], man["query_granularity"],
                         man.get("partition", 0), man.get("num_partitions", 1), time_host=th)
         ds.shard_key = man.get("shard_key")
+        ds.global_num_rows = man.get("global_num_rows", n)
         ds.spatial = man.get("spatial", {})
         ds.rollup = man.get("rollup", False)
         ds.build_indexes(bitmap_max_card=bitmap_max_card)

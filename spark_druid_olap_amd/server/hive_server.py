@@ -543,6 +543,35 @@ class _Tee:
             raise T.ProtocolError(f"bad type {t}")
 
 
+def _load_datasources(sess, world, ingest_specs, store, dev) -> None:
+    """Deployment: datasources from index tasks (``--ingest``) and/or a persisted segment store
+    (``--segments``: ``<store>/<datasource>/rank<r>/manifest.json`` per shard, written by
+    ``DataSource.save``).  A shard saved for a different world size is refused: its rows belong to
+    another partitioning."""
+    from ..segment.datasource import DataSource
+    from ..segment.ingest import ingest
+
+    log = logging.getLogger("sdo.thrift")
+    for item in ingest_specs:
+        spec, _, data_dir = item.partition("@")
+        ds = ingest(spec, dev, rank=world.rank, world=world.size, data_dir=data_dir or None)
+        sess.register_datasource(ds)
+        log.info("ingested %s: %d rows on rank %d (%d total)", ds.name, ds.num_rows, world.rank, ds.global_num_rows)
+        if store:
+            ds.save(os.path.join(store, ds.name, f"rank{world.rank}"))
+    if store and not ingest_specs and os.path.isdir(store):
+        for name in sorted(os.listdir(store)):
+            shard = os.path.join(store, name, f"rank{world.rank}")
+            if not os.path.exists(os.path.join(shard, "manifest.json")):
+                continue
+            ds = DataSource.load(shard, dev)
+            if ds.num_partitions != world.size:
+                raise RuntimeError(f"segment store {shard} was written by {ds.num_partitions} ranks, "
+                                   f"this server has {world.size}")
+            sess.register_datasource(ds)
+            log.info("loaded %s: %d rows on rank %d", ds.name, ds.num_rows, world.rank)
+
+
 def main(argv=None):
     """``python -m spark_druid_olap_amd.server.hive_server --port 10000 [--tpch-sf 1] [--gpus N]``
     (the ``start-sparklinedatathriftserver.sh`` entry, scripts/start-sparklinedatathriftserver.sh).
@@ -562,6 +591,12 @@ def main(argv=None):
     ap.add_argument("--conf", action="append", default=[], help="key=value session conf (repeatable)")
     ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU) to start when not under torchrun")
     ap.add_argument("--port-file", default=None, help="write the bound Thrift port here (rank 0)")
+    ap.add_argument("--ingest", action="append", default=[], metavar="SPEC[@DATA_DIR]",
+                    help="run a Druid index task (JSON spec file) at startup; every rank keeps its hash "
+                         "partition (repeatable)")
+    ap.add_argument("--segments", default=None,
+                    help="segment store root: load every datasource saved under DIR/<datasource>/rank<r> "
+                         "(resume after restart); with --ingest, the ingested shards are saved there")
     a = ap.parse_args(argv)
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         import sys
@@ -587,6 +622,7 @@ def main(argv=None):
         sess.register_datasource(ds)
         sess.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)
         sess.sql(tpch.druid_ddl(with_column_mapping=False))
+    _load_datasources(sess, world, a.ingest, a.segments, dev)
     if a.init_sql:
         with open(a.init_sql) as f:
             for st in f.read().split(";"):
