@@ -524,40 +524,79 @@ class PreparedQuery:
                 "count": np.array([counts[i] for i in order], dtype=np.int64)}
         return QueryResult(["dimension", "value", "count"], data, "search")
 
-    def _select(self) -> QueryResult:
-        from ..ops.reference import run_reference_mask
+    def selected_rows(self) -> torch.Tensor:
+        """This shard's row ids passing the Select filter (device, ascending), computed once per
+        prepared query -- datasources are immutable, so every later page is a slice + gather, not
+        a re-scan (the reference re-issues the Select per page, asd/DruidSelectResultIterator.scala
+        116-137).  Compacted by the mask kernel + compact_rows (O(selected) memory)."""
+        rows = getattr(self, "_sel_rows", None)
+        if rows is None:
+            from ..ops.reference import run_reference_mask
+
+            _, prog, prep = self.scans[0]
+            rows = prep.run() if prep is not None else run_reference_mask(prog)
+            if self.qs.descending:
+                rows = rows.flip(0)
+            self._sel_rows = rows
+        return rows
+
+    def run_page(self, paging: Optional[S.PagingSpec] = None) -> QueryResult:
+        """One Select page (``paging`` overrides the spec's pagingSpec): the cursor protocol of
+        Druid's select query -- pagingIdentifiers map each shard (``<datasource>_<rank>``) to the
+        last row offset returned."""
+        t0 = time.perf_counter()
+        res = self._select(paging)
+        res.stats["exec_ms"] = (time.perf_counter() - t0) * 1e3
+        return res
+
+    def _select(self, paging: Optional[S.PagingSpec] = None) -> QueryResult:
         from .lower import column_tensor
 
         qs = self.qs
         ds = self.ds
-        _, prog, prep = self.scans[0]
-        rows = prep.run() if prep is not None else run_reference_mask(prog)
-        if qs.descending:
-            rows = rows.flip(0)
-        ident = f"{ds.name}_{self.world.rank}"
-        paging = qs.pagingSpec or S.PagingSpec()
-        start = int((paging.pagingIdentifiers or {}).get(ident, -1)) + 1 if paging.pagingIdentifiers else 0
-        page = rows[start: start + int(paging.threshold)]
+        rows = self.selected_rows()
+        paging = paging or qs.pagingSpec or S.PagingSpec()
+        ids_in = paging.pagingIdentifiers or {}
+        thr = int(paging.threshold)
+        W = self.world.size if self.world.distributed else 1
+
+        def start_of(r):
+            k = f"{ds.name}_{r}"
+            return int(ids_in[k]) + 1 if k in ids_in else 0
+
+        start = start_of(self.world.rank if W > 1 else 0)
+        page = rows[start: start + thr]
         dims = qs.dimensions or list(ds.dims)
         mets = qs.metrics or list(ds.metrics)
-        data: Dict[str, np.ndarray] = {}
-        u = ds.time_unit_ms
-        data["timestamp"] = ds.time[page].to(torch.int64).cpu().numpy() * u
-        for d in dims:
-            ids = column_tensor(ds, d)[page].to(torch.int64).cpu().numpy()
-            data[d] = DictColumn(ids, ds.dims[d].dictionary)
+        # one int64 block per page: time, dimension ids, metric bit patterns -> a single device
+        # gather across ranks (C4: per-GPU compaction, then a GatherV of the page)
+        parts = [ds.time[page].to(torch.int64)]
+        parts += [column_tensor(ds, d)[page].to(torch.int64) for d in dims]
         for m in mets:
+            v = ds.metrics[m].data[page]
+            parts.append(v.contiguous().view(torch.int64) if v.dtype == torch.float64 else v.to(torch.int64))
+        block = torch.stack(parts, dim=1) if page.numel() else \
+            torch.zeros((0, len(parts)), dtype=torch.int64, device=rows.device)
+        if W > 1:
+            blocks = self.world.all_gather_varlen(block)
+            ns = [int(x.shape[0]) for x in blocks]
+            block = torch.cat(blocks)
+        else:
+            ns = [int(block.shape[0])]
+        host = block.cpu().numpy()
+        data: Dict[str, np.ndarray] = {"timestamp": host[:, 0] * ds.time_unit_ms}
+        for j, d in enumerate(dims):
+            data[d] = DictColumn(host[:, 1 + j], ds.dims[d].dictionary)
+        for j, m in enumerate(mets):
             mc = ds.metrics[m]
-            v = mc.data[page].cpu().numpy()
-            if mc.kind == "decimal" and mc.scale:
+            v = host[:, 1 + len(dims) + j]
+            if mc.data.dtype == torch.float64:
+                v = v.view(np.float64)
+            elif mc.kind == "decimal" and mc.scale:
                 v = v.astype(np.float64) / (10.0 ** mc.scale)
             data[m] = v
-        if self.world.distributed:
-            # gather every rank's page to all ranks (each shard pages independently)
-            gathered = _gather_columns(self.world, data)
-            data = gathered
         cols = ["timestamp"] + list(dims) + list(mets)
-        nxt = {ident: start + int(page.numel()) - 1} if page.numel() else {ident: start - 1}
+        nxt = {f"{ds.name}_{r}": start_of(r) + ns[r] - 1 for r in range(W)}
         return QueryResult(cols, data, "select", {"rows": int(rows.numel())}, paging=nxt)
 
 
@@ -694,17 +733,6 @@ def combine_local(prog: ScanProgram, parts: List[Partials]) -> Partials:
         hll = [torch.stack([p.hll[i] for p in parts]).amax(dim=0) for i in range(len(parts[0].hll))]
         return Partials("dense", acc, None, hll)
     return merge_sparse([p.compact() for p in parts], prog.slots)
-
-
-def _gather_columns(world: World, data: Dict[str, np.ndarray]) -> Dict[str, np.ndarray]:
-    import torch.distributed as dist
-
-    lst = [None] * world.size
-    dist.all_gather_object(lst, {k: materialize(v) for k, v in data.items()})
-    out = {}
-    for k in data:
-        out[k] = np.concatenate([np.asarray(d[k]) for d in lst])
-    return out
 
 
 def _sorted_unique_pairs(g: torch.Tensor, h: torch.Tensor) -> torch.Tensor:

@@ -50,6 +50,9 @@ class Operation:
         self.cols: List[list] = []
         self.nrows = 0
         self.cursor = 0
+        self.base = 0
+        self.stream = None
+        self.factory = None
         self.started = int(time.time() * 1000)
         self.completed = 0
         self.thread: Optional[threading.Thread] = None
@@ -66,6 +69,43 @@ class Operation:
         self.names, self.types = list(names), list(types)
         self.cols = [df.iloc[:, i].tolist() for i in range(df.shape[1])]
         self.nrows = len(df)
+        self.base = 0
+        self.stream = None
+
+    def set_stream(self, names, types, pages_factory):
+        """Rows produced page by page (a pushed Select's cursor, session.DataFrame.iter_batches):
+        FetchResults pulls pages on demand and only the unread rows stay buffered."""
+        self.names, self.types = list(names), list(types)
+        self.cols = [[] for _ in self.names]
+        self.nrows = 0
+        self.base = 0  # absolute offset of the first buffered row
+        self.factory = pages_factory
+        self.stream = pages_factory()
+
+    def fill(self, upto: int) -> None:
+        """Buffer rows until ``upto`` (absolute) rows are available or the stream ends."""
+        while self.stream is not None and self.nrows < upto:
+            page = next(self.stream, None)
+            if page is None:
+                self.stream = None
+                break
+            for i in range(len(self.names)):
+                self.cols[i].extend(page.iloc[:, i].tolist())
+            self.nrows += len(page)
+
+    def trim(self) -> None:
+        """Drop rows before the cursor (streamed results keep one page of lookahead)."""
+        k = self.cursor - self.base
+        if self.factory is not None and k > 0:
+            self.cols = [c[k:] for c in self.cols]
+            self.base = self.cursor
+
+    def rewind(self) -> None:
+        if getattr(self, "factory", None) is not None and self.base > 0:
+            self.cols = [[] for _ in self.names]
+            self.nrows = self.base = 0
+            self.stream = self.factory()
+        self.cursor = 0
 
 
 class HiveThriftServer:
@@ -261,6 +301,15 @@ class HiveThriftServer:
                 for k, v in overlay.items():
                     sess.conf.set(k, v)
                 df = sess.sql(stmt)
+                if df.plan is not None and df._stream_source()[1] is not None and \
+                        sess.conf.typed("spark.sparklinedata.druid.stream.results"):
+                    # Select-backed result: stream pages to the client instead of materialising
+                    op.set_stream(df.columns, [t for _, t in df.schema],
+                                  lambda df=df: df.iter_batches(token=op.token))
+                    op.fill(1)  # run the scan now: errors surface in ExecuteStatement
+                    op.state = T.OP_FINISHED if not op.cancelled.is_set() else T.OP_CANCELED
+                    op.completed = int(time.time() * 1000)
+                    return
                 if df.plan is None:  # a command: already executed by sql()
                     pdf = df.to_pandas()
                 else:
@@ -323,12 +372,17 @@ class HiveThriftServer:
         if op.state == T.OP_ERROR:
             return {"status": _err(op.error)}
         if req.get("orientation", 0) == 4:  # FETCH_FIRST
-            op.cursor = 0
+            op.rewind()
         n = int(req.get("maxRows", 1000) or 1000)
+        try:
+            op.fill(op.cursor + n + 1)  # one row of lookahead decides hasMoreRows
+        except Exception as e:  # noqa: BLE001  (a streamed page failed)
+            return {"status": _err(f"{type(e).__name__}: {e}")}
         a, b = op.cursor, min(op.nrows, op.cursor + n)
-        cols = [_tcolumn(op.types[i], op.cols[i][a:b]) for i in range(len(op.names))]
+        cols = [_tcolumn(op.types[i], op.cols[i][a - op.base:b - op.base]) for i in range(len(op.names))]
         op.cursor = b
-        return {"status": _ok(), "hasMoreRows": b < op.nrows,
+        op.trim()
+        return {"status": _ok(), "hasMoreRows": b < op.nrows or op.stream is not None,
                 "results": {"startRowOffset": a, "rows": [], "columns": cols}}
 
     # metadata calls -> result sets

@@ -15,7 +15,7 @@ from __future__ import annotations
 import json
 import threading
 import time
-from typing import Any, Dict, List, Optional, Sequence, Tuple
+from typing import Any, Dict, List, Optional, Sequence, Tuple, Iterator
 
 import numpy as np
 import pandas as pd
@@ -102,6 +102,51 @@ class DataFrame:
         return self._run(token).to_pandas(self.names)
 
     toPandas = to_pandas
+
+    def _stream_source(self):
+        """(Limit n or None, DruidQuery) when the plan is Project/Filter operators over a pushed
+        Select (the reference's push_project_and_filters path): those can run page by page."""
+        node, limit = self.plan, None
+        if isinstance(node, P.Limit):
+            limit, node = node.n, node.child
+        while isinstance(node, (P.Project, P.Filter)):
+            node = node.child
+        if isinstance(node, P.DruidQuery) and isinstance(node.spec, S.SelectSpec) and \
+                not S.find_deferred(node.spec) and not node.info.get("historical"):
+            return limit, node
+        return None, None
+
+    def iter_batches(self, page_rows: Optional[int] = None, token=None) -> Iterator[pd.DataFrame]:
+        """The result as a stream of pandas pages: a Select-backed plan is executed one Druid page
+        at a time (``spark.sparklinedata.druid.selectquery.pagesize`` rows per shard page, the
+        reference's DruidSelectResultIterator.scala:116-137 cursor), so host memory holds one page;
+        any other plan is computed, then sliced."""
+        page_rows = int(page_rows or self.session.conf.typed("spark.sparklinedata.druid.selectquery.pagesize"))
+        limit, dq = (None, None) if self.plan is None else self._stream_source()
+        if dq is None:
+            df = self.to_pandas(token)
+            for a in range(0, max(len(df), 1), page_rows):
+                if a < len(df) or a == 0:
+                    yield df.iloc[a: a + page_rows].reset_index(drop=True)
+            return
+        left = limit
+        for res in self.session.iter_select_pages(dq, page_rows):
+            ex = Executor(self.session, token)
+            ex.preload(dq, res)
+            b = self.session._with_sql(self.sql_text, lambda: ex.run(self.plan if limit is None else self.plan.child))
+            out = b.to_pandas(self.names)
+            if left is not None:
+                out = out.iloc[:left]
+                left -= len(out)
+            if len(out):
+                yield out
+            if left is not None and left <= 0:
+                return
+
+    def toLocalIterator(self, page_rows: Optional[int] = None) -> Iterator[tuple]:
+        """Rows one at a time over ``iter_batches`` (Spark's ``DataFrame.toLocalIterator``)."""
+        for page in self.iter_batches(page_rows):
+            yield from page.itertuples(index=False, name=None)
 
     def count(self) -> int:
         return self._run().n
@@ -316,6 +361,20 @@ class Session:
             self._tl.sql = prev
 
     # ------------------------------------------------------------------------------ druid exec
+    def iter_select_pages(self, dq: P.DruidQuery, page_rows: int) -> Iterator[Any]:
+        """Pages of a pushed Select: the engine computes the shard's selected rows once and each
+        page gathers ``page_rows`` rows per shard (engine/executor.py run_page); the paging
+        identifiers of one page are the cursor of the next."""
+        spec = dq.spec
+        prep = self.engine.prepare(spec.copy(pagingSpec=S.PagingSpec({}, page_rows)), dq.relation.info.datasource)
+        ident: Dict[str, int] = {}
+        while True:
+            res = prep.run_page(S.PagingSpec(dict(ident), page_rows))
+            if res.num_rows == 0:
+                return
+            yield res
+            ident = res.paging
+
     def run_druid(self, dq: P.DruidQuery):
         ds = dq.relation.info.datasource
         spec = dq.spec

@@ -224,6 +224,10 @@ class Executor:
         idx = np.nonzero(keep.to_numpy())[0]
         return lb.take(idx)
 
+    def preload(self, p: P.DruidQuery, res) -> None:
+        """Use ``res`` as the result of pushed query ``p`` (a streamed Select page)."""
+        self._druid_results[share_key(p)] = res
+
     def _DruidQuery(self, p: P.DruidQuery) -> Batch:
         t0 = time.perf_counter()
         if self._host_checks:
@@ -245,12 +249,7 @@ class Executor:
                                               p.info)
             p = q
         # identical pushed queries within one statement (a CTE referenced twice, TPC-H Q15) run once
-        key = p.__dict__.get("_share_key")
-        if key is None:
-            import json
-
-            key = p._share_key = json.dumps(p.spec.to_json(), sort_keys=True, default=str) + \
-                str(id(p.relation.info.datasource)) + repr(p.info.get("historical"))
+        key = share_key(p)
         res = self._druid_results.get(key)
         if res is None:
             res = self._druid_results[key] = self.session.run_druid(p)
@@ -260,6 +259,16 @@ class Executor:
             cols[r.rid] = druid_value_series(res.data[name], sqlt, kind, n)
         self.druid_stats.append({"spec": p.spec, "ms": (time.perf_counter() - t0) * 1e3, "rows": n})
         return Batch(p.refs, cols, n)
+
+
+def share_key(p: P.DruidQuery) -> str:
+    key = p.__dict__.get("_share_key")
+    if key is None:
+        import json
+
+        key = p._share_key = json.dumps(p.spec.to_json(), sort_keys=True, default=str) + \
+            str(id(p.relation.info.datasource)) + repr(p.info.get("historical"))
+    return key
 
 
 # ------------------------------------------------------------------------------------------------
