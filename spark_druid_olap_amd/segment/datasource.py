@@ -262,6 +262,10 @@ class DataSource:
             json.dump(man, f)
 
     @staticmethod
+    def concat(shards: Sequence["DataSource"]) -> "DataSource":
+        return concat_shards(shards)
+
+    @staticmethod
     def load(path: str, device="cpu", bitmap_max_card: int = 256) -> "DataSource":
         with open(os.path.join(path, "manifest.json")) as f:
             man = json.load(f)
@@ -293,6 +297,62 @@ class DataSource:
         ds.rollup = man.get("rollup", False)
         ds.build_indexes(bitmap_max_card=bitmap_max_card)
         return ds
+
+
+def concat_shards(shards: Sequence["DataSource"]) -> "DataSource":
+    """One shard holding the rows of several shards of the same datasource (same global
+    dictionaries), time-ordered: how a surviving GPU adopts a lost GPU's segments
+    (parallel/recovery.py).  Sketch columns (CSR) are re-offset row by row."""
+    a = shards[0]
+    for b in shards[1:]:
+        if set(b.dims) != set(a.dims) or set(b.metrics) != set(a.metrics):
+            raise ValueError("shards of different schemas")
+        for k, d in a.dims.items():
+            if len(d.dictionary) != len(b.dims[k].dictionary):
+                raise ValueError(f"dimension {k!r}: shards were encoded with different dictionaries")
+    dev = a.device
+    units = {s.time_unit_ms for s in shards}
+    unit = min(units)
+    th = np.concatenate([s.time_host.astype(np.int64) * (s.time_unit_ms // unit) for s in shards])
+    perm_h = np.argsort(th, kind="stable")
+    perm = torch.from_numpy(perm_h).to(dev)
+    n = len(th)
+
+    def cat(get):
+        return torch.cat([get(s)[: s.num_rows] for s in shards])
+
+    time_units = torch.from_numpy(th[perm_h]).to(dev)
+    dim_ids = {k: cat(lambda s, k=k: s.dims[k].ids)[perm] for k in a.dims}
+    dicts = {k: d.dictionary for k, d in a.dims.items()}
+    mdata = {k: cat(lambda s, k=k: s.metrics[k].data)[perm] for k in a.metrics}
+    ds = make_datasource(a.name, n, time_units, unit, dim_ids, dicts, mdata, {k: m.kind for k, m in a.metrics.items()},
+                         {k: m.scale for k, m in a.metrics.items()}, a.segment_granularity, a.query_granularity,
+                         a.partition, a.num_partitions, [k for k, d in a.dims.items() if d.spatial])
+    for k, m in a.metrics.items():
+        if m.sketch is None:
+            continue
+        offs, vals, base = [], [], 0
+        for s in shards:
+            sk = s.metrics[k].sketch
+            offs.append(sk.offsets[:-1] + base)
+            vals.append(sk.values)
+            base += int(sk.values.numel())
+        start = torch.cat(offs)
+        allv = torch.cat(vals)
+        cnt = torch.cat([s.metrics[k].sketch.offsets.diff() for s in shards])
+        start, cnt = start[perm], cnt[perm]
+        new_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        new_off[1:] = torch.cumsum(cnt, 0)
+        idx = torch.repeat_interleave(start - new_off[:-1], cnt) + torch.arange(int(cnt.sum()), device=dev)
+        ds.metrics[k].sketch = SketchColumn(k, m.sketch.kind, new_off, allv[idx].contiguous(), m.sketch.p,
+                                            m.sketch.salt, m.sketch.size)
+    ds.shard_key = a.shard_key
+    ds.spatial = getattr(a, "spatial", {})
+    ds.rollup = getattr(a, "rollup", False)
+    ds.global_num_rows = a.global_num_rows
+    ds.build_indexes(bitmap_max_card=max((d.cardinality for d in a.dims.values() if d.bitmap is not None),
+                                         default=0))
+    return ds
 
 
 def build_bitmap(ids: torch.Tensor, num_rows: int, card: int) -> torch.Tensor:

@@ -651,6 +651,9 @@ def main(argv=None):
     ap.add_argument("--segments", default=None,
                     help="segment store root: load every datasource saved under DIR/<datasource>/rank<r> "
                          "(resume after restart); with --ingest, the ingested shards are saved there")
+    ap.add_argument("--elastic", action="store_true",
+                    help="survive a lost GPU process: heartbeats, communicator rebuild over the survivors and "
+                         "re-homing of its shards from --segments (parallel/recovery.py)")
     a = ap.parse_args(argv)
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         import sys
@@ -677,6 +680,10 @@ def main(argv=None):
         sess.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)
         sess.sql(tpch.druid_ddl(with_column_mapping=False))
     _load_datasources(sess, world, a.ingest, a.segments, dev)
+    if a.elastic and world.distributed:
+        from ..parallel import recovery
+
+        recovery.enable(world, segment_store=a.segments)
     if a.init_sql:
         with open(a.init_sql) as f:
             for st in f.read().split(";"):

@@ -120,7 +120,12 @@ class SpmdDispatcher:
             except queue.Empty:
                 if self._stop.is_set():
                     break
-                w.broadcast_object({"op": "noop"})
+                try:
+                    w.broadcast_object({"op": "noop"})
+                except BaseException as e:  # noqa: BLE001
+                    if not _elastic_recover(self.root, e):
+                        raise
+                    w = self.world = self.root.engine.world
                 self.stats["heartbeats"] += 1
                 continue
             batch = [first]
@@ -134,13 +139,19 @@ class SpmdDispatcher:
             try:
                 w.broadcast_object({"op": "batch", "msgs": msgs})
             except BaseException as e:  # noqa: BLE001
+                if _elastic_recover(self.root, e):  # a peer is gone: rebuild, then serve again
+                    w = self.world = self.root.engine.world
+                    for it in batch:
+                        self._q.put(it)
+                    continue
                 for it in batch:
                     it.error = e
                     it.event.set()
                 raise
             for g in groups:
                 try:
-                    res = _execute(self.sessions, self.root, g[0].msg)
+                    res = _run_elastic(self.root, lambda m=g[0].msg: _execute(self.sessions, self.root, m))
+                    w = self.world = self.root.engine.world
                     for it in g:
                         it.result = res
                 except BaseException as e:  # noqa: BLE001  (every rank raised the same way)
@@ -182,11 +193,37 @@ def _is_query(stmt: str) -> bool:
     return head in ("select", "with")
 
 
+def _elastic_recover(session, e: BaseException) -> bool:
+    """Elastic mode (parallel/recovery.py enabled): a collective failed because a rank is gone --
+    agree, rebuild the communicator over the survivors and re-home the lost shards."""
+    from ..parallel import recovery
+
+    if not recovery.is_comm_failure(e):
+        return False
+    log.warning("SPMD stream: collective failed (%s), recovering", e)
+    recovery.recover(session)
+    return True
+
+
+def _run_elastic(session, fn):
+    from ..parallel import recovery
+
+    if recovery.state() is None:
+        return fn()
+    return recovery.run_with_recovery(session, fn)
+
+
 def serve_peer(session, world) -> None:
     """Ranks 1..N-1: execute the statement stream broadcast by rank 0 until it stops."""
     sessions: Dict[bytes, Any] = {}
     while True:
-        msg = world.broadcast_object(None)
+        try:
+            msg = world.broadcast_object(None)
+        except BaseException as e:  # noqa: BLE001
+            if not _elastic_recover(session, e):
+                raise
+            world = session.engine.world
+            continue
         op = msg.get("op")
         if op == "stop":
             return
@@ -194,6 +231,7 @@ def serve_peer(session, world) -> None:
             continue
         for m in msg.get("msgs", []):
             try:
-                _execute(sessions, session, m)
+                _run_elastic(session, lambda m=m: _execute(sessions, session, m))
+                world = session.engine.world
             except BaseException as e:  # noqa: BLE001  (rank 0 reports the error to the client)
                 log.debug("peer statement failed: %s", e)

@@ -1,0 +1,105 @@
+"""Elastic recovery: a rank dies outright; the survivors detect it in the
+query's collective, agree on the membership through the rendezvous store, rebuild the process
+group over themselves, re-home the dead rank's shard from the segment store, and re-run the
+query -- which must return exactly the answer of the full world."""
+import os
+import pickle
+import socket
+import tempfile
+
+import pytest
+import torch.multiprocessing as mp
+
+QUERIES = [
+    "select l_returnflag, l_linestatus, count(*), sum(l_quantity), sum(l_extendedprice) "
+    "from orderLineItemPartSupplier group by l_returnflag, l_linestatus",
+    "select s_nation, count(*) from orderLineItemPartSupplier where s_region = 'ASIA' group by s_nation",
+    "select o_orderkey, sum(l_quantity) q from orderLineItemPartSupplier group by o_orderkey having sum(l_quantity) > 150",
+]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _norm(rows):
+    return sorted(tuple(round(x, 6) if isinstance(x, float) else x for x in r) for r in rows)
+
+
+def _worker(rank, world, port, outdir, victim):
+    try:
+        _work(rank, world, port, outdir, victim)
+    except BaseException:
+        import traceback
+
+        with open(os.path.join(outdir, f"err{rank}.txt"), "w") as f:
+            f.write(traceback.format_exc())
+        raise
+
+
+def _work(rank, world, port, outdir, victim):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), OMP_NUM_THREADS="1", SDO_COLLECTIVE_TIMEOUT_S="30")
+    from spark_druid_olap_amd.engine.executor import Engine
+    from spark_druid_olap_amd.models import tpch
+    from spark_druid_olap_amd.parallel import recovery
+    from spark_druid_olap_amd.parallel.world import init_world
+    from spark_druid_olap_amd.session import Session
+
+    w = init_world(backend="gloo")
+    recovery.enable(w, interval_s=0.2)
+    store = os.path.join(outdir, "store")
+    ds = tpch.to_datasource(tpch.generate_flat(0.004, "cpu", rank=rank, world=world), profile="bench")
+    ds.save(os.path.join(store, ds.name, f"rank{rank}"))
+    s = Session(engine=Engine(w, use_native=False))
+    s.register_datasource(ds)
+    s.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)
+    s.sql(tpch.druid_ddl(with_column_mapping=False))
+    full = {q: _norm(s.sql(q).collect()) for q in QUERIES}
+    w.barrier()
+    if rank == victim:
+        os._exit(0)  # the GPU process dies without a word
+    got, info = {}, None
+    for q in QUERIES:
+        def run(q=q):
+            return _norm(s.sql(q).collect())
+        if info is None:
+            try:
+                got[q] = run()
+                raise AssertionError("the collective should have failed with a dead peer")
+            except AssertionError:
+                raise
+            except Exception:  # noqa: BLE001  -- the failure run_with_recovery would see
+                info = recovery.recover(s, store, stale_s=1.5, settle_s=15)
+        got[q] = recovery.run_with_recovery(s, run, store)
+    with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
+        pickle.dump({"full": full, "got": got, "info": info, "world": (s.engine.world.rank, s.engine.world.size)}, f)
+    import torch.distributed as dist
+
+    dist.barrier()
+    recovery.state().stop()
+
+
+@pytest.mark.parametrize("victim", [2, 1])
+def test_survivors_rebuild_and_rehome_the_lost_shard(victim):
+    world = 3
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.start_processes(_worker, args=(world, _free_port(), d, victim), nprocs=world, join=False,
+                                 start_method="spawn")
+        for p in ctx.processes:
+            p.join(240)
+        errs = [open(os.path.join(d, f)).read() for f in sorted(os.listdir(d)) if f.startswith("err")]
+        assert all(p.exitcode == 0 for p in ctx.processes), ([p.exitcode for p in ctx.processes], errs)
+        outs = {r: pickle.load(open(os.path.join(d, f"r{r}.pkl"), "rb")) for r in range(world) if r != victim}
+    survivors = sorted(outs)
+    for r, o in outs.items():
+        assert o["info"]["failed"] == [victim] and o["info"]["members"] == survivors
+        assert o["world"] == (survivors.index(r), world - 1)
+        for q in QUERIES:
+            assert o["got"][q] == o["full"][q], q
+    adopted = [a for o in outs.values() for a in o["info"]["adopted"]]
+    assert adopted == [("tpch", victim)]
