@@ -917,6 +917,12 @@ class Engine:
             from .nested import NestedPreparedQuery
 
             return NestedPreparedQuery(self, qs, ds, segments_per_query)
+        from ..segment.streamed import HostShard
+
+        if isinstance(ds, HostShard):  # larger than HBM: streamed window by window
+            from ..segment.streamed import StreamedQuery
+
+            return StreamedQuery(self, qs, ds)
         return PreparedQuery(self, qs, ds, segments_per_query)
 
     def execute(self, qs: S.QuerySpec, ds: DataSource, segments_per_query: Optional[int] = None) -> QueryResult:

@@ -813,11 +813,13 @@ class Lowerer:
 
     def _metric_range(self, metric: str) -> Tuple[int, int]:
         """Global (all ranks) min/max of a metric's stored integer values, cached on the metric."""
-        m = self.ds.metrics[metric]
+        # a streamed window (segment/streamed.py) measures (and caches on) its whole host shard
+        src = getattr(self.ds, "fd_source", None) or self.ds
+        m = src.metrics[metric]
         rng = getattr(m, "_value_range", None)
         if rng is None:
             # global value range (every rank must build the same key space)
-            t = column_tensor(self.ds, metric)[:self.ds.num_rows]
+            t = column_tensor(src, metric)[:src.num_rows]
             big = 2 ** 62
             lo_t = (t.min() if t.numel() else torch.tensor(big, device=t.device)).to(torch.int64).reshape(1)
             hi_t = (t.max() if t.numel() else torch.tensor(-big, device=t.device)).to(torch.int64).reshape(1)
@@ -1500,6 +1502,7 @@ def fd_metric_table(ds: DataSource, a: str, metric: str, world=None) -> Optional
     dimension ``a`` (o_totalprice per order, c_acctbal per customer); cached per datasource."""
     cache = ds.__dict__.setdefault("_fd_cache", {})
     key = (a, "metric:" + metric)
+    ds = getattr(ds, "fd_source", None) or ds  # streamed window: decide over the whole shard
     if key not in cache:
         cache[key] = _fd_lut(ds.dims[a].ids, len(ds.dims[a].dictionary), column_tensor(ds, metric), ds.num_rows,
                              world)
@@ -1514,6 +1517,7 @@ def fd_table(ds: DataSource, a: str, b: str, world=None) -> Optional[torch.Tenso
     key = (a, b)
     if key in cache:
         return cache[key]
+    ds = getattr(ds, "fd_source", None) or ds  # streamed window: decide over the whole shard
     da, db = ds.dims[a], ds.dims[b]
     ca = len(da.dictionary)
     dev = da.ids.device
