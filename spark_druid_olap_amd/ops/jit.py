@@ -118,6 +118,11 @@ def reg_eligible(prog, mode: int) -> bool:
     return regs <= REG_BUDGET
 
 
+# accumulator copies per wave for tiny dense key spaces (lanes l, l+C, l+2C.. share copy l % C; up
+# to 64 = lane-private, no same-address LDS atomics) -- the LDS budget may halve it
+MAX_NCOPY = int(os.environ.get("SDO_JIT_NCOPY", "16"))
+
+
 def layout(prog, mode: int, U: int, hll_lds: bool, m: int, reg: bool = False, pipe: bool = False,
            budget: int = 150 * 1024, regstage: bool = False, shared: bool = False) -> JitLayout:
     cols = col_infos(prog)
@@ -136,7 +141,7 @@ def layout(prog, mode: int, U: int, hll_lds: bool, m: int, reg: bool = False, pi
         acc_bytes = prog.G * prog.nslots * 8
     elif mode == D.M_DENSE_LDS:
         base = prog.G * prog.nslots * 8 * W
-        ncopy = 1 if reg else 16
+        ncopy = 1 if reg else MAX_NCOPY
         while ncopy > 1 and base * ncopy + hll_bytes + stage > budget:
             ncopy //= 2
         acc_bytes = base * ncopy

@@ -2,7 +2,7 @@
 
   python tools/query_probe.py SF [variant ...] [-- query names]
 
-A variant is ``reg{0|1}pipe{0|1}[b<workgroups per CU>][slds|sreg]``: register accumulators,
+A variant is ``reg{0|1}pipe{0|1}[b<workgroups per CU>][c<accumulator copies per wave>][slds|sreg]``: register accumulators,
 double-buffered DMA, target workgroups per CU, forced LDS-DMA / VGPR staging (see ops/jit.py);
 results of every variant are checked against the first one.  Used to locate slow or hung kernels
 and to A/B kernel-generation choices on the GPU box."""
@@ -73,10 +73,17 @@ def main():
     print(f"data ready sf={sf} rows={ds.num_rows}", flush=True)
     specs = bench_specs() + extra_specs()
     base = {}
+    import re
+
+    from spark_druid_olap_amd.ops import jit as J
+
     for var in variants:
         DE.USE_REG = "reg1" in var
         DE.USE_PIPE = "pipe1" in var
-        DE.JIT_BLOCKS = int(var.split("b")[-1].split("s")[0]) if "b" in var else 3
+        mb = re.search(r"b(\d+)", var)
+        DE.JIT_BLOCKS = int(mb.group(1)) if mb else 3
+        mc = re.search(r"c(\d+)", var)
+        J.MAX_NCOPY = int(mc.group(1)) if mc else 16
         DE.JIT_STAGE = "lds" if "slds" in var else ("reg" if "sreg" in var else "auto")
         DE.BLOCKS_PER_CU = max(3, DE.JIT_BLOCKS)
         print(f"== {var}", flush=True)
