@@ -116,6 +116,10 @@ def segment_metadata(ds) -> List[Dict[str, Any]]:
              "size": int(ds.size_bytes()), "numRows": int(getattr(ds, "global_num_rows", ds.num_rows))}]
 
 
+class PlainText(str):
+    """Marker type: sent as text/plain (Prometheus exposition format)."""
+
+
 class DruidHTTPServer:
     def __init__(self, session, host: str = "127.0.0.1", port: int = 8082):
         self.session = session
@@ -154,6 +158,8 @@ class DruidHTTPServer:
             if qid in self.cancelled:
                 self.cancelled.discard(qid)
                 token.cancel(f"query {qid} cancelled")
+        t0 = time.perf_counter()
+        ok = False
         try:
             with scope(token):
                 token.check()
@@ -162,9 +168,14 @@ class DruidHTTPServer:
             if self.session.conf.typed("spark.sparklinedata.enable.druid.query.history"):
                 self.session.history.record(spec, res.stats.get("exec_ms", 0.0), res.stats.get("exec_ms", 0.0),
                                             res.num_rows, "http", None)
-            return format_result(spec, res)
+            out = format_result(spec, res)
+            ok = True
+            return out
         finally:
             self.running.pop(qid, None)
+            from ..utils.metrics import metrics_of
+
+            metrics_of(self.session).record("druid_http", (time.perf_counter() - t0) * 1e3, ok)
 
     # -------------------------------------------------------------------------------- routes
     def handle(self, method: str, path: str, query: Dict[str, List[str]], body: Optional[bytes]):
@@ -174,6 +185,14 @@ class DruidHTTPServer:
             return 200, queries_page(self.session.history.entries())
         if method == "GET" and parts == ["sparklinedata", "druid", "queries.json"]:
             return 200, self.session.history.rows()
+        if method == "GET" and parts == ["sparklinedata", "metrics"]:
+            from ..utils.metrics import metrics_of
+
+            return 200, metrics_of(self.session).snapshot()
+        if method == "GET" and parts == ["metrics"]:  # Prometheus text exposition
+            from ..utils.metrics import metrics_of
+
+            return 200, PlainText(metrics_of(self.session).prometheus())
         if method == "GET" and parts == ["status"]:
             return 200, {"version": "spark-druid-olap-amd", "modules": [], "gpus": self.session.engine.world.size}
         if parts[:2] == ["druid", "v2"]:
@@ -278,6 +297,8 @@ class DruidHTTPServer:
             def _send(self, code, obj):
                 if isinstance(obj, HTMLPage):
                     data, ct = obj.encode("utf-8"), "text/html; charset=utf-8"
+                elif isinstance(obj, PlainText):
+                    data, ct = obj.encode("utf-8"), "text/plain; version=0.0.4"
                 elif getattr(self, "_smile", False):
                     data, ct = smile.dumps(json.loads(json.dumps(obj, default=_py))), smile.MIME
                 else:

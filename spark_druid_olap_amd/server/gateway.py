@@ -208,6 +208,12 @@ class NativeHiveServer(HiveThriftServer):
             self._publish(op.session_id)  # SET / USE / CREATE TEMPORARY VIEW may have changed it
 
     # ------------------------------------------------------------------ batch executors
+    @property
+    def _metrics(self):
+        from ..utils.metrics import metrics_of
+
+        return metrics_of(self.session)
+
     def _executor(self):
         gw = self._gw
         while not self._stop.is_set():
@@ -215,12 +221,15 @@ class NativeHiveServer(HiveThriftServer):
             if b is None:
                 continue
             bid, sid, stmt = b
+            t0 = time.perf_counter()
             try:
                 names, types, pdf = self._execute(bid, sid, stmt)
+                self._metrics.record("gateway", (time.perf_counter() - t0) * 1e3, True)
                 schema = encode_schema(names, types)
                 cols = encode_columns(types, pdf)
                 gw.finish_batch(bid, schema, cols, len(pdf), None)
             except Exception as e:  # noqa: BLE001  (every attached operation reports it)
+                self._metrics.record("gateway", (time.perf_counter() - t0) * 1e3, False)
                 log.debug("batch %d failed: %s", bid, e)
                 try:
                     gw.finish_batch(bid, b"", [], 0, f"{type(e).__name__}: {e}")

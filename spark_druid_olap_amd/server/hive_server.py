@@ -285,6 +285,15 @@ class HiveThriftServer:
         return {"status": _ok(), "operationHandle": op.handle()}
 
     def _run(self, op: Operation, stmt: str, overlay: Dict[str, str]):
+        from ..utils.metrics import metrics_of
+
+        t0 = time.perf_counter()
+        try:
+            self._run_stmt(op, stmt, overlay)
+        finally:
+            metrics_of(self.session).record("thrift", (time.perf_counter() - t0) * 1e3, op.state != T.OP_ERROR)
+
+    def _run_stmt(self, op: Operation, stmt: str, overlay: Dict[str, str]):
         op.state = T.OP_RUNNING
         try:
             if op.cancelled.is_set():

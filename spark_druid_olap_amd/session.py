@@ -193,6 +193,9 @@ class Session:
         self.conf = Conf(conf)
         self.catalog = Catalog()
         self.history = DruidQueryHistory(int(self.conf.typed("sparkline.queryhistory.maxsize")))
+        from .utils.metrics import ServerMetrics
+
+        self.metrics = ServerMetrics()  # per-endpoint latency percentiles / QPS (servers record)
         self._plan_cache: Dict[Tuple[str, int, int, str], DataFrame] = {}
         self._lock = threading.RLock()
         self._tl = threading.local()
@@ -212,6 +215,7 @@ class Session:
         s.conf = self.conf.copy()
         s.catalog = self.catalog.session_view()
         s.history = self.history
+        s.metrics = self.metrics
         # plans (and their prepared GPU queries and per-slot device buffers) are shared by every
         # session whose statement text, conf, current database and temp views match (the cache key)
         s._plan_cache = self._plan_cache
