@@ -58,13 +58,15 @@ def test_streamed_copies_only_the_columns_read(ds_small):
 
 
 @pytest.mark.gpu
-def test_gpu_streamed_equals_resident():
+def test_gpu_streamed_equals_resident(tmp_path):
     """Host shard streamed through the HIP kernels with double-buffered H2D copies vs the same
-    shard resident in HBM."""
+    shard resident in HBM (the same rows: saved once, loaded on each side)."""
     from spark_druid_olap_amd.models import tpch
+    from spark_druid_olap_amd.segment.datasource import DataSource
 
-    host = tpch.to_datasource(tpch.generate_flat(0.1, "cpu"), profile="bench")
-    dev = tpch.to_datasource(tpch.generate_flat(0.1, "cuda"), profile="bench")
+    tpch.to_datasource(tpch.generate_flat(0.1, "cpu"), profile="bench").save(str(tmp_path / "s"))
+    host = DataSource.load(str(tmp_path / "s"), "cpu")
+    dev = DataSource.load(str(tmp_path / "s"), "cuda")
     eng = Engine(use_native=True)
     shard = HostShard(host, "cuda", window_rows=1 << 17)
     assert shard.copy_stream is not None and len(shard.windows) >= 4
