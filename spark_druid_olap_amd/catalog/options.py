@@ -135,6 +135,8 @@ CONF_ENTRIES: List[ConfEntry] = [
               "push COUNT(DISTINCT x) as a cardinality (HLL) aggregator instead of the exact 2-level rewrite", bool),
     ConfEntry("spark.sparklinedata.druid.planCache.enabled", True, "cache optimized plans by SQL text", bool),
     ConfEntry("spark.sparklinedata.druid.query.timeout.ms", 0, "per-query deadline (0 = none)", int),
+    ConfEntry("spark.sparklinedata.druid.fuse.groupingsets", True,
+              "answer the per-set Druid queries of CUBE / ROLLUP / GROUPING SETS from one scan", bool),
     ConfEntry("spark.sparklinedata.druid.deterministic", False,
               "float sums in exact fixed point: bitwise reproducible results under any reduction order", bool),
     ConfEntry("sparkline.queryhistory.maxsize", 500, "query history capacity", int),

@@ -925,5 +925,155 @@ class Engine:
             return StreamedQuery(self, qs, ds)
         return PreparedQuery(self, qs, ds, segments_per_query)
 
+    def execute_sets(self, specs, ds: DataSource, out_types=None) -> Optional[List[QueryResult]]:
+        """Grouping-set queries from one scan (``execute_grouping_sets``); None if not fusable."""
+        return execute_grouping_sets(self, specs, ds, out_types)
+
     def execute(self, qs: S.QuerySpec, ds: DataSource, segments_per_query: Optional[int] = None) -> QueryResult:
         return self.prepare(qs, ds, segments_per_query).run()
+
+
+# ---------------------------------------------------------------------------------------------
+# Grouping sets in one scan (SURVEY C5 / 2.5 "query-level fan-out": the reference issues one Druid
+# query per grouping set and unions them, asd/DruidStrategy.scala:74-75)
+_SET_FIELDS = ("dataSource", "intervals", "granularity", "filter")
+
+
+def _set_signature(qs) -> str:
+    import json
+
+    d = qs.to_json()
+    return json.dumps({k: d.get(k) for k in _SET_FIELDS}, sort_keys=True, default=str)
+
+
+def _set_dims(qs):
+    return list(getattr(qs, "dimensions", None) or [])  # a timeseries is the empty grouping set
+
+
+def _union_by_name(items, name_of) -> Optional[list]:
+    """Union of specs keyed by output name; None if one name carries two different specs."""
+    import json
+
+    out, seen = [], {}
+    for it in items:
+        enc = json.dumps(it.to_json(), sort_keys=True, default=str)
+        k = name_of(it)
+        if k in seen:
+            if seen[k] != enc:
+                return None
+            continue
+        seen[k] = enc
+        out.append(it)
+    return out
+
+
+def fused_spec(specs):
+    """The one groupBy answering every grouping set: the union of their dimensions and aggregators
+    (None when the specs are not fusable: different source / filter / intervals / granularity,
+    post-processing of their own, or one output name meaning two things)."""
+    if len(specs) < 2 or any(not isinstance(q, (S.GroupByQuerySpec, S.TimeSeriesQuerySpec)) for q in specs):
+        return None
+    if not any(isinstance(q, S.GroupByQuerySpec) for q in specs):
+        return None
+    if any(getattr(q, "having", None) is not None or getattr(q, "limitSpec", None) is not None or q.postAggregations
+           or getattr(q, "descending", False) or isinstance(q.dataSource, S.QueryDataSourceSpec) for q in specs):
+        return None
+    sig = _set_signature(specs[0])
+    if any(_set_signature(q) != sig for q in specs[1:]):
+        return None
+    dims = _union_by_name([d for q in specs for d in _set_dims(q)], lambda d: d.outputName)
+    aggs = _union_by_name([a for q in specs for a in (q.aggregations or [])], lambda a: a.name)
+    if dims is None or aggs is None:
+        return None
+    q0 = specs[0]
+    return S.GroupByQuerySpec(q0.dataSource, dims, filter=q0.filter, granularity=q0.granularity,
+                              aggregations=aggs, intervals=q0.intervals)
+
+
+def fusable_sets(specs) -> bool:
+    """Plain groupBys (and the empty set's timeseries) over the same source, filter, intervals and
+    granularity -- a CUBE / ROLLUP / GROUPING SETS expansion."""
+    return fused_spec(specs) is not None
+
+
+def _shell(engine, qs, ds) -> "PreparedQuery":
+    """A PreparedQuery without a scan of its own: runs the post-merge tail (having / top-k prune /
+    finalize / post-processing) for ``qs`` over partials computed elsewhere."""
+    sh = PreparedQuery.__new__(PreparedQuery)
+    sh.engine, sh.qs, sh.ds, sh.world = engine, qs, ds, engine.world
+    sh.window, sh.scans, sh.segments_per_query = None, [], None
+    return sh
+
+
+def execute_grouping_sets(engine, specs, ds, out_types=None) -> Optional[List[QueryResult]]:
+    """Answer several grouping-set queries from ONE scan: the widest set's groupBy runs once (scan
+    + cross-GPU merge), then each set re-aggregates the merged fine partials on the device by its
+    projected key (sum / min / max slot ops, HLL registers by max -- every pushed aggregator is
+    decomposable).  None when the specs are not fusable (theta sketches, functionally-eliminated
+    keys, non-injective key formats): the caller runs them one by one."""
+    import copy
+    import dataclasses
+    import json
+
+    widest = fused_spec(specs)
+    if widest is None:
+        return None
+    cache = engine.__dict__.setdefault("_sets_cache", {})
+    key = (json.dumps(widest.to_json(), sort_keys=True, default=str), id(ds))
+    pq = cache.get(key)
+    if pq is None:
+        pq = PreparedQuery(engine, widest, ds)
+        if len(cache) > 32:
+            cache.clear()
+        cache[key] = pq
+    fine = pq._full_prog
+    if fine.thetas or fine.stored_hll or fine.derived_aggs or any(kc.collapse for kc in fine.keys):
+        return None
+    t0 = time.perf_counter()
+    prog, part, _ = pq.run_partials(t0)
+    fp = part.compact()
+    g = fp.keys.to(torch.int64)
+    from .partials import merge_sparse
+
+    fine_ids = [torch.remainder(torch.div(g, kc.stride, rounding_mode="floor"), max(1, kc.card)) for kc in prog.keys]
+    out = []
+    for i, qs in enumerate(specs):
+        names = {d.outputName for d in _set_dims(qs)}
+        keep = [j for j, kc in enumerate(prog.keys) if kc.name in names or kc.is_timestamp]
+        keys = [copy.copy(prog.keys[j]) for j in keep]
+        comps = [fine_ids[j] for j in keep]
+        derived = []
+        for kc, det, lut in prog.derived:
+            if kc.name not in names:
+                continue
+            if det in keep:  # still functionally determined by a kept key: stays derived
+                derived.append((kc, keep.index(det), lut))
+                continue
+            # its determinant is not in this set: the dependent dimension becomes a real key,
+            # its ids looked up from the fine determinant ids (the FD table)
+            did = fine_ids[det]
+            orig = prog.keys[det].orig
+            if orig is not None:
+                did = torch.from_numpy(orig).to(did.device)[did]
+            k2 = copy.copy(kc)
+            k2.orig, k2.remap = None, None
+            keys.append(k2)
+            comps.append(lut.to(did.device)[did].to(torch.int64))
+        G = 1
+        for kc in reversed(keys):
+            kc.stride = G
+            G *= max(1, kc.card)
+        coarse = dataclasses.replace(prog, keys=keys, G=G, derived=derived,
+                                     key_order=[n for n in prog.key_order if n in names or n == "timestamp"])
+        ck = torch.zeros_like(g)
+        for kc, ids in zip(keys, comps):
+            ck += ids * kc.stride
+        cp = merge_sparse([Partials("sparse", fp.acc, ck, fp.hll)], prog.slots) if g.numel() else \
+            Partials("sparse", fp.acc, ck, fp.hll)
+        sh = _shell(engine, qs, ds)
+        sh._full_prog = coarse
+        cols = finalize(coarse, cp, out_types[i] if out_types else None)
+        res = sh._post(coarse, cols)
+        res.stats.update(fused_sets=len(specs), exec_ms=(time.perf_counter() - t0) * 1e3)
+        out.append(res)
+    return out

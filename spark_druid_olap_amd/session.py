@@ -379,6 +379,23 @@ class Session:
             yield res
             ident = res.paging
 
+    def run_druid_sets(self, dqs: List[P.DruidQuery]):
+        """Grouping-set branches from one engine scan (engine/executor.py execute_grouping_sets);
+        None when they cannot be fused (each branch then runs on its own)."""
+        if not self.conf.typed("spark.sparklinedata.druid.fuse.groupingsets"):
+            return None
+        ds = dqs[0].relation.info.datasource
+        t0 = time.perf_counter()
+        out_types = [{n: t for n, t, k in dq.columns if k == "value"} for dq in dqs]
+        res = self.engine.execute_sets([dq.spec for dq in dqs], ds, out_types)
+        if res is not None and self.conf.typed("spark.sparklinedata.enable.druid.query.history"):
+            ms = (time.perf_counter() - t0) * 1e3
+            for dq, r in zip(dqs, res):
+                self.history.record(dq.spec, r.stats.get("exec_ms", ms), ms, r.num_rows,
+                                    f"gpu:0-{self.engine.world.size - 1}", getattr(self._tl, "sql", None),
+                                    len(ds.segments))
+        return res
+
     def run_druid(self, dq: P.DruidQuery):
         ds = dq.relation.info.datasource
         spec = dq.spec

@@ -200,6 +200,7 @@ class Executor:
         return join(p, lb, rb, self._subquery)
 
     def _Union(self, p: P.Union) -> Batch:
+        self._fuse_grouping_sets(p)
         parts = [self.run(c) for c in p.children]
         cols = {}
         n = sum(b.n for b in parts)
@@ -223,6 +224,25 @@ class Executor:
         keep = (m["_merge"] == "both") if p.kind == "intersect" else (m["_merge"] == "left_only")
         idx = np.nonzero(keep.to_numpy())[0]
         return lb.take(idx)
+
+    def _fuse_grouping_sets(self, p: P.Union) -> None:
+        """A UNION of pushed groupBys that differ only in their dimensions (CUBE / ROLLUP / GROUPING
+        SETS, one Druid query per set as the reference plans them) executes as ONE scan on the
+        engine; each branch then finds its result already computed."""
+        dqs = []
+        for c in p.children:
+            node = c.child if isinstance(c, P.Project) else c
+            if not isinstance(node, P.DruidQuery) or not isinstance(node.spec, S.GroupByQuerySpec) or \
+                    node.info.get("historical") or S.find_deferred(node.spec):
+                return
+            dqs.append(node)
+        if len({id(d.relation.info.datasource) for d in dqs}) != 1 or \
+                any(share_key(d) in self._druid_results for d in dqs):
+            return
+        res = self.session.run_druid_sets(dqs)
+        if res is not None:
+            for d, r in zip(dqs, res):
+                self._druid_results[share_key(d)] = r
 
     def preload(self, p: P.DruidQuery, res) -> None:
         """Use ``res`` as the result of pushed query ``p`` (a streamed Select page)."""
