@@ -55,3 +55,28 @@ def test_not_fusable_falls_back(ds_small, df_small):
     b = a.copy(filter=S.SelectorFilterSpec("l_linestatus", "F"))
     assert not fusable_sets([a, b])
     assert Engine(use_native=False).execute_sets([a, b], ds_small) is None
+
+
+@pytest.mark.gpu
+def test_gpu_fused_sets_equal_per_set_queries():
+    """Fine scan + device re-aggregation on the HIP path (dense LDS table -> compacted partials)."""
+    from spark_druid_olap_amd.engine.columns import materialize
+
+    flat = tpch.generate_flat(0.05, "cuda")
+    ds = tpch.to_datasource(flat, profile="bench")
+    df = tpch.to_pandas(flat)
+    for q in QUERIES:
+        a = _session_native(ds, df, True).sql(q).collect()
+        b = _session_native(ds, df, False).sql(q).collect()
+        assert _norm(a) == _norm(b), q
+    del materialize
+
+
+def _session_native(ds, df, fuse):
+    s = Session(engine=Engine(use_native=True),
+                conf={"spark.sparklinedata.druid.fuse.groupingsets": str(fuse).lower(),
+                      "spark.sparklinedata.druid.approxCountDistinct": "true"})
+    s.register_datasource(ds)
+    s.register_table("orderLineItemPartSupplierBase", df, schema=tpch.FLAT_SCHEMA)
+    s.sql(tpch.druid_ddl(with_column_mapping=False))
+    return s
