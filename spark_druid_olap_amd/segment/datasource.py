@@ -261,6 +261,26 @@ class DataSource:
         with open(os.path.join(path, "manifest.json"), "w") as f:
             json.dump(man, f)
 
+    def to(self, device) -> "DataSource":
+        """A copy of this shard on ``device`` (host <-> HBM), indexes and sketches included."""
+        dev = torch.device(device)
+        mv = lambda t: None if t is None else t.to(dev)  # noqa: E731
+        dims = {k: DimColumn(k, d.dictionary, mv(d.ids), mv(d.bitmap), mv(d.zmin), mv(d.zmax), d.spatial)
+                for k, d in self.dims.items()}
+        mets = {}
+        for k, m in self.metrics.items():
+            sk = m.sketch
+            if sk is not None:
+                sk = SketchColumn(k, sk.kind, mv(sk.offsets), mv(sk.values), sk.p, sk.salt, sk.size)
+            mets[k] = MetricColumn(k, m.kind, mv(m.data), m.scale, sk)
+        ds = DataSource(self.name, self.num_rows, mv(self.time), self.time_unit_ms, dims, mets,
+                        self.segment_granularity, self.query_granularity, self.partition, self.num_partitions,
+                        time_host=self.time_host)
+        for a in ("global_num_rows", "shard_key", "spatial", "rollup", "global_interval_ms"):
+            if hasattr(self, a):
+                setattr(ds, a, getattr(self, a))
+        return ds
+
     @staticmethod
     def concat(shards: Sequence["DataSource"]) -> "DataSource":
         return concat_shards(shards)
