@@ -116,6 +116,14 @@ def segment_metadata(ds) -> List[Dict[str, Any]]:
              "size": int(ds.size_bytes()), "numRows": int(getattr(ds, "global_num_rows", ds.num_rows))}]
 
 
+class JSONStream(list):
+    """Marker type: a large result array sent with chunked transfer encoding, rows serialized a
+    block at a time (the client can start parsing before the last row is encoded)."""
+
+
+STREAM_ROWS = 4096  # results with more rows than this are streamed
+
+
 class PlainText(str):
     """Marker type: sent as text/plain (Prometheus exposition format)."""
 
@@ -170,6 +178,8 @@ class DruidHTTPServer:
                                             res.num_rows, "http", None)
             out = format_result(spec, res)
             ok = True
+            if isinstance(out, list) and len(out) > STREAM_ROWS:
+                return JSONStream(out)
             return out
         finally:
             self.running.pop(qid, None)
@@ -295,6 +305,25 @@ class DruidHTTPServer:
                 self._send(code, obj)
 
             def _send(self, code, obj):
+                if isinstance(obj, JSONStream) and not getattr(self, "_smile", False):
+                    self.send_response(code)
+                    self.send_header("Content-Type", "application/json")
+                    self.send_header("Transfer-Encoding", "chunked")
+                    self.end_headers()
+
+                    def chunk(b: bytes):
+                        self.wfile.write(b"%x\r\n" % len(b) + b + b"\r\n")
+
+                    try:
+                        chunk(b"[")
+                        for i in range(0, len(obj), 1024):
+                            part = ",".join(json.dumps(r, default=_py) for r in obj[i:i + 1024])
+                            chunk(((b"," if i else b"") + part.encode()))
+                        chunk(b"]")
+                        self.wfile.write(b"0\r\n\r\n")
+                    except (BrokenPipeError, ConnectionResetError):
+                        self.close_connection = True  # the client stopped reading (closed its iterator)
+                    return
                 if isinstance(obj, HTMLPage):
                     data, ct = obj.encode("utf-8"), "text/html; charset=utf-8"
                 elif isinstance(obj, PlainText):

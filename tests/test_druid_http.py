@@ -125,3 +125,25 @@ def test_delete_cancels_a_running_query(srv, monkeypatch):
     th.join(60)
     assert "err" in out and "cancel" in out["err"].lower(), out
     assert out["s"] < 10  # far less than scanning every monthly segment batch at 0.3 s each
+
+
+def test_streamed_results_iterator(srv, ds_small):
+    """A large groupBy (every order) is sent chunked and parsed row by row by the client's
+    ResultIterator -- the same rows as the buffered call; closing early drops the connection."""
+    c = DruidQueryServerClient("127.0.0.1", srv.port)
+    q = {"queryType": "groupBy", "dataSource": "tpch", "granularity": "all", "intervals": ["1992-01-01/1999-01-01"],
+         "dimensions": ["o_orderkey"], "aggregations": [{"type": "longSum", "name": "q", "fieldName": "l_quantity"}]}
+    full = c.execute_query(q)
+    assert len(full) > 4096  # above the server's streaming threshold
+    with c.execute_query_iter(q, chunk_bytes=4096) as it:
+        rows = list(it)
+    assert rows == full and it.rows == len(full)
+    it2 = c.execute_query_iter(q, chunk_bytes=1024)
+    first = [next(it2) for _ in range(10)]
+    it2.close()
+    assert first == full[:10]
+    # the cancel hook reaches the server (DELETE /druid/v2/{queryId})
+    it3 = c.execute_query_iter({**q, "context": {"queryId": "stream-cancel-1"}})
+    next(it3)
+    it3.cancel()
+    assert it3.query_id == "stream-cancel-1"
