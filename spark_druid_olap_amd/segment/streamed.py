@@ -79,7 +79,7 @@ class HostShard:
         return getattr(self.ds, item)
 
     # ------------------------------------------------------------------ windows
-    def window(self, j: int, dims: Set[str], metrics: Set[str], bitmaps: Set[str]) -> _WindowDataSource:
+    def window(self, j: int, dims: Set[str], metrics: Set[str], bitmaps: Dict[str, Set[int]]) -> _WindowDataSource:
         """Device view of window ``j`` holding only the listed columns (the rest are empty
         placeholders: any access would fail loudly).  Copies are issued on the copy stream; the
         caller orders the compute stream after ``ready``."""
@@ -107,10 +107,14 @@ class HostShard:
                 ids = rows(d.ids) if k in dims else torch.empty(0, dtype=d.ids.dtype, device=dev)
                 bm = None
                 if d.bitmap is not None and k in bitmaps:
+                    # only the value planes the query's bitmap leaves read, each a contiguous copy
+                    # (a whole [card, words] window of a 150-value dimension is ~19 B/row)
                     bm = torch.zeros((d.bitmap.shape[0], nw), dtype=torch.int64, device=dev)
                     m = min(nw, d.bitmap.shape[1] - w0)
-                    bm[:, :m].copy_(d.bitmap[:, w0: w0 + m], non_blocking=True)
-                    self.bytes_copied += bm.numel() * 8
+                    for v in sorted(bitmaps[k]):
+                        bm[v, :m].copy_(d.bitmap[v, w0: w0 + m], non_blocking=True)
+                    self.bytes_copied += len(bitmaps[k]) * m * 8
+                    bm.staged_values = frozenset(bitmaps[k])
                 zmin = zmax = None
                 if k in self._zones:
                     zm, zx = self._zones[k]
@@ -180,13 +184,14 @@ def _columns_of(prog) -> Tuple[Set[str], Set[str], Set[str]]:
         walk(d.get("filter"))
     dims |= {c for c in named if c in ds.dims}
     mets |= {c for c in named if c in ds.metrics}
-    bitmaps = set()
-    for row, _, _ in prog.bm_leaves:  # a leaf addresses planes of one dimension's bitmap index
+    bitmaps: Dict[str, Set[int]] = {}
+    for row, _, count in prog.bm_leaves:  # a leaf addresses `count` value planes of one bitmap index
         p = row.data_ptr()
         for k, d in ds.dims.items():
             b = d.bitmap
             if b is not None and b.data_ptr() <= p < b.data_ptr() + b.numel() * 8:
-                bitmaps.add(k)
+                v0 = (p - b.data_ptr()) // (b.shape[1] * 8)
+                bitmaps.setdefault(k, set()).update(range(v0, v0 + count))
     return dims, mets, bitmaps
 
 
@@ -269,9 +274,16 @@ def _check_resident(prog, w) -> None:
     for c in prog.cols:
         if column_tensor(w, c).numel() < w.padded_rows:
             raise RuntimeError(f"streamed window lowered to read column {c!r} that was not staged")
-    for row, _, _ in prog.bm_leaves:
+    for row, _, count in prog.bm_leaves:
         if row.numel() == 0 or row.device != w.device:
             raise RuntimeError("streamed window lowered to read a bitmap that was not staged")
+        for d in w.dims.values():
+            b = d.bitmap
+            if b is not None and b.data_ptr() <= row.data_ptr() < b.data_ptr() + b.numel() * 8:
+                v0 = (row.data_ptr() - b.data_ptr()) // (b.shape[1] * 8)
+                staged = getattr(b, "staged_values", frozenset())
+                if any(v not in staged for v in range(v0, v0 + count)):
+                    raise RuntimeError(f"streamed window reads bitmap planes of {d.name!r} that were not staged")
 
 
 def _own(part):
