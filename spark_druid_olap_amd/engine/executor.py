@@ -908,7 +908,8 @@ class Engine:
             self._coalescer = Coalescer(StreamScheduler(n, self.world.device()))
         return self._coalescer
 
-    def prepare(self, qs: S.QuerySpec, ds: DataSource, segments_per_query: Optional[int] = None) -> PreparedQuery:
+    def prepare(self, qs: S.QuerySpec, ds: DataSource, segments_per_query: Optional[int] = None,
+                key_passes: bool = True) -> PreparedQuery:
         """``segments_per_query`` set = historical execution (``sd/DruidRDD.scala:62-84, 244-277``):
         the query runs as one partial per batch of that many segments and the partials are merged
         by the engine (the reference's Spark-side PostAggregate, ``asd/PostAggregate.scala``);
@@ -923,7 +924,17 @@ class Engine:
             from ..segment.streamed import StreamedQuery
 
             return StreamedQuery(self, qs, ds)
-        return PreparedQuery(self, qs, ds, segments_per_query)
+        pq = PreparedQuery(self, qs, ds, segments_per_query)
+        if key_passes and qs.queryType == "groupBy" and not self.world.distributed and not segments_per_query \
+                and len(pq.scans) == 1 and pq.window is None:
+            from ..planner.cost import plan_key_passes
+
+            passes = plan_key_passes(pq.scans[0][2])
+            forced = int(os.environ.get("SDO_FORCE_KEY_PASSES", "0")) > 1
+            key = _pass_key(pq.scans[0][1], 2 if forced else 1 << 20) if passes > 1 else None
+            if key is not None:
+                return KeyRangePasses(self, qs, ds, key, passes)
+        return pq
 
     def execute_sets(self, specs, ds: DataSource, out_types=None) -> Optional[List[QueryResult]]:
         """Grouping-set queries from one scan (``execute_grouping_sets``); None if not fusable."""
@@ -1077,3 +1088,69 @@ def execute_grouping_sets(engine, specs, ds, out_types=None) -> Optional[List[Qu
         res.stats.update(fused_sets=len(specs), exec_ms=(time.perf_counter() - t0) * 1e3)
         out.append(res)
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# Key-range passes: dense group tables far larger than the Infinity Cache
+class KeyRangePasses:
+    """A groupBy whose dense HBM table is far larger than the 256 MB Infinity Cache (TPC-H Q18:
+    150M orders) runs as P scans, each restricted to 1/P of the largest key's dictionary ids
+    (``IdRangeFilterSpec``); the filter-implied key compaction of the lowering (engine/lower.py
+    compact_key) gives every pass a cache-resident table.  Group keys are disjoint across passes,
+    so HAVING applies per pass and the results concatenate; ORDER BY ... LIMIT k keeps each pass's
+    top k (a superset) and re-orders the union.  Planned by planner/cost.py plan_key_passes."""
+
+    def __init__(self, engine, qs, ds, key, passes: int):
+        self.engine, self.qs, self.ds = engine, qs, ds
+        self.key = key
+        card = max(1, int(key.card))
+        step = -(-card // passes)
+        self.ranges = [(lo, min(card, lo + step)) for lo in range(0, card, step)]
+        self.subs = []
+        for lo, hi in self.ranges:
+            f = S.IdRangeFilterSpec(key.col, lo, hi)
+            filt = f if qs.filter is None else S.LogicalFilterSpec("and", [qs.filter, f])
+            self.subs.append(PreparedQuery(engine, qs.copy(filter=filt), ds))
+        self.deterministic = bool(self.subs[0].deterministic) if self.subs else False
+        self.scans = self.subs[0].scans if self.subs else []
+
+    @property
+    def out_types(self):
+        return getattr(self.subs[0], "out_types", None)
+
+    @out_types.setter
+    def out_types(self, v):
+        for p in self.subs:
+            p.out_types = v
+
+    def run(self) -> QueryResult:
+        t0 = time.perf_counter()
+        res = [p.run() for p in self.subs]
+        cols = list(res[0].columns)
+        data: Dict[str, Any] = {}
+        for c in cols:
+            parts = [r.data[c] for r in res]
+            if isinstance(parts[0], DictColumn):
+                data[c] = DictColumn(np.concatenate([np.asarray(x.codes, dtype=np.int64) for x in parts]),
+                                     parts[0].dictionary)
+            else:
+                data[c] = np.concatenate([np.asarray(x) for x in parts])
+        n = len(data[cols[0]]) if cols else 0
+        ls = getattr(self.qs, "limitSpec", None)
+        if ls is not None and n:
+            idx = order_and_limit(data, np.arange(n), ls.columns, ls.limit)
+            data = {c: take(v, idx) for c, v in data.items()}
+        out = QueryResult(cols, data, res[0].query_type, {"groups": sum(r.stats.get("groups", 0) for r in res)})
+        out.stats.update(passes=len(self.subs), exec_ms=(time.perf_counter() - t0) * 1e3)
+        self.last_stats = out.stats
+        return out
+
+
+def _pass_key(prog, min_card: int = 1 << 20):
+    """The key to split on: the widest plain dictionary-id key (not already compacted)."""
+    best = None
+    for kc in prog.keys:
+        if kc.kind == D.K_ID and kc.orig is None and kc.base == 0 and kc.card >= min_card and \
+                (best is None or kc.card > best.card):
+            best = kc
+    return best

@@ -393,6 +393,10 @@ class Lowerer:
         if dim not in ds.dims:
             raise LoweringError(f"filter on unknown dimension {dim!r}")
         d = ds.dims[dim].dictionary
+        if isinstance(f, S.IdRangeFilterSpec):
+            mask = np.zeros(len(d), dtype=bool)
+            mask[max(0, int(f.lo)): min(len(d), int(f.hi))] = True
+            return ("ids", dim, mask)
         if isinstance(f, S.SelectorFilterSpec):
             v = f.value
             mask = np.zeros(len(d), dtype=bool)
@@ -1618,6 +1622,16 @@ def compact_key(kc: KeyComp, mask: np.ndarray) -> KeyComp:
     ids = np.flatnonzero(mask)
     if len(ids) == 0:
         ids = np.array([0])
+    a, n = int(ids[0]), len(ids)
+    if kc.kind == D.K_ID and kc.base == 0 and int(ids[-1]) - a + 1 == n and n > 1:
+        # a contiguous id run (a value range, a key-range pass): a key window [a, a+n) -- the
+        # kernel subtracts the base, no remap table to upload or gather through
+        dec = kc.decoder
+        ids_t = ids.astype(np.int64)
+        out = KeyComp(kc.name, D.K_ID, kc.col, n, base=a, orig=ids_t,
+                      decoder=(lambda c: dec(np.asarray(c, dtype=np.int64) + a)) if dec else (lambda c: np.asarray(c) + a))
+        out.dictionary = getattr(kc, "dictionary", None)
+        return out
     remap = np.zeros(len(mask), dtype=np.int32)
     remap[ids] = np.arange(len(ids), dtype=np.int32)
     dec = kc.decoder

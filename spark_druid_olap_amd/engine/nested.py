@@ -204,7 +204,7 @@ class NestedPreparedQuery:
             ictx = getattr(inner_q, "context", None)
             inner_q = inner_q.copy(context=ictx.copy(deterministic=True) if ictx is not None
                                    else S.QuerySpecContext(deterministic=True))
-        self.inner = engine.prepare(inner_q, ds, segments_per_query)
+        self.inner = engine.prepare(inner_q, ds, segments_per_query, key_passes=False)
         for d in qs.dimensions:
             if not isinstance(d, S.DefaultDimensionSpec):
                 raise LoweringError("nested groupBy dimensions must be default dimension specs")

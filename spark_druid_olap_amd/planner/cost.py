@@ -320,6 +320,33 @@ class MergePlan:
         return f"{self.kind} {alts}"
 
 
+MALL_BYTES = 256 << 20  # MI355X Infinity Cache (last level, shared by the XCDs)
+PASS_TABLE_BYTES = int(os.environ.get("SDO_PASS_TABLE_BYTES", 96 << 20))
+KEY_PASSES = os.environ.get("SDO_KEY_PASSES", "1") != "0"
+
+
+def plan_key_passes(prep) -> int:
+    """Key-range passes for a dense HBM group table far larger than the Infinity Cache (TPC-H Q18:
+    150M orders x 8 B = 1.2 GB): every row is an HBM read-modify-write atomic on a random line of the
+    table, so split the key space into P ranges whose tables (<= PASS_TABLE_BYTES) stay
+    cache-resident.  Each pass re-reads only the key and payload columns (a few bytes per row at
+    streaming bandwidth) and its atomics hit the 256 MB Infinity Cache.  Returns P (1 = no split)."""
+    from ..ops import desc as D
+
+    forced = int(os.environ.get("SDO_FORCE_KEY_PASSES", "0"))  # tests: split any groupBy
+    if forced > 1:
+        return forced
+    if not KEY_PASSES or prep is None or getattr(prep, "mode", None) != D.M_DENSE_GLOBAL:
+        return 1
+    if getattr(prep, "pres_bytes", False) or getattr(prep, "touch", False):
+        return 1
+    prog = prep.prog
+    table = prog.G * max(1, prog.nslots) * 8
+    if table <= 2 * MALL_BYTES or prog.nhll or prog.thetas or getattr(prog, "stored_hll", None):
+        return 1
+    return int(math.ceil(table / PASS_TABLE_BYTES))
+
+
 def plan_merge(dense: bool, state_bytes: int, world_size: int, disjoint: bool = False) -> MergePlan:
     """Cross-GPU merge of one query's partials.  Inputs must be identical on every rank (layout
     sizes, never local row counts) so every rank takes the same collective path.

@@ -245,6 +245,18 @@ class SelectorFilterSpec(Spec, _Decodable):
     type: str = "selector"
 
 
+@_register("filter", "idRange")
+@dataclass
+class IdRangeFilterSpec(Spec, _Decodable):
+    """Engine extension: rows whose dimension dictionary id lies in [lo, hi) (dictionaries are
+    sorted, so this is a value range).  Emitted by the engine itself for key-range passes
+    (engine/executor.py KeyRangePasses), never by the SQL planner."""
+    dimension: str
+    lo: int
+    hi: int
+    type: str = "idRange"
+
+
 @_register("filter", "regex")
 @dataclass
 class RegexFilterSpec(Spec, _Decodable):
