@@ -338,9 +338,11 @@ def plan_key_passes(prep) -> int:
         return forced
     if not KEY_PASSES or prep is None or getattr(prep, "mode", None) != D.M_DENSE_GLOBAL:
         return 1
-    if getattr(prep, "pres_bytes", False) or getattr(prep, "touch", False):
+    if getattr(prep, "pres_bytes", False):
         return 1
     prog = prep.prog
+    if prog.est_rows < prog.G / 4:
+        return 1  # few groups touched (first-touch table, TPC-H Q3): the atomics are sparse anyway
     table = prog.G * max(1, prog.nslots) * 8
     if table <= 2 * MALL_BYTES or prog.nhll or prog.thetas or getattr(prog, "stored_hll", None):
         return 1
