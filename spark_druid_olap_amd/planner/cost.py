@@ -322,7 +322,11 @@ class MergePlan:
 
 MALL_BYTES = 256 << 20  # MI355X Infinity Cache (last level, shared by the XCDs)
 PASS_TABLE_BYTES = int(os.environ.get("SDO_PASS_TABLE_BYTES", 96 << 20))
-KEY_PASSES = os.environ.get("SDO_KEY_PASSES", "1") != "0"
+# Measured on MI355X (tools/sql_probe.py, TPC-H Q18 at SF100): 12 cache-sized passes run 2.9 ms of
+# scan each -- the random-atomic rate into a 100 MB Infinity-Cache-resident table (~17 G/s) is no
+# better than into the 1.2 GB HBM table (~16 G/s), and every pass repeats compaction / HAVING /
+# key decoding: 130 ms vs 41 ms single-pass.  Kept as an opt-in plan (SDO_KEY_PASSES=1).
+KEY_PASSES = os.environ.get("SDO_KEY_PASSES", "0") != "0"
 
 
 def plan_key_passes(prep) -> int:
