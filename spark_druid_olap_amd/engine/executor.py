@@ -194,8 +194,11 @@ class PreparedQuery:
             slot = keys
         else:  # group key -> row of the sparse partials
             order = torch.argsort(part.keys)
-            pos = torch.searchsorted(part.keys[order], keys).clamp_(max=max(0, part.rows - 1))
+            sk = part.keys[order]
+            pos = torch.searchsorted(sk, keys).clamp_(max=max(0, part.rows - 1))
             slot = order[pos] if part.rows else torch.full_like(keys, -1)
+            if part.rows and keys.numel() and not bool((sk[pos] == keys).all()):
+                raise RuntimeError("stored-sketch rows map to groups missing from the scan's partials")
         hll = list(part.hll)
         for name, metric, filt in prog.stored_hll:
             sk = self.ds.metrics[metric].sketch
