@@ -892,6 +892,10 @@ def _numeric_key_join(lks, rks, lok: np.ndarray, rok: np.ndarray):
         arrs.append((x, y))
     li_all = np.nonzero(lok)[0]
     ri_all = np.nonzero(rok)[0]
+    if len(li_all) + len(ri_all) >= _DEVICE_JOIN_MIN:
+        out = _numeric_key_join_device(arrs, li_all, ri_all)
+        if out is not None:
+            return out
     lc = np.zeros(len(li_all), dtype=np.int64)
     rc = np.zeros(len(ri_all), dtype=np.int64)
     span = 1
@@ -916,6 +920,45 @@ def _numeric_key_join(lks, rks, lok: np.ndarray, rok: np.ndarray):
     start = np.repeat(lo - (np.cumsum(cnt) - cnt), cnt)
     ri = ri_all[order[start + np.arange(tot)]]
     return li, ri
+
+
+_DEVICE_JOIN_MIN = 1 << 16
+
+
+def _numeric_key_join_device(arrs, li_all: np.ndarray, ri_all: np.ndarray):
+    """The same join on the GPU (torch radix sorts instead of numpy's single-threaded ones: TPC-H
+    Q2 / Q17 join ~0.5M aggregated rows, 15 ms on the host).  None without a GPU."""
+    import torch
+
+    if not torch.cuda.is_available():
+        return None
+    dev = torch.device("cuda", torch.cuda.current_device())
+    nl = len(li_all)
+    lc = torch.zeros(nl, dtype=torch.int64, device=dev)
+    rc = torch.zeros(len(ri_all), dtype=torch.int64, device=dev)
+    span = 1
+    for a, b in arrs:
+        x, y = a[li_all], b[ri_all]
+        if x.dtype.kind == "f" or y.dtype.kind == "f":
+            t = torch.from_numpy(np.concatenate([x.astype(np.float64), y.astype(np.float64)])).to(dev)
+        else:
+            t = torch.from_numpy(np.concatenate([x.astype(np.int64), y.astype(np.int64)])).to(dev)
+        u, inv = torch.unique(t, return_inverse=True)
+        if span * max(1, int(u.numel())) >= 2 ** 62:
+            return None
+        lc += inv[:nl] * span
+        rc += inv[nl:] * span
+        span *= max(1, int(u.numel()))
+    rs, order = torch.sort(rc, stable=True)
+    lo = torch.searchsorted(rs, lc, right=False)
+    cnt = torch.searchsorted(rs, lc, right=True) - lo
+    tot = int(cnt.sum())
+    li_t = torch.from_numpy(li_all).to(dev)
+    ri_t = torch.from_numpy(ri_all).to(dev)
+    li = torch.repeat_interleave(li_t, cnt)
+    start = torch.repeat_interleave(lo - (torch.cumsum(cnt, 0) - cnt), cnt)
+    ri = ri_t[order[start + torch.arange(tot, device=dev)]]
+    return li.cpu().numpy(), ri.cpu().numpy()
 
 
 def _pair_batch(lb: Batch, rb: Batch, li, ri) -> Batch:
