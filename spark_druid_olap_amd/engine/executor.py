@@ -28,6 +28,9 @@ from .columns import DictColumn, materialize, take
 from .lower import Lowerer, LoweringError, ScanProgram
 from .partials import Partials, finalize
 
+# segment-batched execution overlaps batch j's merge collectives with batch j+1's scan
+PIPELINE_MERGE = os.environ.get("SDO_PIPELINE_MERGE", "1") not in ("0", "")
+
 
 @dataclass
 class QueryResult:
@@ -80,6 +83,8 @@ class PreparedQuery:
         self.low = Lowerer(ds, world=engine.world, deterministic=self.deterministic)
         self.scans: List[tuple] = []  # (tag, prog, prepared)
         self.segments_per_query = segments_per_query
+        self._nbatches: Optional[int] = None   # batch count agreed across ranks (pipelined merge)
+        self._pipeline_ok: Optional[bool] = None
         self.window: Optional["ShardWindow"] = None
         qt = qs.queryType
         if qt in ("groupBy", "timeseries", "topN"):
@@ -261,6 +266,12 @@ class PreparedQuery:
         from ..utils.cancel import checkpoint
 
         _, prog, prep = self.scans[0]
+        if self.segments_per_query and self.world.distributed and self.window is None and PIPELINE_MERGE:
+            out = self._run_pipelined(prog)
+            if out is not None:
+                part, t1 = out
+                part, hv = self._device_having(prog, part)
+                return prog, self._device_prune(prog, part, hv), t1
         err = None
         try:
             with T.span("sdo.scan"):
@@ -287,6 +298,58 @@ class PreparedQuery:
         part, hv = self._device_having(prog, part)
         part = self._device_prune(prog, part, hv)
         return prog, part, t1
+
+    def _run_pipelined(self, prog):
+        """Segment-batched execution with each batch's merge overlapping the next batch's scan:
+        batch j's dense partials start their collectives (``parallel/merge.start_dense_merge``:
+        RCCL runs them on the process group's stream) and batch j+1's kernel is launched behind
+        them on the compute stream; the merged batches combine locally at the end.  Ranks agree on
+        the batch count once per prepared query (shards hold different segment counts: a rank with
+        fewer batches contributes identity partials), so every rank issues the same collectives.
+        Returns None -- before any collective -- when the partials are sparse (hash group-by):
+        those merge once after a local combine (``run_partials``)."""
+        from ..parallel.fault import STATUS_FAILED, STATUS_OK, raise_if_failed
+        from ..parallel.merge import start_dense_merge
+        from ..utils.cancel import checkpoint
+
+        if self._nbatches is None:
+            n = torch.tensor([len(self.scans)], dtype=torch.int64, device=self._coll_device())
+            self._nbatches = int(self.world.all_reduce(n, "max").item())
+        if self._nbatches <= 1 or self._pipeline_ok is False:
+            return None
+        # one merge in flight: merge j runs while batch j+1 scans, then merge j completes (RCCL:
+        # the compute stream waits for it -- no host sync until the final status check)
+        done, inflight, err = [], None, None
+        for j in range(self._nbatches):
+            _, p_, q_ = self.scans[min(j, len(self.scans) - 1)]
+            with T.span("sdo.scan"):
+                try:
+                    if j >= len(self.scans) or err is not None:
+                        part = self._placeholder(p_, q_)  # identity (nothing left here) / failed
+                    else:
+                        checkpoint()
+                        part = self._scan(p_, q_)
+                except Exception as e:  # noqa: BLE001  (peers learn about it in the merge)
+                    err, part = e, self._placeholder(p_, q_)
+            if self._pipeline_ok is None:
+                # decided from the layout (identical on every rank), before the first collective
+                self._pipeline_ok = part.kind == "dense"
+                if not self._pipeline_ok:
+                    return None
+            if inflight is not None:
+                done.append(inflight.result())
+            inflight = start_dense_merge(self.world, prog, part, STATUS_FAILED if err else STATUS_OK)
+        t1 = time.perf_counter()
+        with T.span("sdo.merge"):
+            done.append(inflight.result())
+            sts = torch.stack([d[1] for d in done]).amax(dim=0).tolist()
+            if err is not None or any(sts):
+                raise_if_failed(sts, self.world.rank, err)
+            part = combine_local(prog, [d[0] for d in done])
+        return part, t1
+
+    def _coll_device(self):
+        return self.ds.device if self.world.backend == "nccl" else torch.device("cpu")
 
     def _device_having(self, prog: ScanProgram, part: Partials):
         """groupBy havingSpec evaluated over the merged accumulators ON THE DEVICE (TPC-H Q18:

@@ -938,7 +938,10 @@ class Lowerer:
 
     def _data_span(self, ivs: List[Interval]) -> Tuple[int, int]:
         ds = self.ds
-        lo, hi = ds.min_time_ms(), ds.max_time_ms() + ds.time_unit_ms
+        gi = getattr(ds, "global_interval_ms", None)
+        # every rank keys time buckets from the CLUSTER-wide span (Session._global_interval), so
+        # shards covering different periods still produce identically laid-out partials
+        lo, hi = gi if gi is not None else (ds.min_time_ms(), ds.max_time_ms() + ds.time_unit_ms)
         if ivs:
             lo = max(lo, min(iv.lo for iv in ivs))
             hi = min(hi, max(iv.hi for iv in ivs))

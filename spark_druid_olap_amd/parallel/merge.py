@@ -57,6 +57,52 @@ def _merge_dense_bucketed(world: World, prog, part: Partials, status: int,
       INT64_MIN unlike negation), so min and max share one MAX collective.
     A failed rank contributes a layout-compatible placeholder, so every rank issues the same
     collectives in the same order and then raises together (parallel/fault.py)."""
+    merged, sts = start_dense_merge(world, prog, part, status, "bucketed-allreduce").wait()
+    if local_error is not None or any(sts):
+        raise_if_failed(sts, world.rank, local_error)
+    return merged
+
+
+class DenseMerge:
+    """An enqueued dense merge.  ``result()`` -> (merged partials, per-rank status words as a
+    device tensor) without a host synchronisation (RCCL: the current stream waits for the
+    collective); ``wait()`` -> (merged partials, status words as a list)."""
+
+    def __init__(self, finish):
+        self._finish = finish
+
+    def result(self):
+        return self._finish()
+
+    def wait(self):
+        part, sts = self._finish()
+        return part, sts.tolist()
+
+
+def start_dense_merge(world: World, prog, part: Partials, status: int, kind: Optional[str] = None) -> DenseMerge:
+    """Enqueue the collectives of a dense merge (the cost model's one-shot gather or bucketed
+    all-reduce) without waiting: segment-batched execution starts batch j's merge and scans batch
+    j+1 while it runs (``PreparedQuery._run_pipelined``)."""
+    kind = kind or merge_plan_for(world, part).kind
+    if kind == "oneshot-allgather":
+        R, ns = part.acc.shape
+        st = torch.full((1,), status, dtype=torch.int64, device=part.acc.device)
+        pieces = [part.acc.reshape(-1)] + [h.reshape(-1).to(torch.int64) for h in part.hll] + [st]
+        pend = world.all_gather_tensor_async(torch.cat(pieces))  # [ranks, L]
+        shapes = [h.shape for h in part.hll]
+
+        def finish_gather():
+            g = pend.wait()
+            acc = _reduce_stacked(prog, g[:, : R * ns].reshape(world.size, R, ns))
+            off = R * ns
+            hll = []
+            for shp in shapes:
+                n = shp.numel()
+                hll.append(g[:, off: off + n].amax(dim=0).to(torch.int32).reshape(shp))
+                off += n
+            return Partials("dense", acc, None, hll), g[:, -1]
+
+        return DenseMerge(finish_gather)
     acc = part.acc.clone()
     R = acc.shape[0]
     by_op = {op: [s for s, (o, _) in enumerate(prog.slots) if o == op]
@@ -65,29 +111,32 @@ def _merge_dense_bucketed(world: World, prog, part: Partials, status: int,
     st = torch.zeros((world.size,), dtype=torch.int64, device=acc.device)
     st[world.rank] = status
     b_sum = torch.cat([acc[:, si].reshape(-1), st]) if si else st
-    world.all_reduce(b_sum, "sum")
+    p_sum = world.all_reduce_async(b_sum, "sum")
+    p_f = p_max = None
     if sf:
         b_f = acc[:, sf].contiguous().view(torch.float64)
-        world.all_reduce(b_f, "sum")
-        acc[:, sf] = b_f.view(torch.int64)
+        p_f = world.all_reduce_async(b_f, "sum")
     if mn or mx:
         b_max = torch.cat([acc[:, mx].reshape(-1), torch.bitwise_not(acc[:, mn]).reshape(-1)])
-        world.all_reduce(b_max, "max")
-        if mx:
-            acc[:, mx] = b_max[: R * len(mx)].reshape(R, len(mx))
-        if mn:
-            acc[:, mn] = torch.bitwise_not(b_max[R * len(mx):].reshape(R, len(mn)))
-    hll = []
-    for h in part.hll:
-        hh = h.clone()
-        world.all_reduce(hh, "max")
-        hll.append(hh)
-    sts = b_sum[-world.size:].tolist()  # one status word per rank (each rank wrote its own slot)
-    if local_error is not None or any(sts):
-        raise_if_failed(sts, world.rank, local_error)
-    if si:
-        acc[:, si] = b_sum[:-world.size].reshape(R, len(si))
-    return Partials("dense", acc, None, hll)
+        p_max = world.all_reduce_async(b_max, "max")
+    p_hll = [world.all_reduce_async(h.clone(), "max") for h in part.hll]
+
+    def finish_reduce():
+        s = p_sum.wait()
+        if p_f is not None:
+            acc[:, sf] = p_f.wait().view(torch.int64)
+        if p_max is not None:
+            m = p_max.wait()
+            if mx:
+                acc[:, mx] = m[: R * len(mx)].reshape(R, len(mx))
+            if mn:
+                acc[:, mn] = torch.bitwise_not(m[R * len(mx):].reshape(R, len(mn)))
+        hll = [p.wait() for p in p_hll]
+        if si:
+            acc[:, si] = s[:-world.size].reshape(R, len(si))
+        return Partials("dense", acc, None, hll), s[-world.size:]  # one status word per rank
+
+    return DenseMerge(finish_reduce)
 
 
 def merge_partials(world: World, prog, part: Partials, disjoint_keys: bool = False,
@@ -102,23 +151,10 @@ def merge_partials(world: World, prog, part: Partials, disjoint_keys: bool = Fal
     status = STATUS_FAILED if local_error is not None else STATUS_OK
     plan = merge_plan_for(world, part, disjoint_keys)
     if plan.kind == "oneshot-allgather":
-        R, ns = part.acc.shape
-        st = torch.full((1,), status, dtype=torch.int64, device=part.acc.device)
-        pieces = [part.acc.reshape(-1)] + [h.reshape(-1).to(torch.int64) for h in part.hll] + [st]
-        buf = torch.cat(pieces)
-        g = world.all_gather_tensor(buf)  # [ranks, L]
-        sts = g[:, -1]
-        if local_error is not None or bool((sts != 0).any()):
-            raise_if_failed(sts.tolist(), world.rank, local_error)
-        acc_all = g[:, : R * ns].reshape(world.size, R, ns)
-        acc = _reduce_stacked(prog, acc_all)
-        off = R * ns
-        hll = []
-        for h in part.hll:
-            n = h.numel()
-            hll.append(g[:, off: off + n].amax(dim=0).to(torch.int32).reshape(h.shape))
-            off += n
-        return Partials("dense", acc, None, hll)
+        merged, sts = start_dense_merge(world, prog, part, status, plan.kind).wait()
+        if local_error is not None or any(sts):
+            raise_if_failed(sts, world.rank, local_error)
+        return merged
     if plan.kind == "bucketed-allreduce":
         return _merge_dense_bucketed(world, prog, part, status, local_error)
     # sparse

@@ -68,13 +68,28 @@ class World:
 
     def all_gather_tensor(self, t: torch.Tensor) -> torch.Tensor:
         """[size, *t.shape] stacked gather (same shape on every rank)."""
+        return self.all_gather_tensor_async(t).wait()
+
+    # Asynchronous forms: the collective is enqueued (RCCL: on the process group's own stream,
+    # ordered after the work already on the current stream; gloo: on its worker thread) and
+    # ``wait()`` returns the result (RCCL: the current stream waits for the collective, no host
+    # sync).  Kernels launched in between -- the next segment batch's scan -- overlap it.
+    def all_reduce_async(self, t: torch.Tensor, op: str = "sum") -> "Pending":
         if not self.distributed:
-            return t.unsqueeze(0)
+            return Pending(None, lambda: t)
+        o = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+        h = self._stage(t)
+        work = dist.all_reduce(h, op=o, group=self.group, async_op=True)
+        return Pending(work, lambda: self._unstage(h, t))
+
+    def all_gather_tensor_async(self, t: torch.Tensor) -> "Pending":
+        if not self.distributed:
+            return Pending(None, lambda: t.unsqueeze(0))
         src = self._stage(t.contiguous().reshape(-1))
         # concatenated layout works on both RCCL and gloo (gloo rejects the stacked form)
         out = torch.empty((self.size * src.numel(),), dtype=t.dtype, device=src.device)
-        dist.all_gather_into_tensor(out, src, group=self.group)
-        return out.to(t.device).view((self.size,) + tuple(t.shape))
+        work = dist.all_gather_into_tensor(out, src, group=self.group, async_op=True)
+        return Pending(work, lambda: out.to(t.device).view((self.size,) + tuple(t.shape)))
 
     def all_to_all_varlen(self, t: torch.Tensor, counts: torch.Tensor, status: Optional[int] = None):
         """Personalized exchange (the reference's hash-partitioned shuffle before the final
@@ -150,6 +165,20 @@ class World:
         t = torch.tensor([x], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return float(t.item())
+
+
+class Pending:
+    """An enqueued collective; ``wait()`` returns its result."""
+    __slots__ = ("work", "_result")
+
+    def __init__(self, work, result):
+        self.work = work
+        self._result = result
+
+    def wait(self):
+        if self.work is not None:
+            self.work.wait()
+        return self._result()
 
 
 _WORLD: Optional[World] = None
