@@ -387,8 +387,11 @@ class NestedPreparedQuery:
             else:
                 op = a.type[4:].lower() if a.type.startswith("long") else a.type[6:].lower()
                 spec[a.name] = (a.fieldName, op)
-        g = df.groupby(keys, dropna=False, sort=False).agg(**spec).reset_index() if n else \
-            pd.DataFrame({**{k: [] for k in keys}, **{a.name: [] for a in qs.aggregations}})
+        if n and not keys:  # global aggregate: one row
+            g = pd.DataFrame({name: [df[col].agg(op)] for name, (col, op) in spec.items()})
+        else:
+            g = df.groupby(keys, dropna=False, sort=False).agg(**spec).reset_index() if n else \
+                pd.DataFrame({**{k: [] for k in keys}, **{a.name: [] for a in qs.aggregations}})
         out = {}
         for d in qs.dimensions:
             out[d.outputName] = np.asarray(g[d.dimension].to_numpy(), dtype=object)

@@ -135,7 +135,8 @@ def spatial(q, ctx):
 
 
 def timeseries(q, ctx):
-    if isinstance(q, S.GroupByQuerySpec) and not q.dimensions and q.having is None and q.limitSpec is None:
+    if isinstance(q, S.GroupByQuerySpec) and not q.dimensions and q.having is None and q.limitSpec is None \
+            and not isinstance(q.dataSource, S.QueryDataSourceSpec):  # nested levels stay groupBys
         return S.TimeSeriesQuerySpec(q.dataSource, q.intervals, False, S.Granularity.parse("all"), q.filter,
                                      q.aggregations, q.postAggregations, q.context)
     return q

@@ -1060,12 +1060,15 @@ class DruidRewriter:
             columns.append((aname, rt, "value"))
             ex = r if rt == out_t else A.Cast(r, out_t)
             final[outs[len(agg.groups) + j].rid] = ex
-        if not dims:
-            raise NotPushable("global aggregate over a groupBy")
         outer = S.GroupByQuerySpec(S.QueryDataSourceSpec(q), dims, None, None, S.Granularity.parse("all"), None,
                                    aggs, None, q.intervals)
-        nq = P.DruidQuery(dq.relation, outer, columns, drefs, {"groupby": True, "nested": True,
-                                                              "historical": dq.info.get("historical")})
+        info = {"groupby": True, "nested": True, "historical": dq.info.get("historical")}
+        if not dims:
+            # global aggregate over a groupBy (TPC-H Q15's max(total_revenue) over 1M supplier
+            # groups): one device reduction instead of shipping every group to the host; SQL's
+            # one-row answer over an empty input is filled in by the executor (count 0, else NULL)
+            info["global_counts"] = [a.name for a in aggs if getattr(a, "type", "") == "count"]
+        nq = P.DruidQuery(dq.relation, outer, columns, drefs, info)
         exprs = [A.Alias(final[r.rid], r.name, r.rid) for r in outs if r.rid in final]
         return P.Project(exprs, nq)
 

@@ -275,6 +275,16 @@ class Executor:
             res = self._druid_results[key] = self.session.run_druid(p)
         cols = {}
         n = res.num_rows
+        gc = p.info.get("global_counts")
+        if gc is not None and n == 0:
+            # a global aggregate answers one row over an empty input: count 0, everything else NULL
+            n = 1
+            for r, (name, sqlt, kind) in zip(p.refs, p.columns):
+                v = np.zeros(1, dtype=np.int64) if name in gc else (
+                    np.full(1, np.nan) if base(sqlt) in ("double", "float", "decimal") else np.array([None], dtype=object))
+                cols[r.rid] = druid_value_series(v, sqlt, kind, 1)
+            self.druid_stats.append({"spec": p.spec, "ms": (time.perf_counter() - t0) * 1e3, "rows": 1})
+            return Batch(p.refs, cols, 1)
         for r, (name, sqlt, kind) in zip(p.refs, p.columns):
             cols[r.rid] = druid_value_series(res.data[name], sqlt, kind, n)
         self.druid_stats.append({"spec": p.spec, "ms": (time.perf_counter() - t0) * 1e3, "rows": n})

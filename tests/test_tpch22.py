@@ -197,3 +197,34 @@ def test_in_subquery_pushed_as_semi_join(sess, q):
     assert len(d.druid_queries()) == 2, d.explain()
     assert '"deferred"' in d.druid_queries()[0].spec.to_json_str(None)
     assert _rows(d) == _rows(sess.sql(q.replace(T, B)))
+
+
+GLOBAL_OVER_GROUPBY = [
+    # TPC-H Q15's scalar subquery shape: one device reduction over the inner groups
+    f"select max(s), min(s), sum(s), count(*) from (select l_suppkey, s_name, sum(l_extendedprice) s from {T} "
+    f"where l_shipdate >= '1996-01-01' and l_shipdate < '1996-04-01' group by l_suppkey, s_name) t",
+    f"select count(*), max(n) from (select o_orderkey, count(*) n from {T} group by o_orderkey) t",
+    # empty inner result: SQL still answers one row (count 0, the rest NULL)
+    f"select count(*), max(s), sum(q) from (select s_nation, sum(l_extendedprice) s, sum(l_quantity) q from {T} "
+    f"where s_nation = 'NO SUCH NATION' group by s_nation) t",
+]
+
+
+@pytest.mark.parametrize("i", range(len(GLOBAL_OVER_GROUPBY)))
+def test_global_aggregate_over_groupby_is_nested(sess, i):
+    q = GLOBAL_OVER_GROUPBY[i]
+    d = sess.sql(q)
+    dqs = d.druid_queries()
+    assert len(dqs) == 1 and dqs[0].info.get("nested") and "global_counts" in dqs[0].info, d.explain()
+    got, exp = _rows(d), _rows(sess.sql(q.replace(T, B)))
+    assert len(got) == len(exp) == 1
+    for a, c in zip(got[0], exp[0]):
+        if isinstance(a, float) or isinstance(c, float):
+            assert a == pytest.approx(c, rel=1e-9, abs=0.02), (got, exp)
+        else:
+            assert a == c, (got, exp)
+
+
+def test_q15_subquery_runs_nested(sess):
+    d = sess.sql(dict(tpch22.QUERIES)["Q15"])
+    assert any(q.info.get("nested") and "global_counts" in q.info for q in d.druid_queries())
