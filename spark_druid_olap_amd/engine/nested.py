@@ -160,9 +160,19 @@ def _nonzero(t: torch.Tensor) -> torch.Tensor:
     return torch.nonzero(t).flatten()
 
 
-def _group_sum(R: int, inv: torch.Tensor, src: torch.Tensor, deterministic: bool) -> torch.Tensor:
-    """Per-group sum of ``src`` rows (group ``inv``).  Deterministic float sums go through the same
-    64.32 fixed point as the scan (engine/lower.py fixed_sum): integer index_add is order-free."""
+def _group_sum(R: int, inv: Optional[torch.Tensor], src: torch.Tensor, deterministic: bool) -> torch.Tensor:
+    """Per-group sum of ``src`` rows (group ``inv``; None = one global group, reduced with a tree
+    reduction instead of a million atomics on one address).  Deterministic float sums go through
+    the same 64.32 fixed point as the scan (engine/lower.py fixed_sum): integer sums are
+    order-free."""
+    if inv is None:
+        if not deterministic or src.dtype != torch.float64:
+            return src.sum().reshape(1).to(src.dtype)
+        from .lower import FIX_ONE, fixed_value
+
+        fl = torch.floor(src)
+        return fixed_value(fl.to(torch.int64).sum().reshape(1),
+                           torch.round((src - fl) * FIX_ONE).to(torch.int64).sum().reshape(1))
     if not deterministic or src.dtype != torch.float64:
         return torch.zeros(R, dtype=src.dtype, device=src.device).index_add_(0, inv, src)
     from .lower import FIX_ONE, fixed_value
@@ -294,7 +304,8 @@ class NestedPreparedQuery:
                 slots = uk
                 firsts = None
         else:
-            inv = torch.zeros(n, dtype=torch.int64, device=dev)
+            # global aggregate (no outer keys): whole-column reductions, no scatter
+            inv = None
             R = 1
             firsts = torch.zeros(1, dtype=torch.int64, device=dev)
         if _TRACE:
@@ -318,6 +329,8 @@ class NestedPreparedQuery:
                     src = src.expand(n).contiguous()
                 if op == "sum":
                     acc = _group_sum(R, inv, src, self.deterministic)
+                elif inv is None:
+                    acc = (src.amin() if op == "min" else src.amax()).reshape(1).to(torch.float64)
                 else:
                     acc = torch.full((R,), float("inf") if op == "min" else float("-inf"), dtype=torch.float64,
                                      device=dev)
@@ -325,8 +338,12 @@ class NestedPreparedQuery:
                 out[a.name] = DeviceColumn(a.name, acc)
                 continue
             if a.type == "count":
-                v = dense_counts if inv is None else \
-                    torch.zeros(R, dtype=torch.int64, device=dev).index_add_(0, inv, torch.ones_like(inv))
+                if dense_counts is not None:
+                    v = dense_counts
+                elif inv is None:
+                    v = torch.full((R,), n, dtype=torch.int64, device=dev)
+                else:
+                    v = torch.zeros(R, dtype=torch.int64, device=dev).index_add_(0, inv, torch.ones_like(inv))
                 out[a.name] = DeviceColumn(a.name, v)
                 continue
             c = cols.get(a.fieldName)
@@ -337,6 +354,8 @@ class NestedPreparedQuery:
             src = c.t if exact else (c.t.to(torch.float64) if c.decode is not None else c.as_float())
             if op == "sum":
                 acc = _group_sum(R, inv, src, self.deterministic)
+            elif inv is None:
+                acc = (src.amin() if op == "min" else src.amax()).reshape(1)
             else:
                 if src.dtype == torch.int64:
                     init = torch.iinfo(torch.int64).max if op == "min" else torch.iinfo(torch.int64).min
