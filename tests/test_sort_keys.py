@@ -44,3 +44,43 @@ def test_categorical_sort_matches_object_sort(has_null, asc, nulls_first):
     if has_null:
         k = sum(v is None for v in lead)
         assert all(v is None for v in (lead[:k] if nf else lead[-k:]))
+
+
+def _oracle(cols, n):
+    """Reference stable multi-key sort: one stable pass per key, last key first."""
+    idx = np.arange(n)
+    for s, asc, nf in reversed(cols):
+        v = s.iloc[idx].reset_index(drop=True)
+        na = v.isna().to_numpy()
+        nf = asc if nf is None else nf
+        ok = np.nonzero(~na)[0]
+        vals = v.iloc[ok].to_numpy(dtype=object)
+        o = sorted(range(len(ok)), key=lambda i: vals[i], reverse=False)
+        if not asc:  # stable descending: sort by negated rank, keeping ties in order
+            o = sorted(range(len(ok)), key=lambda i: vals[i], reverse=True)
+            # python's reverse sort keeps stability
+        ok = ok[np.asarray(o, dtype=np.int64)] if len(ok) else ok
+        nas = np.nonzero(na)[0]
+        idx = idx[np.concatenate([nas, ok]) if nf else np.concatenate([ok, nas])]
+    return idx
+
+
+@pytest.mark.parametrize("limit", [None, 5, 40])
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_multikey_sort_and_topk_match_stable_oracle(limit, seed):
+    rng = np.random.default_rng(seed)
+    n = 300
+    ints = pd.Series(rng.integers(-3, 4, n))
+    flt = pd.Series(rng.integers(0, 6, n).astype(np.float64))
+    flt[rng.integers(0, n, 20)] = np.nan
+    strs = pd.Series(rng.choice(["x", "y", "z", "w"], n), dtype=object)
+    nullable = pd.Series(rng.integers(0, 3, n)).astype("Int64")
+    nullable[rng.integers(0, n, 15)] = pd.NA
+    pools = [ints, flt, strs, nullable]
+    for perm in itertools.permutations(range(4), 3):
+        for dirs in itertools.product([True, False], repeat=3):
+            cols = [(pools[k], d, None) for k, d in zip(perm, dirs)]
+            got = sort_indices(cols, n, limit=limit)
+            exp = _oracle(cols, n)
+            m = n if limit is None else limit
+            assert got[:m].tolist() == exp[:m].tolist(), (perm, dirs, limit)
