@@ -121,3 +121,18 @@ def test_star_schema_validation():
             {"leftTable": "d1", "rightTable": "d2", "relationType": "n-1",
              "joinCondition": [{"leftAttribute": "k1", "rightAttribute": "k2"}]}]}),
             lambda t: {"f": ["a"], "d1": ["k1"], "d2": ["k2"]}[t.split(".")[-1]])
+
+
+def test_cached_dimension_tables_still_star_join(sess):
+    """CACHE TABLE on dimension tables (``spark.sparklinedata.druid.cache.tables.tocheck``, the
+    reference's CachedTablePattern, ``asql/CachedTablePattern.scala:39-158``): a cached copy is
+    the same catalog relation here, so the star join is still recognised and eliminated."""
+    for t in ("customer", "orders"):
+        sess.sql(f"CACHE TABLE {t}")
+    try:
+        d = sess.sql(Q["q3"])
+        assert len(d.druid_queries()) == 1
+        assert not any(type(p).__name__ == "Join" for p in d.plan.walk()), d.explain()
+    finally:
+        for t in ("customer", "orders"):
+            sess.sql(f"UNCACHE TABLE {t}")
