@@ -1,0 +1,131 @@
+"""Group existence over the dictionary domain instead of the rows.
+
+An existence-only group-by (no aggregator reads the groups' counts: the inner level of TPC-H Q13's
+``count(distinct o_orderkey)``, Search queries, DISTINCT) keyed on ONE dimension ``K``, over the
+whole shard (no time restriction), whose filter only reads ``K`` itself or dimensions that ``K``
+functionally determines, has the answer
+
+    { k : k occurs in the shard  and  filter(FD(k)) }
+
+-- a predicate over ``C_K`` dictionary entries instead of ``N`` rows.  This is the dictionary-domain
+evaluation of SURVEY K3 ("O(C_d) instead of O(N)") carried one step further, and the GPU analogue
+of what Druid answers from its per-value bitmap indexes (a value's bitmap is non-empty iff it
+occurs).  Q13 at SF100: 600M rows -> 150M order ids; the per-row random byte stores into a 150 MB
+presence table disappear.
+
+The per-dimension occurrence bitmap and the FD tables (``lower.fd_table``) are computed once per
+shard on the device and cached, like the dictionaries themselves.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from ..ops import desc as D
+from .partials import Partials
+
+_CHUNK = 1 << 27
+
+
+def occurrence(ds, col: str) -> torch.Tensor:
+    """bool [C_col]: dictionary id occurs in this shard (cached on the datasource)."""
+    cache = ds.__dict__.setdefault("_occurrence_cache", {})
+    t = cache.get(col)
+    if t is None:
+        d = ds.dims[col]
+        t = torch.zeros(len(d.dictionary), dtype=torch.bool, device=d.ids.device)
+        n = ds.num_rows
+        for s0 in range(0, n, _CHUNK):  # (id columns are padded past num_rows)
+            t[d.ids[s0:min(n, s0 + _CHUNK)].to(torch.int64)] = True
+        cache[col] = t
+    return t
+
+
+def _leaf_cols(x, out: set) -> bool:
+    """Collect the dimensions the filter reads; False if it has anything but id-set leaves."""
+    k = x[0]
+    if k in ("true", "false"):
+        return True
+    if k in ("and", "or"):
+        return all(_leaf_cols(c, out) for c in x[1])
+    if k == "not":
+        return _leaf_cols(x[1], out)
+    if k == "ids":
+        out.add(x[1])
+        return True
+    return False  # time / numeric / expression leaves read rows
+
+
+def plan(prog) -> Optional[Tuple[str, Tuple[str, ...]]]:
+    """(key dimension, dimensions the filter reads) when the program qualifies, else None.
+    Structural checks only (no device work)."""
+    ds = prog.ds
+    if prog.empty or not prog.presence_only or prog.nhll or prog.stored_hll or prog.thetas:
+        return None
+    if len(prog.keys) != 1 or prog.nslots != 1 or getattr(ds, "fd_source", None) is not None:
+        return None
+    kc = prog.keys[0]
+    if kc.kind not in (D.K_ID, D.K_REMAP) or kc.col not in ds.dims:
+        return None
+    if sum(hi - lo for lo, hi in prog.ranges) < ds.num_rows:
+        return None  # a time restriction: rows decide
+    cols: set = set()  # (zone maps are chunk-pruning hints implied by these leaves)
+    if not _leaf_cols(prog.bexpr, cols) or any(c not in ds.dims for c in cols):
+        return None
+    if len(ds.dims[kc.col].dictionary) > ds.num_rows:
+        return None  # more dictionary entries than rows: the scan is cheaper
+    return kc.col, tuple(sorted(cols - {kc.col}))
+
+
+def _eval(x, key_col: str, masks: dict, n: int, dev) -> torch.Tensor:
+    k = x[0]
+    if k == "true":
+        return torch.ones(n, dtype=torch.bool, device=dev)
+    if k == "false":
+        return torch.zeros(n, dtype=torch.bool, device=dev)
+    if k == "and":
+        out = torch.ones(n, dtype=torch.bool, device=dev)
+        for c in x[1]:
+            out &= _eval(c, key_col, masks, n, dev)
+        return out
+    if k == "or":
+        out = torch.zeros(n, dtype=torch.bool, device=dev)
+        for c in x[1]:
+            out |= _eval(c, key_col, masks, n, dev)
+        return out
+    if k == "not":
+        return ~_eval(x[1], key_col, masks, n, dev)
+    m = torch.from_numpy(np.ascontiguousarray(x[2], dtype=np.bool_)).to(dev)
+    if x[1] == key_col:
+        return m[:n] if m.numel() >= n else torch.nn.functional.pad(m, (0, n - m.numel()))
+    fd = masks[x[1]]  # key id -> dependent id (-1: absent everywhere)
+    return m[fd.clamp(min=0).to(torch.int64)] & (fd >= 0)
+
+
+def run(prog, key_col: str, dep_cols, world=None) -> Optional[Partials]:
+    """The existence partials (sparse: group keys + a count slot of ones, like the presence-byte
+    scan), or None when a filter dimension is not functionally determined by the key."""
+    from .lower import fd_table
+
+    ds = prog.ds
+    fds = {}
+    for c in dep_cols:
+        t = fd_table(ds, key_col, c, world)
+        if t is None:
+            return None
+        fds[c] = t
+    occ = occurrence(ds, key_col)
+    n = occ.numel()
+    sel = occ & _eval(prog.bexpr, key_col, fds, n, occ.device)
+    ids = torch.nonzero(sel).flatten()
+    kc = prog.keys[0]
+    if kc.kind == D.K_REMAP:
+        rm = torch.from_numpy(np.asarray(kc.remap, dtype=np.int64)).to(ids.device)
+        keys = rm[ids]
+        keys = torch.sort(keys[keys >= 0]).values
+    else:
+        keys = ids - kc.base
+        keys = keys[(keys >= 0) & (keys < kc.card)]
+    return Partials("sparse", torch.ones((keys.numel(), 1), dtype=torch.int64, device=keys.device), keys, [])

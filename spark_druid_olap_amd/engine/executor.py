@@ -30,6 +30,8 @@ from .partials import Partials, finalize
 
 # segment-batched execution overlaps batch j's merge collectives with batch j+1's scan
 PIPELINE_MERGE = os.environ.get("SDO_PIPELINE_MERGE", "1") not in ("0", "")
+# existence-only group-bys over the key's dictionary domain (engine/dict_exist.py)
+DICT_EXIST = os.environ.get("SDO_DICT_EXIST", "1") not in ("0", "")
 
 
 @dataclass
@@ -172,7 +174,15 @@ class PreparedQuery:
         from ..parallel.fault import FAULTS
 
         FAULTS.maybe_fail("scan", self.world.rank)
-        if prep is not None:
+        de = self._dict_exist_plan(prog)
+        part = None
+        if de is not None:
+            from . import dict_exist
+
+            part = dict_exist.run(prog, *de)
+        if part is not None:
+            pass
+        elif prep is not None:
             part = prep.run()
         else:
             from ..ops.reference import run_reference
@@ -181,6 +191,19 @@ class PreparedQuery:
         if prog.stored_hll:
             part = self._merge_stored_hll(prog, part)
         return part
+
+    def _dict_exist_plan(self, prog):
+        """engine/dict_exist.py: existence-only group-bys answered over the key's dictionary
+        (one GPU / process: the FD tables it reads are shard-local decisions otherwise)."""
+        if not DICT_EXIST or self.world.distributed:
+            return None
+        cache = self.__dict__.setdefault("_dict_exist", {})
+        k = id(prog)
+        if k not in cache:
+            from . import dict_exist
+
+            cache[k] = dict_exist.plan(prog)
+        return cache[k]
 
     def _merge_stored_hll(self, prog, part: Partials) -> Partials:
         """Registers of hyperUnique aggregators over rolled-up sketch metrics: the stored sparse
