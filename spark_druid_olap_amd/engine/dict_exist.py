@@ -100,8 +100,8 @@ def _eval(x, key_col: str, masks: dict, n: int, dev) -> torch.Tensor:
     m = torch.from_numpy(np.ascontiguousarray(x[2], dtype=np.bool_)).to(dev)
     if x[1] == key_col:
         return m[:n] if m.numel() >= n else torch.nn.functional.pad(m, (0, n - m.numel()))
-    fd = masks[x[1]]  # key id -> dependent id (-1: absent everywhere)
-    return m[fd.clamp(min=0).to(torch.int64)] & (fd >= 0)
+    fd = masks[x[1]]  # key id -> dependent id (int32; -1: absent everywhere, so never occurring)
+    return torch.index_select(m, 0, fd.clamp(min=0))
 
 
 def run(prog, key_col: str, dep_cols, world=None) -> Optional[Partials]:
@@ -119,7 +119,12 @@ def run(prog, key_col: str, dep_cols, world=None) -> Optional[Partials]:
     occ = occurrence(ds, key_col)
     n = occ.numel()
     sel = occ & _eval(prog.bexpr, key_col, fds, n, occ.device)
-    ids = torch.nonzero(sel).flatten()
+    if sel.is_cuda:
+        from ..ops import native
+
+        ids = native.nonzero_rows(sel.view(torch.uint8))  # ballot + compaction kernels
+    else:
+        ids = torch.nonzero(sel).flatten()
     kc = prog.keys[0]
     if kc.kind == D.K_REMAP:
         rm = torch.from_numpy(np.asarray(kc.remap, dtype=np.int64)).to(ids.device)

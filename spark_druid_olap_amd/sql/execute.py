@@ -158,8 +158,9 @@ class Executor:
             return b
         return b.take(np.nonzero(mask)[0])
 
-    def _Project(self, p: P.Project) -> Batch:
-        b = self.run(p.child)
+    def _Project(self, p: P.Project, b: Optional[Batch] = None) -> Batch:
+        if b is None:
+            b = self.run(p.child)
         prog = p.__dict__.get("_proj")
         if prog is None:
             # compiled once per plan node: column passthroughs and numpy closures for the
@@ -198,14 +199,22 @@ class Executor:
         return b.take(idx)
 
     def _Limit(self, p: P.Limit) -> Batch:
-        if isinstance(p.child, P.Sort):
-            # ORDER BY ... LIMIT k: sort only the top-k candidates and gather k rows
-            b = self.run(p.child.child)
-            if b.n <= 1:
-                return b if b.n <= p.n else b.take(np.arange(p.n))
-            fr = b.frame(self._subquery)
-            keys = [(eval_series(o.expr, fr), o.ascending, o.nulls_first) for o in p.child.orders]
-            return b.take(sort_indices(keys, b.n, limit=p.n)[:p.n])
+        node, projs = p.child, []
+        while isinstance(node, P.Project):  # row-wise projections commute with the top-k gather
+            projs.append(node)
+            node = node.child
+        if isinstance(node, P.Sort):
+            # ORDER BY ... LIMIT k: sort only the top-k candidates, gather k rows, then project them
+            b = self.run(node.child)
+            if b.n > 1:
+                fr = b.frame(self._subquery)
+                keys = [(eval_series(o.expr, fr), o.ascending, o.nulls_first) for o in node.orders]
+                b = b.take(sort_indices(keys, b.n, limit=p.n)[:p.n])
+            elif b.n > p.n:
+                b = b.take(np.arange(p.n))
+            for pr in reversed(projs):
+                b = self._Project(pr, b)
+            return b
         b = self.run(p.child)
         if b.n <= p.n:
             return b
@@ -645,6 +654,9 @@ def _sort_key(s: pd.Series, asc: bool):
     isna = s.isna().to_numpy()
     if s.dtype.kind == "M":
         arr = np.where(isna, 0, s.astype("int64").to_numpy())
+    elif isinstance(s.dtype, np.dtype) and s.dtype.kind in "iuf":
+        arr = s.to_numpy()
+        arr = np.where(isna, 0.0, arr) if arr.dtype.kind == "f" else arr.astype(np.int64, copy=False)
     elif str(s.dtype) in ("Int64", "Float64", "boolean") or s.dtype.kind in "iufb":
         arr = s.astype("Float64").to_numpy(dtype="float64", na_value=0.0) if str(s.dtype) != "Int64" else \
             s.to_numpy(dtype="int64", na_value=0)

@@ -25,9 +25,9 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, device="cpu"):
     try:
-        _work(rank, world, port, outdir)
+        _work(rank, world, port, outdir, device)
     except BaseException:
         import traceback
 
@@ -36,7 +36,9 @@ def _worker(rank, world, port, outdir):
         raise
 
 
-def _work(rank, world, port, outdir):
+def _work(rank, world, port, outdir, device="cpu"):
+    if device == "cuda":
+        os.environ["SDO_GLOO_GPU"] = "1"  # ranks share the one card, collectives over gloo
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), OMP_NUM_THREADS="1",
                       SDO_REF_SPARSE_G="1000")  # Q3's order-key groups come back sparse (hash-like)
@@ -51,14 +53,14 @@ def _work(rank, world, port, outdir):
     w = init_world(backend="gloo")
     # uneven shards: the last rank keeps the earliest quarter of its rows (fewer segment batches;
     # same dictionaries, so the group-by layouts agree)
-    flat = tpch.generate_flat(0.004, "cpu", rank=rank, world=world)
+    flat = tpch.generate_flat(0.004 if device == "cpu" else 0.05, device, rank=rank, world=world)
     if rank == world - 1:
         n = flat.num_rows // 4
         flat = dataclasses.replace(flat, num_rows=n, ship_day=flat.ship_day[:n],
                                    dims={k: (dct, t[:n]) for k, (dct, t) in flat.dims.items()},
                                    nums={k: (t[:n], kind, sc) for k, (t, kind, sc) in flat.nums.items()})
     ds = tpch.to_datasource(flat, profile="bench")
-    eng = X.Engine(w, use_native=False)
+    eng = X.Engine(w, use_native=device == "cuda")
     from spark_druid_olap_amd.session import Session
 
     Session(engine=eng).register_datasource(ds)  # the cluster-wide time interval (same layouts)
@@ -120,16 +122,31 @@ def _close(a, b):
     return True
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_pipelined_merge_matches_combined_merge(world):
+def _run(world, device):
     with tempfile.TemporaryDirectory() as d:
-        ctx = mp.start_processes(_worker, args=(world, _free_port(), d), nprocs=world, join=False,
+        ctx = mp.start_processes(_worker, args=(world, _free_port(), d, device), nprocs=world, join=False,
                                  start_method="spawn")
         for p in ctx.processes:
             p.join(300)
         errs = [open(os.path.join(d, f)).read() for f in sorted(os.listdir(d)) if f.startswith("err")]
         assert all(p.exitcode == 0 for p in ctx.processes), ([p.exitcode for p in ctx.processes], errs)
         outs = [pickle.load(open(os.path.join(d, f"r{r}.pkl"), "rb")) for r in range(world)]
+    _check(outs, device)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pipelined_merge_matches_combined_merge(world):
+    _run(world, "cpu")
+
+
+@pytest.mark.gpu
+def test_pipelined_merge_on_gpu_scans():
+    """The HIP scan kernels per segment batch with gloo collectives staged through the host (two
+    ranks on the one card of the test box)."""
+    _run(2, "cuda")
+
+
+def _check(outs, device):
     for name in NAMES:
         for oneshot in (True, False):
             per_rank = [o[(name, oneshot)] for o in outs]
@@ -137,7 +154,7 @@ def test_pipelined_merge_matches_combined_merge(world):
             assert len(nb) == 1, (name, nb)  # the agreed batch count
             for a, b, nbatches, nscans, ok in per_rank:
                 assert _close(a, b), (name, oneshot)
-                if name == "TPCH Q3":
+                if name == "TPCH Q3" and device == "cpu":
                     assert ok is False  # hash partials: one merge after the local combine
                 else:
                     assert ok is True and nbatches >= nscans
