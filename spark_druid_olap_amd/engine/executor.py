@@ -336,8 +336,7 @@ class PreparedQuery:
         from ..utils.cancel import checkpoint
 
         if self._nbatches is None:
-            n = torch.tensor([len(self.scans)], dtype=torch.int64, device=self._coll_device())
-            self._nbatches = int(self.world.all_reduce(n, "max").item())
+            self._nbatches = int(self.world.max_float(float(len(self.scans))))
         if self._nbatches <= 1 or self._pipeline_ok is False:
             return None
         # one merge in flight: merge j runs while batch j+1 scans, then merge j completes (RCCL:
@@ -370,9 +369,6 @@ class PreparedQuery:
                 raise_if_failed(sts, self.world.rank, err)
             part = combine_local(prog, [d[0] for d in done])
         return part, t1
-
-    def _coll_device(self):
-        return self.ds.device if self.world.backend == "nccl" else torch.device("cpu")
 
     def _device_having(self, prog: ScanProgram, part: Partials):
         """groupBy havingSpec evaluated over the merged accumulators ON THE DEVICE (TPC-H Q18:

@@ -1358,6 +1358,11 @@ class Lowerer:
             raise LoweringError("group key space exceeds 64 bits")
         prog.G = G
         prog.est_rows = prog.rows_in_ranges * self.selectivity(bexpr)
+        w = self.world
+        if w is not None and w.distributed and getattr(self.ds, "fd_source", None) is None:
+            # the group-by table (and so the partials' dense/sparse layout) is planned from the row
+            # estimate: every rank must decide alike, also when shards differ in size
+            prog.est_rows = w.max_float(float(prog.est_rows))
         if not prog.empty:
             for kc in prog.keys:
                 kc.col_idx = prog.col(kc.col)  # payload section

@@ -163,8 +163,9 @@ class World:
             return x
         dev = self.device() if self.backend == "nccl" else torch.device("cpu")
         t = torch.tensor([x], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-        return float(t.item())
+        # an all-gather, not a ring all-reduce: every rank talks to every peer, so a dead rank is
+        # noticed by all survivors at once (parallel/recovery.py agrees on membership right after)
+        return float(self.all_gather_tensor(t).max().item())
 
 
 class Pending:

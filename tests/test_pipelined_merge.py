@@ -53,7 +53,7 @@ def _work(rank, world, port, outdir, device="cpu"):
     w = init_world(backend="gloo")
     # uneven shards: the last rank keeps the earliest quarter of its rows (fewer segment batches;
     # same dictionaries, so the group-by layouts agree)
-    flat = tpch.generate_flat(0.004 if device == "cpu" else 0.05, device, rank=rank, world=world)
+    flat = tpch.generate_flat(float(os.environ.get("PM_SF", 0.004 if device == "cpu" else 0.05)), device, rank=rank, world=world)
     if rank == world - 1:
         n = flat.num_rows // 4
         flat = dataclasses.replace(flat, num_rows=n, ship_day=flat.ship_day[:n],
