@@ -160,6 +160,15 @@ def _nonzero(t: torch.Tensor) -> torch.Tensor:
     return torch.nonzero(t).flatten()
 
 
+def _histogram(keys: torch.Tensor, nbins: int) -> torch.Tensor:
+    """Per-bin counts (native 32-bit-atomic histogram kernel on the GPU)."""
+    if keys.is_cuda:
+        from ..ops import native
+
+        return native.histogram(keys.contiguous(), nbins)
+    return torch.bincount(keys, minlength=nbins)
+
+
 def _group_sum(R: int, inv: Optional[torch.Tensor], src: torch.Tensor, deterministic: bool) -> torch.Tensor:
     """Per-group sum of ``src`` rows (group ``inv``; None = one global group, reduced with a tree
     reduction instead of a million atomics on one address).  Deterministic float sums go through
@@ -283,7 +292,7 @@ class NestedPreparedQuery:
             if span <= max(1 << 26, 4 * n) and count_only:
                 # dense key space, counts only (Q13's orders per customer): one histogram pass +
                 # compaction of the non-empty bins -- no per-row group index at all
-                counts = torch.bincount(packed, minlength=span)
+                counts = _histogram(packed, span)
                 slots = _nonzero(counts)
                 R = int(slots.numel())
                 inv = None

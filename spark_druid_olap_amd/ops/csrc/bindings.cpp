@@ -28,6 +28,7 @@ __global__ void topk_hist_kernel(const int64_t* acc, int64_t n, int nslots, int 
                                  const uint64_t* state, int level, unsigned int* hist);
 __global__ void topk_pick_kernel(unsigned int* hist, uint64_t* state, int level);
 __global__ void nonzero_mask_kernel(const unsigned char* base, int esize, int64_t n, int64_t stride, uint64_t* words);
+__global__ void histogram_kernel(const int64_t* keys, int64_t n, int64_t nbins, unsigned int* counts);
 struct ResetArgs {
   int64_t* acc;
   const int64_t* init;
@@ -153,6 +154,15 @@ static void nonzero_mask(uint64_t base, int esize, int64_t n, int64_t stride, ui
   hipLaunchKernelGGL(sdo::nonzero_mask_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
                      (const unsigned char*)base, esize, n, stride, (uint64_t*)words);
   check(hipGetLastError(), "nonzero_mask_kernel launch");
+}
+
+static void histogram(uint64_t keys, int64_t n, int64_t nbins, uint64_t counts, uint64_t stream) {
+  if (n <= 0 || nbins <= 0) return;
+  int64_t blocks = (n + 1023) / 1024;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(sdo::histogram_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     (const int64_t*)keys, n, nbins, (unsigned int*)counts);
+  check(hipGetLastError(), "histogram_kernel launch");
 }
 
 // One-launch re-initialisation of a prepared scan's buffers (post_scan.hip reset_bufs_kernel).
@@ -327,6 +337,7 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("compact_write", &compact_write);
   m.def("topk_keep", &topk_keep);
   m.def("nonzero_mask", &nonzero_mask);
+  m.def("histogram", &histogram);
   m.def("reset_bufs", &reset_bufs);
   m.def("hll_pairs", &hll_pairs);
   m.def("hll_merge_stored", &hll_merge_stored);

@@ -132,6 +132,27 @@ __global__ void __launch_bounds__(256) nonzero_mask_kernel(const unsigned char* 
   }
 }
 
+// Per-bin counts of int64 group ids (nested count-only levels: TPC-H Q13's orders per customer):
+// one no-return 32-bit device atomic per id, four ids in flight per thread, no min/max pre-pass
+// (the bin count is known from the key radix).  Ids outside [0, nbins) are ignored.
+__global__ void __launch_bounds__(256) histogram_kernel(const int64_t* __restrict__ keys, int64_t n, int64_t nbins,
+                                                       unsigned int* __restrict__ counts) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    int64_t k[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) k[u] = keys[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if ((uint64_t)k[u] < (uint64_t)nbins) atomicAdd(counts + k[u], 1u);
+  }
+  for (; i < n; i += stride) {
+    const int64_t k = keys[i];
+    if ((uint64_t)k < (uint64_t)nbins) atomicAdd(counts + k, 1u);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // top-k threshold over one accumulator slot of the merged partials ([rows, nslots] int64).
 // The slot is mapped to an order-preserving unsigned key (larger = better) on the fly: f64 sums by

@@ -180,6 +180,17 @@ def nonzero_rows(col: torch.Tensor) -> torch.Tensor:
     return compact_rows(words)
 
 
+def histogram(keys: torch.Tensor, nbins: int) -> torch.Tensor:
+    """int64 counts per bin of int64 ids in [0, nbins) (post_scan.hip histogram_kernel: 32-bit
+    device atomics, no min/max pre-pass); replaces ``torch.bincount`` for nested count levels."""
+    m = load()
+    assert keys.dim() == 1 and keys.is_cuda and keys.dtype == torch.int64 and keys.is_contiguous()
+    assert keys.numel() < (1 << 32)
+    counts = torch.zeros(nbins, dtype=torch.int32, device=keys.device)
+    m.histogram(keys.data_ptr(), keys.numel(), nbins, counts.data_ptr(), _stream(keys.device))
+    return counts.to(torch.int64)
+
+
 def hll_pairs(vals: torch.Tensor, p: int, salt: int) -> torch.Tensor:
     """Packed (bucket << 8 | rho) int32 HLL pair of every 64-bit value (sketch.hip hll_pairs)."""
     m = load()

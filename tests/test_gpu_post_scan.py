@@ -40,6 +40,16 @@ def test_nonzero_rows_strided(dtype):
     assert torch.equal(got, torch.nonzero(col).flatten())
 
 
+@pytest.mark.parametrize("n,nbins", [(1, 1), (1000, 7), (3_000_017, 1_000_003), (10_000_000, 64)])
+def test_histogram_matches_bincount(n, nbins):
+    g = torch.Generator(device="cuda").manual_seed(n)
+    keys = torch.randint(0, nbins, (n,), generator=g, device="cuda", dtype=torch.int64)
+    keys[::97] = nbins + 5  # out-of-range ids are ignored
+    got = _native().histogram(keys, nbins)
+    exp = torch.bincount(keys[keys < nbins], minlength=nbins)
+    assert torch.equal(got, exp)
+
+
 @pytest.mark.parametrize("kind", ["f64", "i64"])
 @pytest.mark.parametrize("desc", [True, False])
 @pytest.mark.parametrize("R,k", [(100, 7), (1_000_003, 100), (2_000_000, 1)])
