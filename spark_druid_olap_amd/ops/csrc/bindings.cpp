@@ -29,6 +29,7 @@ __global__ void topk_hist_kernel(const int64_t* acc, int64_t n, int nslots, int 
 __global__ void topk_pick_kernel(unsigned int* hist, uint64_t* state, int level);
 __global__ void nonzero_mask_kernel(const unsigned char* base, int esize, int64_t n, int64_t stride, uint64_t* words);
 __global__ void histogram_kernel(const int64_t* keys, int64_t n, int64_t nbins, unsigned int* counts);
+__global__ void histogram_lds_kernel(const int64_t* keys, int64_t n, int nbins, unsigned int* counts);
 struct ResetArgs {
   int64_t* acc;
   const int64_t* init;
@@ -158,6 +159,14 @@ static void nonzero_mask(uint64_t base, int esize, int64_t n, int64_t stride, ui
 
 static void histogram(uint64_t keys, int64_t n, int64_t nbins, uint64_t counts, uint64_t stream) {
   if (n <= 0 || nbins <= 0) return;
+  if (nbins <= 16384) {  // LDS-privatised counts (64 KB at most)
+    int64_t blocks = (n + 4095) / 4096;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(sdo::histogram_lds_kernel, dim3((unsigned)blocks), dim3(256), (unsigned)(nbins * 4),
+                       (hipStream_t)stream, (const int64_t*)keys, n, (int)nbins, (unsigned int*)counts);
+    check(hipGetLastError(), "histogram_lds_kernel launch");
+    return;
+  }
   int64_t blocks = (n + 1023) / 1024;
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(sdo::histogram_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,

@@ -153,6 +153,24 @@ __global__ void __launch_bounds__(256) histogram_kernel(const int64_t* __restric
   }
 }
 
+// Few bins (TPC-H Q13's outer level: 15M customers into ~30 order counts): every block counts
+// into an LDS copy first and flushes it with one global atomic per non-empty bin -- global
+// atomics on a handful of addresses would serialise.
+__global__ void __launch_bounds__(256) histogram_lds_kernel(const int64_t* __restrict__ keys, int64_t n, int nbins,
+                                                           unsigned int* __restrict__ counts) {
+  extern __shared__ unsigned int h[];
+  for (int b = threadIdx.x; b < nbins; b += blockDim.x) h[b] = 0u;
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t k = keys[i];
+    if ((uint64_t)k < (uint64_t)nbins) atomicAdd(h + k, 1u);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < nbins; b += blockDim.x)
+    if (h[b]) atomicAdd(counts + b, h[b]);
+}
+
 // ---------------------------------------------------------------------------------------------
 // top-k threshold over one accumulator slot of the merged partials ([rows, nslots] int64).
 // The slot is mapped to an order-preserving unsigned key (larger = better) on the fly: f64 sums by

@@ -40,7 +40,7 @@ def test_nonzero_rows_strided(dtype):
     assert torch.equal(got, torch.nonzero(col).flatten())
 
 
-@pytest.mark.parametrize("n,nbins", [(1, 1), (1000, 7), (3_000_017, 1_000_003), (10_000_000, 64)])
+@pytest.mark.parametrize("n,nbins", [(1, 1), (1000, 7), (3_000_017, 1_000_003), (10_000_000, 64), (5_000_000, 16384), (5_000_000, 16385)])
 def test_histogram_matches_bincount(n, nbins):
     g = torch.Generator(device="cuda").manual_seed(n)
     keys = torch.randint(0, nbins, (n,), generator=g, device="cuda", dtype=torch.int64)
