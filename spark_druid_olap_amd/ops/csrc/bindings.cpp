@@ -28,6 +28,7 @@ __global__ void topk_hist_kernel(const int64_t* acc, int64_t n, int nslots, int 
                                  const uint64_t* state, int level, unsigned int* hist);
 __global__ void topk_pick_kernel(unsigned int* hist, uint64_t* state, int level);
 __global__ void nonzero_mask_kernel(const unsigned char* base, int esize, int64_t n, int64_t stride, uint64_t* words);
+__global__ void nonzero_mask_u8_kernel(const unsigned char* base, int64_t n, uint64_t* words);
 __global__ void histogram_kernel(const int64_t* keys, int64_t n, int64_t nbins, unsigned int* counts);
 __global__ void histogram_lds_kernel(const int64_t* keys, int64_t n, int nbins, unsigned int* counts);
 struct ResetArgs {
@@ -150,6 +151,15 @@ static void nonzero_mask(uint64_t base, int esize, int64_t n, int64_t stride, ui
   if (n <= 0) return;
   if (esize != 1 && esize != 8) throw std::invalid_argument("esize must be 1 or 8");
   int64_t nwords = (n + 63) / 64;
+  if (esize == 1 && stride == 1 && (base & 15) == 0) {  // contiguous bytes: 16-byte loads
+    int64_t nchunks = (n + 1023) / 1024;
+    int64_t blocks = (nchunks + 3) / 4;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(sdo::nonzero_mask_u8_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const unsigned char*)base, n, (uint64_t*)words);
+    check(hipGetLastError(), "nonzero_mask_u8_kernel launch");
+    return;
+  }
   int64_t blocks = (nwords + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(sdo::nonzero_mask_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,

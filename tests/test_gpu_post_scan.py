@@ -40,6 +40,17 @@ def test_nonzero_rows_strided(dtype):
     assert torch.equal(got, torch.nonzero(col).flatten())
 
 
+@pytest.mark.parametrize("n", [1, 15, 16, 1023, 1024, 1025, 150_001, 3_000_000])
+def test_nonzero_rows_contiguous_bytes(n):
+    """The 16-byte-load path for contiguous byte tables (and its ragged tail)."""
+    g = torch.Generator(device="cuda").manual_seed(n)
+    col = (torch.rand(n, generator=g, device="cuda") < 0.3).to(torch.uint8) * 7
+    got = _native().nonzero_rows(col)
+    assert torch.equal(got, torch.nonzero(col).flatten())
+    b = torch.rand(n, generator=g, device="cuda") < 0.5
+    assert torch.equal(_native().nonzero_rows(b.view(torch.uint8)), torch.nonzero(b).flatten())
+
+
 @pytest.mark.parametrize("n,nbins", [(1, 1), (1000, 7), (3_000_017, 1_000_003), (10_000_000, 64), (5_000_000, 16384), (5_000_000, 16385)])
 def test_histogram_matches_bincount(n, nbins):
     g = torch.Generator(device="cuda").manual_seed(n)
