@@ -404,6 +404,14 @@ def to_datasource(flat: FlatTPCH, name: str = "tpch", bitmap_max_card: int = 256
         elif d in flat.nums or d in _NUM_ALIAS:
             t, _, scale = flat.nums[_NUM_ALIAS.get(d, d)]
             dicts[d], dim_ids[d] = _numeric_dim(t, scale)
+        elif d == "order_year" and "o_orderdate" in flat.dims:
+            # the test index's order_year dimension (tpch_index_task.json.template:39): the year of
+            # o_orderdate, one id per distinct year
+            od_dict, od_ids = flat.dims["o_orderdate"]
+            vals = [str(v)[:4] for v in od_dict.all_values()]
+            years = sorted(set(vals))
+            remap = torch.tensor([years.index(v) for v in vals], dtype=torch.int16, device=od_ids.device)
+            dicts[d], dim_ids[d] = Dictionary(years, STRING), remap[od_ids.to(torch.int64)]
     mdata, mkinds, mscales = {}, {}, {}
     for mname, (src, kind, scale) in mets.items():
         if src in flat.nums:
