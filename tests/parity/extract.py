@@ -263,9 +263,10 @@ def extract_from_reference():
             rest = src[i:i + 40]
             if kind == "test":
                 mm = re.match(r"\s*,\s*(\d+)", rest)
-                if not mm:
-                    continue
-                out.append((fn[:-6], name, "shape", sql, int(mm.group(1)), None))
+                if mm:
+                    out.append((fn[:-6], name, "shape", sql, int(mm.group(1)), None))
+                elif re.match(r"\s*\)", rest):  # numDruidQueries defaults to 1 (tc/AbstractTest.scala:105-106)
+                    out.append((fn[:-6], name, "shape", sql, 1, None))
             else:
                 mm = re.match(r"\s*,\s*", rest)
                 if not mm:
