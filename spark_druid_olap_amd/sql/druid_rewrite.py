@@ -42,6 +42,12 @@ MIN_MS = -(2 ** 62)
 MAX_MS = 2 ** 62
 
 
+
+def _is_day_expr(e: A.Expr) -> bool:
+    """to_date(x) / cast(x as date): a value that is already a whole day."""
+    return (isinstance(e, A.Call) and e.name == "to_date" and len(e.args) == 1) or \
+        (isinstance(e, A.Cast) and e.to == "date")
+
 class NotPushable(Exception):
     pass
 
@@ -272,6 +278,12 @@ class DruidRewriter:
             if isinstance(e, A.Call) and e.name in ("datetime", "datetimewithtz") and len(e.args) == 1:
                 e = e.args[0]
             elif isinstance(e, A.Call) and e.name == "to_date" and len(e.args) == 1:
+                e, trunc = e.args[0], True
+            elif isinstance(e, A.Call) and e.name == "concat" and len(e.args) == 2 and \
+                    isinstance(e.args[1], A.Lit) and isinstance(e.args[1].value, str) and \
+                    re.fullmatch(r"[ T]00:00:00(\.0+)?Z?", e.args[1].value) and _is_day_expr(e.args[0]):
+                # Cast(Concat(To_date(t), ' 00:00:00') AS TIMESTAMP): midnight of t's day (the BI-tool
+                # spelling the reference's SparkIntervalConditionExtractor folds, DateTimeExtractor.scala:374-436)
                 e, trunc = e.args[0], True
             elif isinstance(e, A.Cast) and e.to in ("date", "timestamp"):
                 trunc = trunc or e.to == "date"
