@@ -1154,6 +1154,16 @@ class Lowerer:
                 return 1
             if k == "col":
                 name = mapping.get(n[1], n[1])
+                vl = virtual_lut(self.ds, name)
+                if vl is not None:
+                    # an expression over one dimension evaluated per dictionary entry by the SQL
+                    # layer (druid_rewrite._dim_expr_agg): one f64 table lookup by the row's id
+                    col, lut = vl
+                    prog.keepalive.append(lut)
+                    c = _ptr_as_double(lut.data_ptr())
+                    prog.lut_ptrs[c] = lut
+                    out.append((D.E_LUT, prog.col(col), c))
+                    return 1
                 if name == TIME:
                     # __time in epoch ms (stored in time units)
                     out.append((D.E_COL, prog.col(TIME), float(self.ds.time_unit_ms)))
@@ -1519,6 +1529,22 @@ def fd_metric_table(ds: DataSource, a: str, metric: str, world=None) -> Optional
         cache[key] = _fd_lut(ds.dims[a].ids, len(ds.dims[a].dictionary), column_tensor(ds, metric), ds.num_rows,
                              world)
     return cache[key]
+
+
+def virtual_lut(ds, name: str):
+    """(column, device f64 table) of a per-dictionary-entry expression table registered by the SQL
+    rewrite under ``name`` (``__vx_*``), or None."""
+    src = getattr(ds, "fd_source", None) or ds
+    reg = src.__dict__.get("_virtual_luts") if hasattr(src, "__dict__") else None
+    if not reg or name not in reg:
+        return None
+    cache = src.__dict__.setdefault("_virtual_luts_dev", {})
+    t = cache.get(name)
+    col, arr = reg[name]
+    if t is None:
+        dev = src.time.device if col == TIME else src.dims[col].ids.device
+        t = cache[name] = torch.from_numpy(arr).to(dev)
+    return col, t
 
 
 def fd_table(ds: DataSource, a: str, b: str, world=None) -> Optional[torch.Tensor]:

@@ -841,11 +841,24 @@ class DruidRewriter:
             if fa is not None:
                 return [fa], lambda rs: rs[0]
             kind = "sum" if n in ("avg", "mean") else n
+            null_t = typeof(x) if n in ("min", "max") else "double"
             if kind in ("min", "max"):
                 tv = self._time_valued_agg(pf, kind, x, names)
+                if tv is None and base(typeof(x)) in ("timestamp", "date"):
+                    tv = self._dim_expr_agg(pf, kind, x, names)
+                if tv == "null":
+                    return [count_spec()], lambda rs: A.Cast(A.Lit(None, "null"), null_t)
                 if tv is not None:
                     return [tv], lambda rs: rs[0]
-            spec_, t = self._numeric_agg(pf, kind, x, names)
+            try:
+                spec_, t = self._numeric_agg(pf, kind, x, names)
+            except NotPushable:
+                de = self._dim_expr_agg(pf, kind, x, names) if base(typeof(x)) not in ("timestamp", "date") else None
+                if de is None:
+                    raise
+                if de == "null":
+                    return [count_spec()], lambda rs: A.Cast(A.Lit(None, "null"), null_t)
+                spec_, t = de[0], de[1]
             if n in ("avg", "mean"):
                 cnt, ct = count_spec()
                 return [(spec_, t), (cnt, ct)], \
@@ -898,6 +911,67 @@ class DruidRewriter:
             agg, comb, reset = js_aggregator(kind, A.Ref(e.rid, p, "double"), {e.rid: p}, [p])
             return S.JavascriptAggregationSpec(names.agg(), [c.druid_column], agg, comb, reset), "timestamp", "time"
         return None
+
+    def _dim_expr_agg(self, pf: PF, kind: str, x: A.Expr, names: "_Names"):
+        """SUM / MIN / MAX of an expression over ONE dimension (or the day-grained time column) that
+        the scan VM cannot evaluate per row -- ``unix_timestamp(l_shipdate) * 1000``, nested
+        to_date / concat / cast chains (tc/CodeGenTest.scala:417-482): the expression is evaluated
+        once per dictionary entry (per day) with the SQL function library, exactly as the base-table
+        plan would, and the aggregator reads that table by the row's id (engine E_LUT) -- the
+        reference sends these as JavaScript aggregators.  Returns (spec, SQL type, kind) or None."""
+        import hashlib
+
+        refs = {r.rid: r for r in x.refs()}
+        if len(refs) != 1:
+            return None
+        r = next(iter(refs.values()))
+        c = pf.cols.get(r.rid)
+        if c is None or c.is_metric:
+            return None
+        ds = pf.table.info.datasource
+        if c.is_time:
+            if ds.time_unit_ms != DAY_MS:
+                return None
+            gi = getattr(ds, "global_interval_ms", None)
+            hi_ms = gi[1] if gi is not None else data_interval(ds)[1]
+            ndays = int(hi_ms // DAY_MS) + 1
+            if ndays > (1 << 20):
+                return None
+            values = [_time_value(d * DAY_MS, c) for d in range(ndays)]
+            column = "__time"
+        else:
+            dc = ds.dims.get(c.druid_column) if hasattr(ds, "dims") else None
+            if dc is None or len(dc.dictionary) > (1 << 22):
+                return None
+            values = list(dc.dictionary.all_values())
+            column = c.druid_column
+        try:
+            v = evaluate(x, _dict_frame(values, r, c))
+        except Exception:  # noqa: BLE001  (an expression the host library cannot evaluate)
+            return None
+        if not is_vec(v):
+            return None
+        timed = v.dtype.kind == "M"
+        if timed:
+            arr = np.where(v.isna().to_numpy(), np.nan, v.astype("int64").to_numpy() / 1e6)
+        elif v.dtype.kind in "iufb" or str(v.dtype) in ("Int64", "Float64", "boolean"):
+            arr = v.astype("Float64").to_numpy(dtype="float64", na_value=np.nan)
+        else:
+            return None
+        if np.isnan(arr).all():
+            return "null"  # every value NULL (e.g. unix_timestamp of a date-only string): SQL NULL
+        if np.isnan(arr).any():
+            return None  # some NULL values: the aggregator would have to skip them
+        name = "__vx_" + hashlib.sha1(f"{column}|{x.sql()}".encode()).hexdigest()[:12]
+        ds.__dict__.setdefault("_virtual_luts", {})[name] = (column, np.ascontiguousarray(arr, dtype=np.float64))
+        p = _js_ident(name)
+        rid = A.new_id()
+        try:
+            agg, comb, reset = js_aggregator(kind, A.Ref(rid, p, "double"), {rid: p}, [p])
+        except JSGenError:
+            return None
+        spec = S.JavascriptAggregationSpec(names.agg(), [name], agg, comb, reset)
+        return (spec, "timestamp", "time") if timed else (spec, "double", None)
 
     def _numeric_agg(self, pf: PF, kind: str, x: A.Expr, names: "_Names"):
         if isinstance(x, A.Cast) and (x.to in ("double", "float") or x.to.startswith("decimal")):

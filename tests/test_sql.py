@@ -301,3 +301,16 @@ def test_numeric_key_join_nullable_ints():
     r = pd.Series([2, 1, 2], dtype="Int64")
     li, ri = _numeric_key_join([l], [r], l.notna().to_numpy(), r.notna().to_numpy())
     assert sorted(zip(li.tolist(), ri.tolist())) == [(0, 1), (1, 0), (1, 2), (3, 0), (3, 2)]
+
+
+@pytest.mark.parametrize("agg", [
+    "max(length(c_name))",
+    "sum(datediff(to_date(l_commitdate), to_date('1992-01-01')))",
+    "min(cast(concat(to_date(l_commitdate), ' 00:00:00') as timestamp))",
+    "avg(month(to_date(o_orderdate)))",
+])
+def test_aggregate_over_one_dimension_expression(sess, agg):
+    """SUM/MIN/MAX/AVG of an expression over one dimension: evaluated once per dictionary entry and
+    aggregated through the entry table (druid_rewrite._dim_expr_agg), the reference's JavaScript
+    aggregator over a dimension (tc/CodeGenTest.scala:417-482)."""
+    ctest(sess, f"select l_returnflag, {agg} from {T} group by l_returnflag", ndruid=1)
