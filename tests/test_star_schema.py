@@ -136,3 +136,51 @@ def test_cached_dimension_tables_still_star_join(sess):
     finally:
         for t in ("customer", "orders"):
             sess.sql(f"UNCACHE TABLE {t}")
+
+
+# --- the reference's StarSchemaMetadataTest (tc/StarSchemaMetadataTest.scala:27-118) ----------
+def _rel(left, right, *pairs):
+    return {"leftTable": left, "rightTable": right, "relationType": "n-1",
+            "joinCondition": [{"leftAttribute": a, "rightAttribute": b} for a, b in pairs]}
+
+
+def _build(*rels):
+    def cols(t):
+        t = t.split(".")[-1]
+        t = {"lineitem": "lineitembase", "partsupp2": "partsupp"}.get(t, t)
+        return [c for c, _ in tpch.STAR_SCHEMAS[t]]
+    return StarSchema.build("lineitem", StarSchemaInfo.parse({"factTable": "lineitem", "relations": list(rels)}), cols)
+
+
+_TPCH_RELS = [
+    _rel("lineitem", "orders", ("l_orderkey", "o_orderkey")),
+    _rel("lineitem", "partsupp", ("l_partkey", "ps_partkey"), ("l_suppkey", "ps_suppkey")),
+    _rel("partsupp", "part", ("ps_partkey", "p_partkey")),
+    _rel("partsupp", "supplier", ("ps_suppkey", "s_suppkey")),
+    _rel("orders", "customer", ("o_custkey", "c_custkey")),
+    _rel("customer", "custnation", ("c_nationkey", "cn_nationkey")),
+    _rel("custnation", "custregion", ("cn_regionkey", "cr_regionkey")),
+    _rel("supplier", "suppnation", ("s_nationkey", "sn_nationkey")),
+    _rel("suppnation", "suppregion", ("sn_regionkey", "sr_regionkey")),
+]
+
+
+@pytest.mark.parametrize("rels", [
+    _TPCH_RELS[:1],                                                                          # simpleStar
+    [_TPCH_RELS[0], _rel("lineitem", "part", ("l_partkey", "p_partkey")),
+     _rel("lineitem", "supplier", ("l_suppkey", "s_suppkey"))],                              # salesStar
+    _TPCH_RELS,                                                                              # tpch
+], ids=["simpleStar", "salesStar", "tpch"])
+def test_valid_star_schemas(rels):
+    s = _build(*rels)
+    assert s.is_star_join(["l_orderkey"], ["o_orderkey"]) == ("lineitem", "orders")
+
+
+def test_multiple_paths_not_allowed():
+    with pytest.raises(StarSchemaError, match="multiple join paths to table 'supplier'"):
+        _build(*_TPCH_RELS[:4], _rel("lineitem", "supplier", ("l_suppkey", "s_suppkey")))
+
+
+def test_non_unique_columns_not_allowed():
+    with pytest.raises(StarSchemaError, match="Column ps_partkey is not unique across Star Schema"):
+        _build(*_TPCH_RELS[:4], _rel("lineitem", "partsupp2", ("l_partkey", "ps_partkey"), ("l_suppkey", "ps_suppkey")))
