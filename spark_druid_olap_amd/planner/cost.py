@@ -240,7 +240,6 @@ DENSE_MAX_SPARSE_MULTI = int(os.environ.get("SDO_DENSE_MAX_SPARSE", 4 << 30))  #
 DENSE_MAX_1GPU = int(os.environ.get("SDO_DENSE_MAX_1GPU", 16 << 30))
 TOUCH_MIN_G = int(os.environ.get("SDO_TOUCH_MIN_G", 1 << 20))
 PROBE_S = 1.0e-9        # hash-table insert (CAS probe + key compare) per qualifying row
-TOUCH_ROW_S = 1.5e-11   # first-touch byte store per qualifying row (TPC-H Q18: 9 ms / 600M rows)
 ONESHOT_MAX_BYTES = 256 << 20   # gather buffer (world x state) ceiling for the one-shot merge
 
 
@@ -288,12 +287,12 @@ def plan_groupby(prog, jit: bool, local: bool) -> GroupByPlan:
                  and not os.environ.get("SDO_NO_TOUCH"))
     table = G * ns * 8 + hll_bytes
     est_rows = max(1.0, float(getattr(prog, "est_rows", G)))
-    if touch and local:
-        # one GPU: a first-touch byte per group pays off only when few groups are touched -- every
-        # qualifying row also stores its group's byte (measured: TPC-H Q18, all 150M orders touched,
-        # 45 -> 36 ms without it; Q3, ~1% touched, 1.15 vs 1.95 ms with it)
-        touch_cost = (2 * G + min(G, est_rows) * ns * 16) / HBM_BW + est_rows * TOUCH_ROW_S
-        touch = touch_cost < 2 * table / HBM_BW
+    if touch and local and est_rows >= G:
+        # one GPU: a first-touch byte per group pays off only when groups go untouched -- every
+        # qualifying row also stores its group's byte.  With at least as many qualifying rows as
+        # groups (TPC-H Q18: 600M lines over 150M orders) the byte table is pure overhead
+        # (45 -> 36 ms without it); selective scans keep it (Q3: 1.0 vs 1.4 ms)
+        touch = False
     if local:
         limit = DENSE_MAX_1GPU
     else:
