@@ -88,9 +88,9 @@ static void bitmap_build(uint64_t ids, int dtype, int64_t n, int64_t nwords, uin
 static void hll_estimate(uint64_t regs, int64_t G, int p, uint64_t est, uint64_t stream) {
   if (G <= 0) return;
   if (p < 4 || p > 18) throw std::invalid_argument("hll precision out of range");
-  if ((1 << p) % (16 * 2) != 0) throw std::invalid_argument("hll registers must split over 16 waves");
+  if (p < 7) throw std::invalid_argument("hll estimate needs >= 128 registers (128-register column chunks)");
   const unsigned blocks = (unsigned)((G + 31) / 32);
-  hipLaunchKernelGGL(sdo::hll_estimate_kernel, dim3(blocks), dim3(1024), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(sdo::hll_estimate_kernel, dim3(blocks), dim3(8 * 64), 0, (hipStream_t)stream,
                      (const uint32_t*)regs, G, p, (double*)est);
   check(hipGetLastError(), "hll_estimate_kernel launch");
 }
@@ -240,8 +240,8 @@ static int glds_probe() {
   check(hipGetLastError(), "glds_probe launch");
   uint32_t h_out[128];
   check(hipMemcpy(h_out, d_out, sizeof(h_out), hipMemcpyDeviceToHost), "hipMemcpy");
-  hipFree(d_src);
-  hipFree(d_out);
+  (void)hipFree(d_src);
+  (void)hipFree(d_out);
   bool dword = true, packed = true;
   for (int l = 0; l < 64; ++l) {
     if ((h_out[l] & 0xff) != (uint32_t)((l + 1) & 0xff)) dword = false;

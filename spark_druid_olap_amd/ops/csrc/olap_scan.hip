@@ -768,33 +768,64 @@ __global__ __launch_bounds__(256) void bitmap_build_kernel(const void* ids, int 
 
 // ---------------------------------------------------------------------------------------------
 // HyperLogLog finalize for G groups x m registers: sum(2^-M) and zero counts per group.
-// The register matrix is multiplied by a ones vector on the matrix cores (MFMA 32x32x2 f32:
-// A = 2^-M tile [32 groups x 2 regs], B = e0 [2 x 32]) -- the batched sketch reduction of the
-// BASELINE north-star.  16 waves per block split the registers; partial column-0 sums meet in LDS.
+// The register matrix is multiplied by a ones vector on the matrix cores (MFMA 32x32x16 bf16, f32
+// accumulate: A = 2^-M tile [32 groups x 16 regs], exact in bf16 for M <= 126, B = e0) -- the batched sketch reduction of the
+// BASELINE north-star.  Each wave owns 128-register column chunks of a 32-group row block: the
+// chunk is read with 16 independent, fully coalesced 16-byte loads per lane (one memory round trip,
+// not one per MFMA step), packed to bytes in a wave-private LDS tile (rho <= 65), and the MFMA
+// steps read it as 8-byte rows with a 136-byte pitch (the 32 rows' dword pairs cover all 64 banks).
+// Partial column-0 sums of the HLL_EST_WAVES waves meet in LDS.
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-__global__ __launch_bounds__(1024) void hll_estimate_kernel(const uint32_t* regs, int64_t G, int p, double* est) {
-  __shared__ float part[16][2][32];
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int HLL_EST_WAVES = 8, HLL_EST_CH = 128, HLL_EST_PITCH = HLL_EST_CH + 8;
+__global__ __launch_bounds__(HLL_EST_WAVES * 64) void hll_estimate_kernel(const uint32_t* regs, int64_t G, int p,
+                                                                          double* est) {
+  __shared__ __attribute__((aligned(16))) unsigned char tiles[HLL_EST_WAVES][32 * HLL_EST_PITCH];
+  __shared__ float part[HLL_EST_WAVES][2][32];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int nw = blockDim.x >> 6;
   const int64_t m = 1ll << p;
   const int64_t g0 = (int64_t)blockIdx.x * 32;
+  unsigned char* tile = tiles[wave];
   f32x16 acc_sum = {0};
   f32x16 acc_zero = {0};
   const int i = lane & 31;
   const int kk = lane >> 5;
-  const int64_t g = g0 + i;
-  const float bsel = (i == 0) ? 1.0f : 0.0f;
-  const int64_t per = m / nw;
-  for (int64_t kb = wave * per; kb < (wave + 1) * per; kb += 2) {
-    float a = 0.f, z = 0.f;
-    if (g < G) {
-      const uint32_t r = regs[g * m + kb + kk];
-      a = __builtin_amdgcn_ldexpf(1.0f, -(int)r);
-      z = r == 0 ? 1.f : 0.f;
+  const uint32_t one = i == 0 ? 0x3f803f80u : 0u;  // B = e0 columns: 1.0 bf16 pairs in column 0
+  const bf16x8 bsel = __builtin_bit_cast(bf16x8, u32x4{one, one, one, one});
+  for (int64_t c0 = (int64_t)wave * HLL_EST_CH; c0 < m; c0 += HLL_EST_WAVES * HLL_EST_CH) {
+    uint4 x[16];  // 32 rows x 32 uint4 = the chunk; lane takes vectors lane, lane+64, ...
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int v = j * 64 + lane;
+      const int64_t g = g0 + (v >> 5);
+      x[j] = g < G ? *(const uint4*)(regs + g * m + c0 + (v & 31) * 4) : make_uint4(0u, 0u, 0u, 0u);
     }
-    acc_sum = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bsel, acc_sum, 0, 0, 0);
-    acc_zero = __builtin_amdgcn_mfma_f32_32x32x2f32(z, bsel, acc_zero, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int v = j * 64 + lane;
+      const uint32_t b = min(x[j].x, 255u) | (min(x[j].y, 255u) << 8) | (min(x[j].z, 255u) << 16) |
+                         (min(x[j].w, 255u) << 24);
+      *(uint32_t*)(tile + (v >> 5) * HLL_EST_PITCH + (v & 31) * 4) = b;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private tile: writes land before reads
+#pragma unroll
+    for (int kb = 0; kb < HLL_EST_CH; kb += 16) {
+      // A[i][k] for k = kb + 8 * kk .. +7: 8 byte registers -> 2^-M and (M == 0) as exact bf16 (powers
+      // of two: bf16 bits (127 - M) << 7)
+      const uint64_t rb = *(const uint64_t*)(tile + i * HLL_EST_PITCH + kb + kk * 8);
+      u32x4 pa, pz;
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const uint32_t r0 = (uint32_t)(rb >> (16 * h)) & 0xffu, r1 = (uint32_t)(rb >> (16 * h + 8)) & 0xffu;
+        pa[h] = ((127u - r0) << 7) | (((127u - r1) << 7) << 16);
+        pz[h] = (r0 == 0 ? 0x3f80u : 0u) | ((r1 == 0 ? 0x3f80u : 0u) << 16);
+      }
+      acc_sum = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, pa), bsel, acc_sum, 0, 0, 0);
+      acc_zero = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, pz), bsel, acc_zero, 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile reads done before the next chunk overwrites it
   }
   // D[row][col]: col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); column 0 = sums
   if ((lane & 31) == 0) {
@@ -810,7 +841,7 @@ __global__ __launch_bounds__(1024) void hll_estimate_kernel(const uint32_t* regs
     const int64_t gg = g0 + threadIdx.x;
     if (gg < G) {
       double s = 0.0, zeros = 0.0;
-      for (int w = 0; w < nw; ++w) {
+      for (int w = 0; w < HLL_EST_WAVES; ++w) {
         s += part[w][0][threadIdx.x];
         zeros += part[w][1][threadIdx.x];
       }
