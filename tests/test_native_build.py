@@ -73,3 +73,16 @@ def test_jit_presence_only_kernel_compiles(tmp_path, monkeypatch, ds_small):
     js = jit.JitScan(prog, D.M_DENSE_GLOBAL, 4, False, 2048, True, load=False)
     assert "(unsigned char*)gacc)[slot]" in js.src
 
+
+
+def test_hll_estimate_bf16_operands_are_exact():
+    """hll_estimate_kernel (ops/csrc/olap_scan.hip) feeds 2^-M to a bf16 MFMA as the bit pattern
+    (127 - M) << 7: exact powers of two for every register value a 64-bit hash can produce (M <= 65),
+    and 1.0 (0x3f80) for the zero-register indicator."""
+    import torch
+
+    for r in range(0, 66):
+        bits = torch.tensor([2.0 ** -r], dtype=torch.float32).to(torch.bfloat16).view(torch.int16).item() & 0xFFFF
+        assert bits == (127 - r) << 7
+        assert torch.tensor([bits], dtype=torch.int32).to(torch.int16).view(torch.bfloat16).float().item() == 2.0 ** -r
+    assert torch.tensor([1.0]).to(torch.bfloat16).view(torch.int16).item() == 0x3F80
