@@ -31,7 +31,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--sf", type=float, default=float(os.environ.get("SDO_BENCH_SF", "100")))
+    ap.add_argument("--sf", type=float, default=float(os.environ.get("SDO_BENCH_SF", "100")),
+                    help="scale factor PER GPU (weak scaling: N GPUs hold N x SF)")
+    ap.add_argument("--total-sf", type=float, default=float(os.environ.get("SDO_BENCH_TOTAL_SF", "0")) or None,
+                    help="scale factor of the WHOLE job, split over the GPUs (strong scaling: the fixed-SF100 "
+                         "curve at 1/2/4/8 GPUs, or SF1000 over 8 GPUs = 125 per GPU)")
     ap.add_argument("--mode", choices=["sql", "spec"], default=os.environ.get("SDO_BENCH_MODE", "sql"))
     ap.add_argument("--model", choices=["tpch", "ssb", "tpch22"], default=os.environ.get("SDO_BENCH_MODEL", "tpch"),
                     help="tpch: the reference's 8-query TPC-H suite (headline); ssb: BASELINE config 4; "
@@ -51,6 +55,9 @@ def main():
     world = init_world()
     if world.size != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but the process group has {world.size} rank(s)")
+    strong = args.total_sf is not None
+    if strong:
+        args.sf = args.total_sf / world.size  # each rank generates its disjoint share of the total
     dev = world.device()
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
@@ -123,6 +130,12 @@ def main():
         if dev.type == "cuda":
             torch.cuda.synchronize()
 
+    from spark_druid_olap_amd.engine.executor import results_on_root
+
+    # rank 0 consumes the answers (df.collect() on the reference's driver): the final groups are
+    # gathered to rank 0 only and only rank 0 decodes them (engine/executor.py results_on_root)
+    ctx = results_on_root(os.environ.get("SDO_RESULTS_ON_ROOT", "1") != "0")
+    ctx.__enter__()
     lat = {name: [] for name, _ in queries}
     stats = {name: {} for name, _ in queries}
     for _ in range(args.warmup):
@@ -150,11 +163,15 @@ def main():
     sync()
     world.barrier()
     total_ms = (time.perf_counter() - tstart) * 1e3
+    ctx.__exit__(None, None, None)
     if prof is not None:
         import pstats
 
         prof.disable()
         pstats.Stats(prof, stream=sys.stderr).sort_stats("cumulative").print_stats(40)
+    if os.environ.get("SDO_BENCH_PER_RANK"):  # diagnostics: every rank's own means
+        print(f"[bench] rank {world.rank}: " + " ".join(f"{k[:12]}={sum(v) / len(v):.3f}" for k, v in lat.items()),
+              file=sys.stderr, flush=True)
     total_ms = world.max_float(total_ms)
     means = {k: world.max_float(sum(v) / len(v)) for k, v in lat.items()}
     geo = math.exp(sum(math.log(max(m, 1e-6)) for m in means.values()) / len(means))
@@ -180,6 +197,10 @@ def main():
             model = (f"TPC-H flattened orderLineItemPartSupplier, SF{args.sf:g} per GPU "
                      f"(SF{args.sf * world.size:g} total), Druid bench index")
             vs = round(geo / BASELINE_GEOMEAN_MS, 8)
+        total_sf = args.sf * world.size
+        if strong:
+            model = model.replace(f"SF{args.sf:g} per GPU (SF{total_sf:g} total)", f"SF{total_sf:g} total "
+                                  f"(SF{args.sf:g} per GPU)")
         out = {
             "metric": metric,
             "value": round(geo, 4),
@@ -189,13 +210,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(total_ms / args.steps, 4),
             "higher_is_better": False,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": vs,
             "dtype": "int64-exact-decimal/f64",
             "data": f"synthetic ({args.model.upper()} dbgen-like distributions, random dictionary values, generated on device)",
             "config": {"model": model,
                        "global_batch": nq, "seq_len": int(nrows), "parallelism": f"dp{world.size} (segment shards)",
-                       "queries": len(queries), "mode": args.mode,
+                       "queries": len(queries), "mode": args.mode, "scale_factor_total": total_sf,
+                       "scale_factor_per_gpu": args.sf,
                        "world": {"size": world.size, "backend": world.backend}},
             "qps": round(nq / (total_ms / 1e3), 3),
             "per_query_ms": {k: round(v, 4) for k, v in means.items()},

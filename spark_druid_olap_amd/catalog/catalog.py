@@ -216,7 +216,8 @@ class DruidCluster:
 
     def __init__(self):
         self.datasources: Dict[str, Any] = {}
-        self.generation = 0
+        self.generation = 0        # datasource registry (plan caches key on it)
+        self.meta_generation = 0   # discovery / metadata views
         self._lock = threading.Lock()
         self.discovery = None
         self.server_name = "gpu:0"
@@ -253,8 +254,13 @@ class DruidCluster:
         return ds
 
     def clear_cache(self, host: Optional[str] = None) -> None:
+        """Metadata changed (a discovery watch fired, or CLEAR DRUID CACHE): the ``d$*`` views must
+        be recomputed.  Only ``meta_generation`` moves: discovery events arrive asynchronously and
+        at different moments on different ranks, and plans of every rank must stay in lock-step
+        (preparing a pushed query issues collectives), so the registry ``generation`` that keys
+        the plan caches moves only with registrations, which every rank performs alike."""
         with self._lock:
-            self.generation += 1
+            self.meta_generation += 1
 
 
 class Catalog:

@@ -186,7 +186,9 @@ class PreparedScan:
         else:
             b.acc = torch.empty((rows, prog.nslots), dtype=torch.int64, device=dev)
         b.keys = torch.empty(rows if self.mode == D.M_HASH else 1, dtype=torch.int64, device=dev)
-        b.hll = [torch.empty(rows * self.m, dtype=torch.int32, device=dev) for _ in range(prog.nhll)]
+        # byte registers (sdo_device.h hll_update8 / hll_merge_word8): the partials, the wire and the
+        # estimator all read u8
+        b.hll = [torch.empty(rows * self.m, dtype=torch.uint8, device=dev) for _ in range(prog.nhll)]
         b.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
         b.touch = torch.zeros(((rows + 7) // 8 * 8) if self.touch else 8, dtype=torch.uint8, device=dev)
         b.clean = False
@@ -302,7 +304,7 @@ class PreparedScan:
         prog = self.prog
         acc = torch.empty((0, prog.nslots), dtype=torch.int64, device=self.dev)
         return Partials("sparse", acc, torch.zeros(0, dtype=torch.int64, device=self.dev),
-                        [torch.zeros((0, self.m), dtype=torch.int32, device=self.dev) for _ in range(prog.nhll)])
+                        [torch.zeros((0, self.m), dtype=torch.uint8, device=self.dev) for _ in range(prog.nhll)])
 
 
 class _Bufs:

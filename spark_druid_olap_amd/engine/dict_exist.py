@@ -29,17 +29,30 @@ from .partials import Partials
 _CHUNK = 1 << 27
 
 
+_OCC_LOCK = __import__("threading").Lock()
+
+
 def occurrence(ds, col: str) -> torch.Tensor:
-    """bool [C_col]: dictionary id occurs in this shard (cached on the datasource)."""
+    """bool [C_col]: dictionary id occurs in this shard (cached on the datasource).
+
+    Queries of the stream scheduler run on different HIP streams of one process: the bitmap is
+    published to the cache only after the producing stream finished its scatter, so a query on
+    another stream never reads a half-built table (it would drop keys from an existence group-by)."""
     cache = ds.__dict__.setdefault("_occurrence_cache", {})
     t = cache.get(col)
-    if t is None:
-        d = ds.dims[col]
-        t = torch.zeros(len(d.dictionary), dtype=torch.bool, device=d.ids.device)
-        n = ds.num_rows
-        for s0 in range(0, n, _CHUNK):  # (id columns are padded past num_rows)
-            t[d.ids[s0:min(n, s0 + _CHUNK)].to(torch.int64)] = True
-        cache[col] = t
+    if t is not None:
+        return t
+    with _OCC_LOCK:
+        t = cache.get(col)
+        if t is None:
+            d = ds.dims[col]
+            t = torch.zeros(len(d.dictionary), dtype=torch.bool, device=d.ids.device)
+            n = ds.num_rows
+            for s0 in range(0, n, _CHUNK):  # (id columns are padded past num_rows)
+                t[d.ids[s0:min(n, s0 + _CHUNK)].to(torch.int64)] = True
+            if t.is_cuda:
+                torch.cuda.current_stream(t.device).synchronize()
+            cache[col] = t
     return t
 
 

@@ -8,6 +8,8 @@ reference gets back from the Druid broker and post-processes in Spark
 """
 from __future__ import annotations
 
+import contextlib
+import contextvars
 import math
 import os
 import time
@@ -32,6 +34,25 @@ from .partials import Partials, finalize
 PIPELINE_MERGE = os.environ.get("SDO_PIPELINE_MERGE", "1") not in ("0", "")
 # existence-only group-bys over the key's dictionary domain (engine/dict_exist.py)
 DICT_EXIST = os.environ.get("SDO_DICT_EXIST", "1") not in ("0", "")
+
+# Multi-rank result placement.  Set (``results_on_root``) by callers that consume a statement's
+# result on rank 0 only -- the benchmark, the SPMD server answering its client: the final groups
+# are gathered to rank 0 alone and only rank 0 finalizes, decodes and copies them to the host; the
+# other ranks take part in every collective and return an empty result of the same schema.
+_ROOT_ONLY: contextvars.ContextVar = contextvars.ContextVar("sdo_results_on_root", default=False)
+
+
+@contextlib.contextmanager
+def results_on_root(flag: bool = True):
+    tok = _ROOT_ONLY.set(bool(flag))
+    try:
+        yield
+    finally:
+        _ROOT_ONLY.reset(tok)
+
+
+def root_only_results() -> bool:
+    return bool(_ROOT_ONLY.get())
 
 
 @dataclass
@@ -147,7 +168,7 @@ class PreparedQuery:
         its peers, so the failure can be agreed on inside the merge)."""
         part = self._placeholder_scan(prog, prep)
         m = 1 << prog.hll_p
-        extra = [torch.zeros((part.rows, m), dtype=torch.int32, device=self.ds.device)
+        extra = [torch.zeros((part.rows, m), dtype=torch.uint8, device=self.ds.device)
                  for _ in range(prog.nhll_total - len(part.hll))]
         return Partials(part.kind, part.acc, part.keys, list(part.hll) + extra) if extra else part
 
@@ -162,13 +183,13 @@ class PreparedQuery:
             if prep.mode == D_.M_HASH:
                 return prep._empty()
             return Partials("dense", _init_acc(prog, prog.G, dev), None,
-                            [torch.zeros((prog.G, m), dtype=torch.int32, device=dev) for _ in range(prog.nhll)])
+                            [torch.zeros((prog.G, m), dtype=torch.uint8, device=dev) for _ in range(prog.nhll)])
         if prog.G > (1 << 22):
             return Partials("sparse", torch.empty((0, prog.nslots), dtype=torch.int64, device=dev),
                             torch.zeros(0, dtype=torch.int64, device=dev),
-                            [torch.zeros((0, m), dtype=torch.int32, device=dev) for _ in range(prog.nhll)])
+                            [torch.zeros((0, m), dtype=torch.uint8, device=dev) for _ in range(prog.nhll)])
         return Partials("dense", _init_acc(prog, prog.G, dev), None,
-                        [torch.zeros((prog.G, m), dtype=torch.int32, device=dev) for _ in range(prog.nhll)])
+                        [torch.zeros((prog.G, m), dtype=torch.uint8, device=dev) for _ in range(prog.nhll)])
 
     def _scan(self, prog, prep) -> Partials:
         from ..parallel.fault import FAULTS
@@ -230,7 +251,7 @@ class PreparedQuery:
         hll = list(part.hll)
         for name, metric, filt in prog.stored_hll:
             sk = self.ds.metrics[metric].sketch
-            regs = torch.zeros((part.rows, m), dtype=torch.int32, device=dev)
+            regs = torch.zeros((part.rows, m), dtype=torch.uint8, device=dev)
             r, g = rows, slot
             if filt is not None and rows.numel():
                 keep = eval_bexpr(prog, filt, rows)
@@ -246,7 +267,7 @@ class PreparedQuery:
                 first = torch.repeat_interleave(lo - (torch.cumsum(cnt, 0) - cnt), cnt)
                 pk = sk.values[torch.arange(int(cnt.sum()), device=dev) + first].to(torch.int64)
                 flat = regs.view(-1)
-                flat.scatter_reduce_(0, gi * m + ((pk >> 8) & (m - 1)), (pk & 0xFF).to(torch.int32), reduce="amax")
+                flat.scatter_reduce_(0, gi * m + ((pk >> 8) & (m - 1)), (pk & 0xFF).to(torch.uint8), reduce="amax")
             hll.append(regs)
         return Partials(part.kind, part.acc, part.keys, hll)
 
@@ -264,9 +285,13 @@ class PreparedQuery:
         t0 = time.perf_counter()
         qt = self.qs.queryType
         if qt in ("groupBy", "timeseries", "topN"):
-            prog, part, t1 = self.run_partials(t0)
+            root_only = self.world.distributed and root_only_results()
+            prog, part, t1 = self.run_partials(t0, root_only)
             t2 = time.perf_counter()
             with T.span("sdo.finalize"):
+                if root_only and self.world.rank != 0:
+                    # a peer: the root answers; finalize an empty slice (host only: the schema)
+                    part = empty_partials(prog, torch.device("cpu"))
                 cols = finalize(prog, part, getattr(self, "out_types", None))
             t3 = time.perf_counter()
             with T.span("sdo.post"):
@@ -283,9 +308,13 @@ class PreparedQuery:
         self.last_stats = res.stats
         return res
 
-    def run_partials(self, t0: float):
+    def run_partials(self, t0: float, root_only: bool = False):
         """scan -> merge across ranks -> device HAVING / top-K pruning; (prog, merged partials,
-        scan end time).  The partials stay on the device (nested queries consume them there)."""
+        scan end time).  The partials stay on the device (nested queries consume them there).
+
+        Across ranks, sparse partials are merged into disjoint per-rank slices first; HAVING and the
+        top-K prune run on every slice (distributed), and only the survivors are gathered -- to
+        rank 0 alone with ``root_only`` (the other ranks then hold an empty slice)."""
         from ..utils.cancel import checkpoint
 
         _, prog, prep = self.scans[0]
@@ -317,9 +346,17 @@ class PreparedQuery:
         t1 = time.perf_counter()
         disjoint = bool(self.ds.shard_key) and any(k.col == self.ds.shard_key for k in prog.keys)
         with T.span("sdo.merge"):
-            part = merge_partials(self.world, prog, part, disjoint_keys=disjoint, local_error=err)
+            part = merge_partials(self.world, prog, part, disjoint_keys=disjoint, local_error=err,
+                                  finish="local" if self.world.distributed else "all")
         part, hv = self._device_having(prog, part)
         part = self._device_prune(prog, part, hv)
+        if part.scattered:
+            from ..parallel.merge import gather_groups
+
+            with T.span("sdo.gather"):
+                part = gather_groups(self.world, part, root_only, part.status, err)
+            if self.world.rank == 0 or not root_only:
+                part = self._device_prune(prog, part, hv)  # the union of per-slice supersets
         return prog, part, t1
 
     def _run_pipelined(self, prog):
@@ -426,7 +463,7 @@ class PreparedQuery:
             return part, False
         keep = torch.nonzero(mask).flatten()
         return Partials("sparse", part.acc.index_select(0, keep), part.keys.index_select(0, keep),
-                        [x.index_select(0, keep) for x in part.hll]), True
+                        [x.index_select(0, keep) for x in part.hll], part.scattered, part.status), True
 
     def _device_prune(self, prog: ScanProgram, part: Partials, having_done: bool = True) -> Partials:
         """ORDER BY <aggregate> LIMIT k (groupBy limitSpec) and numeric topN, applied to the merged
@@ -470,7 +507,7 @@ class PreparedQuery:
             kth = torch.topk(key, limit, sorted=False).values.min()
             keep = torch.nonzero(key >= kth).flatten()
         return Partials("sparse", part.acc.index_select(0, keep), part.keys.index_select(0, keep),
-                        [h.index_select(0, keep) for h in part.hll])
+                        [h.index_select(0, keep) for h in part.hll], part.scattered, part.status)
 
     # ------------------------------------------------------------------ theta sketches
     def _theta(self, prog: ScanProgram, cols: Dict[str, np.ndarray]) -> None:
@@ -703,7 +740,7 @@ class ShardWindow:
         m = 1 << self.glob.hll_p
         return Partials("sparse", torch.empty((0, self.glob.nslots), dtype=torch.int64, device=dev),
                         torch.zeros(0, dtype=torch.int64, device=dev),
-                        [torch.zeros((0, m), dtype=torch.int32, device=dev) for _ in range(self.glob.nhll)])
+                        [torch.zeros((0, m), dtype=torch.uint8, device=dev) for _ in range(self.glob.nhll)])
 
     def to_global(self, part: Partials) -> Partials:
         sp = part.compact()
@@ -761,6 +798,14 @@ def shard_window(prog: ScanProgram, ds: DataSource, world: World) -> Optional[Sh
 
     local = dataclasses.replace(prog, keys=keys, G=G)
     return ShardWindow(prog, local)
+
+
+def empty_partials(prog: ScanProgram, dev) -> Partials:
+    """No groups, in the program's layout (a peer's share of a result answered on rank 0)."""
+    m = 1 << prog.hll_p
+    return Partials("sparse", torch.empty((0, prog.nslots), dtype=torch.int64, device=dev),
+                    torch.zeros(0, dtype=torch.int64, device=dev),
+                    [torch.zeros((0, m), dtype=torch.uint8, device=dev) for _ in range(prog.nhll_total)])
 
 
 def _init_acc(prog: ScanProgram, rows: int, dev) -> torch.Tensor:
@@ -1126,7 +1171,10 @@ def execute_grouping_sets(engine, specs, ds, out_types=None) -> Optional[List[Qu
     if fine.thetas or fine.stored_hll or fine.derived_aggs or any(kc.collapse for kc in fine.keys):
         return None
     t0 = time.perf_counter()
-    prog, part, _ = pq.run_partials(t0)
+    root_only = engine.world.distributed and root_only_results()
+    prog, part, _ = pq.run_partials(t0, root_only)
+    if root_only and engine.world.rank != 0:
+        part = empty_partials(prog, torch.device("cpu"))  # rank 0 answers every set
     fp = part.compact()
     g = fp.keys.to(torch.int64)
     from .partials import merge_sparse

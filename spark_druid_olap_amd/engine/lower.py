@@ -247,6 +247,12 @@ class KeyComp:
     orig: Optional[np.ndarray] = None  # compacted key: key id -> original dictionary id
     col_idx: int = -1             # descriptor column index (payload section)
     dictionary: Any = None        # plain dictionary-id key: its dictionary (device-side typed decode)
+    # K_TIME over a coarse time unit (days): the key of every raw time value of the cluster-wide
+    # data span, precomputed (``Lowerer._attach_time_lut``) -- the JIT kernel gathers
+    # ``tlut[v - tlut_lo]`` instead of running the calendar arithmetic (civil_from_days: several
+    # 64-bit divisions) for all 64 lanes of every word a filter leaves non-empty
+    tlut: Optional[np.ndarray] = None
+    tlut_lo: int = 0
 
 
 @dataclass
@@ -915,6 +921,7 @@ class Lowerer:
         else:
             a, b = joda.field_domain(tf)
             kc.base, kc.card = a, b - a + 1
+        self._attach_time_lut(kc)
         base, tfv = kc.base, tf
         if fn is None:
             kc.decoder = lambda ids: np.array([bucket_start_from_value(int(i) + base, tfv) for i in ids], dtype=np.int64)
@@ -929,6 +936,29 @@ class Lowerer:
             kc.decoder = lambda ids: np.array([f(bucket_start_from_value(int(i) + base, tfv)) for i in ids], dtype=object)
             kc.collapse = True
         return kc
+
+    TIME_LUT_MAX = 1 << 16
+
+    def _attach_time_lut(self, kc: KeyComp) -> None:
+        """Key table over the raw time values of the cluster-wide data span (identical on every
+        rank), when the storage unit is coarse enough for it to stay small (days: ~2,600 entries
+        for TPC-H).  Values are the reference executor's own (ops/reference.py _time_field), so
+        the LUT and the arithmetic paths agree bit for bit; out-of-span values clamp like the key."""
+        ds = self.ds
+        u = int(ds.time_unit_ms)
+        if u < 1000:
+            return
+        lo, hi = self._data_span([])
+        v0, v1 = lo // u, (hi - 1) // u
+        span = v1 - v0 + 1
+        if span <= 0 or span > self.TIME_LUT_MAX:
+            return
+        from ..ops.reference import _time_field
+
+        vals = torch.arange(v0, v1 + 1, dtype=torch.int64)
+        t = (_time_field(vals * u, kc) - kc.base).clamp(0, max(0, kc.card - 1))
+        kc.tlut = t.numpy().astype(np.int32)
+        kc.tlut_lo = int(v0)
 
     def _unit_field(self) -> int:
         from ..query.granularity import T_DAY, T_MS, T_SECOND
@@ -958,6 +988,7 @@ class Lowerer:
         b1 = bucket_value(hi - 1 + g.tz_ms, tf, p, o)
         kc = KeyComp("timestamp", D.K_TIME, TIME, max(1, b1 - b0 + 1), base=b0, tfield=tf, tz_ms=g.tz_ms,
                      period_ms=p, origin_ms=o, is_timestamp=True)
+        self._attach_time_lut(kc)
         kc.decoder = lambda ids: np.array([bucket_start_from_value(int(i) + b0, tf, p, o) - g.tz_ms for i in ids],
                                           dtype=np.int64)
         return kc
@@ -1786,10 +1817,11 @@ def pack(prog: ScanProgram, mode: int, dedup: int, hll_lds: int, lds_bytes: int,
         k["stride"], k["base"], k["card"] = kc.stride, kc.base, kc.card
         k["unit_ms"] = ds.time_unit_ms
         k["tz_ms"], k["period_ms"], k["origin_ms"] = kc.tz_ms, kc.period_ms or 1, kc.origin_ms
-        if kc.remap is not None:
+        table = kc.remap if kc.remap is not None else (kc.tlut if kc.kind == D.K_TIME else None)
+        if table is not None:
             t = getattr(kc, "_remap_dev", None)
             if t is None or t.device != ds.device:
-                t = torch.from_numpy(kc.remap).to(ds.device)
+                t = torch.from_numpy(table).to(ds.device)
                 kc._remap_dev = t  # type: ignore[attr-defined]
             prog.keepalive.append(t)
             k["remap"] = t.data_ptr()

@@ -18,7 +18,12 @@ class Partials:
     kind: str                        # dense | sparse
     acc: torch.Tensor                # [R, nslots] int64 (f64 slots hold bit patterns)
     keys: Optional[torch.Tensor]     # [R] int64 (sparse)
-    hll: List[torch.Tensor] = field(default_factory=list)  # [R, m] int32 each
+    hll: List[torch.Tensor] = field(default_factory=list)  # [R, m] uint8 byte registers each
+    # multi-rank: this rank holds a DISJOINT slice of the final groups (after the shuffle, or when
+    # grouped on the shard key); parallel/merge.py gather_groups concatenates the slices, carrying
+    # ``status`` (this rank's failure word, parallel/fault.py) in that collective
+    scattered: bool = False
+    status: int = 0
 
     @property
     def rows(self) -> int:
@@ -34,7 +39,8 @@ class Partials:
             idx = native.nonzero_rows(self.acc[:, 0])  # ballot mask + compact_rows kernels
         else:
             idx = torch.nonzero(self.acc[:, 0] > 0).flatten()
-        return Partials("sparse", self.acc.index_select(0, idx), idx, [h.index_select(0, idx) for h in self.hll])
+        return Partials("sparse", self.acc.index_select(0, idx), idx, [h.index_select(0, idx) for h in self.hll],
+                        self.scattered, self.status)
 
 
 def merge_sparse(parts: List[Partials], slots) -> Partials:
@@ -61,11 +67,11 @@ def merge_sparse(parts: List[Partials], slots) -> Partials:
         out[:, s] = col
     hll = []
     for i in range(len(parts[0].hll)):
-        h = torch.cat([p.hll[i] for p in parts]).to(torch.int64)
+        h = torch.cat([p.hll[i] for p in parts])
         m = h.shape[1]
-        o = torch.zeros((R, m), dtype=torch.int64, device=acc.device)
+        o = torch.zeros((R, m), dtype=h.dtype, device=acc.device)
         o.scatter_reduce_(0, inv.unsqueeze(1).expand(-1, m), h, reduce="amax", include_self=True)
-        hll.append(o.to(torch.int32))
+        hll.append(o)
     return Partials("sparse", out, uk, hll)
 
 
@@ -358,10 +364,10 @@ def finalize(prog, parts: Partials, out_types: Optional[Dict[str, str]] = None) 
         inv_t = torch.from_numpy(inv)
         new_hll = []
         for h in hll_d:
-            hc = h.cpu().to(torch.int64)
-            o = torch.zeros((R, hc.shape[1]), dtype=torch.int64)
+            hc = h.cpu()
+            o = torch.zeros((R, hc.shape[1]), dtype=hc.dtype)
             o.scatter_reduce_(0, inv_t.unsqueeze(1).expand(-1, hc.shape[1]), hc, reduce="amax", include_self=True)
-            new_hll.append(o.to(torch.int32))
+            new_hll.append(o)
         keys_first = [None] * R
         for t, i in uniq.items():
             keys_first[i] = t

@@ -18,7 +18,7 @@ template <int U>
 __global__ void olap_scan_kernel(const ScanDesc* __restrict__ d);
 __global__ void bitmap_build_kernel(const void* ids, int dtype, int64_t n, int64_t nwords, uint64_t* out,
                                     int64_t card);
-__global__ void hll_estimate_kernel(const uint32_t* regs, int64_t G, int p, double* est);
+__global__ void hll_estimate_kernel(const unsigned char* regs, int64_t G, int p, double* est);
 __global__ void glds_probe_kernel(const unsigned char* src, uint32_t* out);
 // post_scan.hip
 __global__ void compact_count_kernel(const uint64_t* mask, int64_t nwords, int* block_counts);
@@ -47,7 +47,7 @@ __global__ void topk_keep_kernel(const int64_t* acc, int64_t n, int nslots, int 
 // sketch.hip
 __global__ void hll_pairs_kernel(const int64_t* vals, int64_t n, int p, int64_t salt, int32_t* out);
 __global__ void hll_merge_stored_kernel(const int64_t* rows, const int64_t* gid, int64_t nsel, const int64_t* offsets,
-                                        const int32_t* pairs, int p, int64_t G, int32_t* regs);
+                                        const int32_t* pairs, int p, int64_t G, unsigned char* regs);
 }  // namespace sdo
 
 namespace py = pybind11;
@@ -91,7 +91,7 @@ static void hll_estimate(uint64_t regs, int64_t G, int p, uint64_t est, uint64_t
   if (p < 7) throw std::invalid_argument("hll estimate needs >= 128 registers (128-register column chunks)");
   const unsigned blocks = (unsigned)((G + 31) / 32);
   hipLaunchKernelGGL(sdo::hll_estimate_kernel, dim3(blocks), dim3(8 * 64), 0, (hipStream_t)stream,
-                     (const uint32_t*)regs, G, p, (double*)est);
+                     (const unsigned char*)regs, G, p, (double*)est);
   check(hipGetLastError(), "hll_estimate_kernel launch");
 }
 
@@ -118,7 +118,7 @@ static void hll_merge_stored(uint64_t rows, uint64_t gid, int64_t nsel, uint64_t
   if (p < 4 || p > 18) throw std::invalid_argument("hll precision out of range");
   hipLaunchKernelGGL(sdo::hll_merge_stored_kernel, dim3(grid_for(nsel, 256, 65536)), dim3(256), 0,
                      (hipStream_t)stream, (const int64_t*)rows, (const int64_t*)gid, nsel, (const int64_t*)offsets,
-                     (const int32_t*)pairs, p, G, (int32_t*)regs);
+                     (const int32_t*)pairs, p, G, (unsigned char*)regs);
   check(hipGetLastError(), "hll_merge_stored_kernel launch");
 }
 

@@ -630,9 +630,12 @@ __global__ __launch_bounds__(512) void olap_scan_kernel(const ScanDesc* __restri
               uint32_t bucket, rho;
               dev::hll_bucket_rho(v, ao.salt, hll_p, bucket, rho);
               const int64_t idx = slot[u] * hll_m + bucket;
-              uint32_t* r = (mode == M_DENSE_LDS && d->hll_lds) ? (uint32_t*)(lds + ao.hll_lds_off) + idx
-                                                                 : (uint32_t*)ao.hll_regs + idx;
-              if (rho > *(volatile uint32_t*)r) atomicMax(r, rho);  // saturated registers: skip the atomic
+              if (mode == M_DENSE_LDS && d->hll_lds) {
+                uint32_t* r = (uint32_t*)(lds + ao.hll_lds_off) + idx;
+                if (rho > *(volatile uint32_t*)r) atomicMax(r, rho);  // saturated registers: skip the atomic
+              } else {
+                dev::hll_max8((unsigned char*)ao.hll_regs, (uint64_t)idx, rho);  // global byte registers
+              }
             }
           }
           continue;
@@ -704,11 +707,13 @@ __global__ __launch_bounds__(512) void olap_scan_kernel(const ScanDesc* __restri
       for (int a = 0; a < d->naggs; ++a) {
         const AOp ao = d->aops[a];
         if (ao.kind != A_HLL) continue;
+        // u32 LDS registers (interpreter layout) -> four packed global byte registers per dword
         const uint32_t* rr = (const uint32_t*)(lds + ao.hll_lds_off);
         uint32_t* g = (uint32_t*)ao.hll_regs;
-        for (int64_t i = threadIdx.x; i < G * hll_m; i += blockDim.x) {
-          const uint32_t v = rr[i];
-          if (v > *(volatile uint32_t*)(g + i)) atomicMax(g + i, v);
+        for (int64_t i = threadIdx.x; i < G * hll_m / 4; i += blockDim.x) {
+          const uint32_t v = min(rr[4 * i], 255u) | (min(rr[4 * i + 1], 255u) << 8) |
+                             (min(rr[4 * i + 2], 255u) << 16) | (min(rr[4 * i + 3], 255u) << 24);
+          dev::hll_merge_word8(g + i, v);
         }
       }
     }
@@ -767,20 +772,28 @@ __global__ __launch_bounds__(256) void bitmap_build_kernel(const void* ids, int 
 }
 
 // ---------------------------------------------------------------------------------------------
-// HyperLogLog finalize for G groups x m registers: sum(2^-M) and zero counts per group.
+// HyperLogLog finalize for G groups x m byte registers: sum(2^-M) and zero counts per group.
 // The register matrix is multiplied by a ones vector on the matrix cores (MFMA 32x32x16 bf16, f32
-// accumulate: A = 2^-M tile [32 groups x 16 regs], exact in bf16 for M <= 126, B = e0) -- the batched sketch reduction of the
-// BASELINE north-star.  Each wave owns 128-register column chunks of a 32-group row block: the
-// chunk is read with 16 independent, fully coalesced 16-byte loads per lane (one memory round trip,
-// not one per MFMA step), packed to bytes in a wave-private LDS tile (rho <= 65), and the MFMA
-// steps read it as 8-byte rows with a 136-byte pitch (the 32 rows' dword pairs cover all 64 banks).
-// Partial column-0 sums of the HLL_EST_WAVES waves meet in LDS.
+// accumulate: A = 2^-M tile [32 groups x 16 regs], exact in bf16 -- a power of two, bits
+// (127 - M) << 7 -- for M <= 126; registers are clamped to 127 on the way into the tile, whose 2^-127
+// encodes as bf16 zero, a negligible term, so no register value can spill into the sign/exponent
+// bits; B = e0) -- the batched sketch reduction of the BASELINE north-star.  Each wave owns 128-
+// register column chunks of a 32-group row block: the 4 KiB chunk is read with 4 independent, fully
+// coalesced 16-byte loads per lane (one memory round trip, not one per MFMA step), copied into a
+// wave-private LDS tile, and the MFMA steps read it as 8-byte rows with a 136-byte pitch (the 32
+// rows' dword pairs cover all 64 banks).  Partial column-0 sums of the HLL_EST_WAVES waves meet in LDS.
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr int HLL_EST_WAVES = 8, HLL_EST_CH = 128, HLL_EST_PITCH = HLL_EST_CH + 8;
-__global__ __launch_bounds__(HLL_EST_WAVES * 64) void hll_estimate_kernel(const uint32_t* regs, int64_t G, int p,
-                                                                          double* est) {
+
+__device__ __forceinline__ uint32_t clamp127_u8x4(uint32_t x) {
+  const uint32_t m = ((x & 0x80808080u) >> 7) * 0xffu;  // 0xff in every byte >= 128
+  return (x & ~m) | (0x7f7f7f7fu & m);
+}
+
+__global__ __launch_bounds__(HLL_EST_WAVES * 64) void hll_estimate_kernel(const unsigned char* regs, int64_t G,
+                                                                          int p, double* est) {
   __shared__ __attribute__((aligned(16))) unsigned char tiles[HLL_EST_WAVES][32 * HLL_EST_PITCH];
   __shared__ float part[HLL_EST_WAVES][2][32];
   const int lane = threadIdx.x & 63;
@@ -795,25 +808,24 @@ __global__ __launch_bounds__(HLL_EST_WAVES * 64) void hll_estimate_kernel(const 
   const uint32_t one = i == 0 ? 0x3f803f80u : 0u;  // B = e0 columns: 1.0 bf16 pairs in column 0
   const bf16x8 bsel = __builtin_bit_cast(bf16x8, u32x4{one, one, one, one});
   for (int64_t c0 = (int64_t)wave * HLL_EST_CH; c0 < m; c0 += HLL_EST_WAVES * HLL_EST_CH) {
-    uint4 x[16];  // 32 rows x 32 uint4 = the chunk; lane takes vectors lane, lane+64, ...
+    uint4 x[4];  // 32 rows x 8 uint4 (16 registers each) = the chunk; lane takes vectors lane, lane+64, ..
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < 4; ++j) {
       const int v = j * 64 + lane;
-      const int64_t g = g0 + (v >> 5);
-      x[j] = g < G ? *(const uint4*)(regs + g * m + c0 + (v & 31) * 4) : make_uint4(0u, 0u, 0u, 0u);
+      const int64_t g = g0 + (v >> 3);
+      x[j] = g < G ? *(const uint4*)(regs + g * m + c0 + (v & 7) * 16) : make_uint4(0u, 0u, 0u, 0u);
     }
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < 4; ++j) {
       const int v = j * 64 + lane;
-      const uint32_t b = min(x[j].x, 255u) | (min(x[j].y, 255u) << 8) | (min(x[j].z, 255u) << 16) |
-                         (min(x[j].w, 255u) << 24);
-      *(uint32_t*)(tile + (v >> 5) * HLL_EST_PITCH + (v & 31) * 4) = b;
+      uint2* dst = (uint2*)(tile + (v >> 3) * HLL_EST_PITCH + (v & 7) * 16);  // 8-byte aligned rows
+      dst[0] = make_uint2(clamp127_u8x4(x[j].x), clamp127_u8x4(x[j].y));
+      dst[1] = make_uint2(clamp127_u8x4(x[j].z), clamp127_u8x4(x[j].w));
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private tile: writes land before reads
 #pragma unroll
     for (int kb = 0; kb < HLL_EST_CH; kb += 16) {
-      // A[i][k] for k = kb + 8 * kk .. +7: 8 byte registers -> 2^-M and (M == 0) as exact bf16 (powers
-      // of two: bf16 bits (127 - M) << 7)
+      // A[i][k] for k = kb + 8 * kk .. +7: 8 byte registers -> 2^-M and (M == 0) as exact bf16
       const uint64_t rb = *(const uint64_t*)(tile + i * HLL_EST_PITCH + kb + kk * 8);
       u32x4 pa, pz;
 #pragma unroll

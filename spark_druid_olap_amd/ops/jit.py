@@ -401,7 +401,7 @@ class _Gen:
         for j, (row, stride, count) in enumerate(p.bm_leaves):
             L.append(f"  const uint64_t* bm{j} = (const uint64_t*)d->bm_bits[{j}];")
         for k, kc in enumerate(p.keys):
-            if kc.kind == D.K_REMAP:
+            if kc.kind == D.K_REMAP or (kc.kind == D.K_TIME and getattr(kc, "tlut", None) is not None):
                 L.append(f"  const int32_t* rm{k} = (const int32_t*)d->kops[{k}].remap;")
         for z in range(len(p.zones)):
             L.append(f"  const int32_t* zmin{z} = (const int32_t*)d->zones[{z}].zmin;")
@@ -411,7 +411,7 @@ class _Gen:
                 if self.hll_lds and mode == D.M_DENSE_LDS:
                     L.append(f"  unsigned char* hll{ai} = lds + {lay.hll_off + a['hll'] * G * self.m};")
                 else:
-                    L.append(f"  uint32_t* hll{ai} = (uint32_t*)d->aops[{ai}].hll_regs;")
+                    L.append(f"  unsigned char* hll{ai} = (unsigned char*)d->aops[{ai}].hll_regs;")
         stage = []
         body = stage
         # ---------------- per-word processing
@@ -444,6 +444,11 @@ class _Gen:
                 body.append(f"        key += (uint64_t)({v}) * {kc.stride}ull;")
             elif kc.kind == D.K_REMAP:
                 body.append(f"        key += (uint64_t)rm{k}[{v}] * {kc.stride}ull;")
+            elif kc.kind == D.K_TIME and getattr(kc, "tlut", None) is not None:
+                n = len(kc.tlut)  # precomputed key per raw time value (engine/lower.py _attach_time_lut)
+                body.append(f"        {{ int64_t i_ = (int64_t)({v}) - {_lit(kc.tlut_lo)};")
+                body.append(f"          i_ = i_ < 0 ? 0 : (i_ >= {n} ? {n - 1} : i_);")
+                body.append(f"          key += (uint64_t)rm{k}[i_] * {kc.stride}ull; }}")
             elif kc.kind == D.K_TIME:
                 body.append(f"        {{ int64_t t = time_field_t<{kc.tfield}>(({v}) * {_lit(p.ds.time_unit_ms)} + "
                             f"{_lit(kc.tz_ms)}, {_lit(kc.period_ms or 1)}, {_lit(kc.origin_ms)}) - {_lit(kc.base)};")
@@ -492,8 +497,7 @@ class _Gen:
             kind = a["kind"]
             val = f"v{ai}_[u]"
             if kind == D.A_HLL:
-                fn = "hll_update8" if self.hll_lds and mode == D.M_DENSE_LDS else "hll_update"
-                body.append(f"        if ({cond}) {fn}(hll{ai}, slot, {p.hll_p}, {val}, {_lit(a.get('salt', 0))});")
+                body.append(f"        if ({cond}) hll_update8(hll{ai}, slot, {p.hll_p}, {val}, {_lit(a.get('salt', 0))});")
                 continue
             s = a["slot"]
             op = p.slots[s][0]
@@ -691,11 +695,11 @@ class _Gen:
                 for ai, a in enumerate(p.aops):
                     if a["kind"] != D.A_HLL:
                         continue
+                    # four byte registers per dword: one read (and rarely a CAS) per 4 registers
                     out.append(f"  {{ uint32_t* g = (uint32_t*)d->aops[{ai}].hll_regs;")
-                    out.append(f"    for (int i = threadIdx.x; i < {G * self.m}; i += {W * 64}) {{")
-                    out.append(f"      const uint32_t v = hll{ai}[i];  // byte register")
-                    out.append("      if (v > *(volatile uint32_t*)(g + i)) atomicMax(g + i, v);")
-                    out.append("    } }")
+                    out.append(f"    const uint32_t* r = (const uint32_t*)hll{ai};")
+                    out.append(f"    for (int i = threadIdx.x; i < {G * self.m // 4}; i += {W * 64}) hll_merge_word8(g + i, r[i]);")
+                    out.append("  }")
         out.append("}")
         return "\n".join(out) + "\n"
 

@@ -99,7 +99,7 @@ def bitmap_build(ids: torch.Tensor, num_rows: int, out: torch.Tensor, card: int)
 
 def hll_estimate(regs: torch.Tensor, G: int, p: int, est: torch.Tensor) -> None:
     m = load()
-    assert regs.dtype == torch.int32 and regs.is_contiguous() and regs.numel() >= G * (1 << p)
+    assert regs.dtype == torch.uint8 and regs.is_contiguous() and regs.numel() >= G * (1 << p)
     assert est.dtype == torch.float64 and est.numel() >= G
     m.hll_estimate(regs.data_ptr(), int(G), int(p), est.data_ptr(), _stream(regs.device))
 
@@ -204,10 +204,10 @@ def hll_pairs(vals: torch.Tensor, p: int, salt: int) -> torch.Tensor:
 def hll_merge_stored(regs: torch.Tensor, rows: torch.Tensor, gid: torch.Tensor, offsets: torch.Tensor,
                      pairs: torch.Tensor, p: int) -> None:
     """Union the stored sparse HLL sketches of ``rows`` into ``regs[gid[i]]`` (sketch.hip
-    hll_merge_stored); ``regs`` is [G, 2^p] int32, gid < 0 skips a row."""
+    hll_merge_stored); ``regs`` is [G, 2^p] uint8 (byte registers), gid < 0 skips a row."""
     m = load()
     G = regs.shape[0]
-    assert regs.dtype == torch.int32 and regs.is_contiguous() and regs.shape[1] == (1 << p) and regs.is_cuda
+    assert regs.dtype == torch.uint8 and regs.is_contiguous() and regs.shape[1] == (1 << p) and regs.is_cuda
     assert rows.dtype == torch.int64 and gid.dtype == torch.int64 and rows.numel() == gid.numel()
     assert offsets.dtype == torch.int64 and pairs.dtype == torch.int32
     if rows.numel():

@@ -382,7 +382,7 @@ def run_reference(prog, sparse: Optional[bool] = None):
         bucket, rho = hll_update_values(v, a.get("salt", 0), prog.hll_p)
         regs = torch.zeros(R * m, dtype=torch.int64, device=dev)
         regs.scatter_reduce_(0, ix * m + bucket, rho, reduce="amax", include_self=True)
-        hlls.append(regs.view(R, m).to(torch.int32))
+        hlls.append(regs.view(R, m).to(torch.uint8))  # byte registers, like the scan kernels
     if sparse:
         return Partials("sparse", acc, uk, hlls)
     return Partials("dense", acc, None, hlls)

@@ -4,18 +4,23 @@ final aggregate, ``asd/PostAggregate.scala:39-103``, re-designed for RCCL over x
 The path is the cost model's (``planner/cost.py plan_merge``), priced from the state's layout:
 
 * Small dense states (the common OLAP case: Q1 is 6 groups) are latency-bound: ONE
-  ``all_gather_into_tensor`` of the packed state (accumulators + HLL registers as int64 words)
-  followed by a local per-slot reduction -- one collective instead of one per reduce-op.
+  ``all_gather_into_tensor`` of the packed state (accumulators as 8-byte words, HLL registers as
+  the bytes they are, the status word) followed by a local per-slot reduction -- one collective
+  instead of one per reduce-op.
 * Large dense states use bandwidth-optimal ring ``all_reduce`` over at most three buckets (int
-  sums + status word, float sums, max + bitwise-NOT(min)) with one host sync at the end; HLL
-  registers reduce with MAX -- mergeable sketches, which the reference could not merge across
-  historicals, ``asd/PostAggregate.scala:62-70``.
+  sums + status word, float sums, max + bitwise-NOT(min)) plus ONE u8 MAX all-reduce of every HLL
+  register block, with one host sync at the end -- mergeable sketches, which the reference could
+  not merge across historicals, ``asd/PostAggregate.scala:62-70``.
 * Sparse (hash) states are compacted per GPU and shuffled by key hash with one
-  ``all_to_all_single`` (the reference's hash-partitioned Exchange before Spark's final aggregate,
-  ``asd/PostAggregate.scala:97-103``): each rank receives ~1/N of the partial rows, merges its key
-  range locally, and only the merged (now disjoint) groups are gathered.  When the datasource is
-  partitioned on a grouping key the groups are already disjoint across ranks and the merge
-  degenerates to a concatenation (no shuffle).
+  ``all_to_all_single`` of packed rows (key, accumulators, register bytes; the reference's
+  hash-partitioned Exchange before Spark's final aggregate, ``asd/PostAggregate.scala:97-103``):
+  each rank receives ~1/N of the partial rows and merges its key range locally.  When the
+  datasource is partitioned on a grouping key the groups are already disjoint and there is no
+  shuffle.  Either way every rank then holds a DISJOINT slice of the final groups
+  (``Partials.scattered``): HAVING and top-k pruning run there, distributed, and only the
+  survivors travel -- to rank 0 alone when the caller only needs the result on the root
+  (``gather_groups``), the reference's final aggregate collecting in one place
+  (``asd/PostAggregate.scala:97-103``).
 """
 from __future__ import annotations
 
@@ -27,7 +32,6 @@ from ..engine.partials import Partials, merge_sparse
 from ..ops import desc as D
 from .fault import STATUS_FAILED, STATUS_OK, raise_if_failed
 from .world import World
-
 
 
 def _reduce_stacked(prog, acc_all: torch.Tensor) -> torch.Tensor:
@@ -46,15 +50,21 @@ def _reduce_stacked(prog, acc_all: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def _u8(h: torch.Tensor) -> torch.Tensor:
+    """HLL registers as bytes (rho <= 65): placeholders and host-built blocks may be wider ints."""
+    return h if h.dtype == torch.uint8 else h.clamp(0, 255).to(torch.uint8)
+
+
 def _merge_dense_bucketed(world: World, prog, part: Partials, status: int,
                           local_error: Optional[BaseException]) -> Partials:
     """Large dense state: at most three ring all-reduces (each per-xGMI-link bandwidth bound) plus
-    one per HLL register block, with ONE host synchronisation after all of them were enqueued.
+    one for all HLL register blocks, with ONE host synchronisation after all of them were enqueued.
 
     * int sums + the status word (sum of the ranks' statuses is non-zero iff one failed);
     * float64 sums;
     * int max slots and the bitwise NOT of int min slots (``min x == ~max ~x``, no overflow at
-      INT64_MIN unlike negation), so min and max share one MAX collective.
+      INT64_MIN unlike negation), so min and max share one MAX collective;
+    * every HLL register block as one u8 MAX.
     A failed rank contributes a layout-compatible placeholder, so every rank issues the same
     collectives in the same order and then raises together (parallel/fault.py)."""
     merged, sts = start_dense_merge(world, prog, part, status, "bucketed-allreduce").wait()
@@ -84,23 +94,28 @@ def start_dense_merge(world: World, prog, part: Partials, status: int, kind: Opt
     all-reduce) without waiting: segment-batched execution starts batch j's merge and scans batch
     j+1 while it runs (``PreparedQuery._run_pipelined``)."""
     kind = kind or merge_plan_for(world, part).kind
+    hll = [_u8(h) for h in part.hll]
+    dev = part.acc.device
     if kind == "oneshot-allgather":
         R, ns = part.acc.shape
-        st = torch.full((1,), status, dtype=torch.int64, device=part.acc.device)
-        pieces = [part.acc.reshape(-1)] + [h.reshape(-1).to(torch.int64) for h in part.hll] + [st]
-        pend = world.all_gather_tensor_async(torch.cat(pieces))  # [ranks, L]
-        shapes = [h.shape for h in part.hll]
+        # one byte buffer per rank: accumulators (8-byte words), register bytes, status word
+        st = torch.full((1,), status, dtype=torch.int64, device=dev)
+        pieces = [part.acc.contiguous().view(torch.uint8).reshape(-1)] + [h.reshape(-1) for h in hll] + \
+            [st.view(torch.uint8)]
+        pend = world.all_gather_tensor_async(torch.cat(pieces))  # [ranks, L] uint8
+        shapes = [h.shape for h in hll]
 
         def finish_gather():
             g = pend.wait()
-            acc = _reduce_stacked(prog, g[:, : R * ns].reshape(world.size, R, ns))
-            off = R * ns
-            hll = []
+            na = R * ns * 8
+            acc = _reduce_stacked(prog, g[:, :na].contiguous().view(torch.int64).reshape(world.size, R, ns))
+            off = na
+            regs = []
             for shp in shapes:
                 n = shp.numel()
-                hll.append(g[:, off: off + n].amax(dim=0).to(torch.int32).reshape(shp))
+                regs.append(g[:, off: off + n].amax(dim=0).reshape(shp))
                 off += n
-            return Partials("dense", acc, None, hll), g[:, -1]
+            return Partials("dense", acc, None, regs), g[:, off:].contiguous().view(torch.int64).reshape(-1)
 
         return DenseMerge(finish_gather)
     acc = part.acc.clone()
@@ -108,18 +123,20 @@ def start_dense_merge(world: World, prog, part: Partials, status: int, kind: Opt
     by_op = {op: [s for s, (o, _) in enumerate(prog.slots) if o == op]
              for op in (D.S_SUM_I, D.S_SUM_F, D.S_MIN_I, D.S_MAX_I)}
     si, sf, mn, mx = by_op[D.S_SUM_I], by_op[D.S_SUM_F], by_op[D.S_MIN_I], by_op[D.S_MAX_I]
-    st = torch.zeros((world.size,), dtype=torch.int64, device=acc.device)
+    st = torch.zeros((world.size,), dtype=torch.int64, device=dev)
     st[world.rank] = status
     b_sum = torch.cat([acc[:, si].reshape(-1), st]) if si else st
     p_sum = world.all_reduce_async(b_sum, "sum")
-    p_f = p_max = None
+    p_f = p_max = p_hll = None
     if sf:
         b_f = acc[:, sf].contiguous().view(torch.float64)
         p_f = world.all_reduce_async(b_f, "sum")
     if mn or mx:
         b_max = torch.cat([acc[:, mx].reshape(-1), torch.bitwise_not(acc[:, mn]).reshape(-1)])
         p_max = world.all_reduce_async(b_max, "max")
-    p_hll = [world.all_reduce_async(h.clone(), "max") for h in part.hll]
+    if hll:
+        p_hll = world.all_reduce_async(torch.cat([h.reshape(-1) for h in hll]), "max")  # u8 registers
+    shapes = [h.shape for h in hll]
 
     def finish_reduce():
         s = p_sum.wait()
@@ -131,19 +148,29 @@ def start_dense_merge(world: World, prog, part: Partials, status: int, kind: Opt
                 acc[:, mx] = m[: R * len(mx)].reshape(R, len(mx))
             if mn:
                 acc[:, mn] = torch.bitwise_not(m[R * len(mx):].reshape(R, len(mn)))
-        hll = [p.wait() for p in p_hll]
+        regs = []
+        if p_hll is not None:
+            flat, off = p_hll.wait(), 0
+            for shp in shapes:
+                regs.append(flat[off: off + shp.numel()].reshape(shp))
+                off += shp.numel()
         if si:
             acc[:, si] = s[:-world.size].reshape(R, len(si))
-        return Partials("dense", acc, None, hll), s[-world.size:]  # one status word per rank
+        return Partials("dense", acc, None, regs), s[-world.size:]  # one status word per rank
 
     return DenseMerge(finish_reduce)
 
 
 def merge_partials(world: World, prog, part: Partials, disjoint_keys: bool = False,
-                   local_error: Optional[BaseException] = None) -> Partials:
+                   local_error: Optional[BaseException] = None, finish: str = "all") -> Partials:
     """Merge this rank's partials with every other rank's.  ``local_error`` set = this rank failed
     its scan and ``part`` is a layout-compatible placeholder: the status word travels in the
-    merge's own collective and every rank raises (parallel/fault.py)."""
+    merge's own collective and every rank raises (parallel/fault.py).
+
+    ``finish`` says where sparse results end up: ``"all"`` -- every rank gets every final group;
+    ``"root"`` -- rank 0 gets them, the other ranks an empty slice; ``"local"`` -- every rank keeps
+    its disjoint slice (``scattered``) for distributed HAVING / top-k before ``gather_groups``.
+    Dense states are merged whole on every rank either way."""
     if not world.distributed:
         if local_error is not None:
             raise local_error
@@ -160,8 +187,11 @@ def merge_partials(world: World, prog, part: Partials, disjoint_keys: bool = Fal
     # sparse
     sp = part.compact()
     if disjoint_keys:
-        return _gather_disjoint(world, sp, status, local_error)
-    return _merge_sparse_shuffle(world, prog, sp, status, local_error)
+        if finish == "local":
+            # no collective yet: the status word rides with the gather that follows (gather_groups)
+            return Partials("sparse", sp.acc, sp.keys, sp.hll, scattered=True, status=status)
+        return gather_groups(world, sp, finish == "root", status, local_error)
+    return _merge_sparse_shuffle(world, prog, sp, status, local_error, finish)
 
 
 def merge_plan_for(world: World, part: Partials, disjoint_keys: bool = False):
@@ -174,23 +204,48 @@ def merge_plan_for(world: World, part: Partials, disjoint_keys: bool = False):
 
 
 def dense_state_bytes(part: Partials) -> int:
-    """Bytes one rank contributes to the one-shot gather: accumulators plus HLL registers (widened
-    to int64 words in the gather buffer) -- the registers are usually the bulk (2048 per group per
-    sketch at HLL_P=11)."""
-    return (part.acc.numel() + sum(h.numel() for h in part.hll)) * 8
+    """Bytes one rank contributes to the one-shot gather: 8-byte accumulator words plus the HLL
+    register bytes (2048 per group per sketch at HLL_P=11 -- usually the bulk)."""
+    return part.acc.numel() * 8 + sum(h.numel() for h in part.hll)
 
 
-def _gather_disjoint(world: World, sp: Partials, status: int, local_error) -> Partials:
-    """Groups are disjoint across ranks (grouped on the shard key): concatenate, no merge."""
-    # keys + accumulators travel as one [n, 1 + nslots] int64 block: one length exchange (which also
-    # carries the status word) + one gather
-    kv = torch.cat([sp.keys.reshape(-1, 1).to(torch.int64), sp.acc], dim=1)
-    kvs, sts = world.all_gather_varlen(kv, status=status)
+# ---------------------------------------------------------------------------------------------
+# packed rows: one uint8 block [n, 8 * (1 + nslots) + nhll * m] per rank, so a shuffle or a gather
+# is ONE collective whatever the number of sketches
+def pack_rows(sp: Partials) -> torch.Tensor:
+    n = int(sp.acc.shape[0])
+    kv = torch.cat([sp.keys.reshape(-1, 1).to(torch.int64), sp.acc], dim=1).contiguous()
+    parts = [kv.view(torch.uint8).reshape(n, 8 * kv.shape[1])] + [_u8(h).reshape(n, h.shape[1]) for h in sp.hll]
+    return torch.cat(parts, dim=1) if len(parts) > 1 else parts[0]
+
+
+def unpack_rows(rows: torch.Tensor, nslots: int, hll_widths: List[int], scattered: bool = False) -> Partials:
+    w = 8 * (1 + nslots)
+    kv = rows[:, :w].contiguous().view(torch.int64).reshape(rows.shape[0], 1 + nslots)
+    hll, off = [], w
+    for m in hll_widths:
+        hll.append(rows[:, off: off + m].contiguous())
+        off += m
+    return Partials("sparse", kv[:, 1:], kv[:, 0], hll, scattered=scattered)
+
+
+def gather_groups(world: World, sp: Partials, root_only: bool, status: int = STATUS_OK,
+                  local_error: Optional[BaseException] = None) -> Partials:
+    """Concatenate every rank's disjoint groups: at rank 0 only (``root_only``: one all-to-all in
+    which every rank sends its rows to the root and the others receive nothing -- the root takes in
+    exactly the result, each peer over its own xGMI link), or on every rank (all-gather)."""
+    ns = sp.acc.shape[1]
+    widths = [int(h.shape[1]) for h in sp.hll]
+    rows = pack_rows(sp)
+    if root_only:
+        got, sts = world.gather_varlen(rows, root=0, status=status)
+    else:
+        got, sts = world.all_gather_varlen(rows, status=status)
     if local_error is not None or any(sts):
         raise_if_failed(sts, world.rank, local_error)
-    hlls = [world.all_gather_varlen(h) for h in sp.hll]
-    kv = torch.cat(kvs)
-    return Partials("sparse", kv[:, 1:], kv[:, 0], [torch.cat(h) for h in hlls])
+    if not got:
+        got = [rows[:0]]
+    return unpack_rows(torch.cat(got) if len(got) > 1 else got[0], ns, widths)
 
 
 def shuffle_owner(keys: torch.Tensor, n: int) -> torch.Tensor:
@@ -200,21 +255,21 @@ def shuffle_owner(keys: torch.Tensor, n: int) -> torch.Tensor:
     return torch.remainder(h, n)
 
 
-def _merge_sparse_shuffle(world: World, prog, sp: Partials, status: int, local_error) -> Partials:
-    """Hash-partitioned shuffle + local merge + gather of the merged groups."""
+def _merge_sparse_shuffle(world: World, prog, sp: Partials, status: int, local_error,
+                          finish: str = "all") -> Partials:
+    """Hash-partitioned shuffle (one all-to-all of packed rows) + local merge; the result is this
+    rank's disjoint key range (``finish="local"``) or gathered (``gather_groups``)."""
     n = world.size
     dest = shuffle_owner(sp.keys, n)
     order = torch.argsort(dest, stable=True)
     counts = torch.bincount(dest, minlength=n)
-    kv = torch.cat([sp.keys.reshape(-1, 1).to(torch.int64), sp.acc], dim=1).index_select(0, order)
-    recv, rc, sts = world.all_to_all_varlen(kv, counts, status=status)
+    rows = pack_rows(sp).index_select(0, order)
+    recv, rc, sts = world.all_to_all_varlen(rows, counts, status=status)
     if local_error is not None or any(sts):
         raise_if_failed(sts, world.rank, local_error)
-    hll = []
-    for h in sp.hll:
-        r, _ = world.all_to_all_varlen(h.index_select(0, order), counts)
-        hll.append(r)
-    mine = Partials("sparse", recv[:, 1:], recv[:, 0], hll)
+    mine = unpack_rows(recv, sp.acc.shape[1], [int(h.shape[1]) for h in sp.hll])
     merged = merge_sparse([mine], prog.slots) if recv.shape[0] else mine
+    if finish == "local":
+        return Partials("sparse", merged.acc, merged.keys, merged.hll, scattered=True)
     # this rank owns a disjoint key range now: the final groups are a concatenation
-    return _gather_disjoint(world, merged, STATUS_OK, None)
+    return gather_groups(world, merged, finish == "root")

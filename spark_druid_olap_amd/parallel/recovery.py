@@ -246,7 +246,27 @@ def _is_comm_failure(e: BaseException) -> bool:
     if isinstance(e, RankFailure):
         return False  # a live rank failed its scan: the ranks already agreed, nothing to rebuild
     names = {type(x).__name__ for x in (e, e.__cause__, e.__context__) if x is not None}
+    if names & {"DistBackendError", "DistNetworkError", "DistStoreError"}:
+        return True
     msg = str(e)
-    return bool(names & {"DistBackendError", "DistNetworkError", "DistStoreError"}) or any(
-        s in msg for s in ("Connection closed", "Connection reset", "Timed out", "timed out", "Broken pipe",
-                           "NCCL", "RCCL", "Socket", "peer"))
+    if not any(s in msg for s in ("Connection closed", "Connection reset", "Timed out", "timed out", "Broken pipe",
+                                  "NCCL", "RCCL", "Socket", "peer")):
+        return False
+    # a transport-sounding message alone (e.g. a socket timeout inside one statement on one rank)
+    # is not evidence of a dead peer: recovery starts only once some member's heartbeat went stale,
+    # otherwise this rank would publish a membership of itself and its live peers would be stranded
+    return _member_went_stale()
+
+
+def _member_went_stale(stale_s: float = 3.0, wait_s: Optional[float] = None) -> bool:
+    st = _STATE
+    if st is None:
+        return False
+    deadline = time.time() + (stale_s + 1.5 if wait_s is None else wait_s)
+    while True:
+        others = [r for r in st.members if r != st.orig_rank]
+        if len(st.membership.alive(others, stale_s)) < len(others):
+            return True
+        if time.time() >= deadline:
+            return False
+        time.sleep(0.1)

@@ -30,6 +30,13 @@ class World:
         return self.size > 1
 
     @property
+    def pg(self):
+        """The process group this thread's collectives use: the SPMD server's per-slot group while
+        a slot worker runs a statement (``slot_group``), else this world's group (default)."""
+        g = getattr(_TLS, "group", None)
+        return g if g is not None else self.group
+
+    @property
     def is_root(self) -> bool:
         return self.rank == 0
 
@@ -54,16 +61,16 @@ class World:
     def barrier(self):
         if self.distributed:
             if self.backend == "nccl":
-                dist.barrier(group=self.group, device_ids=[self.local_rank])
+                dist.barrier(group=self.pg, device_ids=[self.local_rank])
             else:
-                dist.barrier(group=self.group)
+                dist.barrier(group=self.pg)
 
     def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         if not self.distributed:
             return t
         o = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
         h = self._stage(t)
-        dist.all_reduce(h, op=o, group=self.group)
+        dist.all_reduce(h, op=o, group=self.pg)
         return self._unstage(h, t)
 
     def all_gather_tensor(self, t: torch.Tensor) -> torch.Tensor:
@@ -79,7 +86,7 @@ class World:
             return Pending(None, lambda: t)
         o = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
         h = self._stage(t)
-        work = dist.all_reduce(h, op=o, group=self.group, async_op=True)
+        work = dist.all_reduce(h, op=o, group=self.pg, async_op=True)
         return Pending(work, lambda: self._unstage(h, t))
 
     def all_gather_tensor_async(self, t: torch.Tensor) -> "Pending":
@@ -88,7 +95,7 @@ class World:
         src = self._stage(t.contiguous().reshape(-1))
         # concatenated layout works on both RCCL and gloo (gloo rejects the stacked form)
         out = torch.empty((self.size * src.numel(),), dtype=t.dtype, device=src.device)
-        work = dist.all_gather_into_tensor(out, src, group=self.group, async_op=True)
+        work = dist.all_gather_into_tensor(out, src, group=self.pg, async_op=True)
         return Pending(work, lambda: out.to(t.device).view((self.size,) + tuple(t.shape)))
 
     def all_to_all_varlen(self, t: torch.Tensor, counts: torch.Tensor, status: Optional[int] = None):
@@ -106,7 +113,7 @@ class World:
         send_meta = torch.stack([counts.to(torch.int64).cpu(), torch.full((n,), int(status or 0), dtype=torch.int64)], 1)
         send_meta = send_meta.to(dev if self.backend == "nccl" else "cpu").reshape(-1).contiguous()
         recv_meta = torch.empty_like(send_meta)
-        dist.all_to_all_single(recv_meta, send_meta, group=self.group)
+        dist.all_to_all_single(recv_meta, send_meta, group=self.pg)
         meta = recv_meta.reshape(n, 2).cpu()
         rc = meta[:, 0]
         sts = meta[:, 1].tolist()
@@ -119,9 +126,25 @@ class World:
         src = self._stage(t.contiguous().reshape(-1))
         out = torch.empty((int(rc.sum()) * width,), dtype=t.dtype, device=src.device)
         dist.all_to_all_single(out, src, output_split_sizes=[int(x) * width for x in rc.tolist()],
-                               input_split_sizes=[int(x) * width for x in counts.cpu().tolist()], group=self.group)
+                               input_split_sizes=[int(x) * width for x in counts.cpu().tolist()], group=self.pg)
         out = out.to(dev).reshape((-1,) + row)
         return (out, rc, sts) if status is not None else (out, rc)
+
+    def gather_varlen(self, t: torch.Tensor, root: int = 0, status: Optional[int] = None):
+        """Rows of every rank concatenated at ``root`` only: an all-to-all in which each rank sends
+        its rows to the root and nothing to anyone else, so the root takes in exactly the result
+        (each peer over its own xGMI link) and no other rank receives a byte of it -- unlike an
+        all-gather, which delivers N copies.  Returns ``(per-source tensors, statuses)``: the root
+        gets one tensor per rank, the others an empty list; every rank learns every status (the
+        count exchange carries it, parallel/fault.py)."""
+        if not self.distributed:
+            return [t], [status or 0]
+        counts = torch.zeros(self.size, dtype=torch.int64)
+        counts[root] = t.shape[0]
+        out, rc, sts = self.all_to_all_varlen(t, counts, status=int(status or 0))
+        if self.rank != root or any(sts):
+            return [], sts
+        return list(torch.split(out, [int(x) for x in rc.tolist()])), sts
 
     def all_gather_varlen(self, t: torch.Tensor, status: Optional[int] = None):
         """Gather tensors whose first dimension differs per rank.  With ``status`` set, every rank's
@@ -147,7 +170,7 @@ class World:
         if not self.distributed:
             return obj
         lst = [obj]
-        dist.broadcast_object_list(lst, src=src, group=self.group)
+        dist.broadcast_object_list(lst, src=src, group=self.pg)
         return lst[0]
 
     def all_gather_object(self, obj: Any) -> List[Any]:
@@ -155,7 +178,7 @@ class World:
         if not self.distributed:
             return [obj]
         out: List[Any] = [None] * self.size
-        dist.all_gather_object(out, obj, group=self.group)
+        dist.all_gather_object(out, obj, group=self.pg)
         return out
 
     def max_float(self, x: float) -> float:
@@ -166,6 +189,30 @@ class World:
         # an all-gather, not a ring all-reduce: every rank talks to every peer, so a dead rank is
         # noticed by all survivors at once (parallel/recovery.py agrees on membership right after)
         return float(self.all_gather_tensor(t).max().item())
+
+
+_TLS = __import__("threading").local()
+
+
+class slot_group:
+    """``with slot_group(g):`` -- collectives issued by this thread go to process group ``g``.
+
+    The SPMD server runs K statements at once, one per execution slot, each slot with its own
+    process group created identically on every rank (``dist.new_group``): statements of different
+    slots then issue their collectives concurrently on independent communicators, while within a
+    slot every rank issues them in the same (broadcast) order."""
+
+    def __init__(self, group):
+        self.group = group
+
+    def __enter__(self):
+        self._prev = getattr(_TLS, "group", None)
+        _TLS.group = self.group
+        return self
+
+    def __exit__(self, *exc):
+        _TLS.group = self._prev
+        return False
 
 
 class Pending:

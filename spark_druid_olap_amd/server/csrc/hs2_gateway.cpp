@@ -673,7 +673,9 @@ class Gateway {
       std::string key = std::to_string(cit->second) + '\x1f' + stmt;
       ++stats_statements_;
       auto pit = pending_.find(key);
-      if (pit != pending_.end()) {
+      // a queued batch whose waiters all cancelled (or left) keeps its sticky cancel flag: a new
+      // statement must not join it, or it would be reported 'cancelled' without ever cancelling
+      if (pit != pending_.end() && !pit->second->cancel) {
         b = pit->second;
         ++stats_coalesced_;
       } else {

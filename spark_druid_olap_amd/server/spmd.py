@@ -1,30 +1,42 @@
 """Drive every GPU rank from one client-facing server (the reference's HiveThriftServer2 fronts the
 whole Spark + Druid cluster, ``asql/hive/thriftserver/sparklinedata/HiveThriftServer2.scala:55-79``).
 
-Each rank holds a shard of every datasource, so every statement must run on every rank, in the same
-order (the merges inside a query are collectives).  Rank 0 accepts the client connections; its
-``SpmdDispatcher`` serialises statements from all client sessions into one stream and broadcasts
-each one -- with the client session's id, ``SET`` overlay and a deadline -- to the other ranks
-(``World.broadcast_object``).  Every rank then executes it over its own shard and the collectives
-inside merge the partial aggregates; rank 0 returns the (global) result to the client.  The other
-ranks run ``serve_peer``: a loop that receives and executes the same stream, keeping a mirror of
+Each rank holds a shard of every datasource, so every statement must run on every rank (the merges
+inside a query are collectives).  Rank 0 accepts the client connections; its ``SpmdDispatcher``
+orders the statements of all client sessions into one stream and broadcasts it -- with the client
+session's id, ``SET`` overlay and a deadline -- to the other ranks (``World.broadcast_object``).
+The other ranks run ``serve_peer``: they receive and apply the same stream, keeping a mirror of
 every client session (conf + current database) so session state evolves identically everywhere.
 
-Identical statements from different clients that queue up together execute once (a shared scan;
-``engine/scheduler.py`` explains the rule).  While idle the dispatcher broadcasts a heartbeat, so
-peers never sit in a collective longer than the process-group timeout.
+Concurrency across all GPUs.  The reference serves many BI clients against the whole cluster at
+once (pooled HTTP client 100/20, ``asd/DruidPlanner.scala:83-90``; a JMeter fair-pool load,
+``docs/bi-benchmark/snap-sales-demo.jmx:87-101``).  Here every rank runs K *execution slots*: one
+worker thread per slot, each with its own process group (``dist.new_group``, created in the same
+order on every rank), its own HIP stream and its own device buffers.  Rank 0 assigns each query to
+a slot and the assignment travels in the broadcast, so within a slot every rank runs the same
+statements in the same order -- its collectives match -- while statements of different slots run
+at the same time on independent communicators.  Everything that may issue collectives outside a
+statement's own slot -- planning and lowering (cluster-wide FD tables, row estimates), commands,
+plans whose pushed queries are re-planned at run time (subquery-parameterised filters, fused
+grouping sets) -- runs in the dispatch thread, in broadcast order, on the default group.
+
+Identical statements from different clients that queue up together may execute once (a shared
+scan; ``engine/scheduler.py`` explains the rule; ``SDO_SPMD_COALESCE=0`` turns it off).  While idle
+the dispatcher broadcasts a heartbeat, so peers never sit in a collective longer than the
+process-group timeout.
 """
 from __future__ import annotations
 
 import logging
+import os
 import queue
 import threading
-import time
 from typing import Any, Dict, List, Optional, Tuple
 
 log = logging.getLogger("sdo.spmd")
 
 HEARTBEAT_S = 20.0
+INLINE = -1  # slot id of statements that run in the dispatch thread
 
 
 class _Item:
@@ -37,9 +49,18 @@ class _Item:
         self.error: Optional[BaseException] = None
 
 
-def _execute(sessions: Dict[bytes, Any], root, msg: Dict[str, Any]):
-    """Apply one broadcast message to this rank's session mirrors; returns a pandas frame for
-    statements (None for session lifecycle messages)."""
+def _session_for(sessions: Dict[bytes, Any], root, msg: Dict[str, Any]):
+    sid = msg.get("sid")
+    s = sessions.get(sid)
+    if s is None:
+        s = sessions[sid] = root.new_session()
+    for k, v in (msg.get("overlay") or {}).items():
+        s.conf.set(k, v)
+    return s
+
+
+def _apply(sessions: Dict[bytes, Any], root, msg: Dict[str, Any]) -> None:
+    """Session lifecycle messages (every rank, dispatch thread, broadcast order)."""
     op = msg["op"]
     sid = msg.get("sid")
     if op == "open":
@@ -49,36 +70,149 @@ def _execute(sessions: Dict[bytes, Any], root, msg: Dict[str, Any]):
         if msg.get("db"):
             s.catalog.use(msg["db"])
         sessions[sid] = s
-        return None
-    if op == "close":
+    elif op == "close":
         sessions.pop(sid, None)
-        return None
-    if op == "exec":
-        s = sessions.get(sid)
-        if s is None:
-            s = sessions[sid] = root.new_session()
-        for k, v in (msg.get("overlay") or {}).items():
-            s.conf.set(k, v)
-        token = None
-        if msg.get("timeout_s"):
-            from ..utils.cancel import CancelToken
 
-            token = CancelToken(float(msg["timeout_s"]) * 1000.0)
-        df = s.sql(msg["stmt"])
-        return df, df.to_pandas(token=token)
+
+def _token(msg):
+    if msg.get("timeout_s"):
+        from ..utils.cancel import CancelToken
+
+        return CancelToken(float(msg["timeout_s"]) * 1000.0)
     return None
 
 
-class SpmdDispatcher:
-    """Rank 0 side: one ordered statement stream for every rank."""
+def _run_statement(df, msg):
+    """Execute a planned statement; rank 0 answers the client, so the final groups of its pushed
+    queries gather there only (engine/executor.py results_on_root)."""
+    from ..engine.executor import results_on_root
 
-    def __init__(self, session, world):
+    with results_on_root():
+        return df, df.to_pandas(token=_token(msg))
+
+
+def _execute(sessions: Dict[bytes, Any], root, msg: Dict[str, Any]):
+    """Apply one message in the dispatch thread: lifecycle ops, commands and statements that do
+    not run on a slot.  Returns (DataFrame, pandas) for statements, None otherwise."""
+    if msg["op"] != "exec":
+        _apply(sessions, root, msg)
+        return None
+    s = _session_for(sessions, root, msg)
+    df = s.sql(msg["stmt"])  # (commands -- CREATE TABLE AS SELECT -- run here, on every rank)
+    return _run_statement(df, msg)
+
+
+def slot_eligible(df) -> bool:
+    """A planned statement may run on a slot when nothing it executes issues collectives outside
+    its own slot: a query plan whose pushed queries are all known (and so prepared) up front."""
+    from ..query import spec as S
+    from ..sql import plan as P
+
+    if df.plan is None:
+        return False
+    if P.find_all(df.plan, P.Union):   # fused grouping sets prepare their scan at run time
+        return False
+    dqs = P.find_all_deep(df.plan, P.DruidQuery)
+    return not any(S.find_deferred(dq.spec) for dq in dqs)
+
+
+def prepare_statement(sessions: Dict[bytes, Any], root, msg: Dict[str, Any]):
+    """Plan the statement and lower every pushed query (dispatch thread, broadcast order: the
+    collectives of lowering run on the default group identically on every rank)."""
+    from ..sql import plan as P
+
+    s = _session_for(sessions, root, msg)
+    df = s.sql(msg["stmt"])
+    for dq in P.find_all_deep(df.plan, P.DruidQuery):
+        s.prepare_druid(dq)
+    return df
+
+
+class SlotWorkers:
+    """K execution slots on this rank: a worker thread each, with its own process group (created
+    collectively, same order on every rank), HIP stream and device-buffer slot."""
+
+    BUFFER_SLOT_BASE = 100  # engine/scheduler.py buffer slots (1..K belong to the local scheduler)
+
+    def __init__(self, session, world, k: int):
+        import torch
+        import torch.distributed as dist
+
+        self.k = k
+        self.groups = [dist.new_group(list(range(world.size))) if world.distributed else None for _ in range(k)]
+        dev = world.device()
+        self.streams = [torch.cuda.Stream(dev) if dev.type == "cuda" else None for _ in range(k)]
+        self.queues: List["queue.Queue"] = [queue.Queue() for _ in range(k)]
+        self.busy = [0] * k
+        self.max_inflight = 0
+        self._lock = threading.Lock()
+        self.threads = [threading.Thread(target=self._work, args=(i,), daemon=True, name=f"spmd-slot-{i}")
+                        for i in range(k)]
+        for t in self.threads:
+            t.start()
+
+    def submit(self, slot: int, df, msg, done) -> None:
+        with self._lock:
+            self.busy[slot] += 1
+        self.queues[slot].put((df, msg, done))
+
+    def least_busy(self) -> int:
+        with self._lock:
+            return min(range(self.k), key=lambda i: self.busy[i])
+
+    def stop(self) -> None:
+        for q in self.queues:
+            q.put(None)
+        for t in self.threads:
+            t.join(timeout=5)
+
+    def _work(self, i: int) -> None:
+        import torch
+
+        from ..engine.scheduler import use_slot
+        from ..parallel.world import slot_group
+
+        while True:
+            job = self.queues[i].get()
+            if job is None:
+                return
+            df, msg, done = job
+            res, err = None, None
+            with self._lock:
+                self.max_inflight = max(self.max_inflight, sum(1 for b in self.busy if b > 0))
+            try:
+                with slot_group(self.groups[i]), use_slot(self.BUFFER_SLOT_BASE + i):
+                    if self.streams[i] is not None:
+                        with torch.cuda.stream(self.streams[i]):
+                            res = _run_statement(df, msg)
+                        self.streams[i].synchronize()
+                    else:
+                        res = _run_statement(df, msg)
+            except BaseException as e:  # noqa: BLE001  (rank 0 reports it; peers drop it)
+                err = e
+            finally:
+                with self._lock:
+                    self.busy[i] -= 1
+            done(res, err)
+
+
+class SpmdDispatcher:
+    """Rank 0 side: one ordered statement stream for every rank, executed on K slots."""
+
+    def __init__(self, session, world, slots: Optional[int] = None, coalesce: Optional[bool] = None):
         self.root = session
         self.world = world
         self.sessions: Dict[bytes, Any] = {}
         self._q: "queue.Queue[_Item]" = queue.Queue()
         self._stop = threading.Event()
-        self.stats = {"statements": 0, "executions": 0, "coalesced": 0, "heartbeats": 0}
+        self.coalesce = coalesce if coalesce is not None else os.environ.get("SDO_SPMD_COALESCE", "1") != "0"
+        k = slots if slots is not None else int(os.environ.get("SDO_SPMD_SLOTS", "4"))
+        if world.distributed:
+            world.broadcast_object({"op": "slots", "k": k})  # peers create the same slot groups
+        self.workers = SlotWorkers(session, world, k) if k > 0 else None
+        self._pinned: Dict[bytes, int] = {}
+        self.stats = {"statements": 0, "executions": 0, "coalesced": 0, "heartbeats": 0, "on_slots": 0,
+                      "inline": 0}
         self._thread = threading.Thread(target=self._loop, daemon=True, name="spmd-dispatch")
         self._thread.start()
 
@@ -102,6 +236,8 @@ class SpmdDispatcher:
         if not self._stop.is_set():
             self._stop.set()
             self._thread.join(timeout=HEARTBEAT_S + 5)
+        if self.workers is not None:
+            self.workers.stop()
 
     def _submit(self, msg):
         it = _Item(msg)
@@ -112,6 +248,32 @@ class SpmdDispatcher:
         return it.result
 
     # ---------------------------------------------------------------- dispatch loop
+    def _assign(self, groups: List[List[_Item]]) -> List[int]:
+        """Slot per group of identical statements: queries whose plans allow it go to a slot, the
+        rest (commands, session ops, run-time re-planned queries) run inline."""
+        out = []
+        for g in groups:
+            m = g[0].msg
+            slot = INLINE
+            if self.workers is not None and m["op"] == "exec" and _is_query(m["stmt"]) and not m.get("overlay"):
+                try:
+                    s = _session_for(self.sessions, self.root, {"sid": m["sid"]})
+                    if slot_eligible(s.sql(m["stmt"])):
+                        slot = self._session_slot(m["sid"])
+                except Exception:  # noqa: BLE001  (the statement fails the same way inline)
+                    slot = INLINE
+            out.append(slot)
+        return out
+
+    def _session_slot(self, sid) -> int:
+        """A session with work still queued keeps its slot (its statements stay in order); else the
+        least busy slot."""
+        s = self._pinned.get(sid)
+        if s is not None and self.workers.busy[s] > 0:
+            return s
+        s = self._pinned[sid] = self.workers.least_busy()
+        return s
+
     def _loop(self):
         w = self.world
         while True:
@@ -135,7 +297,8 @@ class SpmdDispatcher:
                 except queue.Empty:
                     break
             groups = self._coalesce(batch)
-            msgs = [g[0].msg for g in groups]
+            slots = self._assign(groups)
+            msgs = [dict(g[0].msg, slot=sl) for g, sl in zip(groups, slots)]
             try:
                 w.broadcast_object({"op": "batch", "msgs": msgs})
             except BaseException as e:  # noqa: BLE001
@@ -148,9 +311,14 @@ class SpmdDispatcher:
                     it.error = e
                     it.event.set()
                 raise
-            for g in groups:
+            for g, m in zip(groups, msgs):
+                if m["slot"] != INLINE:
+                    self.stats["on_slots"] += 1
+                    self._dispatch_slot(g, m)
+                    continue
+                self.stats["inline"] += 1
                 try:
-                    res = _run_elastic(self.root, lambda m=g[0].msg: _execute(self.sessions, self.root, m))
+                    res = _run_elastic(self.root, lambda m=m: _execute(self.sessions, self.root, m))
                     w = self.world = self.root.engine.world
                     for it in g:
                         it.result = res
@@ -163,6 +331,21 @@ class SpmdDispatcher:
                 break
         w.broadcast_object({"op": "stop"})
 
+    def _dispatch_slot(self, g: List[_Item], m: Dict[str, Any]) -> None:
+        try:
+            df = prepare_statement(self.sessions, self.root, m)
+        except BaseException as e:  # noqa: BLE001
+            for it in g:
+                it.error = e
+                it.event.set()
+            return
+
+        def done(res, err, g=g):
+            for it in g:
+                it.result, it.error = res, err
+                it.event.set()
+        self.workers.submit(m["slot"], df, m, done)
+
     def _coalesce(self, batch: List[_Item]) -> List[List[_Item]]:
         """Group identical read-only statements of sessions in the same state (same conf and
         current database): they execute once."""
@@ -171,7 +354,7 @@ class SpmdDispatcher:
         for it in batch:
             m = it.msg
             key = None
-            if m["op"] == "exec" and not m.get("overlay") and _is_query(m["stmt"]):
+            if self.coalesce and m["op"] == "exec" and not m.get("overlay") and _is_query(m["stmt"]):
                 s = self.sessions.get(m["sid"])
                 if s is not None and not s.catalog.temp:
                     key = (m["stmt"].strip(), s.catalog.current_db, tuple(sorted(s.conf.items().items())))
@@ -216,6 +399,7 @@ def _run_elastic(session, fn):
 def serve_peer(session, world) -> None:
     """Ranks 1..N-1: execute the statement stream broadcast by rank 0 until it stops."""
     sessions: Dict[bytes, Any] = {}
+    workers: Optional[SlotWorkers] = None
     while True:
         try:
             msg = world.broadcast_object(None)
@@ -226,11 +410,22 @@ def serve_peer(session, world) -> None:
             continue
         op = msg.get("op")
         if op == "stop":
+            if workers is not None:
+                workers.stop()
             return
         if op == "noop":
             continue
+        if op == "slots":
+            k = int(msg["k"])
+            workers = SlotWorkers(session, world, k) if k > 0 else None
+            continue
         for m in msg.get("msgs", []):
+            slot = m.get("slot", INLINE)
             try:
+                if slot != INLINE and workers is not None:
+                    df = prepare_statement(sessions, session, m)
+                    workers.submit(slot, df, m, lambda res, err: None)  # rank 0 answers the client
+                    continue
                 _run_elastic(session, lambda m=m: _execute(sessions, session, m))
                 world = session.engine.world
             except BaseException as e:  # noqa: BLE001  (rank 0 reports the error to the client)

@@ -78,17 +78,28 @@ class DataFrame:
                 from .utils.cancel import CancelToken
 
                 token = CancelToken(tmo)
+        from .engine.executor import results_on_root, root_only_results
         from .utils.cancel import scope
 
         ex = Executor(self.session, token)
         t0 = time.perf_counter()
-        with scope(token):
+        # results on rank 0 only (the caller asked, engine/executor.py results_on_root) unless a
+        # pushed query's spec is parameterized by another query's result: every rank needs those
+        root_only = root_only_results() and self._root_only_safe()
+        with scope(token), results_on_root(root_only):
             b = self.session._with_sql(self.sql_text, lambda: ex.run(self.plan))
         self.last_stats = {"ms": (time.perf_counter() - t0) * 1e3, "druid": ex.druid_stats}
         return b
 
     def prepared(self) -> "DataFrame":
         return self
+
+    def _root_only_safe(self) -> bool:
+        ok = self.__dict__.get("_root_ok")
+        if ok is None:
+            ok = self._root_ok = self.plan is not None and not any(
+                S.find_deferred(dq.spec) for dq in P.find_all_deep(self.plan, P.DruidQuery))
+        return ok
 
     def run(self, token=None) -> Batch:
         return self._run(token)
@@ -308,7 +319,9 @@ class Session:
         return self._command(text, st)
 
     def _query(self, text: str, st) -> DataFrame:
-        cache_on = bool(self.conf.typed("spark.sparklinedata.druid.planCache.enabled"))
+        # statements over the d$* metadata views are planned afresh (their rows are the metadata
+        # at planning time); everything else is cached by text + catalog / registry / conf state
+        cache_on = bool(self.conf.typed("spark.sparklinedata.druid.planCache.enabled")) and "d$" not in text.lower()
         key = (text, self.catalog.version, self.catalog.current_db, id(self.catalog.temp) if self.catalog.temp else 0,
                self.catalog.cluster.generation, json.dumps(self.conf.items(), sort_keys=True))
         if cache_on:
@@ -400,6 +413,26 @@ class Session:
         ds = dq.relation.info.datasource
         spec = dq.spec
         t0 = time.perf_counter()
+        prep = self.prepare_druid(dq)
+        from .utils import trace as T
+
+        with T.span(f"sdo.druid.{spec.queryType}"):
+            res = prep.run()
+        if isinstance(spec, S.TimeSeriesQuerySpec) and res.num_rows == 0:
+            res = _empty_global_agg(res, spec)
+        ms = (time.perf_counter() - t0) * 1e3
+        if self.conf.typed("spark.sparklinedata.enable.druid.query.history"):
+            self.history.record(spec, res.stats.get("exec_ms", ms), ms, res.num_rows,
+                                f"gpu:0-{self.engine.world.size - 1}", getattr(self._tl, "sql", None),
+                                len(ds.segments))
+        return res
+
+    def prepare_druid(self, dq: P.DruidQuery):
+        """The engine's prepared query for pushed query ``dq`` (lowered once, cached on the plan
+        node).  Lowering may issue collectives (cluster-wide FD tables, row estimates), so the SPMD
+        server calls this in broadcast order on every rank before a statement runs on a slot."""
+        ds = dq.relation.info.datasource
+        spec = dq.spec
         run_spec = spec
         if isinstance(spec, S.SelectSpec):
             # one page holding every row (the reference's paging loop, DruidSelectResultIterator.scala:116-137,
@@ -425,16 +458,7 @@ class Session:
                     prep.out_types = {n: t for n, t, k in dq.columns if k == "value"}
                     dq._prepared = prep
                     dq._prepared_spec = spec
-        with T.span(f"sdo.druid.{spec.queryType}"):
-            res = prep.run()
-        if isinstance(spec, S.TimeSeriesQuerySpec) and res.num_rows == 0:
-            res = _empty_global_agg(res, spec)
-        ms = (time.perf_counter() - t0) * 1e3
-        if self.conf.typed("spark.sparklinedata.enable.druid.query.history"):
-            self.history.record(spec, res.stats.get("exec_ms", ms), ms, res.num_rows,
-                                f"gpu:0-{self.engine.world.size - 1}", getattr(self._tl, "sql", None),
-                                len(ds.segments))
-        return res
+        return prep
 
     # ------------------------------------------------------------------------------ commands
     def _rows_df(self, cols: List[Tuple[str, str]], rows: List[tuple]) -> DataFrame:

@@ -13,7 +13,7 @@ from spark_druid_olap_amd.models.bench_queries import bench_specs
 from spark_druid_olap_amd.query import spec as S
 from spark_druid_olap_amd.query.spec import query_from_json
 
-REF_Q = sorted(glob.glob("/root/reference/docs/benchmark/druid/queries/*.json"))
+REF_Q = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "parity", "benchmark_queries", "*.json")))
 
 
 def run(q, ds):

@@ -32,7 +32,7 @@ def _partial(rank: int, R: int = 300):
             acc[:, s] = (torch.rand(R, generator=g, dtype=torch.float64) * 1e6).view(torch.int64)
     acc[0, 2] = -2 ** 63       # INT64_MIN in a min slot (negation would overflow)
     acc[1, 3] = 2 ** 63 - 1    # INT64_MAX in a max slot
-    hll = [torch.randint(0, 30, (R, 64), generator=g, dtype=torch.int32)]
+    hll = [torch.randint(0, 30, (R, 64), generator=g, dtype=torch.int32).to(torch.uint8)]
     return acc, hll
 
 
@@ -139,7 +139,7 @@ def _sparse_partial(rank: int, n: int = 4000):
     keys = torch.randperm(12000, generator=g)[:n].to(torch.int64) * 7919  # overlapping key sets
     acc = torch.randint(0, 10 ** 9, (n, len(SPARSE_SLOTS)), generator=g, dtype=torch.int64)
     acc[:, 1] = (torch.rand(n, generator=g, dtype=torch.float64) * 1e3).view(torch.int64)
-    hll = [torch.randint(0, 20, (n, 16), generator=g, dtype=torch.int32)]
+    hll = [torch.randint(0, 20, (n, 16), generator=g, dtype=torch.int32).to(torch.uint8)]
     return keys, acc, hll
 
 
@@ -157,7 +157,7 @@ def _shuffle_worker(rank, world, port, outdir):
 
     def spy(t, counts, status=None):
         out = orig(t, counts, status)
-        if t.dim() == 2 and t.shape[1] == 1 + len(SPARSE_SLOTS):
+        if t.dim() == 2 and t.dtype == torch.uint8 and t.shape[1] == 8 * (1 + len(SPARSE_SLOTS)) + 16:
             recv["rows"] = int(out[0].shape[0])
         return out
     w.all_to_all_varlen = spy

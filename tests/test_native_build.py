@@ -86,3 +86,30 @@ def test_hll_estimate_bf16_operands_are_exact():
         assert bits == (127 - r) << 7
         assert torch.tensor([bits], dtype=torch.int32).to(torch.int16).view(torch.bfloat16).float().item() == 2.0 ** -r
     assert torch.tensor([1.0]).to(torch.bfloat16).view(torch.int16).item() == 0x3F80
+
+
+def test_hll_register_clamp_and_bytewise_max_formulas():
+    """The packed-byte helpers of the byte-register HLL path (olap_scan.hip clamp127_u8x4,
+    sdo_device.h max_u8x4), evaluated with the same integer expressions on the host: every byte of
+    a dword clamps to min(b, 127) independently, and the bytewise max is per byte."""
+    import random
+
+    def clamp127(x):
+        m = ((x & 0x80808080) >> 7) * 0xFF
+        return ((x & ~m) | (0x7F7F7F7F & m)) & 0xFFFFFFFF
+
+    def max4(a, b):
+        r = 0
+        for k in range(0, 32, 8):
+            r |= max((a >> k) & 0xFF, (b >> k) & 0xFF) << k
+        return r
+
+    rnd = random.Random(5)
+    vals = [0, 1, 65, 126, 127, 128, 129, 200, 255]
+    for _ in range(4000):
+        bs = [rnd.choice(vals + [rnd.randrange(256)]) for _ in range(4)]
+        cs = [rnd.randrange(256) for _ in range(4)]
+        x = sum(b << (8 * i) for i, b in enumerate(bs))
+        y = sum(c << (8 * i) for i, c in enumerate(cs))
+        assert clamp127(x) == sum(min(b, 127) << (8 * i) for i, b in enumerate(bs))
+        assert max4(x, y) == sum(max(b, c) << (8 * i) for i, (b, c) in enumerate(zip(bs, cs)))

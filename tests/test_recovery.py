@@ -103,3 +103,36 @@ def test_survivors_rebuild_and_rehome_the_lost_shard(victim):
             assert o["got"][q] == o["full"][q], q
     adopted = [a for o in outs.values() for a in o["info"]["adopted"]]
     assert adopted == [("tpch", victim)]
+
+
+def test_transport_message_alone_is_not_a_dead_peer(monkeypatch):
+    """a RuntimeError that merely mentions a socket timeout on ONE rank must not start a
+    recovery while every peer still heart-beats (it would shrink the cluster to that rank); a
+    typed c10d error, or a message plus a stale heartbeat, still does."""
+    from spark_druid_olap_amd.parallel import recovery as R
+
+    class _M:
+        def __init__(self, live):
+            self.live = live
+
+        def alive(self, ranks, stale_s):
+            return [r for r in ranks if r in self.live]
+
+    class _S:
+        members = [0, 1, 2]
+        orig_rank = 0
+
+    st = _S()
+    st.membership = _M({0, 1, 2})
+    monkeypatch.setattr(R, "_STATE", st)
+    monkeypatch.setattr(R, "_member_went_stale", lambda *a, **k: len(st.membership.alive([1, 2], 3.0)) < 2)
+    assert not R.is_comm_failure(RuntimeError("recv: Socket timed out inside a statement"))
+    assert not R.is_comm_failure(ValueError("bad literal"))
+    st.membership = _M({0, 1})
+    assert R.is_comm_failure(RuntimeError("Connection closed by peer"))
+
+    class DistBackendError(RuntimeError):
+        pass
+
+    st.membership = _M({0, 1, 2})
+    assert R.is_comm_failure(DistBackendError("anything"))

@@ -149,6 +149,52 @@ def test_native_gateway_batches_identical_waiting_statements(ds_small, df_small)
         srv.stop()
 
 
+def test_native_gateway_new_statement_does_not_join_cancelled_batch(ds_small, df_small):
+    """A queued batch whose only waiter cancelled keeps a sticky cancel flag; the same statement
+    from another session must start a batch of its own and finish (it used to join the
+    cancelled batch and fail with 'cancelled')."""
+    import time as _t
+
+    from spark_druid_olap_amd.server.gateway import NativeHiveServer
+
+    s = Session(engine=Engine(use_native=False))
+    s.register_datasource(ds_small)
+    s.register_table("orderLineItemPartSupplierBase", df_small, schema=tpch.FLAT_SCHEMA)
+    s.sql(tpch.druid_ddl(with_column_mapping=False))
+    srv = NativeHiveServer(s, port=0, executors=1)
+    gate = threading.Event()
+    real = srv._execute
+
+    def gated(bid, sid, stmt):
+        if "s_region" in stmt:
+            gate.wait(10)
+        return real(bid, sid, stmt)
+
+    srv._execute = gated
+    srv.start()
+    try:
+        q_block = "select s_region, count(*) from orderLineItemPartSupplier group by s_region"
+        q = "select l_returnflag, count(*) from orderLineItemPartSupplier group by l_returnflag order by l_returnflag"
+        exp = [tuple(r) for r in df_small.groupby("l_returnflag").size().reset_index().itertuples(index=False)]
+        blocker = threading.Thread(target=lambda: connect(port=srv.port).cursor().execute(q_block).fetchall())
+        blocker.start()
+        _t.sleep(0.3)  # the only executor now holds the blocking batch: q stays queued
+        with connect(port=srv.port) as a, connect(port=srv.port) as b:
+            r = a.call("ExecuteStatement", {"sessionHandle": a.session, "statement": q, "runAsync": True})
+            a.call("CancelOperation", {"operationHandle": r["operationHandle"]})
+            out = []
+            t = threading.Thread(target=lambda: out.append(b.cursor().execute(q).fetchall()))
+            t.start()
+            _t.sleep(0.3)
+            gate.set()
+            t.join(60)
+            blocker.join(60)
+            assert out and [tuple(x) for x in out[0]] == exp
+    finally:
+        gate.set()
+        srv.stop()
+
+
 def test_sessions_do_not_share_set_or_use(server):
     """Per-client session state (Session.new_session): SET and USE in one client session are not
     seen by another; tables stay shared."""

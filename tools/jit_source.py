@@ -1,0 +1,46 @@
+"""Print the lowered program and the generated JIT kernel source of the headline queries (CPU
+only: the SQL is planned over a small synthetic shard, lowered and emitted, not run).
+
+  python tools/jit_source.py [query name substring ...]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    from spark_druid_olap_amd.engine.executor import Engine
+    from spark_druid_olap_amd.engine import device_exec as DE
+    from spark_druid_olap_amd.models import tpch
+    from spark_druid_olap_amd.ops import jit
+    from spark_druid_olap_amd.planner.cost import plan_groupby
+    from spark_druid_olap_amd.session import Session
+    from spark_druid_olap_amd.ops import desc as D
+
+    want = sys.argv[1:]
+    flat = tpch.generate_flat(0.05, "cpu")
+    ds = tpch.to_datasource(flat, profile="bench")
+    sess = Session(engine=Engine(use_native=False), conf={"spark.sparklinedata.druid.approxCountDistinct": "true"})
+    sess.register_datasource(ds)
+    sess.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)
+    sess.sql(tpch.druid_ddl(source="orderLineItemPartSupplierBase", datasource="tpch", with_column_mapping=False))
+    for name, q in tpch.BENCH_QUERIES:
+        if want and not any(w.lower() in name.lower() for w in want):
+            continue
+        df = sess.sql(q)
+        for dq in df.druid_queries():
+            pq = sess.engine.prepare(dq.spec, ds)
+            for _, prog, _ in pq.scans:
+                gp = plan_groupby(prog, True, True)
+                mode = {"dense-lds": D.M_DENSE_LDS, "dense-global": D.M_DENSE_GLOBAL, "hash": D.M_HASH}[gp.mode]
+                print(f"==== {name}: G={prog.G} keys={[(k.name, k.kind, k.card) for k in prog.keys]} "
+                      f"slots={prog.slots} plan={gp.describe()}")
+                regstage = jit.prefer_regstage(prog)
+                lay = jit.layout(prog, mode, 4, bool(prog.nhll) and gp.hll_lds, 1 << prog.hll_p, False, False,
+                                 (160 * 1024) // 3 - 512, regstage, gp.shared)
+                g = jit._Gen(prog, mode, 4, bool(prog.nhll) and gp.hll_lds, True, lay, 1 << prog.hll_p)
+                print(g.source("sdo_jit_probe"))
+
+
+if __name__ == "__main__":
+    main()
