@@ -144,7 +144,7 @@ def main():
     world.barrier()
     sync()
     prof = None
-    if os.environ.get("SDO_BENCH_PROFILE") and world.rank == 0:
+    if os.environ.get("SDO_BENCH_PROFILE") and world.rank == int(os.environ.get("SDO_BENCH_PROFILE_RANK", "0")):
         import cProfile
 
         prof = cProfile.Profile()
@@ -168,7 +168,7 @@ def main():
         import pstats
 
         prof.disable()
-        pstats.Stats(prof, stream=sys.stderr).sort_stats("cumulative").print_stats(40)
+        pstats.Stats(prof, stream=sys.stderr).sort_stats("cumulative").print_stats(60)
     if os.environ.get("SDO_BENCH_PER_RANK"):  # diagnostics: every rank's own means
         print(f"[bench] rank {world.rank}: " + " ".join(f"{k[:12]}={sum(v) / len(v):.3f}" for k, v in lat.items()),
               file=sys.stderr, flush=True)

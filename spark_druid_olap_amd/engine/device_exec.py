@@ -39,10 +39,36 @@ JIT_BLOCKS = int(os.environ.get("SDO_JIT_BLOCKS", "3"))  # target resident workg
 JIT_STAGE = os.environ.get("SDO_JIT_STAGE", "auto")       # auto | reg (VGPR loads) | lds (LDS-DMA planes)
 
 
+def _attach_packed(prog) -> None:
+    """Bit-packed copies (segment/packed.py) of the integer columns the program reads: the JIT
+    kernel reads those instead of the byte-wide columns (the interpreter never does)."""
+    from ..segment import packed as PK
+
+    prog.packed = {}
+    if not PK.ENABLED or prog.empty or prog.ds.device.type != "cuda":
+        return
+    for name in list(prog.fcols) + list(prog.pcols):
+        pc = PK.packed_column(prog.ds, name)
+        if pc is not None:
+            prog.packed[name] = pc
+
+
 def _jit_for(prog, mode: int, hll_lds: bool, m: int, shared: bool = False):
-    """Specialized kernel for this program shape (None -> use the interpreter)."""
+    """Specialized kernel for this program shape (None -> use the interpreter, plain columns)."""
     if not USE_JIT:
+        prog.packed = {}
         return None
+    from ..ops import jit
+
+    if getattr(prog, "packed", None) is None:
+        _attach_packed(prog)
+    js = _jit_build(prog, mode, hll_lds, m, shared)
+    if js is None:
+        prog.packed = {}  # the interpreter reads the plain columns
+    return js
+
+
+def _jit_build(prog, mode: int, hll_lds: bool, m: int, shared: bool = False):
     from ..ops import jit
 
     nplanes = sum(2 if column_tensor_size(prog, c) == 8 else 1 for c in prog.cols)
@@ -214,6 +240,22 @@ class PreparedScan:
         self.lds_total = total
         b.desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
         self.grid = _grid(dev, int(d[0]["total_chunks"]), self.jit.lay.total if self.jit else total)
+        b.run_args = b.noreset_args = None
+        b.fetch = None
+        if self.mode != D.M_HASH:
+            # the whole launch path of one execution as cached arguments of ONE native call
+            # (ops/csrc/bindings.cpp run_scan): fused reset of this slot's buffers + the kernel
+            zeros = list(b.hll) + ([b.touch] if self.touch else []) + ([b.acc] if self.pres_bytes else [])
+            if len(zeros) <= 4 and all(z.numel() * z.element_size() % 8 == 0 for z in zeros):
+                acc = None if self.pres_bytes else b.acc
+                h = self.jit.handle if self.jit is not None else -1
+                tail = (h, b.desc.data_ptr(), int(self.grid), BLOCK,
+                        int(self.jit.lay.total if self.jit is not None else self.lds_total), UNROLL)
+                b.run_args = (acc.data_ptr() if acc is not None else 0, b.init_row.data_ptr(),
+                              int(acc.shape[0]) if acc is not None else 0, int(b.init_row.numel()),
+                              [z.data_ptr() for z in zeros], [z.numel() * z.element_size() // 8 for z in zeros],
+                              b.overflow.data_ptr()) + tail
+                b.noreset_args = (0, 0, 0, 0, [], [], 0) + tail
         return b
 
     def _launch(self, b: "_Bufs"):
@@ -258,9 +300,13 @@ class PreparedScan:
                 return Partials("dense", b.acc, None, [h.view(b.rows, self.m) for h in b.hll])
             return self._empty()
         while True:
-            self._reset(b)
+            if b.run_args is not None:
+                native.run_scan(*(b.noreset_args if (self.touch and b.clean) else b.run_args),
+                                native._stream(self.dev))
+            else:
+                self._reset(b)
+                self._launch(b)
             b.clean = False  # dirty until the touched rows are re-initialised below
-            self._launch(b)
             if self.touch:
                 idx = native.nonzero_rows(b.touch)
                 acc = b.acc.index_select(0, idx)
@@ -309,7 +355,8 @@ class PreparedScan:
 
 class _Bufs:
     """One execution slot's device buffers for a prepared scan."""
-    __slots__ = ("cap", "rows", "init_row", "acc", "keys", "hll", "overflow", "desc", "touch", "clean")
+    __slots__ = ("cap", "rows", "init_row", "acc", "keys", "hll", "overflow", "desc", "touch", "clean", "run_args",
+                 "noreset_args", "fetch")
 
 
 class PreparedMask:

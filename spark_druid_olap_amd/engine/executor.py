@@ -290,8 +290,9 @@ class PreparedQuery:
             t2 = time.perf_counter()
             with T.span("sdo.finalize"):
                 if root_only and self.world.rank != 0:
-                    # a peer: the root answers; finalize an empty slice (host only: the schema)
-                    part = empty_partials(prog, torch.device("cpu"))
+                    # a peer: the root answers; finalize an empty slice for the schema (on the
+                    # device: device-resident FD / decode tables must not be copied to the host)
+                    part = empty_partials(prog, self.ds.device)
                 cols = finalize(prog, part, getattr(self, "out_types", None))
             t3 = time.perf_counter()
             with T.span("sdo.post"):
@@ -1174,7 +1175,7 @@ def execute_grouping_sets(engine, specs, ds, out_types=None) -> Optional[List[Qu
     root_only = engine.world.distributed and root_only_results()
     prog, part, _ = pq.run_partials(t0, root_only)
     if root_only and engine.world.rank != 0:
-        part = empty_partials(prog, torch.device("cpu"))  # rank 0 answers every set
+        part = empty_partials(prog, ds.device)  # rank 0 answers every set
     fp = part.compact()
     g = fp.keys.to(torch.int64)
     from .partials import merge_sparse

@@ -1787,13 +1787,16 @@ def pack(prog: ScanProgram, mode: int, dedup: int, hll_lds: int, lds_bytes: int,
     r = d[0]
     r["ncols"] = len(prog.cols)
     plane = 0
+    packed = getattr(prog, "packed", None) or {}
     for base, names in ((0, prog.fcols), (D.PAYLOAD_BASE, prog.pcols)):
         for j, name in enumerate(names):
             t = column_tensor(ds, name)
             meta, npl = col_meta(t, plane)
             plane += npl
             c = r["cols"][base + j]
-            c["ptr"], c["dtype"], c["meta"] = t.data_ptr(), dtype_code(t), meta
+            # the JIT kernel of this program reads the bit-packed copy (segment/packed.py)
+            ptr = packed[name].data.data_ptr() if name in packed else t.data_ptr()
+            c["ptr"], c["dtype"], c["meta"] = ptr, dtype_code(t), meta
     r["nfc"], r["npc"], r["nplanes"] = len(prog.fcols), len(prog.pcols), plane
     r["lds_cache_off"], r["lds_wave_bytes"], r["unroll"] = cache_off, wave_bytes, unroll
     if ds.device.type == "cuda":

@@ -309,6 +309,42 @@ static void module_launch(int h, uint64_t desc, int grid, int block, int lds, ui
         "jit kernel launch");
 }
 
+// One host call per execution of a prepared scan: the fused reset of its slot buffers, then the
+// specialized kernel (or the interpreter) -- the Python side caches every argument, so a small
+// query's launch path is a single pybind call (the per-call Python work showed as ~25 us of a
+// 0.2 ms query on the benchmark host).
+static void run_scan(uint64_t acc, uint64_t init, int64_t rows, int nslots, std::vector<uint64_t> zptr,
+                     std::vector<int64_t> zwords, uint64_t overflow, int jit, uint64_t desc, int grid, int block,
+                     int lds, int unroll, uint64_t stream) {
+  if (acc || !zptr.empty() || overflow) reset_bufs(acc, init, rows, nslots, zptr, zwords, overflow, stream);
+  if (jit >= 0) module_launch(jit, desc, grid, block, lds, stream);
+  else scan(desc, grid, block, lds, unroll, stream);
+}
+
+// Small dense result: HLL estimates of every register block (MFMA kernel) + the accumulator table
+// and the estimates copied into one pinned host buffer + a stream synchronisation, in one call with
+// the GIL released while the device works.
+static void fetch_small(uint64_t acc, int64_t acc_bytes, std::vector<uint64_t> hll, int64_t G, int p,
+                        uint64_t est_dev, uint64_t host, uint64_t stream) {
+  hipStream_t st = (hipStream_t)stream;
+  for (size_t i = 0; i < hll.size(); ++i) hll_estimate(hll[i], G, p, est_dev + i * (uint64_t)G * 8, stream);
+  {
+    py::gil_scoped_release nogil;
+    if (acc_bytes > 0) check(hipMemcpyAsync((void*)host, (const void*)acc, acc_bytes, hipMemcpyDeviceToHost, st),
+                             "fetch_small acc");
+    if (!hll.empty())
+      check(hipMemcpyAsync((void*)(host + acc_bytes), (const void*)est_dev, hll.size() * G * 8, hipMemcpyDeviceToHost,
+                           st),
+            "fetch_small est");
+    check(hipStreamSynchronize(st), "fetch_small sync");
+  }
+}
+
+static void stream_sync(uint64_t stream) {
+  py::gil_scoped_release nogil;
+  check(hipStreamSynchronize((hipStream_t)stream), "stream sync");
+}
+
 static int desc_size() { return (int)sizeof(sdo::ScanDesc); }
 
 static py::dict layout() {
@@ -364,6 +400,9 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("rtc_compile", &rtc_compile);
   m.def("module_load", [](py::bytes code, const std::string& name) { return module_load(std::string(code), name); });
   m.def("module_launch", &module_launch);
+  m.def("run_scan", &run_scan);
+  m.def("fetch_small", &fetch_small);
+  m.def("stream_sync", &stream_sync);
   m.def("glds_probe", &glds_probe);
   m.def("layout", &layout);
   m.def("device_info", &device_info);

@@ -43,7 +43,13 @@ class ColInfo:
     lg: int
     sgn: bool
     flt: bool
-    plane: int
+    plane: int     # LDS staging plane (-1: bit-packed, always loaded into registers)
+    pw: int = 0    # bit-packed width (segment/packed.py); 0 = plain column
+    pbase: int = 0
+
+# bit-packed loads as one 8-byte buffer load at a dword-aligned offset (needs the unaligned
+# access mode) instead of two dword loads
+PK_X2 = os.environ.get("SDO_PK_X2", "0") != "0"
 
 
 @dataclass
@@ -67,6 +73,8 @@ def pipe_eligible(prog, mode: int, U: int) -> bool:
         return False
     if any(a.get("filt_len") or a.get("filter") is not None for a in prog.aops):
         return False
+    if getattr(prog, "packed", None):
+        return False
     cols = col_infos(prog)
     nld = sum(2 if c.lg == 3 else 1 for i, c in cols.items() if i >= D.PAYLOAD_BASE) * U
     return nld <= 63
@@ -77,10 +85,15 @@ def col_infos(prog) -> Dict[int, ColInfo]:
 
     out = {}
     plane = 0
+    packed = getattr(prog, "packed", None) or {}
     for base, names in ((0, prog.fcols), (D.PAYLOAD_BASE, prog.pcols)):
         for j, name in enumerate(names):
             t = column_tensor(prog.ds, name)
             lg = {1: 0, 2: 1, 4: 2, 8: 3}[t.element_size()]
+            pk = packed.get(name)
+            if pk is not None:
+                out[base + j] = ColInfo(name, base + j, lg, False, False, -1, pk.width, pk.base)
+                continue
             out[base + j] = ColInfo(name, base + j, lg, t.dtype in (torch.int16, torch.int32, torch.int64),
                                     t.dtype.is_floating_point, plane)
             plane += 2 if lg == 3 else 1
@@ -126,7 +139,7 @@ MAX_NCOPY = int(os.environ.get("SDO_JIT_NCOPY", "16"))
 def layout(prog, mode: int, U: int, hll_lds: bool, m: int, reg: bool = False, pipe: bool = False,
            budget: int = 150 * 1024, regstage: bool = False, shared: bool = False) -> JitLayout:
     cols = col_infos(prog)
-    nplanes = 0 if regstage else sum(2 if c.lg == 3 else 1 for c in cols.values())
+    nplanes = 0 if regstage else sum(2 if c.lg == 3 else 1 for c in cols.values() if not c.pw)
     need_bmw = _needs_word_bitmaps(prog)
     wave_bytes = U * nplanes * 256 * (2 if pipe else 1) + (len(prog.bm_leaves) * 512 if need_bmw else 0)
     wave_bytes = (wave_bytes + 15) // 16 * 16
@@ -160,7 +173,7 @@ def prefer_regstage(prog) -> bool:
     if prog.filter_len and not prog.final_pre:
         return False
     cols = col_infos(prog)
-    return sum(1 << c.lg for i, c in cols.items() if i >= D.PAYLOAD_BASE) > 4
+    return sum((c.pw / 8) if c.pw else (1 << c.lg) for i, c in cols.items() if i >= D.PAYLOAD_BASE) > 4
 
 
 def _needs_word_bitmaps(prog) -> bool:
@@ -201,12 +214,14 @@ class _Gen:
         self.lay = lay
         self.m = m
         self.cols = col_infos(prog)
-        self.NP = sum(2 if c.lg == 3 else 1 for c in self.cols.values())
+        self.NP = sum(2 if c.lg == 3 else 1 for c in self.cols.values() if not c.pw)
         self.pre_lines: List[str] = []  # kernel-entry pointer loads
 
     # ---------------------------------------------------------------- values
     def ival(self, idx: int) -> str:
         c = self.cols[idx]
+        if c.pw:
+            return f"(pk_field<{c.pw}>(xp{idx}[u], psh{c.pw}) + {_lit(c.pbase)})"
         if self.regstage:
             return f"cv_int<{c.lg}, {'true' if c.sgn else 'false'}, {'true' if c.flt else 'false'}>(x{idx}[u])"
         return (f"ld_int<{c.lg}, {'true' if c.sgn else 'false'}, {'true' if c.flt else 'false'}, {self.n4}>"
@@ -214,6 +229,8 @@ class _Gen:
 
     def dval(self, idx: int) -> str:
         c = self.cols[idx]
+        if c.pw:
+            return f"((double){self.ival(idx)})"
         if self.regstage:
             return f"cv_dbl<{c.lg}, {'true' if c.sgn else 'false'}, {'true' if c.flt else 'false'}>(x{idx}[u])"
         return (f"ld_dbl<{c.lg}, {'true' if c.sgn else 'false'}, {'true' if c.flt else 'false'}, {self.n4}>"
@@ -322,6 +339,19 @@ class _Gen:
         (``rs<i>``) -- into VGPR arrays ``x<i>[u]`` (register staging) or LDS planes (DMA);
         ``wl`` names the per-u word-in-chunk array."""
         U, NP = self.U, self.NP
+        pk = [i for i in cols if self.cols[i].pw]
+        cols = [i for i in cols if not self.cols[i].pw]
+        if pk:  # bit-packed columns: straight into registers in either staging mode
+            x2 = "true" if PK_X2 else "false"
+            for i in pk:
+                o.append(f"{ind}uint64_t xp{i}[{U}];")
+            o.append(f"#pragma unroll\n{ind}for (int u = 0; u < {U}; ++u) {{")
+            for i in pk:
+                c = self.cols[i]
+                o.append(f"{ind}  xp{i}[u] = ld_pk<{x2}>(rs{i}, (uint32_t){wl}[u] * {8 * c.pw}u, pko{c.pw});")
+            o.append(f"{ind}}}")
+        if not cols:
+            return
         if self.regstage:
             for i in cols:
                 o.append(f"{ind}{'uint64_t' if self.cols[i].lg == 3 else 'uint32_t'} x{i}[{U}];")
@@ -542,8 +572,13 @@ class _Gen:
         out.append("  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];")
         out.append("  const int lane = threadIdx.x & 63;")
         out.append("  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);")
-        for lg in sorted({c.lg for c in self.cols.values()}):
+        for lg in sorted({c.lg for c in self.cols.values() if not c.pw}):
             out.append(f"  const uint32_t lo{lg} = (uint32_t)lane << {lg};")
+        for w in sorted({c.pw for c in self.cols.values() if c.pw}):
+            # lane l's field of a packed word: bits [l*W, l*W + W), read through the 8 bytes at the
+            # dword holding its first bit
+            out.append(f"  const uint32_t pko{w} = (((uint32_t)lane * {w}u) >> 5) * 4u;")
+            out.append(f"  const uint32_t psh{w} = ((uint32_t)lane * {w}u) & 31u;")
         out.append(f"  unsigned char* wb = lds + {lay.cache_off} + wave * {lay.wave_bytes};")
         stage_bytes = 0 if self.regstage else U * NP * 256 * (2 if self.pipe else 1)
         out.append(f"  uint64_t* bmw = (uint64_t*)(wb + {stage_bytes});")
@@ -600,7 +635,10 @@ class _Gen:
         out.append(f"    const int64_t crows = num_rows - crow0 < {D.CHUNK_ROWS} ? num_rows - crow0 : {D.CHUNK_ROWS};")
         staged = (fcols if word_filter is not None else []) + (pcols if mode != D.M_MASK else [])
         for i in staged:
-            out.append(f"    const __amdgpu_buffer_rsrc_t rs{i} = chunk_rsrc(c{i}, crow0, crows, {self.cols[i].lg});")
+            if self.cols[i].pw:
+                out.append(f"    const __amdgpu_buffer_rsrc_t rs{i} = chunk_rsrc_pk(c{i}, kchunk, {self.cols[i].pw});")
+            else:
+                out.append(f"    const __amdgpu_buffer_rsrc_t rs{i} = chunk_rsrc(c{i}, crow0, crows, {self.cols[i].lg});")
         out.append("    const int64_t my_r0 = (cw0 + lane) * 64;")
         out.append("    const int64_t lo_off = clo - my_r0, hi_off = chi - my_r0;")
         out.append("    uint64_t pre = range_bits((int)(lo_off < 0 ? 0 : (lo_off > 64 ? 64 : lo_off)),")
@@ -757,4 +795,4 @@ class JitScan:
         from . import native
 
         native.load().module_launch(self.handle, desc.data_ptr(), int(grid), W * 64, int(self.lay.total),
-                                    torch.cuda.current_stream(desc.device).cuda_stream)
+                                    native._stream(desc.device))

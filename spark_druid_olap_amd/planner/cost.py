@@ -11,8 +11,9 @@ kernel, so the decisions are different, but the estimation machinery is the same
     input rows (``estimateOutputCardinality`` 691-716);
   * scan time: bytes streamed from HBM / bandwidth + launch overhead;
   * group-by table choice: dense LDS (fits the per-block LDS budget), dense global, or hash;
-  * merge: one-shot all_gather for small partials, per-op all_reduce for large dense ones, varlen
-    all_gather by key for sparse (hash) partials; priced by the xGMI ring model (7 links x ~153 GB/s).
+  * merge: one-shot all_gather for small partials, per-op all_reduce for large dense ones, a
+    hash-partitioned all-to-all plus a gather to rank 0 for sparse (hash) partials; priced by the
+    xGMI model (7 point-to-point links x ~153 GB/s per direction).
 """
 from __future__ import annotations
 
@@ -150,18 +151,26 @@ def estimate(ds, spec, info=None, world_size: int = 1) -> CostEstimate:
     else:
         mode = "hash"
     scan_s = nbytes / HBM_BW + LAUNCH_S
-    if world_size <= 1:
-        merge, merge_s = "none", 0.0
-    elif mode == "hash":
-        merge = "varlen-allgather(keys)"
-        merge_s = COLL_LAT_S * 2 + acc_bytes * (world_size - 1) / (7 * XGMI_LINK_BW)
-    elif acc_bytes <= 4 << 20:
-        merge = "oneshot-allgather"
-        merge_s = COLL_LAT_S + acc_bytes * (world_size - 1) / (7 * XGMI_LINK_BW)
-    else:
-        merge = "ring-allreduce"
-        merge_s = COLL_LAT_S + 2 * acc_bytes * (world_size - 1) / world_size / XGMI_LINK_BW
+    merge, merge_s = merge_cost_s(mode, acc_bytes, world_size)
     return CostEstimate(rows, sel, inp, out, nbytes, mode, merge, scan_s * 1e3, merge_s * 1e3)
+
+
+def merge_cost_s(mode: str, state_bytes: float, world_size: int):
+    """(merge path, seconds) of one cross-rank merge of a state of ``state_bytes`` per rank -- the
+    paths parallel/merge.py takes: sparse states go through one hash-partitioned all-to-all (each
+    rank sends (N-1)/N of its rows, each peer over its own xGMI link) and the merged slices to rank
+    0; small dense states one all-gather; large dense states a ring all-reduce."""
+    n = world_size
+    if n <= 1:
+        return "none", 0.0
+    links = min(7, n - 1)
+    if mode == "hash":
+        shuffle = state_bytes * (n - 1) / n / (links * XGMI_LINK_BW)
+        gather = state_bytes / (links * XGMI_LINK_BW)  # rank 0 takes in ~one state's worth of groups
+        return "alltoall-shuffle+gather-to-root", 4 * COLL_LAT_S + shuffle + gather
+    if state_bytes * n <= ONESHOT_MAX_BYTES:
+        return "oneshot-allgather", COLL_LAT_S + state_bytes * (n - 1) / (links * XGMI_LINK_BW)
+    return "ring-allreduce", 3 * COLL_LAT_S + 2 * state_bytes * (n - 1) / n / XGMI_LINK_BW
 
 
 def explain_cost(session, dq) -> str:
@@ -171,8 +180,14 @@ def explain_cost(session, dq) -> str:
         "DruidQuery cost ::",
         f"  rowsInInterval={c.rows_in_interval}  selectivity={c.selectivity:.4g}  inputRows={c.input_rows:.4g}",
         f"  outputRows={c.output_rows:.4g}  bytesScanned={c.bytes_scanned}",
-        f"  estScanMs={c.scan_ms:.4f}  estMergeMs={c.merge_ms:.4f}  gpus={session.engine.world.size}",
+        f"  estScanMs={c.scan_ms:.4f}  estMergeMs={c.merge_ms:.4f}  merge={c.merge}  gpus={session.engine.world.size}",
     ]
+    h = dq.info.get("historical")
+    lines.append(f"  method: {'broker' if not h else f'historical(segmentsPerQuery={h})'}"
+                 f"  [{dq.info.get('method_reason', '')}]")
+    mc = dq.info.get("method_costs")
+    if mc:
+        lines.append("  method costs: " + "  ".join(f"{k}={v:.4f}ms" for k, v in sorted(mc.items(), key=lambda kv: kv[1])))
     prep = getattr(dq, "_prepared", None)
     if prep is None:
         try:  # plan it now (EXPLAIN before the first execution)
@@ -193,36 +208,65 @@ def explain_cost(session, dq) -> str:
     return "\n".join(lines)
 
 
-def historical_cost_ms(ds, spec, segments_per_query: int, info=None) -> float:
-    """Segment-batched ("historical") execution: one scan launch + partial compaction per batch of
-    segments, then a merge of the partials (the reference's historical waves + Spark shuffle/agg,
-    ``asd/DruidQueryCostModel.scala:505-547``)."""
-    c = estimate(ds, spec, info)
+def broker_cost_ms(ds, spec, info=None, world_size: int = 1) -> float:
+    """One fused scan over every resident segment of the shard, then ONE cross-rank merge of the
+    whole state (not overlapped with anything)."""
+    return estimate(ds, spec, info, world_size).total_ms
+
+
+def historical_cost_ms(ds, spec, segments_per_query: int, info=None, world_size: int = 1) -> float:
+    """Segment-batched ("historical") execution (the reference's historical waves + Spark
+    shuffle/agg, ``asd/DruidQueryCostModel.scala:505-547``): B = segments / n scans, each followed
+    by a merge of that batch's partials that runs while the next batch scans
+    (``engine/executor.py _run_pipelined``), then a local combine of the B merged states.  The
+    executor merges every batch in the full dense layout, so each batch's merge moves the whole
+    state: pipelining pays only when one merge is shorter than one batch's scan, and even then
+    the last merge and B launches remain -- on one MI355X, and for dense states on xGMI, the
+    broker plan is never more expensive, which is what this model says."""
+    c = estimate(ds, spec, info, world_size)
     nseg = max(1, sum(1 for _ in ds.segments))
-    batches = math.ceil(nseg / max(1, segments_per_query))
-    per_batch_out = min(c.output_rows, c.input_rows / batches if batches else c.input_rows)
-    merge_bytes = batches * per_batch_out * (len(spec.aggregation_specs) + 2) * 8
-    return c.scan_ms + batches * LAUNCH_S * 1e3 + merge_bytes / HBM_BW * 1e3 * 4
+    batches = max(1, math.ceil(nseg / max(1, segments_per_query)))
+    s_b = c.scan_ms / batches + LAUNCH_S * 1e3
+    m_b = c.merge_ms
+    combine = batches * c.output_rows * (len(spec.aggregation_specs) + 2) * 8 / HBM_BW * 1e3
+    pipelined = s_b + (batches - 1) * max(s_b, m_b) + m_b
+    return pipelined + combine
 
 
-def choose_method(ds, spec, conf=None, info=None):
-    """Broker (None) or historical (segments per query).  On one MI355X the broker plan -- one
-    fused scan over every resident segment with the partials merged in LDS/HBM -- is never more
-    expensive than batching segments into several launches plus a merge, so the GPU cost model
-    picks broker unless the batched plan is estimated cheaper (it is not, for any batch count)."""
+@dataclass
+class MethodChoice:
+    segments_per_query: Optional[int]          # None = broker
+    costs: Dict[str, float] = field(default_factory=dict)
+
+    def describe(self) -> str:
+        alts = "  ".join(f"{k}={v:.4f}ms" for k, v in sorted(self.costs.items(), key=lambda kv: kv[1]))
+        m = "broker" if self.segments_per_query is None else f"historical(segmentsPerQuery={self.segments_per_query})"
+        return f"{m} {alts}"
+
+
+def choose_method_costed(ds, spec, conf=None, info=None, world_size: int = 1) -> MethodChoice:
+    """Broker vs historical and the segments per historical query, by the cheaper estimate
+    (``DruidQueryCostModel.druidQueryMethod``, ``asd/DruidQueryCostModel.scala:343-413``): the
+    broker plan against every n in 1..histSegsPerQueryLimit."""
     limit = 5
     if conf is not None:
         try:
             limit = int(conf.typed("spark.sparklinedata.druid.querycostmodel.histSegsPerQueryLimit"))
         except Exception:  # noqa: BLE001
             pass
-    broker = estimate(ds, spec, info).total_ms
-    best = None
+    costs = {"broker": broker_cost_ms(ds, spec, info, world_size)}
+    best, best_n = costs["broker"], None
     for n in range(1, max(1, limit) + 1):
-        h = historical_cost_ms(ds, spec, n, info)
-        if h < broker and (best is None or h < best[0]):
-            best = (h, n)
-    return None if best is None else best[1]
+        h = historical_cost_ms(ds, spec, n, info, world_size)
+        costs[f"historical(n={n})"] = h
+        if h < best:
+            best, best_n = h, n
+    return MethodChoice(best_n, costs)
+
+
+def choose_method(ds, spec, conf=None, info=None, world_size: int = 1):
+    """Segments per historical query, or None for broker (``choose_method_costed``)."""
+    return choose_method_costed(ds, spec, conf, info, world_size).segments_per_query
 
 
 # ================================================================================================

@@ -109,8 +109,15 @@ class IndexSpec:
             paths = sorted(glob.glob(os.path.join(base, fh.get("filter", "*"))))
         inp = io.get("inputSpec")
         if inp and inp.get("paths"):
+            # index_hadoop "static" input: comma-separated paths; a directory means its files that
+            # match ``filePattern`` (tools/spinup-tool/tpch1_configFiles/indexing/tpch_1_index_hadoop.json)
+            pat = inp.get("filePattern") or "*"
             for p in str(inp["paths"]).split(","):
-                paths += sorted(glob.glob(p.strip())) or [p.strip()]
+                p = p.strip()
+                if os.path.isdir(p):
+                    paths += sorted(f for f in glob.glob(os.path.join(p, pat)) if os.path.isfile(f))
+                else:
+                    paths += sorted(glob.glob(p)) or [p]
         tc = spec.get("tuningConfig", {})
         tps = (tc.get("partitionsSpec") or {}).get("targetPartitionSize")
         return IndexSpec(

@@ -696,28 +696,41 @@ class DruidRewriter:
                                     final[rid])
         q = S.GroupByQuerySpec(info.ds_name, dims, None, None, S.Granularity.parse("all"), filt, aggs, None,
                                intervals)
+        method = {}
         dq = P.DruidQuery(pf.table, q, columns, drefs, {"groupby": True, "noop_conds": pf.noop_conds,
-                                                         "historical": self._historical(pf, q)})
+                                                         "historical": self._historical(pf, q, method)})
+        dq.info.update(method)
         exprs = []
         for r in outs:
             if r.rid in final:
                 exprs.append(A.Alias(final[r.rid], r.name, r.rid))
         return P.Project(exprs, dq)
 
-    def _historical(self, pf: PF, q) -> Optional[int]:
+    def _historical(self, pf: PF, q, out: Optional[dict] = None) -> Optional[int]:
         """Broker vs historical execution (``asd/DruidStrategy.scala:324-332``).  With the cost model
-        on, the GPU cost model decides (planner/cost.py: ``choose_method``); with it off, the
-        relation's ``queryHistoricalServers`` / ``numSegmentsPerHistoricalQuery`` options (and their
-        ``spark.sparklinedata.druid.option.*`` session overrides) decide.  Returns segments per
-        historical query, or None for broker execution."""
-        from ..planner.cost import choose_method
+        on, the GPU cost model decides between broker and every segments-per-query up to the limit
+        (planner/cost.py ``choose_method_costed``, ``asd/DruidQueryCostModel.scala:343-413``); with
+        it off, the relation's ``queryHistoricalServers`` / ``numSegmentsPerHistoricalQuery`` options
+        (and their ``spark.sparklinedata.druid.option.*`` session overrides) decide.  Returns
+        segments per historical query, or None for broker execution; ``out`` receives the priced
+        alternatives and the reason (EXPLAIN DRUID REWRITE prints them)."""
+        from ..planner.cost import choose_method_costed
 
+        out = out if out is not None else {}
         opts = pf.table.info.options
+        wanted = opts.query_historical(self.conf)
+        nseg = max(1, min(opts.num_segments_per_query(self.conf), 1 << 30))
         if bool(self.conf.typed("spark.sparklinedata.druid.querycostmodel.enabled")):
-            return choose_method(pf.table.info.datasource, q, self.conf)
-        if not opts.query_historical(self.conf):
+            mc = choose_method_costed(pf.table.info.datasource, q, self.conf, pf.table.info,
+                                      self.session.engine.world.size)
+            out["method_costs"] = mc.costs
+            out["method_reason"] = (f"cost model (queryHistoricalServers={str(wanted).lower()}, "
+                                    f"numSegmentsPerHistoricalQuery={nseg} in the DDL)")
+            return mc.segments_per_query
+        out["method_reason"] = f"relation options queryHistoricalServers={str(wanted).lower()}"
+        if not wanted:
             return None
-        return max(1, min(opts.num_segments_per_query(self.conf), 1 << 30))
+        return nseg
 
     # -- grouping expressions ------------------------------------------------------------------
     def _dim_spec(self, pf: PF, e: A.Expr, out: str):

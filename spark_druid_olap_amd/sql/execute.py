@@ -165,10 +165,11 @@ class Executor:
         if prog is None:
             # compiled once per plan node: column passthroughs and numpy closures for the
             # arithmetic over Druid results (no per-run expression-tree dispatch)
-            prog = p._proj = [_compile_proj(e, r) for e, r in zip(p.exprs, p.output)]
+            p._out = list(p.output)
+            prog = p._proj = [_compile_proj(e, r) for e, r in zip(p.exprs, p._out)]
         fr = None
         cols = {}
-        refs = p.output
+        refs = p._out
         for (kind, x), e, r in zip(prog, p.exprs, refs):
             if kind == "ref":
                 cols[r.rid] = b.cols[x]
@@ -582,9 +583,25 @@ def druid_value_series(col, sqlt: str, kind: str, n: int) -> pd.Series:
         if not np.isnan(arr).any():
             return pd.Series(np.rint(arr).astype(np.int64))
         return to_series(pd.Series(arr), sqlt)
+    if arr.dtype.kind == "O" and bt in ("tinyint", "smallint", "int", "bigint") and len(arr):
+        try:  # digit strings of a numeric time format (year(...) -> 'yyyy'): one numpy cast
+            return fast_series(arr.astype(np.int64))
+        except (TypeError, ValueError):
+            pass
     if arr.dtype.kind == "O" and base(sqlt) != "string":
         return to_series(pd.Series(arr), sqlt)
     return to_series(pd.Series(arr), sqlt)
+
+
+def _categorical(codes: np.ndarray, dtype) -> pd.Categorical:
+    """A Categorical over validated codes of a cached dtype (pandas' internal constructor: the
+    public ``from_codes`` re-derives the code width and checks every code on each call)."""
+    try:
+        from pandas.core.dtypes.cast import coerce_indexer_dtype
+
+        return pd.Categorical._simple_new(coerce_indexer_dtype(codes, dtype.categories), dtype=dtype)
+    except Exception:  # noqa: BLE001  (pandas internals moved)
+        return pd.Categorical.from_codes(codes, dtype=dtype, validate=False)
 
 
 _FULL_DICT_MAX = 1 << 20
@@ -627,7 +644,7 @@ def _dict_series(col, sqlt: str) -> pd.Series:
             cdt = cache.get("__cdtype__")
             if cdt is None:
                 cdt = cache["__cdtype__"] = pd.CategoricalDtype(cats)
-            return fast_series(pd.Categorical.from_codes(c, dtype=cdt, validate=False))
+            return fast_series(_categorical(c, cdt))
         if full[0] == "numpy":
             return fast_series(full[1][codes])
         return pd.Series(full[1].array.take(codes))

@@ -207,3 +207,45 @@ def test_historical_segment_batches_native(gpu_ds, name):
     a = eng.execute(q, gpu_ds)
     b = eng.execute(q, gpu_ds, segments_per_query=9)
     assert_same(a, b, hll_cols=_hll_names(q), rtol=1e-9)
+
+
+def test_packed_columns_roundtrip_on_device(gpu_ds):
+    """segment/packed.py on the device shard: every integer column the kernels may read packs to
+    its exact bit width and decodes back to the resident column."""
+    from spark_druid_olap_amd.engine.lower import column_tensor
+    from spark_druid_olap_amd.segment import packed as PK
+    from spark_druid_olap_amd.segment.packed import packed_column, unpack
+
+    old, PK.ENABLED = PK.ENABLED, True
+    n = gpu_ds.num_rows
+    seen = 0
+    for name in list(gpu_ds.dims)[:12] + [m for m in gpu_ds.metrics][:8]:
+        pc = packed_column(gpu_ds, name)
+        if pc is None:
+            continue
+        seen += 1
+        t = column_tensor(gpu_ds, name)[:n].to(torch.int64)
+        assert pc.width < 8 * column_tensor(gpu_ds, name).element_size()
+        assert torch.equal(unpack(pc), t), name
+    PK.ENABLED = old
+    assert seen >= 5
+
+
+def test_packed_jit_matches_plain_jit(gpu_ds, kernel_path):
+    """The same headline query with the JIT reading bit-packed columns and plain columns."""
+    from spark_druid_olap_amd.models.bench_queries import bench_specs
+    from spark_druid_olap_amd.segment import packed as PK
+
+    if kernel_path != "jit":
+        pytest.skip("the interpreter never reads packed columns")
+    for name in ("TPCH Q1", "TPCH Q7", "TPCH Q3", "TPCH Q8"):
+        q = dict(bench_specs())[name]
+        old = PK.ENABLED
+        try:
+            PK.ENABLED = True
+            a = Engine(use_native=True).execute(q, gpu_ds)
+            PK.ENABLED = False
+            b = Engine(use_native=True).execute(q, gpu_ds)
+        finally:
+            PK.ENABLED = old
+        assert_same(a, b, hll_cols=_hll_names(q), rtol=1e-12)

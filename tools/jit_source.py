@@ -35,11 +35,26 @@ def main():
                 mode = {"dense-lds": D.M_DENSE_LDS, "dense-global": D.M_DENSE_GLOBAL, "hash": D.M_HASH}[gp.mode]
                 print(f"==== {name}: G={prog.G} keys={[(k.name, k.kind, k.card) for k in prog.keys]} "
                       f"slots={prog.slots} plan={gp.describe()}")
+                if os.environ.get("SDO_PACKED", "1") != "0":  # bit-packed columns (CPU copies here)
+                    from spark_druid_olap_amd.engine.lower import column_tensor
+                    from spark_druid_olap_amd.segment import packed as PK
+
+                    prog.packed = {}
+                    for c in list(prog.fcols) + list(prog.pcols):
+                        t = column_tensor(ds, c)
+                        if not t.is_floating_point():
+                            lo, hi = int(t[:ds.num_rows].min()), int(t[:ds.num_rows].max())
+                            if PK.worth_packing(t, PK.width_for(lo, hi)):
+                                prog.packed[c] = PK.pack(t, ds.num_rows, lo, hi)
                 regstage = jit.prefer_regstage(prog)
                 lay = jit.layout(prog, mode, 4, bool(prog.nhll) and gp.hll_lds, 1 << prog.hll_p, False, False,
                                  (160 * 1024) // 3 - 512, regstage, gp.shared)
                 g = jit._Gen(prog, mode, 4, bool(prog.nhll) and gp.hll_lds, True, lay, 1 << prog.hll_p)
-                print(g.source("sdo_jit_probe"))
+                src = g.source("sdo_jit_probe")
+                print(src)
+                if os.environ.get("SDO_JIT_COMPILE"):  # hipRTC for gfx950 (no GPU needed)
+                    code = jit.compile_code(src, "sdo_jit_probe")
+                    print(f"// compiled: {len(code)} bytes of gfx950 code object")
 
 
 if __name__ == "__main__":

@@ -7,8 +7,9 @@ from collections import defaultdict
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
 filt = sys.argv[2] if len(sys.argv) > 2 else "olap_scan"
+pat = sys.argv[3] if len(sys.argv) > 3 else "pmc*"   # run directories, e.g. pmcab_p1_*
 vals = defaultdict(list)
-for f in glob.glob(f"{root}/pmc*/**/*counter_collection.csv", recursive=True):
+for f in glob.glob(f"{root}/{pat}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         if filt in r.get("Kernel_Name", ""):
             vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
