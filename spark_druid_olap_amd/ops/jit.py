@@ -215,7 +215,8 @@ class _Gen:
         self.m = m
         self.cols = col_infos(prog)
         self.NP = sum(2 if c.lg == 3 else 1 for c in self.cols.values() if not c.pw)
-        self.pre_lines: List[str] = []  # kernel-entry pointer loads
+        self.pre_lines: List[str] = []  # kernel-entry pointer / constant loads
+        self._const_set = set()
 
     # ---------------------------------------------------------------- values
     def ival(self, idx: int) -> str:
@@ -236,6 +237,19 @@ class _Gen:
         return (f"ld_dbl<{c.lg}, {'true' if c.sgn else 'false'}, {'true' if c.flt else 'false'}, {self.n4}>"
                 f"({self.wbv} + (u * {self.NP} + {c.plane}) * 256, lane)")
 
+    # ---------------------------------------------------------------- query constants
+    # Filter bounds, zone bounds, key bases / cards / strides and expression constants are read
+    # from the descriptor (scalar loads once per kernel), not baked into the source: every
+    # parameterization of one query shape -- another date range, nation, segment -- reuses ONE
+    # compiled code object (a dashboard's distinct statements would otherwise each pay a hipRTC
+    # compile), and the source hash keys only the shape.
+    def const(self, name: str, expr: str, ctype: str = "int64_t") -> str:
+        line = f"const {ctype} {name} = {expr};"
+        if line not in self._const_set:
+            self._const_set.add(line)
+            self.pre_lines.append(line)
+        return name
+
     # ---------------------------------------------------------------- filters
     def word_expr(self, lo: int, hi: int) -> str:
         st: List[str] = []
@@ -249,8 +263,10 @@ class _Gen:
                 st.append(f"uniform64(bmw[{int(a)} * 64 + wl[u]])")
             elif op in (D.F_ID_RANGE, D.F_INT_RANGE):
                 cmp = "<" if op == D.F_ID_RANGE else "<="
+                fl = self.const(f"fl{i}", f"d->fops[{i}].lo")
+                fh = self.const(f"fh{i}", f"d->fops[{i}].hi")
                 st.append(f"([&]() {{ const int64_t v = {self.ival(col)}; "
-                          f"return (uint64_t)__ballot(v >= {_lit(a)} && v {cmp} {_lit(b)}); }}())")
+                          f"return (uint64_t)__ballot(v >= {fl} && v {cmp} {fh}); }}())")
             elif op == D.F_IN_SET:
                 self.pre_lines.append(f"const uint64_t* inset{i} = (const uint64_t*)d->fops[{i}].bits;")
                 st.append(f"([&]() {{ const int64_t v = {self.ival(col)}; "
@@ -258,14 +274,18 @@ class _Gen:
             elif op == D.F_FLT_RANGE:
                 lo_c = ">" if flags & 1 else ">="
                 hi_c = "<" if flags & 2 else "<="
+                fl = self.const(f"ff{i}", f"d->fops[{i}].flo", "double")
+                fh = self.const(f"fg{i}", f"d->fops[{i}].fhi", "double")
                 st.append(f"([&]() {{ const double v = {self.dval(col)}; "
-                          f"return (uint64_t)__ballot(v {lo_c} {_dlit(fa)} && v {hi_c} {_dlit(fb)}); }}())")
+                          f"return (uint64_t)__ballot(v {lo_c} {fl} && v {hi_c} {fh}); }}())")
             elif op == D.F_EXPR:
                 lo_c = ">" if flags & 1 else ">="
                 hi_c = "<" if flags & 2 else "<="
                 ev = self.expr(self.p.eops[int(a):int(a) + int(b)], int(a))
+                fl = self.const(f"ff{i}", f"d->fops[{i}].flo", "double")
+                fh = self.const(f"fg{i}", f"d->fops[{i}].fhi", "double")
                 st.append(f"([&]() {{ const double v = {ev}; "
-                          f"return (uint64_t)__ballot(v {lo_c} {_dlit(fa)} && v {hi_c} {_dlit(fb)}); }}())")
+                          f"return (uint64_t)__ballot(v {lo_c} {fl} && v {hi_c} {fh}); }}())")
             elif op in (D.F_AND, D.F_OR):
                 y, x = st.pop(), st.pop()
                 st.append(f"({x} {'&' if op == D.F_AND else '|'} {y})")
@@ -306,9 +326,10 @@ class _Gen:
                           f"[{self.ival(col)}])")
             elif op == D.E_COL:
                 v = self.dval(col)
-                st.append(f"({v} * {_dlit(c)})" if c != 0.0 else f"({v})")
+                st.append(f"({v} * {self.const(f'ec{off + j}', f'd->eops[{off + j}].c', 'double')})"
+                          if c != 0.0 else f"({v})")
             elif op == D.E_CONST:
-                st.append(f"({_dlit(c)})")
+                st.append(f"({self.const(f'ec{off + j}', f'd->eops[{off + j}].c', 'double')})")
             elif op == D.E_NEG:
                 st.append(f"(-{st.pop()})")
             elif op == D.E_ABS:
@@ -436,6 +457,8 @@ class _Gen:
         for z in range(len(p.zones)):
             L.append(f"  const int32_t* zmin{z} = (const int32_t*)d->zones[{z}].zmin;")
             L.append(f"  const int32_t* zmax{z} = (const int32_t*)d->zones[{z}].zmax;")
+            L.append(f"  const int64_t zlo{z} = d->zones[{z}].lo;")
+            L.append(f"  const int64_t zhi{z} = d->zones[{z}].hi;")
         for ai, a in enumerate(p.aops):
             if a["kind"] == D.A_HLL:
                 if self.hll_lds and mode == D.M_DENSE_LDS:
@@ -468,26 +491,34 @@ class _Gen:
         body.append("        uint64_t key = 0;")
         for k, kc in enumerate(p.keys):
             v = self.ival(kc.col_idx)
+            # stride / base / card from the descriptor (query constants); for LDS tables the
+            # layout (G) is part of the shape anyway
+            ks = self.const(f"ks{k}", f"(uint64_t)d->kops[{k}].stride", "uint64_t")
+            kb = self.const(f"kb{k}", f"d->kops[{k}].base")
+            kn = self.const(f"kn{k}", f"d->kops[{k}].card")
             if kc.kind == D.K_ID and kc.base:  # shard-local key window (engine/executor.py ShardWindow)
-                body.append(f"        key += (uint64_t)((int64_t)({v}) - {_lit(kc.base)}) * {kc.stride}ull;")
+                body.append(f"        key += (uint64_t)((int64_t)({v}) - {kb}) * {ks};")
             elif kc.kind == D.K_ID:
-                body.append(f"        key += (uint64_t)({v}) * {kc.stride}ull;")
+                body.append(f"        key += (uint64_t)({v}) * {ks};")
             elif kc.kind == D.K_REMAP:
-                body.append(f"        key += (uint64_t)rm{k}[{v}] * {kc.stride}ull;")
+                body.append(f"        key += (uint64_t)rm{k}[{v}] * {ks};")
             elif kc.kind == D.K_TIME and getattr(kc, "tlut", None) is not None:
                 n = len(kc.tlut)  # precomputed key per raw time value (engine/lower.py _attach_time_lut)
                 body.append(f"        {{ int64_t i_ = (int64_t)({v}) - {_lit(kc.tlut_lo)};")
                 body.append(f"          i_ = i_ < 0 ? 0 : (i_ >= {n} ? {n - 1} : i_);")
-                body.append(f"          key += (uint64_t)rm{k}[i_] * {kc.stride}ull; }}")
+                body.append(f"          key += (uint64_t)rm{k}[i_] * {ks}; }}")
             elif kc.kind == D.K_TIME:
+                ktz = self.const(f"ktz{k}", f"d->kops[{k}].tz_ms")
+                kpm = self.const(f"kpm{k}", f"d->kops[{k}].period_ms")
+                kor = self.const(f"kor{k}", f"d->kops[{k}].origin_ms")
                 body.append(f"        {{ int64_t t = time_field_t<{kc.tfield}>(({v}) * {_lit(p.ds.time_unit_ms)} + "
-                            f"{_lit(kc.tz_ms)}, {_lit(kc.period_ms or 1)}, {_lit(kc.origin_ms)}) - {_lit(kc.base)};")
-                body.append(f"          t = t < 0 ? 0 : (t >= {_lit(kc.card)} ? {_lit(kc.card - 1)} : t);")
-                body.append(f"          key += (uint64_t)t * {kc.stride}ull; }}")
+                            f"{ktz}, {kpm}, {kor}) - {kb};")
+                body.append(f"          t = t < 0 ? 0 : (t >= {kn} ? {kn} - 1 : t);")
+                body.append(f"          key += (uint64_t)t * {ks}; }}")
             else:
-                body.append(f"        {{ int64_t t = ({v}) - {_lit(kc.base)};")
-                body.append(f"          t = t < 0 ? 0 : (t >= {_lit(kc.card)} ? {_lit(kc.card - 1)} : t);")
-                body.append(f"          key += (uint64_t)t * {kc.stride}ull; }}")
+                body.append(f"        {{ int64_t t = ({v}) - {kb};")
+                body.append(f"          t = t < 0 ? 0 : (t >= {kn} ? {kn} - 1 : t);")
+                body.append(f"          key += (uint64_t)t * {ks}; }}")
         body.append("        key_[u] = key;")
         for ai, a in enumerate(p.aops):
             kind = a["kind"]
@@ -629,7 +660,7 @@ class _Gen:
         out.append("    if (chi > num_rows) chi = num_rows;")
         out.append("    if (chi <= clo) continue;")
         for z, (dim, zlo, zhi) in enumerate(p.zones):
-            out.append(f"    if ((int64_t)zmax{z}[kchunk] < {_lit(zlo)} || (int64_t)zmin{z}[kchunk] >= {_lit(zhi)}) continue;")
+            out.append(f"    if ((int64_t)zmax{z}[kchunk] < zlo{z} || (int64_t)zmin{z}[kchunk] >= zhi{z}) continue;")
         out.append(f"    const int64_t cw0 = kchunk * {D.CHUNK_WORDS};")
         out.append(f"    const int64_t crow0 = kchunk * {D.CHUNK_ROWS};")
         out.append(f"    const int64_t crows = num_rows - crow0 < {D.CHUNK_ROWS} ? num_rows - crow0 : {D.CHUNK_ROWS};")

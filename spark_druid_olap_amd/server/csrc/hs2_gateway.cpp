@@ -366,6 +366,12 @@ class Gateway {
     done_cv_.notify_all();
   }
 
+  // identical queued statements execute once (on by default); off measures engine throughput
+  void set_coalesce(bool on) {
+    std::lock_guard<std::mutex> g(mu_);
+    coalesce_ = on;
+  }
+
   bool is_cancelled(int64_t id) {
     std::lock_guard<std::mutex> g(mu_);
     auto it = running_batches_.find(id);
@@ -675,7 +681,7 @@ class Gateway {
       auto pit = pending_.find(key);
       // a queued batch whose waiters all cancelled (or left) keeps its sticky cancel flag: a new
       // statement must not join it, or it would be reported 'cancelled' without ever cancelling
-      if (pit != pending_.end() && !pit->second->cancel) {
+      if (coalesce_ && pit != pending_.end() && !pit->second->cancel) {
         b = pit->second;
         ++stats_coalesced_;
       } else {
@@ -889,6 +895,7 @@ class Gateway {
   std::deque<std::shared_ptr<Batch>> queue_;
   std::unordered_map<std::string, Op> ops_;
   int64_t next_batch_ = 0;
+  bool coalesce_ = true;
   int64_t stats_statements_ = 0, stats_batches_ = 0, stats_coalesced_ = 0, stats_forwarded_ = 0;
   std::mt19937_64 rng_;
 };
@@ -907,5 +914,6 @@ PYBIND11_MODULE(_sdo_gateway, m) {
       .def("next_batch", &Gateway::next_batch)
       .def("finish_batch", &Gateway::finish_batch)
       .def("is_cancelled", &Gateway::is_cancelled)
+      .def("set_coalesce", &Gateway::set_coalesce)
       .def("stats", &Gateway::stats);
 }

@@ -161,6 +161,8 @@ class NativeHiveServer(HiveThriftServer):
     def start(self) -> "NativeHiveServer":
         mod = load_native()
         self._gw = mod.Gateway(self.host, self.port, self._forward)
+        # SDO_COALESCE=0: every statement executes (engine throughput, not result sharing)
+        self._gw.set_coalesce(os.environ.get("SDO_COALESCE", "1") != "0")
         self.port = self._gw.start()
         for i in range(self.nexec):
             t = threading.Thread(target=self._executor, daemon=True, name=f"hs2-exec-{i}")

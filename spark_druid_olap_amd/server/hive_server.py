@@ -325,7 +325,8 @@ class HiveThriftServer:
                     # a stream slot per execution; identical queued statements (same cached plan,
                     # i.e. same text + conf + database) execute once
                     co = sess.engine.coalescer()
-                    key = id(df) if sess.conf.typed("spark.sparklinedata.druid.planCache.enabled") else None
+                    key = id(df) if sess.conf.typed("spark.sparklinedata.druid.planCache.enabled") and \
+                        os.environ.get("SDO_COALESCE", "1") != "0" else None
                     pdf = co.run(key, lambda: df.to_pandas(token=op.token))
             # row-set encoding (host only) runs after the slot is released
             op.set_frame(df.columns, [t for _, t in df.schema], pdf)

@@ -94,11 +94,15 @@ def test_concurrent_clients(server):
         assert st["statements"] >= 24 and st["batches"] <= st["statements"]
 
 
-def test_native_gateway_batches_identical_waiting_statements(ds_small, df_small):
+@pytest.mark.parametrize("coalesce", ["1", "0"])
+def test_native_gateway_batches_identical_waiting_statements(ds_small, df_small, monkeypatch, coalesce):
     """With every executor busy, identical statements from different sessions that queue together
     execute once (one batch) and every client gets the full, correct result; a different statement
-    is its own batch."""
+    is its own batch.  SDO_COALESCE=0 turns the sharing off: every statement is its own execution
+    (what the concurrency benchmark's ``--coalesce off`` measures)."""
     import time as _t
+
+    monkeypatch.setenv("SDO_COALESCE", coalesce)
 
     from spark_druid_olap_amd.server.gateway import NativeHiveServer
 
@@ -144,7 +148,10 @@ def test_native_gateway_batches_identical_waiting_statements(ds_small, df_small)
         assert not errs, errs
         assert len(outs) == 6 and all([tuple(r) for r in o] == exp for o in outs)
         st = srv.stats()
-        assert before["coalesced"] >= 5 and st["batches"] == 2, (before, st)
+        if coalesce == "1":
+            assert before["coalesced"] >= 5 and st["batches"] == 2, (before, st)
+        else:
+            assert st["coalesced"] == 0 and st["batches"] == 7, (before, st)
     finally:
         srv.stop()
 

@@ -28,9 +28,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+WORKLOAD = "fixed"
+
+
 def queries():
+    """The statements the clients cycle through: the 8 benchmark queries (``fixed``), or
+    ``varied``: ~2,000 distinct parameterizations of the same 8 shapes -- random ship / order date
+    windows, nations, regions, market segments, part types -- so no two clients share a text by
+    construction and every execution is a real scan (identical-statement sharing cannot help)."""
     from spark_druid_olap_amd.models import tpch
 
+    if WORKLOAD == "varied":
+        return varied_queries()
     out = []
     for name, q in tpch.BENCH_QUERIES:
         if name == "TPCH Q3":
@@ -39,13 +48,67 @@ def queries():
     return out
 
 
-def _client_proc(pid, nthreads, nclients, start_q, out_q):
+def varied_queries(n: int = 2000, seed: int = 7):
+    import random
+
+    from spark_druid_olap_amd.models import tpch
+
+    T = tpch.T
+    rnd = random.Random(seed)
+    nations = ["ALGERIA", "ARGENTINA", "BRAZIL", "CANADA", "EGYPT", "ETHIOPIA", "FRANCE", "GERMANY", "INDIA",
+               "INDONESIA", "IRAN", "IRAQ", "JAPAN", "JORDAN", "KENYA", "MOROCCO", "MOZAMBIQUE", "PERU", "CHINA",
+               "ROMANIA", "SAUDI ARABIA", "VIETNAM", "RUSSIA", "UNITED KINGDOM", "UNITED STATES"]
+    regions = ["AFRICA", "AMERICA", "ASIA", "EUROPE", "MIDDLE EAST"]
+    segs = ["AUTOMOBILE", "BUILDING", "FURNITURE", "HOUSEHOLD", "MACHINERY"]
+    types = [f"{a} {b} {c}" for a in ("ECONOMY", "PROMO", "STANDARD") for b in ("ANODIZED", "BRUSHED", "PLATED")
+             for c in ("STEEL", "BRASS", "COPPER")]
+
+    def day(lo=1992, hi=1998):
+        return f"{rnd.randint(lo, hi)}-{rnd.randint(1, 12):02d}-{rnd.randint(1, 28):02d}"
+
+    shapes = [
+        ("ShipDate", lambda: f"select l_returnflag, l_linestatus, count(*) from {T} where l_shipdate >= '{day(1992, 1995)}' "
+                             f"and l_shipdate < '{day(1996, 1998)}' group by l_returnflag, l_linestatus"),
+        ("Q1-window", lambda: f"select l_returnflag, l_linestatus, count(*), sum(l_extendedprice), max(ps_supplycost), "
+                              f"avg(ps_availqty) from {T} where l_shipdate <= '{day(1996, 1998)}' "
+                              f"group by l_returnflag, l_linestatus"),
+        ("Q3", lambda: f"select o_orderkey, sum(l_extendedprice) as price, o_orderdate, o_shippriority from {T} "
+                       f"where c_mktsegment = '{rnd.choice(segs)}' and o_orderdate < '{day(1994, 1996)}' "
+                       f"and l_shipdate > '{day(1994, 1996)}' group by o_orderkey, o_orderdate, o_shippriority "
+                       f"order by price desc, o_orderdate limit 10"),
+        ("Q5", lambda: f"select s_nation, sum(l_extendedprice) from {T} where s_region = '{rnd.choice(regions)}' "
+                       f"and o_orderdate >= '{day(1993, 1995)}' and o_orderdate < '{day(1996, 1997)}' group by s_nation"),
+        ("Q7", lambda: (lambda a, b: f"select s_nation, c_nation, year(dateTime(`l_shipdate`)) as y, sum(l_extendedprice) "
+                                     f"from {T} where ((s_nation = '{a}' and c_nation = '{b}') or "
+                                     f"(c_nation = '{a}' and s_nation = '{b}')) group by s_nation, c_nation, "
+                                     f"year(dateTime(`l_shipdate`))")(*rnd.sample(nations, 2))),
+        ("Q8", lambda: f"select year(dateTime(`o_orderdate`)) as y, sum(l_extendedprice) from {T} "
+                       f"where c_region = '{rnd.choice(regions)}' and p_type = '{rnd.choice(types)}' "
+                       f"and o_orderdate >= '{day(1993, 1994)}' and o_orderdate <= '{day(1995, 1997)}' "
+                       f"group by year(dateTime(`o_orderdate`))"),
+        ("Nation-mix", lambda: f"select c_nation, count(*), sum(l_quantity) from {T} where s_nation = "
+                               f"'{rnd.choice(nations)}' and l_shipdate >= '{day()}' group by c_nation"),
+        ("Segment", lambda: f"select c_mktsegment, count(*), sum(l_extendedprice) from {T} where "
+                            f"p_type = '{rnd.choice(types)}' and o_orderdate < '{day()}' group by c_mktsegment"),
+    ]
+    out, seen = [], set()
+    while len(out) < n:
+        name, f = shapes[len(out) % len(shapes)]
+        q = " ".join(f().split())
+        if q not in seen:
+            seen.add(q)
+            out.append((name, q))
+    return out
+
+
+def _client_proc(pid, nthreads, nclients, start_q, out_q, workload="fixed"):
     import threading
 
     from spark_druid_olap_amd.server.hive_client import connect
 
-    global NCLIENTS
+    global NCLIENTS, WORKLOAD
     NCLIENTS = nclients
+    WORKLOAD = workload
     port, t_start, duration, interval = start_q.get()
 
     qs = queries()
@@ -71,8 +134,8 @@ def _client_proc(pid, nthreads, nclients, start_q, out_q):
                 if now > t_start + duration:
                     break
                 sched = now
-            name, sql = qs[i % len(qs)]
-            i += 1
+            name, sql = qs[(i * 7919) % len(qs)] if WORKLOAD == "varied" else qs[i % len(qs)]
+            i += NCLIENTS if WORKLOAD == "varied" else 1
             err = None
             try:
                 cur = conn.cursor().execute(sql)
@@ -117,7 +180,16 @@ def main():
     ap.add_argument("--server", default="native", choices=["native", "python"],
                     help="native C++ gateway (server/csrc/hs2_gateway.cpp) or the pure-Python server")
     ap.add_argument("--sample", default=None, help="write a sampling profile of the server threads here")
+    ap.add_argument("--workload", default="fixed", choices=["fixed", "varied"],
+                    help="fixed: the 8 benchmark texts; varied: ~2,000 distinct parameterizations")
+    ap.add_argument("--coalesce", default="on", choices=["on", "off"],
+                    help="off: every statement executes (identical queued statements are not shared)")
+    ap.add_argument("--prewarm", type=int, default=0,
+                    help="varied workload: plan + compile this many distinct texts before the clock starts")
     a = ap.parse_args()
+    global WORKLOAD
+    WORKLOAD = a.workload
+    os.environ["SDO_COALESCE"] = "1" if a.coalesce == "on" else "0"
     NCLIENTS = a.clients
     nthreads = max(1, a.clients // a.procs)
     nproc = max(1, a.clients // nthreads)
@@ -125,7 +197,8 @@ def main():
     ctx = mp.get_context("spawn")
     res_q = ctx.Queue()
     start_q = ctx.Queue()
-    ps = [ctx.Process(target=_client_proc, args=(i, nthreads, a.clients, start_q, res_q)) for i in range(nproc)]
+    ps = [ctx.Process(target=_client_proc, args=(i, nthreads, a.clients, start_q, res_q, a.workload))
+          for i in range(nproc)]
     for p in ps:
         p.start()
     import torch
@@ -150,9 +223,12 @@ def main():
         srv = HiveThriftServer(s, port=0).start()
     print(f"[conc] server up on {srv.port}: SF{a.sf:g} {ds.num_rows} rows on {dev} in {time.time() - t0:.1f}s",
           file=sys.stderr, flush=True)
-    # warm every query's plan + kernel once through the server
+    # warm every query's plan + kernel once through the server (varied: the kernel shapes, and
+    # --prewarm texts; the rest are planned on first sight, inside the measured window)
     with connect(port=srv.port) as c:
-        for _, sql in queries():
+        qs = queries()
+        warm = qs if a.workload == "fixed" else qs[:max(len(qs) and 8, a.prewarm)]
+        for _, sql in warm:
             c.cursor().execute(sql).fetchall()
     interval = (a.clients / a.qps) if a.qps > 0 else 0.0
     t_start = time.time() + 1.0 + a.warmup
@@ -194,10 +270,12 @@ def main():
     lat = [(r[2] - r[1]) * 1e3 for r in res if not r[4]]
     span = max((r[2] for r in res), default=t_start) - t_start
     per = {}
-    for name, _ in queries():
+    for name in dict(queries()):
         xs = [(r[2] - r[1]) * 1e3 for r in res if r[0] == name and not r[4]]
         per[name] = {"n": len(xs), "p50_ms": pct(xs, 50), "p99_ms": pct(xs, 99)}
     out = {"metric": "thrift_concurrent_latency", "clients": nproc * nthreads, "target_qps": a.qps,
+           "workload": a.workload, "coalesce": a.coalesce, "distinct_texts": len(qs),
+           "executions_per_s": round((ex1 - ex0) / a.duration, 2),
            "achieved_qps": round(len(lat) / span, 2) if span > 0 else None, "queries": len(res),
            "errors": len(errs), "p50_ms": pct(lat, 50), "p90_ms": pct(lat, 90), "p99_ms": pct(lat, 99),
            "max_ms": max(lat) if lat else None, "sf": a.sf, "device": dev, "per_query": per,
