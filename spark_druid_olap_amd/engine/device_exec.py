@@ -53,7 +53,7 @@ def _attach_packed(prog) -> None:
             prog.packed[name] = pc
 
 
-def _jit_for(prog, mode: int, hll_lds: bool, m: int, shared: bool = False):
+def _jit_for(prog, mode: int, hll_lds: bool, m: int, shared: bool = False, part_phase: int = 0):
     """Specialized kernel for this program shape (None -> use the interpreter, plain columns)."""
     if not USE_JIT:
         prog.packed = {}
@@ -62,13 +62,13 @@ def _jit_for(prog, mode: int, hll_lds: bool, m: int, shared: bool = False):
 
     if getattr(prog, "packed", None) is None:
         _attach_packed(prog)
-    js = _jit_build(prog, mode, hll_lds, m, shared)
+    js = _jit_build(prog, mode, hll_lds, m, shared, part_phase)
     if js is None:
         prog.packed = {}  # the interpreter reads the plain columns
     return js
 
 
-def _jit_build(prog, mode: int, hll_lds: bool, m: int, shared: bool = False):
+def _jit_build(prog, mode: int, hll_lds: bool, m: int, shared: bool = False, part_phase: int = 0):
     from ..ops import jit
 
     nplanes = sum(2 if column_tensor_size(prog, c) == 8 else 1 for c in prog.cols)
@@ -89,7 +89,7 @@ def _jit_build(prog, mode: int, hll_lds: bool, m: int, shared: bool = False):
                                         or U == prefs[-1]):
                 try:
                     return jit.JitScan(prog, mode, U, hll_lds, m, bool(native.narrow4()), reg=reg, pipe=pipe,
-                                       budget=budget, regstage=regstage, shared=shared)
+                                       budget=budget, regstage=regstage, shared=shared, part_phase=part_phase)
                 except Exception as e:  # pragma: no cover - compile problems fall back loudly
                     import warnings
 
@@ -135,7 +135,8 @@ class PreparedScan:
 
         self.plan = plan_groupby(prog, USE_JIT, dense_max is not None)
         if mode is None:
-            mode = {"dense-lds": D.M_DENSE_LDS, "dense-global": D.M_DENSE_GLOBAL, "hash": D.M_HASH}[self.plan.mode]
+            mode = {"dense-lds": D.M_DENSE_LDS, "dense-global": D.M_DENSE_GLOBAL, "hash": D.M_HASH,
+                    "partitioned": D.M_PART}[self.plan.mode]
             self.shared = self.plan.shared
             self.hll_lds = 1 if self.plan.hll_lds else 0
         self.mode = mode
@@ -151,6 +152,20 @@ class PreparedScan:
         else:
             self.cap = 0
         self.jit = None
+        self.jit_scatter = None
+        self.part = None
+        if mode == D.M_PART and not prog.empty:
+            # radix-partitioned group-by (ops/csrc/partition.hip): count + scatter JIT producers
+            self.jit = _jit_for(prog, D.M_PART, False, self.m, part_phase=0)
+            self.jit_scatter = _jit_for(prog, D.M_PART, False, self.m, part_phase=1) if self.jit else None
+            if self.jit_scatter is None:
+                self.jit = None
+                mode = D.M_DENSE_GLOBAL  # no JIT: the HBM table with atomics
+            else:
+                self.part = part_layout(prog)
+        elif mode == D.M_PART:
+            mode = D.M_DENSE_GLOBAL
+        self.mode = mode
         # existence-only dense HBM scan on one GPU: one byte per group (150M order groups -> 150 MB,
         # which stays in the 256 MB Infinity Cache) instead of an 8-byte counter row
         self.pres_bytes = bool(mode == D.M_DENSE_GLOBAL and self.plan.presence_bytes)
@@ -160,7 +175,7 @@ class PreparedScan:
         # the touched rows are re-initialised after the run (no full-table fill per execution)
         self.touch = bool(mode == D.M_DENSE_GLOBAL and self.plan.touch and not self.pres_bytes)
         prog.touch_table = self.touch
-        if not prog.empty:
+        if not prog.empty and mode != D.M_PART:
             # the JIT keeps LDS registers one byte each (hll_update8)
             jit_hll_lds = bool(prog.nhll) and mode == D.M_DENSE_LDS and hll_bytes // 4 <= LDS_BUDGET \
                 and not self.shared
@@ -238,11 +253,14 @@ class PreparedScan:
                  [h.data_ptr() for h in b.hll], hll_offs,
                  unroll=UNROLL, cache_off=cache_off, wave_bytes=wave_bytes)
         self.lds_total = total
-        b.desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
         self.grid = _grid(dev, int(d[0]["total_chunks"]), self.jit.lay.total if self.jit else total)
+        b.part = None
+        if self.mode == D.M_PART:
+            b.part = self._part_bufs(d)
+        b.desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
         b.run_args = b.noreset_args = None
         b.fetch = None
-        if self.mode != D.M_HASH:
+        if self.mode not in (D.M_HASH, D.M_PART):
             # the whole launch path of one execution as cached arguments of ONE native call
             # (ops/csrc/bindings.cpp run_scan): fused reset of this slot's buffers + the kernel
             zeros = list(b.hll) + ([b.touch] if self.touch else []) + ([b.acc] if self.pres_bytes else [])
@@ -257,6 +275,58 @@ class PreparedScan:
                               b.overflow.data_ptr()) + tail
                 b.noreset_args = (0, 0, 0, 0, [], [], 0) + tail
         return b
+
+    def _part_bufs(self, d) -> dict:
+        """Record / count / offset buffers of the partitioned group-by for this slot; fills the
+        descriptor's part_* fields (level-1 buckets, written by the JIT producers)."""
+        L, prog, dev = self.part, self.prog, self.dev
+        u32 = torch.int32
+        cap = int(prog.ds.num_rows)  # records <= rows of the shard (one per qualifying row)
+        if cap * L["rw"] >= (1 << 32) or cap >= (1 << 32):
+            raise RuntimeError("partitioned group-by: shard too large for u32 record offsets")
+        P1, nsub = L["p1"], L["nsub"]
+        pb = {
+            "recs1": torch.empty(max(1, cap * L["rw"]), dtype=u32, device=dev),
+            "counts1": torch.empty(P1 * self.grid, dtype=u32, device=dev),
+            "totals1": torch.empty(P1, dtype=u32, device=dev),
+            "base1": torch.empty(P1 + 1, dtype=u32, device=dev),
+        }
+        if L["levels"] == 2:
+            pb["recs2"] = torch.empty_like(pb["recs1"])
+            pb["counts2"] = torch.empty(nsub * L["k"], dtype=u32, device=dev)
+            pb["totals2"] = torch.empty(nsub, dtype=u32, device=dev)
+            pb["base2"] = torch.empty(nsub + 1, dtype=u32, device=dev)
+        d[0]["part_recs"] = pb["recs1"].data_ptr()
+        d[0]["part_counts"] = pb["counts1"].data_ptr()
+        d[0]["part_base"] = pb["base1"].data_ptr()
+        d[0]["part_shift"] = L["shift1"]
+        d[0]["part_n"] = P1
+        return pb
+
+    def _run_part(self, b: "_Bufs") -> None:
+        """count -> bucket offsets -> scatter -> [split by the next bits] -> LDS aggregation into the
+        dense table (every row of it written: no reset)."""
+        L, nat, st = self.part, native.load(), native._stream(self.dev)
+        pb = b.part
+        prog = self.prog
+        W = BLOCK
+        nat.module_launch(self.jit.handle, b.desc.data_ptr(), int(self.grid), W, int(self.jit.lay.total), st)
+        nat.part_scan(pb["counts1"].data_ptr(), L["p1"], int(self.grid), pb["totals1"].data_ptr(),
+                      pb["base1"].data_ptr(), st)
+        nat.module_launch(self.jit_scatter.handle, b.desc.data_ptr(), int(self.grid), W,
+                          int(self.jit_scatter.lay.total), st)
+        recs, base = pb["recs1"], pb["base1"]
+        if L["levels"] == 2:
+            args = (pb["recs1"].data_ptr(), L["rw"], pb["base1"].data_ptr(), L["p1"], L["k"], L["shift"], L["p2"],
+                    pb["counts2"].data_ptr())
+            nat.part_split(*args, 0, 0, 0, st)
+            nat.part_scan(pb["counts2"].data_ptr(), L["nsub"], L["k"], pb["totals2"].data_ptr(),
+                          pb["base2"].data_ptr(), st)
+            nat.part_split(*args, pb["base2"].data_ptr(), pb["recs2"].data_ptr(), 1, st)
+            recs, base = pb["recs2"], pb["base2"]
+        nat.part_agg(recs.data_ptr(), L["rw"], base.data_ptr(), L["nsub"], int(prog.G), L["shift"],
+                     [f[0] for f in L["fields"]], [f[1] for f in L["fields"]], [int(op) for op, _ in prog.slots],
+                     [int(init) for _, init in prog.slots], b.acc.data_ptr(), st)
 
     def _launch(self, b: "_Bufs"):
         if self.jit is not None:
@@ -303,6 +373,8 @@ class PreparedScan:
             if b.run_args is not None:
                 native.run_scan(*(b.noreset_args if (self.touch and b.clean) else b.run_args),
                                 native._stream(self.dev))
+            elif self.mode == D.M_PART:
+                self._run_part(b)
             else:
                 self._reset(b)
                 self._launch(b)
@@ -356,7 +428,7 @@ class PreparedScan:
 class _Bufs:
     """One execution slot's device buffers for a prepared scan."""
     __slots__ = ("cap", "rows", "init_row", "acc", "keys", "hll", "overflow", "desc", "touch", "clean", "run_args",
-                 "noreset_args", "fetch")
+                 "noreset_args", "fetch", "part")
 
 
 class PreparedMask:
@@ -411,6 +483,35 @@ class PreparedMask:
         else:
             native.scan(desc, self.grid, BLOCK, self.lds_total, UNROLL)
         return native.compact_rows(mask)
+
+
+PART_TABLE_BYTES = int(os.environ.get("SDO_PART_TABLE_BYTES", 32 << 10))  # LDS table per sub-bucket
+
+
+def part_layout(prog) -> dict:
+    """Bucket geometry of the partitioned group-by for G keys: sub-buckets of 2^shift keys whose
+    table (2^shift x nslots x 8 B) fits PART_TABLE_BYTES of LDS; the remaining key bits split
+    over one level (<= 2^10 buckets) or two (level 1 <= 2^10 buckets, each split into P2 by K blocks)."""
+    from ..ops import jit
+
+    ns = max(1, prog.nslots)
+    shift = max(0, int(math.floor(math.log2(max(8, PART_TABLE_BYTES // (8 * ns))))))
+    gbits = max(1, int(math.ceil(math.log2(max(2, prog.G)))))
+    rem = max(0, gbits - shift)
+    fields = jit.part_fields(prog)
+    rw = 1 + sum(w for _, w in fields)
+    if rem <= 10:
+        p1 = 1 << rem
+        return {"levels": 1, "shift": shift, "shift1": shift, "p1": p1, "p2": 1, "k": 1, "nsub": p1,
+                "fields": fields, "rw": rw}
+    b1 = min(10, (rem + 1) // 2)
+    b2 = rem - b1
+    if b2 > 14:
+        raise ValueError(f"partitioned group-by: {prog.G} keys need more than two levels")
+    p1, p2 = 1 << b1, 1 << b2
+    k = max(1, min(64, 4096 // p1))
+    return {"levels": 2, "shift": shift, "shift1": shift + b2, "p1": p1, "p2": p2, "k": k, "nsub": p1 * p2,
+            "fields": fields, "rw": rw}
 
 
 def _grid(dev: torch.device, total_chunks: int, lds_total: int) -> int:

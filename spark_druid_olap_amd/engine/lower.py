@@ -123,6 +123,17 @@ def b_not(x):
 
 
 # =================================================================================== extraction
+def _fn_key(fn) -> Optional[str]:
+    """Cache key of an extraction function: its Druid JSON (JavaScript functions carry their
+    source, which the SQL planner generates from the grouping expression)."""
+    try:
+        import json
+
+        return json.dumps(fn.to_json(), sort_keys=True, default=str)
+    except Exception:  # noqa: BLE001
+        return None
+
+
 def extraction_callable(fn) -> Callable[[Any], Any]:
     """Python callable for a Druid extraction function (evaluated over a dictionary)."""
     if fn is None:
@@ -806,19 +817,31 @@ class Lowerer:
             return KeyComp(name, D.K_ID, dim, len(d), decoder=lambda ids, _d=d: DictColumn(ids, _d), dictionary=d)
         if isinstance(fn, S.TimeFormatExtractionFunctionSpec) and d.vtype != "string":
             pass
-        pv = getattr(fn, "_pyvec", None)
-        if pv is not None:  # vectorised dictionary-domain extraction (SQL planner)
-            derived = np.asarray(pv(d.all_values()), dtype=object)
-        else:
-            derived = d.map_values(extraction_callable(fn))
-        vals = derived.tolist()
-        uniq = sorted({v for v in vals if v is not None}, key=lambda v: (str(type(v)), v))
-        has_null = any(v is None for v in vals)
-        numeric = all(isinstance(v, (int, float)) and not isinstance(v, bool) for v in uniq)
-        # non-numeric, non-string derived values (dates, timestamps, booleans) keep their Python objects
-        dd = Dictionary(uniq, "double" if numeric and uniq else "string", has_null)
-        pos = {v: i + (1 if has_null else 0) for i, v in enumerate(uniq)}
-        remap = np.array([0 if v is None else pos[v] for v in vals], dtype=np.int32)
+        # the derived dictionary + id remap depend only on (dictionary, extraction function): cached
+        # on the dictionary, so every statement of one shape -- a dashboard's parameterizations --
+        # maps the dictionary domain once (the Joda formatting of 2,400 dates was ~65 ms a query)
+        ck = _fn_key(fn)
+        cache = d.__dict__.setdefault("_derived_keys", {}) if ck is not None else None
+        hit = cache.get(ck) if cache is not None else None
+        if hit is None:
+            pv = getattr(fn, "_pyvec", None)
+            if pv is not None:  # vectorised dictionary-domain extraction (SQL planner)
+                derived = np.asarray(pv(d.all_values()), dtype=object)
+            else:
+                derived = d.map_values(extraction_callable(fn))
+            vals = derived.tolist()
+            uniq = sorted({v for v in vals if v is not None}, key=lambda v: (str(type(v)), v))
+            has_null = any(v is None for v in vals)
+            numeric = all(isinstance(v, (int, float)) and not isinstance(v, bool) for v in uniq)
+            # non-numeric, non-string derived values (dates, timestamps, booleans) keep their Python objects
+            dd = Dictionary(uniq, "double" if numeric and uniq else "string", has_null)
+            pos = {v: i + (1 if has_null else 0) for i, v in enumerate(uniq)}
+            remap = np.array([0 if v is None else pos[v] for v in vals], dtype=np.int32)
+            remap.setflags(write=False)
+            hit = (dd, remap)
+            if cache is not None:
+                cache[ck] = hit
+        dd, remap = hit
         return KeyComp(name, D.K_REMAP, dim, len(dd), remap=remap, decoder=lambda ids, _d=dd: DictColumn(ids, _d))
 
     def _metric_range(self, metric: str) -> Tuple[int, int]:

@@ -48,6 +48,16 @@ __global__ void topk_keep_kernel(const int64_t* acc, int64_t n, int nslots, int 
 __global__ void hll_pairs_kernel(const int64_t* vals, int64_t n, int p, int64_t salt, int32_t* out);
 __global__ void hll_merge_stored_kernel(const int64_t* rows, const int64_t* gid, int64_t nsel, const int64_t* offsets,
                                         const int32_t* pairs, int p, int64_t G, unsigned char* regs);
+// partition.hip
+__global__ void part_rowscan_small_kernel(uint32_t* c, int64_t R, int B, uint32_t* totals);
+__global__ void part_rowscan_kernel(uint32_t* c, int64_t R, int B, uint32_t* totals);
+__global__ void part_basescan_kernel(const uint32_t* totals, int64_t R, uint32_t* base);
+__global__ void part_keys_kernel(const int64_t* keys, int64_t n, int shift1, int P1, uint32_t* counts1,
+                                 const uint32_t* base1, uint32_t* out, int phase);
+__global__ void part_split_kernel(const uint32_t* in, int RW, const uint32_t* base1, int K, int shift2, int P2,
+                                  uint32_t* counts2, const uint32_t* base2, uint32_t* out, int phase);
+__global__ void part_agg_kernel(const uint32_t* recs, int RW, const uint32_t* base, int64_t nsub, int64_t G, int shift,
+                                PartFields f, uint64_t* gacc);
 }  // namespace sdo
 
 namespace py = pybind11;
@@ -345,6 +355,78 @@ static void stream_sync(uint64_t stream) {
   check(hipStreamSynchronize((hipStream_t)stream), "stream sync");
 }
 
+// ---------------------------------------------------------------------------------------------
+// Radix-partitioned group-by (partition.hip).  Every launch below is sized from host-known layout
+// numbers (buckets, blocks); record counts stay on the device (no synchronisation per run).
+static void part_scan(uint64_t counts, int64_t R, int B, uint64_t totals, uint64_t base, uint64_t stream) {
+  if (R <= 0 || B <= 0) return;
+  hipStream_t s = (hipStream_t)stream;
+  if (B <= 64) {
+    hipLaunchKernelGGL(sdo::part_rowscan_small_kernel, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, s,
+                       (uint32_t*)counts, R, B, (uint32_t*)totals);
+  } else {
+    const int64_t g = R < 65536 ? R : 65536;
+    hipLaunchKernelGGL(sdo::part_rowscan_kernel, dim3((unsigned)g), dim3(256), 0, s, (uint32_t*)counts, R, B,
+                       (uint32_t*)totals);
+  }
+  check(hipGetLastError(), "part_rowscan launch");
+  hipLaunchKernelGGL(sdo::part_basescan_kernel, dim3(1), dim3(1024), 0, s, (const uint32_t*)totals, R,
+                     (uint32_t*)base);
+  check(hipGetLastError(), "part_basescan launch");
+}
+
+static void part_keys(uint64_t keys, int64_t n, int shift1, int P1, uint64_t counts1, uint64_t base1, uint64_t out,
+                      int phase, int grid, uint64_t stream) {
+  if (n <= 0 || grid <= 0) return;
+  if (P1 <= 0 || P1 > 16384) throw std::invalid_argument("part_keys: 1..16384 buckets");
+  hipLaunchKernelGGL(sdo::part_keys_kernel, dim3(grid), dim3(512), (unsigned)(P1 * 4), (hipStream_t)stream,
+                     (const int64_t*)keys, n, shift1, P1, (uint32_t*)counts1, (const uint32_t*)base1,
+                     (uint32_t*)out, phase);
+  check(hipGetLastError(), "part_keys_kernel launch");
+}
+
+static void part_split(uint64_t in, int RW, uint64_t base1, int P1, int K, int shift2, int P2, uint64_t counts2,
+                       uint64_t base2, uint64_t out, int phase, uint64_t stream) {
+  if (P1 <= 0 || K <= 0) return;
+  if (P2 <= 0 || P2 > 16384 || (P2 & (P2 - 1))) throw std::invalid_argument("part_split: P2 a power of two <= 16384");
+  if (RW < 1 || RW > 2 + 2 * sdo::MAX_SLOTS) throw std::invalid_argument("part_split: record width");
+  hipLaunchKernelGGL(sdo::part_split_kernel, dim3((unsigned)((int64_t)P1 * K)), dim3(512), (unsigned)(P2 * 4),
+                     (hipStream_t)stream, (const uint32_t*)in, RW, (const uint32_t*)base1, K, shift2, P2,
+                     (uint32_t*)counts2, (const uint32_t*)base2, (uint32_t*)out, phase);
+  check(hipGetLastError(), "part_split_kernel launch");
+}
+
+static void part_agg(uint64_t recs, int RW, uint64_t base, int64_t nsub, int64_t G, int shift, std::vector<int> slot,
+                     std::vector<int> width, std::vector<int> ops, std::vector<int64_t> init, uint64_t gacc,
+                     uint64_t stream) {
+  if (nsub <= 0 || G <= 0) return;
+  sdo::PartFields f{};
+  if (slot.size() != width.size() || slot.size() > (size_t)sdo::MAX_SLOTS) throw std::invalid_argument("part_agg: fields");
+  if (ops.size() != init.size() || ops.empty() || ops.size() > (size_t)sdo::MAX_SLOTS)
+    throw std::invalid_argument("part_agg: slots");
+  f.nfields = (int)slot.size();
+  f.nslots = (int)ops.size();
+  int words = 1;
+  for (size_t j = 0; j < slot.size(); ++j) {
+    if (slot[j] < 0 || slot[j] >= f.nslots || width[j] < 0 || width[j] > 2) throw std::invalid_argument("part_agg: field");
+    f.slot[j] = slot[j];
+    f.width[j] = width[j];
+    words += width[j];
+  }
+  if (words != RW) throw std::invalid_argument("part_agg: record width does not match the fields");
+  for (size_t s = 0; s < ops.size(); ++s) {
+    f.op[s] = ops[s];
+    f.init[s] = init[s];
+  }
+  const int64_t lds = ((int64_t)1 << shift) * f.nslots * 8;
+  if (shift < 0 || lds > 64 * 1024) throw std::invalid_argument("part_agg: sub-bucket table exceeds 64 KiB of LDS");
+  const int64_t grid = (nsub + 7) / 8 * 8;
+  if (grid > ((int64_t)1 << 31) - 8) throw std::invalid_argument("part_agg: too many sub-buckets");
+  hipLaunchKernelGGL(sdo::part_agg_kernel, dim3((unsigned)grid), dim3(512), (unsigned)lds, (hipStream_t)stream,
+                     (const uint32_t*)recs, RW, (const uint32_t*)base, nsub, G, shift, f, (uint64_t*)gacc);
+  check(hipGetLastError(), "part_agg_kernel launch");
+}
+
 static int desc_size() { return (int)sizeof(sdo::ScanDesc); }
 
 static py::dict layout() {
@@ -404,6 +486,10 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("fetch_small", &fetch_small);
   m.def("stream_sync", &stream_sync);
   m.def("glds_probe", &glds_probe);
+  m.def("part_scan", &part_scan);
+  m.def("part_keys", &part_keys);
+  m.def("part_split", &part_split);
+  m.def("part_agg", &part_agg);
   m.def("layout", &layout);
   m.def("device_info", &device_info);
   m.attr("ARCH") = "gfx950";

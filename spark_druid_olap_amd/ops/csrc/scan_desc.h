@@ -145,7 +145,7 @@ struct Range {
   int64_t nchunks;
 };
 
-enum Mode : int32_t { M_DENSE_LDS = 0, M_DENSE_GLOBAL = 1, M_HASH = 2, M_MASK = 3 };
+enum Mode : int32_t { M_DENSE_LDS = 0, M_DENSE_GLOBAL = 1, M_HASH = 2, M_MASK = 3, M_PART = 4 };
 
 struct ScanDesc {
   int32_t ncols, nfops, nkops, naggs;
@@ -192,6 +192,25 @@ struct ScanDesc {
   uint64_t bm_bits[MAX_BM];
   int64_t bm_stride[MAX_BM];
   int64_t bm_count[MAX_BM];
+  // radix-partitioned group-by (mode M_PART, partition.hip): the scan emits records instead of
+  // updating a table.  part_counts is [part_n][gridDim.x] (count pass), part_base [part_n + 1]
+  // (scatter pass: bucket p of block b starts at part_base[p] + part_counts[p][b]).
+  uint64_t part_recs;
+  uint64_t part_counts;
+  uint64_t part_base;
+  int32_t part_shift;     // bucket = key >> part_shift
+  int32_t part_n;         // buckets (LDS counters)
+};
+
+// Fields of a partition record (partition.hip part_agg_kernel): value j is width[j] u32 words
+// (0 = implicit 1, 1 = i32, 2 = i64) folded into slot[j] with op[slot].
+struct PartFields {
+  int32_t nfields;
+  int32_t nslots;
+  int32_t slot[MAX_SLOTS];
+  int32_t width[MAX_SLOTS];
+  int32_t op[MAX_SLOTS];
+  int64_t init[MAX_SLOTS];
 };
 
 }  // namespace sdo

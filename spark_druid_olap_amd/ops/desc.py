@@ -32,7 +32,7 @@ S_SUM_I, S_SUM_F, S_MIN_I, S_MAX_I = range(4)
 E_COL, E_CONST, E_ADD, E_SUB, E_MUL, E_DIV, E_NEG, E_ABS, E_MIN, E_MAX = range(10)
 E_FLOOR, E_CEIL, E_SQRT, E_LOG, E_EXP, E_MOD, E_PMOD, E_POW, E_LUT = range(10, 19)
 E_UNARY = (E_NEG, E_ABS, E_FLOOR, E_CEIL, E_SQRT, E_LOG, E_EXP)
-M_DENSE_LDS, M_DENSE_GLOBAL, M_HASH, M_MASK = range(4)
+M_DENSE_LDS, M_DENSE_GLOBAL, M_HASH, M_MASK, M_PART = range(5)
 
 INT64_MAX = np.iinfo(np.int64).max
 INT64_MIN = np.iinfo(np.int64).min
@@ -67,6 +67,7 @@ SCANDESC = np.dtype([
     ("nplanes", "<i4"), ("lds_cache_off", "<i4"), ("lds_wave_bytes", "<i4"), ("unroll", "<i4"),
     ("narrow4", "<i4"), ("pad2", "<i4"),
     ("bm_bits", "<u8", (MAX_BM,)), ("bm_stride", "<i8", (MAX_BM,)), ("bm_count", "<i8", (MAX_BM,)),
+    ("part_recs", "<u8"), ("part_counts", "<u8"), ("part_base", "<u8"), ("part_shift", "<i4"), ("part_n", "<i4"),
 ], align=True)
 
 

@@ -100,6 +100,40 @@ def col_infos(prog) -> Dict[int, ColInfo]:
     return out
 
 
+PART_MAX_BUCKETS = 1024  # level-1 buckets of the partitioned group-by (LDS counters per block)
+
+
+def part_fields(prog, cols=None) -> List[Tuple[int, int]]:
+    """(slot, u32 words) of every aggregator's value in a partition record (partition.hip
+    part_agg_kernel): 0 = an unfiltered count (implicit 1), 1 = a value that fits int32 (filtered
+    counts, integer columns of <= 4 signed / <= 2 unsigned bytes), 2 = int64 / double bits."""
+    if not hasattr(prog, "aops"):  # planner-level estimate without a lowered program: int64 values
+        return [(s, 2) for s in range(max(1, prog.nslots))]
+    cols = col_infos(prog) if cols is None else cols
+    out = []
+    for a in prog.aops:
+        kind = a["kind"]
+        if kind == D.A_HLL:
+            continue
+        if kind == D.A_COUNT:
+            out.append((a["slot"], 1 if a.get("filt_len") else 0))
+            continue
+        w = 2
+        if kind in (D.A_SUM_I, D.A_MIN_I, D.A_MAX_I) and not a.get("expr") and a.get("col") in cols:
+            c = cols[a["col"]]
+            if not c.flt and not c.pw and (c.lg <= 1 or (c.lg == 2 and c.sgn)):
+                w = 1
+        out.append((a["slot"], w))
+    return out
+
+
+def part_eligible(prog) -> bool:
+    """The partitioned group-by handles every slot operator; it needs u32 keys and no HLL sketch."""
+    slots = getattr(prog, "slots", None)
+    n = len(slots) if slots is not None else prog.nslots
+    return n > 0 and not prog.nhll and 0 < prog.G < (1 << 32) and not prog.empty
+
+
 REG_BUDGET = int(os.environ.get("SDO_JIT_REG_BUDGET", "96"))  # VGPRs for register accumulators
 
 
@@ -158,6 +192,8 @@ def layout(prog, mode: int, U: int, hll_lds: bool, m: int, reg: bool = False, pi
         while ncopy > 1 and base * ncopy + hll_bytes + stage > budget:
             ncopy //= 2
         acc_bytes = base * ncopy
+    if mode == D.M_PART:
+        acc_bytes = PART_MAX_BUCKETS * 4  # level-1 bucket counters / cursors
     acc_off = 0
     hll_off = (acc_bytes + 15) // 16 * 16
     cache_off = (hll_off + hll_bytes + 15) // 16 * 16
@@ -201,8 +237,9 @@ def _dlit(v: float) -> str:
 
 class _Gen:
     def __init__(self, prog, mode: int, U: int, hll_lds: bool, narrow4: bool, lay: JitLayout, m: int,
-                 reg: bool = False):
+                 reg: bool = False, part_phase: int = 0):
         self.p = prog
+        self.part_phase = part_phase
         self.reg = reg
         self.pipe = lay.pipe
         self.regstage = lay.regstage
@@ -435,6 +472,50 @@ class _Gen:
         return o
 
     # ---------------------------------------------------------------- whole kernel
+    def _part_record(self, body: List[str]) -> None:
+        """M_PART: the row becomes a partition record instead of a table update (ops/csrc/partition.hip).
+        Phase 0 counts the rows of each bucket (LDS counters); phase 1 appends the record -- u32 key,
+        then every aggregator's value (``part_fields``: implicit / i32 / i64 words; a row an
+        aggregator's own filter rejects carries the slot's identity)."""
+        p = self.p
+        body.append("        const bool mine = act[u];")
+        body.append("        if (mine) {")
+        body.append("          const uint32_t pb_ = (uint32_t)(key >> pshift);")
+        if self.part_phase == 0:
+            body.append("          atomicAdd(&pcnt[pb_], 1u);")
+            body.append("        }")
+            return
+        fields = part_fields(p, self.cols)
+        rw = 1 + sum(w for _, w in fields)
+        body.append("          const uint32_t pos_ = atomicAdd(&pcnt[pb_], 1u);")
+        body.append(f"          uint32_t* o_ = precs + (uint64_t)pos_ * {rw}u;")
+        body.append("          o_[0] = (uint32_t)key;")
+        w = 1
+        fi = 0
+        for ai, a in enumerate(p.aops):
+            if a["kind"] == D.A_HLL:
+                continue
+            slot, width = fields[fi]
+            fi += 1
+            cond = None
+            if a.get("filt_len"):
+                cond = f"((({self.word_expr(a['filt_off'], a['filt_off'] + a['filt_len'])}) >> lane) & 1ull)"
+            if width == 0:
+                w += 0
+                continue
+            val = f"v{ai}_[u]"
+            if a["kind"] == D.A_COUNT:
+                val = f"({cond} ? 1LL : 0LL)" if cond else "1LL"
+            elif cond:
+                val = f"({cond} ? {val} : (int64_t){_lit(p.slots[slot][1])})"
+            if width == 1:
+                body.append(f"          o_[{w}] = (uint32_t)(int32_t)({val});")
+            else:
+                body.append(f"          {{ const uint64_t x_ = (uint64_t)({val}); o_[{w}] = (uint32_t)x_; "
+                            f"o_[{w + 1}] = (uint32_t)(x_ >> 32); }}")
+            w += width
+        body.append("        }")
+
     def source(self, name: str) -> str:
         p, U, NP, lay = self.p, self.U, self.NP, self.lay
         mode = self.mode
@@ -537,7 +618,9 @@ class _Gen:
         body.append("      }")
         body.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{")
         body.append("        const uint64_t key = key_[u];")
-        if mode == D.M_HASH:
+        if mode == D.M_PART:
+            self._part_record(body)
+        elif mode == D.M_HASH:
             body.append("        int64_t slot = act[u] ? hash_slot(hkeys, hcap, key, overflow) : -1;")
             body.append("        const bool mine = act[u] && slot >= 0;")
         else:
@@ -549,7 +632,7 @@ class _Gen:
                 # touched groups compact from this table instead of the accumulator table, and only
                 # they are re-initialised after the run (no full-table fill per execution)
                 body.append("        if (mine) ((unsigned char*)d->out_mask)[slot] = (unsigned char)1;")
-        for ai, a in enumerate(p.aops):
+        for ai, a in enumerate(p.aops if mode != D.M_PART else []):
             cond = "mine"
             if a.get("filt_len"):
                 fx = self.word_expr(a["filt_off"], a["filt_off"] + a["filt_len"])
@@ -625,6 +708,20 @@ class _Gen:
         out.append("  (void)bmw; (void)acc; (void)copy; (void)gacc; (void)hkeys; (void)hcap; (void)overflow;")
         out.extend(L)
         out.extend("  " + x for x in self.pre_lines)
+        if mode == D.M_PART:
+            out.append("  uint32_t* pcnt = (uint32_t*)lds;")
+            out.append("  uint32_t* precs = (uint32_t*)d->part_recs;")
+            out.append("  uint32_t* pcounts = (uint32_t*)d->part_counts;")
+            out.append("  const uint32_t* pbase = (const uint32_t*)d->part_base;")
+            out.append("  const int pshift = d->part_shift;")
+            out.append("  const int pn = d->part_n;")
+            out.append("  (void)precs; (void)pbase;")
+            if self.part_phase == 0:
+                out.append(f"  for (int i = threadIdx.x; i < pn; i += {W * 64}) pcnt[i] = 0u;")
+            else:
+                out.append(f"  for (int i = threadIdx.x; i < pn; i += {W * 64}) "
+                           "pcnt[i] = pbase[i] + pcounts[(int64_t)i * gridDim.x + blockIdx.x];")
+            out.append("  __syncthreads();")
         if mode == D.M_DENSE_LDS:
             out.append(f"  for (int i = threadIdx.x; i < {G * NS * NCT}; i += {W * 64}) {{")
             inits = ", ".join(_lit(init) for _, init in p.slots)
@@ -739,6 +836,10 @@ class _Gen:
                         out.append("    const int64_t b = v;")
                     out.append(f"    if (lane == 0) acc[({g} * {NS} + {s}) * {NCT} + wave] = (uint64_t)b;")
                     out.append("  }")
+        if mode == D.M_PART and self.part_phase == 0:
+            out.append("  __syncthreads();")
+            out.append(f"  for (int i = threadIdx.x; i < pn; i += {W * 64}) "
+                       "pcounts[(int64_t)i * gridDim.x + blockIdx.x] = pcnt[i];")
         if mode == D.M_DENSE_LDS:
             out.append("  __syncthreads();")
             out.append(f"  for (int i = threadIdx.x; i < {G * NS}; i += {W * 64}) {{")
@@ -807,14 +908,14 @@ class JitScan:
 
     def __init__(self, prog, mode: int, U: int, hll_lds: bool, m: int, narrow4: bool, load: bool = True,
                  reg: Optional[bool] = None, pipe: bool = False, budget: int = 150 * 1024,
-                 regstage: bool = False, shared: bool = False):
+                 regstage: bool = False, shared: bool = False, part_phase: int = 0):
         self.reg = False if shared else (reg_eligible(prog, mode) if reg is None else reg)
         self.lay = layout(prog, mode, U, hll_lds, m, self.reg, pipe and not regstage, budget, regstage, shared)
         if self.lay.total > 160 * 1024:
             raise ValueError(f"jit layout needs {self.lay.total} B of LDS")
-        g = _Gen(prog, mode, U, hll_lds, narrow4, self.lay, m, self.reg)
-        tag = hashlib.sha1(repr((mode, U, self.reg, pipe, self.lay.ncopy, regstage, self.lay.shared)).encode()
-                           ).hexdigest()[:6]
+        g = _Gen(prog, mode, U, hll_lds, narrow4, self.lay, m, self.reg, part_phase)
+        tag = hashlib.sha1(repr((mode, U, self.reg, pipe, self.lay.ncopy, regstage, self.lay.shared,
+                                 part_phase)).encode()).hexdigest()[:6]
         self.name = f"sdo_jit_{tag}"
         self.src = g.source(self.name)
         self.handle = compile_source(self.src, self.name) if load else -1

@@ -284,12 +284,19 @@ DENSE_MAX_SPARSE_MULTI = int(os.environ.get("SDO_DENSE_MAX_SPARSE", 4 << 30))  #
 DENSE_MAX_1GPU = int(os.environ.get("SDO_DENSE_MAX_1GPU", 16 << 30))
 TOUCH_MIN_G = int(os.environ.get("SDO_TOUCH_MIN_G", 1 << 20))
 PROBE_S = 1.0e-9        # hash-table insert (CAS probe + key compare) per qualifying row
+# Random read-modify-write atomics into a table beyond the L2: ~16-20 G updates/s on MI355X whether
+# the table sits in HBM or in the Infinity Cache (TPC-H Q18 at SF100: 600M updates, 29 ms; see the
+# KEY_PASSES note below) -- each update is its own cache-line transaction.
+ATOMIC_RATE = float(os.environ.get("SDO_ATOMIC_RATE", 18e9))
+L2_TABLE_BYTES = 4 << 20   # one XCD's L2: tables this small take their atomics in cache
+PARTITIONED = os.environ.get("SDO_PARTITIONED", "1") != "0"
+FORCE_PARTITIONED = os.environ.get("SDO_FORCE_PARTITIONED", "0") != "0"  # tests: any eligible HBM-table plan
 ONESHOT_MAX_BYTES = 256 << 20   # gather buffer (world x state) ceiling for the one-shot merge
 
 
 @dataclass
 class GroupByPlan:
-    mode: str                      # dense-lds | dense-global | hash
+    mode: str                      # dense-lds | dense-global | partitioned | hash
     shared: bool = False           # one LDS table per workgroup (else one copy per wave)
     hll_lds: bool = False          # HLL registers in LDS
     touch: bool = False            # first-touch byte table (dense-global)
@@ -350,14 +357,46 @@ def plan_groupby(prog, jit: bool, local: bool) -> GroupByPlan:
             dense = (2 * G + touched * ns * 8 * 2) / HBM_BW
         else:
             dense = 2 * table / HBM_BW
+        if not presence:
+            # one random atomic per qualifying row and slot
+            dense += est_rows * ns / (ATOMIC_RATE * (8 if table <= L2_TABLE_BYTES else 1))
         costs["dense-global"] = dense * 1e3
+        part = partitioned_cost_s(prog, est_rows) if (jit and PARTITIONED and not presence and not empty) else None
+        if part is not None:
+            costs["partitioned"] = part * 1e3
     cap = 1 << max(10, math.ceil(math.log2(max(2.0, 2 * (min(G, est_rows * 1.2) + 1024)))))
     costs["hash"] = (2 * cap * (8 + ns * 8) / HBM_BW + est_rows * PROBE_S) * 1e3
+    if "partitioned" in costs and (FORCE_PARTITIONED or costs["partitioned"] <= min(costs["dense-global"],
+                                                                                    costs["hash"])):
+        return GroupByPlan("partitioned", costs=costs,
+                           reason="radix-partitioned records aggregated in LDS (no random HBM atomics)")
     if "dense-global" in costs and costs["dense-global"] <= costs["hash"]:
         return GroupByPlan("dense-global", touch=touch, presence_bytes=presence, costs=costs,
                            reason="HBM table indexed by the packed key")
     why = "table over budget" if "dense-global" not in costs else "few qualifying rows for the key space"
     return GroupByPlan("hash", costs=costs, reason=why)
+
+
+def partitioned_cost_s(prog, est_rows: float) -> Optional[float]:
+    """Radix-partitioned group-by (ops/csrc/partition.hip): two producer scans (count, scatter),
+    records written once per level and read by the next, and the dense table written once."""
+    from ..ops import jit
+
+    if not jit.part_eligible(prog):
+        return None
+    if est_rows < prog.G / 4:
+        # few updates per group: the touched lines are sparse (TPC-H Q3 touches ~1M of 150M orders)
+        # and stay cached; the atomic table wins and a full-table write would be waste
+        return None
+    from ..engine.device_exec import part_layout
+
+    try:
+        L = part_layout(prog)
+    except ValueError:
+        return None
+    rec = 4 * L["rw"]
+    traffic = est_rows * rec * (2 * L["levels"]) + 2 * est_rows * rec + prog.G * max(1, prog.nslots) * 8
+    return traffic / HBM_BW + (4 + 4 * L["levels"]) * LAUNCH_S
 
 
 @dataclass

@@ -130,3 +130,27 @@ def test_cost_small_result_query(ds_small):
 
     c = estimate(ds_small, _gb(["l_returnflag", "l_linestatus"], _ONE_YEAR))
     assert c.output_rows <= 6 and c.groupby_mode == "dense-lds"
+
+
+def test_saturating_updates_over_a_huge_key_space_are_partitioned():
+    # TPC-H Q18 at SF100: 600M lines into 150M order groups -- 600M random HBM atomics (~29 ms
+    # measured) vs radix-partitioned records aggregated in LDS
+    p = cost.plan_groupby(_prog(150_000_000, ns=1, est_rows=600e6), jit=True, local=True)
+    assert p.mode == "partitioned", p.describe()
+    assert p.costs["partitioned"] < p.costs["dense-global"] / 3
+    # no JIT (the producers are generated kernels) -> the atomic table
+    assert cost.plan_groupby(_prog(150_000_000, ns=1, est_rows=600e6), jit=False, local=True).mode != "partitioned"
+    # HLL sketches are not partition records
+    assert cost.plan_groupby(_prog(1_000_000, ns=1, nhll=1, est_rows=600e6), jit=True, local=True).mode != \
+        "partitioned"
+
+
+def test_partition_geometry():
+    from spark_druid_olap_amd.engine.device_exec import part_layout
+
+    L = part_layout(_prog(150_000_000, ns=1))
+    assert L["levels"] == 2 and L["p1"] * L["p2"] * (1 << L["shift"]) >= 150_000_000
+    assert (1 << L["shift"]) * 8 <= 64 << 10 and L["p1"] <= 1024
+    assert L["shift1"] == L["shift"] + int(math.log2(L["p2"]))
+    small = part_layout(_prog(100_000, ns=3))
+    assert small["levels"] == 1 and small["p1"] * (1 << small["shift"]) >= 100_000

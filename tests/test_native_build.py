@@ -74,6 +74,32 @@ def test_jit_presence_only_kernel_compiles(tmp_path, monkeypatch, ds_small):
     assert "(unsigned char*)gacc)[slot]" in js.src
 
 
+def test_jit_partition_producers_compile(tmp_path, monkeypatch, ds_small):
+    """M_PART (radix-partitioned group-by): the count producer bumps LDS bucket counters and the
+    scatter producer appends u32 key + value records (narrow sums as one word, doubles as two,
+    filtered aggregators carry the slot identity when their filter rejects the row)."""
+    from spark_druid_olap_amd.engine.lower import Lowerer
+    from spark_druid_olap_amd.ops import desc as D
+    from spark_druid_olap_amd.ops import jit
+    from spark_druid_olap_amd.query import spec as S
+
+    monkeypatch.setenv("SDO_JIT_CACHE", str(tmp_path))
+    aggs = [S.FunctionAggregationSpec("count", "c"), S.FunctionAggregationSpec("longSum", "q", "l_quantity"),
+            S.FunctionAggregationSpec("doubleSum", "s", "l_extendedprice"),
+            S.FilteredAggregationSpec(S.SelectorFilterSpec("l_returnflag", "R"),
+                                      S.FunctionAggregationSpec("longSum", "q_r", "l_quantity"), "q_r")]
+    prog = Lowerer(ds_small).lower_aggregate(["1992-01-01/1999-01-01"], None,
+                                             [S.DefaultDimensionSpec("o_orderkey")], None, aggs)
+    assert jit.part_eligible(prog)
+    fields = jit.part_fields(prog)
+    assert [w for _, w in fields] == [0, 1, 1, 1]  # extendedprice: exact i32 cents
+    c = jit.JitScan(prog, D.M_PART, 4, False, 2048, True, load=False, part_phase=0)
+    w = jit.JitScan(prog, D.M_PART, 4, False, 2048, True, load=False, part_phase=1)
+    assert "atomicAdd(&pcnt[pb_], 1u);" in c.src and "precs" not in c.src.split("pcounts[(int64_t)i")[0][-300:]
+    assert "uint32_t* o_ = precs + (uint64_t)pos_ * 4u;" in w.src
+    assert c.lay.acc_bytes == jit.PART_MAX_BUCKETS * 4 and c.name != w.name
+
+
 
 def test_hll_estimate_bf16_operands_are_exact():
     """hll_estimate_kernel (ops/csrc/olap_scan.hip) feeds 2^-M to a bf16 MFMA as the bit pattern

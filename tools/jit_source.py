@@ -17,14 +17,19 @@ def main():
     from spark_druid_olap_amd.session import Session
     from spark_druid_olap_amd.ops import desc as D
 
-    want = sys.argv[1:]
+    want = [a for a in sys.argv[1:] if not a.startswith("--")]
+    queries = tpch.BENCH_QUERIES
+    if "--tpch22" in sys.argv:
+        from spark_druid_olap_amd.models import tpch22
+
+        queries = tpch22.QUERIES
     flat = tpch.generate_flat(0.05, "cpu")
     ds = tpch.to_datasource(flat, profile="bench")
     sess = Session(engine=Engine(use_native=False), conf={"spark.sparklinedata.druid.approxCountDistinct": "true"})
     sess.register_datasource(ds)
     sess.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)
     sess.sql(tpch.druid_ddl(source="orderLineItemPartSupplierBase", datasource="tpch", with_column_mapping=False))
-    for name, q in tpch.BENCH_QUERIES:
+    for name, q in queries:
         if want and not any(w.lower() in name.lower() for w in want):
             continue
         df = sess.sql(q)
@@ -32,7 +37,10 @@ def main():
             pq = sess.engine.prepare(dq.spec, ds)
             for _, prog, _ in pq.scans:
                 gp = plan_groupby(prog, True, True)
-                mode = {"dense-lds": D.M_DENSE_LDS, "dense-global": D.M_DENSE_GLOBAL, "hash": D.M_HASH}[gp.mode]
+                if os.environ.get("SDO_FORCE_PART") and jit.part_eligible(prog) and prog.G > 4096:
+                    gp.mode = "partitioned"
+                mode = {"dense-lds": D.M_DENSE_LDS, "dense-global": D.M_DENSE_GLOBAL, "hash": D.M_HASH,
+                        "partitioned": D.M_PART}[gp.mode]
                 print(f"==== {name}: G={prog.G} keys={[(k.name, k.kind, k.card) for k in prog.keys]} "
                       f"slots={prog.slots} plan={gp.describe()}")
                 if os.environ.get("SDO_PACKED", "1") != "0":  # bit-packed columns (CPU copies here)
@@ -49,12 +57,14 @@ def main():
                 regstage = jit.prefer_regstage(prog)
                 lay = jit.layout(prog, mode, 4, bool(prog.nhll) and gp.hll_lds, 1 << prog.hll_p, False, False,
                                  (160 * 1024) // 3 - 512, regstage, gp.shared)
-                g = jit._Gen(prog, mode, 4, bool(prog.nhll) and gp.hll_lds, True, lay, 1 << prog.hll_p)
-                src = g.source("sdo_jit_probe")
-                print(src)
-                if os.environ.get("SDO_JIT_COMPILE"):  # hipRTC for gfx950 (no GPU needed)
-                    code = jit.compile_code(src, "sdo_jit_probe")
-                    print(f"// compiled: {len(code)} bytes of gfx950 code object")
+                for phase in ((0, 1) if mode == D.M_PART else (0,)):
+                    g = jit._Gen(prog, mode, 4, bool(prog.nhll) and gp.hll_lds, True, lay, 1 << prog.hll_p,
+                                 part_phase=phase)
+                    src = g.source("sdo_jit_probe")
+                    print(src)
+                    if os.environ.get("SDO_JIT_COMPILE"):  # hipRTC for gfx950 (no GPU needed)
+                        code = jit.compile_code(src, "sdo_jit_probe")
+                        print(f"// compiled: {len(code)} bytes of gfx950 code object")
 
 
 if __name__ == "__main__":
