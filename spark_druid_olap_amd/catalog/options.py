@@ -149,6 +149,7 @@ class Conf:
 
     def __init__(self, init: Optional[Dict[str, Any]] = None):
         self._vals: Dict[str, str] = {}
+        self._key: Optional[str] = None  # canonical form of the SET values (plan-cache key part)
         for k, v in os.environ.items():
             if k.startswith("SDO_CONF_"):
                 self._vals[k[len("SDO_CONF_"):].replace("__", ".")] = v
@@ -159,14 +160,25 @@ class Conf:
     def copy(self) -> "Conf":
         c = Conf.__new__(Conf)
         c._vals = dict(self._vals)
+        c._key = self._key
         return c
 
     def set(self, key: str, value: Any) -> None:
         self._vals[key] = value if isinstance(value, str) else json.dumps(value) if not isinstance(
             value, (int, float, bool)) else str(value).lower() if isinstance(value, bool) else str(value)
+        self._key = None
 
     def unset(self, key: str) -> None:
         self._vals.pop(key, None)
+        self._key = None
+
+    def cache_key(self) -> str:
+        """The SET values in canonical form, recomputed only after a SET / UNSET (every statement's
+        plan-cache lookup uses it)."""
+        k = self._key
+        if k is None:
+            k = self._key = json.dumps(sorted(self._vals.items()))
+        return k
 
     def get(self, key: str, default: Any = None) -> Optional[str]:
         if key in self._vals:

@@ -53,7 +53,7 @@ def _attach_packed(prog) -> None:
             prog.packed[name] = pc
 
 
-def _jit_for(prog, mode: int, hll_lds: bool, m: int, shared: bool = False, part_phase: int = 0):
+def _jit_for(prog, mode: int, hll_lds: bool, m: int, shared: bool = False):
     """Specialized kernel for this program shape (None -> use the interpreter, plain columns)."""
     if not USE_JIT:
         prog.packed = {}
@@ -62,13 +62,13 @@ def _jit_for(prog, mode: int, hll_lds: bool, m: int, shared: bool = False, part_
 
     if getattr(prog, "packed", None) is None:
         _attach_packed(prog)
-    js = _jit_build(prog, mode, hll_lds, m, shared, part_phase)
+    js = _jit_build(prog, mode, hll_lds, m, shared)
     if js is None:
         prog.packed = {}  # the interpreter reads the plain columns
     return js
 
 
-def _jit_build(prog, mode: int, hll_lds: bool, m: int, shared: bool = False, part_phase: int = 0):
+def _jit_build(prog, mode: int, hll_lds: bool, m: int, shared: bool = False):
     from ..ops import jit
 
     nplanes = sum(2 if column_tensor_size(prog, c) == 8 else 1 for c in prog.cols)
@@ -89,7 +89,7 @@ def _jit_build(prog, mode: int, hll_lds: bool, m: int, shared: bool = False, par
                                         or U == prefs[-1]):
                 try:
                     return jit.JitScan(prog, mode, U, hll_lds, m, bool(native.narrow4()), reg=reg, pipe=pipe,
-                                       budget=budget, regstage=regstage, shared=shared, part_phase=part_phase)
+                                       budget=budget, regstage=regstage, shared=shared)
                 except Exception as e:  # pragma: no cover - compile problems fall back loudly
                     import warnings
 
@@ -152,14 +152,13 @@ class PreparedScan:
         else:
             self.cap = 0
         self.jit = None
-        self.jit_scatter = None
         self.part = None
+        self.part_having = None
+        self.part_cap = 1 << 16
         if mode == D.M_PART and not prog.empty:
-            # radix-partitioned group-by (ops/csrc/partition.hip): count + scatter JIT producers
-            self.jit = _jit_for(prog, D.M_PART, False, self.m, part_phase=0)
-            self.jit_scatter = _jit_for(prog, D.M_PART, False, self.m, part_phase=1) if self.jit else None
-            if self.jit_scatter is None:
-                self.jit = None
+            # radix-partitioned group-by (ops/csrc/partition.hip): the JIT producer appends records
+            self.jit = _jit_for(prog, D.M_PART, False, self.m)
+            if self.jit is None:
                 mode = D.M_DENSE_GLOBAL  # no JIT: the HBM table with atomics
             else:
                 self.part = part_layout(prog)
@@ -278,55 +277,91 @@ class PreparedScan:
 
     def _part_bufs(self, d) -> dict:
         """Record / count / offset buffers of the partitioned group-by for this slot; fills the
-        descriptor's part_* fields (level-1 buckets, written by the JIT producers)."""
+        descriptor's part_* fields (the producer's record regions and per-chunk end offsets)."""
         L, prog, dev = self.part, self.prog, self.dev
         u32 = torch.int32
-        cap = int(prog.ds.num_rows)  # records <= rows of the shard (one per qualifying row)
+        nch = int(d[0]["total_chunks"])
+        cap = nch * D.CHUNK_ROWS            # chunk c owns records [4096 c, 4096 c + 4096)
         if cap * L["rw"] >= (1 << 32) or cap >= (1 << 32):
             raise RuntimeError("partitioned group-by: shard too large for u32 record offsets")
         P1, nsub = L["p1"], L["nsub"]
+        k1 = max(1, min(nch, 2048))
         pb = {
             "recs1": torch.empty(max(1, cap * L["rw"]), dtype=u32, device=dev),
-            "counts1": torch.empty(P1 * self.grid, dtype=u32, device=dev),
+            "recs2": torch.empty(max(1, cap * L["rw"]), dtype=u32, device=dev),
+            "seg_lo": (torch.arange(nch, dtype=torch.int64) * D.CHUNK_ROWS).to(u32).to(dev),
+            "pend": torch.empty(max(1, nch), dtype=u32, device=dev),
+            "k1": k1, "nch": nch,
+            "counts1": torch.empty(P1 * k1, dtype=u32, device=dev),
             "totals1": torch.empty(P1, dtype=u32, device=dev),
             "base1": torch.empty(P1 + 1, dtype=u32, device=dev),
         }
         if L["levels"] == 2:
-            pb["recs2"] = torch.empty_like(pb["recs1"])
             pb["counts2"] = torch.empty(nsub * L["k"], dtype=u32, device=dev)
             pb["totals2"] = torch.empty(nsub, dtype=u32, device=dev)
             pb["base2"] = torch.empty(nsub + 1, dtype=u32, device=dev)
         d[0]["part_recs"] = pb["recs1"].data_ptr()
-        d[0]["part_counts"] = pb["counts1"].data_ptr()
-        d[0]["part_base"] = pb["base1"].data_ptr()
+        d[0]["part_counts"] = pb["pend"].data_ptr()
         d[0]["part_shift"] = L["shift1"]
         d[0]["part_n"] = P1
         return pb
 
-    def _run_part(self, b: "_Bufs") -> None:
-        """count -> bucket offsets -> scatter -> [split by the next bits] -> LDS aggregation into the
-        dense table (every row of it written: no reset)."""
+    def _run_part(self, b: "_Bufs") -> Optional[Partials]:
+        """producer (records into chunk regions) -> level-1 split (count, offsets, tile-sorted
+        scatter) -> [level-2 split] -> LDS aggregation into the dense table (every row written: no
+        reset), or, with a fused HAVING, straight to the surviving groups (sparse)."""
         L, nat, st = self.part, native.load(), native._stream(self.dev)
         pb = b.part
         prog = self.prog
-        W = BLOCK
-        nat.module_launch(self.jit.handle, b.desc.data_ptr(), int(self.grid), W, int(self.jit.lay.total), st)
-        nat.part_scan(pb["counts1"].data_ptr(), L["p1"], int(self.grid), pb["totals1"].data_ptr(),
-                      pb["base1"].data_ptr(), st)
-        nat.module_launch(self.jit_scatter.handle, b.desc.data_ptr(), int(self.grid), W,
-                          int(self.jit_scatter.lay.total), st)
-        recs, base = pb["recs1"], pb["base1"]
+        nat.module_launch(self.jit.handle, b.desc.data_ptr(), int(self.grid), BLOCK, int(self.jit.lay.total), st)
+        rw, P1, k1 = L["rw"], L["p1"], pb["k1"]
+        # level 1: one input group = every chunk region, P1 buckets by the top key bits
+        a1 = (pb["recs1"].data_ptr(), rw, pb["seg_lo"].data_ptr(), pb["pend"].data_ptr(), 1, pb["nch"], k1,
+              L["shift1"], P1, pb["counts1"].data_ptr())
+        nat.part_split(*a1, 0, 0, 0, st)
+        nat.part_scan(pb["counts1"].data_ptr(), P1, k1, pb["totals1"].data_ptr(), pb["base1"].data_ptr(), st)
+        nat.part_split(*a1, pb["base1"].data_ptr(), pb["recs2"].data_ptr(), 1, st)
+        recs, base = pb["recs2"], pb["base1"]
         if L["levels"] == 2:
-            args = (pb["recs1"].data_ptr(), L["rw"], pb["base1"].data_ptr(), L["p1"], L["k"], L["shift"], L["p2"],
-                    pb["counts2"].data_ptr())
-            nat.part_split(*args, 0, 0, 0, st)
+            # level 2: group p = level-1 bucket p (one segment [base1[p], base1[p+1])), P2 sub-buckets
+            b1 = pb["base1"].data_ptr()
+            a2 = (pb["recs2"].data_ptr(), rw, b1, b1 + 4, P1, 1, L["k"], L["shift"], L["p2"],
+                  pb["counts2"].data_ptr())
+            nat.part_split(*a2, 0, 0, 0, st)
             nat.part_scan(pb["counts2"].data_ptr(), L["nsub"], L["k"], pb["totals2"].data_ptr(),
                           pb["base2"].data_ptr(), st)
-            nat.part_split(*args, pb["base2"].data_ptr(), pb["recs2"].data_ptr(), 1, st)
-            recs, base = pb["recs2"], pb["base2"]
-        nat.part_agg(recs.data_ptr(), L["rw"], base.data_ptr(), L["nsub"], int(prog.G), L["shift"],
-                     [f[0] for f in L["fields"]], [f[1] for f in L["fields"]], [int(op) for op, _ in prog.slots],
-                     [int(init) for _, init in prog.slots], b.acc.data_ptr(), st)
+            nat.part_split(*a2, pb["base2"].data_ptr(), pb["recs1"].data_ptr(), 1, st)
+            recs, base = pb["recs1"], pb["base2"]
+        hv = self.part_having
+        if hv is None:
+            nat.part_agg(recs.data_ptr(), L["rw"], base.data_ptr(), L["nsub"], int(prog.G), L["shift"],
+                         [f[0] for f in L["fields"]], [f[1] for f in L["fields"]], [int(op) for op, _ in prog.slots],
+                         [int(init) for _, init in prog.slots], b.acc.data_ptr(), [], 1, 0, 0, 0, st)
+            return None
+        while True:
+            out = pb.get("hv_out")
+            if out is None or out[0].shape[0] < self.part_cap:
+                out = pb["hv_out"] = (torch.empty((self.part_cap, prog.nslots), dtype=torch.int64, device=self.dev),
+                                      torch.empty(self.part_cap, dtype=torch.int64, device=self.dev),
+                                      torch.zeros(1, dtype=torch.int64, device=self.dev))
+            acc, keys, cnt = out
+            nat.part_agg(recs.data_ptr(), L["rw"], base.data_ptr(), L["nsub"], int(prog.G), L["shift"],
+                         [f[0] for f in L["fields"]], [f[1] for f in L["fields"]], [int(op) for op, _ in prog.slots],
+                         [int(init) for _, init in prog.slots], acc.data_ptr(), hv[0], hv[1], keys.data_ptr(),
+                         cnt.data_ptr(), int(acc.shape[0]), st)
+            n = int(cnt.item())
+            if n <= acc.shape[0]:
+                return Partials("sparse", acc[:n], keys[:n], [])
+            self.part_cap = _next_pow2(n + n // 4)  # more survivors than room: grow, aggregate again
+
+    def set_part_having(self, terms, conj: bool) -> bool:
+        """Fuse a groupBy HAVING into the partitioned aggregation (engine/executor.py): only existing
+        groups passing it leave the kernel, as sparse partials.  terms: [(slot, is_f64, op, divisor,
+        constant)], op 0 equalTo / 1 greaterThan / 2 lessThan.  False when this scan cannot."""
+        if self.mode != D.M_PART or not terms or len(terms) > 4:
+            return False
+        self.part_having = ([tuple(t) for t in terms], 1 if conj else 0)
+        return True
 
     def _launch(self, b: "_Bufs"):
         if self.jit is not None:
@@ -374,7 +409,9 @@ class PreparedScan:
                 native.run_scan(*(b.noreset_args if (self.touch and b.clean) else b.run_args),
                                 native._stream(self.dev))
             elif self.mode == D.M_PART:
-                self._run_part(b)
+                sp = self._run_part(b)
+                if sp is not None:
+                    return sp
             else:
                 self._reset(b)
                 self._launch(b)
@@ -506,7 +543,7 @@ def part_layout(prog) -> dict:
                 "fields": fields, "rw": rw}
     b1 = min(10, (rem + 1) // 2)
     b2 = rem - b1
-    if b2 > 14:
+    if b2 > 10:
         raise ValueError(f"partitioned group-by: {prog.G} keys need more than two levels")
     p1, p2 = 1 << b1, 1 << b2
     k = max(1, min(64, 4096 // p1))

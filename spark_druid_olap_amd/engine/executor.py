@@ -108,6 +108,7 @@ class PreparedQuery:
         self.segments_per_query = segments_per_query
         self._nbatches: Optional[int] = None   # batch count agreed across ranks (pipelined merge)
         self._pipeline_ok: Optional[bool] = None
+        self._having_fused: Optional[bool] = None  # HAVING handed to a partitioned scan (decided once)
         self.window: Optional["ShardWindow"] = None
         qt = qs.queryType
         if qt in ("groupBy", "timeseries", "topN"):
@@ -326,6 +327,10 @@ class PreparedQuery:
                 part, hv = self._device_having(prog, part)
                 return prog, self._device_prune(prog, part, hv), t1
         err = None
+        disjoint = bool(self.ds.shard_key) and any(k.col == self.ds.shard_key for k in self._full_prog.keys) \
+            if getattr(self, "_full_prog", None) is not None else False
+        if self._having_fused is None:
+            self._having_fused = self._fuse_having(prog, prep, disjoint)
         try:
             with T.span("sdo.scan"):
                 checkpoint()  # inside the merge's failure agreement: every rank aborts together
@@ -407,6 +412,42 @@ class PreparedQuery:
                 raise_if_failed(sts, self.world.rank, err)
             part = combine_local(prog, [d[0] for d in done])
         return part, t1
+
+    def _fuse_having(self, prog: ScanProgram, prep, disjoint: bool) -> bool:
+        """Hand a simple HAVING (comparisons of count / integer / double aggregates, AND-ed or OR-ed)
+        to a partitioned group-by scan (engine/device_exec.py set_part_having): the aggregation
+        kernel then emits only the surviving groups -- TPC-H Q18 keeps ~6K of 150M orders without
+        writing or compacting the 150M-row table.  Only where a group's partial is already final:
+        one rank, or keys that never span ranks (shard-key groups)."""
+        from ..ops import desc as D_
+
+        h = getattr(self.qs, "having", None)
+        if h is None or self.qs.queryType != "groupBy" or prog.thetas or any(kc.collapse for kc in prog.keys):
+            return False
+        if prep is None or getattr(prep, "mode", None) != D_.M_PART or len(self.scans) != 1:
+            return False
+        if self.world.distributed and not disjoint:
+            return False
+        aggs = {a.name: a for a in prog.aggs}
+
+        def term(x):
+            if not isinstance(x, S.ComparisonHavingSpec) or x.type not in ("equalTo", "greaterThan", "lessThan"):
+                return None
+            a = aggs.get(x.aggregation)
+            if a is None or a.slot < 0 or a.kind not in ("count", "sum_i", "sum_f", "min_i", "max_i"):
+                return None
+            op = {"equalTo": 0, "greaterThan": 1, "lessThan": 2}[x.type]
+            return (a.slot, 1 if a.kind == "sum_f" else 0, op, float(10.0 ** a.scale) if a.scale else 1.0,
+                    float(x.value))
+
+        if isinstance(h, S.LogicalHavingSpec) and h.type in ("and", "or"):
+            terms = [term(y) for y in h.havingSpecs]
+            conj = h.type == "and"
+        else:
+            terms, conj = [term(h)], True
+        if not terms or any(t is None for t in terms) or len(terms) > 4:
+            return False
+        return bool(prep.set_part_having(terms, conj))
 
     def _device_having(self, prog: ScanProgram, part: Partials):
         """groupBy havingSpec evaluated over the merged accumulators ON THE DEVICE (TPC-H Q18:

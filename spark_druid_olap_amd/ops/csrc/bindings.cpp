@@ -10,6 +10,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <tuple>
 #include <vector>
 #include "scan_desc.h"
 
@@ -54,10 +55,13 @@ __global__ void part_rowscan_kernel(uint32_t* c, int64_t R, int B, uint32_t* tot
 __global__ void part_basescan_kernel(const uint32_t* totals, int64_t R, uint32_t* base);
 __global__ void part_keys_kernel(const int64_t* keys, int64_t n, int shift1, int P1, uint32_t* counts1,
                                  const uint32_t* base1, uint32_t* out, int phase);
-__global__ void part_split_kernel(const uint32_t* in, int RW, const uint32_t* base1, int K, int shift2, int P2,
-                                  uint32_t* counts2, const uint32_t* base2, uint32_t* out, int phase);
+template <int PU>
+__global__ void part_split_kernel(const uint32_t* in, int RW, const uint32_t* seg_lo, const uint32_t* seg_hi, int spg,
+                                  int K, int shift2, int P2, uint32_t* counts2, const uint32_t* base2, uint32_t* out,
+                                  int phase);
 __global__ void part_agg_kernel(const uint32_t* recs, int RW, const uint32_t* base, int64_t nsub, int64_t G, int shift,
-                                PartFields f, uint64_t* gacc);
+                                PartFields f, uint64_t* gacc, PartHaving hv, int64_t* out_keys,
+                                unsigned long long* out_count, int64_t cap);
 }  // namespace sdo
 
 namespace py = pybind11;
@@ -385,20 +389,41 @@ static void part_keys(uint64_t keys, int64_t n, int shift1, int P1, uint64_t cou
   check(hipGetLastError(), "part_keys_kernel launch");
 }
 
-static void part_split(uint64_t in, int RW, uint64_t base1, int P1, int K, int shift2, int P2, uint64_t counts2,
-                       uint64_t base2, uint64_t out, int phase, uint64_t stream) {
-  if (P1 <= 0 || K <= 0) return;
-  if (P2 <= 0 || P2 > 16384 || (P2 & (P2 - 1))) throw std::invalid_argument("part_split: P2 a power of two <= 16384");
+// groups x K blocks; group g's segments are [g*spg, (g+1)*spg) of seg_lo/seg_hi (a level-1 bucket
+// table passes base1 and base1 + 1 with spg = 1).
+static void part_split(uint64_t in, int RW, uint64_t seg_lo, uint64_t seg_hi, int64_t groups, int spg, int K,
+                       int shift2, int P2, uint64_t counts2, uint64_t base2, uint64_t out, int phase, uint64_t stream) {
+  if (groups <= 0 || K <= 0) return;
+  if (P2 <= 0 || P2 > 4096 || (P2 & (P2 - 1))) throw std::invalid_argument("part_split: P2 a power of two <= 4096");
   if (RW < 1 || RW > 2 + 2 * sdo::MAX_SLOTS) throw std::invalid_argument("part_split: record width");
-  hipLaunchKernelGGL(sdo::part_split_kernel, dim3((unsigned)((int64_t)P1 * K)), dim3(512), (unsigned)(P2 * 4),
-                     (hipStream_t)stream, (const uint32_t*)in, RW, (const uint32_t*)base1, K, shift2, P2,
-                     (uint32_t*)counts2, (const uint32_t*)base2, (uint32_t*)out, phase);
+  if (spg < 1) throw std::invalid_argument("part_split: segments per group");
+  // tile of 512 x PU records, ~32 KB of LDS whatever the record width
+  const int PU = RW <= 2 ? 8 : (RW <= 4 ? 4 : (RW <= 8 ? 2 : 1));
+  const int64_t lds = phase == 0 ? (int64_t)P2 * 4 : ((int64_t)3 * P2 + (int64_t)512 * PU * RW) * 4;
+  if (lds > 64 * 1024) throw std::invalid_argument("part_split: tile does not fit 64 KiB of LDS");
+  const void* f = PU == 8 ? (const void*)sdo::part_split_kernel<8>
+                : PU == 4 ? (const void*)sdo::part_split_kernel<4>
+                : PU == 2 ? (const void*)sdo::part_split_kernel<2> : (const void*)sdo::part_split_kernel<1>;
+  const uint32_t* in_ = (const uint32_t*)in;
+  const uint32_t* lo_ = (const uint32_t*)seg_lo;
+  const uint32_t* hi_ = (const uint32_t*)seg_hi;
+  uint32_t* c2 = (uint32_t*)counts2;
+  const uint32_t* b2 = (const uint32_t*)base2;
+  uint32_t* o = (uint32_t*)out;
+  void* args[] = {(void*)&in_, (void*)&RW, (void*)&lo_, (void*)&hi_, (void*)&spg, (void*)&K, (void*)&shift2,
+                  (void*)&P2, (void*)&c2, (void*)&b2, (void*)&o, (void*)&phase};
+  check(hipLaunchKernel(f, dim3((unsigned)(groups * K)), dim3(512), args, (size_t)lds, (hipStream_t)stream),
+        "part_split_kernel launch");
   check(hipGetLastError(), "part_split_kernel launch");
 }
 
+// having: [] for the dense table, else up to 4 (slot, is_f64, op, divisor, constant) terms; conj 1 = AND.
+// With terms, gacc receives the surviving rows ([cap][nslots]), out_keys their keys, out_count
+// (zeroed here) their number.
 static void part_agg(uint64_t recs, int RW, uint64_t base, int64_t nsub, int64_t G, int shift, std::vector<int> slot,
                      std::vector<int> width, std::vector<int> ops, std::vector<int64_t> init, uint64_t gacc,
-                     uint64_t stream) {
+                     std::vector<std::tuple<int, int, int, double, double>> having, int conj, uint64_t out_keys,
+                     uint64_t out_count, int64_t cap, uint64_t stream) {
   if (nsub <= 0 || G <= 0) return;
   sdo::PartFields f{};
   if (slot.size() != width.size() || slot.size() > (size_t)sdo::MAX_SLOTS) throw std::invalid_argument("part_agg: fields");
@@ -422,8 +447,25 @@ static void part_agg(uint64_t recs, int RW, uint64_t base, int64_t nsub, int64_t
   if (shift < 0 || lds > 64 * 1024) throw std::invalid_argument("part_agg: sub-bucket table exceeds 64 KiB of LDS");
   const int64_t grid = (nsub + 7) / 8 * 8;
   if (grid > ((int64_t)1 << 31) - 8) throw std::invalid_argument("part_agg: too many sub-buckets");
+  sdo::PartHaving hv{};
+  if (having.size() > 4) throw std::invalid_argument("part_agg: at most 4 having terms");
+  hv.nterms = (int)having.size();
+  hv.conj = conj;
+  for (size_t j = 0; j < having.size(); ++j) {
+    hv.slot[j] = std::get<0>(having[j]);
+    hv.f64[j] = std::get<1>(having[j]);
+    hv.op[j] = std::get<2>(having[j]);
+    hv.div[j] = std::get<3>(having[j]);
+    hv.c[j] = std::get<4>(having[j]);
+    if (hv.slot[j] < 0 || hv.slot[j] >= f.nslots || hv.op[j] < 0 || hv.op[j] > 2)
+      throw std::invalid_argument("part_agg: having term");
+  }
+  if (hv.nterms && (!out_keys || !out_count || cap < 0)) throw std::invalid_argument("part_agg: having output");
+  if (hv.nterms)
+    check(hipMemsetAsync((void*)out_count, 0, 8, (hipStream_t)stream), "part_agg count reset");
   hipLaunchKernelGGL(sdo::part_agg_kernel, dim3((unsigned)grid), dim3(512), (unsigned)lds, (hipStream_t)stream,
-                     (const uint32_t*)recs, RW, (const uint32_t*)base, nsub, G, shift, f, (uint64_t*)gacc);
+                     (const uint32_t*)recs, RW, (const uint32_t*)base, nsub, G, shift, f, (uint64_t*)gacc, hv,
+                     (int64_t*)out_keys, (unsigned long long*)out_count, cap);
   check(hipGetLastError(), "part_agg_kernel launch");
 }
 

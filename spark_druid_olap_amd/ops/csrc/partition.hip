@@ -139,37 +139,175 @@ __global__ __launch_bounds__(512) void part_keys_kernel(const int64_t* __restric
   }
 }
 
-// Level 2: K blocks per level-1 bucket p split it into P2 sub-buckets by bits [shift2, shift2+log2 P2).
-// counts2 is [P1 * P2][K] (row = p * P2 + q); phase 1 copies whole records (RW u32 words).
+// Split: records of input segments are partitioned into P2 buckets by bits [shift2, shift2+log2 P2)
+// of the key.  Input groups: group g owns segments [g*spg, (g+1)*spg), each [seg_lo[s], seg_hi[s]);
+// its output buckets are rows g*P2 .. g*P2+P2-1 (counts2 is [groups * P2][K]).  K blocks per group:
+// with one segment per group (a level-1 bucket) block k takes the k-th slice of its records, with
+// many (the producer's chunk regions) the k-th slice of its segments.
+//
+// phase 0 counts (LDS histogram).  phase 1 scatters through an LDS tile sort: a tile of 512 x PU
+// records is ranked per bucket (LDS atomics), reordered in LDS by bucket, and each thread then
+// writes consecutive sorted records -- a bucket's run of the tile lands as one contiguous,
+// coalesced store sequence instead of 64 scattered lines per wave instruction.  PU shrinks as
+// records widen (the tile stays ~32 KB of LDS).
+
+__device__ __forceinline__ void split_range_count(const uint32_t* __restrict__ in, int RW, uint32_t lo, uint32_t hi,
+                                                  int shift2, uint32_t mask, uint32_t* h) {
+  if (RW == 2) {
+    // two records per 16-byte load, 8 records per thread in flight
+    uint32_t i = lo;
+    if (i < hi && (i & 1u)) {  // align to a record pair
+      if (threadIdx.x == 0) atomicAdd(&h[(in[(uint64_t)i * 2] >> shift2) & mask], 1u);
+      ++i;
+    }
+    if (i >= hi) return;  // (empty, or the single odd record above)
+    const uint32_t npair = (hi - i) / 2;
+    const uint4* pr = (const uint4*)(in + (uint64_t)i * 2);
+    for (uint32_t j0 = threadIdx.x; j0 < npair; j0 += blockDim.x * 4) {
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t j = j0 + u * blockDim.x;
+        if (j < npair) v[u] = pr[j];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (j0 + u * blockDim.x < npair) {
+          atomicAdd(&h[(v[u].x >> shift2) & mask], 1u);
+          atomicAdd(&h[(v[u].z >> shift2) & mask], 1u);
+        }
+      }
+    }
+    if (((hi - i) & 1u) && threadIdx.x == 0) atomicAdd(&h[(in[(uint64_t)(hi - 1) * 2] >> shift2) & mask], 1u);
+    return;
+  }
+  for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += blockDim.x * 4) {
+    uint32_t key[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t i = i0 + u * blockDim.x;
+      key[u] = i < hi ? in[(uint64_t)i * RW] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i0 + u * blockDim.x < hi) atomicAdd(&h[(key[u] >> shift2) & mask], 1u);
+  }
+}
+
+template <int PU>
+__device__ __forceinline__ void split_range_scatter(const uint32_t* __restrict__ in, int RW, uint32_t lo, uint32_t hi,
+                                                    int shift2, uint32_t P2, uint32_t* cur, uint32_t* hist,
+                                                    uint32_t* tstart, uint32_t* tile, uint32_t* scan_lds,
+                                                    uint32_t* __restrict__ out) {
+  const uint32_t mask = P2 - 1u;
+  constexpr uint32_t TILE = 512u * PU;
+  for (uint32_t t0 = lo; t0 < hi; t0 += TILE) {
+    const uint32_t tn = hi - t0 < TILE ? hi - t0 : TILE;
+    for (uint32_t q = threadIdx.x; q < P2; q += blockDim.x) hist[q] = 0u;
+    __syncthreads();
+    uint32_t q_[PU], r_[PU];
+    uint2 v2[PU];
+#pragma unroll
+    for (int u = 0; u < PU; ++u) {
+      const uint32_t j = threadIdx.x + u * blockDim.x;
+      if (j < tn) {
+        const uint64_t i = (uint64_t)t0 + j;
+        if (RW == 2) {
+          v2[u] = *(const uint2*)(in + i * 2);
+        } else {
+          v2[u].x = in[i * RW];
+          v2[u].y = 0u;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PU; ++u) {
+      const uint32_t j = threadIdx.x + u * blockDim.x;
+      if (j < tn) {
+        q_[u] = (v2[u].x >> shift2) & mask;
+        r_[u] = atomicAdd(&hist[q_[u]], 1u);
+      }
+    }
+    __syncthreads();
+    // exclusive scan of the tile histogram -> bucket starts inside the tile
+    const uint32_t per = (P2 + blockDim.x - 1) / blockDim.x;
+    const uint32_t qa = threadIdx.x * per;
+    uint32_t sum = 0;
+    for (uint32_t q = qa; q < qa + per && q < P2; ++q) sum += hist[q];
+    uint32_t tot;
+    uint32_t pre = block_excl_scan_u32<512>(sum, scan_lds, &tot);
+    for (uint32_t q = qa; q < qa + per && q < P2; ++q) {
+      tstart[q] = pre;
+      pre += hist[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < PU; ++u) {
+      const uint32_t j = threadIdx.x + u * blockDim.x;
+      if (j < tn) {
+        const uint32_t d = tstart[q_[u]] + r_[u];
+        if (RW == 2) {
+          ((uint2*)tile)[d] = v2[u];
+        } else {
+          const uint32_t* rec = in + ((uint64_t)t0 + j) * RW;
+          for (int w = 0; w < RW; ++w) tile[(uint64_t)d * RW + w] = rec[w];
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < PU; ++u) {
+      const uint32_t j = threadIdx.x + u * blockDim.x;
+      if (j < tn) {
+        const uint32_t key = tile[(uint64_t)j * RW];
+        const uint32_t q = (key >> shift2) & mask;
+        const uint64_t pos = (uint64_t)cur[q] + (j - tstart[q]);
+        if (RW == 2) {
+          *(uint2*)(out + pos * 2) = ((const uint2*)tile)[j];
+        } else {
+          for (int w = 0; w < RW; ++w) out[pos * RW + w] = tile[(uint64_t)j * RW + w];
+        }
+      }
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < P2; q += blockDim.x) cur[q] += hist[q];
+    __syncthreads();
+  }
+}
+
+// dynamic LDS: phase 0: P2 words; phase 1: 3 * P2 + 512 * PU * RW words
+template <int PU>
 __global__ __launch_bounds__(512) void part_split_kernel(const uint32_t* __restrict__ in, int RW,
-                                                        const uint32_t* __restrict__ base1, int K, int shift2, int P2,
-                                                        uint32_t* __restrict__ counts2, const uint32_t* __restrict__ base2,
-                                                        uint32_t* __restrict__ out, int phase) {
+                                                        const uint32_t* __restrict__ seg_lo,
+                                                        const uint32_t* __restrict__ seg_hi, int spg, int K, int shift2,
+                                                        int P2, uint32_t* __restrict__ counts2,
+                                                        const uint32_t* __restrict__ base2, uint32_t* __restrict__ out,
+                                                        int phase) {
   extern __shared__ uint32_t h[];
-  const int64_t p = blockIdx.x / K;
+  __shared__ uint32_t scan_lds[8];
+  const int64_t g = blockIdx.x / K;
   const int k = blockIdx.x % K;
-  const uint32_t lo = base1[p], hi = base1[p + 1];
-  const uint64_t n = hi - lo;
-  const uint32_t a = lo + (uint32_t)(n * k / K), e = lo + (uint32_t)(n * (k + 1) / K);
-  const int64_t row0 = p * P2;
+  const int64_t row0 = g * P2;
   for (int q = threadIdx.x; q < P2; q += blockDim.x)
     h[q] = phase == 0 ? 0u : base2[row0 + q] + counts2[(row0 + q) * K + k];
   __syncthreads();
   const uint32_t mask = (uint32_t)P2 - 1u;
-  for (uint32_t i = a + threadIdx.x; i < e; i += blockDim.x) {
-    const uint32_t* rec = in + (uint64_t)i * RW;
-    const uint32_t key = rec[0];
-    const uint32_t q = (key >> shift2) & mask;
-    if (phase == 0) {
-      atomicAdd(&h[q], 1u);
-    } else {
-      const uint32_t pos = atomicAdd(&h[q], 1u);
-      uint32_t* o = out + (uint64_t)pos * RW;
-      if (RW == 2) {
-        *(uint2*)o = *(const uint2*)rec;
-      } else {
-        for (int w = 0; w < RW; ++w) o[w] = rec[w];
-      }
+  uint32_t* hist = h + P2;
+  uint32_t* tstart = h + 2 * P2;
+  uint32_t* tile = h + 3 * P2;
+  if (spg == 1) {
+    const uint32_t lo = seg_lo[g], hi = seg_hi[g];
+    const uint64_t n = hi > lo ? hi - lo : 0;
+    const uint32_t a = lo + (uint32_t)(n * k / K), e = lo + (uint32_t)(n * (k + 1) / K);
+    if (phase == 0) split_range_count(in, RW, a, e, shift2, mask, h);
+    else split_range_scatter<PU>(in, RW, a, e, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds, out);
+  } else {
+    const int64_t s0 = g * spg + (int64_t)spg * k / K, s1 = g * spg + (int64_t)spg * (k + 1) / K;
+    for (int64_t sgi = s0; sgi < s1; ++sgi) {
+      const uint32_t lo = seg_lo[sgi], hi = seg_hi[sgi];
+      if (hi <= lo) continue;  // (uniform across the block: every thread reads the same segment)
+      if (phase == 0) split_range_count(in, RW, lo, hi, shift2, mask, h);
+      else split_range_scatter<PU>(in, RW, lo, hi, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds, out);
     }
   }
   if (phase == 0) {
@@ -177,6 +315,15 @@ __global__ __launch_bounds__(512) void part_split_kernel(const uint32_t* __restr
     for (int q = threadIdx.x; q < P2; q += blockDim.x) counts2[(row0 + q) * K + k] = h[q];
   }
 }
+
+template __global__ void part_split_kernel<8>(const uint32_t*, int, const uint32_t*, const uint32_t*, int, int, int, int,
+                                             uint32_t*, const uint32_t*, uint32_t*, int);
+template __global__ void part_split_kernel<4>(const uint32_t*, int, const uint32_t*, const uint32_t*, int, int, int, int,
+                                             uint32_t*, const uint32_t*, uint32_t*, int);
+template __global__ void part_split_kernel<2>(const uint32_t*, int, const uint32_t*, const uint32_t*, int, int, int, int,
+                                             uint32_t*, const uint32_t*, uint32_t*, int);
+template __global__ void part_split_kernel<1>(const uint32_t*, int, const uint32_t*, const uint32_t*, int, int, int, int,
+                                             uint32_t*, const uint32_t*, uint32_t*, int);
 
 __device__ __forceinline__ void lds_fold(uint64_t* t, int op, int64_t v) {
   switch (op) {
@@ -192,9 +339,26 @@ __device__ __forceinline__ void lds_fold(uint64_t* t, int op, int64_t v) {
 // hardware deals block ids round-robin over the 8 XCDs), which keeps each XCD's writes to
 // neighbouring table lines.  The grid is a multiple of 8 blocks (>= nsub), so every r < nsub has
 // exactly one block.
+__device__ __forceinline__ bool having_pass(const PartHaving& h, const uint64_t* row) {
+  bool all = true, any = false;
+  for (int j = 0; j < h.nterms; ++j) {
+    const int64_t x = (int64_t)row[h.slot[j]];
+    const double v = h.f64[j] ? __longlong_as_double(x) : (double)x / h.div[j];
+    const bool t = h.op[j] == 0 ? v == h.c[j] : (h.op[j] == 1 ? v > h.c[j] : v < h.c[j]);
+    all = all && t;
+    any = any || t;
+  }
+  return h.conj ? all : any;
+}
+
+// HAVING mode: the groups of the sub-bucket that exist (presence count, slot 0, > 0) and pass the
+// predicate are appended -- key + slots -- at a position reserved with one global atomic per block;
+// writes past `cap` are dropped (the host sees out_count > cap and re-runs with room).
 __global__ __launch_bounds__(512) void part_agg_kernel(const uint32_t* __restrict__ recs, int RW,
                                                       const uint32_t* __restrict__ base, int64_t nsub, int64_t G,
-                                                      int shift, PartFields f, uint64_t* __restrict__ gacc) {
+                                                      int shift, PartFields f, uint64_t* __restrict__ gacc,
+                                                      PartHaving hv, int64_t* __restrict__ out_keys,
+                                                      unsigned long long* __restrict__ out_count, int64_t cap) {
   extern __shared__ __attribute__((aligned(16))) uint64_t t[];
   const int64_t x = blockIdx.x;
   const int64_t per_xcd = gridDim.x / 8;
@@ -207,26 +371,91 @@ __global__ __launch_bounds__(512) void part_agg_kernel(const uint32_t* __restric
   for (int64_t i = threadIdx.x; i < nk * NS; i += blockDim.x) t[i] = (uint64_t)f.init[i % NS];
   __syncthreads();
   const uint32_t lo = base[r], hi = base[r + 1];
-  for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-    const uint32_t* rec = recs + (uint64_t)i * RW;
-    const int64_t local = (int64_t)rec[0] - k0;
-    if ((uint64_t)local >= (uint64_t)nk) continue;  // cannot happen for consistent buckets; never fault
-    uint64_t* row = t + local * NS;
-    int w = 1;
-    for (int j = 0; j < f.nfields; ++j) {
-      const int wd = f.width[j];
-      int64_t v;
-      if (wd == 0) v = 1;
-      else if (wd == 1) v = (int64_t)(int32_t)rec[w];
-      else v = (int64_t)((uint64_t)rec[w] | ((uint64_t)rec[w + 1] << 32));
-      w += wd;
-      const int s = f.slot[j];
-      lds_fold(row + s, f.op[s], v);
+  constexpr int PU = 4;
+  const uint32_t step = blockDim.x * PU;
+  if (RW == 2 && f.nfields == 1 && f.width[0] == 1) {
+    // u32 key + one i32 value (TPC-H Q18: sum(l_quantity) per order): 8-byte record loads, PU in flight
+    const int s0 = f.slot[0], op = f.op[s0];
+    for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += step) {
+      uint2 r2[PU];
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        const uint32_t i = i0 + u * blockDim.x;
+        if (i < hi) r2[u] = *(const uint2*)(recs + (uint64_t)i * 2);
+      }
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        if (i0 + u * blockDim.x >= hi) break;
+        const int64_t local = (int64_t)r2[u].x - k0;
+        if ((uint64_t)local >= (uint64_t)nk) continue;
+        lds_fold(t + local * NS + s0, op, (int64_t)(int32_t)r2[u].y);
+      }
+    }
+  } else if (RW == 1 && f.nfields == 1 && f.width[0] == 0) {
+    // key only (histograms, unfiltered counts)
+    const int s0 = f.slot[0], op = f.op[s0];
+    for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += step) {
+      uint32_t kk[PU];
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        const uint32_t i = i0 + u * blockDim.x;
+        if (i < hi) kk[u] = recs[i];
+      }
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        if (i0 + u * blockDim.x >= hi) break;
+        const int64_t local = (int64_t)kk[u] - k0;
+        if ((uint64_t)local >= (uint64_t)nk) continue;
+        lds_fold(t + local * NS + s0, op, 1);
+      }
+    }
+  } else {
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+      const uint32_t* rec = recs + (uint64_t)i * RW;
+      const int64_t local = (int64_t)rec[0] - k0;
+      if ((uint64_t)local >= (uint64_t)nk) continue;  // cannot happen for consistent buckets; never fault
+      uint64_t* row = t + local * NS;
+      int w = 1;
+      for (int j = 0; j < f.nfields; ++j) {
+        const int wd = f.width[j];
+        int64_t v;
+        if (wd == 0) v = 1;
+        else if (wd == 1) v = (int64_t)(int32_t)rec[w];
+        else v = (int64_t)((uint64_t)rec[w] | ((uint64_t)rec[w + 1] << 32));
+        w += wd;
+        const int s = f.slot[j];
+        lds_fold(row + s, f.op[s], v);
+      }
     }
   }
   __syncthreads();
-  uint64_t* g = gacc + k0 * NS;
-  for (int64_t i = threadIdx.x; i < nk * NS; i += blockDim.x) g[i] = t[i];
+  if (hv.nterms == 0) {
+    uint64_t* g = gacc + k0 * NS;
+    for (int64_t i = threadIdx.x; i < nk * NS; i += blockDim.x) g[i] = t[i];
+    return;
+  }
+  __shared__ uint32_t scan_lds[8];
+  __shared__ unsigned long long blk_base;
+  uint32_t mine = 0;
+  for (int64_t i = threadIdx.x; i < nk; i += blockDim.x) {
+    const uint64_t* row = t + i * NS;
+    mine += ((int64_t)row[0] > 0 && having_pass(hv, row)) ? 1u : 0u;
+  }
+  uint32_t total;
+  uint32_t pre = block_excl_scan_u32<512>(mine, scan_lds, &total);
+  if (threadIdx.x == 0) blk_base = total ? atomicAdd(out_count, (unsigned long long)total) : 0ull;
+  __syncthreads();
+  if (total == 0) return;
+  int64_t pos = (int64_t)blk_base + pre;
+  for (int64_t i = threadIdx.x; i < nk; i += blockDim.x) {
+    const uint64_t* row = t + i * NS;
+    if (!((int64_t)row[0] > 0 && having_pass(hv, row))) continue;
+    if (pos < cap) {
+      out_keys[pos] = k0 + i;
+      for (int s = 0; s < NS; ++s) gacc[pos * NS + s] = row[s];
+    }
+    ++pos;
+  }
 }
 
 }  // namespace sdo

@@ -213,4 +213,18 @@ struct PartFields {
   int64_t init[MAX_SLOTS];
 };
 
+// HAVING fused into the partitioned aggregation (partition.hip part_agg_kernel): up to 4
+// comparisons of a slot value (int64 / scale divisor, or f64 bits) with a constant, AND-ed or
+// OR-ed.  nterms == 0: write the dense table instead.
+struct PartHaving {
+  int32_t nterms;
+  int32_t conj;           // 1: all terms, 0: any term
+  int32_t slot[4];
+  int32_t f64[4];         // slot holds double bits (else int64 divided by div)
+  int32_t op[4];          // 0 equalTo, 1 greaterThan, 2 lessThan
+  int32_t pad;
+  double div[4];
+  double c[4];
+};
+
 }  // namespace sdo

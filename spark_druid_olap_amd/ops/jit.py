@@ -100,7 +100,7 @@ def col_infos(prog) -> Dict[int, ColInfo]:
     return out
 
 
-PART_MAX_BUCKETS = 1024  # level-1 buckets of the partitioned group-by (LDS counters per block)
+PART_MAX_BUCKETS = 1024  # level-1 buckets of the partitioned group-by (split kernel LDS cursors)
 
 
 def part_fields(prog, cols=None) -> List[Tuple[int, int]]:
@@ -192,8 +192,6 @@ def layout(prog, mode: int, U: int, hll_lds: bool, m: int, reg: bool = False, pi
         while ncopy > 1 and base * ncopy + hll_bytes + stage > budget:
             ncopy //= 2
         acc_bytes = base * ncopy
-    if mode == D.M_PART:
-        acc_bytes = PART_MAX_BUCKETS * 4  # level-1 bucket counters / cursors
     acc_off = 0
     hll_off = (acc_bytes + 15) // 16 * 16
     cache_off = (hll_off + hll_bytes + 15) // 16 * 16
@@ -237,9 +235,8 @@ def _dlit(v: float) -> str:
 
 class _Gen:
     def __init__(self, prog, mode: int, U: int, hll_lds: bool, narrow4: bool, lay: JitLayout, m: int,
-                 reg: bool = False, part_phase: int = 0):
+                 reg: bool = False):
         self.p = prog
-        self.part_phase = part_phase
         self.reg = reg
         self.pipe = lay.pipe
         self.regstage = lay.regstage
@@ -473,22 +470,19 @@ class _Gen:
 
     # ---------------------------------------------------------------- whole kernel
     def _part_record(self, body: List[str]) -> None:
-        """M_PART: the row becomes a partition record instead of a table update (ops/csrc/partition.hip).
-        Phase 0 counts the rows of each bucket (LDS counters); phase 1 appends the record -- u32 key,
-        then every aggregator's value (``part_fields``: implicit / i32 / i64 words; a row an
-        aggregator's own filter rejects carries the slot's identity)."""
+        """M_PART producer: the row becomes a partition record (ops/csrc/partition.hip) instead of a
+        table update -- u32 key, then every aggregator's value (``part_fields``: implicit / i32 /
+        i64 words; a row an aggregator's own filter rejects carries the slot's identity).  Records
+        are appended to the chunk's own region (chunk c owns records [4096 c, 4096 c + 4096)), at
+        the wave's running offset plus the lane's rank among the active lanes: consecutive lanes
+        write consecutive records, no atomics; the split kernels then bucket them."""
         p = self.p
         body.append("        const bool mine = act[u];")
-        body.append("        if (mine) {")
-        body.append("          const uint32_t pb_ = (uint32_t)(key >> pshift);")
-        if self.part_phase == 0:
-            body.append("          atomicAdd(&pcnt[pb_], 1u);")
-            body.append("        }")
-            return
+        body.append("        const uint64_t am_ = __ballot(mine);")
         fields = part_fields(p, self.cols)
         rw = 1 + sum(w for _, w in fields)
-        body.append("          const uint32_t pos_ = atomicAdd(&pcnt[pb_], 1u);")
-        body.append(f"          uint32_t* o_ = precs + (uint64_t)pos_ * {rw}u;")
+        body.append("        if (mine) {")
+        body.append(f"          uint32_t* o_ = precs + (uint64_t)(cbase + woff + (uint32_t)__popcll(am_ & lmlt)) * {rw}u;")
         body.append("          o_[0] = (uint32_t)key;")
         w = 1
         fi = 0
@@ -497,12 +491,11 @@ class _Gen:
                 continue
             slot, width = fields[fi]
             fi += 1
+            if width == 0:
+                continue
             cond = None
             if a.get("filt_len"):
                 cond = f"((({self.word_expr(a['filt_off'], a['filt_off'] + a['filt_len'])}) >> lane) & 1ull)"
-            if width == 0:
-                w += 0
-                continue
             val = f"v{ai}_[u]"
             if a["kind"] == D.A_COUNT:
                 val = f"({cond} ? 1LL : 0LL)" if cond else "1LL"
@@ -515,6 +508,7 @@ class _Gen:
                             f"o_[{w + 1}] = (uint32_t)(x_ >> 32); }}")
             w += width
         body.append("        }")
+        body.append("        woff += (uint32_t)__popcll(am_);")
 
     def source(self, name: str) -> str:
         p, U, NP, lay = self.p, self.U, self.NP, self.lay
@@ -709,19 +703,9 @@ class _Gen:
         out.extend(L)
         out.extend("  " + x for x in self.pre_lines)
         if mode == D.M_PART:
-            out.append("  uint32_t* pcnt = (uint32_t*)lds;")
             out.append("  uint32_t* precs = (uint32_t*)d->part_recs;")
-            out.append("  uint32_t* pcounts = (uint32_t*)d->part_counts;")
-            out.append("  const uint32_t* pbase = (const uint32_t*)d->part_base;")
-            out.append("  const int pshift = d->part_shift;")
-            out.append("  const int pn = d->part_n;")
-            out.append("  (void)precs; (void)pbase;")
-            if self.part_phase == 0:
-                out.append(f"  for (int i = threadIdx.x; i < pn; i += {W * 64}) pcnt[i] = 0u;")
-            else:
-                out.append(f"  for (int i = threadIdx.x; i < pn; i += {W * 64}) "
-                           "pcnt[i] = pbase[i] + pcounts[(int64_t)i * gridDim.x + blockIdx.x];")
-            out.append("  __syncthreads();")
+            out.append("  uint32_t* pend = (uint32_t*)d->part_counts;  // end offset of each chunk's records")
+            out.append("  const uint64_t lmlt = (1ull << lane) - 1ull;")
         if mode == D.M_DENSE_LDS:
             out.append(f"  for (int i = threadIdx.x; i < {G * NS * NCT}; i += {W * 64}) {{")
             inits = ", ".join(_lit(init) for _, init in p.slots)
@@ -747,6 +731,10 @@ class _Gen:
         out.append("  const int64_t num_rows = d->num_rows;")
         out.append("  const int nranges = d->nranges;")
         out.append("  for (int64_t c = gw; c < d->total_chunks; c += total_waves) {")
+        if mode == D.M_PART:
+            out.append(f"    const uint32_t cbase = (uint32_t)c * {D.CHUNK_ROWS}u;")
+            out.append("    uint32_t woff = 0;")
+            out.append("    if (lane == 0) pend[c] = cbase;  // (a skipped chunk holds no records)")
         out.append("    int r = 0;")
         out.append("    int64_t cc = c;")
         out.append("    while (r < nranges - 1 && cc >= d->ranges[r].nchunks) { cc -= d->ranges[r].nchunks; ++r; }")
@@ -818,6 +806,8 @@ class _Gen:
         for g in range(G if narrow else 0):
             for s in sorted(narrow):
                 out.append(f"    r{g}_{s} += n{g}_{s}; n{g}_{s} = 0;")
+        if mode == D.M_PART:
+            out.append("    if (lane == 0) pend[c] = cbase + woff;")
         out.append("  }")
         if self.reg:
             # wave-reduce each register partial; lane 0 stores the wave's copy for the block flush
@@ -836,10 +826,6 @@ class _Gen:
                         out.append("    const int64_t b = v;")
                     out.append(f"    if (lane == 0) acc[({g} * {NS} + {s}) * {NCT} + wave] = (uint64_t)b;")
                     out.append("  }")
-        if mode == D.M_PART and self.part_phase == 0:
-            out.append("  __syncthreads();")
-            out.append(f"  for (int i = threadIdx.x; i < pn; i += {W * 64}) "
-                       "pcounts[(int64_t)i * gridDim.x + blockIdx.x] = pcnt[i];")
         if mode == D.M_DENSE_LDS:
             out.append("  __syncthreads();")
             out.append(f"  for (int i = threadIdx.x; i < {G * NS}; i += {W * 64}) {{")
@@ -908,14 +894,14 @@ class JitScan:
 
     def __init__(self, prog, mode: int, U: int, hll_lds: bool, m: int, narrow4: bool, load: bool = True,
                  reg: Optional[bool] = None, pipe: bool = False, budget: int = 150 * 1024,
-                 regstage: bool = False, shared: bool = False, part_phase: int = 0):
+                 regstage: bool = False, shared: bool = False):
         self.reg = False if shared else (reg_eligible(prog, mode) if reg is None else reg)
         self.lay = layout(prog, mode, U, hll_lds, m, self.reg, pipe and not regstage, budget, regstage, shared)
         if self.lay.total > 160 * 1024:
             raise ValueError(f"jit layout needs {self.lay.total} B of LDS")
-        g = _Gen(prog, mode, U, hll_lds, narrow4, self.lay, m, self.reg, part_phase)
-        tag = hashlib.sha1(repr((mode, U, self.reg, pipe, self.lay.ncopy, regstage, self.lay.shared,
-                                 part_phase)).encode()).hexdigest()[:6]
+        g = _Gen(prog, mode, U, hll_lds, narrow4, self.lay, m, self.reg)
+        tag = hashlib.sha1(repr((mode, U, self.reg, pipe, self.lay.ncopy, regstage, self.lay.shared)).encode()
+                           ).hexdigest()[:6]
         self.name = f"sdo_jit_{tag}"
         self.src = g.source(self.name)
         self.handle = compile_source(self.src, self.name) if load else -1

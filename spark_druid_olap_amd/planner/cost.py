@@ -208,13 +208,14 @@ def explain_cost(session, dq) -> str:
     return "\n".join(lines)
 
 
-def broker_cost_ms(ds, spec, info=None, world_size: int = 1) -> float:
+def broker_cost_ms(ds, spec, info=None, world_size: int = 1, est: Optional[CostEstimate] = None) -> float:
     """One fused scan over every resident segment of the shard, then ONE cross-rank merge of the
     whole state (not overlapped with anything)."""
-    return estimate(ds, spec, info, world_size).total_ms
+    return (est or estimate(ds, spec, info, world_size)).total_ms
 
 
-def historical_cost_ms(ds, spec, segments_per_query: int, info=None, world_size: int = 1) -> float:
+def historical_cost_ms(ds, spec, segments_per_query: int, info=None, world_size: int = 1,
+                       est: Optional[CostEstimate] = None) -> float:
     """Segment-batched ("historical") execution (the reference's historical waves + Spark
     shuffle/agg, ``asd/DruidQueryCostModel.scala:505-547``): B = segments / n scans, each followed
     by a merge of that batch's partials that runs while the next batch scans
@@ -223,7 +224,7 @@ def historical_cost_ms(ds, spec, segments_per_query: int, info=None, world_size:
     state: pipelining pays only when one merge is shorter than one batch's scan, and even then
     the last merge and B launches remain -- on one MI355X, and for dense states on xGMI, the
     broker plan is never more expensive, which is what this model says."""
-    c = estimate(ds, spec, info, world_size)
+    c = est or estimate(ds, spec, info, world_size)
     nseg = max(1, sum(1 for _ in ds.segments))
     batches = max(1, math.ceil(nseg / max(1, segments_per_query)))
     s_b = c.scan_ms / batches + LAUNCH_S * 1e3
@@ -254,10 +255,11 @@ def choose_method_costed(ds, spec, conf=None, info=None, world_size: int = 1) ->
             limit = int(conf.typed("spark.sparklinedata.druid.querycostmodel.histSegsPerQueryLimit"))
         except Exception:  # noqa: BLE001
             pass
-    costs = {"broker": broker_cost_ms(ds, spec, info, world_size)}
+    est = estimate(ds, spec, info, world_size)  # one estimate prices every alternative
+    costs = {"broker": broker_cost_ms(ds, spec, info, world_size, est)}
     best, best_n = costs["broker"], None
     for n in range(1, max(1, limit) + 1):
-        h = historical_cost_ms(ds, spec, n, info, world_size)
+        h = historical_cost_ms(ds, spec, n, info, world_size, est)
         costs[f"historical(n={n})"] = h
         if h < best:
             best, best_n = h, n
@@ -378,8 +380,8 @@ def plan_groupby(prog, jit: bool, local: bool) -> GroupByPlan:
 
 
 def partitioned_cost_s(prog, est_rows: float) -> Optional[float]:
-    """Radix-partitioned group-by (ops/csrc/partition.hip): two producer scans (count, scatter),
-    records written once per level and read by the next, and the dense table written once."""
+    """Radix-partitioned group-by (ops/csrc/partition.hip): one producer scan appending records,
+    a count + tile-sorted scatter pass per level, the LDS aggregation, the dense table written once."""
     from ..ops import jit
 
     if not jit.part_eligible(prog):
@@ -395,8 +397,10 @@ def partitioned_cost_s(prog, est_rows: float) -> Optional[float]:
     except ValueError:
         return None
     rec = 4 * L["rw"]
-    traffic = est_rows * rec * (2 * L["levels"]) + 2 * est_rows * rec + prog.G * max(1, prog.nslots) * 8
-    return traffic / HBM_BW + (4 + 4 * L["levels"]) * LAUNCH_S
+    # producer write, per level a count read + a scatter read and write, the aggregation read, the table
+    passes = 1 + 3 * L["levels"] + 1
+    traffic = est_rows * rec * passes + prog.G * max(1, prog.nslots) * 8
+    return traffic / HBM_BW + (2 + 4 * L["levels"]) * LAUNCH_S
 
 
 @dataclass

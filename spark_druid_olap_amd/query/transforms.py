@@ -178,9 +178,11 @@ BATCHES = [
 def transform(q: S.QuerySpec, ctx: TransformContext) -> S.QuerySpec:
     for _name, max_iter, fns in BATCHES:
         for _ in range(max_iter):
-            before = q.to_json()
+            before = q
             for fn in fns:
                 q = fn(q, ctx)
-            if q.to_json() == before:
+            # fixpoint: rules return their input when they do not apply; otherwise compare the
+            # specs field by field (dataclass equality -- no JSON rendering per iteration)
+            if q is before or q == before:
                 break
     return q

@@ -13,7 +13,9 @@ rank's shard and merge over RCCL inside the engine, so results are global on eve
 from __future__ import annotations
 
 import json
+import os
 import threading
+from collections import OrderedDict
 import time
 from typing import Any, Dict, List, Optional, Sequence, Tuple, Iterator
 
@@ -207,7 +209,7 @@ class Session:
         from .utils.metrics import ServerMetrics
 
         self.metrics = ServerMetrics()  # per-endpoint latency percentiles / QPS (servers record)
-        self._plan_cache: Dict[Tuple[str, int, int, str], DataFrame] = {}
+        self._plan_cache: "OrderedDict[tuple, DataFrame]" = OrderedDict()
         self._lock = threading.RLock()
         self._tl = threading.local()
         from .modules import load_modules
@@ -308,6 +310,11 @@ class Session:
                     return r
         from .utils import trace as T
 
+        # a statement planned before (same text, catalog, database, temp views, SET values) skips
+        # the parser too: the cache only holds queries
+        hit = self._cached_plan(text)
+        if hit is not None:
+            return hit
         try:
             with T.span("sdo.parse"):
                 st = parse(text)
@@ -318,22 +325,40 @@ class Session:
                 return self._query(text, st)
         return self._command(text, st)
 
-    def _query(self, text: str, st) -> DataFrame:
+    PLAN_CACHE_MAX = int(os.environ.get("SDO_PLAN_CACHE_MAX", "4096"))
+
+    def _plan_key(self, text: str):
         # statements over the d$* metadata views are planned afresh (their rows are the metadata
         # at planning time); everything else is cached by text + catalog / registry / conf state
-        cache_on = bool(self.conf.typed("spark.sparklinedata.druid.planCache.enabled")) and "d$" not in text.lower()
-        key = (text, self.catalog.version, self.catalog.current_db, id(self.catalog.temp) if self.catalog.temp else 0,
-               self.catalog.cluster.generation, json.dumps(self.conf.items(), sort_keys=True))
-        if cache_on:
+        if "d$" in text.lower() or not self.conf.typed("spark.sparklinedata.druid.planCache.enabled"):
+            return None
+        return (text, self.catalog.version, self.catalog.current_db, id(self.catalog.temp) if self.catalog.temp else 0,
+                self.catalog.cluster.generation, self.conf.cache_key())
+
+    def _cached_plan(self, text: str) -> Optional[DataFrame]:
+        key = self._plan_key(text)
+        if key is None:
+            return None
+        hit = self._plan_cache.get(key)
+        if hit is not None:
+            try:
+                self._plan_cache.move_to_end(key)  # LRU (a dashboard's few thousand parameterizations)
+            except KeyError:
+                pass
+        return hit
+
+    def _query(self, text: str, st) -> DataFrame:
+        key = self._plan_key(text)
+        if key is not None:
             hit = self._plan_cache.get(key)
             if hit is not None:
                 return hit
         df = self.plan(text, st)
-        if cache_on:
+        if key is not None:
             with self._lock:
-                if len(self._plan_cache) > 256:
-                    self._plan_cache.clear()
                 self._plan_cache[key] = df
+                while len(self._plan_cache) > self.PLAN_CACHE_MAX:
+                    self._plan_cache.popitem(last=False)
         return df
 
     def plan(self, text: str, st=None) -> DataFrame:

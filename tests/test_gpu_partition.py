@@ -40,7 +40,7 @@ def _compare(prog, table_bytes, monkeypatch):
 
     monkeypatch.setattr(DE, "PART_TABLE_BYTES", table_bytes)
     part = DE.PreparedScan(prog, mode=D.M_PART)
-    assert part.mode == D.M_PART and part.jit_scatter is not None, "partitioned path did not compile"
+    assert part.mode == D.M_PART and part.jit is not None, "partitioned path did not compile"
     ref = DE.PreparedScan(prog, mode=D.M_DENSE_GLOBAL)
     for _ in range(2):  # re-execution: no reset pass, every table row rewritten
         a = part.run()
@@ -101,13 +101,14 @@ def test_part_keys_histogram_vs_bincount():
     nat.part_keys(keys.data_ptr(), keys.numel(), s1, P1, c1.data_ptr(), 0, recs1.data_ptr(), 0, grid, st)
     nat.part_scan(c1.data_ptr(), P1, grid, t1.data_ptr(), base1.data_ptr(), st)
     nat.part_keys(keys.data_ptr(), keys.numel(), s1, P1, c1.data_ptr(), base1.data_ptr(), recs1.data_ptr(), 1, grid, st)
-    args = (recs1.data_ptr(), 1, base1.data_ptr(), P1, K, shift, P2, c2.data_ptr())
+    b1 = base1.data_ptr()
+    args = (recs1.data_ptr(), 1, b1, b1 + 4, P1, 1, K, shift, P2, c2.data_ptr())
     nat.part_split(*args, 0, 0, 0, st)
     nat.part_scan(c2.data_ptr(), P1 * P2, K, t2.data_ptr(), base2.data_ptr(), st)
     nat.part_split(*args, base2.data_ptr(), recs2.data_ptr(), 1, st)
     out = torch.empty(nbins, dtype=torch.int64, device=dev)
     nat.part_agg(recs2.data_ptr(), 1, base2.data_ptr(), P1 * P2, nbins, shift, [0], [0], [D.S_SUM_I], [0],
-                 out.data_ptr(), st)
+                 out.data_ptr(), [], 1, 0, 0, 0, st)
     torch.cuda.synchronize()
     valid = keys[(keys >= 0) & (keys < nbins)]
     assert int(base1[-1]) == valid.numel() == int(base2[-1])
@@ -133,3 +134,56 @@ def test_tpch_q18_forced_partitioned_vs_reference(monkeypatch):
         q = dict(tpch22.QUERIES)["Q18"]
         outs.append(sorted(tuple(r) for r in s.sql(q).collect()))
     assert outs[0] == outs[1] and len(outs[0]) > 0
+
+
+@pytest.mark.parametrize("conj", [True, False])
+def test_fused_having_matches_dense_then_filter(gpu_ds, monkeypatch, conj):
+    """HAVING fused into the partitioned aggregation == the dense table filtered afterwards (only
+    existing groups; both conjunction and disjunction; a tiny first capacity forces the re-run)."""
+    from spark_druid_olap_amd.engine import device_exec as DE
+
+    prog = _order_prog(gpu_ds)
+    dense = DE.PreparedScan(prog, mode=D.M_PART).run().acc.clone()
+    hv = DE.PreparedScan(prog, mode=D.M_PART)
+    hv.part_cap = 64
+    # slot 1: sum(l_quantity); slot 0: the presence count
+    terms = [(1, 0, 1, 1.0, 120.0), (0, 0, 2, 1.0, 4.0)]
+    assert hv.set_part_having(terms, conj)
+    got = hv.run()
+    assert got.kind == "sparse"
+    q, c = dense[:, 1].double(), dense[:, 0].double()
+    m = (q > 120) & (c < 4) if conj else (q > 120) | (c < 4)
+    m &= dense[:, 0] > 0
+    want = torch.nonzero(m).flatten()
+    order = torch.argsort(got.keys)
+    assert torch.equal(got.keys[order].cpu(), want.cpu())
+    assert torch.equal(got.acc[order].cpu(), dense[want].cpu())
+
+
+@pytest.mark.parametrize("nbins", [(1 << 18) + 5, (1 << 24) + 3])
+def test_native_histogram_partitioned_vs_bincount(nbins):
+    """native.histogram over a large bin range takes the partitioned path (one and two levels)."""
+    from spark_druid_olap_amd.ops import native
+
+    g = torch.Generator(device="cpu").manual_seed(nbins)
+    keys = torch.randint(0, nbins, (2_500_000,), generator=g, dtype=torch.int64).cuda()
+    got = native.histogram(keys, nbins)
+    assert got.dtype == torch.int64 and torch.equal(got, torch.bincount(keys, minlength=nbins))
+
+
+def test_two_level_narrow_records_with_empty_buckets(gpu_ds, monkeypatch):
+    """8-byte records (key + one i32 sum: the vectorised count path) over a key space that is not a
+    power of two, so high level-1 buckets are empty and level-2 slices start at odd offsets."""
+    from spark_druid_olap_amd.engine import device_exec as DE
+    from spark_druid_olap_amd.engine.lower import Lowerer
+
+    prog = Lowerer(gpu_ds).lower_aggregate(["1992-01-01/1999-01-01"], None, [S.DefaultDimensionSpec("o_orderkey")],
+                                           S.Granularity.parse("all"),
+                                           [S.FunctionAggregationSpec("longSum", "q", "l_quantity")])
+    monkeypatch.setattr(DE, "PART_TABLE_BYTES", 256)
+    part = DE.PreparedScan(prog, mode=D.M_PART)
+    assert part.mode == D.M_PART and part.part["levels"] == 2 and part.part["rw"] == 2
+    assert part.part["p1"] * part.part["p2"] * (1 << part.part["shift"]) > 1.5 * prog.G  # empty buckets exist
+    a = part.run().acc.clone()
+    b = DE.PreparedScan(prog, mode=D.M_DENSE_GLOBAL).run().acc
+    assert torch.equal(a, b)

@@ -75,9 +75,9 @@ def test_jit_presence_only_kernel_compiles(tmp_path, monkeypatch, ds_small):
 
 
 def test_jit_partition_producers_compile(tmp_path, monkeypatch, ds_small):
-    """M_PART (radix-partitioned group-by): the count producer bumps LDS bucket counters and the
-    scatter producer appends u32 key + value records (narrow sums as one word, doubles as two,
-    filtered aggregators carry the slot identity when their filter rejects the row)."""
+    """M_PART (radix-partitioned group-by): the producer appends u32 key + value records into its
+    chunk's region without atomics (narrow sums as one word, doubles as two, filtered aggregators
+    carry the slot identity when their filter rejects the row)."""
     from spark_druid_olap_amd.engine.lower import Lowerer
     from spark_druid_olap_amd.ops import desc as D
     from spark_druid_olap_amd.ops import jit
@@ -93,11 +93,9 @@ def test_jit_partition_producers_compile(tmp_path, monkeypatch, ds_small):
     assert jit.part_eligible(prog)
     fields = jit.part_fields(prog)
     assert [w for _, w in fields] == [0, 1, 1, 1]  # extendedprice: exact i32 cents
-    c = jit.JitScan(prog, D.M_PART, 4, False, 2048, True, load=False, part_phase=0)
-    w = jit.JitScan(prog, D.M_PART, 4, False, 2048, True, load=False, part_phase=1)
-    assert "atomicAdd(&pcnt[pb_], 1u);" in c.src and "precs" not in c.src.split("pcounts[(int64_t)i")[0][-300:]
-    assert "uint32_t* o_ = precs + (uint64_t)pos_ * 4u;" in w.src
-    assert c.lay.acc_bytes == jit.PART_MAX_BUCKETS * 4 and c.name != w.name
+    w = jit.JitScan(prog, D.M_PART, 4, False, 2048, True, load=False)
+    assert "uint32_t* o_ = precs + (uint64_t)(cbase + woff + (uint32_t)__popcll(am_ & lmlt)) * 4u;" in w.src
+    assert "pend[c] = cbase + woff;" in w.src and "atomic" not in w.src.split("void sdo_jit")[-1]
 
 
 

@@ -215,10 +215,22 @@ def main():
     s.register_datasource(ds)
     s.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)
     s.sql(tpch.druid_ddl(source="orderLineItemPartSupplierBase", datasource="tpch", with_column_mapping=False))
+    exec_cost = []  # (thread CPU s, wall s) of every server-side execution
     if a.server == "native":
         from spark_druid_olap_amd.server.gateway import NativeHiveServer
 
-        srv = NativeHiveServer(s, port=0).start()
+        srv = NativeHiveServer(s, port=0)
+        real = srv._execute
+
+        def timed(bid, sid, stmt):
+            c0, w0 = time.thread_time(), time.perf_counter()
+            try:
+                return real(bid, sid, stmt)
+            finally:
+                exec_cost.append((time.thread_time() - c0, time.perf_counter() - w0))
+
+        srv._execute = timed
+        srv.start()
     else:
         srv = HiveThriftServer(s, port=0).start()
     print(f"[conc] server up on {srv.port}: SF{a.sf:g} {ds.num_rows} rows on {dev} in {time.time() - t0:.1f}s",
@@ -259,6 +271,7 @@ def main():
             f.write(sampler.report(60))
     cpu1 = time.process_time()
     co1, ex1 = counters()
+    ncost = len(exec_cost)
     res = []
     for _ in ps:
         res.extend(res_q.get())
@@ -281,6 +294,9 @@ def main():
            "max_ms": max(lat) if lat else None, "sf": a.sf, "device": dev, "per_query": per,
            "first_error": errs[0][4] if errs else None,
            "server": {"kind": a.server, "cpu_cores": round((cpu1 - cpu0) / a.duration, 2), "executions": ex1 - ex0,
+                      "exec_thread_cpu_ms": round(1e3 * sum(c for c, _ in exec_cost[:ncost]) / max(1, ncost), 3),
+                      "exec_wall_ms": round(1e3 * sum(w for _, w in exec_cost[:ncost]) / max(1, ncost), 3),
+                      "executors": getattr(srv, "nexec", None),
                       "coalesced": co1 - co0, "slots": co.scheduler.nslots,
                       "slot_wait_ms_total": round(co.scheduler.stats["wait_ms"], 1)}}
     print(json.dumps(out), flush=True)

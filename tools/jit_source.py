@@ -57,14 +57,12 @@ def main():
                 regstage = jit.prefer_regstage(prog)
                 lay = jit.layout(prog, mode, 4, bool(prog.nhll) and gp.hll_lds, 1 << prog.hll_p, False, False,
                                  (160 * 1024) // 3 - 512, regstage, gp.shared)
-                for phase in ((0, 1) if mode == D.M_PART else (0,)):
-                    g = jit._Gen(prog, mode, 4, bool(prog.nhll) and gp.hll_lds, True, lay, 1 << prog.hll_p,
-                                 part_phase=phase)
-                    src = g.source("sdo_jit_probe")
-                    print(src)
-                    if os.environ.get("SDO_JIT_COMPILE"):  # hipRTC for gfx950 (no GPU needed)
-                        code = jit.compile_code(src, "sdo_jit_probe")
-                        print(f"// compiled: {len(code)} bytes of gfx950 code object")
+                g = jit._Gen(prog, mode, 4, bool(prog.nhll) and gp.hll_lds, True, lay, 1 << prog.hll_p)
+                src = g.source("sdo_jit_probe")
+                print(src)
+                if os.environ.get("SDO_JIT_COMPILE"):  # hipRTC for gfx950 (no GPU needed)
+                    code = jit.compile_code(src, "sdo_jit_probe")
+                    print(f"// compiled: {len(code)} bytes of gfx950 code object")
 
 
 if __name__ == "__main__":
