@@ -13,6 +13,9 @@ from __future__ import annotations
 
 import math
 import os
+import threading
+import weakref
+from collections import OrderedDict
 from typing import List, Optional
 
 import numpy as np
@@ -188,10 +191,9 @@ class PreparedScan:
                 # the interpreter kernel only knows per-wave copies: accumulate in HBM instead
                 self.mode, self.shared, self.lds = D.M_DENSE_GLOBAL, False, 0
                 self.jit = _jit_for(prog, self.mode, False, self.m)
-        import threading
-
         self._slot_lock = threading.Lock()
         self._slots = {}
+        weakref.finalize(self, _forget_prep, id(self))
         self._bufs()  # the preparing slot's buffers (settles the LDS-budget mode fallback)
 
     # ------------------------------------------------------------------ buffers
@@ -208,6 +210,9 @@ class PreparedScan:
                 b = self._slots.get(slot)
                 if b is None:
                     b = self._slots[slot] = self._alloc(self.cap)
+            _buffers_acquired(self, slot, b)
+        else:
+            _buffers_used(self, slot)
         return b
 
     def _alloc(self, cap: int) -> "_Bufs":
@@ -431,6 +436,7 @@ class PreparedScan:
             if int(b.overflow.item()) == 0:
                 break
             b = self._slots[current_slot()] = self._alloc(b.cap * 4)  # grow and retry
+            _buffers_acquired(self, current_slot(), b)
             self.cap = max(self.cap, b.cap)
         if self.mode == D.M_HASH:
             valid = _nonzero_big(b.keys != -1)
@@ -442,7 +448,8 @@ class PreparedScan:
             want = _next_pow2(2 * int(valid.numel()) + 1024)
             if want * 4 <= b.cap:
                 self.cap = want
-                self._slots[current_slot()] = self._alloc(want)
+                nb = self._slots[current_slot()] = self._alloc(want)
+                _buffers_acquired(self, current_slot(), nb)
             return out
         return Partials("dense", b.acc, None, [h.view(b.rows, self.m) for h in b.hll])
 
@@ -460,6 +467,68 @@ class PreparedScan:
         acc = torch.empty((0, prog.nslots), dtype=torch.int64, device=self.dev)
         return Partials("sparse", acc, torch.zeros(0, dtype=torch.int64, device=self.dev),
                         [torch.zeros((0, self.m), dtype=torch.uint8, device=self.dev) for _ in range(prog.nhll)])
+
+
+# ------------------------------------------------------------------------------------------------
+# Device-buffer budget across prepared scans.  Plans stay cached (a dashboard's thousands of
+# parameterizations), but their per-slot device buffers -- a 150M-group table is 1.2-2.4 GB -- are
+# released least-recently-used first once all prepared scans together hold more than the budget;
+# a released scan re-allocates on its next run (from the caching allocator's free blocks, usually:
+# parameterizations of one shape have the same buffer sizes).  Callers still holding partials keep
+# those tensors alive by reference, so a release never pulls memory from under a running query.
+BUF_BUDGET = int(os.environ.get("SDO_SCAN_BUF_BUDGET", str(24 << 30)))
+_buf_lru: "OrderedDict[tuple, tuple]" = OrderedDict()   # (id(prep), slot) -> (weakref(prep), bytes)
+_buf_total = [0]
+_buf_lock = threading.Lock()
+
+
+def _bufs_nbytes(b: "_Bufs") -> int:
+    n = 0
+    for t in [b.acc, b.keys, b.overflow, b.desc, b.touch, b.init_row] + list(b.hll):
+        n += t.numel() * t.element_size()
+    for v in (b.part or {}).values():
+        if isinstance(v, torch.Tensor):
+            n += v.numel() * v.element_size()
+        elif isinstance(v, tuple):
+            n += sum(t.numel() * t.element_size() for t in v if isinstance(t, torch.Tensor))
+    return n
+
+
+def _buffers_acquired(prep, slot, b) -> None:
+    key = (id(prep), slot)
+    nb = _bufs_nbytes(b)
+    victims = []
+    with _buf_lock:
+        old = _buf_lru.pop(key, None)
+        if old is not None:
+            _buf_total[0] -= old[1]
+        _buf_lru[key] = (weakref.ref(prep), nb)
+        _buf_total[0] += nb
+        while _buf_total[0] > BUF_BUDGET and len(_buf_lru) > 1:
+            k, (ref, n) = next(iter(_buf_lru.items()))
+            if k == key:
+                break
+            _buf_lru.pop(k)
+            _buf_total[0] -= n
+            victims.append((ref(), k[1]))
+    for p, sl in victims:
+        if p is not None:
+            with p._slot_lock:
+                p._slots.pop(sl, None)
+
+
+def _buffers_used(prep, slot) -> None:
+    key = (id(prep), slot)
+    with _buf_lock:
+        if key in _buf_lru:
+            _buf_lru.move_to_end(key)
+
+
+def _forget_prep(pid: int) -> None:
+    """A prepared scan was collected: its buffers went with it."""
+    with _buf_lock:
+        for k in [k for k in _buf_lru if k[0] == pid]:
+            _buf_total[0] -= _buf_lru.pop(k)[1]
 
 
 class _Bufs:

@@ -66,7 +66,7 @@ def context_token(sess) -> int:
     """Everything per-session that changes how a statement plans (the plan cache key minus the
     statement text and the shared catalog state)."""
     cat = sess.catalog
-    key = (cat.current_db, id(cat.temp) if cat.temp else 0, json.dumps(sess.conf.items(), sort_keys=True))
+    key = (cat.current_db, id(cat.temp) if cat.temp else 0, sess.conf.cache_key())
     return hash(key) & 0x7FFFFFFFFFFFFFFF
 
 
@@ -96,17 +96,26 @@ def encode_columns(types: List[str], df: pd.DataFrame) -> List[Tuple[int, bytes,
                     vals = num.fillna(0).to_numpy().astype(dt)
             out.append((kind, np.ascontiguousarray(vals, dtype=dt).tobytes(), b"", nulls))
             continue
+        vals = s.tolist()
+        offs = np.zeros(len(vals) + 1, dtype=np.int64)
+        if vals and not isna.any() and all(type(v) is str for v in vals):
+            # plain strings (the common case): C-level join / len; byte lengths equal character
+            # lengths when the text is ASCII (checked on the joined bytes)
+            text = "".join(vals)
+            blob = text.encode()
+            if len(blob) == len(text):
+                np.cumsum(np.fromiter(map(len, vals), dtype=np.int64, count=len(vals)), out=offs[1:])
+                out.append((6, blob, offs.tobytes(), nulls))
+                continue
         strs = []
-        for v, n in zip(s.tolist(), isna):
+        for v, n in zip(vals, isna):
             if n:
                 strs.append(b"")
             elif isinstance(v, pd.Timestamp):
                 strs.append((v.strftime("%Y-%m-%d") if base == "date" else str(v)).encode())
             else:
                 strs.append(str(v).encode())
-        lens = np.fromiter((len(x) for x in strs), dtype=np.int64, count=len(strs))
-        offs = np.zeros(len(strs) + 1, dtype=np.int64)
-        np.cumsum(lens, out=offs[1:])
+        np.cumsum(np.fromiter(map(len, strs), dtype=np.int64, count=len(strs)), out=offs[1:])
         out.append((6, b"".join(strs), offs.tobytes(), nulls))
     return out
 

@@ -229,3 +229,39 @@ def test_device_topk_prune_matches_full_sort(ds_small, direction, metric):
     sign = -1 if direction == "descending" else 1
     rows.sort(key=lambda r: (sign * r[m], r[0]))
     assert got.rows() == rows[:25]
+
+
+def test_scan_buffer_budget_releases_least_recently_used(monkeypatch):
+    """Cached plans keep their programs, but per-slot device buffers beyond the budget are released
+    LRU-first (engine/device_exec.py); a released scan re-allocates on its next run."""
+    import threading
+
+    import torch
+
+    from spark_druid_olap_amd.engine import device_exec as DE
+
+    class Prep:
+        def __init__(self):
+            self._slots, self._slot_lock = {}, threading.Lock()
+
+    def bufs(n):
+        b = DE._Bufs()
+        b.acc, b.keys, b.overflow, b.desc = torch.zeros(n, dtype=torch.int64), torch.zeros(1), torch.zeros(1), \
+            torch.zeros(1)
+        b.touch, b.init_row, b.hll, b.part = torch.zeros(1), torch.zeros(1), [], None
+        return b
+
+    monkeypatch.setattr(DE, "BUF_BUDGET", 28_000)
+    preps = [Prep() for _ in range(4)]
+    for p in preps:
+        p._slots[0] = bufs(1000)
+        DE._buffers_acquired(p, 0, p._slots[0])
+    # ~8 KB each against a 24 KB budget: the oldest went
+    assert not preps[0]._slots and all(p._slots for p in preps[1:])
+    DE._buffers_used(preps[1], 0)          # touched: now the most recent
+    preps[0]._slots[0] = bufs(1000)
+    DE._buffers_acquired(preps[0], 0, preps[0]._slots[0])
+    assert preps[1]._slots and not preps[2]._slots
+    for p in preps:
+        DE._forget_prep(id(p))
+    assert DE._buf_total[0] >= 0

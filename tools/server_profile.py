@@ -67,7 +67,10 @@ def main():
     srv._execute = exec_
     GW.encode_columns = enc
     srv.start()
-    qs = [" ".join(q.split()) for _, q in tpch.BENCH_QUERIES]
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import concurrency_bench as CB
+
+    qs = [q for _, q in CB.queries()]  # the concurrency benchmark's texts (TPC-H Q3 with its LIMIT 10)
     with connect(port=srv.port) as c:
         for q in qs * 3:
             c.cursor().execute(q).fetchall()
