@@ -191,6 +191,9 @@ class PreparedScan:
                 # the interpreter kernel only knows per-wave copies: accumulate in HBM instead
                 self.mode, self.shared, self.lds = D.M_DENSE_GLOBAL, False, 0
                 self.jit = _jit_for(prog, self.mode, False, self.m)
+        # stored (rolled-up) HLL sketches: the JIT kernel unions them in the scan (A_HLL_STORED);
+        # the interpreter leaves them to the executor (engine/executor.py _merge_stored_hll)
+        self.stored_fused = bool(prog.stored_hll) and self.jit is not None and self.mode != D.M_PART
         self._slot_lock = threading.Lock()
         self._slots = {}
         weakref.finalize(self, _forget_prep, id(self))
@@ -233,7 +236,8 @@ class PreparedScan:
         b.keys = torch.empty(rows if self.mode == D.M_HASH else 1, dtype=torch.int64, device=dev)
         # byte registers (sdo_device.h hll_update8 / hll_merge_word8): the partials, the wire and the
         # estimator all read u8
-        b.hll = [torch.empty(rows * self.m, dtype=torch.uint8, device=dev) for _ in range(prog.nhll)]
+        nblocks = prog.nhll_total if self.stored_fused else prog.nhll
+        b.hll = [torch.empty(rows * self.m, dtype=torch.uint8, device=dev) for _ in range(nblocks)]
         b.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
         b.touch = torch.zeros(((rows + 7) // 8 * 8) if self.touch else 8, dtype=torch.uint8, device=dev)
         b.clean = False
@@ -466,7 +470,8 @@ class PreparedScan:
         prog = self.prog
         acc = torch.empty((0, prog.nslots), dtype=torch.int64, device=self.dev)
         return Partials("sparse", acc, torch.zeros(0, dtype=torch.int64, device=self.dev),
-                        [torch.zeros((0, self.m), dtype=torch.uint8, device=self.dev) for _ in range(prog.nhll)])
+                        [torch.zeros((0, self.m), dtype=torch.uint8, device=self.dev)
+                         for _ in range(prog.nhll_total if self.stored_fused else prog.nhll)])
 
 
 # ------------------------------------------------------------------------------------------------

@@ -210,7 +210,7 @@ class PreparedQuery:
             from ..ops.reference import run_reference
 
             part = run_reference(prog)
-        if prog.stored_hll:
+        if prog.stored_hll and not getattr(prep, "stored_fused", False):
             part = self._merge_stored_hll(prog, part)
         return part
 

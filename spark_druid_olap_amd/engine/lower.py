@@ -1130,6 +1130,10 @@ class Lowerer:
                 raise LoweringError(f"hyperUnique over a {sk.kind} sketch metric {a.fieldName!r}")
             prog.stored_hll.append((a.name, a.fieldName, filt))
             prog.aggs.append(AggOut(a.name, "hll", hll_index=-len(prog.stored_hll), out_type="double", combine="hll"))
+            # the JIT scan unions each selected row's stored pairs in place (A_HLL_STORED); without
+            # the JIT the executor does it after the scan (engine/executor.py _merge_stored_hll)
+            d = aop(D.A_HLL_STORED)
+            d["stored"] = len(prog.stored_hll) - 1
             return
         if isinstance(a, (S.CardinalityAggregationSpec, S.HyperUniqueAggregationSpec)):
             fields = a.fieldNames if isinstance(a, S.CardinalityAggregationSpec) else [a.fieldName]
@@ -1861,6 +1865,11 @@ def pack(prog: ScanProgram, mode: int, dedup: int, hll_lds: int, lds_bytes: int,
             o["hll_regs"] = hll_ptrs[a["hll"]]
             o["hll_lds_off"] = hll_lds_offs[a["hll"]] if hll_lds_offs else 0
             o["salt"] = a.get("salt", 0)
+        elif a["kind"] == D.A_HLL_STORED and len(hll_ptrs) > prog.nhll + a["stored"]:
+            # (registers exist only when the JIT fuses the union: PreparedScan allocates them)
+            sk = ds.metrics[prog.stored_hll[a["stored"]][1]].sketch
+            o["hll_regs"] = hll_ptrs[prog.nhll + a["stored"]]
+            o["sk_off"], o["sk_val"] = sk.offsets.data_ptr(), sk.values.data_ptr()
     r["neops"] = len(prog.eops)
     for i, (op, col, c) in enumerate(prog.eops):
         e = r["eops"][i]

@@ -98,7 +98,8 @@ struct KOp {
 // ---- aggregators ----
 enum AKind : int32_t {
   A_COUNT = 0, A_SUM_I = 1, A_SUM_F = 2, A_MIN_I = 3, A_MAX_I = 4, A_MIN_F = 5, A_MAX_F = 6, A_HLL = 7,
-  A_SUM_X = 8  // exact decimal expression sum: llrint(expr) (expr pre-scaled by 10^scale) into S_SUM_I
+  A_SUM_X = 8,  // exact decimal expression sum: llrint(expr) (expr pre-scaled by 10^scale) into S_SUM_I
+  A_HLL_STORED = 9  // union of the row's stored (rolled-up) HLL sketch into the group's registers (JIT only)
 };
 // accumulator slot update ops
 enum SlotOp : int32_t { S_SUM_I = 0, S_SUM_F = 1, S_MIN_I = 2, S_MAX_I = 3 };
@@ -112,8 +113,10 @@ struct AOp {
   int32_t filt_len;
   int32_t slot;       // accumulator slot (non-HLL)
   int32_t hll_lds_off;// byte offset of this HLL's registers in LDS (when desc.hll_lds)
-  uint64_t hll_regs;  // global u32 registers [groups][1<<hll_p]
+  uint64_t hll_regs;  // global byte registers [groups][1<<hll_p]
   int64_t salt;
+  uint64_t sk_off;    // A_HLL_STORED: int64 [rows + 1] CSR offsets of the rows' stored sketches
+  uint64_t sk_val;    //               int32 packed (bucket << 8 | rho) pairs
 };
 
 enum EOpCode : int32_t {

@@ -71,7 +71,7 @@ def pipe_eligible(prog, mode: int, U: int) -> bool:
     """Double-buffer the payload DMA (see ``_Gen._pipelined_words``)."""
     if mode != D.M_DENSE_LDS or prog.filter_len and not prog.final_pre or not prog.pcols:
         return False
-    if any(a.get("filt_len") or a.get("filter") is not None for a in prog.aops):
+    if any(a.get("filt_len") or a.get("filter") is not None or a["kind"] == D.A_HLL_STORED for a in prog.aops):
         return False
     if getattr(prog, "packed", None):
         return False
@@ -113,7 +113,7 @@ def part_fields(prog, cols=None) -> List[Tuple[int, int]]:
     out = []
     for a in prog.aops:
         kind = a["kind"]
-        if kind == D.A_HLL:
+        if kind in (D.A_HLL, D.A_HLL_STORED):
             continue
         if kind == D.A_COUNT:
             out.append((a["slot"], 1 if a.get("filt_len") else 0))
@@ -131,7 +131,8 @@ def part_eligible(prog) -> bool:
     """The partitioned group-by handles every slot operator; it needs u32 keys and no HLL sketch."""
     slots = getattr(prog, "slots", None)
     n = len(slots) if slots is not None else prog.nslots
-    return n > 0 and not prog.nhll and 0 < prog.G < (1 << 32) and not prog.empty
+    return n > 0 and not prog.nhll and not getattr(prog, "stored_hll", None) and 0 < prog.G < (1 << 32) \
+        and not prog.empty
 
 
 REG_BUDGET = int(os.environ.get("SDO_JIT_REG_BUDGET", "96"))  # VGPRs for register accumulators
@@ -487,7 +488,7 @@ class _Gen:
         w = 1
         fi = 0
         for ai, a in enumerate(p.aops):
-            if a["kind"] == D.A_HLL:
+            if a["kind"] in (D.A_HLL, D.A_HLL_STORED):
                 continue
             slot, width = fields[fi]
             fi += 1
@@ -540,6 +541,10 @@ class _Gen:
                     L.append(f"  unsigned char* hll{ai} = lds + {lay.hll_off + a['hll'] * G * self.m};")
                 else:
                     L.append(f"  unsigned char* hll{ai} = (unsigned char*)d->aops[{ai}].hll_regs;")
+            elif a["kind"] == D.A_HLL_STORED:
+                L.append(f"  unsigned char* hll{ai} = (unsigned char*)d->aops[{ai}].hll_regs;")
+                L.append(f"  const int64_t* sko{ai} = (const int64_t*)d->aops[{ai}].sk_off;")
+                L.append(f"  const int32_t* skv{ai} = (const int32_t*)d->aops[{ai}].sk_val;")
         stage = []
         body = stage
         # ---------------- per-word processing
@@ -599,6 +604,8 @@ class _Gen:
             kind = a["kind"]
             if kind == D.A_HLL:
                 val = self.ival(a["col"])
+            elif kind == D.A_HLL_STORED:
+                val = "((cw0 + wl[u]) * 64 + lane)"  # the row: its stored sketch is a CSR run
             elif kind == D.A_COUNT:
                 val = "1LL"
             elif kind == D.A_SUM_X:
@@ -636,6 +643,9 @@ class _Gen:
             val = f"v{ai}_[u]"
             if kind == D.A_HLL:
                 body.append(f"        if ({cond}) hll_update8(hll{ai}, slot, {p.hll_p}, {val}, {_lit(a.get('salt', 0))});")
+                continue
+            if kind == D.A_HLL_STORED:
+                body.append(f"        if ({cond}) hll_merge_csr(hll{ai}, slot, {p.hll_p}, sko{ai}, skv{ai}, {val});")
                 continue
             s = a["slot"]
             op = p.slots[s][0]

@@ -21,6 +21,7 @@ a CPU-only checkout) and is the reference the native one is tested against (test
 """
 from __future__ import annotations
 
+import functools
 import importlib
 import json
 import logging
@@ -75,27 +76,45 @@ _KIND = {"boolean": (0, np.uint8), "tinyint": (1, np.int8), "smallint": (2, np.i
          "bigint": (4, np.int64), "double": (5, np.float64), "float": (5, np.float64), "decimal": (5, np.float64)}
 
 
-def encode_columns(types: List[str], df: pd.DataFrame) -> List[Tuple[int, bytes, bytes, bytes]]:
+def result_columns(df) -> List[pd.Series]:
+    """The result's columns as Series: a pandas frame, or the SQL executor's Batch (no DataFrame is
+    built on the serving path)."""
+    if isinstance(df, pd.DataFrame):
+        return [df.iloc[:, i] for i in range(df.shape[1])]
+    return [df.cols[r.rid] for r in df.refs]
+
+
+def encode_columns(types: List[str], df) -> List[Tuple[int, bytes, bytes, bytes]]:
     """Typed columns for the gateway: (kind, little-endian values | utf-8 blob, int64 offsets for
-    strings, one null byte per row).  Same value rendering as the Python server (_tcolumn)."""
+    strings, one null byte per row).  Same value rendering as the Python server (_tcolumn).
+    ``df``: a pandas frame, a list of Series, or the SQL executor's Batch."""
     out = []
-    for i, t in enumerate(types):
-        s = df.iloc[:, i]
+    cols = df if isinstance(df, list) else result_columns(df)
+    for t, s in zip(types, cols):
         base = t.split("(")[0]
-        isna = s.isna().to_numpy(dtype=bool) if len(s) else np.zeros(0, dtype=bool)
-        nulls = isna.astype(np.uint8).tobytes()
+        arr = s.to_numpy() if isinstance(s, pd.Series) else np.asarray(s)
+        if arr.dtype.kind in "iub":
+            isna = np.zeros(len(arr), dtype=bool)            # numpy ints / bools hold no nulls
+        elif arr.dtype.kind == "f":
+            isna = np.isnan(arr)
+        else:
+            isna = pd.isna(s).to_numpy(dtype=bool) if len(arr) else np.zeros(0, dtype=bool)
+        nulls = isna.view(np.uint8).tobytes()
         if base in _KIND:
             kind, dt = _KIND[base]
             if base == "boolean":
-                vals = np.array([bool(v) if not n else False for v, n in zip(s.tolist(), isna)], dtype=np.uint8)
+                vals = np.array([bool(v) if not n else False for v, n in zip(arr.tolist(), isna)], dtype=np.uint8)
+            elif arr.dtype.kind in "iufb":
+                vals = np.where(isna, 0, arr) if isna.any() else arr
             else:
-                num = pd.to_numeric(s, errors="coerce")
+                num = pd.to_numeric(pd.Series(arr), errors="coerce")
                 if kind == 5:
                     vals = num.to_numpy(dtype=np.float64, na_value=0.0)
                 else:
                     vals = num.fillna(0).to_numpy().astype(dt)
             out.append((kind, np.ascontiguousarray(vals, dtype=dt).tobytes(), b"", nulls))
             continue
+        s = pd.Series(arr) if not isinstance(s, pd.Series) else s
         vals = s.tolist()
         offs = np.zeros(len(vals) + 1, dtype=np.int64)
         if vals and not isna.any() and all(type(v) is str for v in vals):
@@ -122,6 +141,11 @@ def encode_columns(types: List[str], df: pd.DataFrame) -> List[Tuple[int, bytes,
 
 def encode_schema(names: List[str], types: List[str]) -> bytes:
     """A complete TTableSchema struct (the gateway splices it into GetResultSetMetadata)."""
+    return _encode_schema(tuple(names), tuple(types))
+
+
+@functools.lru_cache(maxsize=4096)
+def _encode_schema(names: Tuple[str, ...], types: Tuple[str, ...]) -> bytes:
     cols = []
     for i, (n, t) in enumerate(zip(names, types)):
         tid = T.TYPE_IDS.get(t.split("(")[0], T.TYPE_IDS["string"])
@@ -234,11 +258,11 @@ class NativeHiveServer(HiveThriftServer):
             bid, sid, stmt = b
             t0 = time.perf_counter()
             try:
-                names, types, pdf = self._execute(bid, sid, stmt)
+                names, types, res = self._execute(bid, sid, stmt)
                 self._metrics.record("gateway", (time.perf_counter() - t0) * 1e3, True)
                 schema = encode_schema(names, types)
-                cols = encode_columns(types, pdf)
-                gw.finish_batch(bid, schema, cols, len(pdf), None)
+                cols = encode_columns(types, res)
+                gw.finish_batch(bid, schema, cols, res.n if hasattr(res, "n") else len(res), None)
             except Exception as e:  # noqa: BLE001  (every attached operation reports it)
                 self._metrics.record("gateway", (time.perf_counter() - t0) * 1e3, False)
                 log.debug("batch %d failed: %s", bid, e)
@@ -258,11 +282,11 @@ class NativeHiveServer(HiveThriftServer):
         sess = ent["session"]
         df = sess.sql(stmt)
         if df.plan is None:  # a command that looked like a query: already executed
-            pdf = df.to_pandas()
+            res = df.to_pandas()
         else:
             with sess.engine.coalescer().scheduler.lease():
-                pdf = df.to_pandas(token=token)
-        return list(df.columns), [t for _, t in df.schema], pdf
+                res = df.run(token=token)  # the executor's columns, encoded without a DataFrame
+        return list(df.columns), [t for _, t in df.schema], res
 
 
 def make_server(session, host: str = "127.0.0.1", port: int = 10000, world=None, native: Optional[bool] = None):

@@ -137,3 +137,36 @@ def test_hll_register_clamp_and_bytewise_max_formulas():
         y = sum(c << (8 * i) for i, c in enumerate(cs))
         assert clamp127(x) == sum(min(b, 127) << (8 * i) for i, b in enumerate(bs))
         assert max4(x, y) == sum(max(b, c) << (8 * i) for i, (b, c) in enumerate(zip(bs, cs)))
+
+
+def test_jit_stored_hll_union_compiles(tmp_path, monkeypatch):
+    """A hyperUnique over a rolled-up sketch metric becomes an A_HLL_STORED aggregator: the JIT scan
+    unions each selected row's CSR run of stored pairs into the group's registers."""
+    import numpy as np
+    import pandas as pd
+
+    from spark_druid_olap_amd.engine.lower import Lowerer
+    from spark_druid_olap_amd.ops import desc as D
+    from spark_druid_olap_amd.ops import jit
+    from spark_druid_olap_amd.query import spec as S
+    from spark_druid_olap_amd.segment.ingest import ingest
+
+    monkeypatch.setenv("SDO_JIT_CACHE", str(tmp_path))
+    rng = np.random.default_rng(1)
+    n = 500
+    df = pd.DataFrame({"ts": pd.date_range("2016-01-01", periods=n, freq="h").strftime("%Y-%m-%dT%H:%M:%S"),
+                       "country": rng.choice(["US", "DE"], n), "user": [f"u{i % 97}" for i in range(n)]})
+    spec = {"type": "index", "spec": {"dataSchema": {
+        "dataSource": "ev", "parser": {"type": "string", "parseSpec": {
+            "format": "tsv", "timestampSpec": {"column": "ts", "format": "iso"}, "columns": ["ts", "country", "user"],
+            "dimensionsSpec": {"dimensions": ["country"]}}},
+        "metricsSpec": [{"type": "count", "name": "count"},
+                        {"type": "hyperUnique", "name": "uu", "fieldName": "user"}],
+        "granularitySpec": {"type": "uniform", "segmentGranularity": "MONTH", "queryGranularity": "day",
+                            "rollup": True, "intervals": ["2016-01-01/2016-12-31"]}}}}
+    ds = ingest(spec, data=df)
+    prog = Lowerer(ds).lower_aggregate(["2016-01-01/2016-12-31"], None, [S.DefaultDimensionSpec("country")], None,
+                                       [S.HyperUniqueAggregationSpec("u", "uu")])
+    assert prog.stored_hll and any(a["kind"] == D.A_HLL_STORED for a in prog.aops)
+    js = jit.JitScan(prog, D.M_DENSE_GLOBAL, 4, False, 1 << prog.hll_p, True, load=False)
+    assert "hll_merge_csr(hll" in js.src and "sko" in js.src

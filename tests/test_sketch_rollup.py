@@ -164,3 +164,33 @@ def test_gpu_ingest_and_stored_merge_match_cpu(data_dir):
     keys = list(zip(materialize(rg.data["country"]).tolist(), materialize(rg.data["platform"]).tolist()))
     got = {k: (rg.data["u"][i], rg.data["t"][i]) for i, k in enumerate(keys)}
     assert got == rc
+
+
+@pytest.mark.gpu
+def test_gpu_stored_hll_union_fused_in_the_scan_kernel(pair):
+    """K12 fused: the JIT scan unions the selected rows' stored sketches in place (A_HLL_STORED) --
+    no post-scan row re-derivation -- and equals query-time HLL over the raw index, also for a
+    filtered hyperUnique."""
+    from spark_druid_olap_amd.segment.datasource import DataSource  # noqa: F401
+
+    rolled, raw = pair
+    gr = rolled.to("cuda")
+    q = _q([S.HyperUniqueAggregationSpec("u", "uniq_users"),
+            S.FilteredAggregationSpec(S.SelectorFilterSpec("platform", "ios"),
+                                      S.HyperUniqueAggregationSpec("u_ios", "uniq_users"), "u_ios")],
+           ("country",))
+    pq = Engine(use_native=True).prepare(q.copy(), gr)
+    preps = [p for _, _, p in pq.scans]
+    assert preps and all(getattr(p, "stored_fused", False) for p in preps), "stored sketches not fused"
+    got, want = _run_native(gr, q.copy()), _run(raw, q.copy())
+    assert got.keys() == want.keys()
+    for k in want:  # same registers; the GPU (MFMA) and host estimators differ in the last ulp
+        assert got[k] == pytest.approx(want[k], rel=1e-12)
+
+
+def _run_native(ds, q):
+    r = Engine(use_native=True).execute(q, ds)
+    keys = [tuple(materialize(r.data[d]).tolist()[i] for d in ("country", "platform") if d in r.data)
+            for i in range(r.num_rows)]
+    return {k: tuple(np.asarray(r.data[c])[i] for c in r.columns if c not in ("country", "platform"))
+            for i, k in enumerate(keys)}
