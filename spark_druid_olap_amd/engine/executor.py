@@ -14,7 +14,7 @@ import math
 import os
 import time
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Optional, Sequence
+from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -108,6 +108,7 @@ class PreparedQuery:
         self.segments_per_query = segments_per_query
         self._nbatches: Optional[int] = None   # batch count agreed across ranks (pipelined merge)
         self._pipeline_ok: Optional[bool] = None
+        self._slices = None   # per-batch dense-key slices (time-leading keys), agreed across ranks
         self._having_fused: Optional[bool] = None  # HAVING handed to a partitioned scan (decided once)
         self.window: Optional["ShardWindow"] = None
         qt = qs.queryType
@@ -382,6 +383,9 @@ class PreparedQuery:
             self._nbatches = int(self.world.max_float(float(len(self.scans))))
         if self._nbatches <= 1 or self._pipeline_ok is False:
             return None
+        if self._slices is None:
+            self._slices = self._batch_key_slices(prog)
+        slices = self._slices
         # one merge in flight: merge j runs while batch j+1 scans, then merge j completes (RCCL:
         # the compute stream waits for it -- no host sync until the final status check)
         done, inflight, err = [], None, None
@@ -403,6 +407,11 @@ class PreparedQuery:
                     return None
             if inflight is not None:
                 done.append(inflight.result())
+            if slices is not None:
+                # time-leading key: this batch's groups live in one slice of the table, so only
+                # that slice crosses the wire (the agreed union over ranks)
+                lo, hi = slices[j]
+                part = Partials("dense", part.acc[lo:hi], None, [h[lo:hi] for h in part.hll])
             inflight = start_dense_merge(self.world, prog, part, STATUS_FAILED if err else STATUS_OK)
         t1 = time.perf_counter()
         with T.span("sdo.merge"):
@@ -410,8 +419,65 @@ class PreparedQuery:
             sts = torch.stack([d[1] for d in done]).amax(dim=0).tolist()
             if err is not None or any(sts):
                 raise_if_failed(sts, self.world.rank, err)
-            part = combine_local(prog, [d[0] for d in done])
+            if slices is None:
+                part = combine_local(prog, [d[0] for d in done])
+            else:
+                part = self._combine_slices(prog, slices, [d[0] for d in done])
         return part, t1
+
+    def _batch_key_slices(self, prog) -> Optional[List[Tuple[int, int]]]:
+        """Dense-table row slice of every segment batch when the leading (most significant) group
+        key is a granularity time bucket: a batch's rows span a time range, so its groups occupy
+        [bucket(t_min) * stride, (bucket(t_max) + 1) * stride) -- the Druid historical's interval
+        partitioning.  Agreed across ranks (min / max over the batch's slices) so every rank sends
+        the same collective; None when the layout has no such key."""
+        from ..ops.reference import _time_field
+
+        G = prog.G
+        lead = [kc for kc in prog.keys if kc.stride * max(1, kc.card) == G]
+        if not lead or not getattr(lead[0], "is_timestamp", False) or len(self.scans) < 1:
+            return None
+        kc = lead[0]
+        ds = self.ds
+        t = ds.time
+        out = torch.zeros((self._nbatches, 2), dtype=torch.int64)
+        out[:, 0] = G
+        for j, (_, bprog, _) in enumerate(self.scans[: self._nbatches]):
+            lo_t, hi_t = None, None
+            for a, b in bprog.ranges:
+                if b <= a:
+                    continue
+                mn, mx = torch.aminmax(t[a:b])
+                lo_t = int(mn) if lo_t is None else min(lo_t, int(mn))
+                hi_t = int(mx) if hi_t is None else max(hi_t, int(mx))
+            if lo_t is None:
+                continue
+            v = torch.tensor([lo_t, hi_t], dtype=torch.int64) * ds.time_unit_ms
+            idx = (_time_field(v, kc) - kc.base).clamp(0, max(0, kc.card - 1))
+            out[j, 0] = int(idx[0]) * kc.stride
+            out[j, 1] = -(int(idx[1]) + 1) * kc.stride
+        if self.world.distributed:
+            out = self.world.all_reduce(out, "min")
+        sl = [(int(a), max(int(a), -int(b))) for a, b in out.tolist()]
+        return [(min(a, G), min(b, G)) for a, b in sl]
+
+    def _combine_slices(self, prog, slices, parts: List[Partials]) -> Partials:
+        """Assemble the full dense table from per-batch merged slices (slices may overlap at a
+        shared time bucket: overlapping rows combine with the slot operators)."""
+        from ..parallel.merge import _reduce_stacked
+
+        dev = self.ds.device
+        G = prog.G
+        acc = torch.tensor([init for _, init in prog.slots], dtype=torch.int64, device=dev).expand(G, -1).clone()
+        m = 1 << prog.hll_p
+        hll = [torch.zeros((G, m), dtype=torch.uint8, device=dev) for _ in parts[0].hll] if parts else []
+        for (lo, hi), p in zip(slices, parts):
+            if hi <= lo:
+                continue
+            acc[lo:hi] = _reduce_stacked(prog, torch.stack([acc[lo:hi], p.acc.to(dev)]))
+            for i, h in enumerate(p.hll):
+                hll[i][lo:hi] = torch.maximum(hll[i][lo:hi], h.to(dev).view(hi - lo, m))
+        return Partials("dense", acc, None, hll)
 
     def _fuse_having(self, prog: ScanProgram, prep, disjoint: bool) -> bool:
         """Hand a simple HAVING (comparisons of count / integer / double aggregates, AND-ed or OR-ed)

@@ -222,14 +222,25 @@ def historical_cost_ms(ds, spec, segments_per_query: int, info=None, world_size:
     (``engine/executor.py _run_pipelined``), then a local combine of the B merged states.  The
     executor merges every batch in the full dense layout, so each batch's merge moves the whole
     state: pipelining pays only when one merge is shorter than one batch's scan, and even then
-    the last merge and B launches remain -- on one MI355X, and for dense states on xGMI, the
-    broker plan is never more expensive, which is what this model says."""
+    the last merge and B launches remain -- except when the time bucket leads the group key: then
+    a batch's groups are one slice of the table, each batch merges only its slice, and the merge
+    of a large time-bucketed state hides behind the scans (historical wins across ranks)."""
     c = est or estimate(ds, spec, info, world_size)
     nseg = max(1, sum(1 for _ in ds.segments))
     batches = max(1, math.ceil(nseg / max(1, segments_per_query)))
     s_b = c.scan_ms / batches + LAUNCH_S * 1e3
-    m_b = c.merge_ms
-    combine = batches * c.output_rows * (len(spec.aggregation_specs) + 2) * 8 / HBM_BW * 1e3
+    g = getattr(spec, "granularity", None)
+    time_leading = g is not None and not getattr(g, "is_all", True) and spec.queryType in ("groupBy", "timeseries")
+    if time_leading and world_size > 1 and c.merge_ms > 0:
+        # the time bucket is the leading group key: a batch of segments covers a time range, so
+        # its groups are one slice of the table and only that slice crosses the wire
+        # (engine/executor.py _batch_key_slices) -- Druid's interval-partitioned historicals
+        lat = COLL_LAT_S * 1e3
+        m_b = lat + max(0.0, c.merge_ms - lat) / batches
+        combine = c.output_rows * (len(spec.aggregation_specs) + 2) * 8 / HBM_BW * 1e3
+    else:
+        m_b = c.merge_ms
+        combine = batches * c.output_rows * (len(spec.aggregation_specs) + 2) * 8 / HBM_BW * 1e3
     pipelined = s_b + (batches - 1) * max(s_b, m_b) + m_b
     return pipelined + combine
 

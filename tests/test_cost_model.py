@@ -154,3 +154,29 @@ def test_partition_geometry():
     assert L["shift1"] == L["shift"] + int(math.log2(L["p2"]))
     small = part_layout(_prog(100_000, ns=3))
     assert small["levels"] == 1 and small["p1"] * (1 << small["shift"]) >= 100_000
+
+
+def test_historical_wins_for_a_large_time_bucketed_state_across_ranks(monkeypatch):
+    """Across 8 ranks a big dense state whose leading key is the time bucket merges slice by slice
+    behind the segment-batch scans (engine/executor.py _batch_key_slices), so the pipelined
+    historical plan is cheaper than one scan + one whole-state merge; the same state without a
+    time-leading key (granularity all) keeps the broker plan."""
+    import types
+
+    from spark_druid_olap_amd.query import spec as S
+
+    est = cost.CostEstimate(rows_in_interval=int(600e6), selectivity=1.0, input_rows=600e6, output_rows=2.0e6,
+                            bytes_scanned=int(9.6e9), groupby_mode="dense-global", merge="ring-allreduce",
+                            scan_ms=12.0, merge_ms=9.0)
+    monkeypatch.setattr(cost, "estimate", lambda *a, **k: est)
+    ds = types.SimpleNamespace(segments=list(range(64)))
+    ts = S.TimeSeriesQuerySpec("tpch", ["1992-01-01/1999-01-01"], granularity=S.Granularity.parse("day"),
+                               aggregations=[S.FunctionAggregationSpec("longSum", "q", "l_quantity")])
+    ch = cost.choose_method_costed(ds, ts, world_size=8)
+    assert ch.segments_per_query is not None, ch.describe()
+    assert min(v for k, v in ch.costs.items() if k != "broker") < ch.costs["broker"]
+    flat = S.TimeSeriesQuerySpec("tpch", ["1992-01-01/1999-01-01"], granularity=S.Granularity.parse("all"),
+                                 aggregations=[S.FunctionAggregationSpec("longSum", "q", "l_quantity")])
+    assert cost.choose_method_costed(ds, flat, world_size=8).segments_per_query is None
+    # one GPU: nothing to overlap
+    assert cost.choose_method_costed(ds, ts, world_size=1).segments_per_query is None

@@ -17,6 +17,27 @@ import torch.multiprocessing as mp
 NAMES = ["TPCH Q1", "TPCH Q7", "Basic Aggregation", "TPCH Q3"]
 
 
+def _ts_month():
+    from spark_druid_olap_amd.query import spec as S
+
+    return S.TimeSeriesQuerySpec("tpch", ["1992-01-01/1999-01-01"], granularity=S.Granularity.parse("month"),
+                                 aggregations=[S.FunctionAggregationSpec("longSum", "q", "l_quantity"),
+                                               S.FunctionAggregationSpec("count", "n")])
+
+
+def _gb_week():
+    from spark_druid_olap_amd.query import spec as S
+
+    return S.GroupByQuerySpec("tpch", [S.DefaultDimensionSpec("l_returnflag")],
+                              granularity=S.Granularity.parse("week"), intervals=["1992-01-01/1999-01-01"],
+                              aggregations=[S.FunctionAggregationSpec("doubleSum", "s", "l_extendedprice")])
+
+
+# time-leading group keys: each batch merges only its slice of the table (historical interval
+# partitioning, engine/executor.py _batch_key_slices)
+TIME_LEADING = {"TS month": _ts_month, "GB week x flag": _gb_week}
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -70,14 +91,15 @@ def _work(rank, world, port, outdir, device="cpu"):
         if not oneshot:
             cost.ONESHOT_MAX_BYTES = 0  # force the bucketed ring all-reduces
         try:
-            for name in NAMES:
-                q = query_from_json(DRUID_JSON[name])
+            for name in NAMES + list(TIME_LEADING):
+                q = query_from_json(DRUID_JSON[name]) if name in NAMES else TIME_LEADING[name]()
                 X.PIPELINE_MERGE = True
                 p = eng.prepare(q, ds, segments_per_query=2)
                 a = p.run().sorted_rows()
                 X.PIPELINE_MERGE = False
                 b = eng.prepare(q, ds, segments_per_query=2).run().sorted_rows()
                 out[(name, oneshot)] = (a, b, p._nbatches, len(p.scans), p._pipeline_ok)
+                out[(name, oneshot, "slices")] = (p._slices, p.scans[0][1].G if p.scans else 0)
         finally:
             cost.ONESHOT_MAX_BYTES = saved
             X.PIPELINE_MERGE = True
@@ -147,15 +169,21 @@ def test_pipelined_merge_on_gpu_scans():
 
 
 def _check(outs, device):
-    for name in NAMES:
+    for name in TIME_LEADING:
+        for oneshot in (True, False):
+            sl = [o[(name, oneshot, "slices")] for o in outs]
+            assert len({repr(x) for x in sl}) == 1, sl  # every rank merges the same slices
+            slices, G = sl[0]
+            assert slices is not None and sum(b - a for a, b in slices) < len(slices) * G, slices
+    for name in NAMES + list(TIME_LEADING):
         for oneshot in (True, False):
             per_rank = [o[(name, oneshot)] for o in outs]
             nb = {x[2] for x in per_rank}
             assert len(nb) == 1, (name, nb)  # the agreed batch count
             for a, b, nbatches, nscans, ok in per_rank:
                 assert _close(a, b), (name, oneshot)
-                if name == "TPCH Q3" and device == "cpu":
-                    assert ok is False  # hash partials: one merge after the local combine
+                if name in ("TPCH Q3", "GB week x flag") and device == "cpu":
+                    assert ok is False  # hash partials (> SDO_REF_SPARSE_G groups): one merge after the combine
                 else:
                     assert ok is True and nbatches >= nscans
             assert _close(per_rank[0][0], per_rank[-1][0])
