@@ -499,12 +499,56 @@ def _shard_hash(cols: List[torch.Tensor], n: int, dev) -> torch.Tensor:
     return h
 
 
+def _global_dictionary(comm, local: Dictionary, local_ids: torch.Tensor) -> Tuple[Dictionary, torch.Tensor]:
+    """Union of every rank's dimension values, sorted like ``_DimBuilder.finish`` (UTF-8 byte order
+    == code-point order), and this rank's ids remapped into it."""
+    vals = [str(v) for v in local.values.tolist()]
+    allv = comm.all_gather_object((vals, bool(local.has_null)))
+    merged = sorted(set().union(*[set(v) for v, _ in allv]))
+    has_null = any(h for _, h in allv)
+    g = np.empty(len(merged), dtype=object)
+    g[:] = merged
+    off_g, off_l = (1 if has_null else 0), (1 if local.has_null else 0)
+    table = np.zeros(len(vals) + off_l, dtype=np.int64)
+    if vals:
+        table[off_l:] = np.searchsorted(g, np.asarray(vals, dtype=object)) + off_g
+    t = torch.from_numpy(table).to(local_ids.device)
+    return Dictionary(g, STRING, has_null), (t[local_ids] if local_ids.numel() else local_ids.to(torch.int64))
+
+
+def _shuffle_rows(comm, owner: torch.Tensor, cols: List[torch.Tensor]) -> List[torch.Tensor]:
+    """Send every row to its owner rank (one all-to-all of the packed columns); returns the rows
+    this rank owns, column by column, with each column's dtype (int64 / float64 bits)."""
+    n = owner.numel()
+    order = torch.argsort(owner, stable=True)
+    counts = torch.bincount(owner, minlength=comm.size)
+    kinds = [c.dtype for c in cols]
+    mat = torch.stack([c.view(torch.int64) if c.dtype == torch.float64 else c.to(torch.int64) for c in cols], 1) \
+        if cols else torch.zeros((n, 0), dtype=torch.int64, device=owner.device)
+    rows, _ = comm.all_to_all_varlen(mat[order].contiguous(), counts)
+    rows = rows.to(owner.device)
+    return [rows[:, i].contiguous().view(torch.float64) if k == torch.float64 else rows[:, i].contiguous()
+            for i, k in enumerate(kinds)]
+
+
 def ingest(spec, device="cpu", rank: int = 0, world: int = 1, data: Optional[pd.DataFrame] = None,
-           data_dir: Optional[str] = None, bitmap_max_card: int = 256, block_bytes: int = 256 << 20) -> DataSource:
-    """Build this rank's shard of the datasource described by ``spec`` (see the module doc)."""
+           data_dir: Optional[str] = None, bitmap_max_card: int = 256, block_bytes: int = 256 << 20,
+           comm=None) -> DataSource:
+    """Build this rank's shard of the datasource described by ``spec`` (see the module doc).
+
+    Across ranks (``comm``: the process group's World, default the initialised one) every rank
+    parses only its share of the input blocks (block i -> rank i mod N), the dimension
+    dictionaries are unified across ranks, and the raw rows travel to their hash-partition owner
+    in one all-to-all before rollup -- each rank parses and rolls up 1/N of the input instead of
+    all of it.  ``SDO_INGEST_SPLIT=0`` restores parse-everything-keep-my-partition."""
     if not isinstance(spec, IndexSpec):
         spec = IndexSpec.parse(spec, data_dir)
     dev = torch.device(device)
+    if comm is None and world > 1:
+        from ..parallel import world as W_
+
+        comm = W_._WORLD if W_._WORLD is not None and W_._WORLD.size == world and W_._WORLD.rank == rank else None
+    split = comm is not None and world > 1 and comm.distributed and os.environ.get("SDO_INGEST_SPLIT", "1") != "0"
     plans = {m["name"]: _metric_plan(m) for m in spec.metrics}
     dims = list(spec.dimensions)
     dim_b: Dict[str, _DimBuilder] = {}
@@ -514,7 +558,7 @@ def ingest(spec, device="cpu", rank: int = 0, world: int = 1, data: Optional[pd.
     from concurrent.futures import ThreadPoolExecutor
 
     pool = ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4))
-    for rb in _batches(spec, data, block_bytes):
+    for bi, rb in enumerate(_batches(spec, data, block_bytes)):
         names = rb.schema.names
         if seen_cols is None:
             seen_cols = set(names)
@@ -522,6 +566,8 @@ def ingest(spec, device="cpu", rank: int = 0, world: int = 1, data: Optional[pd.
                 raise IngestError(f"timestamp column {spec.ts_column!r} missing")
             dims = [d for d in dims if d in seen_cols]
             dim_b = {d: _DimBuilder(dev) for d in dims}
+        if split and bi % world != rank:
+            continue  # another rank parses this block
         n = rb.num_rows
         if n == 0:
             continue
@@ -562,7 +608,19 @@ def ingest(spec, device="cpu", rank: int = 0, world: int = 1, data: Optional[pd.
                                                                       torch.zeros(n, dtype=torch.float64, device=dev))
     if seen_cols is None:
         raise IngestError("index task input is empty")
-    cat = {k: (torch.cat(v) if v else torch.zeros(0, device=dev)) for k, v in parts.items()}
+    if split:  # a rank without blocks still needs every column (empty, with the right dtype)
+        for m in spec.metrics:
+            parts.setdefault("m:" + m["name"], [])
+        for sd in spec.spatial:
+            for i, _ in enumerate(sd["dims"]):
+                parts.setdefault(f"s:{sd['dimName']}.{i}", [])
+
+    def _empty(k):
+        if k == "__t" or k.startswith("m:") and plans[k[2:]][0] not in ("double",):
+            return torch.zeros(0, dtype=torch.int64, device=dev)
+        return torch.zeros(0, dtype=torch.float64, device=dev)
+
+    cat = {k: (torch.cat(v) if v else _empty(k)) for k, v in parts.items()}
     ms = cat.pop("__t")
     keep = ms != _NULL_MS
     if spec.intervals:
@@ -575,8 +633,24 @@ def ingest(spec, device="cpu", rank: int = 0, world: int = 1, data: Optional[pd.
     cols = {k: v[sel] for k, v in cat.items()}
     dicts, ids = {}, {}
     for d, (dic, full) in zip(dims, pool.map(lambda d: dim_b[d].finish(), dims)):
+        if split:
+            dic, full = _global_dictionary(comm, dic, full)
         dicts[d], ids[d] = dic, full[sel]
     pool.shutdown()
+    if split:
+        # raw rows to their partition's owner (the same hash the rolled-up rows are kept by), so
+        # rollup is local and complete
+        hk = [ids[d] for d in dims] or [ms]
+        owner = torch.remainder(_shard_hash(hk, int(ms.numel()), dev), world)
+        names_ = sorted(cols)
+        moved = _shuffle_rows(comm, owner, [ms] + [ids[d] for d in dims] + [cols[k] for k in names_])
+        ms, moved = moved[0], moved[1:]
+        for d in dims:
+            ids[d], moved = moved[0], moved[1:]
+        cols = dict(zip(names_, moved))
+        world_keep = 1
+    else:
+        world_keep = world
     spatial = {sd["dimName"]: [f"{sd['dimName']}.{i}" for i in range(len(sd["dims"]))] for sd in spec.spatial}
     n = int(ms.numel())
     # ---- rollup on the device: rows with equal (truncated time, every dimension, spatial point)
@@ -594,7 +668,7 @@ def ingest(spec, device="cpu", rank: int = 0, world: int = 1, data: Optional[pd.
         R = n
     # ---- this rank's hash partition of the (rolled-up) rows; dictionaries are global
     row_keep = None
-    if world > 1:
+    if world_keep > 1:
         hk = [ids[d][first] for d in dims] or [ms[first]]
         row_keep = torch.remainder(_shard_hash(hk, R, dev), world) == rank
     out_rows = torch.nonzero(row_keep).flatten() if row_keep is not None else torch.arange(R, device=dev)
@@ -652,8 +726,12 @@ def ingest(spec, device="cpu", rank: int = 0, world: int = 1, data: Optional[pd.
         ds.metrics[nm].sketch = skc
     ds.spatial = spatial
     ds.rollup = rollup
+    if split:  # each rank rolled up its own partition: the totals are sums over ranks
+        tot = comm.all_gather_object((int(R), int(n_total)))
+        R, n_total = sum(a for a, _ in tot), sum(b for _, b in tot)
     ds.global_num_rows = R
     ds.ingested_rows = n_total
+    ds.ingest_split = split  # this rank parsed only its share of the input
     ds.build_indexes(bitmap_max_card=bitmap_max_card)
     return ds
 

@@ -194,3 +194,54 @@ def _run_native(ds, q):
             for i in range(r.num_rows)]
     return {k: tuple(np.asarray(r.data[c])[i] for c in r.columns if c not in ("country", "platform"))
             for i, k in enumerate(keys)}
+
+
+def _split_worker(rank, world, port, data_dir, outdir):
+    import os
+    import pickle
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), OMP_NUM_THREADS="1")
+    from spark_druid_olap_amd.parallel.world import init_world
+
+    w = init_world(backend="gloo")
+    ds = ingest(_spec(data_dir), rank=rank, world=world, block_bytes=1 << 14)  # many blocks: split by rank
+    out = {"rows": ds.num_rows, "global": ds.global_num_rows, "split": ds.ingest_split,
+           "dicts": {d: list(map(str, ds.dims[d].dictionary.values.tolist())) for d in ("platform", "country")},
+           "pairs": int(ds.metrics["uniq_users"].sketch.values.numel()),
+           "amount": float(ds.metrics["amount"].data[: ds.num_rows].sum()),
+           "count": int(ds.metrics["count"].data[: ds.num_rows].sum())}
+    with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
+        pickle.dump(out, f)
+    w.barrier()
+
+
+def test_split_ingest_across_ranks_equals_single_ingest(data_dir, tmp_path):
+    """Each rank parses only its blocks, dictionaries are unified and raw rows shuffled to their
+    partition owner before rollup: the union of the shards equals one whole ingest (gloo, 3 ranks)."""
+    import pickle
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    world = 3
+    ctx = mp.start_processes(_split_worker, args=(world, port, str(data_dir), str(tmp_path)), nprocs=world,
+                             join=False, start_method="spawn")
+    for p in ctx.processes:
+        p.join(240)
+    assert all(p.exitcode == 0 for p in ctx.processes)
+    outs = [pickle.load(open(tmp_path / f"r{r}.pkl", "rb")) for r in range(world)]
+    whole = ingest(_spec(data_dir))
+    assert all(o["split"] for o in outs)
+    assert sum(o["rows"] for o in outs) == whole.num_rows
+    assert all(o["global"] == whole.num_rows for o in outs)
+    for d in ("platform", "country"):
+        want = list(map(str, whole.dims[d].dictionary.values.tolist()))
+        assert all(o["dicts"][d] == want for o in outs)
+    assert sum(o["pairs"] for o in outs) == int(whole.metrics["uniq_users"].sketch.values.numel())
+    assert sum(o["count"] for o in outs) == int(whole.metrics["count"].data[: whole.num_rows].sum())
+    assert sum(o["amount"] for o in outs) == pytest.approx(float(whole.metrics["amount"].data[: whole.num_rows].sum()))
