@@ -53,6 +53,7 @@ class Operation:
         self.base = 0
         self.stream = None
         self.factory = None
+        self.close_hook = None  # releases an open multi-rank cursor (server/spmd.py streams)
         self.started = int(time.time() * 1000)
         self.completed = 0
         self.thread: Optional[threading.Thread] = None
@@ -304,7 +305,28 @@ class HiveThriftServer:
                 tmo = None
                 if op.token.deadline is not None:
                     tmo = max(0.001, op.token.deadline - time.monotonic())
-                df, pdf = self.spmd.execute(op.session_id, stmt, overlay, tmo)
+                sp = self.spmd
+                df, pdf = sp.execute(op.session_id, stmt, overlay, tmo, stream=True)
+                if isinstance(pdf, tuple) and pdf and pdf[0] == "stream":
+                    # Select-backed result over every rank: pages pulled on demand through the
+                    # broadcast stream (each rank advances its cursor on the same message)
+                    first = [pdf[1]]
+
+                    def pages(first=first, sid=op.session_id, stmt=stmt, overlay=dict(overlay), tmo=tmo):
+                        sid_ = first.pop() if first else sp.execute(sid, stmt, overlay, tmo, stream=True)[1][1]
+                        op.close_hook = lambda: sp.close_stream(sid_)
+                        while True:
+                            page = sp.stream_next(sid_)
+                            if page is None:
+                                op.close_hook = None
+                                return
+                            yield page
+
+                    op.set_stream(df.columns, [t for _, t in df.schema], pages)
+                    op.fill(1)  # the first page now: errors surface in ExecuteStatement
+                    op.state = T.OP_FINISHED if not op.cancelled.is_set() else T.OP_CANCELED
+                    op.completed = int(time.time() * 1000)
+                    return
             else:
                 sess = self.sessions[op.session_id]["session"]
                 for k, v in overlay.items():
@@ -356,7 +378,13 @@ class HiveThriftServer:
         return {"status": _ok()}
 
     def rpc_CloseOperation(self, req):
-        self.ops.pop(_oid(req), None)
+        op = self.ops.pop(_oid(req), None)
+        hook = getattr(op, "close_hook", None) if op is not None else None
+        if hook is not None:  # an unfinished cursor over every rank: release it everywhere
+            try:
+                hook()
+            except Exception:  # noqa: BLE001
+                log.debug("closing the statement's cursor failed", exc_info=True)
         return {"status": _ok()}
 
     def rpc_GetResultSetMetadata(self, req):

@@ -91,14 +91,41 @@ def _run_statement(df, msg):
         return df, df.to_pandas(token=_token(msg))
 
 
+# Open Select cursors of streamed statements on this rank (stream id -> page iterator).  Every
+# rank advances a cursor on the same broadcast message, so the page's collectives (the Select
+# page gather) run in lock step; rank 0 hands the page to the client.
+_STREAMS: Dict[int, Any] = {}
+
+
+def _streamable(df, s) -> bool:
+    return df.plan is not None and df._stream_source()[1] is not None and \
+        bool(s.conf.typed("spark.sparklinedata.druid.stream.results"))
+
+
 def _execute(sessions: Dict[bytes, Any], root, msg: Dict[str, Any]):
-    """Apply one message in the dispatch thread: lifecycle ops, commands and statements that do
-    not run on a slot.  Returns (DataFrame, pandas) for statements, None otherwise."""
-    if msg["op"] != "exec":
+    """Apply one message in the dispatch thread: lifecycle ops, commands, statements that do not
+    run on a slot and Select cursor steps.  Returns (DataFrame, pandas) for statements --
+    (DataFrame, ("stream", id)) for a streamed Select -- a page for a cursor step, else None."""
+    op = msg["op"]
+    if op == "stream_next":
+        it = _STREAMS.get(msg["stream_id"])
+        page = next(it, None) if it is not None else None
+        if page is None:
+            _STREAMS.pop(msg["stream_id"], None)
+        return page
+    if op == "stream_close":
+        _STREAMS.pop(msg["stream_id"], None)
+        return None
+    if op != "exec":
         _apply(sessions, root, msg)
         return None
     s = _session_for(sessions, root, msg)
     df = s.sql(msg["stmt"])  # (commands -- CREATE TABLE AS SELECT -- run here, on every rank)
+    if msg.get("stream_id") is not None and _streamable(df, s):
+        # a Select-backed result pages through the cursor instead of materialising (the
+        # reference's DruidSelectResultIterator); the first page runs on the first step
+        _STREAMS[msg["stream_id"]] = df.iter_batches(token=_token(msg))
+        return df, ("stream", msg["stream_id"])
     return _run_statement(df, msg)
 
 
@@ -211,6 +238,8 @@ class SpmdDispatcher:
             world.broadcast_object({"op": "slots", "k": k})  # peers create the same slot groups
         self.workers = SlotWorkers(session, world, k) if k > 0 else None
         self._pinned: Dict[bytes, int] = {}
+        self._sid_lock = threading.Lock()
+        self._stream_seq = 0
         self.stats = {"statements": 0, "executions": 0, "coalesced": 0, "heartbeats": 0, "on_slots": 0,
                       "inline": 0}
         self._thread = threading.Thread(target=self._loop, daemon=True, name="spmd-dispatch")
@@ -227,10 +256,23 @@ class SpmdDispatcher:
         return self.sessions.get(sid)
 
     def execute(self, sid: bytes, stmt: str, overlay: Optional[Dict[str, str]] = None,
-                timeout_s: Optional[float] = None) -> Tuple[Any, Any]:
-        """Run ``stmt`` for client session ``sid`` on every rank; returns (DataFrame, pandas)."""
-        return self._submit({"op": "exec", "sid": sid, "stmt": stmt, "overlay": dict(overlay or {}),
-                             "timeout_s": timeout_s})
+                timeout_s: Optional[float] = None, stream: bool = False) -> Tuple[Any, Any]:
+        """Run ``stmt`` for client session ``sid`` on every rank; returns (DataFrame, pandas).  With
+        ``stream`` a Select-backed statement returns (DataFrame, ("stream", id)) instead: pull its
+        pages with ``stream_next(id)``, release it with ``close_stream(id)``."""
+        msg = {"op": "exec", "sid": sid, "stmt": stmt, "overlay": dict(overlay or {}), "timeout_s": timeout_s}
+        if stream:
+            with self._sid_lock:
+                self._stream_seq += 1
+                msg["stream_id"] = self._stream_seq
+        return self._submit(msg)
+
+    def stream_next(self, stream_id: int):
+        """The next page (pandas) of a streamed statement on every rank; None at the end."""
+        return self._submit({"op": "stream_next", "stream_id": stream_id})
+
+    def close_stream(self, stream_id: int) -> None:
+        self._submit({"op": "stream_close", "stream_id": stream_id})
 
     def shutdown(self) -> None:
         if not self._stop.is_set():
@@ -258,7 +300,9 @@ class SpmdDispatcher:
             if self.workers is not None and m["op"] == "exec" and _is_query(m["stmt"]) and not m.get("overlay"):
                 try:
                     s = _session_for(self.sessions, self.root, {"sid": m["sid"]})
-                    if slot_eligible(s.sql(m["stmt"])):
+                    df = s.sql(m["stmt"])
+                    streamed = m.get("stream_id") is not None and _streamable(df, s)  # cursors run inline
+                    if slot_eligible(df) and not streamed:
                         slot = self._session_slot(m["sid"])
                 except Exception:  # noqa: BLE001  (the statement fails the same way inline)
                     slot = INLINE
@@ -354,7 +398,8 @@ class SpmdDispatcher:
         for it in batch:
             m = it.msg
             key = None
-            if self.coalesce and m["op"] == "exec" and not m.get("overlay") and _is_query(m["stmt"]):
+            if self.coalesce and m["op"] == "exec" and not m.get("overlay") and _is_query(m["stmt"]) and \
+                    m.get("stream_id") is None:  # (a cursor belongs to one client)
                 s = self.sessions.get(m["sid"])
                 if s is not None and not s.catalog.temp:
                     key = (m["stmt"].strip(), s.catalog.current_db, tuple(sorted(s.conf.items().items())))

@@ -120,3 +120,43 @@ def test_slots_run_statements_concurrently_and_match_serial():
         for r in runs:
             assert _norm(r) == _norm(out["serial"][q]), q
     assert sum(len(v) for v in out["conc"].values()) == 8 * len(statements())
+
+
+def test_dispatcher_streams_select_pages(ds_small, df_small):
+    """The dispatcher's cursor protocol (one rank here): a Select-backed statement returns a stream
+    id, pages come one ``stream_next`` at a time (page size 11), the concatenation equals the
+    materialised answer, and an aggregate statement still comes back whole."""
+    from spark_druid_olap_amd.engine.executor import Engine
+    from spark_druid_olap_amd.models import tpch
+    from spark_druid_olap_amd.parallel.world import World
+    from spark_druid_olap_amd.server import spmd
+    from spark_druid_olap_amd.session import Session
+
+    s = Session(engine=Engine(use_native=False))
+    s.register_datasource(ds_small)
+    s.register_table("orderLineItemPartSupplierBase", df_small, schema=tpch.FLAT_SCHEMA)
+    s.sql(tpch.druid_ddl(with_column_mapping=False,
+                         extra_options=', nonAggregateQueryHandling "push_project_and_filters"'))
+    d = spmd.SpmdDispatcher(s, World(0, 1, 0, "none"), slots=0)
+    try:
+        d.open_session(b"s1", {"spark.sparklinedata.druid.selectquery.pagesize": "11"}, None)
+        q = "select o_orderkey, l_quantity from orderLineItemPartSupplier where l_returnflag = 'R'"
+        df, res = d.execute(b"s1", q, stream=True)
+        assert isinstance(res, tuple) and res[0] == "stream"
+        pages = []
+        while True:
+            pg = d.stream_next(res[1])
+            if pg is None:
+                break
+            pages.append(pg)
+        assert len(pages) > 1 and max(len(p) for p in pages) <= 11
+        got = sorted(tuple(r) for p in pages for r in p.itertuples(index=False))
+        want = sorted(tuple(r) for r in d.execute(b"s1", q)[1].itertuples(index=False))
+        assert got == want and res[1] not in spmd._STREAMS
+        df2, res2 = d.execute(b"s1", "select count(*) from orderLineItemPartSupplier", stream=True)
+        assert not isinstance(res2, tuple)
+        df3, res3 = d.execute(b"s1", q, stream=True)
+        d.close_stream(res3[1])
+        assert res3[1] not in spmd._STREAMS
+    finally:
+        d.shutdown()

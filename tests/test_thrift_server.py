@@ -303,3 +303,56 @@ def test_two_rank_server_returns_merged_answer(tmp_path):
         except subprocess.TimeoutExpired:
             p.kill()
     assert p.returncode == 0, p.stderr.read().decode()[-3000:]
+
+
+def test_two_rank_python_server_streams_select_pages(tmp_path):
+    """A Select-backed statement on the multi-rank Python server pages through a cursor that every
+    rank advances on the same broadcast message (server/spmd.py streams): the client gets every
+    row of both shards, a page at a time (page size 7)."""
+    import os
+    import signal
+    import subprocess
+    import sys
+    import time as _t
+
+    import pandas as pd
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pf = tmp_path / "port"
+    init = tmp_path / "init.sql"
+    # a second table over the same index whose plain selects push down as Druid Select queries
+    init.write_text(tpch.druid_ddl(table="lineitemSelect", with_column_mapping=False,
+                                   star_schema='{"factTable" : "lineitemSelect", "relations" : []}',
+                                   extra_options=', nonAggregateQueryHandling "push_project_and_filters"'))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(OMP_NUM_THREADS="2", PYTHONPATH=root, SDO_NATIVE_GATEWAY="0")
+    p = subprocess.Popen([sys.executable, "-m", "spark_druid_olap_amd.server.hive_server", "--gpus", "2",
+                          "--tpch-sf", "0.002", "--port", "0", "--port-file", str(pf), "--ui-port", "-1",
+                          "--init-sql", str(init)],
+                         cwd=root, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+    try:
+        t0 = _t.time()
+        while not pf.exists():
+            assert p.poll() is None, p.stderr.read().decode()[-3000:]
+            assert _t.time() - t0 < 200, "server did not start"
+            _t.sleep(0.2)
+        port = int(pf.read_text())
+        full = pd.concat([tpch.to_pandas(tpch.generate_flat(0.002, "cpu", rank=r, world=2)) for r in range(2)])
+        want = sorted(zip(full[full.l_returnflag == "R"].o_orderkey, full[full.l_returnflag == "R"].l_quantity))
+        with connect(port=port) as c:
+            c.cursor().execute("set spark.sparklinedata.druid.selectquery.pagesize=7")
+            cur = c.cursor().execute("select o_orderkey, l_quantity from lineitemSelect where l_returnflag = 'R'")
+            got = sorted((int(a), int(b)) for a, b in cur.fetchall())
+            assert got == [(int(a), int(b)) for a, b in want]
+            # a cursor closed before its end releases the stream on every rank; the server goes on
+            cur = c.cursor().execute("select o_orderkey from lineitemSelect")
+            cur.close()
+            n = c.cursor().execute("select count(*) from orderLineItemPartSupplier").fetchall()[0][0]
+            assert n == len(full)
+    finally:
+        p.send_signal(signal.SIGTERM)
+        try:
+            p.wait(60)
+        except subprocess.TimeoutExpired:
+            p.kill()
+    assert p.returncode == 0, p.stderr.read().decode()[-3000:]
