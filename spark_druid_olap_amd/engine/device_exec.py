@@ -40,6 +40,22 @@ USE_REG = os.environ.get("SDO_JIT_REG", "0") != "0"     # register accumulators 
 USE_PIPE = os.environ.get("SDO_JIT_PIPE", "0") != "0"   # double-buffered payload DMA
 JIT_BLOCKS = int(os.environ.get("SDO_JIT_BLOCKS", "3"))  # target resident workgroups per CU
 JIT_STAGE = os.environ.get("SDO_JIT_STAGE", "auto")       # auto | reg (VGPR loads) | lds (LDS-DMA planes)
+# Literal specialization of repeated statements (ops/jit.py JitScan.specialized): a prepared scan's
+# first runs use the shape's shared kernel (query constants read from the descriptor: every
+# parameterization of a dashboard query shares one code object); from its SPECIALIZE_AFTER-th run
+# a kernel with the constants baked in is compiled -- in the background ("async": serving never
+# waits for hipRTC) or at once ("sync": a benchmark's warmup) -- and swapped in.
+SPECIALIZE = os.environ.get("SDO_JIT_SPECIALIZE", "async")  # off | async | sync
+SPECIALIZE_AFTER = int(os.environ.get("SDO_JIT_SPECIALIZE_AFTER", "2"))
+_spec_pool = []
+
+
+def _spec_executor():
+    if not _spec_pool:
+        from concurrent.futures import ThreadPoolExecutor
+
+        _spec_pool.append(ThreadPoolExecutor(max_workers=2, thread_name_prefix="sdo-jit-spec"))
+    return _spec_pool[0]
 
 
 def _attach_packed(prog) -> None:
@@ -155,6 +171,8 @@ class PreparedScan:
         else:
             self.cap = 0
         self.jit = None
+        self._runs = 0
+        self._spec_future = None
         self.part = None
         self.part_having = None
         self.part_cap = 1 << 16
@@ -296,8 +314,7 @@ class PreparedScan:
         P1, nsub = L["p1"], L["nsub"]
         k1 = max(1, min(nch, 2048))
         pb = {
-            "recs1": torch.empty(max(1, cap * L["rw"]), dtype=u32, device=dev),
-            "recs2": torch.empty(max(1, cap * L["rw"]), dtype=u32, device=dev),
+            "cap_words": max(1, cap * L["rw"]), "desc_recs": 0,
             "seg_lo": (torch.arange(nch, dtype=torch.int64) * D.CHUNK_ROWS).to(u32).to(dev),
             "pend": torch.empty(max(1, nch), dtype=u32, device=dev),
             "k1": k1, "nch": nch,
@@ -309,7 +326,7 @@ class PreparedScan:
             pb["counts2"] = torch.empty(nsub * L["k"], dtype=u32, device=dev)
             pb["totals2"] = torch.empty(nsub, dtype=u32, device=dev)
             pb["base2"] = torch.empty(nsub + 1, dtype=u32, device=dev)
-        d[0]["part_recs"] = pb["recs1"].data_ptr()
+        d[0]["part_recs"] = 0  # the slot's scratch, patched in at run time (_run_part)
         d[0]["part_counts"] = pb["pend"].data_ptr()
         d[0]["part_shift"] = L["shift1"]
         d[0]["part_n"] = P1
@@ -319,9 +336,19 @@ class PreparedScan:
         """producer (records into chunk regions) -> level-1 split (count, offsets, tile-sorted
         scatter) -> [level-2 split] -> LDS aggregation into the dense table (every row written: no
         reset), or, with a fused HAVING, straight to the surviving groups (sparse)."""
+        from .scheduler import current_slot
+
         L, nat, st = self.part, native.load(), native._stream(self.dev)
-        pb = b.part
+        pb = dict(b.part)
         prog = self.prog
+        slot = current_slot()
+        pb["recs1"] = _scratch(self.dev, slot, "recs1", pb["cap_words"])
+        pb["recs2"] = _scratch(self.dev, slot, "recs2", pb["cap_words"])
+        if b.part["desc_recs"] != pb["recs1"].data_ptr():
+            off = D.SCANDESC.fields["part_recs"][1]
+            ptr = torch.tensor([pb["recs1"].data_ptr()], dtype=torch.int64).view(torch.uint8)
+            b.desc[off:off + 8].copy_(ptr.to(self.dev))
+            b.part["desc_recs"] = pb["recs1"].data_ptr()
         nat.module_launch(self.jit.handle, b.desc.data_ptr(), int(self.grid), BLOCK, int(self.jit.lay.total), st)
         rw, P1, k1 = L["rw"], L["p1"], pb["k1"]
         # level 1: one input group = every chunk region, P1 buckets by the top key bits
@@ -348,9 +375,9 @@ class PreparedScan:
                          [int(init) for _, init in prog.slots], b.acc.data_ptr(), [], 1, 0, 0, 0, st)
             return None
         while True:
-            out = pb.get("hv_out")
+            out = b.part.get("hv_out")
             if out is None or out[0].shape[0] < self.part_cap:
-                out = pb["hv_out"] = (torch.empty((self.part_cap, prog.nslots), dtype=torch.int64, device=self.dev),
+                out = b.part["hv_out"] = (torch.empty((self.part_cap, prog.nslots), dtype=torch.int64, device=self.dev),
                                       torch.empty(self.part_cap, dtype=torch.int64, device=self.dev),
                                       torch.zeros(1, dtype=torch.int64, device=self.dev))
             acc, keys, cnt = out
@@ -400,10 +427,43 @@ class PreparedScan:
         if self.mode == D.M_HASH:
             b.keys.fill_(-1)
 
+    # ------------------------------------------------------------------ specialization
+    def _maybe_specialize(self) -> None:
+        self._runs += 1
+        fut = self._spec_future
+        if fut is not None and fut.done():
+            self._spec_future = None
+            try:
+                self._adopt(fut.result())
+            except Exception as e:  # noqa: BLE001  (keep the shared kernel)
+                import warnings
+
+                warnings.warn(f"literal specialization failed: {e}")
+        if self._runs != SPECIALIZE_AFTER or SPECIALIZE == "off" or self.jit is None or self.jit.literals:
+            return
+        if SPECIALIZE == "sync":
+            self._adopt(self.jit.specialized())
+        else:
+            self._spec_future = _spec_executor().submit(self.jit.specialized)
+
+    def _adopt(self, js) -> None:
+        """Swap in a kernel of the same layout (the launch arguments cached per slot name the
+        kernel handle)."""
+        with self._slot_lock:
+            self.jit = js
+            for b in self._slots.values():
+                for attr in ("run_args", "noreset_args"):
+                    a = getattr(b, attr)
+                    if a is not None:
+                        a = list(a)
+                        a[-6] = js.handle  # (jit, desc, grid, block, lds, unroll)
+                        setattr(b, attr, tuple(a))
+
     # ------------------------------------------------------------------ run
     def run(self) -> Partials:
         from .scheduler import current_slot
 
+        self._maybe_specialize()
         prog = self.prog
         b = self._bufs()
         if prog.empty:
@@ -481,7 +541,41 @@ class PreparedScan:
 # a released scan re-allocates on its next run (from the caching allocator's free blocks, usually:
 # parameterizations of one shape have the same buffer sizes).  Callers still holding partials keep
 # those tensors alive by reference, so a release never pulls memory from under a running query.
-BUF_BUDGET = int(os.environ.get("SDO_SCAN_BUF_BUDGET", str(24 << 30)))
+BUF_BUDGET = int(os.environ.get("SDO_SCAN_BUF_BUDGET", "0"))  # 0: 35% of the device's memory
+
+
+def _budget() -> int:
+    if BUF_BUDGET > 0:
+        return BUF_BUDGET
+    b = _budget_cache.get("b")
+    if b is None:
+        b = 24 << 30
+        try:
+            if torch.cuda.is_available():
+                b = max(b, int(0.35 * torch.cuda.get_device_properties(torch.cuda.current_device()).total_memory))
+        except Exception:  # noqa: BLE001
+            pass
+        _budget_cache["b"] = b
+    return b
+
+
+_budget_cache: dict = {}
+
+# Partition records (ops/csrc/partition.hip) are scratch of one execution: one pair of buffers per
+# (device, execution slot), grown to the largest need, shared by every prepared scan of the slot
+# (a slot runs one statement at a time) instead of held per cached plan.
+_SCRATCH: dict = {}
+_scratch_lock = threading.Lock()
+
+
+def _scratch(dev, slot, name: str, nelem: int) -> torch.Tensor:
+    k = (str(dev), slot, name)
+    with _scratch_lock:
+        t = _SCRATCH.get(k)
+        if t is None or t.numel() < nelem:
+            _SCRATCH[k] = None
+            t = _SCRATCH[k] = torch.empty(max(1, nelem), dtype=torch.int32, device=dev)
+    return t
 _buf_lru: "OrderedDict[tuple, tuple]" = OrderedDict()   # (id(prep), slot) -> (weakref(prep), bytes)
 _buf_total = [0]
 _buf_lock = threading.Lock()
@@ -509,7 +603,7 @@ def _buffers_acquired(prep, slot, b) -> None:
             _buf_total[0] -= old[1]
         _buf_lru[key] = (weakref.ref(prep), nb)
         _buf_total[0] += nb
-        while _buf_total[0] > BUF_BUDGET and len(_buf_lru) > 1:
+        while _buf_total[0] > _budget() and len(_buf_lru) > 1:
             k, (ref, n) = next(iter(_buf_lru.items()))
             if k == key:
                 break

@@ -63,6 +63,19 @@ def main():
                 if os.environ.get("SDO_JIT_COMPILE"):  # hipRTC for gfx950 (no GPU needed)
                     code = jit.compile_code(src, "sdo_jit_probe")
                     print(f"// compiled: {len(code)} bytes of gfx950 code object")
+                    if os.environ.get("SDO_JIT_REGS"):  # register budget of the kernel (code-object notes)
+                        import re
+                        import subprocess
+                        import tempfile
+
+                        with tempfile.NamedTemporaryFile(suffix=".co") as f:
+                            f.write(code)
+                            f.flush()
+                            notes = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", f.name],
+                                                   capture_output=True, text=True).stdout
+                        regs = {k: (re.findall(r"\." + k + r":\s+(\d+)", notes) or ["?"])[0]
+                                for k in ("sgpr_count", "vgpr_count", "sgpr_spill_count", "vgpr_spill_count")}
+                        print(f"@@ {name}: {regs}", file=sys.stderr)
 
 
 if __name__ == "__main__":
