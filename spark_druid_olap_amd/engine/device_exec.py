@@ -636,6 +636,66 @@ class _Bufs:
                  "noreset_args", "fetch", "part")
 
 
+class PreparedEmit:
+    """(group key, row id) of every row the program selects, written by the JIT scan -- the M_PART
+    producer with one row-id field, then one split pass that compacts the chunk regions in order.
+    Sketch aggregators that need the selected rows themselves (theta KMV) read these instead of a
+    torch re-scan of the shard (``_rows`` + ``eval_bexpr`` + ``compute_keys``)."""
+
+    def __init__(self, prog: ScanProgram):
+        import copy
+
+        from .lower import lds_layout
+
+        ep = copy.copy(prog)
+        ep.aops = [{"kind": D.A_ROWID, "col": -1, "expr": None, "filter": None, "slot": 0, "hll": -1}]
+        ep.slots = [(D.S_SUM_I, 0)]
+        ep.nhll, ep.stored_hll, ep.thetas, ep.packed = 0, [], [], {}
+        ep.presence_only = False
+        self.prog = ep
+        self.dev = prog.ds.device
+        from ..ops import jit as J
+
+        if prog.empty or not J.part_eligible(ep):
+            raise RuntimeError("emit: program not eligible")
+        self.jit = _jit_for(ep, D.M_PART, False, 1 << prog.hll_p)
+        if self.jit is None:
+            raise RuntimeError("emit: no JIT kernel")
+        cache_off, wave_bytes, _, total = lds_layout(ep, 0, UNROLL, BLOCK // 64)
+        d = pack(ep, D.M_PART, 0, 0, 0, 0, 0, 0, 0, 0, 0, [], [], unroll=UNROLL, cache_off=cache_off,
+                 wave_bytes=wave_bytes)
+        self.nch = int(d[0]["total_chunks"])
+        self.grid = _grid(self.dev, self.nch, self.jit.lay.total)
+        cap = self.nch * D.CHUNK_ROWS
+        if 2 * cap >= (1 << 32):
+            raise RuntimeError("emit: shard too large for u32 offsets")
+        u32 = torch.int32
+        self.recs1 = torch.empty(max(1, 2 * cap), dtype=u32, device=self.dev)
+        self.recs2 = torch.empty_like(self.recs1)
+        self.pend = torch.empty(max(1, self.nch), dtype=u32, device=self.dev)
+        self.seg_lo = (torch.arange(self.nch, dtype=torch.int64) * D.CHUNK_ROWS).to(u32).to(self.dev)
+        self.k = max(1, min(self.nch, 1024))
+        self.counts = torch.empty(self.k, dtype=u32, device=self.dev)
+        self.totals = torch.empty(1, dtype=u32, device=self.dev)
+        self.base = torch.empty(2, dtype=u32, device=self.dev)
+        d[0]["part_recs"] = self.recs1.data_ptr()
+        d[0]["part_counts"] = self.pend.data_ptr()
+        self.desc = torch.from_numpy(d.view(np.uint8).copy()).to(self.dev)
+
+    def run(self):
+        """(keys int64, rows int64) of the selected rows, in row order within each chunk."""
+        nat, st = native.load(), native._stream(self.dev)
+        nat.module_launch(self.jit.handle, self.desc.data_ptr(), int(self.grid), BLOCK, int(self.jit.lay.total), st)
+        a = (self.recs1.data_ptr(), 2, self.seg_lo.data_ptr(), self.pend.data_ptr(), 1, self.nch, self.k, 0, 1,
+             self.counts.data_ptr())
+        nat.part_split(*a, 0, 0, 0, st)
+        nat.part_scan(self.counts.data_ptr(), 1, self.k, self.totals.data_ptr(), self.base.data_ptr(), st)
+        nat.part_split(*a, self.base.data_ptr(), self.recs2.data_ptr(), 1, st)
+        n = int(self.base[1].item())
+        rec = self.recs2[: 2 * n].view(n, 2).to(torch.int64) & 0xFFFFFFFF
+        return rec[:, 0].contiguous(), rec[:, 1].contiguous()
+
+
 class PreparedMask:
     """Filter-only scan: writes one u64 mask word per 64 rows (select queries); the mask becomes
     row ids with the ``compact_rows`` kernel (ops/csrc/post_scan.hip).  Mask + descriptor are

@@ -631,10 +631,23 @@ class PreparedQuery:
 
         ds = self.ds
         dev = ds.device
-        rows = _rows(prog) if not prog.empty else torch.zeros(0, dtype=torch.int64, device=dev)
-        if rows.numel():
-            rows = rows[eval_bexpr(prog, prog.bexpr, rows)]
-        keys = compute_keys(prog, rows)
+        keys = rows = None
+        if not prog.empty and dev.type == "cuda" and self.engine.use_native:
+            # the JIT scan emits (key, row) of the selected rows (engine/device_exec.py PreparedEmit)
+            try:
+                em = self.__dict__.get("_emit")
+                if em is None:
+                    from .device_exec import PreparedEmit
+
+                    em = self._emit = PreparedEmit(prog)
+                keys, rows = em.run()
+            except RuntimeError:
+                keys = rows = None
+        if rows is None:
+            rows = _rows(prog) if not prog.empty else torch.zeros(0, dtype=torch.int64, device=dev)
+            if rows.numel():
+                rows = rows[eval_bexpr(prog, prog.bexpr, rows)]
+            keys = compute_keys(prog, rows)
         gid_order = np.asarray(cols["__gid__"], dtype=np.int64)
         for name, col, size in prog.thetas:
             from .lower import column_tensor

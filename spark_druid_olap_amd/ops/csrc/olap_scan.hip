@@ -613,7 +613,7 @@ __global__ __launch_bounds__(512) void olap_scan_kernel(const ScanDesc* __restri
       uint64_t* accbase = lds_acc ? acc_wave : gacc;
       for (int a = 0; a < d->naggs; ++a) {
         const AOp ao = d->aops[a];
-        if (ao.kind == A_HLL_STORED) continue;  // JIT only (the host unions stored sketches otherwise)
+        if (ao.kind == A_HLL_STORED || ao.kind == A_ROWID) continue;  // JIT only
         uint64_t ma[U];
         if (ao.filt_len > 0) {
           eval_word_program<U>(d, ao.filt_off, ao.filt_len, wb, wl, bmw, lane, ma);

@@ -119,6 +119,9 @@ def part_fields(prog, cols=None) -> List[Tuple[int, int]]:
         if kind == D.A_COUNT:
             out.append((a["slot"], 1 if a.get("filt_len") else 0))
             continue
+        if kind == D.A_ROWID:
+            out.append((a["slot"], 1))  # u32 row id (emit producers, engine/device_exec.py PreparedEmit)
+            continue
         w = 2
         if kind in (D.A_SUM_I, D.A_MIN_I, D.A_MAX_I) and not a.get("expr") and a.get("col") in cols:
             c = cols[a["col"]]
@@ -635,8 +638,8 @@ class _Gen:
             kind = a["kind"]
             if kind == D.A_HLL:
                 val = self.ival(a["col"])
-            elif kind == D.A_HLL_STORED:
-                val = "((cw0 + wl[u]) * 64 + lane)"  # the row: its stored sketch is a CSR run
+            elif kind in (D.A_HLL_STORED, D.A_ROWID):
+                val = "((cw0 + wl[u]) * 64 + lane)"  # the row (a stored sketch's CSR run / emitted id)
             elif kind == D.A_COUNT:
                 val = "1LL"
             elif kind == D.A_SUM_X:

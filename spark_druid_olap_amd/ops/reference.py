@@ -349,7 +349,7 @@ def run_reference(prog, sparse: Optional[bool] = None):
     for s, (op, init) in enumerate(prog.slots):
         acc[:, s] = init
     for a in prog.aops:
-        if a["kind"] in (D.A_HLL, D.A_HLL_STORED):
+        if a["kind"] in (D.A_HLL, D.A_HLL_STORED, D.A_ROWID):
             continue
         amask = torch.ones(rows.numel(), dtype=torch.bool, device=dev)
         if a.get("filter") is not None:

@@ -187,3 +187,23 @@ def test_two_level_narrow_records_with_empty_buckets(gpu_ds, monkeypatch):
     a = part.run().acc.clone()
     b = DE.PreparedScan(prog, mode=D.M_DENSE_GLOBAL).run().acc
     assert torch.equal(a, b)
+
+
+def test_emit_producer_rows_match_the_torch_rescan(gpu_ds):
+    """PreparedEmit: (key, row) of the selected rows from the JIT scan == the plain-PyTorch re-scan
+    (_rows + eval_bexpr + compute_keys) it replaces for theta sketches."""
+    from spark_druid_olap_amd.engine.device_exec import PreparedEmit
+    from spark_druid_olap_amd.engine.lower import Lowerer
+    from spark_druid_olap_amd.ops.reference import _rows, compute_keys, eval_bexpr
+
+    f = S.LogicalFilterSpec("and", [S.SelectorFilterSpec("c_mktsegment", "BUILDING"),
+                                    S.BoundFilterSpec("o_orderdate", "1994-01-01", "1996-12-31", False, False)])
+    prog = Lowerer(gpu_ds).lower_aggregate(["1993-01-01/1998-01-01"], f,
+                                           [S.DefaultDimensionSpec("s_nation"), S.DefaultDimensionSpec("p_brand")],
+                                           S.Granularity.parse("all"), [S.FunctionAggregationSpec("count", "c")])
+    keys, rows = PreparedEmit(prog).run()
+    r = _rows(prog)
+    r = r[eval_bexpr(prog, prog.bexpr, r)]
+    k = compute_keys(prog, r)
+    o = torch.argsort(rows)
+    assert torch.equal(rows[o], r) and torch.equal(keys[o], k)
