@@ -101,6 +101,8 @@ def col_infos(prog) -> Dict[int, ColInfo]:
 
 
 JIT_LITERALS = os.environ.get("SDO_JIT_LITERALS", "0") != "0"
+JIT_VREG = os.environ.get("SDO_JIT_VREG", "0") != "0"  # opt-in: query constants / bitmap pointers in VGPRs
+VREG_MIN_CONSTS = int(os.environ.get("SDO_JIT_VREG_MIN", "16"))
 PART_MAX_BUCKETS = 1024  # level-1 buckets of the partitioned group-by (split kernel LDS cursors)
 
 
@@ -240,9 +242,11 @@ def _dlit(v: float) -> str:
 
 class _Gen:
     def __init__(self, prog, mode: int, U: int, hll_lds: bool, narrow4: bool, lay: JitLayout, m: int,
-                 reg: bool = False, literals: bool = False):
+                 reg: bool = False, literals: bool = False, vreg: bool = False):
         self.p = prog
         self.literals = literals
+        self.vreg = vreg      # park query constants / bitmap pointers in VGPRs (many-constant filters)
+        self.nconst = 0
         self.reg = reg
         self.pipe = lay.pipe
         self.regstage = lay.regstage
@@ -287,7 +291,9 @@ class _Gen:
         if lit is not None and (self.literals or JIT_LITERALS):
             return lit  # (A/B switch: the value baked into the source, one code object per value)
         if name[:2] in ("fl", "fh", "ff", "fg", "ec"):
-            expr = f"vreg(({ctype})({expr}))"  # filter / expression constants live in VGPRs
+            self.nconst += 1
+            if self.vreg:
+                expr = f"vreg(({ctype})({expr}))"  # filter / expression constants live in VGPRs
         line = f"const {ctype} {name} = {expr};"
         if line not in self._const_set:
             self._const_set.add(line)
@@ -336,7 +342,8 @@ class _Gen:
                 else:
                     st.append(f"({{ {vdecl} (uint64_t)__ballot({' && '.join(conds)}); }})")
             elif op == D.F_IN_SET:
-                self.pre_lines.append(f"const uint64_t* inset{i} = (const uint64_t*)vreg((uint64_t)d->fops[{i}].bits);")
+                self.pre_lines.append(f"const uint64_t* inset{i} = (const uint64_t*)" +
+                                      (f"vreg((uint64_t)d->fops[{i}].bits);" if self.vreg else f"d->fops[{i}].bits;"))
                 st.append(f"({{ const int64_t v = {self.ival(col)}; "
                           f"(uint64_t)__ballot((inset{i}[((uint64_t)v) >> 6] >> (v & 63)) & 1ull); }})")
             elif op == D.F_FLT_RANGE:
@@ -560,7 +567,8 @@ class _Gen:
             L.append(f"  const unsigned char* c{i} = (const unsigned char*)d->cols[{i}].ptr;")
         for j, (row, stride, count) in enumerate(p.bm_leaves):
             # (VGPR-resident: read once per chunk with a per-lane address anyway)
-            L.append(f"  const uint64_t* bm{j} = (const uint64_t*)vreg((uint64_t)d->bm_bits[{j}]);")
+            L.append(f"  const uint64_t* bm{j} = (const uint64_t*)" +
+                     (f"vreg((uint64_t)d->bm_bits[{j}]);" if self.vreg else f"d->bm_bits[{j}];"))
         for k, kc in enumerate(p.keys):
             if kc.kind == D.K_REMAP or (kc.kind == D.K_TIME and getattr(kc, "tlut", None) is not None):
                 L.append(f"  const int32_t* rm{k} = (const int32_t*)d->kops[{k}].remap;")
@@ -950,6 +958,13 @@ class JitScan:
                            ).hexdigest()[:6]
         self.name = f"sdo_jit_{tag}"
         self.src = g.source(self.name)
+        if JIT_VREG and not literals and g.nconst >= VREG_MIN_CONSTS:
+            # dozens of descriptor-loaded bounds (TPC-H Q19: 26) spill SGPRs inside the scan loop;
+            # VGPRs hold them without spills (Q19 5.4 -> 3.8 ms) but cost occupancy elsewhere (Q16's
+            # hash scan 13.4 -> 15.9 ms), and a repeated statement's literal-specialized kernel
+            # (JitScan.specialized) has neither problem: opt-in (SDO_JIT_VREG=1)
+            g = _Gen(prog, mode, U, hll_lds, narrow4, self.lay, m, self.reg, literals, vreg=True)
+            self.src = g.source(self.name)
         self.handle = compile_source(self.src, self.name) if load else -1
         if not load:
             compile_code(self.src, self.name)
