@@ -683,11 +683,18 @@ class _Gen:
                 cond = f"f{ai}"
             kind = a["kind"]
             val = f"v{ai}_[u]"
+            wide = getattr(p, "hll32", False) and not (self.hll_lds and mode == D.M_DENSE_LDS)
             if kind == D.A_HLL:
-                body.append(f"        if ({cond}) hll_update8(hll{ai}, slot, {p.hll_p}, {val}, {_lit(a.get('salt', 0))});")
+                if wide:  # global u32 registers (engine/device_exec.py narrows them after the scan)
+                    body.append(f"        if ({cond}) hll_update32((uint32_t*)hll{ai}, slot, {p.hll_p}, {val}, "
+                                f"{_lit(a.get('salt', 0))});")
+                else:
+                    body.append(f"        if ({cond}) hll_update8(hll{ai}, slot, {p.hll_p}, {val}, "
+                                f"{_lit(a.get('salt', 0))});")
                 continue
             if kind == D.A_HLL_STORED:
-                body.append(f"        if ({cond}) hll_merge_csr(hll{ai}, slot, {p.hll_p}, sko{ai}, skv{ai}, {val});")
+                fn = "hll_merge_csr32((uint32_t*)" if getattr(p, "hll32", False) else "hll_merge_csr("
+                body.append(f"        if ({cond}) {fn}hll{ai}, slot, {p.hll_p}, sko{ai}, skv{ai}, {val});")
                 continue
             s = a["slot"]
             op = p.slots[s][0]

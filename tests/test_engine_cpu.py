@@ -248,7 +248,7 @@ def test_scan_buffer_budget_releases_least_recently_used(monkeypatch):
         b = DE._Bufs()
         b.acc, b.keys, b.overflow, b.desc = torch.zeros(n, dtype=torch.int64), torch.zeros(1), torch.zeros(1), \
             torch.zeros(1)
-        b.touch, b.init_row, b.hll, b.part = torch.zeros(1), torch.zeros(1), [], None
+        b.touch, b.init_row, b.hll, b.hll32, b.part = torch.zeros(1), torch.zeros(1), [], [], None
         return b
 
     monkeypatch.setattr(DE, "BUF_BUDGET", 28_000)
