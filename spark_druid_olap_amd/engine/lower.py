@@ -969,7 +969,7 @@ class Lowerer:
         the LUT and the arithmetic paths agree bit for bit; out-of-span values clamp like the key."""
         ds = self.ds
         u = int(ds.time_unit_ms)
-        if u < 1000:
+        if u < 1000 or os.environ.get("SDO_TIME_LUT", "1") == "0":
             return
         lo, hi = self._data_span([])
         v0, v1 = lo // u, (hi - 1) // u

@@ -615,9 +615,9 @@ class _Gen:
             v = self.ival(kc.col_idx)
             # stride / base / card from the descriptor (query constants); for LDS tables the
             # layout (G) is part of the shape anyway
-            ks = self.const(f"ks{k}", f"(uint64_t)d->kops[{k}].stride", "uint64_t")
-            kb = self.const(f"kb{k}", f"d->kops[{k}].base")
-            kn = self.const(f"kn{k}", f"d->kops[{k}].card")
+            ks = self.const(f"ks{k}", f"(uint64_t)d->kops[{k}].stride", "uint64_t", f"{int(kc.stride)}ull")
+            kb = self.const(f"kb{k}", f"d->kops[{k}].base", lit=_lit(kc.base))
+            kn = self.const(f"kn{k}", f"d->kops[{k}].card", lit=_lit(kc.card))
             if kc.kind == D.K_ID and kc.base:  # shard-local key window (engine/executor.py ShardWindow)
                 body.append(f"        key += (uint64_t)((int64_t)({v}) - {kb}) * {ks};")
             elif kc.kind == D.K_ID:
@@ -630,9 +630,9 @@ class _Gen:
                 body.append(f"          i_ = i_ < 0 ? 0 : (i_ >= {n} ? {n - 1} : i_);")
                 body.append(f"          key += (uint64_t)rm{k}[i_] * {ks}; }}")
             elif kc.kind == D.K_TIME:
-                ktz = self.const(f"ktz{k}", f"d->kops[{k}].tz_ms")
-                kpm = self.const(f"kpm{k}", f"d->kops[{k}].period_ms")
-                kor = self.const(f"kor{k}", f"d->kops[{k}].origin_ms")
+                ktz = self.const(f"ktz{k}", f"d->kops[{k}].tz_ms", lit=_lit(kc.tz_ms))
+                kpm = self.const(f"kpm{k}", f"d->kops[{k}].period_ms", lit=_lit(kc.period_ms or 1))
+                kor = self.const(f"kor{k}", f"d->kops[{k}].origin_ms", lit=_lit(kc.origin_ms))
                 body.append(f"        {{ int64_t t = time_field_t<{kc.tfield}>(({v}) * {_lit(p.ds.time_unit_ms)} + "
                             f"{ktz}, {kpm}, {kor}) - {kb};")
                 body.append(f"          t = t < 0 ? 0 : (t >= {kn} ? {kn} - 1 : t);")
