@@ -368,6 +368,12 @@ def column_tensor(ds: DataSource, name: str) -> torch.Tensor:
         return ds.dims[name].ids
     if name in ds.metrics:
         return ds.metrics[name].data
+    if "#hll" in name:
+        from ..segment.hllcode import lookup
+
+        t = lookup(ds, name)
+        if t is not None:
+            return t
     raise LoweringError(f"unknown column {name!r} in datasource {ds.name}")
 
 
@@ -1144,8 +1150,12 @@ class Lowerer:
                 raise LoweringError(f"cardinality over unknown column {col!r}")
             if col in ds.metrics and ds.metrics[col].sketch is not None:
                 raise LoweringError(f"cardinality by row over the sketch metric {col!r}")
-            ci = prog.col(col)
-            d = aop(D.A_HLL, ci)
+            from ..segment.hllcode import code_column
+
+            code = code_column(ds, col, prog.hll_p, _salt(col))
+            # a resident (bucket, rho) code plane when the dimension has one (segment/hllcode.py):
+            # half the bytes of an int32 id and no per-row hashing; registers are identical
+            d = aop(D.A_HLL_CODE, prog.col(code)) if code is not None else aop(D.A_HLL, prog.col(col))
             d["hll"] = prog.nhll
             d["salt"] = _salt(col)
             prog.aggs.append(AggOut(a.name, "hll", hll_index=prog.nhll, out_type="double", combine="hll"))
@@ -1861,7 +1871,7 @@ def pack(prog: ScanProgram, mode: int, dedup: int, hll_lds: int, lds_bytes: int,
         o["kind"], o["col"], o["slot"] = a["kind"], a["col"], max(a["slot"], 0)
         o["expr_off"], o["expr_len"] = a.get("expr_off", 0), a.get("expr_len", 0)
         o["filt_off"], o["filt_len"] = a.get("filt_off", 0), a.get("filt_len", 0)
-        if a["kind"] == D.A_HLL:
+        if a["kind"] in D.HLL_KINDS:
             o["hll_regs"] = hll_ptrs[a["hll"]]
             o["hll_lds_off"] = hll_lds_offs[a["hll"]] if hll_lds_offs else 0
             o["salt"] = a.get("salt", 0)

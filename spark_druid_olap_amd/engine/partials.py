@@ -146,6 +146,12 @@ class _Const:
         self.value, self.dtype = value, dtype
 
 
+def _const_column(R: int, v: "_Const") -> np.ndarray:
+    """A read-only length-R view of one value (stride 0): a constant key of a million-row result
+    (TPC-H Q3's o_shippriority) costs nothing instead of a 4 MB fill."""
+    return np.broadcast_to(np.asarray(v.value, dtype=v.dtype), (R,))
+
+
 def _device_typed(kc, ids: torch.Tensor, sqlt: Optional[str]):
     """Typed values of a dictionary-id key computed ON THE DEVICE for a numeric SQL output type
     (the same values ``sql/execute.py:_dict_series`` would produce on the host): integer range
@@ -367,7 +373,7 @@ def finalize(prog, parts: Partials, out_types: Optional[Dict[str, str]] = None) 
         hll_d = parts.hll
         for i, v in typed.items():
             if isinstance(v, _Const):
-                (key_ids if i < nk else derived_ids)[i if i < nk else i - nk] = np.full(R, v.value, dtype=v.dtype)
+                (key_ids if i < nk else derived_ids)[i if i < nk else i - nk] = _const_column(R, v)
     if parts.kind != "sparse":
         agg_host = {}
     cols: Dict[str, np.ndarray] = {}

@@ -623,13 +623,18 @@ __global__ __launch_bounds__(512) void olap_scan_kernel(const ScanDesc* __restri
 #pragma unroll
           for (int u = 0; u < U; ++u) ma[u] = m[u];
         }
-        if (ao.kind == A_HLL) {
+        if (ao.kind == A_HLL || ao.kind == A_HLL_CODE) {
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             if ((ma[u] >> lane) & 1ull) {
               const int64_t v = col_int<U>(d, wb, ao.col, u, lane);
               uint32_t bucket, rho;
-              dev::hll_bucket_rho(v, ao.salt, hll_p, bucket, rho);
+              if (ao.kind == A_HLL_CODE) {  // precomputed u16 bucket << 5 | rho (segment/hllcode.py)
+                bucket = ((uint32_t)v & 0xffffu) >> 5;
+                rho = (uint32_t)v & 31u;
+              } else {
+                dev::hll_bucket_rho(v, ao.salt, hll_p, bucket, rho);
+              }
               const int64_t idx = slot[u] * hll_m + bucket;
               if (mode == M_DENSE_LDS && d->hll_lds) {
                 uint32_t* r = (uint32_t*)(lds + ao.hll_lds_off) + idx;
@@ -707,7 +712,7 @@ __global__ __launch_bounds__(512) void olap_scan_kernel(const ScanDesc* __restri
     if (d->hll_lds) {
       for (int a = 0; a < d->naggs; ++a) {
         const AOp ao = d->aops[a];
-        if (ao.kind != A_HLL) continue;
+        if (ao.kind != A_HLL && ao.kind != A_HLL_CODE) continue;
         // u32 LDS registers (interpreter layout) -> four packed global byte registers per dword
         const uint32_t* rr = (const uint32_t*)(lds + ao.hll_lds_off);
         uint32_t* g = (uint32_t*)ao.hll_regs;

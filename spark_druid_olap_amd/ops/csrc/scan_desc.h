@@ -100,7 +100,8 @@ enum AKind : int32_t {
   A_COUNT = 0, A_SUM_I = 1, A_SUM_F = 2, A_MIN_I = 3, A_MAX_I = 4, A_MIN_F = 5, A_MAX_F = 6, A_HLL = 7,
   A_SUM_X = 8,  // exact decimal expression sum: llrint(expr) (expr pre-scaled by 10^scale) into S_SUM_I
   A_HLL_STORED = 9,  // union of the row's stored (rolled-up) HLL sketch into the group's registers (JIT only)
-  A_ROWID = 10       // emit producers: the row id as a record field (JIT only)
+  A_ROWID = 10,      // emit producers: the row id as a record field (JIT only)
+  A_HLL_CODE = 11    // HLL over a code column: u16 (bucket << 5 | rho) per row (segment/hllcode.py)
 };
 // accumulator slot update ops
 enum SlotOp : int32_t { S_SUM_I = 0, S_SUM_F = 1, S_MIN_I = 2, S_MAX_I = 3 };

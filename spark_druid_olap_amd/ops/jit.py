@@ -116,7 +116,7 @@ def part_fields(prog, cols=None) -> List[Tuple[int, int]]:
     out = []
     for a in prog.aops:
         kind = a["kind"]
-        if kind in (D.A_HLL, D.A_HLL_STORED):
+        if kind in (D.A_HLL, D.A_HLL_CODE, D.A_HLL_STORED):
             continue
         if kind == D.A_COUNT:
             out.append((a["slot"], 1 if a.get("filt_len") else 0))
@@ -528,7 +528,7 @@ class _Gen:
         w = 1
         fi = 0
         for ai, a in enumerate(p.aops):
-            if a["kind"] in (D.A_HLL, D.A_HLL_STORED):
+            if a["kind"] in (D.A_HLL, D.A_HLL_CODE, D.A_HLL_STORED):
                 continue
             slot, width = fields[fi]
             fi += 1
@@ -578,7 +578,7 @@ class _Gen:
             L.append(f"  const int64_t zlo{z} = d->zones[{z}].lo;")
             L.append(f"  const int64_t zhi{z} = d->zones[{z}].hi;")
         for ai, a in enumerate(p.aops):
-            if a["kind"] == D.A_HLL:
+            if a["kind"] in D.HLL_KINDS:
                 if self.hll_lds and mode == D.M_DENSE_LDS:
                     L.append(f"  unsigned char* hll{ai} = lds + {lay.hll_off + a['hll'] * G * self.m};")
                 else:
@@ -644,7 +644,7 @@ class _Gen:
         body.append("        key_[u] = key;")
         for ai, a in enumerate(p.aops):
             kind = a["kind"]
-            if kind == D.A_HLL:
+            if kind in D.HLL_KINDS:
                 val = self.ival(a["col"])
             elif kind in (D.A_HLL_STORED, D.A_ROWID):
                 val = "((cw0 + wl[u]) * 64 + lane)"  # the row (a stored sketch's CSR run / emitted id)
@@ -684,6 +684,12 @@ class _Gen:
             kind = a["kind"]
             val = f"v{ai}_[u]"
             wide = getattr(p, "hll32", False) and not (self.hll_lds and mode == D.M_DENSE_LDS)
+            if kind == D.A_HLL_CODE:
+                # precomputed (bucket, rho) plane (segment/hllcode.py): no per-row hash
+                ix = f"((uint64_t)slot << {p.hll_p}) + ((uint32_t){val} >> 5)"
+                fn = "hll_max32((uint32_t*)" if wide else "hll_max8("
+                body.append(f"        if ({cond}) {fn}hll{ai}, {ix}, (uint32_t){val} & 31u);")
+                continue
             if kind == D.A_HLL:
                 if wide:  # global u32 registers (engine/device_exec.py narrows them after the scan)
                     body.append(f"        if ({cond}) hll_update32((uint32_t*)hll{ai}, slot, {p.hll_p}, {val}, "
@@ -908,7 +914,7 @@ class _Gen:
             out.append("  }")
             if self.hll_lds and p.nhll:
                 for ai, a in enumerate(p.aops):
-                    if a["kind"] != D.A_HLL:
+                    if a["kind"] not in D.HLL_KINDS:
                         continue
                     # four byte registers per dword: one read (and rarely a CAS) per 4 registers
                     out.append(f"  {{ uint32_t* g = (uint32_t*)d->aops[{ai}].hll_regs;")

@@ -349,7 +349,7 @@ def run_reference(prog, sparse: Optional[bool] = None):
     for s, (op, init) in enumerate(prog.slots):
         acc[:, s] = init
     for a in prog.aops:
-        if a["kind"] in (D.A_HLL, D.A_HLL_STORED, D.A_ROWID):
+        if a["kind"] in (D.A_HLL, D.A_HLL_CODE, D.A_HLL_STORED, D.A_ROWID):
             continue
         amask = torch.ones(rows.numel(), dtype=torch.bool, device=dev)
         if a.get("filter") is not None:
@@ -372,14 +372,18 @@ def run_reference(prog, sparse: Optional[bool] = None):
         acc[:, s] = col
     hlls = []
     for a in prog.aops:
-        if a["kind"] != D.A_HLL:
+        if a["kind"] not in D.HLL_KINDS:
             continue
         amask = torch.ones(rows.numel(), dtype=torch.bool, device=dev)
         if a.get("filter") is not None:
             amask = eval_bexpr(prog, a["filter"], rows)
         r, ix = rows[amask], idx[amask]
-        v = _col(prog, prog.colname(a["col"]))[r].to(torch.int64)
-        bucket, rho = hll_update_values(v, a.get("salt", 0), prog.hll_p)
+        c = _col(prog, prog.colname(a["col"]))
+        if a["kind"] == D.A_HLL_CODE:  # u16 bucket << 5 | rho (segment/hllcode.py)
+            code = c.view(torch.int16)[r].to(torch.int64) & 0xFFFF
+            bucket, rho = code >> 5, code & 31
+        else:
+            bucket, rho = hll_update_values(c[r].to(torch.int64), a.get("salt", 0), prog.hll_p)
         regs = torch.zeros(R * m, dtype=torch.int64, device=dev)
         regs.scatter_reduce_(0, ix * m + bucket, rho, reduce="amax", include_self=True)
         hlls.append(regs.view(R, m).to(torch.uint8))  # byte registers, like the scan kernels

@@ -37,6 +37,8 @@ TORCH_DT = {"uint8": torch.uint8, "int16": torch.int16, "int32": torch.int32, "i
             "float32": torch.float32, "float64": torch.float64}
 # kernel dtype codes (scan_desc.h DType)
 DT_CODE = {torch.uint8: 0, torch.int16: 1, torch.int32: 2, torch.int64: 3, torch.float32: 4, torch.float64: 5}
+if hasattr(torch, "uint16"):
+    DT_CODE[torch.uint16] = 6  # HLL code planes (segment/hllcode.py)
 
 
 def dtype_code(t: torch.Tensor) -> int:
