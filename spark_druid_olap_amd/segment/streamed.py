@@ -35,6 +35,8 @@ class _WindowDataSource(DataSource):
     """Rows [lo, hi) of a host shard on the device.  Reports the WHOLE shard's time span so
     time-bucket key bases (lower.granularity_key) agree across windows."""
 
+    hll_codes_ok = False  # columns are staged per window: no resident derived planes (segment/hllcode.py)
+
     def min_time_ms(self) -> int:
         return self.fd_source.min_time_ms()
 
@@ -50,6 +52,7 @@ class HostShard:
         if ds.device.type != "cpu":
             raise ValueError("HostShard wraps a host-resident (CPU) datasource")
         self.ds = ds
+        ds.hll_codes_ok = False  # programs lowered over the shard read only columns a window stages
         self.device = torch.device(device)
         self.window_rows = max(CHUNK_ROWS, window_rows // CHUNK_ROWS * CHUNK_ROWS)
         if pin and torch.cuda.is_available():

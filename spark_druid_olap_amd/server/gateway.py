@@ -76,12 +76,16 @@ _KIND = {"boolean": (0, np.uint8), "tinyint": (1, np.int8), "smallint": (2, np.i
          "bigint": (4, np.int64), "double": (5, np.float64), "float": (5, np.float64), "decimal": (5, np.float64)}
 
 
-def result_columns(df) -> List[pd.Series]:
-    """The result's columns as Series: a pandas frame, or the SQL executor's Batch (no DataFrame is
-    built on the serving path)."""
+def result_columns(df) -> list:
+    """The result's columns: Series of a pandas frame, or the SQL executor's Batch columns -- numeric
+    ones as their numpy values (no DataFrame and no Series are built on the serving path)."""
     if isinstance(df, pd.DataFrame):
         return [df.iloc[:, i] for i in range(df.shape[1])]
-    return [df.cols[r.rid] for r in df.refs]
+    out = []
+    for r in df.refs:
+        a = df.cols.array(r.rid)
+        out.append(a if a is not None else df.cols[r.rid])
+    return out
 
 
 def encode_columns(types: List[str], df) -> List[Tuple[int, bytes, bytes, bytes]]:

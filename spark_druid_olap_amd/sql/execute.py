@@ -34,12 +34,66 @@ def take_series(v: pd.Series, idx: np.ndarray) -> pd.Series:
         return v.iloc[idx].reset_index(drop=True)
 
 
+class LazySeries:
+    """A result column whose values are final (typed numpy values, or dictionary codes over cached
+    categories) but whose pandas wrapper is built on first access.  Numeric columns carry their
+    array (``arr``), so compiled projections and the serving encoder read it without a Series:
+    a small query's result costs no pandas constructions unless a caller asks for pandas."""
+
+    __slots__ = ("make", "arr")
+
+    def __init__(self, make, arr: Optional[np.ndarray] = None):
+        self.make, self.arr = make, arr
+
+
+class Cols(dict):
+    """Batch columns by attribute id; ``LazySeries`` entries become Series when read through the
+    mapping interface (``raw`` returns an entry as stored)."""
+
+    __slots__ = ()
+
+    def __getitem__(self, k):
+        v = dict.__getitem__(self, k)
+        if type(v) is LazySeries:
+            v = v.make()
+            dict.__setitem__(self, k, v)
+        return v
+
+    def get(self, k, default=None):
+        return self[k] if k in self else default
+
+    def items(self):
+        return [(k, self[k]) for k in self]
+
+    def values(self):
+        return [self[k] for k in self]
+
+    def raw(self, k):
+        return dict.get(self, k)
+
+    def array(self, k) -> Optional[np.ndarray]:
+        """The numeric numpy values of column ``k`` when available without building pandas
+        objects (a lazy numeric column, or a Series over a plain numeric numpy dtype)."""
+        v = dict.get(self, k)
+        if type(v) is LazySeries:
+            return v.arr
+        if v is not None:
+            dt = v.dtype
+            if isinstance(dt, np.dtype) and dt.kind in "iuf":
+                return v.to_numpy()
+        return None
+
+
+def lazy_series(arr: np.ndarray) -> LazySeries:
+    return LazySeries(lambda: fast_series(arr), arr)
+
+
 class Batch:
     """Columns (by attribute id) of equal length, in ``refs`` order."""
 
     def __init__(self, refs: List[A.Ref], cols: Dict[int, pd.Series], n: int):
         self.refs = refs
-        self.cols = cols
+        self.cols = cols if type(cols) is Cols else Cols(cols)
         self.n = n
 
     def frame(self, subq=None) -> Frame:
@@ -170,17 +224,19 @@ class Executor:
         fr = None
         cols = {}
         refs = p._out
+        bcols = b.cols
         for (kind, x), e, r in zip(prog, p.exprs, refs):
             if kind == "ref":
-                cols[r.rid] = b.cols[x]
+                v = bcols.raw(x)
+                cols[r.rid] = v if v is not None else bcols[x]
                 continue
             if x is not None and b.n <= _NP_FAST_MAX_ROWS:
                 try:
-                    a = x(b.cols)
+                    a = x(bcols)
                 except _NoFast:
                     a = None
                 if a is not None:
-                    cols[r.rid] = fast_series(a)
+                    cols[r.rid] = lazy_series(a)
                     continue
             if fr is None:
                 fr = b.frame(self._subquery)
@@ -317,7 +373,7 @@ class Executor:
             self.druid_stats.append({"spec": p.spec, "ms": (time.perf_counter() - t0) * 1e3, "rows": 1})
             return Batch(p.refs, cols, 1)
         for r, (name, sqlt, kind) in zip(p.refs, p.columns):
-            cols[r.rid] = druid_value_series(res.data[name], sqlt, kind, n)
+            cols[r.rid] = druid_value_lazy(res.data[name], sqlt, kind, n)
         self.druid_stats.append({"spec": p.spec, "ms": (time.perf_counter() - t0) * 1e3, "rows": n})
         return Batch(p.refs, cols, n)
 
@@ -454,13 +510,10 @@ def _np_compile(e: A.Expr):
         rid = e.rid
 
         def ref(cols):
-            s = cols.get(rid)
-            if s is None:
+            a = cols.array(rid)
+            if a is None:
                 raise _NoFast
-            dt = s.dtype
-            if not isinstance(dt, np.dtype) or dt.kind not in "iuf":
-                raise _NoFast
-            return s.to_numpy()
+            return a
         return ref
     if isinstance(e, A.Lit):
         if isinstance(e.value, bool) or not isinstance(e.value, (int, float)):
@@ -591,6 +644,30 @@ def druid_value_series(col, sqlt: str, kind: str, n: int) -> pd.Series:
     if arr.dtype.kind == "O" and base(sqlt) != "string":
         return to_series(pd.Series(arr), sqlt)
     return to_series(pd.Series(arr), sqlt)
+
+
+_DictColumn = None
+
+
+def druid_value_lazy(col, sqlt: str, kind: str, n: int):
+    """``druid_value_series`` with the pandas wrapper deferred (``LazySeries``) for the common
+    result columns: numeric aggregates / integer keys (their final numpy values are computed here)
+    and dictionary-coded strings (codes over cached categories)."""
+    global _DictColumn
+    if _DictColumn is None:
+        from ..engine.columns import DictColumn as _DC
+
+        _DictColumn = _DC
+    if isinstance(col, _DictColumn):
+        return LazySeries(lambda: _dict_series(col, sqlt))
+    if kind != "time":
+        arr = np.asarray(col)
+        bt = base(sqlt)
+        if arr.dtype.kind in "fiu" and bt in ("double", "float", "decimal"):
+            return lazy_series(arr.astype(np.float64, copy=False))
+        if arr.dtype.kind in "iu" and bt in ("tinyint", "smallint", "int", "bigint"):
+            return lazy_series(arr if (arr.dtype == np.int32 and bt != "bigint") else arr.astype(np.int64, copy=False))
+    return druid_value_series(col, sqlt, kind, n)
 
 
 def _categorical(codes: np.ndarray, dtype) -> pd.Categorical:

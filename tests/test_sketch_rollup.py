@@ -214,6 +214,11 @@ def _split_worker(rank, world, port, data_dir, outdir):
     with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
         pickle.dump(out, f)
     w.barrier()
+    import torch.distributed as dist
+
+    dist.destroy_process_group()
+    # (Arrow's CSV reader pool can abort interpreter teardown under load: the result is written)
+    os._exit(0)
 
 
 def test_split_ingest_across_ranks_equals_single_ingest(data_dir, tmp_path):
