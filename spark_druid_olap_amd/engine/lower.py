@@ -1861,7 +1861,8 @@ def pack(prog: ScanProgram, mode: int, dedup: int, hll_lds: int, lds_bytes: int,
         if table is not None:
             t = getattr(kc, "_remap_dev", None)
             if t is None or t.device != ds.device:
-                t = torch.from_numpy(table).to(ds.device)
+                # (cached remap tables are read-only arrays: torch gets its own copy)
+                t = torch.from_numpy(table if table.flags.writeable else table.copy()).to(ds.device)
                 kc._remap_dev = t  # type: ignore[attr-defined]
             prog.keepalive.append(t)
             k["remap"] = t.data_ptr()

@@ -175,6 +175,29 @@ def reg_eligible(prog, mode: int) -> bool:
 # accumulator copies per wave for tiny dense key spaces (lanes l, l+C, l+2C.. share copy l % C; up
 # to 64 = lane-private, no same-address LDS atomics) -- the LDS budget may halve it
 MAX_NCOPY = int(os.environ.get("SDO_JIT_NCOPY", "16"))
+# counts of tiny dense key spaces as wave ballots: per 64-row step and group one compare whose lane
+# mask popcounts into a wave-uniform (scalar) counter -- no LDS atomic per row; lane 0 adds the
+# wave's totals into its accumulator copy at the end.  Up to this many groups (0: off).  Measured
+# slower than the LDS copies on MI355X (count by l_returnflag, l_linestatus over SF100: 0.83 vs
+# 0.47 ms; the VALU-compare -> SALU-popcount chain serializes): opt-in.
+BALLOT_G = int(os.environ.get("SDO_JIT_BALLOT_G", "0"))
+# whole-chunk fast path: a chunk entirely inside the scan's row range with no chunk-level bitmap
+# prefilter walks its 64 words in order (every word's row mask all ones, then refined by the
+# per-row filter) instead of the find-first-set / readlane chain over its non-empty words
+FULL_CHUNKS = os.environ.get("SDO_JIT_FULL", "1") != "0"
+
+
+def ballot_slots(prog, mode: int, reg: bool, shared: bool) -> set:
+    """Accumulator slots updated only by (optionally filtered) counts, for the ballot path."""
+    if mode != D.M_DENSE_LDS or reg or shared or not (0 < prog.G <= BALLOT_G):
+        return set()
+    out = set()
+    for s in range(prog.nslots):
+        users = [a for a in prog.aops if a.get("slot") == s and a["kind"] not in
+                 (D.A_HLL, D.A_HLL_CODE, D.A_HLL_STORED, D.A_ROWID)]
+        if users and all(a["kind"] == D.A_COUNT for a in users) and prog.slots[s][0] == D.S_SUM_I:
+            out.add(s)
+    return out
 
 
 def layout(prog, mode: int, U: int, hll_lds: bool, m: int, reg: bool = False, pipe: bool = False,
@@ -551,6 +574,34 @@ class _Gen:
         body.append("        }")
         body.append("        woff += (uint32_t)__popcll(am_);")
 
+    def _words_tail(self, fcols, word_filter, mode: int, U: int, stage: List[str], body: List[str]) -> List[str]:
+        """The per-step tail of a word loop (wl / m set): the per-row word filter, the empty-step
+        skip, then the staged loads and updates."""
+        out: List[str] = []
+        if word_filter is not None:
+            if fcols:
+                if not self.regstage:
+                    out.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
+                self.stage_words(out, fcols, "wl", "wb")
+                if not self.regstage:
+                    out.append('      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
+            out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) m[u] &= {word_filter};")
+        out.append("      uint64_t any = 0;")
+        out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) any |= m[u];")
+        out.append("      if (any == 0) continue;")
+        if mode == D.M_MASK:
+            out.append("      if (lane == 0) {")
+            out.append("        unsigned long long cnt = 0;")
+            out.append(f"#pragma unroll\n        for (int u = 0; u < {U}; ++u) {{")
+            out.append("          if (m[u]) ((uint64_t*)d->out_mask)[cw0 + wl[u]] = m[u];")
+            out.append("          cnt += __popcll(m[u]);")
+            out.append("        }")
+            out.append("        atomicAdd((unsigned long long*)d->out_count, cnt);")
+            out.append("      }")
+        else:
+            out.extend(stage + body)
+        return out
+
     def source(self, name: str) -> str:
         p, U, NP, lay = self.p, self.U, self.NP, self.lay
         mode = self.mode
@@ -563,6 +614,7 @@ class _Gen:
         G, NS = p.G, p.nslots
         NCT = 1 if lay.shared else W * lay.ncopy
         narrow = {s for s in range(NS) if _narrow_slot(p, s, self.cols)} if self.reg else set()
+        bslots = ballot_slots(p, mode, self.reg, lay.shared)
         for i in sorted(self.cols):
             L.append(f"  const unsigned char* c{i} = (const unsigned char*)d->cols[{i}].ptr;")
         for j, (row, stride, count) in enumerate(p.bm_leaves):
@@ -704,6 +756,10 @@ class _Gen:
                 continue
             s = a["slot"]
             op = p.slots[s][0]
+            if s in bslots:
+                for g in range(G):
+                    body.append(f"        bc{g}_{s} += (uint64_t)__builtin_popcountll(__ballot({cond} && key == {g}ull));")
+                continue
             if self.reg:
                 body.append(f"        {{ const int64_t v_ = {val}; const int kk_ = (int)key;")
                 for g in range(G):
@@ -781,6 +837,8 @@ class _Gen:
                 out.append(f"  for (int i = threadIdx.x; i < {lay.hll_bytes // 4}; i += {W * 64}) "
                            f"((uint32_t*)(lds + {lay.hll_off}))[i] = 0u;")
             out.append("  __syncthreads();")
+        for s in sorted(bslots):
+            out.append("  " + " ".join(f"uint64_t bc{g}_{s} = 0;" for g in range(G)))
         if self.reg:
             for g in range(G):
                 for s in range(NS):
@@ -838,6 +896,16 @@ class _Gen:
         if self.pipe:
             out.extend(self._pipelined_words(pcols, stage, body))
         else:
+            full = FULL_CHUNKS and not pre and mode in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL, D.M_HASH)
+            if full:
+                out.append(f"    if (clo == crow0 && chi == crow0 + {D.CHUNK_ROWS}) {{")
+                out.append(f"    for (int w0_ = 0; w0_ < {D.CHUNK_WORDS}; w0_ += {U}) {{")
+                out.append(f"      int wl[{U}];")
+                out.append(f"      uint64_t m[{U}];")
+                out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{ wl[u] = w0_ + u; m[u] = ~0ull; }}")
+                out.extend(self._words_tail(fcols, word_filter, mode, U, stage, body))
+                out.append("    }")
+                out.append("    } else {")
             out.append("    while (nz) {")
             out.append(f"      int wl[{U}];")
             out.append(f"      uint64_t m[{U}];")
@@ -845,35 +913,21 @@ class _Gen:
             out.append("        if (nz) { wl[u] = __builtin_ctzll(nz); nz &= nz - 1ull; m[u] = readlane64(pre, wl[u]); }")
             out.append("        else { wl[u] = 0; m[u] = 0ull; }")
             out.append("      }")
-            if word_filter is not None:
-                if fcols:
-                    if not self.regstage:
-                        out.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
-                    self.stage_words(out, fcols, "wl", "wb")
-                    if not self.regstage:
-                        out.append('      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
-                out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) m[u] &= {word_filter};")
-            out.append("      uint64_t any = 0;")
-            out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) any |= m[u];")
-            out.append("      if (any == 0) continue;")
-            if mode == D.M_MASK:
-                out.append("      if (lane == 0) {")
-                out.append("        unsigned long long cnt = 0;")
-                out.append(f"#pragma unroll\n        for (int u = 0; u < {U}; ++u) {{")
-                out.append("          if (m[u]) ((uint64_t*)d->out_mask)[cw0 + wl[u]] = m[u];")
-                out.append("          cnt += __popcll(m[u]);")
-                out.append("        }")
-                out.append("        atomicAdd((unsigned long long*)d->out_count, cnt);")
-                out.append("      }")
-            else:
-                out.extend(stage + body)
+            out.extend(self._words_tail(fcols, word_filter, mode, U, stage, body))
             out.append("    }")
+            if full:
+                out.append("    }")
         for g in range(G if narrow else 0):
             for s in sorted(narrow):
                 out.append(f"    r{g}_{s} += n{g}_{s}; n{g}_{s} = 0;")
         if mode == D.M_PART:
             out.append("    if (lane == 0) pend[c] = cbase + woff;")
         out.append("  }")
+        for s in sorted(bslots):
+            # the wave's ballot counts (uniform) into lane 0's accumulator copy
+            for g in range(G):
+                out.append(f"  if (lane == 0 && bc{g}_{s}) acc_update<{D.S_SUM_I}>(acc + ({g} * {NS} + {s}) * {NCT} + copy, "
+                           f"(int64_t)bc{g}_{s});")
         if self.reg:
             # wave-reduce each register partial; lane 0 stores the wave's copy for the block flush
             for g in range(G):

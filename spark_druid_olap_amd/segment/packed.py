@@ -122,7 +122,8 @@ def packed_column(ds, name: str) -> Optional[PackedColumn]:
 
     t = column_tensor(ds, name)
     pc = None
-    if not t.is_floating_point() and t.dtype != torch.bool and t.device.type == "cuda":
+    if not t.is_floating_point() and t.dtype in (torch.uint8, torch.int16, torch.int32, torch.int64) and \
+            t.device.type == "cuda":  # (not the u16 HLL code planes, segment/hllcode.py)
         n = int(ds.num_rows)
         lo, hi = _range(t, n)
         W = width_for(lo, hi)
