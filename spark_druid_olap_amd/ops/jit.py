@@ -185,6 +185,10 @@ BALLOT_G = int(os.environ.get("SDO_JIT_BALLOT_G", "0"))
 # prefilter walks its 64 words in order (every word's row mask all ones, then refined by the
 # per-row filter) instead of the find-first-set / readlane chain over its non-empty words
 FULL_CHUNKS = os.environ.get("SDO_JIT_FULL", "1") != "0"
+# a prefiltered chunk with at least this many non-empty words (of 64) also walks them in order,
+# reading each word's mask by lane index (independent readlanes) and skipping all-empty steps;
+# sparser chunks take the find-first-set chain over their non-empty words only (0: always chain)
+DENSE_WORDS = int(os.environ.get("SDO_JIT_DENSE_WORDS", "48"))
 
 
 def ballot_slots(prog, mode: int, reg: bool, shared: bool) -> set:
@@ -906,6 +910,16 @@ class _Gen:
                 out.extend(self._words_tail(fcols, word_filter, mode, U, stage, body))
                 out.append("    }")
                 out.append("    } else {")
+            dense = DENSE_WORDS > 0 and bool(pre) and mode in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL, D.M_HASH)
+            if dense:
+                out.append(f"    if (__popcll(nz) >= {DENSE_WORDS}) {{")
+                out.append(f"    for (int w0_ = 0; w0_ < {D.CHUNK_WORDS}; w0_ += {U}) {{")
+                out.append(f"      int wl[{U}];")
+                out.append(f"      uint64_t m[{U}];")
+                out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{ wl[u] = w0_ + u; m[u] = readlane64(pre, w0_ + u); }}")
+                out.extend(self._words_tail(fcols, word_filter, mode, U, stage, body))
+                out.append("    }")
+                out.append("    } else {")
             out.append("    while (nz) {")
             out.append(f"      int wl[{U}];")
             out.append(f"      uint64_t m[{U}];")
@@ -915,6 +929,8 @@ class _Gen:
             out.append("      }")
             out.extend(self._words_tail(fcols, word_filter, mode, U, stage, body))
             out.append("    }")
+            if dense:
+                out.append("    }")
             if full:
                 out.append("    }")
         for g in range(G if narrow else 0):
