@@ -65,6 +65,7 @@ class JitLayout:
     pipe: bool = False
     regstage: bool = False
     shared: bool = False  # one accumulator copy per workgroup (LDS atomics shared by its 8 waves)
+    hll32: bool = False   # LDS HLL registers as u32 words (HLL32_LDS, when they fit the budget)
 
 
 def pipe_eligible(prog, mode: int, U: int) -> bool:
@@ -189,6 +190,52 @@ FULL_CHUNKS = os.environ.get("SDO_JIT_FULL", "1") != "0"
 # reading each word's mask by lane index (independent readlanes) and skipping all-empty steps;
 # sparser chunks take the find-first-set chain over their non-empty words only (0: always chain)
 DENSE_WORDS = int(os.environ.get("SDO_JIT_DENSE_WORDS", "48"))
+# LDS HLL registers as u32 words updated with one fire-and-forget ds_max_u32 per row (no register
+# read, no compare-and-swap loop) instead of packed byte registers (4x the LDS bytes; narrowed to
+# bytes in the block's final merge)
+HLL32_LDS = os.environ.get("SDO_JIT_HLL32LDS", "0") != "0"
+# LDS accumulator slots whose kernel-wide value provably fits 32 bits -- unfiltered or filtered
+# counts, min / max of integer columns inside int32 -- update the low dword of their 8-byte cell
+# with a 32-bit LDS atomic (ds_add_u32 / ds_max_i32: half the LDS bytes of ds_add_u64, no 64-bit
+# data registers); the block fold widens them
+NARROW_LDS = os.environ.get("SDO_JIT_NARROW_LDS", "0") != "0"
+
+
+def _col_range(c) -> Optional[Tuple[int, int]]:
+    """[lo, hi] of an integer column's stored values (None: float / unknown)."""
+    if c.flt:
+        return None
+    if c.pw:
+        return c.pbase, c.pbase + (1 << c.pw) - 1
+    bits = 8 << c.lg
+    return (-(1 << (bits - 1)), (1 << (bits - 1)) - 1) if c.sgn else (0, (1 << bits) - 1)
+
+
+def narrow_lds_slots(prog, mode: int, reg: bool, cols=None) -> Dict[int, str]:
+    """slot -> 'cnt' | 'max' | 'min' for the 32-bit LDS accumulator cells (see NARROW_LDS)."""
+    if not NARROW_LDS or mode != D.M_DENSE_LDS or reg:
+        return {}
+    cols = col_infos(prog) if cols is None else cols
+    out = {}
+    for s in range(prog.nslots):
+        users = [a for a in prog.aops if a.get("slot") == s and a["kind"] not in
+                 (D.A_HLL, D.A_HLL_CODE, D.A_HLL_STORED, D.A_ROWID)]
+        if not users:
+            continue
+        op = prog.slots[s][0]
+        if all(a["kind"] == D.A_COUNT for a in users) and op == D.S_SUM_I:
+            out[s] = "cnt"  # (a copy counts at most the rows of its wave: far below 2^32)
+            continue
+        if len(users) != 1 or op not in (D.S_MAX_I, D.S_MIN_I):
+            continue
+        a = users[0]
+        if a["kind"] not in (D.A_MAX_I, D.A_MIN_I) or a.get("expr") or a.get("col") not in cols:
+            continue
+        r = _col_range(cols[a["col"]])
+        # the untouched cell (INT32_MIN for max / INT32_MAX for min) must not be a real value
+        if r is not None and -(1 << 31) < r[0] and r[1] < (1 << 31) - 1:
+            out[s] = "max" if op == D.S_MAX_I else "min"
+    return out
 
 
 def ballot_slots(prog, mode: int, reg: bool, shared: bool) -> set:
@@ -213,6 +260,11 @@ def layout(prog, mode: int, U: int, hll_lds: bool, m: int, reg: bool = False, pi
     wave_bytes = (wave_bytes + 15) // 16 * 16
     hll_bytes = prog.nhll * prog.G * m if hll_lds else 0  # byte registers (hll_update8)
     stage = W * wave_bytes
+    hll32 = False
+    if HLL32_LDS and hll_bytes and mode == D.M_DENSE_LDS:
+        acc_min = prog.G * prog.nslots * 8 * (1 if shared else W * (1 if reg else 4))
+        if acc_min + 4 * hll_bytes + stage <= budget:  # u32 registers (ds_max_u32) when they fit
+            hll_bytes, hll32 = 4 * hll_bytes, True
     ncopy = 1
     acc_bytes = 0
     if mode == D.M_DENSE_LDS and shared:
@@ -231,7 +283,7 @@ def layout(prog, mode: int, U: int, hll_lds: bool, m: int, reg: bool = False, pi
     cache_off = (hll_off + hll_bytes + 15) // 16 * 16
     total = cache_off + stage
     return JitLayout(acc_off, acc_bytes, hll_off, hll_bytes, cache_off, wave_bytes, total, ncopy, pipe, regstage,
-                     shared and mode == D.M_DENSE_LDS)
+                     shared and mode == D.M_DENSE_LDS, hll32)
 
 
 def prefer_regstage(prog) -> bool:
@@ -286,6 +338,7 @@ class _Gen:
         self.m = m
         self.cols = col_infos(prog)
         self.NP = sum(2 if c.lg == 3 else 1 for c in self.cols.values() if not c.pw)
+        self.hw = 4 if lay.hll32 else 1  # LDS bytes per HLL register
         self.pre_lines: List[str] = []  # kernel-entry pointer / constant loads
         self._const_set = set()
 
@@ -619,6 +672,7 @@ class _Gen:
         NCT = 1 if lay.shared else W * lay.ncopy
         narrow = {s for s in range(NS) if _narrow_slot(p, s, self.cols)} if self.reg else set()
         bslots = ballot_slots(p, mode, self.reg, lay.shared)
+        nl = {s: k for s, k in narrow_lds_slots(p, mode, self.reg, self.cols).items() if s not in bslots}
         for i in sorted(self.cols):
             L.append(f"  const unsigned char* c{i} = (const unsigned char*)d->cols[{i}].ptr;")
         for j, (row, stride, count) in enumerate(p.bm_leaves):
@@ -636,7 +690,7 @@ class _Gen:
         for ai, a in enumerate(p.aops):
             if a["kind"] in D.HLL_KINDS:
                 if self.hll_lds and mode == D.M_DENSE_LDS:
-                    L.append(f"  unsigned char* hll{ai} = lds + {lay.hll_off + a['hll'] * G * self.m};")
+                    L.append(f"  unsigned char* hll{ai} = lds + {lay.hll_off + a['hll'] * G * self.m * self.hw};")
                 else:
                     L.append(f"  unsigned char* hll{ai} = (unsigned char*)d->aops[{ai}].hll_regs;")
             elif a["kind"] == D.A_HLL_STORED:
@@ -743,7 +797,7 @@ class _Gen:
             if kind == D.A_HLL_CODE:
                 # precomputed (bucket, rho) plane (segment/hllcode.py): no per-row hash
                 ix = f"((uint64_t)slot << {p.hll_p}) + ((uint32_t){val} >> 5)"
-                fn = "hll_max32((uint32_t*)" if wide else "hll_max8("
+                fn = "hll_max32((uint32_t*)" if wide else ("hll_lds_max32((uint32_t*)" if self.hw == 4 else "hll_max8(")
                 body.append(f"        if ({cond}) {fn}hll{ai}, {ix}, (uint32_t){val} & 31u);")
                 continue
             if kind == D.A_HLL:
@@ -751,7 +805,8 @@ class _Gen:
                     body.append(f"        if ({cond}) hll_update32((uint32_t*)hll{ai}, slot, {p.hll_p}, {val}, "
                                 f"{_lit(a.get('salt', 0))});")
                 else:
-                    body.append(f"        if ({cond}) hll_update8(hll{ai}, slot, {p.hll_p}, {val}, "
+                    fn = "hll_lds_update32((uint32_t*)" if self.hw == 4 else "hll_update8("
+                    body.append(f"        if ({cond}) {fn}hll{ai}, slot, {p.hll_p}, {val}, "
                                 f"{_lit(a.get('salt', 0))});")
                 continue
             if kind == D.A_HLL_STORED:
@@ -794,6 +849,11 @@ class _Gen:
                 else:
                     body.append(f"        if ({cond}) *({tgt}) = 1ull;")
                 continue
+            if s in nl:
+                fn = {"cnt": "lds_add_u32(", "max": "lds_max_i32(", "min": "lds_min_i32("}[nl[s]]
+                arg = "1u" if nl[s] == "cnt" else f"(int32_t){val}"
+                body.append(f"        if ({cond}) {fn}{tgt}, {arg});")
+                continue
             body.append(f"        if ({cond}) acc_update<{op}>({tgt}, {val});")
         body.append("      }")
         # ---------------- kernel text
@@ -833,7 +893,8 @@ class _Gen:
             out.append("  const uint64_t lmlt = (1ull << lane) - 1ull;")
         if mode == D.M_DENSE_LDS:
             out.append(f"  for (int i = threadIdx.x; i < {G * NS * NCT}; i += {W * 64}) {{")
-            inits = ", ".join(_lit(init) for _, init in p.slots)
+            cinit = {"cnt": 0, "max": -(1 << 31) & 0xffffffff, "min": (1 << 31) - 1}
+            inits = ", ".join(_lit(cinit[nl[s]]) if s in nl else _lit(init) for s, (_, init) in enumerate(p.slots))
             out.append(f"    constexpr int64_t init[{NS}] = {{{inits}}};")
             out.append(f"    acc[i] = (uint64_t)init[(i / {NCT}) % {NS}];")
             out.append("  }")
@@ -970,9 +1031,25 @@ class _Gen:
             out.append(f"    constexpr int ops[{NS}] = {{{ops}}};")
             out.append(f"    constexpr int64_t init[{NS}] = {{{inits}}};")
             out.append(f"    const uint64_t* a = acc + (int64_t)i * {NCT};")
-            out.append("    int64_t v = (int64_t)a[0];")
-            out.append(f"    for (int k = 1; k < {NCT}; ++k) {{")
-            out.append("      const int64_t x = (int64_t)a[k];")
+            if nl:
+                # 32-bit cells widen: counts zero-extend, min / max sign-extend (untouched -> init)
+                kinds = ", ".join(str({"cnt": 1, "max": 2, "min": 3}.get(nl.get(s2), 0)) for s2 in range(NS))
+                out.append(f"    constexpr int nk[{NS}] = {{{kinds}}};")
+                out.append("    auto wid = [&](uint64_t r) -> int64_t {")
+                out.append("      if (nk[s] == 0) return (int64_t)r;")
+                out.append("      if (nk[s] == 1) return (int64_t)(uint32_t)r;")
+                out.append("      const int32_t x = (int32_t)(uint32_t)r;")
+                out.append("      if (nk[s] == 2 && x == (-2147483647 - 1)) return init[s];")
+                out.append("      if (nk[s] == 3 && x == 2147483647) return init[s];")
+                out.append("      return (int64_t)x;")
+                out.append("    };")
+                out.append("    int64_t v = wid(a[0]);")
+                out.append(f"    for (int k = 1; k < {NCT}; ++k) {{")
+                out.append("      const int64_t x = wid(a[k]);")
+            else:
+                out.append("    int64_t v = (int64_t)a[0];")
+                out.append(f"    for (int k = 1; k < {NCT}; ++k) {{")
+                out.append("      const int64_t x = (int64_t)a[k];")
             out.append("      switch (ops[s]) {")
             out.append(f"        case {D.S_SUM_I}: v += x; break;")
             out.append(f"        case {D.S_SUM_F}: v = __double_as_longlong(__longlong_as_double(v) + __longlong_as_double(x)); break;")
@@ -989,7 +1066,12 @@ class _Gen:
                     # four byte registers per dword: one read (and rarely a CAS) per 4 registers
                     out.append(f"  {{ uint32_t* g = (uint32_t*)d->aops[{ai}].hll_regs;")
                     out.append(f"    const uint32_t* r = (const uint32_t*)hll{ai};")
-                    out.append(f"    for (int i = threadIdx.x; i < {G * self.m // 4}; i += {W * 64}) hll_merge_word8(g + i, r[i]);")
+                    if self.hw == 4:  # u32 registers -> four packed bytes per global dword
+                        out.append(f"    for (int i = threadIdx.x; i < {G * self.m // 4}; i += {W * 64}) "
+                                   "hll_merge_word8(g + i, pack_regs8(r + 4 * i));")
+                    else:
+                        out.append(f"    for (int i = threadIdx.x; i < {G * self.m // 4}; i += {W * 64}) "
+                                   "hll_merge_word8(g + i, r[i]);")
                     out.append("  }")
         out.append("}")
         return "\n".join(out) + "\n"

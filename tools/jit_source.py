@@ -5,6 +5,8 @@ only: the SQL is planned over a small synthetic shard, lowered and emitted, not 
 import os
 import sys
 
+import torch
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
@@ -51,7 +53,8 @@ def main():
                     for c in list(prog.fcols) + list(prog.pcols):
                         t = column_tensor(ds, c)
                         if not t.is_floating_point():
-                            lo, hi = int(t[:ds.num_rows].min()), int(t[:ds.num_rows].max())
+                            tt = t[:ds.num_rows].to(torch.int64) if t.dtype == torch.uint16 else t[:ds.num_rows]
+                            lo, hi = int(tt.min()), int(tt.max())
                             if PK.worth_packing(t, PK.width_for(lo, hi)):
                                 prog.packed[c] = PK.pack(t, ds.num_rows, lo, hi)
                 regstage = jit.prefer_regstage(prog)
