@@ -66,6 +66,7 @@ class JitLayout:
     regstage: bool = False
     shared: bool = False  # one accumulator copy per workgroup (LDS atomics shared by its 8 waves)
     hll32: bool = False   # LDS HLL registers as u32 words (HLL32_LDS, when they fit the budget)
+    blocked: bool = False  # row-blocked staging of full chunks (BLOCKED)
 
 
 def pipe_eligible(prog, mode: int, U: int) -> bool:
@@ -201,6 +202,50 @@ HLL32_LDS = os.environ.get("SDO_JIT_HLL32LDS", "0") != "0"
 NARROW_LDS = os.environ.get("SDO_JIT_NARROW_LDS", "0") != "0"
 
 
+# Row-blocked staging of whole chunks (the full-chunk branch of unfiltered scans): a 256-row block of
+# every column is copied into the wave's LDS with exactly-sized LDS-DMA loads (a bit-packed column's
+# 32 * width bytes, not one 4-byte lane fetch per row per load: the vector-memory return path, not
+# HBM, bounds the one-row-per-lane layout -- TPC-H Q1 issues ~10 dword loads per 64-row word), then
+# each lane reads ITS BR consecutive rows of each column back with one LDS read and extracts the
+# fields at compile-time bit offsets.
+BLOCKED = os.environ.get("SDO_JIT_BLOCKED", "0") != "0"
+# register double-buffering of whole chunks (register staging, no row filter): the loads of the next
+# U words are issued before the current U words are aggregated, so each wave keeps two groups of
+# loads in flight instead of paying one memory round trip per group (the scan is latency-bound:
+# ~384 dependent round trips per wave at SF100 / 768 workgroups)
+REG_PIPE = os.environ.get("SDO_JIT_REGPIPE", "0") != "0"
+# "2": two staging buffers per wave -- block b+1's copies are in flight while block b is aggregated
+# (one s_waitcnt vmcnt(<copies of one block>) instead of a drain); dense LDS tables only
+BLOCKED_PIPE = os.environ.get("SDO_JIT_BLOCKED", "0") == "2"
+BR = 4  # consecutive rows per lane (a block is 64 * BR = 256 rows)
+
+
+def blocked_eligible(prog, mode: int, regstage: bool = True) -> bool:
+    """Scans whose per-row work reads no word-granular state: no row filter (or a chunk-final
+    one), no per-aggregator filters, no row ids, bit-packed widths <= 32."""
+    if not BLOCKED or mode not in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL, D.M_HASH) or not regstage:
+        return False
+    if prog.filter_len and not prog.final_pre:
+        return False
+    if not prog.pcols or any(a.get("filt_len") or a["kind"] in (D.A_HLL_STORED, D.A_ROWID) for a in prog.aops):
+        return False
+    cols = col_infos(prog)
+    return all(c.pw <= 32 for i, c in cols.items() if i >= D.PAYLOAD_BASE)
+
+
+def _blk_dwords(c) -> int:
+    """LDS dwords of one column's 256-row block (plus the tail a lane's window read may touch)."""
+    if c.pw:
+        nd = (8 * c.pw) + ((31 + (BR - 1) * c.pw) // 32 + 2) + 1
+        return (nd + 63) // 64 * 64
+    return (64 * BR << c.lg) // 4
+
+
+def blocked_bytes(prog) -> int:
+    cols = col_infos(prog)
+    return sum(_blk_dwords(c) * 4 for i, c in cols.items() if i >= D.PAYLOAD_BASE)
+
+
 def _col_range(c) -> Optional[Tuple[int, int]]:
     """[lo, hi] of an integer column's stored values (None: float / unknown)."""
     if c.flt:
@@ -257,6 +302,9 @@ def layout(prog, mode: int, U: int, hll_lds: bool, m: int, reg: bool = False, pi
     nplanes = 0 if regstage else sum(2 if c.lg == 3 else 1 for c in cols.values() if not c.pw)
     need_bmw = _needs_word_bitmaps(prog)
     wave_bytes = U * nplanes * 256 * (2 if pipe else 1) + (len(prog.bm_leaves) * 512 if need_bmw else 0)
+    blocked = blocked_eligible(prog, mode, regstage) and not pipe
+    if blocked:  # the block staging area sits after the word staging planes / bitmap words
+        wave_bytes += blocked_bytes(prog) * (2 if BLOCKED_PIPE and mode == D.M_DENSE_LDS else 1)
     wave_bytes = (wave_bytes + 15) // 16 * 16
     hll_bytes = prog.nhll * prog.G * m if hll_lds else 0  # byte registers (hll_update8)
     stage = W * wave_bytes
@@ -283,7 +331,7 @@ def layout(prog, mode: int, U: int, hll_lds: bool, m: int, reg: bool = False, pi
     cache_off = (hll_off + hll_bytes + 15) // 16 * 16
     total = cache_off + stage
     return JitLayout(acc_off, acc_bytes, hll_off, hll_bytes, cache_off, wave_bytes, total, ncopy, pipe, regstage,
-                     shared and mode == D.M_DENSE_LDS, hll32)
+                     shared and mode == D.M_DENSE_LDS, hll32, blocked)
 
 
 def prefer_regstage(prog) -> bool:
@@ -339,12 +387,17 @@ class _Gen:
         self.cols = col_infos(prog)
         self.NP = sum(2 if c.lg == 3 else 1 for c in self.cols.values() if not c.pw)
         self.hw = 4 if lay.hll32 else 1  # LDS bytes per HLL register
+        self.blocked = False  # emitting the row-blocked body (ival / dval read bv<i>[u])
         self.pre_lines: List[str] = []  # kernel-entry pointer / constant loads
         self._const_set = set()
 
     # ---------------------------------------------------------------- values
     def ival(self, idx: int) -> str:
         c = self.cols[idx]
+        if self.blocked:  # raw field of row u of the lane's block (_blocked_loop)
+            if c.pw:
+                return f"((int64_t)bv{idx}[u] + {_lit(c.pbase)})"
+            return f"cv_int<{c.lg}, {'true' if c.sgn else 'false'}, {'true' if c.flt else 'false'}>(bv{idx}[u])"
         if c.pw:
             return f"(pk_field<{c.pw}>(xp{idx}[u], psh{c.pw}) + {_lit(c.pbase)})"
         if self.regstage:
@@ -354,6 +407,8 @@ class _Gen:
 
     def dval(self, idx: int) -> str:
         c = self.cols[idx]
+        if self.blocked and not c.pw:
+            return f"cv_dbl<{c.lg}, {'true' if c.sgn else 'false'}, {'true' if c.flt else 'false'}>(bv{idx}[u])"
         if c.pw:
             return f"((double){self.ival(idx)})"
         if self.regstage:
@@ -589,6 +644,138 @@ class _Gen:
         o.append("    }")
         return o
 
+    def _reg_piped_words(self, pcols, body: List[str]) -> List[str]:
+        """Full-chunk word loop with the payload loads of step k+1 issued before step k's updates
+        (REG_PIPE): next-step registers ``<x>n`` are copied into the step's ``<x>`` at its top (the
+        copy waits only for loads issued one step earlier)."""
+        U = self.U
+        o: List[str] = []
+        names = [(f"xp{i}", "uint64_t") if self.cols[i].pw else
+                 (f"x{i}", "uint64_t" if self.cols[i].lg == 3 else "uint32_t") for i in pcols]
+
+        def loads(wl: str, ind: str) -> None:
+            o.append(f"#pragma unroll\n{ind}for (int u = 0; u < {U}; ++u) {{")
+            for i in pcols:
+                c = self.cols[i]
+                x2 = "true" if PK_X2 else "false"
+                if c.pw:
+                    o.append(f"{ind}  xp{i}n[u] = ld_pk<{x2}>(rs{i}, (uint32_t)({wl}) * {8 * c.pw}u, pko{c.pw});")
+                else:
+                    o.append(f"{ind}  x{i}n[u] = ld_b<{c.lg}>(rs{i}, (uint32_t)({wl}) << {6 + c.lg}, lo{c.lg});")
+            o.append(f"{ind}}}")
+
+        for nm, t in names:
+            o.append(f"    {t} {nm}n[{U}];")
+        loads("u", "    ")
+        o.append(f"    for (int w0_ = 0; w0_ < {D.CHUNK_WORDS}; w0_ += {U}) {{")
+        o.append(f"      int wl[{U}];")
+        o.append(f"      uint64_t m[{U}];")
+        o.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{ wl[u] = w0_ + u; m[u] = ~0ull; }}")
+        for nm, t in names:
+            o.append(f"      {t} {nm}[{U}];")
+        o.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{ " +
+                 " ".join(f"{nm}[u] = {nm}n[u];" for nm, _ in names) + " }")
+        o.append(f"      if (w0_ + {U} < {D.CHUNK_WORDS}) {{")
+        loads(f"w0_ + {U} + u", "        ")
+        o.append("      }")
+        o.append(f"      bool act[{U}];")
+        o.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) act[u] = true;")
+        o.extend(body)
+        o.append("    }")
+        return o
+
+    # ---------------------------------------------------------------- row-blocked full chunks
+    def _blocked_loop(self, pcols, boff: int, bbody: List[str]) -> List[str]:
+        """The full-chunk loop of BLOCKED: per 256-row block, exactly-sized LDS-DMA copies of every
+        payload column into the wave's staging area, then lane l takes rows 4l..4l+3 of each
+        column with one LDS read per column and extracts them at compile-time offsets (a packed
+        width that is not a multiple of 8 selects its 64-bit window by the lane's bit phase)."""
+        o: List[str] = []
+        nblk = D.CHUNK_ROWS // (64 * BR)
+        pipe = BLOCKED_PIPE and self.mode == D.M_DENSE_LDS
+        bbytes = sum(_blk_dwords(self.cols[i]) * 4 for i in pcols)
+        offs = {}
+        off = 0
+        for i in pcols:
+            offs[i] = off
+            off += _blk_dwords(self.cols[i]) * 4
+
+        def issue(blk: str, dst: str, ind: str) -> int:
+            n = 0
+            for i in pcols:
+                c = self.cols[i]
+                if c.pw:
+                    nd = 8 * c.pw + ((31 + (BR - 1) * c.pw) // 32 + 3)  # dwords a lane window may touch
+                    for j in range((nd + 63) // 64):
+                        cond = f"lane < {nd - 64 * j}" if nd - 64 * j < 64 else None
+                        ld = (f"dma_b<2>(rs{i}, (uint32_t)({blk}) * {32 * c.pw}u + {256 * j}u, (uint32_t)lane << 2, "
+                              f"{dst} + {offs[i] + 256 * j});")
+                        o.append(f"{ind}if ({cond}) {ld}" if cond else f"{ind}{ld}")
+                        n += 1
+                else:
+                    for j in range(BR << c.lg >> 2):
+                        o.append(f"{ind}dma_b<2>(rs{i}, (uint32_t)({blk}) * {64 * BR << c.lg}u + {256 * j}u, "
+                                 f"(uint32_t)lane << 2, {dst} + {offs[i] + 256 * j});")
+                        n += 1
+            return n
+
+        if pipe:
+            o.append('    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
+            issue("0", f"(wb + {boff})", "    ")
+        o.append(f"    for (int b_ = 0; b_ < {nblk}; ++b_) {{")
+        if pipe:
+            o.append(f"      unsigned char* sbk = wb + {boff} + (b_ & 1) * {bbytes};")
+            o.append(f"      if (b_ + 1 < {nblk}) {{")
+            o.append('        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the other buffer are done')
+            n = issue("b_ + 1", f"(wb + {boff} + ((b_ + 1) & 1) * {bbytes})", "        ")
+            o.append(f'        asm volatile("s_waitcnt vmcnt({n})" ::: "memory");  // block b_ has landed')
+            o.append("      } else {")
+            o.append('        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
+            o.append("      }")
+        else:
+            o.append(f"      unsigned char* sbk = wb + {boff};")
+            o.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous block\'s reads are done')
+            issue("b_", "sbk", "      ")
+            o.append('      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
+        for i in pcols:
+            c = self.cols[i]
+            o.append(f"      uint64_t bv{i}[{BR}];")
+            if c.pw:
+                w = c.pw
+                nd = (31 + (BR - 1) * w) // 32 + 3
+                o.append(f"      {{ const uint32_t* q_ = (const uint32_t*)(sbk + {offs[i]}) + bda{w};")
+                o.append(f"        uint32_t dw_[{nd}];")
+                o.append(f"#pragma unroll\n        for (int k = 0; k < {nd}; ++k) dw_[k] = q_[k];")
+                mask = f"{(1 << w) - 1}ull"
+                for u in range(BR):
+                    a, sh = (u * w) >> 5, (u * w) & 31
+                    if w % 8 == 0:  # every lane starts dword-aligned: constant window and shift
+                        o.append(f"        bv{i}[{u}] = ((((uint64_t)dw_[{a + 1}] << 32) | dw_[{a}]) >> {sh}) & {mask};")
+                    else:
+                        o.append(f"        {{ const uint32_t p_ = bsh{w} + {u * w}u; const bool h_ = (p_ >> 5) != {a}u;")
+                        o.append(f"          const uint64_t w_ = h_ ? (((uint64_t)dw_[{a + 2}] << 32) | dw_[{a + 1}]) "
+                                 f": (((uint64_t)dw_[{a + 1}] << 32) | dw_[{a}]);")
+                        o.append(f"          bv{i}[{u}] = (w_ >> (p_ & 31u)) & {mask}; }}")
+                o.append("      }")
+            elif c.lg == 0:
+                o.append(f"      {{ const uint32_t x_ = ((const uint32_t*)(sbk + {offs[i]}))[lane];")
+                o.append(f"#pragma unroll\n        for (int u = 0; u < {BR}; ++u) bv{i}[u] = (x_ >> (8 * u)) & 0xffu; }}")
+            elif c.lg == 1:
+                o.append(f"      {{ const uint64_t x_ = ((const uint64_t*)(sbk + {offs[i]}))[lane];")
+                o.append(f"#pragma unroll\n        for (int u = 0; u < {BR}; ++u) bv{i}[u] = (x_ >> (16 * u)) & 0xffffu; }}")
+            elif c.lg == 2:
+                o.append(f"      {{ const uint4 x_ = ((const uint4*)(sbk + {offs[i]}))[lane];")
+                o.append(f"        bv{i}[0] = x_.x; bv{i}[1] = x_.y; bv{i}[2] = x_.z; bv{i}[3] = x_.w; }}")
+            else:
+                o.append(f"      {{ const uint4 x_ = ((const uint4*)(sbk + {offs[i]}))[2 * lane];")
+                o.append(f"        const uint4 y_ = ((const uint4*)(sbk + {offs[i]}))[2 * lane + 1];")
+                o.append(f"        bv{i}[0] = ((uint64_t)x_.y << 32) | x_.x; bv{i}[1] = ((uint64_t)x_.w << 32) | x_.z;")
+                o.append(f"        bv{i}[2] = ((uint64_t)y_.y << 32) | y_.x; bv{i}[3] = ((uint64_t)y_.w << 32) | y_.z; }}")
+        o.append(f"      const bool act[{BR}] = {{{', '.join(['true'] * BR)}}};")
+        o.extend(bbody)
+        o.append("    }")
+        return o
+
     # ---------------------------------------------------------------- whole kernel
     def _part_record(self, body: List[str]) -> None:
         """M_PART producer: the row becomes a partition record (ops/csrc/partition.hip) instead of a
@@ -709,153 +896,162 @@ class _Gen:
             self.stage_words(body, pcols, "wl", "wb")
             if not self.regstage:
                 body.append('      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
-        body = []
-        if self.pipe:
-            body.append(f"      bool act[{U}];")
-            body.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) act[u] = (m[u] >> lane) & 1ull;")
-        # phase 1: every staged read for the U words (keys + aggregator inputs) -- straight-line
-        # LDS reads the compiler can issue back to back; phase 2 applies the updates.
-        body.append(f"      uint64_t key_[{U}];")
-        vals: Dict[int, str] = {}
-        for ai, a in enumerate(p.aops):
-            body.append(f"      int64_t v{ai}_[{U}];")
-        body.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{")
-        body.append("        uint64_t key = 0;")
-        for k, kc in enumerate(p.keys):
-            v = self.ival(kc.col_idx)
-            # stride / base / card from the descriptor (query constants); for LDS tables the
-            # layout (G) is part of the shape anyway
-            ks = self.const(f"ks{k}", f"(uint64_t)d->kops[{k}].stride", "uint64_t", f"{int(kc.stride)}ull")
-            kb = self.const(f"kb{k}", f"d->kops[{k}].base", lit=_lit(kc.base))
-            kn = self.const(f"kn{k}", f"d->kops[{k}].card", lit=_lit(kc.card))
-            if kc.kind == D.K_ID and kc.base:  # shard-local key window (engine/executor.py ShardWindow)
-                body.append(f"        key += (uint64_t)((int64_t)({v}) - {kb}) * {ks};")
-            elif kc.kind == D.K_ID:
-                body.append(f"        key += (uint64_t)({v}) * {ks};")
-            elif kc.kind == D.K_REMAP:
-                body.append(f"        key += (uint64_t)rm{k}[{v}] * {ks};")
-            elif kc.kind == D.K_TIME and getattr(kc, "tlut", None) is not None:
-                n = len(kc.tlut)  # precomputed key per raw time value (engine/lower.py _attach_time_lut)
-                body.append(f"        {{ int64_t i_ = (int64_t)({v}) - {_lit(kc.tlut_lo)};")
-                body.append(f"          i_ = i_ < 0 ? 0 : (i_ >= {n} ? {n - 1} : i_);")
-                body.append(f"          key += (uint64_t)rm{k}[i_] * {ks}; }}")
-            elif kc.kind == D.K_TIME:
-                ktz = self.const(f"ktz{k}", f"d->kops[{k}].tz_ms", lit=_lit(kc.tz_ms))
-                kpm = self.const(f"kpm{k}", f"d->kops[{k}].period_ms", lit=_lit(kc.period_ms or 1))
-                kor = self.const(f"kor{k}", f"d->kops[{k}].origin_ms", lit=_lit(kc.origin_ms))
-                body.append(f"        {{ int64_t t = time_field_t<{kc.tfield}>(({v}) * {_lit(p.ds.time_unit_ms)} + "
-                            f"{ktz}, {kpm}, {kor}) - {kb};")
-                body.append(f"          t = t < 0 ? 0 : (t >= {kn} ? {kn} - 1 : t);")
-                body.append(f"          key += (uint64_t)t * {ks}; }}")
-            else:
-                body.append(f"        {{ int64_t t = ({v}) - {kb};")
-                body.append(f"          t = t < 0 ? 0 : (t >= {kn} ? {kn} - 1 : t);")
-                body.append(f"          key += (uint64_t)t * {ks}; }}")
-        body.append("        key_[u] = key;")
-        for ai, a in enumerate(p.aops):
-            kind = a["kind"]
-            if kind in D.HLL_KINDS:
-                val = self.ival(a["col"])
-            elif kind in (D.A_HLL_STORED, D.A_ROWID):
-                val = "((cw0 + wl[u]) * 64 + lane)"  # the row (a stored sketch's CSR run / emitted id)
-            elif kind == D.A_COUNT:
-                val = "1LL"
-            elif kind == D.A_SUM_X:
-                val = f"(int64_t)rint({self.expr(a['expr'], a.get('expr_off', 0))})"
-            elif kind in (D.A_SUM_F, D.A_MIN_F, D.A_MAX_F):
-                dv = self.expr(a["expr"], a.get("expr_off", 0)) if a.get("expr") else self.dval(a["col"])
-                val = f"__double_as_longlong({dv})" if kind == D.A_SUM_F else f"f2ord({dv})"
-            else:
-                val = self.ival(a["col"])
-            body.append(f"        v{ai}_[u] = {val};")
-        body.append("      }")
-        body.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{")
-        body.append("        const uint64_t key = key_[u];")
-        if mode == D.M_PART:
-            self._part_record(body)
-        elif mode == D.M_HASH:
-            body.append("        int64_t slot = act[u] ? hash_slot(hkeys, hcap, key, overflow) : -1;")
-            body.append("        const bool mine = act[u] && slot >= 0;")
-        else:
-            body.append("        const int64_t slot = (int64_t)key;")
-            body.append("        const bool mine = act[u];")
-            if mode == D.M_DENSE_GLOBAL and getattr(p, "touch_table", False):
-                # first-touch byte table (engine/device_exec.py): every group a qualifying row
-                # reaches is marked with a plain byte store (same-value races are benign); the
-                # touched groups compact from this table instead of the accumulator table, and only
-                # they are re-initialised after the run (no full-table fill per execution)
-                body.append("        if (mine) ((unsigned char*)d->out_mask)[slot] = (unsigned char)1;")
-        for ai, a in enumerate(p.aops if mode != D.M_PART else []):
-            cond = "mine"
-            if a.get("filt_len"):
-                fx = self.word_expr(a["filt_off"], a["filt_off"] + a["filt_len"])
-                body.append(f"        const bool f{ai} = mine && ((({fx}) >> lane) & 1ull);")
-                cond = f"f{ai}"
-            kind = a["kind"]
-            val = f"v{ai}_[u]"
-            wide = getattr(p, "hll32", False) and not (self.hll_lds and mode == D.M_DENSE_LDS)
-            if kind == D.A_HLL_CODE:
-                # precomputed (bucket, rho) plane (segment/hllcode.py): no per-row hash
-                ix = f"((uint64_t)slot << {p.hll_p}) + ((uint32_t){val} >> 5)"
-                fn = "hll_max32((uint32_t*)" if wide else ("hll_lds_max32((uint32_t*)" if self.hw == 4 else "hll_max8(")
-                body.append(f"        if ({cond}) {fn}hll{ai}, {ix}, (uint32_t){val} & 31u);")
-                continue
-            if kind == D.A_HLL:
-                if wide:  # global u32 registers (engine/device_exec.py narrows them after the scan)
-                    body.append(f"        if ({cond}) hll_update32((uint32_t*)hll{ai}, slot, {p.hll_p}, {val}, "
-                                f"{_lit(a.get('salt', 0))});")
+        def _mk_body(U: int) -> List[str]:
+            body = []
+            if self.pipe:
+                body.append(f"      bool act[{U}];")
+                body.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) act[u] = (m[u] >> lane) & 1ull;")
+            # phase 1: every staged read for the U words (keys + aggregator inputs) -- straight-line
+            # LDS reads the compiler can issue back to back; phase 2 applies the updates.
+            body.append(f"      uint64_t key_[{U}];")
+            vals: Dict[int, str] = {}
+            for ai, a in enumerate(p.aops):
+                body.append(f"      int64_t v{ai}_[{U}];")
+            body.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{")
+            body.append("        uint64_t key = 0;")
+            for k, kc in enumerate(p.keys):
+                v = self.ival(kc.col_idx)
+                # stride / base / card from the descriptor (query constants); for LDS tables the
+                # layout (G) is part of the shape anyway
+                ks = self.const(f"ks{k}", f"(uint64_t)d->kops[{k}].stride", "uint64_t", f"{int(kc.stride)}ull")
+                kb = self.const(f"kb{k}", f"d->kops[{k}].base", lit=_lit(kc.base))
+                kn = self.const(f"kn{k}", f"d->kops[{k}].card", lit=_lit(kc.card))
+                if kc.kind == D.K_ID and kc.base:  # shard-local key window (engine/executor.py ShardWindow)
+                    body.append(f"        key += (uint64_t)((int64_t)({v}) - {kb}) * {ks};")
+                elif kc.kind == D.K_ID:
+                    body.append(f"        key += (uint64_t)({v}) * {ks};")
+                elif kc.kind == D.K_REMAP:
+                    body.append(f"        key += (uint64_t)rm{k}[{v}] * {ks};")
+                elif kc.kind == D.K_TIME and getattr(kc, "tlut", None) is not None:
+                    n = len(kc.tlut)  # precomputed key per raw time value (engine/lower.py _attach_time_lut)
+                    body.append(f"        {{ int64_t i_ = (int64_t)({v}) - {_lit(kc.tlut_lo)};")
+                    body.append(f"          i_ = i_ < 0 ? 0 : (i_ >= {n} ? {n - 1} : i_);")
+                    body.append(f"          key += (uint64_t)rm{k}[i_] * {ks}; }}")
+                elif kc.kind == D.K_TIME:
+                    ktz = self.const(f"ktz{k}", f"d->kops[{k}].tz_ms", lit=_lit(kc.tz_ms))
+                    kpm = self.const(f"kpm{k}", f"d->kops[{k}].period_ms", lit=_lit(kc.period_ms or 1))
+                    kor = self.const(f"kor{k}", f"d->kops[{k}].origin_ms", lit=_lit(kc.origin_ms))
+                    body.append(f"        {{ int64_t t = time_field_t<{kc.tfield}>(({v}) * {_lit(p.ds.time_unit_ms)} + "
+                                f"{ktz}, {kpm}, {kor}) - {kb};")
+                    body.append(f"          t = t < 0 ? 0 : (t >= {kn} ? {kn} - 1 : t);")
+                    body.append(f"          key += (uint64_t)t * {ks}; }}")
                 else:
-                    fn = "hll_lds_update32((uint32_t*)" if self.hw == 4 else "hll_update8("
-                    body.append(f"        if ({cond}) {fn}hll{ai}, slot, {p.hll_p}, {val}, "
-                                f"{_lit(a.get('salt', 0))});")
-                continue
-            if kind == D.A_HLL_STORED:
-                fn = "hll_merge_csr32((uint32_t*)" if getattr(p, "hll32", False) else "hll_merge_csr("
-                body.append(f"        if ({cond}) {fn}hll{ai}, slot, {p.hll_p}, sko{ai}, skv{ai}, {val});")
-                continue
-            s = a["slot"]
-            op = p.slots[s][0]
-            if s in bslots:
-                for g in range(G):
-                    body.append(f"        bc{g}_{s} += (uint64_t)__builtin_popcountll(__ballot({cond} && key == {g}ull));")
-                continue
-            if self.reg:
-                body.append(f"        {{ const int64_t v_ = {val}; const int kk_ = (int)key;")
-                for g in range(G):
-                    r = f"r{g}_{s}"
-                    pg = f"({cond} && kk_ == {g})"
-                    if s in narrow:
-                        body.append(f"          n{g}_{s} += {pg} ? (int32_t)v_ : 0;")
-                    elif op == D.S_SUM_I:
-                        body.append(f"          {r} += {pg} ? v_ : 0LL;")
-                    elif op == D.S_SUM_F:
-                        body.append(f"          {r} += {pg} ? __longlong_as_double(v_) : 0.0;")
-                    elif op == D.S_MIN_I:
-                        body.append(f"          {r} = ({pg} && v_ < {r}) ? v_ : {r};")
+                    body.append(f"        {{ int64_t t = ({v}) - {kb};")
+                    body.append(f"          t = t < 0 ? 0 : (t >= {kn} ? {kn} - 1 : t);")
+                    body.append(f"          key += (uint64_t)t * {ks}; }}")
+            body.append("        key_[u] = key;")
+            for ai, a in enumerate(p.aops):
+                kind = a["kind"]
+                if kind in D.HLL_KINDS:
+                    val = self.ival(a["col"])
+                elif kind in (D.A_HLL_STORED, D.A_ROWID):
+                    val = "((cw0 + wl[u]) * 64 + lane)"  # the row (a stored sketch's CSR run / emitted id)
+                elif kind == D.A_COUNT:
+                    val = "1LL"
+                elif kind == D.A_SUM_X:
+                    val = f"(int64_t)rint({self.expr(a['expr'], a.get('expr_off', 0))})"
+                elif kind in (D.A_SUM_F, D.A_MIN_F, D.A_MAX_F):
+                    dv = self.expr(a["expr"], a.get("expr_off", 0)) if a.get("expr") else self.dval(a["col"])
+                    val = f"__double_as_longlong({dv})" if kind == D.A_SUM_F else f"f2ord({dv})"
+                else:
+                    val = self.ival(a["col"])
+                body.append(f"        v{ai}_[u] = {val};")
+            body.append("      }")
+            body.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{")
+            body.append("        const uint64_t key = key_[u];")
+            if mode == D.M_PART:
+                self._part_record(body)
+            elif mode == D.M_HASH:
+                body.append("        int64_t slot = act[u] ? hash_slot(hkeys, hcap, key, overflow) : -1;")
+                body.append("        const bool mine = act[u] && slot >= 0;")
+            else:
+                body.append("        const int64_t slot = (int64_t)key;")
+                body.append("        const bool mine = act[u];")
+                if mode == D.M_DENSE_GLOBAL and getattr(p, "touch_table", False):
+                    # first-touch byte table (engine/device_exec.py): every group a qualifying row
+                    # reaches is marked with a plain byte store (same-value races are benign); the
+                    # touched groups compact from this table instead of the accumulator table, and only
+                    # they are re-initialised after the run (no full-table fill per execution)
+                    body.append("        if (mine) ((unsigned char*)d->out_mask)[slot] = (unsigned char)1;")
+            for ai, a in enumerate(p.aops if mode != D.M_PART else []):
+                cond = "mine"
+                if a.get("filt_len"):
+                    fx = self.word_expr(a["filt_off"], a["filt_off"] + a["filt_len"])
+                    body.append(f"        const bool f{ai} = mine && ((({fx}) >> lane) & 1ull);")
+                    cond = f"f{ai}"
+                kind = a["kind"]
+                val = f"v{ai}_[u]"
+                wide = getattr(p, "hll32", False) and not (self.hll_lds and mode == D.M_DENSE_LDS)
+                if kind == D.A_HLL_CODE:
+                    # precomputed (bucket, rho) plane (segment/hllcode.py): no per-row hash
+                    ix = f"((uint64_t)slot << {p.hll_p}) + ((uint32_t){val} >> 5)"
+                    fn = "hll_max32((uint32_t*)" if wide else ("hll_lds_max32((uint32_t*)" if self.hw == 4 else "hll_max8(")
+                    body.append(f"        if ({cond}) {fn}hll{ai}, {ix}, (uint32_t){val} & 31u);")
+                    continue
+                if kind == D.A_HLL:
+                    if wide:  # global u32 registers (engine/device_exec.py narrows them after the scan)
+                        body.append(f"        if ({cond}) hll_update32((uint32_t*)hll{ai}, slot, {p.hll_p}, {val}, "
+                                    f"{_lit(a.get('salt', 0))});")
                     else:
-                        body.append(f"          {r} = ({pg} && v_ > {r}) ? v_ : {r};")
-                body.append("        }")
-                continue
-            if mode == D.M_DENSE_LDS:
-                tgt = f"acc + (slot * {NS} + {s}) * {NCT} + copy"
-            else:
-                tgt = f"gacc + slot * {NS} + {s}"
-            if getattr(p, "presence_only", False) and mode == D.M_DENSE_GLOBAL and kind == D.A_COUNT and NS == 1:
-                # existence only (nested inner level, SELECT DISTINCT): a plain vector store of 1
-                # instead of an HBM read-modify-write atomic per row (same-value races are benign);
-                # with presence_bytes the table is one byte per group
-                if getattr(p, "presence_bytes", False):
-                    body.append(f"        if ({cond}) ((unsigned char*)gacc)[slot] = (unsigned char)1;")
+                        fn = "hll_lds_update32((uint32_t*)" if self.hw == 4 else "hll_update8("
+                        body.append(f"        if ({cond}) {fn}hll{ai}, slot, {p.hll_p}, {val}, "
+                                    f"{_lit(a.get('salt', 0))});")
+                    continue
+                if kind == D.A_HLL_STORED:
+                    fn = "hll_merge_csr32((uint32_t*)" if getattr(p, "hll32", False) else "hll_merge_csr("
+                    body.append(f"        if ({cond}) {fn}hll{ai}, slot, {p.hll_p}, sko{ai}, skv{ai}, {val});")
+                    continue
+                s = a["slot"]
+                op = p.slots[s][0]
+                if s in bslots:
+                    for g in range(G):
+                        body.append(f"        bc{g}_{s} += (uint64_t)__builtin_popcountll(__ballot({cond} && key == {g}ull));")
+                    continue
+                if self.reg:
+                    body.append(f"        {{ const int64_t v_ = {val}; const int kk_ = (int)key;")
+                    for g in range(G):
+                        r = f"r{g}_{s}"
+                        pg = f"({cond} && kk_ == {g})"
+                        if s in narrow:
+                            body.append(f"          n{g}_{s} += {pg} ? (int32_t)v_ : 0;")
+                        elif op == D.S_SUM_I:
+                            body.append(f"          {r} += {pg} ? v_ : 0LL;")
+                        elif op == D.S_SUM_F:
+                            body.append(f"          {r} += {pg} ? __longlong_as_double(v_) : 0.0;")
+                        elif op == D.S_MIN_I:
+                            body.append(f"          {r} = ({pg} && v_ < {r}) ? v_ : {r};")
+                        else:
+                            body.append(f"          {r} = ({pg} && v_ > {r}) ? v_ : {r};")
+                    body.append("        }")
+                    continue
+                if mode == D.M_DENSE_LDS:
+                    tgt = f"acc + (slot * {NS} + {s}) * {NCT} + copy"
                 else:
-                    body.append(f"        if ({cond}) *({tgt}) = 1ull;")
-                continue
-            if s in nl:
-                fn = {"cnt": "lds_add_u32(", "max": "lds_max_i32(", "min": "lds_min_i32("}[nl[s]]
-                arg = "1u" if nl[s] == "cnt" else f"(int32_t){val}"
-                body.append(f"        if ({cond}) {fn}{tgt}, {arg});")
-                continue
-            body.append(f"        if ({cond}) acc_update<{op}>({tgt}, {val});")
-        body.append("      }")
+                    tgt = f"gacc + slot * {NS} + {s}"
+                if getattr(p, "presence_only", False) and mode == D.M_DENSE_GLOBAL and kind == D.A_COUNT and NS == 1:
+                    # existence only (nested inner level, SELECT DISTINCT): a plain vector store of 1
+                    # instead of an HBM read-modify-write atomic per row (same-value races are benign);
+                    # with presence_bytes the table is one byte per group
+                    if getattr(p, "presence_bytes", False):
+                        body.append(f"        if ({cond}) ((unsigned char*)gacc)[slot] = (unsigned char)1;")
+                    else:
+                        body.append(f"        if ({cond}) *({tgt}) = 1ull;")
+                    continue
+                if s in nl:
+                    fn = {"cnt": "lds_add_u32(", "max": "lds_max_i32(", "min": "lds_min_i32("}[nl[s]]
+                    arg = "1u" if nl[s] == "cnt" else f"(int32_t){val}"
+                    body.append(f"        if ({cond}) {fn}{tgt}, {arg});")
+                    continue
+                body.append(f"        if ({cond}) acc_update<{op}>({tgt}, {val});")
+            body.append("      }")
+            return body
+
+        body = _mk_body(U)
+        blk = lay.blocked and not pre
+        if blk:  # the same updates over a lane's BR consecutive rows of a block (see BLOCKED)
+            self.blocked = True
+            bbody = _mk_body(BR)
+            self.blocked = False
         # ---------------- kernel text
         out = []
         out.append('#include "sdo_device.h"')
@@ -872,6 +1068,10 @@ class _Gen:
             # dword holding its first bit
             out.append(f"  const uint32_t pko{w} = (((uint32_t)lane * {w}u) >> 5) * 4u;")
             out.append(f"  const uint32_t psh{w} = ((uint32_t)lane * {w}u) & 31u;")
+        if blk:  # a lane's first dword / bit of its BR consecutive rows in a packed block
+            for w in sorted({c.pw for i, c in self.cols.items() if c.pw and i >= D.PAYLOAD_BASE}):
+                out.append(f"  const uint32_t bda{w} = ((uint32_t)lane * {BR * w}u) >> 5;")
+                out.append(f"  const uint32_t bsh{w} = ((uint32_t)lane * {BR * w}u) & 31u;")
         out.append(f"  unsigned char* wb = lds + {lay.cache_off} + wave * {lay.wave_bytes};")
         stage_bytes = 0 if self.regstage else U * NP * 256 * (2 if self.pipe else 1)
         out.append(f"  uint64_t* bmw = (uint64_t*)(wb + {stage_bytes});")
@@ -964,12 +1164,18 @@ class _Gen:
             full = FULL_CHUNKS and not pre and mode in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL, D.M_HASH)
             if full:
                 out.append(f"    if (clo == crow0 && chi == crow0 + {D.CHUNK_ROWS}) {{")
-                out.append(f"    for (int w0_ = 0; w0_ < {D.CHUNK_WORDS}; w0_ += {U}) {{")
-                out.append(f"      int wl[{U}];")
-                out.append(f"      uint64_t m[{U}];")
-                out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{ wl[u] = w0_ + u; m[u] = ~0ull; }}")
-                out.extend(self._words_tail(fcols, word_filter, mode, U, stage, body))
-                out.append("    }")
+                if blk:
+                    boff = stage_bytes + (len(p.bm_leaves) * 512 if need_bmw else 0)
+                    out.extend(self._blocked_loop(pcols, boff, bbody))
+                elif REG_PIPE and self.regstage and (p.final_pre or not p.filter_len) and pcols:
+                    out.extend(self._reg_piped_words(pcols, body))
+                else:
+                    out.append(f"    for (int w0_ = 0; w0_ < {D.CHUNK_WORDS}; w0_ += {U}) {{")
+                    out.append(f"      int wl[{U}];")
+                    out.append(f"      uint64_t m[{U}];")
+                    out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{ wl[u] = w0_ + u; m[u] = ~0ull; }}")
+                    out.extend(self._words_tail(fcols, word_filter, mode, U, stage, body))
+                    out.append("    }")
                 out.append("    } else {")
             dense = DENSE_WORDS > 0 and bool(pre) and mode in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL, D.M_HASH)
             if dense:
@@ -1077,11 +1283,28 @@ class _Gen:
         return "\n".join(out) + "\n"
 
 
+_HDR_HASH: List[str] = []
+
+
+def _hdr_hash() -> str:
+    """Hash of the device headers the kernels include: a header change invalidates cached code."""
+    if not _HDR_HASH:
+        h = hashlib.sha256()
+        for f in sorted(CSRC.glob("*.h")):
+            h.update(f.read_bytes())
+        _HDR_HASH.append(h.hexdigest())
+    return _HDR_HASH[0]
+
+
+def _code_key(src: str) -> str:
+    return hashlib.sha256((src + "\0".join(OPTS) + _hdr_hash()).encode()).hexdigest()[:24]
+
+
 def compile_code(src: str, name: str) -> bytes:
-    """hipRTC-compile for gfx950 (no GPU needed), disk-cached by source hash."""
+    """hipRTC-compile for gfx950 (no GPU needed), disk-cached by source + header hash."""
     from . import native
 
-    key = hashlib.sha256((src + "\0".join(OPTS)).encode()).hexdigest()[:24]
+    key = _code_key(src)
     path = cache_dir() / f"{key}.co"
     if path.exists():
         return path.read_bytes()
@@ -1096,7 +1319,7 @@ def compile_source(src: str, name: str) -> int:
     """Compile (cached) and load into the current HIP context; returns a launch handle."""
     from . import native
 
-    key = hashlib.sha256((src + "\0".join(OPTS)).encode()).hexdigest()[:24]
+    key = _code_key(src)
     with _lock:
         if key in _handles:
             return _handles[key]
