@@ -288,7 +288,11 @@ class PreparedQuery:
         qt = self.qs.queryType
         if qt in ("groupBy", "timeseries", "topN"):
             root_only = self.world.distributed and root_only_results()
-            prog, part, t1 = self.run_partials(t0, root_only)
+            fast = self._graph_run()
+            if fast is not None:
+                prog, part, t1 = fast
+            else:
+                prog, part, t1 = self.run_partials(t0, root_only)
             t2 = time.perf_counter()
             with T.span("sdo.finalize"):
                 if root_only and self.world.rank != 0:
@@ -310,6 +314,29 @@ class PreparedQuery:
         res.stats["exec_ms"] = (time.perf_counter() - t0) * 1e3
         self.last_stats = res.stats
         return res
+
+    def _graph_run(self):
+        """One GPU, one scan, a small dense state that merge / HAVING / top-K pruning pass through
+        unchanged (<= 4096 groups): the execution is one replayed HIP graph of reset + scan + HLL
+        estimates + D2H (engine/device_exec.py run_graph_small).  (prog, partials with their host
+        copy, scan end time) or None for the ordinary path."""
+        if self.world.distributed or len(self.scans) != 1 or self.window is not None:
+            return None
+        _, prog, prep = self.scans[0]
+        if prep is None or not hasattr(prep, "run_graph_small") or prog.G > 4096 or prog.nslots > 256:
+            return None
+        if (prog.stored_hll and not getattr(prep, "stored_fused", False)) or self._dict_exist_plan(prog) is not None:
+            return None
+        from ..parallel.fault import FAULTS
+        from ..utils.cancel import checkpoint
+
+        with T.span("sdo.scan"):
+            checkpoint()
+            FAULTS.maybe_fail("scan", self.world.rank)
+            part = prep.run_graph_small(not any(kc.collapse for kc in prog.keys))
+        if part is None:
+            return None
+        return prog, part, time.perf_counter()
 
     def run_partials(self, t0: float, root_only: bool = False):
         """scan -> merge across ranks -> device HAVING / top-K pruning; (prog, merged partials,

@@ -354,6 +354,75 @@ static void fetch_small(uint64_t acc, int64_t acc_bytes, std::vector<uint64_t> h
   }
 }
 
+// HIP graph of one small dense execution: the fused buffer reset, the scan kernel, the HLL estimates
+// and both D2H copies into a pinned host buffer, captured once per prepared-scan slot and replayed
+// with ONE hipGraphLaunch (no per-launch host work, no gaps between the dependent launches).  The
+// capture runs on a private non-blocking stream (the legacy default stream cannot be captured); the
+// replay is ordered on the caller's stream and waited for with the GIL released.
+struct SmallGraph {
+  hipGraphExec_t exec;
+  bool live;
+};
+static std::vector<SmallGraph> g_graphs;
+static std::mutex g_graph_mu;
+
+static int graph_small_capture(uint64_t acc, uint64_t init, int64_t rows, int nslots, std::vector<uint64_t> zptr,
+                               std::vector<int64_t> zwords, uint64_t overflow, int jit, uint64_t desc, int grid,
+                               int block, int lds, int unroll, std::vector<uint64_t> hll, int64_t G, int p,
+                               uint64_t est_dev, uint64_t host, int64_t acc_bytes, uint64_t acc_src) {
+  hipStream_t cs;
+  check(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "graph capture stream");
+  hipGraph_t g = nullptr;
+  try {
+    check(hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
+    try {
+      run_scan(acc, init, rows, nslots, zptr, zwords, overflow, jit, desc, grid, block, lds, unroll, (uint64_t)cs);
+      for (size_t i = 0; i < hll.size(); ++i) hll_estimate(hll[i], G, p, est_dev + i * (uint64_t)G * 8, (uint64_t)cs);
+      if (acc_bytes > 0)
+        check(hipMemcpyAsync((void*)host, (const void*)acc_src, acc_bytes, hipMemcpyDeviceToHost, cs), "graph acc copy");
+      if (!hll.empty())
+        check(hipMemcpyAsync((void*)(host + acc_bytes), (const void*)est_dev, hll.size() * G * 8,
+                             hipMemcpyDeviceToHost, cs),
+              "graph est copy");
+    } catch (...) {
+      hipGraph_t dead = nullptr;
+      (void)hipStreamEndCapture(cs, &dead);
+      if (dead) (void)hipGraphDestroy(dead);
+      throw;
+    }
+    check(hipStreamEndCapture(cs, &g), "hipStreamEndCapture");
+    hipGraphExec_t ex;
+    check(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0), "hipGraphInstantiate");
+    (void)hipGraphDestroy(g);
+    (void)hipStreamDestroy(cs);
+    std::lock_guard<std::mutex> lk(g_graph_mu);
+    g_graphs.push_back({ex, true});
+    return (int)g_graphs.size() - 1;
+  } catch (...) {
+    (void)hipStreamDestroy(cs);
+    throw;
+  }
+}
+
+static void graph_launch(int h, uint64_t stream) {
+  hipGraphExec_t ex;
+  {
+    std::lock_guard<std::mutex> lk(g_graph_mu);
+    if (h < 0 || h >= (int)g_graphs.size() || !g_graphs[h].live) throw std::invalid_argument("bad graph handle");
+    ex = g_graphs[h].exec;
+  }
+  py::gil_scoped_release nogil;
+  check(hipGraphLaunch(ex, (hipStream_t)stream), "hipGraphLaunch");
+  check(hipStreamSynchronize((hipStream_t)stream), "graph sync");
+}
+
+static void graph_destroy(int h) {
+  std::lock_guard<std::mutex> lk(g_graph_mu);
+  if (h < 0 || h >= (int)g_graphs.size() || !g_graphs[h].live) return;
+  (void)hipGraphExecDestroy(g_graphs[h].exec);
+  g_graphs[h].live = false;
+}
+
 static void stream_sync(uint64_t stream) {
   py::gil_scoped_release nogil;
   check(hipStreamSynchronize((hipStream_t)stream), "stream sync");
@@ -527,6 +596,9 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("run_scan", &run_scan);
   m.def("fetch_small", &fetch_small);
   m.def("stream_sync", &stream_sync);
+  m.def("graph_small_capture", &graph_small_capture);
+  m.def("graph_launch", &graph_launch);
+  m.def("graph_destroy", &graph_destroy);
   m.def("glds_probe", &glds_probe);
   m.def("part_scan", &part_scan);
   m.def("part_keys", &part_keys);

@@ -298,5 +298,28 @@ def fetch_small(acc: torch.Tensor, hll: Sequence[torch.Tensor], G: int, p: int, 
                        host.data_ptr(), _stream(acc.device))
 
 
+def graph_small_capture(run_args, hll: Sequence[torch.Tensor], G: int, p: int, est_dev: torch.Tensor,
+                        host: torch.Tensor, acc: torch.Tensor) -> int:
+    """Capture reset + scan (``run_args`` as for run_scan, minus the stream) + HLL estimates + the
+    D2H of ``acc`` and the estimates into pinned ``host`` as one HIP graph (bindings.cpp)."""
+    assert acc.is_contiguous() and host.is_pinned()
+    nb = acc.numel() * acc.element_size()
+    assert host.numel() * host.element_size() >= nb + len(hll) * G * 8
+    assert est_dev.numel() * est_dev.element_size() >= len(hll) * G * 8
+    for h in hll:
+        assert h.dtype == torch.uint8 and h.is_contiguous() and h.numel() >= G * (1 << p)
+    return int(load().graph_small_capture(*run_args, [h.data_ptr() for h in hll], int(G), int(p), est_dev.data_ptr(),
+                                          host.data_ptr(), nb, acc.data_ptr()))
+
+
+def graph_launch(h: int, dev) -> None:
+    """Replay a captured graph on the caller's stream and wait for it (GIL released)."""
+    load().graph_launch(int(h), _stream(dev))
+
+
+def graph_destroy(h: int) -> None:
+    load().graph_destroy(int(h))
+
+
 def stream_sync(dev) -> None:
     load().stream_sync(_stream(dev))

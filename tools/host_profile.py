@@ -38,8 +38,9 @@ def main():
         qs = [(n, s.sql(q)) for n, q in tpch.BENCH_QUERIES]
     else:
         qs = [(n, eng.prepare(q, ds)) for n, q in bench_specs()]
-    if a.query:
-        qs = [(n, q) for n, q in qs if a.query.lower() in n.lower()]
+    if a.query:  # comma-separated name substrings
+        want = [w.strip().lower() for w in a.query.split(",")]
+        qs = [(n, q) for n, q in qs if any(w in n.lower() for w in want)]
     for _ in range(2):
         for n, q in qs:
             q.run()
@@ -73,7 +74,7 @@ def main():
     pr.disable()
     st = pstats.Stats(pr)
     st.sort_stats("cumulative").print_stats(a.top)
-    st.sort_stats("tottime").print_stats(25)
+    st.sort_stats("tottime").print_stats(40)
 
 
 if __name__ == "__main__":
