@@ -25,6 +25,7 @@ from ..ops import desc as D
 from ..ops import native
 from .lower import ScanProgram, pack
 from .partials import Partials
+from .scheduler import current_slot
 
 from ..planner.cost import PLAN_LDS_BUDGET as LDS_BUDGET  # noqa: E402  (single source: the cost model)
 # one accumulator table per workgroup (JIT only) for key spaces whose per-wave copies do not fit:
@@ -234,8 +235,6 @@ class PreparedScan:
     # registers / descriptor, so concurrent runs of one prepared query on different streams never
     # share device state; the generated kernel, grid and mode are shared.
     def _bufs(self) -> "_Bufs":
-        from .scheduler import current_slot
-
         slot = current_slot()
         b = self._slots.get(slot)
         if b is None:
@@ -352,8 +351,6 @@ class PreparedScan:
         """producer (records into chunk regions) -> level-1 split (count, offsets, tile-sorted
         scatter) -> [level-2 split] -> LDS aggregation into the dense table (every row written: no
         reset), or, with a fused HAVING, straight to the surviving groups (sparse)."""
-        from .scheduler import current_slot
-
         L, nat, st = self.part, native.load(), native._stream(self.dev)
         pb = dict(b.part)
         prog = self.prog
@@ -477,8 +474,6 @@ class PreparedScan:
 
     # ------------------------------------------------------------------ run
     def run(self) -> Partials:
-        from .scheduler import current_slot
-
         self._maybe_specialize()
         prog = self.prog
         b = self._bufs()
@@ -787,8 +782,6 @@ class PreparedMask:
         self._bufs()
 
     def _bufs(self):
-        from .scheduler import current_slot
-
         slot = current_slot()
         b = self._slots.get(slot)
         if b is None:

@@ -29,6 +29,20 @@ from ..segment.datasource import DataSource
 from .columns import DictColumn, materialize, take
 from .lower import Lowerer, LoweringError, ScanProgram
 from .partials import Partials, finalize
+from ..parallel.fault import FAULTS
+from ..utils.cancel import checkpoint
+
+
+_DE: list = []
+
+
+def _graphs_on() -> bool:
+    """device_exec.USE_GRAPHS (the module is imported lazily: it pulls in the native extension)."""
+    if not _DE:
+        from . import device_exec as DE_
+
+        _DE.append(DE_)
+    return _DE[0].USE_GRAPHS
 
 # segment-batched execution overlaps batch j's merge collectives with batch j+1's scan
 PIPELINE_MERGE = os.environ.get("SDO_PIPELINE_MERGE", "1") not in ("0", "")
@@ -194,8 +208,6 @@ class PreparedQuery:
                         [torch.zeros((prog.G, m), dtype=torch.uint8, device=dev) for _ in range(prog.nhll)])
 
     def _scan(self, prog, prep) -> Partials:
-        from ..parallel.fault import FAULTS
-
         FAULTS.maybe_fail("scan", self.world.rank)
         de = self._dict_exist_plan(prog)
         part = None
@@ -320,16 +332,13 @@ class PreparedQuery:
         unchanged (<= 4096 groups): the execution is one replayed HIP graph of reset + scan + HLL
         estimates + D2H (engine/device_exec.py run_graph_small).  (prog, partials with their host
         copy, scan end time) or None for the ordinary path."""
-        if self.world.distributed or len(self.scans) != 1 or self.window is not None:
+        if not _graphs_on() or self.world.distributed or len(self.scans) != 1 or self.window is not None:
             return None
         _, prog, prep = self.scans[0]
         if prep is None or not hasattr(prep, "run_graph_small") or prog.G > 4096 or prog.nslots > 256:
             return None
         if (prog.stored_hll and not getattr(prep, "stored_fused", False)) or self._dict_exist_plan(prog) is not None:
             return None
-        from ..parallel.fault import FAULTS
-        from ..utils.cancel import checkpoint
-
         with T.span("sdo.scan"):
             checkpoint()
             FAULTS.maybe_fail("scan", self.world.rank)
@@ -345,8 +354,6 @@ class PreparedQuery:
         Across ranks, sparse partials are merged into disjoint per-rank slices first; HAVING and the
         top-K prune run on every slice (distributed), and only the survivors are gathered -- to
         rank 0 alone with ``root_only`` (the other ranks then hold an empty slice)."""
-        from ..utils.cancel import checkpoint
-
         _, prog, prep = self.scans[0]
         if self.segments_per_query and self.world.distributed and self.window is None and PIPELINE_MERGE:
             out = self._run_pipelined(prog)

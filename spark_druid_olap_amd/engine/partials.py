@@ -10,7 +10,7 @@ import numpy as np
 import torch
 
 from ..ops import desc as D
-from .lower import fixed_value
+from .lower import fixed_value, ord2f
 
 
 @dataclass
@@ -114,12 +114,21 @@ def d2h(ts: List[torch.Tensor]) -> List[np.ndarray]:
 
 
 _STAGE = __import__("threading").local()
+_NATIVE: list = []
+
+
+def _native():
+    if not _NATIVE:
+        from ..ops import native
+
+        _NATIVE.append(native)
+    return _NATIVE[0]
 
 
 def _fetch_small(acc: torch.Tensor, hll: List[torch.Tensor], G: int, p: int) -> List[np.ndarray]:
     """[acc as host int64 [G, ns], estimates per register block...] of a small dense state,
     read back through per-thread pinned / device scratch buffers (reused across executions)."""
-    from ..ops import native
+    native = _native()
 
     nb = acc.numel() * 8
     need = nb + len(hll) * G * 8
@@ -272,8 +281,6 @@ def finalize(prog, parts: Partials, out_types: Optional[Dict[str, str]] = None) 
     their dictionary's width, numeric dictionary keys as final SQL-typed values when ``out_types``
     (output name -> SQL type, from the SQL layer) asks for them, constant keys not at all, and only
     the accumulator slots an output reads."""
-    from .lower import ord2f
-
     want_gid = bool(getattr(prog, "thetas", None))
     collapse = any(kc.collapse for kc in prog.keys)
     typed: Dict[int, object] = {}

@@ -70,6 +70,23 @@ static void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// Result waits of small queries: the host has nothing else to do, and a blocking
+// hipStreamSynchronize may sleep until an interrupt wakes it -- latency that lands on every
+// query's wall time.  With spinning on, the wait polls hipStreamQuery instead (set_spin_sync).
+static bool g_spin_sync = false;
+static void set_spin_sync(bool on) { g_spin_sync = on; }
+
+static void wait_stream(hipStream_t st, const char* what) {
+  if (g_spin_sync) {
+    hipError_t e;
+    while ((e = hipStreamQuery(st)) == hipErrorNotReady) {
+    }
+    check(e, what);
+    return;
+  }
+  check(hipStreamSynchronize(st), what);
+}
+
 static void scan(uint64_t desc, int grid, int block, int lds, int unroll, uint64_t stream) {
   hipStream_t s = (hipStream_t)stream;
   if (block % 64 != 0 || block > 512 || block <= 0) throw std::invalid_argument("block must be a multiple of 64 <= 512");
@@ -350,7 +367,7 @@ static void fetch_small(uint64_t acc, int64_t acc_bytes, std::vector<uint64_t> h
       check(hipMemcpyAsync((void*)(host + acc_bytes), (const void*)est_dev, hll.size() * G * 8, hipMemcpyDeviceToHost,
                            st),
             "fetch_small est");
-    check(hipStreamSynchronize(st), "fetch_small sync");
+    wait_stream(st, "fetch_small sync");
   }
 }
 
@@ -413,7 +430,7 @@ static void graph_launch(int h, uint64_t stream) {
   }
   py::gil_scoped_release nogil;
   check(hipGraphLaunch(ex, (hipStream_t)stream), "hipGraphLaunch");
-  check(hipStreamSynchronize((hipStream_t)stream), "graph sync");
+  wait_stream((hipStream_t)stream, "graph sync");
 }
 
 static void graph_destroy(int h) {
@@ -425,7 +442,7 @@ static void graph_destroy(int h) {
 
 static void stream_sync(uint64_t stream) {
   py::gil_scoped_release nogil;
-  check(hipStreamSynchronize((hipStream_t)stream), "stream sync");
+  wait_stream((hipStream_t)stream, "stream sync");
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -596,6 +613,7 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("run_scan", &run_scan);
   m.def("fetch_small", &fetch_small);
   m.def("stream_sync", &stream_sync);
+  m.def("set_spin_sync", &set_spin_sync);
   m.def("graph_small_capture", &graph_small_capture);
   m.def("graph_launch", &graph_launch);
   m.def("graph_destroy", &graph_destroy);

@@ -54,6 +54,9 @@ def load(build_if_missing: bool = True):
             except Exception as e:  # pragma: no cover - no compiler on the box
                 raise NativeUnavailable(f"native extension is stale and rebuild failed: {e}") from e
         _mod = importlib.import_module("spark_druid_olap_amd.ops._sdo_native")
+        if hasattr(_mod, "set_spin_sync"):
+            # result waits poll instead of sleeping in hipStreamSynchronize (bindings.cpp wait_stream)
+            _mod.set_spin_sync(os.environ.get("SDO_SPIN_SYNC", "0") != "0")
         return _mod
 
 

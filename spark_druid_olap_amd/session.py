@@ -36,6 +36,19 @@ from .sql.execute import Batch, Executor
 from .sql.optimizer import optimize
 from .sql.parser import ParseError, parse
 from .sql.types import AnalysisError, series_to_list, to_series
+from .utils import trace as T
+
+_RUN_HELPERS: list = []
+
+
+def _run_helpers():
+    """(results_on_root, root_only_results, cancel scope), imported once (the engine imports lazily)."""
+    if not _RUN_HELPERS:
+        from .engine.executor import results_on_root, root_only_results
+        from .utils.cancel import scope
+
+        _RUN_HELPERS.append((results_on_root, root_only_results, scope))
+    return _RUN_HELPERS[0]
 
 _PANDAS_TO_SQL = {"i": "bigint", "u": "bigint", "f": "double", "b": "boolean", "M": "timestamp"}
 
@@ -80,9 +93,7 @@ class DataFrame:
                 from .utils.cancel import CancelToken
 
                 token = CancelToken(tmo)
-        from .engine.executor import results_on_root, root_only_results
-        from .utils.cancel import scope
-
+        results_on_root, root_only_results, scope = _run_helpers()
         ex = Executor(self.session, token)
         t0 = time.perf_counter()
         # results on rank 0 only (the caller asked, engine/executor.py results_on_root) unless a
@@ -439,8 +450,6 @@ class Session:
         spec = dq.spec
         t0 = time.perf_counter()
         prep = self.prepare_druid(dq)
-        from .utils import trace as T
-
         with T.span(f"sdo.druid.{spec.queryType}"):
             res = prep.run()
         if isinstance(spec, S.TimeSeriesQuerySpec) and res.num_rows == 0:
@@ -468,8 +477,6 @@ class Session:
             ctx = getattr(run_spec, "context", None)
             run_spec = run_spec.copy(context=ctx.copy(deterministic=True) if ctx is not None
                                      else S.QuerySpecContext(deterministic=True))
-        from .utils import trace as T
-
         prep = getattr(dq, "_prepared", None)
         stale = lambda p: p is None or getattr(dq, "_prepared_spec", None) is not spec or \
             getattr(p, "deterministic", False) != (det or getattr(p, "deterministic", False))  # noqa: E731

@@ -80,12 +80,19 @@ def reset() -> Timeline:
     return _TL.tl
 
 
-@contextlib.contextmanager
+_NOOP = contextlib.nullcontext()
+
+
 def span(name: str):
-    """roctx range + timeline entry (no-op unless tracing is enabled)."""
+    """roctx range + timeline entry (no-op unless tracing is enabled).  Disabled, it returns one
+    shared null context: no generator per call (a few of these wrap every query's hot path)."""
     if not _ENABLED:
-        yield
-        return
+        return _NOOP
+    return _span(name)
+
+
+@contextlib.contextmanager
+def _span(name: str):
     lib = _lib()
     tl = timeline()
     if lib:
