@@ -101,6 +101,8 @@ class DataFrame:
         root_only = root_only_results() and self._root_only_safe()
         with scope(token), results_on_root(root_only):
             b = self.session._with_sql(self.sql_text, lambda: ex.run(self.plan))
+        if isinstance(b, Batch):
+            b.materialize_gathers()  # the statement's result rows are real arrays, not deferred gathers
         self.last_stats = {"ms": (time.perf_counter() - t0) * 1e3, "druid": ex.druid_stats}
         return b
 
