@@ -9,7 +9,7 @@ from spark_druid_olap_amd.sql.execute import Batch, LazyGather, LazySeries, lazy
 
 
 def _batch():
-    refs = [A.Ref("a", "bigint", 1), A.Ref("b", "double", 2), A.Ref("c", "string", 3)]
+    refs = [A.Ref(1, "a", "bigint"), A.Ref(2, "b", "double"), A.Ref(3, "c", "string")]
     cols = {1: lazy_series(np.arange(10, dtype=np.int64)), 2: pd.Series(np.arange(10) * 0.5),
             3: pd.Series([f"s{i}" for i in range(10)])}
     return Batch(refs, cols, 10)
@@ -33,7 +33,7 @@ def test_unread_columns_are_never_gathered():
         calls.append(1)
         return pd.Series(np.arange(10))
 
-    refs = [A.Ref("a", "bigint", 1), A.Ref("b", "bigint", 2)]
+    refs = [A.Ref(1, "a", "bigint"), A.Ref(2, "b", "bigint")]
     b = Batch(refs, {1: LazySeries(make), 2: pd.Series(np.arange(10))}, 10)
     t = b.take(np.array([1, 2]))
     assert list(t.cols[2]) == [1, 2] and not calls  # column 1 never built, never gathered
