@@ -7,6 +7,7 @@
 #include <hip/hiprtc.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+#include <algorithm>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -43,6 +44,7 @@ struct ResetArgs {
   int* overflow;
 };
 __global__ void reset_bufs_kernel(ResetArgs a);
+__global__ void copy_words_kernel(const uint64_t* src, int64_t n, uint64_t* dst);
 __global__ void topk_keep_kernel(const int64_t* acc, int64_t n, int nslots, int slot, int is_f64, int desc,
                                  const uint64_t* state, uint64_t* keep);
 // sketch.hip
@@ -355,9 +357,28 @@ static void run_scan(uint64_t acc, uint64_t init, int64_t rows, int nslots, std:
 // Small dense result: HLL estimates of every register block (MFMA kernel) + the accumulator table
 // and the estimates copied into one pinned host buffer + a stream synchronisation, in one call with
 // the GIL released while the device works.
+static bool g_zero_copy = false;
+static void set_zero_copy(bool on) { g_zero_copy = on; }
+
 static void fetch_small(uint64_t acc, int64_t acc_bytes, std::vector<uint64_t> hll, int64_t G, int p,
                         uint64_t est_dev, uint64_t host, uint64_t stream) {
   hipStream_t st = (hipStream_t)stream;
+  if (g_zero_copy && acc_bytes % 8 == 0) {
+    // the kernels write the pinned host buffer directly: estimates from the MFMA finalize, the
+    // accumulator words from one copy block -- no SDMA copies
+    for (size_t i = 0; i < hll.size(); ++i)
+      hll_estimate(hll[i], G, p, host + (uint64_t)acc_bytes + i * (uint64_t)G * 8, stream);
+    const int64_t nw = acc_bytes / 8;
+    if (nw > 0) {
+      const unsigned blocks = (unsigned)std::min<int64_t>((nw + 255) / 256, 64);
+      hipLaunchKernelGGL(sdo::copy_words_kernel, dim3(blocks), dim3(256), 0, st, (const uint64_t*)acc, nw,
+                         (uint64_t*)host);
+      check(hipGetLastError(), "copy_words_kernel launch");
+    }
+    py::gil_scoped_release nogil;
+    wait_stream(st, "fetch_small sync");
+    return;
+  }
   for (size_t i = 0; i < hll.size(); ++i) hll_estimate(hll[i], G, p, est_dev + i * (uint64_t)G * 8, stream);
   {
     py::gil_scoped_release nogil;
@@ -614,6 +635,7 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("fetch_small", &fetch_small);
   m.def("stream_sync", &stream_sync);
   m.def("set_spin_sync", &set_spin_sync);
+  m.def("set_zero_copy", &set_zero_copy);
   m.def("graph_small_capture", &graph_small_capture);
   m.def("graph_launch", &graph_launch);
   m.def("graph_destroy", &graph_destroy);

@@ -57,6 +57,9 @@ def load(build_if_missing: bool = True):
         if hasattr(_mod, "set_spin_sync"):
             # result waits poll instead of sleeping in hipStreamSynchronize (bindings.cpp wait_stream)
             _mod.set_spin_sync(os.environ.get("SDO_SPIN_SYNC", "0") != "0")
+        if hasattr(_mod, "set_zero_copy"):
+            # small results written into pinned host memory by the kernels (bindings.cpp fetch_small)
+            _mod.set_zero_copy(os.environ.get("SDO_ZERO_COPY", "0") != "0")
         return _mod
 
 
