@@ -130,6 +130,7 @@ def main():
     only = [x for x in os.environ.get("SDO_BENCH_ONLY", "").split(",") if x]
     if only:  # diagnostics: a subset of the suite (the JSON line then describes only that subset)
         queries = [(n, q) for n, q in queries if n in only]
+    nsuite = len(queries)
 
     def sync():
         if dev.type == "cuda":
@@ -174,13 +175,43 @@ def main():
 
         prof.disable()
         pstats.Stats(prof, stream=sys.stderr).sort_stats("cumulative").print_stats(60)
+    shape_geo = None
+    if args.mode == "sql" and not only and os.environ.get("SDO_BENCH_SHAPE", "1") != "0":
+        # untimed, reported alongside: the same suite on the shape-shared kernels a first-seen
+        # parameterization runs (query constants read from the descriptor, no literal-specialized
+        # code object) -- freshly planned statements with specialization switched off
+        from spark_druid_olap_amd.engine import device_exec as DE
+
+        texts = {n: df.sql_text for n, df in queries}
+        queries = pq = None  # (release the specialized statements' buffers first)
+        import gc
+
+        gc.collect()
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
+        DE.SPECIALIZE = "off"
+        sess._plan_cache.clear()
+        shaped = [(n, sess.sql(t).prepared()) for n, t in texts.items()]
+        with results_on_root(os.environ.get("SDO_RESULTS_ON_ROOT", "1") != "0"):
+            for n, q in shaped:
+                q.run()
+            world.barrier()
+            slat = {n: [] for n, _ in shaped}
+            for _ in range(max(2, min(args.steps, 5))):
+                for n, q in shaped:
+                    a = time.perf_counter()
+                    q.run()
+                    slat[n].append((time.perf_counter() - a) * 1e3)
+            world.barrier()
+        smeans = {k: world.max_float(sum(v) / len(v)) for k, v in slat.items()}
+        shape_geo = math.exp(sum(math.log(max(m, 1e-6)) for m in smeans.values()) / len(smeans))
     if os.environ.get("SDO_BENCH_PER_RANK"):  # diagnostics: every rank's own means
         print(f"[bench] rank {world.rank}: " + " ".join(f"{k[:12]}={sum(v) / len(v):.3f}" for k, v in lat.items()),
               file=sys.stderr, flush=True)
     total_ms = world.max_float(total_ms)
     means = {k: world.max_float(sum(v) / len(v)) for k, v in lat.items()}
     geo = math.exp(sum(math.log(max(m, 1e-6)) for m in means.values()) / len(means))
-    nq = len(queries) * args.steps
+    nq = nsuite * args.steps
     mins = {k: world.max_float(min(v)) for k, v in lat.items()}
     maxs = {k: world.max_float(max(v)) for k, v in lat.items()}
     if world.rank == 0:
@@ -221,7 +252,7 @@ def main():
             "data": f"synthetic ({args.model.upper()} dbgen-like distributions, random dictionary values, generated on device)",
             "config": {"model": model,
                        "global_batch": nq, "seq_len": int(nrows), "parallelism": f"dp{world.size} (segment shards)",
-                       "queries": len(queries), "mode": args.mode, "scale_factor_total": total_sf,
+                       "queries": nsuite, "mode": args.mode, "scale_factor_total": total_sf,
                        "scale_factor_per_gpu": args.sf,
                        "world": {"size": world.size, "backend": world.backend}},
             "qps": round(nq / (total_ms / 1e3), 3),
@@ -229,6 +260,13 @@ def main():
             "per_query_min_ms": {k: round(v, 4) for k, v in mins.items()},
             "per_query_max_ms": {k: round(v, 4) for k, v in maxs.items()},
             "rows_per_gpu": int(nrows),
+            # the timed steps run each prepared statement's literal-specialized kernel (compiled
+            # synchronously at its first warmup run, SDO_JIT_SPECIALIZE=sync / _AFTER=1; a server
+            # compiles it in the background for statements that repeat); the shape-shared kernels
+            # of a first-seen parameterization are reported untimed next to it
+            "kernels": {"timed": f"literal-specialized ({os.environ.get('SDO_JIT_SPECIALIZE')}, after "
+                                 f"{os.environ.get('SDO_JIT_SPECIALIZE_AFTER')} run)",
+                        "shape_shared_geomean_ms": round(shape_geo, 4) if shape_geo is not None else None},
         }
         print(json.dumps(out), flush=True)
     from spark_druid_olap_amd.parallel.world import shutdown

@@ -46,8 +46,16 @@ JIT_STAGE = os.environ.get("SDO_JIT_STAGE", "auto")       # auto | reg (VGPR loa
 # parameterization of a dashboard query shares one code object); from its SPECIALIZE_AFTER-th run
 # a kernel with the constants baked in is compiled -- in the background ("async": serving never
 # waits for hipRTC) or at once ("sync": a benchmark's warmup) -- and swapped in.
+# A background compile costs ~0.3-1 s of a host core (hipRTC, GIL released) and saves a few to tens
+# of microseconds per run, so only statements that keep coming back are worth it: at most
+# SPEC_MAX_PENDING compiles queue at once, and a statement that finds the queue full asks again
+# after twice as many runs (a dashboard's hot statements get there; 2,000 one-off
+# parameterizations do not flood the host with compiles).
 SPECIALIZE = os.environ.get("SDO_JIT_SPECIALIZE", "async")  # off | async | sync
-SPECIALIZE_AFTER = int(os.environ.get("SDO_JIT_SPECIALIZE_AFTER", "2"))
+SPECIALIZE_AFTER = int(os.environ.get("SDO_JIT_SPECIALIZE_AFTER", "4"))
+SPEC_MAX_PENDING = 2
+_spec_pending = [0]
+_spec_lock = threading.Lock()
 # small dense executions as replayed HIP graphs (PreparedScan.run_graph_small).  On this ROCm
 # (7.x) one hipGraphLaunch + sync of the 4-5 node graph costs more host time than the fused native
 # launch path it replaces (headline geomean 0.441 vs 0.428 ms)
@@ -59,8 +67,16 @@ def _spec_executor():
     if not _spec_pool:
         from concurrent.futures import ThreadPoolExecutor
 
-        _spec_pool.append(ThreadPoolExecutor(max_workers=2, thread_name_prefix="sdo-jit-spec"))
+        _spec_pool.append(ThreadPoolExecutor(max_workers=SPEC_MAX_PENDING, thread_name_prefix="sdo-jit-spec"))
     return _spec_pool[0]
+
+
+def _spec_job(js):
+    try:
+        return js.specialized()
+    finally:
+        with _spec_lock:
+            _spec_pending[0] -= 1
 
 
 def _attach_packed(prog) -> None:
@@ -177,6 +193,7 @@ class PreparedScan:
             self.cap = 0
         self.jit = None
         self._runs = 0
+        self._spec_at = SPECIALIZE_AFTER  # run count at which a literal-specialized kernel is asked for
         self._spec_future = None
         self.part = None
         self.part_having = None
@@ -228,7 +245,7 @@ class PreparedScan:
         self._slot_lock = threading.Lock()
         self._slots = {}
         weakref.finalize(self, _forget_prep, id(self))
-        self._bufs()  # the preparing slot's buffers (settles the LDS-budget mode fallback)
+        self._settle()
 
     # ------------------------------------------------------------------ buffers
     # Every execution slot (engine/scheduler.py) gets its own accumulators / hash table / HLL
@@ -246,6 +263,16 @@ class PreparedScan:
         else:
             _buffers_used(self, slot)
         return b
+
+    def _settle(self) -> None:
+        """The LDS-budget mode fallback, decided at prepare time without allocating: buffers are
+        allocated per execution slot on first use (a server prepares outside any slot)."""
+        from .lower import lds_layout
+
+        if self.mode == D.M_DENSE_LDS:
+            _, _, _, total = lds_layout(self.prog, 0 if self.shared else self.lds, UNROLL, BLOCK // 64)
+            if total > 160 * 1024:
+                self.mode, self.lds, self.hll_lds = D.M_DENSE_GLOBAL, 0, 0
 
     def _alloc(self, cap: int) -> "_Bufs":
         from .lower import lds_layout
@@ -452,12 +479,19 @@ class PreparedScan:
                 import warnings
 
                 warnings.warn(f"literal specialization failed: {e}")
-        if self._runs != SPECIALIZE_AFTER or SPECIALIZE == "off" or self.jit is None or self.jit.literals:
+        if self._runs < self._spec_at or SPECIALIZE == "off" or self.jit is None or self.jit.literals:
             return
         if SPECIALIZE == "sync":
+            self._spec_at = 1 << 62
             self._adopt(self.jit.specialized())
-        else:
-            self._spec_future = _spec_executor().submit(self.jit.specialized)
+            return
+        with _spec_lock:
+            if _spec_pending[0] >= SPEC_MAX_PENDING:
+                self._spec_at = 2 * self._runs  # the compile queue is full: ask again later
+                return
+            _spec_pending[0] += 1
+        self._spec_at = 1 << 62
+        self._spec_future = _spec_executor().submit(_spec_job, self.jit)
 
     def _adopt(self, js) -> None:
         """Swap in a kernel of the same layout (the launch arguments cached per slot name the

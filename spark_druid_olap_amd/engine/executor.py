@@ -107,6 +107,10 @@ def is_cuda_ds(ds: DataSource) -> bool:
     return ds.device.type == "cuda"
 
 
+# below this many merged groups HAVING is left to the host (_post re-applies it either way)
+HAVING_MIN_ROWS = 4096
+
+
 class PreparedQuery:
     """A lowered query bound to a shard; run() can be called repeatedly (benchmarks, dashboards)."""
 
@@ -158,6 +162,15 @@ class PreparedQuery:
             self.scans.append(("mask", prog, self._prepare_mask(prog)))
         else:
             raise LoweringError(f"unsupported query type {qt}")
+        if segments_per_query and self.world.distributed and self.window is None and PIPELINE_MERGE \
+                and qt in ("groupBy", "timeseries", "topN"):
+            # the pipelined merge's cross-rank agreements (batch count, per-batch key slices) are
+            # collectives: made here, while preparing -- in the same order on every rank -- and never
+            # lazily at run time, where two execution slots running this shared prepared query
+            # could each issue them on a different process group (server/spmd.py slots)
+            self._nbatches = int(self.world.max_float(float(len(self.scans))))
+            if self._nbatches > 1:
+                self._slices = self._batch_key_slices(self.scans[0][1])
 
     def _prepare(self, prog: ScanProgram):
         if is_cuda_ds(self.ds) and self.engine.use_native:
@@ -413,12 +426,8 @@ class PreparedQuery:
         from ..parallel.merge import start_dense_merge
         from ..utils.cancel import checkpoint
 
-        if self._nbatches is None:
-            self._nbatches = int(self.world.max_float(float(len(self.scans))))
-        if self._nbatches <= 1 or self._pipeline_ok is False:
-            return None
-        if self._slices is None:
-            self._slices = self._batch_key_slices(prog)
+        if self._nbatches is None or self._nbatches <= 1 or self._pipeline_ok is False:
+            return None  # (agreed in __init__)
         slices = self._slices
         # one merge in flight: merge j runs while batch j+1 scans, then merge j completes (RCCL:
         # the compute stream waits for it -- no host sync until the final status check)
@@ -557,7 +566,9 @@ class PreparedQuery:
         h = getattr(self.qs, "having", None)
         if h is None or self.qs.queryType != "groupBy" or prog.thetas or any(kc.collapse for kc in prog.keys):
             return part, h is None
-        if part.rows <= 4096:
+        if part.rows <= HAVING_MIN_ROWS and not part.scattered:
+            # (a scattered slice's row count differs per rank: the flag must not, because the
+            # post-gather top-K prune on the root trusts it for the union of every rank's slice)
             return part, False
         aggs = {a.name: a for a in prog.aggs}
 

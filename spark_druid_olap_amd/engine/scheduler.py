@@ -86,6 +86,9 @@ class StreamScheduler:
                 if st is None:
                     yield slot
                 else:
+                    # work the statement's preparation launched on the default stream (lowering:
+                    # HLL code planes, FD tables) precedes the slot's kernels
+                    st.wait_stream(torch.cuda.default_stream(st.device))
                     with torch.cuda.stream(st):
                         yield slot
                     st.synchronize()

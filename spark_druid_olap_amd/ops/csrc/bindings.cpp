@@ -288,7 +288,12 @@ static int glds_probe() {
 // ---------------------------------------------------------------------------------------------
 // Per-query JIT kernels (ops/jit.py): hipRTC compile -> code object bytes (cached on disk by the
 // caller) -> hipModuleLoadData -> launch.  Compilation needs no GPU.
-static py::bytes rtc_compile(const std::string& src, const std::string& name, const std::vector<std::string>& opts) {
+//
+// A compile takes 0.3-2 s of host CPU: it runs with the GIL released, so serving threads (plan,
+// launch, encode) keep running while a background literal specialization or a first-seen shape
+// compiles (ops/jit.py compile_source runs different shapes' compiles in parallel).
+static std::string rtc_compile_nogil(const std::string& src, const std::string& name,
+                                     const std::vector<std::string>& opts) {
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, src.c_str(), (name + ".hip").c_str(), 0, nullptr, nullptr) != HIPRTC_SUCCESS)
     throw std::runtime_error("hiprtcCreateProgram failed");
@@ -308,6 +313,15 @@ static py::bytes rtc_compile(const std::string& src, const std::string& name, co
   std::string code(cs, '\0');
   hiprtcGetCode(prog, &code[0]);
   hiprtcDestroyProgram(&prog);
+  return code;
+}
+
+static py::bytes rtc_compile(const std::string& src, const std::string& name, const std::vector<std::string>& opts) {
+  std::string code;
+  {
+    py::gil_scoped_release nogil;
+    code = rtc_compile_nogil(src, name, opts);
+  }
   return py::bytes(code);
 }
 
@@ -629,7 +643,11 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("hll_merge_stored", &hll_merge_stored);
   m.def("desc_size", &desc_size);
   m.def("rtc_compile", &rtc_compile);
-  m.def("module_load", [](py::bytes code, const std::string& name) { return module_load(std::string(code), name); });
+  m.def("module_load", [](py::bytes code, const std::string& name) {
+    std::string c(code);
+    py::gil_scoped_release nogil;  // hipModuleLoadData: code-object load + relocation
+    return module_load(c, name);
+  });
   m.def("module_launch", &module_launch);
   m.def("run_scan", &run_scan);
   m.def("fetch_small", &fetch_small);

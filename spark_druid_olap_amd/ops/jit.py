@@ -1315,18 +1315,52 @@ def compile_code(src: str, name: str) -> bytes:
     return code
 
 
+_inflight: Dict[str, "Future"] = {}
+COMPILE_STATS = {"compiles": 0, "waits": 0}
+
+
 def compile_source(src: str, name: str) -> int:
-    """Compile (cached) and load into the current HIP context; returns a launch handle."""
+    """Compile (cached) and load into the current HIP context; returns a launch handle.
+
+    ``_lock`` only guards the handle table: the compile itself (hipRTC, GIL released in the native
+    binding) runs outside it, so different shapes compile in parallel and never stall a thread that
+    only launches.  One future per source key: concurrent requests for the same shape wait on the
+    first one's compile instead of compiling it again."""
+    from concurrent.futures import Future
+
     from . import native
 
     key = _code_key(src)
     with _lock:
-        if key in _handles:
-            return _handles[key]
+        h = _handles.get(key)
+        if h is not None:
+            return h
+        fut = _inflight.get(key)
+        owner = fut is None
+        if owner:
+            fut = _inflight[key] = Future()
+    if not owner:
+        COMPILE_STATS["waits"] += 1
+        return fut.result()
+    try:
         code = compile_code(src, name)
         h = native.load().module_load(code, name)
+    except BaseException as e:
+        with _lock:
+            _inflight.pop(key, None)
+        fut.set_exception(e)
+        raise
+    with _lock:
         _handles[key] = h
-        return h
+        _inflight.pop(key, None)
+    COMPILE_STATS["compiles"] += 1
+    fut.set_result(h)
+    return h
+
+
+def is_loaded(src: str) -> bool:
+    """This source's kernel is compiled and loaded (no compile would run)."""
+    return _code_key(src) in _handles
 
 
 class JitScan:

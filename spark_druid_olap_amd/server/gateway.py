@@ -288,6 +288,7 @@ class NativeHiveServer(HiveThriftServer):
         if df.plan is None:  # a command that looked like a query: already executed
             res = df.to_pandas()
         else:
+            df.prepare()  # lowering + a first-seen shape's compile: before a stream slot is held
             with sess.engine.coalescer().scheduler.lease():
                 res = df.run(token=token)  # the executor's columns, encoded without a DataFrame
         return list(df.columns), [t for _, t in df.schema], res

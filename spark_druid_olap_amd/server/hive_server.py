@@ -346,6 +346,7 @@ class HiveThriftServer:
                 else:
                     # a stream slot per execution; identical queued statements (same cached plan,
                     # i.e. same text + conf + database) execute once
+                    df.prepare()  # lowering / compiling before a stream slot is leased
                     co = sess.engine.coalescer()
                     key = id(df) if sess.conf.typed("spark.sparklinedata.druid.planCache.enabled") and \
                         os.environ.get("SDO_COALESCE", "1") != "0" else None

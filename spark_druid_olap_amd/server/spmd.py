@@ -72,6 +72,11 @@ def _apply(sessions: Dict[bytes, Any], root, msg: Dict[str, Any]) -> None:
         sessions[sid] = s
     elif op == "close":
         sessions.pop(sid, None)
+        # a client that closes its session without closing its cursors: release them (every rank
+        # applies the close in broadcast order, so every rank drops the same iterators)
+        for k in [k for k, owner in _STREAM_OWNER.items() if owner == sid]:
+            _STREAMS.pop(k, None)
+            _STREAM_OWNER.pop(k, None)
 
 
 def _token(msg):
@@ -95,6 +100,7 @@ def _run_statement(df, msg):
 # rank advances a cursor on the same broadcast message, so the page's collectives (the Select
 # page gather) run in lock step; rank 0 hands the page to the client.
 _STREAMS: Dict[int, Any] = {}
+_STREAM_OWNER: Dict[int, Any] = {}  # stream id -> client session id (released with the session)
 
 
 def _streamable(df, s) -> bool:
@@ -112,9 +118,11 @@ def _execute(sessions: Dict[bytes, Any], root, msg: Dict[str, Any]):
         page = next(it, None) if it is not None else None
         if page is None:
             _STREAMS.pop(msg["stream_id"], None)
+            _STREAM_OWNER.pop(msg["stream_id"], None)
         return page
     if op == "stream_close":
         _STREAMS.pop(msg["stream_id"], None)
+        _STREAM_OWNER.pop(msg["stream_id"], None)
         return None
     if op != "exec":
         _apply(sessions, root, msg)
@@ -125,6 +133,7 @@ def _execute(sessions: Dict[bytes, Any], root, msg: Dict[str, Any]):
         # a Select-backed result pages through the cursor instead of materialising (the
         # reference's DruidSelectResultIterator); the first page runs on the first step
         _STREAMS[msg["stream_id"]] = df.iter_batches(token=_token(msg))
+        _STREAM_OWNER[msg["stream_id"]] = msg.get("sid")
         return df, ("stream", msg["stream_id"])
     return _run_statement(df, msg)
 
@@ -210,6 +219,9 @@ class SlotWorkers:
             try:
                 with slot_group(self.groups[i]), use_slot(self.BUFFER_SLOT_BASE + i):
                     if self.streams[i] is not None:
+                        # preparation (dispatch thread, default stream) launched device work the
+                        # scan reads -- e.g. the u16 HLL code planes of segment/hllcode.py
+                        self.streams[i].wait_stream(torch.cuda.default_stream(self.streams[i].device))
                         with torch.cuda.stream(self.streams[i]):
                             res = _run_statement(df, msg)
                         self.streams[i].synchronize()
@@ -297,7 +309,8 @@ class SpmdDispatcher:
         for g in groups:
             m = g[0].msg
             slot = INLINE
-            if self.workers is not None and m["op"] == "exec" and _is_query(m["stmt"]) and not m.get("overlay"):
+            if self.workers is not None and m["op"] == "exec" and _is_query(m["stmt"]) and not m.get("overlay") \
+                    and not _plans_collectively(m["stmt"]):
                 try:
                     s = _session_for(self.sessions, self.root, {"sid": m["sid"]})
                     df = s.sql(m["stmt"])
@@ -414,6 +427,14 @@ class SpmdDispatcher:
                 self.stats["statements"] += 1
         self.stats["executions"] += len(out)
         return out
+
+
+def _plans_collectively(stmt: str) -> bool:
+    """Statements whose *planning* issues collectives: the ``d$*`` metadata views gather the
+    cluster-wide inventory from every rank when analysed (catalog/views.py cluster_inventory).  Rank
+    0 must not plan them alone while deciding a slot (its peers sit in the broadcast): they run
+    inline, planned once, in broadcast order on every rank."""
+    return "d$" in stmt.lower()
 
 
 def _is_query(stmt: str) -> bool:

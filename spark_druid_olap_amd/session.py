@@ -109,6 +109,18 @@ class DataFrame:
     def prepared(self) -> "DataFrame":
         return self
 
+    def prepare(self) -> "DataFrame":
+        """Lower every pushed query whose spec is known up front (the GPU kernels of a first-seen
+        shape compile here).  Servers call this before leasing an execution slot, so a compile
+        never holds a stream slot; pushed queries parameterized by another query's result are
+        prepared when they run.  One process only: several ranks prepare in broadcast order
+        (server/spmd.py prepare_statement)."""
+        if self.plan is not None and not self.session.engine.world.distributed:
+            for dq in P.find_all_deep(self.plan, P.DruidQuery):
+                if not S.find_deferred(dq.spec):
+                    self.session.prepare_druid(dq)
+        return self
+
     def _root_only_safe(self) -> bool:
         ok = self.__dict__.get("_root_ok")
         if ok is None:
@@ -483,7 +495,13 @@ class Session:
         stale = lambda p: p is None or getattr(dq, "_prepared_spec", None) is not spec or \
             getattr(p, "deterministic", False) != (det or getattr(p, "deterministic", False))  # noqa: E731
         if stale(prep):
-            with self._lock:  # concurrent sessions share cached plans: prepare once
+            # concurrent sessions share cached plans: prepare once -- under a lock of this pushed
+            # query only, so preparing (and compiling) one statement never blocks another's
+            lock = dq.__dict__.get("_prep_lock")
+            if lock is None:
+                with self._lock:
+                    lock = dq.__dict__.setdefault("_prep_lock", threading.Lock())
+            with lock:
                 prep = getattr(dq, "_prepared", None)
                 if stale(prep):
                     with T.span("sdo.lower"):

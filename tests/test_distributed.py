@@ -208,6 +208,10 @@ ROOT_QUERIES = [
     _tpch.Q10[1],
     "select c_name, count(*), sum(l_quantity), max(l_discount) from orderLineItemPartSupplier group by c_name",
     "select c_name, sum(l_quantity) q from orderLineItemPartSupplier group by c_name having sum(l_quantity) > 60",
+    # HAVING + ORDER BY <agg> LIMIT over scattered slices (the worker makes the device-HAVING
+    # threshold differ per rank: some ranks apply HAVING to their slice, some would not)
+    "select c_name, l_shipmode, sum(l_quantity) q from orderLineItemPartSupplier group by c_name, l_shipmode "
+    "having sum(l_quantity) > 100 order by q, c_name, l_shipmode limit 7",
     APPROX,
 ]
 
@@ -224,6 +228,11 @@ def _root_worker(rank, world, port, outdir, env=None):
     from spark_druid_olap_amd.parallel.world import init_world, shutdown
     from spark_druid_olap_amd.session import Session
 
+    from spark_druid_olap_amd.engine import executor as EX
+
+    # straddle the device-HAVING row threshold across ranks (the applied flag must not
+    # depend on a rank's own slice size)
+    EX.HAVING_MIN_ROWS = 1 << 30 if rank % 2 else 0
     w = init_world(backend="gloo")
     flat = tpch.generate_flat(0.008 / world, "cpu", rank=rank, world=world)
     ds = tpch.to_datasource(flat, profile="bench")

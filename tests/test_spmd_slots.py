@@ -70,6 +70,10 @@ def _worker(rank, world, port, outdir):
     d.open_session(b"serial", {}, None)
     for q in stmts:
         serial[q] = d.execute(b"serial", q)[1].values.tolist()
+    # a metadata view gathers the cluster inventory from every rank while it is planned: it must
+    # plan in broadcast order on both ranks, not on rank 0 alone while picking a slot
+    views = d.execute(b"serial", "select druidHost, numSegments from `d$druidservers`")[1].values.tolist()
+    views2 = d.execute(b"serial", "select druidHost, numSegments from `d$druidservers`")[1].values.tolist()
     errs, conc = [], {}
 
     def client(i):
@@ -87,7 +91,8 @@ def _worker(rank, world, port, outdir):
         t.start()
     for t in ts:
         t.join(300)
-    out = {"serial": serial, "conc": conc, "errs": errs, "max_inflight": d.workers.max_inflight,
+    out = {"serial": serial, "conc": conc, "errs": errs, "max_inflight": d.workers.max_inflight, "views": views,
+           "views2": views2,
            "stats": dict(d.stats)}
     d.shutdown()
     with open(os.path.join(outdir, "r0.pkl"), "wb") as f:
@@ -114,6 +119,7 @@ def test_slots_run_statements_concurrently_and_match_serial():
         with open(os.path.join(td, "r0.pkl"), "rb") as f:
             out = pickle.load(f)
     assert not out["errs"], out["errs"]
+    assert sorted(h for h, _ in out["views"]) == ["gpu:0", "gpu:1"] and out["views"] == out["views2"], out["views"]
     assert out["max_inflight"] >= 2, out
     assert out["stats"]["on_slots"] > 0 and out["stats"]["coalesced"] == 0, out["stats"]
     for q, runs in out["conc"].items():
@@ -158,5 +164,11 @@ def test_dispatcher_streams_select_pages(ds_small, df_small):
         df3, res3 = d.execute(b"s1", q, stream=True)
         d.close_stream(res3[1])
         assert res3[1] not in spmd._STREAMS
+        # a session closed with a cursor still open releases it (no leaked device-resident rows)
+        d.open_session(b"s2", {"spark.sparklinedata.druid.selectquery.pagesize": "11"}, None)
+        _, res4 = d.execute(b"s2", q, stream=True)
+        assert d.stream_next(res4[1]) is not None and res4[1] in spmd._STREAMS
+        d.close_session(b"s2")
+        assert res4[1] not in spmd._STREAMS and res4[1] not in spmd._STREAM_OWNER
     finally:
         d.shutdown()
