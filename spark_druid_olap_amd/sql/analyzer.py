@@ -198,6 +198,8 @@ class Analyzer:
             cond = self.resolve(s.where, scope)
             if _has_agg(cond):
                 raise AnalysisError("aggregate functions are not allowed in WHERE")
+            if _has_window(cond):
+                raise AnalysisError("window functions are not allowed in WHERE")
             plan = P.Filter(cond, plan)
         # expand stars
         items: List[Tuple[A.Expr, Optional[str]]] = []
@@ -228,6 +230,7 @@ class Analyzer:
                 proj.append(A.Alias(e, n))
         alias_map = {n.lower(): e for e, n in items}
         if s.distinct:
+            plan, proj, _ = _with_windows(plan, proj, [])
             plan = P.Project(proj, plan)
             outs = plan.output
             groups = [A.Alias(o, o.name) for o in outs]
@@ -245,11 +248,12 @@ class Analyzer:
                     orders.append(A.SortOrder(e, o.ascending, o.nulls_first))
                 plan = P.Sort(orders, plan)
         else:
-            if s.order_by:
-                orders = []
-                for o in s.order_by:
-                    orders.append(A.SortOrder(self._order_expr(o.expr, items, alias_map, scope), o.ascending,
-                                              o.nulls_first))
+            orders = []
+            for o in s.order_by:
+                orders.append(A.SortOrder(self._order_expr(o.expr, items, alias_map, scope), o.ascending,
+                                          o.nulls_first))
+            plan, proj, orders = _with_windows(plan, proj, orders)
+            if orders:
                 plan = P.Sort(orders, plan)
             plan = P.Project(proj, plan)
         if s.limit is not None:
@@ -303,6 +307,14 @@ class Analyzer:
         gid = A.Alias(A.Lit(0, "int"), "grouping__id") if sets is not None else None
 
         def rw(e: A.Expr) -> A.Expr:
+            if isinstance(e, A.WindowExpr):
+                # the window runs over the aggregated rows: its arguments, partition and order
+                # expressions are rewritten to group / aggregate references, the function stays
+                f = e.func
+                return A.WindowExpr(A.Call(f.name, tuple(rw(a) for a in f.args), f.distinct),
+                                    tuple(rw(p) for p in e.partition),
+                                    tuple(A.SortOrder(rw(o.expr), o.ascending, o.nulls_first) for o in e.orders),
+                                    e.frame)
             k = e.key()
             if k in gkeys and not isinstance(e, A.Lit):
                 g = gkeys[k]
@@ -360,7 +372,10 @@ class Analyzer:
             orders.append(A.SortOrder(rw(ex), o.ascending, o.nulls_first))
         plan = P.Aggregate(groups, aggs, plan, sets, gid)
         if having is not None:
+            if _has_window(having):
+                raise AnalysisError("window functions are not allowed in HAVING")
             plan = P.Filter(having, plan)
+        plan, proj, orders = _with_windows(plan, proj, orders)
         if orders:
             plan = P.Sort(orders, plan)
         plan = P.Project(proj, plan)
@@ -415,6 +430,17 @@ class Analyzer:
                 if x.kind in ("scalar", "in") and len(p.output) != 1:
                     raise AnalysisError("subquery must return exactly one column")
                 return A.SubqueryExpr(x.kind, p, child, x.negated)
+            if isinstance(x, A.WindowExpr):
+                f = x.func
+                if not (f.is_agg or f.name in A.WINDOW_FUNCS):
+                    raise AnalysisError(f"{f.name} is not a window function")
+                fargs = tuple(go(a) for a in f.args)
+                if f.name == "count" and fargs and all(isinstance(a, A.Lit) and a.value is not None for a in fargs) \
+                        and not f.distinct:
+                    fargs = ()
+                return A.WindowExpr(A.Call(f.name, fargs, f.distinct), tuple(go(p) for p in x.partition),
+                                    tuple(A.SortOrder(go(o.expr), o.ascending, o.nulls_first) for o in x.orders),
+                                    x.frame)
             if isinstance(x, A.Call):
                 if not has_function(x.name):
                     raise AnalysisError(f"Undefined function: '{x.name}'. This function is neither a registered "
@@ -434,9 +460,40 @@ class Analyzer:
 
 
 def _has_agg(e: A.Expr) -> bool:
-    for x in e.walk():
-        if isinstance(x, A.Call) and x.is_agg:
-            return True
-        if isinstance(x, A.SubqueryExpr):
-            continue
-    return False
+    """An aggregate of the enclosing GROUP BY inside ``e`` (a window function itself is not one:
+    ``sum(x) OVER (..)`` aggregates over the window, ``avg(sum(x)) OVER (..)`` holds one)."""
+    if isinstance(e, A.WindowExpr):
+        return any(_has_agg(c) for c in e.func.args) or any(_has_agg(c) for c in e.children[1:])
+    if isinstance(e, A.Call) and e.is_agg:
+        return True
+    return any(_has_agg(c) for c in e.children)
+
+
+def _has_window(e: A.Expr) -> bool:
+    return any(isinstance(x, A.WindowExpr) for x in e.walk())
+
+
+def _extract_windows(exprs: List[A.Expr], windows: List[A.Alias], wkeys: Dict[tuple, A.Alias]) -> List[A.Expr]:
+    """Replace every window expression by a reference to the column a ``Window`` node computes."""
+    def ex(e):
+        if isinstance(e, A.WindowExpr):
+            k = e.key()
+            a = wkeys.get(k)
+            if a is None:
+                a = wkeys[k] = A.Alias(e, auto_name(e))
+                windows.append(a)
+            return a.to_ref(typeof(e))
+        return None
+    return [e.transform(ex) for e in exprs]
+
+
+def _with_windows(plan: P.Plan, proj: List[A.Expr], orders: List[A.SortOrder]):
+    """(plan with a Window node on top if any select item / ORDER BY uses one, proj, orders)."""
+    if not any(_has_window(e) for e in proj) and not any(_has_window(o.expr) for o in orders):
+        return plan, proj, orders
+    windows: List[A.Alias] = []
+    wkeys: Dict[tuple, A.Alias] = {}
+    proj = _extract_windows(proj, windows, wkeys)
+    oex = _extract_windows([o.expr for o in orders], windows, wkeys)
+    orders = [A.SortOrder(e, o.ascending, o.nulls_first) for e, o in zip(oex, orders)]
+    return P.Window(windows, plan), proj, orders

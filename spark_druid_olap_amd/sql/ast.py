@@ -362,6 +362,53 @@ class SortOrder:
         return f"{self.expr.sql()} {'ASC' if self.ascending else 'DESC'}"
 
 
+# functions that only exist over a window (Spark's ranking / offset functions); the aggregates of
+# AGG_FUNCS may also be used over a window
+WINDOW_FUNCS = {"rank", "dense_rank", "row_number", "percent_rank", "cume_dist", "ntile", "lag", "lead",
+                "first_value", "last_value"}
+
+
+@dataclass(frozen=True, repr=False)
+class WindowExpr(Expr):
+    """``func(args) OVER (PARTITION BY .. ORDER BY .. [ROWS|RANGE frame])``.  ``frame`` is
+    (kind, lo, hi) with row offsets relative to the current row (negative = preceding, None =
+    unbounded); None = Spark's default frame (RANGE UNBOUNDED PRECEDING .. CURRENT ROW with an
+    ORDER BY, the whole partition without one).  Evaluated on the host over the (aggregated) rows
+    below it (``sql/window.py``), like Spark's WindowExec above the reference's pushed Druid
+    aggregate (the BI workload's windowed templates, docs/bi-benchmark/snap-sales-demo.jmx)."""
+    func: Call
+    partition: Tuple[Expr, ...] = ()
+    orders: Tuple[SortOrder, ...] = ()
+    frame: Optional[Tuple[str, Optional[int], Optional[int]]] = None
+
+    @property
+    def children(self):
+        return (self.func,) + tuple(self.partition) + tuple(o.expr for o in self.orders)
+
+    def with_children(self, ch):
+        np_ = len(self.partition)
+        f = ch[0]
+        orders = tuple(SortOrder(c, o.ascending, o.nulls_first) for c, o in zip(ch[1 + np_:], self.orders))
+        return WindowExpr(f, tuple(ch[1:1 + np_]), orders, self.frame)
+
+    def key(self):
+        return ("Window", self.func.key(), tuple(p.key() for p in self.partition),
+                tuple((o.expr.key(), o.ascending, o.nulls_first) for o in self.orders), self.frame)
+
+    def sql(self):
+        parts = []
+        if self.partition:
+            parts.append("PARTITION BY " + ", ".join(p.sql() for p in self.partition))
+        if self.orders:
+            parts.append("ORDER BY " + ", ".join(o.sql() for o in self.orders))
+        if self.frame is not None:
+            k, lo, hi = self.frame
+            b = lambda v, side: ("UNBOUNDED " + side) if v is None else (  # noqa: E731
+                "CURRENT ROW" if v == 0 else f"{abs(v)} {'PRECEDING' if v < 0 else 'FOLLOWING'}")
+            parts.append(f"{k.upper()} BETWEEN {b(lo, 'PRECEDING')} AND {b(hi, 'FOLLOWING')}")
+        return f"{self.func.sql()} OVER ({' '.join(parts)})"
+
+
 def conjuncts(e: Optional[Expr]) -> List[Expr]:
     if e is None:
         return []

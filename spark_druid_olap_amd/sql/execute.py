@@ -269,6 +269,18 @@ class Executor:
             cols[r.rid] = _conform(eval_series(e, fr), r.dtype)
         return Batch(refs, cols, b.n)
 
+    def _Window(self, p: P.Window) -> Batch:
+        from .window import evaluate_window
+
+        b = self.run(p.child)
+        fr = b.frame(self._subquery)
+        cols = {r.rid: dict.__getitem__(b.cols, r.rid) for r in b.refs if r.rid in b.cols}
+        layouts: dict = {}  # one sort per distinct (PARTITION BY, ORDER BY) spec
+        outs = p.output[len(b.refs):]
+        for a, r in zip(p.exprs, outs):
+            cols[r.rid] = _conform(evaluate_window(a.child, fr, layouts), r.dtype)
+        return Batch(list(b.refs) + list(outs), cols, b.n)
+
     def _Sort(self, p: P.Sort) -> Batch:
         b = self.run(p.child)
         if b.n <= 1:

@@ -118,6 +118,15 @@ def typeof(e: A.Expr) -> str:
         if e.kind == "scalar":
             return e.query.output[0].dtype
         return "boolean"
+    if isinstance(e, A.WindowExpr):
+        f = e.func
+        if f.name in ("rank", "dense_rank", "row_number", "ntile"):
+            return "int"
+        if f.name in ("percent_rank", "cume_dist"):
+            return "double"
+        if f.name in ("lag", "lead", "first_value", "last_value"):
+            return typeof(f.args[0]) if f.args else "null"
+        return typeof(f)
     if isinstance(e, A.Call):
         ts = [typeof(a) for a in e.args]
         if e.is_agg:
@@ -1351,9 +1360,9 @@ def is_deterministic(e: A.Expr) -> bool:
 def constant_fold(e: A.Expr) -> A.Expr:
     """Fold sub-expressions without column references into literals."""
     def fold(x: A.Expr):
-        if isinstance(x, (A.Lit, A.Ref, A.IntervalLit, A.SubqueryExpr, A.Alias)) or not x.children:
+        if isinstance(x, (A.Lit, A.Ref, A.IntervalLit, A.SubqueryExpr, A.Alias, A.WindowExpr)) or not x.children:
             return None
-        if isinstance(x, A.Call) and x.is_agg:
+        if isinstance(x, A.Call) and (x.is_agg or x.name in A.WINDOW_FUNCS):
             return None
         if isinstance(x, A.Case):
             # branches with a constant condition: drop the false / NULL ones, stop at a true one

@@ -786,6 +786,51 @@ class Parser:
         self.expect("END")
         return A.Case(tuple(whens), else_)
 
+    def _over(self, call: A.Call) -> A.WindowExpr:
+        """``OVER ( [PARTITION BY e, ..] [ORDER BY o, ..] [ROWS|RANGE frame] )``"""
+        self.i += 1
+        self.expect("(")
+        part: List[A.Expr] = []
+        orders: List[A.SortOrder] = []
+        frame = None
+        if self.at_seq("PARTITION", "BY") or self.at_seq("DISTRIBUTE", "BY"):
+            self.i += 2
+            part = self.expr_list()
+        if self.at_seq("ORDER", "BY") or self.at_seq("SORT", "BY"):
+            self.i += 2
+            orders = self.sort_items()
+        t = self.peek()
+        if t.kind == "id" and t.up in ("ROWS", "RANGE"):
+            self.i += 1
+            kind = t.up.lower()
+            if self.accept("BETWEEN"):
+                lo = self._frame_bound()
+                self.expect("AND")
+                hi = self._frame_bound()
+            else:  # "ROWS 10 PRECEDING" = BETWEEN 10 PRECEDING AND CURRENT ROW
+                lo, hi = self._frame_bound(), 0
+            frame = (kind, lo, hi)
+        self.expect(")")
+        return A.WindowExpr(call, tuple(part), tuple(orders), frame)
+
+    def _frame_bound(self) -> Optional[int]:
+        """UNBOUNDED PRECEDING|FOLLOWING -> None, CURRENT ROW -> 0, n PRECEDING -> -n, n FOLLOWING -> n."""
+        t = self.next()
+        if t.up == "UNBOUNDED":
+            self.next()
+            return None
+        if t.up == "CURRENT":
+            self.next()  # ROW
+            return 0
+        try:
+            n = int(t.text)
+        except ValueError:
+            raise ParseError(f"bad window frame bound {t.text!r}") from None
+        side = self.next().up
+        if side not in ("PRECEDING", "FOLLOWING"):
+            raise ParseError(f"bad window frame bound {t.text} {side}")
+        return -n if side == "PRECEDING" else n
+
     def _column_or_call(self):
         name = self.ident()
         if self.peek().kind == "op" and self.peek().text == "(":
@@ -802,7 +847,11 @@ class Parser:
             self.expect(")")
             if fname == "count" and args and isinstance(args[0], A.Star):
                 args = []
-            return A.Call(fname, tuple(args), distinct)
+            call = A.Call(fname, tuple(args), distinct)
+            if self.peek().kind == "id" and self.peek().up == "OVER" and self.peek(1).kind == "op" and \
+                    self.peek(1).text == "(":
+                return self._over(call)
+            return call
         parts = [name]
         while self.peek().kind == "op" and self.peek().text == ".":
             if self.peek(1).kind == "op" and self.peek(1).text == "*":

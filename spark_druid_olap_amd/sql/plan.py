@@ -154,6 +154,26 @@ class Aggregate(Plan):
                 ", ".join(a.sql() for a in self.aggs) + "]" + gs)
 
 
+class Window(Plan):
+    """Window expressions (``A.WindowExpr`` under Aliases) evaluated over the child's rows on the
+    host (``sql/window.py``); output = the child's columns + one column per expression."""
+
+    def __init__(self, exprs: List[A.Alias], child: Plan):
+        self.exprs = exprs
+        self.child = child
+        self.children = (child,)
+
+    @property
+    def output(self):
+        return list(self.child.output) + [out_ref(e) for e in self.exprs]
+
+    def with_children(self, ch):
+        return Window(self.exprs, ch[0])
+
+    def describe(self):
+        return "Window [" + ", ".join(e.sql() for e in self.exprs) + "]"
+
+
 class Sort(Plan):
     def __init__(self, orders: List[A.SortOrder], child: Plan):
         self.orders = orders

@@ -27,6 +27,7 @@ class Sampler:
         self.interval = interval
         self.self_counts = collections.Counter()
         self.incl_counts = collections.Counter()
+        self.line_counts = collections.Counter()  # innermost frame at its current line
         self.samples = 0
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
@@ -49,6 +50,7 @@ class Sampler:
                     continue
                 self.samples += 1
                 self.self_counts[self._key(f)] += 1
+                self.line_counts[f"{self._key(f)}@{f.f_lineno}"] += 1
                 seen = set()
                 while f is not None:
                     k = self._key(f)
@@ -79,6 +81,8 @@ class Sampler:
         n = max(1, self.samples)
         out = [f"{self.samples} busy-thread samples", "--- self (innermost frame)"]
         out += [f"{c / n * 100:6.1f}%  {k}" for k, c in self.self_counts.most_common(top)]
+        out.append("--- self, by line")
+        out += [f"{c / n * 100:6.1f}%  {k}" for k, c in self.line_counts.most_common(top)]
         out.append("--- inclusive")
         out += [f"{c / n * 100:6.1f}%  {k}" for k, c in self.incl_counts.most_common(top)]
         return "\n".join(out)

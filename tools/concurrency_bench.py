@@ -40,6 +40,10 @@ def queries():
 
     if WORKLOAD == "varied":
         return varied_queries()
+    if WORKLOAD == "jmx":
+        from spark_druid_olap_amd.models import bi
+
+        return [(n, q) for n, _, q in bi.statements(25, BIND)]
     out = []
     for name, q in tpch.BENCH_QUERIES:
         if name == "TPCH Q3":
@@ -101,14 +105,15 @@ def varied_queries(n: int = 2000, seed: int = 7):
     return out
 
 
-def _client_proc(pid, nthreads, nclients, start_q, out_q, workload="fixed"):
+def _client_proc(pid, nthreads, nclients, start_q, out_q, workload="fixed", bind="years"):
     import threading
 
     from spark_druid_olap_amd.server.hive_client import connect
 
-    global NCLIENTS, WORKLOAD
+    global NCLIENTS, WORKLOAD, BIND
     NCLIENTS = nclients
     WORKLOAD = workload
+    BIND = bind
     port, t_start, duration, interval = start_q.get()
 
     qs = queries()
@@ -119,6 +124,13 @@ def _client_proc(pid, nthreads, nclients, start_q, out_q, workload="fixed"):
         cid = pid * nthreads + k
         conn = connect(port=port)
         i = cid
+        sched_it = None
+        if WORKLOAD == "jmx":
+            # the JMeter plan: this client belongs to one thread group and walks its templates in
+            # random order per iteration, the shared CSV cursors giving each iteration's parameters
+            from spark_druid_olap_amd.models import bi
+
+            sched_it = bi.client_schedule(cid, NCLIENTS, BIND)
         # stagger the open-loop schedules so the aggregate arrival rate is uniform
         nxt = t_start + (cid * interval / max(1, NCLIENTS)) if interval else t_start
         while True:
@@ -134,7 +146,10 @@ def _client_proc(pid, nthreads, nclients, start_q, out_q, workload="fixed"):
                 if now > t_start + duration:
                     break
                 sched = now
-            name, sql = qs[(i * 7919) % len(qs)] if WORKLOAD == "varied" else qs[i % len(qs)]
+            if sched_it is not None:
+                name, sql = next(sched_it)
+            else:
+                name, sql = qs[(i * 7919) % len(qs)] if WORKLOAD == "varied" else qs[i % len(qs)]
             i += NCLIENTS if WORKLOAD == "varied" else 1
             err = None
             try:
@@ -158,6 +173,7 @@ def _client_proc(pid, nthreads, nclients, start_q, out_q, workload="fixed"):
 
 
 NCLIENTS = 1
+BIND = "years"
 
 
 def pct(xs, p):
@@ -180,15 +196,19 @@ def main():
     ap.add_argument("--server", default="native", choices=["native", "python"],
                     help="native C++ gateway (server/csrc/hs2_gateway.cpp) or the pure-Python server")
     ap.add_argument("--sample", default=None, help="write a sampling profile of the server threads here")
-    ap.add_argument("--workload", default="fixed", choices=["fixed", "varied"],
-                    help="fixed: the 8 benchmark texts; varied: ~2,000 distinct parameterizations")
+    ap.add_argument("--workload", default="fixed", choices=["fixed", "varied", "jmx"],
+                    help="fixed: the 8 benchmark texts; varied: ~2,000 distinct parameterizations; jmx: the "
+                         "reference's BI plan (docs/bi-benchmark/snap-sales-demo.jmx, models/bi)")
+    ap.add_argument("--bind", default="years", choices=["years", "jmeter"],
+                    help="jmx workload: CSV binding (models/bi: 'jmeter' reproduces the plan's ccode overwrite)")
     ap.add_argument("--coalesce", default="on", choices=["on", "off"],
                     help="off: every statement executes (identical queued statements are not shared)")
     ap.add_argument("--prewarm", type=int, default=0,
                     help="varied workload: plan + compile this many distinct texts before the clock starts")
     a = ap.parse_args()
-    global WORKLOAD
+    global WORKLOAD, BIND
     WORKLOAD = a.workload
+    BIND = a.bind
     os.environ["SDO_COALESCE"] = "1" if a.coalesce == "on" else "0"
     NCLIENTS = a.clients
     nthreads = max(1, a.clients // a.procs)
@@ -197,7 +217,7 @@ def main():
     ctx = mp.get_context("spawn")
     res_q = ctx.Queue()
     start_q = ctx.Queue()
-    ps = [ctx.Process(target=_client_proc, args=(i, nthreads, a.clients, start_q, res_q, a.workload))
+    ps = [ctx.Process(target=_client_proc, args=(i, nthreads, a.clients, start_q, res_q, a.workload, a.bind))
           for i in range(nproc)]
     for p in ps:
         p.start()
@@ -215,6 +235,10 @@ def main():
     s.register_datasource(ds)
     s.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)
     s.sql(tpch.druid_ddl(source="orderLineItemPartSupplierBase", datasource="tpch", with_column_mapping=False))
+    if a.workload == "jmx":
+        from spark_druid_olap_amd.models import bi
+
+        bi.register(s)  # sales_demo_source (a shared view: every client session sees it)
     exec_cost = []  # (thread CPU s, wall s) of every server-side execution
     if a.server == "native":
         from spark_druid_olap_amd.server.gateway import NativeHiveServer
@@ -239,7 +263,16 @@ def main():
     # --prewarm texts; the rest are planned on first sight, inside the measured window)
     with connect(port=srv.port) as c:
         qs = queries()
-        warm = qs if a.workload == "fixed" else qs[:max(len(qs) and 8, a.prewarm)]
+        if a.workload == "jmx":
+            # one text per template (the shapes' kernels), like the varied workload's 8
+            seen_t, warm = set(), []
+            for n, q in qs:
+                if n not in seen_t:
+                    seen_t.add(n)
+                    warm.append((n, q))
+            warm += qs[len(warm):max(len(warm), a.prewarm)]
+        else:
+            warm = qs if a.workload == "fixed" else qs[:max(len(qs) and 8, a.prewarm)]
         for _, sql in warm:
             c.cursor().execute(sql).fetchall()
     interval = (a.clients / a.qps) if a.qps > 0 else 0.0
@@ -288,6 +321,7 @@ def main():
         per[name] = {"n": len(xs), "p50_ms": pct(xs, 50), "p99_ms": pct(xs, 99)}
     out = {"metric": "thrift_concurrent_latency", "clients": nproc * nthreads, "target_qps": a.qps,
            "workload": a.workload, "coalesce": a.coalesce, "distinct_texts": len(qs),
+           "bind": a.bind if a.workload == "jmx" else None,
            "executions_per_s": round((ex1 - ex0) / a.duration, 2),
            "achieved_qps": round(len(lat) / span, 2) if span > 0 else None, "queries": len(res),
            "errors": len(errs), "p50_ms": pct(lat, 50), "p90_ms": pct(lat, 90), "p99_ms": pct(lat, 99),
