@@ -108,7 +108,9 @@ def _jit_for(prog, mode: int, hll_lds: bool, m: int, shared: bool = False):
     return js
 
 
-def _jit_build(prog, mode: int, hll_lds: bool, m: int, shared: bool = False):
+def _jit_build(prog, mode: int, hll_lds: bool, m: int, shared: bool = False, load: bool = True):
+    """(``load=False``: compile only -- tools/jit_isa.py inspects the exact kernel a scan would run
+    on a host without a GPU.)"""
     from ..ops import jit
 
     nplanes = sum(2 if column_tensor_size(prog, c) == 8 else 1 for c in prog.cols)
@@ -128,8 +130,9 @@ def _jit_build(prog, mode: int, hll_lds: bool, m: int, shared: bool = False):
             if lay.total <= budget and (reg or shared or mode != D.M_DENSE_LDS or lay.ncopy >= 4
                                         or U == prefs[-1]):
                 try:
-                    return jit.JitScan(prog, mode, U, hll_lds, m, bool(native.narrow4()), reg=reg, pipe=pipe,
-                                       budget=budget, regstage=regstage, shared=shared)
+                    return jit.JitScan(prog, mode, U, hll_lds, m, bool(native.narrow4()) if load else True,
+                                       load=load, reg=reg, pipe=pipe, budget=budget, regstage=regstage,
+                                       shared=shared)
                 except Exception as e:  # pragma: no cover - compile problems fall back loudly
                     import warnings
 
@@ -282,7 +285,7 @@ class PreparedScan:
         b.cap = cap
         rows = cap if self.mode == D.M_HASH else prog.G
         b.rows = rows
-        b.init_row = torch.tensor([init for _, init in prog.slots], dtype=torch.int64, device=dev)
+        b.init_row = _init_row(dev, tuple(int(init) for _, init in prog.slots))
         if self.pres_bytes:
             # padded to whole 8-byte words (the fused reset zeroes words; padding bytes stay 0 and
             # never compact)
@@ -325,7 +328,7 @@ class PreparedScan:
         b.part = None
         if self.mode == D.M_PART:
             b.part = self._part_bufs(d)
-        b.desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
+        b.desc = _upload(d.view(np.uint8), dev)
         b.run_args = b.noreset_args = None
         b.fetch = None
         if self.mode not in (D.M_HASH, D.M_PART):
@@ -883,6 +886,40 @@ def _grid(dev: torch.device, total_chunks: int, lds_total: int) -> int:
     need = max(1, (total_chunks + waves - 1) // waves)
     per_cu = max(1, min(BLOCKS_PER_CU, (160 * 1024) // max(lds_total, 1)))
     return max(1, min(need, num_cus(dev) * per_cu))
+
+
+_INIT_ROWS: dict = {}
+_init_lock = threading.Lock()
+
+
+def _init_row(dev, inits: tuple) -> torch.Tensor:
+    """Device copy of a slot-init row, shared by every prepared scan with the same slots (read-only:
+    the fused reset copies it into the accumulators)."""
+    k = (str(dev), inits)
+    t = _INIT_ROWS.get(k)
+    if t is None:
+        with _init_lock:
+            t = _INIT_ROWS.get(k)
+            if t is None:
+                t = _upload(np.asarray(inits, dtype=np.int64).view(np.uint8), dev).view(torch.int64)
+                if dev.type == "cuda":
+                    torch.cuda.current_stream(dev).synchronize()  # (once: other streams read it)
+                _INIT_ROWS[k] = t
+    return t
+
+
+def _upload(buf: np.ndarray, dev) -> torch.Tensor:
+    """Host bytes -> a new device tensor without a synchronous pageable copy: staged through the
+    caching pinned allocator and copied on the current stream (the staging block is not reused
+    before that copy completes).  A statement first seen by a server allocates its descriptor this
+    way on every slot; the pageable ``.to(dev)`` blocked the serving thread for each."""
+    if dev.type != "cuda":
+        return torch.from_numpy(buf.copy())
+    h = torch.empty(buf.nbytes, dtype=torch.uint8, pin_memory=True)
+    h.numpy()[:] = buf.reshape(-1)
+    out = torch.empty(buf.nbytes, dtype=torch.uint8, device=dev)
+    out.copy_(h, non_blocking=True)
+    return out
 
 
 def _nonzero_big(mask: torch.Tensor) -> torch.Tensor:

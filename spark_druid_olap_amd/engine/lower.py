@@ -544,7 +544,7 @@ class Lowerer:
 
     def _time_values(self) -> np.ndarray:
         if self._tv_cache is None:
-            self._tv_cache = np.unique(self.ds.time_host)
+            self._tv_cache = self.ds.distinct_times()
         return self._tv_cache
 
     def _time_filter(self, f) -> tuple:
@@ -563,6 +563,10 @@ class Lowerer:
             return b_or([("time", iv.lo, iv.hi) for iv in (Interval.parse(s) for s in f.intervals)])
         # generic predicate over the distinct time values -> set of allowed time units
         if isinstance(f, S.JavascriptFilterSpec):
+            pv = getattr(f, "_pyvec", None)
+            if pv is not None:  # vectorised over the distinct time values (SQL planner)
+                tv = self._time_values()
+                return ("timeset", tv[np.asarray(pv(tv.astype(np.int64) * u), dtype=bool)])
             py = getattr(f, "_pyfn", None)
             if py is None:
                 jf = compile_function(f.function)

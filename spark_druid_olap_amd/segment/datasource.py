@@ -179,6 +179,25 @@ class DataSource:
         return n
 
     # ----------------------------------------------------------------- time
+    def distinct_times(self) -> np.ndarray:
+        """The distinct __time values (in time units), ascending -- cached.  The column is sorted,
+        so this hops from value to value with binary searches (~2,500 days at SF100: a few
+        milliseconds, where np.unique over 600M rows took seconds per lowered query)."""
+        tv = self.__dict__.get("_distinct_times")
+        if tv is None:
+            t = self.time_host
+            if len(t) > 1 and not bool((t[1:] >= t[:-1]).all()):  # (once per datasource)
+                tv = self._distinct_times = np.unique(t)
+                return tv
+            out = []
+            i, n = 0, len(t)
+            while i < n:
+                v = t[i]
+                out.append(v)
+                i = int(np.searchsorted(t, v, side="right"))
+            tv = self._distinct_times = np.asarray(out, dtype=t.dtype)
+        return tv
+
     def rows_for_interval(self, lo_ms: int, hi_ms: int):
         """Half-open row range whose __time is in [lo_ms, hi_ms)."""
         u = self.time_unit_ms

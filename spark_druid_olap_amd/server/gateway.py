@@ -196,6 +196,9 @@ class NativeHiveServer(HiveThriftServer):
 
     # ------------------------------------------------------------------ lifecycle
     def start(self) -> "NativeHiveServer":
+        from ..utils.memory import serving_gc
+
+        serving_gc()
         mod = load_native()
         self._gw = mod.Gateway(self.host, self.port, self._forward)
         # SDO_COALESCE=0: every statement executes (engine throughput, not result sharing)

@@ -128,6 +128,9 @@ class HiveThriftServer:
 
     # ------------------------------------------------------------------------------ lifecycle
     def start(self) -> "HiveThriftServer":
+        from ..utils.memory import serving_gc
+
+        serving_gc()
         server = self
 
         class Handler(socketserver.BaseRequestHandler):

@@ -596,6 +596,7 @@ class DruidRewriter:
             js = js_single_column_fn(e, r, "__time")
             f = S.JavascriptFilterSpec("__time", js)
             f._pyfn = _time_predicate(e, r, c)  # type: ignore[attr-defined]
+            f._pyvec = _time_predicate_vec(e, r, c)  # type: ignore[attr-defined]
             return f
         raise NotPushable(f"predicate over metric {c.column}: {e.sql()}")
 
@@ -1536,6 +1537,34 @@ def _time_value(ms: int, c):
     if t in ("bigint", "int"):
         return int(ms)
     return ts
+
+
+def _time_values_vec(ms: np.ndarray, c) -> pd.Series:
+    """``_time_value`` over an array of epoch milliseconds (one evaluation per distinct time value
+    of the shard, vectorised: the BI templates' ``substr(l_shipdate, 1, 4) = '1995'`` over ~2,500
+    days costs one pandas expression instead of 2,500 interpreted ones)."""
+    ms = np.asarray(ms, dtype=np.int64)
+    idx = pd.to_datetime(ms, unit="ms")
+    t = base(c.sql_type)
+    if t == "string":
+        if len(ms) and (ms % DAY_MS == 0).all():
+            return pd.Series(idx.strftime("%Y-%m-%d"), dtype=object)
+        return pd.Series([_time_value(int(x), c) for x in ms], dtype=object)
+    if t == "date":
+        return pd.Series(idx.normalize())
+    if t in ("bigint", "int"):
+        return pd.Series(ms)
+    return pd.Series(idx)
+
+
+def _time_predicate_vec(e: A.Expr, r: A.Ref, c) -> Callable:
+    def fn(ms):
+        s = to_series(_time_values_vec(ms, c), c.sql_type) if base(c.sql_type) == "string" else _time_values_vec(ms, c)
+        v = evaluate(e, Frame({r.rid: s}, len(s)))
+        if not is_vec(v):
+            return np.full(len(s), bool(v) if v is not None else False)
+        return v.fillna(False).to_numpy(dtype=bool)
+    return fn
 
 
 def _time_predicate(e: A.Expr, r: A.Ref, c) -> Callable:
