@@ -324,7 +324,8 @@ class PreparedScan:
                  [h.data_ptr() for h in (b.hll32 or b.hll)], hll_offs,
                  unroll=UNROLL, cache_off=cache_off, wave_bytes=wave_bytes)
         self.lds_total = total
-        self.grid = _grid(dev, int(d[0]["total_chunks"]), self.jit.lay.total if self.jit else total)
+        self._total_chunks = int(d[0]["total_chunks"])
+        self.grid = _grid(dev, self._total_chunks, self.jit.lay.total if self.jit else total, self.jit)
         b.part = None
         if self.mode == D.M_PART:
             b.part = self._part_bufs(d)
@@ -501,12 +502,16 @@ class PreparedScan:
         kernel handle)."""
         with self._slot_lock:
             self.jit = js
+            if getattr(self, "_total_chunks", None) is not None:
+                # the specialized kernel's register use may allow a different resident grid
+                self.grid = _grid(self.dev, self._total_chunks, js.lay.total, js)
             for b in self._slots.values():
                 for attr in ("run_args", "noreset_args"):
                     a = getattr(b, attr)
                     if a is not None:
                         a = list(a)
                         a[-6] = js.handle  # (jit, desc, grid, block, lds, unroll)
+                        a[-4] = int(self.grid)
                         setattr(b, attr, tuple(a))
 
     # ------------------------------------------------------------------ run
@@ -767,7 +772,7 @@ class PreparedEmit:
         d = pack(ep, D.M_PART, 0, 0, 0, 0, 0, 0, 0, 0, 0, [], [], unroll=UNROLL, cache_off=cache_off,
                  wave_bytes=wave_bytes)
         self.nch = int(d[0]["total_chunks"])
-        self.grid = _grid(self.dev, self.nch, self.jit.lay.total)
+        self.grid = _grid(self.dev, self.nch, self.jit.lay.total, self.jit)
         cap = self.nch * D.CHUNK_ROWS
         if 2 * cap >= (1 << 32):
             raise RuntimeError("emit: shard too large for u32 offsets")
@@ -832,7 +837,7 @@ class PreparedMask:
                              unroll=UNROLL, cache_off=self._layout[0], wave_bytes=self._layout[1])
                     desc = torch.from_numpy(d.view(np.uint8).copy()).to(self.dev)
                     self.grid = _grid(self.dev, int(d[0]["total_chunks"]),
-                                      self.jit.lay.total if self.jit else self.lds_total)
+                                      self.jit.lay.total if self.jit else self.lds_total, self.jit)
                     b = self._slots[slot] = (mask, count, desc)
         return b
 
@@ -880,11 +885,15 @@ def part_layout(prog) -> dict:
             "fields": fields, "rw": rw}
 
 
-def _grid(dev: torch.device, total_chunks: int, lds_total: int) -> int:
-    """Persistent grid: enough 8-wave blocks for the chunks, at most what the CUs hold at once."""
+def _grid(dev: torch.device, total_chunks: int, lds_total: int, jit=None) -> int:
+    """Persistent grid: enough 8-wave blocks for the chunks, at most what the CUs hold at once --
+    by LDS and, for a JIT kernel, by its compiled register use (the chunks are dealt to waves
+    statically, so blocks beyond the resident set would run as a second, partial wave)."""
     waves = BLOCK // 64
     need = max(1, (total_chunks + waves - 1) // waves)
     per_cu = max(1, min(BLOCKS_PER_CU, (160 * 1024) // max(lds_total, 1)))
+    if jit is not None:
+        per_cu = max(1, min(per_cu, jit.occupancy()))
     return max(1, min(need, num_cus(dev) * per_cu))
 
 

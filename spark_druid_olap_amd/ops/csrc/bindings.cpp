@@ -356,6 +356,22 @@ static void module_launch(int h, uint64_t desc, int grid, int block, int lds, ui
         "jit kernel launch");
 }
 
+// Resident workgroups per CU of a JIT kernel at this block size and dynamic LDS (VGPR / SGPR / LDS
+// limits of the compiled code): the persistent scan grid is sized to what is resident at once --
+// a grid of 3 blocks per CU for a 117-VGPR kernel that fits 2 leaves a second, half-empty wave of
+// workgroups (TPC-H Q1 at SF100: 1.56 -> 1.46 ms at 2 per CU).
+static int module_occupancy(int h, int block, int lds) {
+  hipFunction_t fn;
+  {
+    std::lock_guard<std::mutex> g(g_jit_mu);
+    if (h < 0 || h >= (int)g_jit.size()) throw std::invalid_argument("bad jit handle");
+    fn = g_jit[h].fn;
+  }
+  int n = 0;
+  check(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, block, (size_t)lds), "occupancy");
+  return n;
+}
+
 // One host call per execution of a prepared scan: the fused reset of its slot buffers, then the
 // specialized kernel (or the interpreter) -- the Python side caches every argument, so a small
 // query's launch path is a single pybind call (the per-call Python work showed as ~25 us of a
@@ -649,6 +665,7 @@ PYBIND11_MODULE(_sdo_native, m) {
     return module_load(c, name);
   });
   m.def("module_launch", &module_launch);
+  m.def("module_occupancy", &module_occupancy);
   m.def("run_scan", &run_scan);
   m.def("fetch_small", &fetch_small);
   m.def("stream_sync", &stream_sync);

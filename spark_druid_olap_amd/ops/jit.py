@@ -1400,6 +1400,15 @@ class JitScan:
         return JitScan(prog, mode, U, hll_lds, m, narrow4, load, reg=reg, pipe=pipe, budget=budget,
                        regstage=regstage, shared=shared, literals=True)
 
+    def occupancy(self) -> int:
+        """Resident 512-thread workgroups per CU of the compiled kernel (registers and LDS)."""
+        occ = self.__dict__.get("_occ")
+        if occ is None:
+            from . import native
+
+            occ = self._occ = max(1, int(native.load().module_occupancy(self.handle, W * 64, int(self.lay.total))))
+        return occ
+
     def launch(self, desc: torch.Tensor, grid: int) -> None:
         from . import native
 

@@ -1038,8 +1038,11 @@ class DruidRewriter:
         ref map sends each visible ref id to the DruidQuery output ref it is a plain copy of."""
         m: Dict[int, int] = {}
         chain = []
-        while isinstance(p, P.Project):
-            chain.append(p)
+        while isinstance(p, P.Project) or (isinstance(p, P.Filter) and p.__dict__.get("_absorbed")):
+            # (a HAVING absorbed into the groupBy's havingSpec: the engine applies it before the
+            # limitSpec, so ORDER BY / LIMIT above it push down too -- the host Filter re-applies it)
+            if isinstance(p, P.Project):
+                chain.append(p)
             p = p.child
         if not isinstance(p, P.DruidQuery) or not p.info.get("groupby"):
             return None, None
@@ -1230,6 +1233,7 @@ class DruidRewriter:
             dq.__dict__.pop("_deferred", None)
             return None
         dq.spec = q.copy(having=conv(f.cond))
+        f._absorbed = True
         return None
 
     def _limit(self, l: P.Limit) -> Optional[P.Plan]:

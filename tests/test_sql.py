@@ -176,6 +176,17 @@ def test_having_order_limit(sess):
     d = sess.sql(f"select c_nation, count(*) c from {T} group by c_nation order by c_nation limit 3")
     assert [r[0] for r in d.collect()] == sorted(r[0] for r in sess.sql(
         f"select distinct c_nation from {B}").collect())[:3]
+    # ORDER BY / LIMIT above a pushed HAVING push down too (the engine applies the havingSpec
+    # before the limitSpec): the BI workload's TopVolumeCustomers over ~180M groups at SF100
+    q = (f"select c_name, month(o_orderdate), sum(o_totalprice) totprice, sum(l_quantity) totqty from {T} "
+         f"group by c_name, month(o_orderdate) having sum(l_quantity) > 30 order by totprice desc limit 3")
+    d = sess.sql(q)
+    spec = d.druid_query_specs()[0]
+    assert spec.having is not None and spec.limitSpec is not None and spec.limitSpec.limit == 3 \
+        and spec.limitSpec.columns
+    got = d.collect()
+    exp = sess.sql(q.replace(T, B)).collect()
+    assert [r[0] for r in got] == [r[0] for r in exp] and len(got) == 3
 
 
 def test_topn_rewrite(sess):
