@@ -261,7 +261,7 @@ class PreparedScan:
             with self._slot_lock:
                 b = self._slots.get(slot)
                 if b is None:
-                    b = self._slots[slot] = self._alloc(self.cap)
+                    b = self._slots[slot] = _with_eviction(lambda: self._alloc(self.cap), self, slot)
             _buffers_acquired(self, slot, b)
         else:
             _buffers_used(self, slot)
@@ -651,18 +651,30 @@ class PreparedScan:
 BUF_BUDGET = int(os.environ.get("SDO_SCAN_BUF_BUDGET", "0"))  # 0: 35% of the device's memory
 
 
+HEADROOM = 16 << 30  # device memory kept free for a statement's temporaries (sorts, gathers, results)
+
+
 def _budget() -> int:
+    """Bytes the cached per-slot scan buffers may hold: 35% of the device, and never more than what
+    is left once everything else allocated (the resident shards, the partition scratch of every
+    slot, results in flight) and ``HEADROOM`` are accounted for -- a many-client BI workload over
+    hundreds of statements with 150M-group tables otherwise grows into an out-of-memory error."""
     if BUF_BUDGET > 0:
         return BUF_BUDGET
     b = _budget_cache.get("b")
+    total = _budget_cache.get("total")
     if b is None:
-        b = 24 << 30
+        b, total = 24 << 30, 0
         try:
             if torch.cuda.is_available():
-                b = max(b, int(0.35 * torch.cuda.get_device_properties(torch.cuda.current_device()).total_memory))
+                total = int(torch.cuda.get_device_properties(torch.cuda.current_device()).total_memory)
+                b = max(b, int(0.35 * total))
         except Exception:  # noqa: BLE001
             pass
-        _budget_cache["b"] = b
+        _budget_cache["b"], _budget_cache["total"] = b, total
+    if total:
+        other = torch.cuda.memory_allocated() - _buf_total[0]
+        b = min(b, max(1 << 30, total - other - HEADROOM))
     return b
 
 
@@ -679,9 +691,12 @@ def _scratch(dev, slot, name: str, nelem: int) -> torch.Tensor:
     k = (str(dev), slot, name)
     with _scratch_lock:
         t = _SCRATCH.get(k)
-        if t is None or t.numel() < nelem:
-            _SCRATCH[k] = None
-            t = _SCRATCH[k] = torch.empty(max(1, nelem), dtype=torch.int32, device=dev)
+        if t is not None and t.numel() >= nelem:
+            return t
+        _SCRATCH[k] = None
+    t = _with_eviction(lambda: torch.empty(max(1, nelem), dtype=torch.int32, device=dev), None, slot)
+    with _scratch_lock:
+        _SCRATCH[k] = t
     return t
 _buf_lru: "OrderedDict[tuple, tuple]" = OrderedDict()   # (id(prep), slot) -> (weakref(prep), bytes)
 _buf_total = [0]
@@ -721,6 +736,32 @@ def _buffers_acquired(prep, slot, b) -> None:
         if p is not None:
             with p._slot_lock:
                 p._slots.pop(sl, None)
+
+
+def _with_eviction(fn, prep, slot):
+    """Run an allocation; on a device out-of-memory error release every other prepared scan's
+    cached slot buffers (least recently used first: all of them) and the allocator's free blocks,
+    then try once more."""
+    try:
+        return fn()
+    except torch.OutOfMemoryError:
+        victims = []
+        with _buf_lock:
+            for k in list(_buf_lru):
+                if k == (id(prep), slot):
+                    continue
+                ref, n = _buf_lru.pop(k)
+                _buf_total[0] -= n
+                victims.append((ref(), k[1]))
+        for p, sl in victims:
+            if p is not None:
+                with p._slot_lock:
+                    p._slots.pop(sl, None)
+        if prep is not None:
+            with _scratch_lock:
+                _SCRATCH.clear()
+        torch.cuda.empty_cache()
+        return fn()
 
 
 def _buffers_used(prep, slot) -> None:

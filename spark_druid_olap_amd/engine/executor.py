@@ -323,6 +323,9 @@ class PreparedQuery:
                 if root_only and self.world.rank != 0:
                     # a peer: the root answers; finalize an empty slice for the schema (on the
                     # device: device-resident FD / decode tables must not be copied to the host)
+                    from ..parallel.p2p import check_status
+
+                    check_status(part)
                     part = empty_partials(prog, self.ds.device)
                 cols = finalize(prog, part, getattr(self, "out_types", None))
             t3 = time.perf_counter()
@@ -401,9 +404,14 @@ class PreparedQuery:
         disjoint = bool(self.ds.shard_key) and any(k.col == self.ds.shard_key for k in prog.keys)
         with T.span("sdo.merge"):
             part = merge_partials(self.world, prog, part, disjoint_keys=disjoint, local_error=err,
-                                  finish="local" if self.world.distributed else "all")
+                                  finish="local" if self.world.distributed else "all", defer_status=True)
+        merged = part
         part, hv = self._device_having(prog, part)
         part = self._device_prune(prog, part, hv)
+        if part is not merged:
+            from ..parallel.p2p import check_status
+
+            check_status(merged)  # (a P2P merge's status words: read now, the state was transformed)
         if part.scattered:
             from ..parallel.merge import gather_groups
 

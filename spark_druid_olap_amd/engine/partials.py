@@ -27,6 +27,10 @@ class Partials:
     # small dense executions replayed as a HIP graph (engine/device_exec.py run_graph_small): the
     # accumulator table and the HLL estimates already on the host, as finalize's _fetch_small returns
     host: Optional[List[np.ndarray]] = None
+    # peer-to-peer merge (parallel/p2p.py): every rank's status word, still on the device -- read
+    # with the result's device-to-host copy (finalize) instead of a separate host synchronisation
+    status_dev: Optional[torch.Tensor] = None
+    status_rank: int = 0
 
     @property
     def rows(self) -> int:
@@ -125,16 +129,22 @@ def _native():
     return _NATIVE[0]
 
 
-def _fetch_small(acc: torch.Tensor, hll: List[torch.Tensor], G: int, p: int) -> List[np.ndarray]:
+def _fetch_small(acc: torch.Tensor, hll: List[torch.Tensor], G: int, p: int,
+                 status: Optional[torch.Tensor] = None) -> List[np.ndarray]:
     """[acc as host int64 [G, ns], estimates per register block...] of a small dense state,
-    read back through per-thread pinned / device scratch buffers (reused across executions)."""
+    read back through per-thread pinned / device scratch buffers (reused across executions).
+    ``status``: a P2P merge's status words, copied in the same stream before the one sync and
+    returned last."""
     native = _native()
 
     nb = acc.numel() * 8
     need = nb + len(hll) * G * 8
+    ns = 0 if status is None else status.numel() * 8
     host = getattr(_STAGE, "host", None)
-    if host is None or host.numel() < need:
-        host = _STAGE.host = torch.empty(max(need, 1 << 16), dtype=torch.uint8, pin_memory=True)
+    if host is None or host.numel() < need + ns:
+        host = _STAGE.host = torch.empty(max(need + ns, 1 << 16), dtype=torch.uint8, pin_memory=True)
+    if status is not None:
+        host[need: need + ns].copy_(status.view(torch.uint8), non_blocking=True)
     est = getattr(_STAGE, "est", None)
     if hll and (est is None or est.numel() < len(hll) * G or est.device != acc.device):
         est = _STAGE.est = torch.empty(max(len(hll) * G, 4096), dtype=torch.float64, device=acc.device)
@@ -143,6 +153,8 @@ def _fetch_small(acc: torch.Tensor, hll: List[torch.Tensor], G: int, p: int) -> 
     out = [buf[:nb].view(np.int64).reshape(acc.shape)]
     for i in range(len(hll)):
         out.append(buf[nb + i * G * 8: nb + (i + 1) * G * 8].view(np.float64))
+    if status is not None:
+        out.append(buf[need: need + ns].view(np.int64).copy())
     return out
 
 
@@ -276,6 +288,8 @@ def _decode_key(kc, ids):
 
 def finalize(prog, parts: Partials, out_types: Optional[Dict[str, str]] = None) -> Dict[str, np.ndarray]:
     """Decode groups into host columns: key outputs then aggregator outputs (Druid types).
+    A P2P-merged state's status words are read with its result copy; any other consumer checks
+    them first (parallel/p2p.py check_status).
 
     Large (sparse) results are decoded on the device and cross the host link narrow: key ids at
     their dictionary's width, numeric dictionary keys as final SQL-typed values when ``out_types``
@@ -297,7 +311,15 @@ def finalize(prog, parts: Partials, out_types: Optional[Dict[str, str]] = None) 
             elif parts.acc.is_cuda and parts.acc.is_contiguous():
                 # estimates + both copies + the sync in one native call (bindings.cpp fetch_small),
                 # through this thread's pinned staging buffer; the fancy indexing below copies out
-                host = _fetch_small(parts.acc, list(parts.hll) if want_est else [], G, prog.hll_p)
+                host = _fetch_small(parts.acc, list(parts.hll) if want_est else [], G, prog.hll_p,
+                                    parts.status_dev)
+                if parts.status_dev is not None:
+                    sts = host.pop()
+                    parts.status_dev = None
+                    if sts.any():
+                        from ..parallel.fault import raise_if_failed
+
+                        raise_if_failed(sts.tolist(), parts.status_rank, None)
             else:
                 if want_est and parts.acc.is_cuda:
                     from ..ops import native
@@ -307,6 +329,10 @@ def finalize(prog, parts: Partials, out_types: Optional[Dict[str, str]] = None) 
                         native.hll_estimate(h.contiguous(), G, prog.hll_p, e)
                         est_dev.append(e)
                 host = d2h([parts.acc] + est_dev)
+            if parts.status_dev is not None:  # (not fetched with the copy above)
+                from ..parallel.p2p import check_status
+
+                check_status(parts)
             acc_h = host[0]
             gid = np.flatnonzero(acc_h[:, 0] > 0)
             acc_h = acc_h[gid]
@@ -324,6 +350,10 @@ def finalize(prog, parts: Partials, out_types: Optional[Dict[str, str]] = None) 
                     did = orig[did]
                 derived_agg_vals.append(lut[torch.from_numpy(did).to(lut.device)].cpu().numpy())
         else:
+            if parts.status_dev is not None:
+                from ..parallel.p2p import check_status
+
+                check_status(parts)
             parts = parts.compact()
     if parts.kind == "sparse":
         # decode key components on the device, then one pinned D2H of every array

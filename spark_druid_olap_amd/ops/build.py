@@ -18,7 +18,7 @@ HERE = Path(__file__).resolve().parent
 CSRC = HERE / "csrc"
 ARCH = os.environ.get("SDO_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["olap_scan.hip", "post_scan.hip", "sketch.hip", "partition.hip", "bindings.cpp"]
+SOURCES = ["olap_scan.hip", "post_scan.hip", "sketch.hip", "partition.hip", "p2p.hip", "bindings.cpp"]
 
 
 def _ext_suffix() -> str:

@@ -8,6 +8,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 #include <algorithm>
+#include <cstring>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -64,6 +65,28 @@ __global__ void part_split_kernel(const uint32_t* in, int RW, const uint32_t* se
 __global__ void part_agg_kernel(const uint32_t* recs, int RW, const uint32_t* base, int64_t nsub, int64_t G, int shift,
                                 PartFields f, uint64_t* gacc, PartHaving hv, int64_t* out_keys,
                                 unsigned long long* out_count, int64_t cap);
+// p2p.hip
+constexpr int P2P_MAX_RANKS = 8;
+constexpr int P2P_MAX_SLOTS = 64;
+struct P2PArgs {
+  uint64_t mbox[P2P_MAX_RANKS];
+  int nranks;
+  int rank;
+  uint64_t epoch;
+  int64_t slot_bytes;
+  int64_t nacc;
+  int64_t nhll;
+  int nslots;
+  int ops[P2P_MAX_SLOTS];
+  const int64_t* acc_src;
+  const uint8_t* hll_src;
+  int64_t status;
+  int64_t* acc_out;
+  uint8_t* hll_out;
+  int64_t* status_out;
+  int64_t timeout_ticks;
+};
+__global__ void p2p_merge_kernel(P2PArgs a);
 }  // namespace sdo
 
 namespace py = pybind11;
@@ -372,6 +395,21 @@ static int module_occupancy(int h, int block, int lds) {
   return n;
 }
 
+static py::dict module_attrs(int h) {
+  hipFunction_t fn;
+  {
+    std::lock_guard<std::mutex> g(g_jit_mu);
+    if (h < 0 || h >= (int)g_jit.size()) throw std::invalid_argument("bad jit handle");
+    fn = g_jit[h].fn;
+  }
+  py::dict d;
+  int v = 0;
+  if (hipFuncGetAttribute(&v, HIP_FUNC_ATTRIBUTE_NUM_REGS, fn) == hipSuccess) d["num_regs"] = v;
+  if (hipFuncGetAttribute(&v, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, fn) == hipSuccess) d["local_bytes"] = v;
+  if (hipFuncGetAttribute(&v, HIP_FUNC_ATTRIBUTE_MAX_THREADS_PER_BLOCK, fn) == hipSuccess) d["max_threads"] = v;
+  return d;
+}
+
 // One host call per execution of a prepared scan: the fused reset of its slot buffers, then the
 // specialized kernel (or the interpreter) -- the Python side caches every argument, so a small
 // query's launch path is a single pybind call (the per-call Python work showed as ~25 us of a
@@ -606,6 +644,70 @@ static void part_agg(uint64_t recs, int RW, uint64_t base, int64_t nsub, int64_t
   check(hipGetLastError(), "part_agg_kernel launch");
 }
 
+// ---------------------------------------------------------------------------------------------
+// Peer-to-peer mailboxes (p2p.hip): one hipMalloc per (process group, rank), exported with an IPC
+// handle and opened by every peer; the small dense merge is then one kernel per rank.
+static py::tuple p2p_alloc(int64_t bytes) {
+  void* p = nullptr;
+  check(hipMalloc(&p, (size_t)bytes), "p2p mailbox hipMalloc");
+  check(hipMemset(p, 0, (size_t)bytes), "p2p mailbox clear");
+  check(hipDeviceSynchronize(), "p2p mailbox clear sync");
+  hipIpcMemHandle_t h;
+  check(hipIpcGetMemHandle(&h, p), "hipIpcGetMemHandle");
+  return py::make_tuple((uint64_t)p, py::bytes((const char*)&h, sizeof(h)));
+}
+
+static uint64_t p2p_open(py::bytes handle) {
+  std::string s(handle);
+  if (s.size() != sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("p2p_open: bad IPC handle size");
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, s.data(), sizeof(h));
+  void* p = nullptr;
+  check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+  return (uint64_t)p;
+}
+
+static void p2p_close(uint64_t p) { (void)hipIpcCloseMemHandle((void*)p); }
+static void p2p_free(uint64_t p) { (void)hipFree((void*)p); }
+
+static void p2p_merge(std::vector<uint64_t> mbox, int rank, uint64_t epoch, int64_t slot_bytes, uint64_t acc_src,
+                      int64_t nacc, uint64_t hll_src, int64_t nhll, std::vector<int> ops, int64_t status,
+                      uint64_t acc_out, uint64_t hll_out, uint64_t status_out, double timeout_s, uint64_t stream) {
+  sdo::P2PArgs a{};
+  const int n = (int)mbox.size();
+  if (n < 1 || n > sdo::P2P_MAX_RANKS) throw std::invalid_argument("p2p_merge: 1..8 ranks");
+  if (rank < 0 || rank >= n) throw std::invalid_argument("p2p_merge: rank");
+  if (ops.empty() || ops.size() > (size_t)sdo::P2P_MAX_SLOTS) throw std::invalid_argument("p2p_merge: 1..64 slots");
+  if (nacc < 0 || nacc % (int64_t)ops.size() != 0) throw std::invalid_argument("p2p_merge: accumulator words");
+  if (nhll < 0 || nhll % 8 != 0) throw std::invalid_argument("p2p_merge: HLL bytes must be a multiple of 8");
+  if ((nacc + nhll / 8 + 1) * 8 > slot_bytes) throw std::invalid_argument("p2p_merge: state exceeds the mailbox");
+  if (epoch < 1) throw std::invalid_argument("p2p_merge: epoch >= 1");
+  for (int i = 0; i < n; ++i) {
+    if (!mbox[i]) throw std::invalid_argument("p2p_merge: unmapped mailbox");
+    a.mbox[i] = mbox[i];
+  }
+  for (size_t j = 0; j < ops.size(); ++j) {
+    if (ops[j] < 0 || ops[j] > 3) throw std::invalid_argument("p2p_merge: slot op");
+    a.ops[j] = ops[j];
+  }
+  a.nranks = n;
+  a.rank = rank;
+  a.epoch = epoch;
+  a.slot_bytes = slot_bytes;
+  a.nacc = nacc;
+  a.nhll = nhll;
+  a.nslots = (int)ops.size();
+  a.acc_src = (const int64_t*)acc_src;
+  a.hll_src = (const uint8_t*)hll_src;
+  a.status = status;
+  a.acc_out = (int64_t*)acc_out;
+  a.hll_out = (uint8_t*)hll_out;
+  a.status_out = (int64_t*)status_out;
+  a.timeout_ticks = (int64_t)(timeout_s * 1e8);  // wall clock: 100 MHz
+  hipLaunchKernelGGL(sdo::p2p_merge_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, a);
+  check(hipGetLastError(), "p2p_merge_kernel launch");
+}
+
 static int desc_size() { return (int)sizeof(sdo::ScanDesc); }
 
 static py::dict layout() {
@@ -666,6 +768,12 @@ PYBIND11_MODULE(_sdo_native, m) {
   });
   m.def("module_launch", &module_launch);
   m.def("module_occupancy", &module_occupancy);
+  m.def("module_attrs", &module_attrs);
+  m.def("p2p_alloc", &p2p_alloc);
+  m.def("p2p_open", &p2p_open);
+  m.def("p2p_close", &p2p_close);
+  m.def("p2p_free", &p2p_free);
+  m.def("p2p_merge", &p2p_merge);
   m.def("run_scan", &run_scan);
   m.def("fetch_small", &fetch_small);
   m.def("stream_sync", &stream_sync);

@@ -30,6 +30,7 @@ import torch
 
 from ..engine.partials import Partials, merge_sparse
 from ..ops import desc as D
+from . import p2p
 from .fault import STATUS_FAILED, STATUS_OK, raise_if_failed
 from .world import World
 
@@ -162,7 +163,8 @@ def start_dense_merge(world: World, prog, part: Partials, status: int, kind: Opt
 
 
 def merge_partials(world: World, prog, part: Partials, disjoint_keys: bool = False,
-                   local_error: Optional[BaseException] = None, finish: str = "all") -> Partials:
+                   local_error: Optional[BaseException] = None, finish: str = "all",
+                   defer_status: bool = False) -> Partials:
     """Merge this rank's partials with every other rank's.  ``local_error`` set = this rank failed
     its scan and ``part`` is a layout-compatible placeholder: the status word travels in the
     merge's own collective and every rank raises (parallel/fault.py).
@@ -177,6 +179,17 @@ def merge_partials(world: World, prog, part: Partials, disjoint_keys: bool = Fal
         return part
     status = STATUS_FAILED if local_error is not None else STATUS_OK
     plan = merge_plan_for(world, part, disjoint_keys)
+    if plan.kind in ("oneshot-allgather", "bucketed-allreduce") and p2p.fits(prog, part):
+        # small dense state: the peer-to-peer one-shot merge (one kernel per rank over IPC-mapped
+        # mailboxes, parallel/p2p.py) -- chosen from the layout and the group's agreed exchange
+        ex = p2p.exchange_for(world)
+        if ex is not None:
+            merged = ex.merge(prog, part, status)
+            if local_error is not None:
+                raise local_error  # (after publishing: the peers read this rank's failed status)
+            if not defer_status:
+                p2p.check_status(merged)
+            return merged
     if plan.kind == "oneshot-allgather":
         merged, sts = start_dense_merge(world, prog, part, status, plan.kind).wait()
         if local_error is not None or any(sts):

@@ -412,7 +412,8 @@ class Executor:
             return Batch(p.refs, cols, 1)
         for r, (name, sqlt, kind) in zip(p.refs, p.columns):
             cols[r.rid] = druid_value_lazy(res.data[name], sqlt, kind, n)
-        self.druid_stats.append({"spec": p.spec, "ms": (time.perf_counter() - t0) * 1e3, "rows": n})
+        self.druid_stats.append({"spec": p.spec, "ms": (time.perf_counter() - t0) * 1e3, "rows": n,
+                                 "stats": getattr(res, "stats", None)})
         return Batch(p.refs, cols, n)
 
 

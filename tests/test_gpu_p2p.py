@@ -1,0 +1,29 @@
+"""Peer-to-peer one-shot merge (parallel/p2p.py, ops/csrc/p2p.hip; verdict r3 #3) on the leased GPU:
+two rank processes share the card (gloo for the handle exchange and the reference merge, IPC
+mappings of each other's mailbox), and the P2P kernel's merge must equal the all-gather merge --
+synthetic states over several epochs, a failed rank's status word, and the headline SQL queries."""
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_p2p_merge_two_ranks_on_one_gpu(tmp_path):
+    from spark_druid_olap_amd.utils.launch import spawn_ranks
+
+    out = tmp_path / "p2p.json"
+    env = dict(os.environ, SDO_GLOO_GPU="1", MASTER_ADDR="127.0.0.1", SDO_P2P_TIMEOUT_S="20")
+    rc = spawn_ranks(2, [sys.executable, os.path.join(ROOT, "tools", "p2p_check.py"), "--out", str(out),
+                         "--sf", "0.2"], env=env)
+    assert rc == 0
+    r = json.loads(out.read_text())
+    print(json.dumps(r)[:3000])
+    assert r["exchange"], "IPC mailboxes could not be mapped"
+    assert r["synthetic_equal"] and r["failed_status_seen"]
+    assert all(r["engine_equal"].values()), r["engine_equal"]
+    assert r["engine_rows"]["TPCH Q1"] > 0 and r["engine_rows"]["TPCH Q5"] > 0

@@ -1,0 +1,155 @@
+#!/usr/bin/env python3
+"""One rank of the peer-to-peer merge check (parallel/p2p.py), run as N processes on the GPU(s):
+
+  python -c "from spark_druid_olap_amd.utils.launch import spawn_ranks; ..."   (tests/test_gpu_p2p.py)
+
+Ranks talk over gloo with their shards on the GPU (``SDO_GLOO_GPU=1``: several ranks may share one
+card -- IPC mappings work within a device as across xGMI).  Checks, on every rank:
+
+1. synthetic dense partials (int sum / f64 sum / min / max slots, HLL register bytes) merged by the
+   P2P kernel equal the RCCL/gloo one-shot all-gather merge, over several epochs (both mailbox
+   slots), and a failed rank's status word reaches every peer;
+2. the 8 headline SQL queries (Q1 / Q5 / Q7 among them) with the P2P merge on and off give the same
+   answers, with the per-phase times (scan / merge / finalize / post, ``PreparedQuery.run`` stats)
+   of both for the rehearsal breakdown.
+
+Rank 0 writes a JSON report to ``--out``."""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+class _Prog:
+    def __init__(self, slots):
+        self.slots = slots
+        self.nslots = len(slots)
+
+
+def synthetic(world, dev, out):
+    import torch
+
+    from spark_druid_olap_amd.engine.partials import Partials
+    from spark_druid_olap_amd.ops import desc as D
+    from spark_druid_olap_amd.parallel import p2p
+    from spark_druid_olap_amd.parallel.merge import start_dense_merge
+
+    slots = [(D.S_SUM_I, 0), (D.S_SUM_F, 0), (D.S_MIN_I, 1 << 62), (D.S_MAX_I, -(1 << 62))]
+    prog = _Prog(slots)
+    ex = p2p.exchange_for(world)
+    out["exchange"] = ex is not None
+    if ex is None:
+        return
+    ok = True
+    for epoch in range(5):
+        g = torch.Generator().manual_seed(1000 * epoch + world.rank)
+        R = 37 + epoch
+        acc = torch.randint(-10 ** 6, 10 ** 6, (R, 4), generator=g, dtype=torch.int64)
+        acc[:, 1] = torch.rand(R, generator=g, dtype=torch.float64).view(torch.int64)
+        hll = [torch.randint(0, 40, (R, 128), generator=g, dtype=torch.int64).to(torch.uint8)]
+        part = Partials("dense", acc.to(dev), None, [h.to(dev) for h in hll])
+        status = 1 if (epoch == 3 and world.rank == world.size - 1) else 0
+        m = ex.merge(prog, part, status)
+        ref, sts_ref = start_dense_merge(world, prog, part, status, "oneshot-allgather").wait()
+        sts = m.status_dev.tolist()
+        if epoch == 3:
+            out["failed_status_seen"] = sts == [0] * (world.size - 1) + [1]
+        same = torch.equal(m.acc[:, [0, 2, 3]].cpu(), ref.acc[:, [0, 2, 3]].cpu()) and \
+            torch.allclose(m.acc[:, 1].cpu().view(torch.float64), ref.acc[:, 1].cpu().view(torch.float64),
+                           rtol=1e-12, atol=1e-12) and \
+            all(torch.equal(a.cpu(), b.cpu()) for a, b in zip(m.hll, ref.hll)) and sts == list(sts_ref)
+        ok = ok and same
+    out["synthetic_equal"] = ok
+    # timing: P2P vs all-gather merge of a Q1-sized state (6 groups, 8 slots, one HLL block)
+    acc = torch.zeros((6, 4), dtype=torch.int64, device=dev)
+    part = Partials("dense", acc, None, [torch.zeros((6, 2048), dtype=torch.uint8, device=dev)])
+    for name, fn in (("p2p", lambda: ex.merge(prog, part, 0).status_dev.tolist()),
+                     ("allgather", lambda: start_dense_merge(world, prog, part, 0, "oneshot-allgather").wait())):
+        ts = []
+        for i in range(30):
+            world.barrier()
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t) * 1e6)
+        out[f"merge_us_{name}"] = statistics.median(ts[5:])
+
+
+def engine(world, dev, sf, out):
+    import torch
+
+    from spark_druid_olap_amd.engine.executor import Engine, results_on_root
+    from spark_druid_olap_amd.models import tpch
+    from spark_druid_olap_amd.parallel import p2p
+    from spark_druid_olap_amd.session import Session
+
+    ds = tpch.to_datasource(tpch.generate_flat(sf, dev, rank=world.rank, world=world.size), profile="bench")
+    sess = Session(engine=Engine(world), conf={"spark.sparklinedata.druid.approxCountDistinct": "true"})
+    sess.register_datasource(ds)
+    sess.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)
+    sess.sql(tpch.druid_ddl(source="orderLineItemPartSupplierBase", datasource="tpch", with_column_mapping=False))
+    res, phases = {}, {}
+    for mode in ("p2p", "rccl"):
+        p2p.ENABLED = mode == "p2p"
+        sess._plan_cache.clear()
+        with results_on_root():
+            for name, q in tpch.BENCH_QUERIES:
+                df = sess.sql(q)
+                for _ in range(2):
+                    df.run()
+                ts, ph = [], {}
+                for _ in range(10):
+                    world.barrier()
+                    torch.cuda.synchronize()
+                    t = time.perf_counter()
+                    b = df.run()
+                    torch.cuda.synchronize()
+                    ts.append((time.perf_counter() - t) * 1e3)
+                    for st in df.last_stats.get("druid", []):
+                        for k, v in (st.get("stats") or {}).items():
+                            if k.endswith("_ms"):
+                                ph.setdefault(k, []).append(v)
+                rows = sorted(tuple(round(x, 6) if isinstance(x, float) else x for x in r)
+                              for r in b.to_pandas().itertuples(index=False, name=None))
+                res.setdefault(name, {})[mode] = rows
+                phases.setdefault(name, {})[mode] = {"ms": statistics.median(ts),
+                                                    **{k: round(statistics.median(v), 4) for k, v in ph.items()}}
+    p2p.ENABLED = True
+    if world.rank == 0:
+        out["engine_equal"] = {n: r["p2p"] == r["rccl"] for n, r in res.items()}
+        out["engine_rows"] = {n: len(r["p2p"]) for n, r in res.items()}
+        out["phases"] = phases
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--sf", type=float, default=1.0, help="scale factor per rank")
+    ap.add_argument("--skip-engine", action="store_true")
+    a = ap.parse_args()
+    import torch
+
+    from spark_druid_olap_amd.parallel.world import init_world, shutdown
+
+    world = init_world(backend="gloo")
+    dev = world.device()
+    assert dev.type == "cuda", "run with SDO_GLOO_GPU=1 on a GPU box"
+    torch.cuda.set_device(dev)
+    out = {"world": world.size, "rank": world.rank}
+    synthetic(world, dev, out)
+    if not a.skip_engine and out.get("exchange"):
+        engine(world, dev, a.sf, out)
+    world.barrier()
+    if world.rank == 0:
+        with open(a.out, "w") as f:
+            json.dump(out, f)
+    shutdown()
+
+
+if __name__ == "__main__":
+    main()
