@@ -715,10 +715,21 @@ class PreparedQuery:
                 h = sk.values[torch.arange(int(cnt.sum()), device=dev) + first]
             else:
                 g, h = keys, theta_hash(column_tensor(ds, col)[rows])
-            pairs = _kmv(_sorted_unique_pairs(g, h), size)
+            G = int(prog.G) if 0 < prog.G < (1 << 62) else 0
+            pairs = kmv_select(g, h, size, G)
             if self.world.distributed:
-                allp = torch.cat(self.world.all_gather_varlen(pairs))
-                pairs = _kmv(_sorted_unique_pairs(allp[:, 0], allp[:, 1]), size)
+                # every rank's k candidates per group travel to the root only when the answer is
+                # needed there (results_on_root), else to every rank; the receivers re-select
+                root_only = root_only_results()
+                if root_only:
+                    got, _ = self.world.gather_varlen(pairs, root=0)
+                else:
+                    got = self.world.all_gather_varlen(pairs)
+                if got:
+                    allp = torch.cat(got)
+                    pairs = _kmv(_sorted_unique_pairs(allp[:, 0], allp[:, 1]), size)
+                else:
+                    pairs = pairs[:0]
             cols[name] = _kmv_estimates(pairs, size, gid_order)
 
     # ------------------------------------------------------------------ post processing
@@ -1065,6 +1076,37 @@ def _kmv_estimates(pairs: torch.Tensor, k: int, gid_order: np.ndarray) -> np.nda
     pos = np.searchsorted(ug, gid_order)
     ok = (pos < len(ug)) & (ug[np.minimum(pos, len(ug) - 1)] == gid_order)
     return np.where(ok, est[np.minimum(pos, len(ug) - 1)], 0.0)
+
+
+THETA_SELECT_MAX_G = 4096  # groups the device radix select handles (histogram G x 2^bits u32)
+
+
+def kmv_select(g: torch.Tensor, h: torch.Tensor, k: int, G: int) -> torch.Tensor:
+    """Per group the k smallest distinct hashes, as sorted unique (group, hash) pairs.  On the GPU a
+    radix select per group (ops/csrc/sketch.hip theta_*) keeps ~2k candidates per group before the
+    sort -- a 600M-row scan's pairs never reach the sort; groups whose candidates hold fewer than k
+    distinct hashes although their bound cut some pairs off (duplicate-heavy groups) are selected
+    again with a 4x larger target.  Elsewhere (CPU, huge key spaces) the full sort."""
+    if g.numel() == 0:
+        return torch.zeros((0, 2), dtype=torch.int64, device=g.device)
+    if not (g.is_cuda and 0 < G <= THETA_SELECT_MAX_G):
+        return _kmv(_sorted_unique_pairs(g, h), k)
+    from ..ops import native
+
+    g = g.to(torch.int64).contiguous()
+    h = h.to(torch.int64).contiguous()
+    bits = 16 if G <= 256 else 12
+    target = torch.full((G,), 2 * k, dtype=torch.int64, device=g.device)
+    for _ in range(6):
+        cg, ch, bound = native.theta_select(g, h, G, target, bits)
+        pairs = _sorted_unique_pairs(cg, ch)
+        distinct = torch.bincount(pairs[:, 0], minlength=G) if pairs.numel() else torch.zeros(G, dtype=torch.int64,
+                                                                                               device=g.device)
+        short = (distinct < k) & (bound < (1 << 62))
+        if not bool(short.any()):
+            return _kmv(pairs, k)
+        target = torch.where(short, target * 4, target)
+    return _kmv(_sorted_unique_pairs(g, h), k)
 
 
 def _kmv(pairs: torch.Tensor, k: int) -> torch.Tensor:

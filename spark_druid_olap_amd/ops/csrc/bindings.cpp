@@ -65,6 +65,10 @@ __global__ void part_split_kernel(const uint32_t* in, int RW, const uint32_t* se
 __global__ void part_agg_kernel(const uint32_t* recs, int RW, const uint32_t* base, int64_t nsub, int64_t G, int shift,
                                 PartFields f, uint64_t* gacc, PartHaving hv, int64_t* out_keys,
                                 unsigned long long* out_count, int64_t cap);
+__global__ void theta_hist_kernel(const int64_t* g, const int64_t* h, int64_t n, int bits, uint32_t* hist);
+__global__ void theta_thresh_kernel(const uint32_t* hist, int bits, const int64_t* target, int64_t* bound);
+__global__ void theta_filter_kernel(const int64_t* g, const int64_t* h, int64_t n, const int64_t* bound,
+                                    int64_t* out_g, int64_t* out_h, unsigned long long* count, int64_t cap);
 // p2p.hip
 constexpr int P2P_MAX_RANKS = 8;
 constexpr int P2P_MAX_SLOTS = 64;
@@ -645,6 +649,33 @@ static void part_agg(uint64_t recs, int RW, uint64_t base, int64_t nsub, int64_t
 }
 
 // ---------------------------------------------------------------------------------------------
+// Theta (KMV) candidate selection (sketch.hip): histogram of the top `bits` hash bits per group,
+// per-group bound for `target` candidates, compaction of the pairs below their bound.
+static void theta_select(uint64_t g, uint64_t h, int64_t n, int64_t G, int bits, uint64_t hist, uint64_t target,
+                         uint64_t bound, uint64_t out_g, uint64_t out_h, uint64_t count, int64_t cap,
+                         uint64_t stream) {
+  if (bits < 4 || bits > 16) throw std::invalid_argument("theta_select: 4..16 histogram bits");
+  if (G <= 0 || G > (1 << 20)) throw std::invalid_argument("theta_select: 1..2^20 groups");
+  hipStream_t s = (hipStream_t)stream;
+  check(hipMemsetAsync((void*)hist, 0, (size_t)G << bits << 2, s), "theta hist clear");
+  check(hipMemsetAsync((void*)count, 0, 8, s), "theta count clear");
+  if (n > 0) {
+    hipLaunchKernelGGL(sdo::theta_hist_kernel, dim3(grid_for(n, 256, 65536)), dim3(256), 0, s, (const int64_t*)g,
+                       (const int64_t*)h, n, bits, (uint32_t*)hist);
+    check(hipGetLastError(), "theta_hist_kernel launch");
+  }
+  hipLaunchKernelGGL(sdo::theta_thresh_kernel, dim3((unsigned)G), dim3(1024), 0, s, (const uint32_t*)hist, bits,
+                     (const int64_t*)target, (int64_t*)bound);
+  check(hipGetLastError(), "theta_thresh_kernel launch");
+  if (n > 0) {
+    hipLaunchKernelGGL(sdo::theta_filter_kernel, dim3(grid_for(n, 256, 65536)), dim3(256), 0, s, (const int64_t*)g,
+                       (const int64_t*)h, n, (const int64_t*)bound, (int64_t*)out_g, (int64_t*)out_h,
+                       (unsigned long long*)count, cap);
+    check(hipGetLastError(), "theta_filter_kernel launch");
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Peer-to-peer mailboxes (p2p.hip): one hipMalloc per (process group, rank), exported with an IPC
 // handle and opened by every peer; the small dense merge is then one kernel per rank.
 static py::tuple p2p_alloc(int64_t bytes) {
@@ -769,6 +800,7 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("module_launch", &module_launch);
   m.def("module_occupancy", &module_occupancy);
   m.def("module_attrs", &module_attrs);
+  m.def("theta_select", &theta_select);
   m.def("p2p_alloc", &p2p_alloc);
   m.def("p2p_open", &p2p_open);
   m.def("p2p_close", &p2p_close);

@@ -50,3 +50,109 @@ __global__ void __launch_bounds__(256) hll_merge_stored_kernel(const int64_t* __
 }
 
 }  // namespace sdo
+
+// ---------------------------------------------------------------------------------------------
+// Theta sketch (KMV) selection on the device: per group, the k smallest distinct 62-bit hashes of the
+// selected rows (ThetaSketch metric, sd/metadata/DruidDataSource.scala:29,38; 16,384-entry sketches
+// in src/test/resources/zip_codeAll.json.template:53-59).  Instead of sorting every (group, hash)
+// pair, a radix select per group on the top THETA_BITS hash bits keeps only the candidates:
+//
+//  * theta_hist   -- histogram [G, 2^B] of the top B bits of every pair's hash (global atomics:
+//    uniform hashes spread the updates; the group-major layout keeps one group's bins together);
+//  * theta_thresh -- one workgroup per group scans its bins (block prefix sum) for the first bin at
+//    which the running count reaches `target` (a margin over k: duplicates are counted), giving the
+//    exclusive hash bound of the group's candidates, or "everything" when the group has fewer;
+//  * theta_filter -- compacts the pairs below their group's bound (one atomic per wave for the
+//    output cursor).
+//
+// The few candidates (~target per group) are then sorted, de-duplicated and cut to k (torch); a
+// group whose candidates hold fewer than k distinct hashes although its bound excluded some pairs
+// is re-selected with a larger target (engine/executor.py _theta_select).
+__global__ void __launch_bounds__(256) theta_hist_kernel(const int64_t* __restrict__ g, const int64_t* __restrict__ h,
+                                                        int64_t n, int bits, uint32_t* __restrict__ hist) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int shift = 62 - bits;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t b = ((uint64_t)h[i]) >> shift;
+    atomicAdd(&hist[((uint64_t)g[i] << bits) + b], 1u);
+  }
+}
+
+// one 1024-thread workgroup per group: bins are scanned in chunks of 1024 (a thread per bin)
+__global__ void __launch_bounds__(1024) theta_thresh_kernel(const uint32_t* __restrict__ hist, int bits,
+                                                            const int64_t* __restrict__ target,
+                                                            int64_t* __restrict__ bound) {
+  __shared__ uint32_t wsum[16];
+  __shared__ int64_t s_found;
+  __shared__ uint64_t s_base;
+  const int64_t grp = blockIdx.x;
+  const int nb = 1 << bits;
+  const uint32_t* hg = hist + ((int64_t)grp << bits);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t want = (uint64_t)target[grp];
+  if (tid == 0) {
+    s_found = -1;
+    s_base = 0;
+  }
+  __syncthreads();
+  for (int c0 = 0; c0 < nb; c0 += 1024) {
+    const uint32_t v = (c0 + tid < nb) ? hg[c0 + tid] : 0u;
+    // inclusive prefix within the wave, then across the 16 waves
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t t = __shfl_up(x, d, 64);
+      if (lane >= d) x += t;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint32_t before = 0;
+    for (int w = 0; w < wave; ++w) before += wsum[w];
+    const uint64_t incl = s_base + before + x;
+    // the first bin whose running count reaches the target (bins are visited in order)
+    const bool hit = incl >= want && incl - v < want && v > 0;
+    if (hit) s_found = c0 + tid;
+    __syncthreads();
+    if (s_found >= 0) break;
+    if (tid == 0) {
+      uint32_t tot = 0;
+      for (int w = 0; w < 16; ++w) tot += wsum[w];
+      s_base += tot;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    // exclusive hash bound: every hash whose top bits are <= the found bin; "no bound" (2^62) when
+    // the group never reached the target
+    bound[grp] = s_found >= 0 ? (int64_t)((uint64_t)(s_found + 1) << (62 - bits)) : ((int64_t)1 << 62);
+  }
+}
+
+__global__ void __launch_bounds__(256) theta_filter_kernel(const int64_t* __restrict__ g, const int64_t* __restrict__ h,
+                                                          int64_t n, const int64_t* __restrict__ bound,
+                                                          int64_t* __restrict__ out_g, int64_t* __restrict__ out_h,
+                                                          unsigned long long* __restrict__ count, int64_t cap) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int lane = threadIdx.x & 63;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += stride) {
+    const int64_t i = i0 + threadIdx.x;
+    bool keep = false;
+    int64_t gi = 0, hi = 0;
+    if (i < n) {
+      gi = g[i];
+      hi = h[i];
+      keep = hi < bound[gi];
+    }
+    const uint64_t m = __ballot(keep);
+    unsigned long long base = 0;
+    if (lane == 0 && m) base = atomicAdd(count, (unsigned long long)__popcll(m));
+    base = __shfl(base, 0, 64);
+    if (keep) {
+      const unsigned long long pos = base + __popcll(m & ((1ull << lane) - 1ull));
+      if ((int64_t)pos < cap) {
+        out_g[pos] = gi;
+        out_h[pos] = hi;
+      }
+    }
+  }
+}

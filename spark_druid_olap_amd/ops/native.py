@@ -142,6 +142,31 @@ def device_info(dev: int = 0) -> dict:
     return load().device_info(dev)
 
 
+def theta_select(g: torch.Tensor, h: torch.Tensor, G: int, target: torch.Tensor, bits: int):
+    """Candidates of a per-group KMV selection (sketch.hip theta_*): (g, h) pairs whose hash lies
+    below their group's bound -- the first top-``bits`` bin at which the group's running pair count
+    reaches ``target[g]`` -- plus the bounds.  Pairs are int64 on the device; ``g`` in [0, G)."""
+    m = load()
+    assert g.dtype == torch.int64 and h.dtype == torch.int64 and g.is_cuda and g.numel() == h.numel()
+    assert target.dtype == torch.int64 and target.numel() == G
+    dev = g.device
+    n = g.numel()
+    hist = torch.empty(G << bits, dtype=torch.int32, device=dev)
+    bound = torch.empty(G, dtype=torch.int64, device=dev)
+    count = torch.zeros(1, dtype=torch.int64, device=dev)
+    cap = int(min(n, int(target.sum()) * 2 + (1 << 16)))
+    st = _stream(dev)
+    while True:
+        og = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+        oh = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+        m.theta_select(g.data_ptr(), h.data_ptr(), n, G, bits, hist.data_ptr(), target.data_ptr(), bound.data_ptr(),
+                       og.data_ptr(), oh.data_ptr(), count.data_ptr(), cap, st)
+        c = int(count.item())
+        if c <= cap:
+            return og[:c], oh[:c], bound
+        cap = c  # a duplicate-heavy bin held more candidates than the first guess: select again
+
+
 def compact_rows(mask: torch.Tensor) -> torch.Tensor:
     """Row ids (int64, ascending) of the set bits of a [nwords] int64 mask (post_scan.hip
     compact_*: popcount per 65536-row block, one-workgroup offset scan, scatter).  Temporaries are

@@ -331,3 +331,80 @@ def test_results_gather_to_root_only_at_8_ranks():
     assert sent > 0
     for o in outs:  # ~total/N partial rows per rank in the shuffles, not the total
         assert 0.5 * sent / world < o["recv"]["shuffle"] < 1.5 * sent / world, [x["recv"] for x in outs]
+
+
+def _theta_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), OMP_NUM_THREADS="1")
+    import pickle
+
+    from spark_druid_olap_amd.engine.executor import Engine, results_on_root
+    from spark_druid_olap_amd.models import tpch
+    from spark_druid_olap_amd.parallel.world import init_world, shutdown
+    from spark_druid_olap_amd.query import spec as S
+
+    w = init_world(backend="gloo")
+    flat = tpch.generate_flat(0.008 / world, "cpu", rank=rank, world=world)
+    ds = tpch.to_datasource(flat, profile="bench")
+    df = tpch.to_pandas(flat)
+    eng = Engine(w, use_native=False)
+    recv = {"gather": 0, "allgather": 0}
+    real_g, real_ag = w.gather_varlen, w.all_gather_varlen
+
+    def gather(t, root=0, status=None):
+        got, sts = real_g(t, root, status)
+        recv["gather"] += sum(int(x.shape[0]) for x in got)
+        return got, sts
+
+    def allgather(t, status=None):
+        out = real_ag(t, status)
+        lst = out[0] if status is not None else out
+        recv["allgather"] += sum(int(x.shape[0]) for x in lst)
+        return out
+    w.gather_varlen, w.all_gather_varlen = gather, allgather
+    q = S.GroupByQuerySpec("tpch", [S.DefaultDimensionSpec("l_returnflag")],
+                           aggregations=[S.FunctionAggregationSpec("count", "c"),
+                                         S.ThetaSketchAggregationSpec("t", "o_orderkey", 65536)],
+                           intervals=["1992-01-01/1999-01-01"])
+    with results_on_root():
+        r = eng.execute(q, ds)
+    res = {k: (int(c), float(t)) for k, c, t in zip(r.data["l_returnflag"], r.data["c"], r.data["t"])}
+    with open(os.path.join(outdir, f"t{rank}.pkl"), "wb") as f:
+        pickle.dump({"res": res, "df": df[["l_returnflag", "o_orderkey"]], "recv": recv}, f)
+    w.barrier()
+    shutdown()
+
+
+@pytest.mark.timeout(600)
+def test_theta_candidates_gather_to_root_only_at_8_ranks():
+    """Verdict r3 #6 (C8): each rank selects its k candidates per group and sends them to rank 0
+    only; the peers receive none, and the root's union equals the exact distinct counts (k above
+    every group's cardinality)."""
+    import pickle
+
+    import pandas as pd
+
+    world = 8
+    with tempfile.TemporaryDirectory() as td:
+        ctx = mp.get_context("spawn")
+        port = _free_port()
+        ps = [ctx.Process(target=_theta_worker, args=(r, world, port, td)) for r in range(world)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(500)
+            assert p.exitcode == 0, f"rank failed with {p.exitcode}"
+        outs = []
+        for r in range(world):
+            with open(os.path.join(td, f"t{r}.pkl"), "rb") as f:
+                outs.append(pickle.load(f))
+    full = pd.concat([o["df"] for o in outs], ignore_index=True)
+    exact = full.groupby("l_returnflag").o_orderkey.nunique().to_dict()
+    counts = full.groupby("l_returnflag").size().to_dict()
+    root = outs[0]["res"]
+    assert set(root) == set(exact)
+    for k, (c, t) in root.items():
+        assert c == counts[k] and t == pytest.approx(exact[k]), (k, c, t, exact[k])
+    assert outs[0]["recv"]["gather"] > 0
+    for o in outs[1:]:
+        assert o["recv"]["gather"] == 0 and o["recv"]["allgather"] == 0, o["recv"]
