@@ -284,6 +284,8 @@ class PreparedScan:
         b = _Bufs()
         b.cap = cap
         rows = cap if self.mode == D.M_HASH else prog.G
+        if self.mode == D.M_PART and self.part is not None and self.part.get("hashed"):
+            rows = 1  # (sparse output: no group table)
         b.rows = rows
         b.init_row = _init_row(dev, tuple(int(init) for _, init in prog.slots))
         if self.pres_bytes:
@@ -412,6 +414,8 @@ class PreparedScan:
                           pb["base2"].data_ptr(), st)
             nat.part_split(*a2, pb["base2"].data_ptr(), pb["recs1"].data_ptr(), 1, st)
             recs, base = pb["recs1"], pb["base2"]
+        if L.get("hashed"):
+            return self._run_part_hashed(b, recs, base)
         hv = self.part_having
         if hv is None:
             nat.part_agg(recs.data_ptr(), L["rw"], base.data_ptr(), L["nsub"], int(prog.G), L["shift"],
@@ -433,6 +437,37 @@ class PreparedScan:
             if n <= acc.shape[0]:
                 return Partials("sparse", acc[:n], keys[:n], [])
             self.part_cap = _next_pow2(n + n // 4)  # more survivors than room: grow, aggregate again
+
+    def _run_part_hashed(self, b: "_Bufs", recs: torch.Tensor, base: torch.Tensor) -> Partials:
+        """Sparse LDS-hash aggregation of the hash-partitioned records (keys beyond 32 bits).  A
+        sub-bucket that held more distinct keys than its table (the planner's group estimate was
+        low) makes the whole execution re-partition into 4x more sub-buckets and run again."""
+        L, nat, st, prog = self.part, native.load(), native._stream(self.dev), self.prog
+        hv = self.part_having or ([], 1)
+        while True:
+            out = b.part.get("hh_out")
+            if out is None or out[0].shape[0] < self.part_cap:
+                out = b.part["hh_out"] = (torch.empty((self.part_cap, prog.nslots), dtype=torch.int64, device=self.dev),
+                                          torch.empty(self.part_cap, dtype=torch.int64, device=self.dev),
+                                          torch.zeros(1, dtype=torch.int64, device=self.dev),
+                                          torch.zeros(1, dtype=torch.int32, device=self.dev))
+            acc, keys, cnt, ovf = out
+            nat.part_hash_agg(recs.data_ptr(), L["rw"], base.data_ptr(), L["nsub"], L["cap_log2"],
+                              [f[0] for f in L["fields"]], [f[1] for f in L["fields"]],
+                              [int(op) for op, _ in prog.slots], [int(init) for _, init in prog.slots], hv[0], hv[1],
+                              keys.data_ptr(), acc.data_ptr(), cnt.data_ptr(), int(acc.shape[0]), ovf.data_ptr(), st)
+            n, overflow = int(cnt.item()), int(ovf.item())
+            if overflow:
+                if L["scale"] >= 1 << 12:
+                    raise RuntimeError("hash-partitioned group-by: sub-bucket overflow persists")
+                with self._slot_lock:
+                    self.part = L = part_hash_layout(prog, L["scale"] * 4)
+                    self._slots.clear()
+                nb = self._bufs()
+                return self._run_part(nb) if nb.part is not None else self._empty()
+            if n <= acc.shape[0]:
+                return Partials("sparse", acc[:n], keys[:n], [])
+            self.part_cap = _next_pow2(n + n // 4)  # more groups than room: grow, aggregate again
 
     def set_part_having(self, terms, conj: bool) -> bool:
         """Fuse a groupBy HAVING into the partitioned aggregation (engine/executor.py): only existing
@@ -804,7 +839,7 @@ class PreparedEmit:
         self.dev = prog.ds.device
         from ..ops import jit as J
 
-        if prog.empty or not J.part_eligible(ep):
+        if prog.empty or not J.part_eligible(ep) or J.part_hashed(ep):
             raise RuntimeError("emit: program not eligible")
         self.jit = _jit_for(ep, D.M_PART, False, 1 << prog.hll_p)
         if self.jit is None:
@@ -897,6 +932,7 @@ class PreparedMask:
 
 
 PART_TABLE_BYTES = int(os.environ.get("SDO_PART_TABLE_BYTES", 32 << 10))  # LDS table per sub-bucket
+HASH_TABLE_BYTES = 128 << 10  # LDS hash table of a hash-partitioned sub-bucket (keys + slots)
 HLL32_MAX_BYTES = int(os.environ.get("SDO_HLL32_MAX_BYTES", str(512 << 20)))  # u32 scan-time registers
 
 
@@ -907,6 +943,8 @@ def part_layout(prog) -> dict:
     from ..ops import jit
 
     ns = max(1, prog.nslots)
+    if jit.part_hashed(prog):
+        return part_hash_layout(prog)
     shift = max(0, int(math.floor(math.log2(max(8, PART_TABLE_BYTES // (8 * ns))))))
     gbits = max(1, int(math.ceil(math.log2(max(2, prog.G)))))
     rem = max(0, gbits - shift)
@@ -924,6 +962,32 @@ def part_layout(prog) -> dict:
     k = max(1, min(64, 4096 // p1))
     return {"levels": 2, "shift": shift, "shift1": shift + b2, "p1": p1, "p2": p2, "k": k, "nsub": p1 * p2,
             "fields": fields, "rw": rw}
+
+
+def part_hash_layout(prog, scale: int = 1) -> dict:
+    """Sub-buckets of a hash-partitioned group-by: enough that each holds ~half its LDS table's
+    capacity of distinct keys by the planner's group estimate (``scale`` x more after an overflow);
+    bucket bits are the top bits of the record's 32-bit hash, split over one level (<= 2^10
+    buckets) or two."""
+    from ..ops import jit
+
+    ns = max(1, prog.nslots)
+    cap_log2 = min(14, int(math.floor(math.log2(HASH_TABLE_BYTES // (8 * (1 + ns))))))
+    groups = max(1.0, min(float(prog.G), float(getattr(prog, "est_rows", prog.G)) * 1.2))
+    nsub = max(8, int(math.ceil(groups * scale / (1 << (cap_log2 - 1)))))
+    bits = min(20, max(3, int(math.ceil(math.log2(nsub)))))
+    fields = jit.part_fields(prog)
+    rw = 3 + sum(w for _, w in fields)
+    if bits <= 10:
+        p1 = 1 << bits
+        return {"levels": 1, "hashed": True, "shift": 32 - bits, "shift1": 32 - bits, "p1": p1, "p2": 1, "k": 1,
+                "nsub": p1, "fields": fields, "rw": rw, "cap_log2": cap_log2, "scale": scale}
+    b1 = min(10, (bits + 1) // 2)
+    b2 = bits - b1
+    p1, p2 = 1 << b1, 1 << b2
+    k = max(1, min(64, 4096 // p1))
+    return {"levels": 2, "hashed": True, "shift": 32 - bits, "shift1": 32 - b1, "p1": p1, "p2": p2, "k": k,
+            "nsub": p1 * p2, "fields": fields, "rw": rw, "cap_log2": cap_log2, "scale": scale}
 
 
 def _grid(dev: torch.device, total_chunks: int, lds_total: int, jit=None) -> int:

@@ -62,6 +62,9 @@ template <int PU>
 __global__ void part_split_kernel(const uint32_t* in, int RW, const uint32_t* seg_lo, const uint32_t* seg_hi, int spg,
                                   int K, int shift2, int P2, uint32_t* counts2, const uint32_t* base2, uint32_t* out,
                                   int phase);
+__global__ void part_hash_agg_kernel(const uint32_t* recs, int RW, const uint32_t* base, int64_t nsub, int cap_log2,
+                                     PartFields f, PartHaving hv, int64_t* out_keys, uint64_t* out_acc,
+                                     unsigned long long* out_count, int64_t cap, int* overflow);
 __global__ void part_agg_kernel(const uint32_t* recs, int RW, const uint32_t* base, int64_t nsub, int64_t G, int shift,
                                 PartFields f, uint64_t* gacc, PartHaving hv, int64_t* out_keys,
                                 unsigned long long* out_count, int64_t cap);
@@ -739,6 +742,69 @@ static void p2p_merge(std::vector<uint64_t> mbox, int rank, uint64_t epoch, int6
   check(hipGetLastError(), "p2p_merge_kernel launch");
 }
 
+// Sparse aggregation of hash-partitioned 64-bit-key records (partition.hip part_hash_agg_kernel):
+// one workgroup per sub-bucket with an LDS table of 2^cap_log2 keys; survivors (every group, or
+// those passing `having`) appended to out_keys / out_acc; *overflow set when a sub-bucket held more
+// distinct keys than its table.
+static void part_hash_agg(uint64_t recs, int RW, uint64_t base, int64_t nsub, int cap_log2, std::vector<int> slot,
+                          std::vector<int> width, std::vector<int> ops, std::vector<int64_t> init,
+                          std::vector<std::tuple<int, int, int, double, double>> having, int conj, uint64_t out_keys,
+                          uint64_t out_acc, uint64_t out_count, int64_t cap, uint64_t overflow, uint64_t stream) {
+  if (nsub <= 0) return;
+  sdo::PartFields f{};
+  if (slot.size() != width.size() || slot.size() > (size_t)sdo::MAX_SLOTS) throw std::invalid_argument("part_hash_agg: fields");
+  if (ops.size() != init.size() || ops.empty() || ops.size() > (size_t)sdo::MAX_SLOTS)
+    throw std::invalid_argument("part_hash_agg: slots");
+  f.nfields = (int)slot.size();
+  f.nslots = (int)ops.size();
+  int words = 3;
+  for (size_t j = 0; j < slot.size(); ++j) {
+    if (slot[j] < 0 || slot[j] >= f.nslots || width[j] < 0 || width[j] > 2)
+      throw std::invalid_argument("part_hash_agg: field");
+    f.slot[j] = slot[j];
+    f.width[j] = width[j];
+    words += width[j];
+  }
+  if (words != RW) throw std::invalid_argument("part_hash_agg: record width does not match the fields");
+  for (size_t s = 0; s < ops.size(); ++s) {
+    f.op[s] = ops[s];
+    f.init[s] = init[s];
+  }
+  if (cap_log2 < 6 || cap_log2 > 14) throw std::invalid_argument("part_hash_agg: table of 2^6..2^14 keys");
+  const int64_t lds = ((int64_t)1 << cap_log2) * (1 + f.nslots) * 8;
+  if (lds > 160 * 1024) throw std::invalid_argument("part_hash_agg: table exceeds 160 KiB of LDS");
+  sdo::PartHaving hv{};
+  if (having.size() > 4) throw std::invalid_argument("part_hash_agg: at most 4 having terms");
+  hv.nterms = (int)having.size();
+  hv.conj = conj;
+  for (size_t j = 0; j < having.size(); ++j) {
+    hv.slot[j] = std::get<0>(having[j]);
+    hv.f64[j] = std::get<1>(having[j]);
+    hv.op[j] = std::get<2>(having[j]);
+    hv.div[j] = std::get<3>(having[j]);
+    hv.c[j] = std::get<4>(having[j]);
+    if (hv.slot[j] < 0 || hv.slot[j] >= f.nslots || hv.op[j] < 0 || hv.op[j] > 2)
+      throw std::invalid_argument("part_hash_agg: having term");
+  }
+  if (!out_keys || !out_acc || !out_count || !overflow || cap < 0) throw std::invalid_argument("part_hash_agg: outputs");
+  hipStream_t s = (hipStream_t)stream;
+  check(hipMemsetAsync((void*)out_count, 0, 8, s), "part_hash_agg count reset");
+  check(hipMemsetAsync((void*)overflow, 0, 4, s), "part_hash_agg overflow reset");
+  const int64_t grid = (nsub + 7) / 8 * 8;
+  if (grid > ((int64_t)1 << 31) - 8) throw std::invalid_argument("part_hash_agg: too many sub-buckets");
+  const void* fn = (const void*)sdo::part_hash_agg_kernel;
+  if (lds > 65536) check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024), "attr");
+  const uint32_t* r_ = (const uint32_t*)recs;
+  const uint32_t* b_ = (const uint32_t*)base;
+  int64_t* ok_ = (int64_t*)out_keys;
+  uint64_t* oa_ = (uint64_t*)out_acc;
+  unsigned long long* oc_ = (unsigned long long*)out_count;
+  int* of_ = (int*)overflow;
+  void* args[] = {(void*)&r_, (void*)&RW, (void*)&b_, (void*)&nsub, (void*)&cap_log2, (void*)&f, (void*)&hv,
+                  (void*)&ok_, (void*)&oa_, (void*)&oc_, (void*)&cap, (void*)&of_};
+  check(hipLaunchKernel(fn, dim3((unsigned)grid), dim3(512), args, (size_t)lds, s), "part_hash_agg_kernel launch");
+}
+
 static int desc_size() { return (int)sizeof(sdo::ScanDesc); }
 
 static py::dict layout() {
@@ -819,6 +885,7 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("part_keys", &part_keys);
   m.def("part_split", &part_split);
   m.def("part_agg", &part_agg);
+  m.def("part_hash_agg", &part_hash_agg);
   m.def("layout", &layout);
   m.def("device_info", &device_info);
   m.attr("ARCH") = "gfx950";

@@ -459,3 +459,101 @@ __global__ __launch_bounds__(512) void part_agg_kernel(const uint32_t* __restric
 }
 
 }  // namespace sdo
+
+namespace sdo {
+
+// ---------------------------------------------------------------------------------------------
+// Key spaces beyond 32 bits (TPC-H Q16's (brand, type, size, supplier) = 1.7e11 keys, ~12M present
+// at SF100): records are bucketed by a 32-bit hash of the 64-bit key (record word 0; words 1-2 the
+// key) through the same split kernels, and each sub-bucket -- ~HASH_SUB_KEYS distinct keys by the
+// planner's estimate -- aggregates in an LDS open-addressing table (64-bit key compare-and-swap,
+// then the slot operators), emitting its groups sparsely (key + slots) at a position reserved with
+// one global atomic per workgroup.  A sub-bucket whose distinct keys overflow the table sets
+// *overflow and drops them; the host re-partitions with more sub-buckets and runs again.
+constexpr uint64_t HASH_EMPTY = ~0ull;
+
+__device__ __forceinline__ uint32_t part_hash_probe(uint32_t h, int cap_log2) {
+  // the partitioning consumed the hash's top bits; a multiplicative re-mix spreads the rest
+  return (h * 0x9E3779B1u) >> (32 - cap_log2);
+}
+
+__global__ __launch_bounds__(512) void part_hash_agg_kernel(const uint32_t* __restrict__ recs, int RW,
+                                                           const uint32_t* __restrict__ base, int64_t nsub,
+                                                           int cap_log2, PartFields f,
+                                                           PartHaving hv, int64_t* __restrict__ out_keys,
+                                                           uint64_t* __restrict__ out_acc,
+                                                           unsigned long long* __restrict__ out_count, int64_t cap,
+                                                           int* __restrict__ overflow) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t t[];
+  const int64_t x = blockIdx.x;
+  const int64_t per_xcd = gridDim.x / 8;
+  const int64_t r = (x % 8) * per_xcd + x / 8;
+  if (r >= nsub) return;
+  const int C = 1 << cap_log2;
+  const int NS = f.nslots;
+  uint64_t* tk = t;           // [C] keys
+  uint64_t* tv = t + C;       // [C][NS] slots
+  for (int i = threadIdx.x; i < C; i += blockDim.x) tk[i] = HASH_EMPTY;
+  for (int i = threadIdx.x; i < C * NS; i += blockDim.x) tv[i] = (uint64_t)f.init[i % NS];
+  __syncthreads();
+  const uint32_t lo = base[r], hi = base[r + 1];
+  bool full = false;
+  for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const uint32_t* rec = recs + (uint64_t)i * RW;
+    const uint64_t key = (uint64_t)rec[1] | ((uint64_t)rec[2] << 32);
+    uint32_t pos = part_hash_probe(rec[0], cap_log2);
+    int slot = -1;
+    for (int probe = 0; probe < C; ++probe) {
+      const uint64_t prev = atomicCAS((unsigned long long*)&tk[pos], (unsigned long long)HASH_EMPTY,
+                                      (unsigned long long)key);
+      if (prev == HASH_EMPTY || prev == key) {
+        slot = (int)pos;
+        break;
+      }
+      pos = (pos + 1u) & (uint32_t)(C - 1);
+    }
+    if (slot < 0) {
+      full = true;
+      continue;
+    }
+    uint64_t* row = tv + (int64_t)slot * NS;
+    int w = 3;
+    for (int j = 0; j < f.nfields; ++j) {
+      const int wd = f.width[j];
+      int64_t v;
+      if (wd == 0) v = 1;
+      else if (wd == 1) v = (int64_t)(int32_t)rec[w];
+      else v = (int64_t)((uint64_t)rec[w] | ((uint64_t)rec[w + 1] << 32));
+      w += wd;
+      const int s = f.slot[j];
+      lds_fold(row + s, f.op[s], v);
+    }
+  }
+  if (full) atomicOr(overflow, 1);
+  __syncthreads();
+  __shared__ uint32_t scan_lds[8];
+  __shared__ unsigned long long blk_base;
+  uint32_t mine = 0;
+  for (int i = threadIdx.x; i < C; i += blockDim.x) {
+    if (tk[i] == HASH_EMPTY) continue;
+    mine += (hv.nterms == 0 || having_pass(hv, tv + (int64_t)i * NS)) ? 1u : 0u;
+  }
+  uint32_t total;
+  uint32_t pre = block_excl_scan_u32<512>(mine, scan_lds, &total);
+  if (threadIdx.x == 0) blk_base = total ? atomicAdd(out_count, (unsigned long long)total) : 0ull;
+  __syncthreads();
+  if (total == 0) return;
+  int64_t pos = (int64_t)blk_base + pre;
+  for (int i = threadIdx.x; i < C; i += blockDim.x) {
+    if (tk[i] == HASH_EMPTY) continue;
+    const uint64_t* row = tv + (int64_t)i * NS;
+    if (hv.nterms && !having_pass(hv, row)) continue;
+    if (pos < cap) {
+      out_keys[pos] = (int64_t)tk[i];
+      for (int s = 0; s < NS; ++s) out_acc[pos * NS + s] = row[s];
+    }
+    ++pos;
+  }
+}
+
+}  // namespace sdo

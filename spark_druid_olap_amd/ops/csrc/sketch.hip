@@ -51,6 +51,8 @@ __global__ void __launch_bounds__(256) hll_merge_stored_kernel(const int64_t* __
 
 }  // namespace sdo
 
+namespace sdo {
+
 // ---------------------------------------------------------------------------------------------
 // Theta sketch (KMV) selection on the device: per group, the k smallest distinct 62-bit hashes of the
 // selected rows (ThetaSketch metric, sd/metadata/DruidDataSource.scala:29,38; 16,384-entry sketches
@@ -156,3 +158,5 @@ __global__ void __launch_bounds__(256) theta_filter_kernel(const int64_t* __rest
     }
   }
 }
+
+}  // namespace sdo

@@ -135,11 +135,26 @@ def part_fields(prog, cols=None) -> List[Tuple[int, int]]:
     return out
 
 
+FORCE_HASHED = False  # tests: the hashed layout for any key space
+
+
+def part_hashed(prog) -> bool:
+    """Key spaces beyond 32 bits partition by a 32-bit hash of the 64-bit key and aggregate sparsely
+    (ops/csrc/partition.hip part_hash_agg_kernel): records are (hash, key lo, key hi, values...)."""
+    return prog.G >= (1 << 32) or FORCE_HASHED
+
+
+def part_record_words(prog) -> int:
+    """Header words of a partition record: the u32 key, or hash + 64-bit key."""
+    return 3 if part_hashed(prog) else 1
+
+
 def part_eligible(prog) -> bool:
-    """The partitioned group-by handles every slot operator; it needs u32 keys and no HLL sketch."""
+    """The partitioned group-by handles every slot operator and any key space (beyond 32 bits by
+    hash); it does not carry HLL sketches."""
     slots = getattr(prog, "slots", None)
     n = len(slots) if slots is not None else prog.nslots
-    return n > 0 and not prog.nhll and not getattr(prog, "stored_hll", None) and 0 < prog.G < (1 << 32) \
+    return n > 0 and not prog.nhll and not getattr(prog, "stored_hll", None) and 0 < prog.G < (1 << 62) \
         and not prog.empty
 
 
@@ -788,11 +803,17 @@ class _Gen:
         body.append("        const bool mine = act[u];")
         body.append("        const uint64_t am_ = __ballot(mine);")
         fields = part_fields(p, self.cols)
-        rw = 1 + sum(w for _, w in fields)
+        hdr = part_record_words(p)
+        rw = hdr + sum(w for _, w in fields)
         body.append("        if (mine) {")
         body.append(f"          uint32_t* o_ = precs + (uint64_t)(cbase + woff + (uint32_t)__popcll(am_ & lmlt)) * {rw}u;")
-        body.append("          o_[0] = (uint32_t)key;")
-        w = 1
+        if hdr == 3:
+            # 64-bit key: partitioned by the top bits of a multiplicative hash
+            body.append("          o_[0] = (uint32_t)(((uint64_t)key * 0x9E3779B97F4A7C15ull) >> 32);")
+            body.append("          o_[1] = (uint32_t)key; o_[2] = (uint32_t)((uint64_t)key >> 32);")
+        else:
+            body.append("          o_[0] = (uint32_t)key;")
+        w = hdr
         fi = 0
         for ai, a in enumerate(p.aops):
             if a["kind"] in (D.A_HLL, D.A_HLL_CODE, D.A_HLL_STORED):

@@ -377,9 +377,14 @@ def plan_groupby(prog, jit: bool, local: bool) -> GroupByPlan:
         part = partitioned_cost_s(prog, est_rows) if (jit and PARTITIONED and not presence and not empty) else None
         if part is not None:
             costs["partitioned"] = part * 1e3
+    if table > limit and jit and PARTITIONED and not empty:
+        # beyond any dense table (TPC-H Q16: 1.7e11 keys): hash-partitioned records, sparse output
+        part = partitioned_cost_s(prog, est_rows)
+        if part is not None:
+            costs["partitioned"] = part * 1e3
     cap = 1 << max(10, math.ceil(math.log2(max(2.0, 2 * (min(G, est_rows * 1.2) + 1024)))))
     costs["hash"] = (2 * cap * (8 + ns * 8) / HBM_BW + est_rows * PROBE_S) * 1e3
-    if "partitioned" in costs and (FORCE_PARTITIONED or costs["partitioned"] <= min(costs["dense-global"],
+    if "partitioned" in costs and (FORCE_PARTITIONED or costs["partitioned"] <= min(costs.get("dense-global", math.inf),
                                                                                     costs["hash"])):
         return GroupByPlan("partitioned", costs=costs,
                            reason="radix-partitioned records aggregated in LDS (no random HBM atomics)")
@@ -397,6 +402,15 @@ def partitioned_cost_s(prog, est_rows: float) -> Optional[float]:
 
     if not jit.part_eligible(prog):
         return None
+    if jit.part_hashed(prog):
+        from ..engine.device_exec import part_hash_layout
+
+        L = part_hash_layout(prog)
+        rec = 4 * L["rw"]
+        passes = 1 + 3 * L["levels"] + 1
+        groups = min(float(prog.G), est_rows)
+        return (est_rows * rec * passes + groups * (1 + max(1, prog.nslots)) * 8) / HBM_BW + \
+            (3 + 4 * L["levels"]) * LAUNCH_S
     if est_rows < prog.G / 4:
         # few updates per group: the touched lines are sparse (TPC-H Q3 touches ~1M of 150M orders)
         # and stay cached; the atomic table wins and a full-table write would be waste
