@@ -56,10 +56,6 @@ SPECIALIZE_AFTER = int(os.environ.get("SDO_JIT_SPECIALIZE_AFTER", "4"))
 SPEC_MAX_PENDING = 2
 _spec_pending = [0]
 _spec_lock = threading.Lock()
-# small dense executions as replayed HIP graphs (PreparedScan.run_graph_small).  On this ROCm
-# (7.x) one hipGraphLaunch + sync of the 4-5 node graph costs more host time than the fused native
-# launch path it replaces (headline geomean 0.441 vs 0.428 ms)
-USE_GRAPHS = os.environ.get("SDO_GRAPHS", "0") != "0"  # opt-in: measured slower (profiles/r3/hip_graph_ab_sf100.txt)
 _spec_pool = []
 
 
@@ -333,7 +329,6 @@ class PreparedScan:
             b.part = self._part_bufs(d)
         b.desc = _upload(d.view(np.uint8), dev)
         b.run_args = b.noreset_args = None
-        b.fetch = None
         if self.mode not in (D.M_HASH, D.M_PART):
             # the whole launch path of one execution as cached arguments of ONE native call
             # (ops/csrc/bindings.cpp run_scan): fused reset of this slot's buffers + the kernel
@@ -609,56 +604,6 @@ class PreparedScan:
             return out
         return Partials("dense", b.acc, None, [h.view(b.rows, self.m) for h in b.hll])
 
-    def run_graph_small(self, want_est: bool) -> Optional[Partials]:
-        """One execution of a small dense scan as a replayed HIP graph (reset + kernel + HLL
-        estimates + D2H, ops/csrc/bindings.cpp graph_small_capture): the dense partials with the
-        host copy finalize needs attached.  Captured per execution slot once the kernel is final
-        (after literal specialization); re-captured if the kernel is swapped.  None when this scan
-        does not qualify (the caller runs the ordinary path)."""
-        if not USE_GRAPHS or self.prog.empty or self.touch or self.pres_bytes or getattr(self, "_graph_off", False) \
-                or self.mode not in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL):
-            return None
-        if self.jit is not None and not self.jit.literals and SPECIALIZE != "off":
-            return None  # the literal-specialized kernel is still to come: capture that one
-        b = self._bufs()
-        if b.run_args is None or b.hll32 or not b.acc.is_contiguous():
-            return None
-        self._maybe_specialize()  # (counts the run; adopts a finished background compile)
-        b = self._bufs()
-        G = int(b.acc.shape[0])
-        m = 1 << self.prog.hll_p
-        want_est = want_est and bool(b.hll) and G * m <= (1 << 26)
-        hll = [h for h in b.hll] if want_est else []
-        key = (b.run_args[-6], want_est)
-        g = b.fetch
-        if g is None or g[0] != key:
-            if g is not None:
-                native.graph_destroy(g[1])  # (the finalizer's later destroy of it is a no-op)
-            nb = b.acc.numel() * 8
-            host = torch.empty(nb + len(hll) * G * 8, dtype=torch.uint8, pin_memory=True)
-            est = torch.empty(max(1, len(hll) * G), dtype=torch.float64, device=self.dev)
-            try:
-                h = native.graph_small_capture(b.run_args, [x.view(-1)[:G * m] for x in hll], G, self.prog.hll_p,
-                                               est, host, b.acc)
-            except Exception as e:  # noqa: BLE001  (not capturable here: the ordinary path)
-                import warnings
-
-                warnings.warn(f"HIP graph capture failed, using direct launches: {e}")
-                self._graph_off = True
-                return None
-            g = b.fetch = (key, h, host, est)
-            # the graph names this slot's buffers: destroyed with them (an evicted slot's buffers
-            # stay alive while a replay that still holds them runs)
-            weakref.finalize(b, native.graph_destroy, h).atexit = False  # (not during interpreter teardown)
-        native.graph_launch(g[1], self.dev)
-        b.clean = False
-        buf = g[2].numpy()
-        nb = b.acc.numel() * 8
-        out = [buf[:nb].view(np.int64).reshape(b.acc.shape)]
-        for i in range(len(hll)):
-            out.append(buf[nb + i * G * 8: nb + (i + 1) * G * 8].view(np.float64))
-        return Partials("dense", b.acc, None, [h.view(b.rows, self.m) for h in b.hll], host=out)
-
     # single-slot views (tests and tools inspect the implicit slot's buffers)
     @property
     def acc(self):
@@ -816,7 +761,7 @@ def _forget_prep(pid: int) -> None:
 class _Bufs:
     """One execution slot's device buffers for a prepared scan."""
     __slots__ = ("cap", "rows", "init_row", "acc", "keys", "hll", "hll32", "overflow", "desc", "touch", "clean",
-                 "run_args", "noreset_args", "fetch", "part", "__weakref__")
+                 "run_args", "noreset_args", "part", "__weakref__")
 
 
 class PreparedEmit:

@@ -33,17 +33,6 @@ from ..parallel.fault import FAULTS
 from ..utils.cancel import checkpoint
 
 
-_DE: list = []
-
-
-def _graphs_on() -> bool:
-    """device_exec.USE_GRAPHS (the module is imported lazily: it pulls in the native extension)."""
-    if not _DE:
-        from . import device_exec as DE_
-
-        _DE.append(DE_)
-    return _DE[0].USE_GRAPHS
-
 # segment-batched execution overlaps batch j's merge collectives with batch j+1's scan
 PIPELINE_MERGE = os.environ.get("SDO_PIPELINE_MERGE", "1") not in ("0", "")
 # existence-only group-bys over the key's dictionary domain (engine/dict_exist.py)
@@ -313,11 +302,7 @@ class PreparedQuery:
         qt = self.qs.queryType
         if qt in ("groupBy", "timeseries", "topN"):
             root_only = self.world.distributed and root_only_results()
-            fast = self._graph_run()
-            if fast is not None:
-                prog, part, t1 = fast
-            else:
-                prog, part, t1 = self.run_partials(t0, root_only)
+            prog, part, t1 = self.run_partials(t0, root_only)
             t2 = time.perf_counter()
             with T.span("sdo.finalize"):
                 if root_only and self.world.rank != 0:
@@ -342,26 +327,6 @@ class PreparedQuery:
         res.stats["exec_ms"] = (time.perf_counter() - t0) * 1e3
         self.last_stats = res.stats
         return res
-
-    def _graph_run(self):
-        """One GPU, one scan, a small dense state that merge / HAVING / top-K pruning pass through
-        unchanged (<= 4096 groups): the execution is one replayed HIP graph of reset + scan + HLL
-        estimates + D2H (engine/device_exec.py run_graph_small).  (prog, partials with their host
-        copy, scan end time) or None for the ordinary path."""
-        if not _graphs_on() or self.world.distributed or len(self.scans) != 1 or self.window is not None:
-            return None
-        _, prog, prep = self.scans[0]
-        if prep is None or not hasattr(prep, "run_graph_small") or prog.G > 4096 or prog.nslots > 256:
-            return None
-        if (prog.stored_hll and not getattr(prep, "stored_fused", False)) or self._dict_exist_plan(prog) is not None:
-            return None
-        with T.span("sdo.scan"):
-            checkpoint()
-            FAULTS.maybe_fail("scan", self.world.rank)
-            part = prep.run_graph_small(not any(kc.collapse for kc in prog.keys))
-        if part is None:
-            return None
-        return prog, part, time.perf_counter()
 
     def run_partials(self, t0: float, root_only: bool = False):
         """scan -> merge across ranks -> device HAVING / top-K pruning; (prog, merged partials,

@@ -24,9 +24,6 @@ class Partials:
     # ``status`` (this rank's failure word, parallel/fault.py) in that collective
     scattered: bool = False
     status: int = 0
-    # small dense executions replayed as a HIP graph (engine/device_exec.py run_graph_small): the
-    # accumulator table and the HLL estimates already on the host, as finalize's _fetch_small returns
-    host: Optional[List[np.ndarray]] = None
     # peer-to-peer merge (parallel/p2p.py): every rank's status word, still on the device -- read
     # with the result's device-to-host copy (finalize) instead of a separate host synchronisation
     status_dev: Optional[torch.Tensor] = None
@@ -306,9 +303,7 @@ def finalize(prog, parts: Partials, out_types: Optional[Dict[str, str]] = None) 
             est_dev = []
             G = parts.rows
             want_est = bool(parts.hll) and G * (1 << prog.hll_p) <= (1 << 26) and not collapse
-            if parts.host is not None and len(parts.host) == 1 + (len(parts.hll) if want_est else 0):
-                host = parts.host
-            elif parts.acc.is_cuda and parts.acc.is_contiguous():
+            if parts.acc.is_cuda and parts.acc.is_contiguous():
                 # estimates + both copies + the sync in one native call (bindings.cpp fetch_small),
                 # through this thread's pinned staging buffer; the fancy indexing below copies out
                 host = _fetch_small(parts.acc, list(parts.hll) if want_est else [], G, prog.hll_p,

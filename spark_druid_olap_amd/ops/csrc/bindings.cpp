@@ -45,7 +45,6 @@ struct ResetArgs {
   int* overflow;
 };
 __global__ void reset_bufs_kernel(ResetArgs a);
-__global__ void copy_words_kernel(const uint64_t* src, int64_t n, uint64_t* dst);
 __global__ void topk_keep_kernel(const int64_t* acc, int64_t n, int nslots, int slot, int is_f64, int desc,
                                  const uint64_t* state, uint64_t* keep);
 // sketch.hip
@@ -102,22 +101,7 @@ static void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
-// Result waits of small queries: the host has nothing else to do, and a blocking
-// hipStreamSynchronize may sleep until an interrupt wakes it -- latency that lands on every
-// query's wall time.  With spinning on, the wait polls hipStreamQuery instead (set_spin_sync).
-static bool g_spin_sync = false;
-static void set_spin_sync(bool on) { g_spin_sync = on; }
-
-static void wait_stream(hipStream_t st, const char* what) {
-  if (g_spin_sync) {
-    hipError_t e;
-    while ((e = hipStreamQuery(st)) == hipErrorNotReady) {
-    }
-    check(e, what);
-    return;
-  }
-  check(hipStreamSynchronize(st), what);
-}
+static void wait_stream(hipStream_t st, const char* what) { check(hipStreamSynchronize(st), what); }
 
 static void scan(uint64_t desc, int grid, int block, int lds, int unroll, uint64_t stream) {
   hipStream_t s = (hipStream_t)stream;
@@ -432,108 +416,17 @@ static void run_scan(uint64_t acc, uint64_t init, int64_t rows, int nslots, std:
 // Small dense result: HLL estimates of every register block (MFMA kernel) + the accumulator table
 // and the estimates copied into one pinned host buffer + a stream synchronisation, in one call with
 // the GIL released while the device works.
-static bool g_zero_copy = false;
-static void set_zero_copy(bool on) { g_zero_copy = on; }
-
 static void fetch_small(uint64_t acc, int64_t acc_bytes, std::vector<uint64_t> hll, int64_t G, int p,
                         uint64_t est_dev, uint64_t host, uint64_t stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (g_zero_copy && acc_bytes % 8 == 0) {
-    // the kernels write the pinned host buffer directly: estimates from the MFMA finalize, the
-    // accumulator words from one copy block -- no SDMA copies
-    for (size_t i = 0; i < hll.size(); ++i)
-      hll_estimate(hll[i], G, p, host + (uint64_t)acc_bytes + i * (uint64_t)G * 8, stream);
-    const int64_t nw = acc_bytes / 8;
-    if (nw > 0) {
-      const unsigned blocks = (unsigned)std::min<int64_t>((nw + 255) / 256, 64);
-      hipLaunchKernelGGL(sdo::copy_words_kernel, dim3(blocks), dim3(256), 0, st, (const uint64_t*)acc, nw,
-                         (uint64_t*)host);
-      check(hipGetLastError(), "copy_words_kernel launch");
-    }
-    py::gil_scoped_release nogil;
-    wait_stream(st, "fetch_small sync");
-    return;
-  }
   for (size_t i = 0; i < hll.size(); ++i) hll_estimate(hll[i], G, p, est_dev + i * (uint64_t)G * 8, stream);
-  {
-    py::gil_scoped_release nogil;
-    if (acc_bytes > 0) check(hipMemcpyAsync((void*)host, (const void*)acc, acc_bytes, hipMemcpyDeviceToHost, st),
-                             "fetch_small acc");
-    if (!hll.empty())
-      check(hipMemcpyAsync((void*)(host + acc_bytes), (const void*)est_dev, hll.size() * G * 8, hipMemcpyDeviceToHost,
-                           st),
-            "fetch_small est");
-    wait_stream(st, "fetch_small sync");
-  }
-}
-
-// HIP graph of one small dense execution: the fused buffer reset, the scan kernel, the HLL estimates
-// and both D2H copies into a pinned host buffer, captured once per prepared-scan slot and replayed
-// with ONE hipGraphLaunch (no per-launch host work, no gaps between the dependent launches).  The
-// capture runs on a private non-blocking stream (the legacy default stream cannot be captured); the
-// replay is ordered on the caller's stream and waited for with the GIL released.
-struct SmallGraph {
-  hipGraphExec_t exec;
-  bool live;
-};
-static std::vector<SmallGraph> g_graphs;
-static std::mutex g_graph_mu;
-
-static int graph_small_capture(uint64_t acc, uint64_t init, int64_t rows, int nslots, std::vector<uint64_t> zptr,
-                               std::vector<int64_t> zwords, uint64_t overflow, int jit, uint64_t desc, int grid,
-                               int block, int lds, int unroll, std::vector<uint64_t> hll, int64_t G, int p,
-                               uint64_t est_dev, uint64_t host, int64_t acc_bytes, uint64_t acc_src) {
-  hipStream_t cs;
-  check(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "graph capture stream");
-  hipGraph_t g = nullptr;
-  try {
-    check(hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
-    try {
-      run_scan(acc, init, rows, nslots, zptr, zwords, overflow, jit, desc, grid, block, lds, unroll, (uint64_t)cs);
-      for (size_t i = 0; i < hll.size(); ++i) hll_estimate(hll[i], G, p, est_dev + i * (uint64_t)G * 8, (uint64_t)cs);
-      if (acc_bytes > 0)
-        check(hipMemcpyAsync((void*)host, (const void*)acc_src, acc_bytes, hipMemcpyDeviceToHost, cs), "graph acc copy");
-      if (!hll.empty())
-        check(hipMemcpyAsync((void*)(host + acc_bytes), (const void*)est_dev, hll.size() * G * 8,
-                             hipMemcpyDeviceToHost, cs),
-              "graph est copy");
-    } catch (...) {
-      hipGraph_t dead = nullptr;
-      (void)hipStreamEndCapture(cs, &dead);
-      if (dead) (void)hipGraphDestroy(dead);
-      throw;
-    }
-    check(hipStreamEndCapture(cs, &g), "hipStreamEndCapture");
-    hipGraphExec_t ex;
-    check(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0), "hipGraphInstantiate");
-    (void)hipGraphDestroy(g);
-    (void)hipStreamDestroy(cs);
-    std::lock_guard<std::mutex> lk(g_graph_mu);
-    g_graphs.push_back({ex, true});
-    return (int)g_graphs.size() - 1;
-  } catch (...) {
-    (void)hipStreamDestroy(cs);
-    throw;
-  }
-}
-
-static void graph_launch(int h, uint64_t stream) {
-  hipGraphExec_t ex;
-  {
-    std::lock_guard<std::mutex> lk(g_graph_mu);
-    if (h < 0 || h >= (int)g_graphs.size() || !g_graphs[h].live) throw std::invalid_argument("bad graph handle");
-    ex = g_graphs[h].exec;
-  }
   py::gil_scoped_release nogil;
-  check(hipGraphLaunch(ex, (hipStream_t)stream), "hipGraphLaunch");
-  wait_stream((hipStream_t)stream, "graph sync");
-}
-
-static void graph_destroy(int h) {
-  std::lock_guard<std::mutex> lk(g_graph_mu);
-  if (h < 0 || h >= (int)g_graphs.size() || !g_graphs[h].live) return;
-  (void)hipGraphExecDestroy(g_graphs[h].exec);
-  g_graphs[h].live = false;
+  if (acc_bytes > 0)
+    check(hipMemcpyAsync((void*)host, (const void*)acc, acc_bytes, hipMemcpyDeviceToHost, st), "fetch_small acc");
+  if (!hll.empty())
+    check(hipMemcpyAsync((void*)(host + acc_bytes), (const void*)est_dev, hll.size() * G * 8, hipMemcpyDeviceToHost, st),
+          "fetch_small est");
+  wait_stream(st, "fetch_small sync");
 }
 
 static void stream_sync(uint64_t stream) {
@@ -875,11 +768,6 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("run_scan", &run_scan);
   m.def("fetch_small", &fetch_small);
   m.def("stream_sync", &stream_sync);
-  m.def("set_spin_sync", &set_spin_sync);
-  m.def("set_zero_copy", &set_zero_copy);
-  m.def("graph_small_capture", &graph_small_capture);
-  m.def("graph_launch", &graph_launch);
-  m.def("graph_destroy", &graph_destroy);
   m.def("glds_probe", &glds_probe);
   m.def("part_scan", &part_scan);
   m.def("part_keys", &part_keys);

@@ -332,13 +332,4 @@ __global__ void __launch_bounds__(256) reset_bufs_kernel(ResetArgs a) {
   if (tid == 0 && a.overflow) *a.overflow = 0;
 }
 
-// Small results straight into pinned host memory (UVA): the accumulator table's words written by
-// one block with vector stores instead of an SDMA copy per array (each costs several microseconds
-// of launch and completion latency on a 200-byte result).
-__global__ void __launch_bounds__(256) copy_words_kernel(const uint64_t* __restrict__ src, int64_t n,
-                                                         uint64_t* __restrict__ dst) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    dst[i] = src[i];
-}
-
 }  // namespace sdo

@@ -54,12 +54,6 @@ def load(build_if_missing: bool = True):
             except Exception as e:  # pragma: no cover - no compiler on the box
                 raise NativeUnavailable(f"native extension is stale and rebuild failed: {e}") from e
         _mod = importlib.import_module("spark_druid_olap_amd.ops._sdo_native")
-        if hasattr(_mod, "set_spin_sync"):
-            # result waits poll instead of sleeping in hipStreamSynchronize (bindings.cpp wait_stream)
-            _mod.set_spin_sync(os.environ.get("SDO_SPIN_SYNC", "0") != "0")
-        if hasattr(_mod, "set_zero_copy"):
-            # small results written into pinned host memory by the kernels (bindings.cpp fetch_small)
-            _mod.set_zero_copy(os.environ.get("SDO_ZERO_COPY", "0") != "0")
         return _mod
 
 
@@ -328,28 +322,6 @@ def fetch_small(acc: torch.Tensor, hll: Sequence[torch.Tensor], G: int, p: int, 
     load().fetch_small(acc.data_ptr(), nb, [h.data_ptr() for h in hll], int(G), int(p), est_dev.data_ptr(),
                        host.data_ptr(), _stream(acc.device))
 
-
-def graph_small_capture(run_args, hll: Sequence[torch.Tensor], G: int, p: int, est_dev: torch.Tensor,
-                        host: torch.Tensor, acc: torch.Tensor) -> int:
-    """Capture reset + scan (``run_args`` as for run_scan, minus the stream) + HLL estimates + the
-    D2H of ``acc`` and the estimates into pinned ``host`` as one HIP graph (bindings.cpp)."""
-    assert acc.is_contiguous() and host.is_pinned()
-    nb = acc.numel() * acc.element_size()
-    assert host.numel() * host.element_size() >= nb + len(hll) * G * 8
-    assert est_dev.numel() * est_dev.element_size() >= len(hll) * G * 8
-    for h in hll:
-        assert h.dtype == torch.uint8 and h.is_contiguous() and h.numel() >= G * (1 << p)
-    return int(load().graph_small_capture(*run_args, [h.data_ptr() for h in hll], int(G), int(p), est_dev.data_ptr(),
-                                          host.data_ptr(), nb, acc.data_ptr()))
-
-
-def graph_launch(h: int, dev) -> None:
-    """Replay a captured graph on the caller's stream and wait for it (GIL released)."""
-    load().graph_launch(int(h), _stream(dev))
-
-
-def graph_destroy(h: int) -> None:
-    load().graph_destroy(int(h))
 
 
 def stream_sync(dev) -> None:
