@@ -35,10 +35,6 @@ BLOCK = 512
 UNROLL = int(os.environ.get("SDO_UNROLL", "2"))
 BLOCKS_PER_CU = int(os.environ.get("SDO_BLOCKS_PER_CU", "3"))
 USE_JIT = os.environ.get("SDO_JIT", "1") != "0"
-# Both measured slower than LDS accumulators + single-buffered staging at 2 workgroups/CU on
-# MI355X (tools/query_probe.py A/B, profiles/): kept as opt-in kernel-generation variants.
-USE_REG = os.environ.get("SDO_JIT_REG", "0") != "0"     # register accumulators for tiny key spaces
-USE_PIPE = os.environ.get("SDO_JIT_PIPE", "0") != "0"   # double-buffered payload DMA
 JIT_BLOCKS = int(os.environ.get("SDO_JIT_BLOCKS", "3"))  # target resident workgroups per CU
 JIT_STAGE = os.environ.get("SDO_JIT_STAGE", "auto")       # auto | reg (VGPR loads) | lds (LDS-DMA planes)
 # Literal specialization of repeated statements (ops/jit.py JitScan.specialized): a prepared scan's
@@ -111,24 +107,17 @@ def _jit_build(prog, mode: int, hll_lds: bool, m: int, shared: bool = False, loa
 
     nplanes = sum(2 if column_tensor_size(prog, c) == 8 else 1 for c in prog.cols)
     prefs = [16, 8, 4, 2] if nplanes <= 3 else ([8, 4, 2] if nplanes <= 8 else [4, 2])
-    reg = jit.reg_eligible(prog, mode) if USE_REG and not shared else False
-    cands = [(U, True) for U in prefs if USE_PIPE and jit.pipe_eligible(prog, mode, U)]
-    cands += [(U, False) for U in prefs]
     # occupancy first: the scan is latency-bound at 8 waves/CU, so prefer the largest U that still
     # leaves room for JIT_BLOCKS workgroups per CU (160 KiB LDS), then fall back to one workgroup
     budgets = [(160 * 1024) // b - 512 for b in (JIT_BLOCKS, 1) if b >= 1]
     regstage = JIT_STAGE == "reg" or (JIT_STAGE == "auto" and jit.prefer_regstage(prog))
-    if regstage:
-        cands = [(U, False) for U in prefs]
     for budget in budgets:
-        for U, pipe in cands:
-            lay = jit.layout(prog, mode, U, hll_lds, m, reg, pipe, budget, regstage, shared)
-            if lay.total <= budget and (reg or shared or mode != D.M_DENSE_LDS or lay.ncopy >= 4
-                                        or U == prefs[-1]):
+        for U in prefs:
+            lay = jit.layout(prog, mode, U, hll_lds, m, budget, regstage, shared)
+            if lay.total <= budget and (shared or mode != D.M_DENSE_LDS or lay.ncopy >= 4 or U == prefs[-1]):
                 try:
                     return jit.JitScan(prog, mode, U, hll_lds, m, bool(native.narrow4()) if load else True,
-                                       load=load, reg=reg, pipe=pipe, budget=budget, regstage=regstage,
-                                       shared=shared)
+                                       load=load, budget=budget, regstage=regstage, shared=shared)
                 except Exception as e:  # pragma: no cover - compile problems fall back loudly
                     import warnings
 

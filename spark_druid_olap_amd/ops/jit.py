@@ -47,10 +47,6 @@ class ColInfo:
     pw: int = 0    # bit-packed width (segment/packed.py); 0 = plain column
     pbase: int = 0
 
-# bit-packed loads as one 8-byte buffer load at a dword-aligned offset (needs the unaligned
-# access mode) instead of two dword loads
-PK_X2 = os.environ.get("SDO_PK_X2", "0") != "0"
-
 
 @dataclass
 class JitLayout:
@@ -62,24 +58,8 @@ class JitLayout:
     wave_bytes: int
     total: int
     ncopy: int
-    pipe: bool = False
     regstage: bool = False
     shared: bool = False  # one accumulator copy per workgroup (LDS atomics shared by its 8 waves)
-    hll32: bool = False   # LDS HLL registers as u32 words (HLL32_LDS, when they fit the budget)
-    blocked: bool = False  # row-blocked staging of full chunks (BLOCKED)
-
-
-def pipe_eligible(prog, mode: int, U: int) -> bool:
-    """Double-buffer the payload DMA (see ``_Gen._pipelined_words``)."""
-    if mode != D.M_DENSE_LDS or prog.filter_len and not prog.final_pre or not prog.pcols:
-        return False
-    if any(a.get("filt_len") or a.get("filter") is not None or a["kind"] == D.A_HLL_STORED for a in prog.aops):
-        return False
-    if getattr(prog, "packed", None):
-        return False
-    cols = col_infos(prog)
-    nld = sum(2 if c.lg == 3 else 1 for i, c in cols.items() if i >= D.PAYLOAD_BASE) * U
-    return nld <= 63
 
 
 def col_infos(prog) -> Dict[int, ColInfo]:
@@ -103,8 +83,6 @@ def col_infos(prog) -> Dict[int, ColInfo]:
 
 
 JIT_LITERALS = os.environ.get("SDO_JIT_LITERALS", "0") != "0"
-JIT_VREG = os.environ.get("SDO_JIT_VREG", "0") != "0"  # opt-in: query constants / bitmap pointers in VGPRs
-VREG_MIN_CONSTS = int(os.environ.get("SDO_JIT_VREG_MIN", "16"))
 PART_MAX_BUCKETS = 1024  # level-1 buckets of the partitioned group-by (split kernel LDS cursors)
 
 
@@ -158,46 +136,9 @@ def part_eligible(prog) -> bool:
         and not prog.empty
 
 
-REG_BUDGET = int(os.environ.get("SDO_JIT_REG_BUDGET", "96"))  # VGPRs for register accumulators
-
-
-def _narrow_slot(prog, s: int, cols) -> bool:
-    """Slot whose per-chunk partial fits int32: counts and sums of <=2-byte integer columns
-    (a lane sees at most 64 rows per 4096-row chunk)."""
-    for a in prog.aops:
-        if a.get("slot") != s:
-            continue
-        if a["kind"] == D.A_COUNT:
-            return True
-        if a["kind"] == D.A_SUM_I and a["col"] in cols and cols[a["col"]].lg <= 1 and not cols[a["col"]].flt:
-            return True
-        return False
-    return False
-
-
-def reg_eligible(prog, mode: int) -> bool:
-    """Small dense key spaces (TPC-H Q1: 6 groups) accumulate in per-lane registers.
-
-    With a handful of groups, every lane of a wave updates one of a few LDS words: the LDS atomic
-    unit serializes same-address lanes and the accumulator rows alias onto the same banks.  A
-    one-hot register update (``acc[g] += key == g ? v : 0``) costs a few VALU ops per group and no
-    LDS traffic; partials are wave-reduced once at the end."""
-    if mode != D.M_DENSE_LDS or prog.G > 16 or not prog.slots:
-        return False
-    cols = col_infos(prog)
-    regs = sum(3 if _narrow_slot(prog, s, cols) else 2 for s in range(prog.nslots)) * prog.G
-    return regs <= REG_BUDGET
-
-
 # accumulator copies per wave for tiny dense key spaces (lanes l, l+C, l+2C.. share copy l % C; up
 # to 64 = lane-private, no same-address LDS atomics) -- the LDS budget may halve it
 MAX_NCOPY = int(os.environ.get("SDO_JIT_NCOPY", "16"))
-# counts of tiny dense key spaces as wave ballots: per 64-row step and group one compare whose lane
-# mask popcounts into a wave-uniform (scalar) counter -- no LDS atomic per row; lane 0 adds the
-# wave's totals into its accumulator copy at the end.  Up to this many groups (0: off).  Measured
-# slower than the LDS copies on MI355X (count by l_returnflag, l_linestatus over SF100: 0.83 vs
-# 0.47 ms; the VALU-compare -> SALU-popcount chain serializes): opt-in.
-BALLOT_G = int(os.environ.get("SDO_JIT_BALLOT_G", "0"))
 # whole-chunk fast path: a chunk entirely inside the scan's row range with no chunk-level bitmap
 # prefilter walks its 64 words in order (every word's row mask all ones, then refined by the
 # per-row filter) instead of the find-first-set / readlane chain over its non-empty words
@@ -206,128 +147,19 @@ FULL_CHUNKS = os.environ.get("SDO_JIT_FULL", "1") != "0"
 # reading each word's mask by lane index (independent readlanes) and skipping all-empty steps;
 # sparser chunks take the find-first-set chain over their non-empty words only (0: always chain)
 DENSE_WORDS = int(os.environ.get("SDO_JIT_DENSE_WORDS", "48"))
-# LDS HLL registers as u32 words updated with one fire-and-forget ds_max_u32 per row (no register
-# read, no compare-and-swap loop) instead of packed byte registers (4x the LDS bytes; narrowed to
-# bytes in the block's final merge)
-HLL32_LDS = os.environ.get("SDO_JIT_HLL32LDS", "0") != "0"
-# LDS accumulator slots whose kernel-wide value provably fits 32 bits -- unfiltered or filtered
-# counts, min / max of integer columns inside int32 -- update the low dword of their 8-byte cell
-# with a 32-bit LDS atomic (ds_add_u32 / ds_max_i32: half the LDS bytes of ds_add_u64, no 64-bit
-# data registers); the block fold widens them
-NARROW_LDS = os.environ.get("SDO_JIT_NARROW_LDS", "0") != "0"
 
 
-# Row-blocked staging of whole chunks (the full-chunk branch of unfiltered scans): a 256-row block of
-# every column is copied into the wave's LDS with exactly-sized LDS-DMA loads (a bit-packed column's
-# 32 * width bytes, not one 4-byte lane fetch per row per load: the vector-memory return path, not
-# HBM, bounds the one-row-per-lane layout -- TPC-H Q1 issues ~10 dword loads per 64-row word), then
-# each lane reads ITS BR consecutive rows of each column back with one LDS read and extracts the
-# fields at compile-time bit offsets.
-BLOCKED = os.environ.get("SDO_JIT_BLOCKED", "0") != "0"
-# register double-buffering of whole chunks (register staging, no row filter): the loads of the next
-# U words are issued before the current U words are aggregated, so each wave keeps two groups of
-# loads in flight instead of paying one memory round trip per group (the scan is latency-bound:
-# ~384 dependent round trips per wave at SF100 / 768 workgroups)
-REG_PIPE = os.environ.get("SDO_JIT_REGPIPE", "0") != "0"
-# "2": two staging buffers per wave -- block b+1's copies are in flight while block b is aggregated
-# (one s_waitcnt vmcnt(<copies of one block>) instead of a drain); dense LDS tables only
-BLOCKED_PIPE = os.environ.get("SDO_JIT_BLOCKED", "0") == "2"
-BR = 4  # consecutive rows per lane (a block is 64 * BR = 256 rows)
 
 
-def blocked_eligible(prog, mode: int, regstage: bool = True) -> bool:
-    """Scans whose per-row work reads no word-granular state: no row filter (or a chunk-final
-    one), no per-aggregator filters, no row ids, bit-packed widths <= 32."""
-    if not BLOCKED or mode not in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL, D.M_HASH) or not regstage:
-        return False
-    if prog.filter_len and not prog.final_pre:
-        return False
-    if not prog.pcols or any(a.get("filt_len") or a["kind"] in (D.A_HLL_STORED, D.A_ROWID) for a in prog.aops):
-        return False
-    cols = col_infos(prog)
-    return all(c.pw <= 32 for i, c in cols.items() if i >= D.PAYLOAD_BASE)
-
-
-def _blk_dwords(c) -> int:
-    """LDS dwords of one column's 256-row block (plus the tail a lane's window read may touch)."""
-    if c.pw:
-        nd = (8 * c.pw) + ((31 + (BR - 1) * c.pw) // 32 + 2) + 1
-        return (nd + 63) // 64 * 64
-    return (64 * BR << c.lg) // 4
-
-
-def blocked_bytes(prog) -> int:
-    cols = col_infos(prog)
-    return sum(_blk_dwords(c) * 4 for i, c in cols.items() if i >= D.PAYLOAD_BASE)
-
-
-def _col_range(c) -> Optional[Tuple[int, int]]:
-    """[lo, hi] of an integer column's stored values (None: float / unknown)."""
-    if c.flt:
-        return None
-    if c.pw:
-        return c.pbase, c.pbase + (1 << c.pw) - 1
-    bits = 8 << c.lg
-    return (-(1 << (bits - 1)), (1 << (bits - 1)) - 1) if c.sgn else (0, (1 << bits) - 1)
-
-
-def narrow_lds_slots(prog, mode: int, reg: bool, cols=None) -> Dict[int, str]:
-    """slot -> 'cnt' | 'max' | 'min' for the 32-bit LDS accumulator cells (see NARROW_LDS)."""
-    if not NARROW_LDS or mode != D.M_DENSE_LDS or reg:
-        return {}
-    cols = col_infos(prog) if cols is None else cols
-    out = {}
-    for s in range(prog.nslots):
-        users = [a for a in prog.aops if a.get("slot") == s and a["kind"] not in
-                 (D.A_HLL, D.A_HLL_CODE, D.A_HLL_STORED, D.A_ROWID)]
-        if not users:
-            continue
-        op = prog.slots[s][0]
-        if all(a["kind"] == D.A_COUNT for a in users) and op == D.S_SUM_I:
-            out[s] = "cnt"  # (a copy counts at most the rows of its wave: far below 2^32)
-            continue
-        if len(users) != 1 or op not in (D.S_MAX_I, D.S_MIN_I):
-            continue
-        a = users[0]
-        if a["kind"] not in (D.A_MAX_I, D.A_MIN_I) or a.get("expr") or a.get("col") not in cols:
-            continue
-        r = _col_range(cols[a["col"]])
-        # the untouched cell (INT32_MIN for max / INT32_MAX for min) must not be a real value
-        if r is not None and -(1 << 31) < r[0] and r[1] < (1 << 31) - 1:
-            out[s] = "max" if op == D.S_MAX_I else "min"
-    return out
-
-
-def ballot_slots(prog, mode: int, reg: bool, shared: bool) -> set:
-    """Accumulator slots updated only by (optionally filtered) counts, for the ballot path."""
-    if mode != D.M_DENSE_LDS or reg or shared or not (0 < prog.G <= BALLOT_G):
-        return set()
-    out = set()
-    for s in range(prog.nslots):
-        users = [a for a in prog.aops if a.get("slot") == s and a["kind"] not in
-                 (D.A_HLL, D.A_HLL_CODE, D.A_HLL_STORED, D.A_ROWID)]
-        if users and all(a["kind"] == D.A_COUNT for a in users) and prog.slots[s][0] == D.S_SUM_I:
-            out.add(s)
-    return out
-
-
-def layout(prog, mode: int, U: int, hll_lds: bool, m: int, reg: bool = False, pipe: bool = False,
-           budget: int = 150 * 1024, regstage: bool = False, shared: bool = False) -> JitLayout:
+def layout(prog, mode: int, U: int, hll_lds: bool, m: int, budget: int = 150 * 1024,
+           regstage: bool = False, shared: bool = False) -> JitLayout:
     cols = col_infos(prog)
     nplanes = 0 if regstage else sum(2 if c.lg == 3 else 1 for c in cols.values() if not c.pw)
     need_bmw = _needs_word_bitmaps(prog)
-    wave_bytes = U * nplanes * 256 * (2 if pipe else 1) + (len(prog.bm_leaves) * 512 if need_bmw else 0)
-    blocked = blocked_eligible(prog, mode, regstage) and not pipe
-    if blocked:  # the block staging area sits after the word staging planes / bitmap words
-        wave_bytes += blocked_bytes(prog) * (2 if BLOCKED_PIPE and mode == D.M_DENSE_LDS else 1)
+    wave_bytes = U * nplanes * 256 + (len(prog.bm_leaves) * 512 if need_bmw else 0)
     wave_bytes = (wave_bytes + 15) // 16 * 16
     hll_bytes = prog.nhll * prog.G * m if hll_lds else 0  # byte registers (hll_update8)
     stage = W * wave_bytes
-    hll32 = False
-    if HLL32_LDS and hll_bytes and mode == D.M_DENSE_LDS:
-        acc_min = prog.G * prog.nslots * 8 * (1 if shared else W * (1 if reg else 4))
-        if acc_min + 4 * hll_bytes + stage <= budget:  # u32 registers (ds_max_u32) when they fit
-            hll_bytes, hll32 = 4 * hll_bytes, True
     ncopy = 1
     acc_bytes = 0
     if mode == D.M_DENSE_LDS and shared:
@@ -337,7 +169,7 @@ def layout(prog, mode: int, U: int, hll_lds: bool, m: int, reg: bool = False, pi
         acc_bytes = prog.G * prog.nslots * 8
     elif mode == D.M_DENSE_LDS:
         base = prog.G * prog.nslots * 8 * W
-        ncopy = 1 if reg else MAX_NCOPY
+        ncopy = MAX_NCOPY
         while ncopy > 1 and base * ncopy + hll_bytes + stage > budget:
             ncopy //= 2
         acc_bytes = base * ncopy
@@ -345,8 +177,8 @@ def layout(prog, mode: int, U: int, hll_lds: bool, m: int, reg: bool = False, pi
     hll_off = (acc_bytes + 15) // 16 * 16
     cache_off = (hll_off + hll_bytes + 15) // 16 * 16
     total = cache_off + stage
-    return JitLayout(acc_off, acc_bytes, hll_off, hll_bytes, cache_off, wave_bytes, total, ncopy, pipe, regstage,
-                     shared and mode == D.M_DENSE_LDS, hll32, blocked)
+    return JitLayout(acc_off, acc_bytes, hll_off, hll_bytes, cache_off, wave_bytes, total, ncopy, regstage,
+                     shared and mode == D.M_DENSE_LDS)
 
 
 def prefer_regstage(prog) -> bool:
@@ -384,15 +216,11 @@ def _dlit(v: float) -> str:
 
 class _Gen:
     def __init__(self, prog, mode: int, U: int, hll_lds: bool, narrow4: bool, lay: JitLayout, m: int,
-                 reg: bool = False, literals: bool = False, vreg: bool = False):
+                 literals: bool = False):
         self.p = prog
         self.literals = literals
-        self.vreg = vreg      # park query constants / bitmap pointers in VGPRs (many-constant filters)
         self.nconst = 0
-        self.reg = reg
-        self.pipe = lay.pipe
         self.regstage = lay.regstage
-        self.wbv = "wbp" if lay.pipe else "wb"
         self.mode = mode
         self.U = U
         self.hll_lds = hll_lds
@@ -401,35 +229,27 @@ class _Gen:
         self.m = m
         self.cols = col_infos(prog)
         self.NP = sum(2 if c.lg == 3 else 1 for c in self.cols.values() if not c.pw)
-        self.hw = 4 if lay.hll32 else 1  # LDS bytes per HLL register
-        self.blocked = False  # emitting the row-blocked body (ival / dval read bv<i>[u])
         self.pre_lines: List[str] = []  # kernel-entry pointer / constant loads
         self._const_set = set()
 
     # ---------------------------------------------------------------- values
     def ival(self, idx: int) -> str:
         c = self.cols[idx]
-        if self.blocked:  # raw field of row u of the lane's block (_blocked_loop)
-            if c.pw:
-                return f"((int64_t)bv{idx}[u] + {_lit(c.pbase)})"
-            return f"cv_int<{c.lg}, {'true' if c.sgn else 'false'}, {'true' if c.flt else 'false'}>(bv{idx}[u])"
         if c.pw:
             return f"(pk_field<{c.pw}>(xp{idx}[u], psh{c.pw}) + {_lit(c.pbase)})"
         if self.regstage:
             return f"cv_int<{c.lg}, {'true' if c.sgn else 'false'}, {'true' if c.flt else 'false'}>(x{idx}[u])"
         return (f"ld_int<{c.lg}, {'true' if c.sgn else 'false'}, {'true' if c.flt else 'false'}, {self.n4}>"
-                f"({self.wbv} + (u * {self.NP} + {c.plane}) * 256, lane)")
+                f"(wb + (u * {self.NP} + {c.plane}) * 256, lane)")
 
     def dval(self, idx: int) -> str:
         c = self.cols[idx]
-        if self.blocked and not c.pw:
-            return f"cv_dbl<{c.lg}, {'true' if c.sgn else 'false'}, {'true' if c.flt else 'false'}>(bv{idx}[u])"
         if c.pw:
             return f"((double){self.ival(idx)})"
         if self.regstage:
             return f"cv_dbl<{c.lg}, {'true' if c.sgn else 'false'}, {'true' if c.flt else 'false'}>(x{idx}[u])"
         return (f"ld_dbl<{c.lg}, {'true' if c.sgn else 'false'}, {'true' if c.flt else 'false'}, {self.n4}>"
-                f"({self.wbv} + (u * {self.NP} + {c.plane}) * 256, lane)")
+                f"(wb + (u * {self.NP} + {c.plane}) * 256, lane)")
 
     # ---------------------------------------------------------------- query constants
     # Filter bounds, zone bounds, key bases / cards / strides and expression constants are read
@@ -442,8 +262,6 @@ class _Gen:
             return lit  # (A/B switch: the value baked into the source, one code object per value)
         if name[:2] in ("fl", "fh", "ff", "fg", "ec"):
             self.nconst += 1
-            if self.vreg:
-                expr = f"vreg(({ctype})({expr}))"  # filter / expression constants live in VGPRs
         line = f"const {ctype} {name} = {expr};"
         if line not in self._const_set:
             self._const_set.add(line)
@@ -493,7 +311,7 @@ class _Gen:
                     st.append(f"({{ {vdecl} (uint64_t)__ballot({' && '.join(conds)}); }})")
             elif op == D.F_IN_SET:
                 self.pre_lines.append(f"const uint64_t* inset{i} = (const uint64_t*)" +
-                                      (f"vreg((uint64_t)d->fops[{i}].bits);" if self.vreg else f"d->fops[{i}].bits;"))
+                                      f"d->fops[{i}].bits;")
                 st.append(f"({{ const int64_t v = {self.ival(col)}; "
                           f"(uint64_t)__ballot((inset{i}[((uint64_t)v) >> 6] >> (v & 63)) & 1ull); }})")
             elif op == D.F_FLT_RANGE:
@@ -588,13 +406,12 @@ class _Gen:
         pk = [i for i in cols if self.cols[i].pw]
         cols = [i for i in cols if not self.cols[i].pw]
         if pk:  # bit-packed columns: straight into registers in either staging mode
-            x2 = "true" if PK_X2 else "false"
             for i in pk:
                 o.append(f"{ind}uint64_t xp{i}[{U}];")
             o.append(f"#pragma unroll\n{ind}for (int u = 0; u < {U}; ++u) {{")
             for i in pk:
                 c = self.cols[i]
-                o.append(f"{ind}  xp{i}[u] = ld_pk<{x2}>(rs{i}, (uint32_t){wl}[u] * {8 * c.pw}u, pko{c.pw});")
+                o.append(f"{ind}  xp{i}[u] = ld_pk(rs{i}, (uint32_t){wl}[u] * {8 * c.pw}u, pko{c.pw});")
             o.append(f"{ind}}}")
         if not cols:
             return
@@ -613,183 +430,6 @@ class _Gen:
             o.append(f"{ind}  dma_b<{c.lg}>(rs{i}, (uint32_t){wl}[u] << {6 + c.lg}, lo{c.lg}, "
                      f"{dst} + (u * {NP} + {c.plane}) * 256);")
         o.append(f"{ind}}}")
-
-    def _pipelined_words(self, pcols, stage, body) -> List[str]:
-        """Double-buffered word loop: the payload DMA of the next U words is in flight while the
-        current U words are aggregated (one ``s_waitcnt vmcnt(N)`` instead of a full drain).  Only
-        used when the body issues no vector-memory ops of its own (LDS/register accumulators)."""
-        U, NP = self.U, self.NP
-        SB = U * NP * 256
-        nld = sum(2 if self.cols[i].lg == 3 else 1 for i in pcols) * U
-        o: List[str] = []
-
-        def take(wl, m, any_):
-            o.append(f"#pragma unroll\n    for (int u = 0; u < {U}; ++u) {{")
-            o.append(f"      if (nz) {{ {wl}[u] = __builtin_ctzll(nz); nz &= nz - 1ull; {m}[u] = readlane64(pre, {wl}[u]); }}")
-            o.append(f"      else {{ {wl}[u] = 0; {m}[u] = 0ull; }}")
-            o.append(f"      {any_} |= {m}[u];")
-            o.append("    }")
-
-        def issue(wl, m, bufexpr):
-            o.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
-            o.append(f"      unsigned char* wbi = wb + ({bufexpr}) * {SB};")
-            self.stage_words(o, pcols, wl, "wbi")
-
-        o.append(f"    int wl[{U}]; uint64_t m[{U}]; int wl2[{U}]; uint64_t m2[{U}];")
-        o.append("    uint64_t any = 0;")
-        take("wl", "m", "any")
-        o.append("    int buf = 0;")
-        o.append("    if (any) {")
-        issue("wl", "m", "0")
-        o.append("    }")
-        o.append("    while (any) {")
-        o.append("      uint64_t any2 = 0;")
-        take("wl2", "m2", "any2")
-        o.append("      if (any2) {")
-        issue("wl2", "m2", "buf ^ 1")
-        o.append(f'        asm volatile("s_waitcnt vmcnt({nld})" ::: "memory");')
-        o.append("      } else {")
-        o.append('        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
-        o.append("      }")
-        o.append(f"      unsigned char* wbp = wb + buf * {SB};")
-        o.extend(body)
-        o.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{ wl[u] = wl2[u]; m[u] = m2[u]; }}")
-        o.append("      any = any2;")
-        o.append("      buf ^= 1;")
-        o.append("    }")
-        return o
-
-    def _reg_piped_words(self, pcols, body: List[str]) -> List[str]:
-        """Full-chunk word loop with the payload loads of step k+1 issued before step k's updates
-        (REG_PIPE): next-step registers ``<x>n`` are copied into the step's ``<x>`` at its top (the
-        copy waits only for loads issued one step earlier)."""
-        U = self.U
-        o: List[str] = []
-        names = [(f"xp{i}", "uint64_t") if self.cols[i].pw else
-                 (f"x{i}", "uint64_t" if self.cols[i].lg == 3 else "uint32_t") for i in pcols]
-
-        def loads(wl: str, ind: str) -> None:
-            o.append(f"#pragma unroll\n{ind}for (int u = 0; u < {U}; ++u) {{")
-            for i in pcols:
-                c = self.cols[i]
-                x2 = "true" if PK_X2 else "false"
-                if c.pw:
-                    o.append(f"{ind}  xp{i}n[u] = ld_pk<{x2}>(rs{i}, (uint32_t)({wl}) * {8 * c.pw}u, pko{c.pw});")
-                else:
-                    o.append(f"{ind}  x{i}n[u] = ld_b<{c.lg}>(rs{i}, (uint32_t)({wl}) << {6 + c.lg}, lo{c.lg});")
-            o.append(f"{ind}}}")
-
-        for nm, t in names:
-            o.append(f"    {t} {nm}n[{U}];")
-        loads("u", "    ")
-        o.append(f"    for (int w0_ = 0; w0_ < {D.CHUNK_WORDS}; w0_ += {U}) {{")
-        o.append(f"      int wl[{U}];")
-        o.append(f"      uint64_t m[{U}];")
-        o.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{ wl[u] = w0_ + u; m[u] = ~0ull; }}")
-        for nm, t in names:
-            o.append(f"      {t} {nm}[{U}];")
-        o.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{ " +
-                 " ".join(f"{nm}[u] = {nm}n[u];" for nm, _ in names) + " }")
-        o.append(f"      if (w0_ + {U} < {D.CHUNK_WORDS}) {{")
-        loads(f"w0_ + {U} + u", "        ")
-        o.append("      }")
-        o.append(f"      bool act[{U}];")
-        o.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) act[u] = true;")
-        o.extend(body)
-        o.append("    }")
-        return o
-
-    # ---------------------------------------------------------------- row-blocked full chunks
-    def _blocked_loop(self, pcols, boff: int, bbody: List[str]) -> List[str]:
-        """The full-chunk loop of BLOCKED: per 256-row block, exactly-sized LDS-DMA copies of every
-        payload column into the wave's staging area, then lane l takes rows 4l..4l+3 of each
-        column with one LDS read per column and extracts them at compile-time offsets (a packed
-        width that is not a multiple of 8 selects its 64-bit window by the lane's bit phase)."""
-        o: List[str] = []
-        nblk = D.CHUNK_ROWS // (64 * BR)
-        pipe = BLOCKED_PIPE and self.mode == D.M_DENSE_LDS
-        bbytes = sum(_blk_dwords(self.cols[i]) * 4 for i in pcols)
-        offs = {}
-        off = 0
-        for i in pcols:
-            offs[i] = off
-            off += _blk_dwords(self.cols[i]) * 4
-
-        def issue(blk: str, dst: str, ind: str) -> int:
-            n = 0
-            for i in pcols:
-                c = self.cols[i]
-                if c.pw:
-                    nd = 8 * c.pw + ((31 + (BR - 1) * c.pw) // 32 + 3)  # dwords a lane window may touch
-                    for j in range((nd + 63) // 64):
-                        cond = f"lane < {nd - 64 * j}" if nd - 64 * j < 64 else None
-                        ld = (f"dma_b<2>(rs{i}, (uint32_t)({blk}) * {32 * c.pw}u + {256 * j}u, (uint32_t)lane << 2, "
-                              f"{dst} + {offs[i] + 256 * j});")
-                        o.append(f"{ind}if ({cond}) {ld}" if cond else f"{ind}{ld}")
-                        n += 1
-                else:
-                    for j in range(BR << c.lg >> 2):
-                        o.append(f"{ind}dma_b<2>(rs{i}, (uint32_t)({blk}) * {64 * BR << c.lg}u + {256 * j}u, "
-                                 f"(uint32_t)lane << 2, {dst} + {offs[i] + 256 * j});")
-                        n += 1
-            return n
-
-        if pipe:
-            o.append('    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
-            issue("0", f"(wb + {boff})", "    ")
-        o.append(f"    for (int b_ = 0; b_ < {nblk}; ++b_) {{")
-        if pipe:
-            o.append(f"      unsigned char* sbk = wb + {boff} + (b_ & 1) * {bbytes};")
-            o.append(f"      if (b_ + 1 < {nblk}) {{")
-            o.append('        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the other buffer are done')
-            n = issue("b_ + 1", f"(wb + {boff} + ((b_ + 1) & 1) * {bbytes})", "        ")
-            o.append(f'        asm volatile("s_waitcnt vmcnt({n})" ::: "memory");  // block b_ has landed')
-            o.append("      } else {")
-            o.append('        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
-            o.append("      }")
-        else:
-            o.append(f"      unsigned char* sbk = wb + {boff};")
-            o.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous block\'s reads are done')
-            issue("b_", "sbk", "      ")
-            o.append('      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
-        for i in pcols:
-            c = self.cols[i]
-            o.append(f"      uint64_t bv{i}[{BR}];")
-            if c.pw:
-                w = c.pw
-                nd = (31 + (BR - 1) * w) // 32 + 3
-                o.append(f"      {{ const uint32_t* q_ = (const uint32_t*)(sbk + {offs[i]}) + bda{w};")
-                o.append(f"        uint32_t dw_[{nd}];")
-                o.append(f"#pragma unroll\n        for (int k = 0; k < {nd}; ++k) dw_[k] = q_[k];")
-                mask = f"{(1 << w) - 1}ull"
-                for u in range(BR):
-                    a, sh = (u * w) >> 5, (u * w) & 31
-                    if w % 8 == 0:  # every lane starts dword-aligned: constant window and shift
-                        o.append(f"        bv{i}[{u}] = ((((uint64_t)dw_[{a + 1}] << 32) | dw_[{a}]) >> {sh}) & {mask};")
-                    else:
-                        o.append(f"        {{ const uint32_t p_ = bsh{w} + {u * w}u; const bool h_ = (p_ >> 5) != {a}u;")
-                        o.append(f"          const uint64_t w_ = h_ ? (((uint64_t)dw_[{a + 2}] << 32) | dw_[{a + 1}]) "
-                                 f": (((uint64_t)dw_[{a + 1}] << 32) | dw_[{a}]);")
-                        o.append(f"          bv{i}[{u}] = (w_ >> (p_ & 31u)) & {mask}; }}")
-                o.append("      }")
-            elif c.lg == 0:
-                o.append(f"      {{ const uint32_t x_ = ((const uint32_t*)(sbk + {offs[i]}))[lane];")
-                o.append(f"#pragma unroll\n        for (int u = 0; u < {BR}; ++u) bv{i}[u] = (x_ >> (8 * u)) & 0xffu; }}")
-            elif c.lg == 1:
-                o.append(f"      {{ const uint64_t x_ = ((const uint64_t*)(sbk + {offs[i]}))[lane];")
-                o.append(f"#pragma unroll\n        for (int u = 0; u < {BR}; ++u) bv{i}[u] = (x_ >> (16 * u)) & 0xffffu; }}")
-            elif c.lg == 2:
-                o.append(f"      {{ const uint4 x_ = ((const uint4*)(sbk + {offs[i]}))[lane];")
-                o.append(f"        bv{i}[0] = x_.x; bv{i}[1] = x_.y; bv{i}[2] = x_.z; bv{i}[3] = x_.w; }}")
-            else:
-                o.append(f"      {{ const uint4 x_ = ((const uint4*)(sbk + {offs[i]}))[2 * lane];")
-                o.append(f"        const uint4 y_ = ((const uint4*)(sbk + {offs[i]}))[2 * lane + 1];")
-                o.append(f"        bv{i}[0] = ((uint64_t)x_.y << 32) | x_.x; bv{i}[1] = ((uint64_t)x_.w << 32) | x_.z;")
-                o.append(f"        bv{i}[2] = ((uint64_t)y_.y << 32) | y_.x; bv{i}[3] = ((uint64_t)y_.w << 32) | y_.z; }}")
-        o.append(f"      const bool act[{BR}] = {{{', '.join(['true'] * BR)}}};")
-        o.extend(bbody)
-        o.append("    }")
-        return o
 
     # ---------------------------------------------------------------- whole kernel
     def _part_record(self, body: List[str]) -> None:
@@ -878,15 +518,12 @@ class _Gen:
         pre = self.chunk_expr() if p.pre_len else None
         G, NS = p.G, p.nslots
         NCT = 1 if lay.shared else W * lay.ncopy
-        narrow = {s for s in range(NS) if _narrow_slot(p, s, self.cols)} if self.reg else set()
-        bslots = ballot_slots(p, mode, self.reg, lay.shared)
-        nl = {s: k for s, k in narrow_lds_slots(p, mode, self.reg, self.cols).items() if s not in bslots}
         for i in sorted(self.cols):
             L.append(f"  const unsigned char* c{i} = (const unsigned char*)d->cols[{i}].ptr;")
         for j, (row, stride, count) in enumerate(p.bm_leaves):
             # (VGPR-resident: read once per chunk with a per-lane address anyway)
             L.append(f"  const uint64_t* bm{j} = (const uint64_t*)" +
-                     (f"vreg((uint64_t)d->bm_bits[{j}]);" if self.vreg else f"d->bm_bits[{j}];"))
+                     f"d->bm_bits[{j}];")
         for k, kc in enumerate(p.keys):
             if kc.kind == D.K_REMAP or (kc.kind == D.K_TIME and getattr(kc, "tlut", None) is not None):
                 L.append(f"  const int32_t* rm{k} = (const int32_t*)d->kops[{k}].remap;")
@@ -898,7 +535,7 @@ class _Gen:
         for ai, a in enumerate(p.aops):
             if a["kind"] in D.HLL_KINDS:
                 if self.hll_lds and mode == D.M_DENSE_LDS:
-                    L.append(f"  unsigned char* hll{ai} = lds + {lay.hll_off + a['hll'] * G * self.m * self.hw};")
+                    L.append(f"  unsigned char* hll{ai} = lds + {lay.hll_off + a['hll'] * G * self.m};")
                 else:
                     L.append(f"  unsigned char* hll{ai} = (unsigned char*)d->aops[{ai}].hll_regs;")
             elif a["kind"] == D.A_HLL_STORED:
@@ -919,9 +556,6 @@ class _Gen:
                 body.append('      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
         def _mk_body(U: int) -> List[str]:
             body = []
-            if self.pipe:
-                body.append(f"      bool act[{U}];")
-                body.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) act[u] = (m[u] >> lane) & 1ull;")
             # phase 1: every staged read for the U words (keys + aggregator inputs) -- straight-line
             # LDS reads the compiler can issue back to back; phase 2 applies the updates.
             body.append(f"      uint64_t key_[{U}];")
@@ -1006,7 +640,7 @@ class _Gen:
                 if kind == D.A_HLL_CODE:
                     # precomputed (bucket, rho) plane (segment/hllcode.py): no per-row hash
                     ix = f"((uint64_t)slot << {p.hll_p}) + ((uint32_t){val} >> 5)"
-                    fn = "hll_max32((uint32_t*)" if wide else ("hll_lds_max32((uint32_t*)" if self.hw == 4 else "hll_max8(")
+                    fn = "hll_max32((uint32_t*)" if wide else "hll_max8("
                     body.append(f"        if ({cond}) {fn}hll{ai}, {ix}, (uint32_t){val} & 31u);")
                     continue
                 if kind == D.A_HLL:
@@ -1014,8 +648,7 @@ class _Gen:
                         body.append(f"        if ({cond}) hll_update32((uint32_t*)hll{ai}, slot, {p.hll_p}, {val}, "
                                     f"{_lit(a.get('salt', 0))});")
                     else:
-                        fn = "hll_lds_update32((uint32_t*)" if self.hw == 4 else "hll_update8("
-                        body.append(f"        if ({cond}) {fn}hll{ai}, slot, {p.hll_p}, {val}, "
+                        body.append(f"        if ({cond}) hll_update8(hll{ai}, slot, {p.hll_p}, {val}, "
                                     f"{_lit(a.get('salt', 0))});")
                     continue
                 if kind == D.A_HLL_STORED:
@@ -1024,27 +657,6 @@ class _Gen:
                     continue
                 s = a["slot"]
                 op = p.slots[s][0]
-                if s in bslots:
-                    for g in range(G):
-                        body.append(f"        bc{g}_{s} += (uint64_t)__builtin_popcountll(__ballot({cond} && key == {g}ull));")
-                    continue
-                if self.reg:
-                    body.append(f"        {{ const int64_t v_ = {val}; const int kk_ = (int)key;")
-                    for g in range(G):
-                        r = f"r{g}_{s}"
-                        pg = f"({cond} && kk_ == {g})"
-                        if s in narrow:
-                            body.append(f"          n{g}_{s} += {pg} ? (int32_t)v_ : 0;")
-                        elif op == D.S_SUM_I:
-                            body.append(f"          {r} += {pg} ? v_ : 0LL;")
-                        elif op == D.S_SUM_F:
-                            body.append(f"          {r} += {pg} ? __longlong_as_double(v_) : 0.0;")
-                        elif op == D.S_MIN_I:
-                            body.append(f"          {r} = ({pg} && v_ < {r}) ? v_ : {r};")
-                        else:
-                            body.append(f"          {r} = ({pg} && v_ > {r}) ? v_ : {r};")
-                    body.append("        }")
-                    continue
                 if mode == D.M_DENSE_LDS:
                     tgt = f"acc + (slot * {NS} + {s}) * {NCT} + copy"
                 else:
@@ -1058,21 +670,11 @@ class _Gen:
                     else:
                         body.append(f"        if ({cond}) *({tgt}) = 1ull;")
                     continue
-                if s in nl:
-                    fn = {"cnt": "lds_add_u32(", "max": "lds_max_i32(", "min": "lds_min_i32("}[nl[s]]
-                    arg = "1u" if nl[s] == "cnt" else f"(int32_t){val}"
-                    body.append(f"        if ({cond}) {fn}{tgt}, {arg});")
-                    continue
                 body.append(f"        if ({cond}) acc_update<{op}>({tgt}, {val});")
             body.append("      }")
             return body
 
         body = _mk_body(U)
-        blk = lay.blocked and not pre
-        if blk:  # the same updates over a lane's BR consecutive rows of a block (see BLOCKED)
-            self.blocked = True
-            bbody = _mk_body(BR)
-            self.blocked = False
         # ---------------- kernel text
         out = []
         out.append('#include "sdo_device.h"')
@@ -1089,12 +691,8 @@ class _Gen:
             # dword holding its first bit
             out.append(f"  const uint32_t pko{w} = (((uint32_t)lane * {w}u) >> 5) * 4u;")
             out.append(f"  const uint32_t psh{w} = ((uint32_t)lane * {w}u) & 31u;")
-        if blk:  # a lane's first dword / bit of its BR consecutive rows in a packed block
-            for w in sorted({c.pw for i, c in self.cols.items() if c.pw and i >= D.PAYLOAD_BASE}):
-                out.append(f"  const uint32_t bda{w} = ((uint32_t)lane * {BR * w}u) >> 5;")
-                out.append(f"  const uint32_t bsh{w} = ((uint32_t)lane * {BR * w}u) & 31u;")
         out.append(f"  unsigned char* wb = lds + {lay.cache_off} + wave * {lay.wave_bytes};")
-        stage_bytes = 0 if self.regstage else U * NP * 256 * (2 if self.pipe else 1)
+        stage_bytes = 0 if self.regstage else U * NP * 256
         out.append(f"  uint64_t* bmw = (uint64_t*)(wb + {stage_bytes});")
         out.append("  uint64_t* acc = (uint64_t*)lds;")
         if lay.shared:
@@ -1114,8 +712,7 @@ class _Gen:
             out.append("  const uint64_t lmlt = (1ull << lane) - 1ull;")
         if mode == D.M_DENSE_LDS:
             out.append(f"  for (int i = threadIdx.x; i < {G * NS * NCT}; i += {W * 64}) {{")
-            cinit = {"cnt": 0, "max": -(1 << 31) & 0xffffffff, "min": (1 << 31) - 1}
-            inits = ", ".join(_lit(cinit[nl[s]]) if s in nl else _lit(init) for s, (_, init) in enumerate(p.slots))
+            inits = ", ".join(_lit(init) for _, init in p.slots)
             out.append(f"    constexpr int64_t init[{NS}] = {{{inits}}};")
             out.append(f"    acc[i] = (uint64_t)init[(i / {NCT}) % {NS}];")
             out.append("  }")
@@ -1123,18 +720,6 @@ class _Gen:
                 out.append(f"  for (int i = threadIdx.x; i < {lay.hll_bytes // 4}; i += {W * 64}) "
                            f"((uint32_t*)(lds + {lay.hll_off}))[i] = 0u;")
             out.append("  __syncthreads();")
-        for s in sorted(bslots):
-            out.append("  " + " ".join(f"uint64_t bc{g}_{s} = 0;" for g in range(G)))
-        if self.reg:
-            for g in range(G):
-                for s in range(NS):
-                    op, init = p.slots[s]
-                    if op == D.S_SUM_F:
-                        out.append(f"  double r{g}_{s} = 0.0;")
-                    else:
-                        out.append(f"  int64_t r{g}_{s} = {_lit(init)};")
-                    if s in narrow:
-                        out.append(f"  int32_t n{g}_{s} = 0;")
         out.append(f"  const int64_t total_waves = (int64_t)gridDim.x * {W};")
         out.append(f"  const int64_t gw = (int64_t)blockIdx.x * {W} + wave;")
         out.append("  const int64_t num_rows = d->num_rows;")
@@ -1179,76 +764,42 @@ class _Gen:
         if pre:
             out.append(f"    pre &= {pre};")
         out.append("    uint64_t nz = __ballot(pre != 0ull);")
-        if self.pipe:
-            out.extend(self._pipelined_words(pcols, stage, body))
-        else:
-            full = FULL_CHUNKS and not pre and mode in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL, D.M_HASH)
-            if full:
-                out.append(f"    if (clo == crow0 && chi == crow0 + {D.CHUNK_ROWS}) {{")
-                if blk:
-                    boff = stage_bytes + (len(p.bm_leaves) * 512 if need_bmw else 0)
-                    out.extend(self._blocked_loop(pcols, boff, bbody))
-                elif REG_PIPE and self.regstage and (p.final_pre or not p.filter_len) and pcols:
-                    out.extend(self._reg_piped_words(pcols, body))
-                else:
-                    out.append(f"    for (int w0_ = 0; w0_ < {D.CHUNK_WORDS}; w0_ += {U}) {{")
-                    out.append(f"      int wl[{U}];")
-                    out.append(f"      uint64_t m[{U}];")
-                    out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{ wl[u] = w0_ + u; m[u] = ~0ull; }}")
-                    out.extend(self._words_tail(fcols, word_filter, mode, U, stage, body))
-                    out.append("    }")
-                out.append("    } else {")
-            dense = DENSE_WORDS > 0 and bool(pre) and mode in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL, D.M_HASH)
-            if dense:
-                out.append(f"    if (__popcll(nz) >= {DENSE_WORDS}) {{")
-                out.append(f"    for (int w0_ = 0; w0_ < {D.CHUNK_WORDS}; w0_ += {U}) {{")
-                out.append(f"      int wl[{U}];")
-                out.append(f"      uint64_t m[{U}];")
-                out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{ wl[u] = w0_ + u; m[u] = readlane64(pre, w0_ + u); }}")
-                out.extend(self._words_tail(fcols, word_filter, mode, U, stage, body))
-                out.append("    }")
-                out.append("    } else {")
-            out.append("    while (nz) {")
+        full = FULL_CHUNKS and not pre and mode in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL, D.M_HASH)
+        if full:
+            out.append(f"    if (clo == crow0 && chi == crow0 + {D.CHUNK_ROWS}) {{")
+            out.append(f"    for (int w0_ = 0; w0_ < {D.CHUNK_WORDS}; w0_ += {U}) {{")
             out.append(f"      int wl[{U}];")
             out.append(f"      uint64_t m[{U}];")
-            out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{")
-            out.append("        if (nz) { wl[u] = __builtin_ctzll(nz); nz &= nz - 1ull; m[u] = readlane64(pre, wl[u]); }")
-            out.append("        else { wl[u] = 0; m[u] = 0ull; }")
-            out.append("      }")
+            out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{ wl[u] = w0_ + u; m[u] = ~0ull; }}")
             out.extend(self._words_tail(fcols, word_filter, mode, U, stage, body))
             out.append("    }")
-            if dense:
-                out.append("    }")
-            if full:
-                out.append("    }")
-        for g in range(G if narrow else 0):
-            for s in sorted(narrow):
-                out.append(f"    r{g}_{s} += n{g}_{s}; n{g}_{s} = 0;")
+            out.append("    } else {")
+        dense = DENSE_WORDS > 0 and bool(pre) and mode in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL, D.M_HASH)
+        if dense:
+            out.append(f"    if (__popcll(nz) >= {DENSE_WORDS}) {{")
+            out.append(f"    for (int w0_ = 0; w0_ < {D.CHUNK_WORDS}; w0_ += {U}) {{")
+            out.append(f"      int wl[{U}];")
+            out.append(f"      uint64_t m[{U}];")
+            out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{ wl[u] = w0_ + u; m[u] = readlane64(pre, w0_ + u); }}")
+            out.extend(self._words_tail(fcols, word_filter, mode, U, stage, body))
+            out.append("    }")
+            out.append("    } else {")
+        out.append("    while (nz) {")
+        out.append(f"      int wl[{U}];")
+        out.append(f"      uint64_t m[{U}];")
+        out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{")
+        out.append("        if (nz) { wl[u] = __builtin_ctzll(nz); nz &= nz - 1ull; m[u] = readlane64(pre, wl[u]); }")
+        out.append("        else { wl[u] = 0; m[u] = 0ull; }")
+        out.append("      }")
+        out.extend(self._words_tail(fcols, word_filter, mode, U, stage, body))
+        out.append("    }")
+        if dense:
+            out.append("    }")
+        if full:
+            out.append("    }")
         if mode == D.M_PART:
             out.append("    if (lane == 0) pend[c] = cbase + woff;")
         out.append("  }")
-        for s in sorted(bslots):
-            # the wave's ballot counts (uniform) into lane 0's accumulator copy
-            for g in range(G):
-                out.append(f"  if (lane == 0 && bc{g}_{s}) acc_update<{D.S_SUM_I}>(acc + ({g} * {NS} + {s}) * {NCT} + copy, "
-                           f"(int64_t)bc{g}_{s});")
-        if self.reg:
-            # wave-reduce each register partial; lane 0 stores the wave's copy for the block flush
-            for g in range(G):
-                for s in range(NS):
-                    op = p.slots[s][0]
-                    v = f"r{g}_{s}"
-                    out.append("  {")
-                    if op == D.S_SUM_F:
-                        out.append(f"    double v = {v};")
-                        out.append("    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);")
-                        out.append("    const int64_t b = __double_as_longlong(v);")
-                    else:
-                        out.append(f"    int64_t v = {v};")
-                        out.append(f"    for (int o = 32; o > 0; o >>= 1) v = acc_combine<{op}>(v, __shfl_xor(v, o));")
-                        out.append("    const int64_t b = v;")
-                    out.append(f"    if (lane == 0) acc[({g} * {NS} + {s}) * {NCT} + wave] = (uint64_t)b;")
-                    out.append("  }")
         if mode == D.M_DENSE_LDS:
             out.append("  __syncthreads();")
             out.append(f"  for (int i = threadIdx.x; i < {G * NS}; i += {W * 64}) {{")
@@ -1258,25 +809,9 @@ class _Gen:
             out.append(f"    constexpr int ops[{NS}] = {{{ops}}};")
             out.append(f"    constexpr int64_t init[{NS}] = {{{inits}}};")
             out.append(f"    const uint64_t* a = acc + (int64_t)i * {NCT};")
-            if nl:
-                # 32-bit cells widen: counts zero-extend, min / max sign-extend (untouched -> init)
-                kinds = ", ".join(str({"cnt": 1, "max": 2, "min": 3}.get(nl.get(s2), 0)) for s2 in range(NS))
-                out.append(f"    constexpr int nk[{NS}] = {{{kinds}}};")
-                out.append("    auto wid = [&](uint64_t r) -> int64_t {")
-                out.append("      if (nk[s] == 0) return (int64_t)r;")
-                out.append("      if (nk[s] == 1) return (int64_t)(uint32_t)r;")
-                out.append("      const int32_t x = (int32_t)(uint32_t)r;")
-                out.append("      if (nk[s] == 2 && x == (-2147483647 - 1)) return init[s];")
-                out.append("      if (nk[s] == 3 && x == 2147483647) return init[s];")
-                out.append("      return (int64_t)x;")
-                out.append("    };")
-                out.append("    int64_t v = wid(a[0]);")
-                out.append(f"    for (int k = 1; k < {NCT}; ++k) {{")
-                out.append("      const int64_t x = wid(a[k]);")
-            else:
-                out.append("    int64_t v = (int64_t)a[0];")
-                out.append(f"    for (int k = 1; k < {NCT}; ++k) {{")
-                out.append("      const int64_t x = (int64_t)a[k];")
+            out.append("    int64_t v = (int64_t)a[0];")
+            out.append(f"    for (int k = 1; k < {NCT}; ++k) {{")
+            out.append("      const int64_t x = (int64_t)a[k];")
             out.append("      switch (ops[s]) {")
             out.append(f"        case {D.S_SUM_I}: v += x; break;")
             out.append(f"        case {D.S_SUM_F}: v = __double_as_longlong(__longlong_as_double(v) + __longlong_as_double(x)); break;")
@@ -1293,12 +828,8 @@ class _Gen:
                     # four byte registers per dword: one read (and rarely a CAS) per 4 registers
                     out.append(f"  {{ uint32_t* g = (uint32_t*)d->aops[{ai}].hll_regs;")
                     out.append(f"    const uint32_t* r = (const uint32_t*)hll{ai};")
-                    if self.hw == 4:  # u32 registers -> four packed bytes per global dword
-                        out.append(f"    for (int i = threadIdx.x; i < {G * self.m // 4}; i += {W * 64}) "
-                                   "hll_merge_word8(g + i, pack_regs8(r + 4 * i));")
-                    else:
-                        out.append(f"    for (int i = threadIdx.x; i < {G * self.m // 4}; i += {W * 64}) "
-                                   "hll_merge_word8(g + i, r[i]);")
+                    out.append(f"    for (int i = threadIdx.x; i < {G * self.m // 4}; i += {W * 64}) "
+                               "hll_merge_word8(g + i, r[i]);")
                     out.append("  }")
         out.append("}")
         return "\n".join(out) + "\n"
@@ -1388,26 +919,17 @@ class JitScan:
     """A compiled, specialized scan kernel for one ScanProgram shape."""
 
     def __init__(self, prog, mode: int, U: int, hll_lds: bool, m: int, narrow4: bool, load: bool = True,
-                 reg: Optional[bool] = None, pipe: bool = False, budget: int = 150 * 1024,
-                 regstage: bool = False, shared: bool = False, literals: bool = False):
-        self.reg = False if shared else (reg_eligible(prog, mode) if reg is None else reg)
+                 budget: int = 150 * 1024, regstage: bool = False, shared: bool = False, literals: bool = False):
         self.literals = literals
-        self._args = (prog, mode, U, hll_lds, m, narrow4, load, self.reg, pipe, budget, regstage, shared)
-        self.lay = layout(prog, mode, U, hll_lds, m, self.reg, pipe and not regstage, budget, regstage, shared)
+        self._args = (prog, mode, U, hll_lds, m, narrow4, load, budget, regstage, shared)
+        self.lay = layout(prog, mode, U, hll_lds, m, budget, regstage, shared)
         if self.lay.total > 160 * 1024:
             raise ValueError(f"jit layout needs {self.lay.total} B of LDS")
-        g = _Gen(prog, mode, U, hll_lds, narrow4, self.lay, m, self.reg, literals)
-        tag = hashlib.sha1(repr((mode, U, self.reg, pipe, self.lay.ncopy, regstage, self.lay.shared)).encode()
+        g = _Gen(prog, mode, U, hll_lds, narrow4, self.lay, m, literals)
+        tag = hashlib.sha1(repr((mode, U, self.lay.ncopy, regstage, self.lay.shared)).encode()
                            ).hexdigest()[:6]
         self.name = f"sdo_jit_{tag}"
         self.src = g.source(self.name)
-        if JIT_VREG and not literals and g.nconst >= VREG_MIN_CONSTS:
-            # dozens of descriptor-loaded bounds (TPC-H Q19: 26) spill SGPRs inside the scan loop;
-            # VGPRs hold them without spills (Q19 5.4 -> 3.8 ms) but cost occupancy elsewhere (Q16's
-            # hash scan 13.4 -> 15.9 ms), and a repeated statement's literal-specialized kernel
-            # (JitScan.specialized) has neither problem: opt-in (SDO_JIT_VREG=1)
-            g = _Gen(prog, mode, U, hll_lds, narrow4, self.lay, m, self.reg, literals, vreg=True)
-            self.src = g.source(self.name)
         self.handle = compile_source(self.src, self.name) if load else -1
         if not load:
             compile_code(self.src, self.name)
@@ -1417,9 +939,9 @@ class JitScan:
         """The same kernel with this program's query constants baked in as literals (a repeated
         statement's own code object: folded bounds, no descriptor loads, fewer live scalars --
         TPC-H Q19 3.4 vs 3.8 ms).  Same layout, grid and descriptor, so it swaps in place."""
-        prog, mode, U, hll_lds, m, narrow4, load, reg, pipe, budget, regstage, shared = self._args
-        return JitScan(prog, mode, U, hll_lds, m, narrow4, load, reg=reg, pipe=pipe, budget=budget,
-                       regstage=regstage, shared=shared, literals=True)
+        prog, mode, U, hll_lds, m, narrow4, load, budget, regstage, shared = self._args
+        return JitScan(prog, mode, U, hll_lds, m, narrow4, load, budget=budget, regstage=regstage,
+                       shared=shared, literals=True)
 
     def occupancy(self) -> int:
         """Resident 512-thread workgroups per CU of the compiled kernel (registers and LDS)."""

@@ -172,42 +172,6 @@ def test_jit_stored_hll_union_compiles(tmp_path, monkeypatch):
     assert "hll_merge_csr(hll" in js.src and "sko" in js.src
 
 
-def test_jit_narrow_lds_cells_and_u32_hll_registers_compile(ds_small, tmp_path, monkeypatch):
-    """TPC-H Q1's kernel with 32-bit LDS cells (count, max of an int32-range column) and u32 LDS HLL
-    registers (one ds_max_u32 per row) compiles for gfx950; the block fold widens the 32-bit cells."""
-    from spark_druid_olap_amd.engine.lower import Lowerer
-    from spark_druid_olap_amd.models.bench_queries import bench_specs
-    from spark_druid_olap_amd.ops import desc as D
-    from spark_druid_olap_amd.ops import jit
-
-    monkeypatch.setenv("SDO_JIT_CACHE", str(tmp_path))
-    monkeypatch.setattr(jit, "NARROW_LDS", True)
-    monkeypatch.setattr(jit, "HLL32_LDS", True)
-    q = dict(bench_specs())["TPCH Q1"]
-    prog = Lowerer(ds_small).lower_aggregate(q.intervals, q.filter, q.dimensions, q.granularity, q.aggregations)
-    from spark_druid_olap_amd.engine.lower import column_tensor
-    from spark_druid_olap_amd.segment import packed as PK
-
-    prog.packed = {}  # bit-packed copies, as the GPU path attaches them (a provable value range)
-    for c in list(prog.fcols) + list(prog.pcols):
-        t = column_tensor(ds_small, c)[:ds_small.num_rows]
-        if not t.is_floating_point():
-            lo, hi = int(t.to(torch.int64).min()), int(t.to(torch.int64).max())
-            prog.packed[c] = PK.pack(column_tensor(ds_small, c), ds_small.num_rows, lo, hi)
-    nl = jit.narrow_lds_slots(prog, D.M_DENSE_LDS, False)
-    assert "cnt" in nl.values() and "max" in nl.values()
-    assert all(prog.slots[s][0] != D.S_SUM_I or k == "cnt" for s, k in nl.items())
-    js = jit.JitScan(prog, D.M_DENSE_LDS, 4, True, 2048, True, load=False, reg=False, budget=159 * 1024)
-    assert js.lay.hll_bytes == prog.nhll * prog.G * 2048 * 4
-    assert "lds_add_u32(" in js.src and "lds_max_i32(" in js.src and "hll_lds_max32(" in js.src
-    assert "pack_regs8(" in js.src and "wid(a[k])" in js.src
-    # off: the 8-byte atomics and byte registers
-    monkeypatch.setattr(jit, "NARROW_LDS", False)
-    monkeypatch.setattr(jit, "HLL32_LDS", False)
-    js0 = jit.JitScan(prog, D.M_DENSE_LDS, 4, True, 2048, True, load=False, reg=False, budget=159 * 1024)
-    assert "lds_add_u32(" not in js0.src and "hll_max8(" in js0.src
-
-
 def _unique_kernel(tag: str) -> str:
     # enough template work that hipRTC takes a noticeable time; the tag makes the source (and the
     # disk-cache key) unique to this test run

@@ -27,6 +27,9 @@ def main():
     from spark_druid_olap_amd.segment import packed as PK
     from spark_druid_olap_amd.session import Session
 
+    dump = sys.argv[sys.argv.index("--dump") + 1] if "--dump" in sys.argv else None
+    if dump:
+        os.makedirs(dump, exist_ok=True)
     jit.compile_code = lambda src, name: b""  # generate only
     jit.compile_source = lambda src, name: -1
     DE.native.narrow4 = lambda: 1
@@ -66,6 +69,11 @@ def main():
                     h1 = hashlib.sha1(js.src.encode()).hexdigest()[:12]
                     h2 = hashlib.sha1(sp.src.encode()).hexdigest()[:12]
                     print(f"{label}/{name}#{i}.{j}: {gp.mode} U={js.U} lds={js.lay.total} {h1} {h2}")
+                    if dump:
+                        tag = f"{label}_{name}_{i}_{j}".replace(" ", "_").replace("/", "_").replace(",", "")
+                        for suffix, src in (("shape", js.src), ("lit", sp.src)):
+                            with open(os.path.join(dump, f"{tag}.{suffix}.hip"), "w") as f:
+                                f.write(src)
 
     flat = tpch.generate_flat(0.05, "cpu")
     ds = tpch.to_datasource(flat, profile="bench")

@@ -58,13 +58,10 @@ def main():
                             if PK.worth_packing(t, PK.width_for(lo, hi)):
                                 prog.packed[c] = PK.pack(t, ds.num_rows, lo, hi)
                 regstage = jit.prefer_regstage(prog)
-                lay = jit.layout(prog, mode, 4, bool(prog.nhll) and gp.hll_lds, 1 << prog.hll_p, False, False,
+                lay = jit.layout(prog, mode, 4, bool(prog.nhll) and gp.hll_lds, 1 << prog.hll_p,
                                  (160 * 1024) // 3 - 512, regstage, gp.shared)
                 g = jit._Gen(prog, mode, 4, bool(prog.nhll) and gp.hll_lds, True, lay, 1 << prog.hll_p)
                 src = g.source("sdo_jit_probe")
-                if jit.JIT_VREG and g.nconst >= jit.VREG_MIN_CONSTS:  # as JitScan decides
-                    g = jit._Gen(prog, mode, 4, bool(prog.nhll) and gp.hll_lds, True, lay, 1 << prog.hll_p, vreg=True)
-                    src = g.source("sdo_jit_probe")
                 print(src)
                 if os.environ.get("SDO_JIT_COMPILE"):  # hipRTC for gfx950 (no GPU needed)
                     code = jit.compile_code(src, "sdo_jit_probe")

@@ -60,7 +60,7 @@ def main():
         only = args[args.index("--") + 1:]
         args = args[:args.index("--")]
     sf = float(args[0]) if args else 100
-    variants = args[1:] or ["reg1pipe1"]
+    variants = args[1:] or ["base"]
     world = init_world()
     dev = world.device()
     torch.cuda.set_device(dev)
@@ -78,8 +78,6 @@ def main():
     from spark_druid_olap_amd.ops import jit as J
 
     for var in variants:
-        DE.USE_REG = "reg1" in var
-        DE.USE_PIPE = "pipe1" in var
         mb = re.search(r"b(\d+)", var)
         DE.JIT_BLOCKS = int(mb.group(1)) if mb else 3
         mc = re.search(r"c(\d+)", var)
@@ -94,8 +92,7 @@ def main():
             pq = eng.prepare(qs, ds)
             sc = pq.scans[0][2]
             j = getattr(sc, "jit", None)
-            info = (f"mode={sc.mode} reg={getattr(j, 'reg', None)} pipe={getattr(j.lay, 'pipe', None) if j else None} "
-                    f"U={getattr(j, 'U', None)} grid={sc.grid} lds={j.lay.total if j else None}")
+            info = (f"mode={sc.mode} U={getattr(j, 'U', None)} grid={sc.grid} lds={j.lay.total if j else None}")
             ts = []
             r = None
             for i in range(6):
