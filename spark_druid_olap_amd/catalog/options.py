@@ -112,7 +112,7 @@ CONF_ENTRIES: List[ConfEntry] = [
     ConfEntry("spark.sparklinedata.tz.id", "UTC", "time zone for date/time evaluation"),
     ConfEntry("spark.sparklinedata.druid.selectquery.pagesize", 10000, "rows per Select page", int),
     ConfEntry("spark.sparklinedata.druid.stream.results", True,
-              "Thrift server: stream Select-backed results page by page instead of materialising them", bool),
+              "Thrift server: stream Select-backed and large groupBy results page by page instead of materialising them", bool),
     ConfEntry("spark.sparklinedata.druid.max.connections", 100, "(remote Druid only)", int),
     ConfEntry("spark.sparklinedata.druid.max.connections.per.route", 20, "(remote Druid only)", int),
     ConfEntry("spark.sparklinedata.druid.querycostmodel.enabled", True, "use the cost model", bool),

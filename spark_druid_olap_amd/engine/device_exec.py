@@ -289,7 +289,8 @@ class PreparedScan:
         b.hll32 = [torch.empty(rows * self.m, dtype=torch.int32, device=dev) for _ in range(nblocks)] \
             if self.hll32 else []
         b.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
-        b.touch = torch.zeros(((rows + 7) // 8 * 8) if self.touch else 8, dtype=torch.uint8, device=dev)
+        # (padded to whole 64-group words: native.touch_compact reads it 16 bytes per lane)
+        b.touch = torch.zeros(((rows + 63) // 64 * 64) if self.touch else 64, dtype=torch.uint8, device=dev)
         b.clean = False
         hll_offs = []
         off = prog.G * prog.nslots * 8 * (BLOCK // 64)
@@ -562,10 +563,8 @@ class PreparedScan:
             for h8, h32 in zip(b.hll, b.hll32):  # scan-time u32 registers -> the byte registers
                 h8.copy_(h32)
             if self.touch:
-                idx = native.nonzero_rows(b.touch)
-                acc = b.acc.index_select(0, idx)
-                b.acc.index_copy_(0, idx, b.init_row.expand(idx.numel(), -1).contiguous())
-                b.touch.index_fill_(0, idx, 0)
+                # touched groups' ids and rows, re-initialised in the same pass (post_scan.hip touch_*)
+                idx, acc = native.touch_compact(b.touch, b.acc, b.init_row)
                 b.clean = True
                 return Partials("sparse", acc, idx, [])
             if self.pres_bytes:
@@ -906,7 +905,7 @@ def part_hash_layout(prog, scale: int = 1) -> dict:
     from ..ops import jit
 
     ns = max(1, prog.nslots)
-    cap_log2 = min(14, int(math.floor(math.log2(HASH_TABLE_BYTES // (8 * (1 + ns))))))
+    cap_log2 = max(6, min(14, int(math.floor(math.log2(HASH_TABLE_BYTES // (8 * (1 + ns)))))))
     groups = max(1.0, min(float(prog.G), float(getattr(prog, "est_rows", prog.G)) * 1.2))
     nsub = max(8, int(math.ceil(groups * scale / (1 << (cap_log2 - 1)))))
     bits = min(20, max(3, int(math.ceil(math.log2(nsub)))))

@@ -98,6 +98,7 @@ def is_cuda_ds(ds: DataSource) -> bool:
 
 # below this many merged groups HAVING is left to the host (_post re-applies it either way)
 HAVING_MIN_ROWS = 4096
+STREAM_MIN_GROUPS = 1 << 18  # planner group estimate above which a groupBy result streams (iter_pages)
 
 
 class PreparedQuery:
@@ -327,6 +328,49 @@ class PreparedQuery:
         res.stats["exec_ms"] = (time.perf_counter() - t0) * 1e3
         self.last_stats = res.stats
         return res
+
+    def streamable(self) -> bool:
+        """A groupBy whose result is its groups in production order (no HAVING / limitSpec / topN
+        ordering on the host, no theta sketches, no re-aggregating key formats) over a key space the
+        planner expects to be large: ``iter_pages`` can then decode and ship it a page at a time
+        (the reference streams group-by rows from Druid, DruidQueryResultIterator.scala:58-90)."""
+        qs = self.qs
+        if qs.queryType != "groupBy" or getattr(qs, "having", None) is not None or qs.limitSpec is not None \
+                or not self.scans:
+            return False
+        prog = self.scans[0][1]
+        if getattr(self._full_prog, "thetas", None) or any(kc.collapse for kc in prog.keys):
+            return False
+        return min(float(prog.G), float(getattr(prog, "est_rows", prog.G) or prog.G)) >= STREAM_MIN_GROUPS
+
+    def iter_pages(self, page_rows: int):
+        """The result as QueryResult pages of at most ``page_rows`` groups: the merged partials stay
+        on the device and each page is finalized (decoded, copied to the host) only when it is
+        pulled, so host memory holds one page of a million-group answer.  Multi-rank: the groups
+        are gathered to rank 0 (root-only results); the other ranks yield one empty page."""
+        from ..parallel.p2p import check_status
+
+        t0 = time.perf_counter()
+        root_only = self.world.distributed and root_only_results()
+        prog, part, _ = self.run_partials(t0, root_only)
+        check_status(part)
+        if root_only and self.world.rank != 0:
+            part = empty_partials(prog, self.ds.device)
+        part = part.compact()
+        # private copies: the slot's scan buffers may be reused by its next execution while the
+        # client is still paging through this one
+        part = Partials("sparse", part.acc.clone(), part.keys.clone(), [h.clone() for h in part.hll],
+                        part.scattered, part.status)
+        if part.acc.is_cuda:
+            torch.cuda.current_stream(part.acc.device).synchronize()  # pages may be pulled on other threads
+        R = part.rows
+        out_types = getattr(self, "out_types", None)
+        for a in range(0, max(R, 1), page_rows):
+            b = min(R, a + page_rows)
+            sub = Partials("sparse", part.acc[a:b], part.keys[a:b], [h[a:b] for h in part.hll])
+            res = self._post(prog, finalize(prog, sub, out_types))
+            res.stats.update(page=a // page_rows, groups_total=R)
+            yield res
 
     def run_partials(self, t0: float, root_only: bool = False):
         """scan -> merge across ranks -> device HAVING / top-K pruning; (prog, merged partials,

@@ -173,14 +173,15 @@ def _const_column(R: int, v: "_Const") -> np.ndarray:
     return np.broadcast_to(np.asarray(v.value, dtype=v.dtype), (R,))
 
 
-def _device_typed(kc, ids: torch.Tensor, sqlt: Optional[str]):
-    """Typed values of a dictionary-id key computed ON THE DEVICE for a numeric SQL output type
-    (the same values ``sql/execute.py:_dict_series`` would produce on the host): integer range
-    dictionaries are ``start + id``; other dictionaries of up to 4M entries gather from a cached
-    device table of their typed values; a one-entry dictionary is a constant.  ``int`` and narrower
-    SQL types travel as int32.  A million-group result (TPC-H Q3: o_orderkey, o_shippriority) then
-    ships final values at their SQL width and the host does no per-row decode pass.  None when not
-    applicable (strings, NULL-bearing dictionaries, huge non-range dictionaries)."""
+def _typed_plan(kc, sqlt: Optional[str], device):
+    """How a dictionary-id key becomes its final numeric SQL-typed values ON THE DEVICE (the same
+    values ``sql/execute.py:_dict_series`` would produce on the host): integer range dictionaries
+    are ``start + id`` -> ("range", start, torch dtype); other dictionaries of up to 4M entries gather
+    from a cached device table of their typed values -> ("table", table); a one-entry dictionary is
+    a ``_Const``.  ``int`` and narrower SQL types travel as int32.  A million-group result (TPC-H
+    Q3: o_orderkey, o_shippriority) then ships final values at their SQL width and the host does no
+    per-row decode pass.  None when not applicable (strings, NULL-bearing dictionaries, huge
+    non-range dictionaries)."""
     d = getattr(kc, "dictionary", None)
     if d is None or sqlt is None or kc.orig is not None:
         return None
@@ -193,13 +194,12 @@ def _device_typed(kc, ids: torch.Tensor, sqlt: Optional[str]):
     if hasattr(d, "start") and not getattr(d, "has_null", False) and not hasattr(d, "prefix"):
         lo, hi = int(d.start), int(d.start) + len(d) - 1
         if narrow and _I32[0] <= lo and hi <= _I32[1]:
-            return ids.to(torch.int32) + lo
-        v = ids.to(torch.int64) + lo
-        return v if bt in _INT_T else v.to(torch.float64)
+            return ("range", lo, torch.int32)
+        return ("range", lo, torch.int64 if bt in _INT_T else torch.float64)
     if len(d) > (1 << 22):
         return None
     cache = d.__dict__.setdefault("_dev_typed", {})
-    key = (bt, str(ids.device))
+    key = (bt, str(device))
     tab = cache.get(key)
     if tab is None:
         from ..sql.execute import _raw
@@ -215,13 +215,27 @@ def _device_typed(kc, ids: torch.Tensor, sqlt: Optional[str]):
             else:
                 if narrow and _I32[0] <= int(arr.min()) and int(arr.max()) <= _I32[1]:
                     arr = arr.astype(np.int32)
-                tab = torch.from_numpy(np.ascontiguousarray(arr)).to(ids.device)
+                tab = torch.from_numpy(np.ascontiguousarray(arr)).to(device)
         cache[key] = tab
     if tab is False:
         return None
     if isinstance(tab, _Const):
         return tab
-    return tab.index_select(0, ids.to(torch.int64))
+    return ("table", tab)
+
+
+def _device_typed(kc, ids: torch.Tensor, sqlt: Optional[str]):
+    """Typed values of a dictionary-id key computed on the device with torch ops (``_typed_plan``)."""
+    plan = _typed_plan(kc, sqlt, ids.device)
+    if plan is None or isinstance(plan, _Const):
+        return plan
+    if plan[0] == "range":
+        lo, dt = plan[1], plan[2]
+        if dt == torch.int32:
+            return ids.to(torch.int32) + lo
+        v = ids.to(torch.int64) + lo
+        return v if dt == torch.int64 else v.to(torch.float64)
+    return plan[1].index_select(0, ids.to(torch.int64))
 
 
 def _narrow_ids(kc, ids: torch.Tensor) -> torch.Tensor:
@@ -261,6 +275,152 @@ def _agg_outputs_dev(prog, acc: torch.Tensor, skip) -> Dict[str, torch.Tensor]:
     return out
 
 
+SMALL_DENSE_WORDS = 1 << 20  # dense states up to this many accumulator words are fetched whole
+NATIVE_DECODE = True  # sparse finalize through post_scan.hip sparse_decode_kernel (tests compare both)
+_LUT_T = {torch.int32: 1, torch.int64: 2, torch.float64: 3}
+_OUT_NP = {0: np.int16, 1: np.int32, 2: np.int64, 3: np.float64, 4: np.float64, 5: np.int64}
+_OUT_W = {0: 2, 1: 4, 2: 8, 3: 8, 4: 8, 5: 8}
+_DT_OUT = {torch.int32: 1, torch.int64: 2, torch.float64: 3}
+
+
+def _dev_table(holder, key, t, device) -> torch.Tensor:
+    """A decode table (FD map, typed dictionary values) on the device as int32 / int64 / f64,
+    cached on ``holder`` (the prepared program or key) -- not re-uploaded per execution."""
+    cache = holder.__dict__.setdefault("_dec_tabs", {})
+    ck = (key, str(device))
+    v = cache.get(ck)
+    if v is None:
+        t = torch.as_tensor(t)
+        if t.dtype not in _LUT_T:
+            t = t.to(torch.float64 if t.is_floating_point() else torch.int64)
+        v = cache[ck] = t.to(device).contiguous()
+    return v
+
+
+def _native_sparse(prog, parts: Partials, out_types, want_gid: bool):
+    """Sparse finalize through ONE kernel and ONE device-to-host copy (ops/csrc/post_scan.hip
+    sparse_decode_kernel): every key component, functionally dependent key, derived aggregate and
+    aggregator output is computed at its final width into one device buffer.  Returns
+    (key_ids, derived_ids, derived_agg_vals, agg_host, gid, typed) or None when a column needs the
+    general torch path (fixed-point float sums, float FD aggregate tables, > 16 columns)."""
+    g = parts.keys
+    if not g.is_cuda or _NO_DEVICE_DECODE:
+        return None
+    dev = g.device
+    R = int(g.numel())
+    specs, consts, typed = [], {}, {}
+
+    def key_base(det):
+        kd = prog.keys[det]
+        orig = 0
+        if kd.orig is not None:
+            orig = _dev_table(kd, "orig", torch.from_numpy(np.asarray(kd.orig, dtype=np.int64)), dev).data_ptr()
+        return int(kd.stride), max(1, int(kd.card)), orig
+
+    def typed_spec(i, kc, stride, card, orig, lut, lut_key):
+        """(key i's spec) through its SQL-typed plan, or as narrow ids."""
+        plan = _typed_plan(kc, out_types.get(kc.name), dev) if out_types else None
+        lut_ptr = lut.data_ptr() if lut is not None else 0
+        lut_t = _LUT_T[lut.dtype] if lut is not None else 0
+        if isinstance(plan, _Const):
+            typed[i] = plan
+            consts[i] = plan
+            return None
+        if plan is not None and plan[0] == "range":
+            typed[i] = "dev"
+            return (0, _DT_OUT[plan[2]], lut_t, 0, stride, card, int(plan[1]), orig, lut_ptr, 0.0)
+        if plan is not None:  # typed table (composed with the FD map for a derived key)
+            tab = plan[1]
+            if lut is not None:
+                tab = _dev_table(prog, ("typed", lut_key, kc.name), tab.index_select(0, lut.to(torch.int64)), dev)
+            typed[i] = "dev"
+            return (0, 4 if tab.dtype == torch.float64 else _DT_OUT[tab.dtype], _LUT_T[tab.dtype], 0, stride, card, 0,
+                    orig, tab.data_ptr(), 0.0)
+        out = 0 if (kc.card <= (1 << 15) and getattr(kc, "dictionary", None) is not None) else \
+            (1 if kc.card < 2 ** 31 else 2)
+        return (0, out, lut_t, 0, stride, card, 0, orig, lut_ptr, 0.0)
+
+    order = []  # (role, index) per spec
+    nk = len(prog.keys)
+    for i, kc in enumerate(prog.keys):
+        sp = typed_spec(i, kc, int(kc.stride), max(1, int(kc.card)), 0, None, None)
+        if sp is not None:
+            specs.append(sp)
+            order.append(("key", i))
+    for j, (kc, det, lut) in enumerate(getattr(prog, "derived", ())):
+        stride, card, orig = key_base(det)
+        lut_d = _dev_table(prog, ("fd", j), lut, dev)
+        if lut_d.dtype == torch.float64:
+            return None
+        sp = typed_spec(nk + j, kc, stride, card, orig, lut_d, ("fd", j))
+        if sp is not None:
+            specs.append(sp)
+            order.append(("key", nk + j))
+    for j, (a, det, lut) in enumerate(getattr(prog, "derived_aggs", ())):
+        stride, card, orig = key_base(det)
+        lut_d = _dev_table(prog, ("dag", j), lut, dev)
+        if lut_d.dtype == torch.float64:
+            return None
+        specs.append((0, 2, _LUT_T[lut_d.dtype], 0, stride, card, 0, orig, lut_d.data_ptr(), 0.0))
+        order.append(("dag", j))
+    derived_names = {a.name for a, _, _ in getattr(prog, "derived_aggs", ())}
+    for a in prog.aggs:
+        if a.name in derived_names or a.slot < 0 or a.kind in ("hll", "theta"):
+            continue
+        if a.kind == "count":
+            sp = (1, 2, 0, a.slot, 1, 1, 0, 0, 0, 0.0)
+        elif a.kind in ("sum_i", "min_i", "max_i"):
+            if a.scale:
+                sp = (1, 3, 0, a.slot, 1, 1, 0, 0, 0, float(10.0 ** a.scale))
+            else:
+                sp = (1, 2 if a.out_type == "long" else 3, 0, a.slot, 1, 1, 0, 0, 0, 0.0)
+        elif a.kind == "sum_f":
+            sp = (3, 4, 0, a.slot, 1, 1, 0, 0, 0, 0.0)
+        elif a.kind in ("min_f", "max_f"):
+            sp = (2, 5 if a.out_type == "long" else 4, 0, a.slot, 1, 1, 0, 0, 0, 0.0)
+        elif a.kind == "sum_fx":
+            return None
+        else:
+            continue
+        specs.append(sp)
+        order.append(("agg", a.name))
+    if want_gid:
+        specs.append((4, 2, 0, 0, 1, 1, 0, 0, 0, 0.0))
+        order.append(("gid", 0))
+    if len(specs) > 16:
+        return None
+    offs, off = [], 0
+    for sp in specs:
+        offs.append(off)
+        off = (off + R * _OUT_W[sp[1]] + 15) // 16 * 16
+    nbytes = off
+    acc = parts.acc if parts.acc.is_contiguous() else parts.acc.contiguous()
+    out = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=dev)
+    host = torch.empty(max(nbytes, 16), dtype=torch.uint8, pin_memory=True)
+    from ..ops import native
+
+    native.load().sparse_decode(g.data_ptr(), acc.data_ptr(), R, int(acc.shape[1]) if acc.dim() == 2 else 1,
+                                [sp + (o,) for sp, o in zip(specs, offs)], out.data_ptr(), nbytes, host.data_ptr(),
+                                native._stream(dev))
+    hb = host.numpy()
+    key_all = [None] * (nk + len(getattr(prog, "derived", ())))
+    dag_vals = [None] * len(getattr(prog, "derived_aggs", ()))
+    agg_host, gid = {}, None
+    for (role, i), sp, o in zip(order, specs, offs):
+        arr = hb[o: o + R * _OUT_W[sp[1]]].view(_OUT_NP[sp[1]])
+        if role == "key":
+            key_all[i] = arr
+        elif role == "dag":
+            dag_vals[i] = arr
+        elif role == "agg":
+            agg_host[i] = arr
+        else:
+            gid = arr
+    for i, c in consts.items():
+        key_all[i] = _const_column(R, c)
+    return R, key_all[:nk], key_all[nk:], dag_vals, agg_host, gid, typed
+
+
 _DECODE_TABLE_MAX = 1 << 16
 
 
@@ -297,7 +457,7 @@ def finalize(prog, parts: Partials, out_types: Optional[Dict[str, str]] = None) 
     typed: Dict[int, object] = {}
     est_host: List[np.ndarray] = []
     if parts.kind == "dense":
-        small = parts.rows * parts.acc.shape[1] <= (1 << 20)
+        small = parts.rows * parts.acc.shape[1] <= SMALL_DENSE_WORDS
         if small:
             # HLL estimates of every group computed before the one D2H (one sync, not two)
             est_dev = []
@@ -350,7 +510,14 @@ def finalize(prog, parts: Partials, out_types: Optional[Dict[str, str]] = None) 
 
                 check_status(parts)
             parts = parts.compact()
-    if parts.kind == "sparse":
+    nat = _native_sparse(prog, parts, out_types, want_gid) \
+        if parts.kind == "sparse" and not collapse and NATIVE_DECODE else None
+    if nat is not None:
+        R, key_ids, derived_ids, derived_agg_vals, agg_host, gid, typed_n = nat
+        typed.update(typed_n)
+        acc_cols = {}
+        hll_d = parts.hll
+    elif parts.kind == "sparse":
         # decode key components on the device, then one pinned D2H of every array
         g = parts.keys
         R = int(g.numel())

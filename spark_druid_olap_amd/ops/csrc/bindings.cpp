@@ -15,6 +15,7 @@
 #include <tuple>
 #include <vector>
 #include "scan_desc.h"
+#include "post_scan.h"
 
 namespace sdo {
 template <int U>
@@ -34,6 +35,10 @@ __global__ void nonzero_mask_kernel(const unsigned char* base, int esize, int64_
 __global__ void nonzero_mask_u8_kernel(const unsigned char* base, int64_t n, uint64_t* words);
 __global__ void histogram_kernel(const int64_t* keys, int64_t n, int64_t nbins, unsigned int* counts);
 __global__ void histogram_lds_kernel(const int64_t* keys, int64_t n, int nbins, unsigned int* counts);
+__global__ void touch_count_kernel(const uint4* touch, int64_t nwords, uint64_t* words, int* block_counts);
+__global__ void touch_gather_kernel(const uint64_t* words, int64_t nwords, const int64_t* offsets, int64_t* acc, int ns,
+                                    const int64_t* init, unsigned char* touch, int64_t* out_idx, int64_t* out_acc);
+__global__ void sparse_decode_kernel(DecArgs a);
 struct ResetArgs {
   int64_t* acc;
   const int64_t* init;
@@ -192,6 +197,80 @@ static void compact_write(uint64_t mask, int64_t nwords, uint64_t offsets, uint6
   hipLaunchKernelGGL(sdo::compact_write_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream,
                      (const uint64_t*)mask, nwords, (const int64_t*)offsets, (int64_t*)rows);
   check(hipGetLastError(), "compact_write_kernel launch");
+}
+
+// First-touch compaction (post_scan.hip touch_*): pass 1 + offsets; the caller reads the total,
+// sizes the outputs and runs pass 3.  The byte table holds nwords * 64 bytes.
+static void touch_count(uint64_t touch, int64_t nwords, uint64_t words, uint64_t block_counts, uint64_t offsets,
+                        uint64_t total, uint64_t stream) {
+  const int64_t nb = compact_blocks(nwords);
+  if (nb <= 0) return;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(sdo::touch_count_kernel, dim3((unsigned)nb), dim3(256), 0, s, (const uint4*)touch, nwords,
+                     (uint64_t*)words, (int*)block_counts);
+  check(hipGetLastError(), "touch_count_kernel launch");
+  hipLaunchKernelGGL(sdo::compact_offsets_kernel, dim3(1), dim3(1024), 0, s, (const int*)block_counts, nb,
+                     (int64_t*)offsets, (int64_t*)total);
+  check(hipGetLastError(), "compact_offsets_kernel launch");
+}
+
+static void touch_gather(uint64_t words, int64_t nwords, uint64_t offsets, uint64_t acc, int ns, uint64_t init,
+                         uint64_t touch, uint64_t out_idx, uint64_t out_acc, uint64_t stream) {
+  const int64_t nb = compact_blocks(nwords);
+  if (nb <= 0) return;
+  if (ns < 1 || ns > sdo::MAX_SLOTS) throw std::invalid_argument("touch_gather: slot count");
+  hipLaunchKernelGGL(sdo::touch_gather_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream,
+                     (const uint64_t*)words, nwords, (const int64_t*)offsets, (int64_t*)acc, ns, (const int64_t*)init,
+                     (unsigned char*)touch, (int64_t*)out_idx, (int64_t*)out_acc);
+  check(hipGetLastError(), "touch_gather_kernel launch");
+}
+
+// Sparse result decode (post_scan.hip sparse_decode_kernel) into one device buffer, then one copy
+// of ``nbytes`` into the pinned host buffer and one stream sync (GIL released while waiting).
+// cols: (kind, out, lut_t, slot, stride, card, add, orig, lut, div, off)
+using DecTuple = std::tuple<int, int, int, int, int64_t, int64_t, int64_t, uint64_t, uint64_t, double, int64_t>;
+static void sparse_decode(uint64_t idx, uint64_t acc, int64_t n, int ns, std::vector<DecTuple> cols, uint64_t out,
+                          int64_t nbytes, uint64_t host, uint64_t stream) {
+  if ((int)cols.size() > sdo::DEC_MAX_COLS) throw std::invalid_argument("sparse_decode: too many columns");
+  sdo::DecArgs a{};
+  a.idx = (const int64_t*)idx;
+  a.acc = (const int64_t*)acc;
+  a.n = n;
+  a.ns = ns;
+  a.ncols = (int)cols.size();
+  a.out = (unsigned char*)out;
+  for (size_t j = 0; j < cols.size(); ++j) {
+    auto& c = a.c[j];
+    c.kind = std::get<0>(cols[j]);
+    c.out = std::get<1>(cols[j]);
+    c.lut_t = std::get<2>(cols[j]);
+    c.slot = std::get<3>(cols[j]);
+    c.stride = std::get<4>(cols[j]);
+    c.card = std::get<5>(cols[j]);
+    c.add = std::get<6>(cols[j]);
+    c.orig = (const int64_t*)std::get<7>(cols[j]);
+    c.lut = (const void*)std::get<8>(cols[j]);
+    c.div = std::get<9>(cols[j]);
+    c.off = std::get<10>(cols[j]);
+    if (c.kind < 0 || c.kind > 4 || c.out < 0 || c.out > 5 || c.lut_t < 0 || c.lut_t > 3)
+      throw std::invalid_argument("sparse_decode: column kind");
+    if (c.kind == 0 && (c.stride <= 0 || c.card <= 0)) throw std::invalid_argument("sparse_decode: key stride/card");
+    if ((c.kind == 1 || c.kind == 2 || c.kind == 3) && (c.slot < 0 || c.slot >= ns))
+      throw std::invalid_argument("sparse_decode: slot");
+    if (c.lut_t && !c.lut) throw std::invalid_argument("sparse_decode: table pointer");
+    const int64_t width = c.out == 0 ? 2 : (c.out == 1 ? 4 : 8);
+    if (c.off < 0 || c.off % width || c.off + n * width > nbytes) throw std::invalid_argument("sparse_decode: column offset");
+  }
+  hipStream_t st = (hipStream_t)stream;
+  if (n > 0 && !cols.empty()) {
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(sdo::sparse_decode_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
+    check(hipGetLastError(), "sparse_decode_kernel launch");
+  }
+  py::gil_scoped_release nogil;
+  if (nbytes > 0) check(hipMemcpyAsync((void*)host, (const void*)out, nbytes, hipMemcpyDeviceToHost, st), "sparse_decode copy");
+  wait_stream(st, "sparse_decode sync");
 }
 
 static void nonzero_mask(uint64_t base, int esize, int64_t n, int64_t stride, uint64_t words, uint64_t stream) {
@@ -665,7 +744,7 @@ static void part_hash_agg(uint64_t recs, int RW, uint64_t base, int64_t nsub, in
   }
   if (cap_log2 < 6 || cap_log2 > 14) throw std::invalid_argument("part_hash_agg: table of 2^6..2^14 keys");
   const int64_t lds = ((int64_t)1 << cap_log2) * (1 + f.nslots) * 8;
-  if (lds > 160 * 1024) throw std::invalid_argument("part_hash_agg: table exceeds 160 KiB of LDS");
+  if (lds > 160 * 1024 - 256) throw std::invalid_argument("part_hash_agg: table exceeds 160 KiB of LDS");
   sdo::PartHaving hv{};
   if (having.size() > 4) throw std::invalid_argument("part_hash_agg: at most 4 having terms");
   hv.nterms = (int)having.size();
@@ -686,7 +765,8 @@ static void part_hash_agg(uint64_t recs, int RW, uint64_t base, int64_t nsub, in
   const int64_t grid = (nsub + 7) / 8 * 8;
   if (grid > ((int64_t)1 << 31) - 8) throw std::invalid_argument("part_hash_agg: too many sub-buckets");
   const void* fn = (const void*)sdo::part_hash_agg_kernel;
-  if (lds > 65536) check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024), "attr");
+  // (the kernel's own static LDS counts against the 160 KiB: ask for exactly the dynamic bytes)
+  if (lds > 65536) check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "part_hash_agg attr");
   const uint32_t* r_ = (const uint32_t*)recs;
   const uint32_t* b_ = (const uint32_t*)base;
   int64_t* ok_ = (int64_t*)out_keys;
@@ -745,6 +825,9 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("compact_write", &compact_write);
   m.def("topk_keep", &topk_keep);
   m.def("nonzero_mask", &nonzero_mask);
+  m.def("touch_count", &touch_count);
+  m.def("touch_gather", &touch_gather);
+  m.def("sparse_decode", &sparse_decode);
   m.def("histogram", &histogram);
   m.def("reset_bufs", &reset_bufs);
   m.def("hll_pairs", &hll_pairs);

@@ -16,6 +16,7 @@
 // the (blockDim/64) wave totals through LDS.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "post_scan.h"
 
 namespace sdo {
 
@@ -330,6 +331,131 @@ __global__ void __launch_bounds__(256) reset_bufs_kernel(ResetArgs a) {
     for (int64_t i = tid; i < a.zn[r]; i += nth) z[i] = 0ull;
   }
   if (tid == 0 && a.overflow) *a.overflow = 0;
+}
+
+// ---- First-touch compaction of a dense HBM accumulator table (TPC-H Q3: 150M order groups, ~1M
+// touched per run).  Pass 1 reads the byte table 16 bytes per lane (as nonzero_mask_u8_kernel),
+// joins four lanes' 16-bit masks into the ballot word of 64 groups and counts per 65536-group block; compact_offsets_kernel scans the counts; pass 3
+// writes each touched group's id and accumulator row, re-initialises the row and clears its byte --
+// one launch instead of the mask / count / write / gather / index_copy / index_fill chain.
+// The byte table is padded to a multiple of 64 groups (engine/device_exec.py _alloc).
+__global__ void __launch_bounds__(CW_THREADS) touch_count_kernel(const uint4* __restrict__ touch, int64_t nwords,
+                                                                uint64_t* __restrict__ words,
+                                                                int* __restrict__ block_counts) {
+  __shared__ int lds[40];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int c = 0;
+  // a wave covers 16 words per step (64 lanes x 16 bytes); the block's 4 waves 64 words; 16 steps
+  // cover the block's 1024 words
+  for (int it = 0; it < CW_THREADS * CW_WORDS / 64; ++it) {
+    const int64_t wb = (int64_t)blockIdx.x * CW_THREADS * CW_WORDS + it * 64 + wave * 16;
+    const int64_t w = wb + (lane >> 2);
+    uint32_t m = 0;
+    if (w < nwords) {
+      const uint4 v = touch[wb * 4 + lane];
+      m = nz4(v.x) | (nz4(v.y) << 4) | (nz4(v.z) << 8) | (nz4(v.w) << 12);
+    }
+    const uint64_t m1 = (uint32_t)__shfl_down((int)m, 1, 64);
+    const uint64_t m2 = (uint32_t)__shfl_down((int)m, 2, 64);
+    const uint64_t m3 = (uint32_t)__shfl_down((int)m, 3, 64);
+    if ((lane & 3) == 0 && w < nwords) {
+      const uint64_t word = (uint64_t)m | (m1 << 16) | (m2 << 32) | (m3 << 48);
+      words[w] = word;
+      c += __popcll(word);
+    }
+  }
+  int total;
+  block_excl_scan(c, lds, &total);
+  if (threadIdx.x == 0) block_counts[blockIdx.x] = total;
+}
+
+__global__ void __launch_bounds__(CW_THREADS) touch_gather_kernel(const uint64_t* __restrict__ words, int64_t nwords,
+                                                                 const int64_t* __restrict__ offsets,
+                                                                 int64_t* __restrict__ acc, int ns,
+                                                                 const int64_t* __restrict__ init,
+                                                                 unsigned char* __restrict__ touch,
+                                                                 int64_t* __restrict__ out_idx,
+                                                                 int64_t* __restrict__ out_acc) {
+  __shared__ int lds[40];
+  const int64_t w0 = ((int64_t)blockIdx.x * CW_THREADS + threadIdx.x) * CW_WORDS;
+  uint64_t w[CW_WORDS];
+  int c = 0;
+#pragma unroll
+  for (int i = 0; i < CW_WORDS; ++i) {
+    w[i] = (w0 + i < nwords) ? words[w0 + i] : 0ull;
+    c += __popcll(w[i]);
+  }
+  int total;
+  int64_t pos = offsets[blockIdx.x] + block_excl_scan(c, lds, &total);
+#pragma unroll
+  for (int i = 0; i < CW_WORDS; ++i) {
+    uint64_t m = w[i];
+    const int64_t rbase = (w0 + i) << 6;
+    while (m) {
+      const int64_t r = rbase + (__ffsll((unsigned long long)m) - 1);
+      m &= m - 1;
+      out_idx[pos] = r;
+      int64_t* a = acc + r * ns;
+      int64_t* o = out_acc + pos * ns;
+      for (int s = 0; s < ns; ++s) {
+        o[s] = a[s];
+        a[s] = init[s];
+      }
+      touch[r] = 0;
+      ++pos;
+    }
+  }
+}
+
+// ---- Sparse result decode: the final host columns of a sparse group set (engine/partials.py
+// finalize) in one pass -- key components ((id / stride) % card, through an FD map and a typed
+// dictionary table, plus a range dictionary's start), aggregator slots (decimal scaling, ordered
+// float decode) -- written at their SQL width into ONE buffer (column c at byte offset off[c]) for
+// a single device-to-host copy, instead of a chain of torch element-wise / gather kernels and one
+// copy per column.
+__global__ void __launch_bounds__(256) sparse_decode_kernel(DecArgs a) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < a.n; r += stride) {
+    const int64_t g = a.idx[r];
+    for (int j = 0; j < a.ncols; ++j) {
+      const DecCol& c = a.c[j];
+      int64_t iv = 0;
+      double dv = 0.0;
+      bool is_d = false;
+      if (c.kind == 0) {
+        int64_t v = (g / c.stride) % c.card;
+        if (c.orig) v = c.orig[v];
+        if (c.lut_t == 1) iv = ((const int32_t*)c.lut)[v];
+        else if (c.lut_t == 2) iv = ((const int64_t*)c.lut)[v];
+        else if (c.lut_t == 3) { dv = ((const double*)c.lut)[v]; is_d = true; }
+        else iv = v;
+        iv += c.add;
+      } else if (c.kind == 4) {
+        iv = g;
+      } else {
+        const int64_t v = a.acc[r * a.ns + c.slot];
+        if (c.kind == 1) {
+          iv = v;
+          if (c.div != 0.0) { dv = (double)v / c.div; is_d = true; }
+        } else if (c.kind == 2) {
+          iv = v >= 0 ? v : (v ^ 0x7FFFFFFFFFFFFFFFLL);
+          dv = __longlong_as_double(iv);
+          is_d = true;
+        } else {
+          iv = v;
+        }
+      }
+      unsigned char* o = a.out + c.off;
+      switch (c.out) {
+        case 0: ((int16_t*)o)[r] = (int16_t)iv; break;
+        case 1: ((int32_t*)o)[r] = (int32_t)iv; break;
+        case 2: ((int64_t*)o)[r] = iv; break;
+        case 3: ((double*)o)[r] = is_d ? dv : (double)iv; break;
+        case 4: ((int64_t*)o)[r] = is_d ? __double_as_longlong(dv) : iv; break;
+        default: ((int64_t*)o)[r] = (is_d ? (isfinite(dv) ? (int64_t)dv : 0) : iv); break;
+      }
+    }
+  }
 }
 
 }  // namespace sdo

@@ -147,6 +147,20 @@ FULL_CHUNKS = os.environ.get("SDO_JIT_FULL", "1") != "0"
 # reading each word's mask by lane index (independent readlanes) and skipping all-empty steps;
 # sparser chunks take the find-first-set chain over their non-empty words only (0: always chain)
 DENSE_WORDS = int(os.environ.get("SDO_JIT_DENSE_WORDS", "48"))
+# Count-only scans of tiny dense key spaces (TPC-H "Ship Date Range": count(*) by l_returnflag,
+# l_linestatus over 150M rows) count in registers: per slot one 64-bit word of eight 8-bit fields,
+# ``pc += (uint64)mine << (key * 8)`` per row (no LDS atomic -- every lane of a wave would otherwise
+# hit the same few LDS words, serialized in the LDS atomic unit), unpacked into per-group u32
+# counters at the end of each chunk (a lane sees <= 64 rows of a chunk, so no field overflows) and
+# wave-reduced once into the accumulator table at the end.
+COUNT_REGS = True
+COUNT_REGS_MAX_G = 8
+
+
+def count_regs(prog, mode: int) -> bool:
+    return (COUNT_REGS and mode == D.M_DENSE_LDS and 0 < prog.G <= COUNT_REGS_MAX_G and not prog.nhll
+            and bool(prog.aops) and all(a["kind"] == D.A_COUNT for a in prog.aops)
+            and not getattr(prog, "presence_only", False))
 
 
 
@@ -518,6 +532,8 @@ class _Gen:
         pre = self.chunk_expr() if p.pre_len else None
         G, NS = p.G, p.nslots
         NCT = 1 if lay.shared else W * lay.ncopy
+        creg = count_regs(p, mode)
+        cslots = sorted({a["slot"] for a in p.aops}) if creg else []
         for i in sorted(self.cols):
             L.append(f"  const unsigned char* c{i} = (const unsigned char*)d->cols[{i}].ptr;")
         for j, (row, stride, count) in enumerate(p.bm_leaves):
@@ -657,6 +673,9 @@ class _Gen:
                     continue
                 s = a["slot"]
                 op = p.slots[s][0]
+                if creg:  # packed 8-bit register counters (COUNT_REGS)
+                    body.append(f"        pc{s} += (uint64_t)({cond}) << ((uint32_t)key << 3);")
+                    continue
                 if mode == D.M_DENSE_LDS:
                     tgt = f"acc + (slot * {NS} + {s}) * {NCT} + copy"
                 else:
@@ -720,6 +739,9 @@ class _Gen:
                 out.append(f"  for (int i = threadIdx.x; i < {lay.hll_bytes // 4}; i += {W * 64}) "
                            f"((uint32_t*)(lds + {lay.hll_off}))[i] = 0u;")
             out.append("  __syncthreads();")
+        for s in cslots:
+            out.append(f"  uint64_t pc{s} = 0;")
+            out.append("  " + " ".join(f"uint32_t cn{s}_{g} = 0;" for g in range(G)))
         out.append(f"  const int64_t total_waves = (int64_t)gridDim.x * {W};")
         out.append(f"  const int64_t gw = (int64_t)blockIdx.x * {W} + wave;")
         out.append("  const int64_t num_rows = d->num_rows;")
@@ -799,7 +821,16 @@ class _Gen:
             out.append("    }")
         if mode == D.M_PART:
             out.append("    if (lane == 0) pend[c] = cbase + woff;")
+        for s in cslots:  # unpack the chunk's 8-bit fields
+            out.append("    " + " ".join(f"cn{s}_{g} += (uint32_t)(pc{s} >> {8 * g}) & 0xffu;" for g in range(G)) +
+                       f" pc{s} = 0;")
         out.append("  }")
+        for s in cslots:  # wave totals into lane 0's accumulator copy
+            for g in range(G):
+                out.append(f"  {{ uint32_t v_ = cn{s}_{g};")
+                out.append("    for (int o = 32; o > 0; o >>= 1) v_ += (uint32_t)__shfl_xor((int)v_, o);")
+                out.append(f"    if (lane == 0 && v_) acc_update<{D.S_SUM_I}>(acc + ({g} * {NS} + {s}) * {NCT} + copy, "
+                           "(int64_t)v_); }")
         if mode == D.M_DENSE_LDS:
             out.append("  __syncthreads();")
             out.append(f"  for (int i = threadIdx.x; i < {G * NS}; i += {W * 64}) {{")

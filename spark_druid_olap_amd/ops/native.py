@@ -215,6 +215,33 @@ def nonzero_rows(col: torch.Tensor) -> torch.Tensor:
     return compact_rows(words)
 
 
+def touch_compact(touch: torch.Tensor, acc: torch.Tensor, init_row: torch.Tensor):
+    """(group ids, accumulator rows) of the groups a first-touch byte table marks, with those rows
+    re-initialised to ``init_row`` and their bytes cleared (post_scan.hip touch_*: fused mask +
+    count pass, offset scan, one gather / re-init / clear pass).  ``touch`` holds a multiple of 64
+    bytes covering every row of ``acc`` [rows, nslots] int64."""
+    m = load()
+    rows, ns = acc.shape
+    nw = (rows + 63) // 64
+    assert touch.dtype == torch.uint8 and touch.is_contiguous() and touch.numel() >= nw * 64
+    assert acc.dtype == torch.int64 and acc.is_contiguous() and init_row.numel() == ns
+    dev = acc.device
+    nb = (nw + 1023) // 1024
+    words = torch.empty(max(nw, 1), dtype=torch.int64, device=dev)
+    counts = torch.empty(max(nb, 1), dtype=torch.int32, device=dev)
+    offs = torch.empty(max(nb, 1), dtype=torch.int64, device=dev)
+    total = torch.zeros(1, dtype=torch.int64, device=dev)
+    st = _stream(dev)
+    m.touch_count(touch.data_ptr(), nw, words.data_ptr(), counts.data_ptr(), offs.data_ptr(), total.data_ptr(), st)
+    n = int(total.item())
+    idx = torch.empty(n, dtype=torch.int64, device=dev)
+    out = torch.empty((n, ns), dtype=torch.int64, device=dev)
+    if n:
+        m.touch_gather(words.data_ptr(), nw, offs.data_ptr(), acc.data_ptr(), ns, init_row.data_ptr(),
+                       touch.data_ptr(), idx.data_ptr(), out.data_ptr(), st)
+    return idx, out
+
+
 def histogram(keys: torch.Tensor, nbins: int) -> torch.Tensor:
     """int64 counts per bin of int64 ids in [0, nbins) (post_scan.hip histogram_kernel: 32-bit
     device atomics, no min/max pre-pass); replaces ``torch.bincount`` for nested count levels."""

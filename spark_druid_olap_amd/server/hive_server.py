@@ -335,9 +335,10 @@ class HiveThriftServer:
                 for k, v in overlay.items():
                     sess.conf.set(k, v)
                 df = sess.sql(stmt)
-                if df.plan is not None and df._stream_source()[1] is not None and \
-                        sess.conf.typed("spark.sparklinedata.druid.stream.results"):
-                    # Select-backed result: stream pages to the client instead of materialising
+                if df.plan is not None and sess.conf.typed("spark.sparklinedata.druid.stream.results") and \
+                        (df._stream_source()[1] is not None or df.agg_streamable()):
+                    # Select-backed or large groupBy result: stream pages to the client instead of
+                    # materialising it
                     op.set_stream(df.columns, [t for _, t in df.schema],
                                   lambda df=df: df.iter_batches(token=op.token))
                     op.fill(1)  # run the scan now: errors surface in ExecuteStatement

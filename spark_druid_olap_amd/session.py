@@ -141,34 +141,35 @@ class DataFrame:
 
     toPandas = to_pandas
 
-    def _stream_source(self):
+    def _stream_source(self, aggregates: bool = False):
         """(Limit n or None, DruidQuery) when the plan is Project/Filter operators over a pushed
-        Select (the reference's push_project_and_filters path): those can run page by page."""
+        Select (the reference's push_project_and_filters path) -- or, with ``aggregates``, over a
+        pushed groupBy: those can run page by page."""
         node, limit = self.plan, None
         if isinstance(node, P.Limit):
             limit, node = node.n, node.child
         while isinstance(node, (P.Project, P.Filter)):
             node = node.child
-        if isinstance(node, P.DruidQuery) and isinstance(node.spec, S.SelectSpec) and \
+        kinds = (S.SelectSpec, S.GroupByQuerySpec) if aggregates else (S.SelectSpec,)
+        if isinstance(node, P.DruidQuery) and isinstance(node.spec, kinds) and \
                 not S.find_deferred(node.spec) and not node.info.get("historical"):
             return limit, node
         return None, None
 
-    def iter_batches(self, page_rows: Optional[int] = None, token=None) -> Iterator[pd.DataFrame]:
-        """The result as a stream of pandas pages: a Select-backed plan is executed one Druid page
-        at a time (``spark.sparklinedata.druid.selectquery.pagesize`` rows per shard page, the
-        reference's DruidSelectResultIterator.scala:116-137 cursor), so host memory holds one page;
-        any other plan is computed, then sliced."""
-        page_rows = int(page_rows or self.session.conf.typed("spark.sparklinedata.druid.selectquery.pagesize"))
-        limit, dq = (None, None) if self.plan is None else self._stream_source()
-        if dq is None:
-            df = self.to_pandas(token)
-            for a in range(0, max(len(df), 1), page_rows):
-                if a < len(df) or a == 0:
-                    yield df.iloc[a: a + page_rows].reset_index(drop=True)
-            return
+    def agg_streamable(self) -> bool:
+        """Project/Filter over a pushed groupBy whose engine result can be produced page by page
+        (engine/executor.py PreparedQuery.streamable: a large key space, no host-side ordering)."""
+        if self.plan is None:
+            return False
+        _, dq = self._stream_source(aggregates=True)
+        if dq is None or not isinstance(dq.spec, S.GroupByQuerySpec) or self.session.engine.world.distributed:
+            return False
+        prep = self.session.prepare_druid(dq)
+        return bool(getattr(prep, "streamable", lambda: False)())
+
+    def _run_pages(self, dq, limit, pages, token):
         left = limit
-        for res in self.session.iter_select_pages(dq, page_rows):
+        for res in pages:
             ex = Executor(self.session, token)
             ex.preload(dq, res)
             b = self.session._with_sql(self.sql_text, lambda: ex.run(self.plan if limit is None else self.plan.child))
@@ -180,6 +181,28 @@ class DataFrame:
                 yield out
             if left is not None and left <= 0:
                 return
+
+    def iter_batches(self, page_rows: Optional[int] = None, token=None) -> Iterator[pd.DataFrame]:
+        """The result as a stream of pandas pages: a Select-backed plan is executed one Druid page
+        at a time (``spark.sparklinedata.druid.selectquery.pagesize`` rows per shard page, the
+        reference's DruidSelectResultIterator.scala:116-137 cursor), so host memory holds one page;
+        any other plan is computed, then sliced."""
+        page_rows = int(page_rows or self.session.conf.typed("spark.sparklinedata.druid.selectquery.pagesize"))
+        limit, dq = (None, None) if self.plan is None else self._stream_source()
+        if dq is None and self.agg_streamable():
+            # a large pushed groupBy: each page's groups are decoded and copied from the device as
+            # they are pulled (engine/executor.py iter_pages)
+            limit, dq = self._stream_source(aggregates=True)
+            prep = self.session.prepare_druid(dq)
+            yield from self._run_pages(dq, limit, prep.iter_pages(page_rows), token)
+            return
+        if dq is None:
+            df = self.to_pandas(token)
+            for a in range(0, max(len(df), 1), page_rows):
+                if a < len(df) or a == 0:
+                    yield df.iloc[a: a + page_rows].reset_index(drop=True)
+            return
+        yield from self._run_pages(dq, limit, self.session.iter_select_pages(dq, page_rows), token)
 
     def toLocalIterator(self, page_rows: Optional[int] = None) -> Iterator[tuple]:
         """Rows one at a time over ``iter_batches`` (Spark's ``DataFrame.toLocalIterator``)."""

@@ -236,10 +236,11 @@ def test_hash_partitioned_sparse_matches_atomic_table(gpu_ds, monkeypatch, level
     from spark_druid_olap_amd.ops import jit
 
     monkeypatch.setattr(jit, "FORCE_HASHED", True)
-    if levels == 2:  # a tiny table capacity forces many sub-buckets -> two split levels
-        monkeypatch.setattr(DE, "HASH_TABLE_BYTES", 4096)
     f = S.BoundFilterSpec("o_orderdate", "1994-01-01", "1996-12-31", False, False)
     prog = _order_prog(gpu_ds, f)
+    if levels == 2:  # the smallest table (64 keys) and a whole-key-space estimate -> two split levels
+        monkeypatch.setattr(DE, "HASH_TABLE_BYTES", 64 * 8 * (1 + prog.nslots))
+        prog.est_rows = float(prog.G)
     part = DE.PreparedScan(prog, mode=D.M_PART)
     assert part.mode == D.M_PART and part.part.get("hashed") and part.part["levels"] == levels
     monkeypatch.setattr(jit, "FORCE_HASHED", False)

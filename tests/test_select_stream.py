@@ -112,6 +112,62 @@ def test_thrift_server_streams_pages(ds_small, df_small):
         srv.stop()
 
 
+GB_SQL = ("select o_orderkey, l_linenumber, count(*) as c, sum(l_extendedprice) as s "
+          "from orderLineItemPartSupplier where l_quantity > 10 group by o_orderkey, l_linenumber")
+
+
+def test_large_groupby_streams_pages(ds_small, df_small, monkeypatch):
+    """A groupBy over a large key space streams: the merged groups stay in device / engine memory
+    and each page is finalized when pulled (engine/executor.py iter_pages)."""
+    from spark_druid_olap_amd.engine import executor as E
+
+    monkeypatch.setattr(E, "STREAM_MIN_GROUPS", 1000)
+    s = _session(ds_small, df_small)
+    d = s.sql(GB_SQL)
+    assert isinstance(d.druid_query_specs()[0], S.GroupByQuerySpec)
+    assert d._stream_source()[1] is None and d.agg_streamable()
+    calls = []
+    real = E.PreparedQuery.iter_pages
+
+    def spy(self, page_rows):
+        calls.append(page_rows)
+        yield from real(self, page_rows)
+
+    monkeypatch.setattr(E.PreparedQuery, "iter_pages", spy)
+    pages = list(d.iter_batches(page_rows=700))
+    assert calls == [700] and len(pages) > 3 and all(len(p) <= 700 for p in pages)
+    streamed = sorted(tuple(r) for p in pages for r in p.itertuples(index=False, name=None))
+    assert streamed == sorted(d.collect())
+    exp = df_small[df_small.l_quantity > 10].groupby(["o_orderkey", "l_linenumber"]).size()
+    assert len(streamed) == len(exp)
+    lim = s.sql(GB_SQL + " limit 900")  # a limit above the pushed groupBy stops the pages early
+    assert sum(len(p) for p in lim.iter_batches(page_rows=400)) == 900
+    # small key spaces and host-ordered results are not streamed
+    assert not s.sql("select s_nation, count(*) from orderLineItemPartSupplier group by s_nation").agg_streamable()
+    assert not s.sql(GB_SQL.replace("group by", "and 1 = 1 group by") + " having count(*) > 1").agg_streamable()
+
+
+def test_thrift_server_streams_groupby_pages(ds_small, df_small, monkeypatch):
+    from spark_druid_olap_amd.engine import executor as E
+    from spark_druid_olap_amd.server.hive_client import connect
+    from spark_druid_olap_amd.server.hive_server import HiveThriftServer
+
+    monkeypatch.setattr(E, "STREAM_MIN_GROUPS", 1000)
+    s = _session(ds_small, df_small)
+    s.conf.set("spark.sparklinedata.druid.selectquery.pagesize", "500")
+    srv = HiveThriftServer(s, port=0).start()
+    try:
+        with connect(port=srv.port) as c:
+            cur = c.cursor()
+            cur.arraysize = 200
+            rows = cur.execute(GB_SQL).fetchall()
+            op = next(iter(srv.ops.values()), None)
+            assert op is not None and op.factory is not None
+        assert sorted(rows) == sorted(s.sql(GB_SQL).collect())
+    finally:
+        srv.stop()
+
+
 def _free_port():
     s_ = socket.socket()
     s_.bind(("127.0.0.1", 0))

@@ -2,9 +2,10 @@
 
   python tools/query_probe.py SF [variant ...] [-- query names]
 
-A variant is ``reg{0|1}pipe{0|1}[b<workgroups per CU>][c<accumulator copies per wave>][slds|sreg]``: register accumulators,
-double-buffered DMA, target workgroups per CU, forced LDS-DMA / VGPR staging (see ops/jit.py);
-results of every variant are checked against the first one.  Used to locate slow or hung kernels
+A variant is ``base[b<workgroups per CU>][c<accumulator copies per wave>][slds|sreg][creg0]``: target
+workgroups per CU, accumulator copies, forced LDS-DMA / VGPR staging, count-only scans through LDS
+atomics instead of register counters (see ops/jit.py); results of every variant are checked against
+the first one.  Used to locate slow or hung kernels
 and to A/B kernel-generation choices on the GPU box."""
 import os
 import statistics
@@ -84,6 +85,7 @@ def main():
         J.MAX_NCOPY = int(mc.group(1)) if mc else 16
         DE.JIT_STAGE = "lds" if "slds" in var else ("reg" if "sreg" in var else "auto")
         DE.BLOCKS_PER_CU = max(3, DE.JIT_BLOCKS)
+        J.COUNT_REGS = "creg0" not in var
         print(f"== {var}", flush=True)
         for name, qs in specs:
             if only and name not in only:
