@@ -209,6 +209,11 @@ def main():
         print(f"[bench] rank {world.rank}: " + " ".join(f"{k[:12]}={sum(v) / len(v):.3f}" for k, v in lat.items()),
               file=sys.stderr, flush=True)
     total_ms = world.max_float(total_ms)
+    hbm = None
+    if dev.type == "cuda":  # peak device memory of the run (data + scan buffers + kernels), max over ranks
+        hbm = {"max_reserved_gb": round(world.max_float(torch.cuda.max_memory_reserved(dev) / 1e9), 2),
+               "max_allocated_gb": round(world.max_float(torch.cuda.max_memory_allocated(dev) / 1e9), 2),
+               "device_total_gb": round(torch.cuda.get_device_properties(dev).total_memory / 1e9, 1)}
     means = {k: world.max_float(sum(v) / len(v)) for k, v in lat.items()}
     geo = math.exp(sum(math.log(max(m, 1e-6)) for m in means.values()) / len(means))
     nq = nsuite * args.steps
@@ -260,6 +265,7 @@ def main():
             "per_query_min_ms": {k: round(v, 4) for k, v in mins.items()},
             "per_query_max_ms": {k: round(v, 4) for k, v in maxs.items()},
             "rows_per_gpu": int(nrows),
+            "hbm": hbm,
             # the timed steps run each prepared statement's literal-specialized kernel (compiled
             # synchronously at its first warmup run, SDO_JIT_SPECIALIZE=sync / _AFTER=1; a server
             # compiles it in the background for statements that repeat); the shape-shared kernels

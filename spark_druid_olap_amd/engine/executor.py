@@ -98,7 +98,8 @@ def is_cuda_ds(ds: DataSource) -> bool:
 
 # below this many merged groups HAVING is left to the host (_post re-applies it either way)
 HAVING_MIN_ROWS = 4096
-STREAM_MIN_GROUPS = 1 << 18  # planner group estimate above which a groupBy result streams (iter_pages)
+# planner group estimate above which a groupBy result streams (iter_pages)
+STREAM_MIN_GROUPS = int(os.environ.get("SDO_STREAM_MIN_GROUPS", str(1 << 18)))
 
 
 class PreparedQuery:
@@ -343,15 +344,17 @@ class PreparedQuery:
             return False
         return min(float(prog.G), float(getattr(prog, "est_rows", prog.G) or prog.G)) >= STREAM_MIN_GROUPS
 
-    def iter_pages(self, page_rows: int):
+    def iter_pages(self, page_rows: int, root_only: Optional[bool] = None):
         """The result as QueryResult pages of at most ``page_rows`` groups: the merged partials stay
         on the device and each page is finalized (decoded, copied to the host) only when it is
-        pulled, so host memory holds one page of a million-group answer.  Multi-rank: the groups
-        are gathered to rank 0 (root-only results); the other ranks yield one empty page."""
+        pulled, so host memory holds one page of a million-group answer.  Multi-rank with
+        ``root_only``: the groups are gathered to rank 0 alone and the other ranks yield one empty
+        page (only the first step issues collectives, so ranks pulling pages in lock step stay
+        matched); without it every rank pages through the whole answer."""
         from ..parallel.p2p import check_status
 
         t0 = time.perf_counter()
-        root_only = self.world.distributed and root_only_results()
+        root_only = self.world.distributed and (root_only_results() if root_only is None else root_only)
         prog, part, _ = self.run_partials(t0, root_only)
         check_status(part)
         if root_only and self.world.rank != 0:

@@ -63,7 +63,7 @@ __global__ void part_basescan_kernel(const uint32_t* totals, int64_t R, uint32_t
 __global__ void part_keys_kernel(const int64_t* keys, int64_t n, int shift1, int P1, uint32_t* counts1,
                                  const uint32_t* base1, uint32_t* out, int phase);
 template <int PU>
-__global__ void part_split_kernel(const uint32_t* in, int RW, const uint32_t* seg_lo, const uint32_t* seg_hi, int spg,
+__global__ void part_split_kernel(const uint32_t* in, int RW, int RS, const uint32_t* seg_lo, const uint32_t* seg_hi, int spg,
                                   int K, int shift2, int P2, uint32_t* counts2, const uint32_t* base2, uint32_t* out,
                                   int phase);
 __global__ void part_hash_agg_kernel(const uint32_t* recs, int RW, const uint32_t* base, int64_t nsub, int cap_log2,
@@ -553,7 +553,10 @@ static void part_split(uint64_t in, int RW, uint64_t seg_lo, uint64_t seg_hi, in
   if (spg < 1) throw std::invalid_argument("part_split: segments per group");
   // tile of 512 x PU records, ~32 KB of LDS whatever the record width
   const int PU = RW <= 2 ? 8 : (RW <= 4 ? 4 : (RW <= 8 ? 2 : 1));
-  const int64_t lds = phase == 0 ? (int64_t)P2 * 4 : ((int64_t)3 * P2 + (int64_t)512 * PU * RW) * 4;
+  // odd tile stride for even record widths >= 4 (conflict-free strided tile reads) when it fits
+  int RS = RW;
+  if (RW >= 4 && RW % 2 == 0 && ((int64_t)3 * P2 + (int64_t)512 * PU * (RW + 1)) * 4 <= 64 * 1024) RS = RW + 1;
+  const int64_t lds = phase == 0 ? (int64_t)P2 * 4 : ((int64_t)3 * P2 + (int64_t)512 * PU * RS) * 4;
   if (lds > 64 * 1024) throw std::invalid_argument("part_split: tile does not fit 64 KiB of LDS");
   const void* f = PU == 8 ? (const void*)sdo::part_split_kernel<8>
                 : PU == 4 ? (const void*)sdo::part_split_kernel<4>
@@ -564,8 +567,8 @@ static void part_split(uint64_t in, int RW, uint64_t seg_lo, uint64_t seg_hi, in
   uint32_t* c2 = (uint32_t*)counts2;
   const uint32_t* b2 = (const uint32_t*)base2;
   uint32_t* o = (uint32_t*)out;
-  void* args[] = {(void*)&in_, (void*)&RW, (void*)&lo_, (void*)&hi_, (void*)&spg, (void*)&K, (void*)&shift2,
-                  (void*)&P2, (void*)&c2, (void*)&b2, (void*)&o, (void*)&phase};
+  void* args[] = {(void*)&in_, (void*)&RW, (void*)&RS, (void*)&lo_, (void*)&hi_, (void*)&spg, (void*)&K,
+                  (void*)&shift2, (void*)&P2, (void*)&c2, (void*)&b2, (void*)&o, (void*)&phase};
   check(hipLaunchKernel(f, dim3((unsigned)(groups * K)), dim3(512), args, (size_t)lds, (hipStream_t)stream),
         "part_split_kernel launch");
   check(hipGetLastError(), "part_split_kernel launch");

@@ -115,7 +115,7 @@ __global__ __launch_bounds__(512) void part_keys_kernel(const int64_t* __restric
                                                        int P1, uint32_t* __restrict__ counts1,
                                                        const uint32_t* __restrict__ base1, uint32_t* __restrict__ out,
                                                        int phase) {
-  extern __shared__ uint32_t h[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t h[];
   const int B = gridDim.x;
   for (int q = threadIdx.x; q < P1; q += blockDim.x)
     h[q] = phase == 0 ? 0u : base1[q] + counts1[(int64_t)q * B + blockIdx.x];
@@ -195,7 +195,7 @@ __device__ __forceinline__ void split_range_count(const uint32_t* __restrict__ i
 }
 
 template <int PU>
-__device__ __forceinline__ void split_range_scatter(const uint32_t* __restrict__ in, int RW, uint32_t lo, uint32_t hi,
+__device__ __forceinline__ void split_range_scatter(const uint32_t* __restrict__ in, int RW, int RS, uint32_t lo, uint32_t hi,
                                                     int shift2, uint32_t P2, uint32_t* cur, uint32_t* hist,
                                                     uint32_t* tstart, uint32_t* tile, uint32_t* scan_lds,
                                                     uint32_t* __restrict__ out) {
@@ -229,16 +229,49 @@ __device__ __forceinline__ void split_range_scatter(const uint32_t* __restrict__
       }
     }
     __syncthreads();
-    // exclusive scan of the tile histogram -> bucket starts inside the tile
-    const uint32_t per = (P2 + blockDim.x - 1) / blockDim.x;
+    // exclusive scan of the tile histogram -> bucket starts inside the tile; a thread's `per`
+    // consecutive counters move as one 8- / 16-byte LDS access (consecutive lanes, consecutive
+    // slots: no bank conflicts -- a scalar walk at stride `per` is a per-way conflict)
+    const uint32_t per = (P2 + blockDim.x - 1) / blockDim.x;  // 1, 2, 4 or 8 (P2 a power of two)
     const uint32_t qa = threadIdx.x * per;
+    uint32_t hv[8];
+    if (qa < P2) {
+      if (per == 8) {
+        const uint4 a = ((const uint4*)hist)[2 * threadIdx.x], b = ((const uint4*)hist)[2 * threadIdx.x + 1];
+        hv[0] = a.x; hv[1] = a.y; hv[2] = a.z; hv[3] = a.w; hv[4] = b.x; hv[5] = b.y; hv[6] = b.z; hv[7] = b.w;
+      } else if (per == 4) {
+        const uint4 a = ((const uint4*)hist)[threadIdx.x];
+        hv[0] = a.x; hv[1] = a.y; hv[2] = a.z; hv[3] = a.w;
+      } else if (per == 2) {
+        const uint2 a = ((const uint2*)hist)[threadIdx.x];
+        hv[0] = a.x; hv[1] = a.y;
+      } else {
+        hv[0] = hist[qa];
+      }
+    }
     uint32_t sum = 0;
-    for (uint32_t q = qa; q < qa + per && q < P2; ++q) sum += hist[q];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if ((uint32_t)i < per && qa < P2) sum += hv[i];
     uint32_t tot;
     uint32_t pre = block_excl_scan_u32<512>(sum, scan_lds, &tot);
-    for (uint32_t q = qa; q < qa + per && q < P2; ++q) {
-      tstart[q] = pre;
-      pre += hist[q];
+    if (qa < P2) {
+      uint32_t ts[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        ts[i] = pre;
+        if ((uint32_t)i < per) pre += hv[i];
+      }
+      if (per == 8) {
+        ((uint4*)tstart)[2 * threadIdx.x] = make_uint4(ts[0], ts[1], ts[2], ts[3]);
+        ((uint4*)tstart)[2 * threadIdx.x + 1] = make_uint4(ts[4], ts[5], ts[6], ts[7]);
+      } else if (per == 4) {
+        ((uint4*)tstart)[threadIdx.x] = make_uint4(ts[0], ts[1], ts[2], ts[3]);
+      } else if (per == 2) {
+        ((uint2*)tstart)[threadIdx.x] = make_uint2(ts[0], ts[1]);
+      } else {
+        tstart[qa] = ts[0];
+      }
     }
     __syncthreads();
 #pragma unroll
@@ -250,7 +283,7 @@ __device__ __forceinline__ void split_range_scatter(const uint32_t* __restrict__
           ((uint2*)tile)[d] = v2[u];
         } else {
           const uint32_t* rec = in + ((uint64_t)t0 + j) * RW;
-          for (int w = 0; w < RW; ++w) tile[(uint64_t)d * RW + w] = rec[w];
+          for (int w = 0; w < RW; ++w) tile[(uint64_t)d * RS + w] = rec[w];
         }
       }
     }
@@ -259,13 +292,13 @@ __device__ __forceinline__ void split_range_scatter(const uint32_t* __restrict__
     for (int u = 0; u < PU; ++u) {
       const uint32_t j = threadIdx.x + u * blockDim.x;
       if (j < tn) {
-        const uint32_t key = tile[(uint64_t)j * RW];
+        const uint32_t key = tile[(uint64_t)j * RS];
         const uint32_t q = (key >> shift2) & mask;
         const uint64_t pos = (uint64_t)cur[q] + (j - tstart[q]);
         if (RW == 2) {
           *(uint2*)(out + pos * 2) = ((const uint2*)tile)[j];
         } else {
-          for (int w = 0; w < RW; ++w) out[pos * RW + w] = tile[(uint64_t)j * RW + w];
+          for (int w = 0; w < RW; ++w) out[pos * RW + w] = tile[(uint64_t)j * RS + w];
         }
       }
     }
@@ -275,15 +308,16 @@ __device__ __forceinline__ void split_range_scatter(const uint32_t* __restrict__
   }
 }
 
-// dynamic LDS: phase 0: P2 words; phase 1: 3 * P2 + 512 * PU * RW words
+// dynamic LDS: phase 0: P2 words; phase 1: 3 * P2 + 512 * PU * RS words (RS: the tile's record
+// stride -- RW, or RW + 1 for even widths >= 4 so a wave's consecutive records start on distinct banks)
 template <int PU>
-__global__ __launch_bounds__(512) void part_split_kernel(const uint32_t* __restrict__ in, int RW,
+__global__ __launch_bounds__(512) void part_split_kernel(const uint32_t* __restrict__ in, int RW, int RS,
                                                         const uint32_t* __restrict__ seg_lo,
                                                         const uint32_t* __restrict__ seg_hi, int spg, int K, int shift2,
                                                         int P2, uint32_t* __restrict__ counts2,
                                                         const uint32_t* __restrict__ base2, uint32_t* __restrict__ out,
                                                         int phase) {
-  extern __shared__ uint32_t h[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t h[];
   __shared__ uint32_t scan_lds[8];
   const int64_t g = blockIdx.x / K;
   const int k = blockIdx.x % K;
@@ -300,14 +334,14 @@ __global__ __launch_bounds__(512) void part_split_kernel(const uint32_t* __restr
     const uint64_t n = hi > lo ? hi - lo : 0;
     const uint32_t a = lo + (uint32_t)(n * k / K), e = lo + (uint32_t)(n * (k + 1) / K);
     if (phase == 0) split_range_count(in, RW, a, e, shift2, mask, h);
-    else split_range_scatter<PU>(in, RW, a, e, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds, out);
+    else split_range_scatter<PU>(in, RW, RS, a, e, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds, out);
   } else {
     const int64_t s0 = g * spg + (int64_t)spg * k / K, s1 = g * spg + (int64_t)spg * (k + 1) / K;
     for (int64_t sgi = s0; sgi < s1; ++sgi) {
       const uint32_t lo = seg_lo[sgi], hi = seg_hi[sgi];
       if (hi <= lo) continue;  // (uniform across the block: every thread reads the same segment)
       if (phase == 0) split_range_count(in, RW, lo, hi, shift2, mask, h);
-      else split_range_scatter<PU>(in, RW, lo, hi, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds, out);
+      else split_range_scatter<PU>(in, RW, RS, lo, hi, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds, out);
     }
   }
   if (phase == 0) {
@@ -316,13 +350,13 @@ __global__ __launch_bounds__(512) void part_split_kernel(const uint32_t* __restr
   }
 }
 
-template __global__ void part_split_kernel<8>(const uint32_t*, int, const uint32_t*, const uint32_t*, int, int, int, int,
+template __global__ void part_split_kernel<8>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int, int,
                                              uint32_t*, const uint32_t*, uint32_t*, int);
-template __global__ void part_split_kernel<4>(const uint32_t*, int, const uint32_t*, const uint32_t*, int, int, int, int,
+template __global__ void part_split_kernel<4>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int, int,
                                              uint32_t*, const uint32_t*, uint32_t*, int);
-template __global__ void part_split_kernel<2>(const uint32_t*, int, const uint32_t*, const uint32_t*, int, int, int, int,
+template __global__ void part_split_kernel<2>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int, int,
                                              uint32_t*, const uint32_t*, uint32_t*, int);
-template __global__ void part_split_kernel<1>(const uint32_t*, int, const uint32_t*, const uint32_t*, int, int, int, int,
+template __global__ void part_split_kernel<1>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int, int,
                                              uint32_t*, const uint32_t*, uint32_t*, int);
 
 __device__ __forceinline__ void lds_fold(uint64_t* t, int op, int64_t v) {

@@ -110,7 +110,11 @@ class World:
             return (t, counts.clone(), [status]) if status is not None else (t, counts.clone())
         n = self.size
         dev = t.device
-        send_meta = torch.stack([counts.to(torch.int64).cpu(), torch.full((n,), int(status or 0), dtype=torch.int64)], 1)
+        # (RCCL: the counts stay on the device -- the meta exchange is queued behind the kernels
+        # that produced them, and the one host wait is for the received meta below)
+        mdev = counts.device if (self.backend == "nccl" and counts.is_cuda) else torch.device("cpu")
+        send_meta = torch.stack([counts.to(device=mdev, dtype=torch.int64),
+                                 torch.full((n,), int(status or 0), dtype=torch.int64, device=mdev)], 1)
         send_meta = send_meta.to(dev if self.backend == "nccl" else "cpu").reshape(-1).contiguous()
         recv_meta = torch.empty_like(send_meta)
         dist.all_to_all_single(recv_meta, send_meta, group=self.pg)

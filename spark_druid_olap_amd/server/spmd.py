@@ -104,8 +104,10 @@ _STREAM_OWNER: Dict[int, Any] = {}  # stream id -> client session id (released w
 
 
 def _streamable(df, s) -> bool:
-    return df.plan is not None and df._stream_source()[1] is not None and \
-        bool(s.conf.typed("spark.sparklinedata.druid.stream.results"))
+    """A Select-backed or large groupBy statement (every rank decides alike: the groupBy check
+    prepares the pushed query, in broadcast order)."""
+    return df.plan is not None and bool(s.conf.typed("spark.sparklinedata.druid.stream.results")) and \
+        (df._stream_source()[1] is not None or df.agg_streamable())
 
 
 def _execute(sessions: Dict[bytes, Any], root, msg: Dict[str, Any]):

@@ -157,15 +157,29 @@ class DataFrame:
         return None, None
 
     def agg_streamable(self) -> bool:
-        """Project/Filter over a pushed groupBy whose engine result can be produced page by page
-        (engine/executor.py PreparedQuery.streamable: a large key space, no host-side ordering)."""
+        """Project/Filter over a pushed groupBy that can be answered page by page: no HAVING,
+        limitSpec or theta sketch, and a key space (the product of its plain dimensions' dictionary
+        sizes) of at least ``engine/executor.py STREAM_MIN_GROUPS``.  Decided from the plan and the
+        catalog alone -- no lowering, no collective -- so the multi-rank dispatcher can ask it on
+        rank 0 while routing a statement (server/spmd.py _assign)."""
         if self.plan is None:
             return False
         _, dq = self._stream_source(aggregates=True)
-        if dq is None or not isinstance(dq.spec, S.GroupByQuerySpec) or self.session.engine.world.distributed:
+        spec = getattr(dq, "spec", None)
+        if not isinstance(spec, S.GroupByQuerySpec) or spec.having is not None or spec.limitSpec is not None:
             return False
-        prep = self.session.prepare_druid(dq)
-        return bool(getattr(prep, "streamable", lambda: False)())
+        if any(isinstance(a, S.ThetaSketchAggregationSpec) for a in (spec.aggregations or [])):
+            return False
+        from .engine import executor as E
+
+        ds = dq.relation.info.datasource
+        space = 1
+        for d in spec.dimensions or []:
+            col = ds.dims.get(getattr(d, "dimension", None)) if type(d) is S.DefaultDimensionSpec else None
+            if col is None:
+                return False
+            space *= max(1, col.cardinality)
+        return space >= E.STREAM_MIN_GROUPS
 
     def _run_pages(self, dq, limit, pages, token):
         left = limit
@@ -194,8 +208,13 @@ class DataFrame:
             # they are pulled (engine/executor.py iter_pages)
             limit, dq = self._stream_source(aggregates=True)
             prep = self.session.prepare_druid(dq)
-            yield from self._run_pages(dq, limit, prep.iter_pages(page_rows), token)
-            return
+            if getattr(prep, "streamable", lambda: False)():
+                # several ranks: only rank 0 pages through the groups (the multi-rank server answers
+                # from rank 0; the peers' cursors end after the first, collective, step)
+                root_only = self.session.engine.world.distributed and self._root_only_safe()
+                yield from self._run_pages(dq, limit, prep.iter_pages(page_rows, root_only), token)
+                return
+            dq = None
         if dq is None:
             df = self.to_pandas(token)
             for a in range(0, max(len(df), 1), page_rows):

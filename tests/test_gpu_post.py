@@ -110,8 +110,8 @@ def test_sparse_decode_kernel_matches_torch_finalize(sess, qi, monkeypatch):
     b = ref.sort_values(cols).reset_index(drop=True)
     for c in cols:
         assert a[c].dtype == b[c].dtype, c
-        if a[c].dtype.kind == "f":
-            np.testing.assert_array_equal(a[c].to_numpy(), b[c].to_numpy())
+        if a[c].dtype.kind == "f":  # (float sums: device atomics add in a different order per run)
+            np.testing.assert_allclose(a[c].to_numpy(), b[c].to_numpy(), rtol=1e-12)
         else:
             assert a[c].tolist() == b[c].tolist(), c
 

@@ -129,9 +129,9 @@ def test_large_groupby_streams_pages(ds_small, df_small, monkeypatch):
     calls = []
     real = E.PreparedQuery.iter_pages
 
-    def spy(self, page_rows):
+    def spy(self, page_rows, root_only=None):
         calls.append(page_rows)
-        yield from real(self, page_rows)
+        yield from real(self, page_rows, root_only)
 
     monkeypatch.setattr(E.PreparedQuery, "iter_pages", spy)
     pages = list(d.iter_batches(page_rows=700))

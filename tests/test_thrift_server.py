@@ -325,7 +325,7 @@ def test_two_rank_python_server_streams_select_pages(tmp_path):
                                    star_schema='{"factTable" : "lineitemSelect", "relations" : []}',
                                    extra_options=', nonAggregateQueryHandling "push_project_and_filters"'))
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
-    env.update(OMP_NUM_THREADS="2", PYTHONPATH=root, SDO_NATIVE_GATEWAY="0")
+    env.update(OMP_NUM_THREADS="2", PYTHONPATH=root, SDO_NATIVE_GATEWAY="0", SDO_STREAM_MIN_GROUPS="1000")
     p = subprocess.Popen([sys.executable, "-m", "spark_druid_olap_amd.server.hive_server", "--gpus", "2",
                           "--tpch-sf", "0.002", "--port", "0", "--port-file", str(pf), "--ui-port", "-1",
                           "--init-sql", str(init)],
@@ -349,6 +349,13 @@ def test_two_rank_python_server_streams_select_pages(tmp_path):
             cur.close()
             n = c.cursor().execute("select count(*) from orderLineItemPartSupplier").fetchall()[0][0]
             assert n == len(full)
+            # a large groupBy streams too: rank 0 pages through the gathered groups
+            c.cursor().execute("set spark.sparklinedata.druid.selectquery.pagesize=997")
+            cur = c.cursor().execute("select o_orderkey, l_linenumber, count(*) from orderLineItemPartSupplier "
+                                     "group by o_orderkey, l_linenumber")
+            got = sorted((int(a), int(b), int(n_)) for a, b, n_ in cur.fetchall())
+            exp = full.groupby(["o_orderkey", "l_linenumber"]).size()
+            assert got == sorted((int(a), int(b), int(v)) for (a, b), v in exp.items())
     finally:
         p.send_signal(signal.SIGTERM)
         try:

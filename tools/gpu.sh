@@ -13,6 +13,7 @@
 #   probe              tools/sql_probe.py (PROBE_ARGS)
 #   pmc                PMC counter passes over tools/kbench_one.py (Q, SF); one pass per counter group
 #   py:SCRIPT          python SCRIPT $PY_ARGS (a tool under tools/)
+#   pyprof:SCRIPT      the same under rocprofv3 --kernel-trace --stats -> gpurun_out/pyprof_<name>/summary.txt
 #
 # Outputs land in gpurun_out/<step>.* ; the tail of each is echoed.
 set -o pipefail
@@ -88,6 +89,20 @@ for step in "$@"; do
       b=$(basename "$s" .py)
       timeout -k 10 ${PY_TIMEOUT:-400} python "$s" ${PY_ARGS:-} > gpurun_out/py_$b.txt 2>&1 || fail "$step" $? gpurun_out/py_$b.txt
       grep -v "^$" gpurun_out/py_$b.txt | tail -${PY_TAIL:-40} ;;
+    pyprof:*)
+      s="${step#pyprof:}"
+      b=$(basename "$s" .py)
+      rm -rf gpurun_out/pyprof_$b
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 ${PY_TIMEOUT:-400} rocprofv3 --kernel-trace --stats \
+        -d "$R/gpurun_out/pyprof_$b" -o run -- python3 "$R/$s" ${PY_ARGS:-} > "$R/gpurun_out/pyprof_$b.log" 2>&1) \
+        || fail "$step" $? gpurun_out/pyprof_$b.log
+      DB=$(find gpurun_out/pyprof_$b -name "*.db" | head -1)
+      if [ -n "$DB" ]; then
+        python tools/rocpd_summary.py "$DB" --top 30 > gpurun_out/pyprof_$b/summary.txt
+      else
+        python tools/prof_summary.py gpurun_out/pyprof_$b > gpurun_out/pyprof_$b/summary.txt
+      fi
+      head -40 gpurun_out/pyprof_$b/summary.txt ;;
     *)
       echo "[gpu.sh] unknown step $step"; exit 2 ;;
   esac

@@ -13,6 +13,9 @@ card -- IPC mappings work within a device as across xGMI).  Checks, on every ran
    answers, with the per-phase times (scan / merge / finalize / post, ``PreparedQuery.run`` stats)
    of both for the rehearsal breakdown.
 
+Run as ONE process it times the same queries on one rank at the same per-rank scale factor (the
+baseline the 2-rank phases compare against; tools/rehearsal.py runs both).
+
 Rank 0 writes a JSON report to ``--out``."""
 import argparse
 import json
@@ -94,7 +97,7 @@ def engine(world, dev, sf, out):
     sess.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)
     sess.sql(tpch.druid_ddl(source="orderLineItemPartSupplierBase", datasource="tpch", with_column_mapping=False))
     res, phases = {}, {}
-    for mode in ("p2p", "rccl"):
+    for mode in (("p2p", "rccl") if world.size > 1 else ("local",)):
         p2p.ENABLED = mode == "p2p"
         sess._plan_cache.clear()
         with results_on_root():
@@ -121,8 +124,9 @@ def engine(world, dev, sf, out):
                                                     **{k: round(statistics.median(v), 4) for k, v in ph.items()}}
     p2p.ENABLED = True
     if world.rank == 0:
-        out["engine_equal"] = {n: r["p2p"] == r["rccl"] for n, r in res.items()}
-        out["engine_rows"] = {n: len(r["p2p"]) for n, r in res.items()}
+        if world.size > 1:
+            out["engine_equal"] = {n: r["p2p"] == r["rccl"] for n, r in res.items()}
+        out["engine_rows"] = {n: len(next(iter(r.values()))) for n, r in res.items()}
         out["phases"] = phases
 
 
@@ -137,13 +141,14 @@ def main():
     from spark_druid_olap_amd.parallel.world import init_world, shutdown
 
     world = init_world(backend="gloo")
-    dev = world.device()
+    dev = world.device() if world.size > 1 else torch.device("cuda", 0)
     assert dev.type == "cuda", "run with SDO_GLOO_GPU=1 on a GPU box"
     torch.cuda.set_device(dev)
-    out = {"world": world.size, "rank": world.rank}
-    synthetic(world, dev, out)
-    if not a.skip_engine and out.get("exchange"):
-        engine(world, dev, a.sf, out)
+    out = {"world": world.size, "rank": world.rank, "sf_per_rank": a.sf}
+    if world.size > 1:
+        synthetic(world, dev, out)
+    if not a.skip_engine and (out.get("exchange") or world.size == 1):
+        engine(world, dev, a.sf, out)  # (one rank: the same-SF baseline of the per-phase split)
     world.barrier()
     if world.rank == 0:
         with open(a.out, "w") as f:
