@@ -403,9 +403,12 @@ class PreparedScan:
             return self._run_part_hashed(b, recs, base)
         hv = self.part_having
         if hv is None:
-            nat.part_agg(recs.data_ptr(), L["rw"], base.data_ptr(), L["nsub"], int(prog.G), L["shift"],
-                         [f[0] for f in L["fields"]], [f[1] for f in L["fields"]], [int(op) for op, _ in prog.slots],
-                         [int(init) for _, init in prog.slots], b.acc.data_ptr(), [], 1, 0, 0, 0, st)
+            # (HLL aggregators: each sub-bucket also writes its groups' rows of the register tables)
+            nat.part_agg_hll(recs.data_ptr(), L["rw"], base.data_ptr(), L["nsub"], int(prog.G), L["shift"],
+                             [f[0] for f in L["fields"]], [f[1] for f in L["fields"]],
+                             [int(op) for op, _ in prog.slots], [int(init) for _, init in prog.slots],
+                             b.acc.data_ptr(), [], 1, 0, 0, 0, [h.data_ptr() for h in b.hll] if L.get("nhll") else [],
+                             int(prog.hll_p), st)
             return None
         while True:
             out = b.part.get("hv_out")
@@ -458,7 +461,7 @@ class PreparedScan:
         """Fuse a groupBy HAVING into the partitioned aggregation (engine/executor.py): only existing
         groups passing it leave the kernel, as sparse partials.  terms: [(slot, is_f64, op, divisor,
         constant)], op 0 equalTo / 1 greaterThan / 2 lessThan.  False when this scan cannot."""
-        if self.mode != D.M_PART or not terms or len(terms) > 4:
+        if self.mode != D.M_PART or not terms or len(terms) > 4 or (self.part or {}).get("nhll"):
             return False
         self.part_having = ([tuple(t) for t in terms], 1 if conj else 0)
         return True
@@ -866,6 +869,7 @@ class PreparedMask:
 
 PART_TABLE_BYTES = int(os.environ.get("SDO_PART_TABLE_BYTES", 32 << 10))  # LDS table per sub-bucket
 HASH_TABLE_BYTES = 128 << 10  # LDS hash table of a hash-partitioned sub-bucket (keys + slots)
+PART_HLL_TABLE_BYTES = 128 << 10  # LDS slots + HLL byte registers of a partitioned sub-bucket
 HLL32_MAX_BYTES = int(os.environ.get("SDO_HLL32_MAX_BYTES", str(512 << 20)))  # u32 scan-time registers
 
 
@@ -878,15 +882,21 @@ def part_layout(prog) -> dict:
     ns = max(1, prog.nslots)
     if jit.part_hashed(prog):
         return part_hash_layout(prog)
-    shift = max(0, int(math.floor(math.log2(max(8, PART_TABLE_BYTES // (8 * ns))))))
+    nh = jit.part_hll_count(prog) if prog.nhll else 0
+    if nh:
+        # a group's slots plus its byte registers: sub-buckets of a few dozen groups per LDS table
+        per = 8 * ns + nh * (1 << prog.hll_p)
+        shift = max(0, int(math.floor(math.log2(max(1, PART_HLL_TABLE_BYTES // per)))))
+    else:
+        shift = max(0, int(math.floor(math.log2(max(8, PART_TABLE_BYTES // (8 * ns))))))
     gbits = max(1, int(math.ceil(math.log2(max(2, prog.G)))))
     rem = max(0, gbits - shift)
     fields = jit.part_fields(prog)
-    rw = 1 + sum(w for _, w in fields)
+    rw = 1 + sum(w for _, w in fields) + nh
     if rem <= 10:
         p1 = 1 << rem
         return {"levels": 1, "shift": shift, "shift1": shift, "p1": p1, "p2": 1, "k": 1, "nsub": p1,
-                "fields": fields, "rw": rw}
+                "fields": fields, "rw": rw, "nhll": nh}
     b1 = min(10, (rem + 1) // 2)
     b2 = rem - b1
     if b2 > 10:
@@ -894,7 +904,7 @@ def part_layout(prog) -> dict:
     p1, p2 = 1 << b1, 1 << b2
     k = max(1, min(64, 4096 // p1))
     return {"levels": 2, "shift": shift, "shift1": shift + b2, "p1": p1, "p2": p2, "k": k, "nsub": p1 * p2,
-            "fields": fields, "rw": rw}
+            "fields": fields, "rw": rw, "nhll": nh}
 
 
 def part_hash_layout(prog, scale: int = 1) -> dict:

@@ -70,7 +70,7 @@ __global__ void part_hash_agg_kernel(const uint32_t* recs, int RW, const uint32_
                                      PartFields f, PartHaving hv, int64_t* out_keys, uint64_t* out_acc,
                                      unsigned long long* out_count, int64_t cap, int* overflow);
 __global__ void part_agg_kernel(const uint32_t* recs, int RW, const uint32_t* base, int64_t nsub, int64_t G, int shift,
-                                PartFields f, uint64_t* gacc, PartHaving hv, int64_t* out_keys,
+                                PartFields f, PartHll hl, uint64_t* gacc, PartHaving hv, int64_t* out_keys,
                                 unsigned long long* out_count, int64_t cap);
 __global__ void theta_hist_kernel(const int64_t* g, const int64_t* h, int64_t n, int bits, uint32_t* hist);
 __global__ void theta_thresh_kernel(const uint32_t* hist, int bits, const int64_t* target, int64_t* bound);
@@ -577,10 +577,12 @@ static void part_split(uint64_t in, int RW, uint64_t seg_lo, uint64_t seg_hi, in
 // having: [] for the dense table, else up to 4 (slot, is_f64, op, divisor, constant) terms; conj 1 = AND.
 // With terms, gacc receives the surviving rows ([cap][nslots]), out_keys their keys, out_count
 // (zeroed here) their number.
-static void part_agg(uint64_t recs, int RW, uint64_t base, int64_t nsub, int64_t G, int shift, std::vector<int> slot,
-                     std::vector<int> width, std::vector<int> ops, std::vector<int64_t> init, uint64_t gacc,
-                     std::vector<std::tuple<int, int, int, double, double>> having, int conj, uint64_t out_keys,
-                     uint64_t out_count, int64_t cap, uint64_t stream) {
+// hll: the [G][2^hll_p] byte register tables of the HLL aggregators the records carry (one word
+// each after the value fields), empty for none.
+static void part_agg_hll(uint64_t recs, int RW, uint64_t base, int64_t nsub, int64_t G, int shift, std::vector<int> slot,
+                         std::vector<int> width, std::vector<int> ops, std::vector<int64_t> init, uint64_t gacc,
+                         std::vector<std::tuple<int, int, int, double, double>> having, int conj, uint64_t out_keys,
+                         uint64_t out_count, int64_t cap, std::vector<uint64_t> hll, int hll_p, uint64_t stream) {
   if (nsub <= 0 || G <= 0) return;
   sdo::PartFields f{};
   if (slot.size() != width.size() || slot.size() > (size_t)sdo::MAX_SLOTS) throw std::invalid_argument("part_agg: fields");
@@ -595,13 +597,24 @@ static void part_agg(uint64_t recs, int RW, uint64_t base, int64_t nsub, int64_t
     f.width[j] = width[j];
     words += width[j];
   }
+  sdo::PartHll hl{};
+  if (hll.size() > (size_t)sdo::PART_MAX_HLL || (!hll.empty() && (hll_p < 4 || hll_p > 16)))
+    throw std::invalid_argument("part_agg: HLL aggregators");
+  hl.n = (int)hll.size();
+  hl.p = hll.empty() ? 0 : hll_p;
+  for (size_t h = 0; h < hll.size(); ++h) hl.regs[h] = (unsigned char*)hll[h];
+  words += hl.n;
   if (words != RW) throw std::invalid_argument("part_agg: record width does not match the fields");
   for (size_t s = 0; s < ops.size(); ++s) {
     f.op[s] = ops[s];
     f.init[s] = init[s];
   }
-  const int64_t lds = ((int64_t)1 << shift) * f.nslots * 8;
-  if (shift < 0 || lds > 64 * 1024) throw std::invalid_argument("part_agg: sub-bucket table exceeds 64 KiB of LDS");
+  const int64_t lds = ((int64_t)1 << shift) * (f.nslots * 8 + (int64_t)hl.n * ((int64_t)1 << hl.p));
+  if (shift < 0 || lds > 160 * 1024 - 256 || (hl.n == 0 && lds > 64 * 1024))
+    throw std::invalid_argument("part_agg: sub-bucket table exceeds the LDS");
+  if (lds > 64 * 1024)  // (the kernel's static LDS counts against the 160 KiB too: exactly the dynamic bytes)
+    check(hipFuncSetAttribute((const void*)sdo::part_agg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+          "part_agg attr");
   const int64_t grid = (nsub + 7) / 8 * 8;
   if (grid > ((int64_t)1 << 31) - 8) throw std::invalid_argument("part_agg: too many sub-buckets");
   sdo::PartHaving hv{};
@@ -621,9 +634,17 @@ static void part_agg(uint64_t recs, int RW, uint64_t base, int64_t nsub, int64_t
   if (hv.nterms)
     check(hipMemsetAsync((void*)out_count, 0, 8, (hipStream_t)stream), "part_agg count reset");
   hipLaunchKernelGGL(sdo::part_agg_kernel, dim3((unsigned)grid), dim3(512), (unsigned)lds, (hipStream_t)stream,
-                     (const uint32_t*)recs, RW, (const uint32_t*)base, nsub, G, shift, f, (uint64_t*)gacc, hv,
+                     (const uint32_t*)recs, RW, (const uint32_t*)base, nsub, G, shift, f, hl, (uint64_t*)gacc, hv,
                      (int64_t*)out_keys, (unsigned long long*)out_count, cap);
   check(hipGetLastError(), "part_agg_kernel launch");
+}
+
+static void part_agg(uint64_t recs, int RW, uint64_t base, int64_t nsub, int64_t G, int shift, std::vector<int> slot,
+                     std::vector<int> width, std::vector<int> ops, std::vector<int64_t> init, uint64_t gacc,
+                     std::vector<std::tuple<int, int, int, double, double>> having, int conj, uint64_t out_keys,
+                     uint64_t out_count, int64_t cap, uint64_t stream) {
+  part_agg_hll(recs, RW, base, nsub, G, shift, slot, width, ops, init, gacc, having, conj, out_keys, out_count, cap, {},
+               0, stream);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -859,6 +880,7 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("part_keys", &part_keys);
   m.def("part_split", &part_split);
   m.def("part_agg", &part_agg);
+  m.def("part_agg_hll", &part_agg_hll);
   m.def("part_hash_agg", &part_hash_agg);
   m.def("layout", &layout);
   m.def("device_info", &device_info);

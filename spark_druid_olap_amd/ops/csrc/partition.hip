@@ -388,9 +388,22 @@ __device__ __forceinline__ bool having_pass(const PartHaving& h, const uint64_t*
 // HAVING mode: the groups of the sub-bucket that exist (presence count, slot 0, > 0) and pass the
 // predicate are appended -- key + slots -- at a position reserved with one global atomic per block;
 // writes past `cap` are dropped (the host sees out_count > cap and re-runs with room).
+// Raise one LDS byte register to v (compare-and-swap on its dword; a relaxed read filters the
+// updates that cannot raise it).
+__device__ __forceinline__ void lds_max_u8(unsigned char* regs, int64_t idx, uint32_t v) {
+  uint32_t* w = (uint32_t*)(regs + (idx & ~(int64_t)3));
+  const uint32_t sh = (uint32_t)(idx & 3) * 8u;
+  uint32_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (((old >> sh) & 0xffu) < v) {
+    const uint32_t prev = atomicCAS(w, old, (old & ~(0xffu << sh)) | (v << sh));
+    if (prev == old) break;
+    old = prev;
+  }
+}
+
 __global__ __launch_bounds__(512) void part_agg_kernel(const uint32_t* __restrict__ recs, int RW,
                                                       const uint32_t* __restrict__ base, int64_t nsub, int64_t G,
-                                                      int shift, PartFields f, uint64_t* __restrict__ gacc,
+                                                      int shift, PartFields f, PartHll hl, uint64_t* __restrict__ gacc,
                                                       PartHaving hv, int64_t* __restrict__ out_keys,
                                                       unsigned long long* __restrict__ out_count, int64_t cap) {
   extern __shared__ __attribute__((aligned(16))) uint64_t t[];
@@ -403,11 +416,15 @@ __global__ __launch_bounds__(512) void part_agg_kernel(const uint32_t* __restric
   const int64_t nk = (G - k0) < ((int64_t)1 << shift) ? (G - k0) : ((int64_t)1 << shift);
   const int NS = f.nslots;
   for (int64_t i = threadIdx.x; i < nk * NS; i += blockDim.x) t[i] = (uint64_t)f.init[i % NS];
+  // HLL byte registers after the slot table: [n][2^shift][2^p]
+  const int64_t m = (int64_t)1 << hl.p;
+  unsigned char* hr = (unsigned char*)(t + ((int64_t)1 << shift) * NS);
+  for (int64_t i = threadIdx.x; i < (hl.n * (m << shift)) / 4; i += blockDim.x) ((uint32_t*)hr)[i] = 0u;
   __syncthreads();
   const uint32_t lo = base[r], hi = base[r + 1];
   constexpr int PU = 4;
   const uint32_t step = blockDim.x * PU;
-  if (RW == 2 && f.nfields == 1 && f.width[0] == 1) {
+  if (hl.n == 0 && RW == 2 && f.nfields == 1 && f.width[0] == 1) {
     // u32 key + one i32 value (TPC-H Q18: sum(l_quantity) per order): 8-byte record loads, PU in flight
     const int s0 = f.slot[0], op = f.op[s0];
     for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += step) {
@@ -425,7 +442,7 @@ __global__ __launch_bounds__(512) void part_agg_kernel(const uint32_t* __restric
         lds_fold(t + local * NS + s0, op, (int64_t)(int32_t)r2[u].y);
       }
     }
-  } else if (RW == 1 && f.nfields == 1 && f.width[0] == 0) {
+  } else if (hl.n == 0 && RW == 1 && f.nfields == 1 && f.width[0] == 0) {
     // key only (histograms, unfiltered counts)
     const int s0 = f.slot[0], op = f.op[s0];
     for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += step) {
@@ -460,12 +477,22 @@ __global__ __launch_bounds__(512) void part_agg_kernel(const uint32_t* __restric
         const int s = f.slot[j];
         lds_fold(row + s, f.op[s], v);
       }
+      for (int h = 0; h < hl.n; ++h) {
+        const uint32_t code = rec[w + h];
+        if (code & 0xffu) lds_max_u8(hr + (((int64_t)h << shift) + local) * m, (int64_t)((code >> 8) & (uint32_t)(m - 1)),
+                                     code & 0xffu);
+      }
     }
   }
   __syncthreads();
   if (hv.nterms == 0) {
     uint64_t* g = gacc + k0 * NS;
     for (int64_t i = threadIdx.x; i < nk * NS; i += blockDim.x) g[i] = t[i];
+    for (int h = 0; h < hl.n; ++h) {  // the sub-bucket's register rows, 16 bytes per thread step
+      const uint4* src = (const uint4*)(hr + ((int64_t)h << shift) * m);
+      uint4* dst = (uint4*)(hl.regs[h] + k0 * m);
+      for (int64_t i = threadIdx.x; i < nk * m / 16; i += blockDim.x) dst[i] = src[i];
+    }
     return;
   }
   __shared__ uint32_t scan_lds[8];

@@ -218,6 +218,16 @@ struct PartFields {
   int64_t init[MAX_SLOTS];
 };
 
+// HLL aggregators of the partitioned group-by (partition.hip part_agg_kernel): each record carries
+// one (bucket << 8 | rho) word per HLL after its value fields; a sub-bucket's groups keep their
+// byte registers in LDS and write them to their rows of the [G][2^p] register tables.
+constexpr int PART_MAX_HLL = 4;
+struct PartHll {
+  int32_t n;
+  int32_t p;
+  unsigned char* regs[PART_MAX_HLL];
+};
+
 // HAVING fused into the partitioned aggregation (partition.hip part_agg_kernel): up to 4
 // comparisons of a slot value (int64 / scale divisor, or f64 bits) with a constant, AND-ed or
 // OR-ed.  nterms == 0: write the dense table instead.

@@ -127,13 +127,30 @@ def part_record_words(prog) -> int:
     return 3 if part_hashed(prog) else 1
 
 
+PART_HLL = True  # HLL aggregators ride the partitioned records as (bucket << 8 | rho) words
+PART_HLL_MAX_BYTES = 1 << 30  # register tables ([G][2^p] bytes per HLL) the partitioned path writes
+
+
+def part_hll_count(prog) -> int:
+    """HLL aggregators a partition record carries (one word each, after the value fields)."""
+    if not hasattr(prog, "aops"):
+        return int(prog.nhll)
+    return sum(1 for a in prog.aops if a["kind"] in D.HLL_KINDS)
+
+
 def part_eligible(prog) -> bool:
     """The partitioned group-by handles every slot operator and any key space (beyond 32 bits by
-    hash); it does not carry HLL sketches."""
+    hash), and query-time HLL sketches of dense (u32) key spaces whose register tables fit
+    PART_HLL_MAX_BYTES; not stored (rolled-up) sketches."""
     slots = getattr(prog, "slots", None)
     n = len(slots) if slots is not None else prog.nslots
-    return n > 0 and not prog.nhll and not getattr(prog, "stored_hll", None) and 0 < prog.G < (1 << 62) \
-        and not prog.empty
+    if not (n > 0 and not getattr(prog, "stored_hll", None) and 0 < prog.G < (1 << 62) and not prog.empty):
+        return False
+    if prog.nhll:
+        nh = part_hll_count(prog)
+        return PART_HLL and nh == prog.nhll and nh <= 4 and not part_hashed(prog) and \
+            prog.G * nh * (1 << prog.hll_p) <= PART_HLL_MAX_BYTES
+    return True
 
 
 # accumulator copies per wave for tiny dense key spaces (lanes l, l+C, l+2C.. share copy l % C; up
@@ -490,6 +507,21 @@ class _Gen:
                 body.append(f"          {{ const uint64_t x_ = (uint64_t)({val}); o_[{w}] = (uint32_t)x_; "
                             f"o_[{w + 1}] = (uint32_t)(x_ >> 32); }}")
             w += width
+        for ai, a in enumerate(p.aops):
+            # HLL: the row's (bucket << 8 | rho) word (rho 0: no update -- a row its filter rejects)
+            if a["kind"] not in D.HLL_KINDS:
+                continue
+            val = f"v{ai}_[u]"
+            if a["kind"] == D.A_HLL_CODE:  # precomputed code plane: bucket << 5 | rho
+                code = f"(((((uint32_t){val}) >> 5) << 8) | ((uint32_t){val} & 31u))"
+            else:
+                code = f"({{ uint32_t b_, r_; hll_bucket_rho({val}, {_lit(a.get('salt', 0))}, {p.hll_p}, b_, r_); " \
+                       f"(b_ << 8) | r_; }})"
+            if a.get("filt_len"):
+                fx = self.word_expr(a["filt_off"], a["filt_off"] + a["filt_len"])
+                code = f"(((({fx}) >> lane) & 1ull) ? {code} : 0u)"
+            body.append(f"          o_[{w}] = {code};")
+            w += 1
         body.append("        }")
         body.append("        woff += (uint32_t)__popcll(am_);")
 

@@ -371,8 +371,8 @@ def plan_groupby(prog, jit: bool, local: bool) -> GroupByPlan:
         else:
             dense = 2 * table / HBM_BW
         if not presence:
-            # one random atomic per qualifying row and slot
-            dense += est_rows * ns / (ATOMIC_RATE * (8 if table <= L2_TABLE_BYTES else 1))
+            # one random atomic per qualifying row and slot (and HLL register: a byte CAS)
+            dense += est_rows * (ns + prog.nhll) / (ATOMIC_RATE * (8 if table <= L2_TABLE_BYTES else 1))
         costs["dense-global"] = dense * 1e3
         part = partitioned_cost_s(prog, est_rows) if (jit and PARTITIONED and not presence and not empty) else None
         if part is not None:
@@ -422,9 +422,10 @@ def partitioned_cost_s(prog, est_rows: float) -> Optional[float]:
     except ValueError:
         return None
     rec = 4 * L["rw"]
-    # producer write, per level a count read + a scatter read and write, the aggregation read, the table
+    # producer write, per level a count read + a scatter read and write, the aggregation read, the
+    # table (and the HLL register tables) written once
     passes = 1 + 3 * L["levels"] + 1
-    traffic = est_rows * rec * passes + prog.G * max(1, prog.nslots) * 8
+    traffic = est_rows * rec * passes + prog.G * (max(1, prog.nslots) * 8 + L.get("nhll", 0) * (1 << prog.hll_p))
     return traffic / HBM_BW + (2 + 4 * L["levels"]) * LAUNCH_S
 
 

@@ -70,6 +70,33 @@ def test_partitioned_two_levels_and_row_filter(gpu_ds, monkeypatch):
     assert p.part["levels"] == 2
 
 
+@pytest.mark.parametrize("table_bytes", [128 << 10, 8 << 10])
+def test_partitioned_hll_registers_match_atomic_table(gpu_ds, monkeypatch, table_bytes):
+    """HLL aggregators on the partitioned path: every group's byte registers (a max, so order-free)
+    equal the HBM-atomic table's exactly -- one and two split levels, a filtered HLL included."""
+    from spark_druid_olap_amd.engine import device_exec as DE
+    from spark_druid_olap_amd.engine.lower import Lowerer
+
+    aggs = [S.FunctionAggregationSpec("count", "c"), S.FunctionAggregationSpec("longSum", "q", "l_quantity"),
+            S.CardinalityAggregationSpec("u", ["l_partkey"]),
+            S.FilteredAggregationSpec(S.SelectorFilterSpec("l_returnflag", "R"),
+                                      S.CardinalityAggregationSpec("ur", ["l_suppkey"]), "ur")]
+    prog = Lowerer(gpu_ds).lower_aggregate(["1992-01-01/1999-01-01"], None, [S.DefaultDimensionSpec("o_orderkey")],
+                                           S.Granularity.parse("all"), aggs)
+    monkeypatch.setattr(DE, "PART_HLL_TABLE_BYTES", table_bytes)
+    part = DE.PreparedScan(prog, mode=D.M_PART)
+    assert part.mode == D.M_PART and part.part["nhll"] == 2
+    ref = DE.PreparedScan(prog, mode=D.M_DENSE_GLOBAL)
+    for _ in range(2):
+        a = part.run()
+    b = ref.run()
+    assert a.kind == "dense" and len(a.hll) == 2
+    assert torch.equal(a.acc.cpu(), b.acc.cpu())
+    for x, y in zip(a.hll, b.hll):
+        assert torch.equal(x.cpu(), y.cpu())
+    assert int(a.hll[0].sum()) > 0 and int(a.hll[1].sum()) > 0
+
+
 def test_part_keys_histogram_vs_bincount():
     """part_keys (level-1 producer over a key array) -> split -> LDS counts == torch.bincount;
     keys outside [0, nbins) are dropped, never written."""

@@ -99,6 +99,34 @@ def test_jit_partition_producers_compile(tmp_path, monkeypatch, ds_small):
 
 
 
+def test_jit_partitioned_producer_carries_hll_words(ds_small, tmp_path, monkeypatch):
+    """HLL aggregators on the partitioned path (verdict r3 #5): each record ends with one
+    (bucket << 8 | rho) word per HLL -- hashed per row, or unpacked from the precomputed code plane,
+    zero when the aggregator's filter rejects the row -- and the producer compiles for gfx950."""
+    from spark_druid_olap_amd.engine import device_exec as DE
+    from spark_druid_olap_amd.engine.lower import Lowerer
+    from spark_druid_olap_amd.ops import desc as D
+    from spark_druid_olap_amd.ops import jit
+    from spark_druid_olap_amd.query import spec as S
+
+    monkeypatch.setenv("SDO_JIT_CACHE", str(tmp_path))
+    aggs = [S.FunctionAggregationSpec("count", "c"), S.FunctionAggregationSpec("longSum", "q", "l_quantity"),
+            S.CardinalityAggregationSpec("u", ["l_partkey"]),
+            S.FilteredAggregationSpec(S.SelectorFilterSpec("l_returnflag", "R"),
+                                      S.CardinalityAggregationSpec("ur", ["l_suppkey"]), "ur")]
+    prog = Lowerer(ds_small).lower_aggregate(["1992-01-01/1999-01-01"], None,
+                                             [S.DefaultDimensionSpec("o_orderkey")], None, aggs)
+    assert prog.nhll == 2 and jit.part_eligible(prog) and jit.part_hll_count(prog) == 2
+    L = DE.part_layout(prog)
+    assert L["nhll"] == 2 and L["rw"] == 1 + sum(w for _, w in L["fields"]) + 2
+    per = 8 * prog.nslots + 2 * (1 << prog.hll_p)
+    assert (1 << L["shift"]) * per <= DE.PART_HLL_TABLE_BYTES
+    w = jit.JitScan(prog, D.M_PART, 4, False, 1 << prog.hll_p, True, load=False)
+    assert w.src.count("hll_bucket_rho(") + w.src.count(">> 5) << 8)") >= 2
+    monkeypatch.setattr(jit, "PART_HLL", False)
+    assert not jit.part_eligible(prog)
+
+
 def test_hll_estimate_bf16_operands_are_exact():
     """hll_estimate_kernel (ops/csrc/olap_scan.hip) feeds 2^-M to a bf16 MFMA as the bit pattern
     (127 - M) << 7: exact powers of two for every register value a 64-bit hash can produce (M <= 65),
