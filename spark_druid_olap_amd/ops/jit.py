@@ -475,7 +475,7 @@ class _Gen:
         body.append("        const uint64_t am_ = __ballot(mine);")
         fields = part_fields(p, self.cols)
         hdr = part_record_words(p)
-        rw = hdr + sum(w for _, w in fields)
+        rw = hdr + sum(w for _, w in fields) + (part_hll_count(p) if p.nhll else 0)
         body.append("        if (mine) {")
         body.append(f"          uint32_t* o_ = precs + (uint64_t)(cbase + woff + (uint32_t)__popcll(am_ & lmlt)) * {rw}u;")
         if hdr == 3:

@@ -123,6 +123,8 @@ def test_jit_partitioned_producer_carries_hll_words(ds_small, tmp_path, monkeypa
     assert (1 << L["shift"]) * per <= DE.PART_HLL_TABLE_BYTES
     w = jit.JitScan(prog, D.M_PART, 4, False, 1 << prog.hll_p, True, load=False)
     assert w.src.count("hll_bucket_rho(") + w.src.count(">> 5) << 8)") >= 2
+    # the record stride the producer writes at is the layout's (header + fields + HLL words)
+    assert f"* {L['rw']}u;" in w.src
     monkeypatch.setattr(jit, "PART_HLL", False)
     assert not jit.part_eligible(prog)
 
