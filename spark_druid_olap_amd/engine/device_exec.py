@@ -454,6 +454,13 @@ class PreparedScan:
                 nb = self._bufs()
                 return self._run_part(nb) if nb.part is not None else self._empty()
             if n <= acc.shape[0]:
+                if not hv[0] and n * 8 < L["nsub"] << (L["cap_log2"] - 1):
+                    # far fewer groups than the row estimate sized for (TPC-H Q16: 12M groups of
+                    # 554M estimated rows -> 262k sub-buckets, each LDS table 128 KB for ~45 keys,
+                    # 8.5 ms of table init and emit): later runs partition for the observed count
+                    with self._slot_lock:
+                        self.part = part_hash_layout(prog, L["scale"], groups=1.25 * n)
+                        self._slots.clear()
                 return Partials("sparse", acc[:n], keys[:n], [])
             self.part_cap = _next_pow2(n + n // 4)  # more groups than room: grow, aggregate again
 
@@ -907,16 +914,19 @@ def part_layout(prog) -> dict:
             "fields": fields, "rw": rw, "nhll": nh}
 
 
-def part_hash_layout(prog, scale: int = 1) -> dict:
+def part_hash_layout(prog, scale: int = 1, groups: Optional[float] = None) -> dict:
     """Sub-buckets of a hash-partitioned group-by: enough that each holds ~half its LDS table's
-    capacity of distinct keys by the planner's group estimate (``scale`` x more after an overflow);
-    bucket bits are the top bits of the record's 32-bit hash, split over one level (<= 2^10
-    buckets) or two."""
+    capacity of distinct keys by the group estimate -- the planner's row estimate at first, the
+    observed group count once a run has seen it (``groups``) -- ``scale`` x more after an
+    overflow; bucket bits are the top bits of the record's 32-bit hash, split over one level
+    (<= 2^10 buckets) or two."""
     from ..ops import jit
 
     ns = max(1, prog.nslots)
     cap_log2 = max(6, min(14, int(math.floor(math.log2(HASH_TABLE_BYTES // (8 * (1 + ns)))))))
-    groups = max(1.0, min(float(prog.G), float(getattr(prog, "est_rows", prog.G)) * 1.2))
+    if groups is None:
+        groups = min(float(prog.G), float(getattr(prog, "est_rows", prog.G)) * 1.2)
+    groups = max(1.0, groups)
     nsub = max(8, int(math.ceil(groups * scale / (1 << (cap_log2 - 1)))))
     bits = min(20, max(3, int(math.ceil(math.log2(nsub)))))
     fields = jit.part_fields(prog)

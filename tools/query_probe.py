@@ -93,8 +93,6 @@ def main():
             t = time.time()
             pq = eng.prepare(qs, ds)
             sc = pq.scans[0][2]
-            j = getattr(sc, "jit", None)
-            info = (f"mode={sc.mode} U={getattr(j, 'U', None)} grid={sc.grid} lds={j.lay.total if j else None}")
             ts = []
             r = None
             for i in range(6):
@@ -103,6 +101,9 @@ def main():
                 r = pq.run()
                 torch.cuda.synchronize()
                 ts.append((time.perf_counter() - t1) * 1e3)
+            j = getattr(sc, "jit", None)
+            info = (f"mode={sc.mode} U={getattr(j, 'U', None)} grid={getattr(sc, 'grid', None)} "
+                    f"lds={j.lay.total if j else None}")
             ok = ""
             if name in base:
                 ok = "same" if _same(base[name], r) else "DIFFERENT"
