@@ -116,8 +116,12 @@ def _jit_build(prog, mode: int, hll_lds: bool, m: int, shared: bool = False, loa
             lay = jit.layout(prog, mode, U, hll_lds, m, budget, regstage, shared)
             if lay.total <= budget and (shared or mode != D.M_DENSE_LDS or lay.ncopy >= 4 or U == prefs[-1]):
                 try:
+                    # a kernel that would spill registers takes the next smaller unroll
                     return jit.JitScan(prog, mode, U, hll_lds, m, bool(native.narrow4()) if load else True,
-                                       load=load, budget=budget, regstage=regstage, shared=shared)
+                                       load=load, budget=budget, regstage=regstage, shared=shared,
+                                       reject_spills=U != prefs[-1])
+                except jit.JitSpill:
+                    continue
                 except Exception as e:  # pragma: no cover - compile problems fall back loudly
                     import warnings
 

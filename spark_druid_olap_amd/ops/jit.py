@@ -978,11 +978,48 @@ def is_loaded(src: str) -> bool:
     return _code_key(src) in _handles
 
 
+def kernel_meta(code: bytes) -> dict:
+    """The AMDGPU metadata of a code object's first kernel (ELF note NT_AMDGPU_METADATA, msgpack):
+    VGPR / SGPR counts and spills, private (scratch) and group segment sizes.  {} if absent."""
+    import struct
+
+    try:
+        shoff = struct.unpack_from("<Q", code, 0x28)[0]
+        shentsize, shnum = struct.unpack_from("<HH", code, 0x3A)
+        for i in range(shnum):
+            off = shoff + i * shentsize
+            if struct.unpack_from("<I", code, off + 4)[0] != 7:  # SHT_NOTE
+                continue
+            so, ss = struct.unpack_from("<QQ", code, off + 0x18)
+            p = so
+            while p + 12 <= so + ss:
+                nsz, dsz, typ = struct.unpack_from("<III", code, p)
+                p += 12 + ((nsz + 3) & ~3)
+                desc = code[p:p + dsz]
+                p += (dsz + 3) & ~3
+                if typ == 32:  # NT_AMDGPU_METADATA
+                    import msgpack
+
+                    md = msgpack.unpackb(desc, raw=False, strict_map_key=False)
+                    ks = md.get("amdhsa.kernels") or [{}]
+                    return dict(ks[0])
+    except (struct.error, ValueError, IndexError, ImportError):
+        pass
+    return {}
+
+
+class JitSpill(RuntimeError):
+    """The kernel would spill registers to scratch (engine/device_exec.py _jit_build then tries a
+    smaller unroll): a spilling scan is slow, and its scratch is allocated by the HIP runtime outside
+    the torch allocator -- under memory pressure that allocation fails and aborts the queue."""
+
+
 class JitScan:
     """A compiled, specialized scan kernel for one ScanProgram shape."""
 
     def __init__(self, prog, mode: int, U: int, hll_lds: bool, m: int, narrow4: bool, load: bool = True,
-                 budget: int = 150 * 1024, regstage: bool = False, shared: bool = False, literals: bool = False):
+                 budget: int = 150 * 1024, regstage: bool = False, shared: bool = False, literals: bool = False,
+                 reject_spills: bool = False):
         self.literals = literals
         self._args = (prog, mode, U, hll_lds, m, narrow4, load, budget, regstage, shared)
         self.lay = layout(prog, mode, U, hll_lds, m, budget, regstage, shared)
@@ -993,9 +1030,12 @@ class JitScan:
                            ).hexdigest()[:6]
         self.name = f"sdo_jit_{tag}"
         self.src = g.source(self.name)
+        self.meta = kernel_meta(compile_code(self.src, self.name) or b"")
+        self.spills = bool(self.meta.get(".private_segment_fixed_size") or self.meta.get(".vgpr_spill_count"))
+        if self.spills and reject_spills:
+            raise JitSpill(f"{self.name} U={U}: {self.meta.get('.vgpr_spill_count')} VGPR spills, "
+                           f"{self.meta.get('.private_segment_fixed_size')} B scratch")
         self.handle = compile_source(self.src, self.name) if load else -1
-        if not load:
-            compile_code(self.src, self.name)
         self.U = U
 
     def specialized(self) -> "JitScan":

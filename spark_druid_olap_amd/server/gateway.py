@@ -196,9 +196,10 @@ class NativeHiveServer(HiveThriftServer):
 
     # ------------------------------------------------------------------ lifecycle
     def start(self) -> "NativeHiveServer":
-        from ..utils.memory import serving_gc
+        from ..utils.memory import reserve_runtime_memory, serving_gc
 
         serving_gc()
+        reserve_runtime_memory()  # device memory the HIP runtime allocates outside torch (scratch, RCCL)
         mod = load_native()
         self._gw = mod.Gateway(self.host, self.port, self._forward)
         # SDO_COALESCE=0: every statement executes (engine throughput, not result sharing)

@@ -128,9 +128,10 @@ class HiveThriftServer:
 
     # ------------------------------------------------------------------------------ lifecycle
     def start(self) -> "HiveThriftServer":
-        from ..utils.memory import serving_gc
+        from ..utils.memory import reserve_runtime_memory, serving_gc
 
         serving_gc()
+        reserve_runtime_memory()  # device memory the HIP runtime allocates outside torch (scratch, RCCL)
         server = self
 
         class Handler(socketserver.BaseRequestHandler):

@@ -41,3 +41,25 @@ def serving_gc() -> None:
     gc.collect()
     gc.freeze()
     gc.set_threshold(50_000, 50, 100)
+
+
+RUNTIME_RESERVE = int(os.environ.get("SDO_RUNTIME_RESERVE_GB", "8")) << 30
+
+
+def reserve_runtime_memory(device=None) -> float:
+    """Cap the torch caching allocator below the device size, leaving ``RUNTIME_RESERVE`` bytes to
+    the HIP runtime's own allocations (kernel scratch, loaded code objects, RCCL buffers).  Those
+    are made outside torch: a serving process whose cache has grown over the whole device gets a
+    scratch allocation failure, which aborts the HIP queue -- every later statement fails.  With
+    the cap torch raises an out-of-memory error first, which the engine answers by evicting cached
+    scan buffers (engine/device_exec.py _with_eviction) or fails that one statement.  Returns the
+    fraction set (0 when there is no GPU)."""
+    import torch
+
+    if not torch.cuda.is_available() or RUNTIME_RESERVE <= 0:
+        return 0.0
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    total = torch.cuda.get_device_properties(dev).total_memory
+    frac = max(0.5, 1.0 - RUNTIME_RESERVE / total)
+    torch.cuda.set_per_process_memory_fraction(frac, dev)
+    return frac

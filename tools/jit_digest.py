@@ -6,6 +6,9 @@ choices as ``engine/device_exec.py _jit_build``.  Refactors of the generator tha
 the default kernels compare the digests before and after:
 
   python tools/jit_digest.py > /tmp/before.txt   ...   python tools/jit_digest.py | diff /tmp/before.txt -
+
+``--spills`` compiles every kernel (hipRTC, no GPU needed) and flags those that use scratch;
+``--dump DIR`` writes the sources.
 """
 import hashlib
 import os
@@ -30,7 +33,9 @@ def main():
     dump = sys.argv[sys.argv.index("--dump") + 1] if "--dump" in sys.argv else None
     if dump:
         os.makedirs(dump, exist_ok=True)
-    jit.compile_code = lambda src, name: b""  # generate only
+    spills = "--spills" in sys.argv  # compile (hipRTC, no GPU) and report kernels that use scratch
+    if not spills:
+        jit.compile_code = lambda src, name: b""  # generate only
     jit.compile_source = lambda src, name: -1
     DE.native.narrow4 = lambda: 1
 
@@ -69,6 +74,11 @@ def main():
                     h1 = hashlib.sha1(js.src.encode()).hexdigest()[:12]
                     h2 = hashlib.sha1(sp.src.encode()).hexdigest()[:12]
                     print(f"{label}/{name}#{i}.{j}: {gp.mode} U={js.U} lds={js.lay.total} {h1} {h2}")
+                    for k in (js, sp) if spills else ():
+                        if k.spills:
+                            print(f"   SPILLS ({'literal' if k is sp else 'shape'}): "
+                                  + " ".join(f"{x}={k.meta.get(x)}" for x in (".vgpr_count", ".vgpr_spill_count",
+                                                                             ".private_segment_fixed_size")))
                     if dump:
                         tag = f"{label}_{name}_{i}_{j}".replace(" ", "_").replace("/", "_").replace(",", "")
                         for suffix, src in (("shape", js.src), ("lit", sp.src)):
