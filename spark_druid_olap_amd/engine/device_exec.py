@@ -247,10 +247,15 @@ class PreparedScan:
         slot = current_slot()
         b = self._slots.get(slot)
         if b is None:
+            # allocated without holding this scan's lock: an out-of-memory eviction takes the locks
+            # of the scans it evicts, and two threads each holding their own scan's lock while
+            # evicting the other's would deadlock (one slot runs one statement at a time, so two
+            # allocations for one (scan, slot) do not race in practice; the re-check keeps one)
+            nb = _with_eviction(lambda: self._alloc(self.cap), self, slot)
             with self._slot_lock:
                 b = self._slots.get(slot)
                 if b is None:
-                    b = self._slots[slot] = _with_eviction(lambda: self._alloc(self.cap), self, slot)
+                    b = self._slots[slot] = nb
             _buffers_acquired(self, slot, b)
         else:
             _buffers_used(self, slot)

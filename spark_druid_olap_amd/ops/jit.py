@@ -915,18 +915,41 @@ def _code_key(src: str) -> str:
     return hashlib.sha256((src + "\0".join(OPTS) + _hdr_hash()).encode()).hexdigest()[:24]
 
 
+_code_inflight: Dict[str, "Future"] = {}
+
+
 def compile_code(src: str, name: str) -> bytes:
-    """hipRTC-compile for gfx950 (no GPU needed), disk-cached by source + header hash."""
+    """hipRTC-compile for gfx950 (no GPU needed), disk-cached by source + header hash.  Concurrent
+    requests for one source wait on the first one's compile (one hipRTC run, one cache write)."""
+    from concurrent.futures import Future
+
     from . import native
 
     key = _code_key(src)
     path = cache_dir() / f"{key}.co"
     if path.exists():
         return path.read_bytes()
-    code = native.load().rtc_compile(src, name, OPTS)
-    tmp = path.with_suffix(f".tmp{os.getpid()}")
-    tmp.write_bytes(code)
-    os.replace(tmp, path)
+    with _lock:
+        fut = _code_inflight.get(key)
+        owner = fut is None
+        if owner:
+            fut = _code_inflight[key] = Future()
+    if not owner:
+        return fut.result()
+    try:
+        code = native.load().rtc_compile(src, name, OPTS)
+        # (unique per process and thread: other processes may share the cache directory)
+        tmp = path.with_suffix(f".tmp{os.getpid()}.{threading.get_ident()}")
+        tmp.write_bytes(code)
+        os.replace(tmp, path)
+    except BaseException as e:
+        with _lock:
+            _code_inflight.pop(key, None)
+        fut.set_exception(e)
+        raise
+    with _lock:
+        _code_inflight.pop(key, None)
+    fut.set_result(code)
     return code
 
 

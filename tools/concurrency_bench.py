@@ -273,8 +273,11 @@ def main():
             warm += qs[len(warm):max(len(warm), a.prewarm)]
         else:
             warm = qs if a.workload == "fixed" else qs[:max(len(qs) and 8, a.prewarm)]
-        for _, sql in warm:
+        for i, (name, sql) in enumerate(warm):
+            tw = time.time()
             c.cursor().execute(sql).fetchall()
+            # (progress on stderr: a long warm-up -- first-seen shapes compile -- stays visibly alive)
+            print(f"[conc] warm {i + 1}/{len(warm)} {name[:40]} {time.time() - tw:.2f}s", file=sys.stderr, flush=True)
     interval = (a.clients / a.qps) if a.qps > 0 else 0.0
     t_start = time.time() + 1.0 + a.warmup
     for _ in ps:
@@ -297,7 +300,10 @@ def main():
         from spark_druid_olap_amd.utils.sampler import Sampler
 
         sampler = Sampler().start()
-    time.sleep(a.duration)
+    t_end = time.time() + a.duration
+    while time.time() < t_end:
+        time.sleep(min(15.0, max(0.0, t_end - time.time())))
+        print(f"[conc] measuring, {max(0.0, t_end - time.time()):.0f}s left", file=sys.stderr, flush=True)
     if sampler is not None:
         sampler.stop()
         with open(a.sample, "w") as f:
@@ -306,8 +312,14 @@ def main():
     co1, ex1 = counters()
     ncost = len(exec_cost)
     res = []
-    for _ in ps:
+    import faulthandler
+
+    # a client that never gets its answer: every server thread's stack, every 60 s, to stderr
+    faulthandler.dump_traceback_later(60, repeat=True, file=sys.stderr)
+    for i, _ in enumerate(ps):
         res.extend(res_q.get())
+        print(f"[conc] client process {i + 1}/{len(ps)} done", file=sys.stderr, flush=True)
+    faulthandler.cancel_dump_traceback_later()
     for p in ps:
         p.join()
     srv.stop()
