@@ -59,6 +59,7 @@ for step in "$@"; do
       else
         python tools/prof_summary.py gpurun_out/prof > gpurun_out/prof/summary.txt
       fi
+      find gpurun_out/prof -name "*.db" -delete  # (summaries only: gpurun returns at most 64 MiB)
       head -50 gpurun_out/prof/summary.txt ;;
     conc)
       tag=${TAG:-${WORKLOAD:-fixed}}
@@ -102,6 +103,7 @@ for step in "$@"; do
       else
         python tools/prof_summary.py gpurun_out/pyprof_$b > gpurun_out/pyprof_$b/summary.txt
       fi
+      find gpurun_out/pyprof_$b -name "*.db" -delete
       head -40 gpurun_out/pyprof_$b/summary.txt ;;
     *)
       echo "[gpu.sh] unknown step $step"; exit 2 ;;
