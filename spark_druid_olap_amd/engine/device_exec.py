@@ -25,7 +25,7 @@ from ..ops import desc as D
 from ..ops import native
 from .lower import ScanProgram, pack
 from .partials import Partials
-from .scheduler import current_slot
+from .scheduler import current_slot, pinned
 
 from ..planner.cost import PLAN_LDS_BUDGET as LDS_BUDGET  # noqa: E402  (single source: the cost model)
 # one accumulator table per workgroup (JIT only) for key spaces whose per-wave copies do not fit:
@@ -251,12 +251,16 @@ class PreparedScan:
             # of the scans it evicts, and two threads each holding their own scan's lock while
             # evicting the other's would deadlock (one slot runs one statement at a time, so two
             # allocations for one (scan, slot) do not race in practice; the re-check keeps one)
-            nb = _with_eviction(lambda: self._alloc(self.cap), self, slot)
+            # another prepared scan's idle buffers of the same geometry on this slot (another
+            # parameterization of one dashboard statement) are taken over instead of allocating
+            victim = _steal(self, slot, self._geom(self.cap))
+            nb = _with_eviction(lambda: self._alloc(self.cap, victim), self, slot)
             with self._slot_lock:
                 b = self._slots.get(slot)
                 if b is None:
                     b = self._slots[slot] = nb
             _buffers_acquired(self, slot, b)
+            _geom_register(self, slot, b.geom)
         else:
             _buffers_used(self, slot)
         return b
@@ -271,35 +275,56 @@ class PreparedScan:
             if total > 160 * 1024:
                 self.mode, self.lds, self.hll_lds = D.M_DENSE_GLOBAL, 0, 0
 
-    def _alloc(self, cap: int) -> "_Bufs":
+    def _rows(self, cap: int) -> int:
+        if self.mode == D.M_PART and self.part is not None and self.part.get("hashed"):
+            return 1  # (sparse output: no group table)
+        return cap if self.mode == D.M_HASH else self.prog.G
+
+    def _geom(self, cap: int) -> tuple:
+        """What a slot's device tensors look like (shapes and dtypes): prepared scans with equal
+        geometry can hand each other their buffers."""
+        prog = self.prog
+        nblocks = prog.nhll_total if self.stored_fused else prog.nhll
+        return (str(self.dev), self.mode, self._rows(cap), prog.nslots, nblocks, self.m, bool(self.hll32),
+                bool(self.touch), bool(self.pres_bytes))
+
+    def _alloc(self, cap: int, reuse: Optional["_Bufs"] = None) -> "_Bufs":
+        """This slot's buffers -- the large tensors taken over from ``reuse`` (another prepared
+        scan's buffers of the same geometry, whose state is then unknown: the first run resets
+        them) -- with this scan's own descriptor and launch arguments."""
         from .lower import lds_layout
 
         prog, dev = self.prog, self.dev
         b = _Bufs()
         b.cap = cap
-        rows = cap if self.mode == D.M_HASH else prog.G
-        if self.mode == D.M_PART and self.part is not None and self.part.get("hashed"):
-            rows = 1  # (sparse output: no group table)
+        rows = self._rows(cap)
         b.rows = rows
+        b.geom = self._geom(cap)
         b.init_row = _init_row(dev, tuple(int(init) for _, init in prog.slots))
-        if self.pres_bytes:
-            # padded to whole 8-byte words (the fused reset zeroes words; padding bytes stay 0 and
-            # never compact)
-            b.acc = torch.empty(((rows + 7) // 8 * 8,), dtype=torch.uint8, device=dev)
-        else:
-            b.acc = torch.empty((rows, prog.nslots), dtype=torch.int64, device=dev)
-        b.keys = torch.empty(rows if self.mode == D.M_HASH else 1, dtype=torch.int64, device=dev)
-        # byte registers (sdo_device.h hll_update8 / hll_merge_word8): the partials, the wire and the
-        # estimator all read u8
         nblocks = prog.nhll_total if self.stored_fused else prog.nhll
-        b.hll = [torch.empty(rows * self.m, dtype=torch.uint8, device=dev) for _ in range(nblocks)]
-        # scan-time u32 registers (narrowed into b.hll after each run) or none: the kernel updates
-        # b.hll's bytes directly
-        b.hll32 = [torch.empty(rows * self.m, dtype=torch.int32, device=dev) for _ in range(nblocks)] \
-            if self.hll32 else []
-        b.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
-        # (padded to whole 64-group words: native.touch_compact reads it 16 bytes per lane)
-        b.touch = torch.zeros(((rows + 63) // 64 * 64) if self.touch else 64, dtype=torch.uint8, device=dev)
+        if reuse is not None and getattr(reuse, "geom", None) == b.geom:
+            b.acc, b.keys, b.hll, b.hll32 = reuse.acc, reuse.keys, reuse.hll, reuse.hll32
+            b.overflow, b.touch = reuse.overflow, reuse.touch
+            if self.touch:
+                b.touch.zero_()  # (the first-touch invariant: every byte clear between runs)
+        else:
+            if self.pres_bytes:
+                # padded to whole 8-byte words (the fused reset zeroes words; padding bytes stay 0
+                # and never compact)
+                b.acc = torch.empty(((rows + 7) // 8 * 8,), dtype=torch.uint8, device=dev)
+            else:
+                b.acc = torch.empty((rows, prog.nslots), dtype=torch.int64, device=dev)
+            b.keys = torch.empty(rows if self.mode == D.M_HASH else 1, dtype=torch.int64, device=dev)
+            # byte registers (sdo_device.h hll_update8 / hll_merge_word8): the partials, the wire and
+            # the estimator all read u8
+            b.hll = [torch.empty(rows * self.m, dtype=torch.uint8, device=dev) for _ in range(nblocks)]
+            # scan-time u32 registers (narrowed into b.hll after each run) or none: the kernel
+            # updates b.hll's bytes directly
+            b.hll32 = [torch.empty(rows * self.m, dtype=torch.int32, device=dev) for _ in range(nblocks)] \
+                if self.hll32 else []
+            b.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
+            # (padded to whole 64-group words: native.touch_compact reads it 16 bytes per lane)
+            b.touch = torch.zeros(((rows + 63) // 64 * 64) if self.touch else 64, dtype=torch.uint8, device=dev)
         b.clean = False
         hll_offs = []
         off = prog.G * prog.nslots * 8 * (BLOCK // 64)
@@ -555,6 +580,7 @@ class PreparedScan:
 
     # ------------------------------------------------------------------ run
     def run(self) -> Partials:
+        pinned().add(id(self))  # (its buffers hold this statement's partials: not to be taken over)
         self._maybe_specialize()
         prog = self.prog
         b = self._bufs()
@@ -768,7 +794,53 @@ def _forget_prep(pid: int) -> None:
 class _Bufs:
     """One execution slot's device buffers for a prepared scan."""
     __slots__ = ("cap", "rows", "init_row", "acc", "keys", "hll", "hll32", "overflow", "desc", "touch", "clean",
-                 "run_args", "noreset_args", "part", "__weakref__")
+                 "run_args", "noreset_args", "part", "geom", "__weakref__")
+
+
+# Buffer hand-over between prepared scans of equal geometry (_Bufs.geom) on one execution slot.
+# A BI dashboard sends one statement shape with many parameterizations; each is its own prepared
+# scan, and without hand-over each would hold its own copy of (say) a 150M-group table per slot.
+# A scan's buffers may be taken only while no statement of this thread can still read them: scans
+# run by the thread's current statement are pinned (``_pin`` in run(), released with the slot
+# lease: engine/scheduler.py pinned) -- a slot runs one statement at a time, so other threads never hold
+# this slot's buffers.
+_GEOM: dict = {}      # (slot, geom) -> {id(prep): weakref(prep)}
+_geom_lock = threading.Lock()
+
+
+def _geom_register(prep, slot, geom) -> None:
+    with _geom_lock:
+        _GEOM.setdefault((slot, geom), {})[id(prep)] = weakref.ref(prep)
+
+
+def _steal(prep, slot, geom) -> Optional["_Bufs"]:
+    """Another (unpinned) prepared scan's buffers of geometry ``geom`` on ``slot``, removed from
+    it; None when there are none."""
+    pins = pinned()
+    with _geom_lock:
+        holders = _GEOM.get((slot, geom))
+        if not holders:
+            return None
+        cands = [(pid, ref) for pid, ref in list(holders.items()) if pid != id(prep) and pid not in pins]
+    for pid, ref in cands:
+        p = ref()
+        if p is None:
+            with _geom_lock:
+                holders.pop(pid, None)
+            continue
+        with p._slot_lock:
+            b = p._slots.get(slot)
+            if b is None or getattr(b, "geom", None) != geom:
+                continue
+            p._slots.pop(slot)
+        with _geom_lock:
+            holders.pop(pid, None)
+        with _buf_lock:
+            old = _buf_lru.pop((pid, slot), None)
+            if old is not None:
+                _buf_total[0] -= old[1]
+        return b
+    return None
 
 
 class PreparedEmit:

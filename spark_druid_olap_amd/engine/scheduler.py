@@ -39,6 +39,15 @@ def current_slot() -> int:
     return getattr(_ctx, "slot", 0)
 
 
+def pinned() -> set:
+    """Prepared scans (ids) whose slot buffers this thread's current statement may still read
+    (engine/device_exec.py: they are not handed over to another scan)."""
+    s = getattr(_ctx, "pins", None)
+    if s is None:
+        s = _ctx.pins = set()
+    return s
+
+
 @contextlib.contextmanager
 def use_slot(slot: int):
     prev = getattr(_ctx, "slot", 0)
@@ -47,6 +56,7 @@ def use_slot(slot: int):
         yield slot
     finally:
         _ctx.slot = prev
+        pinned().clear()  # the statement on this slot is done with its scans' buffers
 
 
 class StreamScheduler:
