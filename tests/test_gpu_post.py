@@ -186,3 +186,25 @@ def test_headline_queries_match_pandas(sess, df):
     sub = d[(d.c_region == "AMERICA") & (d.p_type == "ECONOMY ANODIZED STEEL") & (d.o_orderdate >= "1995-01-01")
             & (d.o_orderdate <= "1996-12-31")]
     check("TPCH Q8", sub.assign(y=sub.o_orderdate.str[:4]), ["y"], dict(s=("l_extendedprice", "sum")))
+
+
+def test_device_lexsort_equals_numpy():
+    """sql/execute.py sort_indices on the GPU (large host sorts: ORDER BY, window partitions) is
+    np.lexsort exactly -- ties keep row order, nulls and DESC folded as on the host."""
+    from spark_druid_olap_amd.sql import execute as X
+
+    rng = np.random.default_rng(5)
+    n = 200_003
+    lex = [rng.integers(0, 50, n), rng.normal(size=n).round(2), rng.integers(0, 7, n).astype(np.int64),
+           rng.random(n) < 0.1]
+    assert np.array_equal(X._lexsort_device(lex), np.lexsort(lex))
+    s = pd.Series(rng.integers(0, 100, n).astype(float))
+    s[rng.random(n) < 0.05] = np.nan
+    keys = [(pd.Series(rng.integers(0, 9, n)), True, None), (s, False, None)]
+    dev = X.sort_indices(keys, n)
+    X.GPU_SORT_MIN_ROWS, old = 1 << 40, X.GPU_SORT_MIN_ROWS
+    try:
+        host = X.sort_indices(keys, n)
+    finally:
+        X.GPU_SORT_MIN_ROWS = old
+    assert np.array_equal(dev, host)

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--bind", default="years")
     ap.add_argument("--profile", default=None, help="cProfile this template's first binding (plan + run)")
     ap.add_argument("--only", default=None)
+    ap.add_argument("--profile-repeat", default=None, help="cProfile the repeat runs of this template's last binding")
     a = ap.parse_args()
     import torch
 
@@ -69,11 +70,24 @@ def main():
 
                 pstats.Stats(prof, stream=sys.stdout).sort_stats("cumulative").print_stats(45)
             reps = []
+            rprof = None
+            if a.profile_repeat and a.profile_repeat.lower() in t["name"].lower() and k == a.iters - 1:
+                import cProfile
+
+                rprof = cProfile.Profile()
+                rprof.enable()
             for _ in range(3):
                 t5 = time.perf_counter()
                 df.run()
                 sync()
                 reps.append((time.perf_counter() - t5) * 1e3)
+            if rprof is not None:
+                rprof.disable()
+                import pstats
+
+                print(f"== repeat runs of {t['name']} (b{k}), cumulative", flush=True)
+                pstats.Stats(rprof, stream=sys.stdout).sort_stats("cumulative").print_stats(40)
+                pstats.Stats(rprof, stream=sys.stdout).sort_stats("tottime").print_stats(25)
             rows.append((t["name"], k, (t2 - t1) * 1e3, (t3 - t2) * 1e3, (t4 - t3) * 1e3, statistics.median(reps), r.n,
                          len(df.druid_queries())))
             print(f"{t['name'][:44]:44s} b{k} plan {rows[-1][2]:8.1f} prep {rows[-1][3]:8.1f} first {rows[-1][4]:8.1f} "
