@@ -732,13 +732,15 @@ def _buffers_acquired(prep, slot, b) -> None:
     key = (id(prep), slot)
     nb = _bufs_nbytes(b)
     victims = []
+    budget = _budget()  # (outside the lock: it allocates)
     with _buf_lock:
+        _settle_forgotten()
         old = _buf_lru.pop(key, None)
         if old is not None:
             _buf_total[0] -= old[1]
         _buf_lru[key] = (weakref.ref(prep), nb)
         _buf_total[0] += nb
-        while _buf_total[0] > _budget() and len(_buf_lru) > 1:
+        while _buf_total[0] > budget and len(_buf_lru) > 1:
             k, (ref, n) = next(iter(_buf_lru.items()))
             if k == key:
                 break
@@ -784,9 +786,20 @@ def _buffers_used(prep, slot) -> None:
             _buf_lru.move_to_end(key)
 
 
+_forgotten: list = []  # ids of collected prepared scans, settled under _buf_lock by the next user
+
+
 def _forget_prep(pid: int) -> None:
-    """A prepared scan was collected: its buffers went with it."""
-    with _buf_lock:
+    """A prepared scan was collected: its buffers went with it.  (A finalizer: it may run inside
+    any allocation -- including one made while this thread holds ``_buf_lock`` -- so it only
+    records the id; ``_settle_forgotten`` drops the accounting under the lock.)"""
+    _forgotten.append(pid)
+
+
+def _settle_forgotten() -> None:
+    """(caller holds _buf_lock)"""
+    while _forgotten:
+        pid = _forgotten.pop()
         for k in [k for k in _buf_lru if k[0] == pid]:
             _buf_total[0] -= _buf_lru.pop(k)[1]
 
