@@ -37,6 +37,7 @@ BLOCKS_PER_CU = int(os.environ.get("SDO_BLOCKS_PER_CU", "3"))
 USE_JIT = os.environ.get("SDO_JIT", "1") != "0"
 JIT_BLOCKS = int(os.environ.get("SDO_JIT_BLOCKS", "3"))  # target resident workgroups per CU
 JIT_STAGE = os.environ.get("SDO_JIT_STAGE", "auto")       # auto | reg (VGPR loads) | lds (LDS-DMA planes)
+FORCE_U = 0  # cap the words per step of generated kernels (0: the register / LDS-driven choice)
 # Literal specialization of repeated statements (ops/jit.py JitScan.specialized): a prepared scan's
 # first runs use the shape's shared kernel (query constants read from the descriptor: every
 # parameterization of a dashboard query shares one code object); from its SPECIALIZE_AFTER-th run
@@ -107,6 +108,8 @@ def _jit_build(prog, mode: int, hll_lds: bool, m: int, shared: bool = False, loa
 
     nplanes = sum(2 if column_tensor_size(prog, c) == 8 else 1 for c in prog.cols)
     prefs = [16, 8, 4, 2] if nplanes <= 3 else ([8, 4, 2] if nplanes <= 8 else [4, 2])
+    if FORCE_U:  # (tools/query_probe.py A/B of the word unroll)
+        prefs = [u for u in prefs if u <= FORCE_U] or [prefs[-1]]
     # occupancy first: the scan is latency-bound at 8 waves/CU, so prefer the largest U that still
     # leaves room for JIT_BLOCKS workgroups per CU (160 KiB LDS), then fall back to one workgroup
     budgets = [(160 * 1024) // b - 512 for b in (JIT_BLOCKS, 1) if b >= 1]

@@ -2,8 +2,8 @@
 
   python tools/query_probe.py SF [variant ...] [-- query names]
 
-A variant is ``base[b<workgroups per CU>][c<accumulator copies per wave>][slds|sreg][creg0]``: target
-workgroups per CU, accumulator copies, forced LDS-DMA / VGPR staging, count-only scans through LDS
+A variant is ``base[b<workgroups per CU>][c<accumulator copies per wave>][u<max words per step>][slds|sreg][creg0]``:
+target workgroups per CU, accumulator copies, word unroll cap, forced LDS-DMA / VGPR staging, count-only scans through LDS
 atomics instead of register counters (see ops/jit.py); results of every variant are checked against
 the first one.  Used to locate slow or hung kernels
 and to A/B kernel-generation choices on the GPU box."""
@@ -86,6 +86,8 @@ def main():
         DE.JIT_STAGE = "lds" if "slds" in var else ("reg" if "sreg" in var else "auto")
         DE.BLOCKS_PER_CU = max(3, DE.JIT_BLOCKS)
         J.COUNT_REGS = "creg0" not in var
+        mu = re.search(r"u(\d+)", var)
+        DE.FORCE_U = int(mu.group(1)) if mu else 0
         print(f"== {var}", flush=True)
         for name, qs in specs:
             if only and name not in only:
