@@ -172,6 +172,9 @@ DENSE_WORDS = int(os.environ.get("SDO_JIT_DENSE_WORDS", "48"))
 # wave-reduced once into the accumulator table at the end.
 COUNT_REGS = True
 COUNT_REGS_MAX_G = 8
+# probe-only (tools/query_probe.py "sink"): dense-LDS slot updates fold into a register instead of
+# the LDS table -- wrong results, used to price the LDS atomics of a scan
+SINK_UPDATES = False
 
 
 def count_regs(prog, mode: int) -> bool:
@@ -708,6 +711,9 @@ class _Gen:
                 if creg:  # packed 8-bit register counters (COUNT_REGS)
                     body.append(f"        pc{s} += (uint64_t)({cond}) << ((uint32_t)key << 3);")
                     continue
+                if mode == D.M_DENSE_LDS and SINK_UPDATES:
+                    body.append(f"        sink_ ^= ({cond}) ? (uint64_t)({val}) + (uint64_t)slot : 0ull;")
+                    continue
                 if mode == D.M_DENSE_LDS:
                     tgt = f"acc + (slot * {NS} + {s}) * {NCT} + copy"
                 else:
@@ -894,6 +900,10 @@ class _Gen:
                     out.append(f"    for (int i = threadIdx.x; i < {G * self.m // 4}; i += {W * 64}) "
                                "hll_merge_word8(g + i, r[i]);")
                     out.append("  }")
+        if SINK_UPDATES:
+            out.insert(out.index("  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);") + 1,
+                       "  uint64_t sink_ = 0;")
+            out.append("  if (sink_ == 0x123456789abcdefull) ((uint64_t*)d->out_acc)[0] = sink_;")
         out.append("}")
         return "\n".join(out) + "\n"
 
@@ -1031,6 +1041,9 @@ def kernel_meta(code: bytes) -> dict:
     return {}
 
 
+SGPR_SPILL_MAX = 128
+
+
 class JitSpill(RuntimeError):
     """The kernel would spill registers to scratch (engine/device_exec.py _jit_build then tries a
     smaller unroll): a spilling scan is slow, and its scratch is allocated by the HIP runtime outside
@@ -1054,9 +1067,14 @@ class JitScan:
         self.name = f"sdo_jit_{tag}"
         self.src = g.source(self.name)
         self.meta = kernel_meta(compile_code(self.src, self.name) or b"")
-        self.spills = bool(self.meta.get(".private_segment_fixed_size") or self.meta.get(".vgpr_spill_count"))
+        # SGPR spills go to VGPR lanes (no scratch), but a few hundred of them turn the word loop into
+        # writelane / readlane traffic: an unrolled count over one key spilled 1435 SGPRs at U=16,
+        # 185 VALU per word instead of 13 at U=8 (profiles/r4/scan_kernel_ab_notes.md)
+        self.spills = bool(self.meta.get(".private_segment_fixed_size") or self.meta.get(".vgpr_spill_count")
+                           or int(self.meta.get(".sgpr_spill_count") or 0) > SGPR_SPILL_MAX)
         if self.spills and reject_spills:
-            raise JitSpill(f"{self.name} U={U}: {self.meta.get('.vgpr_spill_count')} VGPR spills, "
+            raise JitSpill(f"{self.name} U={U}: {self.meta.get('.vgpr_spill_count')} VGPR / "
+                           f"{self.meta.get('.sgpr_spill_count')} SGPR spills, "
                            f"{self.meta.get('.private_segment_fixed_size')} B scratch")
         self.handle = compile_source(self.src, self.name) if load else -1
         self.U = U
@@ -1066,8 +1084,11 @@ class JitScan:
         statement's own code object: folded bounds, no descriptor loads, fewer live scalars --
         TPC-H Q19 3.4 vs 3.8 ms).  Same layout, grid and descriptor, so it swaps in place."""
         prog, mode, U, hll_lds, m, narrow4, load, budget, regstage, shared = self._args
-        return JitScan(prog, mode, U, hll_lds, m, narrow4, load, budget=budget, regstage=regstage,
-                       shared=shared, literals=True)
+        js = JitScan(prog, mode, U, hll_lds, m, narrow4, load, budget=budget, regstage=regstage,
+                     shared=shared, literals=True)
+        # literals can free or cost registers; a specialization that spills where the shape kernel
+        # does not would be slower than the kernel it replaces
+        return self if js.spills and not self.spills else js
 
     def occupancy(self) -> int:
         """Resident 512-thread workgroups per CU of the compiled kernel (registers and LDS)."""

@@ -14,6 +14,7 @@
 #   pmc                PMC counter passes over tools/kbench_one.py (Q, SF); one pass per counter group
 #   py:SCRIPT          python SCRIPT $PY_ARGS (a tool under tools/)
 #   pyprof:SCRIPT      the same under rocprofv3 --kernel-trace --stats -> gpurun_out/pyprof_<name>/summary.txt
+#                      (PYPROF_ARGS: extra tools/rocpd_summary.py options, e.g. --tail-ms 40 --timeline-ms 20)
 #
 # Outputs land in gpurun_out/<step>.* ; the tail of each is echoed.
 set -o pipefail
@@ -99,7 +100,7 @@ for step in "$@"; do
         || fail "$step" $? gpurun_out/pyprof_$b.log
       DB=$(find gpurun_out/pyprof_$b -name "*.db" | head -1)
       if [ -n "$DB" ]; then
-        python tools/rocpd_summary.py "$DB" --top 30 > gpurun_out/pyprof_$b/summary.txt
+        python tools/rocpd_summary.py "$DB" --top 30 ${PYPROF_ARGS:-} > gpurun_out/pyprof_$b/summary.txt
       else
         python tools/prof_summary.py gpurun_out/pyprof_$b > gpurun_out/pyprof_$b/summary.txt
       fi

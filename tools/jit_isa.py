@@ -133,11 +133,15 @@ def main():
     sess.register_datasource(ds)
     sess.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)
     sess.sql(tpch.druid_ddl(source="orderLineItemPartSupplierBase", datasource="tpch", with_column_mapping=False))
-    for name, q in tpch.BENCH_QUERIES:
-        if want and not any(w.lower() in name.lower() for w in want):
-            continue
-        for dq in sess.sql(q).druid_queries():
-            pq = sess.engine.prepare(dq.spec, ds)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from query_probe import extra_specs
+
+    todo = [(n, [dq.spec for dq in sess.sql(q).druid_queries()]) for n, q in tpch.BENCH_QUERIES
+            if not want or any(w.lower() in n.lower() for w in want)]
+    todo += [(n, [qs]) for n, qs in extra_specs() if n in want]  # (tools/query_probe.py x:* isolation specs)
+    for name, qspecs in todo:
+        for spec in qspecs:
+            pq = sess.engine.prepare(spec, ds)
             for _, prog, _ in pq.scans:
                 gp = plan_groupby(prog, True, True)
                 mode = {"dense-lds": D.M_DENSE_LDS, "dense-global": D.M_DENSE_GLOBAL, "hash": D.M_HASH,
@@ -158,6 +162,8 @@ def main():
                 print(f"#### {name}: G={prog.G} plan={gp.describe()}")
                 kernels = [js] if "--shape" in sys.argv else [js.specialized()]
                 for k in kernels:
+                    if "--src" in sys.argv:
+                        print(k.src)
                     report(name, k, jit.compile_code(k.src, k.name), dump)
 
 

@@ -43,7 +43,13 @@ def extra_specs():
             ("x:no-hll", S.GroupByQuerySpec("tpch", dims, aggregations=aggs[:5], intervals=BQ.ALL)),
             ("x:hll-only", S.GroupByQuerySpec("tpch", dims, aggregations=aggs[5:], intervals=BQ.ALL)),
             ("x:sum-ext", S.GroupByQuerySpec("tpch", dims, aggregations=aggs[1:2], intervals=BQ.ALL)),
-            ("x:nodims-count", S.GroupByQuerySpec("tpch", [], aggregations=aggs[:1], intervals=BQ.ALL))]
+            ("x:nodims-count", S.GroupByQuerySpec("tpch", [], aggregations=aggs[:1], intervals=BQ.ALL)),
+            ("x:nodims-sum-ext", S.GroupByQuerySpec("tpch", [], aggregations=aggs[1:2], intervals=BQ.ALL)),
+            ("x:nodims-no-hll", S.GroupByQuerySpec("tpch", [], aggregations=aggs[:5], intervals=BQ.ALL)),
+            ("x:count-1key", S.GroupByQuerySpec("tpch", BQ._dims("l_linestatus"), aggregations=aggs[:1],
+                                                intervals=BQ.ALL)),
+            ("x:count-2key-1", S.GroupByQuerySpec("tpch", BQ._dims("l_returnflag"), aggregations=aggs[:1],
+                                                  intervals=BQ.ALL))]
 
 
 def main():
@@ -86,11 +92,12 @@ def main():
         DE.JIT_STAGE = "lds" if "slds" in var else ("reg" if "sreg" in var else "auto")
         DE.BLOCKS_PER_CU = max(3, DE.JIT_BLOCKS)
         J.COUNT_REGS = "creg0" not in var
+        J.SINK_UPDATES = "sink" in var  # (slot updates priced by dropping them: results differ)
         mu = re.search(r"u(\d+)", var)
         DE.FORCE_U = int(mu.group(1)) if mu else 0
         print(f"== {var}", flush=True)
         for name, qs in specs:
-            if only and name not in only:
+            if only and name not in only and name.replace(" ", "_") not in only:  # (TPCH_Q1 for "TPCH Q1")
                 continue
             t = time.time()
             pq = eng.prepare(qs, ds)
