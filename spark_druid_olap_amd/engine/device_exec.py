@@ -72,13 +72,25 @@ def _spec_job(js):
             _spec_pending[0] -= 1
 
 
-def _attach_packed(prog) -> None:
+PACKED_MODES = (D.M_DENSE_LDS, D.M_DENSE_GLOBAL, D.M_HASH)
+# the packed layout pays off on whole-chunk walks; a selective scan mostly walks single nonzero
+# words (two stream loads per packed column and word vs one plain load): TPC-H Q5 (2.5% of rows)
+# 0.25 -> 0.18 ms packed, Q7 (0.3%) 0.37 -> 0.50 ms (profiles/r4/scan_kernel_ab_notes.md)
+PACK_MIN_SELECTIVITY = 0.02
+
+
+def _attach_packed(prog, mode: int) -> None:
     """Bit-packed copies (segment/packed.py) of the integer columns the program reads: the JIT
-    kernel reads those instead of the byte-wide columns (the interpreter never does)."""
+    kernel reads those instead of the byte-wide columns (the interpreter never does).  Only the
+    table-aggregating modes walk whole chunks in the static runs the layout is built for; the
+    partition / emit producers keep the plain columns."""
     from ..segment import packed as PK
 
     prog.packed = {}
-    if not PK.ENABLED or prog.empty or prog.ds.device.type != "cuda":
+    if not PK.ENABLED or prog.empty or prog.ds.device.type != "cuda" or mode not in PACKED_MODES:
+        return
+    n = max(1, int(prog.ds.num_rows))
+    if float(getattr(prog, "est_rows", n)) < PACK_MIN_SELECTIVITY * n:
         return
     for name in list(prog.fcols) + list(prog.pcols):
         pc = PK.packed_column(prog.ds, name)
@@ -94,7 +106,7 @@ def _jit_for(prog, mode: int, hll_lds: bool, m: int, shared: bool = False):
     from ..ops import jit
 
     if getattr(prog, "packed", None) is None:
-        _attach_packed(prog)
+        _attach_packed(prog, mode)
     js = _jit_build(prog, mode, hll_lds, m, shared)
     if js is None:
         prog.packed = {}  # the interpreter reads the plain columns

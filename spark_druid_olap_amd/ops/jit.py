@@ -164,6 +164,7 @@ FULL_CHUNKS = os.environ.get("SDO_JIT_FULL", "1") != "0"
 # reading each word's mask by lane index (independent readlanes) and skipping all-empty steps;
 # sparser chunks take the find-first-set chain over their non-empty words only (0: always chain)
 DENSE_WORDS = int(os.environ.get("SDO_JIT_DENSE_WORDS", "48"))
+DENSE_WORDS_PACKED = 16  # (the same switch for kernels reading lane-interleaved packed columns)
 # Count-only scans of tiny dense key spaces (TPC-H "Ship Date Range": count(*) by l_returnflag,
 # l_linestatus over 150M rows) count in registers: per slot one 64-bit word of eight 8-bit fields,
 # ``pc += (uint64)mine << (key * 8)`` per row (no LDS atomic -- every lane of a wave would otherwise
@@ -175,6 +176,7 @@ COUNT_REGS_MAX_G = 8
 # probe-only (tools/query_probe.py "sink"): dense-LDS slot updates fold into a register instead of
 # the LDS table -- wrong results, used to price the LDS atomics of a scan
 SINK_UPDATES = False
+STATIC_RUNS = True  # whole-chunk word runs with compile-time packed-field offsets (A/B switch)
 
 
 def count_regs(prog, mode: int) -> bool:
@@ -270,7 +272,7 @@ class _Gen:
     def ival(self, idx: int) -> str:
         c = self.cols[idx]
         if c.pw:
-            return f"(pk_field<{c.pw}>(xp{idx}[u], psh{c.pw}) + {_lit(c.pbase)})"
+            return f"(pk_field<{c.pw}>(xp{idx}[u], pks{idx}[u]) + {_lit(c.pbase)})"
         if self.regstage:
             return f"cv_int<{c.lg}, {'true' if c.sgn else 'false'}, {'true' if c.flt else 'false'}>(x{idx}[u])"
         return (f"ld_int<{c.lg}, {'true' if c.sgn else 'false'}, {'true' if c.flt else 'false'}, {self.n4}>"
@@ -432,20 +434,41 @@ class _Gen:
                     st.append(f"{'fmin' if op == D.E_MIN else 'fmax'}({x}, {y})")
         return st[-1]
 
-    def stage_words(self, o: List[str], cols, wl: str, dst: str, ind: str = "      ") -> None:
+    def stage_words(self, o: List[str], cols, wl: str, dst: str, ind: str = "      ",
+                    j0: Optional[int] = None) -> None:
         """Load the given columns of U whole 64-row words through the per-chunk buffer resources
         (``rs<i>``) -- into VGPR arrays ``x<i>[u]`` (register staging) or LDS planes (DMA);
-        ``wl`` names the per-u word-in-chunk array."""
+        ``wl`` names the per-u word-in-chunk array.  Bit-packed columns (segment/packed.py
+        lane-interleaved streams) land as a 64-bit window ``xp<i>[u]`` + field shift ``pks<i>[u]``:
+        for words ``g_ * 32 + j0 + u`` (``j0`` static) as the ``U W / 32`` (+1) coalesced stream
+        dwords of the run with compile-time field offsets, else two dword loads per word."""
         U, NP = self.U, self.NP
         pk = [i for i in cols if self.cols[i].pw]
         cols = [i for i in cols if not self.cols[i].pw]
-        if pk:  # bit-packed columns: straight into registers in either staging mode
-            for i in pk:
-                o.append(f"{ind}uint64_t xp{i}[{U}];")
+        for i in pk:  # bit-packed columns: straight into registers in either staging mode
+            W = self.cols[i].pw
+            o.append(f"{ind}uint64_t xp{i}[{U}]; uint32_t pks{i}[{U}];")
+            if j0 is None:
+                o.append(f"#pragma unroll\n{ind}for (int u = 0; u < {U}; ++u) {{")
+                o.append(f"{ind}  const uint32_t b_ = ((uint32_t){wl}[u] & 31u) * {W}u;")
+                soff = f"((uint32_t){wl}[u] >> 5) * {256 * W}u + ((b_ >> 5) << 8)"
+                if 32 % W == 0:  # (a field never straddles a stream dword: one load)
+                    o.append(f"{ind}  xp{i}[u] = __builtin_amdgcn_raw_buffer_load_b32(rs{i}, lq4, {soff}, 0);")
+                else:
+                    o.append(f"{ind}  xp{i}[u] = ld_il(rs{i}, {soff}, lq4);")
+                o.append(f"{ind}  pks{i}[u] = b_ & 31u;")
+                o.append(f"{ind}}}")
+                continue
+            k0, k1 = (j0 * W) >> 5, ((j0 + U) * W - 1) >> 5
+            n = k1 - k0 + 1
+            o.append(f"{ind}uint32_t xd{i}[{n + 1}];")
+            o.append(f"#pragma unroll\n{ind}for (int k = 0; k < {n}; ++k) xd{i}[k] = __builtin_amdgcn_raw_buffer_load_b32("
+                     f"rs{i}, lq4, (uint32_t)g_ * {256 * W}u + ({k0} + k) * 256u, 0);")
+            o.append(f"{ind}xd{i}[{n}] = 0u;")
             o.append(f"#pragma unroll\n{ind}for (int u = 0; u < {U}; ++u) {{")
-            for i in pk:
-                c = self.cols[i]
-                o.append(f"{ind}  xp{i}[u] = ld_pk(rs{i}, (uint32_t){wl}[u] * {8 * c.pw}u, pko{c.pw});")
+            o.append(f"{ind}  const int b_ = ({j0} + u) * {W} - {32 * k0};")
+            o.append(f"{ind}  xp{i}[u] = (uint64_t)xd{i}[b_ >> 5] | ((uint64_t)xd{i}[(b_ >> 5) + 1] << 32);")
+            o.append(f"{ind}  pks{i}[u] = (uint32_t)(b_ & 31);")
             o.append(f"{ind}}}")
         if not cols:
             return
@@ -528,16 +551,18 @@ class _Gen:
         body.append("        }")
         body.append("        woff += (uint32_t)__popcll(am_);")
 
-    def _words_tail(self, fcols, word_filter, mode: int, U: int, stage: List[str], body: List[str]) -> List[str]:
+    def _words_tail(self, fcols, word_filter, mode: int, U: int, stage: List[str], body: List[str],
+                    j0: Optional[int] = None) -> List[str]:
         """The per-step tail of a word loop (wl / m set): the per-row word filter, the empty-step
         skip, then the staged loads and updates."""
         out: List[str] = []
         if word_filter is not None:
             if fcols:
-                if not self.regstage:
+                dma = not self.regstage and any(not self.cols[i].pw for i in fcols)
+                if dma:
                     out.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
-                self.stage_words(out, fcols, "wl", "wb")
-                if not self.regstage:
+                self.stage_words(out, fcols, "wl", "wb", j0=j0)
+                if dma:
                     out.append('      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
             out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) m[u] &= {word_filter};")
         out.append("      uint64_t any = 0;")
@@ -593,18 +618,20 @@ class _Gen:
                 L.append(f"  unsigned char* hll{ai} = (unsigned char*)d->aops[{ai}].hll_regs;")
                 L.append(f"  const int64_t* sko{ai} = (const int64_t*)d->aops[{ai}].sk_off;")
                 L.append(f"  const int32_t* skv{ai} = (const int32_t*)d->aops[{ai}].sk_val;")
-        stage = []
-        body = stage
+        def mk_stage(j0: Optional[int]) -> List[str]:
+            st = ["      // ---- payload staging (whole words) ----", f"      bool act[{U}];",
+                  f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) act[u] = (m[u] >> lane) & 1ull;"]
+            if pcols:
+                dma = not self.regstage and any(not self.cols[i].pw for i in pcols)
+                if dma:
+                    st.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
+                self.stage_words(st, pcols, "wl", "wb", j0=j0)
+                if dma:
+                    st.append('      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
+            return st
+
         # ---------------- per-word processing
-        body.append("      // ---- payload staging (whole words) ----")
-        body.append(f"      bool act[{U}];")
-        body.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) act[u] = (m[u] >> lane) & 1ull;")
-        if pcols:
-            if not self.regstage:
-                body.append('      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");')
-            self.stage_words(body, pcols, "wl", "wb")
-            if not self.regstage:
-                body.append('      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");')
+        stage = mk_stage(None)
         def _mk_body(U: int) -> List[str]:
             body = []
             # phase 1: every staged read for the U words (keys + aggregator inputs) -- straight-line
@@ -743,11 +770,8 @@ class _Gen:
         out.append("  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);")
         for lg in sorted({c.lg for c in self.cols.values() if not c.pw}):
             out.append(f"  const uint32_t lo{lg} = (uint32_t)lane << {lg};")
-        for w in sorted({c.pw for c in self.cols.values() if c.pw}):
-            # lane l's field of a packed word: bits [l*W, l*W + W), read through the 8 bytes at the
-            # dword holding its first bit
-            out.append(f"  const uint32_t pko{w} = (((uint32_t)lane * {w}u) >> 5) * 4u;")
-            out.append(f"  const uint32_t psh{w} = ((uint32_t)lane * {w}u) & 31u;")
+        if any(c.pw for c in self.cols.values()):
+            out.append("  const uint32_t lq4 = (uint32_t)lane << 2;")
         out.append(f"  unsigned char* wb = lds + {lay.cache_off} + wave * {lay.wave_bytes};")
         stage_bytes = 0 if self.regstage else U * NP * 256
         out.append(f"  uint64_t* bmw = (uint64_t*)(wb + {stage_bytes});")
@@ -825,24 +849,41 @@ class _Gen:
             out.append(f"    pre &= {pre};")
         out.append("    uint64_t nz = __ballot(pre != 0ull);")
         full = FULL_CHUNKS and not pre and mode in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL, D.M_HASH)
-        if full:
-            out.append(f"    if (clo == crow0 && chi == crow0 + {D.CHUNK_ROWS}) {{")
+        # whole-chunk walks over a bit-packed column run as static runs of U words per 32-word
+        # stream group: each run's stream dwords are U W / 32 (+1) coalesced loads with
+        # compile-time field offsets (segment/packed.py); `continue` leaves only its own run
+        static = STATIC_RUNS and U >= 4 and 32 % U == 0 and any(self.cols[i].pw for i in staged)
+
+        def whole_chunk(mask: str) -> None:
+            if static:
+                out.append("    for (int g_ = 0; g_ < 2; ++g_) {")
+                for j0 in range(0, 32, U):
+                    out.append("    do {")
+                    out.append(f"      int wl[{U}];")
+                    out.append(f"      uint64_t m[{U}];")
+                    out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{ wl[u] = g_ * 32 + {j0} + u; "
+                               f"m[u] = {mask}; }}")
+                    out.extend(self._words_tail(fcols, word_filter, mode, U, mk_stage(j0), body, j0=j0))
+                    out.append("    } while (0);")
+                out.append("    }")
+                return
             out.append(f"    for (int w0_ = 0; w0_ < {D.CHUNK_WORDS}; w0_ += {U}) {{")
             out.append(f"      int wl[{U}];")
             out.append(f"      uint64_t m[{U}];")
-            out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{ wl[u] = w0_ + u; m[u] = ~0ull; }}")
+            out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{ wl[u] = w0_ + u; m[u] = {mask}; }}")
             out.extend(self._words_tail(fcols, word_filter, mode, U, stage, body))
             out.append("    }")
+
+        if full:
+            out.append(f"    if (clo == crow0 && chi == crow0 + {D.CHUNK_ROWS}) {{")
+            whole_chunk("~0ull")
             out.append("    } else {")
         dense = DENSE_WORDS > 0 and bool(pre) and mode in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL, D.M_HASH)
         if dense:
-            out.append(f"    if (__popcll(nz) >= {DENSE_WORDS}) {{")
-            out.append(f"    for (int w0_ = 0; w0_ < {D.CHUNK_WORDS}; w0_ += {U}) {{")
-            out.append(f"      int wl[{U}];")
-            out.append(f"      uint64_t m[{U}];")
-            out.append(f"#pragma unroll\n      for (int u = 0; u < {U}; ++u) {{ wl[u] = w0_ + u; m[u] = readlane64(pre, w0_ + u); }}")
-            out.extend(self._words_tail(fcols, word_filter, mode, U, stage, body))
-            out.append("    }")
+            # a static whole-chunk walk costs ~2W stream loads per packed column; the sparse walk
+            # two per column and nonzero word -- with packed columns it wins from far fewer words
+            out.append(f"    if (__popcll(nz) >= {DENSE_WORDS_PACKED if static else DENSE_WORDS}) {{")
+            whole_chunk("readlane64(pre, wl[u])")
             out.append("    } else {")
         out.append("    while (nz) {")
         out.append(f"      int wl[{U}];")

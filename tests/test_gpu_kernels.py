@@ -225,7 +225,7 @@ def test_packed_columns_roundtrip_on_device(gpu_ds):
             continue
         seen += 1
         t = column_tensor(gpu_ds, name)[:n].to(torch.int64)
-        assert pc.width < 8 * column_tensor(gpu_ds, name).element_size()
+        assert pc.width <= 8 * column_tensor(gpu_ds, name).element_size()
         assert torch.equal(unpack(pc), t), name
     PK.ENABLED = old
     assert seen >= 5

@@ -58,7 +58,7 @@ def main():
                     mode = {"dense-lds": D.M_DENSE_LDS, "dense-global": D.M_DENSE_GLOBAL, "hash": D.M_HASH,
                             "partitioned": D.M_PART}[gp.mode]
                     prog.packed = {}
-                    for c in list(prog.fcols) + list(prog.pcols):
+                    for c in (list(prog.fcols) + list(prog.pcols)) if mode in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL, D.M_HASH) else []:
                         t = column_tensor(ds, c)
                         if not t.is_floating_point():
                             tt = t[:ds.num_rows].to(torch.int64) if t.dtype == torch.uint16 else t[:ds.num_rows]

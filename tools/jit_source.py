@@ -50,7 +50,7 @@ def main():
                     from spark_druid_olap_amd.segment import packed as PK
 
                     prog.packed = {}
-                    for c in list(prog.fcols) + list(prog.pcols):
+                    for c in (list(prog.fcols) + list(prog.pcols)) if mode in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL, D.M_HASH) else []:
                         t = column_tensor(ds, c)
                         if not t.is_floating_point():
                             tt = t[:ds.num_rows].to(torch.int64) if t.dtype == torch.uint16 else t[:ds.num_rows]
