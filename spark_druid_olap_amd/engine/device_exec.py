@@ -72,10 +72,13 @@ def _spec_job(js):
             _spec_pending[0] -= 1
 
 
-PACKED_MODES = (D.M_DENSE_LDS, D.M_DENSE_GLOBAL, D.M_HASH)
-# the packed layout pays off on whole-chunk walks; a selective scan mostly walks single nonzero
-# words (two stream loads per packed column and word vs one plain load): TPC-H Q5 (2.5% of rows)
-# 0.25 -> 0.18 ms packed, Q7 (0.3%) 0.37 -> 0.50 ms (profiles/r4/scan_kernel_ab_notes.md)
+# The packed layout pays off where a scan streams: whole-chunk walks over LDS tables.  A selective
+# scan mostly walks single nonzero words (two stream loads per packed column and word vs one plain
+# load): TPC-H Q5 (2.5% of rows) 0.25 -> 0.18 ms packed, Q7 (0.3%) 0.37 -> 0.50 ms.  Scans bound
+# by random accesses -- id-set filter probes, HBM-table atomics -- lose occupancy to the unrolled
+# runs and gain nothing: TPC-H22 Q9 (p_name id set) 4.95 -> 5.49 ms, Q11 (HBM table) 3.61 ->
+# 4.18 ms packed (profiles/r4/scan_kernel_ab_notes.md).
+PACKED_MODES = (D.M_DENSE_LDS,)
 PACK_MIN_SELECTIVITY = 0.02
 
 
@@ -91,6 +94,8 @@ def _attach_packed(prog, mode: int) -> None:
         return
     n = max(1, int(prog.ds.num_rows))
     if float(getattr(prog, "est_rows", n)) < PACK_MIN_SELECTIVITY * n:
+        return
+    if any(int(f[0]) == D.F_IN_SET for f in prog.fops):
         return
     for name in list(prog.fcols) + list(prog.pcols):
         pc = PK.packed_column(prog.ds, name)

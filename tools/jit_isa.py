@@ -147,7 +147,7 @@ def main():
                 mode = {"dense-lds": D.M_DENSE_LDS, "dense-global": D.M_DENSE_GLOBAL, "hash": D.M_HASH,
                         "partitioned": D.M_PART}[gp.mode]
                 prog.packed = {}
-                for c in (list(prog.fcols) + list(prog.pcols)) if mode in DE.PACKED_MODES and prog.est_rows >= DE.PACK_MIN_SELECTIVITY * ds.num_rows else []:
+                for c in (list(prog.fcols) + list(prog.pcols)) if mode in DE.PACKED_MODES and prog.est_rows >= DE.PACK_MIN_SELECTIVITY * ds.num_rows and not any(int(f[0]) == D.F_IN_SET for f in prog.fops) else []:
                     t = column_tensor(ds, c)
                     if not t.is_floating_point():
                         tt = t[:ds.num_rows].to(torch.int64) if t.dtype == torch.uint16 else t[:ds.num_rows]
