@@ -773,6 +773,27 @@ def _buffers_acquired(prep, slot, b) -> None:
                 p._slots.pop(sl, None)
 
 
+def release_device_memory(keep=None) -> None:
+    """Drop every prepared scan's cached slot buffers (but ``keep``'s (prep, slot)), the shared
+    scratch and the allocator's free blocks.  A scan running on a dropped slot keeps its tensors
+    alive through its own references until it finishes."""
+    victims = []
+    with _buf_lock:
+        for k in list(_buf_lru):
+            if k == keep:
+                continue
+            ref, n = _buf_lru.pop(k)
+            _buf_total[0] -= n
+            victims.append((ref(), k[1]))
+    for p, sl in victims:
+        if p is not None:
+            with p._slot_lock:
+                p._slots.pop(sl, None)
+    with _scratch_lock:
+        _SCRATCH.clear()
+    torch.cuda.empty_cache()
+
+
 def _with_eviction(fn, prep, slot):
     """Run an allocation; on a device out-of-memory error release every other prepared scan's
     cached slot buffers (least recently used first: all of them) and the allocator's free blocks,
@@ -780,22 +801,7 @@ def _with_eviction(fn, prep, slot):
     try:
         return fn()
     except torch.OutOfMemoryError:
-        victims = []
-        with _buf_lock:
-            for k in list(_buf_lru):
-                if k == (id(prep), slot):
-                    continue
-                ref, n = _buf_lru.pop(k)
-                _buf_total[0] -= n
-                victims.append((ref(), k[1]))
-        for p, sl in victims:
-            if p is not None:
-                with p._slot_lock:
-                    p._slots.pop(sl, None)
-        if prep is not None:
-            with _scratch_lock:
-                _SCRATCH.clear()
-        torch.cuda.empty_cache()
+        release_device_memory(keep=(id(prep), slot))
         return fn()
 
 

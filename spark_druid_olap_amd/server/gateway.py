@@ -30,6 +30,8 @@ import threading
 import time
 from typing import List, Optional, Tuple
 
+import torch
+
 import numpy as np
 import pandas as pd
 
@@ -294,7 +296,15 @@ class NativeHiveServer(HiveThriftServer):
         else:
             df.prepare()  # lowering + a first-seen shape's compile: before a stream slot is held
             with sess.engine.coalescer().scheduler.lease():
-                res = df.run(token=token)  # the executor's columns, encoded without a DataFrame
+                try:
+                    res = df.run(token=token)  # the executor's columns, encoded without a DataFrame
+                except torch.OutOfMemoryError:
+                    # the HBM is held by other statements' cached slot tables (many concurrent
+                    # large group-bys): drop every cache and run the statement once more
+                    from ..engine.device_exec import release_device_memory
+
+                    release_device_memory()
+                    res = df.run(token=token)
         return list(df.columns), [t for _, t in df.schema], res
 
 
