@@ -85,6 +85,7 @@ for step in "$@"; do
           --iters 3 > "$R/gpurun_out/pmc$i.log" 2>&1) || fail pmc $? gpurun_out/pmc$i.log
       done
       python tools/pmc_summary.py gpurun_out "${PMC_FILT:-sdo_}" "pmc[0-9]*" > gpurun_out/pmc_summary.txt 2>&1 || true
+      rm -rf gpurun_out/pmc[0-9]*  # (the per-pass CSVs exceed what gpurun copies back; the summary stays)
       tail -40 gpurun_out/pmc_summary.txt ;;
     py:*)
       s="${step#py:}"
