@@ -600,7 +600,8 @@ class PreparedScan:
 
     # ------------------------------------------------------------------ run
     def run(self) -> Partials:
-        pinned().add(id(self))  # (its buffers hold this statement's partials: not to be taken over)
+        if current_slot() != 0:
+            pinned().add(id(self))  # (its buffers hold this statement's partials: not to be taken over)
         self._maybe_specialize()
         prog = self.prog
         b = self._bufs()
@@ -854,7 +855,11 @@ def _geom_register(prep, slot, geom) -> None:
 
 def _steal(prep, slot, geom) -> Optional["_Bufs"]:
     """Another (unpinned) prepared scan's buffers of geometry ``geom`` on ``slot``, removed from
-    it; None when there are none."""
+    it; None when there are none.  Never on slot 0: it is not leased (every thread that runs a
+    statement outside the scheduler shares it), so one thread's pins say nothing about the scans
+    another thread is still running there."""
+    if slot == 0:
+        return None
     pins = pinned()
     with _geom_lock:
         holders = _GEOM.get((slot, geom))

@@ -37,6 +37,8 @@ from ..utils.cancel import checkpoint
 PIPELINE_MERGE = os.environ.get("SDO_PIPELINE_MERGE", "1") not in ("0", "")
 # existence-only group-bys over the key's dictionary domain (engine/dict_exist.py)
 DICT_EXIST = os.environ.get("SDO_DICT_EXIST", "1") not in ("0", "")
+# GPU-event phase attribution of PreparedQuery.run (scan / merge / gather / finalize)
+PHASE_EVENTS = os.environ.get("SDO_PHASE_EVENTS", "0") not in ("0", "")
 
 # Multi-rank result placement.  Set (``results_on_root``) by callers that consume a statement's
 # result on rank 0 only -- the benchmark, the SPMD server answering its client: the final groups
@@ -299,12 +301,51 @@ class PreparedQuery:
         return merge_partials(self.world, prog, part, disjoint_keys=disjoint)
 
     # ------------------------------------------------------------------ run
+    def _mark(self, name: str) -> None:
+        """GPU phase attribution (``SDO_PHASE_EVENTS=1`` / ``phase_events``): a HIP event recorded
+        on the compute stream at each phase boundary, so scan / merge / gather / finalize are the
+        device's own times, not host stamps around asynchronous launches."""
+        ev = self.__dict__.get("_events")
+        if ev is not None and self.ds.device.type == "cuda":
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(torch.cuda.current_stream(self.ds.device))
+            ev.append((name, e))
+
+    def _phase_stats(self) -> Dict[str, float]:
+        ev = self.__dict__.get("_events")
+        self._events = None
+        if not ev:
+            return {}
+        ev[-1][1].synchronize()
+        out: Dict[str, float] = {}
+        for (_, a), (name, b) in zip(ev, ev[1:]):
+            out["gpu_" + name + "_ms"] = out.get("gpu_" + name + "_ms", 0.0) + a.elapsed_time(b)
+        return out
+
     def run(self) -> QueryResult:
+        """Execute once.  A peer-to-peer merge epoch abandoned by every rank (parallel/p2p.py)
+        raises ``P2PRetry`` on every rank together: the statement then re-runs with its merges over
+        RCCL, so a slow or unreachable peer costs a retry, not a failed statement."""
+        from ..parallel import p2p
+        from ..parallel.fault import P2PRetry
+
+        try:
+            return self._run()
+        except P2PRetry:
+            p2p.note_retry(self.world)
+            with p2p.suppressed():
+                res = self._run()
+            res.stats["p2p_retry"] = 1
+            return res
+
+    def _run(self) -> QueryResult:
         t0 = time.perf_counter()
         qt = self.qs.queryType
+        self._events = [] if (PHASE_EVENTS or getattr(self, "phase_events", False)) else None
+        self._mark("start")
         if qt in ("groupBy", "timeseries", "topN"):
             root_only = self.world.distributed and root_only_results()
-            prog, part, t1 = self.run_partials(t0, root_only)
+            prog, part, t1 = self.run_partials(t0, root_only, check=False)
             t2 = time.perf_counter()
             with T.span("sdo.finalize"):
                 if root_only and self.world.rank != 0:
@@ -315,6 +356,7 @@ class PreparedQuery:
                     check_status(part)
                     part = empty_partials(prog, self.ds.device)
                 cols = finalize(prog, part, getattr(self, "out_types", None))
+            self._mark("finalize")
             t3 = time.perf_counter()
             with T.span("sdo.post"):
                 self._theta(self._full_prog, cols)
@@ -322,6 +364,7 @@ class PreparedQuery:
             t4 = time.perf_counter()
             res.stats.update(scan_ms=(t1 - t0) * 1e3, merge_ms=(t2 - t1) * 1e3, finalize_ms=(t3 - t2) * 1e3,
                              post_ms=(t4 - t3) * 1e3)
+            res.stats.update(self._phase_stats())
         elif qt == "search":
             res = self._search()
         else:
@@ -351,12 +394,9 @@ class PreparedQuery:
         ``root_only``: the groups are gathered to rank 0 alone and the other ranks yield one empty
         page (only the first step issues collectives, so ranks pulling pages in lock step stay
         matched); without it every rank pages through the whole answer."""
-        from ..parallel.p2p import check_status
-
         t0 = time.perf_counter()
         root_only = self.world.distributed and (root_only_results() if root_only is None else root_only)
         prog, part, _ = self.run_partials(t0, root_only)
-        check_status(part)
         if root_only and self.world.rank != 0:
             part = empty_partials(prog, self.ds.device)
         part = part.compact()
@@ -375,13 +415,34 @@ class PreparedQuery:
             res.stats.update(page=a // page_rows, groups_total=R)
             yield res
 
-    def run_partials(self, t0: float, root_only: bool = False):
+    def run_partials(self, t0: float, root_only: bool = False, check: bool = True):
         """scan -> merge across ranks -> device HAVING / top-K pruning; (prog, merged partials,
         scan end time).  The partials stay on the device (nested queries consume them there).
 
         Across ranks, sparse partials are merged into disjoint per-rank slices first; HAVING and the
         top-K prune run on every slice (distributed), and only the survivors are gathered -- to
-        rank 0 alone with ``root_only`` (the other ranks then hold an empty slice)."""
+        rank 0 alone with ``root_only`` (the other ranks then hold an empty slice).
+
+        ``check``: a P2P merge's status words are read here (one host sync) -- the default, for
+        consumers that transform the state further (nested levels, grouping sets, paging).
+        ``run()`` passes False and reads them with the result's copy in ``finalize``.  An epoch
+        every rank abandoned re-runs the scan with the merge over RCCL (parallel/p2p.py)."""
+        from ..parallel import p2p
+        from ..parallel.fault import P2PRetry
+
+        try:
+            out = self._run_partials(t0, root_only)
+            if check:
+                p2p.check_status(out[1])
+            return out
+        except P2PRetry:
+            p2p.note_retry(self.world)
+            with p2p.suppressed():
+                out = self._run_partials(t0, root_only)
+            p2p.check_status(out[1])  # (no P2P state: RCCL statuses were checked in the merge)
+            return out
+
+    def _run_partials(self, t0: float, root_only: bool):
         _, prog, prep = self.scans[0]
         if self.segments_per_query and self.world.distributed and self.window is None and PIPELINE_MERGE:
             out = self._run_pipelined(prog)
@@ -412,6 +473,7 @@ class PreparedQuery:
             err, part = e, self._placeholder(prog, prep)
         if self.window is not None:
             prog = self._full_prog
+        self._mark("scan")
         t1 = time.perf_counter()
         disjoint = bool(self.ds.shard_key) and any(k.col == self.ds.shard_key for k in prog.keys)
         with T.span("sdo.merge"):
@@ -424,6 +486,7 @@ class PreparedQuery:
             from ..parallel.p2p import check_status
 
             check_status(merged)  # (a P2P merge's status words: read now, the state was transformed)
+        self._mark("merge")
         if part.scattered:
             from ..parallel.merge import gather_groups
 
@@ -431,6 +494,7 @@ class PreparedQuery:
                 part = gather_groups(self.world, part, root_only, part.status, err)
             if self.world.rank == 0 or not root_only:
                 part = self._device_prune(prog, part, hv)  # the union of per-slice supersets
+            self._mark("gather")
         return prog, part, t1
 
     def _run_pipelined(self, prog):

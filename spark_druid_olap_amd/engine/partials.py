@@ -34,9 +34,14 @@ class Partials:
         return int(self.acc.shape[0])
 
     def compact(self) -> "Partials":
-        """dense -> sparse keeping groups with a non-zero presence count (slot 0)."""
+        """dense -> sparse keeping groups with a non-zero presence count (slot 0).  A P2P-merged
+        state's status words are checked first: the compacted state no longer carries them."""
         if self.kind == "sparse":
             return self
+        if self.status_dev is not None:
+            from ..parallel.p2p import check_status
+
+            check_status(self)
         if self.acc.is_cuda:
             from ..ops import native
 
@@ -472,9 +477,9 @@ def finalize(prog, parts: Partials, out_types: Optional[Dict[str, str]] = None) 
                     sts = host.pop()
                     parts.status_dev = None
                     if sts.any():
-                        from ..parallel.fault import raise_if_failed
+                        from ..parallel.p2p import raise_status
 
-                        raise_if_failed(sts.tolist(), parts.status_rank, None)
+                        raise_status(sts.tolist(), parts.status_rank)
             else:
                 if want_est and parts.acc.is_cuda:
                     from ..ops import native

@@ -13,6 +13,8 @@
 #include <stdexcept>
 #include <string>
 #include <tuple>
+
+#include "p2p.h"
 #include <vector>
 #include "scan_desc.h"
 #include "post_scan.h"
@@ -76,27 +78,7 @@ __global__ void theta_hist_kernel(const int64_t* g, const int64_t* h, int64_t n,
 __global__ void theta_thresh_kernel(const uint32_t* hist, int bits, const int64_t* target, int64_t* bound);
 __global__ void theta_filter_kernel(const int64_t* g, const int64_t* h, int64_t n, const int64_t* bound,
                                     int64_t* out_g, int64_t* out_h, unsigned long long* count, int64_t cap);
-// p2p.hip
-constexpr int P2P_MAX_RANKS = 8;
-constexpr int P2P_MAX_SLOTS = 64;
-struct P2PArgs {
-  uint64_t mbox[P2P_MAX_RANKS];
-  int nranks;
-  int rank;
-  uint64_t epoch;
-  int64_t slot_bytes;
-  int64_t nacc;
-  int64_t nhll;
-  int nslots;
-  int ops[P2P_MAX_SLOTS];
-  const int64_t* acc_src;
-  const uint8_t* hll_src;
-  int64_t status;
-  int64_t* acc_out;
-  uint8_t* hll_out;
-  int64_t* status_out;
-  int64_t timeout_ticks;
-};
+// p2p.hip (P2PArgs: p2p.h)
 __global__ void p2p_merge_kernel(P2PArgs a);
 }  // namespace sdo
 
@@ -675,16 +657,32 @@ static void theta_select(uint64_t g, uint64_t h, int64_t n, int64_t G, int bits,
 }
 
 // ---------------------------------------------------------------------------------------------
-// Peer-to-peer mailboxes (p2p.hip): one hipMalloc per (process group, rank), exported with an IPC
+// Peer-to-peer mailboxes (p2p.hip): one allocation per (process group, rank), exported with an IPC
 // handle and opened by every peer; the small dense merge is then one kernel per rank.
+// The mailbox is UNCACHED device memory: the writer's stores and the peers' xGMI reads meet in
+// HBM, with no L2 line of either GPU in between.  (A plain hipMalloc is the fallback when the
+// uncached allocation cannot be exported; the kernel's system-scope fences / atomics cover it, and
+// the exchange's known-value self-test decides whether the path is used at all, parallel/p2p.py.)
+// Returns (pointer, IPC handle, "uncached" | "coarse").
 static py::tuple p2p_alloc(int64_t bytes) {
   void* p = nullptr;
-  check(hipMalloc(&p, (size_t)bytes), "p2p mailbox hipMalloc");
+  const char* kind = "uncached";
+  hipIpcMemHandle_t h;
+  bool ok = hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached) == hipSuccess;
+  if (ok && hipIpcGetMemHandle(&h, p) != hipSuccess) {
+    (void)hipFree(p);
+    p = nullptr;
+    ok = false;
+  }
+  if (!ok) {
+    (void)hipGetLastError();
+    kind = "coarse";
+    check(hipMalloc(&p, (size_t)bytes), "p2p mailbox hipMalloc");
+    check(hipIpcGetMemHandle(&h, p), "hipIpcGetMemHandle");
+  }
   check(hipMemset(p, 0, (size_t)bytes), "p2p mailbox clear");
   check(hipDeviceSynchronize(), "p2p mailbox clear sync");
-  hipIpcMemHandle_t h;
-  check(hipIpcGetMemHandle(&h, p), "hipIpcGetMemHandle");
-  return py::make_tuple((uint64_t)p, py::bytes((const char*)&h, sizeof(h)));
+  return py::make_tuple((uint64_t)p, py::bytes((const char*)&h, sizeof(h)), kind);
 }
 
 static uint64_t p2p_open(py::bytes handle) {
@@ -702,7 +700,8 @@ static void p2p_free(uint64_t p) { (void)hipFree((void*)p); }
 
 static void p2p_merge(std::vector<uint64_t> mbox, int rank, uint64_t epoch, int64_t slot_bytes, uint64_t acc_src,
                       int64_t nacc, uint64_t hll_src, int64_t nhll, std::vector<int> ops, int64_t status,
-                      uint64_t acc_out, uint64_t hll_out, uint64_t status_out, double timeout_s, uint64_t stream) {
+                      uint64_t acc_out, uint64_t hll_out, uint64_t status_out, double soft_s, double hard_s,
+                      uint64_t stream) {
   sdo::P2PArgs a{};
   const int n = (int)mbox.size();
   if (n < 1 || n > sdo::P2P_MAX_RANKS) throw std::invalid_argument("p2p_merge: 1..8 ranks");
@@ -733,7 +732,8 @@ static void p2p_merge(std::vector<uint64_t> mbox, int rank, uint64_t epoch, int6
   a.acc_out = (int64_t*)acc_out;
   a.hll_out = (uint8_t*)hll_out;
   a.status_out = (int64_t*)status_out;
-  a.timeout_ticks = (int64_t)(timeout_s * 1e8);  // wall clock: 100 MHz
+  a.soft_ticks = (int64_t)(soft_s * 1e8);  // wall clock: 100 MHz
+  a.hard_ticks = (int64_t)(hard_s * 1e8);
   hipLaunchKernelGGL(sdo::p2p_merge_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, a);
   check(hipGetLastError(), "p2p_merge_kernel launch");
 }

@@ -5,50 +5,32 @@
 // after a shuffle (asd/PostAggregate.scala:97-103, sd/DruidRDD.scala:62-99).  Across GPUs the small
 // dense states of typical OLAP queries (TPC-H Q1: 6 groups) are latency-bound: an RCCL all-gather, a
 // torch reduction per slot and a host read of the status words cost several launches and a host
-// round trip.  Here every rank owns a *mailbox* (one hipMalloc, exported once with hipIpcGetMemHandle
-// and opened by every peer), and ONE kernel per rank and merge:
+// round trip.  Here every rank owns a *mailbox* (uncached device memory, exported once with an IPC
+// handle and opened by every peer), and ONE kernel per rank and merge:
 //
-//   1. waits until every peer is done reading the mailbox slot it is about to overwrite
-//      (double-buffered by epoch parity: slot e % 2 was last read in epoch e - 2);
+//   1. waits until every peer is done with the epoch before (so the data slot it is about to
+//      overwrite -- double-buffered by epoch parity -- is no longer read);
 //   2. writes its packed partial -- accumulator words, HLL register bytes, its status word -- into
 //      its own slot, then publishes the epoch in its header with a system-scope release;
-//   3. waits for every peer's epoch (system-scope acquire) and reduces the N mailboxes with the
-//      per-slot operators (int sum, f64 sum, min, max; u8 max for HLL registers), reading peer
-//      memory with system-scope loads (over xGMI across GPUs; through the shared memory side of
-//      the same device when two ranks share a card);
-//   4. writes every rank's status word next to the merged result and marks itself done.
+//   3. waits (bounded by the SOFT timeout) for every peer's epoch and reduces the N mailboxes with
+//      the per-slot operators (int sum, f64 sum, min, max; u8 max for HLL registers), reading peer
+//      memory with system-scope loads (over xGMI across GPUs; through the same HBM when two ranks
+//      share a card);
+//   4. publishes its VERDICT for the epoch -- "I saw every peer's partial" or "I gave up" -- then
+//      its done word, and waits (HARD timeout) for every peer's verdict.
 //
-// No host synchronisation: the caller's result copy carries the status words.  Every spin wait is
-// bounded (wall clock, P2P_TIMEOUT_TICKS): a missing peer turns into a failed status word, never a
-// kernel that does not finish.
+// Every rank reads the same N verdict words, so every rank reaches the same outcome: all succeed,
+// or -- when any rank's soft wait expired (a peer slow to arrive, or a coherence failure) -- all
+// report P2P_STATUS_RETRY and the host re-runs the merge over RCCL (parallel/p2p.py).  Only a
+// peer that never posts a verdict within the hard timeout (a dead process) becomes a failed
+// status word.  No host synchronisation on the fast path: the caller's result copy carries the
+// status words.  Every spin wait is bounded: no kernel that does not finish.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "p2p.h"
+
 namespace sdo {
-
-constexpr int P2P_MAX_RANKS = 8;
-constexpr int P2P_MAX_SLOTS = 64;
-constexpr int64_t P2P_HEADER = 256;  // bytes: flag word, done word, error word, padding
-constexpr int64_t P2P_STATUS_TIMEOUT = 3;  // status word of a rank that did not arrive in time
-
-struct P2PArgs {
-  uint64_t mbox[P2P_MAX_RANKS];  // every rank's mailbox base, as mapped in this process (own included)
-  int nranks;
-  int rank;
-  uint64_t epoch;                // >= 1, strictly increasing per exchange
-  int64_t slot_bytes;            // capacity of one data slot
-  int64_t nacc;                  // accumulator words (rows x nslots)
-  int64_t nhll;                  // HLL register bytes (multiple of 8)
-  int nslots;
-  int ops[P2P_MAX_SLOTS];        // SlotOp per slot
-  const int64_t* acc_src;
-  const uint8_t* hll_src;
-  int64_t status;
-  int64_t* acc_out;
-  uint8_t* hll_out;
-  int64_t* status_out;           // [nranks]
-  int64_t timeout_ticks;         // wall_clock64 ticks (100 MHz)
-};
 
 __device__ __forceinline__ uint64_t p2p_load(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -62,26 +44,28 @@ __device__ __forceinline__ void p2p_release(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// header words: [0] published epoch, [1] done epoch
+// header words: [0] published epoch, [1] done epoch, [2 + (e & 1)] verdict of epoch e = (e << 1) | gave_up
 __device__ __forceinline__ uint64_t* hdr(uint64_t base, int w) { return (uint64_t*)base + w; }
 
 __device__ __forceinline__ uint64_t* slot_ptr(const P2PArgs& a, int r, uint64_t epoch) {
   return (uint64_t*)(a.mbox[r] + P2P_HEADER + (int64_t)(epoch & 1) * a.slot_bytes);
 }
 
+__device__ __forceinline__ unsigned all_mask(int n) { return n >= 32 ? 0xffffffffu : ((1u << n) - 1u); }
+
 // Bounded wait until every peer's header word w reaches at least `want`; returns a bit mask of the
 // ranks that did (all ranks' bits set = success).
-__device__ unsigned wait_peers(const P2PArgs& a, int w, uint64_t want) {
+__device__ unsigned wait_peers(const P2PArgs& a, int w, uint64_t want, int64_t ticks) {
   unsigned ok = 1u << a.rank;
   const uint64_t t0 = wall_clock64();
-  const unsigned all = (a.nranks >= 32) ? 0xffffffffu : ((1u << a.nranks) - 1u);
+  const unsigned all = all_mask(a.nranks);
   while (ok != all) {
     for (int r = 0; r < a.nranks; ++r) {
       if (ok & (1u << r)) continue;
       if (p2p_acquire(hdr(a.mbox[r], w)) >= want) ok |= 1u << r;
     }
     if (ok == all) break;
-    if ((int64_t)(wall_clock64() - t0) > a.timeout_ticks) break;
+    if ((int64_t)(wall_clock64() - t0) > ticks) break;
     __builtin_amdgcn_s_sleep(2);
   }
   return ok;
@@ -89,13 +73,15 @@ __device__ unsigned wait_peers(const P2PArgs& a, int w, uint64_t want) {
 
 // One workgroup of 1024 threads per merge (states are <= 64 KB: a few loads per thread).
 __global__ void __launch_bounds__(1024) p2p_merge_kernel(P2PArgs a) {
-  __shared__ unsigned s_ok;
+  __shared__ unsigned s_prev, s_have, s_done, s_gaveup;
   const int tid = threadIdx.x;
   const uint64_t e = a.epoch;
-  // 1. the slot of epoch e was last read in epoch e - 2: every peer must be done with it
-  if (tid == 0) s_ok = e > 2 ? wait_peers(a, 1, e - 2) : ((1u << a.nranks) - 1u);
+  const unsigned all = all_mask(a.nranks);
+  // 1. every peer finished epoch e - 1 (so nobody still reads the slot of parity e, last used in
+  //    epoch e - 2, and every verdict word of parity e + 1 has been read)
+  if (tid == 0) s_prev = e > 1 ? wait_peers(a, 1, e - 1, a.hard_ticks) : all;
   __syncthreads();
-  // 2. publish this rank's partial (even after a timeout: a late peer must still find data)
+  // 2. publish this rank's partial (even after a failed wait: a late peer must still find data)
   uint64_t* mine = slot_ptr(a, a.rank, e);
   for (int64_t i = tid; i < a.nacc; i += blockDim.x) mine[i] = (uint64_t)a.acc_src[i];
   const uint64_t* hsrc = (const uint64_t*)a.hll_src;
@@ -104,53 +90,68 @@ __global__ void __launch_bounds__(1024) p2p_merge_kernel(P2PArgs a) {
   __threadfence_system();
   __syncthreads();
   if (tid == 0) p2p_release(hdr(a.mbox[a.rank], 0), e);
-  // 3. every peer's partial of this epoch
-  __shared__ unsigned s_have;
-  if (tid == 0) s_have = wait_peers(a, 0, e);
+  // 3. every peer's partial of this epoch (soft bound)
+  if (tid == 0) s_have = (s_prev == all) ? wait_peers(a, 0, e, a.soft_ticks) : (1u << a.rank);
   __syncthreads();
   const unsigned have = s_have;
-  for (int64_t i = tid; i < a.nacc; i += blockDim.x) {
-    const int op = a.ops[i % a.nslots];
-    int64_t v = a.acc_src[i];
-    double f = __longlong_as_double(v);
-    for (int r = 0; r < a.nranks; ++r) {
-      if (r == a.rank || !(have & (1u << r))) continue;
-      const int64_t x = (int64_t)p2p_load(slot_ptr(a, r, e) + i);
-      if (op == 0) v += x;
-      else if (op == 1) f += __longlong_as_double(x);
-      else if (op == 2) v = x < v ? x : v;
-      else v = x > v ? x : v;
-    }
-    a.acc_out[i] = op == 1 ? __double_as_longlong(f) : v;
-  }
-  uint64_t* hout = (uint64_t*)a.hll_out;
-  for (int64_t i = tid; i < a.nhll / 8; i += blockDim.x) {
-    uint64_t v = hsrc[i];
-    for (int r = 0; r < a.nranks; ++r) {
-      if (r == a.rank || !(have & (1u << r))) continue;
-      const uint64_t x = p2p_load(slot_ptr(a, r, e) + a.nacc + i);
-      uint64_t m = 0;
-#pragma unroll
-      for (int b = 0; b < 64; b += 8) {
-        const uint64_t p = (v >> b) & 0xff, q = (x >> b) & 0xff;
-        m |= (p > q ? p : q) << b;
+  if (have == all) {
+    for (int64_t i = tid; i < a.nacc; i += blockDim.x) {
+      const int op = a.ops[i % a.nslots];
+      int64_t v = a.acc_src[i];
+      double f = __longlong_as_double(v);
+      for (int r = 0; r < a.nranks; ++r) {
+        if (r == a.rank) continue;
+        const int64_t x = (int64_t)p2p_load(slot_ptr(a, r, e) + i);
+        if (op == 0) v += x;
+        else if (op == 1) f += __longlong_as_double(x);
+        else if (op == 2) v = x < v ? x : v;
+        else v = x > v ? x : v;
       }
-      v = m;
+      a.acc_out[i] = op == 1 ? __double_as_longlong(f) : v;
     }
-    hout[i] = v;
+    uint64_t* hout = (uint64_t*)a.hll_out;
+    for (int64_t i = tid; i < a.nhll / 8; i += blockDim.x) {
+      uint64_t v = hsrc[i];
+      for (int r = 0; r < a.nranks; ++r) {
+        if (r == a.rank) continue;
+        const uint64_t x = p2p_load(slot_ptr(a, r, e) + a.nacc + i);
+        uint64_t m = 0;
+#pragma unroll
+        for (int b = 0; b < 64; b += 8) {
+          const uint64_t p = (v >> b) & 0xff, q = (x >> b) & 0xff;
+          m |= (p > q ? p : q) << b;
+        }
+        v = m;
+      }
+      hout[i] = v;
+    }
   }
+  // 4. verdict + done (after every read of the peers' slots), then every peer's verdict
+  __threadfence_system();
+  __syncthreads();
+  if (tid == 0) {
+    p2p_release(hdr(a.mbox[a.rank], 2 + (int)(e & 1)), (e << 1) | (have == all ? 0u : 1u));
+    p2p_release(hdr(a.mbox[a.rank], 1), e);
+    const unsigned done = wait_peers(a, 1, e, a.hard_ticks);
+    unsigned gaveup = 0;
+    for (int r = 0; r < a.nranks; ++r) {
+      if (!(done & (1u << r))) continue;
+      const uint64_t v = p2p_acquire(hdr(a.mbox[r], 2 + (int)(e & 1)));
+      if ((v >> 1) != e || (v & 1)) gaveup |= 1u << r;
+    }
+    s_done = done;
+    s_gaveup = gaveup;
+  }
+  __syncthreads();
   if (tid < a.nranks) {
     const int r = tid;
     int64_t st;
-    if (r == a.rank) st = a.status;
-    else if (!(have & (1u << r)) || !(s_ok & (1u << r))) st = P2P_STATUS_TIMEOUT;
+    if (!(s_prev & (1u << r)) || !(s_done & (1u << r))) st = P2P_STATUS_TIMEOUT;
+    else if (s_gaveup) st = P2P_STATUS_RETRY;  // every rank sees the same verdicts: all retry together
+    else if (r == a.rank) st = a.status;
     else st = (int64_t)p2p_load(slot_ptr(a, r, e) + a.nacc + a.nhll / 8);
     a.status_out[r] = st;
   }
-  // 4. done reading every peer's slot of epoch e
-  __threadfence_system();
-  __syncthreads();
-  if (tid == 0) p2p_release(hdr(a.mbox[a.rank], 1), e);
 }
 
 }  // namespace sdo

@@ -24,6 +24,8 @@ from ..utils.errors import DruidDataSourceException
 
 STATUS_OK = 0
 STATUS_FAILED = 1
+STATUS_P2P_TIMEOUT = 3   # a peer never finished a peer-to-peer merge epoch (ops/csrc/p2p.h)
+STATUS_P2P_RETRY = 4     # a P2P merge epoch was abandoned by every rank: re-run it over RCCL
 
 
 class InjectedFault(DruidDataSourceException):
@@ -32,6 +34,11 @@ class InjectedFault(DruidDataSourceException):
 
 class RankFailure(DruidDataSourceException):
     """Another rank failed its part of the query; every rank aborts the query consistently."""
+
+
+class P2PRetry(RankFailure):
+    """Every rank abandoned a peer-to-peer merge epoch together (a soft wait expired somewhere):
+    the statement is re-run with the merge over RCCL (parallel/p2p.py, engine/executor.py)."""
 
 
 class FaultInjector:
@@ -69,5 +76,9 @@ def raise_if_failed(statuses, my_rank: int, local_error: Optional[BaseException]
     bad = [r for r, s in enumerate(statuses) if int(s) != STATUS_OK]
     if local_error is not None:
         raise local_error
+    if bad and all(int(statuses[r]) == STATUS_P2P_RETRY for r in bad):
+        raise P2PRetry("peer-to-peer merge epoch abandoned by every rank: retrying over RCCL")
     if bad:
-        raise RankFailure(f"query aborted: rank(s) {bad} failed their local scan")
+        what = "timed out in a peer-to-peer merge" if any(int(statuses[r]) == STATUS_P2P_TIMEOUT for r in bad) \
+            else "failed their local scan"
+        raise RankFailure(f"query aborted: rank(s) {bad} {what}")

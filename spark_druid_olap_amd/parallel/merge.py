@@ -186,7 +186,15 @@ def merge_partials(world: World, prog, part: Partials, disjoint_keys: bool = Fal
         if ex is not None:
             merged = ex.merge(prog, part, status)
             if local_error is not None:
-                raise local_error  # (after publishing: the peers read this rank's failed status)
+                # (after publishing: the peers read this rank's failed status) -- unless every rank
+                # abandoned the epoch, in which case this rank retries over RCCL with its peers
+                sts = merged.status_dev.tolist()
+                from .fault import STATUS_P2P_RETRY, P2PRetry
+
+                if any(sts) and all(int(v) in (STATUS_OK, STATUS_P2P_RETRY) for v in sts) and \
+                        STATUS_P2P_RETRY in [int(v) for v in sts]:
+                    raise P2PRetry("peer-to-peer merge epoch abandoned by every rank: retrying over RCCL")
+                raise local_error
             if not defer_status:
                 p2p.check_status(merged)
             return merged

@@ -38,6 +38,18 @@ def test_steal_respects_geometry_pins_and_slots():
     assert 1 not in a._slots
 
 
+def test_no_handover_on_unleased_slot_zero():
+    """Slot 0 is every unscheduled thread's: another thread may be running a scan there right now
+    (advisor r4), so its buffers are never handed over and runs there pin nothing."""
+    g = ("cpu", 1, 100, 2, 0, 2048, False, True, False)
+    a = _Fake(g)
+    a._slots = {0: a._slots[1]}
+    DE._geom_register(a, 0, g)
+    me = _Fake(g)
+    assert DE._steal(me, 0, g) is None
+    assert 0 in a._slots
+
+
 @pytest.mark.gpu
 def test_parameterizations_share_one_table_per_slot():
     """Two parameterizations of one large group-by (dense HBM table with a first-touch byte table)

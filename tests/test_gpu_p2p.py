@@ -27,3 +27,44 @@ def test_p2p_merge_two_ranks_on_one_gpu(tmp_path):
     assert r["synthetic_equal"] and r["failed_status_seen"]
     assert all(r["engine_equal"].values()), r["engine_equal"]
     assert r["engine_rows"]["TPCH Q1"] > 0 and r["engine_rows"]["TPCH Q5"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_p2p_selftest_failure_falls_back(tmp_path):
+    """One rank's known-value self-test fails (test hook): no rank uses the exchange, and every
+    headline statement completes over the collective path with the same answers."""
+    from spark_druid_olap_amd.utils.launch import spawn_ranks
+
+    out = tmp_path / "p2p_selftest.json"
+    env = dict(os.environ, SDO_GLOO_GPU="1", MASTER_ADDR="127.0.0.1", SDO_P2P_SELFTEST_FAIL="1")
+    rc = spawn_ranks(2, [sys.executable, os.path.join(ROOT, "tools", "p2p_check.py"), "--out", str(out),
+                         "--sf", "0.05", "--scenario", "selftest_fail"], env=env)
+    assert rc == 0
+    r = json.loads(out.read_text())
+    print(json.dumps(r)[:3000])
+    assert r["p2p_stats"] == {"built": True, "enabled": False}, r["p2p_stats"]
+    assert all(r["engine_equal"].values()), r["engine_equal"]
+    assert r["engine_rows"]["TPCH Q1"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_p2p_soft_timeout_retries_over_collectives(tmp_path):
+    """Rank 1 launches one merge 1.5 s late: rank 0's soft wait (0.5 s) expires, both ranks read
+    the abandoned verdict, and the statement re-runs over the collective path -- one retry, the
+    same answers, the exchange still enabled afterwards."""
+    from spark_druid_olap_amd.utils.launch import spawn_ranks
+
+    out = tmp_path / "p2p_delay.json"
+    env = dict(os.environ, SDO_GLOO_GPU="1", MASTER_ADDR="127.0.0.1", SDO_P2P_DELAY="rank=1,s=1.5,times=1",
+               SDO_P2P_TIMEOUT_S="0.5")
+    rc = spawn_ranks(2, [sys.executable, os.path.join(ROOT, "tools", "p2p_check.py"), "--out", str(out),
+                         "--sf", "0.05", "--scenario", "delay"], env=env)
+    assert rc == 0
+    r = json.loads(out.read_text())
+    print(json.dumps(r)[:3000])
+    st = r["p2p_stats"]
+    assert st["enabled"] and st["retries"] == 1 and st["selftest"] is True, st
+    assert sum(r["retried_statements"].values()) == 1, r["retried_statements"]
+    assert all(r["engine_equal"].values()), r["engine_equal"]

@@ -16,6 +16,19 @@ card -- IPC mappings work within a device as across xGMI).  Checks, on every ran
 Run as ONE process it times the same queries on one rank at the same per-rank scale factor (the
 baseline the 2-rank phases compare against; tools/rehearsal.py runs both).
 
+Per-phase times are GPU-event times (``SDO_PHASE_EVENTS``: HIP events recorded on the compute
+stream at the scan / merge / gather / finalize boundaries, ``gpu_*_ms``) next to the host stamps
+(``*_ms``).  The non-P2P mode is labelled with the process group's backend (``gloo`` in the
+one-card rehearsal, ``nccl`` = RCCL across GPUs).
+
+Fail-safe scenarios (``--scenario``, tests/test_gpu_p2p.py):
+
+* ``selftest_fail`` (with ``SDO_P2P_SELFTEST_FAIL=<rank>``): the exchange's known-value self-test
+  fails on one rank, so no rank uses P2P and every statement completes over the collective path;
+* ``delay`` (with ``SDO_P2P_DELAY=rank=1,s=1.5,times=1``): one rank launches a merge after the
+  peers' soft wait expired; every rank abandons that epoch together and the statement re-runs over
+  the collective path with the same answer.
+
 Rank 0 writes a JSON report to ``--out``."""
 import argparse
 import json
@@ -97,7 +110,10 @@ def engine(world, dev, sf, out):
     sess.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)
     sess.sql(tpch.druid_ddl(source="orderLineItemPartSupplierBase", datasource="tpch", with_column_mapping=False))
     res, phases = {}, {}
-    for mode in (("p2p", "rccl") if world.size > 1 else ("local",)):
+    other = "gloo" if world.backend == "gloo" else "rccl"
+    modes = ("p2p", other) if world.size > 1 else ("local",)
+    retries = {}
+    for mode in modes:
         p2p.ENABLED = mode == "p2p"
         sess._plan_cache.clear()
         with results_on_root():
@@ -105,6 +121,9 @@ def engine(world, dev, sf, out):
                 df = sess.sql(q)
                 for _ in range(2):
                     df.run()
+                    for st in df.last_stats.get("druid", []):
+                        if (st.get("stats") or {}).get("p2p_retry"):
+                            retries[name] = retries.get(name, 0) + 1
                 ts, ph = [], {}
                 for _ in range(10):
                     world.barrier()
@@ -117,15 +136,19 @@ def engine(world, dev, sf, out):
                         for k, v in (st.get("stats") or {}).items():
                             if k.endswith("_ms"):
                                 ph.setdefault(k, []).append(v)
+                            if k == "p2p_retry":
+                                retries[name] = retries.get(name, 0) + 1
                 rows = sorted(tuple(round(x, 6) if isinstance(x, float) else x for x in r)
                               for r in b.to_pandas().itertuples(index=False, name=None))
                 res.setdefault(name, {})[mode] = rows
                 phases.setdefault(name, {})[mode] = {"ms": statistics.median(ts),
                                                     **{k: round(statistics.median(v), 4) for k, v in ph.items()}}
     p2p.ENABLED = True
+    out["p2p_stats"] = p2p.stats(world)
+    out["retried_statements"] = retries
     if world.rank == 0:
         if world.size > 1:
-            out["engine_equal"] = {n: r["p2p"] == r["rccl"] for n, r in res.items()}
+            out["engine_equal"] = {n: r["p2p"] == r[other] for n, r in res.items()}
         out["engine_rows"] = {n: len(next(iter(r.values()))) for n, r in res.items()}
         out["phases"] = phases
 
@@ -135,7 +158,9 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--sf", type=float, default=1.0, help="scale factor per rank")
     ap.add_argument("--skip-engine", action="store_true")
+    ap.add_argument("--scenario", default="normal", choices=["normal", "selftest_fail", "delay"])
     a = ap.parse_args()
+    os.environ.setdefault("SDO_PHASE_EVENTS", "1")
     import torch
 
     from spark_druid_olap_amd.parallel.world import init_world, shutdown
@@ -145,9 +170,10 @@ def main():
     assert dev.type == "cuda", "run with SDO_GLOO_GPU=1 on a GPU box"
     torch.cuda.set_device(dev)
     out = {"world": world.size, "rank": world.rank, "sf_per_rank": a.sf}
-    if world.size > 1:
+    out["scenario"] = a.scenario
+    if world.size > 1 and a.scenario == "normal":
         synthetic(world, dev, out)
-    if not a.skip_engine and (out.get("exchange") or world.size == 1):
+    if not a.skip_engine and (out.get("exchange") or world.size == 1 or a.scenario != "normal"):
         engine(world, dev, a.sf, out)  # (one rank: the same-SF baseline of the per-phase split)
     world.barrier()
     if world.rank == 0:

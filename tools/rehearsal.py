@@ -22,7 +22,7 @@ def main():
     a = ap.parse_args()
     from spark_druid_olap_amd.utils.launch import spawn_ranks
 
-    env = dict(os.environ, SDO_GLOO_GPU="1", MASTER_ADDR="127.0.0.1", SDO_P2P_TIMEOUT_S="30")
+    env = dict(os.environ, SDO_GLOO_GPU="1", MASTER_ADDR="127.0.0.1")
     rc = 0
     for n in (2, 1):
         path = f"{a.out}_{n}rank.json"
