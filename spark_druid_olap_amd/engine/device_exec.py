@@ -658,6 +658,22 @@ class PreparedScan:
             return out
         return Partials("dense", b.acc, None, [h.view(b.rows, self.m) for h in b.hll])
 
+    def fast_launch(self) -> Optional["_Bufs"]:
+        """``run()`` of a dense-LDS scan with a fused launch (engine/executor.py _SmallDenseRunner):
+        the slot's buffers after the reset + kernel are enqueued, or None when this slot's buffers
+        have no fused launch (the caller then takes ``run()``)."""
+        if current_slot() != 0:
+            pinned().add(id(self))
+        self._maybe_specialize()
+        b = self._bufs()
+        if b.run_args is None:
+            return None
+        native.run_scan(*b.run_args, native._stream(self.dev))
+        b.clean = False
+        for h8, h32 in zip(b.hll, b.hll32):  # scan-time u32 registers -> the byte registers
+            h8.copy_(h32)
+        return b
+
     # single-slot views (tests and tools inspect the implicit slot's buffers)
     @property
     def acc(self):

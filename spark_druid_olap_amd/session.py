@@ -32,7 +32,7 @@ from .sql import ast as A
 from .sql import plan as P
 from .sql.analyzer import Analyzer
 from .sql.druid_rewrite import DruidRewriter
-from .sql.execute import Batch, Executor
+from .sql.execute import Batch, Executor, FastStatement
 from .sql.optimizer import optimize
 from .sql.parser import ParseError, parse
 from .sql.types import AnalysisError, series_to_list, to_series
@@ -94,8 +94,25 @@ class DataFrame:
 
                 token = CancelToken(tmo)
         results_on_root, root_only_results, scope = _run_helpers()
-        ex = Executor(self.session, token)
         t0 = time.perf_counter()
+        if token is None:
+            # projections over one pushed query (sql/execute.py FastStatement): no operator dispatch
+            fast = self.__dict__.get("_fast")
+            if fast is None:
+                fast = self._fast = (FastStatement.compile(self.plan) or False) if self.plan is not None else False
+            if fast:
+                root_only = root_only_results() and self._root_only_safe()
+                with results_on_root(root_only):
+                    b, res, dst = self.session._with_sql(self.sql_text, lambda: fast.run(self.session))
+                if b is not None:
+                    self.last_stats = {"ms": (time.perf_counter() - t0) * 1e3, "druid": dst}
+                    return b
+                ex = Executor(self.session, token)
+                ex.preload(fast.dq, res)  # the general operators finish from the same result
+            else:
+                ex = Executor(self.session, token)
+        else:
+            ex = Executor(self.session, token)
         # results on rank 0 only (the caller asked, engine/executor.py results_on_root) unless a
         # pushed query's spec is parameterized by another query's result: every rank needs those
         root_only = root_only_results() and self._root_only_safe()

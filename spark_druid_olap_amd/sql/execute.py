@@ -40,12 +40,20 @@ class LazySeries:
     array (``arr``), so compiled projections and the serving encoder read it without a Series:
     a small query's result costs no pandas constructions unless a caller asks for pandas."""
 
-    __slots__ = ("make", "arr", "dc")
+    __slots__ = ("_make", "arr", "dc")
 
     def __init__(self, make, arr: Optional[np.ndarray] = None, dc=None):
         # dc: (dictionary-coded column, SQL type) when the values are a dictionary decode -- a
-        # gather then moves codes and decodes only the rows it keeps
-        self.make, self.arr, self.dc = make, arr, dc
+        # gather then moves codes and decodes only the rows it keeps.  make None: the Series is
+        # built from ``arr`` / ``dc`` (no closure per result column)
+        self._make, self.arr, self.dc = make, arr, dc
+
+    def make(self):
+        if self._make is not None:
+            return self._make()
+        if self.arr is not None:
+            return fast_series(self.arr)
+        return _dict_series(*self.dc)
 
 
 class LazyGather(LazySeries):
@@ -111,7 +119,7 @@ class Cols(dict):
 
 
 def lazy_series(arr: np.ndarray) -> LazySeries:
-    return LazySeries(lambda: fast_series(arr), arr)
+    return LazySeries(None, arr)
 
 
 class Batch:
@@ -425,6 +433,79 @@ class Executor:
         return Batch(p.refs, cols, n)
 
 
+class FastStatement:
+    """A repeated statement of the dashboard shape -- projections over ONE pushed query (the
+    reference's benchmark suite, ``TpchBenchMark.scala:137-291``, is all of this form) -- run without
+    the general operator dispatch: the pushed query's result columns become the batch directly and
+    each projection applies its compiled numpy closures (``_compile_proj``).  Built once per plan
+    (``compile``); ``run`` returns None whenever the general executor must answer instead (a
+    projection that needs the full evaluator for this result, an empty global aggregate), so the
+    answer is always the general executor's.  Saves the per-statement interpreter overhead that
+    dominates small queries' host latency (``tools/host_floor.py``)."""
+
+    __slots__ = ("dq", "projs", "colspec")
+
+    def __init__(self, dq, projs, colspec):
+        self.dq, self.projs, self.colspec = dq, projs, colspec
+
+    @staticmethod
+    def compile(plan) -> Optional["FastStatement"]:
+        projs = []
+        node = plan
+        while isinstance(node, P.Project):
+            projs.append(node)
+            node = node.child
+        if not isinstance(node, P.DruidQuery) or node.info.get("historical") or S.find_deferred(node.spec):
+            return None
+        if not isinstance(node.spec, (S.GroupByQuerySpec, S.TimeSeriesQuerySpec, S.TopNQuerySpec)):
+            return None
+        out = []
+        for pr in reversed(projs):  # innermost first
+            prog = pr.__dict__.get("_proj")
+            if prog is None:
+                pr._out = list(pr.output)
+                prog = pr._proj = [_compile_proj(e, r) for e, r in zip(pr.exprs, pr._out)]
+            if any(kind == "expr" and x is None for kind, x in prog):
+                return None
+            out.append((pr._out, [(kind, x, r.rid) for (kind, x), r in zip(prog, pr._out)]))
+        colspec = [(r.rid, name, sqlt, kind) for r, (name, sqlt, kind) in zip(node.refs, node.columns)]
+        return FastStatement(node, out, colspec)
+
+    def run(self, session):
+        """(batch, pushed query's result, druid stats); batch None = let the general executor
+        finish (it is handed the result: the pushed query does not run twice)."""
+        dq = self.dq
+        t0 = time.perf_counter()
+        res = session.run_druid(dq)
+        n = res.num_rows
+        stats = [{"spec": dq.spec, "ms": (time.perf_counter() - t0) * 1e3, "rows": n, "stats": res.stats}]
+        if n == 0 and dq.info.get("global_counts") is not None:
+            return None, res, stats
+        data = res.data
+        cols = Cols()
+        for rid, name, sqlt, kind in self.colspec:
+            dict.__setitem__(cols, rid, druid_value_lazy(data[name], sqlt, kind, n))
+        refs = dq.refs
+        if n > _NP_FAST_MAX_ROWS and any(kind != "ref" for _, prog in self.projs for kind, _, _ in prog):
+            return None, res, stats
+        for out_refs, prog in self.projs:
+            nc = Cols()
+            for kind, x, rid in prog:
+                if kind == "ref":
+                    v = dict.get(cols, x)
+                    if v is None:
+                        return None, res, stats
+                    dict.__setitem__(nc, rid, v)
+                    continue
+                try:
+                    a = x(cols)
+                except _NoFast:
+                    return None, res, stats
+                dict.__setitem__(nc, rid, lazy_series(a))
+            cols, refs = nc, out_refs
+        return Batch(refs, cols, n), res, stats
+
+
 def share_key(p: P.DruidQuery) -> str:
     key = p.__dict__.get("_share_key")
     if key is None:
@@ -596,9 +677,9 @@ def _np_compile(e: A.Expr):
             def div(cols):
                 lf = np.asarray(fl(cols), dtype=np.float64)
                 rf = np.asarray(fr_(cols), dtype=np.float64)
-                with np.errstate(divide="ignore", invalid="ignore"):
-                    out = lf / rf
-                return np.where(rf == 0, np.nan, out)      # x / 0 is NULL in Spark SQL
+                # x / 0 is NULL in Spark SQL (NaN here); no floating-point state switch per call
+                out = np.full(np.broadcast(lf, rf).shape, np.nan)
+                return np.divide(lf, rf, out=out, where=rf != 0)
             return div
         t = base(typeof(e))
         if t not in _INT_T and t not in ("double", "float"):
@@ -705,16 +786,27 @@ def druid_value_lazy(col, sqlt: str, kind: str, n: int):
         from ..engine.columns import DictColumn as _DC
 
         _DictColumn = _DC
-    if isinstance(col, _DictColumn):
-        return LazySeries(lambda: _dict_series(col, sqlt), dc=(col, sqlt))
+    if type(col) is _DictColumn:
+        return LazySeries(None, None, (col, sqlt))
     if kind != "time":
+        if type(col) is np.ndarray:
+            # (the common numeric result columns: already at their final numpy dtype)
+            conv = _LAZY_CONV.get((col.dtype, sqlt))
+            if conv is not None:
+                return LazySeries(None, col if conv is True else col.astype(conv))
         arr = np.asarray(col)
         bt = base(sqlt)
         if arr.dtype.kind in "fiu" and bt in ("double", "float", "decimal"):
+            _LAZY_CONV[(arr.dtype, sqlt)] = True if arr.dtype == np.float64 else np.float64
             return lazy_series(arr.astype(np.float64, copy=False))
         if arr.dtype.kind in "iu" and bt in ("tinyint", "smallint", "int", "bigint"):
-            return lazy_series(arr if (arr.dtype == np.int32 and bt != "bigint") else arr.astype(np.int64, copy=False))
+            keep = arr.dtype == np.int64 or (arr.dtype == np.int32 and bt != "bigint")
+            _LAZY_CONV[(arr.dtype, sqlt)] = True if keep else np.int64
+            return lazy_series(arr if keep else arr.astype(np.int64))
     return druid_value_series(col, sqlt, kind, n)
+
+
+_LAZY_CONV: Dict[tuple, object] = {}  # (numpy dtype, SQL type) -> True (as is) | target dtype
 
 
 def _categorical(codes: np.ndarray, dtype) -> pd.Categorical:

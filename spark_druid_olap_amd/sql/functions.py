@@ -793,8 +793,17 @@ def _half_up(x: float, d: int) -> float:
 
 
 def _half_up_np(arr, d):
-    m = 10.0 ** d
-    return np.sign(arr) * np.floor(np.abs(arr) * m + 0.5 + 1e-9) / m
+    """ROUND(x, d) half away from zero (the magnitude rounded, the sign copied back)."""
+    a = np.abs(np.asarray(arr, dtype=np.float64))
+    if d:
+        m = 10.0 ** d
+        a *= m
+    a += 0.5
+    a += 1e-9
+    np.floor(a, out=a)
+    if d:
+        a /= m
+    return np.copysign(a, arr)
 
 
 @_reg("rand random", _const("double"))
