@@ -129,6 +129,8 @@ CONF_ENTRIES: List[ConfEntry] = [
     ConfEntry("spark.sparklinedata.druid.topNMaxThreshold", 100000, "max TopN threshold", int),
     ConfEntry("spark.sparklinedata.druid.option.use.v2.groupByEngine", False, "groupByStrategy v2 hint", bool),
     ConfEntry("spark.sparklinedata.enable.druid.query.history", False, "record executed Druid queries", bool),
+    ConfEntry("spark.sparklinedata.druid.window.rankone.pushdown", True,
+              "pre-filter rank()/dense_rank() = 1 windows over a pushed groupBy on the device", bool),
     ConfEntry("spark.sparklinedata.modules", "", "extra planner modules (python import paths)"),
     # MI355X engine knobs (new)
     ConfEntry("spark.sparklinedata.druid.approxCountDistinct", False,

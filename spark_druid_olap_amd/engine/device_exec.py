@@ -666,12 +666,11 @@ class PreparedScan:
             pinned().add(id(self))
         self._maybe_specialize()
         b = self._bufs()
-        if b.run_args is None:
+        if b.run_args is None or b.hll32:
             return None
-        native.run_scan(*b.run_args, native._stream(self.dev))
+        # clean: the previous fast run re-initialised the buffers behind its result copy
+        native.run_scan(*(b.noreset_args if b.clean else b.run_args), native._stream(self.dev))
         b.clean = False
-        for h8, h32 in zip(b.hll, b.hll32):  # scan-time u32 registers -> the byte registers
-            h8.copy_(h32)
         return b
 
     # single-slot views (tests and tools inspect the implicit slot's buffers)

@@ -143,8 +143,14 @@ class _SmallDenseRunner:
         if b is None:
             return None
         prog = self.prog
-        part = Partials("dense", b.acc, None, [h.view(b.rows, prep.m) for h in b.hll])
-        cols = finalize(prog, part, getattr(self.pq, "out_types", None))
+        from .partials import _fetch_small
+
+        hll = [h.view(b.rows, prep.m) for h in b.hll]
+        G = b.rows
+        host = _fetch_small(b.acc, hll if prog.nhll else [], G, prog.hll_p, None, b.run_args[1:7])
+        b.clean = True  # (reset behind the copies: the next run launches the scan alone)
+        part = Partials("dense", b.acc, None, hll)
+        cols = finalize(prog, part, getattr(self.pq, "out_types", None), prefetched=host)
         res = QueryResult(self.out_cols, {c: cols[c] for c in self.out_cols}, self.qt,
                           {"groups": len(cols["__rows__"]), "exec_ms": (time.perf_counter() - t0) * 1e3})
         self.pq.last_stats = res.stats
@@ -545,6 +551,7 @@ class PreparedQuery:
                                   finish="local" if self.world.distributed else "all", defer_status=True)
         merged = part
         part, hv = self._device_having(prog, part)
+        part = self._device_extreme(prog, part, hv)
         part = self._device_prune(prog, part, hv)
         if part is not merged:
             from ..parallel.p2p import check_status
@@ -765,6 +772,66 @@ class PreparedQuery:
         keep = torch.nonzero(mask).flatten()
         return Partials("sparse", part.acc.index_select(0, keep), part.keys.index_select(0, keep),
                         [x.index_select(0, keep) for x in part.hll], part.scattered, part.status), True
+
+    def _device_extreme(self, prog: ScanProgram, part: Partials, having_done: bool = True) -> Partials:
+        """``rank() / dense_rank() OVER (PARTITION BY p ORDER BY metric) = 1`` above this groupBy
+        (sql/window.py push_rank_one): keep only the groups whose metric equals their partition's
+        minimum (maximum for DESC) -- rank 1 under either function -- ON THE DEVICE, so ~10^5 groups
+        are not decoded and shipped to be ranked on the host.  Partition ids are the groups' key
+        components (or functionally dependent keys through their FD tables); over per-rank disjoint
+        slices the per-partition extremes are all-reduced.  Left to the host when the HAVING could
+        not be applied here first, when a metric value is NaN (Spark sorts NaN last), or when the
+        partition space is too large for a table."""
+        pe = getattr(self, "partition_extreme", None)
+        if not pe or self.qs.queryType != "groupBy" or prog.thetas or any(kc.collapse for kc in prog.keys):
+            return part
+        pnames, metric, asc = pe
+        agg = next((a for a in prog.aggs if a.name == metric), None)
+        if agg is None or agg.slot < 0 or agg.kind not in ("count", "sum_i", "sum_f", "min_i", "max_i", "min_f",
+                                                          "max_f") or not having_done:
+            return part
+        if part.kind == "dense":
+            part = part.compact()
+        keys = part.keys
+        dev = keys.device
+        pid = torch.zeros_like(keys)
+        npart = 1
+        for name in pnames:
+            kc = next((k for k in prog.keys if k.name == name), None)
+            if kc is not None:
+                ids, card = torch.remainder(torch.div(keys, kc.stride, rounding_mode="floor"), max(1, kc.card)), \
+                    max(1, kc.card)
+            else:
+                d = next(((k, det, lut) for k, det, lut in getattr(prog, "derived", ()) if k.name == name), None)
+                if d is None:
+                    return part
+                k, det, lut = d
+                kd = prog.keys[det]
+                did = torch.remainder(torch.div(keys, kd.stride, rounding_mode="floor"), max(1, kd.card))
+                if kd.orig is not None:
+                    did = torch.as_tensor(np.asarray(kd.orig, dtype=np.int64), device=dev)[did]
+                lut_t = torch.as_tensor(lut).to(device=dev, dtype=torch.int64)
+                ids, card = lut_t[did], max(1, int(getattr(k, "card", 0)) or int(lut_t.max().item()) + 1)
+            npart *= card
+            if npart > (1 << 22):
+                return part
+            pid = pid * card + ids
+        col = part.acc[:, agg.slot]
+        if agg.kind == "sum_f":
+            v = col.contiguous().view(torch.float64)
+        elif agg.kind in ("min_f", "max_f"):
+            v = torch.where(col >= 0, col, col ^ 0x7FFFFFFFFFFFFFFF).view(torch.float64)
+        else:
+            v = col.to(torch.float64)
+        if part.rows and bool(torch.isnan(v).any()):
+            return part
+        ext = torch.full((npart,), math.inf if asc else -math.inf, dtype=torch.float64, device=dev)
+        ext.scatter_reduce_(0, pid, v, reduce="amin" if asc else "amax", include_self=True)
+        if part.scattered and self.world.distributed:
+            ext = self.world.all_reduce(ext, "min" if asc else "max")
+        keep = torch.nonzero(v == ext[pid]).flatten()
+        return Partials("sparse", part.acc.index_select(0, keep), keys.index_select(0, keep),
+                        [h.index_select(0, keep) for h in part.hll], part.scattered, part.status)
 
     def _device_prune(self, prog: ScanProgram, part: Partials, having_done: bool = True) -> Partials:
         """ORDER BY <aggregate> LIMIT k (groupBy limitSpec) and numeric topN, applied to the merged

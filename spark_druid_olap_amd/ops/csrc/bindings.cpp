@@ -490,6 +490,28 @@ static void fetch_small(uint64_t acc, int64_t acc_bytes, std::vector<uint64_t> h
   wait_stream(st, "fetch_small sync");
 }
 
+// fetch_small, then this scan's buffers reset for its next execution -- enqueued behind the copies
+// while the scan still runs, so the reset leaves the next launch's critical path; the host waits
+// for the copies only (an event recorded before the reset), not for the reset.
+static void fetch_small_reset(uint64_t acc, int64_t acc_bytes, std::vector<uint64_t> hll, int64_t G, int p,
+                              uint64_t est_dev, uint64_t host, uint64_t init, int64_t rows, int nslots,
+                              std::vector<uint64_t> zptr, std::vector<int64_t> zwords, uint64_t overflow,
+                              uint64_t stream) {
+  hipStream_t st = (hipStream_t)stream;
+  thread_local hipEvent_t ev = nullptr;
+  if (!ev) check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "fetch_small_reset event");
+  for (size_t i = 0; i < hll.size(); ++i) hll_estimate(hll[i], G, p, est_dev + i * (uint64_t)G * 8, stream);
+  if (acc_bytes > 0)
+    check(hipMemcpyAsync((void*)host, (const void*)acc, acc_bytes, hipMemcpyDeviceToHost, st), "fetch_small acc");
+  if (!hll.empty())
+    check(hipMemcpyAsync((void*)(host + acc_bytes), (const void*)est_dev, hll.size() * G * 8, hipMemcpyDeviceToHost, st),
+          "fetch_small est");
+  check(hipEventRecord(ev, st), "fetch_small_reset record");
+  reset_bufs(acc, init, rows, nslots, zptr, zwords, overflow, stream);
+  py::gil_scoped_release nogil;
+  check(hipEventSynchronize(ev), "fetch_small_reset wait");
+}
+
 static void stream_sync(uint64_t stream) {
   py::gil_scoped_release nogil;
   wait_stream((hipStream_t)stream, "stream sync");
@@ -874,6 +896,7 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("p2p_merge", &p2p_merge);
   m.def("run_scan", &run_scan);
   m.def("fetch_small", &fetch_small);
+  m.def("fetch_small_reset", &fetch_small_reset);
   m.def("stream_sync", &stream_sync);
   m.def("glds_probe", &glds_probe);
   m.def("part_scan", &part_scan);

@@ -351,5 +351,16 @@ def fetch_small(acc: torch.Tensor, hll: Sequence[torch.Tensor], G: int, p: int, 
 
 
 
+def fetch_small_reset(acc: torch.Tensor, hll: Sequence[torch.Tensor], G: int, p: int, est_dev: torch.Tensor,
+                      host: torch.Tensor, reset_args: tuple) -> None:
+    """``fetch_small`` + the scan's buffer reset for its next run enqueued behind the copies; waits
+    for the copies only.  ``reset_args``: a prepared scan's cached (init, rows, nslots, zero
+    pointers, zero words, overflow) -- the reset half of its fused launch arguments (the
+    accumulator table reset is ``acc`` itself)."""
+    nb = acc.numel() * acc.element_size()
+    load().fetch_small_reset(acc.data_ptr(), nb, [h.data_ptr() for h in hll], int(G), int(p), est_dev.data_ptr(),
+                             host.data_ptr(), *reset_args, _stream(acc.device))
+
+
 def stream_sync(dev) -> None:
     load().stream_sync(_stream(dev))

@@ -473,6 +473,10 @@ class Session:
             for rule in getattr(m, "logical_rules", []) or []:
                 opt = rule(opt, self) or opt
         phys = rw.rewrite(opt)
+        if self.conf.typed("spark.sparklinedata.druid.window.rankone.pushdown"):
+            from .sql.window import push_rank_one
+
+            phys = push_rank_one(phys)  # rank() = 1 over a pushed aggregate: a device pre-filter
         for m in self.modules:
             for rule in getattr(m, "physical_rules", []) or []:
                 phys = rule(phys, self) or phys
@@ -566,7 +570,11 @@ class Session:
                     with T.span("sdo.lower"):
                         prep = self.engine.prepare(run_spec, ds, dq.info.get("historical"))
                     # output SQL types: large results decode numeric dictionary keys on the device
-                    prep.out_types = {n: t for n, t, k in dq.columns if k == "value"}
+                    # (and integer outputs of string-valued extractions: 'yyyy' time formats)
+                    prep.out_types = {n: t for n, t, k in dq.columns
+                                      if k == "value" or (k == "string" and t in ("tinyint", "smallint", "int", "bigint"))}
+                    # rank() = 1 window above (sql/window.py push_rank_one): device pre-filter
+                    prep.partition_extreme = dq.info.get("partition_extreme")
                     dq._prepared = prep
                     dq._prepared_spec = spec
         return prep

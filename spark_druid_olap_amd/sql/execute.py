@@ -512,7 +512,8 @@ def share_key(p: P.DruidQuery) -> str:
         import json
 
         key = p._share_key = json.dumps(p.spec.to_json(), sort_keys=True, default=str) + \
-            str(id(p.relation.info.datasource)) + repr(p.info.get("historical"))
+            str(id(p.relation.info.datasource)) + repr(p.info.get("historical")) + \
+            repr(p.info.get("partition_extreme"))
     return key
 
 

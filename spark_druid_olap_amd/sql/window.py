@@ -230,3 +230,109 @@ def evaluate_window(w: A.WindowExpr, fr: Frame, cache: Optional[dict] = None) ->
     if nl.any():
         s = s.astype(object).where(~pd.Series(nl), None)
     return s
+
+
+# ------------------------------------------------------------------------------------------------
+# rank() / dense_rank() = 1 over a pushed aggregate -> a device pre-filter
+#
+# The BI plan's "MinCost Supplier by Part in each Region" template (docs/bi-benchmark/
+# snap-sales-demo.jmx) ranks ~10^5 groups of a pushed groupBy per region by sum(ps_supplycost) and
+# keeps rank 1: the reference ships every group to Spark's WindowExec.  Rank 1 of rank() and of
+# dense_rank() is exactly "the value equals the partition's minimum" (maximum for DESC), so the
+# engine can drop every other group on the device (engine/executor.py _device_extreme) before the
+# groups are decoded and shipped; the host window and filter still run, over the survivors, and
+# return the same rows (all survivors have rank 1 among themselves).
+def _rank_one_rid(cond) -> Optional[int]:
+    """The window-output ref id that the filter condition pins to 1 (as ``= 1`` or ``<= 1`` / ``< 2``
+    in a conjunction), else None."""
+    if isinstance(cond, A.BinOp) and cond.op == "and":
+        return _rank_one_rid(cond.l) or _rank_one_rid(cond.r)
+    if not isinstance(cond, A.BinOp):
+        return None
+    l, r, op = cond.l, cond.r, cond.op
+    if isinstance(l, A.Lit) and isinstance(r, A.Ref):
+        l, r = r, l
+        op = {"<=": ">=", ">=": "<=", "<": ">", ">": "<"}.get(op, op)
+    if not isinstance(l, A.Ref) or not isinstance(r, A.Lit) or isinstance(r.value, bool) or \
+            not isinstance(r.value, (int, float)):
+        return None
+    if (op == "=" and r.value == 1) or (op == "<=" and 1 <= r.value < 2) or (op == "<" and 1 < r.value <= 2):
+        return l.rid
+    return None
+
+
+_MONOTONE_CASTS = ("tinyint", "smallint", "int", "bigint", "float", "double")
+
+
+def _through_projects(rid: int, projs, monotone: bool = False) -> Optional[int]:
+    """Follow a column down a chain of projections (outermost first) as long as it is passed through
+    or renamed (``monotone``: or numerically cast -- an order-preserving map, so the device filter's
+    f64 comparison keeps a superset of the rank-1 rows); None when it is computed."""
+    from . import plan as P
+
+    for pr in projs:
+        nxt = None
+        for e in pr.exprs:
+            if P.out_ref(e).rid != rid:
+                continue
+            c = e.child if isinstance(e, A.Alias) else e
+            if monotone and isinstance(c, A.Cast) and c.to in _MONOTONE_CASTS:
+                c = c.child
+            if isinstance(c, A.Ref):
+                nxt = c.rid
+            break
+        if nxt is None:
+            return None
+        rid = nxt
+    return rid
+
+
+def push_rank_one(plan):
+    """Annotate pushed groupBys under ``Filter(rank = 1) <- Window(rank | dense_rank)`` with their
+    partition-extreme pre-filter (``info["partition_extreme"] = (partition output names, metric
+    name, ascending)``)."""
+    from ..query import spec as S
+    from . import plan as P
+
+    def rule(p):
+        if not isinstance(p, P.Filter) or not isinstance(p.child, P.Window):
+            return None
+        w = p.child
+        rid = _rank_one_rid(p.cond)
+        if rid is None or len(w.exprs) != 1 or P.out_ref(w.exprs[0]).rid != rid:
+            return None
+        we = w.exprs[0].child
+        if not isinstance(we, A.WindowExpr) or we.func.name not in ("rank", "dense_rank") or \
+                len(we.orders) != 1 or we.frame is not None:
+            return None
+        projs, node = [], w.child
+        while isinstance(node, P.Project):
+            projs.append(node)
+            node = node.child
+        if not isinstance(node, P.DruidQuery) or not isinstance(node.spec, S.GroupByQuerySpec) or \
+                node.spec.limitSpec is not None or node.info.get("partition_extreme"):
+            return None
+        o = we.orders[0]
+        if not isinstance(o.expr, A.Ref) or any(not isinstance(x, A.Ref) for x in we.partition):
+            return None
+        if o.nulls_first is not None and o.nulls_first != o.ascending:
+            return None  # (Spark's default null placement only: our aggregates are never NULL anyway)
+        by_rid = {r.rid: c for r, c in zip(node.refs, node.columns)}
+        m = _through_projects(o.expr.rid, projs, monotone=True)
+        parts = [_through_projects(x.rid, projs) for x in we.partition]
+        if m is None or m not in by_rid or any(x is None or x not in by_rid for x in parts):
+            return None
+        dims = {d.outputName for d in (node.spec.dimensions or [])}
+        aggs = {a.name for a in (node.spec.aggregations or [])}
+        metric = by_rid[m][0]
+        pnames = tuple(by_rid[x][0] for x in parts)
+        if metric not in aggs or any(n not in dims for n in pnames):
+            return None
+        dq = P.DruidQuery(node.relation, node.spec, node.columns, node.refs,
+                          dict(node.info, partition_extreme=(pnames, metric, bool(o.ascending))))
+        chain = dq
+        for pr in reversed(projs):
+            chain = P.Project(pr.exprs, chain)
+        return P.Filter(p.cond, P.Window(w.exprs, chain))
+
+    return plan.transform_up(rule)

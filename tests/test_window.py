@@ -74,6 +74,38 @@ def test_window_over_pushed_aggregate(ds_small, df_small):
     assert (m.rk == m.rk_e).all()
 
 
+@pytest.mark.parametrize("fn,order,partition", [("dense_rank", "asc", "p_mfgr"), ("rank", "desc", "p_mfgr"),
+                                                  ("rank", "asc", "p_mfgr, s_region"), ("dense_rank", "desc", "c_region")])
+def test_rank_one_pushdown(ds_small, df_small, fn, order, partition):
+    """rank() / dense_rank() = 1 over a pushed groupBy (the BI plan's MinCost template): the
+    groupBy carries a device pre-filter (sql/window.py push_rank_one) and the answer equals the
+    unpushed plan's and pandas'."""
+    from spark_druid_olap_amd.sql import plan as P
+
+    s = Session(engine=Engine(use_native=False))
+    s.register_datasource(ds_small)
+    s.register_table("orderLineItemPartSupplierBase", df_small, schema=tpch.FLAT_SCHEMA)
+    s.sql(tpch.druid_ddl(with_column_mapping=False))
+    keys = ["p_mfgr", "p_brand", "s_region", "c_region"]
+    q = (f"select {', '.join(keys)}, cnt from (select {', '.join(keys)}, count(*) cnt, "
+         f"{fn}() over (partition by {partition} order by sum(l_quantity) {order}) rk "
+         f"from orderLineItemPartSupplier group by {', '.join(keys)}) t where rk = 1")
+    d = s.sql(q)
+    dqs = P.find_all_deep(d.plan, P.DruidQuery)
+    assert dqs and dqs[0].info.get("partition_extreme") is not None
+    got = sorted(d.collect())
+    s.conf.set("spark.sparklinedata.druid.window.rankone.pushdown", "false")
+    s._plan_cache.clear()
+    d0 = s.sql(q)
+    assert not P.find_all_deep(d0.plan, P.DruidQuery)[0].info.get("partition_extreme")
+    assert got == sorted(d0.collect())
+    g = df_small.groupby(keys).agg(cnt=("l_quantity", "size"), q=("l_quantity", "sum")).reset_index()
+    parts = [x.strip() for x in partition.split(",")]
+    ext = g.groupby(parts).q.transform("min" if order == "asc" else "max")
+    want = sorted(tuple(r) for r in g[g.q == ext][keys + ["cnt"]].itertuples(index=False, name=None))
+    assert got == want
+
+
 def test_window_errors(sess):
     from spark_druid_olap_amd.sql.types import AnalysisError
 
