@@ -180,6 +180,21 @@ def main():
 
         prof.disable()
         pstats.Stats(prof, stream=sys.stderr).sort_stats("cumulative").print_stats(60)
+    # untimed, reported alongside: each query end to end INCLUDING host materialization of every result
+    # column (dictionary-coded strings decoded to Python objects, as the reference's df.collect() returns
+    # them): the timed value leaves string columns dictionary-coded (engine/columns.py DictColumn)
+    coll = {}
+    if args.mode == "sql":
+        with results_on_root(os.environ.get("SDO_RESULTS_ON_ROOT", "1") != "0"):
+            for _ in range(max(2, min(args.steps, 3))):
+                for name, pq in queries:
+                    a = time.perf_counter()
+                    b = pq.run()
+                    if world.rank == 0 and b is not None:
+                        for r in b.refs:
+                            b.cols[r.rid].to_numpy()
+                    coll.setdefault(name, []).append((time.perf_counter() - a) * 1e3)
+                world.barrier()
     shape_geo = None
     if args.mode == "sql" and not only and os.environ.get("SDO_BENCH_SHAPE", "1") != "0":
         # untimed, reported alongside: the same suite on the shape-shared kernels a first-seen
@@ -226,6 +241,8 @@ def main():
     nq = nsuite * args.steps
     mins = {k: world.max_float(min(v)) for k, v in lat.items()}
     maxs = {k: world.max_float(max(v)) for k, v in lat.items()}
+    cmeans = {k: world.max_float(sum(v) / len(v)) for k, v in coll.items()}
+    cgeo = math.exp(sum(math.log(max(m, 1e-6)) for m in cmeans.values()) / len(cmeans)) if cmeans else None
     if world.rank == 0:
         if args.verbose:
             for k, v in means.items():
@@ -271,6 +288,9 @@ def main():
             "per_query_ms": {k: round(v, 4) for k, v in means.items()},
             "per_query_min_ms": {k: round(v, 4) for k, v in mins.items()},
             "per_query_max_ms": {k: round(v, 4) for k, v in maxs.items()},
+            # untimed: run + decode of every result column to host objects (df.collect()'s work)
+            "collect_ms": {k: round(v, 4) for k, v in cmeans.items()} or None,
+            "collect_geomean_ms": round(cgeo, 4) if cgeo is not None else None,
             "rows_per_gpu": int(nrows),
             "hbm": hbm,
             # the timed steps run each prepared statement's literal-specialized kernel (compiled

@@ -25,7 +25,7 @@ from ..ops import desc as D
 from ..ops import native
 from .lower import ScanProgram, pack
 from .partials import Partials
-from .scheduler import current_slot, pinned
+from .scheduler import current_slot
 
 from ..planner.cost import PLAN_LDS_BUDGET as LDS_BUDGET  # noqa: E402  (single source: the cost model)
 # one accumulator table per workgroup (JIT only) for key spaces whose per-wave copies do not fit:
@@ -262,28 +262,90 @@ class PreparedScan:
     # ------------------------------------------------------------------ buffers
     # Every execution slot (engine/scheduler.py) gets its own accumulators / hash table / HLL
     # registers / descriptor, so concurrent runs of one prepared query on different streams never
-    # share device state; the generated kernel, grid and mode are shared.
+    # share device state; the generated kernel, grid and mode are shared.  Leased slots carve the
+    # large tensors from the slot's arena (SlotArena), slot 0 allocates them per scan.
     def _bufs(self) -> "_Bufs":
         slot = current_slot()
         b = self._slots.get(slot)
+        if slot != 0:
+            return self._arena_bufs(slot, b, self.cap)
         if b is None:
             # allocated without holding this scan's lock: an out-of-memory eviction takes the locks
             # of the scans it evicts, and two threads each holding their own scan's lock while
-            # evicting the other's would deadlock (one slot runs one statement at a time, so two
-            # allocations for one (scan, slot) do not race in practice; the re-check keeps one)
-            # another prepared scan's idle buffers of the same geometry on this slot (another
-            # parameterization of one dashboard statement) are taken over instead of allocating
-            victim = _steal(self, slot, self._geom(self.cap))
-            nb = _with_eviction(lambda: self._alloc(self.cap, victim), self, slot)
+            # evicting the other's would deadlock
+            nb = _with_eviction(lambda: self._alloc(self.cap), self, slot)
             with self._slot_lock:
                 b = self._slots.get(slot)
                 if b is None:
                     b = self._slots[slot] = nb
             _buffers_acquired(self, slot, b)
-            _geom_register(self, slot, b.geom)
         else:
             _buffers_used(self, slot)
         return b
+
+    def _rebuf(self, cap: int) -> "_Bufs":
+        """This slot's buffers re-made for a new capacity (hash-table growth / adaptive size)."""
+        slot = current_slot()
+        if slot != 0:
+            with self._slot_lock:
+                self._slots.pop(slot, None)
+            return self._arena_bufs(slot, None, cap)
+        nb = self._slots[slot] = _with_eviction(lambda: self._alloc(cap), self, slot)
+        _buffers_acquired(self, slot, nb)
+        return nb
+
+    def _tensor_layout(self, cap: int) -> list:
+        """(name, elements, dtype, shape) of the large per-slot tensors, in carving order."""
+        prog = self.prog
+        rows = self._rows(cap)
+        nblocks = prog.nhll_total if self.stored_fused else prog.nhll
+        if self.pres_bytes:
+            # padded to whole 8-byte words (the fused reset zeroes words; padding bytes stay 0
+            # and never compact)
+            items = [("acc", (rows + 7) // 8 * 8, torch.uint8, None)]
+        else:
+            items = [("acc", rows * prog.nslots, torch.int64, (rows, prog.nslots))]
+        items.append(("keys", rows if self.mode == D.M_HASH else 1, torch.int64, None))
+        # byte registers (sdo_device.h hll_update8 / hll_merge_word8): the partials, the wire and
+        # the estimator all read u8; scan-time u32 registers (narrowed into them after each run)
+        items += [("hll", rows * self.m, torch.uint8, None)] * nblocks
+        if self.hll32:
+            items += [("hll32", rows * self.m, torch.int32, None)] * nblocks
+        # (padded to whole 64-group words: native.touch_compact reads it 16 bytes per lane)
+        items.append(("touch", ((rows + 63) // 64 * 64) if self.touch else 64, torch.uint8, None))
+        return items
+
+    def _arena_bufs(self, slot: int, b: Optional["_Bufs"], cap: int) -> "_Bufs":
+        from .scheduler import slot_epoch
+
+        ar = slot_arena(self.dev, slot)
+        ep = slot_epoch(slot)
+        if b is not None and b.arena is not None and b.arena[0] == ar.gen and b.arena[2] == ep:
+            return b  # already carved in this statement
+        items = self._tensor_layout(cap)
+        sizes = [n * torch.empty((), dtype=dt).element_size() for _, n, dt, _ in items]
+        offs, total = _carve_aligned(sizes)
+        gen, off, intact = ar.carve(total, self)
+        if b is not None and b.arena is not None and b.arena[:2] == (gen, off) and b.cap == cap:
+            b.arena = (gen, off, ep)
+            if not intact:
+                b.clean = False  # another scan wrote over the region: the next launch resets it
+            return b
+        v = _Bufs()
+        v.geom = self._geom(cap)
+        v.hll, v.hll32 = [], []
+        for (name, n, dt, shape), o in zip(items, offs):
+            t = ar.view(off + o, n, dt, shape)
+            if name in ("hll", "hll32"):
+                getattr(v, name).append(t)
+            else:
+                setattr(v, name, t)
+        v.overflow = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        nb = self._alloc(cap, v)
+        nb.arena = (gen, off, ep)
+        with self._slot_lock:
+            self._slots[slot] = nb
+        return nb
 
     def _settle(self) -> None:
         """The LDS-budget mode fallback, decided at prepare time without allocating: buffers are
@@ -309,9 +371,9 @@ class PreparedScan:
                 bool(self.touch), bool(self.pres_bytes))
 
     def _alloc(self, cap: int, reuse: Optional["_Bufs"] = None) -> "_Bufs":
-        """This slot's buffers -- the large tensors taken over from ``reuse`` (another prepared
-        scan's buffers of the same geometry, whose state is then unknown: the first run resets
-        them) -- with this scan's own descriptor and launch arguments."""
+        """This slot's buffers -- the large tensors given by ``reuse`` (views of the slot's arena,
+        whose contents are unknown: the first run resets them) or allocated here -- with this scan's
+        own descriptor and launch arguments."""
         from .lower import lds_layout
 
         prog, dev = self.prog, self.dev
@@ -321,30 +383,23 @@ class PreparedScan:
         b.rows = rows
         b.geom = self._geom(cap)
         b.init_row = _init_row(dev, tuple(int(init) for _, init in prog.slots))
-        nblocks = prog.nhll_total if self.stored_fused else prog.nhll
+        b.arena = None
         if reuse is not None and getattr(reuse, "geom", None) == b.geom:
             b.acc, b.keys, b.hll, b.hll32 = reuse.acc, reuse.keys, reuse.hll, reuse.hll32
             b.overflow, b.touch = reuse.overflow, reuse.touch
             if self.touch:
                 b.touch.zero_()  # (the first-touch invariant: every byte clear between runs)
         else:
-            if self.pres_bytes:
-                # padded to whole 8-byte words (the fused reset zeroes words; padding bytes stay 0
-                # and never compact)
-                b.acc = torch.empty(((rows + 7) // 8 * 8,), dtype=torch.uint8, device=dev)
-            else:
-                b.acc = torch.empty((rows, prog.nslots), dtype=torch.int64, device=dev)
-            b.keys = torch.empty(rows if self.mode == D.M_HASH else 1, dtype=torch.int64, device=dev)
-            # byte registers (sdo_device.h hll_update8 / hll_merge_word8): the partials, the wire and
-            # the estimator all read u8
-            b.hll = [torch.empty(rows * self.m, dtype=torch.uint8, device=dev) for _ in range(nblocks)]
-            # scan-time u32 registers (narrowed into b.hll after each run) or none: the kernel
-            # updates b.hll's bytes directly
-            b.hll32 = [torch.empty(rows * self.m, dtype=torch.int32, device=dev) for _ in range(nblocks)] \
-                if self.hll32 else []
+            b.hll, b.hll32 = [], []
+            for name, n, dt, shape in self._tensor_layout(cap):
+                t = torch.empty(n, dtype=dt, device=dev)
+                t = t.view(shape) if shape is not None else t
+                if name in ("hll", "hll32"):
+                    getattr(b, name).append(t)
+                else:
+                    setattr(b, name, t)
             b.overflow = torch.zeros(1, dtype=torch.int32, device=dev)
-            # (padded to whole 64-group words: native.touch_compact reads it 16 bytes per lane)
-            b.touch = torch.zeros(((rows + 63) // 64 * 64) if self.touch else 64, dtype=torch.uint8, device=dev)
+            b.touch.zero_()
         b.clean = False
         hll_offs = []
         off = prog.G * prog.nslots * 8 * (BLOCK // 64)
@@ -600,8 +655,6 @@ class PreparedScan:
 
     # ------------------------------------------------------------------ run
     def run(self) -> Partials:
-        if current_slot() != 0:
-            pinned().add(id(self))  # (its buffers hold this statement's partials: not to be taken over)
         self._maybe_specialize()
         prog = self.prog
         b = self._bufs()
@@ -640,8 +693,7 @@ class PreparedScan:
                 break
             if int(b.overflow.item()) == 0:
                 break
-            b = self._slots[current_slot()] = self._alloc(b.cap * 4)  # grow and retry
-            _buffers_acquired(self, current_slot(), b)
+            b = self._rebuf(b.cap * 4)  # grow and retry
             self.cap = max(self.cap, b.cap)
         if self.mode == D.M_HASH:
             valid = _nonzero_big(b.keys != -1)
@@ -653,8 +705,7 @@ class PreparedScan:
             want = _next_pow2(2 * int(valid.numel()) + 1024)
             if want * 4 <= b.cap:
                 self.cap = want
-                nb = self._slots[current_slot()] = self._alloc(want)
-                _buffers_acquired(self, current_slot(), nb)
+                self._rebuf(want)
             return out
         return Partials("dense", b.acc, None, [h.view(b.rows, self.m) for h in b.hll])
 
@@ -662,8 +713,6 @@ class PreparedScan:
         """``run()`` of a dense-LDS scan with a fused launch (engine/executor.py _SmallDenseRunner):
         the slot's buffers after the reset + kernel are enqueued, or None when this slot's buffers
         have no fused launch (the caller then takes ``run()``)."""
-        if current_slot() != 0:
-            pinned().add(id(self))
         self._maybe_specialize()
         b = self._bufs()
         if b.run_args is None or b.hll32:
@@ -789,10 +838,16 @@ def _buffers_acquired(prep, slot, b) -> None:
                 p._slots.pop(sl, None)
 
 
-def release_device_memory(keep=None) -> None:
-    """Drop every prepared scan's cached slot buffers (but ``keep``'s (prep, slot)), the shared
-    scratch and the allocator's free blocks.  A scan running on a dropped slot keeps its tensors
-    alive through its own references until it finishes."""
+def release_device_memory(keep=None, keep_arena=None) -> None:
+    """Drop every prepared scan's cached slot buffers (but ``keep``'s (prep, slot)), the other slots'
+    arenas (but ``keep_arena``), the shared scratch and the allocator's free blocks.  A scan running
+    on a dropped slot keeps its tensors alive through its own references until it finishes."""
+    from ..utils.metrics import count_event
+
+    count_event("device_memory_release")
+    for ar in list(_ARENAS.values()):
+        if ar is not keep_arena and ar.slot != (keep[1] if keep else None):
+            ar.release()
     victims = []
     with _buf_lock:
         for k in list(_buf_lru):
@@ -810,14 +865,17 @@ def release_device_memory(keep=None) -> None:
     torch.cuda.empty_cache()
 
 
-def _with_eviction(fn, prep, slot):
+def _with_eviction(fn, prep, slot, arena=None):
     """Run an allocation; on a device out-of-memory error release every other prepared scan's
-    cached slot buffers (least recently used first: all of them) and the allocator's free blocks,
-    then try once more."""
+    cached slot buffers, the other slots' arenas and the allocator's free blocks, then try once
+    more."""
     try:
         return fn()
     except torch.OutOfMemoryError:
-        release_device_memory(keep=(id(prep), slot))
+        import logging
+
+        logging.getLogger(__name__).warning("device out of memory on slot %s: releasing cached buffers", slot)
+        release_device_memory(keep=(id(prep), slot), keep_arena=arena)
         return fn()
 
 
@@ -849,57 +907,117 @@ def _settle_forgotten() -> None:
 class _Bufs:
     """One execution slot's device buffers for a prepared scan."""
     __slots__ = ("cap", "rows", "init_row", "acc", "keys", "hll", "hll32", "overflow", "desc", "touch", "clean",
-                 "run_args", "noreset_args", "part", "geom", "__weakref__")
+                 "run_args", "noreset_args", "part", "geom", "arena", "__weakref__")
 
 
-# Buffer hand-over between prepared scans of equal geometry (_Bufs.geom) on one execution slot.
-# A BI dashboard sends one statement shape with many parameterizations; each is its own prepared
-# scan, and without hand-over each would hold its own copy of (say) a 150M-group table per slot.
-# A scan's buffers may be taken only while no statement of this thread can still read them: scans
-# run by the thread's current statement are pinned (``_pin`` in run(), released with the slot
-# lease: engine/scheduler.py pinned) -- a slot runs one statement at a time, so other threads never hold
-# this slot's buffers.
-_GEOM: dict = {}      # (slot, geom) -> {id(prep): weakref(prep)}
-_geom_lock = threading.Lock()
+# Slot arenas.  A BI dashboard sends many statement shapes and parameterizations; caching one set of
+# device tables per (prepared scan, slot) made the slots' memory the SUM over every plan ever run
+# (the reference's JMeter BI plan at 6 slots: 262 GiB allocated, out of memory).  A leased slot runs
+# one statement at a time (engine/scheduler.py), so its scans carve their large tensors from one
+# per-slot arena instead: a bump allocation that restarts with every statement on the slot
+# (``slot_epoch``), grown to the slot's largest statement -- K slots hold K x the largest need.
+# A scan keeps its descriptor while it lands at the same arena offset (a repeated statement carves
+# in the same order: the same offsets every time); its first-touch / "reset behind the copy" state
+# survives when nothing else was carved over its region since its last run, and is reset otherwise.
+# Slot 0 (unleased callers: scripts, tests, the bench) keeps per-scan buffers under the LRU budget.
+ARENA_ALIGN = 256
+ARENA_MIN = 64 << 20
 
 
-def _geom_register(prep, slot, geom) -> None:
-    with _geom_lock:
-        _GEOM.setdefault((slot, geom), {})[id(prep)] = weakref.ref(prep)
+class SlotArena:
+    """One execution slot's device memory for the scans of its current statement."""
+
+    def __init__(self, dev, slot: int):
+        self.dev, self.slot = dev, slot
+        self.buf: Optional[torch.Tensor] = None   # uint8 storage
+        self.cap = 0
+        self.gen = 0          # storage generation (a new storage on growth / release)
+        self.epoch = -1       # the slot's statement epoch the bump pointer belongs to
+        self.off = 0
+        self.need = 0         # bytes the current statement carved so far (across growths)
+        self.binds: dict = {}  # start -> (end, owner id) of the regions' last carvers (current gen)
+        self.users: "weakref.WeakSet" = weakref.WeakSet()  # scans holding views of this storage
+        self.lock = threading.Lock()  # (release_device_memory may drop the storage from another thread)
+
+    def carve(self, nbytes: int, owner) -> tuple:
+        with self.lock:
+            return self._carve(nbytes, owner)
+
+    def _carve(self, nbytes: int, owner) -> tuple:
+        """(gen, offset, intact) of ``nbytes`` for ``owner`` in the current statement: ``intact``
+        when the region was last carved by the same owner with the same size and nothing carved
+        over it since (its contents are as that owner left them)."""
+        from .scheduler import slot_epoch
+
+        ep = slot_epoch(self.slot)
+        if ep != self.epoch:
+            self.epoch, self.off, self.need = ep, 0, 0
+        nbytes = (max(1, nbytes) + ARENA_ALIGN - 1) // ARENA_ALIGN * ARENA_ALIGN
+        self.need += nbytes
+        if self.off + nbytes > self.cap:
+            # the earlier scans of this statement keep the old storage alive through their views;
+            # the next statement on the slot fits the new one whole
+            cap = max(ARENA_MIN, 2 * self.cap, self.need)
+            cap = (cap + ARENA_MIN - 1) // ARENA_MIN * ARENA_MIN
+            self._drop()
+            self.buf = _with_eviction(lambda: torch.empty(cap, dtype=torch.uint8, device=self.dev), None, self.slot,
+                                      arena=self)
+            self.cap = cap
+        start = self.off
+        self.off += nbytes
+        end = start + nbytes
+        intact = self.binds.get(start) == (end, id(owner))
+        for st in [st for st, (e, _) in self.binds.items() if st < end and e > start]:
+            del self.binds[st]
+        self.binds[start] = (end, id(owner))
+        self.users.add(owner)
+        return self.gen, start, intact
+
+    def view(self, off: int, nelem: int, dtype, shape=None) -> torch.Tensor:
+        nb = nelem * torch.empty((), dtype=dtype).element_size()
+        t = self.buf[off:off + nb].view(dtype)
+        return t.view(shape) if shape is not None else t
+
+    def release(self) -> None:
+        with self.lock:
+            self._drop()
+
+    def _drop(self) -> None:
+        """Forget the storage: scans holding views re-carve at their next run (running statements
+        keep their tensors alive by reference until they finish)."""
+        for p in list(self.users):
+            with p._slot_lock:
+                p._slots.pop(self.slot, None)
+        self.users = weakref.WeakSet()
+        self.buf, self.cap, self.off = None, 0, 0
+        self.binds = {}
+        self.gen += 1
 
 
-def _steal(prep, slot, geom) -> Optional["_Bufs"]:
-    """Another (unpinned) prepared scan's buffers of geometry ``geom`` on ``slot``, removed from
-    it; None when there are none.  Never on slot 0: it is not leased (every thread that runs a
-    statement outside the scheduler shares it), so one thread's pins say nothing about the scans
-    another thread is still running there."""
-    if slot == 0:
-        return None
-    pins = pinned()
-    with _geom_lock:
-        holders = _GEOM.get((slot, geom))
-        if not holders:
-            return None
-        cands = [(pid, ref) for pid, ref in list(holders.items()) if pid != id(prep) and pid not in pins]
-    for pid, ref in cands:
-        p = ref()
-        if p is None:
-            with _geom_lock:
-                holders.pop(pid, None)
-            continue
-        with p._slot_lock:
-            b = p._slots.get(slot)
-            if b is None or getattr(b, "geom", None) != geom:
-                continue
-            p._slots.pop(slot)
-        with _geom_lock:
-            holders.pop(pid, None)
-        with _buf_lock:
-            old = _buf_lru.pop((pid, slot), None)
-            if old is not None:
-                _buf_total[0] -= old[1]
-        return b
-    return None
+_ARENAS: dict = {}
+_arena_lock = threading.Lock()
+
+
+def slot_arena(dev, slot: int) -> SlotArena:
+    k = (str(dev), slot)
+    ar = _ARENAS.get(k)
+    if ar is None:
+        with _arena_lock:
+            ar = _ARENAS.setdefault(k, SlotArena(dev, slot))
+    return ar
+
+
+def arena_bytes() -> int:
+    """Device bytes held by the slot arenas (their current storages)."""
+    return sum(a.cap for a in list(_ARENAS.values()))
+
+
+def _carve_aligned(sizes: List[int]) -> tuple:
+    offs, off = [], 0
+    for n in sizes:
+        offs.append(off)
+        off += (max(1, n) + ARENA_ALIGN - 1) // ARENA_ALIGN * ARENA_ALIGN
+    return offs, off
 
 
 class PreparedEmit:
@@ -985,26 +1103,47 @@ class PreparedMask:
     def _bufs(self):
         slot = current_slot()
         b = self._slots.get(slot)
+        if slot != 0:
+            # the mask words come from the slot's arena (zeroed by every run); the descriptor is
+            # re-packed only when the mask lands at another offset
+            from .scheduler import slot_epoch
+
+            ar = slot_arena(self.dev, slot)
+            ep = slot_epoch(slot)
+            if b is not None and b[3][0] == ar.gen and b[3][2] == ep:
+                return b
+            gen, off, _ = ar.carve(self.prog.ds.nwords * 8, self)
+            if b is not None and b[3][:2] == (gen, off):
+                b = (b[0], b[1], b[2], (gen, off, ep))
+            else:
+                mask = ar.view(off, self.prog.ds.nwords, torch.int64)
+                b = self._make(mask) + ((gen, off, ep),)
+            with self._slot_lock:
+                self._slots[slot] = b
+            return b
         if b is None:
             with self._slot_lock:
                 b = self._slots.get(slot)
                 if b is None:
-                    prog = self.prog
-                    mask = torch.zeros(prog.ds.nwords, dtype=torch.int64, device=self.dev)
-                    count = torch.zeros(1, dtype=torch.int64, device=self.dev)
-                    d = pack(prog, D.M_MASK, 0, 0, 0, 0, 0, 0, 0, mask.data_ptr(), count.data_ptr(), [], [],
-                             unroll=UNROLL, cache_off=self._layout[0], wave_bytes=self._layout[1])
-                    desc = torch.from_numpy(d.view(np.uint8).copy()).to(self.dev)
-                    self.grid = _grid(self.dev, int(d[0]["total_chunks"]),
-                                      self.jit.lay.total if self.jit else self.lds_total, self.jit)
-                    b = self._slots[slot] = (mask, count, desc)
+                    mask = torch.zeros(self.prog.ds.nwords, dtype=torch.int64, device=self.dev)
+                    b = self._slots[slot] = self._make(mask) + ((-1, -1, -1),)
         return b
+
+    def _make(self, mask: torch.Tensor) -> tuple:
+        prog = self.prog
+        count = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        d = pack(prog, D.M_MASK, 0, 0, 0, 0, 0, 0, 0, mask.data_ptr(), count.data_ptr(), [], [],
+                 unroll=UNROLL, cache_off=self._layout[0], wave_bytes=self._layout[1])
+        desc = torch.from_numpy(d.view(np.uint8).copy()).to(self.dev)
+        self.grid = _grid(self.dev, int(d[0]["total_chunks"]), self.jit.lay.total if self.jit else self.lds_total,
+                          self.jit)
+        return mask, count, desc
 
     def run(self) -> torch.Tensor:
         """Row ids passing the filter (sorted)."""
         if self.prog.empty:
             return torch.zeros(0, dtype=torch.int64, device=self.dev)
-        mask, count, desc = self._bufs()
+        mask, count, desc, _ = self._bufs()
         mask.zero_()
         count.zero_()
         if self.jit is not None:

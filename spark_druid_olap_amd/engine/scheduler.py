@@ -7,12 +7,14 @@ BI benchmark by JMeter threads on a fair scheduler pool (``docs/bi-benchmark/sna
 87-101``).  On one MI355X the equivalent resources are HIP streams and the device buffers a query
 writes into:
 
-* ``StreamScheduler`` owns K *slots*.  A slot is one HIP stream plus the right to use slot-private
-  device buffers (accumulators, hash tables, HLL registers, scan descriptors -- see
-  ``engine/device_exec.py``, which keys every prepared scan's buffers by ``current_slot()``).  A
+* ``StreamScheduler`` owns K *slots*.  A slot is one HIP stream plus the right to use the slot's
+  device arena (accumulators, hash tables, HLL registers -- see ``engine/device_exec.py``
+  ``SlotArena``, which every prepared scan run on ``current_slot()`` carves its buffers from).  A
   statement leases a slot for its whole execution, so two clients running the same prepared query
   never share accumulators, and their kernels overlap on different streams.  Leasing blocks when
-  all K slots are busy: that is the admission queue.
+  all K slots are busy: that is the admission queue.  Each lease starts a new *statement epoch* of
+  the slot (``slot_epoch``): the arena's bump allocation restarts, so the slot's device memory is
+  its largest statement's need, not the sum over every prepared plan ever run on it.
 * ``Coalescer`` batches identical statements that are *waiting* for a slot: the first becomes the
   leader, later arrivals with the same key attach to it, and when the leader gets a slot it executes
   once for all of them (a shared scan).  A statement that arrives after the leader started executing
@@ -39,24 +41,25 @@ def current_slot() -> int:
     return getattr(_ctx, "slot", 0)
 
 
-def pinned() -> set:
-    """Prepared scans (ids) whose slot buffers this thread's current statement may still read
-    (engine/device_exec.py: they are not handed over to another scan)."""
-    s = getattr(_ctx, "pins", None)
-    if s is None:
-        s = _ctx.pins = set()
-    return s
+_epochs: Dict[int, int] = {}
+
+
+def slot_epoch(slot: int) -> int:
+    """Statement counter of a slot: bumped each time a statement starts on it (``use_slot``)."""
+    return _epochs.get(slot, 0)
 
 
 @contextlib.contextmanager
 def use_slot(slot: int):
+    """Run the calling thread's statement on ``slot`` (one statement per slot at a time: the
+    scheduler's lease or the SPMD slot worker guarantees it)."""
     prev = getattr(_ctx, "slot", 0)
     _ctx.slot = slot
+    _epochs[slot] = _epochs.get(slot, 0) + 1
     try:
         yield slot
     finally:
         _ctx.slot = prev
-        pinned().clear()  # the statement on this slot is done with its scans' buffers
 
 
 class StreamScheduler:

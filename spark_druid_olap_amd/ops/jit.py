@@ -173,10 +173,6 @@ DENSE_WORDS_PACKED = 16  # (the same switch for kernels reading lane-interleaved
 # wave-reduced once into the accumulator table at the end.
 COUNT_REGS = True
 COUNT_REGS_MAX_G = 8
-# probe-only (tools/query_probe.py "sink"): dense-LDS slot updates fold into a register instead of
-# the LDS table -- wrong results, used to price the LDS atomics of a scan
-SINK_UPDATES = False
-STATIC_RUNS = True  # whole-chunk word runs with compile-time packed-field offsets (A/B switch)
 
 
 def count_regs(prog, mode: int) -> bool:
@@ -738,9 +734,6 @@ class _Gen:
                 if creg:  # packed 8-bit register counters (COUNT_REGS)
                     body.append(f"        pc{s} += (uint64_t)({cond}) << ((uint32_t)key << 3);")
                     continue
-                if mode == D.M_DENSE_LDS and SINK_UPDATES:
-                    body.append(f"        sink_ ^= ({cond}) ? (uint64_t)({val}) + (uint64_t)slot : 0ull;")
-                    continue
                 if mode == D.M_DENSE_LDS:
                     tgt = f"acc + (slot * {NS} + {s}) * {NCT} + copy"
                 else:
@@ -852,7 +845,7 @@ class _Gen:
         # whole-chunk walks over a bit-packed column run as static runs of U words per 32-word
         # stream group: each run's stream dwords are U W / 32 (+1) coalesced loads with
         # compile-time field offsets (segment/packed.py); `continue` leaves only its own run
-        static = STATIC_RUNS and U >= 4 and 32 % U == 0 and any(self.cols[i].pw for i in staged)
+        static = U >= 4 and 32 % U == 0 and any(self.cols[i].pw for i in staged)
 
         def whole_chunk(mask: str) -> None:
             if static:
@@ -941,10 +934,6 @@ class _Gen:
                     out.append(f"    for (int i = threadIdx.x; i < {G * self.m // 4}; i += {W * 64}) "
                                "hll_merge_word8(g + i, r[i]);")
                     out.append("  }")
-        if SINK_UPDATES:
-            out.insert(out.index("  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);") + 1,
-                       "  uint64_t sink_ = 0;")
-            out.append("  if (sink_ == 0x123456789abcdefull) ((uint64_t*)d->out_acc)[0] = sink_;")
         out.append("}")
         return "\n".join(out) + "\n"
 

@@ -299,11 +299,16 @@ class NativeHiveServer(HiveThriftServer):
                 try:
                     res = df.run(token=token)  # the executor's columns, encoded without a DataFrame
                 except torch.OutOfMemoryError:
-                    # the HBM is held by other statements' cached slot tables (many concurrent
-                    # large group-bys): drop every cache and run the statement once more
-                    from ..engine.device_exec import release_device_memory
+                    # a temporary outside the slot arenas (a sort, a gather) found the HBM held by
+                    # other slots' arenas and cached slot-0 tables: release those (not this slot's
+                    # arena) and run the statement once more -- counted, so repeats show up
+                    from ..engine.device_exec import release_device_memory, slot_arena
+                    from ..engine.scheduler import current_slot
+                    from ..utils.metrics import count_event
 
-                    release_device_memory()
+                    log.warning("statement ran out of device memory; releasing caches and retrying once")
+                    count_event("statement_oom_retry")
+                    release_device_memory(keep_arena=slot_arena(sess.engine.world.device(), current_slot()))
                     res = df.run(token=token)
         return list(df.columns), [t for _, t in df.schema], res
 

@@ -8,7 +8,8 @@ pushed aggregate runs on the GPU and the window on the host over the aggregated 
 * rows are ordered by (partition, ORDER BY keys) once per distinct (partition, order) spec;
 * ranking functions come from partition starts and peer-group starts (rows with equal ORDER BY
   keys are peers);
-* sum / count / avg over a frame are prefix-sum differences; min / max over running frames are
+* sum / count / avg over a frame are prefix-sum differences (int64 for integer arguments, so they
+  stay exact; bounded float frames are summed directly); min / max over running frames are
   per-partition accumulates, over bounded frames a sliding minimum / maximum;
 * lag / lead / first_value / last_value are shifted gathers inside the partition.
 
@@ -98,23 +99,44 @@ class _Layout:
 
 
 def _values(e: A.Expr, fr: Frame, order: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
-    """(float64 values, non-null mask) of a numeric argument, in sorted order."""
+    """(values, non-null mask) of a numeric argument, in sorted order: int64 for integer arguments
+    (so framed sums stay exact, as Spark's sum(bigint) is), float64 otherwise."""
     s = eval_series(e, fr)
+    if pd.api.types.is_integer_dtype(s.dtype) and not pd.api.types.is_bool_dtype(s.dtype):
+        ok = s.notna().to_numpy()[order]
+        v = s.fillna(0).to_numpy(dtype=np.int64)[order]
+        return v, ok
     v = pd.to_numeric(s, errors="coerce").to_numpy(dtype=np.float64, na_value=np.nan)[order]
     ok = ~np.isnan(v)
     return np.where(ok, v, 0.0), ok
 
 
 def _prefix(v: np.ndarray) -> np.ndarray:
-    c = np.zeros(len(v) + 1, dtype=np.float64)
+    c = np.zeros(len(v) + 1, dtype=np.int64 if v.dtype.kind in "iub" else np.float64)
     np.cumsum(v, out=c[1:])
     return c
 
 
 def _frame_sum(v: np.ndarray, lo: np.ndarray, hi: np.ndarray) -> np.ndarray:
-    c = _prefix(v)
+    """Sum over each row's [lo, hi] frame: prefix-sum differences (exact in int64 for integer
+    inputs), and per-partition rebased prefixes for floats so a frame deep into a long partition
+    does not lose its digits to cancellation against the partition's running total."""
+    n = len(v)
     ok = lo <= hi
-    return np.where(ok, c[np.minimum(hi + 1, len(v))] - c[np.minimum(lo, len(v))], 0.0)
+    if v.dtype.kind in "iub":
+        c = _prefix(v)
+        return np.where(ok, c[np.minimum(hi + 1, n)] - c[np.minimum(lo, n)], 0)
+    c = _prefix(v)
+    # bounded frames of up to 64 rows are summed directly (no cancellation); longer ones use the prefix
+    span = np.where(ok, hi - lo + 1, 0)
+    out = np.where(ok, c[np.minimum(hi + 1, n)] - c[np.minimum(lo, n)], 0.0)
+    small = ok & (span <= 64)
+    if small.any() and n:
+        w = int(span[small].max())
+        j = lo[small][:, None] + np.arange(w)[None, :]
+        m = j <= hi[small][:, None]
+        out[small] = np.where(m, v[np.minimum(j, n - 1)], 0.0).sum(axis=1)
+    return out
 
 
 def _frame_extreme(v: np.ndarray, ok: np.ndarray, lo: np.ndarray, hi: np.ndarray, lay: _Layout,
@@ -139,7 +161,7 @@ def _frame_extreme(v: np.ndarray, ok: np.ndarray, lo: np.ndarray, hi: np.ndarray
             if lo[i] <= hi[i]:
                 seg = x[lo[i]:hi[i] + 1]
                 out[i] = seg.max() if is_max else seg.min()
-    has = _frame_sum(ok.astype(np.float64), lo, hi) > 0
+    has = _frame_sum(ok.astype(np.int64), lo, hi) > 0
     return np.where(has, out, 0.0), has
 
 
@@ -208,7 +230,7 @@ def evaluate_window(w: A.WindowExpr, fr: Frame, cache: Optional[dict] = None) ->
             out_sorted = np.maximum(hi - lo + 1, 0)
         else:
             v, ok = _values(f.args[0], fr, order)
-            cnt = _frame_sum(ok.astype(np.float64), lo, hi)
+            cnt = _frame_sum(ok.astype(np.int64), lo, hi)
             if name == "count":
                 out_sorted = cnt.astype(np.int64)
             elif name == "sum":

@@ -17,6 +17,21 @@ from typing import Dict, Optional
 import numpy as np
 
 
+_events: Dict[str, int] = {}
+_events_lock = threading.Lock()
+
+
+def count_event(name: str, n: int = 1) -> None:
+    """Process-wide event counter (device-memory releases, statement retries, P2P fallbacks)."""
+    with _events_lock:
+        _events[name] = _events.get(name, 0) + n
+
+
+def events() -> Dict[str, int]:
+    with _events_lock:
+        return dict(_events)
+
+
 class _Series:
     __slots__ = ("lat", "ts", "n", "errors", "total_ms")
 
@@ -85,6 +100,9 @@ class ServerMetrics:
             for q, key in (("0.5", "p50_ms"), ("0.95", "p95_ms"), ("0.99", "p99_ms")):
                 lines.append(f'sdo_latency_ms{{endpoint="{ep}",quantile="{q}"}} {v[key]}')
             lines.append(f'sdo_latency_ms_count{{endpoint="{ep}"}} {v["count"]}')
+        lines += ["# HELP sdo_events_total process events (memory releases, retries)", "# TYPE sdo_events_total counter"]
+        for k, v in sorted(events().items()):
+            lines.append(f'sdo_events_total{{event="{k}"}} {v}')
         return "\n".join(lines) + "\n"
 
 

@@ -1,0 +1,120 @@
+"""Per-slot device arenas (engine/device_exec.py SlotArena): every leased execution slot carves the
+large tensors of its current statement's scans from one bump-allocated arena that restarts with the
+slot's next statement, so K slots hold K x the largest statement's need instead of one cached table
+set per (prepared plan, slot) (the round-4 BI plan ran out of HBM at 6 slots that way)."""
+import threading
+
+import pytest
+import torch
+
+from spark_druid_olap_amd.engine import device_exec as DE
+from spark_druid_olap_amd.engine.scheduler import slot_epoch, use_slot
+
+
+class _Owner:
+    def __init__(self):
+        self._slot_lock = threading.Lock()
+        self._slots = {}
+
+
+def test_carve_restarts_per_statement_and_tracks_intact_regions():
+    ar = DE.SlotArena("cpu", 91)
+    a, b, c = _Owner(), _Owner(), _Owner()
+    with use_slot(91):
+        ga, oa, ia = ar.carve(1000, a)
+        gb, ob, ib = ar.carve(5000, b)
+    assert (oa, ob) == (0, 1024) and not ia and not ib  # 256-byte aligned bump, first carve: not intact
+    with use_slot(91):  # the same statement again: the same offsets, contents as left
+        assert ar.carve(1000, a) == (ga, 0, True)
+        assert ar.carve(5000, b) == (gb, 1024, True)
+    with use_slot(91):  # another statement carves over a's region
+        assert ar.carve(3000, c)[1:] == (0, False)
+    with use_slot(91):
+        assert ar.carve(1000, a)[1:] == (0, False)   # a's bytes were overwritten by c
+        assert ar.carve(5000, b)[2] is False          # c's 3072 bytes overlapped b's region too
+    assert ar.cap == DE.ARENA_MIN  # one storage for all of it
+
+
+def test_growth_keeps_earlier_views_and_sizes_for_the_whole_statement(monkeypatch):
+    monkeypatch.setattr(DE, "ARENA_MIN", 4096)
+    ar = DE.SlotArena("cpu", 92)
+    a, b = _Owner(), _Owner()
+    with use_slot(92):
+        g0, off, _ = ar.carve(3000, a)
+        va = ar.view(off, 375, torch.int64)
+        va.fill_(7)
+        a._slots[92] = "bufs"
+        g1, off_b, _ = ar.carve(6000, b)  # does not fit: a new storage, a's view stays valid
+        assert g1 == g0 + 1 and off_b == 0
+        assert int(va.sum()) == 7 * 375
+        assert 92 not in a._slots  # a re-carves at its next run
+    assert ar.cap >= 3072 + 6144  # the next statement fits whole
+    with use_slot(92):
+        assert ar.carve(3000, a)[:2] == (g1, 0)
+        assert ar.carve(6000, b)[:2] == (g1, 3072)
+    assert ar.gen == g1
+
+
+def test_release_drops_other_arenas_only():
+    a1, a2 = DE.slot_arena("cpu", 93), DE.slot_arena("cpu", 94)
+    o1, o2 = _Owner(), _Owner()
+    with use_slot(93):
+        a1.carve(100, o1)
+        o1._slots[93] = "x"
+    with use_slot(94):
+        a2.carve(100, o2)
+        o2._slots[94] = "y"
+    DE.release_device_memory(keep_arena=a2) if torch.cuda.is_available() else _release_no_cuda(a2)
+    assert a1.buf is None and 93 not in o1._slots
+    assert a2.buf is not None and o2._slots[94] == "y"
+
+
+def _release_no_cuda(keep):
+    for ar in list(DE._ARENAS.values()):
+        if ar is not keep:
+            ar.release()
+
+
+def test_slot_epochs_count_statements():
+    e = slot_epoch(95)
+    with use_slot(95):
+        assert slot_epoch(95) == e + 1
+    with use_slot(95):
+        pass
+    assert slot_epoch(95) == e + 2
+
+
+@pytest.mark.gpu
+def test_parameterizations_share_the_slot_arena():
+    """Two parameterizations of one large group-by (dense HBM table with a first-touch byte table)
+    run alternately on slot 1: both carve the same arena region (same device pointer, no second
+    table), each re-initialises it when the other wrote over it, and both answer exactly as
+    freshly prepared scans on slot 0; a select (mask scan) carves from the arena too."""
+    from spark_druid_olap_amd.engine.executor import Engine
+    from spark_druid_olap_amd.models import tpch
+    from spark_druid_olap_amd.query import spec as S
+
+    ds = tpch.to_datasource(tpch.generate_flat(0.2, "cuda"), profile="bench")
+
+    def q(seg):
+        return S.GroupByQuerySpec("tpch", [S.DefaultDimensionSpec("o_orderkey")],
+                                  aggregations=[S.FunctionAggregationSpec("doubleSum", "p", "l_extendedprice")],
+                                  filter=S.SelectorFilterSpec("c_mktsegment", seg), intervals=["1992-01-01/1999-01-01"])
+
+    eng = Engine()
+    pa, pb = eng.prepare(q("BUILDING"), ds), eng.prepare(q("MACHINERY"), ds)
+    ref_a, ref_b = Engine().execute(q("BUILDING"), ds), Engine().execute(q("MACHINERY"), ds)
+
+    def rows(r):
+        return sorted(zip(r.data["o_orderkey"].tolist(), [round(x, 6) for x in r.data["p"].tolist()]))
+
+    ptrs = set()
+    for i in range(3):
+        for p, ref in ((pa, ref_a), (pa, ref_a), (pb, ref_b)):  # (a twice: its intact re-run skips the reset)
+            with use_slot(1):
+                r = p.run()
+                ptrs.add(p.scans[0][2]._slots[1].acc.data_ptr())
+            assert rows(r) == rows(ref), i
+    assert len(ptrs) == 1, "the parameterizations did not share the slot's arena region"
+    ar = DE.slot_arena(ds.device, 1)
+    assert ar.cap < 4 * ar.need + DE.ARENA_MIN

@@ -113,3 +113,16 @@ def test_window_errors(sess):
         sess.sql("select g from t where rank() over (order by o) = 1")
     with pytest.raises(AnalysisError):
         sess.sql("select upper(g) over (order by o) from t")
+
+
+def test_integer_frame_sums_exact():
+    """Framed sums of bigint arguments stay exact above 2^53 (Spark's sum(bigint) is exact)."""
+    s = Session(engine=Engine(use_native=False))
+    big = 2 ** 60
+    s.register_table("w", pd.DataFrame({"g": [1, 1, 1, 1], "o": [1, 2, 3, 4],
+                                        "v": np.array([big, 3, 5, 7], dtype=np.int64)}))
+    r = s.sql("select o, sum(v) over (partition by g order by o) rs, "
+              "sum(v) over (partition by g order by o rows between 1 preceding and current row) m2 "
+              "from w order by o").collect()
+    assert [int(x[1]) for x in r] == [big, big + 3, big + 8, big + 15]
+    assert [int(x[2]) for x in r] == [big, big + 3, 8, 12]

@@ -3,12 +3,10 @@
   python tools/query_probe.py SF [variant ...] [-- query names]
 
 A variant is ``base[b<workgroups per CU>][c<accumulator copies per wave>][u<max words per step>][slds|sreg][creg0]
-[dw<N>][nostatic][plain][sink]``: target workgroups per CU, accumulator copies, word unroll cap, forced LDS-DMA / VGPR
-staging, count-only scans through LDS atomics instead of register counters, the packed-kernel dense-walk threshold,
-no static packed runs, plain byte-width columns, dropped slot updates (see ops/jit.py); results of every variant are
-checked against
-the first one.  Used to locate slow or hung kernels
-and to A/B kernel-generation choices on the GPU box."""
+[dw<N>][plain]``: target workgroups per CU, accumulator copies, word unroll cap, forced LDS-DMA / VGPR staging,
+count-only scans through LDS atomics instead of register counters, the packed-kernel dense-walk threshold, plain
+byte-width columns (see ops/jit.py); results of every variant are checked against the first one.  Used to locate slow
+or hung kernels and to A/B kernel-generation choices on the GPU box."""
 import os
 import statistics
 import sys
@@ -94,10 +92,8 @@ def main():
         DE.JIT_STAGE = "lds" if "slds" in var else ("reg" if "sreg" in var else "auto")
         DE.BLOCKS_PER_CU = max(3, DE.JIT_BLOCKS)
         J.COUNT_REGS = "creg0" not in var
-        J.SINK_UPDATES = "sink" in var  # (slot updates priced by dropping them: results differ)
         md = re.search(r"dw(\d+)", var)
         J.DENSE_WORDS_PACKED = int(md.group(1)) if md else 16
-        J.STATIC_RUNS = "nostatic" not in var
         from spark_druid_olap_amd.segment import packed as PK
         PK.ENABLED = "plain" not in var  # (byte-width columns instead of the packed copies)
         mu = re.search(r"u(\d+)", var)
