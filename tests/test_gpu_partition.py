@@ -293,3 +293,65 @@ def test_hash_partitioned_overflow_repartitions(gpu_ds, monkeypatch):
     assert part.part["scale"] > s0
     monkeypatch.setattr(jit, "FORCE_HASHED", False)
     _sparse_vs_dense(a, DE.PreparedScan(prog, mode=D.M_DENSE_GLOBAL).run(), prog)
+
+
+# ------------------------------------------------------------------------------------------------
+# Engine-independent oracle: the same SQL over the plain base table answered by the host SQL
+# operators (pandas), with the planner forced onto the partitioned (and hashed) layouts.
+@pytest.fixture(scope="module")
+def sql_pair():
+    from spark_druid_olap_amd.engine.executor import Engine
+    from spark_druid_olap_amd.models import tpch
+    from spark_druid_olap_amd.session import Session
+
+    flat = tpch.generate_flat(0.05, "cuda")
+    ds = tpch.to_datasource(flat, profile="bench")
+    s = Session(engine=Engine(use_native=True))
+    s.register_datasource(ds)
+    s.register_table("orderLineItemPartSupplierBase", tpch.to_pandas(flat), schema=tpch.FLAT_SCHEMA)
+    s.sql(tpch.druid_ddl(with_column_mapping=False))
+    return s
+
+
+def _oracle_rows(d):
+    import math
+
+    def n(v):
+        return None if isinstance(v, float) and math.isnan(v) else (round(v, 2) if isinstance(v, float) else v)
+    return sorted(tuple(n(v) for v in r) for r in d.collect())
+
+
+@pytest.mark.parametrize("hashed,table_bytes", [(False, 32 << 10), (False, 1024), (True, None)])
+@pytest.mark.parametrize("sql", [
+    "select o_orderkey, count(*) c, sum(l_quantity) q, sum(l_extendedprice) s, min(l_quantity) mn, "
+    "max(l_discount) mx from {T} group by o_orderkey",
+    "select o_orderkey, sum(l_quantity) q from {T} where o_orderdate >= '1994-01-01' group by o_orderkey "
+    "having sum(l_quantity) > 150",
+    "select l_partkey, l_suppkey, count(*) c, sum(l_quantity) q from {T} group by l_partkey, l_suppkey",
+])
+def test_partitioned_paths_vs_base_table_oracle(sql_pair, monkeypatch, sql, hashed, table_bytes):
+    from spark_druid_olap_amd.engine import device_exec as DE
+    from spark_druid_olap_amd.ops import jit
+    from spark_druid_olap_amd.planner import cost
+
+    monkeypatch.setattr(cost, "FORCE_PARTITIONED", True)
+    monkeypatch.setattr(jit, "FORCE_HASHED", hashed)
+    if table_bytes:
+        monkeypatch.setattr(DE, "PART_TABLE_BYTES", table_bytes)
+    s = sql_pair
+    s._plan_cache.clear()
+    d = s.sql(sql.format(T="orderLineItemPartSupplier"))
+    assert d.druid_queries()
+    got = _oracle_rows(d)
+    exp = _oracle_rows(s.sql(sql.format(T="orderLineItemPartSupplierBase")))
+    assert len(got) == len(exp) > 0
+    for x, y in zip(got, exp):
+        for u, v in zip(x, y):
+            if isinstance(u, float) or isinstance(v, float):
+                assert u == pytest.approx(v, rel=1e-9, abs=0.011), (x, y)
+            else:
+                assert u == v, (x, y)
+    modes = {getattr(sc[2], "mode", None) for dq in d.druid_queries()
+             for sc in getattr(getattr(dq, "_prepared", None), "scans", [])}
+    if hashed or "o_orderkey" in sql:  # (few lines per (part, supplier) group: the atomic table wins unhashed)
+        assert D.M_PART in modes, modes
