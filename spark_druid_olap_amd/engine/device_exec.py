@@ -325,7 +325,7 @@ class PreparedScan:
         items = self._tensor_layout(cap)
         sizes = [n * torch.empty((), dtype=dt).element_size() for _, n, dt, _ in items]
         offs, total = _carve_aligned(sizes)
-        gen, off, intact = ar.carve(total, self)
+        gen, off, intact, buf = ar.carve(total, self)
         if b is not None and b.arena is not None and b.arena[:2] == (gen, off) and b.cap == cap:
             b.arena = (gen, off, ep)
             if not intact:
@@ -335,7 +335,7 @@ class PreparedScan:
         v.geom = self._geom(cap)
         v.hll, v.hll32 = [], []
         for (name, n, dt, shape), o in zip(items, offs):
-            t = ar.view(off + o, n, dt, shape)
+            t = SlotArena.view(buf, off + o, n, dt, shape)
             if name in ("hll", "hll32"):
                 getattr(v, name).append(t)
             else:
@@ -478,12 +478,17 @@ class PreparedScan:
         """producer (records into chunk regions) -> level-1 split (count, offsets, tile-sorted
         scatter) -> [level-2 split] -> LDS aggregation into the dense table (every row written: no
         reset), or, with a fused HAVING, straight to the surviving groups (sparse)."""
+        slab = PART_POOL.acquire(self.dev, b.part["cap_words"])
+        try:
+            return self._run_part_on(b, slab)
+        finally:
+            PART_POOL.release(slab)
+
+    def _run_part_on(self, b: "_Bufs", slab: "_Slab") -> Optional[Partials]:
         L, nat, st = self.part, native.load(), native._stream(self.dev)
         pb = dict(b.part)
         prog = self.prog
-        slot = current_slot()
-        pb["recs1"] = _scratch(self.dev, slot, "recs1", pb["cap_words"])
-        pb["recs2"] = _scratch(self.dev, slot, "recs2", pb["cap_words"])
+        pb["recs1"], pb["recs2"] = slab.recs1, slab.recs2
         if b.part["desc_recs"] != pb["recs1"].data_ptr():
             off = D.SCANDESC.fields["part_recs"][1]
             ptr = torch.tensor([pb["recs1"].data_ptr()], dtype=torch.int64).view(torch.uint8)
@@ -520,12 +525,7 @@ class PreparedScan:
                              int(prog.hll_p), st)
             return None
         while True:
-            out = b.part.get("hv_out")
-            if out is None or out[0].shape[0] < self.part_cap:
-                out = b.part["hv_out"] = (torch.empty((self.part_cap, prog.nslots), dtype=torch.int64, device=self.dev),
-                                      torch.empty(self.part_cap, dtype=torch.int64, device=self.dev),
-                                      torch.zeros(1, dtype=torch.int64, device=self.dev))
-            acc, keys, cnt = out
+            acc, keys, cnt = self._sparse_out(b, "hv_out", False)
             nat.part_agg(recs.data_ptr(), L["rw"], base.data_ptr(), L["nsub"], int(prog.G), L["shift"],
                          [f[0] for f in L["fields"]], [f[1] for f in L["fields"]], [int(op) for op, _ in prog.slots],
                          [int(init) for _, init in prog.slots], acc.data_ptr(), hv[0], hv[1], keys.data_ptr(),
@@ -542,13 +542,7 @@ class PreparedScan:
         L, nat, st, prog = self.part, native.load(), native._stream(self.dev), self.prog
         hv = self.part_having or ([], 1)
         while True:
-            out = b.part.get("hh_out")
-            if out is None or out[0].shape[0] < self.part_cap:
-                out = b.part["hh_out"] = (torch.empty((self.part_cap, prog.nslots), dtype=torch.int64, device=self.dev),
-                                          torch.empty(self.part_cap, dtype=torch.int64, device=self.dev),
-                                          torch.zeros(1, dtype=torch.int64, device=self.dev),
-                                          torch.zeros(1, dtype=torch.int32, device=self.dev))
-            acc, keys, cnt, ovf = out
+            acc, keys, cnt, ovf = self._sparse_out(b, "hh_out", True)
             nat.part_hash_agg(recs.data_ptr(), L["rw"], base.data_ptr(), L["nsub"], L["cap_log2"],
                               [f[0] for f in L["fields"]], [f[1] for f in L["fields"]],
                               [int(op) for op, _ in prog.slots], [int(init) for _, init in prog.slots], hv[0], hv[1],
@@ -572,6 +566,26 @@ class PreparedScan:
                         self._slots.clear()
                 return Partials("sparse", acc[:n], keys[:n], [])
             self.part_cap = _next_pow2(n + n // 4)  # more groups than room: grow, aggregate again
+
+    def _sparse_out(self, b: "_Bufs", name: str, ovf: bool) -> tuple:
+        """(acc [part_cap][nslots], keys, count[, overflow]) the partitioned aggregation appends its
+        surviving groups to: carved from the slot's arena on a leased slot (they live as long as the
+        statement's partials), cached on the buffers on slot 0.  (Counts are reset by the launch.)"""
+        cap, ns, dev = self.part_cap, self.prog.nslots, self.dev
+        slot = current_slot()
+        if slot == 0:
+            out = b.part.get(name)
+            if out is None or out[0].shape[0] < cap:
+                out = b.part[name] = (torch.empty((cap, ns), dtype=torch.int64, device=dev),
+                                      torch.empty(cap, dtype=torch.int64, device=dev),
+                                      torch.zeros(1, dtype=torch.int64, device=dev)) + \
+                    ((torch.zeros(1, dtype=torch.int32, device=dev),) if ovf else ())
+            return out
+        items = [(cap * ns, torch.int64, (cap, ns)), (cap, torch.int64, None), (1, torch.int64, None)] + \
+            ([(1, torch.int32, None)] if ovf else [])
+        offs, total = _carve_aligned([n * torch.empty((), dtype=dt).element_size() for n, dt, _ in items])
+        _, off, _, buf = slot_arena(dev, slot).carve(total, self)
+        return tuple(SlotArena.view(buf, off + o, n, dt, shape) for (n, dt, shape), o in zip(items, offs))
 
     def set_part_having(self, terms, conj: bool) -> bool:
         """Fuse a groupBy HAVING into the partitioned aggregation (engine/executor.py): only existing
@@ -778,24 +792,97 @@ def _budget() -> int:
 
 _budget_cache: dict = {}
 
-# Partition records (ops/csrc/partition.hip) are scratch of one execution: one pair of buffers per
-# (device, execution slot), grown to the largest need, shared by every prepared scan of the slot
-# (a slot runs one statement at a time) instead of held per cached plan.
-_SCRATCH: dict = {}
-_scratch_lock = threading.Lock()
+# Partition records (ops/csrc/partition.hip) are scratch of one execution: two record buffers
+# (producer regions / split output), sized for every row of the scanned chunks -- 4.8-14 GB at SF100.
+# Held per execution slot they multiplied by the slot count (6 slots of a BI plan: ~86 GB); instead
+# one device-wide pool hands out slabs under a byte budget.  A slab goes back to the pool once the
+# execution's kernels are enqueued, with an event on its stream: the next holder's stream waits for
+# that event, so the memory is reused in device order without a host sync.  A thread already
+# holding a slab never waits for another (a hashed re-partition takes a second one over budget).
+PART_SCRATCH_BUDGET = int(os.environ.get("SDO_PART_SCRATCH_BUDGET", "0"))  # 0: 12% of the device
 
 
-def _scratch(dev, slot, name: str, nelem: int) -> torch.Tensor:
-    k = (str(dev), slot, name)
-    with _scratch_lock:
-        t = _SCRATCH.get(k)
-        if t is not None and t.numel() >= nelem:
-            return t
-        _SCRATCH[k] = None
-    t = _with_eviction(lambda: torch.empty(max(1, nelem), dtype=torch.int32, device=dev), None, slot)
-    with _scratch_lock:
-        _SCRATCH[k] = t
-    return t
+class _Slab:
+    __slots__ = ("dev", "recs1", "recs2", "words", "event")
+
+
+class PartScratchPool:
+    def __init__(self):
+        self.cv = threading.Condition()
+        self.free: List[_Slab] = []
+        self.total = 0
+        self.held = threading.local()
+
+    def _budget(self, dev) -> int:
+        if PART_SCRATCH_BUDGET > 0:
+            return PART_SCRATCH_BUDGET
+        try:
+            return int(0.12 * torch.cuda.get_device_properties(dev).total_memory)
+        except Exception:  # noqa: BLE001
+            return 32 << 30
+
+    def acquire(self, dev, words: int) -> _Slab:
+        """Two u32 record buffers of at least ``words`` each; the current stream waits for the
+        slab's previous holder."""
+        words = max(1, int(words))
+        need = 2 * words * 4
+        depth = getattr(self.held, "n", 0)
+        with self.cv:
+            while True:
+                fit = [x for x in self.free if x.dev == str(dev) and x.words >= words]
+                if fit:
+                    sl = min(fit, key=lambda x: x.words)
+                    self.free.remove(sl)
+                    break
+                # drop free slabs too small (or of another device) while the new one does not fit
+                while self.free and self.total + need > self._budget(dev):
+                    x = self.free.pop(0)
+                    self.total -= 2 * x.words * 4
+                if self.total + need <= self._budget(dev) or self.total == 0 or depth > 0:
+                    sl = None
+                    self.total += need
+                    break
+                self.cv.wait(timeout=1.0)
+        if sl is None:
+            try:
+                sl = _Slab()
+                sl.dev, sl.words, sl.event = str(dev), words, None
+                sl.recs1 = _with_eviction(lambda: torch.empty(words, dtype=torch.int32, device=dev), None, None)
+                sl.recs2 = _with_eviction(lambda: torch.empty(words, dtype=torch.int32, device=dev), None, None)
+            except BaseException:
+                with self.cv:
+                    self.total -= need
+                    self.cv.notify_all()
+                raise
+        if sl.event is not None and sl.recs1.is_cuda:
+            torch.cuda.current_stream(sl.recs1.device).wait_event(sl.event)
+        self.held.n = depth + 1
+        return sl
+
+    def release(self, sl: _Slab) -> None:
+        if sl.recs1.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(sl.recs1.device))
+            sl.event = ev
+        self.held.n = max(0, getattr(self.held, "n", 1) - 1)
+        with self.cv:
+            self.free.append(sl)
+            self.cv.notify_all()
+
+    def clear(self) -> None:
+        with self.cv:
+            for x in self.free:
+                self.total -= 2 * x.words * 4
+            self.free = []
+            self.cv.notify_all()
+
+    def bytes(self) -> int:
+        return self.total
+
+
+PART_POOL = PartScratchPool()
+
+
 _buf_lru: "OrderedDict[tuple, tuple]" = OrderedDict()   # (id(prep), slot) -> (weakref(prep), bytes)
 _buf_total = [0]
 _buf_lock = threading.Lock()
@@ -860,8 +947,7 @@ def release_device_memory(keep=None, keep_arena=None) -> None:
         if p is not None:
             with p._slot_lock:
                 p._slots.pop(sl, None)
-    with _scratch_lock:
-        _SCRATCH.clear()
+    PART_POOL.clear()
     torch.cuda.empty_cache()
 
 
@@ -940,13 +1026,16 @@ class SlotArena:
         self.lock = threading.Lock()  # (release_device_memory may drop the storage from another thread)
 
     def carve(self, nbytes: int, owner) -> tuple:
+        """(gen, offset, intact, storage) of ``nbytes`` for ``owner`` in the current statement:
+        ``intact`` when the region was last carved by the same owner with the same size and nothing
+        carved over it since (its contents are as that owner left them).  Views are taken from the
+        returned storage (another thread's out-of-memory release may drop the arena's own reference
+        at any time)."""
         with self.lock:
-            return self._carve(nbytes, owner)
+            r = self._carve(nbytes, owner)
+            return r + (self.buf,)
 
     def _carve(self, nbytes: int, owner) -> tuple:
-        """(gen, offset, intact) of ``nbytes`` for ``owner`` in the current statement: ``intact``
-        when the region was last carved by the same owner with the same size and nothing carved
-        over it since (its contents are as that owner left them)."""
         from .scheduler import slot_epoch
 
         ep = slot_epoch(self.slot)
@@ -973,9 +1062,10 @@ class SlotArena:
         self.users.add(owner)
         return self.gen, start, intact
 
-    def view(self, off: int, nelem: int, dtype, shape=None) -> torch.Tensor:
+    @staticmethod
+    def view(buf: torch.Tensor, off: int, nelem: int, dtype, shape=None) -> torch.Tensor:
         nb = nelem * torch.empty((), dtype=dtype).element_size()
-        t = self.buf[off:off + nb].view(dtype)
+        t = buf[off:off + nb].view(dtype)
         return t.view(shape) if shape is not None else t
 
     def release(self) -> None:
@@ -1010,6 +1100,23 @@ def slot_arena(dev, slot: int) -> SlotArena:
 def arena_bytes() -> int:
     """Device bytes held by the slot arenas (their current storages)."""
     return sum(a.cap for a in list(_ARENAS.values()))
+
+
+def device_memory_report() -> dict:
+    """Where the device memory is (GB): the allocator's totals, the slot arenas, the partition
+    scratch, the slot-0 cached scan buffers, and the release / retry events so far."""
+    from ..utils.metrics import events
+
+    g = 1e9
+    out = {"arenas_gb": round(arena_bytes() / g, 3),
+           "arena_per_slot_gb": {f"{k[1]}": round(a.cap / g, 3) for k, a in sorted(_ARENAS.items(), key=lambda x: x[0][1])},
+           "part_scratch_gb": round(PART_POOL.bytes() / g, 3),
+           "slot0_bufs_gb": round(_buf_total[0] / g, 3), "events": events()}
+    if torch.cuda.is_available():
+        out.update(allocated_gb=round(torch.cuda.memory_allocated() / g, 2),
+                   reserved_gb=round(torch.cuda.memory_reserved() / g, 2),
+                   max_allocated_gb=round(torch.cuda.max_memory_allocated() / g, 2))
+    return out
 
 
 def _carve_aligned(sizes: List[int]) -> tuple:
@@ -1053,31 +1160,38 @@ class PreparedEmit:
         cap = self.nch * D.CHUNK_ROWS
         if 2 * cap >= (1 << 32):
             raise RuntimeError("emit: shard too large for u32 offsets")
-        u32 = torch.int32
-        self.recs1 = torch.empty(max(1, 2 * cap), dtype=u32, device=self.dev)
-        self.recs2 = torch.empty_like(self.recs1)
-        self.pend = torch.empty(max(1, self.nch), dtype=u32, device=self.dev)
-        self.seg_lo = (torch.arange(self.nch, dtype=torch.int64) * D.CHUNK_ROWS).to(u32).to(self.dev)
+        self.words = max(1, 2 * cap)
+        self.seg_lo = (torch.arange(self.nch, dtype=torch.int64) * D.CHUNK_ROWS).to(torch.int32).to(self.dev)
         self.k = max(1, min(self.nch, 1024))
-        self.counts = torch.empty(self.k, dtype=u32, device=self.dev)
-        self.totals = torch.empty(1, dtype=u32, device=self.dev)
-        self.base = torch.empty(2, dtype=u32, device=self.dev)
-        d[0]["part_recs"] = self.recs1.data_ptr()
-        d[0]["part_counts"] = self.pend.data_ptr()
-        self.desc = torch.from_numpy(d.view(np.uint8).copy()).to(self.dev)
+        self._d = d  # (host descriptor: each run uploads a copy naming its own record / offset buffers)
 
     def run(self):
-        """(keys int64, rows int64) of the selected rows, in row order within each chunk."""
+        """(keys int64, rows int64) of the selected rows, in row order within each chunk.  The
+        record buffers come from the shared partition-scratch pool and the small per-run state is
+        allocated per run, so concurrent slots never share device state."""
         nat, st = native.load(), native._stream(self.dev)
-        nat.module_launch(self.jit.handle, self.desc.data_ptr(), int(self.grid), BLOCK, int(self.jit.lay.total), st)
-        a = (self.recs1.data_ptr(), 2, self.seg_lo.data_ptr(), self.pend.data_ptr(), 1, self.nch, self.k, 0, 1,
-             self.counts.data_ptr())
-        nat.part_split(*a, 0, 0, 0, st)
-        nat.part_scan(self.counts.data_ptr(), 1, self.k, self.totals.data_ptr(), self.base.data_ptr(), st)
-        nat.part_split(*a, self.base.data_ptr(), self.recs2.data_ptr(), 1, st)
-        n = int(self.base[1].item())
-        rec = self.recs2[: 2 * n].view(n, 2).to(torch.int64) & 0xFFFFFFFF
-        return rec[:, 0].contiguous(), rec[:, 1].contiguous()
+        u32 = torch.int32
+        pend = torch.empty(max(1, self.nch), dtype=u32, device=self.dev)
+        counts = torch.empty(self.k, dtype=u32, device=self.dev)
+        totals = torch.empty(1, dtype=u32, device=self.dev)
+        base = torch.empty(2, dtype=u32, device=self.dev)
+        slab = PART_POOL.acquire(self.dev, self.words)
+        try:
+            d = self._d.copy()
+            d[0]["part_recs"] = slab.recs1.data_ptr()
+            d[0]["part_counts"] = pend.data_ptr()
+            desc = _upload(d.view(np.uint8), self.dev)
+            nat.module_launch(self.jit.handle, desc.data_ptr(), int(self.grid), BLOCK, int(self.jit.lay.total), st)
+            a = (slab.recs1.data_ptr(), 2, self.seg_lo.data_ptr(), pend.data_ptr(), 1, self.nch, self.k, 0, 1,
+                 counts.data_ptr())
+            nat.part_split(*a, 0, 0, 0, st)
+            nat.part_scan(counts.data_ptr(), 1, self.k, totals.data_ptr(), base.data_ptr(), st)
+            nat.part_split(*a, base.data_ptr(), slab.recs2.data_ptr(), 1, st)
+            n = int(base[1].item())
+            rec = slab.recs2[: 2 * n].view(n, 2).to(torch.int64) & 0xFFFFFFFF
+            return rec[:, 0].contiguous(), rec[:, 1].contiguous()
+        finally:
+            PART_POOL.release(slab)
 
 
 class PreparedMask:
@@ -1112,11 +1226,11 @@ class PreparedMask:
             ep = slot_epoch(slot)
             if b is not None and b[3][0] == ar.gen and b[3][2] == ep:
                 return b
-            gen, off, _ = ar.carve(self.prog.ds.nwords * 8, self)
+            gen, off, _, buf = ar.carve(self.prog.ds.nwords * 8, self)
             if b is not None and b[3][:2] == (gen, off):
                 b = (b[0], b[1], b[2], (gen, off, ep))
             else:
-                mask = ar.view(off, self.prog.ds.nwords, torch.int64)
+                mask = SlotArena.view(buf, off, self.prog.ds.nwords, torch.int64)
                 b = self._make(mask) + ((gen, off, ep),)
             with self._slot_lock:
                 self._slots[slot] = b

@@ -36,6 +36,14 @@ from ..utils.cancel import checkpoint
 
 # segment-batched execution overlaps batch j's merge collectives with batch j+1's scan
 PIPELINE_MERGE = os.environ.get("SDO_PIPELINE_MERGE", "1") not in ("0", "")
+# ... and is chosen by itself across ranks (no segments_per_query asked for) when the dense state
+# is large and keyed by a leading time bucket: each batch then merges only its time slice of the
+# table while the next batch scans, so all but the last slice's collective hide behind scans.
+# Small states are never split: their merge is latency-bound, every batch would pay it again and
+# the last one stays exposed anyway.
+AUTO_PIPELINE = os.environ.get("SDO_AUTO_PIPELINE", "1") not in ("0", "")
+AUTO_PIPELINE_MIN_BYTES = int(os.environ.get("SDO_AUTO_PIPELINE_MIN_BYTES", str(256 << 10)))
+AUTO_PIPELINE_BATCHES = int(os.environ.get("SDO_AUTO_PIPELINE_BATCHES", "3"))
 # existence-only group-bys over the key's dictionary domain (engine/dict_exist.py)
 DICT_EXIST = os.environ.get("SDO_DICT_EXIST", "1") not in ("0", "")
 # GPU-event phase attribution of PreparedQuery.run (scan / merge / gather / finalize)
@@ -204,6 +212,9 @@ class PreparedQuery:
             self.window = shard_window(prog, ds, self.world)
             if self.window is not None:
                 prog = self.window.local
+            if not segments_per_query and self.window is None:
+                segments_per_query = self._auto_batches(prog, ds)
+                self.segments_per_query = segments_per_query
             if segments_per_query:
                 # "historical" execution: one partial query per batch of segments, merged here
                 for bprog in segment_batches(prog, ds, segments_per_query):
@@ -233,6 +244,28 @@ class PreparedQuery:
             self._nbatches = int(self.world.max_float(float(len(self.scans))))
             if self._nbatches > 1:
                 self._slices = self._batch_key_slices(self.scans[0][1])
+
+    def _auto_batches(self, prog: ScanProgram, ds: DataSource) -> Optional[int]:
+        """Segments per batch for an automatically pipelined multi-rank scan (``AUTO_PIPELINE``), or
+        None.  Decided from the layout alone -- the packed key, slots and sketches are the same on
+        every rank, the shard's row ranges are not -- plus one agreement that every rank's scan keeps
+        dense partials, so all ranks take the same (pipelined or one-merge) collective pattern."""
+        if not (AUTO_PIPELINE and PIPELINE_MERGE and self.world.distributed) or \
+                self.qs.queryType not in ("groupBy", "timeseries", "topN"):
+            return None
+        G = int(prog.G)
+        lead = [kc for kc in prog.keys if kc.stride * max(1, kc.card) == G]
+        if not lead or not getattr(lead[0], "is_timestamp", False) or max(1, lead[0].card) < AUTO_PIPELINE_BATCHES:
+            return None
+        nbytes = G * max(1, prog.nslots) * 8 + prog.nhll_total * G * (1 << prog.hll_p)
+        if nbytes < AUTO_PIPELINE_MIN_BYTES:
+            return None
+        probe = self._prepare(prog)
+        dense = probe is None or getattr(probe, "mode", None) in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL)
+        if -self.world.max_float(-float(dense)) < 1.0:  # (min over ranks)
+            return None
+        nseg = sum(1 for sg in ds.segments if any(min(hi, sg.row_hi) > max(lo, sg.row_lo) for lo, hi in prog.ranges))
+        return max(1, -(-nseg // AUTO_PIPELINE_BATCHES))
 
     def _prepare(self, prog: ScanProgram):
         if is_cuda_ds(self.ds) and self.engine.use_native:

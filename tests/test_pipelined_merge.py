@@ -1,5 +1,7 @@
 """Segment-batched ("historical") execution across ranks with batch j's merge collectives
-overlapping batch j+1's scan (``PreparedQuery._run_pipelined``, ``parallel/merge.start_dense_merge``).
+overlapping batch j+1's scan (``PreparedQuery._run_pipelined``, ``parallel/merge.start_dense_merge``),
+asked for (``segments_per_query``) or chosen by itself on the default path (``AUTO_PIPELINE``: a large
+dense state keyed by a leading time bucket).
 
 Ranks hold shards of different sizes, so their batch counts differ: the smaller shard pads with
 identity partials after agreeing on the count.  Results must equal the one-merge-after-combine
@@ -103,6 +105,21 @@ def _work(rank, world, port, outdir, device="cpu"):
         finally:
             cost.ONESHOT_MAX_BYTES = saved
             X.PIPELINE_MERGE = True
+    # the default path (no segments_per_query): a time-leading dense state above the size threshold
+    # pipelines by itself, with the batch count agreed across ranks; below it, one merge
+    saved_min = X.AUTO_PIPELINE_MIN_BYTES
+    X.AUTO_PIPELINE_MIN_BYTES = 512
+    try:
+        p = eng.prepare(_ts_month(), ds)
+        a = p.run().sorted_rows()
+        X.AUTO_PIPELINE = False
+        q0 = eng.prepare(_ts_month(), ds)
+        b = q0.run().sorted_rows()
+        out["auto"] = (a, b, p._nbatches, bool(p.segments_per_query), p._pipeline_ok, bool(q0.segments_per_query))
+    finally:
+        X.AUTO_PIPELINE, X.AUTO_PIPELINE_MIN_BYTES = True, saved_min
+    small = eng.prepare(query_from_json(DRUID_JSON["TPCH Q1"]), ds)
+    out["auto_small"] = bool(small.segments_per_query)
     # a scan failure in the second batch of rank 0: both ranks abort consistently
     q = query_from_json(DRUID_JSON["TPCH Q1"])
     p = eng.prepare(q, ds, segments_per_query=2)
@@ -187,6 +204,11 @@ def _check(outs, device):
                 else:
                     assert ok is True and nbatches >= nscans
             assert _close(per_rank[0][0], per_rank[-1][0])
+    for o in outs:
+        a, b, nb, auto, ok, off = o["auto"]
+        assert _close(a, b) and auto and ok is True and nb > 1 and not off, o["auto"][2:]
+        assert not o["auto_small"]  # Q1's 4-group state: never split
+    assert len({o["auto"][2] for o in outs}) == 1
     # the small last shard ran fewer batches than the agreed count (identity padding exercised)
     last = outs[-1][("TPCH Q1", True)]
     assert last[3] < last[2]

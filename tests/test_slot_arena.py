@@ -21,16 +21,16 @@ def test_carve_restarts_per_statement_and_tracks_intact_regions():
     ar = DE.SlotArena("cpu", 91)
     a, b, c = _Owner(), _Owner(), _Owner()
     with use_slot(91):
-        ga, oa, ia = ar.carve(1000, a)
-        gb, ob, ib = ar.carve(5000, b)
+        ga, oa, ia, _ = ar.carve(1000, a)
+        gb, ob, ib, _ = ar.carve(5000, b)
     assert (oa, ob) == (0, 1024) and not ia and not ib  # 256-byte aligned bump, first carve: not intact
     with use_slot(91):  # the same statement again: the same offsets, contents as left
-        assert ar.carve(1000, a) == (ga, 0, True)
-        assert ar.carve(5000, b) == (gb, 1024, True)
+        assert ar.carve(1000, a)[:3] == (ga, 0, True)
+        assert ar.carve(5000, b)[:3] == (gb, 1024, True)
     with use_slot(91):  # another statement carves over a's region
-        assert ar.carve(3000, c)[1:] == (0, False)
+        assert ar.carve(3000, c)[1:3] == (0, False)
     with use_slot(91):
-        assert ar.carve(1000, a)[1:] == (0, False)   # a's bytes were overwritten by c
+        assert ar.carve(1000, a)[1:3] == (0, False)   # a's bytes were overwritten by c
         assert ar.carve(5000, b)[2] is False          # c's 3072 bytes overlapped b's region too
     assert ar.cap == DE.ARENA_MIN  # one storage for all of it
 
@@ -40,11 +40,11 @@ def test_growth_keeps_earlier_views_and_sizes_for_the_whole_statement(monkeypatc
     ar = DE.SlotArena("cpu", 92)
     a, b = _Owner(), _Owner()
     with use_slot(92):
-        g0, off, _ = ar.carve(3000, a)
-        va = ar.view(off, 375, torch.int64)
+        g0, off, _, buf = ar.carve(3000, a)
+        va = DE.SlotArena.view(buf, off, 375, torch.int64)
         va.fill_(7)
         a._slots[92] = "bufs"
-        g1, off_b, _ = ar.carve(6000, b)  # does not fit: a new storage, a's view stays valid
+        g1, off_b, _, _ = ar.carve(6000, b)  # does not fit: a new storage, a's view stays valid
         assert g1 == g0 + 1 and off_b == 0
         assert int(va.sum()) == 7 * 375
         assert 92 not in a._slots  # a re-carves at its next run
@@ -118,3 +118,38 @@ def test_parameterizations_share_the_slot_arena():
     assert len(ptrs) == 1, "the parameterizations did not share the slot's arena region"
     ar = DE.slot_arena(ds.device, 1)
     assert ar.cap < 4 * ar.need + DE.ARENA_MIN
+
+
+def test_partition_scratch_pool_budget_reuse_and_wait(monkeypatch):
+    """The device-wide partition scratch (engine/device_exec.py PartScratchPool): slabs are reused
+    smallest-fit, a new slab over the byte budget waits for a release from another thread, and a
+    thread that already holds one (hashed re-partition) never waits."""
+    import time
+
+    monkeypatch.setattr(DE, "PART_SCRATCH_BUDGET", 20000)  # bytes: a 1000-word and a 1250-word slab
+    pool = DE.PartScratchPool()
+    a = pool.acquire("cpu", 1000)
+    assert a.recs1.numel() == 1000 and pool.bytes() == 8000
+    nested = pool.acquire("cpu", 1500)  # same thread holds one: over budget without waiting
+    assert pool.bytes() == 8000 + 12000
+    pool.release(nested)
+    got = {}
+
+    def other():
+        t0 = time.perf_counter()
+        got["slab"] = pool.acquire("cpu", 2000)  # does not fit next to a: waits for a release
+        got["waited"] = time.perf_counter() - t0
+        pool.release(got["slab"])
+
+    th = threading.Thread(target=other)
+    th.start()
+    time.sleep(0.3)
+    assert "slab" not in got
+    pool.release(a)
+    th.join(5)
+    assert got["slab"].words == 2000 and got["waited"] >= 0.25
+    again = pool.acquire("cpu", 900)  # smallest free slab that fits is reused
+    assert again.words == 2000 and pool.bytes() == 16000
+    pool.release(again)
+    pool.clear()
+    assert pool.bytes() == 0

@@ -344,8 +344,18 @@ def main():
                       "exec_wall_ms": round(1e3 * sum(w for _, w in exec_cost[:ncost]) / max(1, ncost), 3),
                       "executors": getattr(srv, "nexec", None),
                       "coalesced": co1 - co0, "slots": co.scheduler.nslots,
-                      "slot_wait_ms_total": round(co.scheduler.stats["wait_ms"], 1)}}
+                      "slot_wait_ms_total": round(co.scheduler.stats["wait_ms"], 1)},
+           "device_memory": _mem_report()}
     print(json.dumps(out), flush=True)
+
+
+def _mem_report():
+    try:
+        from spark_druid_olap_amd.engine.device_exec import device_memory_report
+
+        return device_memory_report()
+    except Exception as e:  # noqa: BLE001
+        return {"error": str(e)}
 
 
 if __name__ == "__main__":
