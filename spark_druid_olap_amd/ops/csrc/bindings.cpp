@@ -547,6 +547,13 @@ static void part_keys(uint64_t keys, int64_t n, int shift1, int P1, uint64_t cou
   check(hipGetLastError(), "part_keys_kernel launch");
 }
 
+// Probe knob (tools/part_probe.py A/B runs): records per thread of the scatter tile (0: by width).
+static int g_part_pu = 0;
+static void part_tune(int pu) {
+  if (pu != 0 && pu != 1 && pu != 2 && pu != 4 && pu != 8) throw std::invalid_argument("part_tune: pu in {0,1,2,4,8}");
+  g_part_pu = pu;
+}
+
 // groups x K blocks; group g's segments are [g*spg, (g+1)*spg) of seg_lo/seg_hi (a level-1 bucket
 // table passes base1 and base1 + 1 with spg = 1).
 static void part_split(uint64_t in, int RW, uint64_t seg_lo, uint64_t seg_hi, int64_t groups, int spg, int K,
@@ -556,7 +563,7 @@ static void part_split(uint64_t in, int RW, uint64_t seg_lo, uint64_t seg_hi, in
   if (RW < 1 || RW > 2 + 2 * sdo::MAX_SLOTS) throw std::invalid_argument("part_split: record width");
   if (spg < 1) throw std::invalid_argument("part_split: segments per group");
   // tile of 512 x PU records, ~32 KB of LDS whatever the record width
-  const int PU = RW <= 2 ? 8 : (RW <= 4 ? 4 : (RW <= 8 ? 2 : 1));
+  const int PU = g_part_pu ? g_part_pu : (RW <= 2 ? 8 : (RW <= 4 ? 4 : (RW <= 8 ? 2 : 1)));
   // odd tile stride for even record widths >= 4 (conflict-free strided tile reads) when it fits
   int RS = RW;
   if (RW >= 4 && RW % 2 == 0 && ((int64_t)3 * P2 + (int64_t)512 * PU * (RW + 1)) * 4 <= 64 * 1024) RS = RW + 1;
@@ -902,6 +909,7 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("part_scan", &part_scan);
   m.def("part_keys", &part_keys);
   m.def("part_split", &part_split);
+  m.def("part_tune", &part_tune);
   m.def("part_agg", &part_agg);
   m.def("part_agg_hll", &part_agg_hll);
   m.def("part_hash_agg", &part_hash_agg);
