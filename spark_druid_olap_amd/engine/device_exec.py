@@ -499,19 +499,22 @@ class PreparedScan:
         # level 1: one input group = every chunk region, P1 buckets by the top key bits
         a1 = (pb["recs1"].data_ptr(), rw, pb["seg_lo"].data_ptr(), pb["pend"].data_ptr(), 1, pb["nch"], k1,
               L["shift1"], P1, pb["counts1"].data_ptr())
-        nat.part_split(*a1, 0, 0, 0, st)
+        # dense keys arrive in runs (rows in time order, then key order within a day): the split
+        # kernels' same-bucket waves add once (partition.hip lds_count_add); hashes are uniform
+        cl = 0 if L.get("hashed") else 2
+        nat.part_split(*a1, 0, 0, cl, st)
         nat.part_scan(pb["counts1"].data_ptr(), P1, k1, pb["totals1"].data_ptr(), pb["base1"].data_ptr(), st)
-        nat.part_split(*a1, pb["base1"].data_ptr(), pb["recs2"].data_ptr(), 1, st)
+        nat.part_split(*a1, pb["base1"].data_ptr(), pb["recs2"].data_ptr(), 1 | cl, st)
         recs, base = pb["recs2"], pb["base1"]
         if L["levels"] == 2:
             # level 2: group p = level-1 bucket p (one segment [base1[p], base1[p+1])), P2 sub-buckets
             b1 = pb["base1"].data_ptr()
             a2 = (pb["recs2"].data_ptr(), rw, b1, b1 + 4, P1, 1, L["k"], L["shift"], L["p2"],
                   pb["counts2"].data_ptr())
-            nat.part_split(*a2, 0, 0, 0, st)
+            nat.part_split(*a2, 0, 0, cl, st)
             nat.part_scan(pb["counts2"].data_ptr(), L["nsub"], L["k"], pb["totals2"].data_ptr(),
                           pb["base2"].data_ptr(), st)
-            nat.part_split(*a2, pb["base2"].data_ptr(), pb["recs1"].data_ptr(), 1, st)
+            nat.part_split(*a2, pb["base2"].data_ptr(), pb["recs1"].data_ptr(), 1 | cl, st)
             recs, base = pb["recs1"], pb["base2"]
         if L.get("hashed"):
             return self._run_part_hashed(b, recs, base)
@@ -1184,9 +1187,9 @@ class PreparedEmit:
             nat.module_launch(self.jit.handle, desc.data_ptr(), int(self.grid), BLOCK, int(self.jit.lay.total), st)
             a = (slab.recs1.data_ptr(), 2, self.seg_lo.data_ptr(), pend.data_ptr(), 1, self.nch, self.k, 0, 1,
                  counts.data_ptr())
-            nat.part_split(*a, 0, 0, 0, st)
+            nat.part_split(*a, 0, 0, 2, st)  # (one bucket: every wave adds once)
             nat.part_scan(counts.data_ptr(), 1, self.k, totals.data_ptr(), base.data_ptr(), st)
-            nat.part_split(*a, base.data_ptr(), slab.recs2.data_ptr(), 1, st)
+            nat.part_split(*a, base.data_ptr(), slab.recs2.data_ptr(), 3, st)
             n = int(base[1].item())
             rec = slab.recs2[: 2 * n].view(n, 2).to(torch.int64) & 0xFFFFFFFF
             return rec[:, 0].contiguous(), rec[:, 1].contiguous()

@@ -18,6 +18,7 @@ shard on the device and cached, like the dictionaries themselves.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import numpy as np
@@ -71,25 +72,58 @@ def _leaf_cols(x, out: set) -> bool:
     return False  # time / numeric / expression leaves read rows
 
 
+_TRACE = bool(os.environ.get("SDO_TRACE_DICT_EXIST"))
+
+
 def plan(prog) -> Optional[Tuple[str, Tuple[str, ...]]]:
     """(key dimension, dimensions the filter reads) when the program qualifies, else None.
     Structural checks only (no device work)."""
+    r, why = _plan(prog)
+    if _TRACE:
+        print(f"[dict_exist] plan keys={[k.name for k in prog.keys]} G={prog.G} -> {r or why}", flush=True)
+    return r
+
+
+def _plan(prog):
     ds = prog.ds
     if prog.empty or not prog.presence_only or prog.nhll or prog.stored_hll or prog.thetas:
-        return None
+        return None, "not existence-only"
     if len(prog.keys) != 1 or prog.nslots != 1 or getattr(ds, "fd_source", None) is not None:
-        return None
+        return None, "not one key"
     kc = prog.keys[0]
     if kc.kind not in (D.K_ID, D.K_REMAP) or kc.col not in ds.dims:
-        return None
-    if sum(hi - lo for lo, hi in prog.ranges) < ds.num_rows:
-        return None  # a time restriction: rows decide
+        return None, "key not a dimension id"
+    covered = sum(hi - lo for lo, hi in prog.ranges)
+    if covered < ds.num_rows:
+        return None, f"time restriction ({covered} of {ds.num_rows} rows)"  # rows decide
     cols: set = set()  # (zone maps are chunk-pruning hints implied by these leaves)
     if not _leaf_cols(prog.bexpr, cols) or any(c not in ds.dims for c in cols):
-        return None
+        return None, "filter reads more than id sets"
     if len(ds.dims[kc.col].dictionary) > ds.num_rows:
-        return None  # more dictionary entries than rows: the scan is cheaper
-    return kc.col, tuple(sorted(cols - {kc.col}))
+        return None, "dictionary larger than the shard"  # the scan is cheaper
+    return (kc.col, tuple(sorted(cols - {kc.col}))), ""
+
+
+_MASKS: "dict" = {}  # id(host id-set array) -> (array, device copy)
+_MASKS_LOCK = __import__("threading").Lock()
+
+
+def _device_mask(arr, dev) -> torch.Tensor:
+    """The device copy of a filter leaf's id set, made once per lowered program: TPC-H Q13's
+    o_comment set has one entry per distinct comment (~150M at SF100) and its pageable upload was
+    9 of the query's 17 ms.  Keyed by the array object (kept alive in the entry, so the id is not
+    reused while cached); bounded to the most recent leaves."""
+    k = (id(arr), str(dev))
+    with _MASKS_LOCK:
+        hit = _MASKS.get(k)
+        if hit is not None and hit[0] is arr:
+            return hit[1]
+    m = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.bool_)).to(dev)
+    with _MASKS_LOCK:
+        _MASKS[k] = (arr, m)
+        while len(_MASKS) > 64:
+            _MASKS.pop(next(iter(_MASKS)))
+    return m
 
 
 def _eval(x, key_col: str, masks: dict, n: int, dev) -> torch.Tensor:
@@ -110,7 +144,7 @@ def _eval(x, key_col: str, masks: dict, n: int, dev) -> torch.Tensor:
         return out
     if k == "not":
         return ~_eval(x[1], key_col, masks, n, dev)
-    m = torch.from_numpy(np.ascontiguousarray(x[2], dtype=np.bool_)).to(dev)
+    m = _device_mask(x[2], dev)
     if x[1] == key_col:
         return m[:n] if m.numel() >= n else torch.nn.functional.pad(m, (0, n - m.numel()))
     fd = masks[x[1]]  # key id -> dependent id (int32; -1: absent everywhere, so never occurring)
@@ -127,6 +161,8 @@ def run(prog, key_col: str, dep_cols, world=None) -> Optional[Partials]:
     for c in dep_cols:
         t = fd_table(ds, key_col, c, world)
         if t is None:
+            if _TRACE:
+                print(f"[dict_exist] {key_col} does not determine {c}: scanning rows", flush=True)
             return None
         fds[c] = t
     occ = occurrence(ds, key_col)

@@ -550,7 +550,8 @@ static void part_keys(uint64_t keys, int64_t n, int shift1, int P1, uint64_t cou
 // Probe knob (tools/part_probe.py A/B runs): records per thread of the scatter tile (0: by width).
 static int g_part_pu = 0;
 static void part_tune(int pu) {
-  if (pu != 0 && pu != 1 && pu != 2 && pu != 4 && pu != 8) throw std::invalid_argument("part_tune: pu in {0,1,2,4,8}");
+  if (pu != 0 && pu != 1 && pu != 2 && pu != 4 && pu != 8 && pu != 16 && pu != 32)
+    throw std::invalid_argument("part_tune: pu in {0,1,2,4,8,16,32}");
   g_part_pu = pu;
 }
 
@@ -566,10 +567,15 @@ static void part_split(uint64_t in, int RW, uint64_t seg_lo, uint64_t seg_hi, in
   const int PU = g_part_pu ? g_part_pu : (RW <= 2 ? 8 : (RW <= 4 ? 4 : (RW <= 8 ? 2 : 1)));
   // odd tile stride for even record widths >= 4 (conflict-free strided tile reads) when it fits
   int RS = RW;
-  if (RW >= 4 && RW % 2 == 0 && ((int64_t)3 * P2 + (int64_t)512 * PU * (RW + 1)) * 4 <= 64 * 1024) RS = RW + 1;
-  const int64_t lds = phase == 0 ? (int64_t)P2 * 4 : ((int64_t)3 * P2 + (int64_t)512 * PU * RS) * 4;
-  if (lds > 64 * 1024) throw std::invalid_argument("part_split: tile does not fit 64 KiB of LDS");
-  const void* f = PU == 8 ? (const void*)sdo::part_split_kernel<8>
+  const int64_t lds_max = PU > 8 ? 160 * 1024 : 64 * 1024;
+  if (RW >= 4 && RW % 2 == 0 && ((int64_t)3 * P2 + (int64_t)512 * PU * (RW + 1)) * 4 <= lds_max) RS = RW + 1;
+  // (phase bit 1: clustered keys, see partition.hip part_split_kernel)
+  if ((phase & ~3) != 0) throw std::invalid_argument("part_split: phase");
+  const int64_t lds = (phase & 1) == 0 ? (int64_t)P2 * 4 : ((int64_t)3 * P2 + (int64_t)512 * PU * RS) * 4;
+  if (lds > lds_max) throw std::invalid_argument("part_split: tile does not fit the LDS");
+  const void* f = PU == 32 ? (const void*)sdo::part_split_kernel<32>
+                : PU == 16 ? (const void*)sdo::part_split_kernel<16>
+                : PU == 8 ? (const void*)sdo::part_split_kernel<8>
                 : PU == 4 ? (const void*)sdo::part_split_kernel<4>
                 : PU == 2 ? (const void*)sdo::part_split_kernel<2> : (const void*)sdo::part_split_kernel<1>;
   const uint32_t* in_ = (const uint32_t*)in;
@@ -580,6 +586,7 @@ static void part_split(uint64_t in, int RW, uint64_t seg_lo, uint64_t seg_hi, in
   uint32_t* o = (uint32_t*)out;
   void* args[] = {(void*)&in_, (void*)&RW, (void*)&RS, (void*)&lo_, (void*)&hi_, (void*)&spg, (void*)&K,
                   (void*)&shift2, (void*)&P2, (void*)&c2, (void*)&b2, (void*)&o, (void*)&phase};
+  if (lds > 64 * 1024) check(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "part_split attr");
   check(hipLaunchKernel(f, dim3((unsigned)(groups * K)), dim3(512), args, (size_t)lds, (hipStream_t)stream),
         "part_split_kernel launch");
   check(hipGetLastError(), "part_split_kernel launch");

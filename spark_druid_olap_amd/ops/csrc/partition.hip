@@ -57,6 +57,54 @@ __device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t v, uint32_t* ld
   return pre + inc - v;
 }
 
+// LDS bucket counters under clustered keys.  Producer chunk regions hold rows in time order and,
+// within a day, in key order, so a wave's 64 consecutive records usually share ONE bucket: a plain
+// per-lane atomic then serializes 64 ways on one LDS address (TPC-H Q18's level-1 count: 2.0 ms,
+// against 0.84 ms on uniform keys, tools/part_probe.py).  When every active lane of the wave has
+// the same bucket, one lane adds the lane count instead; otherwise each lane adds its own 1.  (The
+// check is two ballots and a readlane: free next to the atomics it saves, ~nothing when keys are
+// uniform.)
+__device__ __forceinline__ void lds_count_add(uint32_t* h, uint32_t q, bool act, bool clustered) {
+  if (!clustered) {  // (hashed keys: uniform buckets, the check would only cost)
+    if (act) atomicAdd(&h[q], 1u);
+    return;
+  }
+  const uint64_t am = __ballot(act);
+  if (!am) return;
+  const int leader = __builtin_ctzll(am);
+  const uint32_t q0 = (uint32_t)__builtin_amdgcn_readlane((int)q, leader);
+  if (__ballot(act && q == q0) == am) {
+    if ((int)(threadIdx.x & 63) == leader) atomicAdd(&h[q0], (uint32_t)__popcll(am));
+  } else if (act) {
+    atomicAdd(&h[q], 1u);
+  }
+}
+
+// Rank form, split in two so a tile's PU adds issue back to back and are waited for once: step 1
+// issues the add (one lane for a uniform wave, else every active lane) and returns the uniform-wave
+// mask (0: plain); step 2 turns the returned value into the lane's rank.
+__device__ __forceinline__ uint64_t lds_rank_issue(uint32_t* h, uint32_t q, bool act, uint32_t& raw, bool clustered) {
+  raw = 0u;
+  if (!clustered) {
+    if (act) raw = atomicAdd(&h[q], 1u);
+    return 0ull;
+  }
+  const uint64_t am = __ballot(act);
+  if (!am) return 0ull;
+  const int leader = __builtin_ctzll(am);
+  const uint32_t q0 = (uint32_t)__builtin_amdgcn_readlane((int)q, leader);
+  const bool fast = __ballot(act && q == q0) == am;
+  if (act && (!fast || (int)(threadIdx.x & 63) == leader)) raw = atomicAdd(&h[q], fast ? (uint32_t)__popcll(am) : 1u);
+  return fast ? am : 0ull;
+}
+
+__device__ __forceinline__ uint32_t lds_rank_finish(uint64_t fm, uint32_t raw) {
+  if (!fm) return raw;
+  const int lane = threadIdx.x & 63;
+  const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)raw, __builtin_ctzll(fm));
+  return base + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
+}
+
 // rows of <= 64 columns: one thread per row
 __global__ void part_rowscan_small_kernel(uint32_t* __restrict__ c, int64_t R, int B, uint32_t* __restrict__ totals) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -122,15 +170,18 @@ __global__ __launch_bounds__(512) void part_keys_kernel(const int64_t* __restric
   __syncthreads();
   const int64_t per = (n + B - 1) / B;
   const int64_t a = (int64_t)blockIdx.x * per, e = a + per < n ? a + per : n;
-  for (int64_t i = a + threadIdx.x; i < e; i += blockDim.x) {
-    const uint32_t k = (uint32_t)keys[i];
+  for (int64_t i0 = a; i0 < e; i0 += blockDim.x) {  // (block-uniform trip count: the bucket adds ballot)
+    const int64_t i = i0 + threadIdx.x;
+    const uint32_t k = i < e ? (uint32_t)keys[i] : 0u;
     const uint32_t p = k >> shift1;
-    if (p >= (uint32_t)P1) continue;  // outside [0, P1 << shift1): never counted, never written
+    const bool act = i < e && p < (uint32_t)P1;  // outside [0, P1 << shift1): never counted, never written
     if (phase == 0) {
-      atomicAdd(&h[p], 1u);
+      lds_count_add(h, p, act, false);
     } else {
-      const uint32_t pos = atomicAdd(&h[p], 1u);
-      out[pos] = k;
+      uint32_t raw;
+      const uint64_t fm = lds_rank_issue(h, p, act, raw, false);
+      const uint32_t pos = lds_rank_finish(fm, raw);
+      if (act) out[pos] = k;
     }
   }
   if (phase == 0) {
@@ -152,7 +203,7 @@ __global__ __launch_bounds__(512) void part_keys_kernel(const int64_t* __restric
 // records widen (the tile stays ~32 KB of LDS).
 
 __device__ __forceinline__ void split_range_count(const uint32_t* __restrict__ in, int RW, uint32_t lo, uint32_t hi,
-                                                  int shift2, uint32_t mask, uint32_t* h) {
+                                                  int shift2, uint32_t mask, uint32_t* h, bool clustered) {
   if (RW == 2) {
     // two records per 16-byte load, 8 records per thread in flight
     uint32_t i = lo;
@@ -163,34 +214,36 @@ __device__ __forceinline__ void split_range_count(const uint32_t* __restrict__ i
     if (i >= hi) return;  // (empty, or the single odd record above)
     const uint32_t npair = (hi - i) / 2;
     const uint4* pr = (const uint4*)(in + (uint64_t)i * 2);
-    for (uint32_t j0 = threadIdx.x; j0 < npair; j0 += blockDim.x * 4) {
+    for (uint32_t b0 = 0; b0 < npair; b0 += blockDim.x * 4) {  // (block-uniform trip count)
       uint4 v[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const uint32_t j = j0 + u * blockDim.x;
+        const uint32_t j = b0 + threadIdx.x + u * blockDim.x;
         if (j < npair) v[u] = pr[j];
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        if (j0 + u * blockDim.x < npair) {
-          atomicAdd(&h[(v[u].x >> shift2) & mask], 1u);
-          atomicAdd(&h[(v[u].z >> shift2) & mask], 1u);
-        }
+        const bool act = b0 + threadIdx.x + u * blockDim.x < npair;
+        // (records 2j and 2j+1 of a lane are neighbours: each half combines across the wave)
+        lds_count_add(h, act ? (v[u].x >> shift2) & mask : 0u, act, clustered);
+        lds_count_add(h, act ? (v[u].z >> shift2) & mask : 0u, act, clustered);
       }
     }
     if (((hi - i) & 1u) && threadIdx.x == 0) atomicAdd(&h[(in[(uint64_t)(hi - 1) * 2] >> shift2) & mask], 1u);
     return;
   }
-  for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += blockDim.x * 4) {
+  for (uint32_t b0 = lo; b0 < hi; b0 += blockDim.x * 4) {  // (block-uniform trip count)
     uint32_t key[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const uint32_t i = i0 + u * blockDim.x;
+      const uint32_t i = b0 + threadIdx.x + u * blockDim.x;
       key[u] = i < hi ? in[(uint64_t)i * RW] : 0u;
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (i0 + u * blockDim.x < hi) atomicAdd(&h[(key[u] >> shift2) & mask], 1u);
+    for (int u = 0; u < 4; ++u) {
+      const bool act = b0 + threadIdx.x + u * blockDim.x < hi;
+      lds_count_add(h, (key[u] >> shift2) & mask, act, clustered);
+    }
   }
 }
 
@@ -198,7 +251,7 @@ template <int PU>
 __device__ __forceinline__ void split_range_scatter(const uint32_t* __restrict__ in, int RW, int RS, uint32_t lo, uint32_t hi,
                                                     int shift2, uint32_t P2, uint32_t* cur, uint32_t* hist,
                                                     uint32_t* tstart, uint32_t* tile, uint32_t* scan_lds,
-                                                    uint32_t* __restrict__ out) {
+                                                    uint32_t* __restrict__ out, bool clustered) {
   const uint32_t mask = P2 - 1u;
   constexpr uint32_t TILE = 512u * PU;
   for (uint32_t t0 = lo; t0 < hi; t0 += TILE) {
@@ -220,14 +273,16 @@ __device__ __forceinline__ void split_range_scatter(const uint32_t* __restrict__
         }
       }
     }
+    uint64_t fm_[PU];
 #pragma unroll
     for (int u = 0; u < PU; ++u) {
       const uint32_t j = threadIdx.x + u * blockDim.x;
-      if (j < tn) {
-        q_[u] = (v2[u].x >> shift2) & mask;
-        r_[u] = atomicAdd(&hist[q_[u]], 1u);
-      }
+      const bool act = j < tn;
+      q_[u] = act ? (v2[u].x >> shift2) & mask : 0u;
+      fm_[u] = lds_rank_issue(hist, q_[u], act, r_[u], clustered);
     }
+#pragma unroll
+    for (int u = 0; u < PU; ++u) r_[u] = lds_rank_finish(fm_[u], r_[u]);
     __syncthreads();
     // exclusive scan of the tile histogram -> bucket starts inside the tile; a thread's `per`
     // consecutive counters move as one 8- / 16-byte LDS access (consecutive lanes, consecutive
@@ -319,6 +374,10 @@ __global__ __launch_bounds__(512) void part_split_kernel(const uint32_t* __restr
                                                         int phase) {
   extern __shared__ __attribute__((aligned(16))) uint32_t h[];
   __shared__ uint32_t scan_lds[8];
+  // phase bit 0: 0 count / 1 scatter; bit 1: the keys come in runs (dense keys of producer chunk
+  // regions and their level-1 buckets; not hashes): same-bucket waves add once (lds_count_add)
+  const bool clustered = (phase & 2) != 0;
+  phase &= 1;
   const int64_t g = blockIdx.x / K;
   const int k = blockIdx.x % K;
   const int64_t row0 = g * P2;
@@ -333,15 +392,15 @@ __global__ __launch_bounds__(512) void part_split_kernel(const uint32_t* __restr
     const uint32_t lo = seg_lo[g], hi = seg_hi[g];
     const uint64_t n = hi > lo ? hi - lo : 0;
     const uint32_t a = lo + (uint32_t)(n * k / K), e = lo + (uint32_t)(n * (k + 1) / K);
-    if (phase == 0) split_range_count(in, RW, a, e, shift2, mask, h);
-    else split_range_scatter<PU>(in, RW, RS, a, e, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds, out);
+    if (phase == 0) split_range_count(in, RW, a, e, shift2, mask, h, clustered);
+    else split_range_scatter<PU>(in, RW, RS, a, e, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds, out, clustered);
   } else {
     const int64_t s0 = g * spg + (int64_t)spg * k / K, s1 = g * spg + (int64_t)spg * (k + 1) / K;
     for (int64_t sgi = s0; sgi < s1; ++sgi) {
       const uint32_t lo = seg_lo[sgi], hi = seg_hi[sgi];
       if (hi <= lo) continue;  // (uniform across the block: every thread reads the same segment)
-      if (phase == 0) split_range_count(in, RW, lo, hi, shift2, mask, h);
-      else split_range_scatter<PU>(in, RW, RS, lo, hi, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds, out);
+      if (phase == 0) split_range_count(in, RW, lo, hi, shift2, mask, h, clustered);
+      else split_range_scatter<PU>(in, RW, RS, lo, hi, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds, out, clustered);
     }
   }
   if (phase == 0) {
@@ -350,6 +409,10 @@ __global__ __launch_bounds__(512) void part_split_kernel(const uint32_t* __restr
   }
 }
 
+template __global__ void part_split_kernel<32>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int, int,
+                                              uint32_t*, const uint32_t*, uint32_t*, int);
+template __global__ void part_split_kernel<16>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int, int,
+                                              uint32_t*, const uint32_t*, uint32_t*, int);
 template __global__ void part_split_kernel<8>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int, int,
                                              uint32_t*, const uint32_t*, uint32_t*, int);
 template __global__ void part_split_kernel<4>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int, int,

@@ -26,7 +26,11 @@ def main():
     ap.add_argument("--fill", type=float, default=1.0, help="fraction of each 4096-record chunk region used")
     ap.add_argument("--pu", default="0", help="scatter-tile records per thread variants (0 = by width)")
     ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--cluster", type=int, default=0,
+                    help="0: uniform keys; C: each chunk's keys sorted within a random window of G/C keys "
+                         "(the index's order: time, then key within a day)")
     ap.add_argument("--check", type=int, default=1)
+    ap.add_argument("--fast", type=int, default=1, help="1: the split kernels' same-bucket-wave path (clustered keys)")
     a = ap.parse_args()
     import torch
 
@@ -46,7 +50,14 @@ def main():
     gen = torch.Generator(device=dev)
     gen.manual_seed(5)
     view = recs.view(nch, CH, RW)[:, :per_chunk]
-    view[..., 0] = torch.randint(0, G, (nch, per_chunk), generator=gen, device=dev, dtype=torch.int64).to(u32)
+    if a.cluster:
+        span = max(1, G // a.cluster)
+        base = torch.randint(0, max(1, G - span), (nch, 1), generator=gen, device=dev, dtype=torch.int64)
+        k = base + torch.randint(0, span, (nch, per_chunk), generator=gen, device=dev, dtype=torch.int64)
+        view[..., 0] = torch.sort(k, dim=1).values.to(u32)
+        del k, base
+    else:
+        view[..., 0] = torch.randint(0, G, (nch, per_chunk), generator=gen, device=dev, dtype=torch.int64).to(u32)
     if RW > 1:
         view[..., 1] = 1
     seg_lo = (torch.arange(nch, dtype=torch.int64, device=dev) * CH).to(u32)
@@ -78,7 +89,7 @@ def main():
         base2 = torch.empty(nsub + 1, dtype=u32, device=dev)
     acc = torch.empty((G, ns), dtype=torch.int64, device=dev)
     mb = n * RW * 4 / 1e6
-    print(f"n={n} G={G} RW={RW} chunks={nch} fill={a.fill} shift={shift} levels={levels} P1={p1} P2={p2} K={K} "
+    print(f"cluster={a.cluster} fast={a.fast} n={n} G={G} RW={RW} chunks={nch} fill={a.fill} shift={shift} levels={levels} P1={p1} P2={p2} K={K} "
           f"k1={k1} records={mb:.0f} MB", flush=True)
 
     def run(pu):
@@ -87,26 +98,27 @@ def main():
         names = []
         ev[0].record()
         a1 = (recs.data_ptr(), RW, seg_lo.data_ptr(), pend.data_ptr(), 1, nch, k1, shift1, p1, c1.data_ptr())
-        nat.part_split(*a1, 0, 0, 0, st)
+        cl = 2 if a.fast else 0
+        nat.part_split(*a1, 0, 0, cl, st)
         ev[1].record()
         names.append(("count1", 1))
         nat.part_scan(c1.data_ptr(), p1, k1, t1.data_ptr(), base1.data_ptr(), st)
         ev[2].record()
         names.append(("scan1", 0))
-        nat.part_split(*a1, base1.data_ptr(), out1.data_ptr(), 1, st)
+        nat.part_split(*a1, base1.data_ptr(), out1.data_ptr(), 1 | cl, st)
         ev[3].record()
         names.append(("scatter1", 2))
         recs_f, base_f = out1, base1
         if levels == 2:
             b1p = base1.data_ptr()
             a2 = (out1.data_ptr(), RW, b1p, b1p + 4, p1, 1, K, shift, p2, c2.data_ptr())
-            nat.part_split(*a2, 0, 0, 0, st)
+            nat.part_split(*a2, 0, 0, cl, st)
             ev[4].record()
             names.append(("count2", 1))
             nat.part_scan(c2.data_ptr(), nsub, K, t2.data_ptr(), base2.data_ptr(), st)
             ev[5].record()
             names.append(("scan2", 0))
-            nat.part_split(*a2, base2.data_ptr(), out2.data_ptr(), 1, st)
+            nat.part_split(*a2, base2.data_ptr(), out2.data_ptr(), 1 | cl, st)
             ev[6].record()
             names.append(("scatter2", 2))
             recs_f, base_f = out2, base2
