@@ -64,7 +64,7 @@ __global__ void part_rowscan_kernel(uint32_t* c, int64_t R, int B, uint32_t* tot
 __global__ void part_basescan_kernel(const uint32_t* totals, int64_t R, uint32_t* base);
 __global__ void part_keys_kernel(const int64_t* keys, int64_t n, int shift1, int P1, uint32_t* counts1,
                                  const uint32_t* base1, uint32_t* out, int phase);
-template <int PU>
+template <int PU, bool CL>
 __global__ void part_split_kernel(const uint32_t* in, int RW, int RS, const uint32_t* seg_lo, const uint32_t* seg_hi, int spg,
                                   int K, int shift2, int P2, uint32_t* counts2, const uint32_t* base2, uint32_t* out,
                                   int phase);
@@ -567,17 +567,24 @@ static void part_split(uint64_t in, int RW, uint64_t seg_lo, uint64_t seg_hi, in
   const int PU = g_part_pu ? g_part_pu : (RW <= 2 ? 8 : (RW <= 4 ? 4 : (RW <= 8 ? 2 : 1)));
   // odd tile stride for even record widths >= 4 (conflict-free strided tile reads) when it fits
   int RS = RW;
-  const int64_t lds_max = PU > 8 ? 160 * 1024 : 64 * 1024;
+  const int64_t lds_max = 160 * 1024 - 256;
   if (RW >= 4 && RW % 2 == 0 && ((int64_t)3 * P2 + (int64_t)512 * PU * (RW + 1)) * 4 <= lds_max) RS = RW + 1;
   // (phase bit 1: clustered keys, see partition.hip part_split_kernel)
   if ((phase & ~3) != 0) throw std::invalid_argument("part_split: phase");
   const int64_t lds = (phase & 1) == 0 ? (int64_t)P2 * 4 : ((int64_t)3 * P2 + (int64_t)512 * PU * RS) * 4;
   if (lds > lds_max) throw std::invalid_argument("part_split: tile does not fit the LDS");
-  const void* f = PU == 32 ? (const void*)sdo::part_split_kernel<32>
-                : PU == 16 ? (const void*)sdo::part_split_kernel<16>
-                : PU == 8 ? (const void*)sdo::part_split_kernel<8>
-                : PU == 4 ? (const void*)sdo::part_split_kernel<4>
-                : PU == 2 ? (const void*)sdo::part_split_kernel<2> : (const void*)sdo::part_split_kernel<1>;
+  const bool cl = (phase & 2) != 0;
+  phase &= 1;
+  const void* f = cl ? (PU == 32 ? (const void*)sdo::part_split_kernel<32, true>
+                        : PU == 16 ? (const void*)sdo::part_split_kernel<16, true>
+                        : PU == 8 ? (const void*)sdo::part_split_kernel<8, true>
+                        : PU == 4 ? (const void*)sdo::part_split_kernel<4, true>
+                        : PU == 2 ? (const void*)sdo::part_split_kernel<2, true> : (const void*)sdo::part_split_kernel<1, true>)
+                     : (PU == 32 ? (const void*)sdo::part_split_kernel<32, false>
+                        : PU == 16 ? (const void*)sdo::part_split_kernel<16, false>
+                        : PU == 8 ? (const void*)sdo::part_split_kernel<8, false>
+                        : PU == 4 ? (const void*)sdo::part_split_kernel<4, false>
+                        : PU == 2 ? (const void*)sdo::part_split_kernel<2, false> : (const void*)sdo::part_split_kernel<1, false>);
   const uint32_t* in_ = (const uint32_t*)in;
   const uint32_t* lo_ = (const uint32_t*)seg_lo;
   const uint32_t* hi_ = (const uint32_t*)seg_hi;
@@ -628,7 +635,7 @@ static void part_agg_hll(uint64_t recs, int RW, uint64_t base, int64_t nsub, int
     f.init[s] = init[s];
   }
   const int64_t lds = ((int64_t)1 << shift) * (f.nslots * 8 + (int64_t)hl.n * ((int64_t)1 << hl.p));
-  if (shift < 0 || lds > 160 * 1024 - 256 || (hl.n == 0 && lds > 64 * 1024))
+  if (shift < 0 || lds > 160 * 1024 - 256)
     throw std::invalid_argument("part_agg: sub-bucket table exceeds the LDS");
   if (lds > 64 * 1024)  // (the kernel's static LDS counts against the 160 KiB too: exactly the dynamic bytes)
     check(hipFuncSetAttribute((const void*)sdo::part_agg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),

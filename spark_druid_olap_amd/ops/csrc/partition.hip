@@ -202,8 +202,9 @@ __global__ __launch_bounds__(512) void part_keys_kernel(const int64_t* __restric
 // coalesced store sequence instead of 64 scattered lines per wave instruction.  PU shrinks as
 // records widen (the tile stays ~32 KB of LDS).
 
+template <bool CL>
 __device__ __forceinline__ void split_range_count(const uint32_t* __restrict__ in, int RW, uint32_t lo, uint32_t hi,
-                                                  int shift2, uint32_t mask, uint32_t* h, bool clustered) {
+                                                  int shift2, uint32_t mask, uint32_t* h) {
   if (RW == 2) {
     // two records per 16-byte load, 8 records per thread in flight
     uint32_t i = lo;
@@ -225,8 +226,8 @@ __device__ __forceinline__ void split_range_count(const uint32_t* __restrict__ i
       for (int u = 0; u < 4; ++u) {
         const bool act = b0 + threadIdx.x + u * blockDim.x < npair;
         // (records 2j and 2j+1 of a lane are neighbours: each half combines across the wave)
-        lds_count_add(h, act ? (v[u].x >> shift2) & mask : 0u, act, clustered);
-        lds_count_add(h, act ? (v[u].z >> shift2) & mask : 0u, act, clustered);
+        lds_count_add(h, act ? (v[u].x >> shift2) & mask : 0u, act, CL);
+        lds_count_add(h, act ? (v[u].z >> shift2) & mask : 0u, act, CL);
       }
     }
     if (((hi - i) & 1u) && threadIdx.x == 0) atomicAdd(&h[(in[(uint64_t)(hi - 1) * 2] >> shift2) & mask], 1u);
@@ -242,16 +243,16 @@ __device__ __forceinline__ void split_range_count(const uint32_t* __restrict__ i
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const bool act = b0 + threadIdx.x + u * blockDim.x < hi;
-      lds_count_add(h, (key[u] >> shift2) & mask, act, clustered);
+      lds_count_add(h, (key[u] >> shift2) & mask, act, CL);
     }
   }
 }
 
-template <int PU>
+template <int PU, bool CL>
 __device__ __forceinline__ void split_range_scatter(const uint32_t* __restrict__ in, int RW, int RS, uint32_t lo, uint32_t hi,
                                                     int shift2, uint32_t P2, uint32_t* cur, uint32_t* hist,
                                                     uint32_t* tstart, uint32_t* tile, uint32_t* scan_lds,
-                                                    uint32_t* __restrict__ out, bool clustered) {
+                                                    uint32_t* __restrict__ out) {
   const uint32_t mask = P2 - 1u;
   constexpr uint32_t TILE = 512u * PU;
   for (uint32_t t0 = lo; t0 < hi; t0 += TILE) {
@@ -279,7 +280,7 @@ __device__ __forceinline__ void split_range_scatter(const uint32_t* __restrict__
       const uint32_t j = threadIdx.x + u * blockDim.x;
       const bool act = j < tn;
       q_[u] = act ? (v2[u].x >> shift2) & mask : 0u;
-      fm_[u] = lds_rank_issue(hist, q_[u], act, r_[u], clustered);
+      fm_[u] = lds_rank_issue(hist, q_[u], act, r_[u], CL);
     }
 #pragma unroll
     for (int u = 0; u < PU; ++u) r_[u] = lds_rank_finish(fm_[u], r_[u]);
@@ -365,7 +366,10 @@ __device__ __forceinline__ void split_range_scatter(const uint32_t* __restrict__
 
 // dynamic LDS: phase 0: P2 words; phase 1: 3 * P2 + 512 * PU * RS words (RS: the tile's record
 // stride -- RW, or RW + 1 for even widths >= 4 so a wave's consecutive records start on distinct banks)
-template <int PU>
+// CL: the keys come in runs (dense keys of producer chunk regions and their level-1 buckets; not
+// hashes): same-bucket waves add once (lds_count_add) -- a compile-time choice, so the hashed
+// instantiation carries none of its code
+template <int PU, bool CL>
 __global__ __launch_bounds__(512) void part_split_kernel(const uint32_t* __restrict__ in, int RW, int RS,
                                                         const uint32_t* __restrict__ seg_lo,
                                                         const uint32_t* __restrict__ seg_hi, int spg, int K, int shift2,
@@ -374,10 +378,6 @@ __global__ __launch_bounds__(512) void part_split_kernel(const uint32_t* __restr
                                                         int phase) {
   extern __shared__ __attribute__((aligned(16))) uint32_t h[];
   __shared__ uint32_t scan_lds[8];
-  // phase bit 0: 0 count / 1 scatter; bit 1: the keys come in runs (dense keys of producer chunk
-  // regions and their level-1 buckets; not hashes): same-bucket waves add once (lds_count_add)
-  const bool clustered = (phase & 2) != 0;
-  phase &= 1;
   const int64_t g = blockIdx.x / K;
   const int k = blockIdx.x % K;
   const int64_t row0 = g * P2;
@@ -392,15 +392,15 @@ __global__ __launch_bounds__(512) void part_split_kernel(const uint32_t* __restr
     const uint32_t lo = seg_lo[g], hi = seg_hi[g];
     const uint64_t n = hi > lo ? hi - lo : 0;
     const uint32_t a = lo + (uint32_t)(n * k / K), e = lo + (uint32_t)(n * (k + 1) / K);
-    if (phase == 0) split_range_count(in, RW, a, e, shift2, mask, h, clustered);
-    else split_range_scatter<PU>(in, RW, RS, a, e, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds, out, clustered);
+    if (phase == 0) split_range_count<CL>(in, RW, a, e, shift2, mask, h);
+    else split_range_scatter<PU, CL>(in, RW, RS, a, e, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds, out);
   } else {
     const int64_t s0 = g * spg + (int64_t)spg * k / K, s1 = g * spg + (int64_t)spg * (k + 1) / K;
     for (int64_t sgi = s0; sgi < s1; ++sgi) {
       const uint32_t lo = seg_lo[sgi], hi = seg_hi[sgi];
       if (hi <= lo) continue;  // (uniform across the block: every thread reads the same segment)
-      if (phase == 0) split_range_count(in, RW, lo, hi, shift2, mask, h, clustered);
-      else split_range_scatter<PU>(in, RW, RS, lo, hi, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds, out, clustered);
+      if (phase == 0) split_range_count<CL>(in, RW, lo, hi, shift2, mask, h);
+      else split_range_scatter<PU, CL>(in, RW, RS, lo, hi, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds, out);
     }
   }
   if (phase == 0) {
@@ -409,18 +409,30 @@ __global__ __launch_bounds__(512) void part_split_kernel(const uint32_t* __restr
   }
 }
 
-template __global__ void part_split_kernel<32>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int, int,
-                                              uint32_t*, const uint32_t*, uint32_t*, int);
-template __global__ void part_split_kernel<16>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int, int,
-                                              uint32_t*, const uint32_t*, uint32_t*, int);
-template __global__ void part_split_kernel<8>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int, int,
-                                             uint32_t*, const uint32_t*, uint32_t*, int);
-template __global__ void part_split_kernel<4>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int, int,
-                                             uint32_t*, const uint32_t*, uint32_t*, int);
-template __global__ void part_split_kernel<2>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int, int,
-                                             uint32_t*, const uint32_t*, uint32_t*, int);
-template __global__ void part_split_kernel<1>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int, int,
-                                             uint32_t*, const uint32_t*, uint32_t*, int);
+template __global__ void part_split_kernel<32, false>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+template __global__ void part_split_kernel<32, true>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+template __global__ void part_split_kernel<16, false>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+template __global__ void part_split_kernel<16, true>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+template __global__ void part_split_kernel<8, false>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+template __global__ void part_split_kernel<8, true>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+template __global__ void part_split_kernel<4, false>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+template __global__ void part_split_kernel<4, true>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+template __global__ void part_split_kernel<2, false>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+template __global__ void part_split_kernel<2, true>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+template __global__ void part_split_kernel<1, false>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+template __global__ void part_split_kernel<1, true>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
 
 __device__ __forceinline__ void lds_fold(uint64_t* t, int op, int64_t v) {
   switch (op) {
@@ -521,6 +533,44 @@ __global__ __launch_bounds__(512) void part_agg_kernel(const uint32_t* __restric
         const int64_t local = (int64_t)kk[u] - k0;
         if ((uint64_t)local >= (uint64_t)nk) continue;
         lds_fold(t + local * NS + s0, op, 1);
+      }
+    }
+  } else if (RW <= 4 && hl.n == 0) {
+    // narrow records without sketches (TopNSuppliersGlobal: key + f64 revenue + presence, 4 words):
+    // PU records per thread loaded before any is folded, so PU loads are in flight, not one
+    for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += step) {
+      uint32_t r4[PU][4];
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        const uint32_t i = i0 + u * blockDim.x;
+        if (i < hi) {
+          const uint32_t* rec = recs + (uint64_t)i * RW;
+          if (RW == 4) {
+            const uint4 q = *(const uint4*)rec;  // (16-byte records: 16-byte aligned)
+            r4[u][0] = q.x; r4[u][1] = q.y; r4[u][2] = q.z; r4[u][3] = q.w;
+          } else {
+#pragma unroll
+            for (int w = 0; w < 4; ++w) r4[u][w] = w < RW ? rec[w] : 0u;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        if (i0 + u * blockDim.x >= hi) break;
+        const int64_t local = (int64_t)r4[u][0] - k0;
+        if ((uint64_t)local >= (uint64_t)nk) continue;  // cannot happen for consistent buckets; never fault
+        uint64_t* row = t + local * NS;
+        int w = 1;
+        for (int j = 0; j < f.nfields; ++j) {
+          const int wd = f.width[j];
+          int64_t v;
+          if (wd == 0) v = 1;
+          else if (wd == 1) v = (int64_t)(int32_t)r4[u][w & 3];
+          else v = (int64_t)((uint64_t)r4[u][w & 3] | ((uint64_t)r4[u][(w + 1) & 3] << 32));
+          w += wd;
+          const int sl = f.slot[j];
+          lds_fold(row + sl, f.op[sl], v);
+        }
       }
     }
   } else {

@@ -62,7 +62,7 @@ def main():
         view[..., 1] = 1
     seg_lo = (torch.arange(nch, dtype=torch.int64, device=dev) * CH).to(u32)
     pend = seg_lo + per_chunk
-    ns = 2
+    ns = 2 if RW <= 2 else 3  # (RW 4: an i32 and an i64 field, like TopNSuppliersGlobal's records)
     shift = max(0, int(math.floor(math.log2(max(8, a.table // (8 * ns))))))
     gbits = max(1, int(math.ceil(math.log2(max(2, G)))))
     rem = max(0, gbits - shift)
@@ -127,11 +127,13 @@ def main():
             ev[5].record()
             ev[6].record()
             names += [("-", 0), ("-", 0), ("-", 0)]
-        widths = [1] * (RW - 1) if RW > 1 else [0]
-        slots = [1] * len(widths) if RW > 1 else [0]
-        nat.part_agg(recs_f.data_ptr(), RW, base_f.data_ptr(), nsub, G, shift, slots[:1] if RW > 1 else [0],
-                     widths[:1] if RW > 1 else [0], [D.S_SUM_I, D.S_SUM_I], [0, 0], acc.data_ptr(), [], 1, 0, 0, 0, st) \
-            if RW <= 2 else None
+        if RW <= 2:
+            slots, widths = ([1], [1]) if RW == 2 else ([0], [0])
+        else:
+            slots, widths = [1, 2], [1, 2]
+        if 1 + sum(widths) == RW:
+            nat.part_agg(recs_f.data_ptr(), RW, base_f.data_ptr(), nsub, G, shift, slots, widths,
+                         [D.S_SUM_I] * ns, [0] * ns, acc.data_ptr(), [], 1, 0, 0, 0, st)
         ev[7].record()
         names.append(("agg", 1))
         torch.cuda.synchronize()
