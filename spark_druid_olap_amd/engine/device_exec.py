@@ -857,8 +857,15 @@ class PartScratchPool:
                     self.total -= need
                     self.cv.notify_all()
                 raise
-        if sl.event is not None and sl.recs1.is_cuda:
-            torch.cuda.current_stream(sl.recs1.device).wait_event(sl.event)
+        if sl.recs1.is_cuda:
+            cs = torch.cuda.current_stream(sl.recs1.device)
+            if sl.event is not None:
+                cs.wait_event(sl.event)
+            # slabs move between slot streams: the caching allocator must not hand their blocks to
+            # an allocation of the stream they were made on while this stream's kernels still use
+            # them (a slab dropped from the pool is freed at once)
+            sl.recs1.record_stream(cs)
+            sl.recs2.record_stream(cs)
         self.held.n = depth + 1
         return sl
 

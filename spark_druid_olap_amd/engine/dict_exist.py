@@ -116,8 +116,11 @@ def _device_mask(arr, dev) -> torch.Tensor:
     k = (id(arr), str(dev))
     with _MASKS_LOCK:
         hit = _MASKS.get(k)
-        if hit is not None and hit[0] is arr:
-            return hit[1]
+    if hit is not None and hit[0] is arr:
+        m = hit[1]
+        if m.is_cuda:  # (statements on other slot streams read it: an eviction must wait for them)
+            m.record_stream(torch.cuda.current_stream(m.device))
+        return m
     m = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.bool_)).to(dev)
     with _MASKS_LOCK:
         _MASKS[k] = (arr, m)
