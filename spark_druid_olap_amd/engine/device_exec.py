@@ -1204,6 +1204,121 @@ class PreparedEmit:
             PART_POOL.release(slab)
 
 
+def theta_producer_prog(prog: ScanProgram, cols: List[str]) -> ScanProgram:
+    """The scan program of a fused theta producer: ``prog``'s filter, ranges and group key, one
+    A_THETA aggregator (a 62-bit KMV hash, two record words) per theta column, no other aggregator.
+    RuntimeError where it does not apply."""
+    import copy
+
+    from ..ops import jit as J
+
+    ds = prog.ds
+    for c in cols:
+        m = ds.metrics.get(c)
+        if c not in ds.dims and (m is None or m.sketch is not None or m.data.dtype.is_floating_point):
+            raise RuntimeError("theta: fused only over dimension ids / integer metrics")
+    ep = copy.copy(prog)
+    ep.pcols, ep.fcols, ep.section = list(prog.pcols), list(prog.fcols), "p"
+    ep.aops = [{"kind": D.A_THETA, "col": ep.col(c), "expr": None, "filter": None, "slot": i, "hll": -1}
+               for i, c in enumerate(cols)]
+    ep.slots = [(D.S_SUM_I, 0)] * len(cols)
+    ep.nhll, ep.stored_hll, ep.thetas, ep.packed = 0, [], [], {}
+    ep.presence_only = False
+    if not J.part_eligible(ep) or J.part_hashed(ep):
+        raise RuntimeError("theta: program not eligible")
+    return ep
+
+
+class PreparedTheta:
+    """thetaSketch aggregators fused into the scan: ONE JIT producer pass (ops/jit.py A_THETA) writes
+    (u32 group key, 62-bit KMV hash per theta column) records of the selected rows into its chunk
+    regions, and the per-group radix select (ops/csrc/sketch.hip theta_*_regions: LDS histograms,
+    bound, compaction) reads them in place -- no (key, row) pairs, no torch gather / hash of the
+    selected rows, no compaction pass (round-4 SF10 7-group theta query: 29.5 ms).  Only the
+    ~2k candidates per group reach the sort.  Query-time sketches over dimension ids and integer
+    metrics (the hash input must equal ``column_tensor``'s value); G <= ``max_g``."""
+
+    def __init__(self, prog: ScanProgram, cols: List[str], max_g: int):
+        import copy
+
+        from .lower import lds_layout
+        from ..ops import jit as J
+
+        ds = prog.ds
+        if prog.empty or not (0 < prog.G <= max_g):
+            raise RuntimeError("theta: program not eligible")
+        ep = theta_producer_prog(prog, cols)
+        self.prog, self.dev, self.G, self.nt = ep, ds.device, int(prog.G), len(cols)
+        self.jit = _jit_for(ep, D.M_PART, False, 1 << prog.hll_p)
+        if self.jit is None:
+            raise RuntimeError("theta: no JIT kernel")
+        cache_off, wave_bytes, _, total = lds_layout(ep, 0, UNROLL, BLOCK // 64)
+        d = pack(ep, D.M_PART, 0, 0, 0, 0, 0, 0, 0, 0, 0, [], [], unroll=UNROLL, cache_off=cache_off,
+                 wave_bytes=wave_bytes)
+        self.nch = int(d[0]["total_chunks"])
+        self.grid = _grid(self.dev, self.nch, self.jit.lay.total, self.jit)
+        self.rw = 1 + 2 * self.nt
+        cap = self.nch * D.CHUNK_ROWS
+        if cap * self.rw >= (1 << 32):
+            raise RuntimeError("theta: shard too large for u32 offsets")
+        self.words = max(1, cap * self.rw)
+        self.seg_lo = (torch.arange(self.nch, dtype=torch.int64) * D.CHUNK_ROWS).to(torch.int32).to(self.dev)
+        self._d = d
+        # histogram bits: per-workgroup LDS [G][2^bits] u32 within 64 KiB when G allows, else 12
+        fit = int(math.floor(math.log2(max(1, (64 * 1024 // 4) // self.G))))
+        self.bits = fit if fit >= 8 else 12
+        self.bits = max(4, min(16, self.bits))
+
+    def select(self, sizes: List[int]) -> List[torch.Tensor]:
+        """Per theta aggregator (``sizes``: its k) the sorted unique (group, hash) pairs of its k
+        smallest distinct hashes per group."""
+        from .executor import _kmv, _sorted_unique_pairs
+
+        nat, st = native.load(), native._stream(self.dev)
+        pend = torch.empty(max(1, self.nch), dtype=torch.int32, device=self.dev)
+        slab = PART_POOL.acquire(self.dev, self.words)
+        out = []
+        try:
+            d = self._d.copy()
+            d[0]["part_recs"] = slab.recs1.data_ptr()
+            d[0]["part_counts"] = pend.data_ptr()
+            desc = _upload(d.view(np.uint8), self.dev)
+            nat.module_launch(self.jit.handle, desc.data_ptr(), int(self.grid), BLOCK, int(self.jit.lay.total), st)
+            G, dev = self.G, self.dev
+            nrec = int((pend.to(torch.int64) - self.seg_lo.to(torch.int64)).clamp_(min=0).sum().item())
+            hist = torch.empty(G << self.bits, dtype=torch.int32, device=dev)
+            bound = torch.empty(G, dtype=torch.int64, device=dev)
+            count = torch.zeros(1, dtype=torch.int64, device=dev)
+            for t, k in enumerate(sizes):
+                target = torch.full((G,), 2 * k, dtype=torch.int64, device=dev)
+                for attempt in range(7):
+                    if attempt == 6:  # (never in practice after six 4x rounds): every pair
+                        target = torch.full((G,), 1 << 62, dtype=torch.int64, device=dev)
+                    cap = max(1, min(nrec, int(target.clamp(max=1 << 40).sum().item()) * 2 + (1 << 16)))
+                    while True:
+                        og = torch.empty(cap, dtype=torch.int64, device=dev)
+                        oh = torch.empty(cap, dtype=torch.int64, device=dev)
+                        nat.theta_select_regions(slab.recs1.data_ptr(), self.rw, 1 + 2 * t, self.seg_lo.data_ptr(),
+                                                 pend.data_ptr(), self.nch, G, self.bits, hist.data_ptr(),
+                                                 target.data_ptr(), bound.data_ptr(), og.data_ptr(), oh.data_ptr(),
+                                                 count.data_ptr(), cap, st)
+                        c = int(count.item())
+                        if c <= cap:
+                            break
+                        cap = c  # a duplicate-heavy bin held more candidates than the first guess
+                    pairs = _sorted_unique_pairs(og[:c], oh[:c])
+                    distinct = torch.bincount(pairs[:, 0], minlength=G) if pairs.numel() else \
+                        torch.zeros(G, dtype=torch.int64, device=dev)
+                    short = (distinct < k) & (bound < (1 << 62))
+                    if not bool(short.any()):
+                        break
+                    target = torch.where(short, target * 4, target)
+                out.append(_kmv(pairs, k))
+        finally:
+            PART_POOL.release(slab)
+        return out
+
+
 class PreparedMask:
     """Filter-only scan: writes one u64 mask word per 64 rows (select queries); the mask becomes
     row ids with the ``compact_rows`` kernel (ops/csrc/post_scan.hip).  Mask + descriptor are

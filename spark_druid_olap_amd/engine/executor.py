@@ -46,6 +46,9 @@ AUTO_PIPELINE_MIN_BYTES = int(os.environ.get("SDO_AUTO_PIPELINE_MIN_BYTES", str(
 AUTO_PIPELINE_BATCHES = int(os.environ.get("SDO_AUTO_PIPELINE_BATCHES", "3"))
 # existence-only group-bys over the key's dictionary domain (engine/dict_exist.py)
 DICT_EXIST = os.environ.get("SDO_DICT_EXIST", "1") not in ("0", "")
+# thetaSketch aggregators fused into one producer scan with an in-place radix select
+# (engine/device_exec.py PreparedTheta) instead of emitting (key, row) of every selected row
+THETA_FUSED = os.environ.get("SDO_THETA_FUSED", "1") not in ("0", "")
 # GPU-event phase attribution of PreparedQuery.run (scan / merge / gather / finalize)
 PHASE_EVENTS = os.environ.get("SDO_PHASE_EVENTS", "0") not in ("0", "")
 
@@ -942,6 +945,12 @@ class PreparedQuery:
 
         ds = self.ds
         dev = ds.device
+        gid_order = np.asarray(cols["__gid__"], dtype=np.int64)
+        fused = self._theta_fused(prog)
+        if fused is not None:
+            for (name, _, size), pairs in zip(prog.thetas, fused):
+                cols[name] = _kmv_estimates(self._theta_union(pairs, size), size, gid_order)
+            return
         keys = rows = None
         if not prog.empty and dev.type == "cuda" and self.engine.use_native:
             # the JIT scan emits (key, row) of the selected rows (engine/device_exec.py PreparedEmit)
@@ -959,7 +968,6 @@ class PreparedQuery:
             if rows.numel():
                 rows = rows[eval_bexpr(prog, prog.bexpr, rows)]
             keys = compute_keys(prog, rows)
-        gid_order = np.asarray(cols["__gid__"], dtype=np.int64)
         for name, col, size in prog.thetas:
             from .lower import column_tensor
 
@@ -975,20 +983,42 @@ class PreparedQuery:
                 g, h = keys, theta_hash(column_tensor(ds, col)[rows])
             G = int(prog.G) if 0 < prog.G < (1 << 62) else 0
             pairs = kmv_select(g, h, size, G)
-            if self.world.distributed:
-                # every rank's k candidates per group travel to the root only when the answer is
-                # needed there (results_on_root), else to every rank; the receivers re-select
-                root_only = root_only_results()
-                if root_only:
-                    got, _ = self.world.gather_varlen(pairs, root=0)
-                else:
-                    got = self.world.all_gather_varlen(pairs)
-                if got:
-                    allp = torch.cat(got)
-                    pairs = _kmv(_sorted_unique_pairs(allp[:, 0], allp[:, 1]), size)
-                else:
-                    pairs = pairs[:0]
-            cols[name] = _kmv_estimates(pairs, size, gid_order)
+            cols[name] = _kmv_estimates(self._theta_union(pairs, size), size, gid_order)
+
+    def _theta_fused(self, prog: ScanProgram) -> Optional[List[torch.Tensor]]:
+        """Per theta aggregator its KMV pairs from the fused producer (engine/device_exec.py
+        PreparedTheta), or None where it does not apply (CPU, stored sketches, float columns, wide
+        key spaces, an empty shard): the (key, row) emit path then runs.  The choice is per shard
+        but issues no collective, so ranks may differ."""
+        if prog.empty or self.ds.device.type != "cuda" or not self.engine.use_native or not THETA_FUSED:
+            return None
+        th = self.__dict__.get("_theta_prep")
+        if th is None:
+            try:
+                from .device_exec import PreparedTheta
+
+                th = PreparedTheta(prog, [c for _, c, _ in prog.thetas], THETA_SELECT_MAX_G)
+            except RuntimeError:
+                th = False
+            self._theta_prep = th
+        if th is False:
+            return None
+        return th.select([size for _, _, size in prog.thetas])
+
+    def _theta_union(self, pairs: torch.Tensor, size: int) -> torch.Tensor:
+        """Across ranks: every rank's k candidates per group travel to the root only when the answer
+        is needed there (results_on_root), else to every rank; the receivers re-select."""
+        if not self.world.distributed:
+            return pairs
+        root_only = root_only_results()
+        if root_only:
+            got, _ = self.world.gather_varlen(pairs, root=0)
+        else:
+            got = self.world.all_gather_varlen(pairs)
+        if got:
+            allp = torch.cat(got)
+            return _kmv(_sorted_unique_pairs(allp[:, 0], allp[:, 1]), size)
+        return pairs[:0]
 
     # ------------------------------------------------------------------ post processing
     def _post(self, prog: ScanProgram, cols: Dict[str, np.ndarray]) -> QueryResult:

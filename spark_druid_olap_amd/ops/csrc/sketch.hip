@@ -159,4 +159,81 @@ __global__ void __launch_bounds__(256) theta_filter_kernel(const int64_t* __rest
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Fused theta: the JIT producer (ops/jit.py A_THETA) writes (u32 group key, 62-bit KMV hash per
+// theta aggregator) records straight into its chunk regions -- no row ids, no torch gather / hash
+// of the selected rows, no compaction pass.  The radix select then reads the regions in place:
+//
+//  * theta_hist_regions -- per-workgroup LDS histograms [G, 2^B] (B sized by the host so they fit),
+//    merged with one global add per non-empty bin -- the old global same-address atomics per pair
+//    were a quarter of a 7-group theta query;
+//  * theta_thresh       -- as above;
+//  * theta_filter_regions -- the pairs below their group's bound, compacted with one atomic per wave.
+__global__ void __launch_bounds__(256) theta_hist_regions_kernel(const uint32_t* __restrict__ recs, int rw, int hoff,
+                                                                const uint32_t* __restrict__ seg_lo,
+                                                                const uint32_t* __restrict__ seg_hi, int64_t nseg,
+                                                                int G, int bits, uint32_t* __restrict__ hist,
+                                                                int use_lds) {
+  extern __shared__ uint32_t lh[];
+  const int64_t nb = (int64_t)G << bits;
+  const int shift = 62 - bits;
+  if (use_lds) {
+    for (int64_t i = threadIdx.x; i < nb; i += blockDim.x) lh[i] = 0u;
+    __syncthreads();
+  }
+  for (int64_t sgi = blockIdx.x; sgi < nseg; sgi += gridDim.x) {
+    const uint32_t lo = seg_lo[sgi], hi = seg_hi[sgi];
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+      const uint32_t* r = recs + (uint64_t)i * rw;
+      const uint32_t g = r[0];
+      const uint64_t h = (uint64_t)r[hoff] | ((uint64_t)r[hoff + 1] << 32);
+      if (g >= (uint32_t)G) continue;  // (never for a consistent layout; never fault)
+      const int64_t idx = ((int64_t)g << bits) + (int64_t)(h >> shift);
+      if (use_lds) atomicAdd(&lh[idx], 1u);
+      else atomicAdd(&hist[idx], 1u);
+    }
+  }
+  if (use_lds) {
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < nb; i += blockDim.x)
+      if (lh[i]) atomicAdd(&hist[i], lh[i]);
+  }
+}
+
+__global__ void __launch_bounds__(256) theta_filter_regions_kernel(const uint32_t* __restrict__ recs, int rw, int hoff,
+                                                                  const uint32_t* __restrict__ seg_lo,
+                                                                  const uint32_t* __restrict__ seg_hi, int64_t nseg,
+                                                                  int G, const int64_t* __restrict__ bound,
+                                                                  int64_t* __restrict__ out_g, int64_t* __restrict__ out_h,
+                                                                  unsigned long long* __restrict__ count, int64_t cap) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t sgi = blockIdx.x; sgi < nseg; sgi += gridDim.x) {
+    const uint32_t lo = seg_lo[sgi], hi = seg_hi[sgi];
+    for (uint32_t i0 = lo; i0 < hi; i0 += blockDim.x) {  // (block-uniform trip count: the ballot below)
+      const uint32_t i = i0 + threadIdx.x;
+      bool keep = false;
+      uint32_t g = 0;
+      uint64_t h = 0;
+      if (i < hi) {
+        const uint32_t* r = recs + (uint64_t)i * rw;
+        g = r[0];
+        h = (uint64_t)r[hoff] | ((uint64_t)r[hoff + 1] << 32);
+        keep = g < (uint32_t)G && (int64_t)h < bound[g];
+      }
+      const uint64_t m = __ballot(keep);
+      unsigned long long base = 0;
+      if (lane == 0 && m) base = atomicAdd(count, (unsigned long long)__popcll(m));
+      base = __shfl(base, 0, 64);
+      if (keep) {
+        const unsigned long long pos = base + __popcll(m & ((1ull << lane) - 1ull));
+        if ((int64_t)pos < cap) {
+          out_g[pos] = (int64_t)g;
+          out_h[pos] = (int64_t)h;
+        }
+      }
+    }
+  }
+}
+
 }  // namespace sdo

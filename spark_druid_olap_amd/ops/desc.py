@@ -28,7 +28,7 @@ F_TRUE, F_BITMAP, F_ID_RANGE, F_IN_SET, F_INT_RANGE, F_FLT_RANGE, F_AND, F_OR, F
     F_EXPR = range(12)
 K_ID, K_REMAP, K_TIME, K_INT = range(4)
 A_COUNT, A_SUM_I, A_SUM_F, A_MIN_I, A_MAX_I, A_MIN_F, A_MAX_F, A_HLL, A_SUM_X, A_HLL_STORED, A_ROWID, \
-    A_HLL_CODE = range(12)
+    A_HLL_CODE, A_THETA = range(13)  # (A_THETA: a theta producer's 62-bit KMV hash of a column, JIT only)
 HLL_KINDS = (A_HLL, A_HLL_CODE)  # query-time HLL over a column (hashed per row / precomputed code)
 S_SUM_I, S_SUM_F, S_MIN_I, S_MAX_I = range(4)
 E_COL, E_CONST, E_ADD, E_SUB, E_MUL, E_DIV, E_NEG, E_ABS, E_MIN, E_MAX = range(10)

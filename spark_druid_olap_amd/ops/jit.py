@@ -104,6 +104,9 @@ def part_fields(prog, cols=None) -> List[Tuple[int, int]]:
         if kind == D.A_ROWID:
             out.append((a["slot"], 1))  # u32 row id (emit producers, engine/device_exec.py PreparedEmit)
             continue
+        if kind == D.A_THETA:
+            out.append((a["slot"], 2))  # 62-bit KMV hash (theta producers, engine/device_exec.py PreparedTheta)
+            continue
         w = 2
         if kind in (D.A_SUM_I, D.A_MIN_I, D.A_MAX_I) and not a.get("expr") and a.get("col") in cols:
             c = cols[a["col"]]
@@ -675,6 +678,10 @@ class _Gen:
                     val = self.ival(a["col"])
                 elif kind in (D.A_HLL_STORED, D.A_ROWID):
                     val = "((cw0 + wl[u]) * 64 + lane)"  # the row (a stored sketch's CSR run / emitted id)
+                elif kind == D.A_THETA:
+                    # the thetaSketch hash of the row's value: theta_hash (segment/ingest.py) in-kernel
+                    val = (f"(int64_t)(mix64((uint64_t)(int64_t)({self.ival(a['col'])}) ^ 0x5BD1E995ull) & "
+                           "0x3FFFFFFFFFFFFFFFull)")
                 elif kind == D.A_COUNT:
                     val = "1LL"
                 elif kind == D.A_SUM_X:

@@ -285,3 +285,25 @@ def test_compile_source_compiles_each_shape_once_and_in_parallel(tmp_path, monke
     assert sorted(calls) == sorted(f"k_{tag}{c}" for c in "ab")  # each shape compiled exactly once
     assert len({h for k, h in res if k == 0}) == 1 and len({h for k, h in res if k == 1}) == 1
     assert jit.is_loaded(srcs[0]) and jit.is_loaded(srcs[1])
+
+
+def test_jit_theta_producer_compiles(ds_small, tmp_path, monkeypatch):
+    """Fused theta producer (engine/device_exec.py PreparedTheta): records are the u32 group key and
+    one 62-bit KMV hash (two words) per theta column -- theta_hash of the column value in-kernel,
+    the same mix as the torch path (segment/ingest.py theta_hash) -- and the kernel builds for gfx950."""
+    from spark_druid_olap_amd.engine import device_exec as DE
+    from spark_druid_olap_amd.engine.lower import Lowerer
+    from spark_druid_olap_amd.ops import desc as D
+    from spark_druid_olap_amd.ops import jit
+    from spark_druid_olap_amd.query import spec as S
+
+    monkeypatch.setenv("SDO_JIT_CACHE", str(tmp_path))
+    aggs = [S.ThetaSketchAggregationSpec("t", "o_orderkey", 512), S.ThetaSketchAggregationSpec("t2", "c_name", 4096)]
+    prog = Lowerer(ds_small).lower_aggregate(["1992-01-01/1999-01-01"], S.SelectorFilterSpec("l_returnflag", "R"),
+                                             [S.DefaultDimensionSpec("l_shipmode")], None, aggs)
+    ep = DE.theta_producer_prog(prog, ["o_orderkey", "c_name"])
+    assert [w for _, w in jit.part_fields(ep)] == [2, 2] and prog.pcols != ep.pcols
+    w = jit.JitScan(ep, D.M_PART, 4, False, 2048, True, load=False)
+    assert w.src.count("0x5BD1E995ull") == 2 and "* 5u;" in w.src
+    with pytest.raises(RuntimeError):
+        DE.theta_producer_prog(prog, ["no_such_column"])  # (not a dimension / integer metric: the torch path)
