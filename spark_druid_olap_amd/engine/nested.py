@@ -81,8 +81,16 @@ def device_columns(pq) -> Tuple[Dict[str, DeviceColumn], int]:
     dev = part.acc.device
     cols: Dict[str, DeviceColumn] = {}
     ids_of = []
+    G = int(prog.G)
     for kc in prog.keys:
-        ids = torch.remainder(torch.div(g, kc.stride, rounding_mode="floor"), max(1, kc.card))
+        # (150M-group inner levels: each elementwise pass over the keys is ~0.4 ms -- skip the
+        # divide / remainder a key's position in the packed key does not need)
+        if kc.stride == 1 and kc.card >= G:
+            ids = g  # the only (or a G-spanning lowest) key: the packed key is its id
+        elif kc.stride * max(1, kc.card) >= G:
+            ids = torch.div(g, kc.stride, rounding_mode="floor")  # the leading key: no wrap-around
+        else:
+            ids = torch.remainder(torch.div(g, kc.stride, rounding_mode="floor"), max(1, kc.card))
         ids_of.append(ids)
         cols[kc.name] = DeviceColumn(kc.name, ids, kc.decoder if kc.decoder is not None else (lambda x: x),
                                      card=max(1, kc.card))
@@ -271,7 +279,7 @@ class NestedPreparedQuery:
             R = 0
             firsts = torch.zeros(0, dtype=torch.int64, device=dev)
         elif keycols:
-            packed = torch.zeros(n, dtype=torch.int64, device=dev)
+            packed = None
             span = 1
             radix = []  # (lo, card, stride) per key column
             for _, c in reversed(keycols):
@@ -283,7 +291,13 @@ class NestedPreparedQuery:
                     card = hi - lo + 1
                 if span * card >= 2 ** 62:
                     raise LoweringError("nested group key space exceeds 64 bits")
-                packed += (c.t - lo) * span
+                term = c.t if lo == 0 else c.t - lo
+                if span != 1:
+                    term = term * span
+                if packed is None:  # (one key column: its ids are the packed key, no extra passes)
+                    packed = term if term.dtype == torch.int64 else term.to(torch.int64)
+                else:
+                    packed = packed + term
                 radix.append((lo, card, span))
                 span *= card
             radix.reverse()
