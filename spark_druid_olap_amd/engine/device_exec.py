@@ -528,7 +528,7 @@ class PreparedScan:
                              int(prog.hll_p), st)
             return None
         while True:
-            acc, keys, cnt = self._sparse_out(b, "hv_out", False)
+            acc, keys, cnt, _ = self._sparse_out(b, "hv_out", False)
             nat.part_agg(recs.data_ptr(), L["rw"], base.data_ptr(), L["nsub"], int(prog.G), L["shift"],
                          [f[0] for f in L["fields"]], [f[1] for f in L["fields"]], [int(op) for op, _ in prog.slots],
                          [int(init) for _, init in prog.slots], acc.data_ptr(), hv[0], hv[1], keys.data_ptr(),
@@ -545,11 +545,12 @@ class PreparedScan:
         L, nat, st, prog = self.part, native.load(), native._stream(self.dev), self.prog
         hv = self.part_having or ([], 1)
         while True:
-            acc, keys, cnt, ovf = self._sparse_out(b, "hh_out", True)
-            nat.part_hash_agg(recs.data_ptr(), L["rw"], base.data_ptr(), L["nsub"], L["cap_log2"],
-                              [f[0] for f in L["fields"]], [f[1] for f in L["fields"]],
-                              [int(op) for op, _ in prog.slots], [int(init) for _, init in prog.slots], hv[0], hv[1],
-                              keys.data_ptr(), acc.data_ptr(), cnt.data_ptr(), int(acc.shape[0]), ovf.data_ptr(), st)
+            acc, keys, cnt, ovf, hll = self._sparse_out(b, "hh_out", True, L.get("nhll", 0))
+            nat.part_hash_agg_hll(recs.data_ptr(), L["rw"], base.data_ptr(), L["nsub"], L["cap_log2"],
+                                  [f[0] for f in L["fields"]], [f[1] for f in L["fields"]],
+                                  [int(op) for op, _ in prog.slots], [int(init) for _, init in prog.slots], hv[0],
+                                  hv[1], keys.data_ptr(), acc.data_ptr(), cnt.data_ptr(), int(acc.shape[0]),
+                                  ovf.data_ptr(), [h.data_ptr() for h in hll], int(prog.hll_p), st)
             n, overflow = int(cnt.item()), int(ovf.item())
             if overflow:
                 if L["scale"] >= 1 << 12:
@@ -567,28 +568,32 @@ class PreparedScan:
                     with self._slot_lock:
                         self.part = part_hash_layout(prog, L["scale"], groups=1.25 * n)
                         self._slots.clear()
-                return Partials("sparse", acc[:n], keys[:n], [])
+                return Partials("sparse", acc[:n], keys[:n], [h[:n] for h in hll])
             self.part_cap = _next_pow2(n + n // 4)  # more groups than room: grow, aggregate again
 
-    def _sparse_out(self, b: "_Bufs", name: str, ovf: bool) -> tuple:
-        """(acc [part_cap][nslots], keys, count[, overflow]) the partitioned aggregation appends its
-        surviving groups to: carved from the slot's arena on a leased slot (they live as long as the
-        statement's partials), cached on the buffers on slot 0.  (Counts are reset by the launch.)"""
-        cap, ns, dev = self.part_cap, self.prog.nslots, self.dev
+    def _sparse_out(self, b: "_Bufs", name: str, ovf: bool, nhll: int = 0) -> tuple:
+        """(acc [part_cap][nslots], keys, count[, overflow], [hll [part_cap][2^p] x nhll]) the
+        partitioned aggregation appends its surviving groups to: carved from the slot's arena on a
+        leased slot (they live as long as the statement's partials), cached on the buffers on slot 0.
+        (Counts are reset by the launch.)"""
+        cap, ns, dev, m = self.part_cap, self.prog.nslots, self.dev, self.m
         slot = current_slot()
         if slot == 0:
             out = b.part.get(name)
-            if out is None or out[0].shape[0] < cap:
+            if out is None or out[0].shape[0] < cap or len(out[-1]) != nhll:
                 out = b.part[name] = (torch.empty((cap, ns), dtype=torch.int64, device=dev),
                                       torch.empty(cap, dtype=torch.int64, device=dev),
                                       torch.zeros(1, dtype=torch.int64, device=dev)) + \
-                    ((torch.zeros(1, dtype=torch.int32, device=dev),) if ovf else ())
+                    ((torch.zeros(1, dtype=torch.int32, device=dev),) if ovf else ()) + \
+                    ([torch.empty((cap, m), dtype=torch.uint8, device=dev) for _ in range(nhll)],)
             return out
         items = [(cap * ns, torch.int64, (cap, ns)), (cap, torch.int64, None), (1, torch.int64, None)] + \
-            ([(1, torch.int32, None)] if ovf else [])
+            ([(1, torch.int32, None)] if ovf else []) + [(cap * m, torch.uint8, (cap, m))] * nhll
         offs, total = _carve_aligned([n * torch.empty((), dtype=dt).element_size() for n, dt, _ in items])
         _, off, _, buf = slot_arena(dev, slot).carve(total, self)
-        return tuple(SlotArena.view(buf, off + o, n, dt, shape) for (n, dt, shape), o in zip(items, offs))
+        views = [SlotArena.view(buf, off + o, n, dt, shape) for (n, dt, shape), o in zip(items, offs)]
+        k = 4 if ovf else 3
+        return tuple(views[:k]) + (views[k:],)
 
     def set_part_having(self, terms, conj: bool) -> bool:
         """Fuse a groupBy HAVING into the partitioned aggregation (engine/executor.py): only existing
@@ -1441,24 +1446,26 @@ def part_hash_layout(prog, scale: int = 1, groups: Optional[float] = None) -> di
     from ..ops import jit
 
     ns = max(1, prog.nslots)
-    cap_log2 = max(6, min(14, int(math.floor(math.log2(HASH_TABLE_BYTES // (8 * (1 + ns)))))))
+    nh = jit.part_hll_count(prog) if prog.nhll else 0
+    per = 8 * (1 + ns) + nh * (1 << prog.hll_p)  # (a slot's key, slots and HLL byte registers)
+    cap_log2 = max(6, min(14, int(math.floor(math.log2(max(1, HASH_TABLE_BYTES // per))))))
     if groups is None:
         groups = min(float(prog.G), float(getattr(prog, "est_rows", prog.G)) * 1.2)
     groups = max(1.0, groups)
     nsub = max(8, int(math.ceil(groups * scale / (1 << (cap_log2 - 1)))))
     bits = min(20, max(3, int(math.ceil(math.log2(nsub)))))
     fields = jit.part_fields(prog)
-    rw = 3 + sum(w for _, w in fields)
+    rw = 3 + sum(w for _, w in fields) + nh
     if bits <= 10:
         p1 = 1 << bits
         return {"levels": 1, "hashed": True, "shift": 32 - bits, "shift1": 32 - bits, "p1": p1, "p2": 1, "k": 1,
-                "nsub": p1, "fields": fields, "rw": rw, "cap_log2": cap_log2, "scale": scale}
+                "nsub": p1, "fields": fields, "rw": rw, "cap_log2": cap_log2, "scale": scale, "nhll": nh}
     b1 = min(10, (bits + 1) // 2)
     b2 = bits - b1
     p1, p2 = 1 << b1, 1 << b2
     k = max(1, min(64, 4096 // p1))
     return {"levels": 2, "hashed": True, "shift": 32 - bits, "shift1": 32 - b1, "p1": p1, "p2": p2, "k": k,
-            "nsub": p1 * p2, "fields": fields, "rw": rw, "cap_log2": cap_log2, "scale": scale}
+            "nsub": p1 * p2, "fields": fields, "rw": rw, "cap_log2": cap_log2, "scale": scale, "nhll": nh}
 
 
 def _grid(dev: torch.device, total_chunks: int, lds_total: int, jit=None) -> int:

@@ -69,7 +69,7 @@ __global__ void part_split_kernel(const uint32_t* in, int RW, int RS, const uint
                                   int K, int shift2, int P2, uint32_t* counts2, const uint32_t* base2, uint32_t* out,
                                   int phase);
 __global__ void part_hash_agg_kernel(const uint32_t* recs, int RW, const uint32_t* base, int64_t nsub, int cap_log2,
-                                     PartFields f, PartHaving hv, int64_t* out_keys, uint64_t* out_acc,
+                                     PartFields f, PartHll hl, PartHaving hv, int64_t* out_keys, uint64_t* out_acc,
                                      unsigned long long* out_count, int64_t cap, int* overflow);
 __global__ void part_agg_kernel(const uint32_t* recs, int RW, const uint32_t* base, int64_t nsub, int64_t G, int shift,
                                 PartFields f, PartHll hl, uint64_t* gacc, PartHaving hv, int64_t* out_keys,
@@ -823,10 +823,13 @@ static void p2p_merge(std::vector<uint64_t> mbox, int rank, uint64_t epoch, int6
 // one workgroup per sub-bucket with an LDS table of 2^cap_log2 keys; survivors (every group, or
 // those passing `having`) appended to out_keys / out_acc; *overflow set when a sub-bucket held more
 // distinct keys than its table.
-static void part_hash_agg(uint64_t recs, int RW, uint64_t base, int64_t nsub, int cap_log2, std::vector<int> slot,
-                          std::vector<int> width, std::vector<int> ops, std::vector<int64_t> init,
-                          std::vector<std::tuple<int, int, int, double, double>> having, int conj, uint64_t out_keys,
-                          uint64_t out_acc, uint64_t out_count, int64_t cap, uint64_t overflow, uint64_t stream) {
+// hll: the [cap][2^hll_p] byte register output tables of the HLL aggregators the records carry (one
+// word each after the value fields), empty for none.
+static void part_hash_agg_hll(uint64_t recs, int RW, uint64_t base, int64_t nsub, int cap_log2, std::vector<int> slot,
+                              std::vector<int> width, std::vector<int> ops, std::vector<int64_t> init,
+                              std::vector<std::tuple<int, int, int, double, double>> having, int conj, uint64_t out_keys,
+                              uint64_t out_acc, uint64_t out_count, int64_t cap, uint64_t overflow,
+                              std::vector<uint64_t> hll, int hll_p, uint64_t stream) {
   if (nsub <= 0) return;
   sdo::PartFields f{};
   if (slot.size() != width.size() || slot.size() > (size_t)sdo::MAX_SLOTS) throw std::invalid_argument("part_hash_agg: fields");
@@ -842,13 +845,23 @@ static void part_hash_agg(uint64_t recs, int RW, uint64_t base, int64_t nsub, in
     f.width[j] = width[j];
     words += width[j];
   }
+  sdo::PartHll hl{};
+  if (hll.size() > (size_t)sdo::PART_MAX_HLL || (!hll.empty() && (hll_p < 4 || hll_p > 16)))
+    throw std::invalid_argument("part_hash_agg: HLL aggregators");
+  hl.n = (int)hll.size();
+  hl.p = hll.empty() ? 0 : hll_p;
+  for (size_t h = 0; h < hll.size(); ++h) {
+    if (!hll[h] || (hll[h] & 15)) throw std::invalid_argument("part_hash_agg: HLL output table");
+    hl.regs[h] = (unsigned char*)hll[h];
+  }
+  words += hl.n;
   if (words != RW) throw std::invalid_argument("part_hash_agg: record width does not match the fields");
   for (size_t s = 0; s < ops.size(); ++s) {
     f.op[s] = ops[s];
     f.init[s] = init[s];
   }
   if (cap_log2 < 6 || cap_log2 > 14) throw std::invalid_argument("part_hash_agg: table of 2^6..2^14 keys");
-  const int64_t lds = ((int64_t)1 << cap_log2) * (1 + f.nslots) * 8;
+  const int64_t lds = ((int64_t)1 << cap_log2) * ((1 + f.nslots) * 8 + (int64_t)hl.n * ((int64_t)1 << hl.p));
   if (lds > 160 * 1024 - 256) throw std::invalid_argument("part_hash_agg: table exceeds 160 KiB of LDS");
   sdo::PartHaving hv{};
   if (having.size() > 4) throw std::invalid_argument("part_hash_agg: at most 4 having terms");
@@ -878,9 +891,17 @@ static void part_hash_agg(uint64_t recs, int RW, uint64_t base, int64_t nsub, in
   uint64_t* oa_ = (uint64_t*)out_acc;
   unsigned long long* oc_ = (unsigned long long*)out_count;
   int* of_ = (int*)overflow;
-  void* args[] = {(void*)&r_, (void*)&RW, (void*)&b_, (void*)&nsub, (void*)&cap_log2, (void*)&f, (void*)&hv,
+  void* args[] = {(void*)&r_, (void*)&RW, (void*)&b_, (void*)&nsub, (void*)&cap_log2, (void*)&f, (void*)&hl, (void*)&hv,
                   (void*)&ok_, (void*)&oa_, (void*)&oc_, (void*)&cap, (void*)&of_};
   check(hipLaunchKernel(fn, dim3((unsigned)grid), dim3(512), args, (size_t)lds, s), "part_hash_agg_kernel launch");
+}
+
+static void part_hash_agg(uint64_t recs, int RW, uint64_t base, int64_t nsub, int cap_log2, std::vector<int> slot,
+                          std::vector<int> width, std::vector<int> ops, std::vector<int64_t> init,
+                          std::vector<std::tuple<int, int, int, double, double>> having, int conj, uint64_t out_keys,
+                          uint64_t out_acc, uint64_t out_count, int64_t cap, uint64_t overflow, uint64_t stream) {
+  part_hash_agg_hll(recs, RW, base, nsub, cap_log2, slot, width, ops, init, having, conj, out_keys, out_acc, out_count,
+                    cap, overflow, {}, 0, stream);
 }
 
 static int desc_size() { return (int)sizeof(sdo::ScanDesc); }
@@ -962,6 +983,7 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("part_keys", &part_keys);
   m.def("part_split", &part_split);
   m.def("part_tune", &part_tune);
+  m.def("part_hash_agg_hll", &part_hash_agg_hll);
   m.def("theta_select_regions", &theta_select_regions);
   m.def("part_agg", &part_agg);
   m.def("part_agg_hll", &part_agg_hll);

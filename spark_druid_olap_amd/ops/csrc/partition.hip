@@ -651,9 +651,12 @@ __device__ __forceinline__ uint32_t part_hash_probe(uint32_t h, int cap_log2) {
   return (h * 0x9E3779B1u) >> (32 - cap_log2);
 }
 
+// HLL aggregators (hl.n > 0): each record ends with one (bucket << 8 | rho) word per HLL; every
+// table slot keeps 2^p byte registers per HLL in LDS after the slot table, and a surviving group's
+// registers are written to row `pos` of the [cap][2^p] output tables (hl.regs).
 __global__ __launch_bounds__(512) void part_hash_agg_kernel(const uint32_t* __restrict__ recs, int RW,
                                                            const uint32_t* __restrict__ base, int64_t nsub,
-                                                           int cap_log2, PartFields f,
+                                                           int cap_log2, PartFields f, PartHll hl,
                                                            PartHaving hv, int64_t* __restrict__ out_keys,
                                                            uint64_t* __restrict__ out_acc,
                                                            unsigned long long* __restrict__ out_count, int64_t cap,
@@ -667,8 +670,11 @@ __global__ __launch_bounds__(512) void part_hash_agg_kernel(const uint32_t* __re
   const int NS = f.nslots;
   uint64_t* tk = t;           // [C] keys
   uint64_t* tv = t + C;       // [C][NS] slots
+  const int64_t m = (int64_t)1 << hl.p;
+  unsigned char* hr = (unsigned char*)(tv + (int64_t)C * NS);  // [n][C][2^p] byte registers
   for (int i = threadIdx.x; i < C; i += blockDim.x) tk[i] = HASH_EMPTY;
   for (int i = threadIdx.x; i < C * NS; i += blockDim.x) tv[i] = (uint64_t)f.init[i % NS];
+  for (int64_t i = threadIdx.x; i < (hl.n * C * m) / 4; i += blockDim.x) ((uint32_t*)hr)[i] = 0u;
   __syncthreads();
   const uint32_t lo = base[r], hi = base[r + 1];
   bool full = false;
@@ -702,6 +708,11 @@ __global__ __launch_bounds__(512) void part_hash_agg_kernel(const uint32_t* __re
       const int s = f.slot[j];
       lds_fold(row + s, f.op[s], v);
     }
+    for (int h = 0; h < hl.n; ++h) {
+      const uint32_t code = rec[w + h];
+      if (code & 0xffu) lds_max_u8(hr + ((int64_t)h * C + slot) * m, (int64_t)((code >> 8) & (uint32_t)(m - 1)),
+                                   code & 0xffu);
+    }
   }
   if (full) atomicOr(overflow, 1);
   __syncthreads();
@@ -725,6 +736,11 @@ __global__ __launch_bounds__(512) void part_hash_agg_kernel(const uint32_t* __re
     if (pos < cap) {
       out_keys[pos] = (int64_t)tk[i];
       for (int s = 0; s < NS; ++s) out_acc[pos * NS + s] = row[s];
+      for (int h = 0; h < hl.n; ++h) {  // (the group's registers: m / 16 16-byte copies)
+        const uint4* src = (const uint4*)(hr + ((int64_t)h * C + i) * m);
+        uint4* dst = (uint4*)(hl.regs[h] + pos * m);
+        for (int64_t q = 0; q < m / 16; ++q) dst[q] = src[q];
+      }
     }
     ++pos;
   }

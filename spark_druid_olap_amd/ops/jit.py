@@ -151,8 +151,13 @@ def part_eligible(prog) -> bool:
         return False
     if prog.nhll:
         nh = part_hll_count(prog)
-        return PART_HLL and nh == prog.nhll and nh <= 4 and not part_hashed(prog) and \
-            prog.G * nh * (1 << prog.hll_p) <= PART_HLL_MAX_BYTES
+        if not (PART_HLL and nh == prog.nhll and nh <= 4):
+            return False
+        if part_hashed(prog):
+            # sparse groups, registers per LDS hash-table slot: the smallest table (64 slots) must
+            # hold every sketch's 2^p registers next to the slots (p = 11: one HLL per query)
+            return 64 * ((1 + n) * 8 + nh * (1 << prog.hll_p)) <= 160 * 1024 - 256
+        return prog.G * nh * (1 << prog.hll_p) <= PART_HLL_MAX_BYTES
     return True
 
 
