@@ -144,6 +144,41 @@ def engine(world, dev, sf, out):
                 phases.setdefault(name, {})[mode] = {"ms": statistics.median(ts),
                                                     **{k: round(statistics.median(v), 4) for k, v in ph.items()}}
     p2p.ENABLED = True
+    # the default path's automatic pipelining (engine/executor.py AUTO_PIPELINE): a groupBy keyed
+    # by day x ship mode holds a 280 KB dense state, so every rank splits its scan into batches and
+    # merges each batch's day slice while the next batch scans; timed against the same query with
+    # the pipelining off (one scan, then one merge of the whole table)
+    if world.size > 1:
+        from spark_druid_olap_amd.engine import executor as X
+        from spark_druid_olap_amd.query import spec as S
+
+        spec = S.GroupByQuerySpec("tpch", [S.DefaultDimensionSpec("l_shipmode")], granularity=S.Granularity.parse("day"),
+                                  intervals=["1992-01-01/1999-01-01"],
+                                  aggregations=[S.FunctionAggregationSpec("doubleSum", "s", "l_extendedprice"),
+                                                S.FunctionAggregationSpec("count", "n")])
+        pipe = {}
+        for auto in (True, False):
+            X.AUTO_PIPELINE = auto
+            pq = sess.engine.prepare(spec.copy(), ds)
+            with results_on_root():
+                for _ in range(2):
+                    pq.run()
+                ts, ph = [], {}
+                for _ in range(10):
+                    world.barrier()
+                    torch.cuda.synchronize()
+                    t = time.perf_counter()
+                    r = pq.run()
+                    torch.cuda.synchronize()
+                    ts.append((time.perf_counter() - t) * 1e3)
+                    for k, v in (r.stats or {}).items():
+                        if k.endswith("_ms"):
+                            ph.setdefault(k, []).append(v)
+            pipe["auto" if auto else "one_merge"] = {
+                "ms": statistics.median(ts), "batches": pq._nbatches, "pipelined": bool(pq._pipeline_ok),
+                "rows": r.num_rows, **{k: round(statistics.median(v), 4) for k, v in ph.items()}}
+        X.AUTO_PIPELINE = True
+        out["auto_pipeline"] = pipe
     out["p2p_stats"] = p2p.stats(world)
     out["retried_statements"] = retries
     if world.rank == 0:

@@ -37,6 +37,9 @@ def main():
             print(f"  {q[:45]:45s} " + "  ".join(
                 f"{m}: {v['ms']:.3f} ms (" + " ".join(f"{k[:-3]}={x:.3f}" for k, x in v.items() if k != "ms") + ")"
                 for m, v in modes.items()), flush=True)
+        for m, v in (r.get("auto_pipeline") or {}).items():
+            print(f"  auto-pipelined day x shipmode ({m}): " + " ".join(
+                f"{k}={x:.3f}" if isinstance(x, float) else f"{k}={x}" for k, x in v.items()), flush=True)
     return rc
 
 
