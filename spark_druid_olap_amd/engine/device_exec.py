@@ -1398,6 +1398,7 @@ class PreparedMask:
 
 
 PART_TABLE_BYTES = int(os.environ.get("SDO_PART_TABLE_BYTES", 32 << 10))  # LDS table per sub-bucket
+PART_MIN_SUBS = 512  # sub-buckets (aggregation workgroups) a partitioned group-by aims for at least
 HASH_TABLE_BYTES = 128 << 10  # LDS hash table of a hash-partitioned sub-bucket (keys + slots)
 PART_HLL_TABLE_BYTES = 128 << 10  # LDS slots + HLL byte registers of a partitioned sub-bucket
 HLL32_MAX_BYTES = int(os.environ.get("SDO_HLL32_MAX_BYTES", str(512 << 20)))  # u32 scan-time registers
@@ -1419,6 +1420,10 @@ def part_layout(prog) -> dict:
         shift = max(0, int(math.floor(math.log2(max(1, PART_HLL_TABLE_BYTES // per)))))
     else:
         shift = max(0, int(math.floor(math.log2(max(8, PART_TABLE_BYTES // (8 * ns))))))
+    # enough sub-buckets to fill the chip: one aggregation workgroup per sub-bucket, so a key space
+    # of a few thousand groups in 64 KiB tables (day x ship mode, 17.7K groups: 9 sub-buckets, 9
+    # busy CUs, 11.6 ms at SF10) is cut into smaller tables instead
+    shift = max(0, min(shift, int(math.floor(math.log2(max(1, prog.G // PART_MIN_SUBS))))))
     gbits = max(1, int(math.ceil(math.log2(max(2, prog.G)))))
     rem = max(0, gbits - shift)
     fields = jit.part_fields(prog)

@@ -264,7 +264,9 @@ class PreparedQuery:
         if nbytes < AUTO_PIPELINE_MIN_BYTES:
             return None
         probe = self._prepare(prog)
-        dense = probe is None or getattr(probe, "mode", None) in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL)
+        # (a partitioned scan writes the dense table too: no HAVING is fused into a batched scan)
+        dense = probe is None or (getattr(probe, "mode", None) in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL, D.M_PART)
+                                  and not (getattr(probe, "part", None) or {}).get("hashed"))
         if -self.world.max_float(-float(dense)) < 1.0:  # (min over ranks)
             return None
         nseg = sum(1 for sg in ds.segments if any(min(hi, sg.row_hi) > max(lo, sg.row_lo) for lo, hi in prog.ranges))
