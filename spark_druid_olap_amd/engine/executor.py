@@ -42,7 +42,8 @@ PIPELINE_MERGE = os.environ.get("SDO_PIPELINE_MERGE", "1") not in ("0", "")
 # Small states are never split: their merge is latency-bound, every batch would pay it again and
 # the last one stays exposed anyway.
 AUTO_PIPELINE = os.environ.get("SDO_AUTO_PIPELINE", "1") not in ("0", "")
-AUTO_PIPELINE_MIN_BYTES = int(os.environ.get("SDO_AUTO_PIPELINE_MIN_BYTES", str(256 << 10)))
+# (a merge this size takes ~0.1 ms over RCCL on 8 GPUs: less would not pay for the extra batches)
+AUTO_PIPELINE_MIN_BYTES = int(os.environ.get("SDO_AUTO_PIPELINE_MIN_BYTES", str(4 << 20)))
 AUTO_PIPELINE_BATCHES = int(os.environ.get("SDO_AUTO_PIPELINE_BATCHES", "3"))
 # existence-only group-bys over the key's dictionary domain (engine/dict_exist.py)
 DICT_EXIST = os.environ.get("SDO_DICT_EXIST", "1") not in ("0", "")
@@ -264,9 +265,10 @@ class PreparedQuery:
         if nbytes < AUTO_PIPELINE_MIN_BYTES:
             return None
         probe = self._prepare(prog)
-        # (a partitioned scan writes the dense table too: no HAVING is fused into a batched scan)
-        dense = probe is None or (getattr(probe, "mode", None) in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL, D.M_PART)
-                                  and not (getattr(probe, "part", None) or {}).get("hashed"))
+        # dense table scans only: a batch of a partitioned scan repeats its whole split pipeline (a
+        # 2-rank rehearsal of day x ship mode at SF10: 3 partitioned batches 4.3 ms against one scan
+        # + one merge 2.8 ms, profiles/r5/rehearsal_auto_pipeline_sf10.txt)
+        dense = probe is None or getattr(probe, "mode", None) in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL)
         if -self.world.max_float(-float(dense)) < 1.0:  # (min over ranks)
             return None
         nseg = sum(1 for sg in ds.segments if any(min(hi, sg.row_hi) > max(lo, sg.row_lo) for lo, hi in prog.ranges))
