@@ -202,6 +202,30 @@ __global__ __launch_bounds__(512) void part_keys_kernel(const int64_t* __restric
 // coalesced store sequence instead of 64 scattered lines per wave instruction.  PU shrinks as
 // records widen (the tile stays ~32 KB of LDS).
 
+// Record addressing of a split pass: records [lo, lo + n) of one segment (Contig), or the
+// concatenation of up to 512 small segments whose start offsets and exclusive length prefix sit in
+// LDS (Packed: a selective producer leaves a few dozen records in each 4096-row chunk region, and a
+// tile per region paid the tile's barriers for almost nothing -- TPC-H Q2's 8M-row inner level over
+// 146K regions).  v -> record index.
+struct Contig {
+  uint32_t lo;
+  __device__ __forceinline__ uint64_t operator()(uint32_t v) const { return (uint64_t)lo + v; }
+};
+struct Packed {
+  const uint32_t* slo;   // [ns] region starts (LDS)
+  const uint32_t* spre;  // [ns + 1] exclusive prefix of the region lengths (LDS)
+  int ns;
+  __device__ __forceinline__ uint64_t operator()(uint32_t v) const {
+    int a = 0, b = ns - 1;  // the last region whose prefix <= v
+    while (a < b) {
+      const int mid = (a + b + 1) >> 1;
+      if (spre[mid] <= v) a = mid;
+      else b = mid - 1;
+    }
+    return (uint64_t)slo[a] + (v - spre[a]);
+  }
+};
+
 template <bool CL>
 __device__ __forceinline__ void split_range_count(const uint32_t* __restrict__ in, int RW, uint32_t lo, uint32_t hi,
                                                   int shift2, uint32_t mask, uint32_t* h) {
@@ -248,15 +272,33 @@ __device__ __forceinline__ void split_range_count(const uint32_t* __restrict__ i
   }
 }
 
-template <int PU, bool CL>
-__device__ __forceinline__ void split_range_scatter(const uint32_t* __restrict__ in, int RW, int RS, uint32_t lo, uint32_t hi,
+template <bool CL, class Map>
+__device__ __forceinline__ void split_map_count(const uint32_t* __restrict__ in, int RW, Map map, uint32_t n, int shift2,
+                                                uint32_t mask, uint32_t* h) {
+  for (uint32_t b0 = 0; b0 < n; b0 += blockDim.x * 4) {  // (block-uniform trip count)
+    uint32_t key[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t v = b0 + threadIdx.x + u * blockDim.x;
+      key[u] = v < n ? in[map(v) * RW] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool act = b0 + threadIdx.x + u * blockDim.x < n;
+      lds_count_add(h, (key[u] >> shift2) & mask, act, CL);
+    }
+  }
+}
+
+template <int PU, bool CL, class Map>
+__device__ __forceinline__ void split_range_scatter(const uint32_t* __restrict__ in, int RW, int RS, Map map, uint32_t n,
                                                     int shift2, uint32_t P2, uint32_t* cur, uint32_t* hist,
                                                     uint32_t* tstart, uint32_t* tile, uint32_t* scan_lds,
                                                     uint32_t* __restrict__ out) {
   const uint32_t mask = P2 - 1u;
   constexpr uint32_t TILE = 512u * PU;
-  for (uint32_t t0 = lo; t0 < hi; t0 += TILE) {
-    const uint32_t tn = hi - t0 < TILE ? hi - t0 : TILE;
+  for (uint32_t t0 = 0; t0 < n; t0 += TILE) {
+    const uint32_t tn = n - t0 < TILE ? n - t0 : TILE;
     for (uint32_t q = threadIdx.x; q < P2; q += blockDim.x) hist[q] = 0u;
     __syncthreads();
     uint32_t q_[PU], r_[PU];
@@ -265,7 +307,7 @@ __device__ __forceinline__ void split_range_scatter(const uint32_t* __restrict__
     for (int u = 0; u < PU; ++u) {
       const uint32_t j = threadIdx.x + u * blockDim.x;
       if (j < tn) {
-        const uint64_t i = (uint64_t)t0 + j;
+        const uint64_t i = map(t0 + j);
         if (RW == 2) {
           v2[u] = *(const uint2*)(in + i * 2);
         } else {
@@ -338,7 +380,7 @@ __device__ __forceinline__ void split_range_scatter(const uint32_t* __restrict__
         if (RW == 2) {
           ((uint2*)tile)[d] = v2[u];
         } else {
-          const uint32_t* rec = in + ((uint64_t)t0 + j) * RW;
+          const uint32_t* rec = in + map(t0 + j) * RW;
           for (int w = 0; w < RW; ++w) tile[(uint64_t)d * RS + w] = rec[w];
         }
       }
@@ -393,14 +435,44 @@ __global__ __launch_bounds__(512) void part_split_kernel(const uint32_t* __restr
     const uint64_t n = hi > lo ? hi - lo : 0;
     const uint32_t a = lo + (uint32_t)(n * k / K), e = lo + (uint32_t)(n * (k + 1) / K);
     if (phase == 0) split_range_count<CL>(in, RW, a, e, shift2, mask, h);
-    else split_range_scatter<PU, CL>(in, RW, RS, a, e, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds, out);
+    else split_range_scatter<PU, CL>(in, RW, RS, Contig{a}, e - a, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds,
+                                     out);
   } else {
+    // the block's regions in groups of up to 512: lengths prefix-summed in LDS; groups of small
+    // regions (< 1024 records on average) run as packed tiles, large ones region by region
+    __shared__ uint32_t slo[512];
+    __shared__ uint32_t spre[513];
     const int64_t s0 = g * spg + (int64_t)spg * k / K, s1 = g * spg + (int64_t)spg * (k + 1) / K;
-    for (int64_t sgi = s0; sgi < s1; ++sgi) {
-      const uint32_t lo = seg_lo[sgi], hi = seg_hi[sgi];
-      if (hi <= lo) continue;  // (uniform across the block: every thread reads the same segment)
-      if (phase == 0) split_range_count<CL>(in, RW, lo, hi, shift2, mask, h);
-      else split_range_scatter<PU, CL>(in, RW, RS, lo, hi, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds, out);
+    for (int64_t sb = s0; sb < s1; sb += 512) {
+      const int ns = (int)(s1 - sb < 512 ? s1 - sb : 512);
+      uint32_t len = 0, lo0 = 0;
+      if ((int)threadIdx.x < ns) {
+        lo0 = seg_lo[sb + threadIdx.x];
+        const uint32_t hi0 = seg_hi[sb + threadIdx.x];
+        len = hi0 > lo0 ? hi0 - lo0 : 0u;
+      }
+      uint32_t tot;
+      const uint32_t pre = block_excl_scan_u32<512>(len, scan_lds, &tot);
+      if ((int)threadIdx.x < ns) {
+        slo[threadIdx.x] = lo0;
+        spre[threadIdx.x] = pre;
+      }
+      if (threadIdx.x == 0) spre[ns] = tot;
+      __syncthreads();
+      if (tot < 1024u * (uint32_t)ns) {
+        const Packed pm{slo, spre, ns};
+        if (phase == 0) split_map_count<CL>(in, RW, pm, tot, shift2, mask, h);
+        else split_range_scatter<PU, CL>(in, RW, RS, pm, tot, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds, out);
+      } else {
+        for (int si = 0; si < ns; ++si) {
+          const uint32_t lo = slo[si], n = spre[si + 1] - spre[si];
+          if (n == 0) continue;  // (uniform across the block: every thread reads the same LDS entry)
+          if (phase == 0) split_range_count<CL>(in, RW, lo, lo + n, shift2, mask, h);
+          else split_range_scatter<PU, CL>(in, RW, RS, Contig{lo}, n, shift2, (uint32_t)P2, h, hist, tstart, tile,
+                                           scan_lds, out);
+        }
+      }
+      __syncthreads();  // (slo / spre are rewritten for the next group)
     }
   }
   if (phase == 0) {
