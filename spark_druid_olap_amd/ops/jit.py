@@ -60,6 +60,7 @@ class JitLayout:
     ncopy: int
     regstage: bool = False
     shared: bool = False  # one accumulator copy per workgroup (LDS atomics shared by its 8 waves)
+    G: int = 0  # groups the LDS table is sized for (a size class >= the program's G)
 
 
 def col_infos(prog) -> Dict[int, ColInfo]:
@@ -191,14 +192,38 @@ def count_regs(prog, mode: int) -> bool:
 
 
 
+# Dense LDS tables are sized for a power-of-two class of the group count, not the exact count: a
+# dashboard's parameterizations differ mostly in how many values a key takes (a date range spans
+# 3, 4 or 5 years -> 12, 16 or 20 groups), and with the count out of the code they share one
+# kernel instead of compiling one per binding (~300 ms each, the BI plan's cold-start tail).  The
+# exact count stays in the descriptor (d->G bounds the flush), and the class is used only when it
+# keeps the same number of per-wave copies within the same LDS budget.
+G_CLASS = os.environ.get("SDO_JIT_G_CLASS", "1") != "0"
+
+
 def layout(prog, mode: int, U: int, hll_lds: bool, m: int, budget: int = 150 * 1024,
            regstage: bool = False, shared: bool = False) -> JitLayout:
+    exact = _layout(prog, mode, U, hll_lds, m, budget, regstage, shared, int(prog.G))
+    G = int(prog.G)
+    if not G_CLASS or mode != D.M_DENSE_LDS or G <= 0 or count_regs(prog, mode):
+        return exact
+    gc = 1 << (G - 1).bit_length()
+    if gc == G:
+        return exact
+    lay = _layout(prog, mode, U, hll_lds, m, budget, regstage, shared, gc)
+    if lay.ncopy != exact.ncopy or (lay.total > budget and exact.total <= budget) or lay.total > 160 * 1024:
+        return exact
+    return lay
+
+
+def _layout(prog, mode: int, U: int, hll_lds: bool, m: int, budget: int, regstage: bool, shared: bool,
+            G: int) -> JitLayout:
     cols = col_infos(prog)
     nplanes = 0 if regstage else sum(2 if c.lg == 3 else 1 for c in cols.values() if not c.pw)
     need_bmw = _needs_word_bitmaps(prog)
     wave_bytes = U * nplanes * 256 + (len(prog.bm_leaves) * 512 if need_bmw else 0)
     wave_bytes = (wave_bytes + 15) // 16 * 16
-    hll_bytes = prog.nhll * prog.G * m if hll_lds else 0  # byte registers (hll_update8)
+    hll_bytes = prog.nhll * G * m if hll_lds else 0  # byte registers (hll_update8)
     stage = W * wave_bytes
     ncopy = 1
     acc_bytes = 0
@@ -206,9 +231,9 @@ def layout(prog, mode: int, U: int, hll_lds: bool, m: int, budget: int = 150 * 1
         # key spaces too large for per-wave copies (thousands of groups, e.g. SSB brand x year):
         # ONE table per workgroup; lanes hitting the same group serialize in the LDS atomic unit,
         # which is still far cheaper than contending HBM atomics on a few hundred hot addresses
-        acc_bytes = prog.G * prog.nslots * 8
+        acc_bytes = G * prog.nslots * 8
     elif mode == D.M_DENSE_LDS:
-        base = prog.G * prog.nslots * 8 * W
+        base = G * prog.nslots * 8 * W
         ncopy = MAX_NCOPY
         while ncopy > 1 and base * ncopy + hll_bytes + stage > budget:
             ncopy //= 2
@@ -218,7 +243,7 @@ def layout(prog, mode: int, U: int, hll_lds: bool, m: int, budget: int = 150 * 1
     cache_off = (hll_off + hll_bytes + 15) // 16 * 16
     total = cache_off + stage
     return JitLayout(acc_off, acc_bytes, hll_off, hll_bytes, cache_off, wave_bytes, total, ncopy, regstage,
-                     shared and mode == D.M_DENSE_LDS)
+                     shared and mode == D.M_DENSE_LDS, G)
 
 
 def prefer_regstage(prog) -> bool:
@@ -595,6 +620,7 @@ class _Gen:
         word_filter = None if p.final_pre else self.word_expr(0, p.filter_len)
         pre = self.chunk_expr() if p.pre_len else None
         G, NS = p.G, p.nslots
+        GL = lay.G or G  # (the LDS table's size class; exact G only for the unrolled count registers)
         NCT = 1 if lay.shared else W * lay.ncopy
         creg = count_regs(p, mode)
         cslots = sorted({a["slot"] for a in p.aops}) if creg else []
@@ -615,7 +641,7 @@ class _Gen:
         for ai, a in enumerate(p.aops):
             if a["kind"] in D.HLL_KINDS:
                 if self.hll_lds and mode == D.M_DENSE_LDS:
-                    L.append(f"  unsigned char* hll{ai} = lds + {lay.hll_off + a['hll'] * G * self.m};")
+                    L.append(f"  unsigned char* hll{ai} = lds + {lay.hll_off + a['hll'] * GL * self.m};")
                 else:
                     L.append(f"  unsigned char* hll{ai} = (unsigned char*)d->aops[{ai}].hll_regs;")
             elif a["kind"] == D.A_HLL_STORED:
@@ -797,7 +823,7 @@ class _Gen:
             out.append("  uint32_t* pend = (uint32_t*)d->part_counts;  // end offset of each chunk's records")
             out.append("  const uint64_t lmlt = (1ull << lane) - 1ull;")
         if mode == D.M_DENSE_LDS:
-            out.append(f"  for (int i = threadIdx.x; i < {G * NS * NCT}; i += {W * 64}) {{")
+            out.append(f"  for (int i = threadIdx.x; i < {GL * NS * NCT}; i += {W * 64}) {{")
             inits = ", ".join(_lit(init) for _, init in p.slots)
             out.append(f"    constexpr int64_t init[{NS}] = {{{inits}}};")
             out.append(f"    acc[i] = (uint64_t)init[(i / {NCT}) % {NS}];")
@@ -917,7 +943,8 @@ class _Gen:
                            "(int64_t)v_); }")
         if mode == D.M_DENSE_LDS:
             out.append("  __syncthreads();")
-            out.append(f"  for (int i = threadIdx.x; i < {G * NS}; i += {W * 64}) {{")
+            out.append(f"  const int flush_n = (int)d->G * {NS};")
+            out.append(f"  for (int i = threadIdx.x; i < flush_n; i += {W * 64}) {{")
             out.append(f"    const int s = i % {NS};")
             ops = ", ".join(str(op) for op, _ in p.slots)
             inits = ", ".join(_lit(init) for _, init in p.slots)
@@ -943,7 +970,7 @@ class _Gen:
                     # four byte registers per dword: one read (and rarely a CAS) per 4 registers
                     out.append(f"  {{ uint32_t* g = (uint32_t*)d->aops[{ai}].hll_regs;")
                     out.append(f"    const uint32_t* r = (const uint32_t*)hll{ai};")
-                    out.append(f"    for (int i = threadIdx.x; i < {G * self.m // 4}; i += {W * 64}) "
+                    out.append(f"    for (int i = threadIdx.x; i < (int)d->G * {self.m // 4}; i += {W * 64}) "
                                "hll_merge_word8(g + i, r[i]);")
                     out.append("  }")
         out.append("}")

@@ -52,8 +52,41 @@ def test_jit_shared_table_kernel_compiles(tmp_path, monkeypatch):
         assert prog.G * prog.nslots * 8 * 8 > 64 * 1024  # per-wave copies would not fit
         js = jit.JitScan(prog, D.M_DENSE_LDS, 4, False, 2048, True, load=False, shared=True,
                          budget=159 * 1024)
-        assert js.lay.shared and js.lay.acc_bytes == prog.G * prog.nslots * 8
+        # (the table is sized for the group count's power-of-two class when that fits the budget)
+        assert js.lay.shared and js.lay.G >= prog.G and js.lay.acc_bytes == js.lay.G * prog.nslots * 8
         assert "const int copy = 0;" in js.src and js.lay.total <= 160 * 1024
+
+
+def test_jit_group_size_class_shares_kernels(tmp_path, monkeypatch, ds_small):
+    """Dense LDS scans whose group counts fall in one power-of-two class compile to one kernel
+    (the flush is bounded by the descriptor's exact count), and the class never costs per-wave
+    copies."""
+    from spark_druid_olap_amd.engine.executor import Engine
+    from spark_druid_olap_amd.models import tpch
+    from spark_druid_olap_amd.ops import desc as D
+    from spark_druid_olap_amd.ops import jit
+    from spark_druid_olap_amd.session import Session
+
+    monkeypatch.setenv("SDO_JIT_CACHE", str(tmp_path / "jit"))
+    s = Session(engine=Engine(use_native=False))
+    s.register_datasource(ds_small)
+    s.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)
+    s.sql(tpch.druid_ddl(with_column_mapping=False))
+    srcs = {}
+    for years in ((1993, 1996), (1993, 1997)):  # 3 and 4 ship years x 2 return flags
+        q = ("select l_returnflag, year(l_shipdate) y, sum(l_extendedprice) from orderLineItemPartSupplier "
+             f"where l_shipdate >= date '{years[0]}-01-01' and l_shipdate < date '{years[1]}-01-01' "
+             "group by l_returnflag, year(l_shipdate)")
+        spec = s.sql(q).druid_query_specs()[0]
+        prog = s.engine.prepare(spec, ds_small).scans[0][1]
+        if prog.G <= jit.COUNT_REGS_MAX_G:
+            pytest.skip("unrolled count kernel")
+        js = jit.JitScan(prog, D.M_DENSE_LDS, 4, False, 2048, True, load=False)
+        exact = jit._layout(prog, D.M_DENSE_LDS, 4, False, 2048, 150 * 1024, False, False, int(prog.G))
+        assert js.lay.ncopy == exact.ncopy and js.lay.G >= prog.G
+        assert "flush_n = (int)d->G" in js.src
+        srcs[prog.G] = js.src
+    assert len(srcs) == 2 and len(set(srcs.values())) == 1, sorted(srcs)
 
 
 def test_jit_presence_only_kernel_compiles(tmp_path, monkeypatch, ds_small):
