@@ -11,6 +11,7 @@ model's row estimate and grown on overflow.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 import threading
@@ -118,10 +119,92 @@ def _jit_for(prog, mode: int, hll_lds: bool, m: int, shared: bool = False):
     return js
 
 
+# First-seen shapes while serving (server/gateway.py: ``with async_compile():`` around a statement's
+# prepare).  A new kernel shape costs a hipRTC compile of ~0.3 s alone and 1-2 s on a host busy
+# with 64 clients -- the BI plan's cold p99 (profiles/r5/thrift_jmx_s8_sf100_c64_cold_*.json).  In
+# the scope, a scan whose kernel is not compiled yet runs on the interpreter kernel (ops/csrc, same
+# results, a few times slower) while the JIT source compiles on a background thread; the session
+# re-prepares the statement once every compile it started has finished (session.py
+# prepare_druid), and the next execution runs the JIT kernel from the code cache.  Only plans the
+# interpreter runs as-is take the detour: per-wave LDS copies, plain HBM tables, hash tables, masks
+# -- shared LDS tables, first-touch / presence byte tables and the partitioned producers would fall
+# back to other modes (a 150M-group HBM table per slot), so those still compile in the foreground.
+ASYNC_JIT = os.environ.get("SDO_ASYNC_JIT", "1") != "0"
+ASYNC_JIT_WORKERS = 4
+_async_tls = threading.local()
+_async_failed: set = set()
+_async_pool: list = []
+
+
+@contextlib.contextmanager
+def async_compile():
+    """Scope in which prepares start first-seen kernel compiles in the background (see above)."""
+    prev = getattr(_async_tls, "pending", None)
+    _async_tls.pending = [] if ASYNC_JIT and USE_JIT else None
+    try:
+        yield
+    finally:
+        _async_tls.pending = prev
+
+
+def prepare_collecting(fn):
+    """``fn()`` and the background compiles it started (empty outside ``async_compile``)."""
+    pend = getattr(_async_tls, "pending", None)
+    if pend is None:
+        return fn(), []
+    n = len(pend)
+    r = fn()
+    return r, pend[n:]
+
+
+def _async_ok(prog, mode: int, shared: bool) -> bool:
+    return (mode in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL, D.M_HASH, D.M_MASK) and not shared
+            and not getattr(prog, "touch_table", False) and not getattr(prog, "presence_bytes", False))
+
+
+def _async_job(prog, mode: int, hll_lds: bool, m: int, shared: bool, narrow4: bool, key: str):
+    try:
+        _jit_select(prog, mode, hll_lds, m, shared, load=False, narrow4=narrow4)
+    except BaseException:
+        _async_failed.add(key)
+        raise
+
+
 def _jit_build(prog, mode: int, hll_lds: bool, m: int, shared: bool = False, load: bool = True):
     """(``load=False``: compile only -- tools/jit_isa.py inspects the exact kernel a scan would run
     on a host without a GPU.)"""
     from ..ops import jit
+
+    pend = getattr(_async_tls, "pending", None)
+    if load and pend is not None and _async_ok(prog, mode, shared):
+        narrow4 = bool(native.narrow4())
+        try:
+            return _jit_select(prog, mode, hll_lds, m, shared, load=True, narrow4=narrow4, cached_only=True)
+        except jit.NotCached as e:
+            if e.key not in _async_failed:
+                import copy
+
+                if not _async_pool:
+                    from concurrent.futures import ThreadPoolExecutor
+
+                    _async_pool.append(ThreadPoolExecutor(max_workers=ASYNC_JIT_WORKERS,
+                                                          thread_name_prefix="sdo-jit-async"))
+                # (a snapshot: the prepare goes on to mark the program for the interpreter)
+                snap = copy.copy(prog)
+                pend.append(_async_pool[0].submit(_async_job, snap, mode, hll_lds, m, shared, narrow4, e.key))
+                from ..utils.metrics import count_event
+
+                count_event("jit_async_interim")
+                return None
+    return _jit_select(prog, mode, hll_lds, m, shared, load=load)
+
+
+def _jit_select(prog, mode: int, hll_lds: bool, m: int, shared: bool = False, load: bool = True,
+                narrow4: Optional[bool] = None, cached_only: bool = False):
+    from ..ops import jit
+
+    if narrow4 is None:
+        narrow4 = bool(native.narrow4()) if load else True
 
     nplanes = sum(2 if column_tensor_size(prog, c) == 8 else 1 for c in prog.cols)
     prefs = [16, 8, 4, 2] if nplanes <= 3 else ([8, 4, 2] if nplanes <= 8 else [4, 2])
@@ -137,11 +220,13 @@ def _jit_build(prog, mode: int, hll_lds: bool, m: int, shared: bool = False, loa
             if lay.total <= budget and (shared or mode != D.M_DENSE_LDS or lay.ncopy >= 4 or U == prefs[-1]):
                 try:
                     # a kernel that would spill registers takes the next smaller unroll
-                    return jit.JitScan(prog, mode, U, hll_lds, m, bool(native.narrow4()) if load else True,
+                    return jit.JitScan(prog, mode, U, hll_lds, m, narrow4,
                                        load=load, budget=budget, regstage=regstage, shared=shared,
-                                       reject_spills=U != prefs[-1])
+                                       reject_spills=U != prefs[-1], cached_only=cached_only)
                 except jit.JitSpill:
                     continue
+                except jit.NotCached:
+                    raise
                 except Exception as e:  # pragma: no cover - compile problems fall back loudly
                     import warnings
 

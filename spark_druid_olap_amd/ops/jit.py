@@ -1119,12 +1119,25 @@ class JitSpill(RuntimeError):
     the torch allocator -- under memory pressure that allocation fails and aborts the queue."""
 
 
+class NotCached(RuntimeError):
+    """(``cached_only``) the kernel is not compiled yet; ``key`` names its code-cache entry."""
+
+    def __init__(self, key: str):
+        super().__init__(key)
+        self.key = key
+
+
+def is_cached(src: str) -> bool:
+    key = _code_key(src)
+    return key in _handles or (cache_dir() / f"{key}.co").exists()
+
+
 class JitScan:
     """A compiled, specialized scan kernel for one ScanProgram shape."""
 
     def __init__(self, prog, mode: int, U: int, hll_lds: bool, m: int, narrow4: bool, load: bool = True,
                  budget: int = 150 * 1024, regstage: bool = False, shared: bool = False, literals: bool = False,
-                 reject_spills: bool = False):
+                 reject_spills: bool = False, cached_only: bool = False):
         self.literals = literals
         self._args = (prog, mode, U, hll_lds, m, narrow4, load, budget, regstage, shared)
         self.lay = layout(prog, mode, U, hll_lds, m, budget, regstage, shared)
@@ -1135,6 +1148,8 @@ class JitScan:
                            ).hexdigest()[:6]
         self.name = f"sdo_jit_{tag}"
         self.src = g.source(self.name)
+        if cached_only and not is_cached(self.src):
+            raise NotCached(_code_key(self.src))
         self.meta = kernel_meta(compile_code(self.src, self.name) or b"")
         # SGPR spills go to VGPR lanes (no scratch), but a few hundred of them turn the word loop into
         # writelane / readlane traffic: an unrolled count over one key spilled 1435 SGPRs at U=16,

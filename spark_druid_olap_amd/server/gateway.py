@@ -294,7 +294,12 @@ class NativeHiveServer(HiveThriftServer):
         if df.plan is None:  # a command that looked like a query: already executed
             res = df.to_pandas()
         else:
-            df.prepare()  # lowering + a first-seen shape's compile: before a stream slot is held
+            # lowering (+ a first-seen shape's compile, in the background: the first runs of a new
+            # shape use the interpreter kernel) -- before a stream slot is held
+            from ..engine.device_exec import async_compile
+
+            with async_compile():
+                df.prepare()
             with sess.engine.coalescer().scheduler.lease():
                 try:
                     res = df.run(token=token)  # the executor's columns, encoded without a DataFrame

@@ -555,8 +555,11 @@ class Session:
             run_spec = run_spec.copy(context=ctx.copy(deterministic=True) if ctx is not None
                                      else S.QuerySpecContext(deterministic=True))
         prep = getattr(dq, "_prepared", None)
+        # (an interim plan -- first-seen kernels compiling in the background, engine/device_exec.py
+        # async_compile -- is replaced once they are all compiled)
         stale = lambda p: p is None or getattr(dq, "_prepared_spec", None) is not spec or \
-            getattr(p, "deterministic", False) != (det or getattr(p, "deterministic", False))  # noqa: E731
+            getattr(p, "deterministic", False) != (det or getattr(p, "deterministic", False)) or \
+            (bool(getattr(p, "jit_pending", None)) and all(f.done() for f in p.jit_pending))  # noqa: E731
         if stale(prep):
             # concurrent sessions share cached plans: prepare once -- under a lock of this pushed
             # query only, so preparing (and compiling) one statement never blocks another's
@@ -567,8 +570,13 @@ class Session:
             with lock:
                 prep = getattr(dq, "_prepared", None)
                 if stale(prep):
+                    from .engine.device_exec import prepare_collecting
+
                     with T.span("sdo.lower"):
-                        prep = self.engine.prepare(run_spec, ds, dq.info.get("historical"))
+                        prep, pending = prepare_collecting(
+                            lambda: self.engine.prepare(run_spec, ds, dq.info.get("historical")))
+                    if pending:
+                        prep.jit_pending = pending
                     # output SQL types: large results decode numeric dictionary keys on the device
                     # (and integer outputs of string-valued extractions: 'yyyy' time formats)
                     prep.out_types = {n: t for n, t, k in dq.columns

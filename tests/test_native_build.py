@@ -365,3 +365,39 @@ def test_jit_hashed_partition_carries_hll_words(ds_small, tmp_path, monkeypatch)
     assert (1 << L["cap_log2"]) * per <= 160 * 1024 - 256
     w = jit.JitScan(prog, D.M_PART, 4, False, 1 << prog.hll_p, True, load=False)
     assert w.src.count("hll_bucket_rho(") + w.src.count(">> 5) << 8)") >= 1 and f"* {L['rw']}u;" in w.src
+
+
+def test_async_compile_interim_then_cached(tmp_path, monkeypatch, ds_small):
+    """Serving scope (engine/device_exec.py async_compile): a first-seen kernel shape is compiled on
+    a background thread and the prepare gets no kernel (the interpreter runs meanwhile); once the
+    compile finishes, the same shape is found in the code cache.  Plans the interpreter would run
+    in another mode (shared LDS tables) keep compiling in the foreground."""
+    from spark_druid_olap_amd.engine import device_exec as DE
+    from spark_druid_olap_amd.engine.executor import Engine
+    from spark_druid_olap_amd.models import tpch
+    from spark_druid_olap_amd.ops import desc as D
+    from spark_druid_olap_amd.ops import jit, native
+    from spark_druid_olap_amd.session import Session
+
+    monkeypatch.setenv("SDO_JIT_CACHE", str(tmp_path / "jit"))
+    monkeypatch.setattr(native, "narrow4", lambda: 1)
+    monkeypatch.setattr(DE, "USE_JIT", True)
+    s = Session(engine=Engine(use_native=False))
+    s.register_datasource(ds_small)
+    s.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)
+    s.sql(tpch.druid_ddl(with_column_mapping=False))
+    q = ("select l_returnflag, l_linestatus, sum(l_quantity), count(*) from orderLineItemPartSupplier "
+         "where l_shipdate <= date '1998-09-02' group by l_returnflag, l_linestatus")
+    prog = s.engine.prepare(s.sql(q).druid_query_specs()[0], ds_small).scans[0][1]
+    prog.packed = {}
+    with DE.async_compile():
+        js, pending = DE.prepare_collecting(lambda: DE._jit_build(prog, D.M_DENSE_LDS, False, 2048))
+        assert js is None and len(pending) == 1
+        pending[0].result(timeout=300)
+    # compiled into the code cache: the next prepare of this shape gets the kernel at once
+    js = DE._jit_select(prog, D.M_DENSE_LDS, False, 2048, load=False, narrow4=True, cached_only=True)
+    assert js is not None and jit.is_cached(js.src)
+    # a shared-table plan is not interpreter-compatible: foreground compile, no pending future
+    assert not DE._async_ok(prog, D.M_DENSE_LDS, True)
+    # outside the scope nothing is deferred
+    assert DE.prepare_collecting(lambda: 1) == (1, [])
