@@ -38,6 +38,7 @@ BLOCKS_PER_CU = int(os.environ.get("SDO_BLOCKS_PER_CU", "3"))
 USE_JIT = os.environ.get("SDO_JIT", "1") != "0"
 JIT_BLOCKS = int(os.environ.get("SDO_JIT_BLOCKS", "3"))  # target resident workgroups per CU
 JIT_STAGE = os.environ.get("SDO_JIT_STAGE", "auto")       # auto | reg (VGPR loads) | lds (LDS-DMA planes)
+JIT_TRACE = os.environ.get("SDO_JIT_TRACE", "0") == "1"  # print the unroll / budget candidates tried
 FORCE_U = 0  # cap the words per step of generated kernels (0: the register / LDS-driven choice)
 # Literal specialization of repeated statements (ops/jit.py JitScan.specialized): a prepared scan's
 # first runs use the shape's shared kernel (query constants read from the descriptor: every
@@ -220,13 +221,17 @@ def _jit_select(prog, mode: int, hll_lds: bool, m: int, shared: bool = False, lo
     for budget in budgets:
         for U in prefs:
             lay = jit.layout(prog, mode, U, hll_lds, m, budget, regstage, shared)
+            if JIT_TRACE:
+                print(f"[jit] U={U} budget={budget} LDS={lay.total} ncopy={lay.ncopy}", flush=True)
             if lay.total <= budget and (shared or mode != D.M_DENSE_LDS or lay.ncopy >= 4 or U == prefs[-1]):
                 try:
                     # a kernel that would spill registers takes the next smaller unroll
                     return jit.JitScan(prog, mode, U, hll_lds, m, narrow4,
                                        load=load, budget=budget, regstage=regstage, shared=shared,
                                        reject_spills=U != prefs[-1], cached_only=cached_only)
-                except jit.JitSpill:
+                except jit.JitSpill as e:
+                    if JIT_TRACE:
+                        print(f"[jit] U={U} budget={budget} rejected: {e}", flush=True)
                     continue
                 except jit.NotCached:
                     raise

@@ -1104,7 +1104,9 @@ def kernel_meta(code: bytes) -> dict:
 
                     md = msgpack.unpackb(desc, raw=False, strict_map_key=False)
                     ks = md.get("amdhsa.kernels") or [{}]
-                    return dict(ks[0])
+                    out = dict(ks[0])
+                    out["amdhsa.target"] = md.get("amdhsa.target")
+                    return out
     except (struct.error, ValueError, IndexError, ImportError):
         pass
     return {}

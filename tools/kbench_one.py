@@ -35,6 +35,13 @@ def main():
         _, prog, prep = pq.scans[0]
         pq.run()
         torch.cuda.synchronize()
+        js = prep.jit
+        if js is not None:  # which kernel shape runs (tag = mode, U, copies, staging, shared table)
+            pk = {c: getattr(v, "width", None) for c, v in (getattr(prog, "packed", None) or {}).items()}
+            print(f"{name}: {js.name} U={js.U} ncopy={js.lay.ncopy} regstage={js.lay.regstage} "
+                  f"LDS={js.lay.total} spills={js.spills} packed={pk} "
+                  f"meta={ {k: js.meta.get(k) for k in ('.vgpr_count', '.sgpr_count', '.sgpr_spill_count', '.vgpr_spill_count', '.private_segment_fixed_size', 'amdhsa.target')} }",
+                  flush=True)
         for _ in range(args.iters):
             b = prep._bufs()
             prep._reset(b)
