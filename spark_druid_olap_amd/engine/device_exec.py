@@ -1327,6 +1327,9 @@ def theta_producer_prog(prog: ScanProgram, cols: List[str]) -> ScanProgram:
     return ep
 
 
+THETA_HIST_BINS = 2048
+
+
 class PreparedTheta:
     """thetaSketch aggregators fused into the scan: ONE JIT producer pass (ops/jit.py A_THETA) writes
     (u32 group key, 62-bit KMV hash per theta column) records of the selected rows into its chunk
@@ -1362,10 +1365,22 @@ class PreparedTheta:
         self.words = max(1, cap * self.rw)
         self.seg_lo = (torch.arange(self.nch, dtype=torch.int64) * D.CHUNK_ROWS).to(torch.int32).to(self.dev)
         self._d = d
-        # histogram bits: per-workgroup LDS [G][2^bits] u32 within 64 KiB when G allows, else 12
-        fit = int(math.floor(math.log2(max(1, (64 * 1024 // 4) // self.G))))
-        self.bits = fit if fit >= 8 else 12
+        # histogram bits: few groups keep G x 2^bits <= THETA_HIST_BINS bins (every workgroup flushes
+        # its nonzero bins with global atomics onto the same addresses: 4096 workgroups x 14K bins of
+        # a 7-group SF10 query were 0.44 ms a pass); coarser bins only add candidates below the bound
+        # (the filter keeps target + one bin's records).  Many groups: per-workgroup LDS [G][2^bits]
+        # within 64 KiB when G allows, else 12 bits in global memory.
+        if self.G <= THETA_HIST_BINS // 16:
+            self.bits = int(math.floor(math.log2(THETA_HIST_BINS // self.G)))
+        else:
+            fit = int(math.floor(math.log2(max(1, (64 * 1024 // 4) // self.G))))
+            self.bits = fit if fit >= 8 else 12
         self.bits = max(4, min(16, self.bits))
+        # first-attempt target per aggregator, in multiples of 2k records: learnt from the previous
+        # run (duplicate-heavy columns -- c_name repeats ~6x per ship mode -- need 4x-16x more records
+        # than 2k below the bound for k distinct hashes; a repeated statement then selects in one pass)
+        self._mult = {}
+        self.attempts = {}  # (per aggregator: select passes of the last run)
 
     def select(self, sizes: List[int]) -> List[torch.Tensor]:
         """Per theta aggregator (``sizes``: its k) the sorted unique (group, hash) pairs of its k
@@ -1388,7 +1403,8 @@ class PreparedTheta:
             bound = torch.empty(G, dtype=torch.int64, device=dev)
             count = torch.zeros(1, dtype=torch.int64, device=dev)
             for t, k in enumerate(sizes):
-                target = torch.full((G,), 2 * k, dtype=torch.int64, device=dev)
+                mult = self._mult.get(t, 1)
+                target = torch.full((G,), 2 * k * mult, dtype=torch.int64, device=dev)
                 for attempt in range(7):
                     if attempt == 6:  # (never in practice after six 4x rounds): every pair
                         target = torch.full((G,), 1 << 62, dtype=torch.int64, device=dev)
@@ -1404,13 +1420,18 @@ class PreparedTheta:
                         if c <= cap:
                             break
                         cap = c  # a duplicate-heavy bin held more candidates than the first guess
-                    pairs = _sorted_unique_pairs(og[:c], oh[:c])
+                    # (candidates are below their group's bound: one sort of g << s | h when they fit)
+                    hmax = int(bound.max().item())
+                    pairs = _sorted_unique_pairs(og[:c], oh[:c], G, hmax)
                     distinct = torch.bincount(pairs[:, 0], minlength=G) if pairs.numel() else \
                         torch.zeros(G, dtype=torch.int64, device=dev)
                     short = (distinct < k) & (bound < (1 << 62))
                     if not bool(short.any()):
                         break
                     target = torch.where(short, target * 4, target)
+                    mult = min(mult * 4, 1 << 12)
+                self._mult[t] = mult
+                self.attempts[t] = attempt + 1
                 out.append(_kmv(pairs, k))
         finally:
             PART_POOL.release(slab)

@@ -1342,11 +1342,21 @@ def combine_local(prog: ScanProgram, parts: List[Partials]) -> Partials:
     return merge_sparse([p.compact() for p in parts], prog.slots)
 
 
-def _sorted_unique_pairs(g: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
+def _sorted_unique_pairs(g: torch.Tensor, h: torch.Tensor, groups: int = 0, hmax: int = -1) -> torch.Tensor:
     """Distinct (group, hash) pairs sorted by group then hash: two stable device radix sorts (LSD)
-    instead of a lexicographic unique over rows."""
+    instead of a lexicographic unique over rows -- or ONE sort of ``g << s | h`` when every hash is
+    below ``hmax`` < 2^s and the ``groups`` fit the bits above (a theta select's candidates: the
+    per-group bounds are far below 2^62)."""
     if g.numel() == 0:
         return torch.zeros((0, 2), dtype=torch.int64, device=g.device)
+    gb = max(1, int(groups - 1).bit_length()) if groups > 0 else 64
+    if 0 <= hmax and gb < 63 and hmax <= (1 << (63 - gb)):
+        sh = 63 - gb
+        key = torch.sort((g.to(torch.int64) << sh) | h.to(torch.int64)).values
+        keep = torch.ones(key.numel(), dtype=torch.bool, device=key.device)
+        keep[1:] = key[1:] != key[:-1]
+        key = key[keep]
+        return torch.stack([key >> sh, key & ((1 << sh) - 1)], dim=1)
     o = torch.sort(h, stable=True).indices
     o = o[torch.sort(g[o], stable=True).indices]
     g, h = g[o].to(torch.int64), h[o].to(torch.int64)

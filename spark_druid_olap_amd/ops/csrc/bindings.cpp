@@ -720,8 +720,11 @@ static void theta_select_regions(uint64_t recs, int rw, int hoff, uint64_t seg_l
   const int64_t lds = (int64_t)(G << bits) * 4;
   const int use_lds = lds <= 64 * 1024 ? 1 : 0;
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(nseg, 4096));
+  // (the histogram's workgroups each flush their LDS bins with global atomics onto the same
+  // addresses: fewer, longer-running workgroups for it)
+  const unsigned hgrid = use_lds ? (unsigned)std::max<int64_t>(1, std::min<int64_t>(nseg, 1024)) : grid;
   if (nseg > 0) {
-    hipLaunchKernelGGL(sdo::theta_hist_regions_kernel, dim3(grid), dim3(256), use_lds ? (size_t)lds : 0, s,
+    hipLaunchKernelGGL(sdo::theta_hist_regions_kernel, dim3(hgrid), dim3(256), use_lds ? (size_t)lds : 0, s,
                        (const uint32_t*)recs, rw, hoff, (const uint32_t*)seg_lo, (const uint32_t*)seg_hi, nseg, (int)G,
                        bits, (uint32_t*)hist, use_lds);
     check(hipGetLastError(), "theta_hist_regions_kernel launch");

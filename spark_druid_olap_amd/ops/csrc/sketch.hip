@@ -182,16 +182,30 @@ __global__ void __launch_bounds__(256) theta_hist_regions_kernel(const uint32_t*
     for (int64_t i = threadIdx.x; i < nb; i += blockDim.x) lh[i] = 0u;
     __syncthreads();
   }
+  constexpr int R = 4;  // records in flight per thread (loads issued before the atomics)
   for (int64_t sgi = blockIdx.x; sgi < nseg; sgi += gridDim.x) {
     const uint32_t lo = seg_lo[sgi], hi = seg_hi[sgi];
-    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-      const uint32_t* r = recs + (uint64_t)i * rw;
-      const uint32_t g = r[0];
-      const uint64_t h = (uint64_t)r[hoff] | ((uint64_t)r[hoff + 1] << 32);
-      if (g >= (uint32_t)G) continue;  // (never for a consistent layout; never fault)
-      const int64_t idx = ((int64_t)g << bits) + (int64_t)(h >> shift);
-      if (use_lds) atomicAdd(&lh[idx], 1u);
-      else atomicAdd(&hist[idx], 1u);
+    for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += R * blockDim.x) {
+      uint32_t g[R];
+      uint64_t h[R];
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const uint32_t i = i0 + u * blockDim.x;
+        g[u] = 0xffffffffu;
+        h[u] = 0;
+        if (i < hi) {
+          const uint32_t* r = recs + (uint64_t)i * rw;
+          g[u] = r[0];
+          h[u] = (uint64_t)r[hoff] | ((uint64_t)r[hoff + 1] << 32);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        if (g[u] >= (uint32_t)G) continue;  // (past the region's end; never fault)
+        const int64_t idx = ((int64_t)g[u] << bits) + (int64_t)(h[u] >> shift);
+        if (use_lds) atomicAdd(&lh[idx], 1u);
+        else atomicAdd(&hist[idx], 1u);
+      }
     }
   }
   if (use_lds) {

@@ -382,6 +382,7 @@ def test_async_compile_interim_then_cached(tmp_path, monkeypatch, ds_small):
     monkeypatch.setenv("SDO_JIT_CACHE", str(tmp_path / "jit"))
     monkeypatch.setattr(native, "narrow4", lambda: 1)
     monkeypatch.setattr(DE, "USE_JIT", True)
+    monkeypatch.setattr(DE, "ASYNC_JIT", True)  # (opt-in, SDO_ASYNC_JIT=1)
     s = Session(engine=Engine(use_native=False))
     s.register_datasource(ds_small)
     s.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)

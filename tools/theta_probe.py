@@ -42,6 +42,10 @@ def main():
         ts.append((time.perf_counter() - t) * 1e3)
     print(f"theta group-by SF{a.sf:g}: median {statistics.median(ts):.3f} ms  min {min(ts):.3f} ms  "
           f"groups {r.num_rows}", flush=True)
+    th = getattr(pq, "_theta_prep", None)
+    if th:
+        print(f"   select passes per aggregator (last run): {th.attempts}  target multipliers: {th._mult}  "
+              f"histogram bits: {th.bits}", flush=True)
     for i in range(r.num_rows):
         print("  ", r.data["l_shipmode"][i], round(float(r.data["orders"][i])), round(float(r.data["customers"][i])))
 
