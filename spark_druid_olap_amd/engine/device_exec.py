@@ -344,7 +344,8 @@ class PreparedScan:
                 self.jit = _jit_for(prog, self.mode, False, self.m)
         # stored (rolled-up) HLL sketches: the JIT kernel unions them in the scan (A_HLL_STORED);
         # the interpreter leaves them to the executor (engine/executor.py _merge_stored_hll)
-        self.stored_fused = bool(prog.stored_hll) and self.jit is not None and self.mode != D.M_PART
+        # (partitioned: the records carry the row ids, part_agg unions the stored pairs per group)
+        self.stored_fused = bool(prog.stored_hll) and self.jit is not None
         self.hll32 = bool(getattr(prog, "hll32", False)) and self.jit is not None
         prog.hll32 = self.hll32
         self._slot_lock = threading.Lock()
@@ -618,7 +619,7 @@ class PreparedScan:
                              [f[0] for f in L["fields"]], [f[1] for f in L["fields"]],
                              [int(op) for op, _ in prog.slots], [int(init) for _, init in prog.slots],
                              b.acc.data_ptr(), [], 1, 0, 0, 0, [h.data_ptr() for h in b.hll] if L.get("nhll") else [],
-                             int(prog.hll_p), st)
+                             int(prog.hll_p), st, self._stored_csr() if L.get("nhll") else [])
             return None
         while True:
             acc, keys, cnt, _ = self._sparse_out(b, "hv_out", False)
@@ -630,6 +631,18 @@ class PreparedScan:
             if n <= acc.shape[0]:
                 return Partials("sparse", acc[:n], keys[:n], [])
             self.part_cap = _next_pow2(n + n // 4)  # more survivors than room: grow, aggregate again
+
+    def _stored_csr(self) -> list:
+        """(offsets, pairs) device pointers of each stored sketch metric, in register-table order."""
+        ds = self.prog.ds
+        out = []
+        for _, metric, _ in self.prog.stored_hll:
+            sk = ds.metrics[metric].sketch
+            if sk.offsets.device != self.dev or sk.values.device != self.dev or sk.offsets.dtype != torch.int64 \
+                    or sk.values.dtype != torch.int32:
+                raise RuntimeError(f"stored sketch {metric!r} is not a device int64/int32 CSR")
+            out.append((sk.offsets.data_ptr(), sk.values.data_ptr()))
+        return out
 
     def _run_part_hashed(self, b: "_Bufs", recs: torch.Tensor, base: torch.Tensor) -> Partials:
         """Sparse LDS-hash aggregation of the hash-partitioned records (keys beyond 32 bits).  A
@@ -1527,7 +1540,7 @@ def part_layout(prog) -> dict:
     ns = max(1, prog.nslots)
     if jit.part_hashed(prog):
         return part_hash_layout(prog)
-    nh = jit.part_hll_count(prog) if prog.nhll else 0
+    nh = jit.part_hll_count(prog) if (prog.nhll or getattr(prog, "stored_hll", None)) else 0
     if nh:
         # a group's slots plus its byte registers: sub-buckets of a few dozen groups per LDS table
         per = 8 * ns + nh * (1 << prog.hll_p)
@@ -1565,7 +1578,7 @@ def part_hash_layout(prog, scale: int = 1, groups: Optional[float] = None) -> di
     from ..ops import jit
 
     ns = max(1, prog.nslots)
-    nh = jit.part_hll_count(prog) if prog.nhll else 0
+    nh = jit.part_hll_count(prog) if (prog.nhll or getattr(prog, "stored_hll", None)) else 0
     per = 8 * (1 + ns) + nh * (1 << prog.hll_p)  # (a slot's key, slots and HLL byte registers)
     cap_log2 = max(6, min(14, int(math.floor(math.log2(max(1, HASH_TABLE_BYTES // per))))))
     if groups is None:

@@ -613,7 +613,8 @@ static void part_split(uint64_t in, int RW, uint64_t seg_lo, uint64_t seg_hi, in
 static void part_agg_hll(uint64_t recs, int RW, uint64_t base, int64_t nsub, int64_t G, int shift, std::vector<int> slot,
                          std::vector<int> width, std::vector<int> ops, std::vector<int64_t> init, uint64_t gacc,
                          std::vector<std::tuple<int, int, int, double, double>> having, int conj, uint64_t out_keys,
-                         uint64_t out_count, int64_t cap, std::vector<uint64_t> hll, int hll_p, uint64_t stream) {
+                         uint64_t out_count, int64_t cap, std::vector<uint64_t> hll, int hll_p, uint64_t stream,
+                         std::vector<std::tuple<uint64_t, uint64_t>> stored = {}) {
   if (nsub <= 0 || G <= 0) return;
   sdo::PartFields f{};
   if (slot.size() != width.size() || slot.size() > (size_t)sdo::MAX_SLOTS) throw std::invalid_argument("part_agg: fields");
@@ -634,6 +635,15 @@ static void part_agg_hll(uint64_t recs, int RW, uint64_t base, int64_t nsub, int
   hl.n = (int)hll.size();
   hl.p = hll.empty() ? 0 : hll_p;
   for (size_t h = 0; h < hll.size(); ++h) hl.regs[h] = (unsigned char*)hll[h];
+  // stored sketches: the LAST stored.size() register tables, each with its (offsets, pairs) CSR
+  if (stored.size() > hll.size()) throw std::invalid_argument("part_agg: stored sketches without register tables");
+  for (size_t j = 0; j < stored.size(); ++j) {
+    const size_t h = hll.size() - stored.size() + j;
+    hl.stored |= 1u << h;
+    hl.sk_off[h] = (const int64_t*)std::get<0>(stored[j]);
+    hl.sk_val[h] = (const int32_t*)std::get<1>(stored[j]);
+    if (!hl.sk_off[h] || !hl.sk_val[h]) throw std::invalid_argument("part_agg: null stored sketch");
+  }
   words += hl.n;
   if (words != RW) throw std::invalid_argument("part_agg: record width does not match the fields");
   for (size_t s = 0; s < ops.size(); ++s) {
@@ -675,7 +685,7 @@ static void part_agg(uint64_t recs, int RW, uint64_t base, int64_t nsub, int64_t
                      std::vector<std::tuple<int, int, int, double, double>> having, int conj, uint64_t out_keys,
                      uint64_t out_count, int64_t cap, uint64_t stream) {
   part_agg_hll(recs, RW, base, nsub, G, shift, slot, width, ops, init, gacc, having, conj, out_keys, out_count, cap, {},
-               0, stream);
+               0, stream, {});
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -664,8 +664,18 @@ __global__ __launch_bounds__(512) void part_agg_kernel(const uint32_t* __restric
       }
       for (int h = 0; h < hl.n; ++h) {
         const uint32_t code = rec[w + h];
-        if (code & 0xffu) lds_max_u8(hr + (((int64_t)h << shift) + local) * m, (int64_t)((code >> 8) & (uint32_t)(m - 1)),
-                                     code & 0xffu);
+        unsigned char* gr = hr + (((int64_t)h << shift) + local) * m;
+        if ((hl.stored >> h) & 1u) {
+          // a stored sketch: union the row's sparse pairs (row id; all-ones = filtered out)
+          if (code == 0xffffffffu) continue;
+          const int64_t a = hl.sk_off[h][code], e = hl.sk_off[h][code + 1];
+          for (int64_t j = a; j < e; ++j) {
+            const uint32_t pk = (uint32_t)hl.sk_val[h][j];
+            if (pk & 0xffu) lds_max_u8(gr, (int64_t)((pk >> 8) & (uint32_t)(m - 1)), pk & 0xffu);
+          }
+          continue;
+        }
+        if (code & 0xffu) lds_max_u8(gr, (int64_t)((code >> 8) & (uint32_t)(m - 1)), code & 0xffu);
       }
     }
   }

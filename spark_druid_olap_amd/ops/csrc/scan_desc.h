@@ -220,12 +220,18 @@ struct PartFields {
 
 // HLL aggregators of the partitioned group-by (partition.hip part_agg_kernel): each record carries
 // one (bucket << 8 | rho) word per HLL after its value fields; a sub-bucket's groups keep their
-// byte registers in LDS and write them to their rows of the [G][2^p] register tables.
+// byte registers in LDS and write them to their rows of the [G][2^p] register tables.  A stored
+// (rolled-up hyperUnique) sketch -- bit h of `stored` -- carries the row id instead (0xffffffff: the
+// aggregator's filter rejected the row), and the row's sparse (bucket << 8 | rho) pairs
+// sk_val[sk_off[row] .. sk_off[row + 1]) are unioned into the group's registers.
 constexpr int PART_MAX_HLL = 4;
 struct PartHll {
   int32_t n;
   int32_t p;
   unsigned char* regs[PART_MAX_HLL];
+  uint32_t stored;
+  const int64_t* sk_off[PART_MAX_HLL];
+  const int32_t* sk_val[PART_MAX_HLL];
 };
 
 // HAVING fused into the partitioned aggregation (partition.hip part_agg_kernel): up to 4

@@ -135,26 +135,40 @@ PART_HLL = True  # HLL aggregators ride the partitioned records as (bucket << 8 
 PART_HLL_MAX_BYTES = 1 << 30  # register tables ([G][2^p] bytes per HLL) the partitioned path writes
 
 
-def part_hll_count(prog) -> int:
-    """HLL aggregators a partition record carries (one word each, after the value fields)."""
+def part_stored_count(prog) -> int:
+    """Stored (rolled-up hyperUnique) sketches a partition record carries: one row-id word each,
+    after the query-time HLL words (partition.hip part_agg_kernel unions the row's stored pairs)."""
     if not hasattr(prog, "aops"):
-        return int(prog.nhll)
-    return sum(1 for a in prog.aops if a["kind"] in D.HLL_KINDS)
+        return len(getattr(prog, "stored_hll", None) or [])
+    return sum(1 for a in prog.aops if a["kind"] == D.A_HLL_STORED)
+
+
+def part_hll_count(prog) -> int:
+    """HLL register tables of a partitioned group-by: query-time HLL words plus stored-sketch row
+    words (one word each per record, after the value fields; the query-time ones first)."""
+    if not hasattr(prog, "aops"):
+        return int(prog.nhll) + part_stored_count(prog)
+    return sum(1 for a in prog.aops if a["kind"] in D.HLL_KINDS) + part_stored_count(prog)
 
 
 def part_eligible(prog) -> bool:
     """The partitioned group-by handles every slot operator and any key space (beyond 32 bits by
-    hash), and query-time HLL sketches of dense (u32) key spaces whose register tables fit
-    PART_HLL_MAX_BYTES; not stored (rolled-up) sketches."""
+    hash), and query-time HLL sketches -- plus stored (rolled-up) sketches on dense (u32) key
+    spaces -- whose register tables fit PART_HLL_MAX_BYTES."""
     slots = getattr(prog, "slots", None)
     n = len(slots) if slots is not None else prog.nslots
-    if not (n > 0 and not getattr(prog, "stored_hll", None) and 0 < prog.G < (1 << 62) and not prog.empty):
+    if not (n > 0 and 0 < prog.G < (1 << 62) and not prog.empty):
         return False
-    if prog.nhll:
+    nst = len(getattr(prog, "stored_hll", None) or [])
+    if nst and int(getattr(getattr(prog, "ds", None), "num_rows", 0)) >= 0xFFFFFFFF:
+        return False  # (a stored sketch's record word is the u32 row id; all-ones = filtered out)
+    if prog.nhll or nst:
         nh = part_hll_count(prog)
-        if not (PART_HLL and nh == prog.nhll and nh <= 4):
+        if not (PART_HLL and nh == prog.nhll + nst and nh <= 4):
             return False
         if part_hashed(prog):
+            if nst:  # (the hashed sparse aggregation has no stored-sketch union)
+                return False
             # sparse groups, registers per LDS hash-table slot: the smallest table (64 slots) must
             # hold every sketch's 2^p registers next to the slots (p = 11: one HLL per query)
             return 64 * ((1 + n) * 8 + nh * (1 << prog.hll_p)) <= 160 * 1024 - 256
@@ -530,7 +544,7 @@ class _Gen:
         body.append("        const uint64_t am_ = __ballot(mine);")
         fields = part_fields(p, self.cols)
         hdr = part_record_words(p)
-        rw = hdr + sum(w for _, w in fields) + (part_hll_count(p) if p.nhll else 0)
+        rw = hdr + sum(w for _, w in fields) + part_hll_count(p)
         body.append("        if (mine) {")
         body.append(f"          uint32_t* o_ = precs + (uint64_t)(cbase + woff + (uint32_t)__popcll(am_ & lmlt)) * {rw}u;")
         if hdr == 3:
@@ -576,6 +590,16 @@ class _Gen:
                 fx = self.word_expr(a["filt_off"], a["filt_off"] + a["filt_len"])
                 code = f"(((({fx}) >> lane) & 1ull) ? {code} : 0u)"
             body.append(f"          o_[{w}] = {code};")
+            w += 1
+        for ai, a in enumerate(p.aops):
+            # stored sketch: the row id (its CSR run of stored pairs), all-ones when filtered out
+            if a["kind"] != D.A_HLL_STORED:
+                continue
+            rid = f"(uint32_t)(v{ai}_[u])"
+            if a.get("filt_len"):
+                fx = self.word_expr(a["filt_off"], a["filt_off"] + a["filt_len"])
+                rid = f"(((({fx}) >> lane) & 1ull) ? {rid} : 0xffffffffu)"
+            body.append(f"          o_[{w}] = {rid};")
             w += 1
         body.append("        }")
         body.append("        woff += (uint32_t)__popcll(am_);")

@@ -250,3 +250,80 @@ def test_split_ingest_across_ranks_equals_single_ingest(data_dir, tmp_path):
     assert sum(o["pairs"] for o in outs) == int(whole.metrics["uniq_users"].sketch.values.numel())
     assert sum(o["count"] for o in outs) == int(whole.metrics["count"].data[: whole.num_rows].sum())
     assert sum(o["amount"] for o in outs) == pytest.approx(float(whole.metrics["amount"].data[: whole.num_rows].sum()))
+
+
+def test_stored_hll_partitioned_producer_compiles(pair, tmp_path, monkeypatch):
+    """The partitioned producer of a rolled-up hyperUnique group-by (CPU compile): each record ends
+    with one row-id word per stored sketch (all-ones when the aggregator's filter rejects the row)."""
+    from spark_druid_olap_amd.engine.lower import Lowerer
+    from spark_druid_olap_amd.ops import desc as D
+    from spark_druid_olap_amd.ops import jit
+
+    monkeypatch.setenv("SDO_JIT_CACHE", str(tmp_path))
+    rolled, _ = pair
+    q = _q([S.HyperUniqueAggregationSpec("u", "uniq_users"),
+            S.FilteredAggregationSpec(S.SelectorFilterSpec("platform", "ios"),
+                                      S.HyperUniqueAggregationSpec("u_ios", "uniq_users"), "u_ios")],
+           ("country", "platform"))
+    prog = Engine(use_native=False).prepare(q, rolled).scans[0][1]
+    assert len(prog.stored_hll) == 2 and prog.nhll == 0
+    assert jit.part_eligible(prog) and jit.part_stored_count(prog) == 2 and jit.part_hll_count(prog) == 2
+    prog.packed = {}
+    js = jit.JitScan(prog, D.M_PART, 4, False, 1 << prog.hll_p, True, load=False)
+    assert "0xffffffffu" in js.src  # the filtered sketch's "no row" word
+    fields = jit.part_fields(prog)
+    assert sum(w for _, w in fields) + 1 + 2 == 3 + sum(w for _, w in fields)
+
+
+@pytest.mark.gpu
+def test_gpu_stored_hll_partitioned(pair, monkeypatch):
+    """A rolled-up hyperUnique group-by through the radix-partitioned path (records carry the row
+    id, partition.hip part_agg unions the row's stored pairs per group) gives the same registers
+    as the fused dense scan, and through the planner the same estimates as query-time HLL over the
+    raw index."""
+    from spark_druid_olap_amd.engine import device_exec as DE
+    from spark_druid_olap_amd.ops import desc as D
+    from spark_druid_olap_amd.planner import cost
+
+    rolled, raw = pair
+    gr = rolled.to("cuda")
+    aggs = [S.HyperUniqueAggregationSpec("u", "uniq_users"),
+            S.FilteredAggregationSpec(S.SelectorFilterSpec("platform", "ios"),
+                                      S.HyperUniqueAggregationSpec("u_ios", "uniq_users"), "u_ios"),
+            S.FunctionAggregationSpec("longSum", "n", "count")]
+    q = _q(aggs, ("country", "platform"))
+    prog = Engine(use_native=True).prepare(q.copy(), gr).scans[0][1]
+    part = DE.PreparedScan(prog, mode=D.M_PART)
+    assert part.mode == D.M_PART and part.stored_fused and part.part["nhll"] == 2, "not partitioned"
+    ref = DE.PreparedScan(prog, mode=D.M_DENSE_GLOBAL)
+    assert ref.stored_fused
+    for _ in range(2):  # re-execution over the same slot buffers
+        a = part.run()
+    b = ref.run()
+    assert a.kind == "dense" and b.kind == "dense" and len(a.hll) == len(b.hll) == 2
+    assert torch.equal(a.acc.cpu(), b.acc.cpu())
+    for x, y in zip(a.hll, b.hll):
+        assert torch.equal(x.cpu(), y.cpu())
+    # end to end: the planner partitions it (forced), estimates equal the raw index's query-time HLL
+    monkeypatch.setattr(cost, "FORCE_PARTITIONED", True)
+    for knob in ("PLAN_LDS_BUDGET", "SHARED_LDS_MAX"):  # (no LDS table plan for the 1,056 groups)
+        monkeypatch.setattr(cost, knob, 0)
+    qd = S.GroupByQuerySpec("events", [S.DefaultDimensionSpec("country"), S.DefaultDimensionSpec("platform")],
+                            aggregations=aggs[:2], intervals=["2016-01-01/2016-12-31"],
+                            granularity=S.Granularity.parse("day"))
+    pq = Engine(use_native=True).prepare(qd.copy(), gr)
+    modes = [getattr(p, "mode", None) for _, _, p in pq.scans]
+    assert D.M_PART in modes, modes
+    got = Engine(use_native=True).execute(qd.copy(), gr)
+    want = Engine(use_native=False).execute(qd.copy(), raw)
+    assert got.num_rows == want.num_rows
+
+    def rows(r):
+        ts = np.asarray(r.data["timestamp"]).tolist()
+        c, p = materialize(r.data["country"]).tolist(), materialize(r.data["platform"]).tolist()
+        return {(ts[i], c[i], p[i]): (float(r.data["u"][i]), float(r.data["u_ios"][i])) for i in range(r.num_rows)}
+
+    g, w = rows(got), rows(want)
+    assert g.keys() == w.keys()
+    for k in w:
+        assert g[k] == pytest.approx(w[k], rel=1e-12)
