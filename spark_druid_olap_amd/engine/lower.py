@@ -105,6 +105,61 @@ def b_or(xs):
     return out[0] if len(out) == 1 else ("or", out)
 
 
+IMPLY_OR = True  # AND the id sets every disjunct of an OR implies (imply_or_conjuncts)
+
+
+def _or_implied(x) -> list:
+    """Per dimension constrained by an id set in EVERY disjunct of OR ``x``: the union of those
+    sets -- a necessary condition of the OR."""
+    per = None
+    for d in x[1]:
+        m: Dict[str, np.ndarray] = {}
+        for c in (d[1] if _is(d, "and") else [d]):
+            if _is(c, "ids"):
+                m[c[1]] = m[c[1]] & c[2] if c[1] in m else c[2].copy()
+        per = m if per is None else {k: per[k] | m[k] for k in per if k in m}
+        if not per:
+            return []
+    return [("ids", k, v) for k, v in (per or {}).items() if not v.all()]
+
+
+def imply_or_conjuncts(x):
+    """``OR_i (A_i and ...)`` whose disjuncts all constrain dimension d implies ``d in U_i A_i(d)``:
+    those implied id sets become top-level conjuncts next to the OR (semantics unchanged).  They are
+    what the scan can use -- bitmap pre-filter leaves, zones, word skipping -- where the OR alone is
+    evaluated row by row: TPC-H Q19's three (brand, containers, sizes, ship mode, instruction,
+    quantity) disjuncts imply ship mode in (AIR, AIR REG), DELIVER IN PERSON and 3 of 25 brands."""
+    if not IMPLY_OR:
+        return x
+
+    def split(o):
+        """(implied conjuncts, the OR without the disjuncts' conjuncts that equal them)"""
+        extra = _or_implied(o)
+        if not extra:
+            return [], o
+        imp = {lf[1]: lf[2] for lf in extra}
+        ds_ = []
+        for d in o[1]:
+            conj = d[1] if _is(d, "and") else [d]
+            keep = [c for c in conj if not (_is(c, "ids") and c[1] in imp and np.array_equal(c[2], imp[c[1]]))]
+            ds_.append(b_and(keep))
+        return extra, b_or(ds_)
+
+    if _is(x, "or"):
+        extra, rest = split(x)
+        return b_and(extra + [rest]) if extra else x
+    if _is(x, "and") and any(_is(c, "or") for c in x[1]):
+        out = []
+        for c in x[1]:
+            if _is(c, "or"):
+                extra, rest = split(c)
+                out += extra + [rest]
+            else:
+                out.append(c)
+        return b_and(out)
+    return x
+
+
 def b_not(x):
     k = x[0]
     if k == "true":
@@ -1394,8 +1449,20 @@ class Lowerer:
     # ------------------------------------------------------------------ whole query
     def lower_aggregate(self, intervals, filter_spec, dimensions, granularity, aggregations,
                         extra_keys: Sequence[KeyComp] = ()) -> ScanProgram:
+        try:
+            return self._lower_aggregate(intervals, filter_spec, dimensions, granularity, aggregations, extra_keys)
+        except LoweringError:
+            if not IMPLY_OR:
+                raise
+            # (the implied conjuncts made the program too large: lower the filter as written)
+            return self._lower_aggregate(intervals, filter_spec, dimensions, granularity, aggregations, extra_keys,
+                                         imply=False)
+
+    def _lower_aggregate(self, intervals, filter_spec, dimensions, granularity, aggregations,
+                         extra_keys: Sequence[KeyComp] = (), imply: bool = True) -> ScanProgram:
         prog = ScanProgram(self.ds)
         bexpr = self.filter_ir(filter_spec)
+        bexpr = imply_or_conjuncts(bexpr) if imply else bexpr
         ranges, bexpr, ivs = self.query_ranges(intervals, bexpr)
         prog.ranges = ranges
         prog.bexpr = bexpr
@@ -1496,8 +1563,17 @@ class Lowerer:
         prog.section = "p"
 
     def lower_mask(self, intervals, filter_spec) -> ScanProgram:
+        try:
+            return self._lower_mask(intervals, filter_spec)
+        except LoweringError:
+            if not IMPLY_OR:
+                raise
+            return self._lower_mask(intervals, filter_spec, imply=False)
+
+    def _lower_mask(self, intervals, filter_spec, imply: bool = True) -> ScanProgram:
         prog = ScanProgram(self.ds)
         bexpr = self.filter_ir(filter_spec)
+        bexpr = imply_or_conjuncts(bexpr) if imply else bexpr
         ranges, bexpr, ivs = self.query_ranges(intervals, bexpr)
         prog.ranges, prog.bexpr = ranges, bexpr
         if _is(bexpr, "false") or not ranges:
