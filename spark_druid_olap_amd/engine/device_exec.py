@@ -1411,17 +1411,20 @@ class PreparedTheta:
             desc = _upload(d.view(np.uint8), self.dev)
             nat.module_launch(self.jit.handle, desc.data_ptr(), int(self.grid), BLOCK, int(self.jit.lay.total), st)
             G, dev = self.G, self.dev
-            nrec = int((pend.to(torch.int64) - self.seg_lo.to(torch.int64)).clamp_(min=0).sum().item())
+            # (host-side targets and capacities: the only syncs are the candidate count with the
+            # largest bound after each filter pass, and the short-group check)
+            cap_all = max(1, self.nch * D.CHUNK_ROWS)
             hist = torch.empty(G << self.bits, dtype=torch.int32, device=dev)
             bound = torch.empty(G, dtype=torch.int64, device=dev)
             count = torch.zeros(1, dtype=torch.int64, device=dev)
             for t, k in enumerate(sizes):
                 mult = self._mult.get(t, 1)
-                target = torch.full((G,), 2 * k * mult, dtype=torch.int64, device=dev)
+                tgt = np.full(G, 2 * k * mult, dtype=np.int64)
                 for attempt in range(7):
                     if attempt == 6:  # (never in practice after six 4x rounds): every pair
-                        target = torch.full((G,), 1 << 62, dtype=torch.int64, device=dev)
-                    cap = max(1, min(nrec, int(target.clamp(max=1 << 40).sum().item()) * 2 + (1 << 16)))
+                        tgt = np.full(G, 1 << 62, dtype=np.int64)
+                    target = torch.from_numpy(tgt).to(dev)
+                    cap = max(1, min(cap_all, int(np.minimum(tgt, 1 << 40).sum()) * 2 + (1 << 16)))
                     while True:
                         og = torch.empty(cap, dtype=torch.int64, device=dev)
                         oh = torch.empty(cap, dtype=torch.int64, device=dev)
@@ -1429,19 +1432,18 @@ class PreparedTheta:
                                                  pend.data_ptr(), self.nch, G, self.bits, hist.data_ptr(),
                                                  target.data_ptr(), bound.data_ptr(), og.data_ptr(), oh.data_ptr(),
                                                  count.data_ptr(), cap, st)
-                        c = int(count.item())
+                        c, hmax = (int(v) for v in torch.stack([count[0], bound.max()]).tolist())
                         if c <= cap:
                             break
                         cap = c  # a duplicate-heavy bin held more candidates than the first guess
                     # (candidates are below their group's bound: one sort of g << s | h when they fit)
-                    hmax = int(bound.max().item())
                     pairs = _sorted_unique_pairs(og[:c], oh[:c], G, hmax)
                     distinct = torch.bincount(pairs[:, 0], minlength=G) if pairs.numel() else \
                         torch.zeros(G, dtype=torch.int64, device=dev)
-                    short = (distinct < k) & (bound < (1 << 62))
-                    if not bool(short.any()):
+                    short = ((distinct < k) & (bound < (1 << 62))).cpu().numpy()
+                    if not short.any():
                         break
-                    target = torch.where(short, target * 4, target)
+                    tgt = np.where(short, tgt * 4, tgt)
                     mult = min(mult * 4, 1 << 12)
                 self._mult[t] = mult
                 self.attempts[t] = attempt + 1

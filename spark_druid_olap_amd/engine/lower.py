@@ -105,6 +105,7 @@ def b_or(xs):
     return out[0] if len(out) == 1 else ("or", out)
 
 
+_PRE_OPS = (D.F_TRUE, D.F_FALSE, D.F_BITMAP, D.F_BITMAP_OR, D.F_AND, D.F_OR, D.F_NOT)  # chunk-level evaluable
 IMPLY_OR = True  # AND the id sets every disjunct of an OR implies (imply_or_conjuncts)
 
 
@@ -1547,6 +1548,19 @@ class Lowerer:
                 nleaves += n
             else:
                 rest.append(c)
+        # the pre-filter is emitted first so its bitmap leaves are reserved (the per-row section may
+        # then fall back to column tests where leaves run out; the chunk-level pre-filter cannot),
+        # and placed after the per-row section
+        head = prog.fops
+        prog.fops = []
+        if pre:
+            depth = self.emit_filter(prog, b_and(pre))
+            if depth > D.STACK_DEPTH:
+                raise LoweringError("filter too deep for the device stack")
+            if any(int(f[0]) not in _PRE_OPS for f in prog.fops):
+                raise LoweringError("chunk pre-filter is not bitmap-only")
+        pre_ops = prog.fops
+        prog.fops = head
         prog.section = "f"
         if rest:
             depth = self.emit_filter(prog, b_and(rest))
@@ -1555,10 +1569,7 @@ class Lowerer:
         prog.filter_len = len(prog.fops)
         prog.final_pre = not rest
         prog.pre_off = len(prog.fops)
-        if pre:
-            depth = self.emit_filter(prog, b_and(pre))
-            if depth > D.STACK_DEPTH:
-                raise LoweringError("filter too deep for the device stack")
+        prog.fops.extend(pre_ops)
         prog.pre_len = len(prog.fops) - prog.pre_off
         prog.section = "p"
 
