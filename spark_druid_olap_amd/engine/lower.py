@@ -135,6 +135,8 @@ def imply_or_conjuncts(x):
 
     def split(o):
         """(implied conjuncts, the OR without the disjuncts' conjuncts that equal them)"""
+        if all(_is(c, "ids") for d in o[1] for c in (d[1] if _is(d, "and") else [d])):
+            return [], o  # (dimension-only: the OR itself is a bitmap pre-filter, TPC-H Q7)
         extra = _or_implied(o)
         if not extra:
             return [], o

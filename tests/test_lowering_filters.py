@@ -27,7 +27,13 @@ def test_or_implies_per_dimension_id_sets():
 
 
 def test_or_without_a_common_dimension_is_unchanged():
-    e = ("or", [_ids("a", 4, [1]), _ids("b", 3, [0])])
+    e = ("or", [("and", [_ids("a", 4, [1]), ("cmp", "q", "<", 5)]), _ids("b", 3, [0])])
+    assert L.imply_or_conjuncts(e) is e
+
+
+def test_dimension_only_or_is_left_to_the_bitmap_prefilter():
+    """(TPC-H Q7's nation pairs: the OR is bitmap-only as written; implied sets would only add leaves)"""
+    e = ("or", [("and", [_ids("a", 4, [1]), _ids("b", 4, [2])]), ("and", [_ids("a", 4, [2]), _ids("b", 4, [1])])])
     assert L.imply_or_conjuncts(e) is e
 
 
