@@ -260,11 +260,19 @@ def _layout(prog, mode: int, U: int, hll_lds: bool, m: int, budget: int, regstag
                      shared and mode == D.M_DENSE_LDS, G)
 
 
+PRE_LDS_SELECTIVITY = 0.25
+
+
 def prefer_regstage(prog) -> bool:
     """Staging choice measured on MI355X (tools/query_probe.py, SF100): VGPR staging wins for wide
     unfiltered payloads (TPC-H Q1: 1.9 vs 2.2 ms), LDS-DMA staging for word-filtered scans and tiny
     payloads (Q8: 0.14 vs 0.29 ms, 2-byte payload count: 0.46 vs 0.65 ms)."""
     if prog.filter_len and not prog.final_pre:
+        return False
+    # a selective chunk pre-filter (bitmap leaves) leaves a few rows per word: LDS-DMA staging
+    # (TPC-H Q11's partitioned producer, 4% of rows: 3.46 -> 2.22 ms; tools/sql_probe.py A/B)
+    n = max(1, int(getattr(getattr(prog, "ds", None), "num_rows", 0) or 1))
+    if prog.pre_len and float(getattr(prog, "est_rows", n)) < PRE_LDS_SELECTIVITY * n:
         return False
     cols = col_infos(prog)
     return sum((c.pw / 8) if c.pw else (1 << c.lg) for i, c in cols.items() if i >= D.PAYLOAD_BASE) > 4
