@@ -1257,6 +1257,10 @@ def _numeric_key_join_device(arrs, li_all: np.ndarray, ri_all: np.ndarray):
     if not torch.cuda.is_available():
         return None
     dev = torch.device("cuda", torch.cuda.current_device())
+    if len(arrs) == 1:
+        out = _unique_right_join_device(arrs[0], li_all, ri_all, dev)
+        if out is not None:
+            return out
     nl = len(li_all)
     lc = torch.zeros(nl, dtype=torch.int64, device=dev)
     rc = torch.zeros(len(ri_all), dtype=torch.int64, device=dev)
@@ -1283,6 +1287,39 @@ def _numeric_key_join_device(arrs, li_all: np.ndarray, ri_all: np.ndarray):
     start = torch.repeat_interleave(lo - (torch.cumsum(cnt, 0) - cnt), cnt)
     ri = ri_t[order[start + torch.arange(tot, device=dev)]]
     return li.cpu().numpy(), ri.cpu().numpy()
+
+
+_DIRECT_JOIN_SPAN = 1 << 26
+
+
+def _unique_right_join_device(arr, li_all: np.ndarray, ri_all: np.ndarray, dev):
+    """One integer key, unique on the right (a pushed group-by's result joined on its own key: TPC-H
+    Q17's part x avg-quantity): a direct-address table over the key range instead of sorts -- one
+    scatter of the right rows' positions, one gather per left row.  None when the keys are not
+    integers, their range exceeds _DIRECT_JOIN_SPAN, or the right keys repeat."""
+    import torch
+
+    a, b = arr
+    if a.dtype.kind not in "iu" or b.dtype.kind not in "iu" or not len(ri_all) or not len(li_all):
+        return None
+    x = torch.from_numpy(np.ascontiguousarray(a[li_all], dtype=np.int64)).to(dev)
+    y = torch.from_numpy(np.ascontiguousarray(b[ri_all], dtype=np.int64)).to(dev)
+    lo, hi, ylo, yhi = (int(v) for v in torch.stack([x.min(), x.max(), y.min(), y.max()]).tolist())
+    lo, hi = min(lo, ylo), max(hi, yhi)
+    span = hi - lo + 1
+    if span > _DIRECT_JOIN_SPAN:
+        return None
+    pos = torch.full((span,), -1, dtype=torch.int64, device=dev)
+    cnt = torch.zeros(span, dtype=torch.int32, device=dev)
+    cnt.index_add_(0, y - lo, torch.ones_like(y, dtype=torch.int32))
+    pos.index_copy_(0, y - lo, torch.arange(len(y), dtype=torch.int64, device=dev))
+    r = pos.index_select(0, x - lo)
+    hit = r >= 0
+    li = torch.nonzero(hit).flatten()
+    ri = r.index_select(0, li)
+    if int(cnt.max()) > 1:
+        return None  # (repeated right keys: the general join pairs them all)
+    return li_all[li.cpu().numpy()], ri_all[ri.cpu().numpy()]
 
 
 def _pair_batch(lb: Batch, rb: Batch, li, ri) -> Batch:

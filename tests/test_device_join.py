@@ -40,3 +40,23 @@ def test_device_join_equals_host(multi, flt, monkeypatch):
     monkeypatch.setattr(X, "_DEVICE_JOIN_MIN", 1)
     dev = X._numeric_key_join(lk, rk, lok, rok)
     assert np.array_equal(host[0], dev[0]) and np.array_equal(host[1], dev[1])
+
+
+@pytest.mark.gpu
+def test_direct_address_join_for_unique_right_keys(monkeypatch):
+    """Unique integer right keys (a group-by result joined on its key, TPC-H Q17) take the
+    direct-address path: same pairs, same order as the host join."""
+    rng = np.random.default_rng(11)
+    rkeys = rng.permutation(2_000_000)[:20_000] + 5
+    lk = [pd.Series(rng.choice(np.concatenate([rkeys, rng.integers(0, 3_000_000, 5_000)]), 450_000))]
+    rk = [pd.Series(rkeys)]
+    lok = rng.random(450_000) > 0.02
+    rok = rng.random(20_000) > 0.02
+    calls = []
+    real = X._unique_right_join_device
+    monkeypatch.setattr(X, "_unique_right_join_device", lambda *a: calls.append(1) or real(*a))
+    monkeypatch.setattr(X, "_DEVICE_JOIN_MIN", 1 << 62)
+    host = X._numeric_key_join(lk, rk, lok, rok)
+    monkeypatch.setattr(X, "_DEVICE_JOIN_MIN", 1)
+    dev = X._numeric_key_join(lk, rk, lok, rok)
+    assert calls and np.array_equal(host[0], dev[0]) and np.array_equal(host[1], dev[1])

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--query", action="append", default=[])
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--sort", default="tottime", help="pstats order: tottime | cumulative")
     a = ap.parse_args()
     import torch
 
@@ -40,7 +41,7 @@ def main():
             df.run()
         pr.disable()
         print(f"== {name}: {(time.perf_counter() - t0) / a.reps * 1e3:.2f} ms per run (profiled)", flush=True)
-        pstats.Stats(pr).sort_stats("tottime").print_stats(a.top)
+        pstats.Stats(pr).sort_stats(a.sort).print_stats(a.top)
 
 
 if __name__ == "__main__":
