@@ -1383,10 +1383,11 @@ class PreparedTheta:
         # a 7-group SF10 query were 0.44 ms a pass); coarser bins only add candidates below the bound
         # (the filter keeps target + one bin's records).  Many groups: per-workgroup LDS [G][2^bits]
         # within 64 KiB when G allows, else 12 bits in global memory.
-        if self.G <= THETA_HIST_BINS // 16:
-            self.bits = int(math.floor(math.log2(THETA_HIST_BINS // self.G)))
+        gt = self.G * min(4, self.nt)  # (up to 4 sketches share one histogram pass: rows t * G + g)
+        if gt <= THETA_HIST_BINS // 16:
+            self.bits = int(math.floor(math.log2(THETA_HIST_BINS // gt)))
         else:
-            fit = int(math.floor(math.log2(max(1, (64 * 1024 // 4) // self.G))))
+            fit = int(math.floor(math.log2(max(1, (64 * 1024 // 4) // gt))))
             self.bits = fit if fit >= 8 else 12
         self.bits = max(4, min(16, self.bits))
         # first-attempt target per aggregator, in multiples of 2k records: learnt from the previous
@@ -1412,42 +1413,57 @@ class PreparedTheta:
             nat.module_launch(self.jit.handle, desc.data_ptr(), int(self.grid), BLOCK, int(self.jit.lay.total), st)
             G, dev = self.G, self.dev
             # (host-side targets and capacities: the only syncs are the candidate count with the
-            # largest bound after each filter pass, and the short-group check)
+            # largest bound after each filter pass, and the short-group check).  Up to 4 sketches
+            # are selected together: one histogram and one filter pass over the records, candidate
+            # groups t * G + g
             cap_all = max(1, self.nch * D.CHUNK_ROWS)
-            hist = torch.empty(G << self.bits, dtype=torch.int32, device=dev)
-            bound = torch.empty(G, dtype=torch.int64, device=dev)
-            count = torch.zeros(1, dtype=torch.int64, device=dev)
-            for t, k in enumerate(sizes):
-                mult = self._mult.get(t, 1)
-                tgt = np.full(G, 2 * k * mult, dtype=np.int64)
+            out = [None] * len(sizes)
+            for t0 in range(0, len(sizes), 4):
+                ks = sizes[t0:t0 + 4]
+                nt = len(ks)
+                GT = G * nt
+                hist = torch.empty(GT << self.bits, dtype=torch.int32, device=dev)
+                bound = torch.empty(GT, dtype=torch.int64, device=dev)
+                count = torch.zeros(1, dtype=torch.int64, device=dev)
+                kk = np.repeat(np.asarray(ks, dtype=np.int64), G)  # k per row t * G + g
+                mult = np.repeat(np.asarray([self._mult.get(t0 + j, 1) for j in range(nt)], dtype=np.int64), G)
+                tgt = 2 * kk * mult
                 for attempt in range(7):
                     if attempt == 6:  # (never in practice after six 4x rounds): every pair
-                        tgt = np.full(G, 1 << 62, dtype=np.int64)
+                        tgt = np.full(GT, 1 << 62, dtype=np.int64)
                     target = torch.from_numpy(tgt).to(dev)
-                    cap = max(1, min(cap_all, int(np.minimum(tgt, 1 << 40).sum()) * 2 + (1 << 16)))
+                    cap = max(1, min(cap_all * nt, int(np.minimum(tgt, 1 << 40).sum()) * 2 + (1 << 16)))
                     while True:
                         og = torch.empty(cap, dtype=torch.int64, device=dev)
                         oh = torch.empty(cap, dtype=torch.int64, device=dev)
-                        nat.theta_select_regions(slab.recs1.data_ptr(), self.rw, 1 + 2 * t, self.seg_lo.data_ptr(),
+                        nat.theta_select_regions(slab.recs1.data_ptr(), self.rw, 1 + 2 * t0, self.seg_lo.data_ptr(),
                                                  pend.data_ptr(), self.nch, G, self.bits, hist.data_ptr(),
                                                  target.data_ptr(), bound.data_ptr(), og.data_ptr(), oh.data_ptr(),
-                                                 count.data_ptr(), cap, st)
+                                                 count.data_ptr(), cap, st, nt)
                         c, hmax = (int(v) for v in torch.stack([count[0], bound.max()]).tolist())
                         if c <= cap:
                             break
                         cap = c  # a duplicate-heavy bin held more candidates than the first guess
                     # (candidates are below their group's bound: one sort of g << s | h when they fit)
-                    pairs = _sorted_unique_pairs(og[:c], oh[:c], G, hmax)
-                    distinct = torch.bincount(pairs[:, 0], minlength=G) if pairs.numel() else \
-                        torch.zeros(G, dtype=torch.int64, device=dev)
-                    short = ((distinct < k) & (bound < (1 << 62))).cpu().numpy()
+                    pairs = _sorted_unique_pairs(og[:c], oh[:c], GT, hmax)
+                    distinct = torch.bincount(pairs[:, 0], minlength=GT) if pairs.numel() else \
+                        torch.zeros(GT, dtype=torch.int64, device=dev)
+                    short = ((distinct < torch.from_numpy(kk).to(dev)) & (bound < (1 << 62))).cpu().numpy()
                     if not short.any():
                         break
                     tgt = np.where(short, tgt * 4, tgt)
-                    mult = min(mult * 4, 1 << 12)
-                self._mult[t] = mult
-                self.attempts[t] = attempt + 1
-                out.append(_kmv(pairs, k))
+                    mult = np.where(short, np.minimum(mult * 4, 1 << 12), mult)
+                # split the candidate rows t * G + g back into per-sketch (g, h) pairs (sorted by row)
+                starts = torch.searchsorted(pairs[:, 0].contiguous(),
+                                            torch.arange(nt + 1, device=dev, dtype=torch.int64) * G).tolist() \
+                    if pairs.numel() else [0] * (nt + 1)
+                for j in range(nt):
+                    pj = pairs[starts[j]:starts[j + 1]]
+                    if pj.numel():
+                        pj = torch.stack([pj[:, 0] - j * G, pj[:, 1]], dim=1)
+                    self._mult[t0 + j] = int(mult[j * G:(j + 1) * G].max())
+                    self.attempts[t0 + j] = attempt + 1
+                    out[t0 + j] = _kmv(pj, ks[j])
         finally:
             PART_POOL.release(slab)
         return out

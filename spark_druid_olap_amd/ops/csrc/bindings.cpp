@@ -76,10 +76,11 @@ __global__ void part_agg_kernel(const uint32_t* recs, int RW, const uint32_t* ba
                                 unsigned long long* out_count, int64_t cap);
 __global__ void theta_hist_regions_kernel(const uint32_t* recs, int rw, int hoff, const uint32_t* seg_lo,
                                           const uint32_t* seg_hi, int64_t nseg, int G, int bits, uint32_t* hist,
-                                          int use_lds);
+                                          int use_lds, int nt);
 __global__ void theta_filter_regions_kernel(const uint32_t* recs, int rw, int hoff, const uint32_t* seg_lo,
                                             const uint32_t* seg_hi, int64_t nseg, int G, const int64_t* bound,
-                                            int64_t* out_g, int64_t* out_h, unsigned long long* count, int64_t cap);
+                                            int64_t* out_g, int64_t* out_h, unsigned long long* count, int64_t cap,
+                                            int nt);
 __global__ void theta_hist_kernel(const int64_t* g, const int64_t* h, int64_t n, int bits, uint32_t* hist);
 __global__ void theta_thresh_kernel(const uint32_t* hist, int bits, const int64_t* target, int64_t* bound);
 __global__ void theta_filter_kernel(const int64_t* g, const int64_t* h, int64_t n, const int64_t* bound,
@@ -716,18 +717,22 @@ static void theta_select(uint64_t g, uint64_t h, int64_t n, int64_t G, int bits,
 }
 
 // The same select over a theta producer's chunk-region records (sketch.hip theta_*_regions):
-// record = u32 group key, then 2 words of 62-bit hash per theta at word `hoff`.  The histogram is
-// per-workgroup LDS when [G][2^bits] u32 fits 64 KiB (the host sizes bits for it), else global.
+// record = u32 group key, then 2 words of 62-bit hash per theta from word `hoff`.  `nt` sketches
+// (<= 4) are selected in ONE histogram and ONE filter pass over the records: rows t * G + g of the
+// histogram / target / bound arrays, candidates written as group t * G + g.  The histogram is
+// per-workgroup LDS when [nt G][2^bits] u32 fits 64 KiB (the host sizes bits for it), else global.
 static void theta_select_regions(uint64_t recs, int rw, int hoff, uint64_t seg_lo, uint64_t seg_hi, int64_t nseg,
                                  int64_t G, int bits, uint64_t hist, uint64_t target, uint64_t bound, uint64_t out_g,
-                                 uint64_t out_h, uint64_t count, int64_t cap, uint64_t stream) {
+                                 uint64_t out_h, uint64_t count, int64_t cap, uint64_t stream, int nt) {
   if (bits < 4 || bits > 16) throw std::invalid_argument("theta_select_regions: 4..16 histogram bits");
   if (G <= 0 || G > (1 << 20)) throw std::invalid_argument("theta_select_regions: 1..2^20 groups");
-  if (rw < 3 || hoff < 1 || hoff + 2 > rw) throw std::invalid_argument("theta_select_regions: record layout");
+  if (nt < 1 || nt > 4) throw std::invalid_argument("theta_select_regions: 1..4 sketches per pass");
+  if (rw < 3 || hoff < 1 || hoff + 2 * nt > rw) throw std::invalid_argument("theta_select_regions: record layout");
   hipStream_t s = (hipStream_t)stream;
-  check(hipMemsetAsync((void*)hist, 0, (size_t)G << bits << 2, s), "theta hist clear");
+  const int64_t GT = G * nt;
+  check(hipMemsetAsync((void*)hist, 0, (size_t)GT << bits << 2, s), "theta hist clear");
   check(hipMemsetAsync((void*)count, 0, 8, s), "theta count clear");
-  const int64_t lds = (int64_t)(G << bits) * 4;
+  const int64_t lds = (int64_t)(GT << bits) * 4;
   const int use_lds = lds <= 64 * 1024 ? 1 : 0;
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(nseg, 4096));
   // (the histogram's workgroups each flush their LDS bins with global atomics onto the same
@@ -736,16 +741,16 @@ static void theta_select_regions(uint64_t recs, int rw, int hoff, uint64_t seg_l
   if (nseg > 0) {
     hipLaunchKernelGGL(sdo::theta_hist_regions_kernel, dim3(hgrid), dim3(256), use_lds ? (size_t)lds : 0, s,
                        (const uint32_t*)recs, rw, hoff, (const uint32_t*)seg_lo, (const uint32_t*)seg_hi, nseg, (int)G,
-                       bits, (uint32_t*)hist, use_lds);
+                       bits, (uint32_t*)hist, use_lds, nt);
     check(hipGetLastError(), "theta_hist_regions_kernel launch");
   }
-  hipLaunchKernelGGL(sdo::theta_thresh_kernel, dim3((unsigned)G), dim3(1024), 0, s, (const uint32_t*)hist, bits,
+  hipLaunchKernelGGL(sdo::theta_thresh_kernel, dim3((unsigned)GT), dim3(1024), 0, s, (const uint32_t*)hist, bits,
                      (const int64_t*)target, (int64_t*)bound);
   check(hipGetLastError(), "theta_thresh_kernel launch");
   if (nseg > 0) {
     hipLaunchKernelGGL(sdo::theta_filter_regions_kernel, dim3(grid), dim3(256), 0, s, (const uint32_t*)recs, rw, hoff,
                        (const uint32_t*)seg_lo, (const uint32_t*)seg_hi, nseg, (int)G, (const int64_t*)bound,
-                       (int64_t*)out_g, (int64_t*)out_h, (unsigned long long*)count, cap);
+                       (int64_t*)out_g, (int64_t*)out_h, (unsigned long long*)count, cap, nt);
     check(hipGetLastError(), "theta_filter_regions_kernel launch");
   }
 }

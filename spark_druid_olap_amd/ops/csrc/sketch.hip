@@ -174,9 +174,10 @@ __global__ void __launch_bounds__(256) theta_hist_regions_kernel(const uint32_t*
                                                                 const uint32_t* __restrict__ seg_lo,
                                                                 const uint32_t* __restrict__ seg_hi, int64_t nseg,
                                                                 int G, int bits, uint32_t* __restrict__ hist,
-                                                                int use_lds) {
+                                                                int use_lds, int nt) {
+  // nt sketches per record (hash t at words hoff + 2t): histogram rows t * G + g
   extern __shared__ uint32_t lh[];
-  const int64_t nb = (int64_t)G << bits;
+  const int64_t nb = ((int64_t)G * nt) << bits;
   const int shift = 62 - bits;
   if (use_lds) {
     for (int64_t i = threadIdx.x; i < nb; i += blockDim.x) lh[i] = 0u;
@@ -186,25 +187,27 @@ __global__ void __launch_bounds__(256) theta_hist_regions_kernel(const uint32_t*
   for (int64_t sgi = blockIdx.x; sgi < nseg; sgi += gridDim.x) {
     const uint32_t lo = seg_lo[sgi], hi = seg_hi[sgi];
     for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += R * blockDim.x) {
-      uint32_t g[R];
-      uint64_t h[R];
+      for (int t = 0; t < nt; ++t) {
+        uint32_t g[R];
+        uint64_t h[R];
 #pragma unroll
-      for (int u = 0; u < R; ++u) {
-        const uint32_t i = i0 + u * blockDim.x;
-        g[u] = 0xffffffffu;
-        h[u] = 0;
-        if (i < hi) {
-          const uint32_t* r = recs + (uint64_t)i * rw;
-          g[u] = r[0];
-          h[u] = (uint64_t)r[hoff] | ((uint64_t)r[hoff + 1] << 32);
+        for (int u = 0; u < R; ++u) {
+          const uint32_t i = i0 + u * blockDim.x;
+          g[u] = 0xffffffffu;
+          h[u] = 0;
+          if (i < hi) {
+            const uint32_t* r = recs + (uint64_t)i * rw;
+            g[u] = r[0];
+            h[u] = (uint64_t)r[hoff + 2 * t] | ((uint64_t)r[hoff + 2 * t + 1] << 32);
+          }
         }
-      }
 #pragma unroll
-      for (int u = 0; u < R; ++u) {
-        if (g[u] >= (uint32_t)G) continue;  // (past the region's end; never fault)
-        const int64_t idx = ((int64_t)g[u] << bits) + (int64_t)(h[u] >> shift);
-        if (use_lds) atomicAdd(&lh[idx], 1u);
-        else atomicAdd(&hist[idx], 1u);
+        for (int u = 0; u < R; ++u) {
+          if (g[u] >= (uint32_t)G) continue;  // (past the region's end; never fault)
+          const int64_t idx = (((int64_t)t * G + g[u]) << bits) + (int64_t)(h[u] >> shift);
+          if (use_lds) atomicAdd(&lh[idx], 1u);
+          else atomicAdd(&hist[idx], 1u);
+        }
       }
     }
   }
@@ -224,7 +227,10 @@ __global__ void __launch_bounds__(256) theta_filter_regions_kernel(const uint32_
                                                                   const uint32_t* __restrict__ seg_hi, int64_t nseg,
                                                                   int G, const int64_t* __restrict__ bound,
                                                                   int64_t* __restrict__ out_g, int64_t* __restrict__ out_h,
-                                                                  unsigned long long* __restrict__ count, int64_t cap) {
+                                                                  unsigned long long* __restrict__ count, int64_t cap,
+                                                                  int nt) {
+  // nt <= 4 sketches per record: bit j * nt + t of `bits` = record j passes sketch t's bound
+  // (bound[t * G + g]); its candidate is written as group t * G + g
   __shared__ uint32_t wsum[4];
   __shared__ unsigned long long s_base;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -233,13 +239,17 @@ __global__ void __launch_bounds__(256) theta_filter_regions_kernel(const uint32_
     if (hi <= lo) continue;  // (uniform: every thread reads the same region bounds)
     uint64_t bits = 0;
     uint32_t mine = 0;
-    for (uint32_t j = 0, i = lo + threadIdx.x; i < hi && j < 64; ++j, i += blockDim.x) {
+    const int per = 64 / nt;  // records per thread the bit set can hold (a region: <= 16)
+    for (uint32_t j = 0, i = lo + threadIdx.x; i < hi && j < (uint32_t)per; ++j, i += blockDim.x) {
       const uint32_t* r = recs + (uint64_t)i * rw;
       const uint32_t g = r[0];
-      const uint64_t h = (uint64_t)r[hoff] | ((uint64_t)r[hoff + 1] << 32);
-      if (g < (uint32_t)G && (int64_t)h < bound[g]) {
-        bits |= 1ull << j;
-        ++mine;
+      if (g >= (uint32_t)G) continue;
+      for (int t = 0; t < nt; ++t) {
+        const uint64_t h = (uint64_t)r[hoff + 2 * t] | ((uint64_t)r[hoff + 2 * t + 1] << 32);
+        if ((int64_t)h < bound[(int64_t)t * G + g]) {
+          bits |= 1ull << (j * nt + t);
+          ++mine;
+        }
       }
     }
     // block exclusive scan of the per-thread counts
@@ -259,14 +269,16 @@ __global__ void __launch_bounds__(256) theta_filter_regions_kernel(const uint32_
     if (threadIdx.x == 0) s_base = tot ? atomicAdd(count, (unsigned long long)tot) : 0ull;
     __syncthreads();
     unsigned long long pos = s_base + pre;
-    for (uint32_t j = 0, i = lo + threadIdx.x; j < 64 && (bits >> j); ++j, i += blockDim.x) {
-      if (!((bits >> j) & 1ull)) continue;
+    for (uint32_t j = 0, i = lo + threadIdx.x; j < (uint32_t)per && (bits >> (j * nt)); ++j, i += blockDim.x) {
       const uint32_t* r = recs + (uint64_t)i * rw;
-      if ((int64_t)pos < cap) {
-        out_g[pos] = (int64_t)r[0];
-        out_h[pos] = (int64_t)((uint64_t)r[hoff] | ((uint64_t)r[hoff + 1] << 32));
+      for (int t = 0; t < nt; ++t) {
+        if (!((bits >> (j * nt + t)) & 1ull)) continue;
+        if ((int64_t)pos < cap) {
+          out_g[pos] = (int64_t)t * G + (int64_t)r[0];
+          out_h[pos] = (int64_t)((uint64_t)r[hoff + 2 * t] | ((uint64_t)r[hoff + 2 * t + 1] << 32));
+        }
+        ++pos;
       }
-      ++pos;
     }
     __syncthreads();  // (wsum / s_base are rewritten for the next region)
   }
