@@ -1396,9 +1396,12 @@ class PreparedTheta:
         self._mult = {}
         self.attempts = {}  # (per aggregator: select passes of the last run)
 
-    def select(self, sizes: List[int]) -> List[torch.Tensor]:
+    def select(self, sizes: List[int], estimates: bool = False) -> list:
         """Per theta aggregator (``sizes``: its k) the sorted unique (group, hash) pairs of its k
-        smallest distinct hashes per group."""
+        smallest distinct hashes per group -- or, with ``estimates`` (one rank: no union across
+        ranks follows), the per-group theta estimates [G] as host float64 arrays, computed from the
+        candidates directly: (k-1) / (h_k / 2^62), or the exact distinct count below k hashes
+        (the same values engine/executor.py _kmv_estimates gives for the k-trimmed pairs)."""
         from .executor import _kmv, _sorted_unique_pairs
 
         nat, st = native.load(), native._stream(self.dev)
@@ -1453,6 +1456,22 @@ class PreparedTheta:
                         break
                     tgt = np.where(short, tgt * 4, tgt)
                     mult = np.where(short, np.minimum(mult * 4, 1 << 12), mult)
+                if estimates:
+                    kt = torch.from_numpy(kk).to(dev)
+                    first = torch.cumsum(distinct, 0) - distinct
+                    kth_i = (first + torch.minimum(kt, distinct) - 1).clamp_(min=0)
+                    kth = pairs[:, 1].index_select(0, kth_i.clamp_(max=max(0, pairs.shape[0] - 1))).to(torch.float64) \
+                        if pairs.numel() else torch.zeros(GT, dtype=torch.float64, device=dev)
+                    # (the same float expression, scalar k over the tensor, as _kmv_estimates: equal bits)
+                    est = torch.cat([torch.where(distinct[j * G:(j + 1) * G] < ks[j],
+                                                 distinct[j * G:(j + 1) * G].to(torch.float64),
+                                                 (ks[j] - 1) / (kth[j * G:(j + 1) * G] / float(1 << 62)))
+                                     for j in range(nt)]).cpu().numpy()
+                    for j in range(nt):
+                        self._mult[t0 + j] = int(mult[j * G:(j + 1) * G].max())
+                        self.attempts[t0 + j] = attempt + 1
+                        out[t0 + j] = est[j * G:(j + 1) * G]
+                    continue
                 # split the candidate rows t * G + g back into per-sketch (g, h) pairs (sorted by row)
                 starts = torch.searchsorted(pairs[:, 0].contiguous(),
                                             torch.arange(nt + 1, device=dev, dtype=torch.int64) * G).tolist() \

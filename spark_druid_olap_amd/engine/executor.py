@@ -950,10 +950,15 @@ class PreparedQuery:
         ds = self.ds
         dev = ds.device
         gid_order = np.asarray(cols["__gid__"], dtype=np.int64)
-        fused = self._theta_fused(prog)
+        local = not self.world.distributed
+        fused = self._theta_fused(prog, estimates=local)
         if fused is not None:
-            for (name, _, size), pairs in zip(prog.thetas, fused):
-                cols[name] = _kmv_estimates(self._theta_union(pairs, size), size, gid_order)
+            for (name, _, size), res in zip(prog.thetas, fused):
+                if local:  # one rank: the per-group estimates came back from the select itself
+                    ok = (gid_order >= 0) & (gid_order < len(res))
+                    cols[name] = np.where(ok, res[np.clip(gid_order, 0, max(0, len(res) - 1))], 0.0)
+                else:
+                    cols[name] = _kmv_estimates(self._theta_union(res, size), size, gid_order)
             return
         keys = rows = None
         if not prog.empty and dev.type == "cuda" and self.engine.use_native:
@@ -989,7 +994,7 @@ class PreparedQuery:
             pairs = kmv_select(g, h, size, G)
             cols[name] = _kmv_estimates(self._theta_union(pairs, size), size, gid_order)
 
-    def _theta_fused(self, prog: ScanProgram) -> Optional[List[torch.Tensor]]:
+    def _theta_fused(self, prog: ScanProgram, estimates: bool = False) -> Optional[list]:
         """Per theta aggregator its KMV pairs from the fused producer (engine/device_exec.py
         PreparedTheta), or None where it does not apply (CPU, stored sketches, float columns, wide
         key spaces, an empty shard): the (key, row) emit path then runs.  The choice is per shard
@@ -1007,7 +1012,7 @@ class PreparedQuery:
             self._theta_prep = th
         if th is False:
             return None
-        return th.select([size for _, _, size in prog.thetas])
+        return th.select([size for _, _, size in prog.thetas], estimates=estimates)
 
     def _theta_union(self, pairs: torch.Tensor, size: int) -> torch.Tensor:
         """Across ranks: every rank's k candidates per group travel to the root only when the answer
