@@ -1395,6 +1395,7 @@ class PreparedTheta:
         # than 2k below the bound for k distinct hashes; a repeated statement then selects in one pass)
         self._mult = {}
         self.attempts = {}  # (per aggregator: select passes of the last run)
+        self._bounds = {}  # first sketch of a select group -> its last run's per-row bounds (device)
 
     def select(self, sizes: List[int], estimates: bool = False) -> list:
         """Per theta aggregator (``sizes``: its k) the sorted unique (group, hash) pairs of its k
@@ -1431,7 +1432,13 @@ class PreparedTheta:
                 kk = np.repeat(np.asarray(ks, dtype=np.int64), G)  # k per row t * G + g
                 mult = np.repeat(np.asarray([self._mult.get(t0 + j, 1) for j in range(nt)], dtype=np.int64), G)
                 tgt = 2 * kk * mult
+                cached = self._bounds.get(t0)
                 for attempt in range(7):
+                    # a repeated statement first filters with its last run's bounds (same rows, same
+                    # candidates: no histogram pass); a short group falls back to the histogram
+                    reuse = attempt == 0 and cached is not None
+                    if reuse:
+                        bound.copy_(torch.from_numpy(cached))
                     if attempt == 6:  # (never in practice after six 4x rounds): every pair
                         tgt = np.full(GT, 1 << 62, dtype=np.int64)
                     target = torch.from_numpy(tgt).to(dev)
@@ -1442,8 +1449,11 @@ class PreparedTheta:
                         nat.theta_select_regions(slab.recs1.data_ptr(), self.rw, 1 + 2 * t0, self.seg_lo.data_ptr(),
                                                  pend.data_ptr(), self.nch, G, self.bits, hist.data_ptr(),
                                                  target.data_ptr(), bound.data_ptr(), og.data_ptr(), oh.data_ptr(),
-                                                 count.data_ptr(), cap, st, nt)
-                        c, hmax = (int(v) for v in torch.stack([count[0], bound.max()]).tolist())
+                                                 count.data_ptr(), cap, st, nt, 1 if reuse else 0)
+                        # (one copy: the candidate count, the largest bound, the bounds themselves --
+                        # kept on the host for the next run, so no device tensor crosses streams)
+                        vals = torch.cat([count.view(1), bound.max().view(1), bound]).cpu().numpy()
+                        c, hmax = int(vals[0]), int(vals[1])
                         if c <= cap:
                             break
                         cap = c  # a duplicate-heavy bin held more candidates than the first guess
@@ -1454,8 +1464,11 @@ class PreparedTheta:
                     short = ((distinct < torch.from_numpy(kk).to(dev)) & (bound < (1 << 62))).cpu().numpy()
                     if not short.any():
                         break
+                    if reuse:
+                        continue  # (the histogram path with this run's targets)
                     tgt = np.where(short, tgt * 4, tgt)
                     mult = np.where(short, np.minimum(mult * 4, 1 << 12), mult)
+                self._bounds[t0] = vals[2:].copy()
                 if estimates:
                     kt = torch.from_numpy(kk).to(dev)
                     first = torch.cumsum(distinct, 0) - distinct

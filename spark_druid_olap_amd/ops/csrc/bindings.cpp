@@ -723,14 +723,16 @@ static void theta_select(uint64_t g, uint64_t h, int64_t n, int64_t G, int bits,
 // per-workgroup LDS when [nt G][2^bits] u32 fits 64 KiB (the host sizes bits for it), else global.
 static void theta_select_regions(uint64_t recs, int rw, int hoff, uint64_t seg_lo, uint64_t seg_hi, int64_t nseg,
                                  int64_t G, int bits, uint64_t hist, uint64_t target, uint64_t bound, uint64_t out_g,
-                                 uint64_t out_h, uint64_t count, int64_t cap, uint64_t stream, int nt) {
+                                 uint64_t out_h, uint64_t count, int64_t cap, uint64_t stream, int nt,
+                                 int reuse_bound) {
+  // reuse_bound: `bound` already holds the rows' bounds (a repeated statement's last ones): filter only
   if (bits < 4 || bits > 16) throw std::invalid_argument("theta_select_regions: 4..16 histogram bits");
   if (G <= 0 || G > (1 << 20)) throw std::invalid_argument("theta_select_regions: 1..2^20 groups");
   if (nt < 1 || nt > 4) throw std::invalid_argument("theta_select_regions: 1..4 sketches per pass");
   if (rw < 3 || hoff < 1 || hoff + 2 * nt > rw) throw std::invalid_argument("theta_select_regions: record layout");
   hipStream_t s = (hipStream_t)stream;
   const int64_t GT = G * nt;
-  check(hipMemsetAsync((void*)hist, 0, (size_t)GT << bits << 2, s), "theta hist clear");
+  if (!reuse_bound) check(hipMemsetAsync((void*)hist, 0, (size_t)GT << bits << 2, s), "theta hist clear");
   check(hipMemsetAsync((void*)count, 0, 8, s), "theta count clear");
   const int64_t lds = (int64_t)(GT << bits) * 4;
   const int use_lds = lds <= 64 * 1024 ? 1 : 0;
@@ -738,15 +740,17 @@ static void theta_select_regions(uint64_t recs, int rw, int hoff, uint64_t seg_l
   // (the histogram's workgroups each flush their LDS bins with global atomics onto the same
   // addresses: fewer, longer-running workgroups for it)
   const unsigned hgrid = use_lds ? (unsigned)std::max<int64_t>(1, std::min<int64_t>(nseg, 1024)) : grid;
-  if (nseg > 0) {
+  if (nseg > 0 && !reuse_bound) {
     hipLaunchKernelGGL(sdo::theta_hist_regions_kernel, dim3(hgrid), dim3(256), use_lds ? (size_t)lds : 0, s,
                        (const uint32_t*)recs, rw, hoff, (const uint32_t*)seg_lo, (const uint32_t*)seg_hi, nseg, (int)G,
                        bits, (uint32_t*)hist, use_lds, nt);
     check(hipGetLastError(), "theta_hist_regions_kernel launch");
   }
-  hipLaunchKernelGGL(sdo::theta_thresh_kernel, dim3((unsigned)GT), dim3(1024), 0, s, (const uint32_t*)hist, bits,
-                     (const int64_t*)target, (int64_t*)bound);
-  check(hipGetLastError(), "theta_thresh_kernel launch");
+  if (!reuse_bound) {
+    hipLaunchKernelGGL(sdo::theta_thresh_kernel, dim3((unsigned)GT), dim3(1024), 0, s, (const uint32_t*)hist, bits,
+                       (const int64_t*)target, (int64_t*)bound);
+    check(hipGetLastError(), "theta_thresh_kernel launch");
+  }
   if (nseg > 0) {
     hipLaunchKernelGGL(sdo::theta_filter_regions_kernel, dim3(grid), dim3(256), 0, s, (const uint32_t*)recs, rw, hoff,
                        (const uint32_t*)seg_lo, (const uint32_t*)seg_hi, nseg, (int)G, (const int64_t*)bound,
