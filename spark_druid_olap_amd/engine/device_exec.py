@@ -1055,7 +1055,7 @@ def release_device_memory(keep=None, keep_arena=None) -> None:
     count_event("device_memory_release")
     for ar in list(_ARENAS.values()):
         if ar is not keep_arena and ar.slot != (keep[1] if keep else None):
-            ar.release()
+            ar.release(blocking=False)
     victims = []
     with _buf_lock:
         for k in list(_buf_lru):
@@ -1189,9 +1189,17 @@ class SlotArena:
         t = buf[off:off + nb].view(dtype)
         return t.view(shape) if shape is not None else t
 
-    def release(self) -> None:
-        with self.lock:
+    def release(self, blocking: bool = True) -> bool:
+        """Drop the storage; ``blocking=False`` skips an arena whose lock is held (an out-of-memory
+        release from another slot: that slot may itself be carving -- growing under its lock -- and
+        waiting on this thread's arena in its own release, a lock-order deadlock)."""
+        if not self.lock.acquire(blocking=blocking):
+            return False
+        try:
             self._drop()
+        finally:
+            self.lock.release()
+        return True
 
     def _drop(self) -> None:
         """Forget the storage: scans holding views re-carve at their next run (running statements

@@ -177,7 +177,10 @@ def run(prog, key_col: str, dep_cols, world=None) -> Optional[Partials]:
     cache = prog.__dict__.setdefault("_dict_exist_filter", {})
     f = cache.get((key_col, n))
     if f is None:
-        f = cache[(key_col, n)] = _eval(prog.bexpr, key_col, fds, n, occ.device)
+        from ..utils.streams import publish
+
+        # (the prepared program is shared by concurrent statements on other slots' streams)
+        f = cache[(key_col, n)] = publish(_eval(prog.bexpr, key_col, fds, n, occ.device), occ.device)
     sel = occ & f
     if sel.is_cuda:
         from ..ops import native

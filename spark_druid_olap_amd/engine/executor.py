@@ -42,9 +42,10 @@ PIPELINE_MERGE = os.environ.get("SDO_PIPELINE_MERGE", "1") not in ("0", "")
 # Small states are never split: their merge is latency-bound, every batch would pay it again and
 # the last one stays exposed anyway.
 AUTO_PIPELINE = os.environ.get("SDO_AUTO_PIPELINE", "1") not in ("0", "")
-# (a merge this size takes ~0.1 ms over RCCL on 8 GPUs: less would not pay for the extra batches)
+# (below this a merge is latency-bound: never split, whatever the price)
 AUTO_PIPELINE_MIN_BYTES = int(os.environ.get("SDO_AUTO_PIPELINE_MIN_BYTES", str(4 << 20)))
-AUTO_PIPELINE_BATCHES = int(os.environ.get("SDO_AUTO_PIPELINE_BATCHES", "3"))
+AUTO_PIPELINE_BATCHES = 3   # (at most: planner/cost.py plan_pipeline prices 2..3)
+AUTO_PIPELINE_FORCE = False  # (tests: split whatever the price)
 # existence-only group-bys over the key's dictionary domain (engine/dict_exist.py)
 DICT_EXIST = os.environ.get("SDO_DICT_EXIST", "1") not in ("0", "")
 # thetaSketch aggregators fused into one producer scan with an in-place radix select
@@ -264,6 +265,18 @@ class PreparedQuery:
         nbytes = G * max(1, prog.nslots) * 8 + prog.nhll_total * G * (1 << prog.hll_p)
         if nbytes < AUTO_PIPELINE_MIN_BYTES:
             return None
+        # priced (planner/cost.py plan_pipeline): only where the hidden merge outweighs the extra
+        # batches' table passes -- never over host-staged (gloo) collectives
+        from ..planner.cost import plan_pipeline
+        from .lower import column_tensor
+
+        rows = sum(max(0, hi - lo) for lo, hi in prog.ranges)
+        row_bytes = sum(column_tensor(ds, c).element_size() for c in prog.cols)
+        nb = plan_pipeline(nbytes, rows * row_bytes, self.world.size, self.world.backend == "gloo",
+                           AUTO_PIPELINE_BATCHES)
+        if nb <= 1 and not AUTO_PIPELINE_FORCE:
+            return None
+        nb = max(nb, AUTO_PIPELINE_BATCHES if AUTO_PIPELINE_FORCE else nb)
         probe = self._prepare(prog)
         # dense table scans only: a batch of a partitioned scan repeats its whole split pipeline (a
         # 2-rank rehearsal of day x ship mode at SF10: 3 partitioned batches 4.3 ms against one scan
@@ -272,7 +285,7 @@ class PreparedQuery:
         if -self.world.max_float(-float(dense)) < 1.0:  # (min over ranks)
             return None
         nseg = sum(1 for sg in ds.segments if any(min(hi, sg.row_hi) > max(lo, sg.row_lo) for lo, hi in prog.ranges))
-        return max(1, -(-nseg // AUTO_PIPELINE_BATCHES))
+        return max(1, -(-nseg // nb))
 
     def _prepare(self, prog: ScanProgram):
         if is_cuda_ds(self.ds) and self.engine.use_native:
@@ -867,7 +880,13 @@ class PreparedQuery:
             v = torch.where(col >= 0, col, col ^ 0x7FFFFFFFFFFFFFFF).view(torch.float64)
         else:
             v = col.to(torch.float64)
-        if part.rows and bool(torch.isnan(v).any()):
+        nan = torch.isnan(v).any().to(torch.float64).reshape(1) if part.rows else \
+            torch.zeros(1, dtype=torch.float64, device=dev)
+        if part.scattered and self.world.distributed:
+            # per-rank disjoint slices see different values: every rank must take the same branch
+            # before the extremes' all-reduce below (one NaN anywhere leaves it to the host)
+            nan = self.world.all_reduce(nan, "max")
+        if bool(nan.item()):
             return part
         # extremes over the order-preserving int64 image of the f64 values: a native integer atomic
         # per group instead of a float compare-and-swap loop -- the BI MinCost template's five
@@ -1258,7 +1277,8 @@ def shard_id_range(ds: DataSource, col: str) -> tuple:
 def shard_window(prog: ScanProgram, ds: DataSource, world: World) -> Optional[ShardWindow]:
     import copy
 
-    if world is None or not world.distributed or not ds.shard_key or prog.empty or prog.thetas:
+    # (everything up to the agreement below depends on the plan only -- identical on every rank)
+    if world is None or not world.distributed or not ds.shard_key or prog.thetas:
         return None
     if os.environ.get("SDO_NO_SHARD_WINDOW"):
         return None
@@ -1268,7 +1288,14 @@ def shard_window(prog: ScanProgram, ds: DataSource, world: World) -> Optional[Sh
         return None
     lo, hi = shard_id_range(ds, ds.shard_key)
     card = max(1, hi - lo + 1)
-    if card * ShardWindow.MIN_SAVING > prog.keys[idx].card:
+    # the window changes this rank's partials from the dense global table to rebased sparse groups,
+    # and the merge's collective pattern follows the partials' layout: every rank must window, or
+    # none.  A shard's own key range decides locally (4 range shards hold ~1/4 of the keys each,
+    # right at MIN_SAVING), so the ranks agree -- one small all-gather, in broadcast order at
+    # prepare time.  (A rank whose filter selects nothing still windows: its empty local table
+    # compacts to no groups.)
+    ok = card * ShardWindow.MIN_SAVING <= prog.keys[idx].card
+    if world.max_float(0.0 if ok else 1.0) != 0.0:
         return None
     keys = [copy.copy(kc) for kc in prog.keys]
     keys[idx].base, keys[idx].card = max(0, lo), card

@@ -1687,8 +1687,10 @@ def fd_metric_table(ds: DataSource, a: str, metric: str, world=None) -> Optional
     key = (a, "metric:" + metric)
     ds = getattr(ds, "fd_source", None) or ds  # streamed window: decide over the whole shard
     if key not in cache:
-        cache[key] = _fd_lut(ds.dims[a].ids, len(ds.dims[a].dictionary), column_tensor(ds, metric), ds.num_rows,
-                             world)
+        from ..utils.streams import publish
+
+        cache[key] = publish(_fd_lut(ds.dims[a].ids, len(ds.dims[a].dictionary), column_tensor(ds, metric),
+                                     ds.num_rows, world), ds.dims[a].ids.device)
     return cache[key]
 
 
@@ -1741,8 +1743,10 @@ def fd_table(ds: DataSource, a: str, b: str, world=None) -> Optional[torch.Tenso
         lut = hi
     # kept on the device (int32): finalize gathers the dependent ids of the result groups there --
     # a host gather into a 150M-entry table costs a cache miss per group
+    from ..utils.streams import publish
+
     out = lut.to(torch.int32) if bool(ok.item()) else None
-    cache[key] = out
+    cache[key] = publish(out, dev)
     if os.environ.get("SDO_TRACE_FD"):
         print(f"[fd] {a} -> {b}: {'yes' if out is not None else 'no'}", flush=True)
     return out
@@ -1767,7 +1771,9 @@ def rank_luts(ds: DataSource, a: str, b: str) -> Tuple[torch.Tensor, torch.Tenso
     dev = ds.dims[a].ids.device
     ta = torch.tensor([pos[v] if v is not None else math.nan for v in sa], dtype=torch.float64, device=dev)
     tb = torch.tensor([pos[v] if v is not None else math.nan for v in sb], dtype=torch.float64, device=dev)
-    cache[key] = (ta, tb)
+    from ..utils.streams import publish
+
+    cache[key] = publish((ta, tb), dev)
     return ta, tb
 
 

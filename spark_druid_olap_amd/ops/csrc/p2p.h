@@ -6,7 +6,7 @@ namespace sdo {
 
 constexpr int P2P_MAX_RANKS = 8;
 constexpr int P2P_MAX_SLOTS = 64;
-constexpr int64_t P2P_HEADER = 256;        // bytes: publish word, done word, 2 verdict words, padding
+constexpr int64_t P2P_HEADER = 256;        // bytes: publish, done, 2 verdict and 2 final words, padding
 constexpr int64_t P2P_STATUS_TIMEOUT = 3;  // a peer never finished the epoch (hard wait expired)
 constexpr int64_t P2P_STATUS_RETRY = 4;    // the epoch was abandoned by agreement: re-merge over RCCL
 

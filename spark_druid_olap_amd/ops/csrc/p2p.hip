@@ -17,14 +17,16 @@
 //      memory with system-scope loads (over xGMI across GPUs; through the same HBM when two ranks
 //      share a card);
 //   4. publishes its VERDICT for the epoch -- "I saw every peer's partial" or "I gave up" -- then
-//      its done word, and waits (HARD timeout) for every peer's verdict.
+//      its done word, and waits (HARD timeout) for every peer's verdict;
+//   5. publishes its FINAL word -- "aborted" when a hard wait expired -- and, if it did not abort,
+//      waits (HARD timeout) for every peer's final word: an aborted epoch is a TIMEOUT everywhere.
 //
 // Every rank reads the same N verdict words, so every rank reaches the same outcome: all succeed,
 // or -- when any rank's soft wait expired (a peer slow to arrive, or a coherence failure) -- all
 // report P2P_STATUS_RETRY and the host re-runs the merge over RCCL (parallel/p2p.py).  Only a
-// peer that never posts a verdict within the hard timeout (a dead process) becomes a failed
-// status word.  No host synchronisation on the fast path: the caller's result copy carries the
-// status words.  Every spin wait is bounded: no kernel that does not finish.
+// peer that never posts a verdict within the hard timeout (a dead process, or one later than the
+// hard deadline -- every rank then sees the aborted final word) becomes a failed status word.
+// No host synchronisation on the fast path: the caller's result copy carries the status words.  Every spin wait is bounded: no kernel that does not finish.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -44,7 +46,8 @@ __device__ __forceinline__ void p2p_release(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// header words: [0] published epoch, [1] done epoch, [2 + (e & 1)] verdict of epoch e = (e << 1) | gave_up
+// header words: [0] published epoch, [1] done epoch, [2 + (e & 1)] verdict of epoch e = (e << 1) | gave_up,
+// [4 + (e & 1)] final word of epoch e = (e << 1) | aborted (posted after the hard wait for the done words)
 __device__ __forceinline__ uint64_t* hdr(uint64_t base, int w) { return (uint64_t*)base + w; }
 
 __device__ __forceinline__ uint64_t* slot_ptr(const P2PArgs& a, int r, uint64_t epoch) {
@@ -63,6 +66,24 @@ __device__ unsigned wait_peers(const P2PArgs& a, int w, uint64_t want, int64_t t
     for (int r = 0; r < a.nranks; ++r) {
       if (ok & (1u << r)) continue;
       if (p2p_acquire(hdr(a.mbox[r], w)) >= want) ok |= 1u << r;
+    }
+    if (ok == all) break;
+    if ((int64_t)(wall_clock64() - t0) > ticks) break;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return ok;
+}
+
+// Bounded wait until every peer's final word of epoch e is posted (exactly epoch e: final words
+// alternate by parity, and a word from epoch e - 2 must not count).
+__device__ unsigned wait_fin(const P2PArgs& a, uint64_t e, int64_t ticks) {
+  unsigned ok = 0;
+  const uint64_t t0 = wall_clock64();
+  const unsigned all = all_mask(a.nranks);
+  while (ok != all) {
+    for (int r = 0; r < a.nranks; ++r) {
+      if (ok & (1u << r)) continue;
+      if ((p2p_acquire(hdr(a.mbox[r], 4 + (int)(e & 1))) >> 1) == e) ok |= 1u << r;
     }
     if (ok == all) break;
     if ((int64_t)(wall_clock64() - t0) > ticks) break;
@@ -95,14 +116,19 @@ __global__ void __launch_bounds__(1024) p2p_merge_kernel(P2PArgs a) {
   __syncthreads();
   const unsigned have = s_have;
   if (have == all) {
+    // every rank folds the N partials in rank order 0..N-1 (its own in its place): f64 sums are
+    // not associative, and ranks that summed in different orders could hold different bits for
+    // one group -- and then take different HAVING / prune decisions on them
     for (int64_t i = tid; i < a.nacc; i += blockDim.x) {
       const int op = a.ops[i % a.nslots];
-      int64_t v = a.acc_src[i];
-      double f = __longlong_as_double(v);
+      int64_t v = 0;
+      double f = 0.0;
       for (int r = 0; r < a.nranks; ++r) {
-        if (r == a.rank) continue;
-        const int64_t x = (int64_t)p2p_load(slot_ptr(a, r, e) + i);
-        if (op == 0) v += x;
+        const int64_t x = r == a.rank ? a.acc_src[i] : (int64_t)p2p_load(slot_ptr(a, r, e) + i);
+        if (r == 0) {
+          v = x;
+          f = __longlong_as_double(x);
+        } else if (op == 0) v += x;
         else if (op == 1) f += __longlong_as_double(x);
         else if (op == 2) v = x < v ? x : v;
         else v = x > v ? x : v;
@@ -139,7 +165,24 @@ __global__ void __launch_bounds__(1024) p2p_merge_kernel(P2PArgs a) {
       const uint64_t v = p2p_acquire(hdr(a.mbox[r], 2 + (int)(e & 1)));
       if ((v >> 1) != e || (v & 1)) gaveup |= 1u << r;
     }
-    s_done = done;
+    // 5. the final word: a rank whose hard wait expired (s_prev / done incomplete) ABORTS the
+    //    epoch -- it reports TIMEOUT and disables its exchange.  A peer that arrives after that
+    //    deadline (alive, only late: shard skew, a first-seen compile on one rank) would otherwise
+    //    find the early rank's give-up verdict and done word and report RETRY, re-running over
+    //    collectives that no longer pair up.  So every rank that completed its own waits also waits
+    //    for every peer's final word, and an aborted (or missing) one is a TIMEOUT here too.
+    const bool aborted = s_prev != all || done != all;
+    p2p_release(hdr(a.mbox[a.rank], 4 + (int)(e & 1)), (e << 1) | (aborted ? 1u : 0u));
+    unsigned fin_ok = all;
+    if (!aborted) {
+      const unsigned fin = wait_fin(a, e, a.hard_ticks);
+      fin_ok = fin;
+      for (int r = 0; r < a.nranks; ++r) {
+        if (!(fin & (1u << r))) continue;
+        if (p2p_acquire(hdr(a.mbox[r], 4 + (int)(e & 1))) & 1u) fin_ok &= ~(1u << r);
+      }
+    }
+    s_done = done & fin_ok;
     s_gaveup = gaveup;
   }
   __syncthreads();

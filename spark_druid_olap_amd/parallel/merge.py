@@ -220,7 +220,9 @@ def merge_plan_for(world: World, part: Partials, disjoint_keys: bool = False):
     the layout only, so every rank takes the same collective path."""
     from ..planner.cost import plan_merge
 
-    return plan_merge(part.kind == "dense", dense_state_bytes(part) if part.kind == "dense" else 0, world.size,
+    # (a forced one-rank group -- the RCCL smoke -- takes the paths a pair of ranks would)
+    n = world.size if world.size > 1 or not world.distributed else 2
+    return plan_merge(part.kind == "dense", dense_state_bytes(part) if part.kind == "dense" else 0, n,
                       disjoint_keys)
 
 

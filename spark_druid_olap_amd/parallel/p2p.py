@@ -20,9 +20,10 @@ Fail-safe by construction:
   (``SDO_P2P_TIMEOUT_S``, 0.5 s).  A rank that gives up posts that verdict; every rank reads every
   verdict, so all of them report ``STATUS_P2P_RETRY`` together, ``finalize`` / ``check_status``
   raise ``P2PRetry`` on every rank, and the statement re-runs with the merge over RCCL
-  (``PreparedQuery``).  After ``MAX_RETRIES`` such epochs the group stops using the exchange (every
-  rank counts the same epochs).  Only a peer that posts no verdict within the HARD timeout (a
-  dead process) turns into a failed status word.
+  (``PreparedQuery``).  After ``MAX_RETRIES`` consecutive such epochs the group stops using the
+  exchange (every rank counts the same epochs).  Only a peer that posts no verdict within the HARD
+  timeout (a dead process, or a live one later than that deadline: the early rank then publishes
+  an aborted final word, so every rank reports the timeout) turns into a failed status word.
 * **One exchange per rank.**  Only statements on the main process group use it: SPMD execution
   slots (``server/spmd.py``) each have their own group and stream, and spinning merge kernels of
   different slots could share one hardware queue in a different order on different ranks.
@@ -92,7 +93,8 @@ class PeerExchange:
             pass
         self.own = own
         self.dev = dev
-        self.retries = 0
+        self.retries = 0        # consecutive abandoned epochs (reset by a completed one)
+        self.total_retries = 0
         self.disabled = False
         # (every step below is collective whatever happened locally, so no rank is left waiting)
         got = world.all_gather_object((world.rank, handle))
@@ -253,6 +255,7 @@ def note_retry(world) -> None:
     ex = _EXCHANGES.get(_key(world))
     if ex:
         ex.retries += 1
+        ex.total_retries += 1
         if ex.retries >= MAX_RETRIES:
             ex.disabled = True
 
@@ -264,7 +267,7 @@ def stats(world) -> Dict[str, object]:
     if ex is None:
         return {"built": True, "enabled": False}
     return {"built": True, "enabled": not ex.disabled, "memory": ex.memory, "epochs": ex.epoch,
-            "retries": ex.retries, "selftest": ex.selftest}
+            "retries": ex.retries, "total_retries": ex.total_retries, "selftest": ex.selftest}
 
 
 def check_status(part) -> None:
@@ -280,6 +283,14 @@ def check_status(part) -> None:
 def raise_status(vals: List[int], rank: int) -> None:
     from .fault import STATUS_P2P_TIMEOUT, raise_if_failed
 
+    if not any(vals):
+        # a completed epoch (every rank reads the same verdicts, so every rank resets together):
+        # ``MAX_RETRIES`` counts CONSECUTIVE abandoned epochs -- a few slow statements over a long
+        # run do not switch the exchange off for good
+        for ex in _EXCHANGES.values():
+            if ex is not None and ex.rank == rank and ex.retries:
+                ex.retries = 0
+        return
     if any(vals):
         if any(int(v) == STATUS_P2P_TIMEOUT for v in vals):
             # a peer missed the hard deadline: this rank's epochs may no longer line up with it

@@ -24,10 +24,14 @@ class World:
     local_rank: int = 0
     backend: str = "none"
     group: Any = None
+    # a real process group of ONE rank whose collectives still run (``SDO_FORCE_COLLECTIVES=1``):
+    # every distributed code path -- RCCL all-gather / all-to-all with splits / all-reduce / barrier
+    # -- executes on a one-GPU box (tools/rccl_smoke.py, tests/test_gpu_rccl.py)
+    force_collectives: bool = False
 
     @property
     def distributed(self) -> bool:
-        return self.size > 1
+        return self.size > 1 or self.force_collectives
 
     @property
     def pg(self):
@@ -60,6 +64,7 @@ class World:
     # ---------------------------------------------------------------- collectives
     def barrier(self):
         if self.distributed:
+            _turn()
             if self.backend == "nccl":
                 dist.barrier(group=self.pg, device_ids=[self.local_rank])
             else:
@@ -68,6 +73,7 @@ class World:
     def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         if not self.distributed:
             return t
+        _turn()
         o = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
         h = self._stage(t)
         dist.all_reduce(h, op=o, group=self.pg)
@@ -84,6 +90,7 @@ class World:
     def all_reduce_async(self, t: torch.Tensor, op: str = "sum") -> "Pending":
         if not self.distributed:
             return Pending(None, lambda: t)
+        _turn()
         o = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
         h = self._stage(t)
         work = dist.all_reduce(h, op=o, group=self.pg, async_op=True)
@@ -92,6 +99,7 @@ class World:
     def all_gather_tensor_async(self, t: torch.Tensor) -> "Pending":
         if not self.distributed:
             return Pending(None, lambda: t.unsqueeze(0))
+        _turn()
         src = self._stage(t.contiguous().reshape(-1))
         # concatenated layout works on both RCCL and gloo (gloo rejects the stacked form)
         out = torch.empty((self.size * src.numel(),), dtype=t.dtype, device=src.device)
@@ -102,25 +110,30 @@ class World:
         """Personalized exchange (the reference's hash-partitioned shuffle before the final
         aggregate, ``asd/PostAggregate.scala:97-103``): ``t``'s rows are grouped by destination rank
         (``counts[r]`` rows for rank r, in rank order); returns the rows every rank sent here,
-        concatenated in source-rank order, plus the per-source counts.  One ``all_to_all_single`` of
-        the counts (carrying the status word, parallel/fault.py) and one of the payload: each rank
-        receives ~total/N rows instead of the all-gather's total.  With ``status`` set,
+        concatenated in source-rank order, plus the per-source counts.  One all-gather of the count
+        vectors (carrying the status word, parallel/fault.py) and one ``all_to_all_single`` of the
+        payload: each rank receives ~total/N rows instead of the all-gather's total.  With ``status`` set,
         ``(rows, recv_counts, statuses)`` is returned and a failure skips the payload exchange."""
         if not self.distributed:
             return (t, counts.clone(), [status]) if status is not None else (t, counts.clone())
+        _turn()
         n = self.size
         dev = t.device
-        # (RCCL: the counts stay on the device -- the meta exchange is queued behind the kernels
-        # that produced them, and the one host wait is for the received meta below)
+        # ONE host wait per exchange: every rank's whole send-count vector (and status word) is
+        # all-gathered -- an [N, N + 1] matrix, on the device under RCCL, queued behind the kernels
+        # that produced the counts -- and read back once.  Row r is what rank r sends, so this
+        # rank's input splits (its own row) and output splits (its column) both come from the one
+        # copy (a count exchange + a separate read of the local counts were two host round trips).
         mdev = counts.device if (self.backend == "nccl" and counts.is_cuda) else torch.device("cpu")
-        send_meta = torch.stack([counts.to(device=mdev, dtype=torch.int64),
-                                 torch.full((n,), int(status or 0), dtype=torch.int64, device=mdev)], 1)
-        send_meta = send_meta.to(dev if self.backend == "nccl" else "cpu").reshape(-1).contiguous()
-        recv_meta = torch.empty_like(send_meta)
-        dist.all_to_all_single(recv_meta, send_meta, group=self.pg)
-        meta = recv_meta.reshape(n, 2).cpu()
-        rc = meta[:, 0]
-        sts = meta[:, 1].tolist()
+        send_meta = torch.cat([counts.to(device=mdev, dtype=torch.int64).reshape(-1),
+                               torch.full((1,), int(status or 0), dtype=torch.int64, device=mdev)])
+        send_meta = send_meta.to(dev if self.backend == "nccl" else "cpu").contiguous()
+        recv_meta = torch.empty(n * (n + 1), dtype=torch.int64, device=send_meta.device)
+        dist.all_gather_into_tensor(recv_meta, send_meta, group=self.pg)
+        meta = recv_meta.reshape(n, n + 1).cpu()
+        rc = meta[:, self.rank].clone()
+        sent = meta[self.rank, :n].tolist()
+        sts = meta[:, n].tolist()
         if status is not None and any(sts):
             return t[:0], rc, sts
         row = tuple(t.shape[1:])
@@ -130,7 +143,7 @@ class World:
         src = self._stage(t.contiguous().reshape(-1))
         out = torch.empty((int(rc.sum()) * width,), dtype=t.dtype, device=src.device)
         dist.all_to_all_single(out, src, output_split_sizes=[int(x) * width for x in rc.tolist()],
-                               input_split_sizes=[int(x) * width for x in counts.cpu().tolist()], group=self.pg)
+                               input_split_sizes=[int(x) * width for x in sent], group=self.pg)
         out = out.to(dev).reshape((-1,) + row)
         return (out, rc, sts) if status is not None else (out, rc)
 
@@ -170,17 +183,22 @@ class World:
         out = [g[i, : ns[i]] for i in range(self.size)]
         return (out, sts) if status is not None else out
 
-    def broadcast_object(self, obj: Any, src: int = 0) -> Any:
+    def broadcast_object(self, obj: Any, src: int = 0, group=None) -> Any:
+        """(``group``: a host-side (gloo) group of the same ranks -- the SPMD server's control
+        stream, which then never occupies a GPU queue next to the statements' collectives)"""
         if not self.distributed:
             return obj
+        if group is None:
+            _turn()
         lst = [obj]
-        dist.broadcast_object_list(lst, src=src, group=self.pg)
+        dist.broadcast_object_list(lst, src=src, group=group if group is not None else self.pg)
         return lst[0]
 
     def all_gather_object(self, obj: Any) -> List[Any]:
         """Small host metadata from every rank (catalog views, segment inventories)."""
         if not self.distributed:
             return [obj]
+        _turn()
         out: List[Any] = [None] * self.size
         dist.all_gather_object(out, obj, group=self.pg)
         return out
@@ -196,6 +214,83 @@ class World:
 
 
 _TLS = __import__("threading").local()
+
+
+# ------------------------------------------------------------------------------------------------
+# Agreed issue order of collectives across concurrent statements (the SPMD server's execution slots,
+# server/spmd.py).  Each slot has its own communicator, and RCCL enqueues a communicator's kernels on
+# its own stream -- but a process has only GPU_MAX_HW_QUEUES (4) hardware queues for all of its
+# streams.  If rank A enqueued slot 1's collective before slot 2's while rank B did the opposite,
+# and the two landed on one in-order hardware queue on each rank, each rank's first kernel would
+# spin waiting for a peer kernel queued behind the other one: a cross-communicator deadlock.  So
+# every statement gets a sequence number in broadcast order (identical on every rank), and a thread
+# running statement s issues a collective only once every statement before s has FINISHED: the
+# collectives of all slots then leave every rank in the same order (statement by statement), and
+# at most one statement is between collectives at a time.  Scans, compiles and host work of the
+# slots still overlap freely; only their collective phases are ordered.
+class IssueOrder:
+    def __init__(self):
+        import threading
+
+        self.cv = threading.Condition()
+        self.next_seq = 0
+        self.active: set = set()
+        self.log: Optional[list] = None  # (tests) the seq of every gated collective, in issue order
+
+    def begin(self, seq: Optional[int] = None) -> int:
+        """The next statement's sequence number (or the one the root assigned it) -- call in
+        broadcast order on every rank."""
+        with self.cv:
+            s = self.next_seq if seq is None else int(seq)
+            self.next_seq = max(self.next_seq, s + 1)
+            self.active.add(s)
+            return s
+
+    def finish(self, seq: int) -> None:
+        with self.cv:
+            self.active.discard(seq)
+            self.cv.notify_all()
+
+    def wait_turn(self, seq: int, timeout_s: float = 3600.0) -> None:
+        with self.cv:
+            if not self.cv.wait_for(lambda: not self.active or min(self.active) >= seq, timeout=timeout_s):
+                raise RuntimeError(f"statement {seq}: earlier statements {sorted(self.active)[:4]} never finished")
+            if self.log is not None:
+                if os.environ.get("SDO_ORDER_DEBUG"):
+                    import threading
+                    import traceback
+
+                    st = traceback.extract_stack(limit=10)
+                    with open(f"{os.environ['SDO_ORDER_DEBUG']}.{os.environ.get('RANK')}", "a") as f:
+                        f.write(f"{seq} {threading.current_thread().name} "
+                                f"{' '.join(x.name + ':' + str(x.lineno) for x in st[:-3])}\n")
+                self.log.append(seq)
+
+
+class statement_turn:
+    """``with statement_turn(order, seq):`` -- this thread runs statement ``seq``: its collectives
+    wait for their turn (``IssueOrder``); the statement is finished on exit (``finish=False``: a
+    part of the statement -- its preparation in the dispatch thread -- that is not the end of it)."""
+
+    def __init__(self, order: Optional[IssueOrder], seq: Optional[int], finish: bool = True):
+        self.order, self.seq, self.finish = order, seq, finish
+
+    def __enter__(self):
+        self._prev = (getattr(_TLS, "order", None), getattr(_TLS, "seq", None))
+        _TLS.order, _TLS.seq = self.order, self.seq
+        return self
+
+    def __exit__(self, *exc):
+        _TLS.order, _TLS.seq = self._prev
+        if self.finish and self.order is not None and self.seq is not None:
+            self.order.finish(self.seq)
+        return False
+
+
+def _turn() -> None:
+    o = getattr(_TLS, "order", None)
+    if o is not None:
+        o.wait_turn(_TLS.seq)
 
 
 class slot_group:
@@ -248,9 +343,11 @@ def init_world(backend: Optional[str] = None, timeout_s: int = 600) -> World:
     size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
-    if size <= 1:
+    forced = size <= 1 and os.environ.get("SDO_FORCE_COLLECTIVES", "0") not in ("0", "")
+    if size <= 1 and not forced:
         _WORLD = World(0, 1, local, "none")
         return _WORLD
+    size = max(1, size)
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() and not _gloo_on_gpu() else "gloo"
     if backend == "gloo" and _gloo_on_gpu() and torch.cuda.is_available():
@@ -264,7 +361,7 @@ def init_world(backend: Optional[str] = None, timeout_s: int = 600) -> World:
         timeout_s = int(os.environ.get("SDO_COLLECTIVE_TIMEOUT_S", timeout_s))
         dist.init_process_group(backend=backend, rank=rank, world_size=size,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
-    _WORLD = World(rank, size, local, backend, None)
+    _WORLD = World(rank, size, local, backend, None, force_collectives=forced)
     return _WORLD
 
 

@@ -25,11 +25,11 @@ from typing import Dict, List, Optional
 from ..query import spec as S
 from ..query.intervals import Interval
 
-HBM_BW = 5.0e12         # achievable streaming bandwidth per MI355X (bytes/s)
+HBM_BW = 6.1e12         # measured streaming bandwidth per MI355X (tools/stream_probe.py: 5.55 GB in 0.91 ms)
 LAUNCH_S = 12e-6        # kernel launch + host overhead per scan
 XGMI_LINK_BW = 153e9    # per direction per link
 COLL_LAT_S = 25e-6      # small-message RCCL latency
-LDS_BUDGET = 64 * 1024
+LDS_PER_CU = 160 * 1024  # CDNA4 (gfx950) LDS per CU
 DENSE_GLOBAL_MAX = 1 << 24
 
 
@@ -144,7 +144,7 @@ def estimate(ds, spec, info=None, world_size: int = 1) -> CostEstimate:
     nbytes = int(rows * sum(_col_bytes(ds, c) for c in cols)) + int(rows * ds.time.element_size())
     aggs = len(spec.aggregation_specs) + 1
     acc_bytes = out * aggs * 8
-    if out * aggs * 8 <= LDS_BUDGET:
+    if out * aggs * 8 <= PLAN_LDS_BUDGET:
         mode = "dense-lds"
     elif out <= DENSE_GLOBAL_MAX:
         mode = "dense-global"
@@ -289,6 +289,9 @@ def choose_method(ds, spec, conf=None, info=None, world_size: int = 1):
 # CU, table budgets); between feasible alternatives the cheaper estimate wins.
 # ------------------------------------------------------------------------------------------------
 BLOCK_WAVES = 8                                             # 512-thread workgroups
+# per-wave accumulator copies + HLL registers of one workgroup: 64 KiB leaves room for the staging
+# planes and keeps 2 workgroups (16 waves) resident in a CU's 160 KiB (LDS_PER_CU); the scan is
+# latency-bound below 8 waves per CU
 PLAN_LDS_BUDGET = int(os.environ.get("SDO_LDS_BUDGET", 64 * 1024))
 SHARED_LDS_MAX = int(os.environ.get("SDO_SHARED_LDS_MAX", 112 * 1024))
 SHARED_MIN_GROUPS = int(os.environ.get("SDO_SHARED_MIN_GROUPS", 512))
@@ -492,3 +495,38 @@ def plan_merge(dense: bool, state_bytes: int, world_size: int, disjoint: bool = 
         costs["oneshot-allgather"] = (COLL_LAT_S + b * (n - 1) / (min(7, n - 1) * XGMI_LINK_BW) + n * b / HBM_BW) * 1e3
     costs["bucketed-allreduce"] = (3 * COLL_LAT_S + 2 * b * (n - 1) / n / XGMI_LINK_BW) * 1e3
     return MergePlan(min(costs, key=costs.get), costs)
+
+
+# Segment-batch pipelining (engine/executor.py _auto_batches / _run_pipelined): batch j's merge of its
+# time slice runs on the process group's stream while batch j+1 scans.  With B batches of a scan
+# taking S and a merge taking M (each slice 1/B of the state):
+#     one merge:  S + M
+#     pipelined:  S/B + (B - 1) * max(S/B, M/B) + M/B + (B - 1) * overhead
+# where every extra batch re-initialises and combines its table (two passes over the state at HBM
+# speed) and pays a few launches.  On xGMI a dense state's all-reduce is fast (2 x 4 MB x 7/8 over
+# 153 GB/s links: ~50 us), so the split pays only for states of tens of MB and more.  Host-staged
+# collectives (gloo: the one-card rehearsal) copy to the host synchronously inside the collective
+# call -- the next batch cannot even be launched before the copy returns -- so they never overlap:
+# measured, 3 batches 4.28 ms against one merge 2.81 ms (profiles/r5/rehearsal_auto_pipeline_sf10.txt).
+BATCH_LAUNCHES = 4
+
+
+def plan_pipeline(state_bytes: int, scan_bytes: int, world_size: int, host_staged: bool,
+                  max_batches: int) -> int:
+    """Batches for a pipelined multi-rank scan (1: scan once, merge once).  Inputs are layout sizes
+    -- identical on every rank."""
+    if host_staged or world_size <= 1 or max_batches <= 1:
+        return 1
+    S = scan_bytes / HBM_BW + LAUNCH_S
+
+    def merge_s(b):
+        return min(plan_merge(True, int(b), world_size).costs.values()) / 1e3
+
+    best_b, best_t = 1, S + merge_s(state_bytes)
+    for B in range(2, max_batches + 1):
+        m = merge_s(state_bytes / B)
+        over = BATCH_LAUNCHES * LAUNCH_S + 2 * state_bytes / HBM_BW
+        t = S / B + (B - 1) * max(S / B, m) + m + (B - 1) * over
+        if t < best_t:
+            best_b, best_t = B, t
+    return best_b

@@ -68,7 +68,10 @@ def code_column(ds, col: str, p: int, salt: int) -> Optional[str]:
         if v.numel() and int(v.min()) < 0:  # (ids are never negative; a 64-bit-mix value has no u16 code)
             return None
         out[lo:hi] = codes(v, salt, p).to(torch.int16)  # low 16 bits (two's complement wrap)
-    cache[name] = out.view(torch.uint16) if hasattr(torch, "uint16") else out
+    from ..utils.streams import publish
+
+    # (complete before any slot's stream can find it: utils/streams.py)
+    cache[name] = publish(out.view(torch.uint16) if hasattr(torch, "uint16") else out, ids.device)
     return name
 
 

@@ -148,5 +148,7 @@ def packed_column(ds, name: str) -> Optional[PackedColumn]:
         W = width_for(lo, hi)
         if W <= 32 and worth_packing(t, W) and n > 0:
             pc = pack(t, n, lo, hi)
-    cache[name] = pc
+    from ..utils.streams import publish
+
+    cache[name] = publish(pc, t.device)  # (every slot's stream reads it: complete before it is visible)
     return pc

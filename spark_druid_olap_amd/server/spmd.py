@@ -33,6 +33,8 @@ import queue
 import threading
 from typing import Any, Dict, List, Optional, Tuple
 
+from ..parallel.world import statement_turn
+
 log = logging.getLogger("sdo.spmd")
 
 HEARTBEAT_S = 20.0
@@ -176,8 +178,19 @@ class SlotWorkers:
         import torch
         import torch.distributed as dist
 
+        from ..parallel.world import IssueOrder
+
         self.k = k
         self.groups = [dist.new_group(list(range(world.size))) if world.distributed else None for _ in range(k)]
+        # the control stream (statement broadcasts, heartbeats) over a host-side gloo group of the
+        # same ranks: under RCCL a control broadcast would otherwise sit in a GPU queue next to the
+        # slots' collectives, in an order that differs per rank
+        self.ctrl = dist.new_group(list(range(world.size)), backend="gloo") \
+            if world.distributed and world.backend == "nccl" else None
+        self.world = world
+        # every statement's sequence number, in broadcast order: the slots' collectives leave this
+        # rank in that order (parallel/world.py IssueOrder -- no cross-communicator deadlock)
+        self.order = IssueOrder() if world.distributed else None
         dev = world.device()
         self.streams = [torch.cuda.Stream(dev) if dev.type == "cuda" else None for _ in range(k)]
         self.queues: List["queue.Queue"] = [queue.Queue() for _ in range(k)]
@@ -193,6 +206,11 @@ class SlotWorkers:
         with self._lock:
             self.busy[slot] += 1
         self.queues[slot].put((df, msg, done))
+
+    def control(self, world):
+        """The group control broadcasts use (None: the world's own) -- only while ``world`` is the
+        one the slots were built for (an elastic recovery replaces it)."""
+        return self.ctrl if world is self.world else None
 
     def least_busy(self) -> int:
         with self._lock:
@@ -219,7 +237,8 @@ class SlotWorkers:
             with self._lock:
                 self.max_inflight = max(self.max_inflight, sum(1 for b in self.busy if b > 0))
             try:
-                with slot_group(self.groups[i]), use_slot(self.BUFFER_SLOT_BASE + i):
+                with statement_turn(self.order, msg.get("seq")), slot_group(self.groups[i]), \
+                        use_slot(self.BUFFER_SLOT_BASE + i):
                     if self.streams[i] is not None:
                         # preparation (dispatch thread, default stream) launched device work the
                         # scan reads -- e.g. the u16 HLL code planes of segment/hllcode.py
@@ -342,7 +361,7 @@ class SpmdDispatcher:
                 if self._stop.is_set():
                     break
                 try:
-                    w.broadcast_object({"op": "noop"})
+                    w.broadcast_object({"op": "noop"}, group=self._ctrl(w))
                 except BaseException as e:  # noqa: BLE001
                     if not _elastic_recover(self.root, e):
                         raise
@@ -358,9 +377,16 @@ class SpmdDispatcher:
             groups = self._coalesce(batch)
             slots = self._assign(groups)
             msgs = [dict(g[0].msg, slot=sl) for g, sl in zip(groups, slots)]
+            order = self._order()
+            if order is not None:
+                for m in msgs:
+                    m["seq"] = order.begin()
             try:
-                w.broadcast_object({"op": "batch", "msgs": msgs})
+                w.broadcast_object({"op": "batch", "msgs": msgs}, group=self._ctrl(w))
             except BaseException as e:  # noqa: BLE001
+                if order is not None:
+                    for m in msgs:
+                        order.finish(m["seq"])
                 if _elastic_recover(self.root, e):  # a peer is gone: rebuild, then serve again
                     w = self.world = self.root.engine.world
                     for it in batch:
@@ -377,7 +403,8 @@ class SpmdDispatcher:
                     continue
                 self.stats["inline"] += 1
                 try:
-                    res = _run_elastic(self.root, lambda m=m: _execute(self.sessions, self.root, m))
+                    with statement_turn(order, m.get("seq")):
+                        res = _run_elastic(self.root, lambda m=m: _execute(self.sessions, self.root, m))
                     w = self.world = self.root.engine.world
                     for it in g:
                         it.result = res
@@ -388,12 +415,21 @@ class SpmdDispatcher:
                     it.event.set()
             if self._stop.is_set() and self._q.empty():
                 break
-        w.broadcast_object({"op": "stop"})
+        w.broadcast_object({"op": "stop"}, group=self._ctrl(w))
+
+    def _ctrl(self, w):
+        return self.workers.control(w) if self.workers is not None else None
+
+    def _order(self):
+        return self.workers.order if self.workers is not None else None
 
     def _dispatch_slot(self, g: List[_Item], m: Dict[str, Any]) -> None:
         try:
-            df = prepare_statement(self.sessions, self.root, m)
+            with statement_turn(self._order(), m.get("seq"), finish=False):
+                df = prepare_statement(self.sessions, self.root, m)
         except BaseException as e:  # noqa: BLE001
+            if self._order() is not None:
+                self._order().finish(m["seq"])
             for it in g:
                 it.error = e
                 it.event.set()
@@ -470,7 +506,7 @@ def serve_peer(session, world) -> None:
     workers: Optional[SlotWorkers] = None
     while True:
         try:
-            msg = world.broadcast_object(None)
+            msg = world.broadcast_object(None, group=workers.control(world) if workers is not None else None)
         except BaseException as e:  # noqa: BLE001
             if not _elastic_recover(session, e):
                 raise
@@ -487,14 +523,25 @@ def serve_peer(session, world) -> None:
             k = int(msg["k"])
             workers = SlotWorkers(session, world, k) if k > 0 else None
             continue
+        order = workers.order if workers is not None else None
+        for m in msg.get("msgs", []):
+            if order is not None and m.get("seq") is not None:
+                order.begin(m["seq"])
         for m in msg.get("msgs", []):
             slot = m.get("slot", INLINE)
+            submitted = False
             try:
                 if slot != INLINE and workers is not None:
-                    df = prepare_statement(sessions, session, m)
+                    with statement_turn(order, m.get("seq"), finish=False):
+                        df = prepare_statement(sessions, session, m)
                     workers.submit(slot, df, m, lambda res, err: None)  # rank 0 answers the client
+                    submitted = True
                     continue
-                _run_elastic(session, lambda m=m: _execute(sessions, session, m))
+                with statement_turn(order, m.get("seq")):
+                    _run_elastic(session, lambda m=m: _execute(sessions, session, m))
                 world = session.engine.world
             except BaseException as e:  # noqa: BLE001  (rank 0 reports the error to the client)
                 log.debug("peer statement failed: %s", e)
+            finally:
+                if order is not None and m.get("seq") is not None and slot != INLINE and not submitted:
+                    order.finish(m["seq"])

@@ -583,6 +583,13 @@ class Session:
                                       if k == "value" or (k == "string" and t in ("tinyint", "smallint", "int", "bigint"))}
                     # rank() = 1 window above (sql/window.py push_rank_one): device pre-filter
                     prep.partition_extreme = dq.info.get("partition_extreme")
+                    # device work the prepare launched on this thread's stream (descriptor-side
+                    # tables, LUTs, packed copies) completes before other slots -- whose streams
+                    # were ordered after the default stream when they were leased, possibly before
+                    # this -- can pick the plan up (utils/streams.py)
+                    from .utils.streams import publish
+
+                    publish(prep, ds.device if hasattr(ds, "device") else None)
                     dq._prepared = prep
                     dq._prepared_spec = spec
         return prep

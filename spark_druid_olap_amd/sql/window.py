@@ -283,13 +283,27 @@ def _rank_one_rid(cond) -> Optional[int]:
     return None
 
 
-_MONOTONE_CASTS = ("tinyint", "smallint", "int", "bigint", "float", "double")
+# Casts the ORDER BY metric may go through.  The device keeps the groups whose f64 image of the
+# metric equals their partition's extreme; that must be a SUPERSET of the groups Spark ranks 1 by
+# the cast value, so the cast may not merge values the f64 image keeps apart: injective casts
+# (integer widening, float -> double) and the cast to double itself (the very f64 image the device
+# compares) qualify.  A narrowing cast (double -> int truncates, double -> float rounds, bigint ->
+# int wraps) maps distinct sums to one value: Spark then ranks several groups 1 where the device
+# would keep only the partition extreme of the uncast sum.
+_INT_WIDTH = {"tinyint": 1, "smallint": 2, "int": 4, "bigint": 8}
+
+
+def _rank_safe_cast(frm: str, to: str) -> bool:
+    if frm == to:
+        return True
+    if frm in _INT_WIDTH and to in _INT_WIDTH:
+        return _INT_WIDTH[to] >= _INT_WIDTH[frm]
+    return to == "double" and (frm in _INT_WIDTH or frm in ("float", "double"))
 
 
 def _through_projects(rid: int, projs, monotone: bool = False) -> Optional[int]:
     """Follow a column down a chain of projections (outermost first) as long as it is passed through
-    or renamed (``monotone``: or numerically cast -- an order-preserving map, so the device filter's
-    f64 comparison keeps a superset of the rank-1 rows); None when it is computed."""
+    or renamed (``monotone``: or cast without merging values -- ``_rank_safe_cast``); None when it is computed."""
     from . import plan as P
 
     for pr in projs:
@@ -298,7 +312,8 @@ def _through_projects(rid: int, projs, monotone: bool = False) -> Optional[int]:
             if P.out_ref(e).rid != rid:
                 continue
             c = e.child if isinstance(e, A.Alias) else e
-            if monotone and isinstance(c, A.Cast) and c.to in _MONOTONE_CASTS:
+            if monotone and isinstance(c, A.Cast) and isinstance(c.child, A.Ref) and \
+                    _rank_safe_cast(str(c.child.dtype).lower(), str(c.to).lower()):
                 c = c.child
             if isinstance(c, A.Ref):
                 nxt = c.rid

@@ -180,3 +180,15 @@ def test_historical_wins_for_a_large_time_bucketed_state_across_ranks(monkeypatc
     assert cost.choose_method_costed(ds, flat, world_size=8).segments_per_query is None
     # one GPU: nothing to overlap
     assert cost.choose_method_costed(ds, ts, world_size=1).segments_per_query is None
+
+
+def test_auto_pipeline_priced_on_measured_constants():
+    """Segment-batch pipelining (planner/cost.py plan_pipeline) is chosen only where the hidden merge
+    outweighs the extra batches' table passes: never over host-staged collectives (the measured
+    one-card gloo rehearsal: 3 batches 4.28 ms vs one merge 2.81 ms), not for a 4 MB state over xGMI
+    (its all-reduce is ~50 us), yes for a multi-hundred-MB state behind a long scan on 8 ranks."""
+    assert cost.HBM_BW == pytest.approx(6.1e12) and cost.LDS_PER_CU == 160 * 1024
+    assert cost.plan_pipeline(4_400_000, 10 ** 10, 2, host_staged=True, max_batches=3) == 1
+    assert cost.plan_pipeline(4_400_000, int(1.3e10), 8, host_staged=False, max_batches=3) == 1
+    assert cost.plan_pipeline(512 << 20, int(6e10), 8, host_staged=False, max_batches=3) > 1
+    assert cost.plan_pipeline(512 << 20, int(6e10), 1, host_staged=False, max_batches=3) == 1

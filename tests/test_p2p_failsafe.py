@@ -97,6 +97,7 @@ def test_retries_disable_exchange_after_limit(monkeypatch):
 
     class Ex:
         retries = 0
+        total_retries = 0
         disabled = False
         rank = 0
 
@@ -105,5 +106,11 @@ def test_retries_disable_exchange_after_limit(monkeypatch):
     for i in range(p2p.MAX_RETRIES - 1):
         p2p.note_retry(w)
         assert not ex.disabled
+    # a completed epoch in between resets the CONSECUTIVE count (every rank sees the same verdicts)
+    p2p.raise_status([0, 0], 0)
+    assert ex.retries == 0 and ex.total_retries == p2p.MAX_RETRIES - 1
+    for i in range(p2p.MAX_RETRIES - 1):
+        p2p.note_retry(w)
+        assert not ex.disabled
     p2p.note_retry(w)
-    assert ex.disabled
+    assert ex.disabled and ex.total_retries == 2 * p2p.MAX_RETRIES - 1

@@ -109,6 +109,7 @@ def _work(rank, world, port, outdir, device="cpu"):
     # pipelines by itself, with the batch count agreed across ranks; below it, one merge
     saved_min = X.AUTO_PIPELINE_MIN_BYTES
     X.AUTO_PIPELINE_MIN_BYTES = 512
+    X.AUTO_PIPELINE_FORCE = True  # (gloo stages through the host: the cost model would never split)
     try:
         p = eng.prepare(_ts_month(), ds)
         a = p.run().sorted_rows()
@@ -117,7 +118,7 @@ def _work(rank, world, port, outdir, device="cpu"):
         b = q0.run().sorted_rows()
         out["auto"] = (a, b, p._nbatches, bool(p.segments_per_query), p._pipeline_ok, bool(q0.segments_per_query))
     finally:
-        X.AUTO_PIPELINE, X.AUTO_PIPELINE_MIN_BYTES = True, saved_min
+        X.AUTO_PIPELINE, X.AUTO_PIPELINE_MIN_BYTES, X.AUTO_PIPELINE_FORCE = True, saved_min, False
     small = eng.prepare(query_from_json(DRUID_JSON["TPCH Q1"]), ds)
     out["auto_small"] = bool(small.segments_per_query)
     # a scan failure in the second batch of rank 0: both ranks abort consistently

@@ -153,3 +153,24 @@ def test_partition_scratch_pool_budget_reuse_and_wait(monkeypatch):
     pool.release(again)
     pool.clear()
     assert pool.bytes() == 0
+
+
+def test_out_of_memory_release_skips_arenas_held_by_other_slots(monkeypatch):
+    """An out-of-memory release while carving (this arena's lock held) must not wait for another
+    slot's arena lock: that slot may be carving too and releasing in turn -- each would hold its own
+    lock and wait on the other's (lock-order deadlock).  Busy arenas are skipped."""
+    monkeypatch.setattr(DE, "_ARENAS", {})
+    a, b = DE.slot_arena("cpu", 93), DE.slot_arena("cpu", 94)
+    own = _Owner()
+    with use_slot(94):
+        b.carve(1000, own)
+    monkeypatch.setattr(DE.torch.cuda, "empty_cache", lambda: None)
+    done = threading.Event()
+    with b.lock:  # slot 94 is busy carving
+        t = threading.Thread(target=lambda: (DE.release_device_memory(keep_arena=a), done.set()))
+        t.start()
+        t.join(10)
+        assert done.is_set(), "release_device_memory blocked on another slot's arena lock"
+    assert b.buf is not None  # (skipped, not dropped)
+    DE.release_device_memory(keep_arena=a)
+    assert b.buf is None

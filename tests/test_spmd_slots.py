@@ -172,3 +172,107 @@ def test_dispatcher_streams_select_pages(ds_small, df_small):
         assert res4[1] not in spmd._STREAMS and res4[1] not in spmd._STREAM_OWNER
     finally:
         d.shutdown()
+
+
+def _order_worker(rank, world, port, outdir):
+    """4 gloo ranks, 2 slots; even ranks hold slot 0's statements back, odd ranks slot 1's -- the
+    slots reach their collectives in opposite orders on alternate ranks.  Every rank logs the
+    statement sequence number of each collective it issues (parallel/world.py IssueOrder)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), OMP_NUM_THREADS="1")
+    import threading as th
+
+    from spark_druid_olap_amd.engine.executor import Engine
+    from spark_druid_olap_amd.models import tpch
+    from spark_druid_olap_amd.parallel import world as W
+    from spark_druid_olap_amd.server import spmd
+    from spark_druid_olap_amd.session import Session
+
+    logs = []
+    init = W.IssueOrder.__init__
+
+    def logged_init(self):
+        init(self)
+        self.log = []
+        logs.append(self.log)
+    W.IssueOrder.__init__ = logged_init
+    w = W.init_world(backend="gloo")
+    ds = tpch.to_datasource(tpch.generate_flat(0.002, "cpu", rank=rank, world=world), profile="bench")
+    s = Session(engine=Engine(w, use_native=False))
+    s.register_datasource(ds)
+    s.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)
+    s.sql(tpch.druid_ddl(with_column_mapping=False))
+    real = spmd._run_statement
+    held = "spmd-slot-0" if rank % 2 == 0 else "spmd-slot-1"
+
+    def skewed(df, msg):
+        time.sleep(0.15 if th.current_thread().name == held else 0.0)
+        return real(df, msg)
+    spmd._run_statement = skewed
+    if rank != 0:
+        spmd.serve_peer(s, w)
+    else:
+        d = spmd.SpmdDispatcher(s, w, slots=2, coalesce=False)
+        stmts = statements()[:12]
+        serial = {}
+        d.open_session(b"serial", {}, None)
+        for q in stmts:
+            serial[q] = d.execute(b"serial", q)[1].values.tolist()
+        conc, errs = {}, []
+
+        def client(i):
+            sid = f"c{i}".encode()
+            try:
+                d.open_session(sid, {}, None)
+                for j in range(len(stmts)):
+                    q = stmts[(i * 5 + j) % len(stmts)]
+                    conc.setdefault(q, []).append(d.execute(sid, q)[1].values.tolist())
+                d.close_session(sid)
+            except Exception as e:  # noqa: BLE001
+                errs.append(repr(e))
+        ts = [th.Thread(target=client, args=(i,)) for i in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(300)
+        with open(os.path.join(outdir, "r0.pkl"), "wb") as f:
+            pickle.dump({"serial": serial, "conc": conc, "errs": errs, "max_inflight": d.workers.max_inflight}, f)
+        d.shutdown()
+    with open(os.path.join(outdir, f"log{rank}.pkl"), "wb") as f:
+        pickle.dump([list(x) for x in logs], f)
+    W.shutdown()
+
+
+@pytest.mark.timeout(900)
+def test_slot_collectives_leave_every_rank_in_one_order():
+    """Concurrent slots with their own communicators (RCCL on a real node) must enqueue their
+    collectives in the same order on every rank, or two ranks can each wait on a kernel queued
+    behind the other's on a shared hardware queue.  With opposite slot skews on alternate ranks,
+    every rank's log of collective issues (by statement sequence number) must be identical and
+    non-decreasing, and every answer must equal the serial one."""
+    world = 4
+    with tempfile.TemporaryDirectory() as td:
+        ctx = mp.get_context("spawn")
+        port = _free_port()
+        ps = [ctx.Process(target=_order_worker, args=(r, world, port, td)) for r in range(world)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(800)
+            assert p.exitcode == 0, f"rank failed with {p.exitcode}"
+        logs = []
+        for r in range(world):
+            with open(os.path.join(td, f"log{r}.pkl"), "rb") as f:
+                logs.append(pickle.load(f))
+        with open(os.path.join(td, "r0.pkl"), "rb") as f:
+            out = pickle.load(f)
+    assert not out["errs"], out["errs"]
+    assert out["max_inflight"] >= 2, out
+    for q, runs in out["conc"].items():
+        for r in runs:
+            assert _norm(r) == _norm(out["serial"][q]), q
+    assert all(len(lg) == 1 for lg in logs), [len(lg) for lg in logs]
+    seqs = [lg[0] for lg in logs]
+    assert len(seqs[0]) > 50
+    assert all(x == seqs[0] for x in seqs[1:]), "ranks issued collectives in different orders"
+    assert seqs[0] == sorted(seqs[0])

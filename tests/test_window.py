@@ -106,6 +106,40 @@ def test_rank_one_pushdown(ds_small, df_small, fn, order, partition):
     assert got == want
 
 
+def test_rank_safe_casts():
+    from spark_druid_olap_amd.sql.window import _rank_safe_cast
+
+    assert _rank_safe_cast("int", "bigint") and _rank_safe_cast("smallint", "int")
+    assert _rank_safe_cast("bigint", "double") and _rank_safe_cast("float", "double")
+    assert not _rank_safe_cast("double", "int") and not _rank_safe_cast("double", "float")
+    assert not _rank_safe_cast("bigint", "int") and not _rank_safe_cast("double", "bigint")
+
+
+@pytest.mark.parametrize("order_expr,pushed", [("cast(sum(l_extendedprice) as int)", False),
+                                               ("cast(sum(l_extendedprice) as float)", False),
+                                               ("cast(count(*) as int)", False)])
+def test_rank_one_pushdown_through_casts(ds_small, df_small, order_expr, pushed):
+    """The rank-one pre-filter only looks through casts that are injective for the metric's type:
+    cast(sum(double) as int) maps distinct sums to one value (1.2 and 1.7 both rank 1 in Spark), so
+    the device must not keep only the partition minimum of the uncast sum."""
+    from spark_druid_olap_amd.sql import plan as P
+
+    s = Session(engine=Engine(use_native=False))
+    s.register_datasource(ds_small)
+    s.register_table("orderLineItemPartSupplierBase", df_small, schema=tpch.FLAT_SCHEMA)
+    s.sql(tpch.druid_ddl(with_column_mapping=False))
+    q = ("select p_mfgr, p_brand, cnt from (select p_mfgr, p_brand, count(*) cnt, "
+         f"dense_rank() over (partition by p_mfgr order by {order_expr}) rk "
+         "from orderLineItemPartSupplier group by p_mfgr, p_brand) t where rk = 1")
+    d = s.sql(q)
+    dqs = P.find_all_deep(d.plan, P.DruidQuery)
+    assert dqs and bool(dqs[0].info.get("partition_extreme")) == pushed
+    got = sorted(d.collect())
+    s.conf.set("spark.sparklinedata.druid.window.rankone.pushdown", "false")
+    s._plan_cache.clear()
+    assert got == sorted(s.sql(q).collect())
+
+
 def test_window_errors(sess):
     from spark_druid_olap_amd.sql.types import AnalysisError
 

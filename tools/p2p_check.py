@@ -27,7 +27,11 @@ Fail-safe scenarios (``--scenario``, tests/test_gpu_p2p.py):
   fails on one rank, so no rank uses P2P and every statement completes over the collective path;
 * ``delay`` (with ``SDO_P2P_DELAY=rank=1,s=1.5,times=1``): one rank launches a merge after the
   peers' soft wait expired; every rank abandons that epoch together and the statement re-runs over
-  the collective path with the same answer.
+  the collective path with the same answer;
+* ``late`` (with ``SDO_P2P_DELAY=rank=1,s=3,times=1`` and ``SDO_P2P_HARD_TIMEOUT_S=1``): one rank,
+  alive, arrives after the peers' HARD deadline.  The early rank aborts the epoch (its final word),
+  so EVERY rank -- the late one too -- reports the timeout, fails that statement and disables its
+  exchange; the next statements run over the collective path with the unchanged answers.
 
 Rank 0 writes a JSON report to ``--out``."""
 import argparse
@@ -188,12 +192,49 @@ def engine(world, dev, sf, out):
         out["phases"] = phases
 
 
+def late(world, dev, sf, out):
+    """A live peer later than the hard deadline: every rank must see the same outcome."""
+    from spark_druid_olap_amd.engine.executor import Engine, results_on_root
+    from spark_druid_olap_amd.models import tpch
+    from spark_druid_olap_amd.parallel import p2p
+    from spark_druid_olap_amd.session import Session
+
+    ds = tpch.to_datasource(tpch.generate_flat(sf, dev, rank=world.rank, world=world.size), profile="bench")
+    sess = Session(engine=Engine(world))
+    sess.register_datasource(ds)
+    sess.register_table("orderLineItemPartSupplierBase", schema=tpch.FLAT_SCHEMA)
+    sess.sql(tpch.druid_ddl(source="orderLineItemPartSupplierBase", datasource="tpch", with_column_mapping=False))
+    q = dict(tpch.BENCH_QUERIES)["TPCH Q1"]
+    rows = lambda b: sorted(tuple(round(x, 6) if isinstance(x, float) else x for x in r)  # noqa: E731
+                            for r in b.to_pandas().itertuples(index=False, name=None))
+    with results_on_root():
+        p2p.ENABLED = False
+        sess._plan_cache.clear()
+        want = rows(sess.sql(q).run())
+        p2p.ENABLED = True
+        sess._plan_cache.clear()
+        df = sess.sql(q)
+        try:
+            df.run()
+            outcome = "ok"
+        except Exception as e:  # noqa: BLE001
+            outcome = type(e).__name__
+        outcomes = world.all_gather_object(outcome)
+        enabled = world.all_gather_object(bool(p2p.stats(world).get("enabled")))
+        after = rows(df.run())
+    out["late_outcomes"] = outcomes
+    out["late_enabled_after"] = enabled
+    same = world.all_gather_object(after == want if world.rank == 0 else True)
+    out["late_answer_equal"] = all(same)
+    out["p2p_stats"] = p2p.stats(world)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", required=True)
     ap.add_argument("--sf", type=float, default=1.0, help="scale factor per rank")
     ap.add_argument("--skip-engine", action="store_true")
-    ap.add_argument("--scenario", default="normal", choices=["normal", "selftest_fail", "delay"])
+    ap.add_argument("--scenario", default="normal", choices=["normal", "selftest_fail", "delay", "late"])
     a = ap.parse_args()
     os.environ.setdefault("SDO_PHASE_EVENTS", "1")
     import torch
@@ -208,7 +249,9 @@ def main():
     out["scenario"] = a.scenario
     if world.size > 1 and a.scenario == "normal":
         synthetic(world, dev, out)
-    if not a.skip_engine and (out.get("exchange") or world.size == 1 or a.scenario != "normal"):
+    if a.scenario == "late":
+        late(world, dev, a.sf, out)
+    elif not a.skip_engine and (out.get("exchange") or world.size == 1 or a.scenario != "normal"):
         engine(world, dev, a.sf, out)  # (one rank: the same-SF baseline of the per-phase split)
     world.barrier()
     if world.rank == 0:
