@@ -36,16 +36,22 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--sf", type=float, default=float(os.environ.get("SDO_BENCH_SF", "100")),
+    ap.add_argument("--sf", type=float, default=100.0,
                     help="scale factor PER GPU (weak scaling: N GPUs hold N x SF)")
-    ap.add_argument("--total-sf", type=float, default=float(os.environ.get("SDO_BENCH_TOTAL_SF", "0")) or None,
+    ap.add_argument("--total-sf", type=float, default=None,
                     help="scale factor of the WHOLE job, split over the GPUs (strong scaling: the fixed-SF100 "
                          "curve at 1/2/4/8 GPUs, or SF1000 over 8 GPUs = 125 per GPU)")
-    ap.add_argument("--mode", choices=["sql", "spec"], default=os.environ.get("SDO_BENCH_MODE", "sql"))
-    ap.add_argument("--model", choices=["tpch", "ssb", "tpch22"], default=os.environ.get("SDO_BENCH_MODEL", "tpch"),
+    ap.add_argument("--mode", choices=["sql", "spec"], default="sql")
+    ap.add_argument("--model", choices=["tpch", "ssb", "tpch22"], default="tpch",
                     help="tpch: the reference's 8-query TPC-H suite (headline); ssb: BASELINE config 4; "
                          "tpch22: the full 22-query TPC-H sweep over the flattened index (BASELINE config 2)")
     ap.add_argument("--verbose", action="store_true")
+    # diagnostics (the JSON line then describes what was run)
+    ap.add_argument("--only", default="", help="comma-separated subset of the suite's query names")
+    ap.add_argument("--profile-rank", type=int, default=None, help="cProfile this rank's timed steps (stderr)")
+    ap.add_argument("--keep-cache", action="store_true", help="keep the allocator cache of data generation")
+    ap.add_argument("--no-shape", action="store_true", help="skip the untimed shape-shared kernel pass")
+    ap.add_argument("--per-rank", action="store_true", help="every rank's own per-query means")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # one process per GPU, started here (never from a process that touched the GPU)
@@ -83,7 +89,7 @@ def main():
     gen_peak = None
     if dev.type == "cuda":
         torch.cuda.synchronize()
-        if not os.environ.get("SDO_BENCH_KEEP_CACHE"):
+        if not args.keep_cache:
             torch.cuda.empty_cache()
         # synthetic data generation holds the raw columns next to the index: its peak is not the
         # engine's, so the run's peak is measured from here on
@@ -132,7 +138,7 @@ def main():
 
         queries = [(name, engine.prepare(q, ds)) for name, q in bench_specs()]
 
-    only = [x for x in os.environ.get("SDO_BENCH_ONLY", "").split(",") if x]
+    only = [x for x in args.only.split(",") if x]
     if only:  # diagnostics: a subset of the suite (the JSON line then describes only that subset)
         queries = [(n, q) for n, q in queries if n in only]
     nsuite = len(queries)
@@ -155,7 +161,7 @@ def main():
     world.barrier()
     sync()
     prof = None
-    if os.environ.get("SDO_BENCH_PROFILE") and world.rank == int(os.environ.get("SDO_BENCH_PROFILE_RANK", "0")):
+    if args.profile_rank is not None and world.rank == args.profile_rank:
         import cProfile
 
         prof = cProfile.Profile()
@@ -196,7 +202,7 @@ def main():
                     coll.setdefault(name, []).append((time.perf_counter() - a) * 1e3)
                 world.barrier()
     shape_geo = None
-    if args.mode == "sql" and not only and os.environ.get("SDO_BENCH_SHAPE", "1") != "0":
+    if args.mode == "sql" and not only and not args.no_shape:
         # untimed, reported alongside: the same suite on the shape-shared kernels a first-seen
         # parameterization runs (query constants read from the descriptor, no literal-specialized
         # code object) -- freshly planned statements with specialization switched off
@@ -225,7 +231,7 @@ def main():
             world.barrier()
         smeans = {k: world.max_float(sum(v) / len(v)) for k, v in slat.items()}
         shape_geo = math.exp(sum(math.log(max(m, 1e-6)) for m in smeans.values()) / len(smeans))
-    if os.environ.get("SDO_BENCH_PER_RANK"):  # diagnostics: every rank's own means
+    if args.per_rank:  # diagnostics: every rank's own means
         print(f"[bench] rank {world.rank}: " + " ".join(f"{k[:12]}={sum(v) / len(v):.3f}" for k, v in lat.items()),
               file=sys.stderr, flush=True)
     total_ms = world.max_float(total_ms)

@@ -33,12 +33,12 @@ from ..planner.cost import PLAN_LDS_BUDGET as LDS_BUDGET  # noqa: E402  (single 
 # up to this many bytes of LDS, instead of HBM atomics contending on the touched groups
 from ..planner.cost import SHARED_LDS_MAX  # noqa: E402,F401
 BLOCK = 512
-UNROLL = int(os.environ.get("SDO_UNROLL", "2"))
-BLOCKS_PER_CU = int(os.environ.get("SDO_BLOCKS_PER_CU", "3"))
+UNROLL = 2  # (interpreter kernel: words per step)
+BLOCKS_PER_CU = 3
 USE_JIT = os.environ.get("SDO_JIT", "1") != "0"
-JIT_BLOCKS = int(os.environ.get("SDO_JIT_BLOCKS", "3"))  # target resident workgroups per CU
-JIT_STAGE = os.environ.get("SDO_JIT_STAGE", "auto")       # auto | reg (VGPR loads) | lds (LDS-DMA planes)
-JIT_TRACE = os.environ.get("SDO_JIT_TRACE", "0") == "1"  # print the unroll / budget candidates tried
+JIT_BLOCKS = 3       # target resident workgroups per CU
+JIT_STAGE = "auto"   # auto | reg (VGPR loads) | lds (LDS-DMA planes)
+JIT_TRACE = False    # (tools: print the unroll / budget candidates tried)
 FORCE_U = 0  # cap the words per step of generated kernels (0: the register / LDS-driven choice)
 # Literal specialization of repeated statements (ops/jit.py JitScan.specialized): a prepared scan's
 # first runs use the shape's shared kernel (query constants read from the descriptor: every
@@ -130,10 +130,17 @@ def _jit_for(prog, mode: int, hll_lds: bool, m: int, shared: bool = False):
 # interpreter runs as-is take the detour: per-wave LDS copies, plain HBM tables, hash tables, masks
 # -- shared LDS tables, first-touch / presence byte tables and the partitioned producers would fall
 # back to other modes (a 150M-group HBM table per slot), so those still compile in the foreground.
-# Off by default: the mechanism passes its own GPU test (tests/test_gpu_async_compile.py), but the
-# BI plan under 64 clients with it on ended in a device memory fault (cause not yet isolated: the
-# interpreter kernel on templates it never ran before, or statements re-prepared on a leased slot).
-ASYNC_JIT = os.environ.get("SDO_ASYNC_JIT", "0") == "1"
+# Round 5 turned this off after the BI plan under 64 clients faulted (illegal address) with it on.
+# Both suspects were checked on the GPU (tests/test_gpu_bi_templates.py): the interpreter kernel
+# answers every BI template correctly, alone and as the interim plan.  What the detour changed is
+# WHEN plans are built: a re-prepare swaps a new plan in while other slots run, and the device
+# artifacts its lowering builds lazily -- bit-packed column copies, HLL code planes, FD tables --
+# were published to datasource-wide caches while their producing kernels were still queued on the
+# preparing thread's stream; a slot whose stream was ordered after the default stream at lease
+# time, earlier, could then scan a half-written column (garbage ids -> out-of-bounds table
+# indices).  Every such cache now publishes only completed artifacts (utils/streams.py), and a
+# fresh plan is published after its prepare's stream drained (session.py prepare_druid).
+ASYNC_JIT = os.environ.get("SDO_ASYNC_JIT", "1") == "1"
 ASYNC_JIT_WORKERS = 4
 _async_tls = threading.local()
 _async_failed: set = set()
@@ -508,7 +515,7 @@ class PreparedScan:
             self.mode, self.lds, self.hll_lds = D.M_DENSE_GLOBAL, 0, 0
             cache_off, wave_bytes, _, total = lds_layout(prog, 0, UNROLL, BLOCK // 64)
         if total > 160 * 1024:
-            raise RuntimeError(f"query needs {total} bytes of LDS staging; reduce SDO_UNROLL")
+            raise RuntimeError(f"query needs {total} bytes of LDS staging")
         d = pack(prog, self.mode, self.dedup, self.hll_lds, 0 if self.shared else self.lds, b.acc.data_ptr(),
                  b.keys.data_ptr(),
                  cap, b.overflow.data_ptr(), b.touch.data_ptr() if self.touch else 0, 0,
@@ -548,12 +555,21 @@ class PreparedScan:
         if cap * L["rw"] >= (1 << 32) or cap >= (1 << 32):
             raise RuntimeError("partitioned group-by: shard too large for u32 record offsets")
         P1, nsub = L["p1"], L["nsub"]
-        k1 = max(1, min(nch, 2048))
+        # the producer counts its level-1 buckets itself (ops/jit.py part_hist_add): one histogram
+        # column per producer block, and chunk end offsets stored in producer-block order
+        # (jit.part_positions, empty padding positions stay 0), so the level-1 split's block k
+        # scatters exactly producer block k's records -- no count pass over the records
+        from ..ops import jit as J
+
+        k1 = int(self.grid)
+        npos, pos = J.part_positions(nch, k1)
+        seg_lo = np.zeros(max(1, npos), dtype=np.int64)
+        seg_lo[pos] = np.arange(nch, dtype=np.int64) * D.CHUNK_ROWS
         pb = {
             "cap_words": max(1, cap * L["rw"]), "desc_recs": 0,
-            "seg_lo": (torch.arange(nch, dtype=torch.int64) * D.CHUNK_ROWS).to(u32).to(dev),
-            "pend": torch.empty(max(1, nch), dtype=u32, device=dev),
-            "k1": k1, "nch": nch,
+            "seg_lo": torch.from_numpy(seg_lo).to(u32).to(dev),
+            "pend": torch.zeros(max(1, npos), dtype=u32, device=dev),
+            "k1": k1, "nch": nch, "npos": npos,
             "counts1": torch.empty(P1 * k1, dtype=u32, device=dev),
             "totals1": torch.empty(P1, dtype=u32, device=dev),
             "base1": torch.empty(P1 + 1, dtype=u32, device=dev),
@@ -564,6 +580,7 @@ class PreparedScan:
             pb["base2"] = torch.empty(nsub + 1, dtype=u32, device=dev)
         d[0]["part_recs"] = 0  # the slot's scratch, patched in at run time (_run_part)
         d[0]["part_counts"] = pb["pend"].data_ptr()
+        d[0]["part_base"] = pb["counts1"].data_ptr()  # (the producer's histogram: [P1][grid])
         d[0]["part_shift"] = L["shift1"]
         d[0]["part_n"] = P1
         return pb
@@ -588,15 +605,20 @@ class PreparedScan:
             ptr = torch.tensor([pb["recs1"].data_ptr()], dtype=torch.int64).view(torch.uint8)
             b.desc[off:off + 8].copy_(ptr.to(self.dev))
             b.part["desc_recs"] = pb["recs1"].data_ptr()
+        if pb["k1"] != int(self.grid):
+            # (a specialized kernel swapped in with another resident grid: _adopt) the histogram
+            # columns and chunk positions follow the producer's block count
+            self._slots.pop(current_slot(), None)
+            return self._run_part(self._bufs())
         nat.module_launch(self.jit.handle, b.desc.data_ptr(), int(self.grid), BLOCK, int(self.jit.lay.total), st)
         rw, P1, k1 = L["rw"], L["p1"], pb["k1"]
-        # level 1: one input group = every chunk region, P1 buckets by the top key bits
-        a1 = (pb["recs1"].data_ptr(), rw, pb["seg_lo"].data_ptr(), pb["pend"].data_ptr(), 1, pb["nch"], k1,
+        # level 1: one input group = every chunk region in producer-block order, block k of the
+        # split = producer block k's chunks (their level-1 histogram came with the records)
+        a1 = (pb["recs1"].data_ptr(), rw, pb["seg_lo"].data_ptr(), pb["pend"].data_ptr(), 1, pb["npos"], k1,
               L["shift1"], P1, pb["counts1"].data_ptr())
         # dense keys arrive in runs (rows in time order, then key order within a day): the split
         # kernels' same-bucket waves add once (partition.hip lds_count_add); hashes are uniform
         cl = 0 if L.get("hashed") else 2
-        nat.part_split(*a1, 0, 0, cl, st)
         nat.part_scan(pb["counts1"].data_ptr(), P1, k1, pb["totals1"].data_ptr(), pb["base1"].data_ptr(), st)
         nat.part_split(*a1, pb["base1"].data_ptr(), pb["recs2"].data_ptr(), 1 | cl, st)
         recs, base = pb["recs2"], pb["base1"]
@@ -1582,11 +1604,11 @@ class PreparedMask:
         return native.compact_rows(mask)
 
 
-PART_TABLE_BYTES = int(os.environ.get("SDO_PART_TABLE_BYTES", 32 << 10))  # LDS table per sub-bucket
+PART_TABLE_BYTES = 32 << 10  # LDS table per sub-bucket
 PART_MIN_SUBS = 512  # sub-buckets (aggregation workgroups) a partitioned group-by aims for at least
 HASH_TABLE_BYTES = 128 << 10  # LDS hash table of a hash-partitioned sub-bucket (keys + slots)
 PART_HLL_TABLE_BYTES = 128 << 10  # LDS slots + HLL byte registers of a partitioned sub-bucket
-HLL32_MAX_BYTES = int(os.environ.get("SDO_HLL32_MAX_BYTES", str(512 << 20)))  # u32 scan-time registers
+HLL32_MAX_BYTES = 512 << 20  # u32 scan-time registers
 
 
 def part_layout(prog) -> dict:

@@ -18,7 +18,6 @@ shard on the device and cached, like the dictionaries themselves.
 """
 from __future__ import annotations
 
-import os
 from typing import Optional, Tuple
 
 import numpy as np
@@ -72,7 +71,7 @@ def _leaf_cols(x, out: set) -> bool:
     return False  # time / numeric / expression leaves read rows
 
 
-_TRACE = bool(os.environ.get("SDO_TRACE_DICT_EXIST"))
+_TRACE = False  # (tools: print the dictionary-domain decisions)
 
 
 def plan(prog) -> Optional[Tuple[str, Tuple[str, ...]]]:

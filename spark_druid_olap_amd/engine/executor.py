@@ -35,22 +35,22 @@ from ..utils.cancel import checkpoint
 
 
 # segment-batched execution overlaps batch j's merge collectives with batch j+1's scan
-PIPELINE_MERGE = os.environ.get("SDO_PIPELINE_MERGE", "1") not in ("0", "")
+PIPELINE_MERGE = True
 # ... and is chosen by itself across ranks (no segments_per_query asked for) when the dense state
 # is large and keyed by a leading time bucket: each batch then merges only its time slice of the
 # table while the next batch scans, so all but the last slice's collective hide behind scans.
 # Small states are never split: their merge is latency-bound, every batch would pay it again and
 # the last one stays exposed anyway.
-AUTO_PIPELINE = os.environ.get("SDO_AUTO_PIPELINE", "1") not in ("0", "")
+AUTO_PIPELINE = True
 # (below this a merge is latency-bound: never split, whatever the price)
-AUTO_PIPELINE_MIN_BYTES = int(os.environ.get("SDO_AUTO_PIPELINE_MIN_BYTES", str(4 << 20)))
+AUTO_PIPELINE_MIN_BYTES = 4 << 20
 AUTO_PIPELINE_BATCHES = 3   # (at most: planner/cost.py plan_pipeline prices 2..3)
 AUTO_PIPELINE_FORCE = False  # (tests: split whatever the price)
 # existence-only group-bys over the key's dictionary domain (engine/dict_exist.py)
-DICT_EXIST = os.environ.get("SDO_DICT_EXIST", "1") not in ("0", "")
+DICT_EXIST = True
 # thetaSketch aggregators fused into one producer scan with an in-place radix select
 # (engine/device_exec.py PreparedTheta) instead of emitting (key, row) of every selected row
-THETA_FUSED = os.environ.get("SDO_THETA_FUSED", "1") not in ("0", "")
+THETA_FUSED = True
 # GPU-event phase attribution of PreparedQuery.run (scan / merge / gather / finalize)
 PHASE_EVENTS = os.environ.get("SDO_PHASE_EVENTS", "0") not in ("0", "")
 
@@ -1280,8 +1280,6 @@ def shard_window(prog: ScanProgram, ds: DataSource, world: World) -> Optional[Sh
     # (everything up to the agreement below depends on the plan only -- identical on every rank)
     if world is None or not world.distributed or not ds.shard_key or prog.thetas:
         return None
-    if os.environ.get("SDO_NO_SHARD_WINDOW"):
-        return None
     idx = next((i for i, kc in enumerate(prog.keys)
                 if kc.kind == D.K_ID and kc.col == ds.shard_key and kc.orig is None and kc.base == 0), None)
     if idx is None or prog.G < int(os.environ.get("SDO_SHARD_WINDOW_MIN_G", 1 << 16)):
@@ -1610,7 +1608,9 @@ class Engine:
             from ..planner.cost import plan_key_passes
 
             passes = plan_key_passes(pq.scans[0][2])
-            forced = int(os.environ.get("SDO_FORCE_KEY_PASSES", "0")) > 1
+            from ..planner import cost as _cost
+
+            forced = _cost.FORCE_KEY_PASSES > 1
             key = _pass_key(pq.scans[0][1], 2 if forced else 1 << 20) if passes > 1 else None
             if key is not None:
                 return KeyRangePasses(self, qs, ds, key, passes)

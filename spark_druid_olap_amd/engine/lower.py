@@ -14,7 +14,6 @@ This is where Druid's per-segment engine semantics are re-designed for the GPU:
 from __future__ import annotations
 
 import math
-import os
 import re
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
@@ -31,6 +30,10 @@ from ..query.jsfunc import JSError, compile_function, jsagg_to_expr, parse_expr
 from ..segment.datasource import CHUNK_ROWS, DataSource, dtype_code
 from ..segment.dictionary import Dictionary
 from .columns import DictColumn
+
+FD_KEYS = True    # (tests / tools: False keeps functionally dependent keys in the scan)
+FOLD_PRESENCE = True  # (tests: False keeps the separate presence-count slot)
+TRACE_FD = False  # (tools: print every functional-dependency decision)
 
 TIME = "__time"
 HLL_P = 11  # 2048 registers, the precision of Druid's HyperUnique
@@ -1037,7 +1040,7 @@ class Lowerer:
         the LUT and the arithmetic paths agree bit for bit; out-of-span values clamp like the key."""
         ds = self.ds
         u = int(ds.time_unit_ms)
-        if u < 1000 or os.environ.get("SDO_TIME_LUT", "1") == "0":
+        if u < 1000:
             return
         lo, hi = self._data_span([])
         v0, v1 = lo // u, (hi - 1) // u
@@ -1231,7 +1234,7 @@ class Lowerer:
             ast = parse_expr(expr)
             mapping = dict(zip(params, a.fieldNames))
             eops = self._emit_expr(prog, ast, mapping)
-            if op == "sum" and not os.environ.get("SDO_NO_EXACT_SUM"):
+            if op == "sum":
                 ex = self._exact_decimal(ast, mapping)
                 if ex is not None:
                     # exact decimal sum: per-row value * 10^scale rounded to int64 (exact: the bound
@@ -1337,7 +1340,7 @@ class Lowerer:
         unfiltered long sum over a metric whose values are all >= 1 (l_quantity) has exactly that
         property, so it becomes slot 0 and the scan does one atomic less per row (TPC-H Q18 over
         150M order groups: 3 -> 2 HBM atomics per line)."""
-        if os.environ.get("SDO_NO_FOLD_PRESENCE") or len(prog.aops) < 2 or prog.aops[0]["slot"] != 0:
+        if not FOLD_PRESENCE or len(prog.aops) < 2 or prog.aops[0]["slot"] != 0:
             return
         if any(d["slot"] == 0 for d in prog.aops[1:]) or any(a.slot == 0 for a in prog.aggs):
             return  # a user count(*) already shares the presence slot
@@ -1376,7 +1379,7 @@ class Lowerer:
         (``functionalDependencies`` DDL option, ``sd/FunctionalDependencies.scala``); here they
         are verified on the index itself (and across ranks), so no declaration can make results
         wrong."""
-        if os.environ.get("SDO_NO_FD"):
+        if not FD_KEYS:
             return
         cand = [i for i, kc in enumerate(prog.keys) if kc.kind == D.K_ID and kc.card > 1]
         if len(cand) < 2:
@@ -1412,7 +1415,7 @@ class Lowerer:
         ``max(o_totalprice)`` per order, Q10 ``max(c_acctbal)`` per customer) needs no per-row
         accumulator: the value is gathered per result group from an FD table (verified on the
         index, all ranks).  Q18 over 150M order groups: one HBM atomic less per line."""
-        if os.environ.get("SDO_NO_FD") or any(kc.collapse for kc in prog.keys):
+        if not FD_KEYS or any(kc.collapse for kc in prog.keys):
             return
         dets = [i for i, kc in enumerate(prog.keys) if kc.kind == D.K_ID and kc.card > 1]
         if not dets:
@@ -1747,7 +1750,7 @@ def fd_table(ds: DataSource, a: str, b: str, world=None) -> Optional[torch.Tenso
 
     out = lut.to(torch.int32) if bool(ok.item()) else None
     cache[key] = publish(out, dev)
-    if os.environ.get("SDO_TRACE_FD"):
+    if TRACE_FD:
         print(f"[fd] {a} -> {b}: {'yes' if out is not None else 'no'}", flush=True)
     return out
 

@@ -15,7 +15,6 @@ query's (executor._post).
 """
 from __future__ import annotations
 
-import os
 import time
 from typing import Callable, Dict, List, Optional, Tuple
 
@@ -29,7 +28,7 @@ from ..segment.datasource import DataSource
 from .lower import LoweringError
 
 
-_TRACE = bool(os.environ.get("SDO_TRACE_NESTED"))
+_TRACE = False  # (tools: print the nested-level plans)
 
 
 class DeviceColumn:

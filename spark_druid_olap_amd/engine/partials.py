@@ -165,7 +165,7 @@ def _fetch_small(acc: torch.Tensor, hll: List[torch.Tensor], G: int, p: int,
 
 
 _INT_T = ("tinyint", "smallint", "int", "bigint")
-_NO_DEVICE_DECODE = bool(__import__("os").environ.get("SDO_NO_DEVICE_DECODE"))
+_NO_DEVICE_DECODE = False  # (tests / tools: decode every result column on the host)
 _I32 = (-(1 << 31), (1 << 31) - 1)
 
 
@@ -506,10 +506,11 @@ def finalize(prog, parts: Partials, out_types: Optional[Dict[str, str]] = None,
                 if parts.status_dev is not None:
                     sts = host.pop()
                     parts.status_dev = None
-                    if sts.any():
-                        from ..parallel.p2p import raise_status
+                    from ..parallel.p2p import note_ok, raise_status
 
+                    if sts.any():
                         raise_status(sts.tolist(), parts.status_rank)
+                    note_ok(parts.status_rank)
             else:
                 if want_est and parts.acc.is_cuda:
                     from ..ops import native

@@ -16,7 +16,7 @@ from typing import Optional
 
 HERE = Path(__file__).resolve().parent
 CSRC = HERE / "csrc"
-ARCH = os.environ.get("SDO_OFFLOAD_ARCH", "gfx950")
+ARCH = "gfx950"
 
 SOURCES = ["olap_scan.hip", "post_scan.hip", "sketch.hip", "partition.hip", "p2p.hip", "bindings.cpp"]
 

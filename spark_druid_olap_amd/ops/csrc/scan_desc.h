@@ -198,13 +198,16 @@ struct ScanDesc {
   int64_t bm_stride[MAX_BM];
   int64_t bm_count[MAX_BM];
   // radix-partitioned group-by (mode M_PART, partition.hip): the scan emits records instead of
-  // updating a table.  part_counts is [part_n][gridDim.x] (count pass), part_base [part_n + 1]
-  // (scatter pass: bucket p of block b starts at part_base[p] + part_counts[p][b]).
+  // updating a table.  part_recs: record storage (chunk c owns records [4096 c, 4096 c + 4096));
+  // part_counts: each chunk's record end offset, stored at the chunk's position in workgroup order
+  // (the chunks of producer block 0, then block 1, ...: ops/jit.py part_positions); part_base,
+  // when set: the level-1 bucket histogram [part_n][gridDim.x] of the records each producer block
+  // appended -- the split's count pass is then skipped.
   uint64_t part_recs;
   uint64_t part_counts;
   uint64_t part_base;
-  int32_t part_shift;     // bucket = key >> part_shift
-  int32_t part_n;         // buckets (LDS counters)
+  int32_t part_shift;     // level-1 bucket = (record key >> part_shift) & (part_n - 1)
+  int32_t part_n;         // level-1 buckets (a power of two <= PART_HIST_BUCKETS)
 };
 
 // Fields of a partition record (partition.hip part_agg_kernel): value j is width[j] u32 words

@@ -83,8 +83,25 @@ def col_infos(prog) -> Dict[int, ColInfo]:
     return out
 
 
-JIT_LITERALS = os.environ.get("SDO_JIT_LITERALS", "0") != "0"
+JIT_LITERALS = False  # (tools: literal-specialized shape kernels from the first compile)
 PART_MAX_BUCKETS = 1024  # level-1 buckets of the partitioned group-by (split kernel LDS cursors)
+PART_HIST_BYTES = 4 * PART_MAX_BUCKETS  # (sdo_device.h PART_HIST_BUCKETS counters)
+
+
+def part_positions(nch: int, grid: int):
+    """(number of positions, position of every chunk) in producer-workgroup order: the M_PART
+    producer deals chunk c to wave c mod (grid x W), and block b's waves own the positions
+    [b x S, (b + 1) x S) with S = ceil(nch / (grid x W)) x W -- chunk j x grid x W + b x W + v at
+    b x S + j x W + v, the unused ones empty.  The level-1 split with grid blocks over the positions
+    then gives block b exactly producer block b's records: the slice its histogram counted."""
+    import numpy as np
+
+    TW = grid * W
+    per = -(-nch // TW) * W
+    c = np.arange(nch, dtype=np.int64)
+    gw = c % TW
+    pos = (gw // W) * per + (c // TW) * W + gw % W
+    return grid * per, pos
 
 
 def part_fields(prog, cols=None) -> List[Tuple[int, int]]:
@@ -178,15 +195,15 @@ def part_eligible(prog) -> bool:
 
 # accumulator copies per wave for tiny dense key spaces (lanes l, l+C, l+2C.. share copy l % C; up
 # to 64 = lane-private, no same-address LDS atomics) -- the LDS budget may halve it
-MAX_NCOPY = int(os.environ.get("SDO_JIT_NCOPY", "16"))
+MAX_NCOPY = 16
 # whole-chunk fast path: a chunk entirely inside the scan's row range with no chunk-level bitmap
 # prefilter walks its 64 words in order (every word's row mask all ones, then refined by the
 # per-row filter) instead of the find-first-set / readlane chain over its non-empty words
-FULL_CHUNKS = os.environ.get("SDO_JIT_FULL", "1") != "0"
+FULL_CHUNKS = True
 # a prefiltered chunk with at least this many non-empty words (of 64) also walks them in order,
 # reading each word's mask by lane index (independent readlanes) and skipping all-empty steps;
 # sparser chunks take the find-first-set chain over their non-empty words only (0: always chain)
-DENSE_WORDS = int(os.environ.get("SDO_JIT_DENSE_WORDS", "48"))
+DENSE_WORDS = 48
 DENSE_WORDS_PACKED = 16  # (the same switch for kernels reading lane-interleaved packed columns)
 # Count-only scans of tiny dense key spaces (TPC-H "Ship Date Range": count(*) by l_returnflag,
 # l_linestatus over 150M rows) count in registers: per slot one 64-bit word of eight 8-bit fields,
@@ -212,7 +229,7 @@ def count_regs(prog, mode: int) -> bool:
 # kernel instead of compiling one per binding (~300 ms each, the BI plan's cold-start tail).  The
 # exact count stays in the descriptor (d->G bounds the flush), and the class is used only when it
 # keeps the same number of per-wave copies within the same LDS budget.
-G_CLASS = os.environ.get("SDO_JIT_G_CLASS", "1") != "0"
+G_CLASS = True
 
 
 def layout(prog, mode: int, U: int, hll_lds: bool, m: int, budget: int = 150 * 1024,
@@ -246,6 +263,8 @@ def _layout(prog, mode: int, U: int, hll_lds: bool, m: int, budget: int, regstag
         # ONE table per workgroup; lanes hitting the same group serialize in the LDS atomic unit,
         # which is still far cheaper than contending HBM atomics on a few hundred hot addresses
         acc_bytes = G * prog.nslots * 8
+    elif mode == D.M_PART:
+        acc_bytes = PART_HIST_BYTES  # the level-1 bucket histogram (sdo_device.h part_hist_add)
     elif mode == D.M_DENSE_LDS:
         base = G * prog.nslots * 8 * W
         ncopy = MAX_NCOPY
@@ -553,14 +572,16 @@ class _Gen:
         fields = part_fields(p, self.cols)
         hdr = part_record_words(p)
         rw = hdr + sum(w for _, w in fields) + part_hll_count(p)
-        body.append("        if (mine) {")
-        body.append(f"          uint32_t* o_ = precs + (uint64_t)(cbase + woff + (uint32_t)__popcll(am_ & lmlt)) * {rw}u;")
         if hdr == 3:
             # 64-bit key: partitioned by the top bits of a multiplicative hash
-            body.append("          o_[0] = (uint32_t)(((uint64_t)key * 0x9E3779B97F4A7C15ull) >> 32);")
-            body.append("          o_[1] = (uint32_t)key; o_[2] = (uint32_t)((uint64_t)key >> 32);")
+            body.append("        const uint32_t pk_ = (uint32_t)(((uint64_t)key * 0x9E3779B97F4A7C15ull) >> 32);")
         else:
-            body.append("          o_[0] = (uint32_t)key;")
+            body.append("        const uint32_t pk_ = (uint32_t)key;")
+        body.append("        if (mine) {")
+        body.append(f"          uint32_t* o_ = precs + (uint64_t)(cbase + woff + (uint32_t)__popcll(am_ & lmlt)) * {rw}u;")
+        body.append("          o_[0] = pk_;")
+        if hdr == 3:
+            body.append("          o_[1] = (uint32_t)key; o_[2] = (uint32_t)((uint64_t)key >> 32);")
         w = hdr
         fi = 0
         for ai, a in enumerate(p.aops):
@@ -610,6 +631,8 @@ class _Gen:
             body.append(f"          o_[{w}] = {rid};")
             w += 1
         body.append("        }")
+        # (dense keys come in runs: the clustered add; hashes are uniform)
+        body.append(f"        if (phout) part_hist_add(phist, (pk_ >> pshift) & pmask, mine, {'false' if hdr == 3 else 'true'});")
         body.append("        woff += (uint32_t)__popcll(am_);")
 
     def _words_tail(self, fcols, word_filter, mode: int, U: int, stage: List[str], body: List[str],
@@ -854,6 +877,17 @@ class _Gen:
             out.append("  uint32_t* precs = (uint32_t*)d->part_recs;")
             out.append("  uint32_t* pend = (uint32_t*)d->part_counts;  // end offset of each chunk's records")
             out.append("  const uint64_t lmlt = (1ull << lane) - 1ull;")
+            # level-1 bucket histogram of this block's records (sdo_device.h part_hist_add), and
+            # the block's chunk positions in workgroup order (part_positions)
+            out.append("  uint32_t* phist = (uint32_t*)lds;")
+            out.append("  uint32_t* phout = (uint32_t*)d->part_base;")
+            out.append("  const int pshift = d->part_shift;")
+            out.append("  const uint32_t pmask = ((uint32_t)d->part_n - 1u) & (PART_HIST_BUCKETS - 1u);")
+            out.append(f"  for (int i = threadIdx.x; i < PART_HIST_BUCKETS; i += {W * 64}) phist[i] = 0u;")
+            out.append("  __syncthreads();")
+            out.append(f"  const int64_t tw_ = (int64_t)gridDim.x * {W};")
+            out.append(f"  int64_t ppos = (int64_t)blockIdx.x * ((d->total_chunks + tw_ - 1) / tw_) * {W} + wave;"
+                       f"  // += {W} per chunk")
         if mode == D.M_DENSE_LDS:
             out.append(f"  for (int i = threadIdx.x; i < {GL * NS * NCT}; i += {W * 64}) {{")
             inits = ", ".join(_lit(init) for _, init in p.slots)
@@ -875,7 +909,9 @@ class _Gen:
         if mode == D.M_PART:
             out.append(f"    const uint32_t cbase = (uint32_t)c * {D.CHUNK_ROWS}u;")
             out.append("    uint32_t woff = 0;")
-            out.append("    if (lane == 0) pend[c] = cbase;  // (a skipped chunk holds no records)")
+            out.append("    const int64_t cpos = phout ? ppos : c;  // (emit / theta producers: chunk order)")
+            out.append(f"    ppos += {W};")
+            out.append("    if (lane == 0) pend[cpos] = cbase;  // (a skipped chunk holds no records)")
         out.append("    int r = 0;")
         out.append("    int64_t cc = c;")
         out.append("    while (r < nranges - 1 && cc >= d->ranges[r].nchunks) { cc -= d->ranges[r].nchunks; ++r; }")
@@ -962,7 +998,7 @@ class _Gen:
         if full:
             out.append("    }")
         if mode == D.M_PART:
-            out.append("    if (lane == 0) pend[c] = cbase + woff;")
+            out.append("    if (lane == 0) pend[cpos] = cbase + woff;")
         for s in cslots:  # unpack the chunk's 8-bit fields
             out.append("    " + " ".join(f"cn{s}_{g} += (uint32_t)(pc{s} >> {8 * g}) & 0xffu;" for g in range(G)) +
                        f" pc{s} = 0;")
@@ -1005,6 +1041,12 @@ class _Gen:
                     out.append(f"    for (int i = threadIdx.x; i < (int)d->G * {self.m // 4}; i += {W * 64}) "
                                "hll_merge_word8(g + i, r[i]);")
                     out.append("  }")
+        if mode == D.M_PART:
+            out.append("  if (phout) {  // this block's level-1 histogram: column blockIdx.x of [part_n][gridDim.x]")
+            out.append("    __syncthreads();")
+            out.append(f"    for (int q = threadIdx.x; q <= (int)pmask; q += {W * 64}) "
+                       "phout[(int64_t)q * gridDim.x + blockIdx.x] = phist[q];")
+            out.append("  }")
         out.append("}")
         return "\n".join(out) + "\n"
 

@@ -47,7 +47,7 @@ MAX_RANKS = 8
 MAX_SLOTS = 64
 SOFT_TIMEOUT_S = float(os.environ.get("SDO_P2P_TIMEOUT_S", "0.5"))
 HARD_TIMEOUT_S = float(os.environ.get("SDO_P2P_HARD_TIMEOUT_S", "10"))
-MAX_RETRIES = int(os.environ.get("SDO_P2P_MAX_RETRIES", "3"))
+MAX_RETRIES = 3
 ENABLED = os.environ.get("SDO_P2P_MERGE", "1") != "0"
 
 
@@ -280,16 +280,20 @@ def check_status(part) -> None:
     raise_status(sts.tolist(), part.status_rank)
 
 
+def note_ok(rank: int) -> None:
+    """A completed epoch (every rank reads the same verdicts, so every rank resets together):
+    ``MAX_RETRIES`` counts CONSECUTIVE abandoned epochs -- a few slow statements over a long run do
+    not switch the exchange off for good."""
+    for ex in _EXCHANGES.values():
+        if ex is not None and ex.rank == rank and ex.retries:
+            ex.retries = 0
+
+
 def raise_status(vals: List[int], rank: int) -> None:
     from .fault import STATUS_P2P_TIMEOUT, raise_if_failed
 
     if not any(vals):
-        # a completed epoch (every rank reads the same verdicts, so every rank resets together):
-        # ``MAX_RETRIES`` counts CONSECUTIVE abandoned epochs -- a few slow statements over a long
-        # run do not switch the exchange off for good
-        for ex in _EXCHANGES.values():
-            if ex is not None and ex.rank == rank and ex.retries:
-                ex.retries = 0
+        note_ok(rank)
         return
     if any(vals):
         if any(int(v) == STATUS_P2P_TIMEOUT for v in vals):

@@ -256,14 +256,6 @@ class IssueOrder:
             if not self.cv.wait_for(lambda: not self.active or min(self.active) >= seq, timeout=timeout_s):
                 raise RuntimeError(f"statement {seq}: earlier statements {sorted(self.active)[:4]} never finished")
             if self.log is not None:
-                if os.environ.get("SDO_ORDER_DEBUG"):
-                    import threading
-                    import traceback
-
-                    st = traceback.extract_stack(limit=10)
-                    with open(f"{os.environ['SDO_ORDER_DEBUG']}.{os.environ.get('RANK')}", "a") as f:
-                        f.write(f"{seq} {threading.current_thread().name} "
-                                f"{' '.join(x.name + ':' + str(x.lineno) for x in st[:-3])}\n")
                 self.log.append(seq)
 
 

@@ -18,7 +18,6 @@ kernel, so the decisions are different, but the estimation machinery is the same
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -292,21 +291,21 @@ BLOCK_WAVES = 8                                             # 512-thread workgro
 # per-wave accumulator copies + HLL registers of one workgroup: 64 KiB leaves room for the staging
 # planes and keeps 2 workgroups (16 waves) resident in a CU's 160 KiB (LDS_PER_CU); the scan is
 # latency-bound below 8 waves per CU
-PLAN_LDS_BUDGET = int(os.environ.get("SDO_LDS_BUDGET", 64 * 1024))
-SHARED_LDS_MAX = int(os.environ.get("SDO_SHARED_LDS_MAX", 112 * 1024))
-SHARED_MIN_GROUPS = int(os.environ.get("SDO_SHARED_MIN_GROUPS", 512))
-DENSE_MAX_MULTI = int(os.environ.get("SDO_DENSE_MAX_BYTES", 128 << 20))     # dense partials merged whole
-DENSE_MAX_SPARSE_MULTI = int(os.environ.get("SDO_DENSE_MAX_SPARSE", 4 << 30))  # touched rows only
-DENSE_MAX_1GPU = int(os.environ.get("SDO_DENSE_MAX_1GPU", 16 << 30))
-TOUCH_MIN_G = int(os.environ.get("SDO_TOUCH_MIN_G", 1 << 20))
+PLAN_LDS_BUDGET = 64 * 1024
+SHARED_LDS_MAX = 112 * 1024
+SHARED_MIN_GROUPS = 512
+DENSE_MAX_MULTI = 128 << 20       # dense partials merged whole
+DENSE_MAX_SPARSE_MULTI = 4 << 30  # touched rows only
+DENSE_MAX_1GPU = 16 << 30
+TOUCH_MIN_G = 1 << 20
 PROBE_S = 1.0e-9        # hash-table insert (CAS probe + key compare) per qualifying row
 # Random read-modify-write atomics into a table beyond the L2: ~16-20 G updates/s on MI355X whether
 # the table sits in HBM or in the Infinity Cache (TPC-H Q18 at SF100: 600M updates, 29 ms; see the
 # KEY_PASSES note below) -- each update is its own cache-line transaction.
-ATOMIC_RATE = float(os.environ.get("SDO_ATOMIC_RATE", 18e9))
+ATOMIC_RATE = 18e9
 L2_TABLE_BYTES = 4 << 20   # one XCD's L2: tables this small take their atomics in cache
-PARTITIONED = os.environ.get("SDO_PARTITIONED", "1") != "0"
-FORCE_PARTITIONED = os.environ.get("SDO_FORCE_PARTITIONED", "0") != "0"  # tests: any eligible HBM-table plan
+PARTITIONED = True
+FORCE_PARTITIONED = False  # (tests: any eligible HBM-table plan)
 ONESHOT_MAX_BYTES = 256 << 20   # gather buffer (world x state) ceiling for the one-shot merge
 
 
@@ -349,9 +348,9 @@ def plan_groupby(prog, jit: bool, local: bool) -> GroupByPlan:
         return GroupByPlan("dense-lds", shared=True, reason="shared LDS table")
     # HBM table vs hash table: priced
     presence = bool(jit and local and getattr(prog, "presence_only", False) and ns == 1 and not prog.nhll
-                    and not empty and not os.environ.get("SDO_NO_PRES_BYTES"))
+                    and not empty)
     touch = bool(jit and not presence and not prog.nhll and not empty and G >= TOUCH_MIN_G
-                 and not os.environ.get("SDO_NO_TOUCH"))
+                 )
     table = G * ns * 8 + hll_bytes
     est_rows = max(1.0, float(getattr(prog, "est_rows", G)))
     if touch and local and est_rows >= G:
@@ -443,12 +442,13 @@ class MergePlan:
 
 
 MALL_BYTES = 256 << 20  # MI355X Infinity Cache (last level, shared by the XCDs)
-PASS_TABLE_BYTES = int(os.environ.get("SDO_PASS_TABLE_BYTES", 96 << 20))
+PASS_TABLE_BYTES = 96 << 20
 # Measured on MI355X (tools/sql_probe.py, TPC-H Q18 at SF100): 12 cache-sized passes run 2.9 ms of
 # scan each -- the random-atomic rate into a 100 MB Infinity-Cache-resident table (~17 G/s) is no
 # better than into the 1.2 GB HBM table (~16 G/s), and every pass repeats compaction / HAVING /
-# key decoding: 130 ms vs 41 ms single-pass.  Kept as an opt-in plan (SDO_KEY_PASSES=1).
-KEY_PASSES = os.environ.get("SDO_KEY_PASSES", "0") != "0"
+# key decoding: 130 ms vs 41 ms single-pass.  Kept as an opt-in plan (KEY_PASSES = True).
+KEY_PASSES = False
+FORCE_KEY_PASSES = 0  # (tests: this many passes for any groupBy)
 
 
 def plan_key_passes(prep) -> int:
@@ -459,7 +459,7 @@ def plan_key_passes(prep) -> int:
     streaming bandwidth) and its atomics hit the 256 MB Infinity Cache.  Returns P (1 = no split)."""
     from ..ops import desc as D
 
-    forced = int(os.environ.get("SDO_FORCE_KEY_PASSES", "0"))  # tests: split any groupBy
+    forced = FORCE_KEY_PASSES  # (tests: split any groupBy)
     if forced > 1:
         return forced
     if not KEY_PASSES or prep is None or getattr(prep, "mode", None) != D.M_DENSE_GLOBAL:

@@ -18,17 +18,16 @@ kernels compute per row (``ops/reference.py:hll_update_values``), so registers -
 and cross-GPU merges built from them -- do not change."""
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
 
-ENABLED = os.environ.get("SDO_HLL_CODES", "1") != "0"
+ENABLED = True
 MAX_P = 11            # bucket (p bits) + rho (5 bits) in 16
 MIN_ID_BYTES = 2      # byte-wide dimensions read no fewer bytes through a u16 plane
 CHUNK = 1 << 24       # rows per build step (bounded int64 temporaries)
 # total bytes of code planes per datasource (HBM is 288 GB; SF100's o_orderkey plane is 1.2 GB)
-MAX_BYTES = int(float(os.environ.get("SDO_HLL_CODE_MAX_GB", "16")) * (1 << 30))
+MAX_BYTES = 16 << 30
 
 
 def code_name(col: str, p: int, salt: int) -> str:

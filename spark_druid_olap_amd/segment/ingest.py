@@ -540,7 +540,7 @@ def ingest(spec, device="cpu", rank: int = 0, world: int = 1, data: Optional[pd.
     parses only its share of the input blocks (block i -> rank i mod N), the dimension
     dictionaries are unified across ranks, and the raw rows travel to their hash-partition owner
     in one all-to-all before rollup -- each rank parses and rolls up 1/N of the input instead of
-    all of it.  ``SDO_INGEST_SPLIT=0`` restores parse-everything-keep-my-partition."""
+    all of it."""
     if not isinstance(spec, IndexSpec):
         spec = IndexSpec.parse(spec, data_dir)
     dev = torch.device(device)
@@ -548,7 +548,7 @@ def ingest(spec, device="cpu", rank: int = 0, world: int = 1, data: Optional[pd.
         from ..parallel import world as W_
 
         comm = W_._WORLD if W_._WORLD is not None and W_._WORLD.size == world and W_._WORLD.rank == rank else None
-    split = comm is not None and world > 1 and comm.distributed and os.environ.get("SDO_INGEST_SPLIT", "1") != "0"
+    split = comm is not None and world > 1 and comm.distributed
     plans = {m["name"]: _metric_plan(m) for m in spec.metrics}
     dims = list(spec.dimensions)
     dim_b: Dict[str, _DimBuilder] = {}

@@ -30,13 +30,12 @@ packed bits.  ``unpack`` is the exact inverse used by the tests.
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 from typing import Optional
 
 import torch
 
-ENABLED = os.environ.get("SDO_PACKED", "1") not in ("0", "")
+ENABLED = True  # (tools / tests: False keeps every scan on the byte-wide columns)
 CHUNK_ROWS = 4096        # ops/desc.py CHUNK_ROWS
 GROUP_WORDS = 32         # words per lane stream
 _PIECE_ROWS = 1 << 26    # packing works through the column in pieces (bounded temporaries)

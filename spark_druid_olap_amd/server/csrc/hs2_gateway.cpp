@@ -67,6 +67,10 @@ int64_t now_ms() {
              std::chrono::system_clock::now().time_since_epoch()).count();
 }
 
+double steady_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 // ------------------------------------------------------------------ writer (big endian)
 struct W {
   std::string b;
@@ -194,6 +198,7 @@ struct Batch {
   std::string error, schema;  // schema: an encoded TTableSchema struct (from Python)
   std::vector<Col> cols;
   int64_t nrows = 0, started = 0, completed = 0;
+  double queued_at = 0.0;  // steady-clock seconds at enqueue (admission wait = pick-up - this)
   int live = 0, cancels = 0;
   bool cancel = false;
 };
@@ -300,6 +305,7 @@ class Gateway {
 
   py::object next_batch(double timeout_s) {
     std::shared_ptr<Batch> b;
+    double waited = 0.0;
     {
       py::gil_scoped_release nogil;
       std::unique_lock<std::mutex> lk(mu_);
@@ -318,12 +324,14 @@ class Gateway {
         }
         b->state = OP_RUNNING;
         b->started = now_ms();
+        waited = steady_s() - b->queued_at;
         ++stats_batches_;
         break;
       }
     }
     if (!b) return py::none();
-    return py::make_tuple(b->id, py::bytes(b->sid), b->stmt);
+    // (id, session, statement, seconds the batch waited in the admission queue)
+    return py::make_tuple(b->id, py::bytes(b->sid), b->stmt, waited);
   }
 
   void finish_batch(int64_t id, py::bytes schema, py::list cols, int64_t nrows, py::object error) {
@@ -690,6 +698,7 @@ class Gateway {
         b->sid = guid->s;
         b->stmt = stmt;
         b->key = key;
+        b->queued_at = steady_s();
         pending_[key] = b;
         queue_.push_back(b);
         running_batches_[b->id] = b;

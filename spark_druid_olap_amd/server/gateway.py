@@ -195,6 +195,10 @@ class NativeHiveServer(HiveThriftServer):
         self._gw = None
         self._stop = threading.Event()
         self._threads: List[threading.Thread] = []
+        # per-statement timeline (tools/concurrency_bench.py --timeline): admission queue, prepare
+        # (lowering / first-seen compile), slot wait, run (host + GPU, lease end synchronised),
+        # encode -- a list of dicts while enabled, None otherwise
+        self.timeline: Optional[list] = None
 
     # ------------------------------------------------------------------ lifecycle
     def start(self) -> "NativeHiveServer":
@@ -265,14 +269,23 @@ class NativeHiveServer(HiveThriftServer):
             b = gw.next_batch(0.25)
             if b is None:
                 continue
-            bid, sid, stmt = b
+            bid, sid, stmt, queued_s = b
             t0 = time.perf_counter()
+            tl = self.timeline
+            rec = {"queue_ms": queued_s * 1e3} if tl is not None else None
             try:
-                names, types, res = self._execute(bid, sid, stmt)
-                self._metrics.record("gateway", (time.perf_counter() - t0) * 1e3, True)
+                names, types, res = self._execute(bid, sid, stmt) if rec is None else \
+                    self._execute(bid, sid, stmt, rec)
+                t1 = time.perf_counter()
+                self._metrics.record("gateway", (t1 - t0) * 1e3, True)
                 schema = encode_schema(names, types)
                 cols = encode_columns(types, res)
                 gw.finish_batch(bid, schema, cols, res.n if hasattr(res, "n") else len(res), None)
+                if rec is not None:
+                    rec["encode_ms"] = (time.perf_counter() - t1) * 1e3
+                    rec["t"] = t0
+                    rec["stmt"] = stmt
+                    tl.append(rec)
             except Exception as e:  # noqa: BLE001  (every attached operation reports it)
                 self._metrics.record("gateway", (time.perf_counter() - t0) * 1e3, False)
                 log.debug("batch %d failed: %s", bid, e)
@@ -281,7 +294,7 @@ class NativeHiveServer(HiveThriftServer):
                 except Exception:  # pragma: no cover
                     log.exception("finish_batch failed")
 
-    def _execute(self, bid: int, sid: bytes, stmt: str):
+    def _execute(self, bid: int, sid: bytes, stmt: str, rec: Optional[dict] = None):
         ent = self.sessions.get(sid)
         if ent is None:
             raise RuntimeError("invalid session")
@@ -298,9 +311,12 @@ class NativeHiveServer(HiveThriftServer):
             # shape use the interpreter kernel) -- before a stream slot is held
             from ..engine.device_exec import async_compile
 
+            tp = time.perf_counter()
             with async_compile():
                 df.prepare()
+            tl = time.perf_counter()
             with sess.engine.coalescer().scheduler.lease():
+                tr = time.perf_counter()
                 try:
                     res = df.run(token=token)  # the executor's columns, encoded without a DataFrame
                 except torch.OutOfMemoryError:
@@ -315,6 +331,10 @@ class NativeHiveServer(HiveThriftServer):
                     count_event("statement_oom_retry")
                     release_device_memory(keep_arena=slot_arena(sess.engine.world.device(), current_slot()))
                     res = df.run(token=token)
+                if rec is not None:
+                    # the slot's stream is synchronised when the lease ends: run = host + GPU
+                    rec.update(prepare_ms=(tl - tp) * 1e3, slot_wait_ms=(tr - tl) * 1e3,
+                               run_ms=(time.perf_counter() - tr) * 1e3)
         return list(df.columns), [t for _, t in df.schema], res
 
 

@@ -13,7 +13,6 @@ rank's shard and merge over RCCL inside the engine, so results are global on eve
 from __future__ import annotations
 
 import json
-import os
 import threading
 from collections import OrderedDict
 import time
@@ -409,7 +408,7 @@ class Session:
                 return self._query(text, st)
         return self._command(text, st)
 
-    PLAN_CACHE_MAX = int(os.environ.get("SDO_PLAN_CACHE_MAX", "4096"))
+    PLAN_CACHE_MAX = 4096
 
     def _plan_key(self, text: str):
         # statements over the d$* metadata views are planned afresh (their rows are the metadata

@@ -4,7 +4,7 @@ Query results are a handful of multi-MB numpy arrays per query (e.g. a 1.2M-grou
 With glibc defaults every such array is its own ``mmap`` and freeing it ``munmap``s and later
 re-faults pages -- a few milliseconds of page-table work billed to whichever query happens to drop
 the previous result.  Raising the mmap threshold to glibc's maximum (32 MB) and disabling heap
-trimming keeps those buffers in the process heap for reuse.  Opt out with ``SDO_NO_MALLOPT=1``."""
+trimming keeps those buffers in the process heap for reuse."""
 from __future__ import annotations
 
 import ctypes
@@ -18,7 +18,7 @@ M_MMAP_THRESHOLD = -3
 
 def tune_host_malloc() -> bool:
     global _DONE
-    if _DONE or os.environ.get("SDO_NO_MALLOPT"):
+    if _DONE:
         return False
     _DONE = True
     try:

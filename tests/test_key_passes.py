@@ -6,6 +6,7 @@ import pytest
 from spark_druid_olap_amd.engine.columns import materialize
 from spark_druid_olap_amd.engine.executor import Engine, KeyRangePasses
 from spark_druid_olap_amd.models import tpch
+from spark_druid_olap_amd.planner import cost
 from spark_druid_olap_amd.query import spec as S
 from spark_druid_olap_amd.session import Session
 
@@ -35,7 +36,7 @@ def _norm(rows):
 @pytest.mark.parametrize("q", [Q18] + OTHERS)
 def test_passes_equal_single_scan(ds_small, df_small, q, monkeypatch):
     want = _sess(ds_small, df_small).sql(q).collect()
-    monkeypatch.setenv("SDO_FORCE_KEY_PASSES", "5")
+    monkeypatch.setattr(cost, "FORCE_KEY_PASSES", 5)
     s = _sess(ds_small, df_small)
     d = s.sql(q)
     got = d.collect()
@@ -50,7 +51,7 @@ def test_passes_equal_single_scan(ds_small, df_small, q, monkeypatch):
 def test_pass_keys_use_a_base_not_a_remap(ds_small, monkeypatch):
     from spark_druid_olap_amd.ops import desc as D
 
-    monkeypatch.setenv("SDO_FORCE_KEY_PASSES", "3")
+    monkeypatch.setattr(cost, "FORCE_KEY_PASSES", 3)
     q = S.GroupByQuerySpec("tpch", [S.DefaultDimensionSpec("o_orderkey")],
                            aggregations=[S.FunctionAggregationSpec("longSum", "q", "l_quantity")],
                            intervals=["1992-01-01/1999-01-01"])
@@ -79,7 +80,7 @@ def test_gpu_passes_equal_single_scan(monkeypatch):
         return s
 
     want = {q: sess().sql(q).collect() for q in [Q18] + OTHERS}
-    monkeypatch.setenv("SDO_FORCE_KEY_PASSES", "4")
+    monkeypatch.setattr(cost, "FORCE_KEY_PASSES", 4)
     s = sess()
     for q in [Q18] + OTHERS:
         got = s.sql(q).collect()

@@ -41,7 +41,9 @@ def test_jit_shared_table_kernel_compiles(tmp_path, monkeypatch):
     from spark_druid_olap_amd.session import Session
 
     monkeypatch.setenv("SDO_JIT_CACHE", str(tmp_path))
-    monkeypatch.setenv("SDO_NO_FOLD_PRESENCE", "1")  # keep the two-slot layout this test sizes
+    from spark_druid_olap_amd.engine import lower as _lower
+
+    monkeypatch.setattr(_lower, "FOLD_PRESENCE", False)  # keep the two-slot layout this test sizes
     ds = ssb.to_datasource(ssb.generate_flat(0.002, "cpu"))
     s = Session(engine=Engine(use_native=False))
     s.register_datasource(ds)
@@ -128,7 +130,7 @@ def test_jit_partition_producers_compile(tmp_path, monkeypatch, ds_small):
     assert [w for _, w in fields] == [0, 1, 1, 1]  # extendedprice: exact i32 cents
     w = jit.JitScan(prog, D.M_PART, 4, False, 2048, True, load=False)
     assert "uint32_t* o_ = precs + (uint64_t)(cbase + woff + (uint32_t)__popcll(am_ & lmlt)) * 4u;" in w.src
-    assert "pend[c] = cbase + woff;" in w.src and "atomic" not in w.src.split("void sdo_jit")[-1]
+    assert "pend[cpos] = cbase + woff;" in w.src and "atomic" not in w.src.split("void sdo_jit")[-1]
 
 
 

@@ -203,6 +203,9 @@ def main():
                     help="jmx workload: CSV binding (models/bi: 'jmeter' reproduces the plan's ccode overwrite)")
     ap.add_argument("--coalesce", default="on", choices=["on", "off"],
                     help="off: every statement executes (identical queued statements are not shared)")
+    ap.add_argument("--timeline", default=None,
+                    help="native server: record every execution's phases (admission queue, prepare, slot wait, "
+                         "run, encode) and write them here; the JSON line gets per-phase percentiles")
     ap.add_argument("--prewarm", type=int, default=0,
                     help="varied workload: plan + compile this many distinct texts before the clock starts")
     a = ap.parse_args()
@@ -246,10 +249,10 @@ def main():
         srv = NativeHiveServer(s, port=0)
         real = srv._execute
 
-        def timed(bid, sid, stmt):
+        def timed(bid, sid, stmt, *rec):
             c0, w0 = time.thread_time(), time.perf_counter()
             try:
-                return real(bid, sid, stmt)
+                return real(bid, sid, stmt, *rec)
             finally:
                 exec_cost.append((time.thread_time() - c0, time.perf_counter() - w0))
 
@@ -293,6 +296,8 @@ def main():
         return co.stats["coalesced"], co.stats["executions"]
 
     time.sleep(max(0.0, t_start - time.time()))
+    if a.timeline and a.server == "native":
+        srv.timeline = []
     cpu0 = time.process_time()
     co0, ex0 = counters()
     sampler = None
@@ -346,7 +351,38 @@ def main():
                       "coalesced": co1 - co0, "slots": co.scheduler.nslots,
                       "slot_wait_ms_total": round(co.scheduler.stats["wait_ms"], 1)},
            "device_memory": _mem_report()}
+    if a.timeline and a.server == "native" and srv.timeline is not None:
+        out["timeline"] = timeline_summary(srv.timeline, a.timeline)
     print(json.dumps(out), flush=True)
+
+
+def timeline_summary(tl, path):
+    """Per-phase percentiles of the server's executions, the phase split of the slowest 1%, and
+    the worst 100 ms windows (executions that started in them and their slowest phase) -- a stall
+    that hits every slot at once shows up as one window with many slow runs."""
+    import math
+
+    tl = list(tl)
+    with open(path, "w") as f:
+        json.dump(tl, f)
+    phases = ("queue_ms", "prepare_ms", "slot_wait_ms", "run_ms", "encode_ms")
+    tot = lambda r: sum(r.get(k, 0.0) for k in phases)  # noqa: E731
+    summ = {k: {"p50": pct([r.get(k, 0.0) for r in tl], 50), "p99": pct([r.get(k, 0.0) for r in tl], 99),
+                "max": max((r.get(k, 0.0) for r in tl), default=None)} for k in phases}
+    slow = sorted(tl, key=tot, reverse=True)[:max(1, len(tl) // 100)]
+    summ["slowest_1pct_mean"] = {k: round(sum(r.get(k, 0.0) for r in slow) / len(slow), 2) for k in phases} \
+        if slow else {}
+    t0 = min((r["t"] for r in tl), default=0.0)
+    win = {}
+    for r in tl:
+        w = int(math.floor((r["t"] - t0) / 0.1))
+        win.setdefault(w, []).append(r)
+    worst = sorted(win.items(), key=lambda kv: max(tot(r) for r in kv[1]), reverse=True)[:5]
+    summ["worst_windows"] = [{"t_s": round(w * 0.1, 1), "n": len(rs), "max_total_ms": round(max(tot(r) for r in rs), 1),
+                              "mean": {k: round(sum(r.get(k, 0.0) for r in rs) / len(rs), 1) for k in phases}}
+                             for w, rs in worst]
+    summ["n"] = len(tl)
+    return summ
 
 
 def _mem_report():

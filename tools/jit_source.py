@@ -45,9 +45,10 @@ def main():
                         "partitioned": D.M_PART}[gp.mode]
                 print(f"==== {name}: G={prog.G} keys={[(k.name, k.kind, k.card) for k in prog.keys]} "
                       f"slots={prog.slots} plan={gp.describe()}")
-                if os.environ.get("SDO_PACKED", "1") != "0":  # bit-packed columns (CPU copies here)
+                from spark_druid_olap_amd.segment import packed as PK
+
+                if PK.ENABLED:  # bit-packed columns (CPU copies here)
                     from spark_druid_olap_amd.engine.lower import column_tensor
-                    from spark_druid_olap_amd.segment import packed as PK
 
                     prog.packed = {}
                     for c in (list(prog.fcols) + list(prog.pcols)) if mode in (D.M_DENSE_LDS, D.M_DENSE_GLOBAL, D.M_HASH) else []:
