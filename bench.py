@@ -155,6 +155,12 @@ def main():
     ctx.__enter__()
     lat = {name: [] for name, _ in queries}
     stats = {name: {} for name, _ in queries}
+    # the serving process's collector settings (server/gateway.py start): everything built so far --
+    # shards, dictionaries, plans -- moves to the permanent generation and young collections come
+    # less often, so a full collection does not walk it in the middle of a query
+    from spark_druid_olap_amd.utils.memory import serving_gc
+
+    serving_gc()
     for _ in range(args.warmup):
         for name, pq in queries:
             pq.run()

@@ -566,6 +566,12 @@ class PreparedScan:
         seg_lo = np.zeros(max(1, npos), dtype=np.int64)
         seg_lo[pos] = np.arange(nch, dtype=np.int64) * D.CHUNK_ROWS
         pb = {
+            # the layout and producer grid these buffers and the descriptor were built for: a run
+            # uses THEM, never the scan's current ones -- another slot running the same prepared
+            # scan may re-layout it (hash overflow, observed group count) or swap in a specialized
+            # kernel with another grid while this run is in flight, and mixing a new bucket count
+            # with these buffers would write past them
+            "L": L, "grid": int(self.grid),
             "cap_words": max(1, cap * L["rw"]), "desc_recs": 0,
             "seg_lo": torch.from_numpy(seg_lo).to(u32).to(dev),
             "pend": torch.zeros(max(1, npos), dtype=u32, device=dev),
@@ -596,8 +602,9 @@ class PreparedScan:
             PART_POOL.release(slab)
 
     def _run_part_on(self, b: "_Bufs", slab: "_Slab") -> Optional[Partials]:
-        L, nat, st = self.part, native.load(), native._stream(self.dev)
+        nat, st = native.load(), native._stream(self.dev)
         pb = dict(b.part)
+        L = pb["L"]
         prog = self.prog
         pb["recs1"], pb["recs2"] = slab.recs1, slab.recs2
         if b.part["desc_recs"] != pb["recs1"].data_ptr():
@@ -605,12 +612,10 @@ class PreparedScan:
             ptr = torch.tensor([pb["recs1"].data_ptr()], dtype=torch.int64).view(torch.uint8)
             b.desc[off:off + 8].copy_(ptr.to(self.dev))
             b.part["desc_recs"] = pb["recs1"].data_ptr()
-        if pb["k1"] != int(self.grid):
-            # (a specialized kernel swapped in with another resident grid: _adopt) the histogram
-            # columns and chunk positions follow the producer's block count
-            self._slots.pop(current_slot(), None)
-            return self._run_part(self._bufs())
-        nat.module_launch(self.jit.handle, b.desc.data_ptr(), int(self.grid), BLOCK, int(self.jit.lay.total), st)
+        # (the grid the histogram columns and chunk positions were laid out for: a kernel swapped in
+        # since, with another resident grid, is still correct at this one -- it loops over chunks)
+        jit = self.jit
+        nat.module_launch(jit.handle, b.desc.data_ptr(), pb["grid"], BLOCK, int(jit.lay.total), st)
         rw, P1, k1 = L["rw"], L["p1"], pb["k1"]
         # level 1: one input group = every chunk region in producer-block order, block k of the
         # split = producer block k's chunks (their level-1 histogram came with the records)
@@ -670,7 +675,7 @@ class PreparedScan:
         """Sparse LDS-hash aggregation of the hash-partitioned records (keys beyond 32 bits).  A
         sub-bucket that held more distinct keys than its table (the planner's group estimate was
         low) makes the whole execution re-partition into 4x more sub-buckets and run again."""
-        L, nat, st, prog = self.part, native.load(), native._stream(self.dev), self.prog
+        L, nat, st, prog = b.part["L"], native.load(), native._stream(self.dev), self.prog
         hv = self.part_having or ([], 1)
         while True:
             acc, keys, cnt, ovf, hll = self._sparse_out(b, "hh_out", True, L.get("nhll", 0))
