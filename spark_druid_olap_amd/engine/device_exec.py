@@ -67,9 +67,12 @@ def _spec_executor():
 
 
 def _spec_job(js):
+    from ..utils.metrics import count_event
+
     try:
         return js.specialized()
     finally:
+        count_event("jit_spec_done")
         with _spec_lock:
             _spec_pending[0] -= 1
 
@@ -174,11 +177,15 @@ def _async_ok(prog, mode: int, shared: bool) -> bool:
 
 
 def _async_job(prog, mode: int, hll_lds: bool, m: int, shared: bool, narrow4: bool, key: str):
+    from ..utils.metrics import count_event
+
     try:
         _jit_select(prog, mode, hll_lds, m, shared, load=False, narrow4=narrow4)
     except BaseException:
         _async_failed.add(key)
         raise
+    finally:
+        count_event("jit_async_done")
 
 
 def _jit_build(prog, mode: int, hll_lds: bool, m: int, shared: bool = False, load: bool = True):
@@ -790,6 +797,9 @@ class PreparedScan:
             _spec_pending[0] += 1
         self._spec_at = 1 << 62
         self._spec_future = _spec_executor().submit(_spec_job, self.jit)
+        from ..utils.metrics import count_event
+
+        count_event("jit_spec_submit")
 
     def _adopt(self, js) -> None:
         """Swap in a kernel of the same layout (the launch arguments cached per slot name the
@@ -807,6 +817,9 @@ class PreparedScan:
                         a[-6] = js.handle  # (jit, desc, grid, block, lds, unroll)
                         a[-4] = int(self.grid)
                         setattr(b, attr, tuple(a))
+        from ..utils.metrics import count_event
+
+        count_event("jit_spec_adopt")
 
     # ------------------------------------------------------------------ run
     def run(self) -> Partials:
@@ -990,6 +1003,9 @@ class PartScratchPool:
                 sl.dev, sl.words, sl.event = str(dev), words, None
                 sl.recs1 = _with_eviction(lambda: torch.empty(words, dtype=torch.int32, device=dev), None, None)
                 sl.recs2 = _with_eviction(lambda: torch.empty(words, dtype=torch.int32, device=dev), None, None)
+                from ..utils.metrics import count_event
+
+                count_event("part_slab_alloc")
             except BaseException:
                 with self.cv:
                     self.total -= need
@@ -1200,6 +1216,9 @@ class SlotArena:
             self.buf = _with_eviction(lambda: torch.empty(cap, dtype=torch.uint8, device=self.dev), None, self.slot,
                                       arena=self)
             self.cap = cap
+            from ..utils.metrics import count_event
+
+            count_event("arena_grow")
         start = self.off
         self.off += nbytes
         end = start + nbytes
@@ -1269,9 +1288,14 @@ def device_memory_report() -> dict:
            "part_scratch_gb": round(PART_POOL.bytes() / g, 3),
            "slot0_bufs_gb": round(_buf_total[0] / g, 3), "events": events()}
     if torch.cuda.is_available():
+        ms = torch.cuda.memory_stats()
         out.update(allocated_gb=round(torch.cuda.memory_allocated() / g, 2),
                    reserved_gb=round(torch.cuda.memory_reserved() / g, 2),
-                   max_allocated_gb=round(torch.cuda.max_memory_allocated() / g, 2))
+                   max_allocated_gb=round(torch.cuda.max_memory_allocated() / g, 2),
+                   # the caching allocator's free-everything-and-retry passes (each frees every cached
+                   # block of every stream: a device-wide stall) and its device allocations / frees
+                   alloc_retries=int(ms.get("num_alloc_retries", 0)), device_allocs=int(ms.get("num_device_alloc", 0)),
+                   device_frees=int(ms.get("num_device_free", 0)))
     return out
 
 

@@ -58,6 +58,7 @@ class Spec:
 
     def copy(self, **changes):
         c = copy.copy(self)
+        c.__dict__.pop("_deferred_memo", None)  # (find_deferred's memo describes the original)
         for k, v in changes.items():
             setattr(c, k, v)
         return c
@@ -348,6 +349,18 @@ class DeferredFilterSpec(Spec):
 
 
 def find_deferred(spec) -> List["DeferredFilterSpec"]:
+    """The DeferredFilterSpecs of a spec tree (memoised on the spec: specs are not mutated once
+    built -- ``copy`` / ``resolve_deferred`` make new ones -- and servers ask for every statement)."""
+    memo = getattr(spec, "__dict__", None)
+    if memo is not None and "_deferred_memo" in memo:
+        return list(memo["_deferred_memo"])
+    out = _find_deferred(spec)
+    if memo is not None:
+        memo["_deferred_memo"] = tuple(out)
+    return out
+
+
+def _find_deferred(spec) -> List["DeferredFilterSpec"]:
     out: List[DeferredFilterSpec] = []
 
     def go(v):

@@ -199,6 +199,13 @@ class NativeHiveServer(HiveThriftServer):
         # (lowering / first-seen compile), slot wait, run (host + GPU, lease end synchronised),
         # encode -- a list of dicts while enabled, None otherwise
         self.timeline: Optional[list] = None
+        # stall watchdog (with the timeline): when no execution has finished for STALL_S while some
+        # are running, the Python stacks of the executor and compile threads -- where a device-wide
+        # pause (allocator free-all, code-object load, a lock) holds every slot at once
+        self.stalls: Optional[list] = None
+        self._busy = 0
+        self._busy_lock = threading.Lock()
+        self._last_done = time.perf_counter()
 
     # ------------------------------------------------------------------ lifecycle
     def start(self) -> "NativeHiveServer":
@@ -215,6 +222,9 @@ class NativeHiveServer(HiveThriftServer):
             t = threading.Thread(target=self._executor, daemon=True, name=f"hs2-exec-{i}")
             t.start()
             self._threads.append(t)
+        t = threading.Thread(target=self._watchdog, daemon=True, name="hs2-stall-watchdog")
+        t.start()
+        self._threads.append(t)
         log.info("HiveServer2 endpoint (native gateway) on %s:%d, %d executors", self.host, self.port, self.nexec)
         return self
 
@@ -273,6 +283,8 @@ class NativeHiveServer(HiveThriftServer):
             t0 = time.perf_counter()
             tl = self.timeline
             rec = {"queue_ms": queued_s * 1e3} if tl is not None else None
+            with self._busy_lock:
+                self._busy += 1
             try:
                 names, types, res = self._execute(bid, sid, stmt) if rec is None else \
                     self._execute(bid, sid, stmt, rec)
@@ -293,6 +305,38 @@ class NativeHiveServer(HiveThriftServer):
                     gw.finish_batch(bid, b"", [], 0, f"{type(e).__name__}: {e}")
                 except Exception:  # pragma: no cover
                     log.exception("finish_batch failed")
+            finally:
+                with self._busy_lock:
+                    self._busy -= 1
+                    self._last_done = time.perf_counter()
+
+    STALL_S = 0.4
+
+    def _watchdog(self):
+        import sys
+        import traceback
+
+        armed = True
+        while not self._stop.wait(0.02):
+            st = self.stalls
+            if st is None:
+                continue
+            idle = time.perf_counter() - self._last_done
+            if self._busy <= 0 or idle < self.STALL_S:
+                armed = True
+                continue
+            if not armed or len(st) >= 16:
+                continue
+            armed = False  # one capture per stall
+            names = {t.ident: t.name for t in threading.enumerate()}
+            stacks = {}
+            for ident, fr in sys._current_frames().items():
+                name = names.get(ident, "")
+                if name.startswith(("hs2-exec", "sdo-jit")):
+                    stacks[name] = [f"{os.path.basename(f.filename)}:{f.lineno} {f.name}"
+                                    for f in traceback.extract_stack(fr)[-10:]]
+            st.append({"t": time.perf_counter(), "idle_ms": round(idle * 1e3, 1), "busy": self._busy,
+                       "stacks": stacks})
 
     def _execute(self, bid: int, sid: bytes, stmt: str, rec: Optional[dict] = None):
         ent = self.sessions.get(sid)
@@ -303,7 +347,10 @@ class NativeHiveServer(HiveThriftServer):
             df, pdf = self.spmd.execute(sid, stmt, {}, None)
             return list(df.columns), [t for _, t in df.schema], pdf
         sess = ent["session"]
+        ts = time.perf_counter()
         df = sess.sql(stmt)
+        if rec is not None:
+            rec["sql_ms"] = (time.perf_counter() - ts) * 1e3
         if df.plan is None:  # a command that looked like a query: already executed
             res = df.to_pandas()
         else:
@@ -312,6 +359,9 @@ class NativeHiveServer(HiveThriftServer):
             from ..engine.device_exec import async_compile
 
             tp = time.perf_counter()
+            # (timeline: the caching allocator's free-everything-and-retry count around the statement
+            # -- a retry frees every cached block of every stream, a device-wide stall)
+            ar0 = _alloc_retries() if rec is not None else 0
             with async_compile():
                 df.prepare()
             tl = time.perf_counter()
@@ -334,8 +384,12 @@ class NativeHiveServer(HiveThriftServer):
                 if rec is not None:
                     # the slot's stream is synchronised when the lease ends: run = host + GPU
                     rec.update(prepare_ms=(tl - tp) * 1e3, slot_wait_ms=(tr - tl) * 1e3,
-                               run_ms=(time.perf_counter() - tr) * 1e3)
+                               run_ms=(time.perf_counter() - tr) * 1e3, alloc_retries=_alloc_retries() - ar0)
         return list(df.columns), [t for _, t in df.schema], res
+
+
+def _alloc_retries() -> int:
+    return int(torch.cuda.memory_stats().get("num_alloc_retries", 0)) if torch.cuda.is_available() else 0
 
 
 def make_server(session, host: str = "127.0.0.1", port: int = 10000, world=None, native: Optional[bool] = None):

@@ -132,9 +132,12 @@ class DataFrame:
         prepared when they run.  One process only: several ranks prepare in broadcast order
         (server/spmd.py prepare_statement)."""
         if self.plan is not None and not self.session.engine.world.distributed:
-            for dq in P.find_all_deep(self.plan, P.DruidQuery):
-                if not S.find_deferred(dq.spec):
-                    self.session.prepare_druid(dq)
+            dqs = self.__dict__.get("_known_dqs")
+            if dqs is None:  # (the plan is fixed: walk it once per cached statement)
+                dqs = self._known_dqs = [dq for dq in P.find_all_deep(self.plan, P.DruidQuery)
+                                         if not S.find_deferred(dq.spec)]
+            for dq in dqs:
+                self.session.prepare_druid(dq)
         return self
 
     def _root_only_safe(self) -> bool:
@@ -576,6 +579,9 @@ class Session:
                             lambda: self.engine.prepare(run_spec, ds, dq.info.get("historical")))
                     if pending:
                         prep.jit_pending = pending
+                    from .utils.metrics import count_event
+
+                    count_event("plan_prepare")
                     # output SQL types: large results decode numeric dictionary keys on the device
                     # (and integer outputs of string-valued extractions: 'yyyy' time formats)
                     prep.out_types = {n: t for n, t, k in dq.columns

@@ -21,10 +21,28 @@ _events: Dict[str, int] = {}
 _events_lock = threading.Lock()
 
 
+_event_log: list = []
+_event_log_on = [False]
+
+
 def count_event(name: str, n: int = 1) -> None:
-    """Process-wide event counter (device-memory releases, statement retries, P2P fallbacks)."""
+    """Process-wide event counter (device-memory releases, statement retries, P2P fallbacks, plan
+    and kernel swaps).  With ``log_events(True)`` every event is also kept with its time
+    (``time.perf_counter``): the serving timeline lines them up with stalls."""
     with _events_lock:
         _events[name] = _events.get(name, 0) + n
+        if _event_log_on[0] and len(_event_log) < 100_000:
+            _event_log.append((time.perf_counter(), name))
+
+
+def log_events(on: bool) -> list:
+    """Start (clearing) or stop the timed event log; returns the events logged so far."""
+    with _events_lock:
+        out = list(_event_log)
+        if on:
+            _event_log.clear()
+        _event_log_on[0] = on
+        return out
 
 
 def events() -> Dict[str, int]:

@@ -282,6 +282,12 @@ def main():
             # (progress on stderr: a long warm-up -- first-seen shapes compile -- stays visibly alive)
             print(f"[conc] warm {i + 1}/{len(warm)} {name[:40]} {time.time() - tw:.2f}s", file=sys.stderr, flush=True)
     interval = (a.clients / a.qps) if a.qps > 0 else 0.0
+    if a.timeline and a.server == "native":
+        # (from the open loop's start: its warm-up seconds -- negative times -- included)
+        from spark_druid_olap_amd.utils.metrics import log_events
+
+        log_events(True)
+        srv.stalls = []
     t_start = time.time() + 1.0 + a.warmup
     for _ in ps:
         start_q.put((srv.port, t_start - a.warmup, a.duration + a.warmup, interval))
@@ -353,6 +359,17 @@ def main():
            "device_memory": _mem_report()}
     if a.timeline and a.server == "native" and srv.timeline is not None:
         out["timeline"] = timeline_summary(srv.timeline, a.timeline)
+        t0 = min((r["t"] for r in srv.timeline), default=0.0)
+        ev = log_events(False)
+        out["stalls"] = [dict(s, t=round(s["t"] - t0, 3),
+                              events=[(round(t - t0, 3), n) for t, n in ev if s["t"] - s["idle_ms"] / 1e3 - 0.2 <= t <= s["t"]][:40])
+                         for s in (srv.stalls or [])]
+        evc = {}
+        for _, n in ev:
+            evc[n] = evc.get(n, 0) + 1
+        out["timeline"]["events"] = evc
+        with open(a.timeline + ".events.json", "w") as f:
+            json.dump([(round(t - t0, 4), n) for t, n in ev], f)
     print(json.dumps(out), flush=True)
 
 
@@ -365,7 +382,8 @@ def timeline_summary(tl, path):
     tl = list(tl)
     with open(path, "w") as f:
         json.dump(tl, f)
-    phases = ("queue_ms", "prepare_ms", "slot_wait_ms", "run_ms", "encode_ms")
+    phases = ("queue_ms", "sql_ms", "prepare_ms", "slot_wait_ms", "run_ms", "encode_ms")
+    retried = [r for r in tl if r.get("alloc_retries")]
     tot = lambda r: sum(r.get(k, 0.0) for k in phases)  # noqa: E731
     summ = {k: {"p50": pct([r.get(k, 0.0) for r in tl], 50), "p99": pct([r.get(k, 0.0) for r in tl], 99),
                 "max": max((r.get(k, 0.0) for r in tl), default=None)} for k in phases}
@@ -382,6 +400,10 @@ def timeline_summary(tl, path):
                               "mean": {k: round(sum(r.get(k, 0.0) for r in rs) / len(rs), 1) for k in phases}}
                              for w, rs in worst]
     summ["n"] = len(tl)
+    # statements during which the caching allocator freed every cached block and retried
+    summ["alloc_retry_statements"] = [{"t_s": round(r["t"] - t0, 3), "retries": r["alloc_retries"],
+                                       "run_ms": round(r.get("run_ms", 0.0), 1), "stmt": r["stmt"][:80]}
+                                      for r in sorted(retried, key=lambda r: r["t"])[:20]]
     return summ
 
 
