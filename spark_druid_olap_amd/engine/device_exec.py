@@ -148,6 +148,20 @@ ASYNC_JIT_WORKERS = 4
 _async_tls = threading.local()
 _async_failed: set = set()
 _async_pool: list = []
+_async_futs: list = []  # background compiles not known to be finished (wait_background_compiles)
+
+
+def wait_background_compiles(timeout: float = 120.0) -> int:
+    """Block until the first-seen-shape compiles started so far have finished (a server's warm-up:
+    the interim plans they belong to re-prepare at their next run); returns how many were waited
+    for."""
+    import concurrent.futures as cf
+
+    with _spec_lock:
+        futs = [f for f in _async_futs if not f.done()]
+    if futs:
+        cf.wait(futs, timeout=timeout)
+    return len(futs)
 
 
 @contextlib.contextmanager
@@ -209,7 +223,10 @@ def _jit_build(prog, mode: int, hll_lds: bool, m: int, shared: bool = False, loa
                                                           thread_name_prefix="sdo-jit-async"))
                 # (a snapshot: the prepare goes on to mark the program for the interpreter)
                 snap = copy.copy(prog)
-                pend.append(_async_pool[0].submit(_async_job, snap, mode, hll_lds, m, shared, narrow4, e.key))
+                fut = _async_pool[0].submit(_async_job, snap, mode, hll_lds, m, shared, narrow4, e.key)
+                pend.append(fut)
+                with _spec_lock:
+                    _async_futs[:] = [f for f in _async_futs if not f.done()] + [fut]
                 from ..utils.metrics import count_event
 
                 count_event("jit_async_interim")
@@ -966,6 +983,7 @@ class PartScratchPool:
         self.free: List[_Slab] = []
         self.total = 0
         self.held = threading.local()
+        self.peak_words: dict = {}  # device -> largest slab asked for (presize)
 
     def _budget(self, dev) -> int:
         if PART_SCRATCH_BUDGET > 0:
@@ -982,6 +1000,8 @@ class PartScratchPool:
         need = 2 * words * 4
         depth = getattr(self.held, "n", 0)
         with self.cv:
+            if words > self.peak_words.get(str(dev), 0):
+                self.peak_words[str(dev)] = words
             while True:
                 fit = [x for x in self.free if x.dev == str(dev) and x.words >= words]
                 if fit:
@@ -1032,6 +1052,37 @@ class PartScratchPool:
         with self.cv:
             self.free.append(sl)
             self.cv.notify_all()
+
+    def presize(self, dev, nslots: int) -> int:
+        """Free slabs of the largest size acquired so far until ``nslots`` of them exist (or the
+        budget is spent); returns how many were added.  (Warm-up only: no slab is held.)"""
+        from ..utils.metrics import count_event
+
+        words = self.peak_words.get(str(dev), 0)
+        if words <= 0:
+            return 0
+        added = 0
+        with self.cv:
+            keep = []
+            for x in self.free:
+                if x.dev == str(dev) and x.words < words:
+                    self.total -= 2 * x.words * 4  # too small for the largest run: replaced below
+                else:
+                    keep.append(x)
+            self.free = keep
+            have = sum(1 for x in self.free if x.dev == str(dev))
+            while have < nslots and self.total + 2 * words * 4 <= self._budget(dev):
+                sl = _Slab()
+                sl.dev, sl.words, sl.event = str(dev), words, None
+                sl.recs1 = torch.empty(words, dtype=torch.int32, device=dev)
+                sl.recs2 = torch.empty(words, dtype=torch.int32, device=dev)
+                self.total += 2 * words * 4
+                self.free.append(sl)
+                have += 1
+                added += 1
+                count_event("part_slab_presize")
+            self.cv.notify_all()
+        return added
 
     def clear(self) -> None:
         with self.cv:
@@ -1209,8 +1260,14 @@ class SlotArena:
         self.need += nbytes
         if self.off + nbytes > self.cap:
             # the earlier scans of this statement keep the old storage alive through their views;
-            # the next statement on the slot fits the new one whole
-            cap = max(ARENA_MIN, 2 * self.cap, self.need)
+            # the next statement on the slot fits the new one whole.  Every slot runs every kind of
+            # statement sooner or later: a growing arena goes straight to the largest peer's size
+            # (one growth per slot, not a doubling series whose dropped steps stay in the caching
+            # allocator's per-stream pools until a free-everything retry)
+            peer = 0
+            if _ARENAS.get((str(self.dev), self.slot)) is self:
+                peer = max((a.cap for k, a in list(_ARENAS.items()) if k[0] == str(self.dev)), default=0)
+            cap = max(ARENA_MIN, 2 * self.cap, self.need, peer)
             cap = (cap + ARENA_MIN - 1) // ARENA_MIN * ARENA_MIN
             self._drop()
             self.buf = _with_eviction(lambda: torch.empty(cap, dtype=torch.uint8, device=self.dev), None, self.slot,
@@ -1270,6 +1327,42 @@ def slot_arena(dev, slot: int) -> SlotArena:
         with _arena_lock:
             ar = _ARENAS.setdefault(k, SlotArena(dev, slot))
     return ar
+
+
+def presize_device_memory(dev=None, nslots: int = 0) -> dict:
+    """Server warm-up: grow every slot arena (1..``nslots``) to the largest one's size and fill the
+    partition scratch pool to one slab per slot at its largest slab, then hand the caching
+    allocator's free blocks -- the growth steps the warm-up statements left in per-stream pools --
+    back to the device.  After this a warmed statement mix carves from storage that exists: no
+    arena grows, no slab is allocated and the allocator never reaches the device cap and frees
+    everything mid-service (a free-all retry synchronises the device under the allocator's lock
+    while the allocating thread holds the GIL: every slot stalls for 1-2 s --
+    profiles/r6/thrift_jmx_q250_stalls.md).  Call it with no statement running (the arenas'
+    storages are replaced)."""
+    from ..utils.metrics import count_event
+
+    if not torch.cuda.is_available():
+        return {}
+    dev = torch.device(dev) if dev is not None else torch.device("cuda", torch.cuda.current_device())
+    mine = [a for k, a in list(_ARENAS.items()) if k[0] == str(dev)]
+    peak = max((a.cap for a in mine), default=0)
+    grown = 0
+    if peak > 0:
+        for slot in range(1, max(0, int(nslots)) + 1):
+            ar = slot_arena(dev, slot)
+            with ar.lock:
+                if ar.cap < peak:
+                    ar._drop()
+                    ar.buf = torch.empty(peak, dtype=torch.uint8, device=dev)
+                    ar.cap = peak
+                    grown += 1
+                    count_event("arena_presize")
+    slabs = PART_POOL.presize(dev, nslots)
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
+    return {"arenas_grown": grown, "arena_gb": round(peak / 1e9, 3), "slabs_added": slabs,
+            "reserved_gb": round(torch.cuda.memory_reserved(dev) / 1e9, 2),
+            "allocated_gb": round(torch.cuda.memory_allocated(dev) / 1e9, 2)}
 
 
 def arena_bytes() -> int:

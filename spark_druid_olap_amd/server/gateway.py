@@ -240,6 +240,19 @@ class NativeHiveServer(HiveThriftServer):
     def stats(self) -> dict:
         return dict(self._gw.stats()) if self._gw is not None else {}
 
+    def settle(self, timeout: float = 120.0) -> dict:
+        """End of a warm-up (no statement running): wait for the background compiles the warm-up
+        statements started, then size every slot's arena and partition scratch for the largest
+        statement seen and return the allocator's leftover blocks to the device
+        (engine/device_exec.py presize_device_memory).  The steady state then allocates nothing."""
+        from ..engine.device_exec import presize_device_memory, wait_background_compiles
+
+        waited = wait_background_compiles(timeout)
+        sched = self.session.engine.coalescer().scheduler
+        out = presize_device_memory(self.session.engine.world.device(), sched.nslots)
+        out["compiles_waited"] = waited
+        return out
+
     # ------------------------------------------------------------------ forwarded RPCs
     def _forward(self, msg: bytes) -> bytes:
         return self._dispatch(msg)

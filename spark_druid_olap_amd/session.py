@@ -551,7 +551,7 @@ class Session:
             # one page holding every row (the reference's paging loop, DruidSelectResultIterator.scala:116-137,
             # collapsed: the scan compacts on device and ships all selected rows at once)
             run_spec = spec.copy(pagingSpec=S.PagingSpec({}, 2 ** 31 - 1))
-        det = bool(self.conf.typed("spark.sparklinedata.druid.deterministic"))
+        det = bool(self.conf.typed("spark.sparklinedata.druid.deterministic")) or bool(dq.info.get("deterministic"))
         if det:
             ctx = getattr(run_spec, "context", None)
             run_spec = run_spec.copy(context=ctx.copy(deterministic=True) if ctx is not None
@@ -577,11 +577,15 @@ class Session:
                     with T.span("sdo.lower"):
                         prep, pending = prepare_collecting(
                             lambda: self.engine.prepare(run_spec, ds, dq.info.get("historical")))
-                    if pending:
-                        prep.jit_pending = pending
                     from .utils.metrics import count_event
 
-                    count_event("plan_prepare")
+                    old = getattr(dq, "_prepared", None)
+                    count_event("plan_prepare" if old is None else "plan_reprepare_jit" if getattr(old, "jit_pending", None)
+                                else "plan_reprepare_spec" if getattr(dq, "_prepared_spec", None) is not spec
+                                else "plan_reprepare", detail=f"{type(spec).__name__} det={det} "
+                                f"old_det={getattr(old, 'deterministic', None)} {str(getattr(spec, 'filter', ''))[:120]}")
+                    if pending:
+                        prep.jit_pending = pending
                     # output SQL types: large results decode numeric dictionary keys on the device
                     # (and integer outputs of string-valued extractions: 'yyyy' time formats)
                     prep.out_types = {n: t for n, t, k in dq.columns

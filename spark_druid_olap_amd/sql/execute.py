@@ -209,7 +209,15 @@ class Executor:
 
     def _subquery_param(self, e: A.SubqueryExpr):
         """Value a deferred filter needs from a subquery: the scalar, or for IN (subquery) the
-        distinct non-NULL values plus whether a NULL was among them."""
+        distinct non-NULL values plus whether a NULL was among them.
+
+        The value becomes a literal of the outer pushed query, whose resolved plan is cached per
+        value: the subquery's own pushed queries sum exactly (deterministic float sums,
+        engine/lower.py fixed_sum), so a repeated statement resolves to the same plan every time --
+        a float sum's last bits vary with the device's atomic order, which re-planned the outer
+        query on every run (the BI plan's SmallQuantityOrdersRevenue under 64 clients)."""
+        for dq in P.find_all_deep(e.query, P.DruidQuery):
+            dq.info["deterministic"] = True
         if e.kind == "scalar":
             return self._subquery(e, None)
         key = id(e.query)

@@ -25,14 +25,15 @@ _event_log: list = []
 _event_log_on = [False]
 
 
-def count_event(name: str, n: int = 1) -> None:
+def count_event(name: str, n: int = 1, detail: Optional[str] = None) -> None:
     """Process-wide event counter (device-memory releases, statement retries, P2P fallbacks, plan
     and kernel swaps).  With ``log_events(True)`` every event is also kept with its time
     (``time.perf_counter``): the serving timeline lines them up with stalls."""
     with _events_lock:
         _events[name] = _events.get(name, 0) + n
         if _event_log_on[0] and len(_event_log) < 100_000:
-            _event_log.append((time.perf_counter(), name))
+            _event_log.append((time.perf_counter(), name) if detail is None else
+                              (time.perf_counter(), name, detail[:160]))
 
 
 def log_events(on: bool) -> list:

@@ -174,3 +174,35 @@ def test_out_of_memory_release_skips_arenas_held_by_other_slots(monkeypatch):
     assert b.buf is not None  # (skipped, not dropped)
     DE.release_device_memory(keep_arena=a)
     assert b.buf is None
+
+
+def test_growing_slot_goes_straight_to_the_largest_peer(monkeypatch):
+    """Every slot runs every kind of statement: a slot arena that must grow takes the largest
+    peer's size at once (one growth per slot instead of a doubling series whose dropped storages
+    pile up in the caching allocator's per-stream pools)."""
+    monkeypatch.setattr(DE, "_ARENAS", {})
+    monkeypatch.setattr(DE, "ARENA_MIN", 4096)
+    big, small = DE.slot_arena("cpu", 1), DE.slot_arena("cpu", 2)
+    with use_slot(1):
+        big.carve(50_000, _Owner())
+    assert big.cap == 53_248
+    with use_slot(2):
+        small.carve(100, _Owner())
+    assert small.cap == big.cap
+
+
+def test_part_pool_presize_fills_one_slab_per_slot(monkeypatch):
+    """Warm-up presizing (NativeHiveServer.settle): the partition scratch pool holds one free slab
+    per slot at the largest size any statement asked for; smaller free slabs are replaced."""
+    pool = DE.PartScratchPool()
+    monkeypatch.setattr(pool, "_budget", lambda dev: 1 << 20)
+    s1 = pool.acquire("cpu", 100)
+    s2 = pool.acquire("cpu", 1000)
+    pool.release(s1)
+    pool.release(s2)
+    assert pool.presize("cpu", 4) == 3
+    assert sorted(x.words for x in pool.free) == [1000] * 4
+    assert pool.total == 4 * 2 * 1000 * 4
+    assert pool.presize("cpu", 4) == 0
+    s = pool.acquire("cpu", 500)  # served from the presized slabs
+    assert s.words == 1000 and pool.total == 4 * 2 * 1000 * 4

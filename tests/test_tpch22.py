@@ -228,3 +228,27 @@ def test_global_aggregate_over_groupby_is_nested(sess, i):
 def test_q15_subquery_runs_nested(sess):
     d = sess.sql(dict(tpch22.QUERIES)["Q15"])
     assert any(q.info.get("nested") and "global_counts" in q.info for q in d.druid_queries())
+
+
+def test_deferred_scalar_subquery_sums_exactly_and_reuses_its_plan(sess):
+    """A scalar subquery whose value parameterises a pushed filter runs its own pushed queries with
+    exact (fixed-point) float sums: the resolved outer query is cached per value, and a float sum's
+    last bits follow the device's atomic order -- every run re-planned the outer query."""
+    from spark_druid_olap_amd.query.spec import find_deferred
+    from spark_druid_olap_amd.sql import plan as P
+    from spark_druid_olap_amd.utils import metrics as M
+
+    q = (f"select sum(l_extendedprice) / 7.0 as avg_yearly from {T} where c_nation = 'JAPAN' and "
+         f"l_quantity < (select 0.2 * avg(l_extendedprice) from {T} where c_nation = 'JAPAN')")
+    d = sess.sql(q)
+    first = _rows(d)
+    outer = [dq for dq in d.druid_queries() if find_deferred(dq.spec)]
+    assert outer, d.explain()
+    inner = [dq for dq in P.find_all_deep(d.plan, P.DruidQuery) if dq not in outer]
+    assert inner and all(dq.info.get("deterministic") for dq in inner)
+    assert all(getattr(dq, "_prepared", None) is None or dq._prepared.deterministic for dq in inner)
+    before = M.events().get("plan_prepare", 0)
+    for _ in range(3):
+        assert _rows(sess.sql(q)) == first
+    assert M.events().get("plan_prepare", 0) == before
+    assert len(outer[0].__dict__["_resolved"]) == 1

@@ -208,6 +208,9 @@ def main():
                          "run, encode) and write them here; the JSON line gets per-phase percentiles")
     ap.add_argument("--prewarm", type=int, default=0,
                     help="varied workload: plan + compile this many distinct texts before the clock starts")
+    ap.add_argument("--settle", action="store_true",
+                    help="after the warm-up: wait for its background compiles and size the slots' device "
+                         "memory for the largest statement (a server's warm-up step)")
     a = ap.parse_args()
     global WORKLOAD, BIND
     WORKLOAD = a.workload
@@ -281,6 +284,16 @@ def main():
             c.cursor().execute(sql).fetchall()
             # (progress on stderr: a long warm-up -- first-seen shapes compile -- stays visibly alive)
             print(f"[conc] warm {i + 1}/{len(warm)} {name[:40]} {time.time() - tw:.2f}s", file=sys.stderr, flush=True)
+    if a.settle and a.server == "native":
+        # the warm-up's background compiles finish, their statements re-prepare once, then the
+        # slots' device memory is sized for the largest statement seen (NativeHiveServer.settle)
+        from spark_druid_olap_amd.engine.device_exec import wait_background_compiles
+
+        if wait_background_compiles():
+            with connect(port=srv.port) as c:
+                for name, sql in warm:
+                    c.cursor().execute(sql).fetchall()
+        print(f"[conc] settled: {srv.settle()}", file=sys.stderr, flush=True)
     interval = (a.clients / a.qps) if a.qps > 0 else 0.0
     if a.timeline and a.server == "native":
         # (from the open loop's start: its warm-up seconds -- negative times -- included)
@@ -362,14 +375,15 @@ def main():
         t0 = min((r["t"] for r in srv.timeline), default=0.0)
         ev = log_events(False)
         out["stalls"] = [dict(s, t=round(s["t"] - t0, 3),
-                              events=[(round(t - t0, 3), n) for t, n in ev if s["t"] - s["idle_ms"] / 1e3 - 0.2 <= t <= s["t"]][:40])
+                              events=[(round(e[0] - t0, 3),) + tuple(e[1:]) for e in ev
+                                      if s["t"] - s["idle_ms"] / 1e3 - 0.2 <= e[0] <= s["t"]][:40])
                          for s in (srv.stalls or [])]
         evc = {}
-        for _, n in ev:
-            evc[n] = evc.get(n, 0) + 1
+        for e in ev:
+            evc[e[1]] = evc.get(e[1], 0) + 1
         out["timeline"]["events"] = evc
         with open(a.timeline + ".events.json", "w") as f:
-            json.dump([(round(t - t0, 4), n) for t, n in ev], f)
+            json.dump([(round(e[0] - t0, 4),) + tuple(e[1:]) for e in ev], f)
     print(json.dumps(out), flush=True)
 
 
