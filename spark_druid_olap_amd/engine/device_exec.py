@@ -333,6 +333,7 @@ class PreparedScan:
         self._spec_future = None
         self.part = None
         self.part_having = None
+        self.part_topk = None  # (k, slot, is_f64, desc): ORDER BY <aggregate> LIMIT k fused (set_part_topk)
         self.part_cap = 1 << 16
         if mode == D.M_PART and not prog.empty:
             # radix-partitioned group-by (ops/csrc/partition.hip): the JIT producer appends records
@@ -663,8 +664,8 @@ class PreparedScan:
             recs, base = pb["recs1"], pb["base2"]
         if L.get("hashed"):
             return self._run_part_hashed(b, recs, base)
-        hv = self.part_having
-        if hv is None:
+        hv, tk = self.part_having, self.part_topk
+        if hv is None and tk is None:
             # (HLL aggregators: each sub-bucket also writes its groups' rows of the register tables)
             nat.part_agg_hll(recs.data_ptr(), L["rw"], base.data_ptr(), L["nsub"], int(prog.G), L["shift"],
                              [f[0] for f in L["fields"]], [f[1] for f in L["fields"]],
@@ -672,13 +673,20 @@ class PreparedScan:
                              b.acc.data_ptr(), [], 1, 0, 0, 0, [h.data_ptr() for h in b.hll] if L.get("nhll") else [],
                              int(prog.hll_p), st, self._stored_csr() if L.get("nhll") else [])
             return None
+        terms, conj = hv if hv is not None else ([], 1)
         while True:
             acc, keys, cnt, _ = self._sparse_out(b, "hv_out", False)
-            nat.part_agg(recs.data_ptr(), L["rw"], base.data_ptr(), L["nsub"], int(prog.G), L["shift"],
-                         [f[0] for f in L["fields"]], [f[1] for f in L["fields"]], [int(op) for op, _ in prog.slots],
-                         [int(init) for _, init in prog.slots], acc.data_ptr(), hv[0], hv[1], keys.data_ptr(),
-                         cnt.data_ptr(), int(acc.shape[0]), st)
-            n = int(cnt.item())
+            args = (recs.data_ptr(), L["rw"], base.data_ptr(), L["nsub"], int(prog.G), L["shift"],
+                    [f[0] for f in L["fields"]], [f[1] for f in L["fields"]], [int(op) for op, _ in prog.slots],
+                    [int(init) for _, init in prog.slots], acc.data_ptr(), terms, conj, keys.data_ptr(),
+                    cnt.data_ptr(), int(acc.shape[0]))
+            if tk is not None:
+                # ORDER BY <aggregate> LIMIT k in the same kernel: a few candidates per sub-bucket
+                # (every tie kept) instead of every surviving group, no radix select after it
+                nat.part_agg_topk(*args, *tk, st)
+            else:
+                nat.part_agg(*args, st)
+            n = int(cnt[0].item())
             if n <= acc.shape[0]:
                 return Partials("sparse", acc[:n], keys[:n], [])
             self.part_cap = _next_pow2(n + n // 4)  # more survivors than room: grow, aggregate again
@@ -708,7 +716,7 @@ class PreparedScan:
                                   [int(op) for op, _ in prog.slots], [int(init) for _, init in prog.slots], hv[0],
                                   hv[1], keys.data_ptr(), acc.data_ptr(), cnt.data_ptr(), int(acc.shape[0]),
                                   ovf.data_ptr(), [h.data_ptr() for h in hll], int(prog.hll_p), st)
-            n, overflow = int(cnt.item()), int(ovf.item())
+            n, overflow = int(cnt[0].item()), int(ovf.item())
             if overflow:
                 if L["scale"] >= 1 << 12:
                     raise RuntimeError("hash-partitioned group-by: sub-bucket overflow persists")
@@ -740,17 +748,31 @@ class PreparedScan:
             if out is None or out[0].shape[0] < cap or len(out[-1]) != nhll:
                 out = b.part[name] = (torch.empty((cap, ns), dtype=torch.int64, device=dev),
                                       torch.empty(cap, dtype=torch.int64, device=dev),
-                                      torch.zeros(1, dtype=torch.int64, device=dev)) + \
+                                      torch.zeros(2, dtype=torch.int64, device=dev)) + \
                     ((torch.zeros(1, dtype=torch.int32, device=dev),) if ovf else ()) + \
                     ([torch.empty((cap, m), dtype=torch.uint8, device=dev) for _ in range(nhll)],)
             return out
-        items = [(cap * ns, torch.int64, (cap, ns)), (cap, torch.int64, None), (1, torch.int64, None)] + \
+        # (the count word is followed by a fused top-k's threshold word)
+        items = [(cap * ns, torch.int64, (cap, ns)), (cap, torch.int64, None), (2, torch.int64, None)] + \
             ([(1, torch.int32, None)] if ovf else []) + [(cap * m, torch.uint8, (cap, m))] * nhll
         offs, total = _carve_aligned([n * torch.empty((), dtype=dt).element_size() for n, dt, _ in items])
         _, off, _, buf = slot_arena(dev, slot).carve(total, self)
         views = [SlotArena.view(buf, off + o, n, dt, shape) for (n, dt, shape), o in zip(items, offs)]
         k = 4 if ovf else 3
         return tuple(views[:k]) + (views[k:],)
+
+    def set_part_topk(self, k: int, slot: int, is_f64: bool, desc: bool) -> bool:
+        """Fuse a groupBy ORDER BY <aggregate slot> LIMIT k into the partitioned aggregation
+        (engine/executor.py _fuse_topk): each sub-bucket emits only groups at or above its k-th best
+        and the best k-th an earlier sub-bucket published -- a superset of the top k with every
+        tie, ordered and limited exactly afterwards.  False when this scan cannot (hash-keyed and
+        sketch layouts keep the radix select after the aggregation)."""
+        L = self.part or {}
+        if self.mode != D.M_PART or not (1 <= int(k) <= 16) or L.get("nhll") or L.get("hashed") or \
+                not (0 <= int(slot) < self.prog.nslots) or L.get("shift", 99) > 12:
+            return False  # (the kernel ranks tables of at most 4096 keys: 8 rows per thread)
+        self.part_topk = (int(k), int(slot), 1 if is_f64 else 0, 1 if desc else 0)
+        return True
 
     def set_part_having(self, terms, conj: bool) -> bool:
         """Fuse a groupBy HAVING into the partitioned aggregation (engine/executor.py): only existing

@@ -578,6 +578,7 @@ class PreparedQuery:
             if getattr(self, "_full_prog", None) is not None else False
         if self._having_fused is None:
             self._having_fused = self._fuse_having(prog, prep, disjoint)
+            self._fuse_topk(prog, prep, disjoint)
         try:
             with T.span("sdo.scan"):
                 checkpoint()  # inside the merge's failure agreement: every rank aborts together
@@ -765,6 +766,41 @@ class PreparedQuery:
         if not terms or any(t is None for t in terms) or len(terms) > 4:
             return False
         return bool(prep.set_part_having(terms, conj))
+
+    def _fuse_topk(self, prog: ScanProgram, prep, disjoint: bool) -> bool:
+        """Hand ORDER BY <aggregate> LIMIT k (one order column, k <= 16) to a partitioned group-by
+        scan (engine/device_exec.py set_part_topk): each sub-bucket emits only its candidates -- the
+        BI plan's TopVolumeCustomers keeps a few hundred of ~60M (customer, month) groups without
+        writing the survivors of its HAVING or radix-selecting over them.  Only where a group's
+        partial is final (as ``_fuse_having``), any HAVING went into the kernel too and no window
+        pre-filter (``partition_extreme``) runs between the aggregation and the limit."""
+        from ..ops import desc as D_
+
+        qs = self.qs
+        if prog.thetas or any(kc.collapse for kc in prog.keys):
+            return False
+        if prep is None or getattr(prep, "mode", None) != D_.M_PART or len(self.scans) != 1:
+            return False
+        if (self.world.distributed and not disjoint) or getattr(self, "partition_extreme", None) is not None:
+            return False
+        if qs.queryType == "groupBy":
+            if getattr(qs, "having", None) is not None and not self._having_fused:
+                return False
+            ls = qs.limitSpec
+            if ls is None or ls.limit is None or not ls.columns or len(ls.columns) != 1:
+                return False
+            oc = ls.columns[0]
+            oc = S.OrderByColumnSpec(oc) if isinstance(oc, str) else oc
+            name, desc, limit = oc.dimension, not oc.ascending, int(ls.limit)
+        elif qs.queryType == "topN" and isinstance(qs.metric, S.NumericTopNMetricSpec) and len(prog.keys) == 1:
+            name, desc, limit = qs.metric.metric, True, int(qs.threshold)
+        else:
+            return False
+        agg = next((a for a in prog.aggs if a.name == name), None)
+        if not (1 <= limit <= 16) or agg is None or agg.slot < 0 or \
+                agg.kind not in ("count", "sum_i", "sum_f", "min_i", "max_i"):
+            return False
+        return bool(prep.set_part_topk(limit, agg.slot, agg.kind == "sum_f", desc))
 
     def _device_having(self, prog: ScanProgram, part: Partials):
         """groupBy havingSpec evaluated over the merged accumulators ON THE DEVICE (TPC-H Q18:

@@ -570,8 +570,11 @@ static void part_split(uint64_t in, int RW, uint64_t seg_lo, uint64_t seg_hi, in
   if (P2 <= 0 || P2 > 4096 || (P2 & (P2 - 1))) throw std::invalid_argument("part_split: P2 a power of two <= 4096");
   if (RW < 1 || RW > 2 + 2 * sdo::MAX_SLOTS) throw std::invalid_argument("part_split: record width");
   if (spg < 1) throw std::invalid_argument("part_split: segments per group");
-  // tile of 512 x PU records, ~32 KB of LDS whatever the record width
-  const int PU = g_part_pu ? g_part_pu : (RW <= 2 ? 8 : (RW <= 4 ? 4 : (RW <= 8 ? 2 : 1)));
+  // tile of 512 x PU records: longer same-bucket runs per tile store fuller lines, more LDS per
+  // block costs residency.  3-word records (the BI plan's TopVolumeCustomers, 343M records over
+  // 512 then 256 buckets at SF100): PU 4 / 8 / 16 scatter at 2.1 / 2.6-2.8 / 1.6-1.8 TB/s; 4-word
+  // records 2.3-2.7 / 2.85 TB/s at PU 4 / 8 (tools/part_probe.py, profiles/r6/part_probe_*.txt)
+  const int PU = g_part_pu ? g_part_pu : (RW <= 4 ? 8 : (RW <= 8 ? 2 : 1));
   // odd tile stride for even record widths >= 4 (conflict-free strided tile reads) when it fits
   int RS = RW;
   const int64_t lds_max = 160 * 1024 - 256;
@@ -615,7 +618,8 @@ static void part_agg_hll(uint64_t recs, int RW, uint64_t base, int64_t nsub, int
                          std::vector<int> width, std::vector<int> ops, std::vector<int64_t> init, uint64_t gacc,
                          std::vector<std::tuple<int, int, int, double, double>> having, int conj, uint64_t out_keys,
                          uint64_t out_count, int64_t cap, std::vector<uint64_t> hll, int hll_p, uint64_t stream,
-                         std::vector<std::tuple<uint64_t, uint64_t>> stored = {}) {
+                         std::vector<std::tuple<uint64_t, uint64_t>> stored = {},
+                         std::tuple<int, int, int, int> topk = {0, 0, 0, 1}) {
   if (nsub <= 0 || G <= 0) return;
   sdo::PartFields f{};
   if (slot.size() != width.size() || slot.size() > (size_t)sdo::MAX_SLOTS) throw std::invalid_argument("part_agg: fields");
@@ -652,7 +656,8 @@ static void part_agg_hll(uint64_t recs, int RW, uint64_t base, int64_t nsub, int
     f.init[s] = init[s];
   }
   const int64_t lds = ((int64_t)1 << shift) * (f.nslots * 8 + (int64_t)hl.n * ((int64_t)1 << hl.p));
-  if (shift < 0 || lds > 160 * 1024 - 256)
+  // (static LDS: the scan / base words and the fused top-k's per-wave lists, ~1.1 KiB)
+  if (shift < 0 || lds > 160 * 1024 - 1536)
     throw std::invalid_argument("part_agg: sub-bucket table exceeds the LDS");
   if (lds > 64 * 1024)  // (the kernel's static LDS counts against the 160 KiB too: exactly the dynamic bytes)
     check(hipFuncSetAttribute((const void*)sdo::part_agg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
@@ -672,13 +677,35 @@ static void part_agg_hll(uint64_t recs, int RW, uint64_t base, int64_t nsub, int
     if (hv.slot[j] < 0 || hv.slot[j] >= f.nslots || hv.op[j] < 0 || hv.op[j] > 2)
       throw std::invalid_argument("part_agg: having term");
   }
-  if (hv.nterms && (!out_keys || !out_count || cap < 0)) throw std::invalid_argument("part_agg: having output");
-  if (hv.nterms)
-    check(hipMemsetAsync((void*)out_count, 0, 8, (hipStream_t)stream), "part_agg count reset");
+  // fused ORDER BY slot LIMIT k: out_count is then [count, threshold] (both reset here)
+  hv.tk = std::get<0>(topk);
+  hv.tk_slot = std::get<1>(topk);
+  hv.tk_f64 = std::get<2>(topk) ? 1 : 0;
+  hv.tk_desc = std::get<3>(topk) ? 1 : 0;
+  if (hv.tk < 0 || hv.tk > sdo::PART_TOPK_MAX || hv.tk_slot < 0 || hv.tk_slot >= f.nslots)
+    throw std::invalid_argument("part_agg: top-k");
+  if (hv.tk && hl.n) throw std::invalid_argument("part_agg: top-k with HLL aggregators");
+  if (hv.tk && ((int64_t)1 << shift) > 512 * 8) throw std::invalid_argument("part_agg: top-k over a table > 4096 keys");
+  if (hv.nterms == 0 && hv.tk) hv.conj = 1;  // (no terms: every existing group passes)
+  if ((hv.nterms || hv.tk) && (!out_keys || !out_count || cap < 0)) throw std::invalid_argument("part_agg: having output");
+  if (hv.nterms || hv.tk)
+    check(hipMemsetAsync((void*)out_count, 0, hv.tk ? 16 : 8, (hipStream_t)stream), "part_agg count reset");
   hipLaunchKernelGGL(sdo::part_agg_kernel, dim3((unsigned)grid), dim3(512), (unsigned)lds, (hipStream_t)stream,
                      (const uint32_t*)recs, RW, (const uint32_t*)base, nsub, G, shift, f, hl, (uint64_t*)gacc, hv,
                      (int64_t*)out_keys, (unsigned long long*)out_count, cap);
   check(hipGetLastError(), "part_agg_kernel launch");
+}
+
+// part_agg with a fused ORDER BY <tk_slot> LIMIT tk (partition.hip part_topk_threshold): out_count
+// must hold two words
+static void part_agg_topk(uint64_t recs, int RW, uint64_t base, int64_t nsub, int64_t G, int shift, std::vector<int> slot,
+                          std::vector<int> width, std::vector<int> ops, std::vector<int64_t> init, uint64_t gacc,
+                          std::vector<std::tuple<int, int, int, double, double>> having, int conj, uint64_t out_keys,
+                          uint64_t out_count, int64_t cap, int tk, int tk_slot, int tk_f64, int tk_desc,
+                          uint64_t stream) {
+  if (tk < 1) throw std::invalid_argument("part_agg_topk: k >= 1");
+  part_agg_hll(recs, RW, base, nsub, G, shift, slot, width, ops, init, gacc, having, conj, out_keys, out_count, cap, {},
+               0, stream, {}, std::make_tuple(tk, tk_slot, tk_f64, tk_desc));
 }
 
 static void part_agg(uint64_t recs, int RW, uint64_t base, int64_t nsub, int64_t G, int shift, std::vector<int> slot,
@@ -1008,7 +1035,15 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("part_hash_agg_hll", &part_hash_agg_hll);
   m.def("theta_select_regions", &theta_select_regions);
   m.def("part_agg", &part_agg);
-  m.def("part_agg_hll", &part_agg_hll);
+  m.def("part_agg_topk", &part_agg_topk);
+  m.def("part_agg_hll", [](uint64_t recs, int RW, uint64_t base, int64_t nsub, int64_t G, int shift, std::vector<int> slot,
+                           std::vector<int> width, std::vector<int> ops, std::vector<int64_t> init, uint64_t gacc,
+                           std::vector<std::tuple<int, int, int, double, double>> having, int conj, uint64_t out_keys,
+                           uint64_t out_count, int64_t cap, std::vector<uint64_t> hll, int hll_p, uint64_t stream,
+                           std::vector<std::tuple<uint64_t, uint64_t>> stored) {
+    part_agg_hll(recs, RW, base, nsub, G, shift, slot, width, ops, init, gacc, having, conj, out_keys, out_count, cap,
+                 hll, hll_p, stream, stored);
+  });
   m.def("part_hash_agg", &part_hash_agg);
   m.def("layout", &layout);
   m.def("device_info", &device_info);

@@ -548,6 +548,110 @@ __device__ __forceinline__ void lds_max_u8(unsigned char* regs, int64_t idx, uin
   }
 }
 
+// Fused ORDER BY <slot> LIMIT k of the partitioned aggregation.  A group's sort value as an
+// unsigned key, larger = better (doubles by their ordered bits, ascending orders inverted; NaN last
+// either way, as 0 -- also the "no group" value).
+__device__ __forceinline__ uint64_t topk_ord(uint64_t bits, int f64, int desc) {
+  uint64_t u;
+  if (f64) {
+    const double d = __longlong_as_double((long long)bits);
+    if (d != d) return 0ull;
+    u = (bits >> 63) ? ~bits : (bits | 0x8000000000000000ull);
+  } else {
+    u = bits ^ 0x8000000000000000ull;
+  }
+  return desc ? u : ~u;
+}
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t lo = __shfl_xor((uint32_t)v, o), hi = __shfl_xor((uint32_t)(v >> 32), o);
+    const uint64_t w = ((uint64_t)hi << 32) | lo;
+    v = w > v ? w : v;
+  }
+  return v;
+}
+
+// The block's emission threshold for a fused top-k: max(its own k-th best sort value, the best
+// k-th value an earlier block published in *gthr).  Any group below it has k better groups in one
+// block, so it is not in the global top k (ties included: a group equal to the threshold is kept).
+// A thread holds the sort values of its own table rows (at most PART_TOPK_RPT: tables of <= 4096
+// keys); each wave extracts its k best by k rounds of a wave max (the lowest lane holding it pops
+// that value), and wave 0 does the same over the 8 waves' lists.  The LDS table is read-only here.
+constexpr int PART_TOPK_RPT = 8;
+
+__device__ uint64_t part_topk_threshold(const uint64_t* t, int64_t nk, int NS, const PartHaving& hv,
+                                        unsigned long long* gthr) {
+  __shared__ uint64_t wtop[8 * PART_TOPK_MAX];
+  __shared__ uint64_t blk_thr;
+  const int k = hv.tk;
+  uint64_t v[PART_TOPK_RPT];
+#pragma unroll
+  for (int j = 0; j < PART_TOPK_RPT; ++j) {
+    const int64_t i = threadIdx.x + (int64_t)j * blockDim.x;
+    v[j] = 0ull;
+    if (i < nk) {
+      const uint64_t* row = t + i * NS;
+      if ((int64_t)row[0] > 0 && having_pass(hv, row)) v[j] = topk_ord(row[hv.tk_slot], hv.tk_f64, hv.tk_desc);
+    }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int r = 0; r < k; ++r) {
+    uint64_t head = 0ull;
+#pragma unroll
+    for (int j = 0; j < PART_TOPK_RPT; ++j) head = v[j] > head ? v[j] : head;
+    const uint64_t m = wave_max_u64(head);
+    const unsigned long long b = __ballot(head == m);
+    if (lane == __ffsll(b) - 1) {  // pop one copy of m
+      bool done = false;
+#pragma unroll
+      for (int j = 0; j < PART_TOPK_RPT; ++j) {
+        if (!done && v[j] == m) {
+          v[j] = 0ull;
+          done = true;
+        }
+      }
+    }
+    if (lane == 0) wtop[wave * PART_TOPK_MAX + r] = m;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    const int nw = (int)(blockDim.x >> 6);
+    const int nc = nw * k;  // candidates c = w * k + r, two per lane (k <= 16, 8 waves)
+    uint64_t a0 = 0ull, a1 = 0ull;
+    if (lane < nc) a0 = wtop[(lane / k) * PART_TOPK_MAX + lane % k];
+    if (lane + 64 < nc) a1 = wtop[((lane + 64) / k) * PART_TOPK_MAX + (lane + 64) % k];
+    if (a1 > a0) {
+      const uint64_t x = a0;
+      a0 = a1;
+      a1 = x;
+    }
+    uint64_t m = 0ull;
+    for (int r = 0; r < k; ++r) {
+      m = wave_max_u64(a0);
+      const unsigned long long b = __ballot(a0 == m);
+      if (lane == __ffsll(b) - 1) {
+        a0 = a1;
+        a1 = 0ull;
+      }
+    }
+    if (lane == 0) {
+      // publish this block's k-th if it raises the global one (a relaxed read first: once the
+      // threshold settles, most blocks issue no atomic)
+      const uint64_t g = __hip_atomic_load(gthr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint64_t best = g > m ? g : m;
+      if (m > g) {
+        const uint64_t old = atomicMax(gthr, (unsigned long long)m);
+        best = old > m ? old : m;
+      }
+      blk_thr = best;
+    }
+  }
+  __syncthreads();
+  return blk_thr;
+}
+
 __global__ __launch_bounds__(512) void part_agg_kernel(const uint32_t* __restrict__ recs, int RW,
                                                       const uint32_t* __restrict__ base, int64_t nsub, int64_t G,
                                                       int shift, PartFields f, PartHll hl, uint64_t* __restrict__ gacc,
@@ -680,7 +784,7 @@ __global__ __launch_bounds__(512) void part_agg_kernel(const uint32_t* __restric
     }
   }
   __syncthreads();
-  if (hv.nterms == 0) {
+  if (hv.nterms == 0 && hv.tk == 0) {
     uint64_t* g = gacc + k0 * NS;
     for (int64_t i = threadIdx.x; i < nk * NS; i += blockDim.x) g[i] = t[i];
     for (int h = 0; h < hl.n; ++h) {  // the sub-bucket's register rows, 16 bytes per thread step
@@ -692,10 +796,13 @@ __global__ __launch_bounds__(512) void part_agg_kernel(const uint32_t* __restric
   }
   __shared__ uint32_t scan_lds[8];
   __shared__ unsigned long long blk_base;
+  // the emission threshold of a fused ORDER BY ... LIMIT tk (0: every surviving group)
+  const uint64_t thr = hv.tk > 0 ? part_topk_threshold(t, nk, NS, hv, out_count + 1) : 0ull;
   uint32_t mine = 0;
   for (int64_t i = threadIdx.x; i < nk; i += blockDim.x) {
     const uint64_t* row = t + i * NS;
-    mine += ((int64_t)row[0] > 0 && having_pass(hv, row)) ? 1u : 0u;
+    mine += ((int64_t)row[0] > 0 && having_pass(hv, row) &&
+             (thr == 0ull || topk_ord(row[hv.tk_slot], hv.tk_f64, hv.tk_desc) >= thr)) ? 1u : 0u;
   }
   uint32_t total;
   uint32_t pre = block_excl_scan_u32<512>(mine, scan_lds, &total);
@@ -705,7 +812,9 @@ __global__ __launch_bounds__(512) void part_agg_kernel(const uint32_t* __restric
   int64_t pos = (int64_t)blk_base + pre;
   for (int64_t i = threadIdx.x; i < nk; i += blockDim.x) {
     const uint64_t* row = t + i * NS;
-    if (!((int64_t)row[0] > 0 && having_pass(hv, row))) continue;
+    if (!((int64_t)row[0] > 0 && having_pass(hv, row) &&
+          (thr == 0ull || topk_ord(row[hv.tk_slot], hv.tk_f64, hv.tk_desc) >= thr)))
+      continue;
     if (pos < cap) {
       out_keys[pos] = k0 + i;
       for (int s = 0; s < NS; ++s) gacc[pos * NS + s] = row[s];

@@ -249,6 +249,15 @@ struct PartHaving {
   int32_t pad;
   double div[4];
   double c[4];
+  // ORDER BY <slot> LIMIT tk fused as well (tk > 0, <= PART_TOPK_MAX; nterms may be 0): only groups
+  // ranking at or above the block's tk-th best and the best tk-th any earlier block published
+  // (out_count[1]) leave the kernel -- a superset of the global top tk with every tie, which the
+  // host orders and limits exactly.  tk_f64: the slot holds double bits; tk_desc: larger first.
+  int32_t tk;
+  int32_t tk_slot;
+  int32_t tk_f64;
+  int32_t tk_desc;
 };
+constexpr int PART_TOPK_MAX = 16;
 
 }  // namespace sdo

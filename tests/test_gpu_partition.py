@@ -387,3 +387,69 @@ def test_hash_partitioned_hll_registers_match_atomic_table(gpu_ds, monkeypatch):
     assert torch.equal(a.acc.cpu()[order], b.acc.cpu()[keys])
     assert torch.equal(a.hll[0].cpu()[order], b.hll[0].cpu()[keys])
     assert int(a.hll[0].sum()) > 0
+
+
+@pytest.mark.parametrize("k,slot,desc,having", [(3, 2, True, False), (10, 1, True, True), (5, 1, False, False),
+                                                (16, 2, False, True), (1, 0, True, False)])
+def test_fused_topk_keeps_every_group_at_or_above_the_kth(gpu_ds, k, slot, desc, having):
+    """ORDER BY <slot> LIMIT k fused into the partitioned aggregation: the emitted groups are a
+    superset of the top k with every tie (the groups at or above the global k-th value) and carry
+    the dense table's exact rows; with a HAVING only passing groups count."""
+    from spark_druid_olap_amd.engine import device_exec as DE
+
+    prog = _order_prog(gpu_ds)
+    dense = DE.PreparedScan(prog, mode=D.M_PART).run().acc.clone()
+    sc = DE.PreparedScan(prog, mode=D.M_PART)
+    sc.part_cap = 64  # (a tiny first capacity also exercises the re-run)
+    terms = [(1, 0, 1, 1.0, 100.0)]
+    if having:
+        assert sc.set_part_having(terms, True)
+    f64 = slot == 2
+    assert sc.set_part_topk(k, slot, f64, desc)
+    got = sc.run()
+    assert got.kind == "sparse"
+    ok = dense[:, 0] > 0
+    if having:
+        ok &= dense[:, 1].double() > 100.0
+    col = dense[:, slot]
+    v = col.view(torch.float64) if f64 else col.double()
+    key = v if desc else -v
+    key = torch.where(ok, key, torch.full_like(key, -float("inf")))
+    kth = torch.topk(key, k).values.min()
+    want = set(torch.nonzero(ok & (key >= kth)).flatten().tolist())
+    keys = got.keys.tolist()
+    assert want <= set(keys), (len(want), len(keys))
+    assert len(keys) < len(want) + 64 * k + 4096  # candidates (and every tie), not every group
+    idx = torch.tensor(keys, dtype=torch.int64, device=dense.device)
+    assert torch.equal(got.acc.cpu(), dense[idx].cpu())
+    assert bool(ok[idx].all())
+
+
+@pytest.mark.parametrize("sql", [
+    "select o_orderkey, sum(l_extendedprice) s, count(*) c from {T} group by o_orderkey order by s desc limit 7",
+    "select o_orderkey, sum(l_extendedprice) s from {T} where o_orderdate >= '1995-01-01' group by o_orderkey "
+    "having sum(l_quantity) > 120 order by s asc limit 3",
+    "select c_name, month(o_orderdate), sum(o_totalprice) totprice, sum(l_quantity) totqty from {T} "
+    "group by c_name, month(o_orderdate) having sum(l_quantity) > 30 order by totprice desc limit 3",
+])
+def test_fused_topk_sql_vs_base_table_oracle(sql_pair, monkeypatch, sql):
+    """The fused ORDER BY ... LIMIT through SQL on the partitioned layout == the base-table answer
+    (pandas operators), and the fusion is what ran."""
+    from spark_druid_olap_amd.planner import cost
+
+    monkeypatch.setattr(cost, "FORCE_PARTITIONED", True)
+    s = sql_pair
+    s._plan_cache.clear()
+    d = s.sql(sql.format(T="orderLineItemPartSupplier"))
+    got = [tuple(r) for r in d.collect()]
+    exp = [tuple(r) for r in s.sql(sql.format(T="orderLineItemPartSupplierBase")).collect()]
+    assert len(got) == len(exp) > 0
+    for x, y in zip(got, exp):
+        for u, w in zip(x, y):
+            if isinstance(u, float) or isinstance(w, float):
+                assert u == pytest.approx(w, rel=1e-9, abs=0.011), (x, y)
+            else:
+                assert u == w, (x, y)
+    fused = [sc[2].part_topk for dq in d.druid_queries()
+             for sc in getattr(getattr(dq, "_prepared", None), "scans", [])]
+    assert any(t is not None for t in fused), fused
