@@ -419,7 +419,8 @@ def test_fused_topk_keeps_every_group_at_or_above_the_kth(gpu_ds, k, slot, desc,
     want = set(torch.nonzero(ok & (key >= kth)).flatten().tolist())
     keys = got.keys.tolist()
     assert want <= set(keys), (len(want), len(keys))
-    assert len(keys) < len(want) + 64 * k + 4096  # candidates (and every tie), not every group
+    # candidates (and every tie), not every group
+    assert len(keys) <= max(len(want) + 64 * k + 4096, int(ok.sum()) // 4)
     idx = torch.tensor(keys, dtype=torch.int64, device=dense.device)
     assert torch.equal(got.acc.cpu(), dense[idx].cpu())
     assert bool(ok[idx].all())

@@ -129,6 +129,8 @@ def main():
             names += [("-", 0), ("-", 0), ("-", 0)]
         if RW <= 2:
             slots, widths = ([1], [1]) if RW == 2 else ([0], [0])
+        elif RW == 3:
+            slots, widths = [1, 2], [1, 1]  # (TopVolumeCustomers: two i32 sums)
         else:
             slots, widths = [1, 2], [1, 2]
         if 1 + sum(widths) == RW:
