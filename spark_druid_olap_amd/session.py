@@ -134,8 +134,16 @@ class DataFrame:
         if self.plan is not None and not self.session.engine.world.distributed:
             dqs = self.__dict__.get("_known_dqs")
             if dqs is None:  # (the plan is fixed: walk it once per cached statement)
-                dqs = self._known_dqs = [dq for dq in P.find_all_deep(self.plan, P.DruidQuery)
-                                         if not S.find_deferred(dq.spec)]
+                alld = P.find_all_deep(self.plan, P.DruidQuery)
+                for dq in alld:
+                    # the pushed queries of a subquery whose value parameterises another's filter
+                    # sum exactly (sql/execute.py _subquery_param): prepared that way from the start
+                    for d in S.find_deferred(dq.spec):
+                        for sq in d.subqueries:
+                            if isinstance(sq.query, P.Plan):
+                                for x in P.find_all_deep(sq.query, P.DruidQuery):
+                                    x.info["deterministic"] = True
+                dqs = self._known_dqs = [dq for dq in alld if not S.find_deferred(dq.spec)]
             for dq in dqs:
                 self.session.prepare_druid(dq)
         return self

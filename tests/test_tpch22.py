@@ -251,4 +251,12 @@ def test_deferred_scalar_subquery_sums_exactly_and_reuses_its_plan(sess):
     for _ in range(3):
         assert _rows(sess.sql(q)) == first
     assert M.events().get("plan_prepare", 0) == before
+    # a server prepares a statement's known pushed queries before running it: the subquery's are
+    # prepared exact from the start (not re-prepared when the run marks them)
+    q2 = q.replace("'JAPAN'", "'CHINA'")
+    d2 = sess.sql(q2)
+    r0 = M.events().get("plan_reprepare", 0)
+    d2.prepare()
+    _rows(d2)
+    assert M.events().get("plan_reprepare", 0) == r0
     assert len(outer[0].__dict__["_resolved"]) == 1
