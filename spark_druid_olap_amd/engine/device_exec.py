@@ -686,6 +686,7 @@ class PreparedScan:
                 nat.part_agg_topk(*args, *tk, st)
             else:
                 nat.part_agg(*args, st)
+            native.stream_sync(self.dev)  # (the whole partition pipeline: a sleeping wait, not a spin)
             n = int(cnt[0].item())
             if n <= acc.shape[0]:
                 return Partials("sparse", acc[:n], keys[:n], [])
@@ -716,6 +717,7 @@ class PreparedScan:
                                   [int(op) for op, _ in prog.slots], [int(init) for _, init in prog.slots], hv[0],
                                   hv[1], keys.data_ptr(), acc.data_ptr(), cnt.data_ptr(), int(acc.shape[0]),
                                   ovf.data_ptr(), [h.data_ptr() for h in hll], int(prog.hll_p), st)
+            native.stream_sync(self.dev)
             n, overflow = int(cnt[0].item()), int(ovf.item())
             if overflow:
                 if L["scale"] >= 1 << 12:

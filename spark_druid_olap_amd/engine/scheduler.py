@@ -104,9 +104,21 @@ class StreamScheduler:
                     st.wait_stream(torch.cuda.default_stream(st.device))
                     with torch.cuda.stream(st):
                         yield slot
-                    st.synchronize()
+                    _sync(st)
         finally:
             self._free.put(slot)
+
+
+def _sync(st) -> None:
+    """The slot stream's end-of-statement wait: the native extension's spin-then-sleep wait when it
+    is loaded (ops/csrc/bindings.cpp wait_stream: a long statement does not spin a core)."""
+    from ..ops import native
+
+    m = native.loaded()
+    if m is not None:
+        m.stream_sync(st.cuda_stream)
+    else:
+        st.synchronize()
 
 
 class _Flight:

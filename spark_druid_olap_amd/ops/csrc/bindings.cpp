@@ -10,6 +10,8 @@
 #include <algorithm>
 #include <cstring>
 #include <mutex>
+#include <thread>
+#include <chrono>
 #include <stdexcept>
 #include <string>
 #include <tuple>
@@ -95,7 +97,32 @@ static void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
-static void wait_stream(hipStream_t st, const char* what) { check(hipStreamSynchronize(st), what); }
+// Host waits for a stream (every native sync: fetch_small, sparse_decode, d2h, stream_sync).  HIP's
+// own wait spins the thread's core for the whole wait (tools/sync_cpu_probe.py: CPU time == wall
+// time), which is right for sub-millisecond scans and wasteful for a server's 10-50 ms partitioned
+// group-bys, whose executor threads then burn the cores the clients and compile threads need
+// (exec_thread_cpu_ms).  Hybrid: poll for g_wait_spin_us (the latency of a short scan is
+// unchanged), then sleep between polls (20 us doubling to 200 us: a long wait ends at most ~0.2 ms
+// late and costs ~1 us of CPU per poll).
+static int64_t g_wait_spin_us = 1000;
+static void set_wait_spin(int64_t us) {
+  if (us < 0) throw std::invalid_argument("set_wait_spin: microseconds >= 0");
+  g_wait_spin_us = us;
+}
+static void wait_stream(hipStream_t st, const char* what) {
+  const auto t0 = std::chrono::steady_clock::now();
+  int64_t nap = 20;
+  while (true) {
+    const hipError_t e = hipStreamQuery(st);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) check(e, what);
+    const int64_t el =
+        std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+    if (el < g_wait_spin_us) continue;
+    std::this_thread::sleep_for(std::chrono::microseconds(nap));
+    nap = nap * 2 > 200 ? 200 : nap * 2;
+  }
+}
 
 static void scan(uint64_t desc, int grid, int block, int lds, int unroll, uint64_t stream) {
   hipStream_t s = (hipStream_t)stream;
@@ -556,10 +583,13 @@ static void part_keys(uint64_t keys, int64_t n, int shift1, int P1, uint64_t cou
 
 // Probe knob (tools/part_probe.py A/B runs): records per thread of the scatter tile (0: by width).
 static int g_part_pu = 0;
-static void part_tune(int pu) {
+static int64_t g_part_lds_min = 0;  // (probe: pad the scatter's LDS request -> fewer blocks per CU)
+static void part_tune(int pu, int64_t lds_min = 0) {
   if (pu != 0 && pu != 1 && pu != 2 && pu != 4 && pu != 8 && pu != 16 && pu != 32)
     throw std::invalid_argument("part_tune: pu in {0,1,2,4,8,16,32}");
+  if (lds_min < 0 || lds_min > 160 * 1024 - 256) throw std::invalid_argument("part_tune: lds_min");
   g_part_pu = pu;
+  g_part_lds_min = lds_min;
 }
 
 // groups x K blocks; group g's segments are [g*spg, (g+1)*spg) of seg_lo/seg_hi (a level-1 bucket
@@ -581,7 +611,8 @@ static void part_split(uint64_t in, int RW, uint64_t seg_lo, uint64_t seg_hi, in
   if (RW >= 4 && RW % 2 == 0 && ((int64_t)3 * P2 + (int64_t)512 * PU * (RW + 1)) * 4 <= lds_max) RS = RW + 1;
   // (phase bit 1: clustered keys, see partition.hip part_split_kernel)
   if ((phase & ~3) != 0) throw std::invalid_argument("part_split: phase");
-  const int64_t lds = (phase & 1) == 0 ? (int64_t)P2 * 4 : ((int64_t)3 * P2 + (int64_t)512 * PU * RS) * 4;
+  int64_t lds = (phase & 1) == 0 ? (int64_t)P2 * 4 : ((int64_t)3 * P2 + (int64_t)512 * PU * RS) * 4;
+  if ((phase & 1) && lds < g_part_lds_min) lds = g_part_lds_min;
   if (lds > lds_max) throw std::invalid_argument("part_split: tile does not fit the LDS");
   const bool cl = (phase & 2) != 0;
   phase &= 1;
@@ -1027,11 +1058,12 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("fetch_small", &fetch_small);
   m.def("fetch_small_reset", &fetch_small_reset);
   m.def("stream_sync", &stream_sync);
+  m.def("set_wait_spin", &set_wait_spin);
   m.def("glds_probe", &glds_probe);
   m.def("part_scan", &part_scan);
   m.def("part_keys", &part_keys);
   m.def("part_split", &part_split);
-  m.def("part_tune", &part_tune);
+  m.def("part_tune", &part_tune, py::arg("pu"), py::arg("lds_min") = 0);
   m.def("part_hash_agg_hll", &part_hash_agg_hll);
   m.def("theta_select_regions", &theta_select_regions);
   m.def("part_agg", &part_agg);

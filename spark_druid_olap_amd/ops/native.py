@@ -23,6 +23,11 @@ class NativeUnavailable(RuntimeError):
     pass
 
 
+def loaded():
+    """The extension module if some caller already loaded it, else None (never builds or imports)."""
+    return _mod
+
+
 def load(build_if_missing: bool = True):
     global _mod
     if _mod is not None:

@@ -695,6 +695,10 @@ def main(argv=None):
     ap.add_argument("--segments", default=None,
                     help="segment store root: load every datasource saved under DIR/<datasource>/rank<r> "
                          "(resume after restart); with --ingest, the ingested shards are saved there")
+    ap.add_argument("--gpu-wait", default="spin", choices=["blocking", "spin"],
+                    help="HIP's wait mode for server threads (utils/hipsync.py): spin (HIP's default; the "
+                         "engine's own waits sleep after 1 ms anyway) or blocking (every wait sleeps on the "
+                         "completion interrupt: least CPU, less throughput near capacity)")
     ap.add_argument("--elastic", action="store_true",
                     help="survive a lost GPU process: heartbeats, communicator rebuild over the survivors and "
                          "re-homing of its shards from --segments (parallel/recovery.py)")
@@ -707,6 +711,11 @@ def main(argv=None):
         sys.exit(spawn_ranks(a.gpus, [sys.executable, "-m", "spark_druid_olap_amd.server.hive_server"] +
                              list(argv if argv is not None else sys.argv[1:]), quiet_peers=False))
     logging.basicConfig(level=logging.INFO)
+    if a.gpu_wait != "spin":
+        # first thing, before torch or the world touch the device (the flag only takes then)
+        from ..utils.hipsync import set_wait_mode
+
+        set_wait_mode(a.gpu_wait, int(os.environ.get("LOCAL_RANK", "0")))
     import torch
 
     from ..parallel.world import init_world

@@ -46,7 +46,7 @@ def test_partitioned_run_uses_its_buffers_layout_and_grid(monkeypatch):
     sc.prog = SimpleNamespace(G=2048, slots=[(D.S_SUM_I, 0)], hll_p=11)
     sc.dev = torch.device("cpu")
     sc.jit = SimpleNamespace(handle=7, lay=SimpleNamespace(total=4096))
-    sc.part_having = None
+    sc.part_having = sc.part_topk = None
     # another slot re-laid the scan out (and swapped in a kernel with another grid) after these
     # buffers were built
     sc.part, sc.grid = new, 999

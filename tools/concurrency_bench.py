@@ -208,6 +208,11 @@ def main():
                          "run, encode) and write them here; the JSON line gets per-phase percentiles")
     ap.add_argument("--prewarm", type=int, default=0,
                     help="varied workload: plan + compile this many distinct texts before the clock starts")
+    ap.add_argument("--wait", default="spin", choices=["blocking", "spin"],
+                    help="HIP's wait mode for the server's threads (utils/hipsync.py): spin (HIP's default; the "
+                         "engine's own waits still sleep after 1 ms, ops/csrc/bindings.cpp wait_stream) or "
+                         "blocking (every wait sleeps on the interrupt: least CPU, ~40%% less capacity at 400 QPS, "
+                         "profiles/r6/thrift_jmx_q400_blocking_wait.json)")
     ap.add_argument("--settle", action="store_true",
                     help="after the warm-up: wait for its background compiles and size the slots' device "
                          "memory for the largest statement (a server's warm-up step)")
@@ -227,6 +232,10 @@ def main():
           for i in range(nproc)]
     for p in ps:
         p.start()
+    # before anything touches the GPU (the flag only takes before the device is initialised)
+    from spark_druid_olap_amd.utils.hipsync import set_wait_mode
+
+    wait_set = set_wait_mode(a.wait, int(os.environ.get("LOCAL_RANK", "0"))) if a.wait != "spin" else False
     import torch
 
     from spark_druid_olap_amd.models import tpch
@@ -368,7 +377,8 @@ def main():
                       "exec_wall_ms": round(1e3 * sum(w for _, w in exec_cost[:ncost]) / max(1, ncost), 3),
                       "executors": getattr(srv, "nexec", None),
                       "coalesced": co1 - co0, "slots": co.scheduler.nslots,
-                      "slot_wait_ms_total": round(co.scheduler.stats["wait_ms"], 1)},
+                      "slot_wait_ms_total": round(co.scheduler.stats["wait_ms"], 1),
+                      "gpu_wait": a.wait if wait_set or a.wait == "spin" else "spin (flag refused)"},
            "device_memory": _mem_report()}
     if a.timeline and a.server == "native" and srv.timeline is not None:
         out["timeline"] = timeline_summary(srv.timeline, a.timeline)

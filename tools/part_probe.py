@@ -31,6 +31,7 @@ def main():
                          "(the index's order: time, then key within a day)")
     ap.add_argument("--check", type=int, default=1)
     ap.add_argument("--fast", type=int, default=1, help="1: the split kernels' same-bucket-wave path (clustered keys)")
+    ap.add_argument("--lds-min", default="0", help="scatter LDS request floor variants in bytes (fewer blocks per CU)")
     a = ap.parse_args()
     import torch
 
@@ -92,8 +93,8 @@ def main():
     print(f"cluster={a.cluster} fast={a.fast} n={n} G={G} RW={RW} chunks={nch} fill={a.fill} shift={shift} levels={levels} P1={p1} P2={p2} K={K} "
           f"k1={k1} records={mb:.0f} MB", flush=True)
 
-    def run(pu):
-        nat.part_tune(pu)
+    def run(pu, lds_min=0):
+        nat.part_tune(pu, lds_min)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(8)]
         names = []
         ev[0].record()
@@ -146,10 +147,10 @@ def main():
             out[nm] = ev[i].elapsed_time(ev[i + 1])
         return out
 
-    for v in [int(x) for x in a.pu.split(",")]:
+    for v, lm in [(int(x), int(y)) for x in a.pu.split(",") for y in a.lds_min.split(",")]:
         ts = []
         for it in range(a.iters + 1):
-            r = run(v)
+            r = run(v, lm)
             if it:
                 ts.append(r)
         med = {k: sorted(t[k] for t in ts)[len(ts) // 2] for k in ts[0]}
@@ -158,7 +159,7 @@ def main():
                "agg": mb / 1e3}
         line = " ".join(f"{k}={ms:.3f}ms" + (f"({gbs[k] / ms:.2f}TB/s)" if k in gbs and ms > 0 else "")
                         for k, ms in med.items())
-        print(f"pu={v}: total {tot:.3f} ms  {line}", flush=True)
+        print(f"pu={v} lds_min={lm}: total {tot:.3f} ms  {line}", flush=True)
         if a.check and RW == 2:
             keys = view[..., 0].reshape(-1).to(torch.int64)
             cnt = torch.bincount(keys, minlength=G)
