@@ -117,7 +117,9 @@ def test_parameterizations_share_the_slot_arena():
             assert rows(r) == rows(ref), i
     assert len(ptrs) == 1, "the parameterizations did not share the slot's arena region"
     ar = DE.slot_arena(ds.device, 1)
-    assert ar.cap < 4 * ar.need + DE.ARENA_MIN
+    # (sized for its own need -- or straight to a larger peer slot's size, set by earlier tests)
+    peers = max((a.cap for k, a in DE._ARENAS.items() if k[0] == str(ds.device) and a is not ar), default=0)
+    assert ar.cap < 4 * ar.need + DE.ARENA_MIN or ar.cap <= peers
 
 
 def test_partition_scratch_pool_budget_reuse_and_wait(monkeypatch):
