@@ -650,7 +650,12 @@ class PreparedScan:
         # kernels' same-bucket waves add once (partition.hip lds_count_add); hashes are uniform
         cl = 0 if L.get("hashed") else 2
         nat.part_scan(pb["counts1"].data_ptr(), P1, k1, pb["totals1"].data_ptr(), pb["base1"].data_ptr(), st)
-        nat.part_split(*a1, pb["base1"].data_ptr(), pb["recs2"].data_ptr(), 1 | cl, st)
+        # (a small value field packed into the key word above shift1: one word less per record for
+        # every later pass -- part_layout "pack")
+        pk = L.get("pack")
+        nat.part_split(*a1, pb["base1"].data_ptr(), pb["recs2"].data_ptr(), 1 | cl | ((pk[1] if pk else 0) << 8), st)
+        rw = L.get("rw1", rw)
+        fields = L.get("agg_fields", L["fields"])
         recs, base = pb["recs2"], pb["base1"]
         if L["levels"] == 2:
             # level 2: group p = level-1 bucket p (one segment [base1[p], base1[p+1])), P2 sub-buckets
@@ -667,8 +672,8 @@ class PreparedScan:
         hv, tk = self.part_having, self.part_topk
         if hv is None and tk is None:
             # (HLL aggregators: each sub-bucket also writes its groups' rows of the register tables)
-            nat.part_agg_hll(recs.data_ptr(), L["rw"], base.data_ptr(), L["nsub"], int(prog.G), L["shift"],
-                             [f[0] for f in L["fields"]], [f[1] for f in L["fields"]],
+            nat.part_agg_hll(recs.data_ptr(), rw, base.data_ptr(), L["nsub"], int(prog.G), L["shift"],
+                             [f[0] for f in fields], [f[1] for f in fields],
                              [int(op) for op, _ in prog.slots], [int(init) for _, init in prog.slots],
                              b.acc.data_ptr(), [], 1, 0, 0, 0, [h.data_ptr() for h in b.hll] if L.get("nhll") else [],
                              int(prog.hll_p), st, self._stored_csr() if L.get("nhll") else [])
@@ -676,8 +681,8 @@ class PreparedScan:
         terms, conj = hv if hv is not None else ([], 1)
         while True:
             acc, keys, cnt, _ = self._sparse_out(b, "hv_out", False)
-            args = (recs.data_ptr(), L["rw"], base.data_ptr(), L["nsub"], int(prog.G), L["shift"],
-                    [f[0] for f in L["fields"]], [f[1] for f in L["fields"]], [int(op) for op, _ in prog.slots],
+            args = (recs.data_ptr(), rw, base.data_ptr(), L["nsub"], int(prog.G), L["shift"],
+                    [f[0] for f in fields], [f[1] for f in fields], [int(op) for op, _ in prog.slots],
                     [int(init) for _, init in prog.slots], acc.data_ptr(), terms, conj, keys.data_ptr(),
                     cnt.data_ptr(), int(acc.shape[0]))
             if tk is not None:
@@ -1783,16 +1788,78 @@ def part_layout(prog) -> dict:
     rw = 1 + sum(w for _, w in fields) + nh
     if rem <= 10:
         p1 = 1 << rem
-        return {"levels": 1, "shift": shift, "shift1": shift, "p1": p1, "p2": 1, "k": 1, "nsub": p1,
-                "fields": fields, "rw": rw, "nhll": nh}
-    b1 = min(10, (rem + 1) // 2)
-    b2 = rem - b1
-    if b2 > 10:
-        raise ValueError(f"partitioned group-by: {prog.G} keys need more than two levels")
-    p1, p2 = 1 << b1, 1 << b2
-    k = max(1, min(64, 4096 // p1))
-    return {"levels": 2, "shift": shift, "shift1": shift + b2, "p1": p1, "p2": p2, "k": k, "nsub": p1 * p2,
-            "fields": fields, "rw": rw, "nhll": nh}
+        L = {"levels": 1, "shift": shift, "shift1": shift, "p1": p1, "p2": 1, "k": 1, "nsub": p1,
+             "fields": fields, "rw": rw, "nhll": nh}
+    else:
+        b1 = min(10, (rem + 1) // 2)
+        b2 = rem - b1
+        if b2 > 10:
+            raise ValueError(f"partitioned group-by: {prog.G} keys need more than two levels")
+        p1, p2 = 1 << b1, 1 << b2
+        k = max(1, min(64, 4096 // p1))
+        L = {"levels": 2, "shift": shift, "shift1": shift + b2, "p1": p1, "p2": p2, "k": k, "nsub": p1 * p2,
+             "fields": fields, "rw": rw, "nhll": nh}
+    # (3+ word records only: one-word records stream at a third of the two-word rate through the
+    # split and aggregation kernels -- TPC-H Q18 packed 2 -> 1 word was slower, profiles/r6/pack_ab.txt)
+    pk = _pack_field(prog, fields, L["shift1"]) if PACK_RECORDS and not nh and rw >= 3 else None
+    if pk is not None:
+        j, word = pk
+        L["pack"] = pk
+        L["rw1"] = rw - 1
+        L["agg_fields"] = [(s_, (3 | (L["shift1"] << 8)) if i == j else w_) for i, (s_, w_) in enumerate(fields)]
+    return L
+
+
+# The level-1 split packs one small non-negative value field of a partition record into the key
+# word's bits above shift1 -- bits the level-1 bucket and the sub-bucket imply -- so the level-2
+# split and the aggregation move one word less per record (the BI plan's TopVolumeCustomers: key +
+# o_totalprice + l_quantity, 12 -> 8 bytes a record after level 1, 15.1 -> 12.6 ms a statement at
+# SF100, tools/pack_ab.py, profiles/r6/pack_ab.txt).
+PACK_RECORDS = True
+
+
+def _value_range(ds, name: str):
+    """(min, max) of a column's stored values (cached per datasource)."""
+    cache = ds.__dict__.setdefault("_value_ranges", {})
+    r = cache.get(name)
+    if r is None:
+        from .lower import column_tensor
+
+        t = column_tensor(ds, name)
+        if t.numel() == 0 or t.is_floating_point():
+            r = cache[name] = False
+        else:
+            mn, mx = torch.aminmax(t)
+            r = cache[name] = (int(mn), int(mx))
+    return r or None
+
+
+def _pack_field(prog, fields, shift1: int):
+    """(field index, record word) of the first one-word field whose values fit the key word's bits
+    above ``shift1``: a filtered count (0 / 1) or an unexpressioned integer sum over a column with
+    non-negative values (a filter that rejects the row writes the identity 0).  None otherwise."""
+    from ..ops import jit
+
+    free = 32 - int(shift1)
+    if free < 1 or not hasattr(prog, "aops"):
+        return None
+    cols = jit.col_infos(prog)
+    by_slot = {a["slot"]: a for a in prog.aops}
+    word = 1
+    for j, (slot, wd) in enumerate(fields):
+        if wd == 1:
+            a = by_slot.get(slot)
+            bits = None
+            if a is not None and a["kind"] == D.A_COUNT and a.get("filt_len"):
+                bits = 1
+            elif a is not None and a["kind"] == D.A_SUM_I and not a.get("expr") and a.get("col") in cols:
+                rng = _value_range(prog.ds, cols[a["col"]].name)
+                if rng is not None and rng[0] >= 0:
+                    bits = max(1, int(rng[1]).bit_length())
+            if bits is not None and bits <= free:
+                return j, word
+        word += wd
+    return None
 
 
 def part_hash_layout(prog, scale: int = 1, groups: Optional[float] = None) -> dict:

@@ -69,7 +69,7 @@ __global__ void part_keys_kernel(const int64_t* keys, int64_t n, int shift1, int
 template <int PU, bool CL>
 __global__ void part_split_kernel(const uint32_t* in, int RW, int RS, const uint32_t* seg_lo, const uint32_t* seg_hi, int spg,
                                   int K, int shift2, int P2, uint32_t* counts2, const uint32_t* base2, uint32_t* out,
-                                  int phase);
+                                  int phase, int pk_w);
 __global__ void part_hash_agg_kernel(const uint32_t* recs, int RW, const uint32_t* base, int64_t nsub, int cap_log2,
                                      PartFields f, PartHll hl, PartHaving hv, int64_t* out_keys, uint64_t* out_acc,
                                      unsigned long long* out_count, int64_t cap, int* overflow);
@@ -609,8 +609,13 @@ static void part_split(uint64_t in, int RW, uint64_t seg_lo, uint64_t seg_hi, in
   int RS = RW;
   const int64_t lds_max = 160 * 1024 - 256;
   if (RW >= 4 && RW % 2 == 0 && ((int64_t)3 * P2 + (int64_t)512 * PU * (RW + 1)) * 4 <= lds_max) RS = RW + 1;
-  // (phase bit 1: clustered keys, see partition.hip part_split_kernel)
+  // (phase bit 1: clustered keys, see partition.hip part_split_kernel; bits 8+: pk_w, the record
+  // word a level-1 scatter packs into the key word above shift2 -- the output is RW - 1 words)
+  int pk_w = (phase >> 8) & 0xff;
+  phase &= 0xff;
   if ((phase & ~3) != 0) throw std::invalid_argument("part_split: phase");
+  if (pk_w && (!(phase & 1) || pk_w >= RW || shift2 < 1 || shift2 > 31))
+    throw std::invalid_argument("part_split: packed word");
   int64_t lds = (phase & 1) == 0 ? (int64_t)P2 * 4 : ((int64_t)3 * P2 + (int64_t)512 * PU * RS) * 4;
   if ((phase & 1) && lds < g_part_lds_min) lds = g_part_lds_min;
   if (lds > lds_max) throw std::invalid_argument("part_split: tile does not fit the LDS");
@@ -633,7 +638,7 @@ static void part_split(uint64_t in, int RW, uint64_t seg_lo, uint64_t seg_hi, in
   const uint32_t* b2 = (const uint32_t*)base2;
   uint32_t* o = (uint32_t*)out;
   void* args[] = {(void*)&in_, (void*)&RW, (void*)&RS, (void*)&lo_, (void*)&hi_, (void*)&spg, (void*)&K,
-                  (void*)&shift2, (void*)&P2, (void*)&c2, (void*)&b2, (void*)&o, (void*)&phase};
+                  (void*)&shift2, (void*)&P2, (void*)&c2, (void*)&b2, (void*)&o, (void*)&phase, (void*)&pk_w};
   if (lds > 64 * 1024) check(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "part_split attr");
   check(hipLaunchKernel(f, dim3((unsigned)(groups * K)), dim3(512), args, (size_t)lds, (hipStream_t)stream),
         "part_split_kernel launch");
@@ -660,10 +665,19 @@ static void part_agg_hll(uint64_t recs, int RW, uint64_t base, int64_t nsub, int
   f.nslots = (int)ops.size();
   int words = 1;
   for (size_t j = 0; j < slot.size(); ++j) {
-    if (slot[j] < 0 || slot[j] >= f.nslots || width[j] < 0 || width[j] > 2) throw std::invalid_argument("part_agg: field");
+    // width PART_PACKED | shift << 8: a value the level-1 split packed into the key word above `shift`
+    const int wd = width[j] & 0xff;
+    if (wd == sdo::PART_PACKED) {
+      const int ps = width[j] >> 8;
+      if (f.pk_shift || ps < shift || ps > 31) throw std::invalid_argument("part_agg: packed field");
+      f.pk_shift = ps;
+    } else if (width[j] < 0 || width[j] > 2) {
+      throw std::invalid_argument("part_agg: field");
+    }
+    if (slot[j] < 0 || slot[j] >= f.nslots) throw std::invalid_argument("part_agg: field");
     f.slot[j] = slot[j];
-    f.width[j] = width[j];
-    words += width[j];
+    f.width[j] = wd;
+    words += wd == sdo::PART_PACKED ? 0 : wd;
   }
   sdo::PartHll hl{};
   if (hll.size() > (size_t)sdo::PART_MAX_HLL || (!hll.empty() && (hll_p < 4 || hll_p > 16)))

@@ -290,11 +290,14 @@ __device__ __forceinline__ void split_map_count(const uint32_t* __restrict__ in,
   }
 }
 
+// pk_w (> 0, level 1 only): record word pk_w -- a small non-negative value -- leaves packed into the
+// key word above bit shift2 (the key bits the bucket and sub-bucket imply), the other words after
+// it: every later pass (level-2 split, aggregation) moves RW - 1 words per record.
 template <int PU, bool CL, class Map>
 __device__ __forceinline__ void split_range_scatter(const uint32_t* __restrict__ in, int RW, int RS, Map map, uint32_t n,
                                                     int shift2, uint32_t P2, uint32_t* cur, uint32_t* hist,
                                                     uint32_t* tstart, uint32_t* tile, uint32_t* scan_lds,
-                                                    uint32_t* __restrict__ out) {
+                                                    uint32_t* __restrict__ out, int pk_w = 0) {
   const uint32_t mask = P2 - 1u;
   constexpr uint32_t TILE = 512u * PU;
   for (uint32_t t0 = 0; t0 < n; t0 += TILE) {
@@ -379,6 +382,8 @@ __device__ __forceinline__ void split_range_scatter(const uint32_t* __restrict__
         const uint32_t d = tstart[q_[u]] + r_[u];
         if (RW == 2) {
           ((uint2*)tile)[d] = v2[u];
+        } else if (RW == 1) {
+          tile[d] = v2[u].x;  // (the key is the record)
         } else {
           const uint32_t* rec = in + map(t0 + j) * RW;
           for (int w = 0; w < RW; ++w) tile[(uint64_t)d * RS + w] = rec[w];
@@ -393,7 +398,19 @@ __device__ __forceinline__ void split_range_scatter(const uint32_t* __restrict__
         const uint32_t key = tile[(uint64_t)j * RS];
         const uint32_t q = (key >> shift2) & mask;
         const uint64_t pos = (uint64_t)cur[q] + (j - tstart[q]);
-        if (RW == 2) {
+        if (pk_w > 0) {
+          const uint32_t lo = key & ((1u << shift2) - 1u);
+          const uint32_t w0 = lo | (tile[(uint64_t)j * RS + pk_w] << shift2);
+          if (RW == 2) {
+            out[pos] = w0;
+          } else {
+            const int RO = RW - 1;
+            out[pos * RO] = w0;
+            int o = 1;
+            for (int w = 1; w < RW; ++w)
+              if (w != pk_w) out[pos * RO + o++] = tile[(uint64_t)j * RS + w];
+          }
+        } else if (RW == 2) {
           *(uint2*)(out + pos * 2) = ((const uint2*)tile)[j];
         } else {
           for (int w = 0; w < RW; ++w) out[pos * RW + w] = tile[(uint64_t)j * RS + w];
@@ -417,7 +434,7 @@ __global__ __launch_bounds__(512) void part_split_kernel(const uint32_t* __restr
                                                         const uint32_t* __restrict__ seg_hi, int spg, int K, int shift2,
                                                         int P2, uint32_t* __restrict__ counts2,
                                                         const uint32_t* __restrict__ base2, uint32_t* __restrict__ out,
-                                                        int phase) {
+                                                        int phase, int pk_w) {
   extern __shared__ __attribute__((aligned(16))) uint32_t h[];
   __shared__ uint32_t scan_lds[8];
   const int64_t g = blockIdx.x / K;
@@ -436,7 +453,7 @@ __global__ __launch_bounds__(512) void part_split_kernel(const uint32_t* __restr
     const uint32_t a = lo + (uint32_t)(n * k / K), e = lo + (uint32_t)(n * (k + 1) / K);
     if (phase == 0) split_range_count<CL>(in, RW, a, e, shift2, mask, h);
     else split_range_scatter<PU, CL>(in, RW, RS, Contig{a}, e - a, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds,
-                                     out);
+                                     out, pk_w);
   } else {
     // the block's regions in groups of up to 512: lengths prefix-summed in LDS; groups of small
     // regions (< 1024 records on average) run as packed tiles, large ones region by region
@@ -462,14 +479,15 @@ __global__ __launch_bounds__(512) void part_split_kernel(const uint32_t* __restr
       if (tot < 1024u * (uint32_t)ns) {
         const Packed pm{slo, spre, ns};
         if (phase == 0) split_map_count<CL>(in, RW, pm, tot, shift2, mask, h);
-        else split_range_scatter<PU, CL>(in, RW, RS, pm, tot, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds, out);
+        else split_range_scatter<PU, CL>(in, RW, RS, pm, tot, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds, out,
+                                         pk_w);
       } else {
         for (int si = 0; si < ns; ++si) {
           const uint32_t lo = slo[si], n = spre[si + 1] - spre[si];
           if (n == 0) continue;  // (uniform across the block: every thread reads the same LDS entry)
           if (phase == 0) split_range_count<CL>(in, RW, lo, lo + n, shift2, mask, h);
           else split_range_scatter<PU, CL>(in, RW, RS, Contig{lo}, n, shift2, (uint32_t)P2, h, hist, tstart, tile,
-                                           scan_lds, out);
+                                           scan_lds, out, pk_w);
         }
       }
       __syncthreads();  // (slo / spre are rewritten for the next group)
@@ -482,29 +500,29 @@ __global__ __launch_bounds__(512) void part_split_kernel(const uint32_t* __restr
 }
 
 template __global__ void part_split_kernel<32, false>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
-                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int, int);
 template __global__ void part_split_kernel<32, true>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
-                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int, int);
 template __global__ void part_split_kernel<16, false>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
-                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int, int);
 template __global__ void part_split_kernel<16, true>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
-                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int, int);
 template __global__ void part_split_kernel<8, false>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
-                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int, int);
 template __global__ void part_split_kernel<8, true>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
-                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int, int);
 template __global__ void part_split_kernel<4, false>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
-                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int, int);
 template __global__ void part_split_kernel<4, true>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
-                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int, int);
 template __global__ void part_split_kernel<2, false>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
-                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int, int);
 template __global__ void part_split_kernel<2, true>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
-                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int, int);
 template __global__ void part_split_kernel<1, false>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
-                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int, int);
 template __global__ void part_split_kernel<1, true>(const uint32_t*, int, int, const uint32_t*, const uint32_t*, int, int, int,
-                                                       int, uint32_t*, const uint32_t*, uint32_t*, int);
+                                                       int, uint32_t*, const uint32_t*, uint32_t*, int, int);
 
 __device__ __forceinline__ void lds_fold(uint64_t* t, int op, int64_t v) {
   switch (op) {
@@ -693,6 +711,26 @@ __global__ __launch_bounds__(512) void part_agg_kernel(const uint32_t* __restric
         lds_fold(t + local * NS + s0, op, (int64_t)(int32_t)r2[u].y);
       }
     }
+  } else if (hl.n == 0 && RW == 1 && f.nfields == 1 && f.width[0] == PART_PACKED) {
+    // one value packed into the key word by the level-1 split (TPC-H Q18: sum(l_quantity) per
+    // order, 600M one-word records): the key's low bits locate the group, the high bits are the value
+    const int s0 = f.slot[0], op = f.op[s0], ps = f.pk_shift;
+    const uint32_t lmask = (1u << shift) - 1u;
+    for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += step) {
+      uint32_t kk[PU];
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        const uint32_t i = i0 + u * blockDim.x;
+        if (i < hi) kk[u] = recs[i];
+      }
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        if (i0 + u * blockDim.x >= hi) break;
+        const int64_t local = (int64_t)(kk[u] & lmask);
+        if (local >= nk) continue;
+        lds_fold(t + local * NS + s0, op, (int64_t)(kk[u] >> ps));
+      }
+    }
   } else if (hl.n == 0 && RW == 1 && f.nfields == 1 && f.width[0] == 0) {
     // key only (histograms, unfiltered counts)
     const int s0 = f.slot[0], op = f.op[s0];
@@ -733,13 +771,19 @@ __global__ __launch_bounds__(512) void part_agg_kernel(const uint32_t* __restric
 #pragma unroll
       for (int u = 0; u < PU; ++u) {
         if (i0 + u * blockDim.x >= hi) break;
-        const int64_t local = (int64_t)r4[u][0] - k0;
+        // (a packed record's key word carries a value above pk_shift: the group is its low bits)
+        const int64_t local = f.pk_shift ? (int64_t)(r4[u][0] & ((1u << shift) - 1u)) : (int64_t)r4[u][0] - k0;
         if ((uint64_t)local >= (uint64_t)nk) continue;  // cannot happen for consistent buckets; never fault
         uint64_t* row = t + local * NS;
         int w = 1;
         for (int j = 0; j < f.nfields; ++j) {
           const int wd = f.width[j];
           int64_t v;
+          if (wd == PART_PACKED) {
+            const int sl = f.slot[j];
+            lds_fold(row + sl, f.op[sl], (int64_t)(r4[u][0] >> f.pk_shift));
+            continue;
+          }
           if (wd == 0) v = 1;
           else if (wd == 1) v = (int64_t)(int32_t)r4[u][w & 3];
           else v = (int64_t)((uint64_t)r4[u][w & 3] | ((uint64_t)r4[u][(w + 1) & 3] << 32));
@@ -752,13 +796,18 @@ __global__ __launch_bounds__(512) void part_agg_kernel(const uint32_t* __restric
   } else {
     for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
       const uint32_t* rec = recs + (uint64_t)i * RW;
-      const int64_t local = (int64_t)rec[0] - k0;
+      const int64_t local = f.pk_shift ? (int64_t)(rec[0] & ((1u << shift) - 1u)) : (int64_t)rec[0] - k0;
       if ((uint64_t)local >= (uint64_t)nk) continue;  // cannot happen for consistent buckets; never fault
       uint64_t* row = t + local * NS;
       int w = 1;
       for (int j = 0; j < f.nfields; ++j) {
         const int wd = f.width[j];
         int64_t v;
+        if (wd == PART_PACKED) {
+          const int sl = f.slot[j];
+          lds_fold(row + sl, f.op[sl], (int64_t)(rec[0] >> f.pk_shift));
+          continue;
+        }
         if (wd == 0) v = 1;
         else if (wd == 1) v = (int64_t)(int32_t)rec[w];
         else v = (int64_t)((uint64_t)rec[w] | ((uint64_t)rec[w + 1] << 32));

@@ -212,6 +212,10 @@ struct ScanDesc {
 
 // Fields of a partition record (partition.hip part_agg_kernel): value j is width[j] u32 words
 // (0 = implicit 1, 1 = i32, 2 = i64) folded into slot[j] with op[slot].
+// width: u32 words of the field in the record (0: an implicit 1, 1: int32, 2: int64 / f64 bits) or
+// PART_PACKED: a small non-negative value the level-1 split packed into the key word above bit
+// pk_shift (the bits the sub-bucket already implies), so the record is one word narrower.
+constexpr int32_t PART_PACKED = 3;
 struct PartFields {
   int32_t nfields;
   int32_t nslots;
@@ -219,6 +223,8 @@ struct PartFields {
   int32_t width[MAX_SLOTS];
   int32_t op[MAX_SLOTS];
   int64_t init[MAX_SLOTS];
+  int32_t pk_shift;  // bit of the packed field in the key word (0: no packed field)
+  int32_t pad_;
 };
 
 // HLL aggregators of the partitioned group-by (partition.hip part_agg_kernel): each record carries
