@@ -401,6 +401,33 @@ class NativeHiveServer(HiveThriftServer):
         return list(df.columns), [t for _, t in df.schema], res
 
 
+def warm_up(session, statements) -> dict:
+    """A server's warm-up before it takes clients (``hive_server --warmup FILE``): each statement is
+    prepared (first-seen kernels compile) and run once on a leased execution slot, once more after
+    the background compiles it started have finished (its final plan), and then every slot's device
+    memory is sized for the largest of them (engine/device_exec.py presize_device_memory) -- the
+    service then starts with its arenas, partition scratch and kernels in place."""
+    from ..engine.device_exec import async_compile, presize_device_memory, wait_background_compiles
+
+    sched = session.engine.coalescer().scheduler
+    ran = 0
+    for rnd in range(2):
+        for st in statements:
+            df = session.sql(st)
+            if df.plan is None:
+                continue
+            with async_compile():
+                df.prepare()
+            with sched.lease():
+                df.run()
+            ran += 1
+        if not wait_background_compiles():
+            break
+    out = presize_device_memory(session.engine.world.device(), sched.nslots)
+    out["statements_run"] = ran
+    return out
+
+
 def _alloc_retries() -> int:
     return int(torch.cuda.memory_stats().get("num_alloc_retries", 0)) if torch.cuda.is_available() else 0
 

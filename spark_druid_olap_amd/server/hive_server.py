@@ -695,6 +695,10 @@ def main(argv=None):
     ap.add_argument("--segments", default=None,
                     help="segment store root: load every datasource saved under DIR/<datasource>/rank<r> "
                          "(resume after restart); with --ingest, the ingested shards are saved there")
+    ap.add_argument("--warmup", default=None,
+                    help="file of ';'-separated statements the server runs (on its execution slots) before "
+                         "taking clients; the slots' device memory is then sized for the largest "
+                         "(server/gateway.py warm_up)")
     ap.add_argument("--gpu-wait", default="spin", choices=["blocking", "spin"],
                     help="HIP's wait mode for server threads (utils/hipsync.py): spin (HIP's default; the "
                          "engine's own waits sleep after 1 ms anyway) or blocking (every wait sleeps on the "
@@ -742,6 +746,12 @@ def main(argv=None):
             for st in f.read().split(";"):
                 if st.strip():
                     sess.sql(st)
+    if a.warmup and not world.distributed:
+        from .gateway import warm_up
+
+        with open(a.warmup) as f:
+            stmts = [st for st in f.read().split(";") if st.strip()]
+        logging.getLogger("sdo.thrift").info("warm-up: %s", warm_up(sess, stmts))
     if world.rank != 0:
         from ..parallel.world import shutdown
         from .spmd import serve_peer

@@ -363,3 +363,19 @@ def test_two_rank_python_server_streams_select_pages(tmp_path):
         except subprocess.TimeoutExpired:
             p.kill()
     assert p.returncode == 0, p.stderr.read().decode()[-3000:]
+
+
+def test_warm_up_runs_each_statement_on_a_slot(ds_small, df_small):
+    """server/gateway.py warm_up: statements run on leased execution slots (commands just execute)
+    and the call reports what it ran; without a GPU the device-memory sizing is a no-op."""
+    from spark_druid_olap_amd.server.gateway import warm_up
+
+    s = Session(engine=Engine(use_native=False))
+    s.register_datasource(ds_small)
+    s.register_table("orderLineItemPartSupplierBase", df_small, schema=tpch.FLAT_SCHEMA)
+    s.sql(tpch.druid_ddl(with_column_mapping=False))
+    leases0 = s.engine.coalescer().scheduler.stats["leases"]
+    out = warm_up(s, ["select l_returnflag, count(*) from orderLineItemPartSupplier group by l_returnflag",
+                      "set spark.sparklinedata.druid.deterministic=false"])
+    assert out["statements_run"] == 1
+    assert s.engine.coalescer().scheduler.stats["leases"] == leases0 + 1
