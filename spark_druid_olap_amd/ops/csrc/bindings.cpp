@@ -101,10 +101,10 @@ static void check(hipError_t e, const char* what) {
 // own wait spins the thread's core for the whole wait (tools/sync_cpu_probe.py: CPU time == wall
 // time), which is right for sub-millisecond scans and wasteful for a server's 10-50 ms partitioned
 // group-bys, whose executor threads then burn the cores the clients and compile threads need
-// (exec_thread_cpu_ms).  Hybrid: poll for g_wait_spin_us (the latency of a short scan is
-// unchanged), then sleep between polls (20 us doubling to 200 us: a long wait ends at most ~0.2 ms
-// late and costs ~1 us of CPU per poll).
-static int64_t g_wait_spin_us = 1000;
+// (exec_thread_cpu_ms).  Hybrid: poll for g_wait_spin_us -- 2 ms, longer than every headline scan
+// (TPC-H Q1 at SF100 waits ~1.05 ms), so their latency is unchanged -- then sleep between polls
+// (20 us doubling to 200 us: a long wait ends at most ~0.2 ms late, ~1 us of CPU per poll).
+static int64_t g_wait_spin_us = 2000;
 static void set_wait_spin(int64_t us) {
   if (us < 0) throw std::invalid_argument("set_wait_spin: microseconds >= 0");
   g_wait_spin_us = us;

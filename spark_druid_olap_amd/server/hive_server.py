@@ -701,7 +701,7 @@ def main(argv=None):
                          "(server/gateway.py warm_up)")
     ap.add_argument("--gpu-wait", default="spin", choices=["blocking", "spin"],
                     help="HIP's wait mode for server threads (utils/hipsync.py): spin (HIP's default; the "
-                         "engine's own waits sleep after 1 ms anyway) or blocking (every wait sleeps on the "
+                         "engine's own waits sleep after 2 ms anyway) or blocking (every wait sleeps on the "
                          "completion interrupt: least CPU, less throughput near capacity)")
     ap.add_argument("--elastic", action="store_true",
                     help="survive a lost GPU process: heartbeats, communicator rebuild over the survivors and "

@@ -9,7 +9,7 @@ clients, compile threads and gateway need (``exec_thread_cpu_ms`` of tools/concu
 ``hipDeviceScheduleBlockingSync`` makes those waits sleep on the completion interrupt instead
 (0.3 ms of CPU per wait, profiles/r6/sync_cpu_probe.txt) -- but every wake-up then comes late: at
 400 QPS of the BI plan the server's capacity fell below the offered load (382/s, p99 2.3 s vs
-126 ms spinning).  The engine's own waits therefore spin for 1 ms and then sleep between polls
+126 ms spinning).  The engine's own waits therefore spin for 2 ms and then sleep between polls
 (ops/csrc/bindings.cpp wait_stream), and the servers keep HIP's spin mode by default.  The flag is
 per device and only takes before the process's first HIP call touches the device, so server entry
 points set it first thing when asked to.

@@ -210,7 +210,7 @@ def main():
                     help="varied workload: plan + compile this many distinct texts before the clock starts")
     ap.add_argument("--wait", default="spin", choices=["blocking", "spin"],
                     help="HIP's wait mode for the server's threads (utils/hipsync.py): spin (HIP's default; the "
-                         "engine's own waits still sleep after 1 ms, ops/csrc/bindings.cpp wait_stream) or "
+                         "engine's own waits still sleep after 2 ms, ops/csrc/bindings.cpp wait_stream) or "
                          "blocking (every wait sleeps on the interrupt: least CPU, ~40%% less capacity at 400 QPS, "
                          "profiles/r6/thrift_jmx_q400_blocking_wait.json)")
     ap.add_argument("--settle", action="store_true",
