@@ -4,6 +4,7 @@
 // builds in seconds with hipcc.  It must be imported after torch so that the HIP runtime torch
 // loaded (same SONAME) is the one this module binds to.
 #include <hip/hip_runtime.h>
+#include <sys/prctl.h>
 #include <hip/hiprtc.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -103,13 +104,18 @@ static void check(hipError_t e, const char* what) {
 // group-bys, whose executor threads then burn the cores the clients and compile threads need
 // (exec_thread_cpu_ms).  Hybrid: poll for g_wait_spin_us -- 2 ms, longer than every headline scan
 // (TPC-H Q1 at SF100 waits ~1.05 ms), so their latency is unchanged -- then sleep between polls
-// (20 us doubling to 200 us: a long wait ends at most ~0.2 ms late, ~1 us of CPU per poll).
+// (20 us, then 40, then 50 us: a long wait ends at most ~50 us late, ~1 us of CPU per poll; naps
+// capped at 200 us left a 0.25 ms gap after TopVolumeCustomers' aggregation,
+// profiles/r6/rocprof_bi_topvolume_sf100_packed.txt).
 static int64_t g_wait_spin_us = 2000;
 static void set_wait_spin(int64_t us) {
   if (us < 0) throw std::invalid_argument("set_wait_spin: microseconds >= 0");
   g_wait_spin_us = us;
 }
 static void wait_stream(hipStream_t st, const char* what) {
+  // (a thread's first sleeping wait drops its timer slack to 1 us: Linux otherwise rounds a 20 us
+  // nap up by its default 50 us slack, and the statement's end is seen that much later)
+  static thread_local bool slack_set = false;
   const auto t0 = std::chrono::steady_clock::now();
   int64_t nap = 20;
   while (true) {
@@ -119,8 +125,12 @@ static void wait_stream(hipStream_t st, const char* what) {
     const int64_t el =
         std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
     if (el < g_wait_spin_us) continue;
+    if (!slack_set) {
+      prctl(PR_SET_TIMERSLACK, 1000UL, 0UL, 0UL, 0UL);
+      slack_set = true;
+    }
     std::this_thread::sleep_for(std::chrono::microseconds(nap));
-    nap = nap * 2 > 200 ? 200 : nap * 2;
+    nap = nap * 2 > 50 ? 50 : nap * 2;
   }
 }
 

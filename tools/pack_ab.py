@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
-"""In-process A/B of the partitioned group-by's record packing (engine/device_exec.py
-PACK_RECORDS): the same statements re-prepared with packing on and off, median wall times.
+"""In-process A/B of partitioned group-by layout choices: record packing (engine/device_exec.py
+PACK_RECORDS, default) or the sub-bucket LDS table size (``--table 32768,65536``: PART_TABLE_BYTES)
+-- the same statements re-prepared under each variant, best-of-two median wall times.
 
-  python tools/pack_ab.py [--sf 100] [--queries Q18,Q13] [--iters 15]"""
+  python tools/pack_ab.py [--sf 100] [--queries Q18,Q13] [--iters 15] [--table 32768,65536]"""
 import argparse
 import os
 import statistics
@@ -19,6 +20,7 @@ def main():
     ap.add_argument("--bi", default="TopVolumeCustomers")
     ap.add_argument("--iters", type=int, default=15)
     ap.add_argument("--only", type=int, default=None, help="1 / 0: run one variant only (profiling)")
+    ap.add_argument("--table", default=None, help="PART_TABLE_BYTES variants instead of packing on / off")
     a = ap.parse_args()
     import torch
 
@@ -38,9 +40,16 @@ def main():
         stmts += [(n, q) for n, _, q in bi.statements(1, "years") if n == a.bi][:1]
     for name, sql in stmts:
         res = {}
+        if a.table:
+            variants = [("table", int(x)) for x in a.table.split(",")]
+        else:
+            variants = [("pack", p) for p in ((True, False) if a.only is None else (bool(a.only),))]
         for rnd in range(2):
-            for pack in ((True, False) if a.only is None else (bool(a.only),)):
-                DE.PACK_RECORDS = pack
+            for kind, val in variants:
+                if kind == "table":
+                    DE.PART_TABLE_BYTES = val
+                else:
+                    DE.PACK_RECORDS = val
                 s._plan_cache.clear()
                 d = s.sql(sql).prepared()
                 for _ in range(3):
@@ -52,9 +61,8 @@ def main():
                     d.run()
                     torch.cuda.synchronize()
                     ts.append((time.perf_counter() - t0) * 1e3)
-                res.setdefault(pack, []).append(statistics.median(ts))
-        print(f"{name:24s} " + "  ".join(f"{'packed' if k else 'unpacked'} {min(v):7.3f} ms" for k, v in res.items()),
-              flush=True)
+                res.setdefault((kind, val), []).append(statistics.median(ts))
+        print(f"{name:24s} " + "  ".join(f"{k}={v} {min(t):7.3f} ms" for (k, v), t in res.items()), flush=True)
     DE.PACK_RECORDS = True
 
 
