@@ -691,8 +691,8 @@ class PreparedScan:
                 nat.part_agg_topk(*args, *tk, st)
             else:
                 nat.part_agg(*args, st)
-            native.stream_sync(self.dev)  # (the whole partition pipeline: a sleeping wait, not a spin)
-            n = int(cnt[0].item())
+            # (the whole partition pipeline: one copy + one sleeping wait, not a spin + a round trip)
+            n = int(native.read_words([cnt], self.dev)[0])
             if n <= acc.shape[0]:
                 return Partials("sparse", acc[:n], keys[:n], [])
             self.part_cap = _next_pow2(n + n // 4)  # more survivors than room: grow, aggregate again
@@ -722,8 +722,7 @@ class PreparedScan:
                                   [int(op) for op, _ in prog.slots], [int(init) for _, init in prog.slots], hv[0],
                                   hv[1], keys.data_ptr(), acc.data_ptr(), cnt.data_ptr(), int(acc.shape[0]),
                                   ovf.data_ptr(), [h.data_ptr() for h in hll], int(prog.hll_p), st)
-            native.stream_sync(self.dev)
-            n, overflow = int(cnt[0].item()), int(ovf.item())
+            n, overflow = (int(x) for x in native.read_words([cnt, ovf], self.dev))
             if overflow:
                 if L["scale"] >= 1 << 12:
                     raise RuntimeError("hash-partitioned group-by: sub-bucket overflow persists")

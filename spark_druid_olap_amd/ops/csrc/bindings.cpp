@@ -561,6 +561,29 @@ static void stream_sync(uint64_t stream) {
   wait_stream((hipStream_t)stream, "stream sync");
 }
 
+// Device int64 words -> host behind the stream's work, ONE wait (the partitioned aggregation's
+// survivor count and overflow flag): a copy into this thread's pinned words, then the stream wait
+// -- instead of a wait for the kernels and a second round trip for each .item().
+static std::vector<int64_t> read_words(std::vector<uint64_t> ptrs, std::vector<int> bytes, uint64_t stream) {
+  static thread_local int64_t* pin = nullptr;
+  if (ptrs.size() > 16 || bytes.size() != ptrs.size()) throw std::invalid_argument("read_words: <= 16 (ptr, bytes)");
+  for (int b : bytes)
+    if (b != 4 && b != 8) throw std::invalid_argument("read_words: 4- or 8-byte words");
+  std::vector<int64_t> out(ptrs.size());
+  {
+    py::gil_scoped_release nogil;
+    if (!pin) check(hipHostMalloc((void**)&pin, 16 * sizeof(int64_t), hipHostMallocDefault), "read_words pin");
+    for (size_t i = 0; i < ptrs.size(); ++i) {
+      pin[i] = 0;
+      check(hipMemcpyAsync(pin + i, (const void*)ptrs[i], (size_t)bytes[i], hipMemcpyDeviceToHost, (hipStream_t)stream),
+            "read_words copy");
+    }
+    wait_stream((hipStream_t)stream, "read_words");
+    for (size_t i = 0; i < ptrs.size(); ++i) out[i] = bytes[i] == 4 ? (int64_t)(int32_t)pin[i] : pin[i];
+  }
+  return out;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Radix-partitioned group-by (partition.hip).  Every launch below is sized from host-known layout
 // numbers (buckets, blocks); record counts stay on the device (no synchronisation per run).
@@ -1082,6 +1105,7 @@ PYBIND11_MODULE(_sdo_native, m) {
   m.def("fetch_small", &fetch_small);
   m.def("fetch_small_reset", &fetch_small_reset);
   m.def("stream_sync", &stream_sync);
+  m.def("read_words", &read_words);
   m.def("set_wait_spin", &set_wait_spin);
   m.def("glds_probe", &glds_probe);
   m.def("part_scan", &part_scan);

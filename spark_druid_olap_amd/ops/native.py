@@ -367,5 +367,13 @@ def fetch_small_reset(acc: torch.Tensor, hll: Sequence[torch.Tensor], G: int, p:
                              host.data_ptr(), *reset_args, _stream(acc.device))
 
 
+def read_words(ts, dev) -> list:
+    """Values of int64 device words (tensors' first elements) after this thread's stream work, with
+    one copy and one wait (bindings.cpp read_words)."""
+    for t in ts:
+        assert t.is_cuda and t.element_size() in (4, 8) and t.numel() >= 1
+    return list(load().read_words([t.data_ptr() for t in ts], [t.element_size() for t in ts], _stream(dev)))
+
+
 def stream_sync(dev) -> None:
     load().stream_sync(_stream(dev))
