@@ -1003,6 +1003,15 @@ def _group_codes(keys: List[pd.Series], n: int):
     return codes, ng, first
 
 
+_GLOBAL_AGG = {
+    "sum": lambda x: x.sum(min_count=1),
+    "avg": lambda x: x.mean(),
+    "mean": lambda x: x.mean(),
+    "min": lambda x: x.min(),
+    "max": lambda x: x.max(),
+}
+
+
 def _agg_one(call: A.Call, fr: Frame, codes: np.ndarray, ng: int, n: int, out_t: str) -> pd.Series:
     name = call.name
     if name == "count" and not call.args:
@@ -1030,6 +1039,13 @@ def _agg_one(call: A.Call, fr: Frame, codes: np.ndarray, ng: int, n: int, out_t:
         r = x[valid].groupby(codes[valid]).nunique()
         return pd.Series(r.reindex(range(ng), fill_value=0).to_numpy().astype(np.int64), dtype="Int64")
     xt = typeof(call.args[0]) if call.args else "null"
+    if ng == 1 and not call.distinct and name in _GLOBAL_AGG and x is not None and n and \
+            pd.api.types.is_numeric_dtype(x.dtype) and not pd.api.types.is_bool_dtype(x.dtype) and \
+            (not len(codes) or not codes.any()):
+        # a global aggregate (no GROUP BY) over a numeric column: the Series reduction itself, not a
+        # one-group groupby (TPC-H Q17's sum over the joined rows: 0.65 -> ~0.05 ms)
+        v = _GLOBAL_AGG[name](x)
+        return to_series(pd.Series([None if v is pd.NA or (isinstance(v, float) and v != v) else v]), out_t)
     if name in ("sum", "avg", "mean", "stddev", "stddev_samp", "stddev_pop", "variance", "var_samp", "var_pop"):
         if base(xt) == "string":
             x = to_series(x, "double")

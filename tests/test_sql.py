@@ -325,3 +325,22 @@ def test_aggregate_over_one_dimension_expression(sess, agg):
     aggregated through the entry table (druid_rewrite._dim_expr_agg), the reference's JavaScript
     aggregator over a dimension (tc/CodeGenTest.scala:417-482)."""
     ctest(sess, f"select l_returnflag, {agg} from {T} group by l_returnflag", ndruid=1)
+
+
+def test_global_aggregates_over_nulls_match_grouped_semantics():
+    """sql/execute.py _agg_one's global-aggregate fast path (no GROUP BY, numeric column) gives the
+    grouped path's answers: NULLs skipped, an all-NULL input sums / averages / min-maxes to NULL."""
+    import pandas as pd
+
+    from spark_druid_olap_amd.engine.executor import Engine
+    from spark_druid_olap_amd.session import Session
+
+    s = Session(engine=Engine(use_native=False))
+    s.register_table("gt", pd.DataFrame({"k": [1, 1, 2, 2], "i": pd.array([1, None, 3, None], dtype="Int64"),
+                                         "f": [1.5, None, 2.5, None], "z": [None, None, None, None]},
+                                        ).astype({"z": "float64"}))
+    got = s.sql("select sum(i), avg(i), min(i), max(i), sum(f), avg(f), sum(z), avg(z), min(z), count(z) "
+                "from gt").collect()[0]
+    assert tuple(got) == (4, 2.0, 1, 3, 4.0, 2.0, None, None, None, 0)
+    grouped = s.sql("select k, sum(i), min(f) from gt group by k order by k").collect()
+    assert [tuple(r) for r in grouped] == [(1, 1, 1.5), (2, 3, 2.5)]
