@@ -1593,6 +1593,14 @@ def order_and_limit(cols: Dict[str, np.ndarray], idx: np.ndarray, order_cols, li
     return idx[: limit] if limit is not None and limit >= 0 else idx
 
 
+def default_slots(dev) -> int:
+    """Execution slots (concurrent statements, one HIP stream each) of a serving engine: 8 on a GPU
+    -- the BI plan's closed loop peaks there (520 executions/s; 473/s at 10 slots, 457/s at 12:
+    profiles/r6/thrift_jmx_s{8,10,12}_*cold*.json) now that the slots carve one arena each -- and 4
+    on the host."""
+    return 8 if getattr(dev, "type", "cpu") == "cuda" else 4
+
+
 class Engine:
     """Executes QuerySpecs on the current rank's shards, merging across the process group."""
 
@@ -1614,11 +1622,12 @@ class Engine:
 
     def coalescer(self, slots: Optional[int] = None):
         """The engine's stream scheduler + identical-statement batching (engine/scheduler.py),
-        created on first use with ``slots`` HIP streams (``SDO_STREAMS``, default 4)."""
+        created on first use with ``slots`` HIP streams (``SDO_STREAMS``; default
+        default_slots())."""
         if self._coalescer is None:
             from .scheduler import Coalescer, StreamScheduler
 
-            n = slots or int(os.environ.get("SDO_STREAMS", "4"))
+            n = slots or int(os.environ.get("SDO_STREAMS", "0")) or default_slots(self.world.device())
             self._coalescer = Coalescer(StreamScheduler(n, self.world.device()))
         return self._coalescer
 

@@ -191,7 +191,7 @@ class NativeHiveServer(HiveThriftServer):
                  executors: Optional[int] = None):
         super().__init__(session, host, port, auth, world)
         self.nexec = executors or int(os.environ.get("SDO_GATEWAY_EXECUTORS", "0")) or \
-            (int(os.environ.get("SDO_STREAMS", "4")) + 2)
+            (session.engine.coalescer().scheduler.nslots + 2)
         self._gw = None
         self._stop = threading.Event()
         self._threads: List[threading.Thread] = []
