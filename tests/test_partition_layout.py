@@ -65,3 +65,32 @@ def test_partitioned_run_uses_its_buffers_layout_and_grid(monkeypatch):
     splits = [c for c in nat.calls if c[0] == "split"]
     assert splits and all(c[3] == grid and c[4] == old["shift1"] and c[5] == old["p1"] for c in splits)
     assert ("agg", old["nsub"], old["shift"]) in nat.calls
+
+
+def test_layout_packs_a_small_field_of_wide_records_only(ds_small, monkeypatch):
+    """part_layout's record packing (engine/device_exec.py _pack_field): a non-negative integer sum
+    whose values fit the key word's bits above shift1 rides in the key word after level 1 -- for
+    3+ word records only; wide value ranges, negative values and 2-word records stay unpacked."""
+    from spark_druid_olap_amd.engine.lower import Lowerer
+    from spark_druid_olap_amd.query import spec as S
+
+    def layout(aggs):
+        prog = Lowerer(ds_small).lower_aggregate(["1992-01-01/1999-01-01"], None,
+                                                 [S.DefaultDimensionSpec("o_orderkey")], None, aggs)
+        return DE.part_layout(prog)
+
+    q = S.FunctionAggregationSpec("longSum", "q", "l_quantity")
+    tp = S.FunctionAggregationSpec("longSum", "tp", "o_totalprice")
+    L = layout([tp, q])  # key + two i32 sums: 3 words
+    assert L["rw"] == 3 and L.get("pack") is not None
+    j, word = L["pack"]
+    assert L["rw1"] == 2 and L["agg_fields"][j][1] == 3 | (L["shift1"] << 8)
+    assert [f for i, f in enumerate(L["agg_fields"]) if i != j] == [f for i, f in enumerate(L["fields"]) if i != j]
+    assert "pack" not in layout([q])  # 2-word records: unpacked
+    monkeypatch.setattr(DE, "_value_range", lambda ds, name: (-5, 10))
+    assert "pack" not in layout([tp, q])  # negative values never pack
+    monkeypatch.setattr(DE, "_value_range", lambda ds, name: (0, 1 << 31))
+    assert "pack" not in layout([tp, q])  # too wide for the free bits
+    monkeypatch.setattr(DE, "PACK_RECORDS", False)
+    monkeypatch.setattr(DE, "_value_range", lambda ds, name: (0, 10))
+    assert "pack" not in layout([tp, q])
