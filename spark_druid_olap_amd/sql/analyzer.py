@@ -21,14 +21,18 @@ class Scope:
     def __init__(self, refs: List[A.Ref], outer: Optional["Scope"] = None):
         self.refs = refs
         self.outer = outer
+        self._by_name: Optional[Dict[str, List[A.Ref]]] = None
 
     def resolve(self, parts: Tuple[str, ...]) -> Optional[A.Ref]:
         name = parts[-1].lower()
         qual = [p.lower() for p in parts[:-1]]
+        if self._by_name is None:  # (a wide view resolves thousands of names per statement)
+            idx: Dict[str, List[A.Ref]] = {}
+            for r in self.refs:
+                idx.setdefault(r.name.lower(), []).append(r)
+            self._by_name = idx
         hits = []
-        for r in self.refs:
-            if r.name.lower() != name:
-                continue
+        for r in self._by_name.get(name, ()):
             if qual:
                 q = (r.qualifier or "").lower()
                 # qualifier may be "alias", "table" or "db.table"
