@@ -768,11 +768,15 @@ class Lowerer:
         dc = self.ds.dims.get(dim)
         if dc is None or dc.bitmap is None:
             return None
-        k = int(mask.sum())
-        if k == 0 or k == len(mask):
+        st = mask_stats(mask)
+        if st.k == 0 or st.k == len(mask):
             return None
-        for use_neg, rr in ((False, _runs(mask)), (True, _runs(~mask))):
-            if len(rr) <= self.bitmap_max_values and sum(b - a for a, b in rr) <= 64:
+        lim = self.bitmap_max_values
+        for use_neg, nr in ((False, st.runs), (True, st.neg_runs)):
+            if nr > lim:
+                continue
+            rr = _runs(~mask if use_neg else mask)
+            if sum(b - a for a, b in rr) <= 64:
                 return (use_neg, rr)
         return None
 
@@ -799,15 +803,14 @@ class Lowerer:
     def _emit_ids(self, prog: ScanProgram, dim: str, mask: np.ndarray) -> int:
         dc = self.ds.dims[dim]
         card = len(mask)
-        k = int(mask.sum())
+        st = mask_stats(mask)
+        k = st.k
         if k == 0:
             prog.fops.append((D.F_FALSE, 0, 0, 0, 0, 0.0, 0.0, None))
             return 1
         if k == card:
             prog.fops.append((D.F_TRUE, 0, 0, 0, 0, 0.0, 0.0, None))
             return 1
-        runs = _runs(mask)
-        neg_runs = _runs(~mask)
         plan = self.bitmap_plan(dim, mask)
         if plan is not None and len(prog.bm_leaves) + len(plan[1]) <= D.MAX_BM:
             use_neg, rr = plan
@@ -821,15 +824,20 @@ class Lowerer:
                 prog.fops.append((D.F_NOT, 0, 0, 0, 0, 0.0, 0.0, None))
             return 2 if len(rr) > 1 else 1
         ci = prog.col(dim)
-        if len(runs) == 1:
-            prog.fops.append((D.F_ID_RANGE, ci, 0, runs[0][0], runs[0][1], 0.0, 0.0, None))
+        if st.runs == 1:
+            prog.fops.append((D.F_ID_RANGE, ci, 0, st.lo, st.hi, 0.0, 0.0, None))
             return 1
-        if len(neg_runs) == 1:
-            prog.fops.append((D.F_ID_RANGE, ci, 0, neg_runs[0][0], neg_runs[0][1], 0.0, 0.0, None))
+        if st.neg_runs == 1:
+            (a, b), = _runs(~mask)
+            prog.fops.append((D.F_ID_RANGE, ci, 0, a, b, 0.0, 0.0, None))
             prog.fops.append((D.F_NOT, 0, 0, 0, 0, 0.0, 0.0, None))
             return 1
-        words = pack_bitset(mask)
-        t = torch.from_numpy(words).to(self.ds.device)
+        dk = str(self.ds.device)
+        t = st.words.get(dk)
+        if t is None:  # (read-only on the device: plans of one cached mask share the words)
+            t = torch.from_numpy(pack_bitset(mask)).to(self.ds.device)
+            if len(mask) >= _MASK_STATS_MIN:
+                st.words[dk] = t
         prog.keepalive.append(t)
         prog.fops.append((D.F_IN_SET, ci, 0, 0, 0, 0.0, 0.0, t))
         return 1
@@ -840,8 +848,10 @@ class Lowerer:
         cands = []
         for c in conj:
             if _is(c, "ids") and self.ds.dims[c[1]].zmin is not None:
-                nz = np.flatnonzero(c[2])
-                lo, hi = int(nz[0]), int(nz[-1]) + 1
+                st = mask_stats(c[2])
+                if st.k == 0:
+                    continue
+                lo, hi = st.lo, st.hi
                 frac = (hi - lo) / max(1, len(c[2]))
                 if frac < 0.9:
                     cands.append((frac, c[1], lo, hi))
@@ -866,7 +876,7 @@ class Lowerer:
         if k == "not":
             return 1.0 - self.selectivity(x[1])
         if k == "ids":
-            return float(x[2].mean())
+            return mask_stats(x[2]).k / max(1, len(x[2]))
         return 1.0 / 3.0
 
     # ------------------------------------------------------------------ dimensions
@@ -1847,10 +1857,10 @@ def compact_key(kc: KeyComp, mask: np.ndarray) -> KeyComp:
 def pack_bitset(mask: np.ndarray) -> np.ndarray:
     """bool[n] -> int64 words, bit (i & 63) of word (i >> 6) == mask[i] (the kernel's F_IN_SET layout)"""
     n64 = (len(mask) + 63) // 64
-    words = np.zeros(n64, dtype=np.uint64)
-    idx = np.flatnonzero(mask).astype(np.uint64)
-    np.bitwise_or.at(words, (idx >> np.uint64(6)).astype(np.int64), np.left_shift(np.uint64(1), idx & np.uint64(63)))
-    return words.view(np.int64)
+    b = np.packbits(np.asarray(mask, dtype=bool), bitorder="little")
+    buf = np.zeros(n64 * 8, dtype=np.uint8)
+    buf[:len(b)] = b
+    return buf.view("<i8").astype(np.int64, copy=False)
 
 
 def _depth(x) -> int:
@@ -1862,12 +1872,56 @@ def _depth(x) -> int:
     return 1
 
 
-def _runs(mask: np.ndarray) -> List[Tuple[int, int]]:
+def _runs(mask: np.ndarray, limit: Optional[int] = None) -> Optional[List[Tuple[int, int]]]:
+    """[(start, end)] of the True runs of ``mask``; None when there are more than ``limit`` (a
+    LIKE over a 20M-value dictionary has ~1M runs: counting them is cheap, listing them is not)."""
+    if limit is not None and mask_stats(mask).runs > limit:
+        return None
     m = np.concatenate([[False], mask.astype(bool), [False]])
     d = np.diff(m.astype(np.int8))
     starts = np.flatnonzero(d == 1)
     ends = np.flatnonzero(d == -1)
     return list(zip(starts.tolist(), ends.tolist()))
+
+
+class MaskStats:
+    """Counts of a dictionary-id mask the lowering asks for more than once: set size, True / False
+    run counts, first / last True id, and its packed F_IN_SET words per device."""
+    __slots__ = ("k", "runs", "neg_runs", "lo", "hi", "words", "mask")
+
+    def __init__(self, mask: np.ndarray):
+        m = mask.astype(bool, copy=False)
+        n = len(m)
+        self.mask = mask  # (pins the id this entry is cached under)
+        self.k = int(np.count_nonzero(m))
+        if n == 0 or self.k == 0:
+            self.runs, self.neg_runs, self.lo, self.hi = 0, min(n, 1), 0, 0
+        else:
+            self.runs = int(np.count_nonzero(np.greater(m[1:], m[:-1]))) + int(m[0])
+            self.neg_runs = self.runs - 1 + int(not m[0]) + int(not m[-1])
+            self.lo = int(np.argmax(m))
+            self.hi = n - int(np.argmax(m[::-1]))
+        self.words: Dict[str, torch.Tensor] = {}
+
+
+_MASK_STATS: "Dict[int, MaskStats]" = {}
+_MASK_STATS_MIN = 1 << 16   # smaller masks are recomputed (cheap, and usually fresh arrays)
+_MASK_STATS_MAX = 16   # (each entry pins its mask: up to a few MB of host memory)
+
+
+def mask_stats(mask: np.ndarray) -> MaskStats:
+    """``MaskStats`` of ``mask``, cached by identity for large masks: a dictionary's LIKE / regex
+    masks are cached per pattern (segment/dictionary.py ``like_mask``), so every parameterization of
+    a template that filters ``p_name LIKE '%green%'`` hands the lowering the same 20M-entry array."""
+    if len(mask) < _MASK_STATS_MIN:
+        return MaskStats(mask)
+    st = _MASK_STATS.get(id(mask))
+    if st is None or st.mask is not mask:
+        st = MaskStats(mask)
+        if len(_MASK_STATS) >= _MASK_STATS_MAX:
+            _MASK_STATS.pop(next(iter(_MASK_STATS)))
+        _MASK_STATS[id(mask)] = st
+    return st
 
 
 def _f2ord(f: float) -> int:
