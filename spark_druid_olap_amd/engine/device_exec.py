@@ -1049,8 +1049,8 @@ class PartScratchPool:
             try:
                 sl = _Slab()
                 sl.dev, sl.words, sl.event = str(dev), words, None
-                sl.recs1 = _with_eviction(lambda: torch.empty(words, dtype=torch.int32, device=dev), None, None)
-                sl.recs2 = _with_eviction(lambda: torch.empty(words, dtype=torch.int32, device=dev), None, None)
+                sl.recs1 = _with_eviction(lambda: shared_empty(words, torch.int32, dev), None, None)
+                sl.recs2 = _with_eviction(lambda: shared_empty(words, torch.int32, dev), None, None)
                 from ..utils.metrics import count_event
 
                 count_event("part_slab_alloc")
@@ -1102,8 +1102,8 @@ class PartScratchPool:
             while have < nslots and self.total + 2 * words * 4 <= self._budget(dev):
                 sl = _Slab()
                 sl.dev, sl.words, sl.event = str(dev), words, None
-                sl.recs1 = torch.empty(words, dtype=torch.int32, device=dev)
-                sl.recs2 = torch.empty(words, dtype=torch.int32, device=dev)
+                sl.recs1 = shared_empty(words, torch.int32, dev)
+                sl.recs2 = shared_empty(words, torch.int32, dev)
                 self.total += 2 * words * 4
                 self.free.append(sl)
                 have += 1
@@ -1252,6 +1252,40 @@ class _Bufs:
 ARENA_ALIGN = 256
 ARENA_MIN = 64 << 20
 
+# Long-lived scratch (slot arena storages, partition slabs) is allocated on ONE allocation stream
+# per device and marked used by each stream that runs on it (``record_stream``).  The caching
+# allocator keeps a freed block for reuse by allocations of the stream it was made on only: made on
+# the 8 slot streams, every arena growth step and dropped slab stayed cached on its own slot's
+# stream, unusable by the others' next (larger) growth, until the allocator hit the device cap and
+# freed everything with the device synchronised -- a 3.3 s freeze of every slot in the cold BI
+# burst (profiles/r6/cold_burst_notes.md).  On one stream the dropped storages are the next
+# growth's free blocks.
+_ALLOC_STREAMS: dict = {}
+
+
+def _alloc_stream(dev) -> "torch.cuda.Stream":
+    k = str(dev)
+    s = _ALLOC_STREAMS.get(k)
+    if s is None:
+        with _arena_lock:
+            s = _ALLOC_STREAMS.get(k)
+            if s is None:
+                s = _ALLOC_STREAMS[k] = torch.cuda.Stream(torch.device(dev))
+    return s
+
+
+def shared_empty(n: int, dtype, dev) -> torch.Tensor:
+    """``torch.empty`` of long-lived scratch on the device's allocation stream, recorded as used by
+    the current stream (callers record any further stream that runs on it)."""
+    dev = torch.device(dev)
+    if dev.type != "cuda":
+        return torch.empty(n, dtype=dtype, device=dev)
+    cur = torch.cuda.current_stream(dev)
+    with torch.cuda.stream(_alloc_stream(dev)):
+        t = torch.empty(n, dtype=dtype, device=dev)
+    t.record_stream(cur)
+    return t
+
 
 class SlotArena:
     """One execution slot's device memory for the scans of its current statement."""
@@ -1266,6 +1300,7 @@ class SlotArena:
         self.need = 0         # bytes the current statement carved so far (across growths)
         self.binds: dict = {}  # start -> (end, owner id) of the regions' last carvers (current gen)
         self.users: "weakref.WeakSet" = weakref.WeakSet()  # scans holding views of this storage
+        self.rec: set = set()  # streams the current storage is recorded as used by
         self.lock = threading.Lock()  # (release_device_memory may drop the storage from another thread)
 
     def carve(self, nbytes: int, owner) -> tuple:
@@ -1298,12 +1333,16 @@ class SlotArena:
             cap = max(ARENA_MIN, 2 * self.cap, self.need, peer)
             cap = (cap + ARENA_MIN - 1) // ARENA_MIN * ARENA_MIN
             self._drop()
-            self.buf = _with_eviction(lambda: torch.empty(cap, dtype=torch.uint8, device=self.dev), None, self.slot,
-                                      arena=self)
+            self.buf = _with_eviction(lambda: shared_empty(cap, torch.uint8, self.dev), None, self.slot, arena=self)
             self.cap = cap
             from ..utils.metrics import count_event
 
             count_event("arena_grow")
+        if self.buf.is_cuda:  # (a storage presized on the warm-up thread's stream runs on the slot's)
+            cs = torch.cuda.current_stream(self.buf.device)
+            if cs.cuda_stream not in self.rec:
+                self.buf.record_stream(cs)
+                self.rec.add(cs.cuda_stream)
         start = self.off
         self.off += nbytes
         end = start + nbytes
@@ -1341,6 +1380,7 @@ class SlotArena:
         self.users = weakref.WeakSet()
         self.buf, self.cap, self.off = None, 0, 0
         self.binds = {}
+        self.rec = set()
         self.gen += 1
 
 
@@ -1381,7 +1421,7 @@ def presize_device_memory(dev=None, nslots: int = 0) -> dict:
             with ar.lock:
                 if ar.cap < peak:
                     ar._drop()
-                    ar.buf = torch.empty(peak, dtype=torch.uint8, device=dev)
+                    ar.buf = shared_empty(peak, torch.uint8, dev)
                     ar.cap = peak
                     grown += 1
                     count_event("arena_presize")

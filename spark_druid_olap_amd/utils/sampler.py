@@ -20,6 +20,9 @@ from typing import Optional
 
 _IDLE = ("wait", "recv", "recv_into", "accept", "select", "poll", "sleep", "get", "_wait_for_tstate_lock",
          "acquire", "readinto", "read")
+# innermost Python frames that are idle inside a native call: a gateway executor blocked in
+# next_batch (server/gateway.py) and a thread-pool worker blocked on its SimpleQueue
+_IDLE_NATIVE = (("gateway.py", "_executor"), ("thread.py", "_worker"))
 
 
 class Sampler:
@@ -47,6 +50,8 @@ class Sampler:
                 if f.f_code.co_name in _IDLE and f.f_back is not None and \
                         f.f_code.co_filename.endswith(("threading.py", "socket.py", "queue.py", "selectors.py",
                                                        "socketserver.py")):
+                    continue
+                if any(f.f_code.co_name == n and f.f_code.co_filename.endswith(fn) for fn, n in _IDLE_NATIVE):
                     continue
                 self.samples += 1
                 self.self_counts[self._key(f)] += 1

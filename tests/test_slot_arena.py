@@ -208,3 +208,27 @@ def test_part_pool_presize_fills_one_slab_per_slot(monkeypatch):
     assert pool.presize("cpu", 4) == 0
     s = pool.acquire("cpu", 500)  # served from the presized slabs
     assert s.words == 1000 and pool.total == 4 * 2 * 1000 * 4
+
+
+@pytest.mark.gpu
+def test_shared_allocation_stream_reuses_dropped_storage():
+    """Arena storages and partition slabs come from one allocation stream: a storage dropped by a
+    slot on one stream is the next growth's free block on another slot's stream (allocated per slot
+    stream, it stayed cached on its own stream until a free-everything retry)."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    n = 256 << 20
+    with torch.cuda.stream(s1):
+        a = DE.shared_empty(n, torch.uint8, dev)
+        a.fill_(1)
+    r0 = torch.cuda.memory_reserved(dev)
+    del a
+    torch.cuda.synchronize(dev)
+    with torch.cuda.stream(s2):
+        b = DE.shared_empty(n, torch.uint8, dev)
+        b.fill_(2)
+    assert torch.cuda.memory_reserved(dev) == r0
+    torch.cuda.synchronize(dev)
+    assert int(b[::1 << 20].min()) == 2

@@ -196,6 +196,8 @@ def main():
     ap.add_argument("--server", default="native", choices=["native", "python"],
                     help="native C++ gateway (server/csrc/hs2_gateway.cpp) or the pure-Python server")
     ap.add_argument("--sample", default=None, help="write a sampling profile of the server threads here")
+    ap.add_argument("--include-warmup", action="store_true",
+                    help="--timeline / --sample also cover the closed loop's warm-up seconds (the cold burst)")
     ap.add_argument("--workload", default="fixed", choices=["fixed", "varied", "jmx"],
                     help="fixed: the 8 benchmark texts; varied: ~2,000 distinct parameterizations; jmx: the "
                          "reference's BI plan (docs/bi-benchmark/snap-sales-demo.jmx, models/bi)")
@@ -310,6 +312,8 @@ def main():
 
         log_events(True)
         srv.stalls = []
+        if a.include_warmup:
+            srv.timeline = []
     t_start = time.time() + 1.0 + a.warmup
     for _ in ps:
         start_q.put((srv.port, t_start - a.warmup, a.duration + a.warmup, interval))
@@ -323,13 +327,22 @@ def main():
             return st["coalesced"], st["batches"]
         return co.stats["coalesced"], co.stats["executions"]
 
+    sampler = None
+    if a.sample and a.include_warmup:
+        from spark_druid_olap_amd.utils.sampler import Sampler
+
+        sampler = Sampler().start()
     time.sleep(max(0.0, t_start - time.time()))
-    if a.timeline and a.server == "native":
+    if sampler is not None:  # (--include-warmup: the profile covers the warm-up seconds only)
+        sampler.stop()
+        with open(a.sample, "w") as f:
+            f.write(sampler.report(60))
+        sampler = None
+    if a.timeline and a.server == "native" and not a.include_warmup:
         srv.timeline = []
     cpu0 = time.process_time()
     co0, ex0 = counters()
-    sampler = None
-    if a.sample:
+    if a.sample and not a.include_warmup:
         from spark_druid_olap_amd.utils.sampler import Sampler
 
         sampler = Sampler().start()
