@@ -207,23 +207,35 @@ __global__ __launch_bounds__(512) void part_keys_kernel(const int64_t* __restric
 // LDS (Packed: a selective producer leaves a few dozen records in each 4096-row chunk region, and a
 // tile per region paid the tile's barriers for almost nothing -- TPC-H Q2's 8M-row inner level over
 // 146K regions).  v -> record index.
+// find / walk / at: a thread's records of one tile (v = t0 + tid + u * 512, increasing in u) look
+// their region up once -- a binary search for the first, a short forward walk for the rest -- and
+// keep the region index for the record copy, instead of a full search per record and use.
 struct Contig {
   uint32_t lo;
   __device__ __forceinline__ uint64_t operator()(uint32_t v) const { return (uint64_t)lo + v; }
+  __device__ __forceinline__ int find(uint32_t) const { return 0; }
+  __device__ __forceinline__ int walk(uint32_t, int a) const { return a; }
+  __device__ __forceinline__ uint64_t at(uint32_t v, int) const { return (uint64_t)lo + v; }
 };
 struct Packed {
   const uint32_t* slo;   // [ns] region starts (LDS)
   const uint32_t* spre;  // [ns + 1] exclusive prefix of the region lengths (LDS)
   int ns;
-  __device__ __forceinline__ uint64_t operator()(uint32_t v) const {
+  __device__ __forceinline__ int find(uint32_t v) const {
     int a = 0, b = ns - 1;  // the last region whose prefix <= v
     while (a < b) {
       const int mid = (a + b + 1) >> 1;
       if (spre[mid] <= v) a = mid;
       else b = mid - 1;
     }
-    return (uint64_t)slo[a] + (v - spre[a]);
+    return a;
   }
+  __device__ __forceinline__ int walk(uint32_t v, int a) const {
+    while (a + 1 < ns && spre[a + 1] <= v) ++a;  // (the same "last region whose prefix <= v")
+    return a;
+  }
+  __device__ __forceinline__ uint64_t at(uint32_t v, int a) const { return (uint64_t)slo[a] + (v - spre[a]); }
+  __device__ __forceinline__ uint64_t operator()(uint32_t v) const { return at(v, find(v)); }
 };
 
 template <bool CL>
@@ -305,12 +317,15 @@ __device__ __forceinline__ void split_range_scatter(const uint32_t* __restrict__
     for (uint32_t q = threadIdx.x; q < P2; q += blockDim.x) hist[q] = 0u;
     __syncthreads();
     uint32_t q_[PU], r_[PU];
+    int ra_[PU];
     uint2 v2[PU];
 #pragma unroll
     for (int u = 0; u < PU; ++u) {
       const uint32_t j = threadIdx.x + u * blockDim.x;
+      ra_[u] = 0;
       if (j < tn) {
-        const uint64_t i = map(t0 + j);
+        ra_[u] = u == 0 ? map.find(t0 + j) : map.walk(t0 + j, ra_[u - 1]);
+        const uint64_t i = map.at(t0 + j, ra_[u]);
         if (RW == 2) {
           v2[u] = *(const uint2*)(in + i * 2);
         } else {
@@ -385,7 +400,7 @@ __device__ __forceinline__ void split_range_scatter(const uint32_t* __restrict__
         } else if (RW == 1) {
           tile[d] = v2[u].x;  // (the key is the record)
         } else {
-          const uint32_t* rec = in + map(t0 + j) * RW;
+          const uint32_t* rec = in + map.at(t0 + j, ra_[u]) * RW;
           for (int w = 0; w < RW; ++w) tile[(uint64_t)d * RS + w] = rec[w];
         }
       }
@@ -476,7 +491,10 @@ __global__ __launch_bounds__(512) void part_split_kernel(const uint32_t* __restr
       }
       if (threadIdx.x == 0) spre[ns] = tot;
       __syncthreads();
-      if (tot < 1024u * (uint32_t)ns) {
+      // packed when the regions average under ~80% of a tile (a region-by-region pass runs one
+      // part-empty tile per region: a date-filtered producer fills its 4096-row regions ~57%)
+      // (the count pass keeps the round-5 rule: its per-record cost is the search itself)
+      if (phase == 0 ? tot < 1024u * (uint32_t)ns : tot * 5u < 4u * 512u * (uint32_t)PU * (uint32_t)ns) {
         const Packed pm{slo, spre, ns};
         if (phase == 0) split_map_count<CL>(in, RW, pm, tot, shift2, mask, h);
         else split_range_scatter<PU, CL>(in, RW, RS, pm, tot, shift2, (uint32_t)P2, h, hist, tstart, tile, scan_lds, out,
