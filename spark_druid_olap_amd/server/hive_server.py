@@ -679,6 +679,9 @@ def main(argv=None):
     the broadcast statement stream (server/spmd.py)."""
     import argparse
 
+    from ..utils.memory import serving_allocator_conf
+
+    serving_allocator_conf()  # (before this process's first device allocation)
     ap = argparse.ArgumentParser()
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=int(os.environ.get("SDO_THRIFT_PORT", "10000")))

@@ -43,6 +43,25 @@ def serving_gc() -> None:
     gc.set_threshold(50_000, 50, 100)
 
 
+SERVING_ALLOC_CONF = "garbage_collection_threshold:0.7"
+
+
+def serving_allocator_conf() -> bool:
+    """A serving process's caching-allocator settings (call before the process's first device
+    allocation; a user's own ``PYTORCH_HIP_ALLOC_CONF`` / ``PYTORCH_CUDA_ALLOC_CONF`` wins).
+
+    Above 70 % of the device the allocator returns its least recently used free blocks a few at a
+    time instead of letting reserved memory reach the cap, where it frees EVERY cached block with
+    the device synchronised and retries -- the cold BI burst's 3.3 s freeze of every slot
+    (profiles/r6/cold_burst_notes.md).  Same-box A/B, cold closed loop, 64 clients, 8 slots:
+    575-579 exec/s and p99 187-188 ms with no retry, against 461-488 exec/s and p99 256-261 ms with
+    one (profiles/r6/thrift_jmx_cold_alloc_gc_ab.txt)."""
+    if os.environ.get("PYTORCH_HIP_ALLOC_CONF") or os.environ.get("PYTORCH_CUDA_ALLOC_CONF"):
+        return False
+    os.environ["PYTORCH_HIP_ALLOC_CONF"] = SERVING_ALLOC_CONF
+    return True
+
+
 RUNTIME_RESERVE = int(os.environ.get("SDO_RUNTIME_RESERVE_GB", "8")) << 30
 
 

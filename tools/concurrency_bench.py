@@ -186,6 +186,9 @@ def pct(xs, p):
 
 def main():
     global NCLIENTS
+    from spark_druid_olap_amd.utils.memory import serving_allocator_conf
+
+    serving_allocator_conf()  # the server's allocator settings (server/hive_server.py main)
     ap = argparse.ArgumentParser()
     ap.add_argument("--sf", type=float, default=1.0)
     ap.add_argument("--clients", type=int, default=64)
