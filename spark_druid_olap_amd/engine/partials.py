@@ -315,6 +315,8 @@ def _native_sparse(prog, parts: Partials, out_types, want_gid: bool):
     g = parts.keys
     if not g.is_cuda or _NO_DEVICE_DECODE:
         return None
+    if not g.is_contiguous():  # (the kernel reads the ids as one contiguous int64 array)
+        g = g.contiguous()
     dev = g.device
     R = int(g.numel())
     specs, consts, typed = [], {}, {}

@@ -249,7 +249,9 @@ def unpack_rows(rows: torch.Tensor, nslots: int, hll_widths: List[int], scattere
     for m in hll_widths:
         hll.append(rows[:, off: off + m].contiguous())
         off += m
-    return Partials("sparse", kv[:, 1:], kv[:, 0], hll, scattered=scattered)
+    # (contiguous: the native decode and top-k kernels take raw pointers -- a strided key column
+    # read as contiguous mixed the count slot into the key ids, tools/rccl_smoke.py at SF1)
+    return Partials("sparse", kv[:, 1:].contiguous(), kv[:, 0].contiguous(), hll, scattered=scattered)
 
 
 def gather_groups(world: World, sp: Partials, root_only: bool, status: int = STATUS_OK,

@@ -19,7 +19,7 @@ def test_rccl_one_rank_smoke(tmp_path):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     env.pop("SDO_GLOO_GPU", None)
     rc = spawn_ranks(1, [sys.executable, os.path.join(ROOT, "tools", "rccl_smoke.py"), "--out", str(out),
-                         "--sf", "0.1"], env=env)
+                         "--sf", "1"], env=env)
     assert rc == 0
     r = json.loads(out.read_text())
     print(json.dumps(r)[:3000])

@@ -58,3 +58,4 @@ def test_mask_stats_cached_by_identity():
     assert L.mask_stats(other) is not a          # an equal but different array is its own entry
     small = np.ones(8, dtype=bool)
     assert L.mask_stats(small) is not L.mask_stats(small)  # small masks are not cached
+

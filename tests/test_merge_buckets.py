@@ -198,3 +198,18 @@ def test_sparse_shuffle_merge(world):
     total = sum(lg["sent"] for lg in logs)
     for lg in logs:  # each rank receives ~total/N partial rows (hash partitioning), not the total
         assert 0.6 * total / world < lg["recv"] < 1.4 * total / world, logs
+
+
+def test_unpacked_rows_are_contiguous():
+    """parallel/merge.py unpack_rows: the exchanged key / accumulator columns go to native kernels
+    that take raw pointers, so they must not be strided views of the packed rows."""
+    import torch
+
+    from spark_druid_olap_amd.engine.partials import Partials
+    from spark_druid_olap_amd.parallel.merge import pack_rows, unpack_rows
+
+    keys = torch.tensor([3, 7, 11], dtype=torch.int64)
+    acc = torch.tensor([[1, 10], [2, 20], [3, 30]], dtype=torch.int64)
+    out = unpack_rows(pack_rows(Partials("sparse", acc, keys, [])), 2, [])
+    assert out.keys.is_contiguous() and out.acc.is_contiguous()
+    assert out.keys.tolist() == [3, 7, 11] and out.acc.tolist() == acc.tolist()

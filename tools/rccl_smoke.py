@@ -98,6 +98,14 @@ def engine(w, dev, sf, out):
                 ms[f"{name}{' (root)' if root else ''}"] = round((time.perf_counter() - t) * 1e3, 3)
                 res[root] = _rows(b)
         eq[name] = res[True] == want and res[False] == want
+        if not eq[name]:  # what differs: row counts and a few rows only one side has
+            diag = out.setdefault("mismatch", {})
+            for root in (True, False):
+                a, b_ = set(res[root]), set(want)
+                diag[f"{name}{' (root)' if root else ''}"] = {
+                    "rows": len(res[root]), "want_rows": len(want),
+                    "only_rccl": [list(map(str, r)) for r in sorted(a - b_)[:3]],
+                    "only_local": [list(map(str, r)) for r in sorted(b_ - a)[:3]]}
         ran[name] = len(want)
     out["engine_equal"] = eq
     out["engine_rows"] = ran
